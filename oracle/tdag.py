@@ -241,3 +241,18 @@ def shuffle(events, rng):
         j = rng.below(i + 1)
         arr[i], arr[j] = arr[j], arr[i]
     return arr
+
+
+def to_dense(events, validators):
+    """Dense arrays for the C ABI: (creator_idx, seq, parent_off, parent_idx),
+    parents as Add-order positions (self-parent first, as in the input)."""
+    import numpy as np
+    pos = {e.id: i for i, e in enumerate(events)}
+    creator = np.array([validators.idxs[e.creator] for e in events], dtype=np.uint32)
+    seq = np.array([e.seq for e in events], dtype=np.uint32)
+    off = np.zeros(len(events) + 1, dtype=np.uint64)
+    flat = []
+    for i, e in enumerate(events):
+        flat.extend(pos[p] for p in e.parents)
+        off[i + 1] = len(flat)
+    return creator, seq, off, np.array(flat, dtype=np.uint32)
