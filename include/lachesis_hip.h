@@ -1,0 +1,138 @@
+/*
+ * lachesis_hip.h -- C ABI of the MI355X-native vector-clock / ForklessCause index.
+ *
+ * Drop-in replacement for the reference's vecfc.Index (embedding
+ * vecengine.Engine) behind the abft.DagIndexer / dagidx interfaces of
+ * github.com/Fantom-foundation/lachesis-base.  Each entry point names the
+ * reference interface it replaces (file:line in the reference tree).
+ *
+ * Conventions
+ *  - Events are identified by dense indices 0..N-1 in Add order (the Go shim
+ *    keeps the hash.Event <-> index map).  Parents are
+ *    given as dense indices, self-parent first (inter/dag/event.go:87-92).
+ *  - Validators are identified by their idx (inter/pos/validators.go:90-113);
+ *    the caller passes weights already sorted in idx order.
+ *  - All pointers are caller-owned; the library never retains them.
+ *    Functions ending in _dev take device pointers (hipMalloc'd on the
+ *    handle's device) and enqueue on the handle's stream unless a stream is
+ *    given; everything else takes host pointers and is synchronous.
+ *  - Return codes: 0 = ok, < 0 = error (lx_last_error() gives the message).
+ *  - One host thread per handle (the reference index is not thread-safe:
+ *    abft/indexed_lachesis.go:68).
+ *  - Byte layouts returned by the getters are the reference's
+ *    (vecfc/vector.go:14-102): LowestAfter = LE u32 per branch;
+ *    HighestBefore = LE (Seq u32, MinSeq u32) per branch; fork marker
+ *    {0, MaxInt32}.
+ */
+#ifndef LACHESIS_HIP_H
+#define LACHESIS_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LX_OK 0
+#define LX_ERR_ARG -1          /* bad argument / unknown event (crit in the reference) */
+#define LX_ERR_ORDER -2        /* parent not found / out of order (vecengine/index.go:159-161) */
+#define LX_ERR_EVENT -3        /* event violates eventcheck invariants (seq/self-parent) */
+#define LX_ERR_STATE -4        /* inconsistent state (vecengine/index.go:107-126) */
+#define LX_ERR_HIP -5          /* HIP runtime / device error */
+#define LX_ERR_NOMEM -6        /* device memory exhausted */
+
+#define LX_NO_EVENT 0xFFFFFFFFu
+
+typedef struct lx_index lx_index;
+
+typedef struct lx_config {
+    int device;                  /* HIP device ordinal */
+    uint64_t event_capacity;     /* events per epoch to pre-allocate (0 = grow on demand) */
+    uint32_t branch_reserve;     /* extra branch columns reserved for forks (0 = default) */
+    uint32_t shard_rank;         /* column shard (multi-GPU): this rank ...          */
+    uint32_t shard_count;        /* ... of shard_count (0 or 1 = unsharded)          */
+} lx_config;
+
+/* NewIndex (vecfc/index.go:69-78).  The cache sizes of IndexConfig
+ * (vecfc/index.go:16-61) only affect speed in the reference and have no
+ * counterpart here. */
+int lx_create(const lx_config *cfg, lx_index **out);
+void lx_destroy(lx_index *h);
+const char *lx_last_error(const lx_index *h);
+
+/* Reset (vecfc/index.go:98-105, vecengine/index.go:56-68): new epoch with
+ * `n_validators` validators whose weights are given in idx order. */
+int lx_reset(lx_index *h, uint32_t n_validators, const uint32_t *weights_by_idx);
+
+/* Add (vecengine/index.go:71-75) for a batch of events in Add order.
+ * parent_off has n+1 entries into parent_idx (dense indices, self-parent
+ * first).  Bit-exact to calling the reference Add once per event in the
+ * given order.  All-or-nothing: on error nothing is added and *err_index (if
+ * non-NULL) receives the batch position of the first offending event.
+ * out_branch (optional, n entries) receives each event's global branch ID
+ * (GetEventBranchID, vecengine/store_branches_info.go:83-88). */
+int lx_add_batch(lx_index *h, uint32_t n, const uint32_t *creator_idx, const uint32_t *seq,
+                 const uint64_t *parent_off, const uint32_t *parent_idx,
+                 uint32_t *out_branch, uint32_t *err_index);
+/* Same, with the batch already resident in device memory (parent_off is
+ * uint32 here: batch-local offsets). */
+int lx_add_batch_dev(lx_index *h, uint32_t n, const uint32_t *creator_idx_dev, const uint32_t *seq_dev,
+                     const uint32_t *parent_off_dev, const uint32_t *parent_idx_dev, uint32_t *err_index);
+
+/* Flush (vecengine/index.go:78-85) and DropNotFlushed (:88-96): rolls the
+ * index back to the last flush, including LowestAfter entries of old events
+ * and fork branches created since. */
+int lx_flush(lx_index *h);
+int lx_drop_not_flushed(lx_index *h);
+
+uint64_t lx_num_events(const lx_index *h);
+uint32_t lx_num_branches(const lx_index *h);           /* len(BranchIDCreatorIdxs) */
+int lx_at_least_one_fork(const lx_index *h);           /* branches_info.go:47-49 */
+
+/* ForklessCause (vecfc/forkless_cause.go:28-82) for n (a, b) pairs. */
+int lx_forkless_cause_batch(lx_index *h, uint64_t n, const uint32_t *a, const uint32_t *b, uint8_t *out);
+/* Device-resident variant; stream may be NULL (handle stream).  Unknown
+ * events yield 0xFF in out and LX_ERR_ARG from the next lx_sync(). */
+int lx_forkless_cause_batch_dev(lx_index *h, uint64_t n, const uint32_t *a_dev, const uint32_t *b_dev,
+                                uint8_t *out_dev, void *stream);
+/* Column-sharded partial: stake sum over this shard's creators, plus
+ * 0x80000000 when this shard owns branch(b) and A observes it as forked.
+ * Sum the partials of all shards (uint32) and apply lx_fc_combine. */
+int lx_forkless_cause_partial_dev(lx_index *h, uint64_t n, const uint32_t *a_dev, const uint32_t *b_dev,
+                                  uint32_t *partial_dev, void *stream);
+int lx_fc_combine_dev(lx_index *h, uint64_t n, const uint32_t *sum_dev, uint8_t *out_dev, void *stream);
+uint32_t lx_quorum(const lx_index *h);                 /* pos/validators.go:187-189 */
+
+/* Getters.  *len receives the byte length; out may be NULL to query it.
+ * GetHighestBefore / GetLowestAfter (vecfc/store_vectors.go:26-51),
+ * GetMergedHighestBefore (vecengine/index.go:235-250). */
+int lx_get_highest_before(lx_index *h, uint32_t ev, uint8_t *out, uint32_t cap, uint32_t *len);
+int lx_get_lowest_after(lx_index *h, uint32_t ev, uint8_t *out, uint32_t cap, uint32_t *len);
+int lx_get_merged_highest_before(lx_index *h, uint32_t ev, uint8_t *out, uint32_t cap, uint32_t *len);
+int lx_get_event_branch_id(lx_index *h, uint32_t ev, uint32_t *out);
+
+/* BranchesInfo (vecengine/branches_info.go:9-14): per branch last seq and
+ * creator idx (arrays of cap entries; *n_branches receives B). */
+int lx_get_branches_info(lx_index *h, uint32_t *last_seq, uint32_t *creator_idx, uint32_t cap,
+                         uint32_t *n_branches);
+
+/* Timing of the last lx_add_batch* call, measured with HIP events on the
+ * handle's stream (milliseconds): branch assignment + record packing,
+ * index walker (HB max-join + LA range fill), fork marks. */
+typedef struct lx_stats {
+    float ms_assign;
+    float ms_index;
+    float ms_marks;
+    uint32_t index_launches;
+} lx_stats;
+int lx_last_stats(const lx_index *h, lx_stats *out);
+
+/* Device views for benchmarks/tests (valid until the next add/reset). */
+int lx_device_planes(lx_index *h, void **hb, void **la, uint32_t *stride, void **stream);
+int lx_sync(lx_index *h);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

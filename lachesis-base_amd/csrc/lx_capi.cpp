@@ -1,0 +1,832 @@
+// lx_capi.cpp -- host engine behind the C ABI (include/lachesis_hip.h).
+//
+// Mirrors the lifecycle of vecfc.Index / vecengine.Engine (Reset, Add, Flush,
+// DropNotFlushed, ForklessCause, getters) on top of the device planes of
+// lx_internal.h.  Host state is O(branches); all per-event work is on the GPU.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/lachesis_hip.h"
+#include "lx_internal.h"
+
+namespace {
+
+constexpr uint32_t kStatusWords = 64;   // [1] fc bad flag, [2] max seq, [8..9] batch error u64, [16..47] jump flags
+
+template <typename T>
+hipError_t dalloc(T **p, uint64_t n) {
+    *p = nullptr;
+    if (!n) n = 1;
+    return hipMalloc((void **)p, n * sizeof(T));
+}
+
+inline uint32_t round_up(uint32_t x, uint32_t m) { return (x + m - 1) / m * m; }
+
+}  // namespace
+
+struct lx_index {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    uint32_t shard_rank = 0, shard_count = 1;
+    std::string err;
+
+    // epoch
+    uint32_t V = 0;
+    std::vector<uint32_t> weights;
+    uint32_t quorum = 0;
+    uint32_t own_lo = 0, own_hi = 0;
+    uint64_t n_events = 0, n_flushed = 0, hwm = 0;
+    uint32_t B = 0, B_flushed = 0;
+    uint32_t max_seq = 0;
+    bool have_epoch = false;
+
+    // host mirror of BranchesInfo (creator / first seq per branch; by creator)
+    std::vector<uint32_t> h_branch_creator, h_branch_first;
+    std::vector<std::vector<uint32_t>> by_creator;
+
+    // capacities
+    uint64_t n_cap = 0;
+    uint32_t stride = 0;   // == branch capacity
+    uint32_t s_cap = 0;
+    uint64_t cap_hint = 0;
+    uint32_t reserve = 0;
+
+    // device state
+    uint32_t *hb = nullptr, *la = nullptr;
+    uint32_t *ev_creator = nullptr, *ev_seq = nullptr, *ev_branch = nullptr, *ev_bbefore = nullptr,
+             *ev_sp = nullptr, *first_child = nullptr;
+    uint32_t *first_root = nullptr, *branch_first = nullptr, *branch_creator = nullptr, *branch_len = nullptr,
+             *brow = nullptr, *wpad = nullptr, *col_list = nullptr;
+    uint32_t *cheat_off = nullptr, *cheat_br = nullptr, *cheat_creator = nullptr;
+    uint32_t n_cheat = 0, ncols = 0;
+    uint64_t cheat_cap = 0;
+    uint32_t *status = nullptr;
+
+    // batch scratch
+    uint64_t batch_cap = 0, par_cap = 0;
+    uint32_t *b_creator = nullptr, *b_seq = nullptr, *b_poff = nullptr, *b_par = nullptr;
+    uint32_t *b_isfork = nullptr, *b_rank = nullptr, *b_tmpbr = nullptr, *b_jmp = nullptr;
+    EventRec *b_rec = nullptr;
+    void *scan_tmp = nullptr;
+    size_t scan_bytes = 0;
+
+    // query scratch
+    uint64_t q_cap = 0;
+    uint32_t *q_a = nullptr, *q_b = nullptr;
+    uint8_t *q_out = nullptr;
+
+    // timing (HIP events on `stream`)
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    lx_stats stats{};
+
+    int fail(int code, const char *fmt, ...) {
+        char buf[512];
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(buf, sizeof buf, fmt, ap);
+        va_end(ap);
+        err = buf;
+        return code;
+    }
+    int hip(hipError_t e, const char *what) {
+        if (e == hipSuccess) return 0;
+        return fail(e == hipErrorOutOfMemory ? LX_ERR_NOMEM : LX_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
+    }
+};
+
+#define HIPCHK(h, expr)                                  \
+    do {                                                 \
+        int _rc = (h)->hip((expr), #expr);               \
+        if (_rc) return _rc;                             \
+    } while (0)
+
+namespace {
+
+void free_all(lx_index *h) {
+    void *ptrs[] = {h->hb, h->la, h->ev_creator, h->ev_seq, h->ev_branch, h->ev_bbefore, h->ev_sp,
+                    h->first_child, h->first_root, h->branch_first, h->branch_creator, h->branch_len, h->brow,
+                    h->wpad, h->col_list, h->cheat_off, h->cheat_br, h->cheat_creator, h->b_creator, h->b_seq,
+                    h->b_poff, h->b_par, h->b_isfork, h->b_rank, h->b_tmpbr, h->b_jmp, h->b_rec, h->scan_tmp,
+                    h->q_a, h->q_b, h->q_out};
+    for (void *p : ptrs)
+        if (p) (void)hipFree(p);
+    h->hb = h->la = nullptr;
+    h->ev_creator = h->ev_seq = h->ev_branch = h->ev_bbefore = h->ev_sp = h->first_child = nullptr;
+    h->first_root = h->branch_first = h->branch_creator = h->branch_len = h->brow = h->wpad = h->col_list = nullptr;
+    h->cheat_off = h->cheat_br = h->cheat_creator = nullptr;
+    h->b_creator = h->b_seq = h->b_poff = h->b_par = h->b_isfork = h->b_rank = h->b_tmpbr = h->b_jmp = nullptr;
+    h->b_rec = nullptr;
+    h->scan_tmp = nullptr;
+    h->q_a = h->q_b = nullptr;
+    h->q_out = nullptr;
+    h->n_cap = h->stride = h->s_cap = 0;
+    h->batch_cap = h->par_cap = h->q_cap = h->cheat_cap = 0;
+    h->scan_bytes = 0;
+}
+
+// per-event arrays + planes for n_cap events (copies the first `keep` events)
+int grow_events(lx_index *h, uint64_t need) {
+    if (need <= h->n_cap) return 0;
+    uint64_t cap = std::max<uint64_t>({need, h->n_cap + h->n_cap / 2, 4096});
+    uint64_t keep = h->hwm;
+    uint32_t **arrs[] = {&h->ev_creator, &h->ev_seq, &h->ev_branch, &h->ev_bbefore, &h->ev_sp, &h->first_child};
+    for (uint32_t **a : arrs) {
+        uint32_t *n = nullptr;
+        HIPCHK(h, dalloc(&n, cap));
+        if (*a && keep) HIPCHK(h, hipMemcpyAsync(n, *a, keep * 4, hipMemcpyDeviceToDevice, h->stream));
+        if (*a) { HIPCHK(h, hipStreamSynchronize(h->stream)); (void)hipFree(*a); }
+        *a = n;
+    }
+    HIPCHK(h, lx::launch_fill_u32(h->first_child + keep, cap - keep, LX_NONE, h->stream));
+    uint32_t **planes[] = {&h->hb, &h->la};
+    for (uint32_t **p : planes) {
+        uint32_t *n = nullptr;
+        HIPCHK(h, dalloc(&n, cap * h->stride));
+        HIPCHK(h, hipMemsetAsync(n, 0, cap * h->stride * 4, h->stream));
+        if (*p && keep) HIPCHK(h, hipMemcpyAsync(n, *p, keep * h->stride * 4, hipMemcpyDeviceToDevice, h->stream));
+        if (*p) { HIPCHK(h, hipStreamSynchronize(h->stream)); (void)hipFree(*p); }
+        *p = n;
+    }
+    h->n_cap = cap;
+    return 0;
+}
+
+// branch capacity (= plane stride) and per-branch arrays
+int grow_branches(lx_index *h, uint32_t need) {
+    if (need <= h->stride) return 0;
+    uint32_t ns = round_up(std::max<uint32_t>(need, h->stride + h->stride / 4), 64);
+    uint32_t os = h->stride;
+    uint64_t keep = h->hwm;
+    if (h->hb) {
+        uint32_t **planes[] = {&h->hb, &h->la};
+        for (uint32_t **p : planes) {
+            uint32_t *n = nullptr;
+            HIPCHK(h, dalloc(&n, h->n_cap * ns));
+            HIPCHK(h, hipMemsetAsync(n, 0, h->n_cap * ns * 4, h->stream));
+            HIPCHK(h, lx::launch_copy_rows(n, ns, *p, os, keep, os, h->stream));
+            HIPCHK(h, hipStreamSynchronize(h->stream));
+            (void)hipFree(*p);
+            *p = n;
+        }
+    }
+    uint32_t **arrs[] = {&h->branch_first, &h->branch_creator, &h->branch_len, &h->wpad, &h->col_list};
+    for (uint32_t **a : arrs) {
+        uint32_t *n = nullptr;
+        HIPCHK(h, dalloc(&n, ns));
+        HIPCHK(h, hipMemsetAsync(n, 0, (uint64_t)ns * 4, h->stream));
+        if (*a) HIPCHK(h, hipMemcpyAsync(n, *a, (uint64_t)os * 4, hipMemcpyDeviceToDevice, h->stream));
+        if (*a) { HIPCHK(h, hipStreamSynchronize(h->stream)); (void)hipFree(*a); }
+        *a = n;
+    }
+    uint32_t *nb = nullptr;
+    HIPCHK(h, dalloc(&nb, (uint64_t)ns * h->s_cap));
+    if (h->brow) {
+        HIPCHK(h, hipMemcpyAsync(nb, h->brow, (uint64_t)os * h->s_cap * 4, hipMemcpyDeviceToDevice, h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        (void)hipFree(h->brow);
+    }
+    h->brow = nb;
+    h->stride = ns;
+    return 0;
+}
+
+int grow_scap(lx_index *h, uint32_t need) {
+    if (need <= h->s_cap) return 0;
+    uint32_t ns = std::max<uint32_t>({need, h->s_cap + h->s_cap / 2, 256});
+    uint32_t *nb = nullptr;
+    HIPCHK(h, dalloc(&nb, (uint64_t)h->stride * ns));
+    if (h->brow && h->s_cap) {
+        HIPCHK(h, lx::launch_copy_rows(nb, ns, h->brow, h->s_cap, h->stride, h->s_cap, h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        (void)hipFree(h->brow);
+    }
+    h->brow = nb;
+    h->s_cap = ns;
+    return 0;
+}
+
+int ensure_batch(lx_index *h, uint64_t n, uint64_t npar) {
+    if (n > h->batch_cap) {
+        uint64_t cap = std::max<uint64_t>(n, 1024);
+        uint32_t **arrs[] = {&h->b_creator, &h->b_seq, &h->b_isfork, &h->b_rank, &h->b_tmpbr, &h->b_jmp};
+        for (uint32_t **a : arrs) {
+            if (*a) (void)hipFree(*a);
+            HIPCHK(h, dalloc(a, cap));
+        }
+        if (h->b_poff) (void)hipFree(h->b_poff);
+        HIPCHK(h, dalloc(&h->b_poff, cap + 1));
+        if (h->b_rec) (void)hipFree(h->b_rec);
+        HIPCHK(h, dalloc(&h->b_rec, cap));
+        size_t sb = 0;
+        HIPCHK(h, lx::scan_tmp_bytes((uint32_t)cap, &sb));
+        if (h->scan_tmp) (void)hipFree(h->scan_tmp);
+        HIPCHK(h, hipMalloc(&h->scan_tmp, sb ? sb : 1));
+        h->scan_bytes = sb;
+        h->batch_cap = cap;
+    }
+    if (npar > h->par_cap) {
+        uint64_t cap = std::max<uint64_t>(npar, 4096);
+        if (h->b_par) (void)hipFree(h->b_par);
+        HIPCHK(h, dalloc(&h->b_par, cap));
+        h->par_cap = cap;
+    }
+    return 0;
+}
+
+// column list of this shard + cheater CSR (restricted to owned creators)
+int rebuild_columns(lx_index *h) {
+    std::vector<uint32_t> cols;
+    for (uint32_t b = 0; b < h->B; b++) {
+        uint32_t c = h->h_branch_creator[b];
+        if (c >= h->own_lo && c < h->own_hi) cols.push_back(b);
+    }
+    h->ncols = (uint32_t)cols.size();
+    if (!cols.empty())
+        HIPCHK(h, hipMemcpyAsync(h->col_list, cols.data(), cols.size() * 4, hipMemcpyHostToDevice, h->stream));
+    std::vector<uint32_t> off{0}, br, cr;
+    for (uint32_t c = h->own_lo; c < h->own_hi; c++) {
+        const auto &l = h->by_creator[c];
+        if (l.size() < 2) continue;
+        cr.push_back(c);
+        br.insert(br.end(), l.begin(), l.end());
+        off.push_back((uint32_t)br.size());
+    }
+    h->n_cheat = (uint32_t)cr.size();
+    uint64_t need = std::max<uint64_t>({off.size(), br.size(), 1});
+    if (need > h->cheat_cap) {
+        uint64_t cap = std::max<uint64_t>(need * 2, 256);
+        uint32_t **arrs[] = {&h->cheat_off, &h->cheat_br, &h->cheat_creator};
+        for (uint32_t **a : arrs) {
+            if (*a) (void)hipFree(*a);
+            HIPCHK(h, dalloc(a, cap));
+        }
+        h->cheat_cap = cap;
+    }
+    if (h->n_cheat) {
+        HIPCHK(h, hipMemcpyAsync(h->cheat_off, off.data(), off.size() * 4, hipMemcpyHostToDevice, h->stream));
+        HIPCHK(h, hipMemcpyAsync(h->cheat_br, br.data(), br.size() * 4, hipMemcpyHostToDevice, h->stream));
+        HIPCHK(h, hipMemcpyAsync(h->cheat_creator, cr.data(), cr.size() * 4, hipMemcpyHostToDevice, h->stream));
+    }
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+BatchArgs batch_args(lx_index *h, uint32_t n, const uint32_t *creator, const uint32_t *seq, const uint32_t *poff,
+                     const uint32_t *par) {
+    BatchArgs a{};
+    a.n = n;
+    a.batch_start = (uint32_t)h->n_events;
+    a.V = h->V;
+    a.B0 = h->B;
+    a.creator = creator;
+    a.seq = seq;
+    a.poff = poff;
+    a.par = par;
+    a.ev_creator = h->ev_creator;
+    a.ev_seq = h->ev_seq;
+    a.ev_branch = h->ev_branch;
+    a.ev_bbefore = h->ev_bbefore;
+    a.ev_sp = h->ev_sp;
+    a.first_child = h->first_child;
+    a.first_root = h->first_root;
+    a.branch_first = h->branch_first;
+    a.branch_creator = h->branch_creator;
+    a.branch_len = h->branch_len;
+    a.brow = h->brow;
+    a.s_cap = h->s_cap;
+    a.isfork = h->b_isfork;
+    a.rank = h->b_rank;
+    a.tmp_br = h->b_tmpbr;
+    a.jmp = h->b_jmp;
+    a.rec = h->b_rec;
+    a.status = h->status;
+    return a;
+}
+
+int add_batch_dev(lx_index *h, uint32_t n, const uint32_t *creator, const uint32_t *seq, const uint32_t *poff,
+                  const uint32_t *par, uint32_t *err_index) {
+    if (!h->have_epoch) return h->fail(LX_ERR_STATE, "lx_add_batch before lx_reset");
+    if (n == 0) return 0;
+    if (h->n_events + n >= 0xFFFFFFF0ull) return h->fail(LX_ERR_ARG, "too many events in one epoch");
+    int rc;
+    if ((rc = grow_events(h, h->n_events + n))) return rc;
+    if ((rc = ensure_batch(h, n, 0))) return rc;
+    hipStream_t s = h->stream;
+
+    HIPCHK(h, hipEventRecord(h->ev[0], s));
+    HIPCHK(h, hipMemsetAsync(h->status, 0, kStatusWords * 4, s));
+    HIPCHK(h, hipMemsetAsync(h->status + 8, 0xFF, 8, s));
+    BatchArgs a = batch_args(h, n, creator, seq, poff, par);
+    HIPCHK(h, lx::launch_batch_prepare(a, h->scan_tmp, h->scan_bytes, s));
+    uint32_t st[16];
+    uint32_t nforks = 0;
+    HIPCHK(h, hipMemcpyAsync(st, h->status, sizeof st, hipMemcpyDeviceToHost, s));
+    HIPCHK(h, hipMemcpyAsync(&nforks, h->b_rank + (n - 1), 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(h, hipStreamSynchronize(s));
+    uint64_t e64;
+    memcpy(&e64, st + 8, 8);
+    if (e64 != ~0ull) {
+        HIPCHK(h, lx::launch_undo_claims(a, s));
+        HIPCHK(h, hipStreamSynchronize(s));
+        uint32_t pos = (uint32_t)(e64 >> 8), code = (uint32_t)(e64 & 0xFF);
+        if (err_index) *err_index = pos;
+        if (code == 2) return h->fail(LX_ERR_ORDER, "event %u: processed out of order, parent not found", pos);
+        if (code == 1) return h->fail(LX_ERR_ARG, "event %u: creator idx out of range", pos);
+        return h->fail(LX_ERR_EVENT, "event %u: violates seq/self-parent invariants (eventcheck)", pos);
+    }
+    uint32_t bmax = st[2];
+    uint32_t B_new = h->B + nforks;
+    if ((rc = grow_branches(h, B_new))) return rc;
+    h->max_seq = std::max(h->max_seq, bmax);
+    if ((rc = grow_scap(h, h->max_seq))) return rc;
+    a = batch_args(h, n, creator, seq, poff, par);   // pointers may have moved
+    HIPCHK(h, lx::launch_batch_finish(a, s));
+    if (nforks) {
+        std::vector<uint32_t> cr(nforks), fs(nforks);
+        HIPCHK(h, hipMemcpyAsync(cr.data(), h->branch_creator + h->B, nforks * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(h, hipMemcpyAsync(fs.data(), h->branch_first + h->B, nforks * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(h, hipStreamSynchronize(s));
+        for (uint32_t i = 0; i < nforks; i++) {
+            h->h_branch_creator.push_back(cr[i]);
+            h->h_branch_first.push_back(fs[i]);
+            h->by_creator[cr[i]].push_back(h->B + i);
+        }
+    }
+    h->B = B_new;
+    if (nforks || h->ncols == 0)
+        if ((rc = rebuild_columns(h))) return rc;
+
+    IndexArgs ia{};
+    ia.hb = h->hb;
+    ia.la = h->la;
+    ia.stride = h->stride;
+    ia.batch_start = (uint32_t)h->n_events;
+    ia.n = n;
+    ia.rec = h->b_rec;
+    ia.par_in = par;
+    ia.col_list = h->col_list;
+    ia.ncols = h->ncols;
+    ia.branch_first = h->branch_first;
+    ia.brow = h->brow;
+    ia.s_cap = h->s_cap;
+    ia.mask = (h->B > h->V) ? 1u : 0u;
+    HIPCHK(h, hipEventRecord(h->ev[1], s));
+    HIPCHK(h, lx::launch_index(ia, s));
+    HIPCHK(h, hipEventRecord(h->ev[2], s));
+    if (h->B > h->V && h->n_cheat) {
+        MarkArgs m{};
+        m.hb = h->hb;
+        m.stride = h->stride;
+        m.batch_start = (uint32_t)h->n_events;
+        m.n = n;
+        m.V = h->V;
+        m.ev_branch = h->ev_branch;
+        m.ev_bbefore = h->ev_bbefore;
+        m.branch_first = h->branch_first;
+        m.n_cheat = h->n_cheat;
+        m.cheat_off = h->cheat_off;
+        m.cheat_br = h->cheat_br;
+        HIPCHK(h, lx::launch_marks(m, s));
+    }
+    HIPCHK(h, hipEventRecord(h->ev[3], s));
+    h->n_events += n;
+    h->hwm = std::max(h->hwm, h->n_events);
+    HIPCHK(h, hipStreamSynchronize(s));
+    float t0 = 0, t1 = 0, t2 = 0;
+    HIPCHK(h, hipEventElapsedTime(&t0, h->ev[0], h->ev[1]));
+    HIPCHK(h, hipEventElapsedTime(&t1, h->ev[1], h->ev[2]));
+    HIPCHK(h, hipEventElapsedTime(&t2, h->ev[2], h->ev[3]));
+    h->stats.ms_assign = t0;
+    h->stats.ms_index = t1;
+    h->stats.ms_marks = t2;
+    h->stats.index_launches = 1;
+    return 0;
+}
+
+int fc_args(lx_index *h, uint64_t n, const uint32_t *a, const uint32_t *b, uint8_t *out, uint32_t *partial,
+            FcArgs *fa) {
+    if (!h->have_epoch) return h->fail(LX_ERR_STATE, "ForklessCause before lx_reset");
+    FcArgs f{};
+    f.hb = h->hb;
+    f.la = h->la;
+    f.stride = h->stride;
+    f.n_events = (uint32_t)h->n_events;
+    f.n = n;
+    f.qa = a;
+    f.qb = b;
+    f.out = out;
+    f.partial = partial;
+    f.wpad = h->wpad;
+    f.vlo4 = h->own_lo / 4;
+    f.vhi4 = (h->own_hi + 3) / 4;
+    f.quorum = h->quorum;
+    f.ev_branch = h->ev_branch;
+    f.n_cheat = h->n_cheat;
+    f.cheat_off = h->cheat_off;
+    f.cheat_br = h->cheat_br;
+    f.cheat_creator = h->cheat_creator;
+    f.own_lo = h->own_lo;
+    f.own_hi = h->own_hi;
+    f.branch_creator = h->branch_creator;
+    f.status = h->status;
+    *fa = f;
+    return 0;
+}
+
+int read_u32(lx_index *h, const uint32_t *dev, uint32_t *out) {
+    HIPCHK(h, hipMemcpy(out, dev, 4, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+}  // namespace
+
+// =============================================================================== C ABI
+extern "C" {
+
+int lx_create(const lx_config *cfg, lx_index **out) {
+    if (!out) return LX_ERR_ARG;
+    lx_index *h = new lx_index();
+    if (cfg) {
+        h->device = cfg->device;
+        h->cap_hint = cfg->event_capacity;
+        h->reserve = cfg->branch_reserve;
+        h->shard_rank = cfg->shard_rank;
+        h->shard_count = cfg->shard_count ? cfg->shard_count : 1;
+    }
+    if (h->shard_rank >= h->shard_count) { delete h; return LX_ERR_ARG; }
+    if (hipSetDevice(h->device) != hipSuccess || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc((void **)&h->status, kStatusWords * 4) != hipSuccess) {
+        delete h;
+        return LX_ERR_HIP;
+    }
+    for (auto &e : h->ev)
+        if (hipEventCreate(&e) != hipSuccess) {
+            delete h;
+            return LX_ERR_HIP;
+        }
+    *out = h;
+    return 0;
+}
+
+void lx_destroy(lx_index *h) {
+    if (!h) return;
+    (void)hipSetDevice(h->device);
+    (void)hipStreamSynchronize(h->stream);
+    free_all(h);
+    if (h->status) (void)hipFree(h->status);
+    for (auto &e : h->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (h->stream) (void)hipStreamDestroy(h->stream);
+    delete h;
+}
+
+const char *lx_last_error(const lx_index *h) { return h ? h->err.c_str() : "null handle"; }
+
+int lx_reset(lx_index *h, uint32_t nv, const uint32_t *w) {
+    if (!h || (nv && !w)) return LX_ERR_ARG;
+    if (nv == 0) return h->fail(LX_ERR_ARG, "empty validator set");
+    uint64_t tot = 0;
+    for (uint32_t i = 0; i < nv; i++) {
+        if (w[i] == 0) return h->fail(LX_ERR_ARG, "zero weight at idx %u (builder drops such validators)", i);
+        tot += w[i];
+    }
+    if (tot > 0x7FFFFFFFull) return h->fail(LX_ERR_ARG, "validators weight overflow");   // validators.go:101-110
+    HIPCHK(h, hipSetDevice(h->device));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    h->V = nv;
+    h->weights.assign(w, w + nv);
+    h->quorum = (uint32_t)(tot * 2 / 3 + 1);
+    if (h->shard_count > 1) {
+        auto bound = [&](uint32_t r) { return r == h->shard_count ? nv : (uint32_t)((uint64_t)nv * r / h->shard_count) & ~3u; };
+        h->own_lo = bound(h->shard_rank);
+        h->own_hi = bound(h->shard_rank + 1);
+    } else {
+        h->own_lo = 0;
+        h->own_hi = nv;
+    }
+    uint32_t reserve = h->reserve ? h->reserve : std::max<uint32_t>(64, nv / 16);
+    uint32_t want_stride = round_up(nv + reserve, 64);
+    // (re)allocate when the layout changes; otherwise zero what the last epoch used
+    if (want_stride > h->stride || (h->stride && want_stride * 2 < h->stride)) {
+        free_all(h);
+        h->stride = 0;
+        int rc;
+        h->s_cap = 0;
+        if ((rc = grow_branches(h, want_stride))) return rc;
+        uint32_t s0 = 1024;
+        if (h->cap_hint) s0 = (uint32_t)std::min<uint64_t>(h->cap_hint / nv + 64, 0x7FFFFFFF);
+        if ((rc = grow_scap(h, s0))) return rc;
+        h->hwm = 0;
+        if ((rc = grow_events(h, h->cap_hint ? h->cap_hint : 4096))) return rc;
+    } else if (h->hwm) {
+        HIPCHK(h, hipMemsetAsync(h->hb, 0, h->hwm * h->stride * 4, h->stream));
+        HIPCHK(h, hipMemsetAsync(h->la, 0, h->hwm * h->stride * 4, h->stream));
+        HIPCHK(h, lx::launch_fill_u32(h->first_child, h->hwm, LX_NONE, h->stream));
+        h->hwm = 0;
+    }
+    if (h->first_root) (void)hipFree(h->first_root);
+    HIPCHK(h, dalloc(&h->first_root, nv));
+    HIPCHK(h, lx::launch_fill_u32(h->first_root, nv, LX_NONE, h->stream));
+    std::vector<uint32_t> ones(nv, 1), idx(nv), wp(h->stride, 0);
+    for (uint32_t i = 0; i < nv; i++) idx[i] = i;
+    for (uint32_t i = h->own_lo; i < h->own_hi; i++) wp[i] = w[i];
+    HIPCHK(h, hipMemsetAsync(h->branch_len, 0, (uint64_t)h->stride * 4, h->stream));
+    HIPCHK(h, hipMemcpyAsync(h->branch_first, ones.data(), nv * 4, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(h, hipMemcpyAsync(h->branch_creator, idx.data(), nv * 4, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(h, hipMemcpyAsync(h->wpad, wp.data(), (uint64_t)h->stride * 4, hipMemcpyHostToDevice, h->stream));
+    h->n_events = h->n_flushed = 0;
+    h->B = h->B_flushed = nv;
+    h->max_seq = 0;
+    h->h_branch_creator = idx;
+    h->h_branch_first = ones;
+    h->by_creator.assign(nv, {});
+    for (uint32_t i = 0; i < nv; i++) h->by_creator[i].push_back(i);
+    h->have_epoch = true;
+    h->ncols = 0;
+    return rebuild_columns(h);
+}
+
+int lx_add_batch(lx_index *h, uint32_t n, const uint32_t *creator, const uint32_t *seq, const uint64_t *poff,
+                 const uint32_t *par, uint32_t *out_branch, uint32_t *err_index) {
+    if (!h) return LX_ERR_ARG;
+    if (n == 0) return 0;
+    if (!creator || !seq || !poff) return h->fail(LX_ERR_ARG, "null input");
+    HIPCHK(h, hipSetDevice(h->device));
+    uint64_t base = poff[0], npar = poff[n] - poff[0];
+    if (poff[n] < poff[0] || npar >= 0xFFFFFFFFull) return h->fail(LX_ERR_ARG, "bad parent offsets");
+    std::vector<uint32_t> off(n + 1);
+    for (uint32_t i = 0; i <= n; i++) {
+        if (i && poff[i] < poff[i - 1]) return h->fail(LX_ERR_ARG, "parent offsets not monotone");
+        off[i] = (uint32_t)(poff[i] - base);
+    }
+    int rc;
+    if ((rc = ensure_batch(h, n, npar))) return rc;
+    HIPCHK(h, hipMemcpyAsync(h->b_creator, creator, n * 4ull, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(h, hipMemcpyAsync(h->b_seq, seq, n * 4ull, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(h, hipMemcpyAsync(h->b_poff, off.data(), (n + 1) * 4ull, hipMemcpyHostToDevice, h->stream));
+    if (npar) HIPCHK(h, hipMemcpyAsync(h->b_par, par + base, npar * 4, hipMemcpyHostToDevice, h->stream));
+    uint64_t start = h->n_events;
+    if ((rc = add_batch_dev(h, n, h->b_creator, h->b_seq, h->b_poff, h->b_par, err_index))) return rc;
+    if (out_branch) HIPCHK(h, hipMemcpy(out_branch, h->ev_branch + start, n * 4ull, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int lx_add_batch_dev(lx_index *h, uint32_t n, const uint32_t *creator, const uint32_t *seq, const uint32_t *poff,
+                     const uint32_t *par, uint32_t *err_index) {
+    if (!h) return LX_ERR_ARG;
+    HIPCHK(h, hipSetDevice(h->device));
+    return add_batch_dev(h, n, creator, seq, poff, par, err_index);
+}
+
+int lx_flush(lx_index *h) {
+    if (!h) return LX_ERR_ARG;
+    h->n_flushed = h->n_events;
+    h->B_flushed = h->B;
+    return 0;
+}
+
+int lx_drop_not_flushed(lx_index *h) {
+    if (!h) return LX_ERR_ARG;
+    if (!h->have_epoch) return 0;
+    HIPCHK(h, hipSetDevice(h->device));
+    if (h->n_events == h->n_flushed && h->B == h->B_flushed) return 0;
+    UnfillArgs u{};
+    u.hb = h->hb;
+    u.la = h->la;
+    u.stride = h->stride;
+    u.lo = (uint32_t)h->n_flushed;
+    u.hi = (uint32_t)h->n_events;
+    u.B = h->B;
+    u.ev_seq = h->ev_seq;
+    u.ev_branch = h->ev_branch;
+    u.ev_bbefore = h->ev_bbefore;
+    u.ev_sp = h->ev_sp;
+    u.ev_creator = h->ev_creator;
+    u.first_child = h->first_child;
+    u.first_root = h->first_root;
+    u.branch_len = h->branch_len;
+    u.branch_first = h->branch_first;
+    u.brow = h->brow;
+    u.s_cap = h->s_cap;
+    u.B_keep = h->B_flushed;
+    HIPCHK(h, lx::launch_unfill(u, h->stream));
+    uint64_t rows = h->n_events - h->n_flushed;
+    if (rows) {
+        HIPCHK(h, hipMemsetAsync(h->hb + h->n_flushed * h->stride, 0, rows * h->stride * 4, h->stream));
+        HIPCHK(h, hipMemsetAsync(h->la + h->n_flushed * h->stride, 0, rows * h->stride * 4, h->stream));
+    }
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    h->n_events = h->n_flushed;
+    if (h->B != h->B_flushed) {
+        h->B = h->B_flushed;
+        h->h_branch_creator.resize(h->B);
+        h->h_branch_first.resize(h->B);
+        for (auto &l : h->by_creator)
+            while (!l.empty() && l.back() >= h->B) l.pop_back();
+        return rebuild_columns(h);
+    }
+    return 0;
+}
+
+uint64_t lx_num_events(const lx_index *h) { return h ? h->n_events : 0; }
+uint32_t lx_num_branches(const lx_index *h) { return h ? h->B : 0; }
+int lx_at_least_one_fork(const lx_index *h) { return h && h->B > h->V; }
+uint32_t lx_quorum(const lx_index *h) { return h ? h->quorum : 0; }
+
+int lx_forkless_cause_batch_dev(lx_index *h, uint64_t n, const uint32_t *a, const uint32_t *b, uint8_t *out,
+                                void *stream) {
+    if (!h) return LX_ERR_ARG;
+    if (!n) return 0;
+    FcArgs f;
+    int rc = fc_args(h, n, a, b, out, nullptr, &f);
+    if (rc) return rc;
+    hipStream_t s = stream ? (hipStream_t)stream : h->stream;
+    HIPCHK(h, lx::launch_fc(f, h->ncols, h->B > h->V, s));
+    return 0;
+}
+
+int lx_forkless_cause_partial_dev(lx_index *h, uint64_t n, const uint32_t *a, const uint32_t *b, uint32_t *partial,
+                                  void *stream) {
+    if (!h) return LX_ERR_ARG;
+    if (!n) return 0;
+    FcArgs f;
+    int rc = fc_args(h, n, a, b, nullptr, partial, &f);
+    if (rc) return rc;
+    hipStream_t s = stream ? (hipStream_t)stream : h->stream;
+    HIPCHK(h, lx::launch_fc(f, h->ncols, h->B > h->V, s));
+    return 0;
+}
+
+int lx_fc_combine_dev(lx_index *h, uint64_t n, const uint32_t *sum, uint8_t *out, void *stream) {
+    if (!h) return LX_ERR_ARG;
+    hipStream_t s = stream ? (hipStream_t)stream : h->stream;
+    HIPCHK(h, lx::launch_fc_combine(sum, out, n, h->quorum, s));
+    return 0;
+}
+
+int lx_forkless_cause_batch(lx_index *h, uint64_t n, const uint32_t *a, const uint32_t *b, uint8_t *out) {
+    if (!h) return LX_ERR_ARG;
+    if (!n) return 0;
+    HIPCHK(h, hipSetDevice(h->device));
+    if (n > h->q_cap) {
+        uint64_t cap = std::max<uint64_t>(n, 4096);
+        if (h->q_a) (void)hipFree(h->q_a);
+        if (h->q_b) (void)hipFree(h->q_b);
+        if (h->q_out) (void)hipFree(h->q_out);
+        HIPCHK(h, dalloc(&h->q_a, cap));
+        HIPCHK(h, dalloc(&h->q_b, cap));
+        HIPCHK(h, dalloc(&h->q_out, cap));
+        h->q_cap = cap;
+    }
+    HIPCHK(h, hipMemsetAsync(h->status + 1, 0, 4, h->stream));
+    HIPCHK(h, hipMemcpyAsync(h->q_a, a, n * 4, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(h, hipMemcpyAsync(h->q_b, b, n * 4, hipMemcpyHostToDevice, h->stream));
+    int rc = lx_forkless_cause_batch_dev(h, n, h->q_a, h->q_b, h->q_out, nullptr);
+    if (rc) return rc;
+    uint32_t bad = 0;
+    HIPCHK(h, hipMemcpyAsync(out, h->q_out, n, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipMemcpyAsync(&bad, h->status + 1, 4, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    if (bad) return h->fail(LX_ERR_ARG, "ForklessCause on an unknown event");   // forkless_cause.go:43-61 (crit)
+    return 0;
+}
+
+int lx_get_event_branch_id(lx_index *h, uint32_t ev, uint32_t *out) {
+    if (!h || !out) return LX_ERR_ARG;
+    if (ev >= h->n_events) return h->fail(LX_ERR_ARG, "failed to read event's branch ID (unknown event %u)", ev);
+    HIPCHK(h, hipSetDevice(h->device));
+    return read_u32(h, h->ev_branch + ev, out);
+}
+
+static int event_row(lx_index *h, const uint32_t *plane, uint32_t ev, std::vector<uint32_t> &row, uint32_t *bbefore,
+                     uint32_t *branch) {
+    if (ev >= h->n_events) return h->fail(LX_ERR_ARG, "unknown event %u", ev);
+    HIPCHK(h, hipSetDevice(h->device));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    row.resize(h->B);
+    HIPCHK(h, hipMemcpy(row.data(), plane + (uint64_t)ev * h->stride, h->B * 4ull, hipMemcpyDeviceToHost));
+    int rc;
+    if ((rc = read_u32(h, h->ev_bbefore + ev, bbefore))) return rc;
+    return read_u32(h, h->ev_branch + ev, branch);
+}
+
+static int put_bytes(uint8_t *out, uint32_t cap, uint32_t *len, const std::vector<uint32_t> &words) {
+    uint32_t nbytes = (uint32_t)words.size() * 4;
+    if (len) *len = nbytes;
+    if (out && cap) memcpy(out, words.data(), std::min(cap, nbytes));   // little-endian host
+    return 0;
+}
+
+// HighestBeforeSeq bytes (vecfc/vector.go:63-102): length 8*max(B_before, last
+// non-empty + 1); MinSeq is the branch's first seq.
+static void encode_hb(lx_index *h, const std::vector<uint32_t> &row, uint32_t bb, uint32_t bafter,
+                      std::vector<uint32_t> &w) {
+    uint32_t n = bb;
+    for (uint32_t c = 0; c < bafter && c < row.size(); c++)
+        if (row[c]) n = std::max(n, c + 1);
+    w.assign(2 * n, 0);
+    for (uint32_t c = 0; c < n && c < bafter; c++) {
+        uint32_t v = row[c];
+        if (v & LX_MARK) { w[2 * c] = 0; w[2 * c + 1] = 0x7FFFFFFF; }
+        else if (v) { w[2 * c] = v; w[2 * c + 1] = h->h_branch_first[c]; }
+    }
+}
+
+int lx_get_highest_before(lx_index *h, uint32_t ev, uint8_t *out, uint32_t cap, uint32_t *len) {
+    if (!h) return LX_ERR_ARG;
+    std::vector<uint32_t> row, w;
+    uint32_t bb, br;
+    int rc = event_row(h, h->hb, ev, row, &bb, &br);
+    if (rc) return rc;
+    encode_hb(h, row, bb, bb + (br == bb ? 1 : 0), w);
+    return put_bytes(out, cap, len, w);
+}
+
+int lx_get_lowest_after(lx_index *h, uint32_t ev, uint8_t *out, uint32_t cap, uint32_t *len) {
+    if (!h) return LX_ERR_ARG;
+    std::vector<uint32_t> row;
+    uint32_t bb, br;
+    int rc = event_row(h, h->la, ev, row, &bb, &br);
+    if (rc) return rc;
+    uint32_t n = bb;
+    for (uint32_t c = 0; c < row.size(); c++)
+        if (row[c]) n = std::max(n, c + 1);
+    row.resize(n, 0);
+    return put_bytes(out, cap, len, row);
+}
+
+// GetMergedHighestBefore (vecengine/index.go:235-250) with GatherFrom
+// (vecfc/vector_ops.go:81-96): first marked branch wins, else strictly
+// greatest Seq (first max wins).
+int lx_get_merged_highest_before(lx_index *h, uint32_t ev, uint8_t *out, uint32_t cap, uint32_t *len) {
+    if (!h) return LX_ERR_ARG;
+    if (h->B <= h->V) return lx_get_highest_before(h, ev, out, cap, len);
+    std::vector<uint32_t> row, w, m(2 * h->V, 0);
+    uint32_t bb, br;
+    int rc = event_row(h, h->hb, ev, row, &bb, &br);
+    if (rc) return rc;
+    encode_hb(h, row, bb, bb + (br == bb ? 1 : 0), w);
+    uint32_t nb = (uint32_t)w.size() / 2;
+    for (uint32_t c = 0; c < h->V; c++) {
+        uint32_t bs = 0, bm = 0;
+        for (uint32_t b : h->by_creator[c]) {
+            uint32_t s = b < nb ? w[2 * b] : 0, mm = b < nb ? w[2 * b + 1] : 0;
+            if (s == 0 && mm == 0x7FFFFFFF) { bs = s; bm = mm; break; }
+            if (s > bs) { bs = s; bm = mm; }
+        }
+        m[2 * c] = bs;
+        m[2 * c + 1] = bm;
+    }
+    return put_bytes(out, cap, len, m);
+}
+
+int lx_get_branches_info(lx_index *h, uint32_t *last_seq, uint32_t *creator_idx, uint32_t cap, uint32_t *n_branches) {
+    if (!h) return LX_ERR_ARG;
+    if (n_branches) *n_branches = h->B;
+    if (!cap) return 0;
+    HIPCHK(h, hipSetDevice(h->device));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    std::vector<uint32_t> len(h->B);
+    HIPCHK(h, hipMemcpy(len.data(), h->branch_len, h->B * 4ull, hipMemcpyDeviceToHost));
+    for (uint32_t b = 0; b < h->B && b < cap; b++) {
+        if (last_seq) last_seq[b] = len[b] ? h->h_branch_first[b] + len[b] - 1 : 0;
+        if (creator_idx) creator_idx[b] = h->h_branch_creator[b];
+    }
+    return 0;
+}
+
+int lx_last_stats(const lx_index *h, lx_stats *out) {
+    if (!h || !out) return LX_ERR_ARG;
+    *out = h->stats;
+    return 0;
+}
+
+int lx_device_planes(lx_index *h, void **hb, void **la, uint32_t *stride, void **stream) {
+    if (!h) return LX_ERR_ARG;
+    if (hb) *hb = h->hb;
+    if (la) *la = h->la;
+    if (stride) *stride = h->stride;
+    if (stream) *stream = h->stream;
+    return 0;
+}
+
+int lx_sync(lx_index *h) {
+    if (!h) return LX_ERR_ARG;
+    HIPCHK(h, hipSetDevice(h->device));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    uint32_t bad = 0;
+    HIPCHK(h, hipMemcpy(&bad, h->status + 1, 4, hipMemcpyDeviceToHost));
+    if (bad) {
+        HIPCHK(h, hipMemset(h->status + 1, 0, 4));
+        return h->fail(LX_ERR_ARG, "ForklessCause on an unknown event");
+    }
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,19 @@
+"""Python mirror of the reference's vecfc.Index API over the HIP C ABI.
+
+``lachesis-base_amd/build/liblachesis_hip.so`` (include/lachesis_hip.h) is
+the product; this package is a thin ctypes layer used by tests and the bench,
+shaped like the reference's Go API so the parity tests read like
+vecfc/forkless_cause_test.go:
+
+* :class:`Index`      -- dense-index handle (what a cgo shim binds 1:1)
+* :class:`VecfcIndex` -- hash-keyed facade: ``reset(validators, get_event)``,
+  ``add(e)``, ``flush()``, ``drop_not_flushed()``, ``forkless_cause(a, b)``,
+  ``get_highest_before(id)`` ... (vecfc/index.go, vecfc/forkless_cause.go)
+
+There is no CPU fallback: importing this package on a machine without the
+built library raises, and every compute call goes to the GPU.
+"""
+
+from .capi import Index, LxError, load_library  # noqa: F401
+from .vecfc import VecfcIndex, HighestBeforeSeq, LowestAfterSeq, BranchSeq  # noqa: F401
+from . import tools  # noqa: F401

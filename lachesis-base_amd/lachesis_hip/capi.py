@@ -1,0 +1,221 @@
+"""ctypes binding of include/lachesis_hip.h (dense event indices)."""
+
+import ctypes
+import os
+
+import numpy as np
+
+_PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(_PKG, "build", "liblachesis_hip.so")
+_lib = None
+
+u8p = ctypes.POINTER(ctypes.c_uint8)
+u32p = ctypes.POINTER(ctypes.c_uint32)
+u64p = ctypes.POINTER(ctypes.c_uint64)
+vp = ctypes.c_void_p
+
+# (name, restype, argtypes) for every entry point of include/lachesis_hip.h
+SIGNATURES = [
+    ("lx_create", ctypes.c_int, [vp, ctypes.POINTER(vp)]),
+    ("lx_destroy", None, [vp]),
+    ("lx_last_error", ctypes.c_char_p, [vp]),
+    ("lx_reset", ctypes.c_int, [vp, ctypes.c_uint32, u32p]),
+    ("lx_add_batch", ctypes.c_int, [vp, ctypes.c_uint32, u32p, u32p, u64p, u32p, u32p, u32p]),
+    ("lx_add_batch_dev", ctypes.c_int, [vp, ctypes.c_uint32, vp, vp, vp, vp, u32p]),
+    ("lx_flush", ctypes.c_int, [vp]),
+    ("lx_drop_not_flushed", ctypes.c_int, [vp]),
+    ("lx_num_events", ctypes.c_uint64, [vp]),
+    ("lx_num_branches", ctypes.c_uint32, [vp]),
+    ("lx_at_least_one_fork", ctypes.c_int, [vp]),
+    ("lx_forkless_cause_batch", ctypes.c_int, [vp, ctypes.c_uint64, u32p, u32p, u8p]),
+    ("lx_forkless_cause_batch_dev", ctypes.c_int, [vp, ctypes.c_uint64, vp, vp, vp, vp]),
+    ("lx_forkless_cause_partial_dev", ctypes.c_int, [vp, ctypes.c_uint64, vp, vp, vp, vp]),
+    ("lx_fc_combine_dev", ctypes.c_int, [vp, ctypes.c_uint64, vp, vp, vp]),
+    ("lx_quorum", ctypes.c_uint32, [vp]),
+    ("lx_get_highest_before", ctypes.c_int, [vp, ctypes.c_uint32, u8p, ctypes.c_uint32, u32p]),
+    ("lx_get_lowest_after", ctypes.c_int, [vp, ctypes.c_uint32, u8p, ctypes.c_uint32, u32p]),
+    ("lx_get_merged_highest_before", ctypes.c_int, [vp, ctypes.c_uint32, u8p, ctypes.c_uint32, u32p]),
+    ("lx_get_event_branch_id", ctypes.c_int, [vp, ctypes.c_uint32, u32p]),
+    ("lx_get_branches_info", ctypes.c_int, [vp, u32p, u32p, ctypes.c_uint32, u32p]),
+    ("lx_last_stats", ctypes.c_int, [vp, vp]),
+    ("lx_device_planes", ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), u32p, ctypes.POINTER(vp)]),
+    ("lx_sync", ctypes.c_int, [vp]),
+]
+
+
+class LxConfig(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int), ("event_capacity", ctypes.c_uint64),
+                ("branch_reserve", ctypes.c_uint32), ("shard_rank", ctypes.c_uint32),
+                ("shard_count", ctypes.c_uint32)]
+
+
+class LxStats(ctypes.Structure):
+    _fields_ = [("ms_assign", ctypes.c_float), ("ms_index", ctypes.c_float),
+                ("ms_marks", ctypes.c_float), ("index_launches", ctypes.c_uint32)]
+
+
+class LxError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("lachesis_hip error %d: %s" % (code, msg))
+        self.code = code
+
+
+def load_library(path=LIB_PATH):
+    """Load the HIP library; raises if it is missing (no fallback path)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(path):
+            raise ImportError("HIP library not built: %s (run __graft_entry__.build())" % path)
+        L = ctypes.CDLL(path)
+        for name, res, args in SIGNATURES:
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _p(a, t):
+    return a.ctypes.data_as(t)
+
+
+def _u32(a):
+    return np.ascontiguousarray(a, dtype=np.uint32)
+
+
+class Index:
+    """Dense-index handle over lx_* (one GPU, one epoch at a time)."""
+
+    def __init__(self, device=0, event_capacity=0, branch_reserve=0, shard_rank=0, shard_count=1):
+        self.L = load_library()
+        cfg = LxConfig(device, event_capacity, branch_reserve, shard_rank, shard_count)
+        h = vp()
+        rc = self.L.lx_create(ctypes.byref(cfg), ctypes.byref(h))
+        if rc != 0:
+            raise LxError(rc, "lx_create failed (device %d)" % device)
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.lx_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def _chk(self, rc):
+        if rc != 0:
+            raise LxError(rc, self.L.lx_last_error(self.h).decode())
+        return rc
+
+    # lifecycle ---------------------------------------------------------------
+    def reset(self, weights_by_idx):
+        w = _u32(weights_by_idx)
+        self._chk(self.L.lx_reset(self.h, len(w), _p(w, u32p)))
+
+    def add_batch(self, creator_idx, seq, parent_off, parent_idx, want_branches=False):
+        creator_idx = _u32(creator_idx)
+        seq = _u32(seq)
+        off = np.ascontiguousarray(parent_off, dtype=np.uint64)
+        par = _u32(parent_idx) if len(parent_idx) else np.zeros(1, dtype=np.uint32)
+        n = len(creator_idx)
+        out = np.zeros(n, dtype=np.uint32) if want_branches else None
+        err = ctypes.c_uint32(0xFFFFFFFF)
+        rc = self.L.lx_add_batch(self.h, n, _p(creator_idx, u32p), _p(seq, u32p), _p(off, u64p),
+                                 _p(par, u32p), _p(out, u32p) if out is not None else None,
+                                 ctypes.byref(err))
+        if rc != 0:
+            e = LxError(rc, self.L.lx_last_error(self.h).decode())
+            e.index = err.value
+            raise e
+        return out
+
+    def add_batch_dev(self, n, creator_ptr, seq_ptr, poff_ptr, par_ptr):
+        err = ctypes.c_uint32(0xFFFFFFFF)
+        rc = self.L.lx_add_batch_dev(self.h, n, creator_ptr, seq_ptr, poff_ptr, par_ptr, ctypes.byref(err))
+        self._chk(rc)
+
+    def add(self, creator_idx, seq, parents):
+        return int(self.add_batch([creator_idx], [seq], [0, len(parents)], list(parents), True)[0])
+
+    def flush(self):
+        self._chk(self.L.lx_flush(self.h))
+
+    def drop_not_flushed(self):
+        self._chk(self.L.lx_drop_not_flushed(self.h))
+
+    def num_events(self):
+        return self.L.lx_num_events(self.h)
+
+    def num_branches(self):
+        return self.L.lx_num_branches(self.h)
+
+    def at_least_one_fork(self):
+        return bool(self.L.lx_at_least_one_fork(self.h))
+
+    def quorum(self):
+        return self.L.lx_quorum(self.h)
+
+    # queries -----------------------------------------------------------------
+    def forkless_cause_batch(self, a, b):
+        a = _u32(a)
+        b = _u32(b)
+        out = np.zeros(len(a), dtype=np.uint8)
+        if len(a):
+            self._chk(self.L.lx_forkless_cause_batch(self.h, len(a), _p(a, u32p), _p(b, u32p), _p(out, u8p)))
+        return out
+
+    def forkless_cause(self, a, b):
+        return bool(self.forkless_cause_batch([a], [b])[0])
+
+    def forkless_cause_batch_dev(self, n, a_ptr, b_ptr, out_ptr, stream=None):
+        self._chk(self.L.lx_forkless_cause_batch_dev(self.h, n, a_ptr, b_ptr, out_ptr, stream))
+
+    def forkless_cause_partial_dev(self, n, a_ptr, b_ptr, partial_ptr, stream=None):
+        self._chk(self.L.lx_forkless_cause_partial_dev(self.h, n, a_ptr, b_ptr, partial_ptr, stream))
+
+    def fc_combine_dev(self, n, sum_ptr, out_ptr, stream=None):
+        self._chk(self.L.lx_fc_combine_dev(self.h, n, sum_ptr, out_ptr, stream))
+
+    def sync(self):
+        self._chk(self.L.lx_sync(self.h))
+
+    def _bytes(self, f, ev):
+        n = ctypes.c_uint32()
+        self._chk(f(self.h, ev, None, 0, ctypes.byref(n)))
+        buf = (ctypes.c_uint8 * max(n.value, 1))()
+        self._chk(f(self.h, ev, buf, n.value, ctypes.byref(n)))
+        return bytes(buf[:n.value])
+
+    def highest_before(self, ev):
+        return self._bytes(self.L.lx_get_highest_before, ev)
+
+    def lowest_after(self, ev):
+        return self._bytes(self.L.lx_get_lowest_after, ev)
+
+    def merged_highest_before(self, ev):
+        return self._bytes(self.L.lx_get_merged_highest_before, ev)
+
+    def branch(self, ev):
+        out = ctypes.c_uint32()
+        self._chk(self.L.lx_get_event_branch_id(self.h, ev, ctypes.byref(out)))
+        return out.value
+
+    def branches_info(self):
+        n = ctypes.c_uint32()
+        self._chk(self.L.lx_get_branches_info(self.h, None, None, 0, ctypes.byref(n)))
+        ls = np.zeros(n.value, dtype=np.uint32)
+        cr = np.zeros(n.value, dtype=np.uint32)
+        self._chk(self.L.lx_get_branches_info(self.h, _p(ls, u32p), _p(cr, u32p), n.value, ctypes.byref(n)))
+        return ls, cr
+
+    def last_stats(self):
+        st = LxStats()
+        self._chk(self.L.lx_last_stats(self.h, ctypes.byref(st)))
+        return {"ms_assign": st.ms_assign, "ms_index": st.ms_index, "ms_marks": st.ms_marks}
+
+    def device_planes(self):
+        hb, la, st = vp(), vp(), vp()
+        stride = ctypes.c_uint32()
+        self._chk(self.L.lx_device_planes(self.h, ctypes.byref(hb), ctypes.byref(la), ctypes.byref(stride),
+                                          ctypes.byref(st)))
+        return hb.value, la.value, stride.value, st.value

@@ -1,0 +1,178 @@
+"""Hash-keyed facade with the reference's vecfc.Index surface.
+
+Mirrors what the cgo shim of INTEGRATION.md does in Go: it keeps the
+event-ID -> dense-index map and forwards to the C ABI.  Method names follow
+vecfc/index.go, vecfc/forkless_cause.go and vecengine/index.go; error
+behaviour follows the reference (``crit`` for unknown events, ``add`` raises
+for out-of-order parents, vecengine/index.go:159-161).
+"""
+
+import struct
+
+from .capi import Index
+
+MAX_INT32 = 0x7FFFFFFF
+
+
+class BranchSeq(tuple):
+    """vecfc.BranchSeq {Seq, MinSeq} (vecfc/vector.go:21-25)."""
+
+    def __new__(cls, seq, min_seq):
+        return super().__new__(cls, (seq, min_seq))
+
+    @property
+    def seq(self):
+        return self[0]
+
+    @property
+    def min_seq(self):
+        return self[1]
+
+    def is_fork_detected(self):                       # vector.go:99-102
+        return self[0] == 0 and self[1] == MAX_INT32
+
+
+class HighestBeforeSeq:
+    """Byte-encoded HighestBefore vector (vecfc/vector.go:63-90)."""
+
+    def __init__(self, raw):
+        self.raw = bytes(raw)
+
+    def size(self):
+        return len(self.raw) // 8
+
+    def get(self, i):
+        if i >= self.size():
+            return BranchSeq(0, 0)
+        return BranchSeq(*struct.unpack_from("<II", self.raw, 8 * i))
+
+    def to_bytes(self):
+        return self.raw
+
+
+class LowestAfterSeq:
+    """Byte-encoded LowestAfter vector (vecfc/vector.go:39-61)."""
+
+    def __init__(self, raw):
+        self.raw = bytes(raw)
+
+    def size(self):
+        return len(self.raw) // 4
+
+    def get(self, i):
+        if i >= self.size():
+            return 0
+        return struct.unpack_from("<I", self.raw, 4 * i)[0]
+
+    def to_bytes(self):
+        return self.raw
+
+
+class VecfcIndex:
+    """vecfc.Index over the HIP library.  ``validators`` needs ``ids``,
+    ``weights`` (idx order) and ``idxs`` (ValidatorID -> idx)."""
+
+    def __init__(self, device=0, event_capacity=0, crit=None):
+        self.ix = Index(device=device, event_capacity=event_capacity)
+        self.crit = crit or self._panic
+        self.pos = {}
+        self.ids = []
+        self.n_flushed = 0
+
+    @staticmethod
+    def _panic(err):
+        raise err
+
+    # vecfc/index.go:98-105
+    def reset(self, validators, get_event=None):
+        self.validators = validators
+        self.get_event = get_event
+        self.ix.reset(validators.weights)
+        self.pos = {}
+        self.ids = []
+        self.n_flushed = 0
+
+    # vecengine/index.go:71-75
+    def add(self, e):
+        parents = []
+        for p in e.parents:
+            if p not in self.pos:
+                raise ValueError("processed out of order, parent not found (inconsistent DB), parent=%r" % (p,))
+            parents.append(self.pos[p])
+        self.ix.add(self.validators.idxs[e.creator], e.seq, parents)
+        self.pos[e.id] = len(self.ids)
+        self.ids.append(e.id)
+
+    def add_events(self, events):
+        """Batched Add of many events (same result as add() one by one)."""
+        import numpy as np
+        base = len(self.ids)
+        local = {e.id: base + k for k, e in enumerate(events)}
+        creator, seq, off, flat = [], [], [0], []
+        for e in events:
+            creator.append(self.validators.idxs[e.creator])
+            seq.append(e.seq)
+            for p in e.parents:
+                q = self.pos.get(p, local.get(p))
+                if q is None:
+                    raise ValueError("processed out of order, parent not found, parent=%r" % (p,))
+                flat.append(q)
+            off.append(len(flat))
+        self.ix.add_batch(creator, seq, np.array(off, dtype=np.uint64), flat)
+        for e in events:
+            self.pos[e.id] = len(self.ids)
+            self.ids.append(e.id)
+
+    # vecengine/index.go:78-96
+    def flush(self):
+        self.ix.flush()
+        self.n_flushed = len(self.ids)
+
+    def drop_not_flushed(self):
+        self.ix.drop_not_flushed()
+        for eid in self.ids[self.n_flushed:]:
+            del self.pos[eid]
+        del self.ids[self.n_flushed:]
+
+    def _idx(self, eid):
+        return self.pos.get(eid)
+
+    # vecfc/forkless_cause.go:28-38
+    def forkless_cause(self, a_id, b_id):
+        a, b = self._idx(a_id), self._idx(b_id)
+        if a is None or b is None:
+            self.crit(RuntimeError("Event A=%r or B=%r not found" % (a_id, b_id)))
+            return False
+        return self.ix.forkless_cause(a, b)
+
+    # vecfc/store_vectors.go:26-51 (nil if unknown)
+    def get_highest_before(self, eid):
+        i = self._idx(eid)
+        return None if i is None else HighestBeforeSeq(self.ix.highest_before(i))
+
+    def get_lowest_after(self, eid):
+        i = self._idx(eid)
+        return None if i is None else LowestAfterSeq(self.ix.lowest_after(i))
+
+    # vecfc/index.go:143-145
+    def get_merged_highest_before(self, eid):
+        i = self._idx(eid)
+        return None if i is None else HighestBeforeSeq(self.ix.merged_highest_before(i))
+
+    # vecengine/store_branches_info.go:83-88
+    def get_event_branch_id(self, eid):
+        i = self._idx(eid)
+        if i is None:
+            self.crit(RuntimeError("failed to read event's branch ID (inconsistent DB)"))
+            return 0
+        return self.ix.branch(i)
+
+    def at_least_one_fork(self):
+        return self.ix.at_least_one_fork()
+
+    def branches_info(self):
+        last_seq, creators = self.ix.branches_info()
+        by = [[] for _ in range(len(self.validators.weights))]
+        for b, c in enumerate(creators):
+            by[int(c)].append(b)
+        return list(map(int, last_seq)), list(map(int, creators)), by

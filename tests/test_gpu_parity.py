@@ -1,0 +1,337 @@
+"""Parity of the HIP path with the oracle (run on an MI355X: pytest -m gpu).
+
+Every test calls the product through the C ABI (lachesis_hip over
+liblachesis_hip.so) and compares with the CPU oracle on the same seeded input:
+bit-exact HB / LA bytes, branch IDs, merged HB and ForklessCause booleans.
+"""
+
+import numpy as np
+import pytest
+
+from oracle import corc, pos, tdag
+from oracle import vecfc_oracle as vo
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def lx():
+    import lachesis_hip
+    return lachesis_hip
+
+
+def oracle_for(dag, weights, flush_each=False):
+    o = corc.OracleIndex(weights)
+    r = o.add_batch(dag.creator, dag.seq, dag.poff, dag.par, flush_each=flush_each)
+    assert r == -1
+    return o
+
+
+def compare_rows(ix, o, events, check_merged=True):
+    for i in events:
+        i = int(i)
+        assert ix.highest_before(i) == o.hb(i), ("hb", i)
+        assert ix.lowest_after(i) == o.la(i), ("la", i)
+        assert ix.branch(i) == o.branch(i), ("branch", i)
+        if check_merged:
+            assert ix.merged_highest_before(i) == o.merged_hb(i), ("merged", i)
+
+
+# ---------------------------------------------------------------- golden tables
+@pytest.mark.parametrize("case", ["classic_step3", "classic_step4", "classic_step5", "random_80"])
+@pytest.mark.parametrize("batched", [False, True])
+def test_golden_forkless_cause(lx, golden, case, batched):
+    """TestForklessCausedClassic / TestForklessCausedRandom through the HIP path."""
+    c = next(x for x in golden["fc_cases"] if x["name"] == case)
+    nodes, _, names, ordered = tdag.ascii_scheme_for_each(c["scheme"])
+    validators = pos.Validators.equal(nodes, 1)
+    ix = lx.VecfcIndex()
+    ix.reset(validators)
+    if batched:
+        ix.add_events(ordered)
+    else:
+        for e in ordered:
+            ix.add(e)
+            ix.flush()
+    for who, e1 in names.items():
+        for whom, e2 in names.items():
+            assert ix.forkless_cause(e1.id, e2.id) == (whom in c["fc"][who]), (who, whom)
+
+
+def test_golden_bench15_rows(lx, golden):
+    c = next(x for x in golden["fc_cases"] if x["name"] == "bench_15")
+    nodes, _, names, ordered = tdag.ascii_scheme_for_each(c["scheme"])
+    validators = pos.Validators.equal(nodes, 1)
+    store = {e.id: e for e in ordered}
+    py = vo.Index()
+    py.reset(validators, store.get)
+    ix = lx.VecfcIndex()
+    ix.reset(validators)
+    for e in ordered:
+        py.add(e)
+        ix.add(e)
+    for e in ordered:
+        assert ix.get_highest_before(e.id).to_bytes() == py.get_highest_before(e.id).to_bytes()
+        assert ix.get_lowest_after(e.id).to_bytes() == py.get_lowest_after(e.id).to_bytes()
+        for f in ordered:
+            assert ix.forkless_cause(e.id, f.id) == py.forkless_cause(e.id, f.id)
+
+
+# ---------------------------------------------------------------- random fork DAGs
+FORK_SHAPES = [
+    # nodes, events/node, parents, cheaters, forks, seed
+    (1, 10, 1, 1, 3, 0), (2, 10, 1, 1, 3, 1), (2, 10, 2, 2, 20, 2), (10, 10, 4, 1, 3, 3),
+    (10, 10, 4, 10, 3, 4), (20, 5, 4, 10, 2, 5), (40, 3, 4, 10, 1, 6), (5, 30, 4, 2, 30, 7),
+    (8, 60, 4, 3, 30, 8), (30, 40, 6, 5, 8, 9), (64, 20, 8, 6, 6, 10), (100, 12, 10, 10, 10, 11),
+]
+
+
+@pytest.mark.parametrize("shape", FORK_SHAPES)
+def test_fork_dag_rows_and_fc(lx, shape):
+    n, ev, p, ch, fk, seed = shape
+    d = lx.tools.gen_dag(n, ev, p, ch, fk, seed)
+    rng = np.random.default_rng(seed)
+    weights = sorted((int(x) for x in rng.integers(1, 9, n)), reverse=True)
+    o = oracle_for(d, weights)
+    ix = lx.Index()
+    ix.reset(weights)
+    br = ix.add_batch(d.creator, d.seq, d.poff, d.par, want_branches=True)
+    assert ix.num_branches() == o.num_branches()
+    assert [int(x) for x in br] == [o.branch(i) for i in range(len(d))]
+    compare_rows(ix, o, range(len(d)))
+    N = len(d)
+    a = np.repeat(np.arange(N, dtype=np.uint32), N)
+    b = np.tile(np.arange(N, dtype=np.uint32), N)
+    if len(a) > 400_000:
+        sel = rng.choice(len(a), 400_000, replace=False)
+        a, b = a[sel], b[sel]
+    np.testing.assert_array_equal(ix.forkless_cause_batch(a, b), o.forkless_cause_batch(a, b))
+    ls, cr = ix.branches_info()
+    assert len(ls) == o.num_branches()
+
+
+@pytest.mark.parametrize("chunk", [1, 7, 64, 1000])
+def test_batching_is_bit_exact(lx, chunk):
+    """lx_add_batch over any split equals per-event Add (fork-heavy DAG)."""
+    d = lx.tools.gen_dag(12, 40, 5, cheaters=4, forks=8, seed=21)
+    w = [1] * 12
+    o = oracle_for(d, w)
+    ix = lx.Index()
+    ix.reset(w)
+    N = len(d)
+    for lo in range(0, N, chunk):
+        hi = min(N, lo + chunk)
+        ix.add_batch(d.creator[lo:hi], d.seq[lo:hi], d.poff[lo:hi + 1], d.par)
+    compare_rows(ix, o, range(N))
+
+
+def test_drop_not_flushed_rollback(lx):
+    """Rollback to the last flush undoes new rows, LA entries set in old rows,
+    fork branches and branch claims; re-adding reproduces the oracle."""
+    d = lx.tools.gen_dag(10, 30, 4, cheaters=3, forks=6, seed=5)
+    w = list(range(10, 0, -1))
+    N = len(d)
+    o = oracle_for(d, w)
+    ix = lx.Index()
+    ix.reset(w)
+    cut = N // 3
+    ix.add_batch(d.creator[:cut], d.seq[:cut], d.poff[:cut + 1], d.par)
+    ix.flush()
+    B_flushed = ix.num_branches()
+    o2 = corc.OracleIndex(w)
+    o2.add_batch(d.creator[:cut], d.seq[:cut], d.poff[:cut + 1], d.par)
+    for attempt in range(3):
+        hi = cut + (N - cut) * (attempt + 1) // 3
+        ix.add_batch(d.creator[cut:hi], d.seq[cut:hi], d.poff[cut:hi + 1], d.par)
+        ix.drop_not_flushed()
+        assert ix.num_events() == cut
+        assert ix.num_branches() == B_flushed
+        compare_rows(ix, o2, range(cut))
+    ix.add_batch(d.creator[cut:], d.seq[cut:], d.poff[cut:], d.par)
+    compare_rows(ix, o, range(N))
+
+
+def test_build_then_drop_per_event(lx):
+    """IndexedLachesis.Build pattern (abft/indexed_lachesis.go:53-63): every
+    event is first added and dropped (Build), then added and flushed (Process)."""
+    d = lx.tools.gen_dag(6, 25, 3, cheaters=2, forks=5, seed=13)
+    w = [3, 3, 2, 2, 1, 1]
+    o = oracle_for(d, w)
+    ix = lx.Index()
+    ix.reset(w)
+    for i in range(len(d)):
+        s = slice(i, i + 1)
+        ix.add_batch(d.creator[s], d.seq[s], d.poff[i:i + 2], d.par)
+        ix.drop_not_flushed()
+        ix.add_batch(d.creator[s], d.seq[s], d.poff[i:i + 2], d.par)
+        ix.flush()
+    compare_rows(ix, o, range(len(d)))
+
+
+def test_reorder_invariance(lx):
+    """TestRandomForks (:719-744): FC over all pairs is invariant under random
+    parents-first reorderings (branch IDs may differ)."""
+    n = 8
+    nodes, evs = tdag.rand_fork_dag(n, 12, 4, cheaters=3, forks_count=5, seed=17)
+    validators = pos.Validators.equal(nodes)
+    ref = lx.VecfcIndex()
+    ref.reset(validators)
+    ref.add_events(evs)
+    fc = {(a.id, b.id): ref.forkless_cause(a.id, b.id) for a in evs for b in evs}
+    rng = tdag.SplitMix64(99)
+    order = evs
+    for _ in range(3):
+        order = tdag.by_parents(tdag.shuffle(order, rng))
+        ix = lx.VecfcIndex()
+        ix.reset(validators)
+        ix.add_events(order)
+        for a in order:
+            for b in order:
+                assert ix.forkless_cause(a.id, b.id) == fc[(a.id, b.id)]
+        ix.drop_not_flushed()
+        for e in order:
+            assert ix.get_highest_before(e.id) is None
+
+
+def test_random_forks_sanity_merged(lx):
+    """TestRandomForksSanity (:520-576) through the HIP path."""
+    n = 8
+    rng = tdag.SplitMix64(42)
+    node_ids = [rng.next() & 0xFFFFFFFF for _ in range(n)]
+    w = {v: 1 for v in node_ids}
+    w[node_ids[0]] = 2
+    w[node_ids[3]] = 2
+    w[node_ids[4]] = 3
+    validators = pos.Validators(w)
+    nodes, evs = tdag.rand_fork_dag(n, 300, 4, cheaters=3, forks_count=30, seed=5, node_ids=node_ids)
+    ix = lx.VecfcIndex()
+    ix.reset(validators)
+    ix.add_events(evs)
+    ix.flush()
+    ix.drop_not_flushed()
+    last = {}
+    for e in evs:
+        last[e.creator] = e
+    for node in nodes:
+        mhb = ix.get_merged_highest_before(last[node].id)
+        for k, cheater in enumerate(nodes):
+            bs = mhb.get(validators.idxs[cheater])
+            assert bs.is_fork_detected() == (k < 3)
+            if k < 3:
+                assert bs.seq == 0
+            else:
+                assert bs.seq != 0
+
+
+def test_errors_leave_state_unchanged(lx):
+    d = lx.tools.gen_dag(4, 10, 3, seed=3)
+    w = [1, 1, 1, 1]
+    ix = lx.Index()
+    ix.reset(w)
+    ix.add_batch(d.creator[:20], d.seq[:20], d.poff[:21], d.par)
+    bad_par = d.par.copy()
+    # a parent index >= its own index: out of order (vecengine/index.go:159-161)
+    lo, hi = d.poff[25], d.poff[26]
+    bad_par[lo] = 30
+    with pytest.raises(lx.LxError) as ei:
+        ix.add_batch(d.creator[20:], d.seq[20:], d.poff[20:], bad_par)
+    assert ei.value.code == -2 and ei.value.index == 5
+    assert ix.num_events() == 20
+    with pytest.raises(lx.LxError):
+        ix.forkless_cause(0, 25)
+    ix.add_batch(d.creator[20:], d.seq[20:], d.poff[20:], d.par)
+    o = oracle_for(d, w)
+    compare_rows(ix, o, range(len(d)))
+
+
+# ---------------------------------------------------------------- configs
+def test_config1_full(lx):
+    """BASELINE configs[0]: 5 validators x 1000 events, P=5, no forks."""
+    d = lx.tools.gen_dag(5, 1000, 5, seed=1)
+    w = [1] * 5
+    o = oracle_for(d, w)
+    ix = lx.Index()
+    ix.reset(w)
+    ix.add_batch(d.creator, d.seq, d.poff, d.par)
+    compare_rows(ix, o, range(0, len(d), 7))
+    qa, qb = lx.tools.fc_queries(d.lamport, 200_000, seed=4)
+    np.testing.assert_array_equal(ix.forkless_cause_batch(qa, qb), o.forkless_cause_batch(qa, qb))
+
+
+def test_config4_scaled(lx):
+    """BASELINE configs[3] shape (V=100, 10 cheaters x F=10) at 60 events per
+    validator (6k events): bit-exact rows, branches and FC vs the oracle."""
+    d = lx.tools.gen_dag(100, 60, 10, cheaters=10, forks=10, seed=2)
+    w = [1] * 100
+    o = oracle_for(d, w)
+    ix = lx.Index()
+    ix.reset(w)
+    N = len(d)
+    for lo in range(0, N, 1500):
+        ix.add_batch(d.creator[lo:lo + 1500], d.seq[lo:lo + 1500], d.poff[lo:min(N, lo + 1500) + 1], d.par)
+    assert ix.num_branches() == o.num_branches() > 100
+    compare_rows(ix, o, range(0, N, 3))
+    qa, qb = lx.tools.fc_queries(d.lamport, 300_000, seed=5)
+    np.testing.assert_array_equal(ix.forkless_cause_batch(qa, qb), o.forkless_cause_batch(qa, qb))
+
+
+def test_config3_shape_skewed(lx):
+    """BASELINE configs[2] shape: V=1000, Zipf weights floor(2^20/(i+1)), P=10,
+    at 8 events per validator (8k events) vs the oracle."""
+    V = 1000
+    w = [(1 << 20) // (i + 1) for i in range(V)]
+    d = lx.tools.gen_dag(V, 8, 10, seed=3)
+    o = oracle_for(d, w)
+    ix = lx.Index()
+    ix.reset(w)
+    ix.add_batch(d.creator, d.seq, d.poff, d.par)
+    compare_rows(ix, o, range(0, len(d), 97))
+    qa, qb = lx.tools.fc_queries(d.lamport, 100_000, seed=6)
+    np.testing.assert_array_equal(ix.forkless_cause_batch(qa, qb), o.forkless_cause_batch(qa, qb))
+
+
+def test_full_size_properties_config2(lx):
+    """BASELINE configs[1] at full size (V=100, 1M events): size-independent
+    properties.  (i) HB of an event on branch j at seq s equals s on column j;
+    (ii) LA/HB duality: LA(x)[j]=s  <=>  HB((j,s))[br(x)] >= seq(x) and
+    HB((j,s-1))[br(x)] < seq(x); (iii) HB monotone along each branch."""
+    V = 100
+    d = lx.tools.gen_dag(V, 10_000, 10, seed=1)
+    ix = lx.Index(event_capacity=len(d))
+    ix.reset([1] * V)
+    N = len(d)
+    step = 250_000
+    for lo in range(0, N, step):
+        hi = min(N, lo + step)
+        ix.add_batch(d.creator[lo:hi], d.seq[lo:hi], d.poff[lo:hi + 1], d.par)
+    rng = np.random.default_rng(0)
+    # index of event (creator c, seq s) in creation order: (s-1)*V + c
+    ev = lambda c, s: (s - 1) * V + c
+    for x in rng.integers(0, N - 5 * V, 200):
+        x = int(x)
+        hb = np.frombuffer(ix.highest_before(x), dtype=np.uint32).reshape(-1, 2)
+        cx, sx = int(d.creator[x]), int(d.seq[x])
+        assert hb[cx, 0] == sx
+        la = np.frombuffer(ix.lowest_after(x), dtype=np.uint32)
+        for j in rng.integers(0, V, 5):
+            j = int(j)
+            s = int(la[j])
+            if s == 0:
+                continue
+            hbj = np.frombuffer(ix.highest_before(ev(j, s)), dtype=np.uint32).reshape(-1, 2)
+            assert hbj[cx, 0] >= sx
+            if s > 1:
+                hbp = np.frombuffer(ix.highest_before(ev(j, s - 1)), dtype=np.uint32).reshape(-1, 2)
+                assert hbp[cx, 0] < sx
+            nxt = ev(cx, sx + 1)
+            if nxt < N:
+                hbn = np.frombuffer(ix.highest_before(nxt), dtype=np.uint32).reshape(-1, 2)
+                assert np.all(hbn[:, 0] >= hb[:, 0])
+    # FC sample against a direct evaluation from the getters
+    qa, qb = lx.tools.fc_queries(d.lamport, 2000, seed=9)
+    got = ix.forkless_cause_batch(qa, qb)
+    for a, b, g in zip(qa[:300], qb[:300], got[:300]):
+        hb = np.frombuffer(ix.highest_before(int(a)), dtype=np.uint32).reshape(-1, 2)[:, 0]
+        la = np.frombuffer(ix.lowest_after(int(b)), dtype=np.uint32)
+        cnt = int(np.sum((la != 0) & (la <= hb[:len(la)])))
+        assert bool(g) == (cnt >= ix.quorum())
