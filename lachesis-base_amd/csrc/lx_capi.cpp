@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -84,6 +85,7 @@ struct lx_index {
     // timing (HIP events on `stream`)
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     lx_stats stats{};
+    uint32_t diag_nofill = 0;   // LX_DIAG_NOFILL=1: timing-only build of the walker (LA left empty)
 
     int fail(int code, const char *fmt, ...) {
         char buf[512];
@@ -376,6 +378,7 @@ int add_batch_dev(lx_index *h, uint32_t n, const uint32_t *creator, const uint32
     ia.brow = h->brow;
     ia.s_cap = h->s_cap;
     ia.mask = (h->B > h->V) ? 1u : 0u;
+    ia.diag_nofill = h->diag_nofill;
     HIPCHK(h, hipEventRecord(h->ev[1], s));
     HIPCHK(h, lx::launch_index(ia, s));
     HIPCHK(h, hipEventRecord(h->ev[2], s));
@@ -465,6 +468,7 @@ int lx_create(const lx_config *cfg, lx_index **out) {
         delete h;
         return LX_ERR_HIP;
     }
+    if (const char *d = getenv("LX_DIAG_NOFILL")) h->diag_nofill = (d[0] == '1');
     for (auto &e : h->ev)
         if (hipEventCreate(&e) != hipSuccess) {
             delete h;

@@ -43,6 +43,7 @@ struct IndexArgs {
     const uint32_t *brow;
     uint32_t s_cap;
     uint32_t mask;               // older rows may carry fork marks
+    uint32_t diag_nofill;        // diagnostic timing build: skip the LA fill (LX_DIAG_NOFILL=1)
 };
 
 struct BatchArgs {

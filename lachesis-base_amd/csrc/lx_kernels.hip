@@ -26,6 +26,15 @@ __device__ __forceinline__ uint32_t ld_l2(const uint32_t *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Same, but consumes the value on the spot so the compiler's vmcnt wait lands
+// inside the (cold) branch issuing it instead of at the merge point, where it
+// would also wait for every store in flight (gfx950 counts stores in vmcnt).
+__device__ __forceinline__ uint32_t ld_l2_now(const uint32_t *p) {
+    uint32_t v = ld_l2(p);
+    asm volatile("" ::"v"(v));
+    return v;
+}
+
 // ---------------------------------------------------------------------------- batch prepare
 __global__ void k_meta(BatchArgs a, unsigned long long *err) {
     uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
@@ -205,27 +214,115 @@ hipError_t launch_batch_finish(const BatchArgs &a, hipStream_t s) {
 // ---------------------------------------------------------------------------- index walker
 //
 // One workgroup owns CPW columns (branches) and walks ALL events of the batch
-// in Add order: lane (g, k) handles column k of events g, g+E, g+2E, ...
-// (E = NT/CPW).  Columns are independent (max-join and LowestAfter range fill
+// in Add order.  Columns are independent (max-join and LowestAfter range fill
 // of column c touch only column c of HB and rows of branch c in LA), so the
-// workgroups never communicate.  In-batch parents are found in an LDS ring of
-// {tag, value} granules (tag = batch position + 1); an overwritten slot means
-// the parent is long done and its value is read from HBM/L2.  Lanes never
-// block: each loop iteration re-checks readiness and completes the event if
-// all its parents are ready, so intra-wave dependencies cannot deadlock.
-template <int CPW, int NT, int RING>
-__global__ __launch_bounds__(NT) void k_index(IndexArgs a) {
-    constexpr int E = NT / CPW;
-    static_assert(RING % E == 0, "ring slot reuse must stay within one lane");
-    __shared__ uint2 ring[RING * CPW];
+// workgroups never communicate.
+//
+// Roles inside the workgroup (NT = 9 waves):
+//  * wave 8, the loader, streams 80-B event records into an LDS record ring by
+//    LDS-DMA (global_load_lds_dwordx4), RR slots, up to RR/64 rounds in flight,
+//    and publishes each slot with a tag after its own vmcnt wait;
+//  * waves 0-7 compute: lane (g, k) handles column k of events g, g+E, ...
+//    (E = 512/CPW).  Their hot path touches only LDS and issues fire-and-forget
+//    stores, so no vmcnt wait (which on gfx950 also waits for stores) sits on
+//    the DAG's critical path.
+// In-batch parents are read from an LDS ring of {tag,seq} granules plus the
+// event index of the branch-c event holding the max (so the common LowestAfter
+// fill needs no dependent global lookup); a slot overwritten by a later event
+// means the parent is older than the ring and its value is read from L2 (slow
+// path).  Before a lane overwrites a ring slot it waits until at most SAFE of
+// its own stores are in flight, which makes the overwritten parent's HB store
+// visible to that slow path.  Lanes never block inside an iteration, so
+// intra-wave dependencies cannot deadlock.
+constexpr int kRR = 512;     // record ring slots (8 rounds of 64)
+constexpr int kBRC = 64;     // recent (seq -> event) entries per owned branch
+
+template <int CPW, int RING, bool FILL>
+__global__ __launch_bounds__(576) void k_index(IndexArgs a) {
+    constexpr int NT = 576;
+    constexpr int E = 512 / CPW;
+    constexpr int SAFE = RING / E - 2;
+    static_assert(RING % E == 0 && RING / E >= 4, "ring slot reuse must stay within one lane group");
+    static_assert(SAFE <= 63, "vmcnt field");
+    __shared__ uint2 ring_tv[RING * CPW];       // {tag = batch pos + 1, seq}
+    __shared__ uint32_t ring_ix[RING * CPW];    // dense index of the branch event holding seq
+    __shared__ uint4 rrec[kRR * 5];             // event records
+    __shared__ uint32_t rtag[kRR];
+    __shared__ uint2 brc[CPW * kBRC];           // {seq, event} of recent events of owned branches
 
     const uint32_t w = blockIdx.x;
     const uint32_t slice = (w % 8) * a.slices_per_xcd + (w / 8);   // XCD-aware: neighbouring slices share an L2
     if (slice >= a.n_slices) return;
 
-    for (int i = threadIdx.x; i < RING * CPW; i += NT) ring[i] = make_uint2(0, 0);
+    for (int i = threadIdx.x; i < RING * CPW; i += NT) ring_tv[i] = make_uint2(0, 0);
+    for (int i = threadIdx.x; i < kRR; i += NT) rtag[i] = 0;
+    for (int i = threadIdx.x; i < CPW * kBRC; i += NT) brc[i] = make_uint2(0, LX_NONE);
     __syncthreads();
 
+    const uint32_t n = a.n;
+    const uint32_t bs = a.batch_start;
+    const int wave = threadIdx.x / 64;
+    const int lane = threadIdx.x % 64;
+
+    if (wave == 8) {
+        // ------------------------------------------------------------ loader
+        const uint32_t nrounds = (n + 63) / 64;
+        constexpr uint32_t D = kRR / 64;
+        uint32_t issued = 0, done = 0;
+        const char *recb = reinterpret_cast<const char *>(a.rec);
+        const uint64_t rec_bytes = (uint64_t)n * sizeof(EventRec);
+        while (done < nrounds) {
+            bool progressed = false;
+            if (issued < nrounds && issued - done < D) {
+                // slots of this round are free once their previous occupants
+                // (events ev - kRR) are done on every column of this slice
+                const uint32_t ev = issued * 64 + lane;
+                bool free = true;
+                if (ev < n && ev >= (uint32_t)kRR) {
+                    const uint32_t q = ev - kRR;
+#pragma unroll
+                    for (int k = 0; k < CPW; k++) {
+                        const uint32_t ci = slice * CPW + k;
+                        if (ci < a.ncols && ring_tv[(q % RING) * CPW + k].x < q + 1) free = false;
+                    }
+                }
+                if (__all(free)) {
+                    const uint32_t s0 = (issued * 64) % kRR;
+                    char *dst = reinterpret_cast<char *>(rrec) + (uint64_t)s0 * sizeof(EventRec);
+                    const uint64_t base = (uint64_t)issued * 64 * sizeof(EventRec);
+#pragma unroll
+                    for (int i = 0; i < 5; i++) {
+                        uint64_t off = base + (uint64_t)(i * 64 + lane) * 16;
+                        if (off + 16 > rec_bytes) off = 0;   // tail of the last round: harmless filler
+                        __builtin_amdgcn_global_load_lds((const void *)(recb + off), (void *)(dst + i * 1024), 16, 0, 0);
+                    }
+                    issued++;
+                    progressed = true;
+                }
+            }
+            if (!progressed && issued > done) {
+                // wait for the oldest round: at most 5 DMAs per younger round in flight
+                switch (issued - done - 1) {
+                    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+                    case 1: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+                    case 2: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+                    case 3: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
+                    case 4: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
+                    case 5: asm volatile("s_waitcnt vmcnt(25)" ::: "memory"); break;
+                    case 6: asm volatile("s_waitcnt vmcnt(30)" ::: "memory"); break;
+                    default: asm volatile("s_waitcnt vmcnt(35)" ::: "memory"); break;
+                }
+                const uint32_t ev = done * 64 + lane;
+                if (ev < n) __hip_atomic_store(&rtag[ev % kRR], ev + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                done++;
+            } else if (!progressed) {
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        return;
+    }
+
+    // ---------------------------------------------------------------- compute
     const int k = threadIdx.x % CPW;
     const uint32_t g = threadIdx.x / CPW;
     const uint32_t ci = slice * CPW + k;
@@ -234,107 +331,147 @@ __global__ __launch_bounds__(NT) void k_index(IndexArgs a) {
     const uint32_t first = a.branch_first[col];
     const uint32_t *brow_c = a.brow + (uint64_t)col * a.s_cap;
     const uint64_t stride = a.stride;
-    const uint32_t bs = a.batch_start;
     const uint32_t mask = a.mask ? LX_SEQ_MASK : 0xFFFFFFFFu;
+    uint2 *brc_k = brc + k * kBRC;
 
     uint32_t lp = g;
     bool have = false;
     uint32_t br = 0, seq = 0, flags = 0, ovf = 0, np = 0, xi = 0;
     uint32_t par[LX_MAXP];
-    uint32_t todo = 0, r = 0, v0 = 0;
+    uint32_t todo = 0, r = 0, ridx = LX_NONE, v0 = 0;
 
-    while (lp < a.n) {
+    while (lp < n) {
         if (!have) {
-            const uint4 *rq = a.rec[lp].q;
-            uint4 q0 = rq[0];
+            const uint32_t slot = lp % kRR;
+            if (__hip_atomic_load(&rtag[slot], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != lp + 1) continue;
+            const uint4 *rq = rrec + slot * 5;
+            const uint4 q0 = rq[0];
             br = q0.x; seq = q0.y; flags = q0.z; ovf = q0.w;
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                uint4 q = rq[1 + j];
+                const uint4 q = rq[1 + j];
                 par[4 * j] = q.x; par[4 * j + 1] = q.y; par[4 * j + 2] = q.z; par[4 * j + 3] = q.w;
             }
             np = flags >> 8;
             todo = (np >= LX_MAXP) ? 0xFFFFu : ((1u << np) - 1u);
             xi = LX_MAXP;
-            r = (col == br) ? seq : 0u;
+            const bool own = (col == br);
+            r = own ? seq : 0u;
+            ridx = own ? (bs + lp) : LX_NONE;
             v0 = 0;
             have = true;
         }
+        // fast path: parents in the LDS ring
+        uint32_t slow = 0;
 #pragma unroll
         for (int j = 0; j < LX_MAXP; j++) {
             if (todo & (1u << j)) {
                 const uint32_t p = par[j];
-                uint32_t v = 0;
-                bool ok = true;
-                if (p < bs) {
-                    v = ld_l2(a.hb + (uint64_t)p * stride + col);
+                const uint32_t lpp = p - bs;
+                if (p >= bs) {
+                    const uint32_t si = (lpp % RING) * CPW + k;
+                    const uint2 t = ring_tv[si];
+                    if (t.x == lpp + 1) {
+                        const uint32_t v = t.y & mask;
+                        const uint32_t vi = ring_ix[si];
+                        if (v > r || (v == r && ridx == LX_NONE)) { r = v; ridx = vi; }
+                        if (j == 0) v0 = v;
+                        todo &= ~(1u << j);
+                    } else if (t.x > lpp + 1) {
+                        slow |= 1u << j;
+                    }
                 } else {
-                    const uint32_t lpp = p - bs;
-                    const uint2 t = ring[(lpp % RING) * CPW + k];
-                    if (t.x == lpp + 1) v = t.y;
-                    else if (t.x > lpp + 1) v = ld_l2(a.hb + (uint64_t)p * stride + col);
-                    else ok = false;
+                    slow |= 1u << j;
                 }
-                if (ok) {
-                    v &= mask;
-                    r = max(r, v);
+            }
+        }
+        if (slow) {
+            // slow path: parents older than the ring (or from an earlier batch)
+#pragma unroll
+            for (int j = 0; j < LX_MAXP; j++) {
+                if (slow & (1u << j)) {
+                    const uint32_t v = ld_l2_now(a.hb + (uint64_t)par[j] * stride + col) & mask;
+                    if (v > r) { r = v; ridx = LX_NONE; }
                     if (j == 0) v0 = v;
                     todo &= ~(1u << j);
                 }
             }
         }
-        if (todo == 0) {
+        if (todo == 0 && xi < np) {
             while (xi < np) {   // parents beyond the inline 16 (rare)
                 const uint32_t p = a.par_in[ovf + (xi - LX_MAXP)];
-                uint32_t v;
+                uint32_t v, vi = LX_NONE;
                 if (p < bs) {
                     v = ld_l2(a.hb + (uint64_t)p * stride + col);
                 } else {
                     const uint32_t lpp = p - bs;
-                    const uint2 t = ring[(lpp % RING) * CPW + k];
-                    if (t.x == lpp + 1) v = t.y;
+                    const uint32_t si = (lpp % RING) * CPW + k;
+                    const uint2 t = ring_tv[si];
+                    if (t.x == lpp + 1) { v = t.y; vi = ring_ix[si]; }
                     else if (t.x > lpp + 1) v = ld_l2(a.hb + (uint64_t)p * stride + col);
                     else break;
                 }
-                r = max(r, v & mask);
+                v &= mask;
+                if (v > r || (v == r && ridx == LX_NONE)) { r = v; ridx = vi; }
                 xi++;
             }
         }
         if (todo == 0 && xi >= np) {
             const uint32_t e = bs + lp;
             a.hb[(uint64_t)e * stride + col] = r;
-            // LowestAfter range fill: events (col, s), s in (h0, r], are first
-            // observed from branch `br` by this event.
-            const uint32_t h0 = (flags & 1u) ? v0 : 0u;
-            uint32_t s = max(h0 + 1u, first);
-            for (; s <= r; s++) {
-                const uint32_t row = brow_c[s - first];
-                a.la[(uint64_t)row * stride + br] = seq;
+            if (col == br) brc_k[seq % kBRC] = make_uint2(seq, e);
+            if (r != 0 && ridx == LX_NONE) {
+                const uint2 c = brc_k[r % kBRC];
+                ridx = c.y;
+                if (c.x != r) ridx = ld_l2_now(brow_c + (r - first));   // slow path (never if-converted: atomic)
             }
-            ring[(lp % RING) * CPW + k] = make_uint2(lp + 1, r);
+            if (FILL) {
+                // LowestAfter range fill: events (col, s), s in (h0, r], are first
+                // observed from branch `br` by this event.
+                const uint32_t h0 = (flags & 1u) ? v0 : 0u;
+                const uint32_t lo = max(h0 + 1u, first);
+                if (r >= lo) {
+                    a.la[(uint64_t)ridx * stride + br] = seq;
+                    for (uint32_t s = lo; s < r; s++) {
+                        const uint2 c = brc_k[s % kBRC];
+                        uint32_t row = c.y;
+                        if (c.x != s) row = ld_l2_now(brow_c + (s - first));
+                        a.la[(uint64_t)row * stride + br] = seq;
+                    }
+                }
+            }
+            // bound this lane's stores in flight so that the HB store of the
+            // event whose slot is overwritten RING/E completions later is done
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SAFE) : "memory");
+            const uint32_t si = (lp % RING) * CPW + k;
+            ring_ix[si] = ridx;
+            __hip_atomic_store(reinterpret_cast<unsigned long long *>(&ring_tv[si]),
+                               ((unsigned long long)r << 32) | (lp + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             lp += E;
             have = false;
         }
     }
 }
 
-template <int CPW, int NT, int RING>
+template <int CPW, int RING>
 static hipError_t launch_index_t(const IndexArgs &a0, hipStream_t s) {
     IndexArgs a = a0;
     a.n_slices = (a.ncols + CPW - 1) / CPW;
     a.slices_per_xcd = (a.n_slices + 7) / 8;
     uint32_t grid = a.slices_per_xcd * 8;
-    hipLaunchKernelGGL((k_index<CPW, NT, RING>), dim3(grid), dim3(NT), 0, s, a);
+    if (a.diag_nofill) hipLaunchKernelGGL((k_index<CPW, RING, false>), dim3(grid), dim3(576), 0, s, a);
+    else hipLaunchKernelGGL((k_index<CPW, RING, true>), dim3(grid), dim3(576), 0, s, a);
     return hipGetLastError();
 }
 
 hipError_t launch_index(const IndexArgs &a, hipStream_t s) {
     if (a.n == 0 || a.ncols == 0) return hipSuccess;
-    // aim at >= ~256 workgroups (one per CU) while keeping per-row writes wide
-    if (a.ncols <= 256) return launch_index_t<1, 512, 2048>(a, s);
-    if (a.ncols <= 512) return launch_index_t<2, 512, 2048>(a, s);
-    if (a.ncols <= 1024) return launch_index_t<4, 512, 2048>(a, s);
-    return launch_index_t<8, 512, 1024>(a, s);
+    // aim at >= ~256 workgroups (one per CU) while keeping per-row writes wide;
+    // the ring (96 KB) must cover the typical parent distance (~V events back)
+    if (a.ncols <= 256) return launch_index_t<1, 8192>(a, s);
+    if (a.ncols <= 512) return launch_index_t<2, 4096>(a, s);
+    if (a.ncols <= 1024) return launch_index_t<4, 2048>(a, s);
+    return launch_index_t<8, 1024>(a, s);
 }
 
 // ---------------------------------------------------------------------------- fork marks
