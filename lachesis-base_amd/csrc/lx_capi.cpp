@@ -86,6 +86,9 @@ struct lx_index {
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     lx_stats stats{};
     uint32_t diag_nofill = 0;   // LX_DIAG_NOFILL=1: timing-only build of the walker (LA left empty)
+    uint32_t cpw_hint = 0, ncw_hint = 0;   // LX_CPW / LX_NCW tuning overrides
+    uint32_t rr_hint = 0, diag = 0;        // LX_RR record ring depth; LX_DIAG timing-only modes
+    uint64_t last_npar = 0;                // parents in the current batch
 
     int fail(int code, const char *fmt, ...) {
         char buf[512];
@@ -330,6 +333,8 @@ int add_batch_dev(lx_index *h, uint32_t n, const uint32_t *creator, const uint32
     uint32_t nforks = 0;
     HIPCHK(h, hipMemcpyAsync(st, h->status, sizeof st, hipMemcpyDeviceToHost, s));
     HIPCHK(h, hipMemcpyAsync(&nforks, h->b_rank + (n - 1), 4, hipMemcpyDeviceToHost, s));
+    uint32_t npar32 = 0;
+    HIPCHK(h, hipMemcpyAsync(&npar32, poff + n, 4, hipMemcpyDeviceToHost, s));
     HIPCHK(h, hipStreamSynchronize(s));
     uint64_t e64;
     memcpy(&e64, st + 8, 8);
@@ -343,6 +348,7 @@ int add_batch_dev(lx_index *h, uint32_t n, const uint32_t *creator, const uint32
         return h->fail(LX_ERR_EVENT, "event %u: violates seq/self-parent invariants (eventcheck)", pos);
     }
     uint32_t bmax = st[2];
+    h->last_npar = npar32;
     uint32_t B_new = h->B + nforks;
     if ((rc = grow_branches(h, B_new))) return rc;
     h->max_seq = std::max(h->max_seq, bmax);
@@ -379,6 +385,15 @@ int add_batch_dev(lx_index *h, uint32_t n, const uint32_t *creator, const uint32
     ia.s_cap = h->s_cap;
     ia.mask = (h->B > h->V) ? 1u : 0u;
     ia.diag_nofill = h->diag_nofill;
+    ia.cpw_hint = h->cpw_hint;
+    ia.rr_hint = h->rr_hint;
+    ia.diag = h->diag;
+    ia.ncw_hint = h->ncw_hint;
+    // antichain width of tdag-like DAGs ~ V / (1.6 P); P from the batch
+    {
+        uint32_t pbar = std::max<uint32_t>(1, (uint32_t)((h->last_npar + n - 1) / n));
+        ia.width_hint = std::max<uint32_t>(1, (uint32_t)(h->V * 10 / (16 * pbar)));
+    }
     HIPCHK(h, hipEventRecord(h->ev[1], s));
     HIPCHK(h, lx::launch_index(ia, s));
     HIPCHK(h, hipEventRecord(h->ev[2], s));
@@ -469,6 +484,10 @@ int lx_create(const lx_config *cfg, lx_index **out) {
         return LX_ERR_HIP;
     }
     if (const char *d = getenv("LX_DIAG_NOFILL")) h->diag_nofill = (d[0] == '1');
+    if (const char *d = getenv("LX_CPW")) h->cpw_hint = (uint32_t)atoi(d);
+    if (const char *d = getenv("LX_NCW")) h->ncw_hint = (uint32_t)atoi(d);
+    if (const char *d = getenv("LX_RR")) h->rr_hint = (uint32_t)atoi(d);
+    if (const char *d = getenv("LX_DIAG")) h->diag = (uint32_t)atoi(d);
     for (auto &e : h->ev)
         if (hipEventCreate(&e) != hipSuccess) {
             delete h;

@@ -19,12 +19,14 @@
 #define LX_SEQ_MASK 0x7FFFFFFFu
 #define LX_MAXP 16   // parents stored inline in an event record
 
-// Event record consumed by the index kernel: 5 x uint4 = 80 B
-//   w0 branch, w1 seq, w2 flags (bit0 = parents[0] is the previous event of the
-//   same branch; bits 8.. = number of parents), w3 offset of parents[16..] in
-//   the batch parent array, w4..w19 parents[0..15] (global dense index, NONE pad)
+// Event record consumed by the index kernel: 6 x uint4 = 96 B
+//   w0 branch, w1 seq, w2 number of parents, w3 previous event of the same
+//   branch (global dense index, NONE if the event opens its branch), w4 offset
+//   of parents[16..] in the batch parent array, w5..w7 reserved,
+//   w8..w23 the first 16 parents sorted newest first (global index, NONE pad)
+#define LX_REC_Q 6
 struct EventRec {
-    uint4 q[5];
+    uint4 q[LX_REC_Q];
 };
 
 struct IndexArgs {
@@ -44,6 +46,11 @@ struct IndexArgs {
     uint32_t s_cap;
     uint32_t mask;               // older rows may carry fork marks
     uint32_t diag_nofill;        // diagnostic timing build: skip the LA fill (LX_DIAG_NOFILL=1)
+    uint32_t cpw_hint;           // columns per workgroup (0 = auto; LX_CPW)
+    uint32_t ncw_hint;           // compute waves per workgroup (0 = auto; LX_NCW)
+    uint32_t width_hint;         // expected antichain width of the batch
+    uint32_t rr_hint;            // record ring depth (LX_RR; 0 = auto)
+    uint32_t diag;               // timing-only diagnostics (LX_DIAG): 2 no deps, 3 no global stores
 };
 
 struct BatchArgs {

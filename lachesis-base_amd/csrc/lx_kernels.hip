@@ -190,17 +190,30 @@ __global__ void k_finalize(BatchArgs a) {
     atomicMax(&a.branch_len[br], s - first + 1);
     uint32_t p0 = a.poff[e], p1 = a.poff[e + 1];
     uint32_t np = p1 - p0;
-    uint32_t prev = (s > 1 && !a.isfork[e]) ? 1u : 0u;
-    uint32_t w[20];
-    w[0] = br;
-    w[1] = s;
-    w[2] = prev | (np << 8);
-    w[3] = p0 + LX_MAXP;
+    uint32_t prev = (s > 1 && !a.isfork[e]) ? a.par[p0] : LX_NONE;
+    // inline parents sorted newest first: the walker spins on the newest one
+    uint32_t w[LX_MAXP];
 #pragma unroll
-    for (int k = 0; k < LX_MAXP; k++) w[4 + k] = (k < (int)np) ? a.par[p0 + k] : LX_NONE;
+    for (int k = 0; k < LX_MAXP; k++) w[k] = (k < (int)np) ? a.par[p0 + k] : 0u;
+#pragma unroll
+    for (int i = 1; i < LX_MAXP; i++) {
+#pragma unroll
+        for (int j = i; j > 0; j--) {
+            const uint32_t x = w[j - 1], y = w[j];
+            w[j - 1] = max(x, y);
+            w[j] = min(x, y);
+        }
+    }
     EventRec r;
+    r.q[0] = make_uint4(br, s, np, prev);
+    r.q[1] = make_uint4(p0 + LX_MAXP, 0, 0, 0);
 #pragma unroll
-    for (int k = 0; k < 5; k++) r.q[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+    for (int k = 0; k < 4; k++) {
+        uint32_t v[4];
+#pragma unroll
+        for (int t = 0; t < 4; t++) v[t] = (4 * k + t < (int)np) ? w[4 * k + t] : LX_NONE;
+        r.q[2 + k] = make_uint4(v[0], v[1], v[2], v[3]);
+    }
     a.rec[e] = r;
 }
 
@@ -216,46 +229,61 @@ hipError_t launch_batch_finish(const BatchArgs &a, hipStream_t s) {
 // One workgroup owns CPW columns (branches) and walks ALL events of the batch
 // in Add order.  Columns are independent (max-join and LowestAfter range fill
 // of column c touch only column c of HB and rows of branch c in LA), so the
-// workgroups never communicate.
+// workgroups never communicate; one launch covers the whole batch.
 //
-// Roles inside the workgroup (NT = 9 waves):
-//  * wave 8, the loader, streams 80-B event records into an LDS record ring by
-//    LDS-DMA (global_load_lds_dwordx4), RR slots, up to RR/64 rounds in flight,
-//    and publishes each slot with a tag after its own vmcnt wait;
-//  * waves 0-7 compute: lane (g, k) handles column k of events g, g+E, ...
-//    (E = 512/CPW).  Their hot path touches only LDS and issues fire-and-forget
-//    stores, so no vmcnt wait (which on gfx950 also waits for stores) sits on
-//    the DAG's critical path.
-// In-batch parents are read from an LDS ring of {tag,seq} granules plus the
-// event index of the branch-c event holding the max (so the common LowestAfter
-// fill needs no dependent global lookup); a slot overwritten by a later event
-// means the parent is older than the ring and its value is read from L2 (slow
-// path).  Before a lane overwrites a ring slot it waits until at most SAFE of
-// its own stores are in flight, which makes the overwritten parent's HB store
-// visible to that slow path.  Lanes never block inside an iteration, so
-// intra-wave dependencies cannot deadlock.
-constexpr int kRR = 512;     // record ring slots (8 rounds of 64)
+// Roles inside the workgroup (NCW compute waves + 1 loader wave):
+//  * the loader streams 80-B event records into an LDS record ring by LDS-DMA
+//    (global_load_lds_dwordx4, RR/64 rounds in flight) and publishes each slot
+//    with a tag after its own vmcnt wait;
+//  * compute lane g handles events g, g+E, g+2E, ... (E = 64*NCW), all CPW
+//    columns of each, so readiness checks are paid once per parent.  The hot
+//    path touches only LDS and issues fire-and-forget stores: no vmcnt wait
+//    (which on gfx950 also waits for stores) sits on the DAG's critical path.
+// Parents are read from an LDS ring of per-column {tag, seq} granules (tag =
+// batch position + 1, each 16-B half written by one ds_write_b128, so atomic
+// per lane).  A slot overwritten by a later event means the parent is older
+// than the ring; its HB row is then read from L2 (slow path).  Before a lane
+// overwrites a slot it bounds its own stores in flight (vmcnt), so that slow
+// path sees the overwritten event's HB store.  Lanes never block inside an
+// iteration (readiness is re-checked every pass): intra-wave dependencies
+// cannot deadlock.  The event holding a column's max seq (needed for the
+// LowestAfter fill) comes from an LDS table of recent events of the owned
+// branches, falling back to the branch-row table in L2.
 constexpr int kBRC = 64;     // recent (seq -> event) entries per owned branch
 
-template <int CPW, int RING, bool FILL>
-__global__ __launch_bounds__(576) void k_index(IndexArgs a) {
-    constexpr int NT = 576;
-    constexpr int E = 512 / CPW;
-    constexpr int SAFE = RING / E - 2;
-    static_assert(RING % E == 0 && RING / E >= 4, "ring slot reuse must stay within one lane group");
-    static_assert(SAFE <= 63, "vmcnt field");
-    __shared__ uint2 ring_tv[RING * CPW];       // {tag = batch pos + 1, seq}
-    __shared__ uint32_t ring_ix[RING * CPW];    // dense index of the branch event holding seq
-    __shared__ uint4 rrec[kRR * 5];             // event records
-    __shared__ uint32_t rtag[kRR];
-    __shared__ uint2 brc[CPW * kBRC];           // {seq, event} of recent events of owned branches
+__device__ __forceinline__ void wait_vmcnt_le(uint32_t n) {
+    switch (n) {
+        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+        case 1: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+        case 2: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+        case 3: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
+        case 4: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
+        case 5: asm volatile("s_waitcnt vmcnt(25)" ::: "memory"); break;
+        case 6: asm volatile("s_waitcnt vmcnt(30)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(35)" ::: "memory"); break;
+    }
+}
+
+template <int CPW, int NCW, int RING, int RR, bool FILL>
+__global__ __launch_bounds__(64 * (NCW + 1)) void k_index(IndexArgs a) {
+    constexpr int NT = 64 * (NCW + 1);
+    constexpr int E = 64 * NCW;
+    constexpr int SAFE0 = RING / E - 2;
+    constexpr int SAFE = SAFE0 > 60 ? 60 : SAFE0;
+    constexpr int RQ = LX_REC_Q;
+    static_assert(RING % E == 0 && RING / E >= 4, "ring slot reuse must stay within one lane");
+    static_assert(RR % 64 == 0 && RR / 64 <= 8 && RR >= E, "record ring");
+    __shared__ uint64_t ring[RING * CPW];        // per event: CPW x {tag, seq} granules
+    __shared__ uint4 rrec[RR * RQ];              // event records
+    __shared__ uint32_t rtag[RR];
+    __shared__ uint2 brc[CPW * kBRC];            // {seq, event} of recent events of owned branches
 
     const uint32_t w = blockIdx.x;
     const uint32_t slice = (w % 8) * a.slices_per_xcd + (w / 8);   // XCD-aware: neighbouring slices share an L2
     if (slice >= a.n_slices) return;
 
-    for (int i = threadIdx.x; i < RING * CPW; i += NT) ring_tv[i] = make_uint2(0, 0);
-    for (int i = threadIdx.x; i < kRR; i += NT) rtag[i] = 0;
+    for (int i = threadIdx.x; i < RING * CPW; i += NT) ring[i] = 0;
+    for (int i = threadIdx.x; i < RR; i += NT) rtag[i] = 0;
     for (int i = threadIdx.x; i < CPW * kBRC; i += NT) brc[i] = make_uint2(0, LX_NONE);
     __syncthreads();
 
@@ -263,11 +291,12 @@ __global__ __launch_bounds__(576) void k_index(IndexArgs a) {
     const uint32_t bs = a.batch_start;
     const int wave = threadIdx.x / 64;
     const int lane = threadIdx.x % 64;
+    const uint32_t diag = a.diag;   // 0 normal; timing-only diagnostics: 2 no deps, 3 no global stores
 
-    if (wave == 8) {
+    if (wave == NCW) {
         // ------------------------------------------------------------ loader
         const uint32_t nrounds = (n + 63) / 64;
-        constexpr uint32_t D = kRR / 64;
+        constexpr uint32_t D = RR / 64;
         uint32_t issued = 0, done = 0;
         const char *recb = reinterpret_cast<const char *>(a.rec);
         const uint64_t rec_bytes = (uint64_t)n * sizeof(EventRec);
@@ -275,23 +304,21 @@ __global__ __launch_bounds__(576) void k_index(IndexArgs a) {
             bool progressed = false;
             if (issued < nrounds && issued - done < D) {
                 // slots of this round are free once their previous occupants
-                // (events ev - kRR) are done on every column of this slice
+                // (events ev - RR) are done
                 const uint32_t ev = issued * 64 + lane;
                 bool free = true;
-                if (ev < n && ev >= (uint32_t)kRR) {
-                    const uint32_t q = ev - kRR;
-#pragma unroll
-                    for (int k = 0; k < CPW; k++) {
-                        const uint32_t ci = slice * CPW + k;
-                        if (ci < a.ncols && ring_tv[(q % RING) * CPW + k].x < q + 1) free = false;
-                    }
+                if (ev < n && ev >= (uint32_t)RR) {
+                    const uint32_t q = ev - RR;
+                    const uint64_t g0 = __hip_atomic_load(ring + (q % RING) * CPW,
+                                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    if ((uint32_t)g0 < q + 1) free = false;
                 }
                 if (__all(free)) {
-                    const uint32_t s0 = (issued * 64) % kRR;
+                    const uint32_t s0 = (issued * 64) % RR;
                     char *dst = reinterpret_cast<char *>(rrec) + (uint64_t)s0 * sizeof(EventRec);
                     const uint64_t base = (uint64_t)issued * 64 * sizeof(EventRec);
 #pragma unroll
-                    for (int i = 0; i < 5; i++) {
+                    for (int i = 0; i < RQ; i++) {
                         uint64_t off = base + (uint64_t)(i * 64 + lane) * 16;
                         if (off + 16 > rec_bytes) off = 0;   // tail of the last round: harmless filler
                         __builtin_amdgcn_global_load_lds((const void *)(recb + off), (void *)(dst + i * 1024), 16, 0, 0);
@@ -301,19 +328,19 @@ __global__ __launch_bounds__(576) void k_index(IndexArgs a) {
                 }
             }
             if (!progressed && issued > done) {
-                // wait for the oldest round: at most 5 DMAs per younger round in flight
+                // oldest round landed once at most RQ DMAs per younger round remain
                 switch (issued - done - 1) {
                     case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-                    case 1: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
-                    case 2: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
-                    case 3: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
-                    case 4: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
-                    case 5: asm volatile("s_waitcnt vmcnt(25)" ::: "memory"); break;
-                    case 6: asm volatile("s_waitcnt vmcnt(30)" ::: "memory"); break;
-                    default: asm volatile("s_waitcnt vmcnt(35)" ::: "memory"); break;
+                    case 1: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+                    case 2: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+                    case 3: asm volatile("s_waitcnt vmcnt(18)" ::: "memory"); break;
+                    case 4: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
+                    case 5: asm volatile("s_waitcnt vmcnt(30)" ::: "memory"); break;
+                    case 6: asm volatile("s_waitcnt vmcnt(36)" ::: "memory"); break;
+                    default: asm volatile("s_waitcnt vmcnt(42)" ::: "memory"); break;
                 }
                 const uint32_t ev = done * 64 + lane;
-                if (ev < n) __hip_atomic_store(&rtag[ev % kRR], ev + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (ev < n) __hip_atomic_store(&rtag[ev % RR], ev + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                 done++;
             } else if (!progressed) {
                 __builtin_amdgcn_s_sleep(1);
@@ -323,66 +350,87 @@ __global__ __launch_bounds__(576) void k_index(IndexArgs a) {
     }
 
     // ---------------------------------------------------------------- compute
-    const int k = threadIdx.x % CPW;
-    const uint32_t g = threadIdx.x / CPW;
-    const uint32_t ci = slice * CPW + k;
-    if (ci >= a.ncols) return;
-    const uint32_t col = a.col_list[ci];
-    const uint32_t first = a.branch_first[col];
-    const uint32_t *brow_c = a.brow + (uint64_t)col * a.s_cap;
+    uint32_t col[CPW], first[CPW];
+    bool valid[CPW];
+#pragma unroll
+    for (int k = 0; k < CPW; k++) {
+        const uint32_t ci = slice * CPW + k;
+        valid[k] = ci < a.ncols;
+        col[k] = valid[k] ? a.col_list[ci] : 0;
+        first[k] = valid[k] ? a.branch_first[col[k]] : 1;
+    }
     const uint64_t stride = a.stride;
     const uint32_t mask = a.mask ? LX_SEQ_MASK : 0xFFFFFFFFu;
-    uint2 *brc_k = brc + k * kBRC;
+    const uint64_t *ring64 = ring;
 
-    uint32_t lp = g;
+    uint32_t lp = threadIdx.x;
     bool have = false;
-    uint32_t br = 0, seq = 0, flags = 0, ovf = 0, np = 0, xi = 0;
+    uint32_t br = 0, seq = 0, np = 0, prev = 0, ovf = 0, xi = 0;
     uint32_t par[LX_MAXP];
-    uint32_t todo = 0, r = 0, ridx = LX_NONE, v0 = 0;
+    uint32_t todo = 0;
+    uint32_t wait_off = 0, wait_tag = 0;          // the one granule this lane spins on
+    uint32_t r[CPW], v0[CPW];
 
     while (lp < n) {
         if (!have) {
-            const uint32_t slot = lp % kRR;
+            const uint32_t slot = lp % RR;
             if (__hip_atomic_load(&rtag[slot], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != lp + 1) continue;
-            const uint4 *rq = rrec + slot * 5;
+            const uint4 *rq = rrec + slot * RQ;
             const uint4 q0 = rq[0];
-            br = q0.x; seq = q0.y; flags = q0.z; ovf = q0.w;
+            br = q0.x; seq = q0.y; np = q0.z; prev = q0.w;
+            ovf = rq[1].x;
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                const uint4 q = rq[1 + j];
-                par[4 * j] = q.x; par[4 * j + 1] = q.y; par[4 * j + 2] = q.z; par[4 * j + 3] = q.w;
+                const uint4 q = rq[2 + j];
+                par[4 * j] = q.x - bs; par[4 * j + 1] = q.y - bs; par[4 * j + 2] = q.z - bs; par[4 * j + 3] = q.w - bs;
             }
-            np = flags >> 8;
             todo = (np >= LX_MAXP) ? 0xFFFFu : ((1u << np) - 1u);
             xi = LX_MAXP;
-            const bool own = (col == br);
-            r = own ? seq : 0u;
-            ridx = own ? (bs + lp) : LX_NONE;
-            v0 = 0;
+#pragma unroll
+            for (int k = 0; k < CPW; k++) { r[k] = (col[k] == br) ? seq : 0u; v0[k] = 0; }
+            // spin on the newest in-batch parent first (parents sorted newest first)
+            const uint32_t l0 = par[0];
+            wait_off = (np > 0 && l0 < n && diag != 2) ? (l0 % RING) * CPW : 0u;
+            wait_tag = (np > 0 && l0 < n && diag != 2) ? l0 + 1 : 0u;
+            if (diag == 2) todo = 0;
             have = true;
         }
-        // fast path: parents in the LDS ring
+        // cheap spin: one granule tag (an overwritten slot reads as >= tag)
+        if ((uint32_t)__hip_atomic_load(ring64 + wait_off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < wait_tag)
+            continue;
+        // fold every pending parent, chunks of 4: issue granule reads, then evaluate
         uint32_t slow = 0;
 #pragma unroll
-        for (int j = 0; j < LX_MAXP; j++) {
-            if (todo & (1u << j)) {
-                const uint32_t p = par[j];
-                const uint32_t lpp = p - bs;
-                if (p >= bs) {
-                    const uint32_t si = (lpp % RING) * CPW + k;
-                    const uint2 t = ring_tv[si];
-                    if (t.x == lpp + 1) {
-                        const uint32_t v = t.y & mask;
-                        const uint32_t vi = ring_ix[si];
-                        if (v > r || (v == r && ridx == LX_NONE)) { r = v; ridx = vi; }
-                        if (j == 0) v0 = v;
-                        todo &= ~(1u << j);
-                    } else if (t.x > lpp + 1) {
-                        slow |= 1u << j;
-                    }
-                } else {
-                    slow |= 1u << j;
+        for (int c = 0; c < LX_MAXP / 4; c++) {
+            if (!__any(todo >> (4 * c))) break;   // wave-uniform
+            uint64_t g[4][CPW];
+#pragma unroll
+            for (int jj = 0; jj < 4; jj++) {
+                const uint64_t *gp = ring64 + (par[4 * c + jj] % RING) * CPW;
+#pragma unroll
+                for (int k = 0; k < CPW; k++)
+                    g[jj][k] = __hip_atomic_load(gp + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+#pragma unroll
+            for (int jj = 0; jj < 4; jj++) {
+                const int j = 4 * c + jj;
+                const uint32_t lpp = par[j];
+                const uint32_t tg = lpp + 1;
+                const uint32_t pend = (todo >> j) & 1u;
+                const uint32_t inb = (uint32_t)(lpp < n);    // in-batch parent (older ones wrap above n)
+                uint32_t rdy = pend & inb;
+#pragma unroll
+                for (int k = 0; k < CPW; k++) rdy &= (uint32_t)((uint32_t)g[jj][k] == tg);
+                const uint32_t old = pend & ((inb ^ 1u) | (uint32_t)((uint32_t)g[jj][0] > tg));
+                const bool isprev = (lpp + bs == prev);
+#pragma unroll
+                for (int k = 0; k < CPW; k++) {
+                    const uint32_t v = rdy ? ((uint32_t)(g[jj][k] >> 32) & mask) : 0u;
+                    r[k] = max(r[k], v);
+                    v0[k] = (rdy && isprev) ? v : v0[k];
                 }
+                todo &= ~((rdy | old) << j);
+                slow |= old << j;
             }
         }
         if (slow) {
@@ -390,88 +438,137 @@ __global__ __launch_bounds__(576) void k_index(IndexArgs a) {
 #pragma unroll
             for (int j = 0; j < LX_MAXP; j++) {
                 if (slow & (1u << j)) {
-                    const uint32_t v = ld_l2_now(a.hb + (uint64_t)par[j] * stride + col) & mask;
-                    if (v > r) { r = v; ridx = LX_NONE; }
-                    if (j == 0) v0 = v;
-                    todo &= ~(1u << j);
+                    const uint32_t *row = a.hb + (uint64_t)(par[j] + bs) * stride;
+                    const bool isprev = (par[j] + bs == prev);
+#pragma unroll
+                    for (int k = 0; k < CPW; k++) {
+                        const uint32_t v = valid[k] ? (ld_l2_now(row + col[k]) & mask) : 0u;
+                        r[k] = max(r[k], v);
+                        if (isprev) v0[k] = v;
+                    }
                 }
             }
         }
-        if (todo == 0 && xi < np) {
+        if (todo) {
+            // some parent still pending: spin on the lowest pending one next
+            const int j = __builtin_ctz(todo);
+            uint32_t l = par[0];
+#pragma unroll
+            for (int t = 0; t < LX_MAXP; t++) l = (t == j) ? par[t] : l;
+            wait_off = (l % RING) * CPW;
+            wait_tag = l + 1;
+            continue;
+        }
+        if (xi < np && diag != 2) {
             while (xi < np) {   // parents beyond the inline 16 (rare)
-                const uint32_t p = a.par_in[ovf + (xi - LX_MAXP)];
-                uint32_t v, vi = LX_NONE;
-                if (p < bs) {
-                    v = ld_l2(a.hb + (uint64_t)p * stride + col);
+                const uint32_t p = ld_l2_now(a.par_in + ovf + (xi - LX_MAXP));
+                const uint32_t lpp = p - bs;
+                bool rd = true;
+                uint64_t gg[CPW];
+                if (lpp < n) {
+                    const uint64_t *gp = ring64 + (lpp % RING) * CPW;
+                    bool ok = true;
+#pragma unroll
+                    for (int k = 0; k < CPW; k++) {
+                        gg[k] = __hip_atomic_load(gp + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        ok &= ((uint32_t)gg[k] == lpp + 1);
+                    }
+                    if (!ok) {
+                        if ((uint32_t)gg[0] > lpp + 1) rd = false;   // overwritten: read L2
+                        else break;                                  // not ready yet
+                    }
                 } else {
-                    const uint32_t lpp = p - bs;
-                    const uint32_t si = (lpp % RING) * CPW + k;
-                    const uint2 t = ring_tv[si];
-                    if (t.x == lpp + 1) { v = t.y; vi = ring_ix[si]; }
-                    else if (t.x > lpp + 1) v = ld_l2(a.hb + (uint64_t)p * stride + col);
-                    else break;
+                    rd = false;
                 }
-                v &= mask;
-                if (v > r || (v == r && ridx == LX_NONE)) { r = v; ridx = vi; }
+#pragma unroll
+                for (int k = 0; k < CPW; k++) {
+                    uint32_t v;
+                    if (rd) v = (uint32_t)(gg[k] >> 32);
+                    else v = valid[k] ? ld_l2_now(a.hb + (uint64_t)p * stride + col[k]) : 0u;
+                    v &= mask;
+                    r[k] = max(r[k], v);
+                    if (p == prev) v0[k] = v;
+                }
                 xi++;
             }
+            if (xi < np) continue;
         }
-        if (todo == 0 && xi >= np) {
+        {
             const uint32_t e = bs + lp;
-            a.hb[(uint64_t)e * stride + col] = r;
-            if (col == br) brc_k[seq % kBRC] = make_uint2(seq, e);
-            if (r != 0 && ridx == LX_NONE) {
-                const uint2 c = brc_k[r % kBRC];
-                ridx = c.y;
-                if (c.x != r) ridx = ld_l2_now(brow_c + (r - first));   // slow path (never if-converted: atomic)
+            uint32_t *hrow = a.hb + (uint64_t)e * stride;
+#pragma unroll
+            for (int k = 0; k < CPW; k++) {
+                if (!valid[k]) continue;
+                if (diag != 3) hrow[col[k]] = r[k];
+                if (col[k] == br)
+                    __hip_atomic_store(reinterpret_cast<uint64_t *>(brc + k * kBRC + seq % kBRC),
+                                       ((uint64_t)e << 32) | seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
-            if (FILL) {
+            if (FILL && diag != 3) {
                 // LowestAfter range fill: events (col, s), s in (h0, r], are first
                 // observed from branch `br` by this event.
-                const uint32_t h0 = (flags & 1u) ? v0 : 0u;
-                const uint32_t lo = max(h0 + 1u, first);
-                if (r >= lo) {
-                    a.la[(uint64_t)ridx * stride + br] = seq;
-                    for (uint32_t s = lo; s < r; s++) {
-                        const uint2 c = brc_k[s % kBRC];
-                        uint32_t row = c.y;
-                        if (c.x != s) row = ld_l2_now(brow_c + (s - first));
+#pragma unroll
+                for (int k = 0; k < CPW; k++) {
+                    if (!valid[k]) continue;
+                    const uint32_t h0 = (prev != LX_NONE) ? v0[k] : 0u;
+                    const uint32_t lo = max(h0 + 1u, first[k]);
+                    for (uint32_t s = lo; s <= r[k]; s++) {
+                        const uint64_t cc = __hip_atomic_load(reinterpret_cast<const uint64_t *>(brc + k * kBRC + s % kBRC),
+                                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        uint32_t row = (uint32_t)(cc >> 32);
+                        if ((uint32_t)cc != s) row = ld_l2_now(a.brow + (uint64_t)col[k] * a.s_cap + (s - first[k]));
                         a.la[(uint64_t)row * stride + br] = seq;
                     }
                 }
             }
-            // bound this lane's stores in flight so that the HB store of the
-            // event whose slot is overwritten RING/E completions later is done
+            // bound this lane's stores in flight so that the HB stores of the
+            // event whose slot is overwritten RING/E completions later are done
             asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SAFE) : "memory");
-            const uint32_t si = (lp % RING) * CPW + k;
-            ring_ix[si] = ridx;
-            __hip_atomic_store(reinterpret_cast<unsigned long long *>(&ring_tv[si]),
-                               ((unsigned long long)r << 32) | (lp + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            uint64_t *dst = ring + (lp % RING) * CPW;
+#pragma unroll
+            for (int k = 0; k < CPW; k++) dst[k] = ((uint64_t)r[k] << 32) | (lp + 1);
             lp += E;
             have = false;
         }
     }
 }
 
-template <int CPW, int RING>
+template <int CPW, int NCW, int RING, int RR>
 static hipError_t launch_index_t(const IndexArgs &a0, hipStream_t s) {
     IndexArgs a = a0;
     a.n_slices = (a.ncols + CPW - 1) / CPW;
     a.slices_per_xcd = (a.n_slices + 7) / 8;
     uint32_t grid = a.slices_per_xcd * 8;
-    if (a.diag_nofill) hipLaunchKernelGGL((k_index<CPW, RING, false>), dim3(grid), dim3(576), 0, s, a);
-    else hipLaunchKernelGGL((k_index<CPW, RING, true>), dim3(grid), dim3(576), 0, s, a);
+    if (a.diag_nofill) hipLaunchKernelGGL((k_index<CPW, NCW, RING, RR, false>), dim3(grid), dim3(64 * (NCW + 1)), 0, s, a);
+    else hipLaunchKernelGGL((k_index<CPW, NCW, RING, RR, true>), dim3(grid), dim3(64 * (NCW + 1)), 0, s, a);
     return hipGetLastError();
+}
+
+template <int CPW, int NCW>
+static hipError_t launch_index_n(const IndexArgs &a, hipStream_t s) {
+    constexpr int RING = 8192 / CPW;             // 64 KB of {tag, seq} granules
+    constexpr int RRMIN = 64 * NCW;
+    if (a.rr_hint >= 512 || RRMIN > 256) return launch_index_t<CPW, NCW, RING, (RRMIN > 512 ? RRMIN : 512)>(a, s);
+    return launch_index_t<CPW, NCW, RING, (RRMIN > 256 ? RRMIN : 256)>(a, s);
+}
+
+template <int CPW>
+static hipError_t launch_index_c(const IndexArgs &a, uint32_t ncw, hipStream_t s) {
+    if (ncw <= 1) return launch_index_n<CPW, 1>(a, s);
+    if (ncw <= 2) return launch_index_n<CPW, 2>(a, s);
+    return launch_index_n<CPW, 4>(a, s);
 }
 
 hipError_t launch_index(const IndexArgs &a, hipStream_t s) {
     if (a.n == 0 || a.ncols == 0) return hipSuccess;
-    // aim at >= ~256 workgroups (one per CU) while keeping per-row writes wide;
-    // the ring (96 KB) must cover the typical parent distance (~V events back)
-    if (a.ncols <= 256) return launch_index_t<1, 8192>(a, s);
-    if (a.ncols <= 512) return launch_index_t<2, 4096>(a, s);
-    if (a.ncols <= 1024) return launch_index_t<4, 2048>(a, s);
-    return launch_index_t<8, 1024>(a, s);
+    // columns per workgroup: aim at ~256 workgroups; compute waves: enough
+    // events in flight for the DAG's antichain width (~V / (1.6 P))
+    uint32_t cpw = a.cpw_hint ? a.cpw_hint : (a.ncols <= 256 ? 1 : a.ncols <= 512 ? 2 : a.ncols <= 1024 ? 4 : 8);
+    uint32_t ncw = a.ncw_hint ? a.ncw_hint : (a.width_hint <= 48 ? 1 : a.width_hint <= 96 ? 2 : 4);
+    if (cpw <= 1) return launch_index_c<1>(a, ncw, s);
+    if (cpw <= 2) return launch_index_c<2>(a, ncw, s);
+    if (cpw <= 4) return launch_index_c<4>(a, ncw, s);
+    return launch_index_c<8>(a, ncw, s);
 }
 
 // ---------------------------------------------------------------------------- fork marks
