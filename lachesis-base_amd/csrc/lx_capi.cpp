@@ -82,6 +82,16 @@ struct lx_index {
     uint32_t *q_a = nullptr, *q_b = nullptr;
     uint8_t *q_out = nullptr;
 
+    // column-shard exchange cache (rows per shard at sc_events)
+    uint64_t sc_events = ~0ull;
+    uint32_t sc_B = 0;
+    std::vector<uint32_t *> sc_rows;
+    std::vector<uint32_t> sc_nrows;
+    uint32_t *sc_flag = nullptr, *sc_pos = nullptr, *sc_cols = nullptr;
+    uint64_t sc_cap = 0;
+    void *sc_tmp = nullptr;
+    size_t sc_tmp_bytes = 0;
+
     // timing (HIP events on `stream`)
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     lx_stats stats{};
@@ -121,6 +131,18 @@ void free_all(lx_index *h) {
                     h->q_a, h->q_b, h->q_out};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
+    for (uint32_t *p : h->sc_rows)
+        if (p) (void)hipFree(p);
+    void *sptrs[] = {h->sc_flag, h->sc_pos, h->sc_cols, h->sc_tmp};
+    for (void *p : sptrs)
+        if (p) (void)hipFree(p);
+    h->sc_rows.clear();
+    h->sc_nrows.clear();
+    h->sc_flag = h->sc_pos = h->sc_cols = nullptr;
+    h->sc_tmp = nullptr;
+    h->sc_cap = 0;
+    h->sc_tmp_bytes = 0;
+    h->sc_events = ~0ull;
     h->hb = h->la = nullptr;
     h->ev_creator = h->ev_seq = h->ev_branch = h->ev_bbefore = h->ev_sp = h->first_child = nullptr;
     h->first_root = h->branch_first = h->branch_creator = h->branch_len = h->brow = h->wpad = h->col_list = nullptr;
@@ -457,6 +479,67 @@ int fc_args(lx_index *h, uint64_t n, const uint32_t *a, const uint32_t *b, uint8
     return 0;
 }
 
+void shard_bounds(const lx_index *h, uint32_t r, uint32_t *lo, uint32_t *hi) {
+    auto bound = [&](uint32_t q) {
+        return q >= h->shard_count ? h->V : (uint32_t)((uint64_t)h->V * q / h->shard_count) & ~3u;
+    };
+    *lo = bound(r);
+    *hi = bound(r + 1);
+}
+
+std::vector<uint32_t> shard_cols(const lx_index *h, uint32_t q) {
+    uint32_t lo, hi;
+    shard_bounds(h, q, &lo, &hi);
+    std::vector<uint32_t> cols;
+    for (uint32_t b = 0; b < h->B; b++)
+        if (h->h_branch_creator[b] >= lo && h->h_branch_creator[b] < hi) cols.push_back(b);
+    return cols;
+}
+
+// rows (events) whose branch belongs to each shard, at the current event count
+int ensure_shard_rows(lx_index *h) {
+    if (h->sc_events == h->n_events && h->sc_B == h->B) return 0;
+    const uint32_t n = (uint32_t)h->n_events;
+    const uint32_t G = h->shard_count;
+    if (n > h->sc_cap || h->sc_rows.size() != G) {
+        for (uint32_t *p : h->sc_rows)
+            if (p) (void)hipFree(p);
+        h->sc_rows.assign(G, nullptr);
+        uint64_t cap = std::max<uint64_t>(n, 4096);
+        for (uint32_t q = 0; q < G; q++) HIPCHK(h, dalloc(&h->sc_rows[q], cap));
+        if (h->sc_flag) (void)hipFree(h->sc_flag);
+        if (h->sc_pos) (void)hipFree(h->sc_pos);
+        HIPCHK(h, dalloc(&h->sc_flag, cap));
+        HIPCHK(h, dalloc(&h->sc_pos, cap));
+        size_t sb = 0;
+        HIPCHK(h, lx::scan_tmp_bytes((uint32_t)cap, &sb));
+        if (h->sc_tmp) (void)hipFree(h->sc_tmp);
+        HIPCHK(h, hipMalloc(&h->sc_tmp, sb ? sb : 1));
+        h->sc_tmp_bytes = sb;
+        h->sc_cap = cap;
+    }
+    h->sc_nrows.assign(G, 0);
+    for (uint32_t q = 0; q < G; q++) {
+        uint32_t lo, hi;
+        shard_bounds(h, q, &lo, &hi);
+        HIPCHK(h, lx::launch_shard_rows(h->ev_branch, h->branch_creator, n, lo, hi, h->sc_flag, h->sc_pos, h->sc_tmp,
+                                        h->sc_tmp_bytes, h->sc_rows[q], h->stream));
+        if (n) HIPCHK(h, hipMemcpyAsync(&h->sc_nrows[q], h->sc_pos + (n - 1), 4, hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+    }
+    h->sc_events = h->n_events;
+    h->sc_B = h->B;
+    return 0;
+}
+
+int upload_cols(lx_index *h, const std::vector<uint32_t> &cols) {
+    if (cols.empty()) return 0;
+    if (h->sc_cols) (void)hipFree(h->sc_cols);
+    HIPCHK(h, dalloc(&h->sc_cols, cols.size()));
+    HIPCHK(h, hipMemcpyAsync(h->sc_cols, cols.data(), cols.size() * 4, hipMemcpyHostToDevice, h->stream));
+    return 0;
+}
+
 int read_u32(lx_index *h, const uint32_t *dev, uint32_t *out) {
     HIPCHK(h, hipMemcpy(out, dev, 4, hipMemcpyDeviceToHost));
     return 0;
@@ -525,14 +608,8 @@ int lx_reset(lx_index *h, uint32_t nv, const uint32_t *w) {
     h->V = nv;
     h->weights.assign(w, w + nv);
     h->quorum = (uint32_t)(tot * 2 / 3 + 1);
-    if (h->shard_count > 1) {
-        auto bound = [&](uint32_t r) { return r == h->shard_count ? nv : (uint32_t)((uint64_t)nv * r / h->shard_count) & ~3u; };
-        h->own_lo = bound(h->shard_rank);
-        h->own_hi = bound(h->shard_rank + 1);
-    } else {
-        h->own_lo = 0;
-        h->own_hi = nv;
-    }
+    shard_bounds(h, h->shard_rank, &h->own_lo, &h->own_hi);
+    h->sc_events = ~0ull;
     uint32_t reserve = h->reserve ? h->reserve : std::max<uint32_t>(64, nv / 16);
     uint32_t want_stride = round_up(nv + reserve, 64);
     // (re)allocate when the layout changes; otherwise zero what the last epoch used
@@ -821,6 +898,49 @@ int lx_get_branches_info(lx_index *h, uint32_t *last_seq, uint32_t *creator_idx,
         if (last_seq) last_seq[b] = len[b] ? h->h_branch_first[b] + len[b] - 1 : 0;
         if (creator_idx) creator_idx[b] = h->h_branch_creator[b];
     }
+    return 0;
+}
+
+int lx_shard_range(const lx_index *h, uint32_t shard, uint32_t *lo, uint32_t *hi) {
+    if (!h || shard >= h->shard_count) return LX_ERR_ARG;
+    shard_bounds(h, shard, lo, hi);
+    return 0;
+}
+
+int lx_shard_block(lx_index *h, uint32_t src, uint32_t dst, uint64_t *elems) {
+    if (!h || !elems || src >= h->shard_count || dst >= h->shard_count) return LX_ERR_ARG;
+    HIPCHK(h, hipSetDevice(h->device));
+    int rc;
+    if ((rc = ensure_shard_rows(h))) return rc;
+    *elems = (uint64_t)h->sc_nrows[src] * shard_cols(h, dst).size();
+    return 0;
+}
+
+int lx_la_pack_dev(lx_index *h, uint32_t dst, uint32_t *out, void *stream) {
+    if (!h || dst >= h->shard_count) return LX_ERR_ARG;
+    HIPCHK(h, hipSetDevice(h->device));
+    int rc;
+    if ((rc = ensure_shard_rows(h))) return rc;
+    std::vector<uint32_t> cols = shard_cols(h, dst);
+    if ((rc = upload_cols(h, cols))) return rc;
+    HIPCHK(h, lx::launch_la_block(h->la, h->stride, h->sc_rows[h->shard_rank], h->sc_nrows[h->shard_rank], h->sc_cols,
+                                  (uint32_t)cols.size(), out, 0, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    (void)stream;
+    return 0;
+}
+
+int lx_la_unpack_dev(lx_index *h, uint32_t src, const uint32_t *in, void *stream) {
+    if (!h || src >= h->shard_count) return LX_ERR_ARG;
+    HIPCHK(h, hipSetDevice(h->device));
+    int rc;
+    if ((rc = ensure_shard_rows(h))) return rc;
+    std::vector<uint32_t> cols = shard_cols(h, h->shard_rank);
+    if ((rc = upload_cols(h, cols))) return rc;
+    HIPCHK(h, lx::launch_la_block(h->la, h->stride, h->sc_rows[src], h->sc_nrows[src], h->sc_cols,
+                                  (uint32_t)cols.size(), const_cast<uint32_t *>(in), 1, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    (void)stream;
     return 0;
 }
 

@@ -265,18 +265,18 @@ __device__ __forceinline__ void wait_vmcnt_le(uint32_t n) {
 }
 
 template <int CPW, int NCW, int RING, int RR, bool FILL>
-__global__ __launch_bounds__(64 * (NCW + 1)) void k_index(IndexArgs a) {
-    constexpr int NT = 64 * (NCW + 1);
+__global__ __launch_bounds__(64 * (NCW + 2)) void k_index(IndexArgs a) {
+    constexpr int NT = 64 * (NCW + 2);
     constexpr int E = 64 * NCW;
-    constexpr int SAFE0 = RING / E - 2;
-    constexpr int SAFE = SAFE0 > 60 ? 60 : SAFE0;
     constexpr int RQ = LX_REC_Q;
+    constexpr int WD = 8;                        // writer rounds (of 64 events) in flight
     static_assert(RING % E == 0 && RING / E >= 4, "ring slot reuse must stay within one lane");
     static_assert(RR % 64 == 0 && RR / 64 <= 8 && RR >= E, "record ring");
     __shared__ uint64_t ring[RING * CPW];        // per event: CPW x {tag, seq} granules
     __shared__ uint4 rrec[RR * RQ];              // event records
     __shared__ uint32_t rtag[RR];
     __shared__ uint2 brc[CPW * kBRC];            // {seq, event} of recent events of owned branches
+    __shared__ uint32_t wm[2];                   // writer watermarks: [0] ring entries copied, [1] HB stores done
 
     const uint32_t w = blockIdx.x;
     const uint32_t slice = (w % 8) * a.slices_per_xcd + (w / 8);   // XCD-aware: neighbouring slices share an L2
@@ -285,6 +285,7 @@ __global__ __launch_bounds__(64 * (NCW + 1)) void k_index(IndexArgs a) {
     for (int i = threadIdx.x; i < RING * CPW; i += NT) ring[i] = 0;
     for (int i = threadIdx.x; i < RR; i += NT) rtag[i] = 0;
     for (int i = threadIdx.x; i < CPW * kBRC; i += NT) brc[i] = make_uint2(0, LX_NONE);
+    if (threadIdx.x < 2) wm[threadIdx.x] = 0;
     __syncthreads();
 
     const uint32_t n = a.n;
@@ -292,6 +293,20 @@ __global__ __launch_bounds__(64 * (NCW + 1)) void k_index(IndexArgs a) {
     const int wave = threadIdx.x / 64;
     const int lane = threadIdx.x % 64;
     const uint32_t diag = a.diag;   // 0 normal; timing-only diagnostics: 2 no deps, 3 no global stores
+    const uint64_t stride = a.stride;
+
+    uint32_t col[CPW], first[CPW];
+    bool valid[CPW];
+    bool contig = true;
+#pragma unroll
+    for (int k = 0; k < CPW; k++) {
+        const uint32_t ci = slice * CPW + k;
+        valid[k] = ci < a.ncols;
+        col[k] = valid[k] ? a.col_list[ci] : 0;
+        first[k] = valid[k] ? a.branch_first[col[k]] : 1;
+        contig &= valid[k] && col[k] == col[0] + k;
+    }
+    contig &= (col[0] % CPW) == 0;
 
     if (wave == NCW) {
         // ------------------------------------------------------------ loader
@@ -304,13 +319,12 @@ __global__ __launch_bounds__(64 * (NCW + 1)) void k_index(IndexArgs a) {
             bool progressed = false;
             if (issued < nrounds && issued - done < D) {
                 // slots of this round are free once their previous occupants
-                // (events ev - RR) are done
+                // (events ev - RR) are done (their ring entry is written)
                 const uint32_t ev = issued * 64 + lane;
                 bool free = true;
                 if (ev < n && ev >= (uint32_t)RR) {
                     const uint32_t q = ev - RR;
-                    const uint64_t g0 = __hip_atomic_load(ring + (q % RING) * CPW,
-                                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    const uint64_t g0 = __hip_atomic_load(ring + (q % RING) * CPW, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     if ((uint32_t)g0 < q + 1) free = false;
                 }
                 if (__all(free)) {
@@ -349,17 +363,76 @@ __global__ __launch_bounds__(64 * (NCW + 1)) void k_index(IndexArgs a) {
         return;
     }
 
-    // ---------------------------------------------------------------- compute
-    uint32_t col[CPW], first[CPW];
-    bool valid[CPW];
+    if (wave == NCW + 1) {
+        // ------------------------------------------------------------ writer
+        // copies completed ring entries to the HB plane in rounds of 64 events
+        // and publishes wm[0] (entries copied: their slots may be reused) and
+        // wm[1] (HB stores complete: an L2 read of those rows is safe)
+        const uint32_t nrounds = (n + 63) / 64;
+        const uint32_t spr = contig ? (CPW + 3) / 4 : CPW;   // store instructions per round
+        uint32_t issued = 0, done = 0;
+        while (done < nrounds) {
+            bool progressed = false;
+            if (issued < nrounds && issued - done < WD) {
+                const uint32_t ev = issued * 64 + lane;
+                uint64_t g[CPW];
+                bool ready = true;
+                if (ev < n) {
 #pragma unroll
-    for (int k = 0; k < CPW; k++) {
-        const uint32_t ci = slice * CPW + k;
-        valid[k] = ci < a.ncols;
-        col[k] = valid[k] ? a.col_list[ci] : 0;
-        first[k] = valid[k] ? a.branch_first[col[k]] : 1;
+                    for (int k = 0; k < CPW; k++) {
+                        g[k] = __hip_atomic_load(ring + (ev % RING) * CPW + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        ready &= ((uint32_t)g[k] == ev + 1);
+                    }
+                }
+                if (__all(ready)) {
+                    if (ev < n && diag != 3) {
+                        uint32_t *hrow = a.hb + (uint64_t)(bs + ev) * stride;
+                        if (contig) {
+                            if (CPW == 1) {
+                                hrow[col[0]] = (uint32_t)(g[0] >> 32);
+                            } else if (CPW == 2) {
+                                *reinterpret_cast<uint2 *>(hrow + col[0]) = make_uint2((uint32_t)(g[0] >> 32), (uint32_t)(g[1 % CPW] >> 32));
+                            } else {
+#pragma unroll
+                                for (int k = 0; k < CPW; k += 4)
+                                    *reinterpret_cast<uint4 *>(hrow + col[0] + k) =
+                                        make_uint4((uint32_t)(g[k] >> 32), (uint32_t)(g[(k + 1) % CPW] >> 32),
+                                                   (uint32_t)(g[(k + 2) % CPW] >> 32), (uint32_t)(g[(k + 3) % CPW] >> 32));
+                            }
+                        } else {
+#pragma unroll
+                            for (int k = 0; k < CPW; k++)
+                                if (valid[k]) hrow[col[k]] = (uint32_t)(g[k] >> 32);
+                        }
+                    }
+                    issued++;
+                    if (lane == 0) __hip_atomic_store(&wm[0], min(issued * 64, n), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    progressed = true;
+                }
+            }
+            if (!progressed && issued > done) {
+                // the oldest round's stores are complete once at most spr per younger round remain
+                const uint32_t younger = (issued - done - 1) * spr;
+                if (younger >= 56) asm volatile("s_waitcnt vmcnt(56)" ::: "memory");
+                else if (younger >= 48) asm volatile("s_waitcnt vmcnt(48)" ::: "memory");
+                else if (younger >= 40) asm volatile("s_waitcnt vmcnt(40)" ::: "memory");
+                else if (younger >= 32) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+                else if (younger >= 24) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+                else if (younger >= 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+                else if (younger >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+                else if (younger >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+                else if (younger >= 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                done++;
+                if (lane == 0) __hip_atomic_store(&wm[1], min(done * 64, n), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            } else if (!progressed) {
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        return;
     }
-    const uint64_t stride = a.stride;
+
+    // ---------------------------------------------------------------- compute
     const uint32_t mask = a.mask ? LX_SEQ_MASK : 0xFFFFFFFFu;
     const uint64_t *ring64 = ring;
 
@@ -367,9 +440,10 @@ __global__ __launch_bounds__(64 * (NCW + 1)) void k_index(IndexArgs a) {
     bool have = false;
     uint32_t br = 0, seq = 0, np = 0, prev = 0, ovf = 0, xi = 0;
     uint32_t par[LX_MAXP];
-    uint32_t todo = 0;
+    uint32_t todo = 0, slow = 0;
     uint32_t wait_off = 0, wait_tag = 0;          // the one granule this lane spins on
     uint32_t r[CPW], v0[CPW];
+    bool filled = false;
 
     while (lp < n) {
         if (!have) {
@@ -385,21 +459,23 @@ __global__ __launch_bounds__(64 * (NCW + 1)) void k_index(IndexArgs a) {
                 par[4 * j] = q.x - bs; par[4 * j + 1] = q.y - bs; par[4 * j + 2] = q.z - bs; par[4 * j + 3] = q.w - bs;
             }
             todo = (np >= LX_MAXP) ? 0xFFFFu : ((1u << np) - 1u);
+            if (diag == 2) todo = 0;
+            slow = 0;
             xi = LX_MAXP;
 #pragma unroll
             for (int k = 0; k < CPW; k++) { r[k] = (col[k] == br) ? seq : 0u; v0[k] = 0; }
             // spin on the newest in-batch parent first (parents sorted newest first)
             const uint32_t l0 = par[0];
-            wait_off = (np > 0 && l0 < n && diag != 2) ? (l0 % RING) * CPW : 0u;
-            wait_tag = (np > 0 && l0 < n && diag != 2) ? l0 + 1 : 0u;
-            if (diag == 2) todo = 0;
+            const bool sp = (np > 0 && l0 < n && diag != 2);
+            wait_off = sp ? (l0 % RING) * CPW : 0u;
+            wait_tag = sp ? l0 + 1 : 0u;
+            filled = false;
             have = true;
         }
         // cheap spin: one granule tag (an overwritten slot reads as >= tag)
         if ((uint32_t)__hip_atomic_load(ring64 + wait_off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < wait_tag)
             continue;
         // fold every pending parent, chunks of 4: issue granule reads, then evaluate
-        uint32_t slow = 0;
 #pragma unroll
         for (int c = 0; c < LX_MAXP / 4; c++) {
             if (!__any(todo >> (4 * c))) break;   // wave-uniform
@@ -434,10 +510,12 @@ __global__ __launch_bounds__(64 * (NCW + 1)) void k_index(IndexArgs a) {
             }
         }
         if (slow) {
-            // slow path: parents older than the ring (or from an earlier batch)
+            // slow path: parents older than the ring (or from an earlier batch);
+            // their HB rows are in L2 once the writer's watermark passed them
+            const uint32_t stored = __hip_atomic_load(&wm[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
 #pragma unroll
             for (int j = 0; j < LX_MAXP; j++) {
-                if (slow & (1u << j)) {
+                if ((slow & (1u << j)) && (par[j] >= n || par[j] < stored)) {
                     const uint32_t *row = a.hb + (uint64_t)(par[j] + bs) * stride;
                     const bool isprev = (par[j] + bs == prev);
 #pragma unroll
@@ -446,8 +524,10 @@ __global__ __launch_bounds__(64 * (NCW + 1)) void k_index(IndexArgs a) {
                         r[k] = max(r[k], v);
                         if (isprev) v0[k] = v;
                     }
+                    slow &= ~(1u << j);
                 }
             }
+            if (slow) continue;   // writer has not stored them yet
         }
         if (todo) {
             // some parent still pending: spin on the lowest pending one next
@@ -474,8 +554,9 @@ __global__ __launch_bounds__(64 * (NCW + 1)) void k_index(IndexArgs a) {
                         ok &= ((uint32_t)gg[k] == lpp + 1);
                     }
                     if (!ok) {
-                        if ((uint32_t)gg[0] > lpp + 1) rd = false;   // overwritten: read L2
-                        else break;                                  // not ready yet
+                        if ((uint32_t)gg[0] <= lpp + 1) break;   // not ready yet
+                        if (lpp >= __hip_atomic_load(&wm[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
+                        rd = false;                                // overwritten and stored: read L2
                     }
                 } else {
                     rd = false;
@@ -495,38 +576,39 @@ __global__ __launch_bounds__(64 * (NCW + 1)) void k_index(IndexArgs a) {
         }
         {
             const uint32_t e = bs + lp;
-            uint32_t *hrow = a.hb + (uint64_t)e * stride;
+            if (!filled) {
 #pragma unroll
-            for (int k = 0; k < CPW; k++) {
-                if (!valid[k]) continue;
-                if (diag != 3) hrow[col[k]] = r[k];
-                if (col[k] == br)
-                    __hip_atomic_store(reinterpret_cast<uint64_t *>(brc + k * kBRC + seq % kBRC),
-                                       ((uint64_t)e << 32) | seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            }
-            if (FILL && diag != 3) {
-                // LowestAfter range fill: events (col, s), s in (h0, r], are first
-                // observed from branch `br` by this event.
+                for (int k = 0; k < CPW; k++)
+                    if (valid[k] && col[k] == br)
+                        __hip_atomic_store(reinterpret_cast<uint64_t *>(brc + k * kBRC + seq % kBRC),
+                                           ((uint64_t)e << 32) | seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (FILL && diag != 3) {
+                    // LowestAfter range fill: events (col, s), s in (h0, r], are first
+                    // observed from branch `br` by this event.
 #pragma unroll
-                for (int k = 0; k < CPW; k++) {
-                    if (!valid[k]) continue;
-                    const uint32_t h0 = (prev != LX_NONE) ? v0[k] : 0u;
-                    const uint32_t lo = max(h0 + 1u, first[k]);
-                    for (uint32_t s = lo; s <= r[k]; s++) {
-                        const uint64_t cc = __hip_atomic_load(reinterpret_cast<const uint64_t *>(brc + k * kBRC + s % kBRC),
-                                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        uint32_t row = (uint32_t)(cc >> 32);
-                        if ((uint32_t)cc != s) row = ld_l2_now(a.brow + (uint64_t)col[k] * a.s_cap + (s - first[k]));
-                        a.la[(uint64_t)row * stride + br] = seq;
+                    for (int k = 0; k < CPW; k++) {
+                        if (!valid[k]) continue;
+                        const uint32_t h0 = (prev != LX_NONE) ? v0[k] : 0u;
+                        const uint32_t lo = max(h0 + 1u, first[k]);
+                        for (uint32_t s = lo; s <= r[k]; s++) {
+                            const uint64_t cc = __hip_atomic_load(reinterpret_cast<const uint64_t *>(brc + k * kBRC + s % kBRC),
+                                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            uint32_t row = (uint32_t)(cc >> 32);
+                            if ((uint32_t)cc != s) row = ld_l2_now(a.brow + (uint64_t)col[k] * a.s_cap + (s - first[k]));
+                            a.la[(uint64_t)row * stride + br] = seq;
+                        }
                     }
                 }
+                filled = true;
             }
-            // bound this lane's stores in flight so that the HB stores of the
-            // event whose slot is overwritten RING/E completions later are done
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SAFE) : "memory");
+            // the slot's previous occupant (lp - RING) must have been copied by the writer
+            if (lp >= (uint32_t)RING &&
+                __hip_atomic_load(&wm[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < lp - RING + 1)
+                continue;
             uint64_t *dst = ring + (lp % RING) * CPW;
 #pragma unroll
-            for (int k = 0; k < CPW; k++) dst[k] = ((uint64_t)r[k] << 32) | (lp + 1);
+            for (int k = 0; k < CPW; k++)
+                __hip_atomic_store(dst + k, ((uint64_t)r[k] << 32) | (lp + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             lp += E;
             have = false;
         }
@@ -539,8 +621,8 @@ static hipError_t launch_index_t(const IndexArgs &a0, hipStream_t s) {
     a.n_slices = (a.ncols + CPW - 1) / CPW;
     a.slices_per_xcd = (a.n_slices + 7) / 8;
     uint32_t grid = a.slices_per_xcd * 8;
-    if (a.diag_nofill) hipLaunchKernelGGL((k_index<CPW, NCW, RING, RR, false>), dim3(grid), dim3(64 * (NCW + 1)), 0, s, a);
-    else hipLaunchKernelGGL((k_index<CPW, NCW, RING, RR, true>), dim3(grid), dim3(64 * (NCW + 1)), 0, s, a);
+    if (a.diag_nofill) hipLaunchKernelGGL((k_index<CPW, NCW, RING, RR, false>), dim3(grid), dim3(64 * (NCW + 2)), 0, s, a);
+    else hipLaunchKernelGGL((k_index<CPW, NCW, RING, RR, true>), dim3(grid), dim3(64 * (NCW + 2)), 0, s, a);
     return hipGetLastError();
 }
 
@@ -749,6 +831,57 @@ hipError_t launch_unfill(const UnfillArgs &a, hipStream_t s) {
     uint64_t total = (uint64_t)(a.hi - a.lo) * a.B;
     hipLaunchKernelGGL(k_unfill, dim3((uint32_t)((total + 255) / 256)), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_unclaim, dim3(nblk(a.hi - a.lo, 256)), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------- column shards
+// Multi-GPU column sharding: rows whose branch belongs to
+// shard q carry complete LowestAfter rows only on q; shard r needs the columns
+// of its own branches for every row.  pack/unpack move the (rows of q) x
+// (columns of r) blocks for an all-to-all.
+__global__ void k_shard_flags(const uint32_t *ev_branch, const uint32_t *branch_creator, uint32_t n,
+                              uint32_t lo, uint32_t hi, uint32_t *flag) {
+    uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n) return;
+    const uint32_t c = branch_creator[ev_branch[e]];
+    flag[e] = (c >= lo && c < hi) ? 1u : 0u;
+}
+
+__global__ void k_compact(const uint32_t *flag, const uint32_t *pos, uint32_t n, uint32_t *rows) {
+    uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n) return;
+    if (flag[e]) rows[pos[e] - 1] = (uint32_t)e;
+}
+
+// out[i][k] = la[rows[i]][cols[k]]   (pack)   /   la[rows[i]][cols[k]] = in[i][k]   (unpack)
+__global__ void k_la_block(uint32_t *la, uint64_t stride, const uint32_t *rows, uint32_t nrows, const uint32_t *cols,
+                           uint32_t ncols, uint32_t *buf, int unpack) {
+    uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (uint64_t)nrows * ncols) return;
+    const uint32_t i = (uint32_t)(t / ncols), k = (uint32_t)(t % ncols);
+    uint32_t *cell = la + (uint64_t)rows[i] * stride + cols[k];
+    if (unpack) *cell = buf[t];
+    else buf[t] = *cell;
+}
+
+hipError_t launch_shard_rows(const uint32_t *ev_branch, const uint32_t *branch_creator, uint32_t n, uint32_t lo,
+                             uint32_t hi, uint32_t *flag, uint32_t *pos, void *scan_tmp, size_t scan_bytes,
+                             uint32_t *rows, hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_shard_flags, dim3(nblk(n, 256)), dim3(256), 0, s, ev_branch, branch_creator, n, lo, hi, flag);
+    size_t tb = scan_bytes;
+    hipError_t r = hipcub::DeviceScan::InclusiveSum(scan_tmp, tb, flag, pos, (int)n, s);
+    if (r != hipSuccess) return r;
+    hipLaunchKernelGGL(k_compact, dim3(nblk(n, 256)), dim3(256), 0, s, flag, pos, n, rows);
+    return hipGetLastError();
+}
+
+hipError_t launch_la_block(uint32_t *la, uint64_t stride, const uint32_t *rows, uint32_t nrows, const uint32_t *cols,
+                           uint32_t ncols, uint32_t *buf, int unpack, hipStream_t s) {
+    uint64_t total = (uint64_t)nrows * ncols;
+    if (!total) return hipSuccess;
+    hipLaunchKernelGGL(k_la_block, dim3((uint32_t)((total + 255) / 256)), dim3(256), 0, s, la, stride, rows, nrows,
+                       cols, ncols, buf, unpack);
     return hipGetLastError();
 }
 

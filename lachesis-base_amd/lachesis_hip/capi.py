@@ -37,6 +37,10 @@ SIGNATURES = [
     ("lx_get_merged_highest_before", ctypes.c_int, [vp, ctypes.c_uint32, u8p, ctypes.c_uint32, u32p]),
     ("lx_get_event_branch_id", ctypes.c_int, [vp, ctypes.c_uint32, u32p]),
     ("lx_get_branches_info", ctypes.c_int, [vp, u32p, u32p, ctypes.c_uint32, u32p]),
+    ("lx_shard_range", ctypes.c_int, [vp, ctypes.c_uint32, u32p, u32p]),
+    ("lx_shard_block", ctypes.c_int, [vp, ctypes.c_uint32, ctypes.c_uint32, u64p]),
+    ("lx_la_pack_dev", ctypes.c_int, [vp, ctypes.c_uint32, vp, vp]),
+    ("lx_la_unpack_dev", ctypes.c_int, [vp, ctypes.c_uint32, vp, vp]),
     ("lx_last_stats", ctypes.c_int, [vp, vp]),
     ("lx_device_planes", ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), u32p, ctypes.POINTER(vp)]),
     ("lx_sync", ctypes.c_int, [vp]),
@@ -207,6 +211,23 @@ class Index:
         cr = np.zeros(n.value, dtype=np.uint32)
         self._chk(self.L.lx_get_branches_info(self.h, _p(ls, u32p), _p(cr, u32p), n.value, ctypes.byref(n)))
         return ls, cr
+
+    # column shards -------------------------------------------------------------
+    def shard_range(self, shard):
+        lo, hi = ctypes.c_uint32(), ctypes.c_uint32()
+        self._chk(self.L.lx_shard_range(self.h, shard, ctypes.byref(lo), ctypes.byref(hi)))
+        return lo.value, hi.value
+
+    def shard_block(self, src, dst):
+        n = ctypes.c_uint64()
+        self._chk(self.L.lx_shard_block(self.h, src, dst, ctypes.byref(n)))
+        return n.value
+
+    def la_pack_dev(self, dst, out_ptr):
+        self._chk(self.L.lx_la_pack_dev(self.h, dst, out_ptr, None))
+
+    def la_unpack_dev(self, src, in_ptr):
+        self._chk(self.L.lx_la_unpack_dev(self.h, src, in_ptr, None))
 
     def last_stats(self):
         st = LxStats()

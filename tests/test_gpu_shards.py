@@ -1,0 +1,65 @@
+"""Column-sharded index on one GPU: G handles, each
+owning a creator range, exchange LowestAfter blocks (what the all-to-all does
+between GPUs), compute ForklessCause partial stake sums, add them (what the
+all-reduce does) and combine.  Must equal the unsharded index and the oracle."""
+
+import numpy as np
+import pytest
+
+from oracle import corc
+
+pytestmark = pytest.mark.gpu
+
+
+def sharded_fc(lx, d, weights, G, qa, qb):
+    import torch
+    dev = torch.device("cuda", 0)
+    shards = []
+    for r in range(G):
+        ix = lx.Index(shard_rank=r, shard_count=G)
+        ix.reset(weights)
+        ix.add_batch(d.creator, d.seq, d.poff, d.par)
+        shards.append(ix)
+    # all-to-all of LowestAfter blocks
+    for s in range(G):
+        for t in range(G):
+            if s == t:
+                continue
+            n = shards[s].shard_block(s, t)
+            assert n == shards[t].shard_block(s, t)
+            buf = torch.zeros(max(n, 1), dtype=torch.int32, device=dev)
+            shards[s].la_pack_dev(t, buf.data_ptr())
+            shards[t].la_unpack_dev(s, buf.data_ptr())
+    a = torch.from_numpy(qa.view(np.int32)).to(dev)
+    b = torch.from_numpy(qb.view(np.int32)).to(dev)
+    total = torch.zeros(len(qa), dtype=torch.int64, device=dev)
+    for ix in shards:
+        part = torch.zeros(len(qa), dtype=torch.int32, device=dev)
+        ix.forkless_cause_partial_dev(len(qa), a.data_ptr(), b.data_ptr(), part.data_ptr())
+        ix.sync()
+        total += part.to(torch.int64) & 0xFFFFFFFF
+    s32 = (total & 0xFFFFFFFF).to(torch.int64)
+    s32 = torch.where(s32 >= 2 ** 31, s32 - 2 ** 32, s32).to(torch.int32)
+    out = torch.zeros(len(qa), dtype=torch.uint8, device=dev)
+    shards[0].fc_combine_dev(len(qa), s32.data_ptr(), out.data_ptr())
+    shards[0].sync()
+    return out.cpu().numpy(), shards
+
+
+@pytest.mark.parametrize("G", [2, 3, 4])
+@pytest.mark.parametrize("shape", [(16, 40, 5, 0, 0, 1), (24, 30, 6, 5, 6, 2)])
+def test_sharded_fc_matches_oracle(G, shape):
+    import lachesis_hip as lx
+    n, ev, p, ch, fk, seed = shape
+    d = lx.tools.gen_dag(n, ev, p, ch, fk, seed)
+    rng = np.random.default_rng(seed)
+    weights = sorted((int(x) for x in rng.integers(1, 20, n)), reverse=True)
+    o = corc.OracleIndex(weights)
+    assert o.add_batch(d.creator, d.seq, d.poff, d.par) == -1
+    qa, qb = lx.tools.fc_queries(d.lamport, 50_000, window=24, seed=seed)
+    got, shards = sharded_fc(lx, d, weights, G, qa, qb)
+    np.testing.assert_array_equal(got, o.forkless_cause_batch(qa, qb))
+    # the shard ranges partition the creators
+    ranges = [shards[0].shard_range(r) for r in range(G)]
+    assert ranges[0][0] == 0 and ranges[-1][1] == n
+    assert all(ranges[i][1] == ranges[i + 1][0] for i in range(G - 1))
