@@ -14,9 +14,13 @@ before timing.
                SURVEY 8d) -- vecfc/forkless_cause.go:28-82
 
 value = events indexed/sec (whole job, all ranks); fc_queries_per_sec is
-reported beside it.  Multi-GPU: one process per GPU; each rank runs the same
-workload as an independent replica (weak scaling; column sharding is a later
-step).
+reported beside it.  Multi-GPU: one process per GPU.
+  --mode replica (default): each rank indexes its own copy of the workload
+      (independent epochs / nodes; no data-path collective; weak scaling).
+  --mode shard: the ranks split ONE epoch by creator columns
+      (lachesis_hip/shard.py): each indexes its columns,
+      the index step ends with the RCCL all-to-all of LowestAfter blocks, and
+      FC sums per-rank partial stakes with an all-reduce (strong scaling).
 """
 
 import argparse
@@ -81,6 +85,7 @@ def main():
     ap.add_argument("--batch", type=int, default=0, help="events per lx_add_batch_dev call (0 = whole epoch)")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--mode", default="replica", choices=["replica", "shard"])
     args = ap.parse_args()
 
     import numpy as np
@@ -124,8 +129,14 @@ def main():
     d_qa, d_qb = to_dev(qa), to_dev(qb)
     d_out = torch.empty(args.fc_queries, dtype=torch.uint8, device=dev)
 
-    ix = lx.Index(device=local, event_capacity=N)
-    hb_ptr, la_ptr, stride, stream_ptr = ix.device_planes()
+    shard = args.mode == "shard" and world > 1
+    if shard:
+        ix = lx.Index(device=local, event_capacity=N, shard_rank=rank, shard_count=world)
+        from lachesis_hip.shard import ShardedIndex
+        sx = ShardedIndex(ix, device=dev)
+        d_part = torch.empty(args.fc_queries, dtype=torch.int32, device=dev)
+    else:
+        ix = lx.Index(device=local, event_capacity=N)
 
     def index_step():
         ix.reset(weights)
@@ -137,6 +148,8 @@ def main():
             s = ix.last_stats()
             st_idx += s["ms_index"]
             st_asg += s["ms_assign"] + s["ms_marks"]
+        if shard:
+            sx.exchange()
         return st_idx, st_asg
 
     _, _, _, stream_ptr = ix.device_planes()
@@ -145,9 +158,17 @@ def main():
     def fc_step(evs=None):
         if evs is not None:
             evs[0].record(lib_stream)
-        ix.forkless_cause_batch_dev(args.fc_queries, d_qa.data_ptr(), d_qb.data_ptr(), d_out.data_ptr())
+        if shard:
+            ix.forkless_cause_partial_dev(args.fc_queries, d_qa.data_ptr(), d_qb.data_ptr(), d_part.data_ptr())
+        else:
+            ix.forkless_cause_batch_dev(args.fc_queries, d_qa.data_ptr(), d_qb.data_ptr(), d_out.data_ptr())
         if evs is not None:
             evs[1].record(lib_stream)
+        if shard:
+            ix.sync()
+            dist.all_reduce(d_part, op=dist.ReduceOp.SUM)   # int32 wrap-around = exact uint32 sum
+            torch.cuda.current_stream(dev).synchronize()
+            ix.fc_combine_dev(args.fc_queries, d_part.data_ptr(), d_out.data_ptr())
 
     def barrier():
         if world > 1:
@@ -192,9 +213,13 @@ def main():
     out_host = d_out[:2000].cpu().numpy()
     assert out_host.max() <= 1
 
-    events_per_s = N * args.steps * world / t_index
-    fc_per_s = args.fc_queries * args.steps * world / t_fc
+    units = 1 if shard else world          # shard: the ranks share one epoch
+    events_per_s = N * args.steps * units / t_index
+    fc_per_s = args.fc_queries * args.steps * units / t_fc
     B = ix.num_branches()
+    if shard:
+        lo, hi = ix.shard_range(rank)
+        B = hi - lo                         # columns this rank streams (no forks in the bench DAG)
     fc_bytes = 8.0 * B * args.fc_queries                       # HB(a).Seq 4B + LA(b) 4B per branch
     fc_achieved = fc_bytes / (fc_kernel_ms * 1e-3) / 1e9
     kidx = float(np.mean(k_index_ms))
@@ -212,14 +237,14 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": t_index / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if shard else "weak",
         "vs_baseline": None,
         "dtype": "u32",
         "data": "synthetic tdag-structured DAG (splitmix64 seed 1), no forks",
         "config": {"workload": "%s: V=%d, %d events (%d/validator), P=%d, %s stakes, cheaters=%d; FC 2^%d queries, b within 64 Lamport of a"
                    % (args.config, V, N, epv, P, wkind, cheaters, int(np.log2(args.fc_queries)), ),
                    "validators": V, "events": N, "parents": P, "fc_queries": args.fc_queries,
-                   "parallelism": "replica%d" % world, "batch": batch},
+                   "parallelism": ("colshard%d" if shard else "replica%d") % world, "batch": batch},
         "fc_queries_per_sec": fc_per_s,
         "fc_ms_per_step": t_fc / args.steps * 1e3,
         "index_kernel_ms": kidx,

@@ -1,0 +1,87 @@
+"""Column-sharded index across GPUs.
+
+One process per GPU; rank r holds an :class:`~lachesis_hip.Index` created
+with ``shard_rank=r, shard_count=world`` and indexes the same event stream
+as every other rank, but only the branches whose creator lies in its creator
+range (``lx_shard_range``).  HighestBefore needs no communication (a column
+depends only on the same column of the parents).  Two steps do:
+
+* :meth:`ShardedIndex.exchange` -- before ForklessCause, every rank needs the
+  LowestAfter entries of *its* columns for events on the other ranks'
+  branches.  Block (src -> dst) = rows on src's branches x dst's columns
+  (``lx_shard_block``); one ``all_to_all_single`` moves all of them.
+* :meth:`ShardedIndex.forkless_cause_dev` -- each rank sums the stake of its
+  own creators that ``b`` is forkless-caused by (``lx_forkless_cause_partial_dev``;
+  bit 31 carries "a observes branch(b) as forked" from the owning rank); one
+  ``all_reduce`` adds the partials and ``lx_fc_combine_dev`` applies quorum.
+
+The reference has no multi-process index (vecfc/index.go is single-node);
+this is the MI355X-side scale-out of the same computation, bit-exact to the
+unsharded index (tests/test_gpu_shards.py).
+
+The protocol is written against a small provider interface (the methods of
+:class:`~lachesis_hip.Index` used below) so the collective plumbing can be
+exercised with gloo on CPU (tests/test_shard_protocol.py).
+"""
+
+import torch
+import torch.distributed as dist
+
+
+class ShardedIndex:
+    def __init__(self, index, group=None, device=None):
+        """``index``: this rank's handle (shard_rank = rank, shard_count = world)."""
+        self.ix = index
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+
+    # ------------------------------------------------------------------ LA
+    def exchange(self):
+        """All-to-all of LowestAfter blocks; returns the element counts sent."""
+        r, G = self.rank, self.world
+        send_n = [self.ix.shard_block(r, t) if t != r else 0 for t in range(G)]
+        recv_n = [self.ix.shard_block(s, r) if s != r else 0 for s in range(G)]
+        send = torch.empty(max(sum(send_n), 1), dtype=torch.int32, device=self.device)
+        recv = torch.empty(max(sum(recv_n), 1), dtype=torch.int32, device=self.device)
+        off = 0
+        for t in range(G):
+            if send_n[t]:
+                self.ix.la_pack_dev(t, send.data_ptr() + 4 * off)
+            off += send_n[t]
+        self.ix.sync()   # packs run on the library stream; the collective on torch's
+        if G > 1:
+            dist.all_to_all_single(recv[:sum(recv_n)] if sum(recv_n) else recv[:0],
+                                   send[:sum(send_n)] if sum(send_n) else send[:0],
+                                   output_split_sizes=recv_n, input_split_sizes=send_n, group=self.group)
+        if self.device.type == "cuda":
+            torch.cuda.current_stream(self.device).synchronize()
+        off = 0
+        for s in range(G):
+            if recv_n[s]:
+                self.ix.la_unpack_dev(s, recv.data_ptr() + 4 * off)
+            off += recv_n[s]
+        self.ix.sync()
+        return send_n
+
+    # ------------------------------------------------------------------ FC
+    def forkless_cause_dev(self, a, b, out=None):
+        """ForklessCause for device int32 index tensors ``a``, ``b`` -> uint8 tensor."""
+        n = a.numel()
+        part = torch.empty(n, dtype=torch.int32, device=self.device)
+        self.ix.forkless_cause_partial_dev(n, a.data_ptr(), b.data_ptr(), part.data_ptr())
+        self.ix.sync()
+        # partials are uint32 (stake sum < 2^31 plus at most one bit-31 mark, from
+        # the rank owning branch(b)); the true total fits 32 bits, so the int32
+        # wrap-around sum of the all-reduce is exact
+        if self.world > 1:
+            dist.all_reduce(part, op=dist.ReduceOp.SUM, group=self.group)
+        if self.device.type == "cuda":
+            torch.cuda.current_stream(self.device).synchronize()
+        s32 = part
+        if out is None:
+            out = torch.empty(n, dtype=torch.uint8, device=self.device)
+        self.ix.fc_combine_dev(n, s32.data_ptr(), out.data_ptr())
+        self.ix.sync()
+        return out
