@@ -15,12 +15,15 @@ before timing.
 
 value = events indexed/sec (whole job, all ranks); fc_queries_per_sec is
 reported beside it.  Multi-GPU: one process per GPU.
-  --mode replica (default): each rank indexes its own copy of the workload
-      (independent epochs / nodes; no data-path collective; weak scaling).
-  --mode shard: the ranks split ONE epoch by creator columns
+  --mode shard (default for N > 1, BASELINE configs[2] "column-sharded across
+      8xMI355X"): the ranks split ONE epoch by creator columns
       (lachesis_hip/shard.py): each indexes its columns,
       the index step ends with the RCCL all-to-all of LowestAfter blocks, and
-      FC sums per-rank partial stakes with an all-reduce (strong scaling).
+      FC sums per-rank partial stakes with an RCCL all-reduce (strong scaling:
+      value = the epoch's events / time).
+  --mode replica: each rank indexes its own copy of the workload (independent
+      epochs; no data-path collective; weak scaling).
+LX_DIST_BACKEND=gloo (rehearsal only) lets several ranks share one GPU.
 """
 
 import argparse
@@ -85,7 +88,7 @@ def main():
     ap.add_argument("--batch", type=int, default=0, help="events per lx_add_batch_dev call (0 = whole epoch)")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--mode", default="replica", choices=["replica", "shard"])
+    ap.add_argument("--mode", default="shard", choices=["replica", "shard"])
     args = ap.parse_args()
 
     import numpy as np
@@ -95,10 +98,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = os.environ.get("LX_DIST_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(1, torch.cuda.device_count())   # rehearsal: ranks may share a GPU
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -166,7 +175,7 @@ def main():
             evs[1].record(lib_stream)
         if shard:
             ix.sync()
-            dist.all_reduce(d_part, op=dist.ReduceOp.SUM)   # int32 wrap-around = exact uint32 sum
+            sx.all_reduce_sum(d_part)   # int32 wrap-around = exact uint32 sum
             torch.cuda.current_stream(dev).synchronize()
             ix.fc_combine_dev(args.fc_queries, d_part.data_ptr(), d_out.data_ptr())
 
@@ -178,7 +187,7 @@ def main():
     def max_over_ranks(x):
         if world == 1:
             return x
-        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        t = torch.tensor([x], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 

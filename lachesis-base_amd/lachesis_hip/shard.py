@@ -36,6 +36,25 @@ class ShardedIndex:
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
         self.device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+        # gloo moves host tensors only: stage device buffers through the host
+        # (a rehearsal mode for several ranks sharing one GPU; RCCL is the product)
+        self.stage = dist.get_backend(group) == "gloo" and self.device.type == "cuda"
+
+    def all_to_all(self, recv, send, recv_n, send_n):
+        if self.stage:
+            r = recv.cpu()
+            dist.all_to_all_single(r, send.cpu(), output_split_sizes=recv_n, input_split_sizes=send_n, group=self.group)
+            recv.copy_(r)
+        else:
+            dist.all_to_all_single(recv, send, output_split_sizes=recv_n, input_split_sizes=send_n, group=self.group)
+
+    def all_reduce_sum(self, t):
+        if self.stage:
+            h = t.cpu()
+            dist.all_reduce(h, op=dist.ReduceOp.SUM, group=self.group)
+            t.copy_(h)
+        else:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
 
     # ------------------------------------------------------------------ LA
     def exchange(self):
@@ -52,9 +71,7 @@ class ShardedIndex:
             off += send_n[t]
         self.ix.sync()   # packs run on the library stream; the collective on torch's
         if G > 1:
-            dist.all_to_all_single(recv[:sum(recv_n)] if sum(recv_n) else recv[:0],
-                                   send[:sum(send_n)] if sum(send_n) else send[:0],
-                                   output_split_sizes=recv_n, input_split_sizes=send_n, group=self.group)
+            self.all_to_all(recv[:sum(recv_n)], send[:sum(send_n)], recv_n, send_n)
         if self.device.type == "cuda":
             torch.cuda.current_stream(self.device).synchronize()
         off = 0
@@ -76,7 +93,7 @@ class ShardedIndex:
         # the rank owning branch(b)); the true total fits 32 bits, so the int32
         # wrap-around sum of the all-reduce is exact
         if self.world > 1:
-            dist.all_reduce(part, op=dist.ReduceOp.SUM, group=self.group)
+            self.all_reduce_sum(part)
         if self.device.type == "cuda":
             torch.cuda.current_stream(self.device).synchronize()
         s32 = part
