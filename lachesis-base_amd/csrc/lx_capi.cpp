@@ -98,6 +98,7 @@ struct lx_index {
     uint32_t diag_nofill = 0;   // LX_DIAG_NOFILL=1: timing-only build of the walker (LA left empty)
     uint32_t cpw_hint = 0, ncw_hint = 0;   // LX_CPW / LX_NCW tuning overrides
     uint32_t rr_hint = 0, diag = 0;        // LX_RR record ring depth; LX_DIAG timing-only modes
+    bool prof = false;                     // LX_PROF=1: per-wave walker counters to stderr
     uint64_t last_npar = 0;                // parents in the current batch
 
     int fail(int code, const char *fmt, ...) {
@@ -416,9 +417,37 @@ int add_batch_dev(lx_index *h, uint32_t n, const uint32_t *creator, const uint32
         uint32_t pbar = std::max<uint32_t>(1, (uint32_t)((h->last_npar + n - 1) / n));
         ia.width_hint = std::max<uint32_t>(1, (uint32_t)(h->V * 10 / (16 * pbar)));
     }
+    const size_t prof_n = (size_t)65536 * 8 * kProfSlots;
+    if (h->prof) {
+        HIPCHK(h, hipMalloc(&ia.prof, prof_n * 8));
+        HIPCHK(h, hipMemsetAsync(ia.prof, 0, prof_n * 8, s));
+    }
     HIPCHK(h, hipEventRecord(h->ev[1], s));
     HIPCHK(h, lx::launch_index(ia, s));
     HIPCHK(h, hipEventRecord(h->ev[2], s));
+    if (h->prof) {
+        std::vector<unsigned long long> pv(prof_n);
+        HIPCHK(h, hipMemcpyAsync(pv.data(), ia.prof, prof_n * 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(h, hipStreamSynchronize(s));
+        HIPCHK(h, hipFree(ia.prof));
+        // summary over workgroups: per compute wave (lane sums), wave passes, wall time
+        double sum[8 * kProfSlots] = {0};
+        uint32_t nb = 0;
+        for (uint32_t b = 0; b < 65536; b++) {
+            const unsigned long long *pb = pv.data() + (size_t)b * 8 * kProfSlots;
+            if (!pb[9]) continue;
+            nb++;
+            for (int i = 0; i < 8 * kProfSlots; i++) sum[i] += (double)pb[i];
+        }
+        fprintf(stderr, "[lx_prof] n=%u blocks=%u (means per block)\n", n, nb);
+        for (int w = 0; w < 8; w++) {
+            const double *q = sum + w * kProfSlots;
+            if (!q[9]) continue;
+            fprintf(stderr, "[lx_prof] wave %d: wall_us=%.0f wave_passes=%.0f lane: pass=%.0f spin=%.0f chunk=%.0f done=%.0f slow=%.0f fill=%.0f wm=%.0f norec=%.0f  ns/pass=%.1f\n",
+                    w, q[9] / nb / 100.0, q[8] / nb, q[0] / nb, q[1] / nb, q[2] / nb, q[3] / nb, q[4] / nb, q[5] / nb, q[6] / nb,
+                    q[7] / nb, q[9] * 10.0 / (q[8] > 0 ? q[8] : 1));
+        }
+    }
     if (h->B > h->V && h->n_cheat) {
         MarkArgs m{};
         m.hb = h->hb;
@@ -571,6 +600,7 @@ int lx_create(const lx_config *cfg, lx_index **out) {
     if (const char *d = getenv("LX_NCW")) h->ncw_hint = (uint32_t)atoi(d);
     if (const char *d = getenv("LX_RR")) h->rr_hint = (uint32_t)atoi(d);
     if (const char *d = getenv("LX_DIAG")) h->diag = (uint32_t)atoi(d);
+    if (const char *d = getenv("LX_PROF")) h->prof = (d[0] == '1');
     for (auto &e : h->ev)
         if (hipEventCreate(&e) != hipSuccess) {
             delete h;

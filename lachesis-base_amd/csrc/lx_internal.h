@@ -51,7 +51,9 @@ struct IndexArgs {
     uint32_t width_hint;         // expected antichain width of the batch
     uint32_t rr_hint;            // record ring depth (LX_RR; 0 = auto)
     uint32_t diag;               // timing-only diagnostics (LX_DIAG): 2 no deps, 3 no global stores
+    unsigned long long *prof;    // optional per-wave counters (LX_PROF=1), kProfSlots per wave
 };
+constexpr int kProfSlots = 16;   // see k_index: passes, spin misses, chunk folds, completes, ...
 
 struct BatchArgs {
     uint32_t n;

@@ -434,6 +434,9 @@ __global__ __launch_bounds__(64 * (NCW + 2)) void k_index(IndexArgs a) {
 
     // ---------------------------------------------------------------- compute
     const uint32_t mask = a.mask ? LX_SEQ_MASK : 0xFFFFFFFFu;
+    // profiling counters (LX_PROF): per lane, summed per wave at the end
+    uint32_t c_pass = 0, c_spin = 0, c_chunk = 0, c_done = 0, c_slow = 0, c_fill = 0, c_wm = 0, c_norec = 0;
+    const unsigned long long t_start = wall_clock64();
     const uint64_t *ring64 = ring;
 
     uint32_t lp = threadIdx.x;
@@ -446,9 +449,10 @@ __global__ __launch_bounds__(64 * (NCW + 2)) void k_index(IndexArgs a) {
     bool filled = false;
 
     while (lp < n) {
+        c_pass++;
         if (!have) {
             const uint32_t slot = lp % RR;
-            if (__hip_atomic_load(&rtag[slot], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != lp + 1) continue;
+            if (__hip_atomic_load(&rtag[slot], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != lp + 1) { c_norec++; continue; }
             const uint4 *rq = rrec + slot * RQ;
             const uint4 q0 = rq[0];
             br = q0.x; seq = q0.y; np = q0.z; prev = q0.w;
@@ -473,12 +477,15 @@ __global__ __launch_bounds__(64 * (NCW + 2)) void k_index(IndexArgs a) {
             have = true;
         }
         // cheap spin: one granule tag (an overwritten slot reads as >= tag)
-        if ((uint32_t)__hip_atomic_load(ring64 + wait_off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < wait_tag)
+        if ((uint32_t)__hip_atomic_load(ring64 + wait_off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < wait_tag) {
+            c_spin++;
             continue;
+        }
         // fold every pending parent, chunks of 4: issue granule reads, then evaluate
 #pragma unroll
         for (int c = 0; c < LX_MAXP / 4; c++) {
             if (!__any(todo >> (4 * c))) break;   // wave-uniform
+            c_chunk += ((todo >> (4 * c)) & 15u) ? 1u : 0u;
             uint64_t g[4][CPW];
 #pragma unroll
             for (int jj = 0; jj < 4; jj++) {
@@ -510,6 +517,7 @@ __global__ __launch_bounds__(64 * (NCW + 2)) void k_index(IndexArgs a) {
             }
         }
         if (slow) {
+            c_slow++;
             // slow path: parents older than the ring (or from an earlier batch);
             // their HB rows are in L2 once the writer's watermark passed them
             const uint32_t stored = __hip_atomic_load(&wm[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -591,6 +599,7 @@ __global__ __launch_bounds__(64 * (NCW + 2)) void k_index(IndexArgs a) {
                         const uint32_t h0 = (prev != LX_NONE) ? v0[k] : 0u;
                         const uint32_t lo = max(h0 + 1u, first[k]);
                         for (uint32_t s = lo; s <= r[k]; s++) {
+                            c_fill++;
                             const uint64_t cc = __hip_atomic_load(reinterpret_cast<const uint64_t *>(brc + k * kBRC + s % kBRC),
                                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                             uint32_t row = (uint32_t)(cc >> 32);
@@ -603,15 +612,26 @@ __global__ __launch_bounds__(64 * (NCW + 2)) void k_index(IndexArgs a) {
             }
             // the slot's previous occupant (lp - RING) must have been copied by the writer
             if (lp >= (uint32_t)RING &&
-                __hip_atomic_load(&wm[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < lp - RING + 1)
+                __hip_atomic_load(&wm[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < lp - RING + 1) {
+                c_wm++;
                 continue;
+            }
             uint64_t *dst = ring + (lp % RING) * CPW;
 #pragma unroll
             for (int k = 0; k < CPW; k++)
                 __hip_atomic_store(dst + k, ((uint64_t)r[k] << 32) | (lp + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             lp += E;
             have = false;
+            c_done++;
         }
+    }
+    if (a.prof) {
+        unsigned long long *pw = a.prof + ((uint64_t)blockIdx.x * 8 + wave) * kProfSlots;
+        const uint32_t cs[8] = {c_pass, c_spin, c_chunk, c_done, c_slow, c_fill, c_wm, c_norec};
+#pragma unroll
+        for (int i = 0; i < 8; i++) atomicAdd(pw + i, (unsigned long long)cs[i]);
+        atomicMax(pw + 8, (unsigned long long)c_pass);               // wave passes = max over lanes
+        if (lane == 0) atomicMax(pw + 9, wall_clock64() - t_start);  // wall ticks (100 MHz)
     }
 }
 
