@@ -191,17 +191,18 @@ __global__ void k_finalize(BatchArgs a) {
     uint32_t p0 = a.poff[e], p1 = a.poff[e + 1];
     uint32_t np = p1 - p0;
     uint32_t prev = (s > 1 && !a.isfork[e]) ? a.par[p0] : LX_NONE;
-    // inline parents sorted newest first: the walker spins on the newest one
+    // inline parents sorted oldest first: the walker folds them in chunks of 4,
+    // so the newest (last to complete) chunk is the only one left at the end
     uint32_t w[LX_MAXP];
 #pragma unroll
-    for (int k = 0; k < LX_MAXP; k++) w[k] = (k < (int)np) ? a.par[p0 + k] : 0u;
+    for (int k = 0; k < LX_MAXP; k++) w[k] = (k < (int)np) ? a.par[p0 + k] : 0xFFFFFFFFu;
 #pragma unroll
     for (int i = 1; i < LX_MAXP; i++) {
 #pragma unroll
         for (int j = i; j > 0; j--) {
             const uint32_t x = w[j - 1], y = w[j];
-            w[j - 1] = max(x, y);
-            w[j] = min(x, y);
+            w[j - 1] = min(x, y);
+            w[j] = max(x, y);
         }
     }
     EventRec r;
@@ -231,69 +232,157 @@ hipError_t launch_batch_finish(const BatchArgs &a, hipStream_t s) {
 // of column c touch only column c of HB and rows of branch c in LA), so the
 // workgroups never communicate; one launch covers the whole batch.
 //
-// Roles inside the workgroup (NCW compute waves + 1 loader wave):
-//  * the loader streams 80-B event records into an LDS record ring by LDS-DMA
+// The batch's DAG depth (not its size) bounds the walk: every level costs one
+// pass of the compute loop, so the compute waves do only what the critical
+// path needs -- fold parents, publish -- and everything else runs beside them.
+// Roles (NCW compute waves + 1 loader + ND drain waves):
+//  * loader: streams the 96-B event records into an LDS record ring by LDS-DMA
 //    (global_load_lds_dwordx4, RR/64 rounds in flight) and publishes each slot
 //    with a tag after its own vmcnt wait;
-//  * compute lane g handles events g, g+E, g+2E, ... (E = 64*NCW), all CPW
-//    columns of each, so readiness checks are paid once per parent.  The hot
-//    path touches only LDS and issues fire-and-forget stores: no vmcnt wait
-//    (which on gfx950 also waits for stores) sits on the DAG's critical path.
-// Parents are read from an LDS ring of per-column {tag, seq} granules (tag =
-// batch position + 1, each 16-B half written by one ds_write_b128, so atomic
-// per lane).  A slot overwritten by a later event means the parent is older
-// than the ring; its HB row is then read from L2 (slow path).  Before a lane
-// overwrites a slot it bounds its own stores in flight (vmcnt), so that slow
-// path sees the overwritten event's HB store.  Lanes never block inside an
-// iteration (readiness is re-checked every pass): intra-wave dependencies
-// cannot deadlock.  The event holding a column's max seq (needed for the
-// LowestAfter fill) comes from an LDS table of recent events of the owned
-// branches, falling back to the branch-row table in L2.
-constexpr int kBRC = 64;     // recent (seq -> event) entries per owned branch
+//  * compute lane g handles events g, g+E, ... (E = 64*NCW).  Parents arrive
+//    oldest first; each pass folds ONE chunk of 4 (so a waiting lane folds its
+//    old parents early and the newest chunk is all that is left when its last
+//    parent completes), then publishes {tag | prev, branch, seq | CPW seqs}
+//    into a 32-B slot of the LDS event ring.  No global access on the hot path;
+//  * drain waves (rounds of 64 events, round r on wave r % ND): store the HB
+//    row and do the LowestAfter range fill, reading RAW(prev) from the ring.
+// Publishing: a writer stores the slot body, then the tag (one asm block, so
+// LDS executes them in that order); a reader issues the tag read, then the
+// body read (one asm block), so a matching tag proves the body is complete.
+// A tag above the expected one means the slot was reused: that parent's HB row
+// is read from L2 once the drain reports it stored (rare: parents older than
+// the ring, or from an earlier batch).  Lanes never block inside a pass, so
+// dependencies between lanes of one wave cannot deadlock; drains only wait for
+// older events, and service "store-complete" requests while they wait.
+constexpr int kRing = 2048;          // event slots, 32 B each (64 KB)
+constexpr int kND = 2;               // drain waves
 
-__device__ __forceinline__ void wait_vmcnt_le(uint32_t n) {
-    switch (n) {
-        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-        case 1: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
-        case 2: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
-        case 3: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
-        case 4: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
-        case 5: asm volatile("s_waitcnt vmcnt(25)" ::: "memory"); break;
-        case 6: asm volatile("s_waitcnt vmcnt(30)" ::: "memory"); break;
-        default: asm volatile("s_waitcnt vmcnt(35)" ::: "memory"); break;
-    }
+template <int CPW>
+struct WalkCfg {
+    static constexpr int KB = 1024 / CPW;   // recent (seq -> event) entries per owned branch
+};
+
+struct WalkShared {
+    uint32_t copied[kND];    // rounds drained (ring data consumed) per drain wave
+    uint32_t stored[kND];    // rounds whose global stores are complete per drain wave
+    uint32_t req;            // a compute lane waits for `stored`: drains flush
+};
+
+__device__ __forceinline__ bool round_done(const uint32_t *cnt, uint32_t ev) {
+    const uint32_t r = ev / 64;
+    return __hip_atomic_load(cnt + (r % kND), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) > r / kND;
 }
 
-template <int CPW, int NCW, int RING, int RR, bool FILL>
-__global__ __launch_bounds__(64 * (NCW + 2)) void k_index(IndexArgs a) {
-    constexpr int NT = 64 * (NCW + 2);
+// read tag, 16 B of seqs, tag again, for 4 ring slots, in that order, and wait.
+// The body is valid iff both tags equal the expected one (ring_publish marks a
+// slot busy before rewriting it, and LDS executes one wave's operations in
+// order, so a body read that overlapped a rewrite sees a changed second tag).
+__device__ __forceinline__ void ring_read4(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3, uint32_t t[4], uint32_t u[4],
+                                           uint4 v[4]) {
+    typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+    u4v x0, x1, x2, x3;
+    uint32_t t0, t1, t2, t3, u0, u1, u2, u3;
+    asm volatile(
+        "ds_read_b32 %0, %12\n\t"
+        "ds_read_b128 %8, %12 offset:16\n\t"
+        "ds_read_b32 %4, %12\n\t"
+        "ds_read_b32 %1, %13\n\t"
+        "ds_read_b128 %9, %13 offset:16\n\t"
+        "ds_read_b32 %5, %13\n\t"
+        "ds_read_b32 %2, %14\n\t"
+        "ds_read_b128 %10, %14 offset:16\n\t"
+        "ds_read_b32 %6, %14\n\t"
+        "ds_read_b32 %3, %15\n\t"
+        "ds_read_b128 %11, %15 offset:16\n\t"
+        "ds_read_b32 %7, %15\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(t0), "=&v"(t1), "=&v"(t2), "=&v"(t3), "=&v"(u0), "=&v"(u1), "=&v"(u2), "=&v"(u3),
+          "=&v"(x0), "=&v"(x1), "=&v"(x2), "=&v"(x3)
+        : "v"(a0), "v"(a1), "v"(a2), "v"(a3)
+        : "memory");
+    t[0] = t0; t[1] = t1; t[2] = t2; t[3] = t3;
+    u[0] = u0; u[1] = u1; u[2] = u2; u[3] = u3;
+    v[0] = make_uint4(x0.x, x0.y, x0.z, x0.w);
+    v[1] = make_uint4(x1.x, x1.y, x1.z, x1.w);
+    v[2] = make_uint4(x2.x, x2.y, x2.z, x2.w);
+    v[3] = make_uint4(x3.x, x3.y, x3.z, x3.w);
+}
+
+// one slot: tag, body (header + seqs), tag
+__device__ __forceinline__ void ring_read1(uint32_t a0, uint32_t &t, uint32_t &u, uint4 &h, uint4 &v) {
+    typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+    u4v x, y;
+    uint32_t t0, u0;
+    asm volatile(
+        "ds_read_b32 %0, %4\n\t"
+        "ds_read_b128 %2, %4\n\t"
+        "ds_read_b128 %3, %4 offset:16\n\t"
+        "ds_read_b32 %1, %4\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(t0), "=&v"(u0), "=&v"(x), "=&v"(y)
+        : "v"(a0)
+        : "memory");
+    t = t0; u = u0;
+    h = make_uint4(x.x, x.y, x.z, x.w);
+    v = make_uint4(y.x, y.y, y.z, y.w);
+}
+
+constexpr uint32_t kBusy = 0xFFFFFFFFu;   // slot being rewritten by a newer event
+
+// publish a slot: busy tag, body (prev, branch, seq; seqs), then the tag
+__device__ __forceinline__ void ring_publish(uint32_t addr, uint32_t tag, uint32_t prev, uint32_t br, uint32_t seq, uint4 v) {
+    typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+    typedef uint32_t u2v __attribute__((ext_vector_type(2)));
+    u4v x; x.x = v.x; x.y = v.y; x.z = v.z; x.w = v.w;
+    u2v m; m.x = br; m.y = seq;
+    const uint32_t busy = kBusy;
+    asm volatile(
+        "ds_write_b32 %0, %5\n\t"
+        "ds_write_b32 %0, %2 offset:4\n\t"
+        "ds_write_b64 %0, %3 offset:8\n\t"
+        "ds_write_b128 %0, %4 offset:16\n\t"
+        "ds_write_b32 %0, %1"
+        :
+        : "v"(addr), "v"(tag), "v"(prev), "v"(m), "v"(x), "v"(busy)
+        : "memory");
+}
+
+__device__ __forceinline__ uint32_t lds_addr(const void *p) {
+    return (uint32_t)(uintptr_t)p;
+}
+
+template <int CPW, int NCW, int RR, bool FILL>
+__global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
+    static_assert(CPW == 1 || CPW == 2 || CPW == 4, "16-B slot body");
+    constexpr int NT = 64 * (NCW + 1 + kND);
     constexpr int E = 64 * NCW;
     constexpr int RQ = LX_REC_Q;
-    constexpr int WD = 8;                        // writer rounds (of 64 events) in flight
-    static_assert(RING % E == 0 && RING / E >= 4, "ring slot reuse must stay within one lane");
+    constexpr int KB = WalkCfg<CPW>::KB;
+    static_assert(kRing % E == 0 && kRing / E >= 4, "ring slot reuse must stay within one lane");
     static_assert(RR % 64 == 0 && RR / 64 <= 8 && RR >= E, "record ring");
-    __shared__ uint64_t ring[RING * CPW];        // per event: CPW x {tag, seq} granules
+    __shared__ uint4 ring[kRing * 2];            // slot s: [2s] = {tag, prev, br, seq}, [2s+1] = CPW seqs
     __shared__ uint4 rrec[RR * RQ];              // event records
     __shared__ uint32_t rtag[RR];
-    __shared__ uint2 brc[CPW * kBRC];            // {seq, event} of recent events of owned branches
-    __shared__ uint32_t wm[2];                   // writer watermarks: [0] ring entries copied, [1] HB stores done
+    __shared__ uint2 brc[CPW * KB];              // {seq, event} of recent events of owned branches
+    __shared__ WalkShared sh;
 
     const uint32_t w = blockIdx.x;
     const uint32_t slice = (w % 8) * a.slices_per_xcd + (w / 8);   // XCD-aware: neighbouring slices share an L2
     if (slice >= a.n_slices) return;
 
-    for (int i = threadIdx.x; i < RING * CPW; i += NT) ring[i] = 0;
+    for (int i = threadIdx.x; i < kRing * 2; i += NT) ring[i] = make_uint4(0, 0, 0, 0);
     for (int i = threadIdx.x; i < RR; i += NT) rtag[i] = 0;
-    for (int i = threadIdx.x; i < CPW * kBRC; i += NT) brc[i] = make_uint2(0, LX_NONE);
-    if (threadIdx.x < 2) wm[threadIdx.x] = 0;
+    for (int i = threadIdx.x; i < CPW * KB; i += NT) brc[i] = make_uint2(0, LX_NONE);
+    if (threadIdx.x < kND) { sh.copied[threadIdx.x] = 0; sh.stored[threadIdx.x] = 0; }
+    if (threadIdx.x == 0) sh.req = 0;
     __syncthreads();
 
     const uint32_t n = a.n;
     const uint32_t bs = a.batch_start;
     const int wave = threadIdx.x / 64;
     const int lane = threadIdx.x % 64;
-    const uint32_t diag = a.diag;   // 0 normal; timing-only diagnostics: 2 no deps, 3 no global stores
     const uint64_t stride = a.stride;
+    const uint32_t mask = a.mask ? LX_SEQ_MASK : 0xFFFFFFFFu;
 
     uint32_t col[CPW], first[CPW];
     bool valid[CPW];
@@ -319,13 +408,13 @@ __global__ __launch_bounds__(64 * (NCW + 2)) void k_index(IndexArgs a) {
             bool progressed = false;
             if (issued < nrounds && issued - done < D) {
                 // slots of this round are free once their previous occupants
-                // (events ev - RR) are done (their ring entry is written)
+                // (events ev - RR) have been published
                 const uint32_t ev = issued * 64 + lane;
                 bool free = true;
                 if (ev < n && ev >= (uint32_t)RR) {
                     const uint32_t q = ev - RR;
-                    const uint64_t g0 = __hip_atomic_load(ring + (q % RING) * CPW, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    if ((uint32_t)g0 < q + 1) free = false;
+                    const uint32_t t = __hip_atomic_load(&ring[(q % kRing) * 2].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    if (t < q + 1) free = false;
                 }
                 if (__all(free)) {
                     const uint32_t s0 = (issued * 64) % RR;
@@ -363,90 +452,126 @@ __global__ __launch_bounds__(64 * (NCW + 2)) void k_index(IndexArgs a) {
         return;
     }
 
-    if (wave == NCW + 1) {
-        // ------------------------------------------------------------ writer
-        // copies completed ring entries to the HB plane in rounds of 64 events
-        // and publishes wm[0] (entries copied: their slots may be reused) and
-        // wm[1] (HB stores complete: an L2 read of those rows is safe)
-        const uint32_t nrounds = (n + 63) / 64;
-        const uint32_t spr = contig ? (CPW + 3) / 4 : CPW;   // store instructions per round
-        uint32_t issued = 0, done = 0;
-        while (done < nrounds) {
-            bool progressed = false;
-            if (issued < nrounds && issued - done < WD) {
-                const uint32_t ev = issued * 64 + lane;
-                uint64_t g[CPW];
+    if (wave > NCW) {
+        // ------------------------------------------------------------ drain
+        const uint32_t d = wave - NCW - 1;
+        uint32_t nd = 0;                 // rounds of this wave completed
+        for (uint32_t R = d; R * 64 < n; R += kND, nd++) {
+            const uint32_t ev = R * 64 + lane;
+            const uint32_t sl = ev % kRing;
+            // wait for the round (servicing store-complete requests meanwhile)
+            while (true) {
                 bool ready = true;
-                if (ev < n) {
-#pragma unroll
-                    for (int k = 0; k < CPW; k++) {
-                        g[k] = __hip_atomic_load(ring + (ev % RING) * CPW + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        ready &= ((uint32_t)g[k] == ev + 1);
-                    }
+                if (ev < n) ready = __hip_atomic_load(&ring[sl * 2].x, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == ev + 1;
+                if (__all(ready)) break;
+                if (__hip_atomic_load(&sh.req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    if (lane == 0) __hip_atomic_store(&sh.stored[d], nd, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
-                if (__all(ready)) {
-                    if (ev < n && diag != 3) {
-                        uint32_t *hrow = a.hb + (uint64_t)(bs + ev) * stride;
-                        if (contig) {
-                            if (CPW == 1) {
-                                hrow[col[0]] = (uint32_t)(g[0] >> 32);
-                            } else if (CPW == 2) {
-                                *reinterpret_cast<uint2 *>(hrow + col[0]) = make_uint2((uint32_t)(g[0] >> 32), (uint32_t)(g[1 % CPW] >> 32));
-                            } else {
-#pragma unroll
-                                for (int k = 0; k < CPW; k += 4)
-                                    *reinterpret_cast<uint4 *>(hrow + col[0] + k) =
-                                        make_uint4((uint32_t)(g[k] >> 32), (uint32_t)(g[(k + 1) % CPW] >> 32),
-                                                   (uint32_t)(g[(k + 2) % CPW] >> 32), (uint32_t)(g[(k + 3) % CPW] >> 32));
-                            }
-                        } else {
-#pragma unroll
-                            for (int k = 0; k < CPW; k++)
-                                if (valid[k]) hrow[col[k]] = (uint32_t)(g[k] >> 32);
-                        }
-                    }
-                    issued++;
-                    if (lane == 0) __hip_atomic_store(&wm[0], min(issued * 64, n), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    progressed = true;
-                }
-            }
-            if (!progressed && issued > done) {
-                // the oldest round's stores are complete once at most spr per younger round remain
-                const uint32_t younger = (issued - done - 1) * spr;
-                if (younger >= 56) asm volatile("s_waitcnt vmcnt(56)" ::: "memory");
-                else if (younger >= 48) asm volatile("s_waitcnt vmcnt(48)" ::: "memory");
-                else if (younger >= 40) asm volatile("s_waitcnt vmcnt(40)" ::: "memory");
-                else if (younger >= 32) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
-                else if (younger >= 24) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
-                else if (younger >= 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-                else if (younger >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-                else if (younger >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-                else if (younger >= 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-                else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                done++;
-                if (lane == 0) __hip_atomic_store(&wm[1], min(done * 64, n), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            } else if (!progressed) {
                 __builtin_amdgcn_s_sleep(1);
             }
+            uint32_t prev = LX_NONE, br = 0, seq = 0;
+            uint32_t r[CPW], h0[CPW];
+            uint4 vv = make_uint4(0, 0, 0, 0);
+            if (ev < n) {
+                const uint4 hd = ring[sl * 2];
+                vv = ring[sl * 2 + 1];
+                prev = hd.y; br = hd.z; seq = hd.w;
+                const uint32_t vs[4] = {vv.x, vv.y, vv.z, vv.w};
+#pragma unroll
+                for (int k = 0; k < CPW; k++) { r[k] = vs[k] & mask; h0[k] = 0; }
+                if (prev != LX_NONE) {
+                    const uint32_t pl = prev - bs;
+                    bool got = false;
+                    if (pl < n) {
+                        uint32_t pt, pu;
+                        uint4 ph, pv;
+                        ring_read1(lds_addr(ring) + (pl % kRing) * 32u, pt, pu, ph, pv);
+                        if (pt == pl + 1 && pu == pl + 1) {
+                            const uint32_t ps4[4] = {pv.x, pv.y, pv.z, pv.w};
+#pragma unroll
+                            for (int k = 0; k < CPW; k++) h0[k] = ps4[k] & mask;
+                            got = true;
+                        } else {
+                            // reused slot: prev's row is (being) stored by a drain
+                            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                            const uint32_t dd = (pl / 64) % kND;
+                            if (dd != d) {
+                                // the other drain may in turn wait for this one: keep
+                                // publishing our own completed rounds while waiting
+                                __hip_atomic_store(&sh.stored[d], nd, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);   // divergent: every active lane
+                                while (!round_done(sh.stored, pl)) {
+                                    __hip_atomic_store(&sh.req, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                                    __builtin_amdgcn_s_sleep(1);
+                                }
+                            }
+                        }
+                    }
+                    if (!got) {
+                        const uint32_t *row = a.hb + (uint64_t)prev * stride;
+#pragma unroll
+                        for (int k = 0; k < CPW; k++) h0[k] = valid[k] ? (ld_l2_now(row + col[k]) & mask) : 0u;
+                    }
+                }
+            }
+            // ring data of this round consumed: its slots may be reused
+            if (lane == 0) __hip_atomic_store(&sh.copied[d], nd + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (ev < n) {
+                // HB row (raw values incl. fork bits as published)
+                uint32_t *hrow = a.hb + (uint64_t)(bs + ev) * stride;
+                if (contig) {
+                    if (CPW == 1) hrow[col[0]] = vv.x;
+                    else if (CPW == 2) *reinterpret_cast<uint2 *>(hrow + col[0]) = make_uint2(vv.x, vv.y);
+                    else *reinterpret_cast<uint4 *>(hrow + col[0]) = vv;
+                } else {
+                    const uint32_t vs[4] = {vv.x, vv.y, vv.z, vv.w};
+#pragma unroll
+                    for (int k = 0; k < CPW; k++)
+                        if (valid[k]) hrow[col[k]] = vs[k];
+                }
+                if (FILL) {
+                    // LowestAfter range fill: events (col, s), s in (h0, r], are first
+                    // observed from branch `br` by this event (DESIGN.md section 3).
+#pragma unroll
+                    for (int k = 0; k < CPW; k++) {
+                        if (!valid[k]) continue;
+                        const uint32_t lo = max(h0[k] + 1u, first[k]);
+                        for (uint32_t s = lo; s <= r[k]; s++) {
+                            const uint64_t cc = __hip_atomic_load(reinterpret_cast<const uint64_t *>(brc + k * KB + s % KB),
+                                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            uint32_t row = (uint32_t)(cc >> 32);
+                            if ((uint32_t)cc != s) row = ld_l2_now(a.brow + (uint64_t)col[k] * a.s_cap + (s - first[k]));
+                            a.la[(uint64_t)row * stride + br] = seq;
+                        }
+                    }
+                }
+            }
+            if (__hip_atomic_load(&sh.req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (lane == 0) {
+                    __hip_atomic_store(&sh.stored[d], nd + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    __hip_atomic_store(&sh.req, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+            }
         }
+        // final: every store of this wave complete (another drain or a compute
+        // lane may still wait for it)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) __hip_atomic_store(&sh.stored[d], 0xFFFFFFFFu, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         return;
     }
 
     // ---------------------------------------------------------------- compute
-    const uint32_t mask = a.mask ? LX_SEQ_MASK : 0xFFFFFFFFu;
-    // profiling counters (LX_PROF): per lane, summed per wave at the end
-    uint32_t c_pass = 0, c_spin = 0, c_chunk = 0, c_done = 0, c_slow = 0, c_fill = 0, c_wm = 0, c_norec = 0;
+    uint32_t c_pass = 0, c_chunk = 0, c_done = 0, c_slow = 0, c_wm = 0, c_norec = 0;
     const unsigned long long t_start = wall_clock64();
-    const uint64_t *ring64 = ring;
 
     uint32_t lp = threadIdx.x;
     bool have = false;
     uint32_t br = 0, seq = 0, np = 0, prev = 0, ovf = 0, xi = 0;
     uint32_t par[LX_MAXP];
-    uint32_t todo = 0, slow = 0;
-    uint32_t wait_off = 0, wait_tag = 0;          // the one granule this lane spins on
-    uint32_t r[CPW], v0[CPW];
-    bool filled = false;
+    uint32_t todo = 0;
+    uint32_t r[CPW];
+    const uint32_t ring_base = lds_addr(ring);
 
     while (lp < n) {
         c_pass++;
@@ -463,163 +588,104 @@ __global__ __launch_bounds__(64 * (NCW + 2)) void k_index(IndexArgs a) {
                 par[4 * j] = q.x - bs; par[4 * j + 1] = q.y - bs; par[4 * j + 2] = q.z - bs; par[4 * j + 3] = q.w - bs;
             }
             todo = (np >= LX_MAXP) ? 0xFFFFu : ((1u << np) - 1u);
-            if (diag == 2) todo = 0;
-            slow = 0;
             xi = LX_MAXP;
 #pragma unroll
-            for (int k = 0; k < CPW; k++) { r[k] = (col[k] == br) ? seq : 0u; v0[k] = 0; }
-            // spin on the newest in-batch parent first (parents sorted newest first)
-            const uint32_t l0 = par[0];
-            const bool sp = (np > 0 && l0 < n && diag != 2);
-            wait_off = sp ? (l0 % RING) * CPW : 0u;
-            wait_tag = sp ? l0 + 1 : 0u;
-            filled = false;
+            for (int k = 0; k < CPW; k++) r[k] = (col[k] == br) ? seq : 0u;
             have = true;
         }
-        // cheap spin: one granule tag (an overwritten slot reads as >= tag)
-        if ((uint32_t)__hip_atomic_load(ring64 + wait_off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < wait_tag) {
-            c_spin++;
-            continue;
+        if (todo) {
+            // fold the oldest pending chunk (par[0..3]; parents sorted oldest first)
+            c_chunk++;
+            uint32_t ad[4], t[4], u[4];
+            uint4 v[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) ad[j] = ring_base + (par[j] % kRing) * 32u;
+            ring_read4(ad[0], ad[1], ad[2], ad[3], t, u, v);
+            // branch-free common case: fold the parents whose slot is valid
+            uint32_t okm = 0, oldm = 0;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const uint32_t x = par[j] + 1u;
+                const uint32_t pend = (todo >> j) & 1u;
+                const uint32_t inb = (uint32_t)(par[j] < n);
+                const uint32_t ok = pend & inb & (uint32_t)(t[j] == x) & (uint32_t)(u[j] == x);
+                const uint32_t old = pend & ((inb ^ 1u) | (uint32_t)(max(t[j], u[j]) > x));
+                const uint32_t vs[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+#pragma unroll
+                for (int k = 0; k < CPW; k++) r[k] = max(r[k], ok ? (vs[k] & mask) : 0u);
+                okm |= ok << j;
+                oldm |= old << j;
+            }
+            todo &= ~okm;
+            if (oldm) {
+                // older than the ring or an earlier batch: HB row from L2 once stored
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    if (!((oldm >> j) & 1u)) continue;
+                    const uint32_t lpp = par[j];
+                    if (lpp < n && !round_done(sh.stored, lpp)) {
+                        c_wm++;
+                        __hip_atomic_store(&sh.req, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    } else {
+                        c_slow++;
+                        const uint32_t *row = a.hb + (uint64_t)(lpp + bs) * stride;
+#pragma unroll
+                        for (int k = 0; k < CPW; k++)
+                            if (valid[k]) r[k] = max(r[k], ld_l2_now(row + col[k]) & mask);
+                        todo &= ~(1u << j);
+                    }
+                }
+            }
+            if (!(todo & 15u)) {
+                // chunk done: shift the next one down
+#pragma unroll
+                for (int j = 0; j < LX_MAXP - 4; j++) par[j] = par[j + 4];
+                todo >>= 4;
+            }
+            if (todo) continue;
         }
-        // fold every pending parent, chunks of 4: issue granule reads, then evaluate
+        if (xi < np) {
+            // parents beyond the inline 16 (rare): one per pass, from the ring or L2
+            const uint32_t p = ld_l2_now(a.par_in + ovf + (xi - LX_MAXP));
+            const uint32_t lpp = p - bs;
+            bool ok = false, old = lpp >= n;
+            if (!old) {
+                uint32_t tg, tu;
+                uint4 ph, pv;
+                ring_read1(ring_base + (lpp % kRing) * 32u, tg, tu, ph, pv);
+                if (tg == lpp + 1 && tu == lpp + 1) {
+                    const uint32_t vs[4] = {pv.x, pv.y, pv.z, pv.w};
 #pragma unroll
-        for (int c = 0; c < LX_MAXP / 4; c++) {
-            if (!__any(todo >> (4 * c))) break;   // wave-uniform
-            c_chunk += ((todo >> (4 * c)) & 15u) ? 1u : 0u;
-            uint64_t g[4][CPW];
-#pragma unroll
-            for (int jj = 0; jj < 4; jj++) {
-                const uint64_t *gp = ring64 + (par[4 * c + jj] % RING) * CPW;
+                    for (int k = 0; k < CPW; k++) r[k] = max(r[k], vs[k] & mask);
+                    ok = true;
+                } else if (max(tg, tu) > lpp + 1) {
+                    if (round_done(sh.stored, lpp)) old = true;
+                    else __hip_atomic_store(&sh.req, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+            }
+            if (old) {
+                const uint32_t *row = a.hb + (uint64_t)p * stride;
 #pragma unroll
                 for (int k = 0; k < CPW; k++)
-                    g[jj][k] = __hip_atomic_load(gp + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    if (valid[k]) r[k] = max(r[k], ld_l2_now(row + col[k]) & mask);
+                ok = true;
             }
-#pragma unroll
-            for (int jj = 0; jj < 4; jj++) {
-                const int j = 4 * c + jj;
-                const uint32_t lpp = par[j];
-                const uint32_t tg = lpp + 1;
-                const uint32_t pend = (todo >> j) & 1u;
-                const uint32_t inb = (uint32_t)(lpp < n);    // in-batch parent (older ones wrap above n)
-                uint32_t rdy = pend & inb;
-#pragma unroll
-                for (int k = 0; k < CPW; k++) rdy &= (uint32_t)((uint32_t)g[jj][k] == tg);
-                const uint32_t old = pend & ((inb ^ 1u) | (uint32_t)((uint32_t)g[jj][0] > tg));
-                const bool isprev = (lpp + bs == prev);
-#pragma unroll
-                for (int k = 0; k < CPW; k++) {
-                    const uint32_t v = rdy ? ((uint32_t)(g[jj][k] >> 32) & mask) : 0u;
-                    r[k] = max(r[k], v);
-                    v0[k] = (rdy && isprev) ? v : v0[k];
-                }
-                todo &= ~((rdy | old) << j);
-                slow |= old << j;
-            }
-        }
-        if (slow) {
-            c_slow++;
-            // slow path: parents older than the ring (or from an earlier batch);
-            // their HB rows are in L2 once the writer's watermark passed them
-            const uint32_t stored = __hip_atomic_load(&wm[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-#pragma unroll
-            for (int j = 0; j < LX_MAXP; j++) {
-                if ((slow & (1u << j)) && (par[j] >= n || par[j] < stored)) {
-                    const uint32_t *row = a.hb + (uint64_t)(par[j] + bs) * stride;
-                    const bool isprev = (par[j] + bs == prev);
-#pragma unroll
-                    for (int k = 0; k < CPW; k++) {
-                        const uint32_t v = valid[k] ? (ld_l2_now(row + col[k]) & mask) : 0u;
-                        r[k] = max(r[k], v);
-                        if (isprev) v0[k] = v;
-                    }
-                    slow &= ~(1u << j);
-                }
-            }
-            if (slow) continue;   // writer has not stored them yet
-        }
-        if (todo) {
-            // some parent still pending: spin on the lowest pending one next
-            const int j = __builtin_ctz(todo);
-            uint32_t l = par[0];
-#pragma unroll
-            for (int t = 0; t < LX_MAXP; t++) l = (t == j) ? par[t] : l;
-            wait_off = (l % RING) * CPW;
-            wait_tag = l + 1;
+            if (ok) xi++;
             continue;
-        }
-        if (xi < np && diag != 2) {
-            while (xi < np) {   // parents beyond the inline 16 (rare)
-                const uint32_t p = ld_l2_now(a.par_in + ovf + (xi - LX_MAXP));
-                const uint32_t lpp = p - bs;
-                bool rd = true;
-                uint64_t gg[CPW];
-                if (lpp < n) {
-                    const uint64_t *gp = ring64 + (lpp % RING) * CPW;
-                    bool ok = true;
-#pragma unroll
-                    for (int k = 0; k < CPW; k++) {
-                        gg[k] = __hip_atomic_load(gp + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        ok &= ((uint32_t)gg[k] == lpp + 1);
-                    }
-                    if (!ok) {
-                        if ((uint32_t)gg[0] <= lpp + 1) break;   // not ready yet
-                        if (lpp >= __hip_atomic_load(&wm[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
-                        rd = false;                                // overwritten and stored: read L2
-                    }
-                } else {
-                    rd = false;
-                }
-#pragma unroll
-                for (int k = 0; k < CPW; k++) {
-                    uint32_t v;
-                    if (rd) v = (uint32_t)(gg[k] >> 32);
-                    else v = valid[k] ? ld_l2_now(a.hb + (uint64_t)p * stride + col[k]) : 0u;
-                    v &= mask;
-                    r[k] = max(r[k], v);
-                    if (p == prev) v0[k] = v;
-                }
-                xi++;
-            }
-            if (xi < np) continue;
         }
         {
+            // complete: the slot's previous occupant (lp - kRing) must be drained
+            if (lp >= (uint32_t)kRing && !round_done(sh.copied, lp - kRing)) { c_wm++; continue; }
             const uint32_t e = bs + lp;
-            if (!filled) {
-#pragma unroll
-                for (int k = 0; k < CPW; k++)
-                    if (valid[k] && col[k] == br)
-                        __hip_atomic_store(reinterpret_cast<uint64_t *>(brc + k * kBRC + seq % kBRC),
-                                           ((uint64_t)e << 32) | seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                if (FILL && diag != 3) {
-                    // LowestAfter range fill: events (col, s), s in (h0, r], are first
-                    // observed from branch `br` by this event (DESIGN.md section 3).
-#pragma unroll
-                    for (int k = 0; k < CPW; k++) {
-                        if (!valid[k]) continue;
-                        const uint32_t h0 = (prev != LX_NONE) ? v0[k] : 0u;
-                        const uint32_t lo = max(h0 + 1u, first[k]);
-                        for (uint32_t s = lo; s <= r[k]; s++) {
-                            c_fill++;
-                            const uint64_t cc = __hip_atomic_load(reinterpret_cast<const uint64_t *>(brc + k * kBRC + s % kBRC),
-                                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                            uint32_t row = (uint32_t)(cc >> 32);
-                            if ((uint32_t)cc != s) row = ld_l2_now(a.brow + (uint64_t)col[k] * a.s_cap + (s - first[k]));
-                            a.la[(uint64_t)row * stride + br] = seq;
-                        }
-                    }
-                }
-                filled = true;
-            }
-            // the slot's previous occupant (lp - RING) must have been copied by the writer
-            if (lp >= (uint32_t)RING &&
-                __hip_atomic_load(&wm[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < lp - RING + 1) {
-                c_wm++;
-                continue;
-            }
-            uint64_t *dst = ring + (lp % RING) * CPW;
 #pragma unroll
             for (int k = 0; k < CPW; k++)
-                __hip_atomic_store(dst + k, ((uint64_t)r[k] << 32) | (lp + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (valid[k] && col[k] == br)
+                    __hip_atomic_store(reinterpret_cast<uint64_t *>(brc + k * KB + seq % KB),
+                                       ((uint64_t)e << 32) | seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            uint32_t o[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (int k = 0; k < CPW; k++) o[k] = r[k];
+            ring_publish(ring_base + (lp % kRing) * 32u, lp + 1, prev, br, seq, make_uint4(o[0], o[1], o[2], o[3]));
             lp += E;
             have = false;
             c_done++;
@@ -627,7 +693,7 @@ __global__ __launch_bounds__(64 * (NCW + 2)) void k_index(IndexArgs a) {
     }
     if (a.prof) {
         unsigned long long *pw = a.prof + ((uint64_t)blockIdx.x * 8 + wave) * kProfSlots;
-        const uint32_t cs[8] = {c_pass, c_spin, c_chunk, c_done, c_slow, c_fill, c_wm, c_norec};
+        const uint32_t cs[8] = {c_pass, 0u, c_chunk, c_done, c_slow, 0u, c_wm, c_norec};
 #pragma unroll
         for (int i = 0; i < 8; i++) atomicAdd(pw + i, (unsigned long long)cs[i]);
         atomicMax(pw + 8, (unsigned long long)c_pass);               // wave passes = max over lanes
@@ -635,23 +701,22 @@ __global__ __launch_bounds__(64 * (NCW + 2)) void k_index(IndexArgs a) {
     }
 }
 
-template <int CPW, int NCW, int RING, int RR>
+template <int CPW, int NCW, int RR>
 static hipError_t launch_index_t(const IndexArgs &a0, hipStream_t s) {
     IndexArgs a = a0;
     a.n_slices = (a.ncols + CPW - 1) / CPW;
     a.slices_per_xcd = (a.n_slices + 7) / 8;
     uint32_t grid = a.slices_per_xcd * 8;
-    if (a.diag_nofill) hipLaunchKernelGGL((k_index<CPW, NCW, RING, RR, false>), dim3(grid), dim3(64 * (NCW + 2)), 0, s, a);
-    else hipLaunchKernelGGL((k_index<CPW, NCW, RING, RR, true>), dim3(grid), dim3(64 * (NCW + 2)), 0, s, a);
+    if (a.diag_nofill) hipLaunchKernelGGL((k_index<CPW, NCW, RR, false>), dim3(grid), dim3(64 * (NCW + 1 + kND)), 0, s, a);
+    else hipLaunchKernelGGL((k_index<CPW, NCW, RR, true>), dim3(grid), dim3(64 * (NCW + 1 + kND)), 0, s, a);
     return hipGetLastError();
 }
 
 template <int CPW, int NCW>
 static hipError_t launch_index_n(const IndexArgs &a, hipStream_t s) {
-    constexpr int RING = 8192 / CPW;             // 64 KB of {tag, seq} granules
     constexpr int RRMIN = 64 * NCW;
-    if (a.rr_hint >= 512 || RRMIN > 256) return launch_index_t<CPW, NCW, RING, (RRMIN > 512 ? RRMIN : 512)>(a, s);
-    return launch_index_t<CPW, NCW, RING, (RRMIN > 256 ? RRMIN : 256)>(a, s);
+    if (a.rr_hint >= 512 || RRMIN > 256) return launch_index_t<CPW, NCW, (RRMIN > 512 ? RRMIN : 512)>(a, s);
+    return launch_index_t<CPW, NCW, (RRMIN > 256 ? RRMIN : 256)>(a, s);
 }
 
 template <int CPW>
@@ -665,12 +730,11 @@ hipError_t launch_index(const IndexArgs &a, hipStream_t s) {
     if (a.n == 0 || a.ncols == 0) return hipSuccess;
     // columns per workgroup: aim at ~256 workgroups; compute waves: enough
     // events in flight for the DAG's antichain width (~V / (1.6 P))
-    uint32_t cpw = a.cpw_hint ? a.cpw_hint : (a.ncols <= 256 ? 1 : a.ncols <= 512 ? 2 : a.ncols <= 1024 ? 4 : 8);
-    uint32_t ncw = a.ncw_hint ? a.ncw_hint : (a.width_hint <= 48 ? 1 : a.width_hint <= 96 ? 2 : 4);
+    uint32_t cpw = a.cpw_hint ? a.cpw_hint : (a.ncols <= 256 ? 1 : a.ncols <= 512 ? 2 : 4);
+    uint32_t ncw = a.ncw_hint ? a.ncw_hint : (a.width_hint <= 24 ? 1 : a.width_hint <= 48 ? 2 : 4);
     if (cpw <= 1) return launch_index_c<1>(a, ncw, s);
     if (cpw <= 2) return launch_index_c<2>(a, ncw, s);
-    if (cpw <= 4) return launch_index_c<4>(a, ncw, s);
-    return launch_index_c<8>(a, ncw, s);
+    return launch_index_c<4>(a, ncw, s);
 }
 
 // ---------------------------------------------------------------------------- fork marks
