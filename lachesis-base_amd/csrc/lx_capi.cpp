@@ -401,6 +401,7 @@ int add_batch_dev(lx_index *h, uint32_t n, const uint32_t *creator, const uint32
     ia.n = n;
     ia.rec = h->b_rec;
     ia.par_in = par;
+    ia.poff_in = poff;
     ia.col_list = h->col_list;
     ia.ncols = h->ncols;
     ia.branch_first = h->branch_first;

@@ -17,14 +17,14 @@
 #define LX_NONE 0xFFFFFFFFu
 #define LX_MARK 0x80000000u
 #define LX_SEQ_MASK 0x7FFFFFFFu
-#define LX_MAXP 16   // parents stored inline in an event record
+#define LX_MAXP 12   // parents stored inline in an event record
 
-// Event record consumed by the index kernel: 6 x uint4 = 96 B
+// Event record consumed by the index kernel: 4 x uint4 = 64 B
 //   w0 branch, w1 seq, w2 number of parents, w3 previous event of the same
-//   branch (global dense index, NONE if the event opens its branch), w4 offset
-//   of parents[16..] in the batch parent array, w5..w7 reserved,
-//   w8..w23 the first 16 parents sorted newest first (global index, NONE pad)
-#define LX_REC_Q 6
+//   branch (global dense index, NONE if the event opens its branch),
+//   w4..w15 the first 12 parents sorted oldest first (global index, NONE pad);
+//   parents beyond 12 are read from the batch parent array
+#define LX_REC_Q 4
 struct EventRec {
     uint4 q[LX_REC_Q];
 };
@@ -37,6 +37,7 @@ struct IndexArgs {
     uint32_t n;
     const EventRec *rec;
     const uint32_t *par_in;      // batch parent array (overflow parents)
+    const uint32_t *poff_in;     // batch parent offsets
     const uint32_t *col_list;
     uint32_t ncols;
     uint32_t n_slices;           // ceil(ncols / CPW)

@@ -207,13 +207,12 @@ __global__ void k_finalize(BatchArgs a) {
     }
     EventRec r;
     r.q[0] = make_uint4(br, s, np, prev);
-    r.q[1] = make_uint4(p0 + LX_MAXP, 0, 0, 0);
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
+    for (int k = 0; k < LX_MAXP / 4; k++) {
         uint32_t v[4];
 #pragma unroll
         for (int t = 0; t < 4; t++) v[t] = (4 * k + t < (int)np) ? w[4 * k + t] : LX_NONE;
-        r.q[2 + k] = make_uint4(v[0], v[1], v[2], v[3]);
+        r.q[1 + k] = make_uint4(v[0], v[1], v[2], v[3]);
     }
     a.rec[e] = r;
 }
@@ -232,119 +231,119 @@ hipError_t launch_batch_finish(const BatchArgs &a, hipStream_t s) {
 // of column c touch only column c of HB and rows of branch c in LA), so the
 // workgroups never communicate; one launch covers the whole batch.
 //
-// The batch's DAG depth (not its size) bounds the walk: every level costs one
-// pass of the compute loop, so the compute waves do only what the critical
-// path needs -- fold parents, publish -- and everything else runs beside them.
-// Roles (NCW compute waves + 1 loader + ND drain waves):
-//  * loader: streams the 96-B event records into an LDS record ring by LDS-DMA
-//    (global_load_lds_dwordx4, RR/64 rounds in flight) and publishes each slot
-//    with a tag after its own vmcnt wait;
-//  * compute lane g handles events g, g+E, ... (E = 64*NCW).  Parents arrive
-//    oldest first; each pass folds ONE chunk of 4 (so a waiting lane folds its
-//    old parents early and the newest chunk is all that is left when its last
-//    parent completes), then publishes {tag | prev, branch, seq | CPW seqs}
-//    into a 32-B slot of the LDS event ring.  No global access on the hot path;
-//  * drain waves (rounds of 64 events, round r on wave r % ND): store the HB
+// The batch's DAG depth (not its size) bounds the walk: every level costs at
+// least one pass of the compute loop, so the compute waves do only what the
+// critical path needs -- fold parents, publish -- and the rest runs beside them.
+// Roles (NCW compute waves + 1 loader + kND drain waves):
+//  * loader: streams the 64-B event records into an LDS record ring by LDS-DMA
+//    (global_load_lds_dwordx4, up to 8 rounds of 64 in flight) and publishes
+//    each slot with a tag after its own vmcnt wait;
+//  * compute lane g handles events g, g+E, ... (E = 64*NCW).  Each pass it
+//    folds ONE chunk of 4 parents, cycling over the chunks that still have
+//    pending parents (so a parent that completes late stalls only its own
+//    chunk), then publishes its CPW seqs into a 32-B slot of the LDS event
+//    ring.  No global access on the hot path;
+//  * drain waves (rounds of 64 events, round r on wave r % kND): store the HB
 //    row and do the LowestAfter range fill, reading RAW(prev) from the ring.
-// Publishing: a writer stores the slot body, then the tag (one asm block, so
-// LDS executes them in that order); a reader issues the tag read, then the
-// body read (one asm block), so a matching tag proves the body is complete.
-// A tag above the expected one means the slot was reused: that parent's HB row
-// is read from L2 once the drain reports it stored (rare: parents older than
-// the ring, or from an earlier batch).  Lanes never block inside a pass, so
-// dependencies between lanes of one wave cannot deadlock; drains only wait for
-// older events, and service "store-complete" requests while they wait.
+// Slots are two 16-B halves {tag, seq0, seq1, seq2}, {tag, seq3, -, -}; one
+// lane's ds_read_b128 / ds_write_b128 is a single LDS access, so a half whose
+// tag matches is consistent, and a slot is valid when every half it needs
+// matches.  A tag above the expected one means the slot was reused: that
+// parent's HB row is read from L2 once its drain reports it stored (rare:
+// parents older than the ring, or from an earlier batch).  Lanes never block
+// inside a pass, so dependencies between lanes of one wave cannot deadlock;
+// drains wait only for older events and keep publishing their own progress.
 constexpr int kRing = 2048;          // event slots, 32 B each (64 KB)
 constexpr int kND = 2;               // drain waves
 
-template <int CPW>
-struct WalkCfg {
-    static constexpr int KB = 1024 / CPW;   // recent (seq -> event) entries per owned branch
-};
-
 struct WalkShared {
-    uint32_t copied[kND];    // rounds drained (ring data consumed) per drain wave
+    uint32_t copied[kND];    // rounds drained (ring and record data consumed) per drain wave
     uint32_t stored[kND];    // rounds whose global stores are complete per drain wave
     uint32_t req;            // a compute lane waits for `stored`: drains flush
 };
 
 __device__ __forceinline__ bool round_done(const uint32_t *cnt, uint32_t ev) {
     const uint32_t r = ev / 64;
-    return __hip_atomic_load(cnt + (r % kND), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) > r / kND;
+    return __hip_atomic_load(cnt + (r % kND), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) > r / kND;
 }
 
-// read tag, 16 B of seqs, tag again, for 4 ring slots, in that order, and wait.
-// The body is valid iff both tags equal the expected one (ring_publish marks a
-// slot busy before rewriting it, and LDS executes one wave's operations in
-// order, so a body read that overlapped a rewrite sees a changed second tag).
-__device__ __forceinline__ void ring_read4(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3, uint32_t t[4], uint32_t u[4],
-                                           uint4 v[4]) {
-    typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint4 to4(u4v x) { return make_uint4(x.x, x.y, x.z, x.w); }
+
+// first halves of 4 slots (CPW <= 3)
+__device__ __forceinline__ void ring_read4a(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3, uint4 h[4]) {
     u4v x0, x1, x2, x3;
-    uint32_t t0, t1, t2, t3, u0, u1, u2, u3;
     asm volatile(
-        "ds_read_b32 %0, %12\n\t"
-        "ds_read_b128 %8, %12 offset:16\n\t"
-        "ds_read_b32 %4, %12\n\t"
-        "ds_read_b32 %1, %13\n\t"
-        "ds_read_b128 %9, %13 offset:16\n\t"
-        "ds_read_b32 %5, %13\n\t"
-        "ds_read_b32 %2, %14\n\t"
-        "ds_read_b128 %10, %14 offset:16\n\t"
-        "ds_read_b32 %6, %14\n\t"
-        "ds_read_b32 %3, %15\n\t"
-        "ds_read_b128 %11, %15 offset:16\n\t"
-        "ds_read_b32 %7, %15\n\t"
+        "ds_read_b128 %0, %4\n\t"
+        "ds_read_b128 %1, %5\n\t"
+        "ds_read_b128 %2, %6\n\t"
+        "ds_read_b128 %3, %7\n\t"
         "s_waitcnt lgkmcnt(0)"
-        : "=&v"(t0), "=&v"(t1), "=&v"(t2), "=&v"(t3), "=&v"(u0), "=&v"(u1), "=&v"(u2), "=&v"(u3),
-          "=&v"(x0), "=&v"(x1), "=&v"(x2), "=&v"(x3)
+        : "=&v"(x0), "=&v"(x1), "=&v"(x2), "=&v"(x3)
         : "v"(a0), "v"(a1), "v"(a2), "v"(a3)
         : "memory");
-    t[0] = t0; t[1] = t1; t[2] = t2; t[3] = t3;
-    u[0] = u0; u[1] = u1; u[2] = u2; u[3] = u3;
-    v[0] = make_uint4(x0.x, x0.y, x0.z, x0.w);
-    v[1] = make_uint4(x1.x, x1.y, x1.z, x1.w);
-    v[2] = make_uint4(x2.x, x2.y, x2.z, x2.w);
-    v[3] = make_uint4(x3.x, x3.y, x3.z, x3.w);
+    h[0] = to4(x0); h[1] = to4(x1); h[2] = to4(x2); h[3] = to4(x3);
 }
 
-// one slot: tag, body (header + seqs), tag
-__device__ __forceinline__ void ring_read1(uint32_t a0, uint32_t &t, uint32_t &u, uint4 &h, uint4 &v) {
-    typedef uint32_t u4v __attribute__((ext_vector_type(4)));
-    u4v x, y;
-    uint32_t t0, u0;
+// both halves of 4 slots (CPW == 4)
+__device__ __forceinline__ void ring_read4b(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3, uint4 h[4], uint4 g[4]) {
+    u4v x0, x1, x2, x3, y0, y1, y2, y3;
     asm volatile(
-        "ds_read_b32 %0, %4\n\t"
-        "ds_read_b128 %2, %4\n\t"
-        "ds_read_b128 %3, %4 offset:16\n\t"
-        "ds_read_b32 %1, %4\n\t"
+        "ds_read_b128 %0, %8\n\t"
+        "ds_read_b128 %4, %8 offset:16\n\t"
+        "ds_read_b128 %1, %9\n\t"
+        "ds_read_b128 %5, %9 offset:16\n\t"
+        "ds_read_b128 %2, %10\n\t"
+        "ds_read_b128 %6, %10 offset:16\n\t"
+        "ds_read_b128 %3, %11\n\t"
+        "ds_read_b128 %7, %11 offset:16\n\t"
         "s_waitcnt lgkmcnt(0)"
-        : "=&v"(t0), "=&v"(u0), "=&v"(x), "=&v"(y)
+        : "=&v"(x0), "=&v"(x1), "=&v"(x2), "=&v"(x3), "=&v"(y0), "=&v"(y1), "=&v"(y2), "=&v"(y3)
+        : "v"(a0), "v"(a1), "v"(a2), "v"(a3)
+        : "memory");
+    h[0] = to4(x0); h[1] = to4(x1); h[2] = to4(x2); h[3] = to4(x3);
+    g[0] = to4(y0); g[1] = to4(y1); g[2] = to4(y2); g[3] = to4(y3);
+}
+
+__device__ __forceinline__ void ring_read1(uint32_t a0, uint4 &h, uint4 &g) {
+    u4v x, y;
+    asm volatile(
+        "ds_read_b128 %0, %2\n\t"
+        "ds_read_b128 %1, %2 offset:16\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(x), "=&v"(y)
         : "v"(a0)
         : "memory");
-    t = t0; u = u0;
-    h = make_uint4(x.x, x.y, x.z, x.w);
-    v = make_uint4(y.x, y.y, y.z, y.w);
+    h = to4(x);
+    g = to4(y);
 }
 
-constexpr uint32_t kBusy = 0xFFFFFFFFu;   // slot being rewritten by a newer event
+template <int CPW>
+__device__ __forceinline__ void ring_publish(uint32_t addr, uint32_t tag, const uint32_t *r) {
+    u4v x;
+    x.x = tag; x.y = r[0]; x.z = CPW > 1 ? r[1 % CPW] : 0u; x.w = CPW > 2 ? r[2 % CPW] : 0u;
+    if (CPW == 4) {
+        u4v y;
+        y.x = tag; y.y = r[3 % CPW]; y.z = 0u; y.w = 0u;
+        asm volatile(
+            "ds_write_b128 %0, %2 offset:16\n\t"
+            "ds_write_b128 %0, %1"
+            :
+            : "v"(addr), "v"(x), "v"(y)
+            : "memory");
+    } else {
+        asm volatile("ds_write_b128 %0, %1" : : "v"(addr), "v"(x) : "memory");
+    }
+}
 
-// publish a slot: busy tag, body (prev, branch, seq; seqs), then the tag
-__device__ __forceinline__ void ring_publish(uint32_t addr, uint32_t tag, uint32_t prev, uint32_t br, uint32_t seq, uint4 v) {
-    typedef uint32_t u4v __attribute__((ext_vector_type(4)));
-    typedef uint32_t u2v __attribute__((ext_vector_type(2)));
-    u4v x; x.x = v.x; x.y = v.y; x.z = v.z; x.w = v.w;
-    u2v m; m.x = br; m.y = seq;
-    const uint32_t busy = kBusy;
-    asm volatile(
-        "ds_write_b32 %0, %5\n\t"
-        "ds_write_b32 %0, %2 offset:4\n\t"
-        "ds_write_b64 %0, %3 offset:8\n\t"
-        "ds_write_b128 %0, %4 offset:16\n\t"
-        "ds_write_b32 %0, %1"
-        :
-        : "v"(addr), "v"(tag), "v"(prev), "v"(m), "v"(x), "v"(busy)
-        : "memory");
+// slot seqs of a valid slot
+template <int CPW>
+__device__ __forceinline__ void slot_vals(const uint4 &h, const uint4 &g, uint32_t *o) {
+    o[0] = h.y;
+    if (CPW > 1) o[1 % CPW] = h.z;
+    if (CPW > 2) o[2 % CPW] = h.w;
+    if (CPW > 3) o[3 % CPW] = g.y;
 }
 
 __device__ __forceinline__ uint32_t lds_addr(const void *p) {
@@ -353,14 +352,14 @@ __device__ __forceinline__ uint32_t lds_addr(const void *p) {
 
 template <int CPW, int NCW, int RR, bool FILL>
 __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
-    static_assert(CPW == 1 || CPW == 2 || CPW == 4, "16-B slot body");
+    static_assert(CPW == 1 || CPW == 2 || CPW == 4, "slot layout");
     constexpr int NT = 64 * (NCW + 1 + kND);
     constexpr int E = 64 * NCW;
     constexpr int RQ = LX_REC_Q;
-    constexpr int KB = WalkCfg<CPW>::KB;
+    constexpr int KB = 1024 / CPW;               // recent (seq -> event) entries per owned branch
     static_assert(kRing % E == 0 && kRing / E >= 4, "ring slot reuse must stay within one lane");
-    static_assert(RR % 64 == 0 && RR / 64 <= 8 && RR >= E, "record ring");
-    __shared__ uint4 ring[kRing * 2];            // slot s: [2s] = {tag, prev, br, seq}, [2s+1] = CPW seqs
+    static_assert(RR % 64 == 0 && RR / 64 >= 4 && RR >= 2 * E, "record ring");
+    __shared__ uint4 ring[kRing * 2];            // slot s: ring[2s], ring[2s+1]
     __shared__ uint4 rrec[RR * RQ];              // event records
     __shared__ uint32_t rtag[RR];
     __shared__ uint2 brc[CPW * KB];              // {seq, event} of recent events of owned branches
@@ -383,6 +382,7 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
     const int lane = threadIdx.x % 64;
     const uint64_t stride = a.stride;
     const uint32_t mask = a.mask ? LX_SEQ_MASK : 0xFFFFFFFFu;
+    const uint32_t ring_base = lds_addr(ring);
 
     uint32_t col[CPW], first[CPW];
     bool valid[CPW];
@@ -400,47 +400,39 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
     if (wave == NCW) {
         // ------------------------------------------------------------ loader
         const uint32_t nrounds = (n + 63) / 64;
-        constexpr uint32_t D = RR / 64;
+        constexpr uint32_t D = RR / 64 < 8 ? RR / 64 : 8;
         uint32_t issued = 0, done = 0;
         const char *recb = reinterpret_cast<const char *>(a.rec);
         const uint64_t rec_bytes = (uint64_t)n * sizeof(EventRec);
         while (done < nrounds) {
             bool progressed = false;
-            if (issued < nrounds && issued - done < D) {
-                // slots of this round are free once their previous occupants
-                // (events ev - RR) have been published
-                const uint32_t ev = issued * 64 + lane;
-                bool free = true;
-                if (ev < n && ev >= (uint32_t)RR) {
-                    const uint32_t q = ev - RR;
-                    const uint32_t t = __hip_atomic_load(&ring[(q % kRing) * 2].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    if (t < q + 1) free = false;
-                }
-                if (__all(free)) {
-                    const uint32_t s0 = (issued * 64) % RR;
-                    char *dst = reinterpret_cast<char *>(rrec) + (uint64_t)s0 * sizeof(EventRec);
-                    const uint64_t base = (uint64_t)issued * 64 * sizeof(EventRec);
+            // a round's record slots are free once the drain consumed their
+            // previous occupants (events ev - RR: same round offset, wave-uniform)
+            if (issued < nrounds && issued - done < D &&
+                (issued * 64 < (uint32_t)RR || round_done(sh.copied, issued * 64 - RR))) {
+                const uint32_t s0 = (issued * 64) % RR;
+                char *dst = reinterpret_cast<char *>(rrec) + (uint64_t)s0 * sizeof(EventRec);
+                const uint64_t base = (uint64_t)issued * 64 * sizeof(EventRec);
 #pragma unroll
-                    for (int i = 0; i < RQ; i++) {
-                        uint64_t off = base + (uint64_t)(i * 64 + lane) * 16;
-                        if (off + 16 > rec_bytes) off = 0;   // tail of the last round: harmless filler
-                        __builtin_amdgcn_global_load_lds((const void *)(recb + off), (void *)(dst + i * 1024), 16, 0, 0);
-                    }
-                    issued++;
-                    progressed = true;
+                for (int i = 0; i < RQ; i++) {
+                    uint64_t off = base + (uint64_t)(i * 64 + lane) * 16;
+                    if (off + 16 > rec_bytes) off = 0;   // tail of the last round: harmless filler
+                    __builtin_amdgcn_global_load_lds((const void *)(recb + off), (void *)(dst + i * 1024), 16, 0, 0);
                 }
+                issued++;
+                progressed = true;
             }
             if (!progressed && issued > done) {
-                // oldest round landed once at most RQ DMAs per younger round remain
+                // the oldest round landed once at most RQ DMAs per younger round remain
                 switch (issued - done - 1) {
                     case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-                    case 1: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-                    case 2: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
-                    case 3: asm volatile("s_waitcnt vmcnt(18)" ::: "memory"); break;
-                    case 4: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
-                    case 5: asm volatile("s_waitcnt vmcnt(30)" ::: "memory"); break;
-                    case 6: asm volatile("s_waitcnt vmcnt(36)" ::: "memory"); break;
-                    default: asm volatile("s_waitcnt vmcnt(42)" ::: "memory"); break;
+                    case 1: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+                    case 2: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+                    case 3: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+                    case 4: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+                    case 5: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
+                    case 6: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
+                    default: asm volatile("s_waitcnt vmcnt(28)" ::: "memory"); break;
                 }
                 const uint32_t ev = done * 64 + lane;
                 if (ev < n) __hip_atomic_store(&rtag[ev % RR], ev + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -458,11 +450,15 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
         uint32_t nd = 0;                 // rounds of this wave completed
         for (uint32_t R = d; R * 64 < n; R += kND, nd++) {
             const uint32_t ev = R * 64 + lane;
-            const uint32_t sl = ev % kRing;
-            // wait for the round (servicing store-complete requests meanwhile)
+            const uint32_t sa = ring_base + (ev % kRing) * 32u;
+            uint4 h = make_uint4(0, 0, 0, 0), g = make_uint4(0, 0, 0, 0);
+            // wait for the round (keep publishing progress: others may wait on it)
             while (true) {
                 bool ready = true;
-                if (ev < n) ready = __hip_atomic_load(&ring[sl * 2].x, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == ev + 1;
+                if (ev < n) {
+                    ring_read1(sa, h, g);
+                    ready = h.x == ev + 1 && (CPW < 4 || g.x == ev + 1);
+                }
                 if (__all(ready)) break;
                 if (__hip_atomic_load(&sh.req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -470,36 +466,30 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
                 }
                 __builtin_amdgcn_s_sleep(1);
             }
-            uint32_t prev = LX_NONE, br = 0, seq = 0;
             uint32_t r[CPW], h0[CPW];
-            uint4 vv = make_uint4(0, 0, 0, 0);
+            uint32_t prev = LX_NONE, br = 0, seq = 0;
             if (ev < n) {
-                const uint4 hd = ring[sl * 2];
-                vv = ring[sl * 2 + 1];
-                prev = hd.y; br = hd.z; seq = hd.w;
-                const uint32_t vs[4] = {vv.x, vv.y, vv.z, vv.w};
+                slot_vals<CPW>(h, g, r);
+                const uint4 q0 = rrec[(ev % RR) * RQ];
+                br = q0.x; seq = q0.y; prev = q0.w;
 #pragma unroll
-                for (int k = 0; k < CPW; k++) { r[k] = vs[k] & mask; h0[k] = 0; }
+                for (int k = 0; k < CPW; k++) h0[k] = 0;
                 if (prev != LX_NONE) {
                     const uint32_t pl = prev - bs;
                     bool got = false;
                     if (pl < n) {
-                        uint32_t pt, pu;
-                        uint4 ph, pv;
-                        ring_read1(lds_addr(ring) + (pl % kRing) * 32u, pt, pu, ph, pv);
-                        if (pt == pl + 1 && pu == pl + 1) {
-                            const uint32_t ps4[4] = {pv.x, pv.y, pv.z, pv.w};
-#pragma unroll
-                            for (int k = 0; k < CPW; k++) h0[k] = ps4[k] & mask;
+                        uint4 ph, pg;
+                        ring_read1(ring_base + (pl % kRing) * 32u, ph, pg);
+                        if (ph.x == pl + 1 && (CPW < 4 || pg.x == pl + 1)) {
+                            slot_vals<CPW>(ph, pg, h0);
                             got = true;
                         } else {
                             // reused slot: prev's row is (being) stored by a drain
                             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                            const uint32_t dd = (pl / 64) % kND;
-                            if (dd != d) {
+                            if ((pl / 64) % kND != d) {
                                 // the other drain may in turn wait for this one: keep
-                                // publishing our own completed rounds while waiting
-                                __hip_atomic_store(&sh.stored[d], nd, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);   // divergent: every active lane
+                                // publishing our completed rounds (divergent: every active lane)
+                                __hip_atomic_store(&sh.stored[d], nd, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                                 while (!round_done(sh.stored, pl)) {
                                     __hip_atomic_store(&sh.req, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                                     __builtin_amdgcn_s_sleep(1);
@@ -510,24 +500,25 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
                     if (!got) {
                         const uint32_t *row = a.hb + (uint64_t)prev * stride;
 #pragma unroll
-                        for (int k = 0; k < CPW; k++) h0[k] = valid[k] ? (ld_l2_now(row + col[k]) & mask) : 0u;
+                        for (int k = 0; k < CPW; k++) h0[k] = valid[k] ? ld_l2_now(row + col[k]) : 0u;
                     }
+#pragma unroll
+                    for (int k = 0; k < CPW; k++) h0[k] &= mask;
                 }
             }
-            // ring data of this round consumed: its slots may be reused
+            // ring and record data of this round consumed: slots may be reused
             if (lane == 0) __hip_atomic_store(&sh.copied[d], nd + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             if (ev < n) {
                 // HB row (raw values incl. fork bits as published)
                 uint32_t *hrow = a.hb + (uint64_t)(bs + ev) * stride;
                 if (contig) {
-                    if (CPW == 1) hrow[col[0]] = vv.x;
-                    else if (CPW == 2) *reinterpret_cast<uint2 *>(hrow + col[0]) = make_uint2(vv.x, vv.y);
-                    else *reinterpret_cast<uint4 *>(hrow + col[0]) = vv;
+                    if (CPW == 1) hrow[col[0]] = r[0];
+                    else if (CPW == 2) *reinterpret_cast<uint2 *>(hrow + col[0]) = make_uint2(r[0], r[1 % CPW]);
+                    else *reinterpret_cast<uint4 *>(hrow + col[0]) = make_uint4(r[0], r[1 % CPW], r[2 % CPW], r[3 % CPW]);
                 } else {
-                    const uint32_t vs[4] = {vv.x, vv.y, vv.z, vv.w};
 #pragma unroll
                     for (int k = 0; k < CPW; k++)
-                        if (valid[k]) hrow[col[k]] = vs[k];
+                        if (valid[k]) hrow[col[k]] = r[k];
                 }
                 if (FILL) {
                     // LowestAfter range fill: events (col, s), s in (h0, r], are first
@@ -536,7 +527,8 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
                     for (int k = 0; k < CPW; k++) {
                         if (!valid[k]) continue;
                         const uint32_t lo = max(h0[k] + 1u, first[k]);
-                        for (uint32_t s = lo; s <= r[k]; s++) {
+                        const uint32_t hi = r[k] & mask;
+                        for (uint32_t s = lo; s <= hi; s++) {
                             const uint64_t cc = __hip_atomic_load(reinterpret_cast<const uint64_t *>(brc + k * KB + s % KB),
                                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                             uint32_t row = (uint32_t)(cc >> 32);
@@ -554,8 +546,7 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
                 }
             }
         }
-        // final: every store of this wave complete (another drain or a compute
-        // lane may still wait for it)
+        // every store of this wave complete; a compute lane or the other drain may wait for it
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (lane == 0) __hip_atomic_store(&sh.stored[d], 0xFFFFFFFFu, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         return;
@@ -567,11 +558,11 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
 
     uint32_t lp = threadIdx.x;
     bool have = false;
-    uint32_t br = 0, seq = 0, np = 0, prev = 0, ovf = 0, xi = 0;
+    uint32_t br = 0, seq = 0, np = 0, xi = 0;
     uint32_t par[LX_MAXP];
-    uint32_t todo = 0;
+    uint32_t todo = 0;   // pending parents (bit j = par[j])
+    uint32_t cc = 0;     // chunk folded next
     uint32_t r[CPW];
-    const uint32_t ring_base = lds_addr(ring);
 
     while (lp < n) {
         c_pass++;
@@ -580,49 +571,64 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
             if (__hip_atomic_load(&rtag[slot], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != lp + 1) { c_norec++; continue; }
             const uint4 *rq = rrec + slot * RQ;
             const uint4 q0 = rq[0];
-            br = q0.x; seq = q0.y; np = q0.z; prev = q0.w;
-            ovf = rq[1].x;
+            br = q0.x; seq = q0.y; np = q0.z;
 #pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const uint4 q = rq[2 + j];
+            for (int j = 0; j < LX_MAXP / 4; j++) {
+                const uint4 q = rq[1 + j];
                 par[4 * j] = q.x - bs; par[4 * j + 1] = q.y - bs; par[4 * j + 2] = q.z - bs; par[4 * j + 3] = q.w - bs;
             }
-            todo = (np >= LX_MAXP) ? 0xFFFFu : ((1u << np) - 1u);
+            todo = (np >= LX_MAXP) ? ((1u << LX_MAXP) - 1u) : ((1u << np) - 1u);
+            cc = 0;
             xi = LX_MAXP;
 #pragma unroll
             for (int k = 0; k < CPW; k++) r[k] = (col[k] == br) ? seq : 0u;
             have = true;
         }
         if (todo) {
-            // fold the oldest pending chunk (par[0..3]; parents sorted oldest first)
+            // fold chunk cc (parents 4cc..4cc+3)
             c_chunk++;
-            uint32_t ad[4], t[4], u[4];
-            uint4 v[4];
+            uint32_t p4[4];
 #pragma unroll
-            for (int j = 0; j < 4; j++) ad[j] = ring_base + (par[j] % kRing) * 32u;
-            ring_read4(ad[0], ad[1], ad[2], ad[3], t, u, v);
+            for (int j = 0; j < 4; j++) {
+                uint32_t x = par[j];
+#pragma unroll
+                for (int c = 1; c < LX_MAXP / 4; c++) x = (cc == (uint32_t)c) ? par[4 * c + j] : x;
+                p4[j] = x;
+            }
+            const uint32_t tc = (todo >> (4 * cc)) & 15u;
+            uint4 h[4], g[4];
+            const uint32_t a0 = ring_base + (p4[0] % kRing) * 32u, a1 = ring_base + (p4[1] % kRing) * 32u;
+            const uint32_t a2 = ring_base + (p4[2] % kRing) * 32u, a3 = ring_base + (p4[3] % kRing) * 32u;
+            if (CPW == 4) ring_read4b(a0, a1, a2, a3, h, g);
+            else ring_read4a(a0, a1, a2, a3, h);
             // branch-free common case: fold the parents whose slot is valid
             uint32_t okm = 0, oldm = 0;
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                const uint32_t x = par[j] + 1u;
-                const uint32_t pend = (todo >> j) & 1u;
-                const uint32_t inb = (uint32_t)(par[j] < n);
-                const uint32_t ok = pend & inb & (uint32_t)(t[j] == x) & (uint32_t)(u[j] == x);
-                const uint32_t old = pend & ((inb ^ 1u) | (uint32_t)(max(t[j], u[j]) > x));
-                const uint32_t vs[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+                const uint32_t x = p4[j] + 1u;
+                const uint32_t pend = (tc >> j) & 1u;
+                const uint32_t inb = (uint32_t)(p4[j] < n);
+                uint32_t ok = pend & inb & (uint32_t)(h[j].x == x);
+                uint32_t newer = (uint32_t)(h[j].x > x);
+                if (CPW == 4) {
+                    ok &= (uint32_t)(g[j].x == x);
+                    newer |= (uint32_t)(g[j].x > x);
+                }
+                const uint32_t old = pend & ((inb ^ 1u) | newer);
+                uint32_t vs[CPW];
+                slot_vals<CPW>(h[j], g[j], vs);
 #pragma unroll
                 for (int k = 0; k < CPW; k++) r[k] = max(r[k], ok ? (vs[k] & mask) : 0u);
                 okm |= ok << j;
                 oldm |= old << j;
             }
-            todo &= ~okm;
+            uint32_t tn = tc & ~okm;
             if (oldm) {
                 // older than the ring or an earlier batch: HB row from L2 once stored
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
                     if (!((oldm >> j) & 1u)) continue;
-                    const uint32_t lpp = par[j];
+                    const uint32_t lpp = p4[j];
                     if (lpp < n && !round_done(sh.stored, lpp)) {
                         c_wm++;
                         __hip_atomic_store(&sh.req, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -632,33 +638,35 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
 #pragma unroll
                         for (int k = 0; k < CPW; k++)
                             if (valid[k]) r[k] = max(r[k], ld_l2_now(row + col[k]) & mask);
-                        todo &= ~(1u << j);
+                        tn &= ~(1u << j);
                     }
                 }
             }
-            if (!(todo & 15u)) {
-                // chunk done: shift the next one down
+            todo = (todo & ~(15u << (4 * cc))) | (tn << (4 * cc));
+            // next chunk: cyclically after cc, among the chunks still pending
+            uint32_t pm = 0;
 #pragma unroll
-                for (int j = 0; j < LX_MAXP - 4; j++) par[j] = par[j + 4];
-                todo >>= 4;
-            }
+            for (int c = 0; c < LX_MAXP / 4; c++) pm |= (uint32_t)(((todo >> (4 * c)) & 15u) != 0) << c;
+            constexpr uint32_t NCH = LX_MAXP / 4;
+            const uint32_t rot = ((pm | (pm << NCH)) >> (cc + 1)) & ((1u << NCH) - 1u);
+            cc = rot ? (cc + 1 + (uint32_t)__builtin_ctz(rot)) % NCH : cc;
             if (todo) continue;
         }
         if (xi < np) {
-            // parents beyond the inline 16 (rare): one per pass, from the ring or L2
-            const uint32_t p = ld_l2_now(a.par_in + ovf + (xi - LX_MAXP));
+            // parents beyond the inline LX_MAXP (rare): one per pass, from the ring or L2
+            const uint32_t p = ld_l2_now(a.par_in + a.poff_in[lp] + xi);
             const uint32_t lpp = p - bs;
             bool ok = false, old = lpp >= n;
             if (!old) {
-                uint32_t tg, tu;
-                uint4 ph, pv;
-                ring_read1(ring_base + (lpp % kRing) * 32u, tg, tu, ph, pv);
-                if (tg == lpp + 1 && tu == lpp + 1) {
-                    const uint32_t vs[4] = {pv.x, pv.y, pv.z, pv.w};
+                uint4 ph, pg;
+                ring_read1(ring_base + (lpp % kRing) * 32u, ph, pg);
+                if (ph.x == lpp + 1 && (CPW < 4 || pg.x == lpp + 1)) {
+                    uint32_t vs[CPW];
+                    slot_vals<CPW>(ph, pg, vs);
 #pragma unroll
                     for (int k = 0; k < CPW; k++) r[k] = max(r[k], vs[k] & mask);
                     ok = true;
-                } else if (max(tg, tu) > lpp + 1) {
+                } else if (ph.x > lpp + 1 || (CPW == 4 && pg.x > lpp + 1)) {
                     if (round_done(sh.stored, lpp)) old = true;
                     else __hip_atomic_store(&sh.req, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
@@ -682,10 +690,7 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
                 if (valid[k] && col[k] == br)
                     __hip_atomic_store(reinterpret_cast<uint64_t *>(brc + k * KB + seq % KB),
                                        ((uint64_t)e << 32) | seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            uint32_t o[4] = {0, 0, 0, 0};
-#pragma unroll
-            for (int k = 0; k < CPW; k++) o[k] = r[k];
-            ring_publish(ring_base + (lp % kRing) * 32u, lp + 1, prev, br, seq, make_uint4(o[0], o[1], o[2], o[3]));
+            ring_publish<CPW>(ring_base + (lp % kRing) * 32u, lp + 1, r);
             lp += E;
             have = false;
             c_done++;
@@ -712,18 +717,11 @@ static hipError_t launch_index_t(const IndexArgs &a0, hipStream_t s) {
     return hipGetLastError();
 }
 
-template <int CPW, int NCW>
-static hipError_t launch_index_n(const IndexArgs &a, hipStream_t s) {
-    constexpr int RRMIN = 64 * NCW;
-    if (a.rr_hint >= 512 || RRMIN > 256) return launch_index_t<CPW, NCW, (RRMIN > 512 ? RRMIN : 512)>(a, s);
-    return launch_index_t<CPW, NCW, (RRMIN > 256 ? RRMIN : 256)>(a, s);
-}
-
 template <int CPW>
 static hipError_t launch_index_c(const IndexArgs &a, uint32_t ncw, hipStream_t s) {
-    if (ncw <= 1) return launch_index_n<CPW, 1>(a, s);
-    if (ncw <= 2) return launch_index_n<CPW, 2>(a, s);
-    return launch_index_n<CPW, 4>(a, s);
+    if (ncw <= 1) return launch_index_t<CPW, 1, 1024>(a, s);
+    if (ncw <= 2) return launch_index_t<CPW, 2, 1024>(a, s);
+    return launch_index_t<CPW, 4, 1024>(a, s);
 }
 
 hipError_t launch_index(const IndexArgs &a, hipStream_t s) {
