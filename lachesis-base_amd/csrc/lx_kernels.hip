@@ -553,40 +553,63 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
     }
 
     // ---------------------------------------------------------------- compute
+    // Straight-line pass: every lane runs the same sequence and state changes
+    // are selects, so a pass costs the same few hundred instructions whatever
+    // mix of lanes is fetching, folding or completing; rare cases sit behind
+    // wave-uniform branches.
     uint32_t c_pass = 0, c_chunk = 0, c_done = 0, c_slow = 0, c_wm = 0, c_norec = 0;
     const unsigned long long t_start = wall_clock64();
 
     uint32_t lp = threadIdx.x;
     bool have = false;
-    uint32_t br = 0, seq = 0, np = 0, xi = 0;
+    uint32_t br = 0, seq = 0, np = 0, xi = LX_MAXP;
     uint32_t par[LX_MAXP];
+#pragma unroll
+    for (int j = 0; j < LX_MAXP; j++) par[j] = 0;
     uint32_t todo = 0;   // pending parents (bit j = par[j])
     uint32_t cc = 0;     // chunk folded next
     uint32_t r[CPW];
+#pragma unroll
+    for (int k = 0; k < CPW; k++) r[k] = 0;
+    const uint32_t dummy = lds_addr(&sh.req) & ~7u;   // harmless target of masked-off brc writes (never read as brc)
+    (void)dummy;
 
-    while (lp < n) {
+    while (!__all(lp >= n)) {
         c_pass++;
-        if (!have) {
+        // A: fetch the record of the next event (lanes without one)
+        {
             const uint32_t slot = lp % RR;
-            if (__hip_atomic_load(&rtag[slot], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != lp + 1) { c_norec++; continue; }
-            const uint4 *rq = rrec + slot * RQ;
-            const uint4 q0 = rq[0];
-            br = q0.x; seq = q0.y; np = q0.z;
+            const uint32_t t = __hip_atomic_load(&rtag[slot], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const bool got = !have && lp < n && t == lp + 1;
+            c_norec += (!have && lp < n && !got) ? 1u : 0u;
+            if (__any(got)) {
+                const uint4 *rq = rrec + slot * RQ;
+                const uint4 q0 = rq[0];
+                uint4 q[LX_MAXP / 4];
 #pragma unroll
-            for (int j = 0; j < LX_MAXP / 4; j++) {
-                const uint4 q = rq[1 + j];
-                par[4 * j] = q.x - bs; par[4 * j + 1] = q.y - bs; par[4 * j + 2] = q.z - bs; par[4 * j + 3] = q.w - bs;
+                for (int j = 0; j < LX_MAXP / 4; j++) q[j] = rq[1 + j];
+                br = got ? q0.x : br;
+                seq = got ? q0.y : seq;
+                np = got ? q0.z : np;
+#pragma unroll
+                for (int j = 0; j < LX_MAXP / 4; j++) {
+                    par[4 * j] = got ? q[j].x - bs : par[4 * j];
+                    par[4 * j + 1] = got ? q[j].y - bs : par[4 * j + 1];
+                    par[4 * j + 2] = got ? q[j].z - bs : par[4 * j + 2];
+                    par[4 * j + 3] = got ? q[j].w - bs : par[4 * j + 3];
+                }
+                const uint32_t init = (q0.z >= LX_MAXP) ? ((1u << LX_MAXP) - 1u) : ((1u << q0.z) - 1u);
+                todo = got ? init : todo;
+                cc = got ? 0u : cc;
+                xi = got ? (uint32_t)LX_MAXP : xi;
+#pragma unroll
+                for (int k = 0; k < CPW; k++) r[k] = got ? ((col[k] == q0.x) ? q0.y : 0u) : r[k];
+                have = have || got;
             }
-            todo = (np >= LX_MAXP) ? ((1u << LX_MAXP) - 1u) : ((1u << np) - 1u);
-            cc = 0;
-            xi = LX_MAXP;
-#pragma unroll
-            for (int k = 0; k < CPW; k++) r[k] = (col[k] == br) ? seq : 0u;
-            have = true;
         }
-        if (todo) {
-            // fold chunk cc (parents 4cc..4cc+3)
-            c_chunk++;
+        // B: fold chunk cc (parents 4cc..4cc+3) of every lane with pending parents
+        if (__any(todo != 0)) {
+            c_chunk += todo ? 1u : 0u;
             uint32_t p4[4];
 #pragma unroll
             for (int j = 0; j < 4; j++) {
@@ -601,7 +624,6 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
             const uint32_t a2 = ring_base + (p4[2] % kRing) * 32u, a3 = ring_base + (p4[3] % kRing) * 32u;
             if (CPW == 4) ring_read4b(a0, a1, a2, a3, h, g);
             else ring_read4a(a0, a1, a2, a3, h);
-            // branch-free common case: fold the parents whose slot is valid
             uint32_t okm = 0, oldm = 0;
 #pragma unroll
             for (int j = 0; j < 4; j++) {
@@ -623,7 +645,7 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
                 oldm |= old << j;
             }
             uint32_t tn = tc & ~okm;
-            if (oldm) {
+            if (__any(oldm != 0)) {
                 // older than the ring or an earlier batch: HB row from L2 once stored
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
@@ -644,56 +666,63 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
             }
             todo = (todo & ~(15u << (4 * cc))) | (tn << (4 * cc));
             // next chunk: cyclically after cc, among the chunks still pending
+            constexpr uint32_t NCH = LX_MAXP / 4;
             uint32_t pm = 0;
 #pragma unroll
-            for (int c = 0; c < LX_MAXP / 4; c++) pm |= (uint32_t)(((todo >> (4 * c)) & 15u) != 0) << c;
-            constexpr uint32_t NCH = LX_MAXP / 4;
+            for (int c = 0; c < (int)NCH; c++) pm |= (uint32_t)(((todo >> (4 * c)) & 15u) != 0) << c;
             const uint32_t rot = ((pm | (pm << NCH)) >> (cc + 1)) & ((1u << NCH) - 1u);
             cc = rot ? (cc + 1 + (uint32_t)__builtin_ctz(rot)) % NCH : cc;
-            if (todo) continue;
         }
-        if (xi < np) {
-            // parents beyond the inline LX_MAXP (rare): one per pass, from the ring or L2
-            const uint32_t p = ld_l2_now(a.par_in + a.poff_in[lp] + xi);
-            const uint32_t lpp = p - bs;
-            bool ok = false, old = lpp >= n;
-            if (!old) {
-                uint4 ph, pg;
-                ring_read1(ring_base + (lpp % kRing) * 32u, ph, pg);
-                if (ph.x == lpp + 1 && (CPW < 4 || pg.x == lpp + 1)) {
-                    uint32_t vs[CPW];
-                    slot_vals<CPW>(ph, pg, vs);
+        // C: parents beyond the inline LX_MAXP (rare): one per pass, from the ring or L2
+        if (__any(have && todo == 0 && xi < np)) {
+            if (have && todo == 0 && xi < np) {
+                const uint32_t p = ld_l2_now(a.par_in + a.poff_in[lp] + xi);
+                const uint32_t lpp = p - bs;
+                bool ok = false, old = lpp >= n;
+                if (!old) {
+                    uint4 ph, pg;
+                    ring_read1(ring_base + (lpp % kRing) * 32u, ph, pg);
+                    if (ph.x == lpp + 1 && (CPW < 4 || pg.x == lpp + 1)) {
+                        uint32_t vs[CPW];
+                        slot_vals<CPW>(ph, pg, vs);
 #pragma unroll
-                    for (int k = 0; k < CPW; k++) r[k] = max(r[k], vs[k] & mask);
-                    ok = true;
-                } else if (ph.x > lpp + 1 || (CPW == 4 && pg.x > lpp + 1)) {
-                    if (round_done(sh.stored, lpp)) old = true;
-                    else __hip_atomic_store(&sh.req, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        for (int k = 0; k < CPW; k++) r[k] = max(r[k], vs[k] & mask);
+                        ok = true;
+                    } else if (ph.x > lpp + 1 || (CPW == 4 && pg.x > lpp + 1)) {
+                        if (round_done(sh.stored, lpp)) old = true;
+                        else __hip_atomic_store(&sh.req, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
                 }
-            }
-            if (old) {
-                const uint32_t *row = a.hb + (uint64_t)p * stride;
+                if (old) {
+                    const uint32_t *row = a.hb + (uint64_t)p * stride;
 #pragma unroll
-                for (int k = 0; k < CPW; k++)
-                    if (valid[k]) r[k] = max(r[k], ld_l2_now(row + col[k]) & mask);
-                ok = true;
+                    for (int k = 0; k < CPW; k++)
+                        if (valid[k]) r[k] = max(r[k], ld_l2_now(row + col[k]) & mask);
+                    ok = true;
+                }
+                if (ok) xi++;
             }
-            if (ok) xi++;
-            continue;
         }
+        // D: complete (the slot's previous occupant, lp - kRing, must be drained)
         {
-            // complete: the slot's previous occupant (lp - kRing) must be drained
-            if (lp >= (uint32_t)kRing && !round_done(sh.copied, lp - kRing)) { c_wm++; continue; }
-            const uint32_t e = bs + lp;
+            bool fin = have && todo == 0 && xi >= np;
+            if (__any(fin)) {
+                const bool reuse_ok = lp < (uint32_t)kRing || round_done(sh.copied, lp - kRing);
+                c_wm += (fin && !reuse_ok) ? 1u : 0u;
+                fin = fin && reuse_ok;
+                if (fin) {
+                    const uint32_t e = bs + lp;
 #pragma unroll
-            for (int k = 0; k < CPW; k++)
-                if (valid[k] && col[k] == br)
-                    __hip_atomic_store(reinterpret_cast<uint64_t *>(brc + k * KB + seq % KB),
-                                       ((uint64_t)e << 32) | seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            ring_publish<CPW>(ring_base + (lp % kRing) * 32u, lp + 1, r);
-            lp += E;
-            have = false;
-            c_done++;
+                    for (int k = 0; k < CPW; k++)
+                        if (valid[k] && col[k] == br)
+                            __hip_atomic_store(reinterpret_cast<uint64_t *>(brc + k * KB + seq % KB),
+                                               ((uint64_t)e << 32) | seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    ring_publish<CPW>(ring_base + (lp % kRing) * 32u, lp + 1, r);
+                }
+                c_done += fin ? 1u : 0u;
+                lp = fin ? lp + E : lp;
+                have = have && !fin;
+            }
         }
     }
     if (a.prof) {
