@@ -250,7 +250,7 @@ int ensure_batch(lx_index *h, uint64_t n, uint64_t npar) {
         if (h->b_poff) (void)hipFree(h->b_poff);
         HIPCHK(h, dalloc(&h->b_poff, cap + 1));
         if (h->b_rec) (void)hipFree(h->b_rec);
-        HIPCHK(h, dalloc(&h->b_rec, cap));
+        HIPCHK(h, dalloc(&h->b_rec, (cap + 63) / 64 * 64));   // whole 64-record rounds (round-blocked SoA)
         size_t sb = 0;
         HIPCHK(h, lx::scan_tmp_bytes((uint32_t)cap, &sb));
         if (h->scan_tmp) (void)hipFree(h->scan_tmp);
@@ -447,6 +447,9 @@ int add_batch_dev(lx_index *h, uint32_t n, const uint32_t *creator, const uint32
             fprintf(stderr, "[lx_prof] wave %d: wall_us=%.0f wave_passes=%.0f lane: pass=%.0f spin=%.0f chunk=%.0f done=%.0f slow=%.0f fill=%.0f wm=%.0f norec=%.0f  ns/pass=%.1f\n",
                     w, q[9] / nb / 100.0, q[8] / nb, q[0] / nb, q[1] / nb, q[2] / nb, q[3] / nb, q[4] / nb, q[5] / nb, q[6] / nb,
                     q[7] / nb, q[9] * 10.0 / (q[8] > 0 ? q[8] : 1));
+            if (q[14] > 0)
+                fprintf(stderr, "[lx_prof] wave %d cycles/pass: fetch=%.0f fold=%.0f ovf=%.0f complete=%.0f total=%.0f\n", w,
+                        q[10] / q[8], q[11] / q[8], q[12] / q[8], q[13] / q[8], q[14] / q[8]);
         }
     }
     if (h->B > h->V && h->n_cheat) {

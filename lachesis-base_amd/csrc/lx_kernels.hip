@@ -205,16 +205,18 @@ __global__ void k_finalize(BatchArgs a) {
             w[j] = max(x, y);
         }
     }
-    EventRec r;
-    r.q[0] = make_uint4(br, s, np, prev);
+    // round-blocked SoA: record e's q-th 16 B at [e/64][q][e%64], so 64
+    // consecutive records form one contiguous 4-KB block (one LDS-DMA round)
+    // and a wave reading field q of 64 consecutive records is conflict-free
+    uint4 *rq = reinterpret_cast<uint4 *>(a.rec) + (uint64_t)(e / 64) * 64 * LX_REC_Q + (e % 64);
+    rq[0] = make_uint4(br, s, np, prev);
 #pragma unroll
     for (int k = 0; k < LX_MAXP / 4; k++) {
         uint32_t v[4];
 #pragma unroll
         for (int t = 0; t < 4; t++) v[t] = (4 * k + t < (int)np) ? w[4 * k + t] : LX_NONE;
-        r.q[1 + k] = make_uint4(v[0], v[1], v[2], v[3]);
+        rq[64 * (1 + k)] = make_uint4(v[0], v[1], v[2], v[3]);
     }
-    a.rec[e] = r;
 }
 
 hipError_t launch_batch_finish(const BatchArgs &a, hipStream_t s) {
@@ -235,26 +237,33 @@ hipError_t launch_batch_finish(const BatchArgs &a, hipStream_t s) {
 // least one pass of the compute loop, so the compute waves do only what the
 // critical path needs -- fold parents, publish -- and the rest runs beside them.
 // Roles (NCW compute waves + 1 loader + kND drain waves):
-//  * loader: streams the 64-B event records into an LDS record ring by LDS-DMA
-//    (global_load_lds_dwordx4, up to 8 rounds of 64 in flight) and publishes
-//    each slot with a tag after its own vmcnt wait;
+//  * loader: streams 64-B event records (round-blocked SoA, one 4-KB block per
+//    64 events) into an LDS record ring by LDS-DMA (global_load_lds_dwordx4,
+//    up to 8 rounds in flight) and publishes each round with a tag after its
+//    own vmcnt wait;
 //  * compute lane g handles events g, g+E, ... (E = 64*NCW).  Each pass it
 //    folds ONE chunk of 4 parents, cycling over the chunks that still have
-//    pending parents (so a parent that completes late stalls only its own
-//    chunk), then publishes its CPW seqs into a 32-B slot of the LDS event
-//    ring.  No global access on the hot path;
+//    pending parents (a parent that completes late stalls only its own
+//    chunk), then publishes its CPW seqs into a slot of the LDS event ring.
+//    No global access on the hot path;
 //  * drain waves (rounds of 64 events, round r on wave r % kND): store the HB
 //    row and do the LowestAfter range fill, reading RAW(prev) from the ring.
-// Slots are two 16-B halves {tag, seq0, seq1, seq2}, {tag, seq3, -, -}; one
-// lane's ds_read_b128 / ds_write_b128 is a single LDS access, so a half whose
-// tag matches is consistent, and a slot is valid when every half it needs
-// matches.  A tag above the expected one means the slot was reused: that
-// parent's HB row is read from L2 once its drain reports it stored (rare:
-// parents older than the ring, or from an earlier batch).  Lanes never block
-// inside a pass, so dependencies between lanes of one wave cannot deadlock;
-// drains wait only for older events and keep publishing their own progress.
-constexpr int kRing = 2048;          // event slots, 32 B each (64 KB)
+// Slots carry their event tag next to the seqs in one 8-B (CPW 1) or 16-B
+// (CPW 2) unit, or two 16-B units in separate arrays (CPW 4: {tag, s0, s1, s2},
+// {tag, s3}); one lane's ds_read/ds_write of such a unit is a single LDS
+// access, so a unit whose tag matches is consistent.  A tag above the
+// expected one means the slot was reused: that parent's HB row is read from
+// L2 once its drain reports it stored (rare: parents older than the ring, or
+// from an earlier batch).  Lanes never block inside a pass, so dependencies
+// between lanes of one wave cannot deadlock; drains wait only for older events
+// and keep publishing their own progress.
 constexpr int kND = 2;               // drain waves
+
+template <int CPW>
+struct Ring {
+    static constexpr int N = CPW == 1 ? 8192 : CPW == 2 ? 4096 : 2048;   // slots (64 KB)
+    static constexpr int UNIT = CPW == 1 ? 8 : 16;                        // bytes per unit
+};
 
 struct WalkShared {
     uint32_t copied[kND];    // rounds drained (ring and record data consumed) per drain wave
@@ -268,86 +277,110 @@ __device__ __forceinline__ bool round_done(const uint32_t *cnt, uint32_t ev) {
 }
 
 typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+typedef uint32_t u2v __attribute__((ext_vector_type(2)));
 
-__device__ __forceinline__ uint4 to4(u4v x) { return make_uint4(x.x, x.y, x.z, x.w); }
-
-// first halves of 4 slots (CPW <= 3)
-__device__ __forceinline__ void ring_read4a(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3, uint4 h[4]) {
-    u4v x0, x1, x2, x3;
-    asm volatile(
-        "ds_read_b128 %0, %4\n\t"
-        "ds_read_b128 %1, %5\n\t"
-        "ds_read_b128 %2, %6\n\t"
-        "ds_read_b128 %3, %7\n\t"
-        "s_waitcnt lgkmcnt(0)"
-        : "=&v"(x0), "=&v"(x1), "=&v"(x2), "=&v"(x3)
-        : "v"(a0), "v"(a1), "v"(a2), "v"(a3)
-        : "memory");
-    h[0] = to4(x0); h[1] = to4(x1); h[2] = to4(x2); h[3] = to4(x3);
-}
-
-// both halves of 4 slots (CPW == 4)
-__device__ __forceinline__ void ring_read4b(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3, uint4 h[4], uint4 g[4]) {
-    u4v x0, x1, x2, x3, y0, y1, y2, y3;
-    asm volatile(
-        "ds_read_b128 %0, %8\n\t"
-        "ds_read_b128 %4, %8 offset:16\n\t"
-        "ds_read_b128 %1, %9\n\t"
-        "ds_read_b128 %5, %9 offset:16\n\t"
-        "ds_read_b128 %2, %10\n\t"
-        "ds_read_b128 %6, %10 offset:16\n\t"
-        "ds_read_b128 %3, %11\n\t"
-        "ds_read_b128 %7, %11 offset:16\n\t"
-        "s_waitcnt lgkmcnt(0)"
-        : "=&v"(x0), "=&v"(x1), "=&v"(x2), "=&v"(x3), "=&v"(y0), "=&v"(y1), "=&v"(y2), "=&v"(y3)
-        : "v"(a0), "v"(a1), "v"(a2), "v"(a3)
-        : "memory");
-    h[0] = to4(x0); h[1] = to4(x1); h[2] = to4(x2); h[3] = to4(x3);
-    g[0] = to4(y0); g[1] = to4(y1); g[2] = to4(y2); g[3] = to4(y3);
-}
-
-__device__ __forceinline__ void ring_read1(uint32_t a0, uint4 &h, uint4 &g) {
-    u4v x, y;
-    asm volatile(
-        "ds_read_b128 %0, %2\n\t"
-        "ds_read_b128 %1, %2 offset:16\n\t"
-        "s_waitcnt lgkmcnt(0)"
-        : "=&v"(x), "=&v"(y)
-        : "v"(a0)
-        : "memory");
-    h = to4(x);
-    g = to4(y);
-}
-
+// a slot as read: tag(s) and seqs
 template <int CPW>
-__device__ __forceinline__ void ring_publish(uint32_t addr, uint32_t tag, const uint32_t *r) {
-    u4v x;
-    x.x = tag; x.y = r[0]; x.z = CPW > 1 ? r[1 % CPW] : 0u; x.w = CPW > 2 ? r[2 % CPW] : 0u;
-    if (CPW == 4) {
-        u4v y;
-        y.x = tag; y.y = r[3 % CPW]; y.z = 0u; y.w = 0u;
+struct Slot {
+    uint32_t t0, t1;       // t1 = second unit's tag (CPW 4), else t0
+    uint32_t v[CPW];
+};
+
+// read 4 slots (A = first-unit array, B = second-unit array), issue all, wait once
+template <int CPW>
+__device__ __forceinline__ void ring_read4(uint32_t A, uint32_t B, const uint32_t s[4], Slot<CPW> o[4]) {
+    if (CPW == 1) {
+        u2v x0, x1, x2, x3;
         asm volatile(
-            "ds_write_b128 %0, %2 offset:16\n\t"
-            "ds_write_b128 %0, %1"
-            :
-            : "v"(addr), "v"(x), "v"(y)
+            "ds_read_b64 %0, %4\n\t"
+            "ds_read_b64 %1, %5\n\t"
+            "ds_read_b64 %2, %6\n\t"
+            "ds_read_b64 %3, %7\n\t"
+            "s_waitcnt lgkmcnt(0)"
+            : "=&v"(x0), "=&v"(x1), "=&v"(x2), "=&v"(x3)
+            : "v"(A + s[0] * 8u), "v"(A + s[1] * 8u), "v"(A + s[2] * 8u), "v"(A + s[3] * 8u)
             : "memory");
+        const u2v xs[4] = {x0, x1, x2, x3};
+#pragma unroll
+        for (int j = 0; j < 4; j++) { o[j].t0 = o[j].t1 = xs[j].x; o[j].v[0] = xs[j].y; }
+    } else if (CPW == 2) {
+        u4v x0, x1, x2, x3;
+        asm volatile(
+            "ds_read_b128 %0, %4\n\t"
+            "ds_read_b128 %1, %5\n\t"
+            "ds_read_b128 %2, %6\n\t"
+            "ds_read_b128 %3, %7\n\t"
+            "s_waitcnt lgkmcnt(0)"
+            : "=&v"(x0), "=&v"(x1), "=&v"(x2), "=&v"(x3)
+            : "v"(A + s[0] * 16u), "v"(A + s[1] * 16u), "v"(A + s[2] * 16u), "v"(A + s[3] * 16u)
+            : "memory");
+        const u4v xs[4] = {x0, x1, x2, x3};
+#pragma unroll
+        for (int j = 0; j < 4; j++) { o[j].t0 = o[j].t1 = xs[j].x; o[j].v[0] = xs[j].y; o[j].v[1 % CPW] = xs[j].z; }
     } else {
-        asm volatile("ds_write_b128 %0, %1" : : "v"(addr), "v"(x) : "memory");
+        u4v x0, x1, x2, x3, y0, y1, y2, y3;
+        asm volatile(
+            "ds_read_b128 %0, %8\n\t"
+            "ds_read_b128 %4, %12\n\t"
+            "ds_read_b128 %1, %9\n\t"
+            "ds_read_b128 %5, %13\n\t"
+            "ds_read_b128 %2, %10\n\t"
+            "ds_read_b128 %6, %14\n\t"
+            "ds_read_b128 %3, %11\n\t"
+            "ds_read_b128 %7, %15\n\t"
+            "s_waitcnt lgkmcnt(0)"
+            : "=&v"(x0), "=&v"(x1), "=&v"(x2), "=&v"(x3), "=&v"(y0), "=&v"(y1), "=&v"(y2), "=&v"(y3)
+            : "v"(A + s[0] * 16u), "v"(A + s[1] * 16u), "v"(A + s[2] * 16u), "v"(A + s[3] * 16u),
+              "v"(B + s[0] * 16u), "v"(B + s[1] * 16u), "v"(B + s[2] * 16u), "v"(B + s[3] * 16u)
+            : "memory");
+        const u4v xs[4] = {x0, x1, x2, x3};
+        const u4v ys[4] = {y0, y1, y2, y3};
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            o[j].t0 = xs[j].x; o[j].t1 = ys[j].x;
+            o[j].v[0] = xs[j].y; o[j].v[1 % CPW] = xs[j].z; o[j].v[2 % CPW] = xs[j].w; o[j].v[3 % CPW] = ys[j].y;
+        }
     }
 }
 
-// slot seqs of a valid slot
 template <int CPW>
-__device__ __forceinline__ void slot_vals(const uint4 &h, const uint4 &g, uint32_t *o) {
-    o[0] = h.y;
-    if (CPW > 1) o[1 % CPW] = h.z;
-    if (CPW > 2) o[2 % CPW] = h.w;
-    if (CPW > 3) o[3 % CPW] = g.y;
+__device__ __forceinline__ void ring_read1(uint32_t A, uint32_t B, uint32_t s, Slot<CPW> &o) {
+    uint32_t ss[4] = {s, s, s, s};
+    Slot<CPW> t[4];
+    ring_read4<CPW>(A, B, ss, t);
+    o = t[0];
+}
+
+template <int CPW>
+__device__ __forceinline__ void ring_publish(uint32_t A, uint32_t B, uint32_t s, uint32_t tag, const uint32_t *r) {
+    if (CPW == 1) {
+        u2v x;
+        x.x = tag; x.y = r[0];
+        asm volatile("ds_write_b64 %0, %1" : : "v"(A + s * 8u), "v"(x) : "memory");
+    } else if (CPW == 2) {
+        u4v x;
+        x.x = tag; x.y = r[0]; x.z = r[1 % CPW]; x.w = 0u;
+        asm volatile("ds_write_b128 %0, %1" : : "v"(A + s * 16u), "v"(x) : "memory");
+    } else {
+        u4v x, y;
+        x.x = tag; x.y = r[0]; x.z = r[1 % CPW]; x.w = r[2 % CPW];
+        y.x = tag; y.y = r[3 % CPW]; y.z = 0u; y.w = 0u;
+        asm volatile(
+            "ds_write_b128 %0, %2\n\t"
+            "ds_write_b128 %1, %3"
+            :
+            : "v"(A + s * 16u), "v"(B + s * 16u), "v"(x), "v"(y)
+            : "memory");
+    }
 }
 
 __device__ __forceinline__ uint32_t lds_addr(const void *p) {
     return (uint32_t)(uintptr_t)p;
+}
+
+// field q of the record in record-ring slot `slot` (round-blocked SoA)
+__device__ __forceinline__ uint32_t rec_off(uint32_t slot, uint32_t q) {
+    return (slot & ~63u) * LX_REC_Q + q * 64u + (slot & 63u);
 }
 
 template <int CPW, int NCW, int RR, bool FILL>
@@ -357,11 +390,12 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
     constexpr int E = 64 * NCW;
     constexpr int RQ = LX_REC_Q;
     constexpr int KB = 1024 / CPW;               // recent (seq -> event) entries per owned branch
-    static_assert(kRing % E == 0 && kRing / E >= 4, "ring slot reuse must stay within one lane");
+    constexpr int RN = Ring<CPW>::N;
+    static_assert(RN % E == 0 && RN / E >= 4, "ring slot reuse must stay within one lane");
     static_assert(RR % 64 == 0 && RR / 64 >= 4 && RR >= 2 * E, "record ring");
-    __shared__ uint4 ring[kRing * 2];            // slot s: ring[2s], ring[2s+1]
+    __shared__ uint4 ring[4096];                 // 64 KB: slot units (A array, then B array for CPW 4)
     __shared__ uint4 rrec[RR * RQ];              // event records
-    __shared__ uint32_t rtag[RR];
+    __shared__ uint32_t rtag[RR / 64];           // per record round: batch round index + 1
     __shared__ uint2 brc[CPW * KB];              // {seq, event} of recent events of owned branches
     __shared__ WalkShared sh;
 
@@ -369,8 +403,8 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
     const uint32_t slice = (w % 8) * a.slices_per_xcd + (w / 8);   // XCD-aware: neighbouring slices share an L2
     if (slice >= a.n_slices) return;
 
-    for (int i = threadIdx.x; i < kRing * 2; i += NT) ring[i] = make_uint4(0, 0, 0, 0);
-    for (int i = threadIdx.x; i < RR; i += NT) rtag[i] = 0;
+    for (int i = threadIdx.x; i < 4096; i += NT) ring[i] = make_uint4(0, 0, 0, 0);
+    for (int i = threadIdx.x; i < RR / 64; i += NT) rtag[i] = 0;
     for (int i = threadIdx.x; i < CPW * KB; i += NT) brc[i] = make_uint2(0, LX_NONE);
     if (threadIdx.x < kND) { sh.copied[threadIdx.x] = 0; sh.stored[threadIdx.x] = 0; }
     if (threadIdx.x == 0) sh.req = 0;
@@ -382,7 +416,8 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
     const int lane = threadIdx.x % 64;
     const uint64_t stride = a.stride;
     const uint32_t mask = a.mask ? LX_SEQ_MASK : 0xFFFFFFFFu;
-    const uint32_t ring_base = lds_addr(ring);
+    const uint32_t RA = lds_addr(ring);
+    const uint32_t RB = RA + (uint32_t)(RN * 16);   // second units (CPW 4 only)
 
     uint32_t col[CPW], first[CPW];
     bool valid[CPW];
@@ -403,22 +438,19 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
         constexpr uint32_t D = RR / 64 < 8 ? RR / 64 : 8;
         uint32_t issued = 0, done = 0;
         const char *recb = reinterpret_cast<const char *>(a.rec);
-        const uint64_t rec_bytes = (uint64_t)n * sizeof(EventRec);
         while (done < nrounds) {
             bool progressed = false;
             // a round's record slots are free once the drain consumed their
-            // previous occupants (events ev - RR: same round offset, wave-uniform)
+            // previous occupants (events ev - RR: same round offset)
             if (issued < nrounds && issued - done < D &&
                 (issued * 64 < (uint32_t)RR || round_done(sh.copied, issued * 64 - RR))) {
                 const uint32_t s0 = (issued * 64) % RR;
                 char *dst = reinterpret_cast<char *>(rrec) + (uint64_t)s0 * sizeof(EventRec);
                 const uint64_t base = (uint64_t)issued * 64 * sizeof(EventRec);
 #pragma unroll
-                for (int i = 0; i < RQ; i++) {
-                    uint64_t off = base + (uint64_t)(i * 64 + lane) * 16;
-                    if (off + 16 > rec_bytes) off = 0;   // tail of the last round: harmless filler
-                    __builtin_amdgcn_global_load_lds((const void *)(recb + off), (void *)(dst + i * 1024), 16, 0, 0);
-                }
+                for (int i = 0; i < RQ; i++)
+                    __builtin_amdgcn_global_load_lds((const void *)(recb + base + (uint64_t)(i * 64 + lane) * 16),
+                                                     (void *)(dst + i * 1024), 16, 0, 0);
                 issued++;
                 progressed = true;
             }
@@ -434,8 +466,7 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
                     case 6: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
                     default: asm volatile("s_waitcnt vmcnt(28)" ::: "memory"); break;
                 }
-                const uint32_t ev = done * 64 + lane;
-                if (ev < n) __hip_atomic_store(&rtag[ev % RR], ev + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (lane == 0) __hip_atomic_store(&rtag[done % (RR / 64)], done + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                 done++;
             } else if (!progressed) {
                 __builtin_amdgcn_s_sleep(1);
@@ -450,14 +481,15 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
         uint32_t nd = 0;                 // rounds of this wave completed
         for (uint32_t R = d; R * 64 < n; R += kND, nd++) {
             const uint32_t ev = R * 64 + lane;
-            const uint32_t sa = ring_base + (ev % kRing) * 32u;
-            uint4 h = make_uint4(0, 0, 0, 0), g = make_uint4(0, 0, 0, 0);
+            const uint32_t sl = ev % RN;
+            Slot<CPW> me;
+            me.t0 = me.t1 = 0;
             // wait for the round (keep publishing progress: others may wait on it)
             while (true) {
                 bool ready = true;
                 if (ev < n) {
-                    ring_read1(sa, h, g);
-                    ready = h.x == ev + 1 && (CPW < 4 || g.x == ev + 1);
+                    ring_read1<CPW>(RA, RB, sl, me);
+                    ready = me.t0 == ev + 1 && me.t1 == ev + 1;
                 }
                 if (__all(ready)) break;
                 if (__hip_atomic_load(&sh.req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
@@ -466,11 +498,10 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
                 }
                 __builtin_amdgcn_s_sleep(1);
             }
-            uint32_t r[CPW], h0[CPW];
+            uint32_t h0[CPW];
             uint32_t prev = LX_NONE, br = 0, seq = 0;
             if (ev < n) {
-                slot_vals<CPW>(h, g, r);
-                const uint4 q0 = rrec[(ev % RR) * RQ];
+                const uint4 q0 = rrec[rec_off(ev % RR, 0)];
                 br = q0.x; seq = q0.y; prev = q0.w;
 #pragma unroll
                 for (int k = 0; k < CPW; k++) h0[k] = 0;
@@ -478,10 +509,11 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
                     const uint32_t pl = prev - bs;
                     bool got = false;
                     if (pl < n) {
-                        uint4 ph, pg;
-                        ring_read1(ring_base + (pl % kRing) * 32u, ph, pg);
-                        if (ph.x == pl + 1 && (CPW < 4 || pg.x == pl + 1)) {
-                            slot_vals<CPW>(ph, pg, h0);
+                        Slot<CPW> ps;
+                        ring_read1<CPW>(RA, RB, pl % RN, ps);
+                        if (ps.t0 == pl + 1 && ps.t1 == pl + 1) {
+#pragma unroll
+                            for (int k = 0; k < CPW; k++) h0[k] = ps.v[k];
                             got = true;
                         } else {
                             // reused slot: prev's row is (being) stored by a drain
@@ -509,6 +541,7 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
             // ring and record data of this round consumed: slots may be reused
             if (lane == 0) __hip_atomic_store(&sh.copied[d], nd + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             if (ev < n) {
+                const uint32_t *r = me.v;
                 // HB row (raw values incl. fork bits as published)
                 uint32_t *hrow = a.hb + (uint64_t)(bs + ev) * stride;
                 if (contig) {
@@ -553,99 +586,69 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
     }
 
     // ---------------------------------------------------------------- compute
-    // Straight-line pass: every lane runs the same sequence and state changes
-    // are selects, so a pass costs the same few hundred instructions whatever
-    // mix of lanes is fetching, folding or completing; rare cases sit behind
-    // wave-uniform branches.
     uint32_t c_pass = 0, c_chunk = 0, c_done = 0, c_slow = 0, c_wm = 0, c_norec = 0;
     const unsigned long long t_start = wall_clock64();
 
     uint32_t lp = threadIdx.x;
     bool have = false;
-    uint32_t br = 0, seq = 0, np = 0, xi = LX_MAXP;
+    uint32_t br = 0, seq = 0, np = 0, xi = 0;
     uint32_t par[LX_MAXP];
-#pragma unroll
-    for (int j = 0; j < LX_MAXP; j++) par[j] = 0;
     uint32_t todo = 0;   // pending parents (bit j = par[j])
     uint32_t cc = 0;     // chunk folded next
     uint32_t r[CPW];
-#pragma unroll
-    for (int k = 0; k < CPW; k++) r[k] = 0;
-    const uint32_t dummy = lds_addr(&sh.req) & ~7u;   // harmless target of masked-off brc writes (never read as brc)
-    (void)dummy;
+    uint32_t drained = 0;   // events < drained are known drained (slot reuse)
 
-    while (!__all(lp >= n)) {
+    while (lp < n) {
         c_pass++;
-        // A: fetch the record of the next event (lanes without one)
-        {
+        if (!have) {
             const uint32_t slot = lp % RR;
-            const uint32_t t = __hip_atomic_load(&rtag[slot], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            const bool got = !have && lp < n && t == lp + 1;
-            c_norec += (!have && lp < n && !got) ? 1u : 0u;
-            if (__any(got)) {
-                const uint4 *rq = rrec + slot * RQ;
-                const uint4 q0 = rq[0];
-                uint4 q[LX_MAXP / 4];
+            if (__hip_atomic_load(&rtag[slot / 64], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != lp / 64 + 1) { c_norec++; continue; }
+            const uint4 q0 = rrec[rec_off(slot, 0)];
+            br = q0.x; seq = q0.y; np = q0.z;
 #pragma unroll
-                for (int j = 0; j < LX_MAXP / 4; j++) q[j] = rq[1 + j];
-                br = got ? q0.x : br;
-                seq = got ? q0.y : seq;
-                np = got ? q0.z : np;
-#pragma unroll
-                for (int j = 0; j < LX_MAXP / 4; j++) {
-                    par[4 * j] = got ? q[j].x - bs : par[4 * j];
-                    par[4 * j + 1] = got ? q[j].y - bs : par[4 * j + 1];
-                    par[4 * j + 2] = got ? q[j].z - bs : par[4 * j + 2];
-                    par[4 * j + 3] = got ? q[j].w - bs : par[4 * j + 3];
-                }
-                const uint32_t init = (q0.z >= LX_MAXP) ? ((1u << LX_MAXP) - 1u) : ((1u << q0.z) - 1u);
-                todo = got ? init : todo;
-                cc = got ? 0u : cc;
-                xi = got ? (uint32_t)LX_MAXP : xi;
-#pragma unroll
-                for (int k = 0; k < CPW; k++) r[k] = got ? ((col[k] == q0.x) ? q0.y : 0u) : r[k];
-                have = have || got;
+            for (int j = 0; j < LX_MAXP / 4; j++) {
+                const uint4 q = rrec[rec_off(slot, 1 + j)];
+                par[4 * j] = q.x - bs; par[4 * j + 1] = q.y - bs; par[4 * j + 2] = q.z - bs; par[4 * j + 3] = q.w - bs;
             }
+            todo = (np >= LX_MAXP) ? ((1u << LX_MAXP) - 1u) : ((1u << np) - 1u);
+            cc = 0;
+            xi = LX_MAXP;
+#pragma unroll
+            for (int k = 0; k < CPW; k++) r[k] = (col[k] == br) ? seq : 0u;
+            have = true;
         }
-        // B: fold chunk cc (parents 4cc..4cc+3) of every lane with pending parents
-        if (__any(todo != 0)) {
-            c_chunk += todo ? 1u : 0u;
-            uint32_t p4[4];
+        if (todo) {
+            // fold chunk cc (parents 4cc..4cc+3)
+            c_chunk++;
+            uint32_t p4[4], sl4[4];
 #pragma unroll
             for (int j = 0; j < 4; j++) {
                 uint32_t x = par[j];
 #pragma unroll
                 for (int c = 1; c < LX_MAXP / 4; c++) x = (cc == (uint32_t)c) ? par[4 * c + j] : x;
                 p4[j] = x;
+                sl4[j] = x % RN;
             }
             const uint32_t tc = (todo >> (4 * cc)) & 15u;
-            uint4 h[4], g[4];
-            const uint32_t a0 = ring_base + (p4[0] % kRing) * 32u, a1 = ring_base + (p4[1] % kRing) * 32u;
-            const uint32_t a2 = ring_base + (p4[2] % kRing) * 32u, a3 = ring_base + (p4[3] % kRing) * 32u;
-            if (CPW == 4) ring_read4b(a0, a1, a2, a3, h, g);
-            else ring_read4a(a0, a1, a2, a3, h);
+            Slot<CPW> o[4];
+            ring_read4<CPW>(RA, RB, sl4, o);
+            // branch-free common case: fold the parents whose slot is valid
             uint32_t okm = 0, oldm = 0;
 #pragma unroll
             for (int j = 0; j < 4; j++) {
                 const uint32_t x = p4[j] + 1u;
                 const uint32_t pend = (tc >> j) & 1u;
                 const uint32_t inb = (uint32_t)(p4[j] < n);
-                uint32_t ok = pend & inb & (uint32_t)(h[j].x == x);
-                uint32_t newer = (uint32_t)(h[j].x > x);
-                if (CPW == 4) {
-                    ok &= (uint32_t)(g[j].x == x);
-                    newer |= (uint32_t)(g[j].x > x);
-                }
+                const uint32_t ok = pend & inb & (uint32_t)(o[j].t0 == x) & (uint32_t)(o[j].t1 == x);
+                const uint32_t newer = (uint32_t)(max(o[j].t0, o[j].t1) > x);
                 const uint32_t old = pend & ((inb ^ 1u) | newer);
-                uint32_t vs[CPW];
-                slot_vals<CPW>(h[j], g[j], vs);
 #pragma unroll
-                for (int k = 0; k < CPW; k++) r[k] = max(r[k], ok ? (vs[k] & mask) : 0u);
+                for (int k = 0; k < CPW; k++) r[k] = max(r[k], ok ? (o[j].v[k] & mask) : 0u);
                 okm |= ok << j;
                 oldm |= old << j;
             }
             uint32_t tn = tc & ~okm;
-            if (__any(oldm != 0)) {
+            if (oldm) {
                 // older than the ring or an earlier batch: HB row from L2 once stored
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
@@ -672,57 +675,51 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
             for (int c = 0; c < (int)NCH; c++) pm |= (uint32_t)(((todo >> (4 * c)) & 15u) != 0) << c;
             const uint32_t rot = ((pm | (pm << NCH)) >> (cc + 1)) & ((1u << NCH) - 1u);
             cc = rot ? (cc + 1 + (uint32_t)__builtin_ctz(rot)) % NCH : cc;
+            if (todo) continue;
         }
-        // C: parents beyond the inline LX_MAXP (rare): one per pass, from the ring or L2
-        if (__any(have && todo == 0 && xi < np)) {
-            if (have && todo == 0 && xi < np) {
-                const uint32_t p = ld_l2_now(a.par_in + a.poff_in[lp] + xi);
-                const uint32_t lpp = p - bs;
-                bool ok = false, old = lpp >= n;
-                if (!old) {
-                    uint4 ph, pg;
-                    ring_read1(ring_base + (lpp % kRing) * 32u, ph, pg);
-                    if (ph.x == lpp + 1 && (CPW < 4 || pg.x == lpp + 1)) {
-                        uint32_t vs[CPW];
-                        slot_vals<CPW>(ph, pg, vs);
+        if (xi < np) {
+            // parents beyond the inline LX_MAXP (rare): one per pass, from the ring or L2
+            const uint32_t p = ld_l2_now(a.par_in + a.poff_in[lp] + xi);
+            const uint32_t lpp = p - bs;
+            bool ok = false, old = lpp >= n;
+            if (!old) {
+                Slot<CPW> ps;
+                ring_read1<CPW>(RA, RB, lpp % RN, ps);
+                if (ps.t0 == lpp + 1 && ps.t1 == lpp + 1) {
 #pragma unroll
-                        for (int k = 0; k < CPW; k++) r[k] = max(r[k], vs[k] & mask);
-                        ok = true;
-                    } else if (ph.x > lpp + 1 || (CPW == 4 && pg.x > lpp + 1)) {
-                        if (round_done(sh.stored, lpp)) old = true;
-                        else __hip_atomic_store(&sh.req, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    }
-                }
-                if (old) {
-                    const uint32_t *row = a.hb + (uint64_t)p * stride;
-#pragma unroll
-                    for (int k = 0; k < CPW; k++)
-                        if (valid[k]) r[k] = max(r[k], ld_l2_now(row + col[k]) & mask);
+                    for (int k = 0; k < CPW; k++) r[k] = max(r[k], ps.v[k] & mask);
                     ok = true;
+                } else if (max(ps.t0, ps.t1) > lpp + 1) {
+                    if (round_done(sh.stored, lpp)) old = true;
+                    else __hip_atomic_store(&sh.req, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
-                if (ok) xi++;
             }
-        }
-        // D: complete (the slot's previous occupant, lp - kRing, must be drained)
-        {
-            bool fin = have && todo == 0 && xi >= np;
-            if (__any(fin)) {
-                const bool reuse_ok = lp < (uint32_t)kRing || round_done(sh.copied, lp - kRing);
-                c_wm += (fin && !reuse_ok) ? 1u : 0u;
-                fin = fin && reuse_ok;
-                if (fin) {
-                    const uint32_t e = bs + lp;
+            if (old) {
+                const uint32_t *row = a.hb + (uint64_t)p * stride;
 #pragma unroll
-                    for (int k = 0; k < CPW; k++)
-                        if (valid[k] && col[k] == br)
-                            __hip_atomic_store(reinterpret_cast<uint64_t *>(brc + k * KB + seq % KB),
-                                               ((uint64_t)e << 32) | seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    ring_publish<CPW>(ring_base + (lp % kRing) * 32u, lp + 1, r);
-                }
-                c_done += fin ? 1u : 0u;
-                lp = fin ? lp + E : lp;
-                have = have && !fin;
+                for (int k = 0; k < CPW; k++)
+                    if (valid[k]) r[k] = max(r[k], ld_l2_now(row + col[k]) & mask);
+                ok = true;
             }
+            if (ok) xi++;
+            continue;
+        }
+        {
+            // complete: the slot's previous occupant (lp - RN) must be drained
+            if (lp >= (uint32_t)RN && lp - RN >= drained) {
+                if (!round_done(sh.copied, lp - RN)) { c_wm++; continue; }
+                drained = ((lp - RN) | 63u) + 1;   // its whole round
+            }
+            const uint32_t e = bs + lp;
+#pragma unroll
+            for (int k = 0; k < CPW; k++)
+                if (valid[k] && col[k] == br)
+                    __hip_atomic_store(reinterpret_cast<uint64_t *>(brc + k * KB + seq % KB),
+                                       ((uint64_t)e << 32) | seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            ring_publish<CPW>(RA, RB, lp % RN, lp + 1, r);
+            lp += E;
+            have = false;
+            c_done++;
         }
     }
     if (a.prof) {
