@@ -99,6 +99,7 @@ struct lx_index {
     uint32_t cpw_hint = 0, ncw_hint = 0;   // LX_CPW / LX_NCW tuning overrides
     uint32_t rr_hint = 0, diag = 0;        // LX_RR record ring depth; LX_DIAG timing-only modes
     bool prof = false;                     // LX_PROF=1: per-wave walker counters to stderr
+    uint32_t small = 0;                    // LX_SMALL=1: small-LDS walker (several workgroups per CU)
     uint64_t last_npar = 0;                // parents in the current batch
 
     int fail(int code, const char *fmt, ...) {
@@ -412,6 +413,7 @@ int add_batch_dev(lx_index *h, uint32_t n, const uint32_t *creator, const uint32
     ia.cpw_hint = h->cpw_hint;
     ia.rr_hint = h->rr_hint;
     ia.diag = h->diag;
+    ia.small = h->small;
     ia.ncw_hint = h->ncw_hint;
     // antichain width of tdag-like DAGs ~ V / (1.6 P); P from the batch
     {
@@ -605,6 +607,7 @@ int lx_create(const lx_config *cfg, lx_index **out) {
     if (const char *d = getenv("LX_RR")) h->rr_hint = (uint32_t)atoi(d);
     if (const char *d = getenv("LX_DIAG")) h->diag = (uint32_t)atoi(d);
     if (const char *d = getenv("LX_PROF")) h->prof = (d[0] == '1');
+    if (const char *d = getenv("LX_SMALL")) h->small = (uint32_t)atoi(d);
     for (auto &e : h->ev)
         if (hipEventCreate(&e) != hipSuccess) {
             delete h;

@@ -53,6 +53,7 @@ struct IndexArgs {
     uint32_t rr_hint;            // record ring depth (LX_RR; 0 = auto)
     uint32_t diag;               // timing-only diagnostics (LX_DIAG): 2 no deps, 3 no global stores
     unsigned long long *prof;    // optional per-wave counters (LX_PROF=1), kProfSlots per wave
+    uint32_t small;              // small-LDS walker variant (LX_SMALL=1)
 };
 constexpr int kProfSlots = 16;   // see k_index: passes, spin misses, chunk folds, completes, ...
 

@@ -259,10 +259,12 @@ hipError_t launch_batch_finish(const BatchArgs &a, hipStream_t s) {
 // and keep publishing their own progress.
 constexpr int kND = 2;               // drain waves
 
-template <int CPW>
+template <int CPW, bool SMALL>
 struct Ring {
-    static constexpr int N = CPW == 1 ? 8192 : CPW == 2 ? 4096 : 2048;   // slots (64 KB)
-    static constexpr int UNIT = CPW == 1 ? 8 : 16;                        // bytes per unit
+    // slots: 64 KB of units, or 16 KB in the small-LDS variant (several
+    // workgroups per CU when each owns few columns)
+    static constexpr int BYTES = SMALL ? 16384 : 65536;
+    static constexpr int N = BYTES / (CPW == 1 ? 8 : 32);
 };
 
 struct WalkShared {
@@ -383,17 +385,18 @@ __device__ __forceinline__ uint32_t rec_off(uint32_t slot, uint32_t q) {
     return (slot & ~63u) * LX_REC_Q + q * 64u + (slot & 63u);
 }
 
-template <int CPW, int NCW, int RR, bool FILL>
+template <int CPW, int NCW, int RR, bool FILL, bool SMALL>
 __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
     static_assert(CPW == 1 || CPW == 2 || CPW == 4, "slot layout");
     constexpr int NT = 64 * (NCW + 1 + kND);
     constexpr int E = 64 * NCW;
     constexpr int RQ = LX_REC_Q;
-    constexpr int KB = 1024 / CPW;               // recent (seq -> event) entries per owned branch
-    constexpr int RN = Ring<CPW>::N;
+    constexpr int KB = (SMALL ? 512 : 1024) / CPW;   // recent (seq -> event) entries per owned branch
+    constexpr int RN = Ring<CPW, SMALL>::N;
+    constexpr int RB16 = Ring<CPW, SMALL>::BYTES / 16;
     static_assert(RN % E == 0 && RN / E >= 4, "ring slot reuse must stay within one lane");
     static_assert(RR % 64 == 0 && RR / 64 >= 4 && RR >= 2 * E, "record ring");
-    __shared__ uint4 ring[4096];                 // 64 KB: slot units (A array, then B array for CPW 4)
+    __shared__ uint4 ring[RB16];                 // slot units (A array, then B array for CPW 4)
     __shared__ uint4 rrec[RR * RQ];              // event records
     __shared__ uint32_t rtag[RR / 64];           // per record round: batch round index + 1
     __shared__ uint2 brc[CPW * KB];              // {seq, event} of recent events of owned branches
@@ -403,7 +406,7 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
     const uint32_t slice = (w % 8) * a.slices_per_xcd + (w / 8);   // XCD-aware: neighbouring slices share an L2
     if (slice >= a.n_slices) return;
 
-    for (int i = threadIdx.x; i < 4096; i += NT) ring[i] = make_uint4(0, 0, 0, 0);
+    for (int i = threadIdx.x; i < RB16; i += NT) ring[i] = make_uint4(0, 0, 0, 0);
     for (int i = threadIdx.x; i < RR / 64; i += NT) rtag[i] = 0;
     for (int i = threadIdx.x; i < CPW * KB; i += NT) brc[i] = make_uint2(0, LX_NONE);
     if (threadIdx.x < kND) { sh.copied[threadIdx.x] = 0; sh.stored[threadIdx.x] = 0; }
@@ -732,22 +735,29 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
     }
 }
 
-template <int CPW, int NCW, int RR>
+template <int CPW, int NCW, int RR, bool SMALL>
 static hipError_t launch_index_t(const IndexArgs &a0, hipStream_t s) {
     IndexArgs a = a0;
     a.n_slices = (a.ncols + CPW - 1) / CPW;
     a.slices_per_xcd = (a.n_slices + 7) / 8;
     uint32_t grid = a.slices_per_xcd * 8;
-    if (a.diag_nofill) hipLaunchKernelGGL((k_index<CPW, NCW, RR, false>), dim3(grid), dim3(64 * (NCW + 1 + kND)), 0, s, a);
-    else hipLaunchKernelGGL((k_index<CPW, NCW, RR, true>), dim3(grid), dim3(64 * (NCW + 1 + kND)), 0, s, a);
+    if (a.diag_nofill) hipLaunchKernelGGL((k_index<CPW, NCW, RR, false, SMALL>), dim3(grid), dim3(64 * (NCW + 1 + kND)), 0, s, a);
+    else hipLaunchKernelGGL((k_index<CPW, NCW, RR, true, SMALL>), dim3(grid), dim3(64 * (NCW + 1 + kND)), 0, s, a);
     return hipGetLastError();
 }
 
 template <int CPW>
 static hipError_t launch_index_c(const IndexArgs &a, uint32_t ncw, hipStream_t s) {
-    if (ncw <= 1) return launch_index_t<CPW, 1, 1024>(a, s);
-    if (ncw <= 2) return launch_index_t<CPW, 2, 1024>(a, s);
-    return launch_index_t<CPW, 4, 1024>(a, s);
+    if constexpr (CPW <= 2) {
+        if (a.small) {
+            // small-LDS variant (~37 KB): several workgroups share a CU
+            if (ncw <= 1) return launch_index_t<CPW, 1, 256, true>(a, s);
+            return launch_index_t<CPW, 2, 256, true>(a, s);
+        }
+    }
+    if (ncw <= 1) return launch_index_t<CPW, 1, 1024, false>(a, s);
+    if (ncw <= 2) return launch_index_t<CPW, 2, 1024, false>(a, s);
+    return launch_index_t<CPW, 4, 1024, false>(a, s);
 }
 
 hipError_t launch_index(const IndexArgs &a, hipStream_t s) {
