@@ -275,6 +275,32 @@ def test_config4_scaled(lx):
     np.testing.assert_array_equal(ix.forkless_cause_batch(qa, qb), o.forkless_cause_batch(qa, qb))
 
 
+def test_config4_full(lx):
+    """BASELINE configs[3] at full size: V=100, first 10 validators double-sign
+    (F=10 forks each), 1000 events per validator (100k events, ~157 branches):
+    bit-exact branch IDs, every 5th HB/LA/merged row and 300k FC vs the oracle;
+    indexed as one batch and as per-level-sized batches."""
+    d = lx.tools.gen_dag(100, 1000, 10, cheaters=10, forks=10, seed=2)
+    w = [1] * 100
+    o = oracle_for(d, w)
+    N = len(d)
+    qa, qb = lx.tools.fc_queries(d.lamport, 300_000, seed=5)
+    want = o.forkless_cause_batch(qa, qb)
+    for chunk in (N, 64):
+        ix = lx.Index(event_capacity=N)
+        ix.reset(w)
+        br = []
+        for lo in range(0, N, chunk):
+            hi = min(N, lo + chunk)
+            br.extend(int(x) for x in ix.add_batch(d.creator[lo:hi], d.seq[lo:hi], d.poff[lo:hi + 1], d.par,
+                                                   want_branches=True))
+        assert ix.num_branches() == o.num_branches() > 100
+        assert br == [o.branch(i) for i in range(N)]
+        compare_rows(ix, o, range(0, N, 5 if chunk == N else 97))
+        np.testing.assert_array_equal(ix.forkless_cause_batch(qa, qb), want)
+        ix.close()
+
+
 def test_config3_shape_skewed(lx):
     """BASELINE configs[2] shape: V=1000, Zipf weights floor(2^20/(i+1)), P=10,
     at 8 events per validator (8k events) vs the oracle."""
@@ -335,3 +361,33 @@ def test_full_size_properties_config2(lx):
         la = np.frombuffer(ix.lowest_after(int(b)), dtype=np.uint32)
         cnt = int(np.sum((la != 0) & (la <= hb[:len(la)])))
         assert bool(g) == (cnt >= ix.quorum())
+
+
+# ---------------------------------------------------------------- walker variants
+WALKER_VARIANTS = [
+    # environment read by lx_create: columns per workgroup, compute waves, small-LDS ring
+    {"LX_CPW": "1", "LX_NCW": "1"}, {"LX_CPW": "2", "LX_NCW": "2"}, {"LX_CPW": "4", "LX_NCW": "4"},
+    {"LX_CPW": "4", "LX_NCW": "1"}, {"LX_CPW": "1", "LX_NCW": "4"},
+    {"LX_SMALL": "1", "LX_CPW": "1", "LX_NCW": "1"}, {"LX_SMALL": "1", "LX_CPW": "2", "LX_NCW": "2"},
+]
+
+
+@pytest.mark.parametrize("env", WALKER_VARIANTS, ids=lambda e: "-".join("%s%s" % (k[3:].lower(), v) for k, v in e.items()))
+def test_walker_variants(lx, env, monkeypatch):
+    """Every walker configuration (slot layouts, ring sizes, wave counts) is bit-exact;
+    the DAG is long enough (6000 events, cheaters) that ring slots are reused and
+    parents older than the ring take the L2 path."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    d = lx.tools.gen_dag(24, 250, 6, 4, 6, 21)
+    weights = list(range(40, 16, -1))
+    o = oracle_for(d, weights)
+    ix = lx.Index()
+    ix.reset(weights)
+    br = ix.add_batch(d.creator, d.seq, d.poff, d.par, want_branches=True)
+    assert [int(x) for x in br] == [o.branch(i) for i in range(len(d))]
+    rng = np.random.default_rng(5)
+    compare_rows(ix, o, rng.choice(len(d), 1500, replace=False))
+    qa, qb = lx.tools.fc_queries(d.lamport, 200_000, window=32, seed=4)
+    np.testing.assert_array_equal(ix.forkless_cause_batch(qa, qb), o.forkless_cause_batch(qa, qb))
+    ix.close()
