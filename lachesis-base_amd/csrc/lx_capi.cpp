@@ -662,7 +662,11 @@ int lx_reset(lx_index *h, uint32_t nv, const uint32_t *w) {
         h->hwm = 0;
         if ((rc = grow_events(h, h->cap_hint ? h->cap_hint : 4096))) return rc;
     } else if (h->hwm) {
-        HIPCHK(h, hipMemsetAsync(h->hb, 0, h->hwm * h->stride * 4, h->stream));
+        // HB: the walker rewrites columns [0, V) of every new event's row (the
+        // original branches always exist); only the fork-branch columns can
+        // keep stale values for rows written before such a branch existed
+        if (h->stride > nv)
+            HIPCHK(h, hipMemset2DAsync(h->hb + nv, (size_t)h->stride * 4, 0, (size_t)(h->stride - nv) * 4, h->hwm, h->stream));
         HIPCHK(h, hipMemsetAsync(h->la, 0, h->hwm * h->stride * 4, h->stream));
         HIPCHK(h, lx::launch_fill_u32(h->first_child, h->hwm, LX_NONE, h->stream));
         h->hwm = 0;

@@ -391,3 +391,21 @@ def test_walker_variants(lx, env, monkeypatch):
     qa, qb = lx.tools.fc_queries(d.lamport, 200_000, window=32, seed=4)
     np.testing.assert_array_equal(ix.forkless_cause_batch(qa, qb), o.forkless_cause_batch(qa, qb))
     ix.close()
+
+
+def test_reset_reuses_planes(lx):
+    """lx_reset on a used handle (same layout) clears exactly what the next epoch
+    may read: epoch 1 dirties fork-branch columns, epoch 2 (different V, new
+    forks, more events) must still equal a fresh oracle bit for bit."""
+    ix = lx.Index()
+    for (n, ev, p, ch, fk, seed) in [(20, 120, 5, 5, 8, 31), (24, 150, 6, 6, 6, 32), (20, 40, 4, 3, 4, 33)]:
+        d = lx.tools.gen_dag(n, ev, p, ch, fk, seed)
+        w = list(range(60, 60 - n, -1))
+        o = oracle_for(d, w)
+        ix.reset(w)
+        ix.add_batch(d.creator, d.seq, d.poff, d.par)
+        assert ix.num_branches() == o.num_branches() > n
+        compare_rows(ix, o, range(len(d)))
+        qa, qb = lx.tools.fc_queries(d.lamport, 50_000, window=32, seed=seed)
+        np.testing.assert_array_equal(ix.forkless_cause_batch(qa, qb), o.forkless_cause_batch(qa, qb))
+    ix.close()
