@@ -49,6 +49,21 @@ CONFIGS = {
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
 
 
+def measured_traffic(config, fc_queries):
+    """HBM bytes per launch from the committed PMC profile of this workload
+    (profiles/r*/traffic_<config>.json, made by scripts/prof_traffic.sh: separate
+    FETCH_SIZE / WRITE_SIZE passes, gfx950 FETCH_SIZE doubled), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "traffic_%s.json" % config)))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        t = json.load(f)
+    if t.get("fc_queries") != fc_queries:
+        return None, None
+    return t["kernels"], os.path.relpath(files[-1], ROOT)
+
+
 def weights_for(V, kind):
     if kind == "zipf":
         return [(1 << 20) // (i + 1) for i in range(V)]
@@ -237,6 +252,9 @@ def main():
     idx_bytes = ((p_mean + 1) * 4 * B + 4 * B + 8) * N
     idx_achieved = idx_bytes / (kidx * 1e-3) / 1e9
 
+    traffic, traffic_src = measured_traffic(args.config, args.fc_queries)
+    if shard:
+        traffic = None   # the committed profile is of the single-GPU run
     result = {
         "metric": "events indexed/sec + ForklessCause queries/sec at 1000 validators, 1/2/4/8 GPU",
         "value": events_per_s,
@@ -260,9 +278,12 @@ def main():
         "assign_and_marks_ms": float(np.mean(k_assign_ms)),
         "roofline": {"bound": "hbm", "kernel": "k_fc (ForklessCause)", "achieved": fc_achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": fc_achieved / HBM_PEAK_GBS,
-                     "traffic": None, "algorithmic_bytes_per_launch": fc_bytes, "kernel_ms": fc_kernel_ms},
+                     "traffic": traffic["k_fc"]["hbm_bytes"] if traffic else None,
+                     "traffic_source": traffic_src,
+                     "algorithmic_bytes_per_launch": fc_bytes, "kernel_ms": fc_kernel_ms},
         "roofline_index": {"bound": "latency (DAG depth); hbm ceiling", "kernel": "k_index", "achieved": idx_achieved,
                            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": idx_achieved / HBM_PEAK_GBS,
+                           "traffic": traffic["k_index"]["hbm_bytes"] if traffic else None,
                            "algorithmic_bytes_per_launch": idx_bytes, "kernel_ms": kidx},
         "host_gen_s": t_gen,
     }
