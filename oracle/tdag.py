@@ -24,7 +24,7 @@ import re
 
 
 class Event:
-    __slots__ = ("id", "creator", "seq", "lamport", "parents", "name")
+    __slots__ = ("id", "creator", "seq", "lamport", "parents", "name", "frame", "epoch")
 
     def __init__(self, eid, creator, seq, lamport, parents, name=""):
         self.id = eid
@@ -33,6 +33,8 @@ class Event:
         self.lamport = lamport
         self.parents = list(parents)
         self.name = name
+        self.frame = 0        # consensus fields set by abft Build (inter/dag/event.go:20-24)
+        self.epoch = 0
 
     def self_parent(self):
         # inter/dag/event.go:87-92: parents[0] iff seq > 1
@@ -163,15 +165,20 @@ class SplitMix64:
 
 
 def rand_fork_dag(n_nodes, events_per_node, parent_count, cheaters=0,
-                  forks_count=0, seed=1, node_ids=None):
+                  forks_count=0, seed=1, node_ids=None, rng=None, build=None, eid_base=0):
     """Structure of tdag.ForEachRandFork (test_common.go:37-136).
 
     Node ``k`` (0-based generation column) is a cheater iff ``k < cheaters``.
     Other parents: ``parent_count-1`` distinct other nodes drawn by rejection
     sampling (stand-in for ``r.Perm(nodeCount)`` minus self).
+    ``build(e)`` (optional) mirrors the ForEachEvent.Build callback
+    (test_common.go:110-116): returning False drops the event (it is neither
+    kept as a parent nor returned).  ``rng`` lets several epochs share one
+    stream, as the reference's epoch tests share ``r``.
     Returns (node_ids, events_in_creation_order).
     """
-    rng = SplitMix64(seed)
+    if rng is None:
+        rng = SplitMix64(seed)
     if node_ids is None:
         node_ids = [k + 1 for k in range(n_nodes)]
     evs_by_node = [[] for _ in range(n_nodes)]
@@ -210,8 +217,10 @@ def rand_fork_dag(n_nodes, events_per_node, parent_count, cheaters=0,
                 parents.append(p.id)
                 if lamport <= p.lamport:
                     lamport = p.lamport + 1
-        e = Event(len(out), node_ids[me], seq, lamport, parents,
+        e = Event(eid_base + i, node_ids[me], seq, lamport, parents,
                   "%s%03d" % (chr(ord("a") + me) if me < 26 else "n%d_" % me, len(ee)))
+        if build is not None and build(e) is False:
+            continue
         ee.append(e)
         out.append(e)
     return node_ids, out

@@ -18,6 +18,11 @@ reference tests state them:
 * ``abft/event_processing_root_test.go`` (TestLachesisClassicRoots /
   TestLachesisRandomRoots): DAGs whose event names encode frame and root-ness
   (``:251-301``), kept for the abft restatement row.
+* ``abft/election/election_test.go:35-170`` (TestProcessRoot, 5 cases) ->
+  ``abft_golden.json``: ASCII DAG, validator weights by node name, and the
+  expected decided frame, Atropos name and decisive roots.  The observe
+  relation of that test is "direct parent edge" (``:213-232``), minus the
+  self-parent of events whose name starts with ``+``.
 
 The fixture is data (inputs and expected outputs); no reference source text is
 kept under tests/.
@@ -97,6 +102,27 @@ def main():
     with open(os.path.join(HERE, "fc_golden.json"), "w", encoding="utf-8") as f:
         json.dump(out, f, ensure_ascii=False, indent=1)
     print("wrote", len(cases), "fc cases,", len(roots), "root cases")
+
+    el_src = open(os.path.join(REF, "abft/election/election_test.go"), encoding="utf-8").read()
+    el_cases = []
+    for m in re.finditer(r't\.Run\("([^"]+)", func\(t \*testing\.T\) \{\s*testProcessRoot\(t,(.*?)`(.*?)`\)', el_src, re.S):
+        label, body, scheme = m.group(1), m.group(2), m.group(3)
+        exp = None
+        if "&testExpected" in body:
+            fr = int(re.search(r"DecidedFrame:\s*(\d+)", body).group(1))
+            at = re.search(r'DecidedAtropos:\s*"(\w+)"', body).group(1)
+            dec = re.search(r"DecisiveRoots:\s*map\[string\]bool\{(.*?)\}", body).group(1)
+            exp = {"frame": fr, "atropos": at, "decisive": sorted(re.findall(r'"([+\w]+)":\s*true', dec))}
+        w = {}
+        for nm, expr in re.findall(r'"(node\w)":\s*([^,\n]+),', body):
+            expr = expr.replace("math.MaxUint32", str(0xFFFFFFFF)).replace("/", "//")
+            w[nm] = int(eval(expr, {"__builtins__": {}}))
+        el_cases.append({"name": label, "source": "abft/election/election_test.go:35-170",
+                         "scheme": scheme, "weights": w, "expected": exp})
+    out2 = {"generated_by": "tests/golden/make_golden.py", "election_cases": el_cases}
+    with open(os.path.join(HERE, "abft_golden.json"), "w", encoding="utf-8") as f:
+        json.dump(out2, f, ensure_ascii=False, indent=1)
+    print("wrote", len(el_cases), "election cases")
 
 
 if __name__ == "__main__":
