@@ -1,0 +1,113 @@
+/*
+ * lachesis_abft.h -- C ABI of the batched abft caller on top of the HIP index.
+ *
+ * Drop-in for the consensus loop that drives the index in the reference:
+ * abft.IndexedLachesis (abft/indexed_lachesis.go:17-107) = abft.Lachesis
+ * (abft/lachesis.go) over abft.Orderer (abft/orderer.go, event_processing.go,
+ * frame_decide.go, bootstrap.go) and election.Election (abft/election/).
+ * Results -- frames, roots, decided frames, Atropos, cheaters, the order in
+ * which confirmed events are applied, epoch sealing -- are those of calling the
+ * reference's Process(e) once per event in the given order.  What changes is
+ * how the ForklessCause questions are asked: frames of a whole batch are
+ * computed level by level in frames, every question of a frame in one GPU
+ * tile launch (events x roots of the frame), and election votes of a whole
+ * round in one launch.
+ *
+ * Conventions are those of lachesis_hip.h: dense event indices (Add order of
+ * the current epoch; they restart at 0 when an epoch is sealed or reset),
+ * validator idx order, caller-owned buffers, 0 = ok / < 0 = error.  The abft
+ * handle drives the index handle it was created on (Add, Flush,
+ * DropNotFlushed, Reset): do not add events to that index directly.
+ * One host thread per handle; callbacks must not call back into the handle.
+ */
+#ifndef LACHESIS_ABFT_H
+#define LACHESIS_ABFT_H
+
+#include "lachesis_hip.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LX_ERR_FRAME -7        /* ErrWrongFrame: claimed frame mismatched (abft/event_processing.go:11-13) */
+#define LX_ERR_BYZANTINE -8    /* election sanity errors (abft/election/election_math.go:68-90, sort_roots.go:23) */
+#define LX_FRAME_BUILD 0xFFFFFFFFu   /* claimed_frame entry: compute as Build does (cap selfParentFrame+100) */
+
+typedef struct lx_abft lx_abft;
+
+/* lachesis.ConsensusCallbacks + BlockCallbacks (lachesis/consensus.go:21-44).
+ * begin_block: decided frame, its Atropos, and the cheaters seen by the Atropos
+ *   (validator idxs in idx order; abft/lachesis.go:57-73).
+ * apply_event: every event newly confirmed by the block, in the reference's
+ *   DFS order from the Atropos (abft/lachesis.go:40-55, abft/traversal.go:13-37).
+ * end_block: return 0 to continue the epoch, or 1 to seal it; then
+ *   *n_validators / *weights (idx order, valid until the next call into the
+ *   library) give the next epoch's validators (frame_decide.go:11-35).
+ * Any pointer may be NULL. */
+typedef struct lx_abft_callbacks {
+    void *user;
+    void (*begin_block)(void *user, uint32_t frame, uint32_t atropos, const uint32_t *cheaters, uint32_t n_cheaters);
+    void (*apply_event)(void *user, uint32_t ev);
+    int (*end_block)(void *user, uint32_t *n_validators, const uint32_t **weights);
+} lx_abft_callbacks;
+
+/* NewIndexedLachesis (abft/indexed_lachesis.go:42-51) over an index handle
+ * (unsharded). */
+int lx_abft_create(lx_index *index, lx_abft **out);
+void lx_abft_destroy(lx_abft *a);
+const char *lx_abft_last_error(const lx_abft *a);
+
+/* ApplyGenesis + Bootstrap (abft/apply_genesis.go:17-44, bootstrap.go:30-52):
+ * epoch and validators (weights in idx order); resets the index. */
+int lx_abft_bootstrap(lx_abft *a, uint32_t epoch, uint32_t n_validators, const uint32_t *weights,
+                      const lx_abft_callbacks *cb);
+
+/* Orderer.Reset (bootstrap.go:54-65): switch to a new empty epoch. */
+int lx_abft_reset(lx_abft *a, uint32_t epoch, uint32_t n_validators, const uint32_t *weights);
+
+/* IndexedLachesis.Process (indexed_lachesis.go:65-82) for n events in
+ * processing order (parents first; parent_off/parent_idx as lx_add_batch,
+ * dense indices of this epoch, self-parent first).  claimed_frame[i] is the
+ * event's Frame() field (LX_FRAME_BUILD: trust the computation, i.e. Build
+ * then Process).  out_frame (optional) receives every consumed event's frame.
+ * Callbacks fire for every frame decided inside the batch, in order.
+ * *consumed = events processed: n, or less when
+ *   - an event's claimed frame is wrong: returns LX_ERR_FRAME and *consumed is
+ *     its position (the events before it are processed, as the reference
+ *     processes them before returning ErrWrongFrame for it);
+ *   - a block sealed the epoch: returns 0, *consumed counts the events up to
+ *     the one whose processing decided the sealing frame; the rest belong to
+ *     no epoch and must be re-submitted by the caller (as the reference test
+ *     drivers do, abft/event_processing_test.go:145-150). */
+int lx_abft_process_batch(lx_abft *a, uint32_t n, const uint32_t *creator_idx, const uint32_t *seq,
+                          const uint64_t *parent_off, const uint32_t *parent_idx, const uint32_t *claimed_frame,
+                          uint32_t *out_frame, uint32_t *consumed);
+
+/* IndexedLachesis.Build (indexed_lachesis.go:53-63): frame of a self-emitted
+ * event (added, evaluated, then dropped again). */
+int lx_abft_build(lx_abft *a, uint32_t creator_idx, uint32_t seq, uint32_t n_parents, const uint32_t *parents,
+                  uint32_t *out_frame);
+
+uint32_t lx_abft_epoch(const lx_abft *a);
+uint32_t lx_abft_last_decided_frame(const lx_abft *a);
+/* GetFrameRoots (abft/store_roots.go:52-93): root events of a frame. */
+int lx_abft_frame_roots(lx_abft *a, uint32_t frame, uint32_t *out_ev, uint32_t cap, uint32_t *n);
+int lx_abft_event_frame(const lx_abft *a, uint32_t ev, uint32_t *frame);
+/* GetEventConfirmedOn (abft/store_event_confirmed.go:20-30): 0 = not confirmed. */
+int lx_abft_event_confirmed_on(const lx_abft *a, uint32_t ev, uint32_t *frame);
+
+/* Wall time of the last lx_abft_process_batch by phase (ms) and its GPU work. */
+typedef struct lx_abft_stats {
+    float ms_index;      /* Add of the batch (lx_add_batch) */
+    float ms_frames;     /* frames + roots (root ForklessCause tiles) */
+    float ms_election;   /* votes, decisions */
+    float ms_blocks;     /* cheaters, confirmation DFS, callbacks */
+    uint32_t frame_steps, fc_launches, vote_launches, blocks;
+    uint64_t fc_pairs;   /* (event, root) pairs evaluated */
+} lx_abft_stats;
+int lx_abft_last_stats(const lx_abft *a, lx_abft_stats *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,798 @@
+// lx_abft.cpp -- batched abft caller (include/lachesis_abft.h).
+//
+// Same results as abft.IndexedLachesis.Process called once per event
+// (abft/indexed_lachesis.go:65-82), reorganised so that the ForklessCause
+// questions of the consensus loop become a few large GPU launches:
+//
+// Frames (calcFrameIdx, abft/event_processing.go:163-189).  frame(e) is the
+// first f >= selfParentFrame(e) at which e is NOT forkless-caused by a quorum
+// of roots(f) (capped by the claimed frame, or selfParentFrame+100 in Build);
+// roots(f) = events with selfParentFrame < f <= frame.  ForklessCause(e, r)
+// can only hold for ancestors r of e, so the answer for e depends only on its
+// ancestors and the batch can be solved frame by frame: at step f every
+// event still undecided has frame >= f, roots(f) is complete, and every event
+// whose loop has reached f asks q_f(e) = quorum(roots(f)) -- all of them in
+// one k_root_fc tile launch.  Self-children of those events are evaluated
+// speculatively in the same launch (their self-parent usually stops at f).
+// An event that passes q_f becomes a root of f+1; its bit row of that launch
+// is exactly the observed-roots set the election needs for that root slot.
+//
+// Election (abft/election/election_math.go:13-114).  Votes of a root slot
+// depend only on the slots it observes, so votes are computed per frame
+// (round) for all slots at once, for every subject (k_vote_round).  The
+// reference skips subjects already decided when a root is processed; that
+// only skips work whose result is never read.  The decision for subject v is
+// the vote of the first deciding root in processing order =
+// atomicMin over (event << 32 | vote); the frame is decided at
+// t = max(previous decision, max_{v <= Atropos subject} first decision(v))
+// (chooseAtropos, sort_roots.go:10-25), final once no uncomputed slot is older
+// than t.  Frames are replayed after each decision as processKnownRoots does.
+//
+// Blocks (abft/lachesis.go:40-86): cheaters from the Atropos' HighestBefore
+// fork markers, confirmation DFS in the reference's stack order on the host.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/lachesis_abft.h"
+#include "lx_internal.h"
+
+namespace {
+
+constexpr uint32_t NONE = LX_NONE;
+constexpr uint32_t kSpecDepth = 4;      // self-children evaluated ahead per launch
+constexpr uint32_t kBuildCap = 100;     // calcFrameIdx: selfParentFrame + 100 in Build
+
+template <typename T>
+struct DVec {
+    T *p = nullptr;
+    uint64_t cap = 0;
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+double now_ms() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+struct Frame {
+    std::vector<uint32_t> ev, creator, dup, bm_len;
+    std::vector<uint64_t> bm_off;
+    std::vector<uint32_t> last_of;   // creator -> last slot index (for dup)
+    uint32_t synced = 0;
+    uint32_t voted = 0;              // slots with votes for the current election
+    DVec<uint32_t> d_ev, d_creator, d_dup, d_bm_len, votes;
+    DVec<uint64_t> d_bm_off;
+    void release() {
+        d_ev.release();
+        d_creator.release();
+        d_dup.release();
+        d_bm_len.release();
+        d_bm_off.release();
+        votes.release();
+    }
+};
+
+}  // namespace
+
+struct lx_abft {
+    lx_index *ix = nullptr;
+    std::string err;
+    lx_abft_callbacks cb{};
+    bool booted = false;
+
+    uint32_t epoch = 0, V = 0, quorum = 0;
+    std::vector<uint32_t> weights;
+    uint32_t last_decided = 0;
+    uint64_t t_prev = 0;                // event whose processing decided the last frame
+
+    // per event of the epoch (dense index)
+    std::vector<uint32_t> ev_frame, ev_sp, ev_confirmed;
+    std::vector<uint64_t> par_off{0};
+    std::vector<uint32_t> par;
+
+    std::vector<Frame> frames;          // [0] unused
+    DVec<uint32_t> arena;               // bit rows (observed roots) of k_root_fc launches
+    uint64_t arena_used = 0;
+
+    // scratch
+    DVec<uint32_t> d_cand;
+    DVec<uint8_t> d_q;
+    DVec<unsigned long long> d_dec;
+    DVec<uint32_t> d_err;
+    DVec<uint32_t> d_kcol, d_kflag, d_kw;
+    uint32_t n_k = 0;
+    uint32_t k_B = NONE;                // branch count the cheater columns were built for
+    std::vector<uint32_t> h_row;
+    bool dec_dirty = true;
+
+    lx_abft_stats stats{};
+
+    int fail(int code, const char *fmt, ...) {
+        char buf[512];
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(buf, sizeof buf, fmt, ap);
+        va_end(ap);
+        err = buf;
+        return code;
+    }
+    int hip(hipError_t e, const char *what) {
+        if (e == hipSuccess) return 0;
+        return fail(e == hipErrorOutOfMemory ? LX_ERR_NOMEM : LX_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
+    }
+    int ixfail(int rc) {
+        err = lx_last_error(ix);
+        return rc;
+    }
+};
+
+#define AHIP(a, expr)                               \
+    do {                                            \
+        int _rc = (a)->hip((expr), #expr);          \
+        if (_rc) return _rc;                        \
+    } while (0)
+#define ARC(expr)                                   \
+    do {                                            \
+        int _rc = (expr);                           \
+        if (_rc) return _rc;                        \
+    } while (0)
+
+namespace {
+
+template <typename T>
+int reserve(lx_abft *a, DVec<T> &v, uint64_t n, uint64_t keep, hipStream_t s) {
+    if (n <= v.cap) return 0;
+    uint64_t cap = std::max<uint64_t>({n, v.cap + v.cap / 2, 256});
+    T *p = nullptr;
+    AHIP(a, hipMalloc((void **)&p, cap * sizeof(T)));
+    if (v.p && keep) AHIP(a, hipMemcpyAsync(p, v.p, keep * sizeof(T), hipMemcpyDeviceToDevice, s));
+    if (v.p) {
+        AHIP(a, hipStreamSynchronize(s));
+        (void)hipFree(v.p);
+    }
+    v.p = p;
+    v.cap = cap;
+    return 0;
+}
+
+template <typename T>
+int upload(lx_abft *a, DVec<T> &v, const std::vector<T> &h, uint64_t from, hipStream_t s) {
+    ARC(reserve(a, v, h.size(), from, s));
+    if (h.size() > from)
+        AHIP(a, hipMemcpyAsync(v.p + from, h.data() + from, (h.size() - from) * sizeof(T), hipMemcpyHostToDevice, s));
+    return 0;
+}
+
+Frame &frame_at(lx_abft *a, uint32_t f) {
+    if (a->frames.size() <= f) a->frames.resize(f + 1);
+    return a->frames[f];
+}
+
+void add_slot(lx_abft *a, uint32_t f, uint32_t e, uint32_t creator, uint64_t bm_off, uint32_t bm_len) {
+    Frame &fr = frame_at(a, f);
+    if (fr.last_of.empty()) fr.last_of.assign(a->V, NONE);
+    uint32_t k = (uint32_t)fr.ev.size();
+    fr.ev.push_back(e);
+    fr.creator.push_back(creator);
+    fr.dup.push_back(fr.last_of[creator]);
+    fr.last_of[creator] = k;
+    fr.bm_off.push_back(bm_off);
+    fr.bm_len.push_back(bm_len);
+}
+
+int sync_frame(lx_abft *a, Frame &fr, hipStream_t s) {
+    uint32_t from = fr.synced;
+    if (from == fr.ev.size()) return 0;
+    ARC(upload(a, fr.d_ev, fr.ev, from, s));
+    ARC(upload(a, fr.d_creator, fr.creator, from, s));
+    ARC(upload(a, fr.d_dup, fr.dup, from, s));
+    ARC(upload(a, fr.d_bm_len, fr.bm_len, from, s));
+    ARC(upload(a, fr.d_bm_off, fr.bm_off, from, s));
+    fr.synced = (uint32_t)fr.ev.size();
+    return 0;
+}
+
+void clear_epoch(lx_abft *a) {
+    for (Frame &f : a->frames) f.release();
+    a->frames.clear();
+    a->ev_frame.clear();
+    a->ev_sp.clear();
+    a->ev_confirmed.clear();
+    a->par_off.assign(1, 0);
+    a->par.clear();
+    a->arena_used = 0;
+    a->last_decided = 0;
+    a->t_prev = 0;
+    a->dec_dirty = true;
+    a->k_B = NONE;
+}
+
+int start_epoch(lx_abft *a, uint32_t epoch, uint32_t nv, const uint32_t *w) {
+    if (!nv || !w) return a->fail(LX_ERR_ARG, "genesis validators shouldn't be empty");
+    int rc = lx_reset(a->ix, nv, w);
+    if (rc) return a->ixfail(rc);
+    IndexView iv;
+    if ((rc = lx_index_view(a->ix, &iv))) return a->ixfail(rc);
+    clear_epoch(a);
+    a->epoch = epoch;
+    a->V = nv;
+    a->weights.assign(w, w + nv);
+    a->quorum = iv.quorum;
+    return 0;
+}
+
+// Cheaters' branch columns, grouped by creator, original first (k_root_fc).
+int refresh_cheaters(lx_abft *a, const IndexView &iv) {
+    if (a->k_B == iv.B) return 0;
+    std::vector<uint32_t> col, flag, kw;
+    for (uint32_t c = 0; c < iv.V; c++) {
+        const auto &l = (*iv.by_creator)[c];
+        if (l.size() < 2) continue;
+        for (size_t i = 0; i < l.size(); i++) {
+            col.push_back(l[i]);
+            flag.push_back((i == 0 ? 1u : 0u) | (i + 1 == l.size() ? 2u : 0u));
+            kw.push_back(i + 1 == l.size() ? (*iv.weights)[c] : 0u);
+        }
+    }
+    a->n_k = (uint32_t)col.size();
+    if (a->n_k) {
+        ARC(upload(a, a->d_kcol, col, 0, iv.stream));
+        ARC(upload(a, a->d_kflag, flag, 0, iv.stream));
+        ARC(upload(a, a->d_kw, kw, 0, iv.stream));
+    }
+    a->k_B = iv.B;
+    return 0;
+}
+
+// One frame step: bits (cands x roots(f)) into the arena, q per candidate.
+int eval_frame(lx_abft *a, const IndexView &iv, uint32_t f, const std::vector<uint32_t> &cand, uint64_t *row0,
+               uint32_t *words_out, std::vector<uint8_t> &q) {
+    hipStream_t s = iv.stream;
+    Frame &fr = frame_at(a, f);
+    ARC(sync_frame(a, fr, s));
+    const uint32_t R = (uint32_t)fr.ev.size();
+    const uint32_t words = (R + 31) / 32;
+    const uint32_t n = (uint32_t)cand.size();
+    *row0 = a->arena_used;
+    *words_out = words;
+    ARC(reserve(a, a->arena, a->arena_used + (uint64_t)n * words + 1, a->arena_used, s));
+    ARC(reserve(a, a->d_cand, n, 0, s));
+    ARC(reserve(a, a->d_q, n, 0, s));
+    AHIP(a, hipMemcpyAsync(a->d_cand.p, cand.data(), n * 4ull, hipMemcpyHostToDevice, s));
+    uint32_t *bits = a->arena.p + a->arena_used;
+    if (words) {
+        ARC(refresh_cheaters(a, iv));
+        RootFcArgs r{};
+        r.hb = iv.hb;
+        r.la = iv.la;
+        r.stride = iv.stride;
+        r.cand = a->d_cand.p;
+        r.n_cand = n;
+        r.roots = fr.d_ev.p;
+        r.n_roots = R;
+        r.roots_fallback = cand[0];
+        r.ncols = (iv.V + 31) / 32 * 32;
+        r.wpad = iv.wpad;
+        r.quorum = a->quorum;
+        r.n_k = a->n_k;
+        r.kcol = a->d_kcol.p;
+        r.kflag = a->d_kflag.p;
+        r.kw = a->d_kw.p;
+        r.ev_branch = iv.ev_branch;
+        r.bits = bits;
+        r.words = words;
+        AHIP(a, lx::launch_root_fc(r, iv.B > iv.V, s));
+        QuorumArgs qa{};
+        qa.bits = bits;
+        qa.words = words;
+        qa.n_cand = n;
+        qa.cand = a->d_cand.p;
+        qa.root_ev = fr.d_ev.p;
+        qa.creator = fr.d_creator.p;
+        qa.dup = fr.d_dup.p;
+        qa.wcreator = iv.wpad;
+        qa.quorum = a->quorum;
+        qa.q = a->d_q.p;
+        AHIP(a, lx::launch_root_quorum(qa, s));
+        q.resize(n);
+        AHIP(a, hipMemcpyAsync(q.data(), a->d_q.p, n, hipMemcpyDeviceToHost, s));
+        AHIP(a, hipStreamSynchronize(s));
+        a->stats.fc_launches++;
+        a->stats.fc_pairs += (uint64_t)n * R;
+    } else {
+        q.assign(n, 0);   // no roots in frame f: no quorum (WeightCounter of nothing)
+    }
+    a->arena_used += (uint64_t)n * words;
+    return 0;
+}
+
+// Frames of events [base, base+n) (all already added to the index).
+// cap[i]: claimed frame (Process) or NONE = Build's selfParentFrame + 100.
+int compute_frames(lx_abft *a, uint64_t base, uint32_t n, const uint32_t *creator, const uint32_t *claimed) {
+    IndexView iv;
+    int rc = lx_index_view(a->ix, &iv);
+    if (rc) return a->ixfail(rc);
+    std::vector<uint32_t> cur(n, NONE), cap(n, NONE), child_head(n, NONE), child_next(n, NONE);
+    std::map<uint32_t, std::vector<uint32_t>> pending;   // frame -> batch positions whose loop is at it
+    for (uint32_t i = 0; i < n; i++) {
+        uint32_t sp = a->ev_sp[base + i];
+        if (sp != NONE && sp >= base) {
+            uint32_t p = (uint32_t)(sp - base);
+            child_next[i] = child_head[p];
+            child_head[p] = i;
+        }
+    }
+    auto cap_of = [&](uint32_t i, uint32_t sp_frame) {
+        uint32_t c = claimed ? claimed[i] : LX_FRAME_BUILD;
+        return c == LX_FRAME_BUILD ? sp_frame + kBuildCap : c;
+    };
+    // resolve(i, f): frame(i) = f; self-children start their loop at f.  A
+    // child evaluated speculatively in the same launch is handled by the walk
+    // below; the others are queued at f by flush().
+    std::vector<std::pair<uint32_t, uint32_t>> pushed;
+    auto resolve = [&](uint32_t i, uint32_t f) {
+        a->ev_frame[base + i] = f;
+        for (uint32_t c = child_head[i]; c != NONE; c = child_next[c]) {
+            cur[c] = f;
+            cap[c] = cap_of(c, f);
+            pushed.emplace_back(c, f);
+        }
+    };
+    auto flush = [&]() {
+        for (auto &pc : pushed)
+            if (a->ev_frame[base + pc.first] == 0 && cur[pc.first] == pc.second) pending[pc.second].push_back(pc.first);
+        pushed.clear();
+    };
+    for (uint32_t i = 0; i < n; i++) {
+        uint32_t sp = a->ev_sp[base + i];
+        if (sp == NONE) {
+            // f = 0: roots(0) is empty, no quorum -> f stays 0 -> frame 1 (:184-187)
+            resolve(i, 1);
+            add_slot(a, 1, (uint32_t)(base + i), creator[i], 0, 0);
+        } else if (sp < base) {
+            cur[i] = a->ev_frame[sp];
+            cap[i] = cap_of(i, cur[i]);
+            pending[cur[i]].push_back(i);
+        }
+    }
+    flush();
+
+    std::vector<uint8_t> spec(n, 0), q;
+    std::vector<uint32_t> cand_pos, cand_ev;
+    while (!pending.empty()) {
+        const uint32_t f = pending.begin()->first;
+        std::vector<uint32_t> Q = std::move(pending.begin()->second);
+        pending.erase(pending.begin());
+        std::vector<uint32_t> ask;
+        for (uint32_t i : Q) {
+            if (f >= cap[i]) resolve(i, f);   // loop bound checked before the quorum (:184)
+            else ask.push_back(i);
+        }
+        if (ask.empty()) {
+            flush();
+            continue;
+        }
+        // speculative self-descendants, kSpecDepth deep
+        cand_pos = ask;
+        for (uint32_t i : ask) spec[i] = 2;
+        {
+            std::vector<uint32_t> lvl = ask, nxt;
+            for (uint32_t d = 0; d < kSpecDepth && !lvl.empty() && n > 1; d++) {
+                nxt.clear();
+                for (uint32_t i : lvl)
+                    for (uint32_t c = child_head[i]; c != NONE; c = child_next[c])
+                        if (!spec[c] && cur[c] == NONE) {
+                            spec[c] = 1;
+                            nxt.push_back(c);
+                            cand_pos.push_back(c);
+                        }
+                lvl.swap(nxt);
+            }
+        }
+        std::sort(cand_pos.begin(), cand_pos.end());
+        cand_ev.resize(cand_pos.size());
+        for (size_t k = 0; k < cand_pos.size(); k++) cand_ev[k] = (uint32_t)(base + cand_pos[k]);
+        uint64_t row0;
+        uint32_t words;
+        ARC(eval_frame(a, iv, f, cand_ev, &row0, &words, q));
+        for (size_t k = 0; k < cand_pos.size(); k++) {
+            const uint32_t i = cand_pos[k];
+            const bool own = spec[i] == 2;
+            spec[i] = 0;
+            // a speculative event counts only if its self-parent stopped at f
+            // during this walk (then i's loop is at f too)
+            if (!own && (cur[i] != f || a->ev_frame[base + i] != 0)) continue;
+            if (f >= cap[i]) {
+                resolve(i, f);
+            } else if (q[k]) {
+                cur[i] = f + 1;                      // root of f+1; its bit row observes roots(f)
+                add_slot(a, f + 1, cand_ev[k], creator[i], row0 + k * (uint64_t)words, (uint32_t)frame_at(a, f).ev.size());
+                pending[f + 1].push_back(i);
+            } else {
+                resolve(i, f);
+            }
+        }
+        flush();
+        a->stats.frame_steps++;
+    }
+    return 0;
+}
+
+// ---------------------------------------------------------------------------- election
+
+int vote_frame(lx_abft *a, const IndexView &iv, uint32_t F, uint32_t g) {
+    hipStream_t s = iv.stream;
+    Frame &fg = frame_at(a, g);
+    Frame &fp = frame_at(a, g - 1);
+    ARC(sync_frame(a, fg, s));
+    ARC(sync_frame(a, fp, s));
+    const uint32_t from = fg.voted, to = (uint32_t)fg.ev.size();
+    if (from == to) return 0;
+    ARC(reserve(a, fg.votes, (uint64_t)to * a->V, (uint64_t)from * a->V, s));
+    VoteArgs v{};
+    v.V = a->V;
+    v.voter_ev = fg.d_ev.p + from;
+    v.bm_off = fg.d_bm_off.p + from;
+    v.bm_len = fg.d_bm_len.p + from;
+    v.bm = a->arena.p;
+    v.prev_creator = fp.d_creator.p;
+    v.prev_dup = fp.d_dup.p;
+    v.prev_votes = fp.votes.p;
+    v.wcreator = iv.wpad;
+    v.quorum = a->quorum;
+    v.votes = fg.votes.p + (uint64_t)from * a->V;
+    v.dec = a->d_dec.p;
+    v.err = a->d_err.p;
+    AHIP(a, lx::launch_votes(v, to - from, g == F + 1, s));
+    fg.voted = to;
+    a->stats.vote_launches++;
+    return 0;
+}
+
+// decision of election F: 0 pending, 1 decided (*t, *atropos slot)
+int check_decision(lx_abft *a, const IndexView &iv, uint32_t F, uint64_t *t, uint32_t *obs, int *state) {
+    std::vector<unsigned long long> dec(a->V);
+    uint32_t err = 0;
+    AHIP(a, hipMemcpyAsync(dec.data(), a->d_dec.p, a->V * 8ull, hipMemcpyDeviceToHost, iv.stream));
+    AHIP(a, hipMemcpyAsync(&err, a->d_err.p, 4, hipMemcpyDeviceToHost, iv.stream));
+    AHIP(a, hipStreamSynchronize(iv.stream));
+    if (err & kVoteErrTwoRoots)
+        return a->fail(LX_ERR_BYZANTINE, "forkless caused by 2 fork roots => more than 1/3W are Byzantine (election frame=%u)", F);
+    if (err & kVoteErrQuorum)
+        return a->fail(LX_ERR_BYZANTINE, "root must be forkless caused by at least 2/3W of prev roots (election frame=%u)", F);
+    if (err & kVoteErrMissing)
+        return a->fail(LX_ERR_BYZANTINE, "every root must vote for every not decided subject (election frame=%u)", F);
+    *state = 0;
+    uint64_t tmax = 0;
+    for (uint32_t v = 0; v < a->V; v++) {   // chooseAtropos: SortedIDs = idx order
+        if (dec[v] == ~0ull) return 0;
+        tmax = std::max<uint64_t>(tmax, dec[v] >> 32);
+        if (dec[v] & 0x80000000ull) {
+            *t = tmax;
+            *obs = (uint32_t)(dec[v] & kVoteNoRoot);
+            *state = 1;
+            return 0;
+        }
+    }
+    return a->fail(LX_ERR_BYZANTINE, "all the roots are decided as 'no', which is possible only if more than 1/3W are Byzantine");
+}
+
+int reset_election(lx_abft *a, const IndexView &iv) {
+    ARC(reserve(a, a->d_dec, a->V, 0, iv.stream));
+    ARC(reserve(a, a->d_err, 1, 0, iv.stream));
+    AHIP(a, hipMemsetAsync(a->d_dec.p, 0xFF, a->V * 8ull, iv.stream));
+    AHIP(a, hipMemsetAsync(a->d_err.p, 0, 4, iv.stream));
+    for (uint32_t g = a->last_decided + 1; g < a->frames.size(); g++) a->frames[g].voted = 0;
+    a->dec_dirty = false;
+    return 0;
+}
+
+// cheaters + confirmation DFS + callbacks; returns 1 in *sealed when EndBlock seals
+int apply_block(lx_abft *a, const IndexView &iv, uint32_t F, uint32_t atropos, bool *sealed,
+                std::vector<uint32_t> *new_w) {
+    *sealed = false;
+    std::vector<uint32_t> row(a->V), cheaters;
+    AHIP(a, hipMemcpyAsync(row.data(), iv.hb + (uint64_t)atropos * iv.stride, a->V * 4ull, hipMemcpyDeviceToHost,
+                           iv.stream));
+    AHIP(a, hipStreamSynchronize(iv.stream));
+    for (uint32_t c = 0; c < a->V; c++)
+        if (row[c] & LX_MARK) cheaters.push_back(c);   // GetMergedHighestBefore(atropos)[c].IsForkDetected()
+    if (!a->cb.begin_block) return 0;   // BeginBlock == nil: no confirmation, no seal (lachesis.go:69-71)
+    if (a->cb.begin_block) a->cb.begin_block(a->cb.user, F, atropos, cheaters.data(), (uint32_t)cheaters.size());
+    // dfsSubgraph(atropos, filter) (abft/traversal.go:13-37, lachesis.go:40-55)
+    std::vector<uint32_t> stack;
+    for (uint32_t walk = atropos;;) {
+        if (a->ev_confirmed[walk] == 0) {
+            a->ev_confirmed[walk] = F;
+            if (a->cb.apply_event) a->cb.apply_event(a->cb.user, walk);
+            for (uint64_t k = a->par_off[walk]; k < a->par_off[walk + 1]; k++) stack.push_back(a->par[k]);
+        }
+        if (stack.empty()) break;
+        walk = stack.back();
+        stack.pop_back();
+    }
+    if (a->cb.end_block) {
+        uint32_t nv = 0;
+        const uint32_t *w = nullptr;
+        if (a->cb.end_block(a->cb.user, &nv, &w)) {
+            if (!nv || !w) return a->fail(LX_ERR_ARG, "end_block sealed the epoch without validators");
+            new_w->assign(w, w + nv);
+            *sealed = true;
+        }
+    }
+    a->stats.blocks++;
+    return 0;
+}
+
+// Runs elections over all known root slots; *sealed_at = event that decided a
+// sealing frame (NONE if none).
+int run_elections(lx_abft *a, uint64_t *sealed_at, std::vector<uint32_t> *new_w) {
+    *sealed_at = ~0ull;
+    IndexView iv;
+    int rc = lx_index_view(a->ix, &iv);
+    if (rc) return a->ixfail(rc);
+    for (;;) {
+        const uint32_t F = a->last_decided + 1;
+        if (a->dec_dirty) ARC(reset_election(a, iv));
+        const uint32_t maxf = (uint32_t)a->frames.size() - 1;
+        if (a->frames.size() <= F + 1) return 0;
+        ARC(sync_frame(a, frame_at(a, F), iv.stream));
+        int state = 0;
+        uint64_t t = 0;
+        uint32_t obs = 0;
+        bool checked = false;
+        for (uint32_t g = F + 1; g <= maxf; g++) {
+            const bool fresh = frame_at(a, g).voted < frame_at(a, g).ev.size();
+            ARC(vote_frame(a, iv, F, g));
+            if (g < F + 2 || (checked && !fresh)) continue;
+            ARC(check_decision(a, iv, F, &t, &obs, &state));
+            checked = true;
+            if (state) {
+                // final unless a slot not yet voted in this election is older
+                uint64_t L = ~0ull;
+                for (uint32_t h = g + 1; h <= maxf; h++) {
+                    const Frame &fh = a->frames[h];
+                    for (size_t k = fh.voted; k < fh.ev.size(); k++) L = std::min<uint64_t>(L, fh.ev[k]);
+                }
+                if (t <= L) break;
+                state = 0;
+            }
+        }
+        if (!state) return 0;
+        const Frame &fF = a->frames[F];
+        if (obs >= fF.ev.size()) return a->fail(LX_ERR_STATE, "decided Atropos has no root (frame %u)", F);
+        const uint32_t atropos = fF.ev[obs];
+        const uint64_t decided_at = std::max<uint64_t>(t, a->t_prev);
+        bool sealed;
+        ARC(apply_block(a, iv, F, atropos, &sealed, new_w));
+        if (sealed) {
+            *sealed_at = decided_at;
+            return 0;
+        }
+        a->t_prev = decided_at;
+        a->last_decided = F;
+        for (uint32_t g = 1; g <= F && g < a->frames.size(); g++) a->frames[g].votes.release();
+        a->dec_dirty = true;
+    }
+}
+
+struct Snapshot {
+    std::vector<size_t> sizes;
+    uint64_t arena_used;
+    uint64_t n_events;
+};
+
+Snapshot take_snapshot(lx_abft *a) {
+    Snapshot s;
+    for (const Frame &f : a->frames) s.sizes.push_back(f.ev.size());
+    s.arena_used = a->arena_used;
+    s.n_events = a->ev_frame.size();
+    return s;
+}
+
+void restore_snapshot(lx_abft *a, const Snapshot &s) {
+    for (size_t f = 0; f < a->frames.size(); f++) {
+        Frame &fr = a->frames[f];
+        size_t keep = f < s.sizes.size() ? s.sizes[f] : 0;
+        while (fr.ev.size() > keep) {
+            uint32_t c = fr.creator.back();
+            fr.last_of[c] = fr.dup.back();
+            fr.ev.pop_back();
+            fr.creator.pop_back();
+            fr.dup.pop_back();
+            fr.bm_off.pop_back();
+            fr.bm_len.pop_back();
+        }
+        fr.synced = std::min<uint32_t>(fr.synced, (uint32_t)keep);
+        fr.voted = std::min<uint32_t>(fr.voted, (uint32_t)keep);
+    }
+    while (a->frames.size() > s.sizes.size() && a->frames.size() > 1 && a->frames.back().ev.empty()) {
+        a->frames.back().release();
+        a->frames.pop_back();
+    }
+    a->arena_used = s.arena_used;
+    a->ev_frame.resize(s.n_events);
+    a->ev_sp.resize(s.n_events);
+    a->ev_confirmed.resize(s.n_events);
+    a->par_off.resize(s.n_events + 1);
+    a->par.resize(a->par_off.back());
+}
+
+// adds the batch to the index and the host event tables
+int add_events(lx_abft *a, uint32_t n, const uint32_t *creator, const uint32_t *seq, const uint64_t *poff,
+               const uint32_t *par) {
+    uint32_t err_index = 0;
+    int rc = lx_add_batch(a->ix, n, creator, seq, poff, par, nullptr, &err_index);
+    if (rc) return a->ixfail(rc);
+    for (uint32_t i = 0; i < n; i++) {
+        const uint64_t p0 = poff[i], p1 = poff[i + 1];
+        a->ev_sp.push_back(seq[i] > 1 && p1 > p0 ? par[p0] : NONE);   // inter/dag/event.go:87-92
+        a->ev_frame.push_back(0);
+        a->ev_confirmed.push_back(0);
+        a->par.insert(a->par.end(), par + p0, par + p1);
+        a->par_off.push_back(a->par.size());
+    }
+    return 0;
+}
+
+int process(lx_abft *a, uint32_t n, const uint32_t *creator, const uint32_t *seq, const uint64_t *poff,
+            const uint32_t *par, const uint32_t *claimed, uint32_t *out_frame, uint32_t *consumed) {
+    *consumed = 0;
+    if (!n) return 0;
+    const uint64_t base = a->ev_frame.size();
+    Snapshot snap = take_snapshot(a);
+    double t0 = now_ms();
+    ARC(add_events(a, n, creator, seq, poff, par));
+    double t1 = now_ms();
+    ARC(compute_frames(a, base, n, creator, claimed));
+    double t2 = now_ms();
+    a->stats.ms_index += (float)(t1 - t0);
+    a->stats.ms_frames += (float)(t2 - t1);
+    // checkAndSaveEvent: claimed frame must equal the computed one
+    uint32_t bad = n;
+    if (claimed)
+        for (uint32_t i = 0; i < n; i++)
+            if (claimed[i] != LX_FRAME_BUILD && claimed[i] != a->ev_frame[base + i]) { bad = i; break; }
+    if (bad < n) {
+        // the reference processes the events before the bad one; redo them alone
+        restore_snapshot(a, snap);
+        int rc = lx_drop_not_flushed(a->ix);
+        if (rc) return a->ixfail(rc);
+        uint32_t c = 0;
+        if (bad) ARC(process(a, bad, creator, seq, poff, par, claimed, out_frame, &c));
+        *consumed = c;
+        if (c == bad) a->err = "claimed frame mismatched with calculated";
+        return c == bad ? LX_ERR_FRAME : 0;
+    }
+    uint64_t sealed_at;
+    std::vector<uint32_t> new_w;
+    double t3 = now_ms();
+    ARC(run_elections(a, &sealed_at, &new_w));
+    double t4 = now_ms();
+    a->stats.ms_election += (float)(t4 - t3);
+    uint32_t done = n;
+    if (sealed_at != ~0ull) done = (uint32_t)(sealed_at - base + 1);
+    if (out_frame)
+        for (uint32_t i = 0; i < done; i++) out_frame[i] = a->ev_frame[base + i];
+    *consumed = done;
+    if (sealed_at != ~0ull) {
+        ARC(start_epoch(a, a->epoch + 1, (uint32_t)new_w.size(), new_w.data()));
+    } else {
+        int rc = lx_flush(a->ix);
+        if (rc) return a->ixfail(rc);
+    }
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int lx_abft_create(lx_index *index, lx_abft **out) {
+    if (!index || !out) return LX_ERR_ARG;
+    lx_abft *a = new lx_abft();
+    a->ix = index;
+    *out = a;
+    return 0;
+}
+
+void lx_abft_destroy(lx_abft *a) {
+    if (!a) return;
+    for (Frame &f : a->frames) f.release();
+    a->arena.release();
+    a->d_cand.release();
+    a->d_q.release();
+    a->d_dec.release();
+    a->d_err.release();
+    a->d_kcol.release();
+    a->d_kflag.release();
+    a->d_kw.release();
+    delete a;
+}
+
+const char *lx_abft_last_error(const lx_abft *a) { return a ? a->err.c_str() : "null handle"; }
+
+int lx_abft_bootstrap(lx_abft *a, uint32_t epoch, uint32_t nv, const uint32_t *w, const lx_abft_callbacks *cb) {
+    if (!a) return LX_ERR_ARG;
+    if (a->booted) return a->fail(LX_ERR_STATE, "already bootstrapped");
+    a->cb = cb ? *cb : lx_abft_callbacks{};
+    ARC(start_epoch(a, epoch, nv, w));
+    a->booted = true;
+    return 0;
+}
+
+int lx_abft_reset(lx_abft *a, uint32_t epoch, uint32_t nv, const uint32_t *w) {
+    if (!a) return LX_ERR_ARG;
+    if (!a->booted) return a->fail(LX_ERR_STATE, "not bootstrapped");
+    return start_epoch(a, epoch, nv, w);
+}
+
+int lx_abft_process_batch(lx_abft *a, uint32_t n, const uint32_t *creator, const uint32_t *seq,
+                          const uint64_t *poff, const uint32_t *par, const uint32_t *claimed, uint32_t *out_frame,
+                          uint32_t *consumed) {
+    if (!a || !consumed) return LX_ERR_ARG;
+    if (!a->booted) return a->fail(LX_ERR_STATE, "not bootstrapped");
+    a->stats = lx_abft_stats{};
+    return process(a, n, creator, seq, poff, par, claimed, out_frame, consumed);
+}
+
+int lx_abft_build(lx_abft *a, uint32_t creator, uint32_t seq, uint32_t np, const uint32_t *parents,
+                  uint32_t *out_frame) {
+    if (!a || !out_frame) return LX_ERR_ARG;
+    if (!a->booted) return a->fail(LX_ERR_STATE, "not bootstrapped");
+    const uint64_t base = a->ev_frame.size();
+    Snapshot snap = take_snapshot(a);
+    uint64_t poff[2] = {0, np};
+    int rc = add_events(a, 1, &creator, &seq, poff, parents);
+    if (rc == 0) rc = compute_frames(a, base, 1, &creator, nullptr);
+    if (rc == 0) *out_frame = a->ev_frame[base];
+    restore_snapshot(a, snap);
+    int rc2 = lx_drop_not_flushed(a->ix);
+    if (rc) return rc;
+    if (rc2) return a->ixfail(rc2);
+    return 0;
+}
+
+uint32_t lx_abft_epoch(const lx_abft *a) { return a ? a->epoch : 0; }
+uint32_t lx_abft_last_decided_frame(const lx_abft *a) { return a ? a->last_decided : 0; }
+
+int lx_abft_frame_roots(lx_abft *a, uint32_t f, uint32_t *out, uint32_t cap, uint32_t *n) {
+    if (!a || !n) return LX_ERR_ARG;
+    *n = 0;
+    if (f >= a->frames.size()) return 0;
+    const auto &ev = a->frames[f].ev;
+    *n = (uint32_t)ev.size();
+    if (out) std::copy(ev.begin(), ev.begin() + std::min<size_t>(cap, ev.size()), out);
+    return 0;
+}
+
+int lx_abft_event_frame(const lx_abft *a, uint32_t ev, uint32_t *frame) {
+    if (!a || !frame || ev >= a->ev_frame.size()) return LX_ERR_ARG;
+    *frame = a->ev_frame[ev];
+    return 0;
+}
+
+int lx_abft_event_confirmed_on(const lx_abft *a, uint32_t ev, uint32_t *frame) {
+    if (!a || !frame || ev >= a->ev_confirmed.size()) return LX_ERR_ARG;
+    *frame = a->ev_confirmed[ev];
+    return 0;
+}
+
+int lx_abft_last_stats(const lx_abft *a, lx_abft_stats *out) {
+    if (!a || !out) return LX_ERR_ARG;
+    *out = a->stats;
+    return 0;
+}
+
+}  // extern "C"

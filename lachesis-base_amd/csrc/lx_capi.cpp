@@ -1014,3 +1014,24 @@ int lx_sync(lx_index *h) {
 }
 
 }  // extern "C"
+
+// view for the abft engine (lx_abft.cpp); see lx_internal.h
+int lx_index_view(lx_index *h, IndexView *o) {
+    if (!h || !o) return LX_ERR_ARG;
+    if (!h->have_epoch) return h->fail(LX_ERR_STATE, "index has no epoch (lx_reset first)");
+    o->stream = h->stream;
+    o->device = h->device;
+    o->hb = h->hb;
+    o->la = h->la;
+    o->stride = h->stride;
+    o->n_events = h->n_events;
+    o->V = h->V;
+    o->B = h->B;
+    o->quorum = h->quorum;
+    o->wpad = h->wpad;
+    o->ev_branch = h->ev_branch;
+    o->weights = &h->weights;
+    o->by_creator = &h->by_creator;
+    o->shard_count = h->shard_count;
+    return 0;
+}

@@ -144,6 +144,61 @@ struct UnfillArgs {
     uint32_t B_keep;             // branches that survive the rollback
 };
 
+// ---- batched abft caller (lx_abft_kernels.hip, lx_abft.cpp)
+struct RootFcArgs {
+    const uint32_t *hb;
+    const uint32_t *la;
+    uint64_t stride;
+    const uint32_t *cand;        // candidate events (rows of bits)
+    uint32_t n_cand;
+    const uint32_t *roots;       // root events of one frame (NONE = dropped slot)
+    uint32_t n_roots;
+    uint32_t roots_fallback;     // any valid event, loaded in place of NONE / padding
+    uint32_t ncols;              // original columns scanned (V rounded up to 32)
+    const uint32_t *wpad;        // weight per column (0 outside the originals)
+    uint32_t quorum;
+    uint32_t n_k;                // cheaters' branch columns, grouped by cheater, original first
+    const uint32_t *kcol;
+    const uint32_t *kflag;       // bit0 first of its group, bit1 last
+    const uint32_t *kw;          // weight of the group's creator (on its last column)
+    const uint32_t *ev_branch;
+    uint32_t *bits;              // out: bits[c * words + r / 32]
+    uint32_t words;
+};
+
+struct QuorumArgs {
+    const uint32_t *bits;
+    uint32_t words;
+    uint32_t n_cand;
+    const uint32_t *cand;        // candidate events (their own slot is skipped)
+    const uint32_t *root_ev;     // root events of the frame
+    const uint32_t *creator;     // creator idx per root (NONE = dropped)
+    const uint32_t *dup;         // previous root of the same creator, or NONE
+    const uint32_t *wcreator;    // weight by creator idx
+    uint32_t quorum;
+    uint8_t *q;                  // out
+};
+
+constexpr uint32_t kVoteVoted = 0x80000000u, kVoteYes = 0x40000000u, kVoteDecided = 0x20000000u,
+                   kVoteNoRoot = 0x1FFFFFFFu;
+constexpr uint32_t kVoteErrMissing = 1, kVoteErrTwoRoots = 2, kVoteErrQuorum = 4;
+
+struct VoteArgs {
+    uint32_t V;
+    const uint32_t *voter_ev;    // per voter slot (NONE = skip)
+    const uint64_t *bm_off;      // voter's observed-roots bitmap (words into bm)
+    const uint32_t *bm_len;      // bits valid
+    const uint32_t *bm;
+    const uint32_t *prev_creator;  // roots of the previous frame
+    const uint32_t *prev_dup;
+    const uint32_t *prev_votes;  // [root][V]
+    const uint32_t *wcreator;
+    uint32_t quorum;
+    uint32_t *votes;             // out [voter][V]
+    unsigned long long *dec;     // per subject: min (event << 32 | yes << 31 | observed root)
+    uint32_t *err;
+};
+
 // kernel launchers (lx_kernels.hip); all enqueue on `s`
 namespace lx {
 hipError_t launch_batch_prepare(const BatchArgs &a, void *scan_tmp, size_t scan_tmp_bytes, hipStream_t s);
@@ -161,6 +216,27 @@ hipError_t launch_shard_rows(const uint32_t *ev_branch, const uint32_t *branch_c
                              uint32_t *rows, hipStream_t s);
 hipError_t launch_la_block(uint32_t *la, uint64_t stride, const uint32_t *rows, uint32_t nrows, const uint32_t *cols,
                            uint32_t ncols, uint32_t *buf, int unpack, hipStream_t s);
+hipError_t launch_root_fc(const RootFcArgs &a, bool forks, hipStream_t s);
+hipError_t launch_root_quorum(const QuorumArgs &a, hipStream_t s);
+hipError_t launch_votes(const VoteArgs &a, uint32_t n_voters, bool round1, hipStream_t s);
 hipError_t launch_copy_rows(uint32_t *dst, uint64_t dst_stride, const uint32_t *src, uint64_t src_stride,
                             uint64_t rows, uint64_t cols, hipStream_t s);
 }  // namespace lx
+
+// Read-only view of an index handle for the abft engine (lx_capi.cpp).
+#include <vector>
+struct lx_index;
+struct IndexView {
+    hipStream_t stream;
+    int device;
+    uint32_t *hb, *la;
+    uint64_t stride;
+    uint64_t n_events;
+    uint32_t V, B, quorum;
+    const uint32_t *wpad;
+    const uint32_t *ev_branch;
+    const std::vector<uint32_t> *weights;
+    const std::vector<std::vector<uint32_t>> *by_creator;
+    uint32_t shard_count;
+};
+int lx_index_view(lx_index *h, IndexView *out);

@@ -44,6 +44,20 @@ SIGNATURES = [
     ("lx_last_stats", ctypes.c_int, [vp, vp]),
     ("lx_device_planes", ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), u32p, ctypes.POINTER(vp)]),
     ("lx_sync", ctypes.c_int, [vp]),
+    # include/lachesis_abft.h
+    ("lx_abft_create", ctypes.c_int, [vp, ctypes.POINTER(vp)]),
+    ("lx_abft_destroy", None, [vp]),
+    ("lx_abft_last_error", ctypes.c_char_p, [vp]),
+    ("lx_abft_bootstrap", ctypes.c_int, [vp, ctypes.c_uint32, ctypes.c_uint32, u32p, vp]),
+    ("lx_abft_reset", ctypes.c_int, [vp, ctypes.c_uint32, ctypes.c_uint32, u32p]),
+    ("lx_abft_process_batch", ctypes.c_int, [vp, ctypes.c_uint32, u32p, u32p, u64p, u32p, u32p, u32p, u32p]),
+    ("lx_abft_build", ctypes.c_int, [vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, u32p, u32p]),
+    ("lx_abft_epoch", ctypes.c_uint32, [vp]),
+    ("lx_abft_last_decided_frame", ctypes.c_uint32, [vp]),
+    ("lx_abft_frame_roots", ctypes.c_int, [vp, ctypes.c_uint32, u32p, ctypes.c_uint32, u32p]),
+    ("lx_abft_event_frame", ctypes.c_int, [vp, ctypes.c_uint32, u32p]),
+    ("lx_abft_event_confirmed_on", ctypes.c_int, [vp, ctypes.c_uint32, u32p]),
+    ("lx_abft_last_stats", ctypes.c_int, [vp, vp]),
 ]
 
 

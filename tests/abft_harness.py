@@ -14,12 +14,18 @@ class FakeLachesis:
     """TestLachesis of abft/common_test.go:30-115 over the oracle (``index`` = a vecfc.Index
     restatement)."""
 
-    def __init__(self, weights_by_id, index=None):
-        self.store = ao.Store()
-        self.store.apply_genesis(ao.FIRST_EPOCH, pos.Validators(weights_by_id))
+    def __init__(self, weights_by_id, index=None, backend="oracle"):
         self.events = {}
-        self.index = index if index is not None else ao.DenseOracleIndex()
-        self.lch = ao.IndexedLachesis(self.store, self.events.get, self.index)
+        if backend == "gpu":
+            # the product: lachesis_hip.abft over the HIP library
+            from lachesis_hip import abft
+            self.lch = abft.IndexedLachesis(pos.Validators(weights_by_id), epoch=ao.FIRST_EPOCH)
+            self.store = self.lch.store
+        else:
+            self.store = ao.Store()
+            self.store.apply_genesis(ao.FIRST_EPOCH, pos.Validators(weights_by_id))
+            self.index = index if index is not None else ao.DenseOracleIndex()
+            self.lch = ao.IndexedLachesis(self.store, self.events.get, self.index)
         self.blocks = {}
         self.block_list = []          # (epoch, frame, atropos, cheaters, confirmed)
         self.epoch_blocks = {}
@@ -50,6 +56,25 @@ class FakeLachesis:
     def process(self, e):
         self.events[e.id] = e
         return self.lch.process(e)
+
+    def process_batch(self, events, claimed=True):
+        """GPU: one lx_abft_process_batch call; oracle: Process per event.
+        Returns (consumed, err); consumed < len(events) without error = the
+        epoch was sealed."""
+        for e in events:
+            self.events[e.id] = e
+        if hasattr(self.lch, "process_batch"):
+            return self.lch.process_batch(events, claimed)
+        epoch = self.store.get_epoch()
+        for i, e in enumerate(events):
+            if not claimed:
+                self.lch.build(e)
+            err = self.lch.process(e)
+            if err is not None:
+                return i, err
+            if self.store.get_epoch() != epoch:
+                return i + 1, None
+        return len(events), None
 
     def frame_of(self, eid):
         return self.events[eid].frame

@@ -13,7 +13,11 @@ from oracle import tdag
 
 
 def header_symbols():
-    src = open(os.path.join(ROOT, "include", "lachesis_hip.h")).read()
+    src = ""
+    for name in sorted(os.listdir(os.path.join(ROOT, "include"))):
+        if name.endswith(".h"):
+            src += open(os.path.join(ROOT, "include", name)).read()
+    # entry points (not the callback members of lx_abft_callbacks: "(*name)(")
     return sorted(set(re.findall(r"\b(lx_[a-z0-9_]+)\s*\(", src)))
 
 

@@ -1,0 +1,210 @@
+"""GPU parity of the batched abft caller (include/lachesis_abft.h) against the
+abft restatement (oracle/abft_oracle.py, itself pinned to the reference's
+abft tests by tests/test_abft_oracle.py).
+
+Bit-exact: every event's frame, root slots per frame, every block (decided
+frame, Atropos, cheaters, confirmed events in ApplyEvent order), epoch seals,
+and the event at which each sealing frame was decided.
+"""
+
+import pytest
+
+from oracle import abft_oracle as ao
+from oracle import tdag
+from oracle.tdag import SplitMix64
+from abft_harness import FakeLachesis, compare_results, mutate_validators, node_ids, topo_shuffle
+from test_abft_oracle import decode_root_name
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("case", ["classic_roots", "random_roots"])
+@pytest.mark.parametrize("batched", [False, True])
+def test_special_named_roots_gpu(golden, case, batched):
+    """TestLachesisClassicRoots / TestLachesisRandomRoots on the GPU path."""
+    c = next(x for x in golden["roots_cases"] if x["name"] == case)
+    nodes, _, names, ordered = tdag.ascii_scheme_for_each(c["scheme"])
+    t = FakeLachesis({v: 1 for v in nodes}, backend="gpu")
+    if batched:
+        consumed, err = t.process_batch(ordered, claimed=False)
+        assert err is None and consumed == len(ordered)
+    else:
+        for e in ordered:
+            t.build(e)
+            assert t.process(e) is None
+    for name, e in names.items():
+        want_frame, want_root = decode_root_name(name)
+        sp = ao.self_parent(e)
+        sp_frame = names_by_id(names)[sp].frame if sp is not None else 0
+        assert e.frame == want_frame, name
+        assert (e.frame != sp_frame) == want_root, name
+
+
+def names_by_id(names):
+    return {e.id: e for e in names.values()}
+
+
+def gen_events(weights, cheaters, events_per_node, parent_count, seed, forks=10):
+    nodes = node_ids(len(weights), seed=seed)
+    _, evs = tdag.rand_fork_dag(len(nodes), events_per_node, parent_count, cheaters=cheaters,
+                                forks_count=forks, node_ids=nodes, rng=SplitMix64(seed))
+    return nodes, evs
+
+
+def run(backend, nodes, weights, evs, mode, chunk=None, seal_every=None, mutate=False):
+    """Processes evs (frames computed by Build semantics) and returns the
+    observable results."""
+    t = FakeLachesis(dict(zip(nodes, weights)), backend=backend)
+    sealed_at = []
+    if seal_every:
+        def apply_block(block):
+            if t.store.last_decided_frame + 1 == seal_every:
+                v = t.store.get_validators()
+                return mutate_validators(v) if mutate else v
+            return None
+        t.apply_block = apply_block
+    frames = {}
+    i = 0
+    epoch0 = t.store.get_epoch()
+    while i < len(evs):
+        if mode == "event":
+            part = evs[i:i + 1]
+        else:
+            part = evs[i:i + (chunk or len(evs))]
+        for e in part:
+            e.frame = 0
+        consumed, err = t.process_batch(part, claimed=False)
+        assert err is None, err
+        for e in part[:consumed]:
+            frames[e.id] = e.frame
+        i += consumed
+        if t.store.get_epoch() != epoch0:
+            sealed_at.append(part[consumed - 1].id)
+            break
+    return dict(frames=frames, blocks=list(t.block_list), sealed_at=sealed_at,
+                last=(t.store.get_epoch(), t.store.last_decided_frame))
+
+
+SHAPES = [
+    # (weights, cheaters, events/node, parents, seed)
+    ([1, 1, 1, 1], 0, 40, 3, 1),
+    ([1, 2, 3, 4], 0, 40, 4, 2),
+    ([11, 11, 11, 67], 0, 40, 4, 3),
+    ([1] * 10, 0, 30, 5, 4),
+    ([1, 1, 1, 1], 1, 40, 3, 5),
+    ([1, 2, 1, 2, 1, 2, 1, 2, 1, 2], 3, 30, 5, 6),
+    ([0xFFFFFFFF // 8, 0xFFFFFFFF // 8, 0xFFFFFFFF // 4], 0, 40, 3, 7),
+    ([5 + (i % 7) for i in range(40)], 4, 15, 8, 8),
+]
+
+
+@pytest.mark.parametrize("shape", SHAPES, ids=[str(i) for i in range(len(SHAPES))])
+def test_abft_matches_oracle(shape):
+    weights, cheaters, epn, pc, seed = shape
+    nodes, evs = gen_events(weights, cheaters, epn, pc, seed)
+    ref = run("oracle", nodes, weights, evs, "event")
+    assert len(ref["blocks"]) >= 3
+    for mode, chunk in (("event", None), ("batch", None), ("batch", 7), ("batch", 64)):
+        got = run("gpu", nodes, weights, evs, mode, chunk)
+        assert got["frames"] == ref["frames"], (mode, chunk)
+        assert got["blocks"] == ref["blocks"], (mode, chunk)
+        assert got["last"] == ref["last"], (mode, chunk)
+
+
+@pytest.mark.parametrize("mutate", [False, True])
+def test_abft_seal_matches_oracle(mutate):
+    """Epoch sealed by EndBlock: same sealing event, same blocks, validators
+    mutated or not (frame_decide.go:11-58)."""
+    weights = [1, 2, 1, 2, 1, 2, 1, 2, 1, 2]
+    nodes, evs = gen_events(weights, 0, 60, 5, 11)
+    ref = run("oracle", nodes, weights, evs, "event", seal_every=3, mutate=mutate)
+    assert ref["sealed_at"]
+    for chunk in (None, 50):
+        got = run("gpu", nodes, weights, evs, "batch", chunk, seal_every=3, mutate=mutate)
+        assert got["sealed_at"] == ref["sealed_at"]
+        assert got["blocks"] == ref["blocks"]
+        assert got["last"] == ref["last"]
+        assert got["frames"] == ref["frames"]
+
+
+def test_abft_three_instances_reordered_gpu():
+    """testLachesisRandomAndReset's consensus check on the GPU path: three
+    instances, different topological orders (one batched), equal blocks over
+    several sealed epochs."""
+    weights = [1, 2, 1, 2, 1, 2, 1, 2, 1, 2]
+    nodes = node_ids(len(weights), seed=77)
+    wmap = dict(zip(nodes, weights))
+    lchs = [FakeLachesis(wmap, backend="gpu") for _ in range(3)]
+    max_blocks = 5
+    for lch in lchs:
+        def apply_block(block, lch=lch):
+            if lch.store.last_decided_frame + 1 == max_blocks:
+                return lch.store.get_validators()
+            return None
+        lch.apply_block = apply_block
+    rng = SplitMix64(1234)
+    ordered = {}
+    for epoch in (1, 2, 3):
+        out = []
+
+        def build(e):
+            if lchs[0].store.get_epoch() != epoch:
+                return False
+            lchs[0].build(e)
+            assert lchs[0].process(e) is None
+            out.append(e)
+            return True
+        tdag.rand_fork_dag(len(nodes), 100, 5, cheaters=3, forks_count=10, node_ids=nodes, rng=rng, build=build,
+                           eid_base=epoch * 10**6)
+        ordered[epoch] = out
+        assert lchs[0].store.get_epoch() == epoch + 1
+    for epoch in (1, 2, 3):
+        for k, lch in enumerate(lchs[1:]):
+            evs = topo_shuffle(ordered[epoch], rng)
+            if k == 0:
+                for e in evs:
+                    assert lch.process(e) is None
+                    if lch.store.get_epoch() != epoch:
+                        break
+            else:
+                consumed, err = lch.process_batch(evs)
+                assert err is None
+            assert lch.store.get_epoch() == epoch + 1
+    compare_results(lchs)
+
+
+def test_abft_wrong_frame_gpu():
+    """checkAndSaveEvent: a wrong claimed frame is rejected (ErrWrongFrame),
+    the events before it are processed, the event is dropped from the index."""
+    weights = [1, 1, 1, 1]
+    nodes, evs = gen_events(weights, 0, 30, 3, 21)
+    ref = run("oracle", nodes, weights, evs, "event")
+    t = FakeLachesis(dict(zip(nodes, weights)), backend="gpu")
+    good = [ref["frames"][e.id] for e in evs]
+    bad = next(i for i, e in enumerate(evs) if i > 40 and ao.self_parent(e) is not None)
+    for e, f in zip(evs, good):
+        e.frame = f
+    evs[bad].frame = good[bad] + 1
+    consumed, err = t.process_batch(evs)
+    assert consumed == bad and err is not None
+    evs[bad].frame = good[bad]
+    consumed2, err = t.process_batch(evs[bad:])
+    assert err is None and consumed2 == len(evs) - bad
+    assert t.block_list == ref["blocks"]
+
+
+def test_abft_build_gpu():
+    """Build sets the frame of a self-emitted event without adding it."""
+    weights = [1, 1, 1, 1, 1]
+    nodes, evs = gen_events(weights, 0, 20, 4, 31)
+    o = FakeLachesis(dict(zip(nodes, weights)))
+    g = FakeLachesis(dict(zip(nodes, weights)), backend="gpu")
+    for e in evs:
+        o.build(e)
+        f = e.frame
+        e.frame = 0
+        g.build(e)
+        assert e.frame == f
+        assert o.process(e) is None
+        assert g.process(e) is None
+    assert g.block_list == o.block_list
