@@ -93,6 +93,69 @@ def cpu_baseline(dag, weights, n_events_max, fc_n, budget_s):
     return done, t_add, fc_n, t_fc
 
 
+ABFT_CONFIG = ("c5", 1000, 50, 10, "zipf")   # BASELINE configs[4]: V, events/validator, parents, stakes
+
+
+def abft_leg(lx, steps, warmup, device, cpu_budget, want_cpu):
+    """BASELINE configs[4]: full abft.IndexedLachesis.Process over one epoch --
+    index Add, frames and roots (batched root ForklessCause tiles), election
+    (vote kernels), blocks (cheaters, confirmation DFS) -- through
+    lx_abft_process_batch with the events' claimed frames.  A step = reset +
+    the whole 50k-event epoch in one batch (host arrays in, so the PCIe copy
+    of the batch, ~44 B/event, is inside the step)."""
+    import numpy as np
+    name, V, epv, P, wkind = ABFT_CONFIG
+    weights = weights_for(V, wkind)
+    dag = lx.tools.gen_dag(V, epv, P, 0, 0, seed=1)
+    N = len(dag)
+    lch = lx.abft.DenseLachesis(weights, device=device, event_capacity=N, apply_events=False)
+    rc, consumed, frames = lch.process_batch(dag.creator, dag.seq, dag.poff, dag.par)   # Build-path frames
+    assert rc == 0 and consumed == N
+    claimed = frames.copy()
+    n_blocks = len(lch.blocks)
+
+    def step():
+        lch.L.lx_abft_reset(lch.h, 1, V, np.ascontiguousarray(weights, dtype=np.uint32).ctypes.data_as(
+            lx.capi.u32p))
+        lch.blocks = []
+        rc, consumed, out = lch.process_batch(dag.creator, dag.seq, dag.poff, dag.par, claimed)
+        assert rc == 0 and consumed == N and len(lch.blocks) == n_blocks
+        return lch.last_stats()
+
+    for _ in range(warmup):
+        step()
+    t0 = time.perf_counter()
+    stats = [step() for _ in range(steps)]
+    dt = (time.perf_counter() - t0) / steps
+    st = {k: float(np.mean([s[k] for s in stats])) for k in stats[0]}
+    res = {"workload": "%s: V=%d, %d events (%d/validator), P=%d, %s stakes, no cheaters; one epoch per step, "
+                       "claimed frames checked" % (name, V, N, epv, P, wkind),
+           "events": N, "events_per_sec": N / dt, "ms_per_step": dt * 1e3, "blocks_decided": n_blocks,
+           "max_frame": int(claimed.max()), "phase_ms": {k: st[k] for k in ("ms_index", "ms_frames", "ms_election", "ms_blocks")},
+           "frame_steps": st["frame_steps"], "fc_launches": st["fc_launches"], "vote_launches": st["vote_launches"],
+           "root_fc_pairs": st["fc_pairs"]}
+    lch.close()
+    if want_cpu:
+        from oracle import corc
+        n = min(N, 3000)
+        o = corc.AbftOracle(weights)
+        t1 = time.perf_counter()
+        done = 0
+        while done < n and time.perf_counter() - t1 < cpu_budget:
+            hi = min(n, done + 250)
+            rc, c, _ = o.process_batch(dag.creator[done:hi], dag.seq[done:hi], dag.poff[done:hi + 1], dag.par,
+                                       claimed[done:hi])
+            assert rc == 0 and c == hi - done
+            done = hi
+        t_cpu = time.perf_counter() - t1
+        res["cpu_baseline"] = {
+            "value": done / t_cpu, "unit": "events/s", "cores": 1, "kind": "port",
+            "sample": "first %d events of the same epoch through the C abft restatement (oracle/csrc/abft_oracle.c "
+                      "over oracle.c: per-event Add with DFS LowestAfter, calcFrameIdx with early exit, per-root "
+                      "election) in %.1fs" % (done, t_cpu)}
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -104,6 +167,7 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--mode", default="shard", choices=["replica", "shard"])
+    ap.add_argument("--no-abft", action="store_true", help="skip the configs[4] abft leg")
     args = ap.parse_args()
 
     import numpy as np
@@ -287,6 +351,14 @@ def main():
                            "algorithmic_bytes_per_launch": idx_bytes, "kernel_ms": kidx},
         "host_gen_s": t_gen,
     }
+
+    if not args.no_abft:
+        ab = abft_leg(lx, args.steps, args.warmup, local, args.cpu_budget, rank == 0 and not args.no_cpu)
+        barrier()
+        ab["ms_per_step"] = max_over_ranks(ab["ms_per_step"])   # replicas: one epoch per rank
+        ab["events_per_sec"] = ab["events"] * world / (ab["ms_per_step"] * 1e-3)
+        ab["parallelism"] = "replica%d" % world
+        result["abft"] = ab
 
     if rank == 0 and not args.no_cpu:
         sample_max = N

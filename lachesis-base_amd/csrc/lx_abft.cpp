@@ -49,6 +49,7 @@ namespace {
 constexpr uint32_t NONE = LX_NONE;
 constexpr uint32_t kSpecDepth = 4;      // self-children evaluated ahead per launch
 constexpr uint32_t kBuildCap = 100;     // calcFrameIdx: selfParentFrame + 100 in Build
+constexpr uint32_t kVoteWindow = 64;    // subjects voted on first (chooseAtropos walks idx order)
 
 template <typename T>
 struct DVec {
@@ -115,6 +116,7 @@ struct lx_abft {
     uint32_t k_B = NONE;                // branch count the cheater columns were built for
     std::vector<uint32_t> h_row;
     bool dec_dirty = true;
+    uint32_t vw = 0;                    // subject window [0, vw) of the current election
 
     lx_abft_stats stats{};
 
@@ -431,15 +433,16 @@ int compute_frames(lx_abft *a, uint64_t base, uint32_t n, const uint32_t *creato
 
 // ---------------------------------------------------------------------------- election
 
-int vote_frame(lx_abft *a, const IndexView &iv, uint32_t F, uint32_t g) {
+// votes of slots [from, to) of frame g for subjects [v_lo, v_hi) (round g - F)
+int vote_slots(lx_abft *a, const IndexView &iv, uint32_t F, uint32_t g, uint32_t from, uint32_t to, uint32_t v_lo,
+               uint32_t v_hi) {
     hipStream_t s = iv.stream;
+    if (from >= to || v_lo >= v_hi) return 0;
     Frame &fg = frame_at(a, g);
     Frame &fp = frame_at(a, g - 1);
     ARC(sync_frame(a, fg, s));
     ARC(sync_frame(a, fp, s));
-    const uint32_t from = fg.voted, to = (uint32_t)fg.ev.size();
-    if (from == to) return 0;
-    ARC(reserve(a, fg.votes, (uint64_t)to * a->V, (uint64_t)from * a->V, s));
+    ARC(reserve(a, fg.votes, (uint64_t)fg.ev.size() * a->V, (uint64_t)fg.voted * a->V, s));
     VoteArgs v{};
     v.V = a->V;
     v.voter_ev = fg.d_ev.p + from;
@@ -449,22 +452,46 @@ int vote_frame(lx_abft *a, const IndexView &iv, uint32_t F, uint32_t g) {
     v.prev_creator = fp.d_creator.p;
     v.prev_dup = fp.d_dup.p;
     v.prev_votes = fp.votes.p;
+    v.prev_has_dup = std::any_of(fp.dup.begin(), fp.dup.end(), [](uint32_t d) { return d != NONE; }) ? 1u : 0u;
+    v.v_lo = v_lo;
+    v.v_hi = v_hi;
     v.wcreator = iv.wpad;
     v.quorum = a->quorum;
     v.votes = fg.votes.p + (uint64_t)from * a->V;
     v.dec = a->d_dec.p;
     v.err = a->d_err.p;
     AHIP(a, lx::launch_votes(v, to - from, g == F + 1, s));
-    fg.voted = to;
     a->stats.vote_launches++;
     return 0;
 }
 
-// decision of election F: 0 pending, 1 decided (*t, *atropos slot)
+// new slots of frame g, current subject window
+int vote_frame(lx_abft *a, const IndexView &iv, uint32_t F, uint32_t g) {
+    Frame &fg = frame_at(a, g);
+    const uint32_t from = fg.voted, to = (uint32_t)fg.ev.size();
+    if (from == to) return 0;
+    ARC(vote_slots(a, iv, F, g, from, to, 0, a->vw));
+    a->frames[g].voted = to;
+    return 0;
+}
+
+// widen the subject window of election F to [0, nw) for every voted slot
+int widen_window(lx_abft *a, const IndexView &iv, uint32_t F, uint32_t nw) {
+    for (uint32_t g = F + 1; g < a->frames.size(); g++) {
+        const uint32_t voted = a->frames[g].voted;
+        if (!voted) break;
+        ARC(vote_slots(a, iv, F, g, 0, voted, a->vw, nw));
+    }
+    a->vw = nw;
+    return 0;
+}
+
+// decision of election F: 0 pending, 1 decided (*t, *atropos slot),
+// 2 every subject of the window decided "no" (widen it)
 int check_decision(lx_abft *a, const IndexView &iv, uint32_t F, uint64_t *t, uint32_t *obs, int *state) {
-    std::vector<unsigned long long> dec(a->V);
+    std::vector<unsigned long long> dec(a->vw);
     uint32_t err = 0;
-    AHIP(a, hipMemcpyAsync(dec.data(), a->d_dec.p, a->V * 8ull, hipMemcpyDeviceToHost, iv.stream));
+    AHIP(a, hipMemcpyAsync(dec.data(), a->d_dec.p, a->vw * 8ull, hipMemcpyDeviceToHost, iv.stream));
     AHIP(a, hipMemcpyAsync(&err, a->d_err.p, 4, hipMemcpyDeviceToHost, iv.stream));
     AHIP(a, hipStreamSynchronize(iv.stream));
     if (err & kVoteErrTwoRoots)
@@ -475,7 +502,7 @@ int check_decision(lx_abft *a, const IndexView &iv, uint32_t F, uint64_t *t, uin
         return a->fail(LX_ERR_BYZANTINE, "every root must vote for every not decided subject (election frame=%u)", F);
     *state = 0;
     uint64_t tmax = 0;
-    for (uint32_t v = 0; v < a->V; v++) {   // chooseAtropos: SortedIDs = idx order
+    for (uint32_t v = 0; v < a->vw; v++) {   // chooseAtropos: SortedIDs = idx order
         if (dec[v] == ~0ull) return 0;
         tmax = std::max<uint64_t>(tmax, dec[v] >> 32);
         if (dec[v] & 0x80000000ull) {
@@ -484,6 +511,10 @@ int check_decision(lx_abft *a, const IndexView &iv, uint32_t F, uint64_t *t, uin
             *state = 1;
             return 0;
         }
+    }
+    if (a->vw < a->V) {
+        *state = 2;
+        return 0;
     }
     return a->fail(LX_ERR_BYZANTINE, "all the roots are decided as 'no', which is possible only if more than 1/3W are Byzantine");
 }
@@ -494,6 +525,7 @@ int reset_election(lx_abft *a, const IndexView &iv) {
     AHIP(a, hipMemsetAsync(a->d_dec.p, 0xFF, a->V * 8ull, iv.stream));
     AHIP(a, hipMemsetAsync(a->d_err.p, 0, 4, iv.stream));
     for (uint32_t g = a->last_decided + 1; g < a->frames.size(); g++) a->frames[g].voted = 0;
+    a->vw = std::min<uint32_t>(a->V, kVoteWindow);
     a->dec_dirty = false;
     return 0;
 }
@@ -557,6 +589,10 @@ int run_elections(lx_abft *a, uint64_t *sealed_at, std::vector<uint32_t> *new_w)
             ARC(vote_frame(a, iv, F, g));
             if (g < F + 2 || (checked && !fresh)) continue;
             ARC(check_decision(a, iv, F, &t, &obs, &state));
+            while (state == 2) {   // all subjects so far decided "no": the Atropos is further down
+                ARC(widen_window(a, iv, F, std::min<uint32_t>(a->V, a->vw * 2)));
+                ARC(check_decision(a, iv, F, &t, &obs, &state));
+            }
             checked = true;
             if (state) {
                 // final unless a slot not yet voted in this election is older

@@ -204,10 +204,15 @@ hipError_t launch_root_quorum(const QuorumArgs &a, hipStream_t s) {
 
 // ---------------------------------------------------------------------------- votes
 // vote word: bit31 voted, bit30 yes, bit29 decided, bits 0..28 observed root
-// (index into the frame-to-decide's root list; kVoteNoRoot = none)
-__global__ void k_vote_init(uint32_t *votes, uint64_t n) {
+// (index into the frame-to-decide's root list; kVoteNoRoot = none).
+// Votes of different subjects never mix (election_math.go:53-110 reads only
+// votes for the same subject), so each launch computes a subject window
+// [v_lo, v_hi); the host widens the window only while chooseAtropos needs it.
+__global__ void k_vote_init(VoteArgs a, uint32_t n_voters) {
+    const uint32_t w = a.v_hi - a.v_lo;
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) votes[i] = kVoteVoted | kVoteNoRoot;
+    if (i < (uint64_t)n_voters * w)
+        a.votes[(i / w) * a.V + a.v_lo + i % w] = kVoteVoted | kVoteNoRoot;
 }
 
 // round 1 (election_math.go:40-52): yes iff the voter forkless-causes the
@@ -221,18 +226,20 @@ __global__ void k_vote_round1(VoteArgs a) {
     for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < len; r += gridDim.x * blockDim.x) {
         if (!((a.bm[off + (r >> 5)] >> (r & 31)) & 1u)) continue;
         const uint32_t c = a.prev_creator[r];
-        if (c == LX_NONE) continue;
+        if (c < a.v_lo || c >= a.v_hi) continue;
         atomicMax(&a.votes[(uint64_t)s * a.V + c], kVoteVoted | kVoteYes | r);
     }
 }
 
-// round >= 2 (election_math.go:53-110): one thread per (voter slot, subject);
-// the voter's observed-root bitmap is uniform across the workgroup.
-__global__ __launch_bounds__(256) void k_vote_round(VoteArgs a) {
-    const uint32_t s = blockIdx.y;
-    const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+// round >= 2 (election_math.go:53-110): one lane per (voter slot, subject),
+// a wave = 64 subjects of one voter, so the voter's observed-root bitmap and
+// the observed root's creator and weight are wave-uniform.
+__global__ __launch_bounds__(256) void k_vote_round(VoteArgs a, uint32_t n_voters) {
+    const uint32_t s = blockIdx.y * 4 + threadIdx.y;
+    const uint32_t v = a.v_lo + blockIdx.x * 64 + threadIdx.x;
+    if (s >= n_voters) return;
     const uint32_t vev = a.voter_ev[s];
-    if (vev == LX_NONE || v >= a.V) return;
+    if (vev == LX_NONE || v >= a.v_hi) return;
     const uint64_t off = a.bm_off[s];
     const uint32_t len = a.bm_len[s];
     uint32_t yes = 0, no = 0, all = 0, subj = kVoteNoRoot, err = 0;
@@ -244,9 +251,9 @@ __global__ __launch_bounds__(256) void k_vote_round(VoteArgs a) {
             m &= m - 1;
             const uint32_t r = wi * 32 + b;
             const uint32_t c = a.prev_creator[r];
-            if (c == LX_NONE) continue;
-            for (uint32_t d = a.prev_dup[r]; d != LX_NONE; d = a.prev_dup[d])
-                if ((a.bm[off + (d >> 5)] >> (d & 31)) & 1u) err |= kVoteErrTwoRoots;   // allVotes.Count == false
+            if (a.prev_has_dup)
+                for (uint32_t d = a.prev_dup[r]; d != LX_NONE; d = a.prev_dup[d])
+                    if ((a.bm[off + (d >> 5)] >> (d & 31)) & 1u) err |= kVoteErrTwoRoots;   // allVotes.Count == false
             const uint32_t pv = a.prev_votes[(uint64_t)r * a.V + v];
             const uint32_t wc = a.wcreator[c];
             if (!(pv & kVoteVoted)) err |= kVoteErrMissing;
@@ -272,13 +279,14 @@ __global__ __launch_bounds__(256) void k_vote_round(VoteArgs a) {
 }
 
 hipError_t launch_votes(const VoteArgs &a, uint32_t n_voters, bool round1, hipStream_t s) {
-    if (!n_voters) return hipSuccess;
-    const uint64_t n = (uint64_t)n_voters * a.V;
-    hipLaunchKernelGGL(k_vote_init, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, a.votes, n);
+    if (!n_voters || a.v_hi <= a.v_lo) return hipSuccess;
+    const uint32_t w = a.v_hi - a.v_lo;
+    const uint64_t n = (uint64_t)n_voters * w;
+    hipLaunchKernelGGL(k_vote_init, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, a, n_voters);
     if (round1) {
-        hipLaunchKernelGGL(k_vote_round1, dim3(4, n_voters), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(k_vote_round1, dim3(2, n_voters), dim3(256), 0, s, a);
     } else {
-        hipLaunchKernelGGL(k_vote_round, dim3((a.V + 255) / 256, n_voters), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(k_vote_round, dim3((w + 63) / 64, (n_voters + 3) / 4), dim3(64, 4), 0, s, a, n_voters);
     }
     return hipGetLastError();
 }

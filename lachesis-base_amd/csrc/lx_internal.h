@@ -192,6 +192,8 @@ struct VoteArgs {
     const uint32_t *prev_creator;  // roots of the previous frame
     const uint32_t *prev_dup;
     const uint32_t *prev_votes;  // [root][V]
+    uint32_t prev_has_dup;       // some validator has two roots in the previous frame
+    uint32_t v_lo, v_hi;         // subject window
     const uint32_t *wcreator;
     uint32_t quorum;
     uint32_t *votes;             // out [voter][V]

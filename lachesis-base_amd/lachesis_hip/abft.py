@@ -274,3 +274,92 @@ class IndexedLachesis:
         st = AbftStats()
         self._chk(self.L.lx_abft_last_stats(self.h, ctypes.byref(st)))
         return {f: getattr(st, f) for f, _ in AbftStats._fields_}
+
+
+class DenseLachesis:
+    """Dense-index handle over lx_abft_* (what a cgo shim binds 1:1): events
+    are Add-order indices of the current epoch, validators are idx-ordered
+    weights.  Records blocks as (epoch, frame, atropos, cheaters, confirmed);
+    ``apply_events=False`` skips the per-event ApplyEvent callback (the
+    confirmation DFS still runs; GetEventConfirmedOn still answers).
+    ``seal(epoch, frame)`` may return the next epoch's weights."""
+
+    def __init__(self, weights, epoch=1, device=0, event_capacity=0, apply_events=True, seal=None):
+        self.ix = Index(device=device, event_capacity=event_capacity)
+        self.L = self.ix.L
+        h = vp()
+        rc = self.L.lx_abft_create(self.ix.h, ctypes.byref(h))
+        if rc != 0:
+            raise LxError(rc, "lx_abft_create failed")
+        self.h = h
+        self.blocks = []
+        self.seal = seal
+        self._cur = None
+        self._seal_w = None
+        self._cb = Callbacks(None, BEGIN_BLOCK(self._begin), APPLY_EVENT(self._apply) if apply_events else APPLY_EVENT(),
+                             END_BLOCK(self._end))
+        w = np.ascontiguousarray(weights, dtype=np.uint32)
+        rc = self.L.lx_abft_bootstrap(self.h, epoch, len(w), _p(w, u32p), ctypes.byref(self._cb))
+        if rc != 0:
+            raise LxError(rc, self.L.lx_abft_last_error(self.h).decode())
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.lx_abft_destroy(self.h)
+            self.h = None
+        if getattr(self, "ix", None) is not None:
+            self.ix.close()
+
+    __del__ = close
+
+    def _begin(self, user, frame, atropos, cheaters, n):
+        self._cur = [self.epoch(), frame, atropos, tuple(cheaters[k] for k in range(n)), []]
+
+    def _apply(self, user, ev):
+        self._cur[4].append(ev)
+
+    def _end(self, user, n_out, w_out):
+        b = self._cur
+        self.blocks.append((b[0], b[1], b[2], b[3], tuple(b[4])))
+        nw = self.seal(b[0], b[1]) if self.seal else None
+        if nw is None:
+            return 0
+        self._seal_w = np.ascontiguousarray(nw, dtype=np.uint32)
+        n_out[0] = len(self._seal_w)
+        w_out[0] = self._seal_w.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
+        return 1
+
+    def process_batch(self, creator, seq, poff, par, claimed=None):
+        """Returns (rc, consumed, frames)."""
+        creator = np.ascontiguousarray(creator, dtype=np.uint32)
+        seq = np.ascontiguousarray(seq, dtype=np.uint32)
+        poff = np.ascontiguousarray(poff, dtype=np.uint64)
+        par = np.ascontiguousarray(par if len(par) else [0], dtype=np.uint32)
+        n = len(creator)
+        out = np.zeros(n, dtype=np.uint32)
+        cl = None if claimed is None else np.ascontiguousarray(claimed, dtype=np.uint32)
+        consumed = ctypes.c_uint32()
+        rc = self.L.lx_abft_process_batch(self.h, n, _p(creator, u32p), _p(seq, u32p), _p(poff, u64p),
+                                          _p(par, u32p), None if cl is None else _p(cl, u32p), _p(out, u32p),
+                                          ctypes.byref(consumed))
+        if rc not in (0, ERR_FRAME):
+            raise LxError(rc, self.L.lx_abft_last_error(self.h).decode())
+        return rc, consumed.value, out
+
+    def epoch(self):
+        return self.L.lx_abft_epoch(self.h)
+
+    def last_decided_frame(self):
+        return self.L.lx_abft_last_decided_frame(self.h)
+
+    def frame_roots(self, f):
+        n = ctypes.c_uint32()
+        self.L.lx_abft_frame_roots(self.h, f, None, 0, ctypes.byref(n))
+        out = np.zeros(max(n.value, 1), dtype=np.uint32)
+        self.L.lx_abft_frame_roots(self.h, f, _p(out, u32p), n.value, ctypes.byref(n))
+        return out[:n.value]
+
+    def last_stats(self):
+        st = AbftStats()
+        self.L.lx_abft_last_stats(self.h, ctypes.byref(st))
+        return {f: getattr(st, f) for f, _ in AbftStats._fields_}

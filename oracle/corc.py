@@ -45,6 +45,19 @@ def lib():
             f.argtypes = [ctypes.c_void_p, ctypes.c_uint32, u8p, ctypes.c_uint32, u32p]
         L.orc_forkless_cause.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32]
         L.orc_forkless_cause_batch.argtypes = [ctypes.c_void_p, ctypes.c_uint64, u32p, u32p, u8p]
+        # abft_oracle.c
+        L.abo_create.restype = ctypes.c_void_p
+        L.abo_create.argtypes = [ctypes.c_uint32, ctypes.c_uint32, u32p, ctypes.c_void_p]
+        L.abo_destroy.argtypes = [ctypes.c_void_p]
+        L.abo_process_batch.argtypes = [ctypes.c_void_p, ctypes.c_uint32, u32p, u32p, u64p, u32p, u32p, u32p, u32p]
+        L.abo_build.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, u32p, u32p]
+        for f in (L.abo_epoch, L.abo_last_decided_frame, L.abo_num_events):
+            f.restype = ctypes.c_uint32
+            f.argtypes = [ctypes.c_void_p]
+        L.abo_event_frame.restype = ctypes.c_uint32
+        L.abo_event_frame.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
+        L.abo_frame_roots.restype = ctypes.c_uint32
+        L.abo_frame_roots.argtypes = [ctypes.c_void_p, ctypes.c_uint32, u32p, ctypes.c_uint32]
         _lib = L
     return _lib
 
@@ -122,3 +135,76 @@ class OracleIndex:
         out = np.zeros(len(a), dtype=np.uint8)
         self.L.orc_forkless_cause_batch(self.h, len(a), _p(a, u32p), _p(b, u32p), _p(out, u8p))
         return out
+
+
+_BEGIN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, u32p, ctypes.c_uint32)
+_APPLY = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_uint32)
+_END = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, u32p, ctypes.POINTER(u32p))
+
+
+class _Cb(ctypes.Structure):
+    _fields_ = [("user", ctypes.c_void_p), ("begin_block", _BEGIN), ("apply_event", _APPLY), ("end_block", _END)]
+
+
+class AbftOracle:
+    """Dense-index C restatement of abft.IndexedLachesis (abft_oracle.c), with
+    the batch semantics of lx_abft_process_batch.  Records every block as
+    (epoch, frame, atropos, cheaters, confirmed events); ``seal(epoch, frame)``
+    may return new weights (idx order) to seal the epoch."""
+
+    def __init__(self, weights, epoch=1, seal=None):
+        self.L = lib()
+        self.blocks = []
+        self.seal = seal
+        self._cur = None
+        self._keep_w = None
+        self._cb = _Cb(None, _BEGIN(self._begin), _APPLY(self._apply), _END(self._end))
+        w = np.ascontiguousarray(weights, dtype=np.uint32)
+        self.h = self.L.abo_create(epoch, len(w), _p(w, u32p), ctypes.cast(ctypes.pointer(self._cb), ctypes.c_void_p))
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            self.L.abo_destroy(self.h)
+            self.h = None
+
+    def _begin(self, user, frame, atropos, cheaters, n):
+        self._cur = [self.epoch(), frame, atropos, tuple(cheaters[k] for k in range(n)), []]
+
+    def _apply(self, user, ev):
+        self._cur[4].append(ev)
+
+    def _end(self, user, n_out, w_out):
+        b = self._cur
+        self.blocks.append((b[0], b[1], b[2], b[3], tuple(b[4])))
+        nw = self.seal(b[0], b[1]) if self.seal else None
+        if nw is None:
+            return 0
+        self._keep_w = np.ascontiguousarray(nw, dtype=np.uint32)
+        n_out[0] = len(self._keep_w)
+        w_out[0] = _p(self._keep_w, u32p)
+        return 1
+
+    def process_batch(self, creator, seq, poff, par, claimed=None):
+        creator = np.ascontiguousarray(creator, dtype=np.uint32)
+        seq = np.ascontiguousarray(seq, dtype=np.uint32)
+        poff = np.ascontiguousarray(poff, dtype=np.uint64)
+        par = np.ascontiguousarray(par if len(par) else [0], dtype=np.uint32)
+        n = len(creator)
+        out = np.zeros(n, dtype=np.uint32)
+        cl = None if claimed is None else np.ascontiguousarray(claimed, dtype=np.uint32)
+        consumed = ctypes.c_uint32()
+        rc = self.L.abo_process_batch(self.h, n, _p(creator, u32p), _p(seq, u32p), _p(poff, u64p), _p(par, u32p),
+                                      None if cl is None else _p(cl, u32p), _p(out, u32p), ctypes.byref(consumed))
+        return rc, consumed.value, out
+
+    def epoch(self):
+        return self.L.abo_epoch(self.h)
+
+    def last_decided_frame(self):
+        return self.L.abo_last_decided_frame(self.h)
+
+    def frame_roots(self, f):
+        n = self.L.abo_frame_roots(self.h, f, None, 0)
+        out = np.zeros(max(n, 1), dtype=np.uint32)
+        self.L.abo_frame_roots(self.h, f, _p(out, u32p), n)
+        return out[:n]

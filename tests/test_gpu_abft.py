@@ -208,3 +208,44 @@ def test_abft_build_gpu():
         assert o.process(e) is None
         assert g.process(e) is None
     assert g.block_list == o.block_list
+
+
+def load_golden(name):
+    import os
+    import numpy as np
+    return np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "abft_%s.npz" % name))
+
+
+def blocks_of(g):
+    out = []
+    for k in range(len(g["block_frame"])):
+        ch = g["cheaters"][g["cheaters_off"][k]:g["cheaters_off"][k + 1]]
+        cf = g["confirmed"][g["confirmed_off"][k]:g["confirmed_off"][k + 1]]
+        out.append((1, int(g["block_frame"][k]), int(g["block_atropos"][k]), tuple(map(int, ch)),
+                    tuple(map(int, cf))))
+    return out
+
+
+@pytest.mark.parametrize("name,chunks", [("c4", 1), ("c4", 7), ("c5", 1), ("c5", 3)])
+def test_abft_full_size_vs_oracle(name, chunks):
+    """BASELINE configs 4 (100 validators, 10 % double-signers, 100k events)
+    and 5 (1000 validators, Zipf stakes, 50k events) at full size: frames of
+    every event, roots per frame and every block (Atropos, cheaters, ApplyEvent
+    order) equal the C abft restatement's (tests/golden/make_abft_golden.py),
+    whole epoch in one batch or in chunks."""
+    import numpy as np
+    from lachesis_hip import abft, tools
+    g = load_golden(name)
+    V, epn, P, ch, fk, seed = map(int, g["config"])
+    d = tools.gen_dag(V, epn, P, cheaters=ch, forks=fk, seed=seed)
+    lch = abft.DenseLachesis(g["weights"], event_capacity=len(d))
+    frames = np.zeros(len(d), dtype=np.uint32)
+    bounds = np.linspace(0, len(d), chunks + 1).astype(np.int64)
+    for lo, hi in zip(bounds[:-1], bounds[1:]):
+        c, s, off, par = d.slice(lo, hi)
+        rc, consumed, out = lch.process_batch(c, s, off, par)
+        assert rc == 0 and consumed == hi - lo
+        frames[lo:hi] = out
+    assert np.array_equal(frames, g["frames"])
+    assert [len(lch.frame_roots(f)) for f in range(len(g["roots_per_frame"]))] == list(g["roots_per_frame"])
+    assert lch.blocks == blocks_of(g)

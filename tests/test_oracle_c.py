@@ -92,3 +92,46 @@ def test_c_oracle_golden(golden):
         for who, e1 in names.items():
             for whom, e2 in names.items():
                 assert c.forkless_cause(posn[e1.id], posn[e2.id]) == (whom in case["fc"][who])
+
+
+# ---------------------------------------------------------------------------- abft
+from oracle import abft_oracle as ao  # noqa: E402
+from abft_harness import FakeLachesis, node_ids  # noqa: E402
+from oracle.tdag import SplitMix64  # noqa: E402
+
+
+@pytest.mark.parametrize("shape", [([1, 1, 1, 1], 1, 40, 3, 1), ([1, 2, 3, 4, 5], 0, 40, 4, 2),
+                                   ([1, 2, 1, 2, 1, 2, 1, 2, 1, 2], 3, 30, 5, 3),
+                                   ([5 + (i % 7) for i in range(30)], 4, 12, 6, 4)])
+@pytest.mark.parametrize("seal", [None, 3])
+def test_abft_c_matches_python(shape, seal):
+    """abft_oracle.c == abft_oracle.py: frames, roots, blocks (Atropos,
+    cheaters, ApplyEvent order), epoch seal point."""
+    weights, cheaters, epn, pc, seed = shape
+    nodes = node_ids(len(weights), seed=seed)
+    _, evs = tdag.rand_fork_dag(len(nodes), epn, pc, cheaters=cheaters, forks_count=10, node_ids=nodes,
+                                rng=SplitMix64(seed))
+    t = FakeLachesis(dict(zip(nodes, weights)))
+    if seal:
+        t.apply_block = lambda b: t.store.get_validators() if t.store.last_decided_frame + 1 == seal else None
+    frames, done = [], 0
+    for e in evs:
+        t.build(e)
+        assert t.process(e) is None
+        frames.append(e.frame)
+        done += 1
+        if t.store.get_epoch() != 1:
+            break
+    v = t.store.get_validators() if not seal else pos.Validators(dict(zip(nodes, weights)))
+    creator, seq, off, flat = tdag.to_dense(evs, v)
+    c = corc.AbftOracle(v.weights, seal=(lambda ep, f: list(v.weights) if f == seal else None) if seal else None)
+    rc, consumed, out = c.process_batch(creator, seq, off, flat)
+    assert rc == 0 and consumed == done
+    assert list(out[:done]) == frames
+    pos_of = {e.id: i for i, e in enumerate(evs)}
+    want = [(ep, f, pos_of[a], tuple(v.idxs[x] for x in ch), tuple(pos_of[x] for x in conf))
+            for ep, f, a, ch, conf in t.block_list]
+    assert c.blocks == want
+    if not seal:
+        for f in range(1, max(frames) + 1):
+            assert [pos_of[x.id] for x in t.store.roots.get(f, [])] == list(c.frame_roots(f))
