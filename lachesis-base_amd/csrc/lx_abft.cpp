@@ -36,6 +36,7 @@
 #include <chrono>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -47,7 +48,7 @@
 namespace {
 
 constexpr uint32_t NONE = LX_NONE;
-constexpr uint32_t kSpecDepth = 4;      // self-children evaluated ahead per launch
+constexpr uint32_t kSpecDepth = 4;      // self-children evaluated ahead per launch (LX_SPEC overrides)
 constexpr uint32_t kBuildCap = 100;     // calcFrameIdx: selfParentFrame + 100 in Build
 constexpr uint32_t kVoteWindow = 64;    // subjects voted on first (chooseAtropos walks idx order)
 
@@ -107,7 +108,7 @@ struct lx_abft {
     uint64_t arena_used = 0;
 
     // scratch
-    DVec<uint32_t> d_cand;
+    DVec<uint32_t> d_cand, d_psum;
     DVec<uint8_t> d_q;
     DVec<unsigned long long> d_dec;
     DVec<uint32_t> d_err;
@@ -117,6 +118,7 @@ struct lx_abft {
     std::vector<uint32_t> h_row;
     bool dec_dirty = true;
     uint32_t vw = 0;                    // subject window [0, vw) of the current election
+    uint32_t spec_depth = kSpecDepth;
 
     lx_abft_stats stats{};
 
@@ -275,6 +277,12 @@ int eval_frame(lx_abft *a, const IndexView &iv, uint32_t f, const std::vector<ui
     uint32_t *bits = a->arena.p + a->arena_used;
     if (words) {
         ARC(refresh_cheaters(a, iv));
+        // split the columns when the tiles alone cannot fill the chip
+        const uint32_t ncols = (iv.V + 31) / 32 * 32;
+        const uint32_t splits = lx::root_fc_splits(n, R, ncols);
+        const uint32_t col_split = ((ncols + splits - 1) / splits + 31) / 32 * 32;
+        const uint32_t n_split = (ncols + col_split - 1) / col_split;
+        ARC(reserve(a, a->d_psum, (uint64_t)n_split * n * words * 32, 0, s));
         RootFcArgs r{};
         r.hb = iv.hb;
         r.la = iv.la;
@@ -284,7 +292,7 @@ int eval_frame(lx_abft *a, const IndexView &iv, uint32_t f, const std::vector<ui
         r.roots = fr.d_ev.p;
         r.n_roots = R;
         r.roots_fallback = cand[0];
-        r.ncols = (iv.V + 31) / 32 * 32;
+        r.ncols = ncols;
         r.wpad = iv.wpad;
         r.quorum = a->quorum;
         r.n_k = a->n_k;
@@ -292,12 +300,17 @@ int eval_frame(lx_abft *a, const IndexView &iv, uint32_t f, const std::vector<ui
         r.kflag = a->d_kflag.p;
         r.kw = a->d_kw.p;
         r.ev_branch = iv.ev_branch;
-        r.bits = bits;
+        r.psum = a->d_psum.p;
         r.words = words;
+        r.col_split = col_split;
+        r.n_split = n_split;
         AHIP(a, lx::launch_root_fc(r, iv.B > iv.V, s));
         QuorumArgs qa{};
+        qa.psum = a->d_psum.p;
+        qa.n_split = n_split;
         qa.bits = bits;
         qa.words = words;
+        qa.n_roots = R;
         qa.n_cand = n;
         qa.cand = a->d_cand.p;
         qa.root_ev = fr.d_ev.p;
@@ -376,25 +389,37 @@ int compute_frames(lx_abft *a, uint64_t base, uint32_t n, const uint32_t *creato
         const uint32_t f = pending.begin()->first;
         std::vector<uint32_t> Q = std::move(pending.begin()->second);
         pending.erase(pending.begin());
-        std::vector<uint32_t> ask;
-        for (uint32_t i : Q) {
-            if (f >= cap[i]) resolve(i, f);   // loop bound checked before the quorum (:184)
-            else ask.push_back(i);
+        // Events whose loop bound is f stop without asking (:184: the bound is
+        // checked before the quorum) -- with claimed frames that is every
+        // non-root event -- and their self-children start at f: drain them
+        // all before launching.
+        std::vector<uint32_t> ask, work = std::move(Q);
+        while (!work.empty()) {
+            const uint32_t i = work.back();
+            work.pop_back();
+            if (f < cap[i]) {
+                ask.push_back(i);
+                continue;
+            }
+            resolve(i, f);
+            for (auto &pc : pushed) work.push_back(pc.first);
+            pushed.clear();
         }
-        if (ask.empty()) {
-            flush();
-            continue;
-        }
-        // speculative self-descendants, kSpecDepth deep
+        if (ask.empty()) continue;
+        std::sort(ask.begin(), ask.end());
+        // speculative self-descendants, spec_depth deep
         cand_pos = ask;
         for (uint32_t i : ask) spec[i] = 2;
         {
             std::vector<uint32_t> lvl = ask, nxt;
-            for (uint32_t d = 0; d < kSpecDepth && !lvl.empty() && n > 1; d++) {
+            for (uint32_t d = 0; d < a->spec_depth && !lvl.empty() && n > 1; d++) {
                 nxt.clear();
                 for (uint32_t i : lvl)
                     for (uint32_t c = child_head[i]; c != NONE; c = child_next[c])
-                        if (!spec[c] && cur[c] == NONE) {
+                        // a claimed frame above f says i passes q_f: its
+                        // children cannot be at f, nothing to speculate
+                        if (!spec[c] && cur[c] == NONE && (!claimed || claimed[i] == LX_FRAME_BUILD ||
+                                                           claimed[i] <= f)) {
                             spec[c] = 1;
                             nxt.push_back(c);
                             cand_pos.push_back(c);
@@ -739,6 +764,7 @@ int lx_abft_create(lx_index *index, lx_abft **out) {
     if (!index || !out) return LX_ERR_ARG;
     lx_abft *a = new lx_abft();
     a->ix = index;
+    if (const char *e = getenv("LX_SPEC")) a->spec_depth = (uint32_t)atoi(e);
     *out = a;
     return 0;
 }
@@ -748,6 +774,7 @@ void lx_abft_destroy(lx_abft *a) {
     for (Frame &f : a->frames) f.release();
     a->arena.release();
     a->d_cand.release();
+    a->d_psum.release();
     a->d_q.release();
     a->d_dec.release();
     a->d_err.release();

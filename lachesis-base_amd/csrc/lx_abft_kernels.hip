@@ -42,7 +42,6 @@ __global__ __launch_bounds__(256) void k_root_fc(RootFcArgs a) {
     __shared__ uint32_t sH[kKc][kLdsPitch];
     __shared__ uint32_t sL[kKc][kLdsPitch];
     __shared__ uint32_t sW[kKc];
-    __shared__ uint32_t sBits[kTile][2];
 
     const uint32_t tid = threadIdx.x;
     const uint32_t tx = tid & 15, ty = tid >> 4;          // roots tx*4.., events ty*4..
@@ -62,7 +61,8 @@ __global__ __launch_bounds__(256) void k_root_fc(RootFcArgs a) {
 #pragma unroll
         for (int k = 0; k < 4; k++) sum[i][k] = 0;
 
-    for (uint32_t j0 = 0; j0 < a.ncols; j0 += kKc) {
+    const uint32_t cs = a.col_split, jlo = blockIdx.z * cs, jhi = jlo + cs < a.ncols ? jlo + cs : a.ncols;
+    for (uint32_t j0 = jlo; j0 < jhi; j0 += kKc) {
         const uint4 h0 = hrow[j0 / 4], h1 = hrow[j0 / 4 + 1];
         const uint4 l0 = lrow[j0 / 4], l1 = lrow[j0 / 4 + 1];
         const uint32_t hv[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
@@ -99,7 +99,7 @@ __global__ __launch_bounds__(256) void k_root_fc(RootFcArgs a) {
     }
 
     uint32_t early = 0;   // bit i*4+k: A observes creator(branch(r)) as forked
-    if (FORKS) {
+    if (FORKS && blockIdx.z == 0) {
         // Cheaters' branches: creator n counts once if any of its branches
         // counts (WeightCounter.CountByIdx, inter/pos/stake.go:47-55); the main
         // loop counted only the original column n.  Columns come grouped by
@@ -138,46 +138,70 @@ __global__ __launch_bounds__(256) void k_root_fc(RootFcArgs a) {
         }
     }
 
-    if (tid < kTile * 2) sBits[tid >> 1][tid & 1] = 0;
-    __syncthreads();
+    // partial stake sums of this column split; split 0 also carries the
+    // cheater fix-ups and the early-false flag (bit 31: total weight < 2^31)
+    const uint32_t rp = a.words * 32;
 #pragma unroll
     for (int i = 0; i < 4; i++) {
-        uint32_t nib = 0;
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const bool ok = rt[k] != LX_NONE && !((early >> (i * 4 + k)) & 1u) && sum[i][k] >= a.quorum;
-            nib |= (ok ? 1u : 0u) << k;
-        }
-        if (nib) atomicOr(&sBits[ty * 4 + i][tx >> 3], nib << ((tx & 7) * 4));
+        const uint32_t ei = e0 + ty * 4 + i;
+        if (ei >= a.n_cand) continue;
+        uint4 o;
+        o.x = sum[i][0] | (((early >> (i * 4 + 0)) & 1u) << 31);
+        o.y = sum[i][1] | (((early >> (i * 4 + 1)) & 1u) << 31);
+        o.z = sum[i][2] | (((early >> (i * 4 + 2)) & 1u) << 31);
+        o.w = sum[i][3] | (((early >> (i * 4 + 3)) & 1u) << 31);
+        const uint32_t ri = r0 + tx * 4;
+        if (ri < rp)
+            *reinterpret_cast<uint4 *>(a.psum + ((uint64_t)blockIdx.z * a.n_cand + ei) * rp + ri) = o;
     }
-    __syncthreads();
-    if (tid < kTile * 2) {
-        const uint32_t ei = e0 + (tid >> 1);
-        const uint32_t wi = blockIdx.x * 2 + (tid & 1);
-        if (ei < a.n_cand && wi < a.words) a.bits[(uint64_t)ei * a.words + wi] = sBits[tid >> 1][tid & 1];
-    }
+}
+
+uint32_t root_fc_splits(uint32_t n_cand, uint32_t n_roots, uint32_t ncols) {
+    // enough workgroups to fill 256 CUs x 4, at least 4 LDS chunks per split
+    const uint32_t tiles = ((n_roots + kTile - 1) / kTile) * ((n_cand + kTile - 1) / kTile);
+    uint32_t s = tiles ? (1024 + tiles - 1) / tiles : 1;
+    const uint32_t max_s = ncols / (4 * kKc) ? ncols / (4 * kKc) : 1;
+    return s < 1 ? 1 : (s > max_s ? max_s : s);
 }
 
 hipError_t launch_root_fc(const RootFcArgs &a, bool forks, hipStream_t s) {
     if (!a.n_cand || !a.words) return hipSuccess;
-    dim3 grid((a.n_roots + kTile - 1) / kTile, (a.n_cand + kTile - 1) / kTile);
-    if (grid.x == 0) grid.x = 1;   // no roots: rows of zeros still get written
+    dim3 grid((a.n_roots + kTile - 1) / kTile, (a.n_cand + kTile - 1) / kTile, a.n_split);
     if (forks) hipLaunchKernelGGL(k_root_fc<true>, grid, dim3(256), 0, s, a);
     else hipLaunchKernelGGL(k_root_fc<false>, grid, dim3(256), 0, s, a);
     return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------- k_root_quorum
-// one wave per candidate; roots with a set bit count their creator once
-// (dup[r] = previous root of the same creator in the frame list, or NONE)
+// One wave per candidate: FC bit per root = (sum over the column splits >=
+// quorum, no early-false flag), written to the bit row; then the stake of the
+// distinct creators of the roots it forkless-causes (dup[r] = previous root of
+// the same creator in the frame list), its own root slot excluded.
+constexpr uint32_t kRowWords = 512;   // bit row kept in LDS: up to 16384 roots per frame
 __global__ __launch_bounds__(256) void k_root_quorum(QuorumArgs a) {
-    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) / 64, lane = threadIdx.x & 63;
+    __shared__ uint32_t sRow[4][kRowWords];
+    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t wave = blockIdx.x * 4 + wv;
     if (wave >= a.n_cand) return;
-    const uint32_t *row = a.bits + (uint64_t)wave * a.words;
+    const uint32_t rp = a.words * 32;
+    uint32_t *row = a.bits + (uint64_t)wave * a.words;
+    for (uint32_t r0 = 0; r0 < rp; r0 += 64) {
+        const uint32_t r = r0 + lane;
+        uint32_t sum = 0;
+        for (uint32_t z = 0; z < a.n_split; z++) sum += a.psum[((uint64_t)z * a.n_cand + wave) * rp + r];
+        const bool ok = r < a.n_roots && !(sum >> 31) && sum >= a.quorum;
+        const unsigned long long m = __ballot(ok);
+        if (lane < 2 && r0 / 32 + lane < a.words) {
+            const uint32_t w = (uint32_t)(m >> (32 * lane));
+            row[r0 / 32 + lane] = w;
+            sRow[wv][r0 / 32 + lane] = w;
+        }
+    }
+    __syncthreads();   // sRow of this wave complete (waves of a block exit together below)
     const uint32_t self = a.cand[wave];
     uint32_t sum = 0;
     for (uint32_t wi = lane; wi < a.words; wi += 64) {
-        uint32_t m = row[wi];
+        uint32_t m = sRow[wv][wi];
         while (m) {
             const uint32_t b = __builtin_ctz(m);
             m &= m - 1;
@@ -187,7 +211,7 @@ __global__ __launch_bounds__(256) void k_root_quorum(QuorumArgs a) {
             if (a.root_ev[r] == self) continue;
             bool first = true;
             for (uint32_t d = a.dup[r]; d != LX_NONE; d = a.dup[d])
-                if ((row[d >> 5] >> (d & 31)) & 1u) { first = false; break; }
+                if ((sRow[wv][d >> 5] >> (d & 31)) & 1u) { first = false; break; }
             if (first) sum += a.wcreator[a.creator[r]];
         }
     }
@@ -231,51 +255,98 @@ __global__ void k_vote_round1(VoteArgs a) {
     }
 }
 
-// round >= 2 (election_math.go:53-110): one lane per (voter slot, subject),
-// a wave = 64 subjects of one voter, so the voter's observed-root bitmap and
-// the observed root's creator and weight are wave-uniform.
+// round >= 2 (election_math.go:53-110): one workgroup per voter slot.  The
+// voter's observed roots are compacted into LDS; 4 waves split them, each
+// lane sums one subject of the 64-subject chunk over its wave's share (loads
+// independent, so many are in flight), then the 4 partial tallies merge.
+constexpr int kVoteSlices = 4;
+constexpr uint32_t kObsChunk = 2048;   // observed-root bits compacted per pass
 __global__ __launch_bounds__(256) void k_vote_round(VoteArgs a, uint32_t n_voters) {
-    const uint32_t s = blockIdx.y * 4 + threadIdx.y;
-    const uint32_t v = a.v_lo + blockIdx.x * 64 + threadIdx.x;
-    if (s >= n_voters) return;
+    __shared__ uint32_t sObs[kObsChunk];
+    __shared__ uint32_t sN;
+    __shared__ uint32_t sYes[kVoteSlices][64], sNo[kVoteSlices][64], sAll[kVoteSlices][64], sSubj[kVoteSlices][64],
+        sErr[kVoteSlices][64];
+    const uint32_t s = blockIdx.y;
+    const uint32_t lane = threadIdx.x & 63, slice = threadIdx.x >> 6;
     const uint32_t vev = a.voter_ev[s];
-    if (vev == LX_NONE || v >= a.v_hi) return;
+    if (vev == LX_NONE) return;
     const uint64_t off = a.bm_off[s];
     const uint32_t len = a.bm_len[s];
-    uint32_t yes = 0, no = 0, all = 0, subj = kVoteNoRoot, err = 0;
-    for (uint32_t wi = 0; wi * 32 < len; wi++) {
-        uint32_t m = a.bm[off + wi];
-        if ((wi + 1) * 32 > len) m &= (1u << (len & 31)) - 1u;
-        while (m) {
-            const uint32_t b = __builtin_ctz(m);
-            m &= m - 1;
-            const uint32_t r = wi * 32 + b;
-            const uint32_t c = a.prev_creator[r];
-            if (a.prev_has_dup)
-                for (uint32_t d = a.prev_dup[r]; d != LX_NONE; d = a.prev_dup[d])
-                    if ((a.bm[off + (d >> 5)] >> (d & 31)) & 1u) err |= kVoteErrTwoRoots;   // allVotes.Count == false
-            const uint32_t pv = a.prev_votes[(uint64_t)r * a.V + v];
-            const uint32_t wc = a.wcreator[c];
-            if (!(pv & kVoteVoted)) err |= kVoteErrMissing;
-            if (pv & kVoteYes) {
-                const uint32_t ix = pv & kVoteNoRoot;
-                if (subj != kVoteNoRoot && subj != ix) err |= kVoteErrTwoRoots;
-                subj = ix;
-                yes += wc;
-            } else {
-                no += wc;
-            }
-            all += wc;
+    if (a.prev_has_dup && blockIdx.x == 0) {
+        // two observed roots of one validator: allVotes.Count == false
+        uint32_t err = 0;
+        for (uint32_t r = threadIdx.x; r < len; r += blockDim.x) {
+            if (!((a.bm[off + (r >> 5)] >> (r & 31)) & 1u)) continue;
+            for (uint32_t d = a.prev_dup[r]; d != LX_NONE; d = a.prev_dup[d])
+                if ((a.bm[off + (d >> 5)] >> (d & 31)) & 1u) err |= kVoteErrTwoRoots;
         }
+        if (err) atomicOr(a.err, err);
     }
-    if (all < a.quorum) err |= kVoteErrQuorum;
-    const bool y = yes >= no;
-    const bool dec = yes >= a.quorum || no >= a.quorum;
-    const uint32_t obs = y ? subj : kVoteNoRoot;
-    a.votes[(uint64_t)s * a.V + v] = kVoteVoted | (y ? kVoteYes : 0u) | (dec ? kVoteDecided : 0u) | obs;
-    if (dec)
-        atomicMin(&a.dec[v], ((unsigned long long)vev << 32) | (y ? 0x80000000ull : 0ull) | obs);
-    if (err) atomicOr(a.err, err);
+    for (uint32_t v0 = a.v_lo + blockIdx.x * 64; v0 < a.v_hi; v0 += gridDim.x * 64) {
+        const uint32_t v = v0 + lane;
+        uint32_t yes = 0, no = 0, all = 0, subj = kVoteNoRoot, err = 0;
+        for (uint32_t c0 = 0; c0 < len; c0 += kObsChunk) {
+            // compact this chunk's observed roots (bit order = root list order)
+            if (threadIdx.x == 0) sN = 0;
+            __syncthreads();
+            const uint32_t clen = len - c0 < kObsChunk ? len - c0 : kObsChunk;
+            for (uint32_t wi = threadIdx.x; wi * 32 < clen; wi += blockDim.x) {
+                uint32_t m = a.bm[off + c0 / 32 + wi];
+                if ((wi + 1) * 32 > clen) m &= (1u << (clen & 31)) - 1u;
+                uint32_t base = m ? atomicAdd(&sN, (uint32_t)__builtin_popcount(m)) : 0;
+                while (m) {
+                    sObs[base++] = c0 + wi * 32 + __builtin_ctz(m);
+                    m &= m - 1;
+                }
+            }
+            __syncthreads();
+            const uint32_t n = sN;
+            if (v < a.v_hi) {
+#pragma unroll 4
+                for (uint32_t k = slice; k < n; k += kVoteSlices) {
+                    const uint32_t r = sObs[k];
+                    const uint32_t pv = a.prev_votes[(uint64_t)r * a.V + v];
+                    const uint32_t wc = a.wcreator[a.prev_creator[r]];
+                    if (!(pv & kVoteVoted)) err |= kVoteErrMissing;
+                    const bool py = (pv & kVoteYes) != 0;
+                    const uint32_t ix = pv & kVoteNoRoot;
+                    if (py && subj != kVoteNoRoot && subj != ix) err |= kVoteErrTwoRoots;
+                    subj = py ? ix : subj;
+                    yes += py ? wc : 0u;
+                    no += py ? 0u : wc;
+                    all += wc;
+                }
+            }
+            __syncthreads();
+        }
+        sYes[slice][lane] = yes;
+        sNo[slice][lane] = no;
+        sAll[slice][lane] = all;
+        sSubj[slice][lane] = subj;
+        sErr[slice][lane] = err;
+        __syncthreads();
+        if (slice == 0 && v < a.v_hi) {
+            for (int q = 1; q < kVoteSlices; q++) {
+                yes += sYes[q][lane];
+                no += sNo[q][lane];
+                all += sAll[q][lane];
+                err |= sErr[q][lane];
+                const uint32_t sq = sSubj[q][lane];
+                if (sq != kVoteNoRoot) {
+                    if (subj != kVoteNoRoot && subj != sq) err |= kVoteErrTwoRoots;
+                    subj = sq;
+                }
+            }
+            if (all < a.quorum) err |= kVoteErrQuorum;
+            const bool y = yes >= no;
+            const bool dec = yes >= a.quorum || no >= a.quorum;
+            const uint32_t obs = y ? subj : kVoteNoRoot;
+            a.votes[(uint64_t)s * a.V + v] = kVoteVoted | (y ? kVoteYes : 0u) | (dec ? kVoteDecided : 0u) | obs;
+            if (dec) atomicMin(&a.dec[v], ((unsigned long long)vev << 32) | (y ? 0x80000000ull : 0ull) | obs);
+            if (err) atomicOr(a.err, err);
+        }
+        __syncthreads();
+    }
 }
 
 hipError_t launch_votes(const VoteArgs &a, uint32_t n_voters, bool round1, hipStream_t s) {
@@ -286,7 +357,8 @@ hipError_t launch_votes(const VoteArgs &a, uint32_t n_voters, bool round1, hipSt
     if (round1) {
         hipLaunchKernelGGL(k_vote_round1, dim3(2, n_voters), dim3(256), 0, s, a);
     } else {
-        hipLaunchKernelGGL(k_vote_round, dim3((w + 63) / 64, (n_voters + 3) / 4), dim3(64, 4), 0, s, a, n_voters);
+        const uint32_t gx = (w + 63) / 64 < 16 ? (w + 63) / 64 : 16;
+        hipLaunchKernelGGL(k_vote_round, dim3(gx, n_voters), dim3(256), 0, s, a, n_voters);
     }
     return hipGetLastError();
 }

@@ -162,13 +162,18 @@ struct RootFcArgs {
     const uint32_t *kflag;       // bit0 first of its group, bit1 last
     const uint32_t *kw;          // weight of the group's creator (on its last column)
     const uint32_t *ev_branch;
-    uint32_t *bits;              // out: bits[c * words + r / 32]
+    uint32_t *psum;              // out: psum[(z * n_cand + c) * words * 32 + r], partial stake of split z
     uint32_t words;
+    uint32_t col_split;          // columns per split (multiple of 32)
+    uint32_t n_split;            // column splits (grid z)
 };
 
 struct QuorumArgs {
-    const uint32_t *bits;
+    const uint32_t *psum;        // partial stake sums of k_root_fc
+    uint32_t n_split;
+    uint32_t *bits;              // out: bits[c * words + r / 32]
     uint32_t words;
+    uint32_t n_roots;
     uint32_t n_cand;
     const uint32_t *cand;        // candidate events (their own slot is skipped)
     const uint32_t *root_ev;     // root events of the frame
@@ -218,6 +223,7 @@ hipError_t launch_shard_rows(const uint32_t *ev_branch, const uint32_t *branch_c
                              uint32_t *rows, hipStream_t s);
 hipError_t launch_la_block(uint32_t *la, uint64_t stride, const uint32_t *rows, uint32_t nrows, const uint32_t *cols,
                            uint32_t ncols, uint32_t *buf, int unpack, hipStream_t s);
+uint32_t root_fc_splits(uint32_t n_cand, uint32_t n_roots, uint32_t ncols);
 hipError_t launch_root_fc(const RootFcArgs &a, bool forks, hipStream_t s);
 hipError_t launch_root_quorum(const QuorumArgs &a, hipStream_t s);
 hipError_t launch_votes(const VoteArgs &a, uint32_t n_voters, bool round1, hipStream_t s);
