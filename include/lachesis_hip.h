@@ -86,6 +86,36 @@ int lx_add_batch_dev(lx_index *h, uint32_t n, const uint32_t *creator_idx_dev, c
 int lx_flush(lx_index *h);
 int lx_drop_not_flushed(lx_index *h);
 
+/* Write-back of Flush to the reference's kvdb tables (vecengine/index.go:78-85,
+ * vecfc/store_vectors.go:53-65, vecengine/store_branches_info.go:57-81): the
+ * Puts the reference's flushable would commit at this Flush, in its byte
+ * formats:
+ *   table "S" (HighestBefore, vecfc/index.go:39): the events added since the
+ *             last flush, first_event .. first_event + n_events - 1;
+ *   table "s" (LowestAfter, vecfc/index.go:40): those events plus every older
+ *             event whose LowestAfter gained an entry since (the DFS Visits of
+ *             vecengine/index.go:212-225), ascending dense index;
+ *   table "b" (branch ID, vecengine/index.go:40): the new events, 4 B big-endian
+ *             (inter/idx/internal.go:13-15);
+ *   table "B" key "c" (vecengine/index.go:41): RLP(BranchesInfo).
+ * lx_writeback_prepare finds the rows on the device and returns the sizes;
+ * lx_writeback_fetch encodes them on the device and copies them out (any
+ * pointer may be NULL to skip that part; offsets have n+1 entries, in bytes).
+ * lx_flush then commits.  Adding, dropping, flushing or resetting in between
+ * invalidates the prepared set (LX_ERR_STATE).  Unsharded handles only.
+ * Restart: replay the persisted epoch (lx_reset + lx_add_batch in the stored
+ * Add order); a write-back prepared right after the replay equals the
+ * persisted tables byte for byte. */
+typedef struct lx_writeback {
+    uint64_t first_event, n_events;   /* rows of tables S and b */
+    uint64_t n_la_rows;               /* rows of table s */
+    uint64_t hb_bytes, la_bytes;      /* value bytes of tables S and s */
+    uint32_t bi_bytes;                /* RLP(BranchesInfo) */
+} lx_writeback;
+int lx_writeback_prepare(lx_index *h, lx_writeback *out);
+int lx_writeback_fetch(lx_index *h, uint64_t *hb_off, uint8_t *hb_bytes, uint32_t *la_ev, uint64_t *la_off,
+                       uint8_t *la_bytes, uint8_t *branch_be, uint8_t *bi_rlp);
+
 uint64_t lx_num_events(const lx_index *h);
 uint32_t lx_num_branches(const lx_index *h);           /* len(BranchIDCreatorIdxs) */
 int lx_at_least_one_fork(const lx_index *h);           /* branches_info.go:47-49 */

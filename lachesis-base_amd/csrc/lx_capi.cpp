@@ -92,6 +92,16 @@ struct lx_index {
     void *sc_tmp = nullptr;
     size_t sc_tmp_bytes = 0;
 
+    // write-back (lx_writeback_*): dirty-row flags, row lists, byte offsets
+    uint64_t wb_cap = 0, wb_buf_cap = 0;
+    uint32_t *wb_flag = nullptr, *wb_pos = nullptr, *wb_la_rows = nullptr, *wb_hb_rows = nullptr, *wb_buf = nullptr;
+    uint64_t *wb_len = nullptr, *wb_la_off = nullptr, *wb_hb_off = nullptr;
+    void *wb_tmp = nullptr;
+    size_t wb_tmp_bytes = 0;
+    bool wb_ready = false;
+    lx_writeback wb{};
+    std::string wb_bi;
+
     // timing (HIP events on `stream`)
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     lx_stats stats{};
@@ -125,7 +135,21 @@ struct lx_index {
 
 namespace {
 
+void free_wb(lx_index *h) {
+    void *p[] = {h->wb_flag, h->wb_pos, h->wb_la_rows, h->wb_hb_rows, h->wb_buf, h->wb_len, h->wb_la_off,
+                 h->wb_hb_off, h->wb_tmp};
+    for (void *x : p)
+        if (x) (void)hipFree(x);
+    h->wb_flag = h->wb_pos = h->wb_la_rows = h->wb_hb_rows = h->wb_buf = nullptr;
+    h->wb_len = h->wb_la_off = h->wb_hb_off = nullptr;
+    h->wb_tmp = nullptr;
+    h->wb_cap = h->wb_buf_cap = 0;
+    h->wb_tmp_bytes = 0;
+    h->wb_ready = false;
+}
+
 void free_all(lx_index *h) {
+    free_wb(h);
     void *ptrs[] = {h->hb, h->la, h->ev_creator, h->ev_seq, h->ev_branch, h->ev_bbefore, h->ev_sp,
                     h->first_child, h->first_root, h->branch_first, h->branch_creator, h->branch_len, h->brow,
                     h->wpad, h->col_list, h->cheat_off, h->cheat_br, h->cheat_creator, h->b_creator, h->b_seq,
@@ -342,6 +366,7 @@ int add_batch_dev(lx_index *h, uint32_t n, const uint32_t *creator, const uint32
                   const uint32_t *par, uint32_t *err_index) {
     if (!h->have_epoch) return h->fail(LX_ERR_STATE, "lx_add_batch before lx_reset");
     if (n == 0) return 0;
+    h->wb_ready = false;
     if (h->n_events + n >= 0xFFFFFFF0ull) return h->fail(LX_ERR_ARG, "too many events in one epoch");
     int rc;
     if ((rc = grow_events(h, h->n_events + n))) return rc;
@@ -580,6 +605,147 @@ int read_u32(lx_index *h, const uint32_t *dev, uint32_t *out) {
     return 0;
 }
 
+// the LowestAfter fills of the events added since the last flush (rollback and write-back)
+UnfillArgs unfill_args(lx_index *h) {
+    UnfillArgs u{};
+    u.hb = h->hb;
+    u.la = h->la;
+    u.stride = h->stride;
+    u.lo = (uint32_t)h->n_flushed;
+    u.hi = (uint32_t)h->n_events;
+    u.B = h->B;
+    u.ev_seq = h->ev_seq;
+    u.ev_branch = h->ev_branch;
+    u.ev_bbefore = h->ev_bbefore;
+    u.ev_sp = h->ev_sp;
+    u.ev_creator = h->ev_creator;
+    u.first_child = h->first_child;
+    u.first_root = h->first_root;
+    u.branch_len = h->branch_len;
+    u.branch_first = h->branch_first;
+    u.brow = h->brow;
+    u.s_cap = h->s_cap;
+    u.B_keep = h->B_flushed;
+    return u;
+}
+
+// ---- write-back helpers
+int ensure_wb(lx_index *h, uint64_t n) {
+    if (n <= h->wb_cap && h->wb_flag) return 0;
+    void *keep_buf = h->wb_buf;
+    uint64_t keep_cap = h->wb_buf_cap;
+    h->wb_buf = nullptr;
+    free_wb(h);
+    h->wb_buf = (uint32_t *)keep_buf;
+    h->wb_buf_cap = keep_cap;
+    const uint64_t cap = std::max<uint64_t>(n, 4096);
+    HIPCHK(h, dalloc(&h->wb_flag, cap));
+    HIPCHK(h, dalloc(&h->wb_pos, cap));
+    HIPCHK(h, dalloc(&h->wb_la_rows, cap));
+    HIPCHK(h, dalloc(&h->wb_hb_rows, cap));
+    HIPCHK(h, dalloc(&h->wb_len, cap + 1));
+    HIPCHK(h, dalloc(&h->wb_la_off, cap + 1));
+    HIPCHK(h, dalloc(&h->wb_hb_off, cap + 1));
+    size_t tb = 0;
+    HIPCHK(h, lx::persist_tmp_bytes((uint32_t)cap, &tb));
+    HIPCHK(h, hipMalloc(&h->wb_tmp, tb ? tb : 1));
+    h->wb_tmp_bytes = tb;
+    h->wb_cap = cap;
+    return 0;
+}
+
+RowsArgs rows_args(lx_index *h, uint32_t hb, const uint32_t *rows, uint32_t n) {
+    RowsArgs a{};
+    a.plane = hb ? h->hb : h->la;
+    a.stride = h->stride;
+    a.rows = rows;
+    a.n = n;
+    a.B = h->B;
+    a.ev_bbefore = h->ev_bbefore;
+    a.ev_branch = h->ev_branch;
+    a.branch_first = h->branch_first;
+    a.hb = hb;
+    return a;
+}
+
+// encoded rows -> host, in chunks of at most kWbChunk bytes of device staging
+constexpr uint64_t kWbChunk = 256ull << 20;
+
+int rows_to_host(lx_index *h, uint32_t hb, const uint32_t *rows, const uint64_t *off_dev, uint32_t n,
+                 uint64_t *off_host, uint8_t *bytes) {
+    std::vector<uint64_t> off(n + 1);
+    HIPCHK(h, hipMemcpyAsync(off.data(), off_dev, (n + 1) * 8ull, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    if (off_host) memcpy(off_host, off.data(), (n + 1) * 8ull);
+    if (!bytes || !n || !off[n]) return 0;
+    uint64_t row_max = 0;
+    for (uint32_t i = 0; i < n; i++) row_max = std::max(row_max, off[i + 1] - off[i]);
+    const uint64_t want = std::max(std::min(off[n], kWbChunk), row_max);
+    if (want > h->wb_buf_cap) {
+        if (h->wb_buf) (void)hipFree(h->wb_buf);
+        h->wb_buf = nullptr;
+        h->wb_buf_cap = 0;
+        HIPCHK(h, dalloc(&h->wb_buf, (want + 3) / 4));
+        h->wb_buf_cap = want;
+    }
+    for (uint32_t i0 = 0; i0 < n;) {
+        uint32_t i1 = i0 + 1;
+        while (i1 < n && off[i1 + 1] - off[i0] <= h->wb_buf_cap) i1++;
+        RowsArgs a = rows_args(h, hb, rows + i0, i1 - i0);
+        HIPCHK(h, lx::launch_encode_rows(a, off_dev + i0, off[i0], h->wb_buf, h->stream));
+        HIPCHK(h, hipMemcpyAsync(bytes + off[i0], h->wb_buf, off[i1] - off[i0], hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        i0 = i1;
+    }
+    return 0;
+}
+
+// go-ethereum rlp (v1.9.22) of BranchesInfo{[]idx.Event, []idx.Validator,
+// [][]idx.Validator} (vecengine/branches_info.go:9-13): structs and slices are
+// lists, uints are minimal big-endian strings (0 = 0x80, < 0x80 = the byte)
+void rlp_uint(std::string &o, uint32_t x) {
+    if (x == 0) { o.push_back((char)0x80); return; }
+    if (x < 0x80) { o.push_back((char)x); return; }
+    const int nb = (x >> 24) ? 4 : (x >> 16) ? 3 : (x >> 8) ? 2 : 1;
+    o.push_back((char)(0x80 + nb));
+    for (int i = nb - 1; i >= 0; i--) o.push_back((char)(x >> (8 * i)));
+}
+
+void rlp_list(std::string &o, const std::string &payload) {
+    const uint64_t n = payload.size();
+    if (n <= 55) {
+        o.push_back((char)(0xC0 + n));
+    } else {
+        int nb = 0;
+        for (uint64_t t = n; t; t >>= 8) nb++;
+        o.push_back((char)(0xF7 + nb));
+        for (int i = nb - 1; i >= 0; i--) o.push_back((char)(n >> (8 * i)));
+    }
+    o += payload;
+}
+
+int branches_info_rlp(lx_index *h, std::string *out) {
+    std::vector<uint32_t> len(h->B);
+    HIPCHK(h, hipMemcpyAsync(len.data(), h->branch_len, h->B * 4ull, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    std::string last, cr, by, body;
+    for (uint32_t b = 0; b < h->B; b++) {
+        rlp_uint(last, len[b] ? h->h_branch_first[b] + len[b] - 1 : 0);   // BranchIDLastSeq
+        rlp_uint(cr, h->h_branch_creator[b]);                              // BranchIDCreatorIdxs
+    }
+    for (const auto &l : h->by_creator) {                                  // BranchIDByCreators
+        std::string x;
+        for (uint32_t b : l) rlp_uint(x, b);
+        rlp_list(by, x);
+    }
+    rlp_list(body, last);
+    rlp_list(body, cr);
+    rlp_list(body, by);
+    out->clear();
+    rlp_list(*out, body);
+    return 0;
+}
+
 }  // namespace
 
 // =============================================================================== C ABI
@@ -642,6 +808,7 @@ int lx_reset(lx_index *h, uint32_t nv, const uint32_t *w) {
     if (tot > 0x7FFFFFFFull) return h->fail(LX_ERR_ARG, "validators weight overflow");   // validators.go:101-110
     HIPCHK(h, hipSetDevice(h->device));
     HIPCHK(h, hipStreamSynchronize(h->stream));
+    h->wb_ready = false;
     h->V = nv;
     h->weights.assign(w, w + nv);
     h->quorum = (uint32_t)(tot * 2 / 3 + 1);
@@ -727,6 +894,7 @@ int lx_add_batch_dev(lx_index *h, uint32_t n, const uint32_t *creator, const uin
 
 int lx_flush(lx_index *h) {
     if (!h) return LX_ERR_ARG;
+    h->wb_ready = false;
     h->n_flushed = h->n_events;
     h->B_flushed = h->B;
     return 0;
@@ -736,27 +904,9 @@ int lx_drop_not_flushed(lx_index *h) {
     if (!h) return LX_ERR_ARG;
     if (!h->have_epoch) return 0;
     HIPCHK(h, hipSetDevice(h->device));
+    h->wb_ready = false;
     if (h->n_events == h->n_flushed && h->B == h->B_flushed) return 0;
-    UnfillArgs u{};
-    u.hb = h->hb;
-    u.la = h->la;
-    u.stride = h->stride;
-    u.lo = (uint32_t)h->n_flushed;
-    u.hi = (uint32_t)h->n_events;
-    u.B = h->B;
-    u.ev_seq = h->ev_seq;
-    u.ev_branch = h->ev_branch;
-    u.ev_bbefore = h->ev_bbefore;
-    u.ev_sp = h->ev_sp;
-    u.ev_creator = h->ev_creator;
-    u.first_child = h->first_child;
-    u.first_root = h->first_root;
-    u.branch_len = h->branch_len;
-    u.branch_first = h->branch_first;
-    u.brow = h->brow;
-    u.s_cap = h->s_cap;
-    u.B_keep = h->B_flushed;
-    HIPCHK(h, lx::launch_unfill(u, h->stream));
+    HIPCHK(h, lx::launch_unfill(unfill_args(h), h->stream));
     uint64_t rows = h->n_events - h->n_flushed;
     if (rows) {
         HIPCHK(h, hipMemsetAsync(h->hb + h->n_flushed * h->stride, 0, rows * h->stride * 4, h->stream));
@@ -772,6 +922,73 @@ int lx_drop_not_flushed(lx_index *h) {
             while (!l.empty() && l.back() >= h->B) l.pop_back();
         return rebuild_columns(h);
     }
+    return 0;
+}
+
+int lx_writeback_prepare(lx_index *h, lx_writeback *out) {
+    if (!h || !out) return LX_ERR_ARG;
+    if (!h->have_epoch) return h->fail(LX_ERR_STATE, "write-back before lx_reset");
+    if (h->shard_count > 1) return h->fail(LX_ERR_STATE, "write-back needs an unsharded handle (shards hold partial rows)");
+    HIPCHK(h, hipSetDevice(h->device));
+    h->wb_ready = false;
+    const uint32_t N = (uint32_t)h->n_events, lo = (uint32_t)h->n_flushed;
+    int rc;
+    if ((rc = ensure_wb(h, N))) return rc;
+    hipStream_t s = h->stream;
+    uint32_t n_la = 0;
+    if (N > lo) {
+        HIPCHK(h, hipMemsetAsync(h->wb_flag, 0, N * 4ull, s));
+        HIPCHK(h, lx::launch_dirty_la(unfill_args(h), h->wb_flag, s));
+        HIPCHK(h, lx::launch_compact(h->wb_flag, h->wb_pos, N, h->wb_tmp, h->wb_tmp_bytes, h->wb_la_rows, s));
+        HIPCHK(h, hipMemcpyAsync(&n_la, h->wb_pos + (N - 1), 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(h, lx::launch_iota(h->wb_hb_rows, lo, N - lo, s));
+        HIPCHK(h, hipStreamSynchronize(s));
+    }
+    // byte offsets of both row sets (wb_len is scratch, reused in stream order)
+    HIPCHK(h, lx::launch_row_offsets(rows_args(h, 0, h->wb_la_rows, n_la), h->wb_len, h->wb_la_off, h->wb_tmp,
+                                     h->wb_tmp_bytes, s));
+    HIPCHK(h, lx::launch_row_offsets(rows_args(h, 1, h->wb_hb_rows, N - lo), h->wb_len, h->wb_hb_off, h->wb_tmp,
+                                     h->wb_tmp_bytes, s));
+    uint64_t tot[2] = {0, 0};
+    HIPCHK(h, hipMemcpyAsync(&tot[0], h->wb_la_off + n_la, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(h, hipMemcpyAsync(&tot[1], h->wb_hb_off + (N - lo), 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(h, hipStreamSynchronize(s));
+    if ((rc = branches_info_rlp(h, &h->wb_bi))) return rc;
+    lx_writeback w{};
+    w.first_event = lo;
+    w.n_events = N - lo;
+    w.n_la_rows = n_la;
+    w.hb_bytes = tot[1];
+    w.la_bytes = tot[0];
+    w.bi_bytes = (uint32_t)h->wb_bi.size();
+    h->wb = w;
+    h->wb_ready = true;
+    *out = w;
+    return 0;
+}
+
+int lx_writeback_fetch(lx_index *h, uint64_t *hb_off, uint8_t *hb_bytes, uint32_t *la_ev, uint64_t *la_off,
+                       uint8_t *la_bytes, uint8_t *branch_be, uint8_t *bi_rlp) {
+    if (!h) return LX_ERR_ARG;
+    if (!h->wb_ready) return h->fail(LX_ERR_STATE, "lx_writeback_fetch without a current lx_writeback_prepare");
+    HIPCHK(h, hipSetDevice(h->device));
+    const lx_writeback &w = h->wb;
+    const uint32_t n = (uint32_t)w.n_events, m = (uint32_t)w.n_la_rows;
+    int rc;
+    if ((hb_off || hb_bytes) && (rc = rows_to_host(h, 1, h->wb_hb_rows, h->wb_hb_off, n, hb_off, hb_bytes))) return rc;
+    if (la_ev && m) {
+        HIPCHK(h, hipMemcpyAsync(la_ev, h->wb_la_rows, m * 4ull, hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+    }
+    if ((la_off || la_bytes) && (rc = rows_to_host(h, 0, h->wb_la_rows, h->wb_la_off, m, la_off, la_bytes))) return rc;
+    if (branch_be && n) {
+        std::vector<uint32_t> br(n);
+        HIPCHK(h, hipMemcpyAsync(br.data(), h->ev_branch + w.first_event, n * 4ull, hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        for (uint32_t i = 0; i < n; i++)
+            for (int k = 0; k < 4; k++) branch_be[4 * i + k] = (uint8_t)(br[i] >> (24 - 8 * k));
+    }
+    if (bi_rlp) memcpy(bi_rlp, h->wb_bi.data(), h->wb_bi.size());
     return 0;
 }
 
@@ -1030,6 +1247,7 @@ int lx_index_view(lx_index *h, IndexView *o) {
     o->quorum = h->quorum;
     o->wpad = h->wpad;
     o->ev_branch = h->ev_branch;
+    o->ev_creator = h->ev_creator;
     o->weights = &h->weights;
     o->by_creator = &h->by_creator;
     o->shard_count = h->shard_count;

@@ -144,6 +144,35 @@ struct UnfillArgs {
     uint32_t B_keep;             // branches that survive the rollback
 };
 
+// ---- write-back to the reference's byte formats (lx_persist.hip)
+struct RowsArgs {
+    const uint32_t *plane;       // hb or la
+    uint64_t stride;
+    const uint32_t *rows;        // dense event indices
+    uint32_t n;
+    uint32_t B;                  // branches in use
+    const uint32_t *ev_bbefore;
+    const uint32_t *ev_branch;
+    const uint32_t *branch_first;
+    uint32_t hb;                 // 1: HighestBefore (8 B per branch), 0: LowestAfter (4 B)
+};
+
+// ---- emitter QuorumIndexer (lx_emitter.hip, lx_emitter.cpp)
+struct QiArgs {
+    const uint32_t *hb;
+    uint64_t stride;
+    uint32_t V;
+    uint32_t forks;              // B > V: fork marks and cheaters' branches exist
+    const int32_t *cheat_of;     // creator -> cheater index (-1: one branch)
+    const uint32_t *cheat_off;   // CSR over all branches of each cheater
+    const uint32_t *cheat_br;
+    const uint32_t *weights;     // by validator idx
+    uint32_t quorum;
+    uint32_t *mt;                // matrix, transposed: mt[creator * V + validator]
+    uint32_t *sp;                // self-parent seqs
+    uint32_t *median;            // global median seqs
+};
+
 // ---- batched abft caller (lx_abft_kernels.hip, lx_abft.cpp)
 struct RootFcArgs {
     const uint32_t *hb;
@@ -223,6 +252,19 @@ hipError_t launch_shard_rows(const uint32_t *ev_branch, const uint32_t *branch_c
                              uint32_t *rows, hipStream_t s);
 hipError_t launch_la_block(uint32_t *la, uint64_t stride, const uint32_t *rows, uint32_t nrows, const uint32_t *cols,
                            uint32_t ncols, uint32_t *buf, int unpack, hipStream_t s);
+hipError_t launch_dirty_la(const UnfillArgs &a, uint32_t *flag, hipStream_t s);
+hipError_t persist_tmp_bytes(uint32_t n, size_t *bytes);
+hipError_t launch_compact(const uint32_t *flag, uint32_t *pos, uint32_t n, void *tmp, size_t tmp_bytes,
+                          uint32_t *rows, hipStream_t s);
+hipError_t launch_iota(uint32_t *rows, uint32_t lo, uint32_t n, hipStream_t s);
+hipError_t launch_row_offsets(const RowsArgs &a, uint64_t *len, uint64_t *off, void *tmp, size_t tmp_bytes,
+                              hipStream_t s);
+hipError_t launch_encode_rows(const RowsArgs &a, const uint64_t *off, uint64_t base, uint32_t *out, hipStream_t s);
+hipError_t launch_gather_u32(const uint32_t *src, const uint32_t *idx, uint32_t n, uint32_t *dst, hipStream_t s);
+hipError_t launch_qi_update(const QiArgs &a, const uint32_t *ev, const uint32_t *target, uint32_t n, hipStream_t s);
+hipError_t launch_qi_median(const QiArgs &a, hipStream_t s);
+hipError_t launch_qi_metric(const QiArgs &a, const uint32_t *ev, uint32_t n, uint32_t cap, unsigned long long *out,
+                            hipStream_t s);
 uint32_t root_fc_splits(uint32_t n_cand, uint32_t n_roots, uint32_t ncols);
 hipError_t launch_root_fc(const RootFcArgs &a, bool forks, hipStream_t s);
 hipError_t launch_root_quorum(const QuorumArgs &a, hipStream_t s);
@@ -243,6 +285,7 @@ struct IndexView {
     uint32_t V, B, quorum;
     const uint32_t *wpad;
     const uint32_t *ev_branch;
+    const uint32_t *ev_creator;
     const std::vector<uint32_t> *weights;
     const std::vector<std::vector<uint32_t>> *by_creator;
     uint32_t shard_count;

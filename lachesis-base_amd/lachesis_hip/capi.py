@@ -24,6 +24,8 @@ SIGNATURES = [
     ("lx_add_batch_dev", ctypes.c_int, [vp, ctypes.c_uint32, vp, vp, vp, vp, u32p]),
     ("lx_flush", ctypes.c_int, [vp]),
     ("lx_drop_not_flushed", ctypes.c_int, [vp]),
+    ("lx_writeback_prepare", ctypes.c_int, [vp, vp]),
+    ("lx_writeback_fetch", ctypes.c_int, [vp, u64p, u8p, u32p, u64p, u8p, u8p, u8p]),
     ("lx_num_events", ctypes.c_uint64, [vp]),
     ("lx_num_branches", ctypes.c_uint32, [vp]),
     ("lx_at_least_one_fork", ctypes.c_int, [vp]),
@@ -58,6 +60,16 @@ SIGNATURES = [
     ("lx_abft_event_frame", ctypes.c_int, [vp, ctypes.c_uint32, u32p]),
     ("lx_abft_event_confirmed_on", ctypes.c_int, [vp, ctypes.c_uint32, u32p]),
     ("lx_abft_last_stats", ctypes.c_int, [vp, vp]),
+    # include/lachesis_emitter.h
+    ("lx_qi_create", ctypes.c_int, [vp, ctypes.POINTER(vp)]),
+    ("lx_qi_destroy", None, [vp]),
+    ("lx_qi_last_error", ctypes.c_char_p, [vp]),
+    ("lx_qi_reset", ctypes.c_int, [vp]),
+    ("lx_qi_process_events", ctypes.c_int, [vp, ctypes.c_uint32, u32p, u8p]),
+    ("lx_qi_median_seqs", ctypes.c_int, [vp, u32p]),
+    ("lx_qi_matrix", ctypes.c_int, [vp, u32p]),
+    ("lx_qi_self_parent_seqs", ctypes.c_int, [vp, u32p]),
+    ("lx_qi_metric_of", ctypes.c_int, [vp, ctypes.c_uint32, u32p, ctypes.c_uint32, u64p]),
 ]
 
 
@@ -70,6 +82,11 @@ class LxConfig(ctypes.Structure):
 class LxStats(ctypes.Structure):
     _fields_ = [("ms_assign", ctypes.c_float), ("ms_index", ctypes.c_float),
                 ("ms_marks", ctypes.c_float), ("index_launches", ctypes.c_uint32)]
+
+
+class LxWriteback(ctypes.Structure):
+    _fields_ = [("first_event", ctypes.c_uint64), ("n_events", ctypes.c_uint64), ("n_la_rows", ctypes.c_uint64),
+                ("hb_bytes", ctypes.c_uint64), ("la_bytes", ctypes.c_uint64), ("bi_bytes", ctypes.c_uint32)]
 
 
 class LxError(RuntimeError):
@@ -160,6 +177,29 @@ class Index:
 
     def drop_not_flushed(self):
         self._chk(self.L.lx_drop_not_flushed(self.h))
+
+    def writeback(self):
+        """The Puts of the next Flush (lx_writeback_prepare + fetch), keyed by
+        dense event index: {"S": {ev: HB bytes}, "s": {ev: LA bytes},
+        "b": {ev: 4-B big-endian branch ID}, "B": RLP(BranchesInfo)}."""
+        wb = LxWriteback()
+        self._chk(self.L.lx_writeback_prepare(self.h, ctypes.byref(wb)))
+        n, m = wb.n_events, wb.n_la_rows
+        hb_off = np.zeros(n + 1, dtype=np.uint64)
+        hb = np.zeros(max(wb.hb_bytes, 1), dtype=np.uint8)
+        la_ev = np.zeros(max(m, 1), dtype=np.uint32)
+        la_off = np.zeros(m + 1, dtype=np.uint64)
+        la = np.zeros(max(wb.la_bytes, 1), dtype=np.uint8)
+        br = np.zeros(max(4 * n, 1), dtype=np.uint8)
+        bi = np.zeros(max(wb.bi_bytes, 1), dtype=np.uint8)
+        self._chk(self.L.lx_writeback_fetch(self.h, _p(hb_off, u64p), _p(hb, u8p), _p(la_ev, u32p), _p(la_off, u64p),
+                                            _p(la, u8p), _p(br, u8p), _p(bi, u8p)))
+        hb_b, la_b, br_b = hb.tobytes(), la.tobytes(), br.tobytes()
+        f = wb.first_event
+        return {"S": {f + i: hb_b[hb_off[i]:hb_off[i + 1]] for i in range(n)},
+                "s": {int(la_ev[k]): la_b[la_off[k]:la_off[k + 1]] for k in range(m)},
+                "b": {f + i: br_b[4 * i:4 * i + 4] for i in range(n)},
+                "B": bi.tobytes()[:wb.bi_bytes]}
 
     def num_events(self):
         return self.L.lx_num_events(self.h)

@@ -124,9 +124,54 @@ class VecfcIndex:
             self.ids.append(e.id)
 
     # vecengine/index.go:78-96
-    def flush(self):
+    def flush(self, db=None):
+        """Flush.  With ``db`` (a dict of tables standing in for the index's
+        kvdb.Store) the write-back Puts go into the reference's tables keyed
+        by event id -- db["S"] HighestBefore bytes, db["s"] LowestAfter
+        bytes, db["b"] 4-B big-endian branch IDs, db["B"][b"c"]
+        RLP(BranchesInfo) (vecfc/index.go:38-41, vecengine/index.go:39-42) --
+        plus db["i"], the shim's own table of Add-order positions that
+        ``restore`` replays from."""
+        if db is not None:
+            wb = self.ix.writeback()
+            for t in ("S", "s", "b", "i", "B"):
+                db.setdefault(t, {})
+            for k, v in wb["S"].items():
+                eid = self.ids[k]
+                db["S"][eid] = v
+                db["b"][eid] = wb["b"][k]
+                db["i"][eid] = k
+            for k, v in wb["s"].items():
+                db["s"][self.ids[k]] = v
+            db["B"][b"c"] = wb["B"]
         self.ix.flush()
         self.n_flushed = len(self.ids)
+
+    def restore(self, validators, db, get_event):
+        """Restart over persisted tables (abft/restart_test.go:156-188 builds a
+        fresh index over a copy of the DB): replays the stored events in their
+        Add order (db["i"]) and checks that the write-back of the replayed
+        epoch equals the persisted tables S, s, b and B byte for byte (crit
+        "inconsistent DB" otherwise, as vecengine/store_branches_info.go:83)."""
+        self.reset(validators, get_event)
+        order = sorted(db.get("i", {}).items(), key=lambda kv: kv[1])
+        if [k for _, k in order] != list(range(len(order))):
+            self.crit(RuntimeError("inconsistent DB: Add-order table has gaps"))
+            return
+        events = [get_event(eid) for eid, _ in order]
+        if events:
+            self.add_events(events)
+        wb = self.ix.writeback()
+        ok = (len(wb["S"]) == len(db.get("S", {})) and len(wb["s"]) == len(db.get("s", {})) and
+              all(db["S"].get(self.ids[k]) == v for k, v in wb["S"].items()) and
+              all(db["s"].get(self.ids[k]) == v for k, v in wb["s"].items()) and
+              all(db["b"].get(self.ids[k]) == v for k, v in wb["b"].items()) and
+              (not events or db.get("B", {}).get(b"c") == wb["B"]))
+        if not ok:
+            self.drop_not_flushed()
+            self.crit(RuntimeError("inconsistent DB: persisted vectors differ from the replayed epoch"))
+            return
+        self.flush()
 
     def drop_not_flushed(self):
         self.ix.drop_not_flushed()
