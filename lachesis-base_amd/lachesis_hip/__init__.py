@@ -9,6 +9,7 @@ vecfc/forkless_cause_test.go:
 * :class:`VecfcIndex` -- hash-keyed facade: ``reset(validators, get_event)``,
   ``add(e)``, ``flush()``, ``drop_not_flushed()``, ``forkless_cause(a, b)``,
   ``get_highest_before(id)`` ... (vecfc/index.go, vecfc/forkless_cause.go)
+* :mod:`emitter`      -- emitter/ancestor.QuorumIndexer over include/lachesis_emitter.h
 * :mod:`abft`         -- abft.IndexedLachesis over include/lachesis_abft.h:
   frames, roots, election, blocks with batched ForklessCause on the GPU
 
@@ -20,3 +21,4 @@ from .capi import Index, LxError, load_library  # noqa: F401
 from .vecfc import VecfcIndex, HighestBeforeSeq, LowestAfterSeq, BranchSeq  # noqa: F401
 from . import tools  # noqa: F401
 from . import abft  # noqa: F401
+from . import emitter  # noqa: F401
