@@ -149,15 +149,20 @@ int lx_get_branches_info(lx_index *h, uint32_t *last_seq, uint32_t *creator_idx,
 
 /* Column shards (multi-GPU).  A handle created with
  * shard_count > 1 indexes only the branches whose creator lies in its creator
- * range: HighestBefore for those columns and complete LowestAfter rows for
- * events on those branches.  Before ForklessCause, shards exchange LowestAfter
- * blocks (an all-to-all): shard s sends lx_la_pack_dev(s -> d) = (rows on s's
- * branches) x (columns of d) and d stores it with lx_la_unpack_dev(from s).
- * lx_shard_block gives the element count (uint32) of that block. */
+ * range and stores only those columns (memory per GPU ~ 1/shard_count):
+ * HighestBefore for those columns and complete LowestAfter rows for events on
+ * those branches.  Before ForklessCause, shards exchange LowestAfter blocks (an
+ * all-to-all): shard s sends lx_la_pack_dev(s -> d) = (rows on s's branches) x
+ * (columns of d) and d stores it with lx_la_unpack_dev(from s); lx_la_own_dev
+ * moves a shard's own block (its rows x its columns).  After an Add or a
+ * DropNotFlushed the exchange is repeated before the next ForklessCause.
+ * lx_shard_block gives the element count (uint32) of a block.  The vector
+ * getters, write-back, abft and the QuorumIndexer need an unsharded handle. */
 int lx_shard_range(const lx_index *h, uint32_t shard, uint32_t *creator_lo, uint32_t *creator_hi);
 int lx_shard_block(lx_index *h, uint32_t src_shard, uint32_t dst_shard, uint64_t *elems);
 int lx_la_pack_dev(lx_index *h, uint32_t dst_shard, uint32_t *out_dev, void *stream);
 int lx_la_unpack_dev(lx_index *h, uint32_t src_shard, const uint32_t *in_dev, void *stream);
+int lx_la_own_dev(lx_index *h, void *stream);
 
 /* Timing of the last lx_add_batch* call, measured with HIP events on the
  * handle's stream (milliseconds): branch assignment + record packing,

@@ -228,6 +228,7 @@ int start_epoch(lx_abft *a, uint32_t epoch, uint32_t nv, const uint32_t *w) {
     if (rc) return a->ixfail(rc);
     IndexView iv;
     if ((rc = lx_index_view(a->ix, &iv))) return a->ixfail(rc);
+    if (iv.shard_count > 1) return a->fail(LX_ERR_STATE, "abft needs an unsharded index");
     clear_epoch(a);
     a->epoch = epoch;
     a->V = nv;

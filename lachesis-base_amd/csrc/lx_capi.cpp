@@ -54,6 +54,7 @@ struct lx_index {
     // capacities
     uint64_t n_cap = 0;
     uint32_t stride = 0;   // == branch capacity
+    uint32_t pstride = 0;  // row stride of hb / la (= stride; a shard's local column capacity)
     uint32_t s_cap = 0;
     uint64_t cap_hint = 0;
     uint32_t reserve = 0;
@@ -65,7 +66,14 @@ struct lx_index {
     uint32_t *first_root = nullptr, *branch_first = nullptr, *branch_creator = nullptr, *branch_len = nullptr,
              *brow = nullptr, *wpad = nullptr, *col_list = nullptr;
     uint32_t *cheat_off = nullptr, *cheat_br = nullptr, *cheat_creator = nullptr;
+    uint32_t *cheat_brl = nullptr, *cheat_crl = nullptr;   // the same as plane columns (shards)
     uint32_t n_cheat = 0, ncols = 0;
+    // column shard (shard_count > 1): own columns only (lx_internal.h)
+    std::vector<uint32_t> h_cmap;          // global branch -> plane column / LX_NONE
+    uint32_t nloc = 0;                     // plane columns in use
+    uint32_t *cmap = nullptr, *lap = nullptr, *wloc = nullptr;
+    uint32_t cmap_cap = 0;
+    bool sharded() const { return shard_count > 1; }
     uint64_t cheat_cap = 0;
     uint32_t *status = nullptr;
 
@@ -157,6 +165,11 @@ void free_all(lx_index *h) {
                     h->q_a, h->q_b, h->q_out};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
+    void *lptrs[] = {h->cheat_brl, h->cheat_crl, h->cmap, h->lap, h->wloc};
+    for (void *p : lptrs)
+        if (p) (void)hipFree(p);
+    h->cheat_brl = h->cheat_crl = h->cmap = h->lap = h->wloc = nullptr;
+    h->cmap_cap = 0;
     for (uint32_t *p : h->sc_rows)
         if (p) (void)hipFree(p);
     void *sptrs[] = {h->sc_flag, h->sc_pos, h->sc_cols, h->sc_tmp};
@@ -178,9 +191,29 @@ void free_all(lx_index *h) {
     h->scan_tmp = nullptr;
     h->q_a = h->q_b = nullptr;
     h->q_out = nullptr;
-    h->n_cap = h->stride = h->s_cap = 0;
+    h->n_cap = h->stride = h->pstride = h->s_cap = 0;
     h->batch_cap = h->par_cap = h->q_cap = h->cheat_cap = 0;
     h->scan_bytes = 0;
+}
+
+// a shard's produced LowestAfter rows lap[(col * s_cap + s) * stride + j] in a
+// new shape (local columns, seq capacity, branch capacity), contents kept
+int relayout_lap(lx_index *h, uint32_t ncol, uint32_t nscap, uint32_t nstride) {
+    uint32_t *n = nullptr;
+    const uint64_t words = (uint64_t)ncol * nscap * nstride;
+    HIPCHK(h, dalloc(&n, words));
+    HIPCHK(h, hipMemsetAsync(n, 0, words * 4, h->stream));
+    if (h->lap) {
+        const uint32_t oc = std::min(h->pstride, ncol), os = std::min(h->s_cap, nscap);
+        for (uint32_t k = 0; k < oc && os; k++)
+            HIPCHK(h, lx::launch_copy_rows(n + (uint64_t)k * nscap * nstride, nstride,
+                                           h->lap + (uint64_t)k * h->s_cap * h->stride, h->stride, os,
+                                           std::min(h->stride, nstride), h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        (void)hipFree(h->lap);
+    }
+    h->lap = n;
+    return 0;
 }
 
 // per-event arrays + planes for n_cap events (copies the first `keep` events)
@@ -200,9 +233,9 @@ int grow_events(lx_index *h, uint64_t need) {
     uint32_t **planes[] = {&h->hb, &h->la};
     for (uint32_t **p : planes) {
         uint32_t *n = nullptr;
-        HIPCHK(h, dalloc(&n, cap * h->stride));
-        HIPCHK(h, hipMemsetAsync(n, 0, cap * h->stride * 4, h->stream));
-        if (*p && keep) HIPCHK(h, hipMemcpyAsync(n, *p, keep * h->stride * 4, hipMemcpyDeviceToDevice, h->stream));
+        HIPCHK(h, dalloc(&n, cap * h->pstride));
+        HIPCHK(h, hipMemsetAsync(n, 0, cap * h->pstride * 4, h->stream));
+        if (*p && keep) HIPCHK(h, hipMemcpyAsync(n, *p, keep * h->pstride * 4, hipMemcpyDeviceToDevice, h->stream));
         if (*p) { HIPCHK(h, hipStreamSynchronize(h->stream)); (void)hipFree(*p); }
         *p = n;
     }
@@ -216,7 +249,19 @@ int grow_branches(lx_index *h, uint32_t need) {
     uint32_t ns = round_up(std::max<uint32_t>(need, h->stride + h->stride / 4), 64);
     uint32_t os = h->stride;
     uint64_t keep = h->hwm;
-    if (h->hb) {
+    if (h->sharded()) {
+        // planes hold local columns; the produced LowestAfter rows are B wide
+        int rc;
+        if (h->lap && (rc = relayout_lap(h, h->pstride, h->s_cap, ns))) return rc;
+        uint32_t *nc = nullptr;
+        HIPCHK(h, dalloc(&nc, ns));
+        HIPCHK(h, lx::launch_fill_u32(nc, ns, LX_NONE, h->stream));
+        if (h->cmap) HIPCHK(h, hipMemcpyAsync(nc, h->cmap, (uint64_t)std::min(os, h->cmap_cap) * 4, hipMemcpyDeviceToDevice, h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        if (h->cmap) (void)hipFree(h->cmap);
+        h->cmap = nc;
+        h->cmap_cap = ns;
+    } else if (h->hb) {
         uint32_t **planes[] = {&h->hb, &h->la};
         for (uint32_t **p : planes) {
             uint32_t *n = nullptr;
@@ -246,6 +291,7 @@ int grow_branches(lx_index *h, uint32_t need) {
     }
     h->brow = nb;
     h->stride = ns;
+    if (!h->sharded()) h->pstride = ns;
     return 0;
 }
 
@@ -260,7 +306,38 @@ int grow_scap(lx_index *h, uint32_t need) {
         (void)hipFree(h->brow);
     }
     h->brow = nb;
+    if (h->sharded()) {
+        int rc;
+        if ((rc = relayout_lap(h, h->pstride, ns, h->stride))) return rc;
+    }
     h->s_cap = ns;
+    return 0;
+}
+
+// a shard's plane columns (own originals + own fork branches) beyond pstride
+int grow_local(lx_index *h, uint32_t need) {
+    if (need <= h->pstride) return 0;
+    uint32_t np = round_up(std::max<uint32_t>(need, h->pstride + h->pstride / 4), 16);
+    int rc;
+    if ((rc = relayout_lap(h, np, h->s_cap, h->stride))) return rc;
+    uint32_t **planes[] = {&h->hb, &h->la};
+    for (uint32_t **p : planes) {
+        uint32_t *n = nullptr;
+        HIPCHK(h, dalloc(&n, h->n_cap * np));
+        HIPCHK(h, hipMemsetAsync(n, 0, h->n_cap * np * 4, h->stream));
+        if (*p) HIPCHK(h, lx::launch_copy_rows(n, np, *p, h->pstride, h->hwm, h->pstride, h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        if (*p) (void)hipFree(*p);
+        *p = n;
+    }
+    uint32_t *nw = nullptr;
+    HIPCHK(h, dalloc(&nw, np));
+    HIPCHK(h, hipMemsetAsync(nw, 0, np * 4ull, h->stream));
+    if (h->wloc) HIPCHK(h, hipMemcpyAsync(nw, h->wloc, h->pstride * 4ull, hipMemcpyDeviceToDevice, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    if (h->wloc) (void)hipFree(h->wloc);
+    h->wloc = nw;
+    h->pstride = np;
     return 0;
 }
 
@@ -314,7 +391,7 @@ int rebuild_columns(lx_index *h) {
     uint64_t need = std::max<uint64_t>({off.size(), br.size(), 1});
     if (need > h->cheat_cap) {
         uint64_t cap = std::max<uint64_t>(need * 2, 256);
-        uint32_t **arrs[] = {&h->cheat_off, &h->cheat_br, &h->cheat_creator};
+        uint32_t **arrs[] = {&h->cheat_off, &h->cheat_br, &h->cheat_creator, &h->cheat_brl, &h->cheat_crl};
         for (uint32_t **a : arrs) {
             if (*a) (void)hipFree(*a);
             HIPCHK(h, dalloc(a, cap));
@@ -325,6 +402,12 @@ int rebuild_columns(lx_index *h) {
         HIPCHK(h, hipMemcpyAsync(h->cheat_off, off.data(), off.size() * 4, hipMemcpyHostToDevice, h->stream));
         HIPCHK(h, hipMemcpyAsync(h->cheat_br, br.data(), br.size() * 4, hipMemcpyHostToDevice, h->stream));
         HIPCHK(h, hipMemcpyAsync(h->cheat_creator, cr.data(), cr.size() * 4, hipMemcpyHostToDevice, h->stream));
+        if (h->sharded()) {
+            for (auto &x : br) x = h->h_cmap[x];
+            for (auto &x : cr) x = h->h_cmap[x];
+        }
+        HIPCHK(h, hipMemcpyAsync(h->cheat_brl, br.data(), br.size() * 4, hipMemcpyHostToDevice, h->stream));
+        HIPCHK(h, hipMemcpyAsync(h->cheat_crl, cr.data(), cr.size() * 4, hipMemcpyHostToDevice, h->stream));
     }
     HIPCHK(h, hipStreamSynchronize(h->stream));
     return 0;
@@ -413,6 +496,12 @@ int add_batch_dev(lx_index *h, uint32_t n, const uint32_t *creator, const uint32
             h->h_branch_creator.push_back(cr[i]);
             h->h_branch_first.push_back(fs[i]);
             h->by_creator[cr[i]].push_back(h->B + i);
+            if (h->sharded())
+                h->h_cmap.push_back(cr[i] >= h->own_lo && cr[i] < h->own_hi ? h->nloc++ : LX_NONE);
+        }
+        if (h->sharded()) {
+            if ((rc = grow_local(h, h->nloc))) return rc;
+            HIPCHK(h, hipMemcpyAsync(h->cmap + h->B, h->h_cmap.data() + h->B, nforks * 4ull, hipMemcpyHostToDevice, s));
         }
     }
     h->B = B_new;
@@ -422,7 +511,10 @@ int add_batch_dev(lx_index *h, uint32_t n, const uint32_t *creator, const uint32
     IndexArgs ia{};
     ia.hb = h->hb;
     ia.la = h->la;
-    ia.stride = h->stride;
+    ia.stride = h->pstride;
+    ia.cmap = h->sharded() ? h->cmap : nullptr;
+    ia.lap = h->sharded() ? h->lap : nullptr;
+    ia.lap_stride = h->stride;
     ia.batch_start = (uint32_t)h->n_events;
     ia.n = n;
     ia.rec = h->b_rec;
@@ -482,7 +574,8 @@ int add_batch_dev(lx_index *h, uint32_t n, const uint32_t *creator, const uint32
     if (h->B > h->V && h->n_cheat) {
         MarkArgs m{};
         m.hb = h->hb;
-        m.stride = h->stride;
+        m.stride = h->pstride;
+        m.cmap = h->sharded() ? h->cmap : nullptr;
         m.batch_start = (uint32_t)h->n_events;
         m.n = n;
         m.V = h->V;
@@ -515,16 +608,26 @@ int fc_args(lx_index *h, uint64_t n, const uint32_t *a, const uint32_t *b, uint8
     FcArgs f{};
     f.hb = h->hb;
     f.la = h->la;
-    f.stride = h->stride;
+    f.stride = h->pstride;
     f.n_events = (uint32_t)h->n_events;
     f.n = n;
     f.qa = a;
     f.qb = b;
     f.out = out;
     f.partial = partial;
-    f.wpad = h->wpad;
-    f.vlo4 = h->own_lo / 4;
-    f.vhi4 = (h->own_hi + 3) / 4;
+    if (h->sharded()) {
+        f.wpad = h->wloc;     // local columns: own originals first
+        f.vlo4 = 0;
+        f.vhi4 = (h->own_hi - h->own_lo + 3) / 4;
+        f.cmap = h->cmap;
+    } else {
+        f.wpad = h->wpad;
+        f.vlo4 = h->own_lo / 4;
+        f.vhi4 = (h->own_hi + 3) / 4;
+        f.cmap = nullptr;
+    }
+    f.cheat_brl = h->cheat_brl;
+    f.cheat_crl = h->cheat_crl;
     f.quorum = h->quorum;
     f.ev_branch = h->ev_branch;
     f.n_cheat = h->n_cheat;
@@ -610,7 +713,10 @@ UnfillArgs unfill_args(lx_index *h) {
     UnfillArgs u{};
     u.hb = h->hb;
     u.la = h->la;
-    u.stride = h->stride;
+    u.stride = h->pstride;
+    u.cmap = h->sharded() ? h->cmap : nullptr;
+    u.lap = h->sharded() ? h->lap : nullptr;
+    u.lap_stride = h->stride;
     u.lo = (uint32_t)h->n_flushed;
     u.hi = (uint32_t)h->n_events;
     u.B = h->B;
@@ -816,27 +922,47 @@ int lx_reset(lx_index *h, uint32_t nv, const uint32_t *w) {
     h->sc_events = ~0ull;
     uint32_t reserve = h->reserve ? h->reserve : std::max<uint32_t>(64, nv / 16);
     uint32_t want_stride = round_up(nv + reserve, 64);
+    // a shard stores its own columns: originals + a share of the fork reserve
+    const uint32_t norig = h->own_hi - h->own_lo;
+    const uint32_t want_p = h->sharded() ? round_up(norig + std::max<uint32_t>(16, reserve / h->shard_count), 16)
+                                         : want_stride;
     // (re)allocate when the layout changes; otherwise zero what the last epoch used
-    if (want_stride > h->stride || (h->stride && want_stride * 2 < h->stride)) {
+    if (want_stride > h->stride || (h->stride && want_stride * 2 < h->stride) || want_p > h->pstride ||
+        (h->pstride && want_p * 2 < h->pstride)) {
         free_all(h);
         h->stride = 0;
         int rc;
         h->s_cap = 0;
+        h->pstride = h->sharded() ? want_p : 0;
         if ((rc = grow_branches(h, want_stride))) return rc;
+        if (h->sharded()) HIPCHK(h, dalloc(&h->wloc, h->pstride));
         uint32_t s0 = 1024;
         if (h->cap_hint) s0 = (uint32_t)std::min<uint64_t>(h->cap_hint / nv + 64, 0x7FFFFFFF);
         if ((rc = grow_scap(h, s0))) return rc;
         h->hwm = 0;
         if ((rc = grow_events(h, h->cap_hint ? h->cap_hint : 4096))) return rc;
     } else if (h->hwm) {
-        // HB: the walker rewrites columns [0, V) of every new event's row (the
-        // original branches always exist); only the fork-branch columns can
+        // HB: the walker rewrites the original columns of every new event's row
+        // (the original branches always exist); only the fork-branch columns can
         // keep stale values for rows written before such a branch existed
-        if (h->stride > nv)
-            HIPCHK(h, hipMemset2DAsync(h->hb + nv, (size_t)h->stride * 4, 0, (size_t)(h->stride - nv) * 4, h->hwm, h->stream));
-        HIPCHK(h, hipMemsetAsync(h->la, 0, h->hwm * h->stride * 4, h->stream));
+        const uint32_t no = h->sharded() ? norig : nv;
+        if (h->pstride > no)
+            HIPCHK(h, hipMemset2DAsync(h->hb + no, (size_t)h->pstride * 4, 0, (size_t)(h->pstride - no) * 4, h->hwm, h->stream));
+        HIPCHK(h, hipMemsetAsync(h->la, 0, h->hwm * h->pstride * 4, h->stream));
+        if (h->lap) HIPCHK(h, hipMemsetAsync(h->lap, 0, (uint64_t)h->pstride * h->s_cap * h->stride * 4, h->stream));
         HIPCHK(h, lx::launch_fill_u32(h->first_child, h->hwm, LX_NONE, h->stream));
         h->hwm = 0;
+    }
+    if (h->sharded()) {
+        h->h_cmap.assign(nv, LX_NONE);
+        for (uint32_t c = h->own_lo; c < h->own_hi; c++) h->h_cmap[c] = c - h->own_lo;
+        h->nloc = norig;
+        std::vector<uint32_t> wl(h->pstride, 0);
+        for (uint32_t c = h->own_lo; c < h->own_hi; c++) wl[c - h->own_lo] = w[c];
+        HIPCHK(h, hipMemcpyAsync(h->wloc, wl.data(), (uint64_t)h->pstride * 4, hipMemcpyHostToDevice, h->stream));
+        HIPCHK(h, lx::launch_fill_u32(h->cmap, h->cmap_cap, LX_NONE, h->stream));
+        HIPCHK(h, hipMemcpyAsync(h->cmap, h->h_cmap.data(), nv * 4ull, hipMemcpyHostToDevice, h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
     }
     if (h->first_root) (void)hipFree(h->first_root);
     HIPCHK(h, dalloc(&h->first_root, nv));
@@ -909,8 +1035,8 @@ int lx_drop_not_flushed(lx_index *h) {
     HIPCHK(h, lx::launch_unfill(unfill_args(h), h->stream));
     uint64_t rows = h->n_events - h->n_flushed;
     if (rows) {
-        HIPCHK(h, hipMemsetAsync(h->hb + h->n_flushed * h->stride, 0, rows * h->stride * 4, h->stream));
-        HIPCHK(h, hipMemsetAsync(h->la + h->n_flushed * h->stride, 0, rows * h->stride * 4, h->stream));
+        HIPCHK(h, hipMemsetAsync(h->hb + h->n_flushed * h->pstride, 0, rows * h->pstride * 4, h->stream));
+        HIPCHK(h, hipMemsetAsync(h->la + h->n_flushed * h->pstride, 0, rows * h->pstride * 4, h->stream));
     }
     HIPCHK(h, hipStreamSynchronize(h->stream));
     h->n_events = h->n_flushed;
@@ -920,6 +1046,14 @@ int lx_drop_not_flushed(lx_index *h) {
         h->h_branch_first.resize(h->B);
         for (auto &l : h->by_creator)
             while (!l.empty() && l.back() >= h->B) l.pop_back();
+        if (h->sharded()) {
+            // dropped fork columns: their plane columns were zeroed with the rows
+            // that used them (rows > n_flushed); older rows never saw them
+            for (uint32_t b = h->B; b < h->h_cmap.size(); b++)
+                if (h->h_cmap[b] != LX_NONE) h->nloc--;
+            h->h_cmap.resize(h->B);
+            HIPCHK(h, lx::launch_fill_u32(h->cmap + h->B, h->cmap_cap - h->B, LX_NONE, h->stream));
+        }
         return rebuild_columns(h);
     }
     return 0;
@@ -1065,6 +1199,7 @@ int lx_get_event_branch_id(lx_index *h, uint32_t ev, uint32_t *out) {
 static int event_row(lx_index *h, const uint32_t *plane, uint32_t ev, std::vector<uint32_t> &row, uint32_t *bbefore,
                      uint32_t *branch) {
     if (ev >= h->n_events) return h->fail(LX_ERR_ARG, "unknown event %u", ev);
+    if (h->sharded()) return h->fail(LX_ERR_STATE, "vector getters need an unsharded handle (shards hold their own columns)");
     HIPCHK(h, hipSetDevice(h->device));
     HIPCHK(h, hipStreamSynchronize(h->stream));
     row.resize(h->B);
@@ -1174,32 +1309,52 @@ int lx_shard_block(lx_index *h, uint32_t src, uint32_t dst, uint64_t *elems) {
     return 0;
 }
 
-int lx_la_pack_dev(lx_index *h, uint32_t dst, uint32_t *out, void *stream) {
-    if (!h || dst >= h->shard_count) return LX_ERR_ARG;
+// rows of shard `rows_of` x columns of shard `cols_of`, moved by `mode`
+static int la_xfer(lx_index *h, uint32_t rows_of, uint32_t cols_of, uint32_t *buf, int mode) {
+    if (!h->sharded()) return h->fail(LX_ERR_STATE, "LowestAfter exchange needs a column-sharded handle");
+    if (!h->have_epoch) return h->fail(LX_ERR_STATE, "exchange before lx_reset");
     HIPCHK(h, hipSetDevice(h->device));
     int rc;
     if ((rc = ensure_shard_rows(h))) return rc;
-    std::vector<uint32_t> cols = shard_cols(h, dst);
+    std::vector<uint32_t> cols = shard_cols(h, cols_of);
     if ((rc = upload_cols(h, cols))) return rc;
-    HIPCHK(h, lx::launch_la_block(h->la, h->stride, h->sc_rows[h->shard_rank], h->sc_nrows[h->shard_rank], h->sc_cols,
-                                  (uint32_t)cols.size(), out, 0, h->stream));
+    XferArgs x{};
+    x.lap = h->lap;
+    x.lap_stride = h->stride;
+    x.s_cap = h->s_cap;
+    x.la = h->la;
+    x.pstride = h->pstride;
+    x.cmap = h->cmap;
+    x.ev_branch = h->ev_branch;
+    x.ev_seq = h->ev_seq;
+    x.branch_first = h->branch_first;
+    x.rows = h->sc_rows[rows_of];
+    x.nrows = h->sc_nrows[rows_of];
+    x.cols = h->sc_cols;
+    x.ncols = (uint32_t)cols.size();
+    x.buf = buf;
+    x.mode = mode;
+    HIPCHK(h, lx::launch_la_xfer(x, h->stream));
     HIPCHK(h, hipStreamSynchronize(h->stream));
-    (void)stream;
     return 0;
 }
 
-int lx_la_unpack_dev(lx_index *h, uint32_t src, const uint32_t *in, void *stream) {
-    if (!h || src >= h->shard_count) return LX_ERR_ARG;
-    HIPCHK(h, hipSetDevice(h->device));
-    int rc;
-    if ((rc = ensure_shard_rows(h))) return rc;
-    std::vector<uint32_t> cols = shard_cols(h, h->shard_rank);
-    if ((rc = upload_cols(h, cols))) return rc;
-    HIPCHK(h, lx::launch_la_block(h->la, h->stride, h->sc_rows[src], h->sc_nrows[src], h->sc_cols,
-                                  (uint32_t)cols.size(), const_cast<uint32_t *>(in), 1, h->stream));
-    HIPCHK(h, hipStreamSynchronize(h->stream));
+int lx_la_pack_dev(lx_index *h, uint32_t dst, uint32_t *out, void *stream) {
+    if (!h || dst >= h->shard_count || dst == h->shard_rank || !out) return LX_ERR_ARG;
     (void)stream;
-    return 0;
+    return la_xfer(h, h->shard_rank, dst, out, 0);
+}
+
+int lx_la_unpack_dev(lx_index *h, uint32_t src, const uint32_t *in, void *stream) {
+    if (!h || src >= h->shard_count || src == h->shard_rank || !in) return LX_ERR_ARG;
+    (void)stream;
+    return la_xfer(h, src, h->shard_rank, const_cast<uint32_t *>(in), 1);
+}
+
+int lx_la_own_dev(lx_index *h, void *stream) {
+    if (!h) return LX_ERR_ARG;
+    (void)stream;
+    return la_xfer(h, h->shard_rank, h->shard_rank, nullptr, 2);
 }
 
 int lx_last_stats(const lx_index *h, lx_stats *out) {
@@ -1212,7 +1367,7 @@ int lx_device_planes(lx_index *h, void **hb, void **la, uint32_t *stride, void *
     if (!h) return LX_ERR_ARG;
     if (hb) *hb = h->hb;
     if (la) *la = h->la;
-    if (stride) *stride = h->stride;
+    if (stride) *stride = h->pstride;
     if (stream) *stream = h->stream;
     return 0;
 }
@@ -1240,7 +1395,7 @@ int lx_index_view(lx_index *h, IndexView *o) {
     o->device = h->device;
     o->hb = h->hb;
     o->la = h->la;
-    o->stride = h->stride;
+    o->stride = h->pstride;
     o->n_events = h->n_events;
     o->V = h->V;
     o->B = h->B;

@@ -6,6 +6,15 @@
 //                       marker of creator(b) as seen by e (branches < B_after(e))
 //   la[e*stride + b]  : LowestAfter seq (0 = none)
 //   brow[b*s_cap + s - first(b)] : dense index of the event of branch b at seq s
+// Column-sharded handles store only their own columns:
+//   cmap[b]           : plane column of global branch b (NONE: another shard's)
+//   hb, la            : rows of pstride = local column capacity (own originals
+//                       first, then own fork branches in creation order);
+//                       `la` holds the exchanged LowestAfter of own columns
+//   lap[(cmap[c]*s_cap + s - first(c)) * stride + j] : LowestAfter entry j of
+//                       the event (c, s) of an own branch c, as the walker
+//                       produces it (all B columns), the source of the exchange
+// Unsharded handles: cmap = NULL (identity), pstride = stride, lap = NULL.
 // Per event: ev_creator, ev_seq, ev_branch, ev_bbefore (B before Add), ev_sp
 // (self-parent or NONE), first_child (first self-child that continued the
 // branch, claimed by atomicMin).  Per branch: branch_first, branch_creator,
@@ -54,6 +63,9 @@ struct IndexArgs {
     uint32_t diag;               // timing-only diagnostics (LX_DIAG): 2 no deps, 3 no global stores
     unsigned long long *prof;    // optional per-wave counters (LX_PROF=1), kProfSlots per wave
     uint32_t small;              // small-LDS walker variant (LX_SMALL=1)
+    const uint32_t *cmap;        // sharded: global branch -> plane column (NULL = identity)
+    uint32_t *lap;               // sharded: LowestAfter rows of own branches (fill target)
+    uint64_t lap_stride;         // = global branch capacity
 };
 constexpr int kProfSlots = 16;   // see k_index: passes, spin misses, chunk folds, completes, ...
 
@@ -105,6 +117,9 @@ struct FcArgs {
     const uint32_t *cheat_off;
     const uint32_t *cheat_br;
     const uint32_t *cheat_creator;
+    const uint32_t *cheat_brl;   // cheat_br / cheat_creator as plane columns
+    const uint32_t *cheat_crl;
+    const uint32_t *cmap;        // sharded: global branch -> plane column (NULL = identity)
     uint32_t own_lo, own_hi;     // creator range owned by this shard
     const uint32_t *branch_creator;
     uint32_t *status;            // status[1] |= bad-event flag
@@ -122,6 +137,7 @@ struct MarkArgs {
     uint32_t n_cheat;
     const uint32_t *cheat_off;
     const uint32_t *cheat_br;
+    const uint32_t *cmap;        // sharded: global branch -> plane column (NULL = identity)
 };
 
 struct UnfillArgs {
@@ -142,6 +158,29 @@ struct UnfillArgs {
     const uint32_t *brow;
     uint32_t s_cap;
     uint32_t B_keep;             // branches that survive the rollback
+    const uint32_t *cmap;        // sharded: global branch -> plane column (NULL = identity)
+    uint32_t *lap;               // sharded: produced LowestAfter rows (see top)
+    uint64_t lap_stride;
+};
+
+// LowestAfter exchange between column shards: mode 0 pack (lap -> buf),
+// 1 unpack (buf -> la), 2 own block (lap -> la); buf is [rows][cols]
+struct XferArgs {
+    const uint32_t *lap;
+    uint64_t lap_stride;
+    uint32_t s_cap;
+    uint32_t *la;
+    uint64_t pstride;
+    const uint32_t *cmap;
+    const uint32_t *ev_branch;
+    const uint32_t *ev_seq;
+    const uint32_t *branch_first;
+    const uint32_t *rows;        // events (global dense indices)
+    uint32_t nrows;
+    const uint32_t *cols;        // global branch ids
+    uint32_t ncols;
+    uint32_t *buf;
+    int mode;
 };
 
 // ---- write-back to the reference's byte formats (lx_persist.hip)
@@ -250,8 +289,7 @@ hipError_t launch_fill_u32(uint32_t *p, uint64_t n, uint32_t v, hipStream_t s);
 hipError_t launch_shard_rows(const uint32_t *ev_branch, const uint32_t *branch_creator, uint32_t n, uint32_t lo,
                              uint32_t hi, uint32_t *flag, uint32_t *pos, void *scan_tmp, size_t scan_bytes,
                              uint32_t *rows, hipStream_t s);
-hipError_t launch_la_block(uint32_t *la, uint64_t stride, const uint32_t *rows, uint32_t nrows, const uint32_t *cols,
-                           uint32_t ncols, uint32_t *buf, int unpack, hipStream_t s);
+hipError_t launch_la_xfer(const XferArgs &a, hipStream_t s);
 hipError_t launch_dirty_la(const UnfillArgs &a, uint32_t *flag, hipStream_t s);
 hipError_t persist_tmp_bytes(uint32_t n, size_t *bytes);
 hipError_t launch_compact(const uint32_t *flag, uint32_t *pos, uint32_t n, void *tmp, size_t tmp_bytes,

@@ -422,7 +422,9 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
     const uint32_t RA = lds_addr(ring);
     const uint32_t RB = RA + (uint32_t)(RN * 16);   // second units (CPW 4 only)
 
-    uint32_t col[CPW], first[CPW];
+    // col = global branch (semantics), pc = plane column (addressing; differs
+    // from col only in a column-sharded handle, which stores its own columns)
+    uint32_t col[CPW], first[CPW], pc[CPW];
     bool valid[CPW];
     bool contig = true;
 #pragma unroll
@@ -430,10 +432,11 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
         const uint32_t ci = slice * CPW + k;
         valid[k] = ci < a.ncols;
         col[k] = valid[k] ? a.col_list[ci] : 0;
+        pc[k] = valid[k] ? (a.cmap ? a.cmap[col[k]] : col[k]) : 0;
         first[k] = valid[k] ? a.branch_first[col[k]] : 1;
-        contig &= valid[k] && col[k] == col[0] + k;
+        contig &= valid[k] && pc[k] == pc[0] + k;
     }
-    contig &= (col[0] % CPW) == 0;
+    contig &= (pc[0] % CPW) == 0;
 
     if (wave == NCW) {
         // ------------------------------------------------------------ loader
@@ -535,7 +538,7 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
                     if (!got) {
                         const uint32_t *row = a.hb + (uint64_t)prev * stride;
 #pragma unroll
-                        for (int k = 0; k < CPW; k++) h0[k] = valid[k] ? ld_l2_now(row + col[k]) : 0u;
+                        for (int k = 0; k < CPW; k++) h0[k] = valid[k] ? ld_l2_now(row + pc[k]) : 0u;
                     }
 #pragma unroll
                     for (int k = 0; k < CPW; k++) h0[k] &= mask;
@@ -548,13 +551,13 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
                 // HB row (raw values incl. fork bits as published)
                 uint32_t *hrow = a.hb + (uint64_t)(bs + ev) * stride;
                 if (contig) {
-                    if (CPW == 1) hrow[col[0]] = r[0];
-                    else if (CPW == 2) *reinterpret_cast<uint2 *>(hrow + col[0]) = make_uint2(r[0], r[1 % CPW]);
-                    else *reinterpret_cast<uint4 *>(hrow + col[0]) = make_uint4(r[0], r[1 % CPW], r[2 % CPW], r[3 % CPW]);
+                    if (CPW == 1) hrow[pc[0]] = r[0];
+                    else if (CPW == 2) *reinterpret_cast<uint2 *>(hrow + pc[0]) = make_uint2(r[0], r[1 % CPW]);
+                    else *reinterpret_cast<uint4 *>(hrow + pc[0]) = make_uint4(r[0], r[1 % CPW], r[2 % CPW], r[3 % CPW]);
                 } else {
 #pragma unroll
                     for (int k = 0; k < CPW; k++)
-                        if (valid[k]) hrow[col[k]] = r[k];
+                        if (valid[k]) hrow[pc[k]] = r[k];
                 }
                 if (FILL) {
                     // LowestAfter range fill: events (col, s), s in (h0, r], are first
@@ -564,6 +567,12 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
                         if (!valid[k]) continue;
                         const uint32_t lo = max(h0[k] + 1u, first[k]);
                         const uint32_t hi = r[k] & mask;
+                        if (a.lap) {
+                            // sharded: rows of own branches addressed by (column, seq)
+                            for (uint32_t s = lo; s <= hi; s++)
+                                a.lap[((uint64_t)pc[k] * a.s_cap + (s - first[k])) * a.lap_stride + br] = seq;
+                            continue;
+                        }
                         for (uint32_t s = lo; s <= hi; s++) {
                             const uint64_t cc = __hip_atomic_load(reinterpret_cast<const uint64_t *>(brc + k * KB + s % KB),
                                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -665,7 +674,7 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
                         const uint32_t *row = a.hb + (uint64_t)(lpp + bs) * stride;
 #pragma unroll
                         for (int k = 0; k < CPW; k++)
-                            if (valid[k]) r[k] = max(r[k], ld_l2_now(row + col[k]) & mask);
+                            if (valid[k]) r[k] = max(r[k], ld_l2_now(row + pc[k]) & mask);
                         tn &= ~(1u << j);
                     }
                 }
@@ -701,7 +710,7 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
                 const uint32_t *row = a.hb + (uint64_t)p * stride;
 #pragma unroll
                 for (int k = 0; k < CPW; k++)
-                    if (valid[k]) r[k] = max(r[k], ld_l2_now(row + col[k]) & mask);
+                    if (valid[k]) r[k] = max(r[k], ld_l2_now(row + pc[k]) & mask);
                 ok = true;
             }
             if (ok) xi++;
@@ -791,20 +800,21 @@ __global__ void k_marks(MarkArgs a) {
     while (m > 0 && lst[m - 1] >= bafter) m--;
     if (m < 2) return;
     uint32_t *row = a.hb + (uint64_t)e * a.stride;
+    const uint32_t *cm = a.cmap;
     bool hit = false;
     for (uint32_t x = 0; x < m && !hit; x++) {
-        uint32_t bx = lst[x], sx = row[bx] & LX_SEQ_MASK;
+        uint32_t bx = lst[x], sx = row[cm ? cm[bx] : bx] & LX_SEQ_MASK;
         if (!sx) continue;
         uint32_t fx = a.branch_first[bx];
         for (uint32_t y = x + 1; y < m; y++) {
-            uint32_t by = lst[y], sy = row[by] & LX_SEQ_MASK;
+            uint32_t by = lst[y], sy = row[cm ? cm[by] : by] & LX_SEQ_MASK;
             if (!sy) continue;
             uint32_t fy = a.branch_first[by];
             if (fx <= sy && fy <= sx) { hit = true; break; }
         }
     }
     if (hit)
-        for (uint32_t x = 0; x < m; x++) row[lst[x]] |= LX_MARK;
+        for (uint32_t x = 0; x < m; x++) row[cm ? cm[lst[x]] : lst[x]] |= LX_MARK;
 }
 
 hipError_t launch_marks(const MarkArgs &a, hipStream_t s) {
@@ -847,13 +857,15 @@ __global__ __launch_bounds__(256) void k_fc(FcArgs a) {
         if (FORKS) {
             const uint32_t *hrow = a.hb + (uint64_t)A * a.stride;
             const uint32_t *lrow = a.la + (uint64_t)Bq * a.stride;
+            // plane columns (cheat_crl / cheat_brl): the creator's original
+            // branch and its fork branches
             for (uint32_t c = lane; c < a.n_cheat; c += LPQ) {
                 const uint32_t o0 = a.cheat_off[c], o1 = a.cheat_off[c + 1];
-                const uint32_t n = a.cheat_creator[c];
+                const uint32_t n = a.cheat_crl[c];
                 const uint32_t cn = fc_term(lrow[n], hrow[n], 1u, true);
                 uint32_t hit = 0;
                 for (uint32_t o = o0 + 1; o < o1; o++) {
-                    const uint32_t j = a.cheat_br[o];
+                    const uint32_t j = a.cheat_brl[o];
                     hit |= fc_term(lrow[j], hrow[j], 1u, true);
                 }
                 if (!cn && hit) sum += a.wpad[n];
@@ -861,7 +873,7 @@ __global__ __launch_bounds__(256) void k_fc(FcArgs a) {
             if (lane == 0) {
                 const uint32_t bb = a.ev_branch[Bq];
                 const uint32_t cb = a.branch_creator[bb];
-                if (cb >= a.own_lo && cb < a.own_hi && (hrow[bb] & LX_MARK)) early = 1;
+                if (cb >= a.own_lo && cb < a.own_hi && (hrow[a.cmap ? a.cmap[bb] : bb] & LX_MARK)) early = 1;
             }
         }
 #pragma unroll
@@ -915,13 +927,19 @@ __global__ void k_unfill(UnfillArgs a) {
     if (t >= total) return;
     uint32_t e = a.lo + (uint32_t)(t / a.B);
     uint32_t c = (uint32_t)(t % a.B);
+    const uint32_t pcol = a.cmap ? a.cmap[c] : c;
+    if (pcol == LX_NONE) return;                      // another shard's column
     uint32_t br = a.ev_branch[e];
     uint32_t sp = a.ev_sp[e];
     bool fork = (br == a.ev_bbefore[e]);
-    uint32_t h1 = a.hb[(uint64_t)e * a.stride + c] & LX_SEQ_MASK;
-    uint32_t h0 = (sp != LX_NONE && !fork) ? (a.hb[(uint64_t)sp * a.stride + c] & LX_SEQ_MASK) : 0u;
+    uint32_t h1 = a.hb[(uint64_t)e * a.stride + pcol] & LX_SEQ_MASK;
+    uint32_t h0 = (sp != LX_NONE && !fork) ? (a.hb[(uint64_t)sp * a.stride + pcol] & LX_SEQ_MASK) : 0u;
     uint32_t first = a.branch_first[c];
     for (uint32_t s = max(h0 + 1u, first); s <= h1; s++) {
+        if (a.lap) {
+            a.lap[((uint64_t)pcol * a.s_cap + (s - first)) * a.lap_stride + br] = 0;
+            continue;
+        }
         uint32_t row = a.brow[(uint64_t)c * a.s_cap + (s - first)];
         a.la[(uint64_t)row * a.stride + br] = 0;
     }
@@ -971,15 +989,24 @@ __global__ void k_compact(const uint32_t *flag, const uint32_t *pos, uint32_t n,
     if (flag[e]) rows[pos[e] - 1] = (uint32_t)e;
 }
 
-// out[i][k] = la[rows[i]][cols[k]]   (pack)   /   la[rows[i]][cols[k]] = in[i][k]   (unpack)
-__global__ void k_la_block(uint32_t *la, uint64_t stride, const uint32_t *rows, uint32_t nrows, const uint32_t *cols,
-                           uint32_t ncols, uint32_t *buf, int unpack) {
+// buf[i][k] is LowestAfter entry cols[k] of event rows[i]:
+//   pack   : from the produced rows (lap) of this shard's branches
+//   unpack : into the query plane (la), own columns
+//   own    : lap -> la for this shard's rows x its own columns
+__global__ void k_la_xfer(XferArgs a) {
     uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= (uint64_t)nrows * ncols) return;
-    const uint32_t i = (uint32_t)(t / ncols), k = (uint32_t)(t % ncols);
-    uint32_t *cell = la + (uint64_t)rows[i] * stride + cols[k];
-    if (unpack) *cell = buf[t];
-    else buf[t] = *cell;
+    if (t >= (uint64_t)a.nrows * a.ncols) return;
+    const uint32_t i = (uint32_t)(t / a.ncols), k = (uint32_t)(t % a.ncols);
+    const uint32_t e = a.rows[i], j = a.cols[k];
+    uint32_t v;
+    if (a.mode == 1) {
+        v = a.buf[t];
+    } else {
+        const uint32_t b = a.ev_branch[e];
+        v = a.lap[((uint64_t)a.cmap[b] * a.s_cap + (a.ev_seq[e] - a.branch_first[b])) * a.lap_stride + j];
+    }
+    if (a.mode == 0) a.buf[t] = v;
+    else a.la[(uint64_t)e * a.pstride + a.cmap[j]] = v;
 }
 
 hipError_t launch_shard_rows(const uint32_t *ev_branch, const uint32_t *branch_creator, uint32_t n, uint32_t lo,
@@ -994,12 +1021,10 @@ hipError_t launch_shard_rows(const uint32_t *ev_branch, const uint32_t *branch_c
     return hipGetLastError();
 }
 
-hipError_t launch_la_block(uint32_t *la, uint64_t stride, const uint32_t *rows, uint32_t nrows, const uint32_t *cols,
-                           uint32_t ncols, uint32_t *buf, int unpack, hipStream_t s) {
-    uint64_t total = (uint64_t)nrows * ncols;
+hipError_t launch_la_xfer(const XferArgs &a, hipStream_t s) {
+    uint64_t total = (uint64_t)a.nrows * a.ncols;
     if (!total) return hipSuccess;
-    hipLaunchKernelGGL(k_la_block, dim3((uint32_t)((total + 255) / 256)), dim3(256), 0, s, la, stride, rows, nrows,
-                       cols, ncols, buf, unpack);
+    hipLaunchKernelGGL(k_la_xfer, dim3((uint32_t)((total + 255) / 256)), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 

@@ -43,6 +43,7 @@ SIGNATURES = [
     ("lx_shard_block", ctypes.c_int, [vp, ctypes.c_uint32, ctypes.c_uint32, u64p]),
     ("lx_la_pack_dev", ctypes.c_int, [vp, ctypes.c_uint32, vp, vp]),
     ("lx_la_unpack_dev", ctypes.c_int, [vp, ctypes.c_uint32, vp, vp]),
+    ("lx_la_own_dev", ctypes.c_int, [vp, vp]),
     ("lx_last_stats", ctypes.c_int, [vp, vp]),
     ("lx_device_planes", ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), u32p, ctypes.POINTER(vp)]),
     ("lx_sync", ctypes.c_int, [vp]),
@@ -99,6 +100,14 @@ def load_library(path=LIB_PATH):
     """Load the HIP library; raises if it is missing (no fallback path)."""
     global _lib
     if _lib is None:
+        # One HIP runtime per process: PyTorch-ROCm bundles its own
+        # libamdhip64.so.7 (same soname as /opt/rocm's).  Loading torch first
+        # makes this library bind to torch's copy; loading ours first would
+        # make torch bind to /opt/rocm's, and torch then finds no GPU.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         if not os.path.exists(path):
             raise ImportError("HIP library not built: %s (run __graft_entry__.build())" % path)
         L = ctypes.CDLL(path)
@@ -282,6 +291,9 @@ class Index:
 
     def la_unpack_dev(self, src, in_ptr):
         self._chk(self.L.lx_la_unpack_dev(self.h, src, in_ptr, None))
+
+    def la_own_dev(self):
+        self._chk(self.L.lx_la_own_dev(self.h, None))
 
     def last_stats(self):
         st = LxStats()

@@ -79,6 +79,7 @@ class ShardedIndex:
             if recv_n[s]:
                 self.ix.la_unpack_dev(s, recv.data_ptr() + 4 * off)
             off += recv_n[s]
+        self.ix.la_own_dev()     # own rows x own columns, no communication
         self.ix.sync()
         return send_n
 

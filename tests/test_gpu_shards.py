@@ -11,16 +11,11 @@ from oracle import corc
 pytestmark = pytest.mark.gpu
 
 
-def sharded_fc(lx, d, weights, G, qa, qb):
+def exchange(shards):
+    """What ShardedIndex.exchange's all-to-all does between GPUs."""
     import torch
     dev = torch.device("cuda", 0)
-    shards = []
-    for r in range(G):
-        ix = lx.Index(shard_rank=r, shard_count=G)
-        ix.reset(weights)
-        ix.add_batch(d.creator, d.seq, d.poff, d.par)
-        shards.append(ix)
-    # all-to-all of LowestAfter blocks
+    G = len(shards)
     for s in range(G):
         for t in range(G):
             if s == t:
@@ -30,6 +25,14 @@ def sharded_fc(lx, d, weights, G, qa, qb):
             buf = torch.zeros(max(n, 1), dtype=torch.int32, device=dev)
             shards[s].la_pack_dev(t, buf.data_ptr())
             shards[t].la_unpack_dev(s, buf.data_ptr())
+    for ix in shards:
+        ix.la_own_dev()
+
+
+def fc(lx, shards, qa, qb):
+    """Partial stake sums per shard, added (the all-reduce), combined."""
+    import torch
+    dev = torch.device("cuda", 0)
     a = torch.from_numpy(qa.view(np.int32)).to(dev)
     b = torch.from_numpy(qb.view(np.int32)).to(dev)
     total = torch.zeros(len(qa), dtype=torch.int64, device=dev)
@@ -43,7 +46,18 @@ def sharded_fc(lx, d, weights, G, qa, qb):
     out = torch.zeros(len(qa), dtype=torch.uint8, device=dev)
     shards[0].fc_combine_dev(len(qa), s32.data_ptr(), out.data_ptr())
     shards[0].sync()
-    return out.cpu().numpy(), shards
+    return out.cpu().numpy()
+
+
+def sharded_fc(lx, d, weights, G, qa, qb):
+    shards = []
+    for r in range(G):
+        ix = lx.Index(shard_rank=r, shard_count=G)
+        ix.reset(weights)
+        ix.add_batch(d.creator, d.seq, d.poff, d.par)
+        shards.append(ix)
+    exchange(shards)
+    return fc(lx, shards, qa, qb), shards
 
 
 @pytest.mark.parametrize("G", [2, 3, 4])
@@ -63,3 +77,62 @@ def test_sharded_fc_matches_oracle(G, shape):
     ranges = [shards[0].shard_range(r) for r in range(G)]
     assert ranges[0][0] == 0 and ranges[-1][1] == n
     assert all(ranges[i][1] == ranges[i + 1][0] for i in range(G - 1))
+
+
+def test_shard_planes_hold_own_columns():
+    """Memory per GPU ~ 1/G: a shard's plane rows are its own columns only."""
+    import lachesis_hip as lx
+    d = lx.tools.gen_dag(64, 10, 5, 0, 0, 3)
+    w = [1] * 64
+    full = lx.Index()
+    full.reset(w)
+    full.add_batch(d.creator, d.seq, d.poff, d.par)
+    stride = full.device_planes()[2]
+    for G in (2, 4):
+        for r in range(G):
+            ix = lx.Index(shard_rank=r, shard_count=G)
+            ix.reset(w)
+            ix.add_batch(d.creator, d.seq, d.poff, d.par)
+            lo, hi = ix.shard_range(r)
+            p = ix.device_planes()[2]
+            assert hi - lo <= p < stride // G + 32, (G, r, p, stride)
+            with pytest.raises(lx.LxError):
+                ix.highest_before(0)          # shards hold partial rows
+
+
+@pytest.mark.parametrize("G", [2, 3])
+def test_sharded_drop_and_reexchange(G):
+    """DropNotFlushed on every shard (incl. fork branches created after the
+    flush), exchange again, FC equals the oracle of the flushed prefix; then
+    re-add and compare with the full oracle."""
+    import lachesis_hip as lx
+    d = lx.tools.gen_dag(20, 30, 5, 4, 6, 5)
+    rng = np.random.default_rng(5)
+    weights = sorted((int(x) for x in rng.integers(1, 30, 20)), reverse=True)
+    cut = 80                   # 26 branches here, 37 at the end: forks after the flush
+    shards = []
+    for r in range(G):
+        ix = lx.Index(shard_rank=r, shard_count=G)
+        ix.reset(weights)
+        ix.add_batch(d.creator[:cut], d.seq[:cut], d.poff[:cut + 1], d.par)
+        ix.flush()
+        ix.add_batch(d.creator[cut:], d.seq[cut:], d.poff[cut:] , d.par)
+        shards.append(ix)
+    assert shards[0].num_branches() == 37
+    o = corc.OracleIndex(weights)
+    assert o.add_batch(d.creator, d.seq, d.poff, d.par) == -1
+    qa, qb = lx.tools.fc_queries(d.lamport, 20_000, window=30, seed=1)
+    exchange(shards)
+    np.testing.assert_array_equal(fc(lx, shards, qa, qb), o.forkless_cause_batch(qa, qb))
+    for ix in shards:
+        ix.drop_not_flushed()
+        assert ix.num_branches() == 26
+    o1 = corc.OracleIndex(weights)
+    assert o1.add_batch(d.creator[:cut], d.seq[:cut], d.poff[:cut + 1], d.par) == -1
+    qa1, qb1 = lx.tools.fc_queries(d.lamport[:cut], 20_000, window=30, seed=2)
+    exchange(shards)
+    np.testing.assert_array_equal(fc(lx, shards, qa1, qb1), o1.forkless_cause_batch(qa1, qb1))
+    for ix in shards:
+        ix.add_batch(d.creator[cut:], d.seq[cut:], d.poff[cut:], d.par)
+    exchange(shards)
+    np.testing.assert_array_equal(fc(lx, shards, qa, qb), o.forkless_cause_batch(qa, qb))

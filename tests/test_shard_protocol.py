@@ -55,6 +55,9 @@ class FakeShard:
         blk = self._view(ptr, n).reshape(len(self.rows[src]), len(self.cols[self.r]))
         self.la[np.ix_(self.rows[src], self.cols[self.r])] = blk
 
+    def la_own_dev(self):
+        pass                                        # own block already in self.la
+
     def forkless_cause_partial_dev(self, n, pa, pb, pout):
         a, b = self._view(pa, n), self._view(pb, n)
         c = self.cols[self.r]
