@@ -168,6 +168,9 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--mode", default="shard", choices=["replica", "shard"])
     ap.add_argument("--no-abft", action="store_true", help="skip the configs[4] abft leg")
+    ap.add_argument("--shard-solo", type=int, default=0,
+                    help="diagnostic: time rank 0 of a G-way column shard alone on this GPU (its index walk, "
+                         "the packing of its outgoing LowestAfter blocks, its partial FC); no collectives")
     args = ap.parse_args()
 
     import numpy as np
@@ -218,7 +221,12 @@ def main():
     d_out = torch.empty(args.fc_queries, dtype=torch.uint8, device=dev)
 
     shard = args.mode == "shard" and world > 1
-    if shard:
+    solo = args.shard_solo if world == 1 and args.shard_solo > 1 else 0
+    if solo:
+        ix = lx.Index(device=local, event_capacity=N, shard_rank=0, shard_count=solo)
+        d_part = torch.empty(args.fc_queries, dtype=torch.int32, device=dev)
+        d_blk = None
+    elif shard:
         ix = lx.Index(device=local, event_capacity=N, shard_rank=rank, shard_count=world)
         from lachesis_hip.shard import ShardedIndex
         sx = ShardedIndex(ix, device=dev)
@@ -238,6 +246,14 @@ def main():
             st_asg += s["ms_assign"] + s["ms_marks"]
         if shard:
             sx.exchange()
+        if solo:
+            nonlocal d_blk
+            sizes = [ix.shard_block(0, t) for t in range(1, solo)]
+            if d_blk is None:
+                d_blk = torch.empty(max(sizes + [1]), dtype=torch.int32, device=dev)
+            for t in range(1, solo):
+                ix.la_pack_dev(t, d_blk.data_ptr())
+            ix.la_own_dev()
         return st_idx, st_asg
 
     _, _, _, stream_ptr = ix.device_planes()
@@ -246,7 +262,7 @@ def main():
     def fc_step(evs=None):
         if evs is not None:
             evs[0].record(lib_stream)
-        if shard:
+        if shard or solo:
             ix.forkless_cause_partial_dev(args.fc_queries, d_qa.data_ptr(), d_qb.data_ptr(), d_part.data_ptr())
         else:
             ix.forkless_cause_batch_dev(args.fc_queries, d_qa.data_ptr(), d_qb.data_ptr(), d_out.data_ptr())
@@ -305,7 +321,7 @@ def main():
     events_per_s = N * args.steps * units / t_index
     fc_per_s = args.fc_queries * args.steps * units / t_fc
     B = ix.num_branches()
-    if shard:
+    if shard or solo:
         lo, hi = ix.shard_range(rank)
         B = hi - lo                         # columns this rank streams (no forks in the bench DAG)
     fc_bytes = 8.0 * B * args.fc_queries                       # HB(a).Seq 4B + LA(b) 4B per branch
@@ -335,7 +351,8 @@ def main():
         "config": {"workload": "%s: V=%d, %d events (%d/validator), P=%d, %s stakes, cheaters=%d; FC 2^%d queries, b within 64 Lamport of a"
                    % (args.config, V, N, epv, P, wkind, cheaters, int(np.log2(args.fc_queries)), ),
                    "validators": V, "events": N, "parents": P, "fc_queries": args.fc_queries,
-                   "parallelism": ("colshard%d" if shard else "replica%d") % world, "batch": batch},
+                   "parallelism": ("solo-shard0-of-%d" % solo) if solo else
+                                  ("colshard%d" if shard else "replica%d") % world, "batch": batch},
         "fc_queries_per_sec": fc_per_s,
         "fc_ms_per_step": t_fc / args.steps * 1e3,
         "index_kernel_ms": kidx,
