@@ -263,8 +263,9 @@ template <int CPW, bool SMALL>
 struct Ring {
     // slots: 64 KB of units, or 16 KB in the small-LDS variant (several
     // workgroups per CU when each owns few columns)
-    static constexpr int BYTES = SMALL ? 16384 : 65536;
-    static constexpr int N = BYTES / (CPW == 1 ? 8 : 32);
+    // (CPW 2 uses one 16-B unit per slot: 2048 slots in 32 KB)
+    static constexpr int BYTES = SMALL ? 16384 : (CPW == 2 ? 32768 : 65536);
+    static constexpr int N = BYTES / (CPW == 1 ? 8 : CPW == 2 ? 16 : 32);
 };
 
 struct WalkShared {
@@ -764,6 +765,14 @@ static hipError_t launch_index_c(const IndexArgs &a, uint32_t ncw, hipStream_t s
             return launch_index_t<CPW, 2, 256, true>(a, s);
         }
     }
+    if constexpr (CPW == 2) {
+        // 512-record ring: ~72 KB of LDS, two workgroups per CU
+        if (a.rr_hint == 512) {
+            if (ncw <= 1) return launch_index_t<CPW, 1, 512, false>(a, s);
+            if (ncw <= 2) return launch_index_t<CPW, 2, 512, false>(a, s);
+            return launch_index_t<CPW, 4, 512, false>(a, s);
+        }
+    }
     if (ncw <= 1) return launch_index_t<CPW, 1, 1024, false>(a, s);
     if (ncw <= 2) return launch_index_t<CPW, 2, 1024, false>(a, s);
     return launch_index_t<CPW, 4, 1024, false>(a, s);
@@ -900,10 +909,15 @@ static hipError_t launch_fc_t(const FcArgs &a, bool forks, hipStream_t s) {
     return hipGetLastError();
 }
 
+// lanes per query: ~4 uint4 per lane, so every lane has ~8 16-B loads in flight
+// (HB and LA) whatever the row length -- short rows (few validators, or a
+// column shard) would otherwise leave one load pair per lane and stay latency-bound
 hipError_t launch_fc(const FcArgs &a, uint32_t cols, bool forks, hipStream_t s) {
     const uint32_t nv = a.vhi4 - a.vlo4;
-    if (nv <= 16) return launch_fc_t<16>(a, forks, s);
-    if (nv <= 32) return launch_fc_t<32>(a, forks, s);
+    if (nv <= 16) return launch_fc_t<4>(a, forks, s);
+    if (nv <= 32) return launch_fc_t<8>(a, forks, s);
+    if (nv <= 64) return launch_fc_t<16>(a, forks, s);
+    if (nv <= 128) return launch_fc_t<32>(a, forks, s);
     return launch_fc_t<64>(a, forks, s);
 }
 

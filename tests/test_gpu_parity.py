@@ -369,6 +369,7 @@ WALKER_VARIANTS = [
     {"LX_CPW": "1", "LX_NCW": "1"}, {"LX_CPW": "2", "LX_NCW": "2"}, {"LX_CPW": "4", "LX_NCW": "4"},
     {"LX_CPW": "4", "LX_NCW": "1"}, {"LX_CPW": "1", "LX_NCW": "4"},
     {"LX_SMALL": "1", "LX_CPW": "1", "LX_NCW": "1"}, {"LX_SMALL": "1", "LX_CPW": "2", "LX_NCW": "2"},
+    {"LX_RR": "512", "LX_CPW": "2", "LX_NCW": "4"}, {"LX_RR": "512", "LX_CPW": "2", "LX_NCW": "2"},
 ]
 
 
