@@ -386,7 +386,18 @@ __device__ __forceinline__ uint32_t rec_off(uint32_t slot, uint32_t q) {
     return (slot & ~63u) * LX_REC_Q + q * 64u + (slot & 63u);
 }
 
-template <int CPW, int NCW, int RR, bool FILL, bool SMALL>
+// Per-wave walker counters (LX_PROF=1) are compiled in only with
+// -DLX_WALKER_PROF (make WPROF=1): the increments cost the compute pass
+// several VALU instructions.
+#ifdef LX_WALKER_PROF
+#define LX_WP(x) x
+#else
+#define LX_WP(x)
+#endif
+
+// MASKED: older rows may carry fork marks in bit 31 (B > V); without forks
+// the seq values are used unmasked.
+template <int CPW, int NCW, int RR, bool FILL, bool SMALL, bool MASKED>
 __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
     static_assert(CPW == 1 || CPW == 2 || CPW == 4, "slot layout");
     constexpr int NT = 64 * (NCW + 1 + kND);
@@ -419,7 +430,7 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
     const int wave = threadIdx.x / 64;
     const int lane = threadIdx.x % 64;
     const uint64_t stride = a.stride;
-    const uint32_t mask = a.mask ? LX_SEQ_MASK : 0xFFFFFFFFu;
+    constexpr uint32_t mask = MASKED ? LX_SEQ_MASK : 0xFFFFFFFFu;
     const uint32_t RA = lds_addr(ring);
     const uint32_t RB = RA + (uint32_t)(RN * 16);   // second units (CPW 4 only)
 
@@ -599,8 +610,10 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
     }
 
     // ---------------------------------------------------------------- compute
+#ifdef LX_WALKER_PROF
     uint32_t c_pass = 0, c_chunk = 0, c_done = 0, c_slow = 0, c_wm = 0, c_norec = 0;
     const unsigned long long t_start = wall_clock64();
+#endif
 
     uint32_t lp = threadIdx.x;
     bool have = false;
@@ -612,10 +625,10 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
     uint32_t drained = 0;   // events < drained are known drained (slot reuse)
 
     while (lp < n) {
-        c_pass++;
+        LX_WP(c_pass++;)
         if (!have) {
             const uint32_t slot = lp % RR;
-            if (__hip_atomic_load(&rtag[slot / 64], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != lp / 64 + 1) { c_norec++; continue; }
+            if (__hip_atomic_load(&rtag[slot / 64], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != lp / 64 + 1) { LX_WP(c_norec++;) continue; }
             const uint4 q0 = rrec[rec_off(slot, 0)];
             br = q0.x; seq = q0.y; np = q0.z;
 #pragma unroll
@@ -632,7 +645,7 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
         }
         if (todo) {
             // fold chunk cc (parents 4cc..4cc+3)
-            c_chunk++;
+            LX_WP(c_chunk++;)
             uint32_t p4[4], sl4[4];
 #pragma unroll
             for (int j = 0; j < 4; j++) {
@@ -668,10 +681,10 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
                     if (!((oldm >> j) & 1u)) continue;
                     const uint32_t lpp = p4[j];
                     if (lpp < n && !round_done(sh.stored, lpp)) {
-                        c_wm++;
+                        LX_WP(c_wm++;)
                         __hip_atomic_store(&sh.req, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     } else {
-                        c_slow++;
+                        LX_WP(c_slow++;)
                         const uint32_t *row = a.hb + (uint64_t)(lpp + bs) * stride;
 #pragma unroll
                         for (int k = 0; k < CPW; k++)
@@ -720,7 +733,7 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
         {
             // complete: the slot's previous occupant (lp - RN) must be drained
             if (lp >= (uint32_t)RN && lp - RN >= drained) {
-                if (!round_done(sh.copied, lp - RN)) { c_wm++; continue; }
+                if (!round_done(sh.copied, lp - RN)) { LX_WP(c_wm++;) continue; }
                 drained = ((lp - RN) | 63u) + 1;   // its whole round
             }
             const uint32_t e = bs + lp;
@@ -732,9 +745,10 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
             ring_publish<CPW>(RA, RB, lp % RN, lp + 1, r);
             lp += E;
             have = false;
-            c_done++;
+            LX_WP(c_done++;)
         }
     }
+#ifdef LX_WALKER_PROF
     if (a.prof) {
         unsigned long long *pw = a.prof + ((uint64_t)blockIdx.x * 8 + wave) * kProfSlots;
         const uint32_t cs[8] = {c_pass, 0u, c_chunk, c_done, c_slow, 0u, c_wm, c_norec};
@@ -743,6 +757,7 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
         atomicMax(pw + 8, (unsigned long long)c_pass);               // wave passes = max over lanes
         if (lane == 0) atomicMax(pw + 9, wall_clock64() - t_start);  // wall ticks (100 MHz)
     }
+#endif
 }
 
 template <int CPW, int NCW, int RR, bool SMALL>
@@ -751,8 +766,10 @@ static hipError_t launch_index_t(const IndexArgs &a0, hipStream_t s) {
     a.n_slices = (a.ncols + CPW - 1) / CPW;
     a.slices_per_xcd = (a.n_slices + 7) / 8;
     uint32_t grid = a.slices_per_xcd * 8;
-    if (a.diag_nofill) hipLaunchKernelGGL((k_index<CPW, NCW, RR, false, SMALL>), dim3(grid), dim3(64 * (NCW + 1 + kND)), 0, s, a);
-    else hipLaunchKernelGGL((k_index<CPW, NCW, RR, true, SMALL>), dim3(grid), dim3(64 * (NCW + 1 + kND)), 0, s, a);
+    const dim3 blk(64 * (NCW + 1 + kND));
+    if (a.diag_nofill) hipLaunchKernelGGL((k_index<CPW, NCW, RR, false, SMALL, true>), dim3(grid), blk, 0, s, a);
+    else if (a.mask) hipLaunchKernelGGL((k_index<CPW, NCW, RR, true, SMALL, true>), dim3(grid), blk, 0, s, a);
+    else hipLaunchKernelGGL((k_index<CPW, NCW, RR, true, SMALL, false>), dim3(grid), blk, 0, s, a);
     return hipGetLastError();
 }
 
