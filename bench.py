@@ -90,7 +90,13 @@ def cpu_baseline(dag, weights, n_events_max, fc_n, budget_s):
     t1 = time.perf_counter()
     o.forkless_cause_batch(qa, qb)
     t_fc = time.perf_counter() - t1
-    return done, t_add, fc_n, t_fc
+    # FC over all host cores given to this job (OpenMP)
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    qa2, qb2 = tools.fc_queries(dag.lamport[:done], fc_n * threads, seed=4)
+    t2 = time.perf_counter()
+    o.forkless_cause_batch_mt(qa2, qb2, threads)
+    t_mt = time.perf_counter() - t2
+    return done, t_add, fc_n, t_fc, (len(qa2), t_mt, threads)
 
 
 ABFT_CONFIG = ("c5", 1000, 50, 10, "zipf")   # BASELINE configs[4]: V, events/validator, parents, stakes
@@ -379,12 +385,14 @@ def main():
 
     if rank == 0 and not args.no_cpu:
         sample_max = N
-        done, t_add, nq, t_q = cpu_baseline(dag, weights, sample_max, 200_000, args.cpu_budget)
+        done, t_add, nq, t_q, (nq_mt, t_mt, thr) = cpu_baseline(dag, weights, sample_max, 200_000, args.cpu_budget)
         result["cpu_baseline"] = {
             "value": done / t_add, "unit": "events/s", "cores": 1, "kind": "port",
             "sample": "first %d events of the same DAG indexed by the C restatement (oracle/csrc/oracle.c, -O2, "
                       "DFS LowestAfter, byte rows) in %.1fs; FC: %d queries over them in %.2fs" % (done, t_add, nq, t_q),
             "fc_value": nq / t_q, "fc_unit": "queries/s",
+            "fc_value_mt": nq_mt / t_mt, "fc_threads": thr,
+            "fc_sample_mt": "%d queries over the same prefix, OpenMP over queries, in %.2fs" % (nq_mt, t_mt),
             "host": "%s, %d logical cpus" % (platform.processor() or platform.machine(), os.cpu_count()),
         }
     if rank == 0:

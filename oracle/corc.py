@@ -45,6 +45,7 @@ def lib():
             f.argtypes = [ctypes.c_void_p, ctypes.c_uint32, u8p, ctypes.c_uint32, u32p]
         L.orc_forkless_cause.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32]
         L.orc_forkless_cause_batch.argtypes = [ctypes.c_void_p, ctypes.c_uint64, u32p, u32p, u8p]
+        L.orc_forkless_cause_batch_mt.argtypes = [ctypes.c_void_p, ctypes.c_uint64, u32p, u32p, u8p, ctypes.c_int]
         # abft_oracle.c
         L.abo_create.restype = ctypes.c_void_p
         L.abo_create.argtypes = [ctypes.c_uint32, ctypes.c_uint32, u32p, ctypes.c_void_p]
@@ -134,6 +135,14 @@ class OracleIndex:
         b = np.ascontiguousarray(b, dtype=np.uint32)
         out = np.zeros(len(a), dtype=np.uint8)
         self.L.orc_forkless_cause_batch(self.h, len(a), _p(a, u32p), _p(b, u32p), _p(out, u8p))
+        return out
+
+    def forkless_cause_batch_mt(self, a, b, threads):
+        """The same over OpenMP threads (CPU baseline; results identical)."""
+        a = np.ascontiguousarray(a, dtype=np.uint32)
+        b = np.ascontiguousarray(b, dtype=np.uint32)
+        out = np.zeros(len(a), dtype=np.uint8)
+        self.L.orc_forkless_cause_batch_mt(self.h, len(a), _p(a, u32p), _p(b, u32p), _p(out, u8p), int(threads))
         return out
 
 

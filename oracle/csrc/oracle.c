@@ -407,32 +407,53 @@ int orc_get_merged_hb(void *h, uint32_t id, uint8_t *out, uint32_t cap, uint32_t
     return 0;
 }
 
-/* ForklessCause (forkless_cause.go:40-82); returns 0/1, -1 unknown event */
-int orc_forkless_cause(void *h, uint32_t a, uint32_t b) {
-    orc_t *o = h;
+/* ForklessCause (forkless_cause.go:40-82) with caller-provided WeightCounter
+ * scratch (V bytes); returns 0/1, -1 unknown event.  Read-only on the index
+ * once BranchesInfo is initialised. */
+static int fc_one(orc_t *o, uint32_t a, uint32_t b, uint8_t *counter) {
     if (a >= o->n_events || b >= o->n_events) return -1;
-    init_branches_info(o);
     row_t *ha = tbl_get(&o->hb, a);
     if (o->bi.n > o->V) {
         uint32_t s, m; hb_get(ha, get_branch(o, b), &s, &m);
         if (is_fork(s, m)) return 0;
     }
     row_t *lb = tbl_get(&o->la, b);
-    memset(o->counter, 0, o->V);
+    memset(counter, 0, o->V);
     uint32_t sum = 0;
     for (uint32_t br = 0; br < o->bi.n; br++) {
         uint32_t l = la_get(lb, br);
         uint32_t s, m; hb_get(ha, br, &s, &m);
         if (l <= s && l != 0 && !is_fork(s, m)) {
             uint32_t c = o->bi.creator[br];
-            if (!o->counter[c]) { o->counter[c] = 1; sum += o->weights[c]; }
+            if (!counter[c]) { counter[c] = 1; sum += o->weights[c]; }
         }
     }
     return sum >= o->quorum;
 }
 
+int orc_forkless_cause(void *h, uint32_t a, uint32_t b) {
+    orc_t *o = h;
+    init_branches_info(o);
+    return fc_one(o, a, b, o->counter);
+}
+
 void orc_forkless_cause_batch(void *h, uint64_t n, const uint32_t *a, const uint32_t *b, uint8_t *out) {
     for (uint64_t i = 0; i < n; i++) out[i] = (uint8_t)orc_forkless_cause(h, a[i], b[i]);
+}
+
+/* The same over `threads` OpenMP threads (the multi-core CPU baseline of
+ * SURVEY 8d; the reference's own index is single-threaded by contract). */
+void orc_forkless_cause_batch_mt(void *h, uint64_t n, const uint32_t *a, const uint32_t *b, uint8_t *out,
+                                 int threads) {
+    orc_t *o = h;
+    init_branches_info(o);
+#pragma omp parallel num_threads(threads)
+    {
+        uint8_t *counter = malloc(o->V ? o->V : 1);
+#pragma omp for schedule(static)
+        for (int64_t i = 0; i < (int64_t)n; i++) out[i] = (uint8_t)fc_one(o, a[i], b[i], counter);
+        free(counter);
+    }
 }
 
 /* bulk add of a CSR batch; returns index of first failing event or -1 */

@@ -135,3 +135,14 @@ def test_abft_c_matches_python(shape, seal):
     if not seal:
         for f in range(1, max(frames) + 1):
             assert [pos_of[x.id] for x in t.store.roots.get(f, [])] == list(c.frame_roots(f))
+
+
+def test_c_oracle_fc_multithreaded_equals_single():
+    """The OpenMP FC batch (bench cpu_baseline, all host cores) answers exactly
+    what the single-threaded restatement answers, forks included."""
+    from lachesis_hip import tools
+    d = tools.gen_dag(12, 40, 4, 3, 5, 7)
+    o = corc.OracleIndex([5, 4, 4, 3, 3, 2, 2, 2, 1, 1, 1, 1])
+    assert o.add_batch(d.creator, d.seq, d.poff, d.par) == -1
+    qa, qb = tools.fc_queries(d.lamport, 40_000, window=20, seed=9)
+    np.testing.assert_array_equal(o.forkless_cause_batch_mt(qa, qb, 4), o.forkless_cause_batch(qa, qb))
