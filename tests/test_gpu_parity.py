@@ -316,6 +316,37 @@ def test_config3_shape_skewed(lx):
     np.testing.assert_array_equal(ix.forkless_cause_batch(qa, qb), o.forkless_cause_batch(qa, qb))
 
 
+def test_full_size_config3_prefix_vs_oracle(lx):
+    """BASELINE configs[2] at full size (V=1000, Zipf stakes, 10M events, one
+    batch -- the bench workload) against the C oracle on the first 120k events:
+    HighestBefore rows of prefix events are final, so they must be identical;
+    a LowestAfter entry the oracle has already set can never change, so every
+    non-zero oracle entry must be identical; ForklessCause between prefix
+    events must be identical (an entry set after the prefix is larger than any
+    prefix seq of its branch, so it never counts)."""
+    V = 1000
+    w = [(1 << 20) // (i + 1) for i in range(V)]
+    d = lx.tools.gen_dag(V, 10_000, 10, seed=1)
+    N = len(d)
+    ix = lx.Index(event_capacity=N)
+    ix.reset(w)
+    ix.add_batch(d.creator, d.seq, d.poff, d.par)
+    P = 120_000
+    o = corc.OracleIndex(w)
+    assert o.add_batch(d.creator[:P], d.seq[:P], d.poff[:P + 1], d.par) == -1
+    rng = np.random.default_rng(3)
+    for x in rng.choice(P, 300, replace=False):
+        x = int(x)
+        assert ix.highest_before(x) == o.hb(x), x
+        want = np.frombuffer(o.la(x), dtype=np.uint32)
+        got = np.frombuffer(ix.lowest_after(x), dtype=np.uint32)
+        nz = np.nonzero(want)[0]
+        assert np.array_equal(got[nz], want[nz]), x
+    qa, qb = lx.tools.fc_queries(d.lamport[:P], 200_000, seed=5)
+    np.testing.assert_array_equal(ix.forkless_cause_batch(qa, qb), o.forkless_cause_batch_mt(qa, qb, 8))
+    ix.close()
+
+
 def test_full_size_properties_config2(lx):
     """BASELINE configs[1] at full size (V=100, 1M events): size-independent
     properties.  (i) HB of an event on branch j at seq s equals s on column j;
