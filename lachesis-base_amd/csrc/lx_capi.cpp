@@ -45,6 +45,7 @@ struct lx_index {
     uint64_t n_events = 0, n_flushed = 0, hwm = 0;
     uint32_t B = 0, B_flushed = 0;
     uint32_t max_seq = 0;
+    uint32_t pcols_used = 0;       // plane columns rows may hold non-zero values in (since the last zeroing)
     bool have_epoch = false;
 
     // host mirror of BranchesInfo (creator / first seq per branch; by creator)
@@ -505,6 +506,7 @@ int add_batch_dev(lx_index *h, uint32_t n, const uint32_t *creator, const uint32
         }
     }
     h->B = B_new;
+    h->pcols_used = std::max(h->pcols_used, h->sharded() ? h->nloc : h->B);
     if (nforks || h->ncols == 0)
         if ((rc = rebuild_columns(h))) return rc;
 
@@ -945,9 +947,12 @@ int lx_reset(lx_index *h, uint32_t nv, const uint32_t *w) {
         // HB: the walker rewrites the original columns of every new event's row
         // (the original branches always exist); only the fork-branch columns can
         // keep stale values for rows written before such a branch existed
+        // (only columns some row may have written: a previous epoch's originals
+        // or fork branches beyond this epoch's originals)
         const uint32_t no = h->sharded() ? norig : nv;
-        if (h->pstride > no)
-            HIPCHK(h, hipMemset2DAsync(h->hb + no, (size_t)h->pstride * 4, 0, (size_t)(h->pstride - no) * 4, h->hwm, h->stream));
+        const uint32_t used = std::min(h->pcols_used, h->pstride);
+        if (used > no)
+            HIPCHK(h, hipMemset2DAsync(h->hb + no, (size_t)h->pstride * 4, 0, (size_t)(used - no) * 4, h->hwm, h->stream));
         HIPCHK(h, hipMemsetAsync(h->la, 0, h->hwm * h->pstride * 4, h->stream));
         if (h->lap) HIPCHK(h, hipMemsetAsync(h->lap, 0, (uint64_t)h->pstride * h->s_cap * h->stride * 4, h->stream));
         HIPCHK(h, lx::launch_fill_u32(h->first_child, h->hwm, LX_NONE, h->stream));
@@ -975,6 +980,7 @@ int lx_reset(lx_index *h, uint32_t nv, const uint32_t *w) {
     HIPCHK(h, hipMemcpyAsync(h->branch_creator, idx.data(), nv * 4, hipMemcpyHostToDevice, h->stream));
     HIPCHK(h, hipMemcpyAsync(h->wpad, wp.data(), (uint64_t)h->stride * 4, hipMemcpyHostToDevice, h->stream));
     h->n_events = h->n_flushed = 0;
+    h->pcols_used = h->sharded() ? norig : nv;
     h->B = h->B_flushed = nv;
     h->max_seq = 0;
     h->h_branch_creator = idx;

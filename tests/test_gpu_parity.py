@@ -441,3 +441,29 @@ def test_reset_reuses_planes(lx):
         qa, qb = lx.tools.fc_queries(d.lamport, 50_000, window=32, seed=seed)
         np.testing.assert_array_equal(ix.forkless_cause_batch(qa, qb), o.forkless_cause_batch(qa, qb))
     ix.close()
+
+
+@pytest.mark.parametrize("shards", [1, 2])
+def test_reset_shrinking_validator_set(lx, shards):
+    """Epochs without forks followed by one with fewer validators: the previous
+    epoch's original columns beyond the new V become fork columns and must read
+    as empty (reset zeroes the columns rows may have written)."""
+    ixs = [lx.Index(shard_rank=r, shard_count=shards) for r in range(shards)]
+    for (n, ev, p, ch, fk, seed) in [(40, 60, 6, 0, 0, 41), (24, 80, 5, 0, 0, 42), (16, 90, 5, 4, 6, 43)]:
+        d = lx.tools.gen_dag(n, ev, p, ch, fk, seed)
+        w = list(range(70, 70 - n, -1))
+        o = oracle_for(d, w)
+        for ix in ixs:
+            ix.reset(w)
+            ix.add_batch(d.creator, d.seq, d.poff, d.par)
+        qa, qb = lx.tools.fc_queries(d.lamport, 40_000, window=32, seed=seed)
+        if shards == 1:
+            compare_rows(ixs[0], o, range(len(d)))
+            got = ixs[0].forkless_cause_batch(qa, qb)
+        else:
+            from test_gpu_shards import exchange, fc
+            exchange(ixs)
+            got = fc(lx, ixs, qa, qb)
+        np.testing.assert_array_equal(got, o.forkless_cause_batch(qa, qb))
+    for ix in ixs:
+        ix.close()
