@@ -73,11 +73,12 @@ def _skewed(n):
     (12, 30, 4, 3, 5, 2, "skewed"),
     (40, 12, 6, 8, 4, 3, "skewed"),
     (100, 8, 10, 10, 3, 4, "equal"),
+    (1000, 3, 10, 0, 0, 5, "zipf"),          # BASELINE configs[4] scale: V = 1000, Zipf stakes
 ])
 def test_quorum_indexer_matches_oracle(lx, shape):
     V, epn, P, cheaters, forks, seed, wk = shape
     nodes, events = tdag.rand_fork_dag(V, epn, P, cheaters, forks, seed=seed)
-    w = [1] * V if wk == "equal" else _skewed(V)
+    w = [1] * V if wk == "equal" else _skewed(V) if wk == "skewed" else [(1 << 20) // (i + 1) for i in range(V)]
     validators = pos.Validators(dict(zip(nodes, w)))
     o = corc.OracleIndex(validators.weights)
     cr, sq, off, par = tdag.to_dense(events, validators)
