@@ -9,6 +9,8 @@ vecfc/forkless_cause_test.go:
 * :class:`VecfcIndex` -- hash-keyed facade: ``reset(validators, get_event)``,
   ``add(e)``, ``flush()``, ``drop_not_flushed()``, ``forkless_cause(a, b)``,
   ``get_highest_before(id)`` ... (vecfc/index.go, vecfc/forkless_cause.go)
+* :mod:`batcher`      -- level-synchronous DAG batcher (include/lachesis_batcher.h):
+  parents-first buffering, bulk release in topological levels
 * :mod:`emitter`      -- emitter/ancestor.QuorumIndexer over include/lachesis_emitter.h
 * :mod:`abft`         -- abft.IndexedLachesis over include/lachesis_abft.h:
   frames, roots, election, blocks with batched ForklessCause on the GPU
@@ -22,3 +24,4 @@ from .vecfc import VecfcIndex, HighestBeforeSeq, LowestAfterSeq, BranchSeq  # no
 from . import tools  # noqa: F401
 from . import abft  # noqa: F401
 from . import emitter  # noqa: F401
+from . import batcher  # noqa: F401

@@ -71,6 +71,16 @@ SIGNATURES = [
     ("lx_qi_matrix", ctypes.c_int, [vp, u32p]),
     ("lx_qi_self_parent_seqs", ctypes.c_int, [vp, u32p]),
     ("lx_qi_metric_of", ctypes.c_int, [vp, ctypes.c_uint32, u32p, ctypes.c_uint32, u64p]),
+    # include/lachesis_batcher.h
+    ("lx_batcher_create", ctypes.c_int, [ctypes.POINTER(vp)]),
+    ("lx_batcher_destroy", None, [vp]),
+    ("lx_batcher_last_error", ctypes.c_char_p, [vp]),
+    ("lx_batcher_reset", ctypes.c_int, [vp]),
+    ("lx_batcher_push", ctypes.c_int, [vp, ctypes.c_uint32, u64p, u32p, u32p, u64p, u64p, u8p]),
+    ("lx_batcher_peek", ctypes.c_int, [vp, u32p, u64p, u32p, u32p]),
+    ("lx_batcher_pop", ctypes.c_int, [vp, u64p, u32p, u32p, u64p, u32p, u32p, u64p]),
+    ("lx_batcher_unpop", ctypes.c_int, [vp]),
+    ("lx_batcher_dense", ctypes.c_int, [vp, ctypes.c_uint64, u32p]),
 ]
 
 
