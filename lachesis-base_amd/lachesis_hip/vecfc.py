@@ -86,7 +86,7 @@ class VecfcIndex:
     # vecfc/index.go:98-105
     def reset(self, validators, get_event=None):
         self.validators = validators
-        self.get_event = get_event
+        self.get_event_fn = get_event
         self.ix.reset(validators.weights)
         self.pos = {}
         self.ids = []
@@ -214,6 +214,26 @@ class VecfcIndex:
 
     def at_least_one_fork(self):
         return self.ix.at_least_one_fork()
+
+    # vecengine/index.go:59-62 (InitBranchesInfo): the library keeps BranchesInfo live
+    def init_branches_info(self):
+        pass
+
+    def get_event(self, eid):
+        return self.get_event_fn(eid) if self.get_event_fn else None
+
+    # vecengine/traversal.go:13-37: iterative DFS over parents, `walk` decides
+    # whether to descend (host traversal through the get_event callback)
+    def dfs_subgraph(self, head, walk):
+        stack = list(head.parents)
+        while stack:
+            cur = stack.pop()
+            if not walk(cur):
+                continue
+            ev = self.get_event(cur)
+            if ev is None:
+                raise RuntimeError("event not found %r" % (cur,))
+            stack.extend(ev.parents)
 
     def branches_info(self):
         last_seq, creators = self.ix.branches_info()

@@ -467,3 +467,52 @@ def test_reset_shrinking_validator_set(lx, shards):
         np.testing.assert_array_equal(got, o.forkless_cause_batch(qa, qb))
     for ix in ixs:
         ix.close()
+
+
+@pytest.mark.parametrize("i", range(8))
+def test_random_forks_gpu(lx, i):
+    """TestRandomForks (vecfc/forkless_cause_test.go:578-747) through the HIP
+    index: every event's HighestBefore fork flags equal the naive
+    duplicate-(creator, seq) DFS over its subgraph (testForksDetected,
+    :491-518, walked with the facade's DfsSubgraph); DropNotFlushed erases the
+    unflushed vectors; ForklessCause is invariant under random topological
+    reorderings (:719-744)."""
+    from test_oracle_golden import RANDOM_FORKS, naive_forks_detected
+    t = RANDOM_FORKS[i]
+    rng = tdag.SplitMix64(1000 + i)
+    node_ids = [rng.next() & 0xFFFFFFFF for _ in range(t["nodes"])]
+    nodes, evs = tdag.rand_fork_dag(t["nodes"], t["events"], t["parents"], cheaters=t["cheaters"],
+                                    forks_count=t["forks"], seed=i, node_ids=node_ids)
+    validators = pos.Validators.equal(nodes, 1)
+    store = {e.id: e for e in evs}
+    ix = lx.VecfcIndex()
+    ix.reset(validators, store.get)
+    for e in evs:
+        ix.add(e)
+    for e in evs:
+        hb = ix.get_highest_before(e.id)
+        expected = naive_forks_detected(ix, e)
+        for v in nodes:
+            bs = hb.get(validators.idxs[v])
+            assert bs.is_fork_detected() == (v in expected), (e.id, v)
+            if v in expected:
+                assert bs.seq == 0
+    ids = [e.id for e in evs]
+
+    def fc_all():
+        qa = np.array([ix.pos[a] for a in ids for _ in ids], dtype=np.uint32)
+        qb = np.array([ix.pos[b] for _ in ids for b in ids], dtype=np.uint32)
+        return ix.ix.forkless_cause_batch(qa, qb)
+
+    fc = fc_all()
+    assert fc[:5].tolist() == [ix.forkless_cause(ids[0], b) for b in ids[:5]]
+    ix.drop_not_flushed()
+    for e in evs:
+        assert ix.get_highest_before(e.id) is None
+        assert ix.get_lowest_after(e.id) is None
+    order = evs
+    for _ in range(min(t["reorder"], 5)):
+        order = tdag.by_parents(tdag.shuffle(order, rng))
+        ix.add_events(order)
+        np.testing.assert_array_equal(fc_all(), fc)
+        ix.drop_not_flushed()
