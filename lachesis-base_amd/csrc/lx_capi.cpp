@@ -953,8 +953,10 @@ int lx_reset(lx_index *h, uint32_t nv, const uint32_t *w) {
         const uint32_t used = std::min(h->pcols_used, h->pstride);
         if (used > no)
             HIPCHK(h, hipMemset2DAsync(h->hb + no, (size_t)h->pstride * 4, 0, (size_t)(used - no) * 4, h->hwm, h->stream));
-        HIPCHK(h, hipMemsetAsync(h->la, 0, h->hwm * h->pstride * 4, h->stream));
+        // a shard's query plane is rewritten whole by the exchange (full blocks,
+        // zeros included) before any ForklessCause: only its fill target needs zeroing
         if (h->lap) HIPCHK(h, hipMemsetAsync(h->lap, 0, (uint64_t)h->pstride * h->s_cap * h->stride * 4, h->stream));
+        else HIPCHK(h, hipMemsetAsync(h->la, 0, h->hwm * h->pstride * 4, h->stream));
         HIPCHK(h, lx::launch_fill_u32(h->first_child, h->hwm, LX_NONE, h->stream));
         h->hwm = 0;
     }
