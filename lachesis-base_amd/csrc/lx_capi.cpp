@@ -97,6 +97,7 @@ struct lx_index {
     std::vector<uint32_t *> sc_rows;
     std::vector<uint32_t> sc_nrows;
     uint32_t *sc_flag = nullptr, *sc_pos = nullptr, *sc_cols = nullptr;
+    std::vector<uint32_t> sc_col_off;    // shard q's columns: sc_cols[sc_col_off[q] .. sc_col_off[q+1])
     uint64_t sc_cap = 0;
     void *sc_tmp = nullptr;
     size_t sc_tmp_bytes = 0;
@@ -661,7 +662,10 @@ std::vector<uint32_t> shard_cols(const lx_index *h, uint32_t q) {
     return cols;
 }
 
+int upload_cols(lx_index *h);
+
 // rows (events) whose branch belongs to each shard, at the current event count
+// (and every shard's column list)
 int ensure_shard_rows(lx_index *h) {
     if (h->sc_events == h->n_events && h->sc_B == h->B) return 0;
     const uint32_t n = (uint32_t)h->n_events;
@@ -692,16 +696,27 @@ int ensure_shard_rows(lx_index *h) {
         if (n) HIPCHK(h, hipMemcpyAsync(&h->sc_nrows[q], h->sc_pos + (n - 1), 4, hipMemcpyDeviceToHost, h->stream));
         HIPCHK(h, hipStreamSynchronize(h->stream));
     }
+    if (int rc = upload_cols(h)) return rc;
+    HIPCHK(h, hipStreamSynchronize(h->stream));
     h->sc_events = h->n_events;
     h->sc_B = h->B;
     return 0;
 }
 
-int upload_cols(lx_index *h, const std::vector<uint32_t> &cols) {
-    if (cols.empty()) return 0;
+// every shard's column list on the device (rebuilt with the shard rows, when
+// the event count or the branch set changed)
+int upload_cols(lx_index *h) {
+    std::vector<uint32_t> all;
+    h->sc_col_off.assign(1, 0);
+    for (uint32_t q = 0; q < h->shard_count; q++) {
+        std::vector<uint32_t> c = shard_cols(h, q);
+        all.insert(all.end(), c.begin(), c.end());
+        h->sc_col_off.push_back((uint32_t)all.size());
+    }
     if (h->sc_cols) (void)hipFree(h->sc_cols);
-    HIPCHK(h, dalloc(&h->sc_cols, cols.size()));
-    HIPCHK(h, hipMemcpyAsync(h->sc_cols, cols.data(), cols.size() * 4, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(h, dalloc(&h->sc_cols, all.size()));
+    if (!all.empty())
+        HIPCHK(h, hipMemcpyAsync(h->sc_cols, all.data(), all.size() * 4, hipMemcpyHostToDevice, h->stream));
     return 0;
 }
 
@@ -1313,7 +1328,7 @@ int lx_shard_block(lx_index *h, uint32_t src, uint32_t dst, uint64_t *elems) {
     HIPCHK(h, hipSetDevice(h->device));
     int rc;
     if ((rc = ensure_shard_rows(h))) return rc;
-    *elems = (uint64_t)h->sc_nrows[src] * shard_cols(h, dst).size();
+    *elems = (uint64_t)h->sc_nrows[src] * (h->sc_col_off[dst + 1] - h->sc_col_off[dst]);
     return 0;
 }
 
@@ -1324,8 +1339,7 @@ static int la_xfer(lx_index *h, uint32_t rows_of, uint32_t cols_of, uint32_t *bu
     HIPCHK(h, hipSetDevice(h->device));
     int rc;
     if ((rc = ensure_shard_rows(h))) return rc;
-    std::vector<uint32_t> cols = shard_cols(h, cols_of);
-    if ((rc = upload_cols(h, cols))) return rc;
+    const uint32_t c0 = h->sc_col_off[cols_of], c1 = h->sc_col_off[cols_of + 1];
     XferArgs x{};
     x.lap = h->lap;
     x.lap_stride = h->stride;
@@ -1338,8 +1352,8 @@ static int la_xfer(lx_index *h, uint32_t rows_of, uint32_t cols_of, uint32_t *bu
     x.branch_first = h->branch_first;
     x.rows = h->sc_rows[rows_of];
     x.nrows = h->sc_nrows[rows_of];
-    x.cols = h->sc_cols;
-    x.ncols = (uint32_t)cols.size();
+    x.cols = h->sc_cols + c0;
+    x.ncols = c1 - c0;
     x.buf = buf;
     x.mode = mode;
     HIPCHK(h, lx::launch_la_xfer(x, h->stream));
