@@ -52,12 +52,40 @@ constexpr uint32_t kSpecDepth = 4;      // self-children evaluated ahead per lau
 constexpr uint32_t kBuildCap = 100;     // calcFrameIdx: selfParentFrame + 100 in Build
 constexpr uint32_t kVoteWindow = 64;    // subjects voted on first (chooseAtropos walks idx order)
 
+// Device buffers recycled within one abft handle.  Every device operation of
+// the handle is enqueued on the index's stream, so a buffer handed back here
+// can be reused by later work on that stream without a host sync (frame
+// arrays and vote tables come and go with every decided frame: allocating
+// them with hipMalloc / hipFree cost ~6 ms per 50k-event epoch).
+struct BufPool {
+    std::multimap<uint64_t, void *> free;
+    void put(void *p, uint64_t bytes) {
+        if (p) free.emplace(bytes, p);
+    }
+    void *take(uint64_t bytes, uint64_t *got) {
+        auto it = free.lower_bound(bytes);
+        if (it == free.end() || it->first > 4 * bytes + 65536) return nullptr;
+        void *p = it->second;
+        *got = it->first;
+        free.erase(it);
+        return p;
+    }
+    void drain() {
+        for (auto &kv : free) (void)hipFree(kv.second);
+        free.clear();
+    }
+};
+
 template <typename T>
 struct DVec {
     T *p = nullptr;
     uint64_t cap = 0;
+    BufPool *pool = nullptr;
     void release() {
-        if (p) (void)hipFree(p);
+        if (p) {
+            if (pool) pool->put(p, cap * sizeof(T));
+            else (void)hipFree(p);
+        }
         p = nullptr;
         cap = 0;
     }
@@ -103,6 +131,7 @@ struct lx_abft {
     std::vector<uint64_t> par_off{0};
     std::vector<uint32_t> par;
 
+    BufPool pool;                       // recycled device buffers (all DVecs below)
     std::vector<Frame> frames;          // [0] unused
     DVec<uint32_t> arena;               // bit rows (observed roots) of k_root_fc launches
     uint64_t arena_used = 0;
@@ -158,13 +187,13 @@ template <typename T>
 int reserve(lx_abft *a, DVec<T> &v, uint64_t n, uint64_t keep, hipStream_t s) {
     if (n <= v.cap) return 0;
     uint64_t cap = std::max<uint64_t>({n, v.cap + v.cap / 2, 256});
-    T *p = nullptr;
-    AHIP(a, hipMalloc((void **)&p, cap * sizeof(T)));
+    uint64_t got = 0;
+    T *p = static_cast<T *>(a->pool.take(cap * sizeof(T), &got));
+    if (p) cap = got / sizeof(T);
+    else AHIP(a, hipMalloc((void **)&p, cap * sizeof(T)));
     if (v.p && keep) AHIP(a, hipMemcpyAsync(p, v.p, keep * sizeof(T), hipMemcpyDeviceToDevice, s));
-    if (v.p) {
-        AHIP(a, hipStreamSynchronize(s));
-        (void)hipFree(v.p);
-    }
+    v.pool = &a->pool;
+    v.release();          // stream-ordered reuse: no sync
     v.p = p;
     v.cap = cap;
     return 0;
@@ -782,6 +811,8 @@ void lx_abft_destroy(lx_abft *a) {
     a->d_kcol.release();
     a->d_kflag.release();
     a->d_kw.release();
+    (void)hipDeviceSynchronize();   // queued work may still use pooled buffers
+    a->pool.drain();
     delete a;
 }
 
