@@ -240,6 +240,8 @@ def main():
     else:
         ix = lx.Index(device=local, event_capacity=N)
 
+    st_x = []   # shard mode: LowestAfter all-to-all (pack + collective + unpack) per step, ms
+
     def index_step():
         ix.reset(weights)
         st_idx = 0.0
@@ -251,7 +253,9 @@ def main():
             st_idx += s["ms_index"]
             st_asg += s["ms_assign"] + s["ms_marks"]
         if shard:
+            tx = time.perf_counter()
             sx.exchange()
+            st_x.append((time.perf_counter() - tx) * 1e3)
         if solo:
             nonlocal d_blk
             sizes = [ix.shard_block(0, t) for t in range(1, solo)]
@@ -374,6 +378,10 @@ def main():
                            "algorithmic_bytes_per_launch": idx_bytes, "kernel_ms": kidx},
         "host_gen_s": t_gen,
     }
+    if shard or solo:
+        result["shard"] = {"columns": B, "wire_bytes_per_entry": ix.shard_wire_bytes(),
+                           "exchange_ms": float(np.mean(st_x[-args.steps:])) if st_x else None,
+                           "note": "index step = walk of own columns + LowestAfter all-to-all (timed inside value)"}
 
     if not args.no_abft:
         ab = abft_leg(lx, args.steps, args.warmup, local, args.cpu_budget, rank == 0 and not args.no_cpu)

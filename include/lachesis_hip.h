@@ -156,12 +156,16 @@ int lx_get_branches_info(lx_index *h, uint32_t *last_seq, uint32_t *creator_idx,
  * (columns of d) and d stores it with lx_la_unpack_dev(from s); lx_la_own_dev
  * moves a shard's own block (its rows x its columns).  After an Add or a
  * DropNotFlushed the exchange is repeated before the next ForklessCause.
- * lx_shard_block gives the element count (uint32) of a block.  The three
+ * lx_shard_block gives the entry count of a block and lx_shard_wire the bytes
+ * per entry in the pack/unpack buffers: 2 while every seq of the epoch is
+ * < 2^16 (entries are seqs or 0), else 4; all shards of an epoch agree on it,
+ * so a block occupies entries x wire bytes on both sides.  The three
  * transfer calls run on the handle's stream and return when done (their
  * `stream` argument is reserved; NULL).  The vector getters, write-back, abft
  * and the QuorumIndexer need an unsharded handle. */
 int lx_shard_range(const lx_index *h, uint32_t shard, uint32_t *creator_lo, uint32_t *creator_hi);
 int lx_shard_block(lx_index *h, uint32_t src_shard, uint32_t dst_shard, uint64_t *elems);
+int lx_shard_wire(lx_index *h, uint32_t *bytes_per_entry);
 int lx_la_pack_dev(lx_index *h, uint32_t dst_shard, uint32_t *out_dev, void *stream);
 int lx_la_unpack_dev(lx_index *h, uint32_t src_shard, const uint32_t *in_dev, void *stream);
 int lx_la_own_dev(lx_index *h, void *stream);

@@ -45,6 +45,7 @@ struct lx_index {
     uint64_t n_events = 0, n_flushed = 0, hwm = 0;
     uint32_t B = 0, B_flushed = 0;
     uint32_t max_seq = 0;
+    uint32_t wire_force = 0;               // LX_SHARD_WIRE=4: LowestAfter blocks always uint32
     uint32_t pcols_used = 0;       // plane columns rows may hold non-zero values in (since the last zeroing)
     bool have_epoch = false;
 
@@ -897,6 +898,7 @@ int lx_create(const lx_config *cfg, lx_index **out) {
     if (const char *d = getenv("LX_DIAG")) h->diag = (uint32_t)atoi(d);
     if (const char *d = getenv("LX_PROF")) h->prof = (d[0] == '1');
     if (const char *d = getenv("LX_SMALL")) h->small = (uint32_t)atoi(d);
+    if (const char *d = getenv("LX_SHARD_WIRE")) h->wire_force = (uint32_t)atoi(d);
     for (auto &e : h->ev)
         if (hipEventCreate(&e) != hipSuccess) {
             delete h;
@@ -1323,6 +1325,20 @@ int lx_shard_range(const lx_index *h, uint32_t shard, uint32_t *lo, uint32_t *hi
     return 0;
 }
 
+// Wire width of a LowestAfter block entry: LA entries are seqs or 0, so while
+// every seq of the epoch is < 2^16 they travel as uint16 (half the all-to-all
+// bytes).  max_seq follows the event stream, which every shard indexes whole,
+// so all shards agree on the width.  LX_SHARD_WIRE=4 forces uint32.
+static uint32_t shard_wire_bytes(const lx_index *h) {
+    return (h->wire_force != 4 && h->max_seq <= 0xFFFFu) ? 2u : 4u;
+}
+
+int lx_shard_wire(lx_index *h, uint32_t *bytes_per_entry) {
+    if (!h || !bytes_per_entry) return LX_ERR_ARG;
+    *bytes_per_entry = shard_wire_bytes(h);
+    return 0;
+}
+
 int lx_shard_block(lx_index *h, uint32_t src, uint32_t dst, uint64_t *elems) {
     if (!h || !elems || src >= h->shard_count || dst >= h->shard_count) return LX_ERR_ARG;
     HIPCHK(h, hipSetDevice(h->device));
@@ -1356,6 +1372,7 @@ static int la_xfer(lx_index *h, uint32_t rows_of, uint32_t cols_of, uint32_t *bu
     x.ncols = c1 - c0;
     x.buf = buf;
     x.mode = mode;
+    x.wire16 = shard_wire_bytes(h) == 2;
     HIPCHK(h, lx::launch_la_xfer(x, h->stream));
     HIPCHK(h, hipStreamSynchronize(h->stream));
     return 0;

@@ -181,6 +181,7 @@ struct XferArgs {
     uint32_t ncols;
     uint32_t *buf;
     int mode;
+    uint32_t wire16;             // buf entries are uint16 (every seq of the epoch < 2^16)
 };
 
 // ---- write-back to the reference's byte formats (lx_persist.hip)

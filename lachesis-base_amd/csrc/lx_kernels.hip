@@ -1051,7 +1051,8 @@ __global__ void k_compact(const uint32_t *flag, const uint32_t *pos, uint32_t n,
     if (flag[e]) rows[pos[e] - 1] = (uint32_t)e;
 }
 
-// buf[i][k] is LowestAfter entry cols[k] of event rows[i]:
+// buf[i][k] is LowestAfter entry cols[k] of event rows[i] (uint32, or uint16 on
+// the wire when every seq of the epoch fits: LA entries are seqs or 0):
 //   pack   : from the produced rows (lap) of this shard's branches
 //   unpack : into the query plane (la), own columns
 //   own    : lap -> la for this shard's rows x its own columns
@@ -1081,14 +1082,21 @@ __global__ __launch_bounds__(256) void k_la_xfer(XferArgs a) {
         __syncthreads();
         if (k >= a.ncols) continue;
         uint32_t v[kXR];
+        const uint16_t *in16 = reinterpret_cast<const uint16_t *>(a.buf);
+        uint16_t *out16 = reinterpret_cast<uint16_t *>(a.buf);
 #pragma unroll
         for (uint32_t r = 0; r < kXR; r++)
-            if (r < nr) v[r] = a.mode == 1 ? a.buf[s_src[r] + k] : a.lap[s_src[r] + j];
+            if (r < nr) v[r] = a.mode == 1 ? (a.wire16 ? (uint32_t)in16[s_src[r] + k] : a.buf[s_src[r] + k])
+                                           : a.lap[s_src[r] + j];
 #pragma unroll
         for (uint32_t r = 0; r < kXR; r++)
             if (r < nr) {
-                if (a.mode == 0) a.buf[s_dst[r] + k] = v[r];
-                else a.la[s_dst[r] + jl] = v[r];
+                if (a.mode == 0) {
+                    if (a.wire16) out16[s_dst[r] + k] = (uint16_t)v[r];
+                    else a.buf[s_dst[r] + k] = v[r];
+                } else {
+                    a.la[s_dst[r] + jl] = v[r];
+                }
             }
     }
 }

@@ -41,6 +41,7 @@ SIGNATURES = [
     ("lx_get_branches_info", ctypes.c_int, [vp, u32p, u32p, ctypes.c_uint32, u32p]),
     ("lx_shard_range", ctypes.c_int, [vp, ctypes.c_uint32, u32p, u32p]),
     ("lx_shard_block", ctypes.c_int, [vp, ctypes.c_uint32, ctypes.c_uint32, u64p]),
+    ("lx_shard_wire", ctypes.c_int, [vp, u32p]),
     ("lx_la_pack_dev", ctypes.c_int, [vp, ctypes.c_uint32, vp, vp]),
     ("lx_la_unpack_dev", ctypes.c_int, [vp, ctypes.c_uint32, vp, vp]),
     ("lx_la_own_dev", ctypes.c_int, [vp, vp]),
@@ -295,6 +296,12 @@ class Index:
         n = ctypes.c_uint64()
         self._chk(self.L.lx_shard_block(self.h, src, dst, ctypes.byref(n)))
         return n.value
+
+    def shard_wire_bytes(self):
+        """Bytes per LowestAfter entry in pack/unpack buffers (2 while every seq < 2^16, else 4)."""
+        b = ctypes.c_uint32()
+        self._chk(self.L.lx_shard_wire(self.h, ctypes.byref(b)))
+        return b.value
 
     def la_pack_dev(self, dst, out_ptr):
         self._chk(self.L.lx_la_pack_dev(self.h, dst, out_ptr, None))

@@ -39,6 +39,7 @@ class ShardedIndex:
         # gloo moves host tensors only: stage device buffers through the host
         # (a rehearsal mode for several ranks sharing one GPU; RCCL is the product)
         self.stage = dist.get_backend(group) == "gloo" and self.device.type == "cuda"
+        self._bufs = {}
 
     def all_to_all(self, recv, send, recv_n, send_n):
         if self.stage:
@@ -58,30 +59,45 @@ class ShardedIndex:
 
     # ------------------------------------------------------------------ LA
     def exchange(self):
-        """All-to-all of LowestAfter blocks; returns the element counts sent."""
+        """All-to-all of LowestAfter blocks; returns the entry counts sent.
+
+        Blocks travel as bytes: ``shard_wire_bytes()`` per entry (uint16 while
+        every seq of the epoch fits, which every rank decides identically)."""
         r, G = self.rank, self.world
+        wb = self.ix.shard_wire_bytes() if hasattr(self.ix, "shard_wire_bytes") else 4
         send_n = [self.ix.shard_block(r, t) if t != r else 0 for t in range(G)]
         recv_n = [self.ix.shard_block(s, r) if s != r else 0 for s in range(G)]
-        send = torch.empty(max(sum(send_n), 1), dtype=torch.int32, device=self.device)
-        recv = torch.empty(max(sum(recv_n), 1), dtype=torch.int32, device=self.device)
+        send_b = [wb * x for x in send_n]
+        recv_b = [wb * x for x in recv_n]
+        send = self._buf("send", sum(send_b))
+        recv = self._buf("recv", sum(recv_b))
         off = 0
         for t in range(G):
-            if send_n[t]:
-                self.ix.la_pack_dev(t, send.data_ptr() + 4 * off)
-            off += send_n[t]
+            if send_b[t]:
+                self.ix.la_pack_dev(t, send.data_ptr() + off)
+            off += send_b[t]
         self.ix.sync()   # packs run on the library stream; the collective on torch's
         if G > 1:
-            self.all_to_all(recv[:sum(recv_n)], send[:sum(send_n)], recv_n, send_n)
+            self.all_to_all(recv[:sum(recv_b)], send[:sum(send_b)], recv_b, send_b)
         if self.device.type == "cuda":
             torch.cuda.current_stream(self.device).synchronize()
         off = 0
         for s in range(G):
-            if recv_n[s]:
-                self.ix.la_unpack_dev(s, recv.data_ptr() + 4 * off)
-            off += recv_n[s]
+            if recv_b[s]:
+                self.ix.la_unpack_dev(s, recv.data_ptr() + off)
+            off += recv_b[s]
         self.ix.la_own_dev()     # own rows x own columns, no communication
         self.ix.sync()
         return send_n
+
+    def _buf(self, name, nbytes):
+        """Byte staging buffer for the exchange, kept between calls (grown on demand)."""
+        cur = self._bufs.get(name)
+        if cur is None or cur.numel() < max(nbytes, 1):
+            self._bufs[name] = None
+            cur = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=self.device)
+            self._bufs[name] = cur
+        return cur
 
     # ------------------------------------------------------------------ FC
     def forkless_cause_dev(self, a, b, out=None):

@@ -16,13 +16,15 @@ def exchange(shards):
     import torch
     dev = torch.device("cuda", 0)
     G = len(shards)
+    wb = shards[0].shard_wire_bytes()
+    assert all(ix.shard_wire_bytes() == wb for ix in shards)   # every shard picks the same width
     for s in range(G):
         for t in range(G):
             if s == t:
                 continue
             n = shards[s].shard_block(s, t)
             assert n == shards[t].shard_block(s, t)
-            buf = torch.zeros(max(n, 1), dtype=torch.int32, device=dev)
+            buf = torch.zeros(max(n * wb, 1), dtype=torch.uint8, device=dev)
             shards[s].la_pack_dev(t, buf.data_ptr())
             shards[t].la_unpack_dev(s, buf.data_ptr())
     for ix in shards:
@@ -77,6 +79,37 @@ def test_sharded_fc_matches_oracle(G, shape):
     ranges = [shards[0].shard_range(r) for r in range(G)]
     assert ranges[0][0] == 0 and ranges[-1][1] == n
     assert all(ranges[i][1] == ranges[i + 1][0] for i in range(G - 1))
+
+
+@pytest.mark.parametrize("force", [None, "4"])
+def test_sharded_wire_width(force, monkeypatch):
+    """LowestAfter blocks travel as uint16 while every seq < 2^16, else (or
+    with LX_SHARD_WIRE=4) as uint32; FC equals the oracle either way."""
+    import lachesis_hip as lx
+    if force:
+        monkeypatch.setenv("LX_SHARD_WIRE", force)
+    d = lx.tools.gen_dag(12, 30, 4, 3, 4, 9)
+    weights = [3, 3, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1]
+    o = corc.OracleIndex(weights)
+    assert o.add_batch(d.creator, d.seq, d.poff, d.par) == -1
+    qa, qb = lx.tools.fc_queries(d.lamport, 20_000, window=24, seed=9)
+    got, shards = sharded_fc(lx, d, weights, 3, qa, qb)
+    assert shards[0].shard_wire_bytes() == (4 if force else 2)
+    np.testing.assert_array_equal(got, o.forkless_cause_batch(qa, qb))
+
+
+def test_sharded_wire_long_branches():
+    """Seqs past 2^16 switch the wire to uint32 (bit-exact FC vs the oracle)."""
+    import lachesis_hip as lx
+    d = lx.tools.gen_dag(3, 66_000, 3, 0, 0, 4)
+    assert int(d.seq.max()) > 0xFFFF
+    weights = [1, 1, 1]
+    o = corc.OracleIndex(weights)
+    assert o.add_batch(d.creator, d.seq, d.poff, d.par) == -1
+    qa, qb = lx.tools.fc_queries(d.lamport, 50_000, window=8, seed=4)
+    got, shards = sharded_fc(lx, d, weights, 2, qa, qb)
+    assert shards[0].shard_wire_bytes() == 4
+    np.testing.assert_array_equal(got, o.forkless_cause_batch(qa, qb))
 
 
 def test_shard_planes_hold_own_columns():
