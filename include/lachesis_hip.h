@@ -163,12 +163,35 @@ int lx_get_branches_info(lx_index *h, uint32_t *last_seq, uint32_t *creator_idx,
  * transfer calls run on the handle's stream and return when done (their
  * `stream` argument is reserved; NULL).  The vector getters, write-back, abft
  * and the QuorumIndexer need an unsharded handle. */
+int lx_shard_of(const lx_index *h, uint32_t *shard_rank, uint32_t *shard_count);
 int lx_shard_range(const lx_index *h, uint32_t shard, uint32_t *creator_lo, uint32_t *creator_hi);
 int lx_shard_block(lx_index *h, uint32_t src_shard, uint32_t dst_shard, uint64_t *elems);
 int lx_shard_wire(lx_index *h, uint32_t *bytes_per_entry);
 int lx_la_pack_dev(lx_index *h, uint32_t dst_shard, uint32_t *out_dev, void *stream);
 int lx_la_unpack_dev(lx_index *h, uint32_t src_shard, const uint32_t *in_dev, void *stream);
 int lx_la_own_dev(lx_index *h, void *stream);
+
+/* Column shards over RCCL without a Python host (the Go caller): one
+ * communicator per shard handle, built from a unique id that rank 0 creates
+ * and the caller distributes (as ncclGetUniqueId / ncclCommInitRank).
+ * lx_shard_exchange = the LowestAfter all-to-all (pack, grouped
+ * ncclSend/ncclRecv of every block on the handle's stream, unpack, own block);
+ * lx_forkless_cause_sharded_dev = partial stake sums, an ncclAllReduce (sum,
+ * uint32: exact, the true total fits 32 bits) and the quorum test, all
+ * stream-ordered on the handle's stream.  Every rank must make the same calls
+ * in the same order (collectives).  RCCL is loaded on first use (dlopen of
+ * librccl.so.1, reusing a copy the process already holds); nranks must equal
+ * the handle's shard_count and rank its shard_rank; one GPU per rank (RCCL
+ * refuses two ranks on one device).  lx_shard_comm_last_error(NULL) tells why
+ * the calling thread's last lx_shard_comm_create failed. */
+typedef struct lx_shard_comm lx_shard_comm;
+int lx_shard_comm_unique_id(uint8_t id[128]);
+int lx_shard_comm_create(lx_index *h, const uint8_t id[128], uint32_t nranks, uint32_t rank, lx_shard_comm **out);
+void lx_shard_comm_destroy(lx_shard_comm *c);
+const char *lx_shard_comm_last_error(const lx_shard_comm *c);
+int lx_shard_exchange(lx_shard_comm *c);
+int lx_forkless_cause_sharded_dev(lx_shard_comm *c, uint64_t n, const uint32_t *a_dev, const uint32_t *b_dev,
+                                  uint8_t *out_dev);
 
 /* Timing of the last lx_add_batch* call, measured with HIP events on the
  * handle's stream (milliseconds): branch assignment + record packing,

@@ -1319,6 +1319,13 @@ int lx_get_branches_info(lx_index *h, uint32_t *last_seq, uint32_t *creator_idx,
     return 0;
 }
 
+int lx_shard_of(const lx_index *h, uint32_t *rank, uint32_t *count) {
+    if (!h) return LX_ERR_ARG;
+    if (rank) *rank = h->shard_rank;
+    if (count) *count = h->shard_count;
+    return 0;
+}
+
 int lx_shard_range(const lx_index *h, uint32_t shard, uint32_t *lo, uint32_t *hi) {
     if (!h || shard >= h->shard_count) return LX_ERR_ARG;
     shard_bounds(h, shard, lo, hi);

@@ -1,0 +1,271 @@
+// Column shards over RCCL for callers without a Python host (the Go shim).
+//
+// The multi-GPU protocol of DESIGN.md section 6, written against the public
+// shard ABI (lx_shard_block / lx_shard_wire / lx_la_pack_dev / lx_la_unpack_dev /
+// lx_la_own_dev / lx_forkless_cause_partial_dev / lx_fc_combine_dev), with the
+// two collectives issued directly on the index handle's HIP stream:
+//   * exchange: every (src -> dst) LowestAfter block in one ncclGroupStart /
+//     ncclGroupEnd of ncclSend/ncclRecv (an all-to-all with uneven blocks),
+//     bytes on the wire = entries x lx_shard_wire;
+//   * ForklessCause: partial stake sums -> ncclAllReduce(sum, uint32) ->
+//     quorum test, stream-ordered (no host round trip).
+// RCCL is resolved with dlopen/dlsym on first use so that loading the index
+// library never pulls RCCL in, and a process that already holds RCCL (e.g.
+// PyTorch's copy, same soname) reuses it.  The reference index is single-node
+// (vecfc/index.go); this is the scale-out of the same computation.
+
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "lachesis_hip.h"
+
+namespace {
+
+struct RcclApi {
+    ncclResult_t (*GetUniqueId)(ncclUniqueId *) = nullptr;
+    ncclResult_t (*CommInitRank)(ncclComm_t *, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*GroupStart)() = nullptr;
+    ncclResult_t (*GroupEnd)() = nullptr;
+    ncclResult_t (*Send)(const void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*Recv)(void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*AllReduce)(const void *, void *, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
+                              hipStream_t) = nullptr;
+    const char *(*ErrorString)(ncclResult_t) = nullptr;
+    std::string error;
+    bool ok = false;
+};
+
+RcclApi &rccl() {
+    static RcclApi api;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        void *lib = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!lib) lib = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!lib) {
+            api.error = std::string("cannot load RCCL: ") + dlerror();
+            return;
+        }
+        bool all = true;
+        auto get = [&](auto &fn, const char *name) {
+            fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(lib, name));
+            all &= fn != nullptr;
+        };
+        get(api.GetUniqueId, "ncclGetUniqueId");
+        get(api.CommInitRank, "ncclCommInitRank");
+        get(api.CommDestroy, "ncclCommDestroy");
+        get(api.GroupStart, "ncclGroupStart");
+        get(api.GroupEnd, "ncclGroupEnd");
+        get(api.Send, "ncclSend");
+        get(api.Recv, "ncclRecv");
+        get(api.AllReduce, "ncclAllReduce");
+        get(api.ErrorString, "ncclGetErrorString");
+        api.ok = all;
+        if (!all) api.error = "RCCL library lacks a required symbol";
+    });
+    return api;
+}
+
+thread_local std::string g_create_error;   // why the last lx_shard_comm_create failed (no handle to hold it)
+
+int create_fail(int code, const std::string &msg) {
+    g_create_error = msg;
+    return code;
+}
+
+}  // namespace
+
+struct lx_shard_comm {
+    lx_index *ix = nullptr;
+    ncclComm_t comm = nullptr;
+    hipStream_t stream = nullptr;
+    int device = 0;
+    uint32_t rank = 0, nranks = 1;
+    uint8_t *send = nullptr, *recv = nullptr;    // exchange staging (bytes), grown on demand
+    size_t send_cap = 0, recv_cap = 0;
+    uint32_t *part = nullptr;                    // FC partial sums, grown on demand
+    uint64_t part_cap = 0;
+    std::string err;
+
+    int fail(int code, const char *fmt, ...) {
+        char buf[512];
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(buf, sizeof buf, fmt, ap);
+        va_end(ap);
+        err = buf;
+        return code;
+    }
+    int hip(hipError_t e, const char *what) {
+        if (e == hipSuccess) return 0;
+        return fail(e == hipErrorOutOfMemory ? LX_ERR_NOMEM : LX_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
+    }
+    int nccl(ncclResult_t r, const char *what) {
+        if (r == ncclSuccess) return 0;
+        return fail(LX_ERR_HIP, "%s: %s", what, rccl().ErrorString(r));
+    }
+    int index(int rc, const char *what) {
+        if (rc == 0) return 0;
+        return fail(rc, "%s: %s", what, lx_last_error(ix));
+    }
+    int grow(uint8_t **p, size_t *cap, size_t need) {
+        if (need <= *cap) return 0;
+        if (*p) {
+            (void)hipStreamSynchronize(stream);
+            (void)hipFree(*p);
+            *p = nullptr;
+            *cap = 0;
+        }
+        if (int rc = hip(hipMalloc(reinterpret_cast<void **>(p), need), "hipMalloc")) return rc;
+        *cap = need;
+        return 0;
+    }
+};
+
+#define LXC(call)                       \
+    do {                                \
+        if (int rc_ = (call)) return rc_; \
+    } while (0)
+
+extern "C" {
+
+int lx_shard_comm_unique_id(uint8_t id[128]) {
+    if (!id) return LX_ERR_ARG;
+    RcclApi &api = rccl();
+    if (!api.ok) return LX_ERR_HIP;
+    ncclUniqueId u;
+    if (api.GetUniqueId(&u) != ncclSuccess) return LX_ERR_HIP;
+    static_assert(sizeof(u) == 128, "ncclUniqueId size");
+    memcpy(id, &u, sizeof u);
+    return 0;
+}
+
+int lx_shard_comm_create(lx_index *h, const uint8_t id[128], uint32_t nranks, uint32_t rank, lx_shard_comm **out) {
+    if (!h || !id || !out || rank >= nranks) return create_fail(LX_ERR_ARG, "bad argument");
+    *out = nullptr;
+    uint32_t srank = 0, scount = 1;
+    if (lx_shard_of(h, &srank, &scount)) return create_fail(LX_ERR_ARG, "bad index handle");
+    if (scount != nranks || srank != rank)
+        return create_fail(LX_ERR_ARG, "rank " + std::to_string(rank) + " of " + std::to_string(nranks) +
+                                           " does not match the handle's shard " + std::to_string(srank) + " of " +
+                                           std::to_string(scount));
+    RcclApi &api = rccl();
+    if (!api.ok) return create_fail(LX_ERR_HIP, api.error);
+    auto *c = new lx_shard_comm();
+    c->ix = h;
+    c->rank = rank;
+    c->nranks = nranks;
+    void *stream = nullptr;
+    std::string why;
+    int rc = lx_device_planes(h, nullptr, nullptr, nullptr, &stream);
+    c->stream = (hipStream_t)stream;
+    hipDevice_t dev = 0;
+    if (!rc && hipStreamGetDevice(c->stream, &dev) != hipSuccess) { rc = LX_ERR_HIP; why = "hipStreamGetDevice failed"; }
+    c->device = dev;
+    if (!rc && hipSetDevice(c->device) != hipSuccess) { rc = LX_ERR_HIP; why = "hipSetDevice failed"; }
+    ncclUniqueId u;
+    memcpy(&u, id, sizeof u);
+    if (!rc) {
+        const ncclResult_t r = api.CommInitRank(&c->comm, (int)nranks, u, (int)rank);
+        if (r != ncclSuccess) {
+            rc = LX_ERR_HIP;
+            why = std::string("ncclCommInitRank: ") + api.ErrorString(r);
+        }
+    }
+    if (rc) {
+        delete c;
+        return create_fail(rc, why);
+    }
+    *out = c;
+    return 0;
+}
+
+void lx_shard_comm_destroy(lx_shard_comm *c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->comm) rccl().CommDestroy(c->comm);
+    (void)hipFree(c->send);
+    (void)hipFree(c->recv);
+    (void)hipFree(c->part);
+    delete c;
+}
+
+const char *lx_shard_comm_last_error(const lx_shard_comm *c) {
+    return c ? c->err.c_str() : g_create_error.c_str();   // NULL: why the last create failed
+}
+
+int lx_shard_exchange(lx_shard_comm *c) {
+    if (!c) return LX_ERR_ARG;
+    RcclApi &api = rccl();
+    LXC(c->hip(hipSetDevice(c->device), "hipSetDevice"));
+    const uint32_t r = c->rank, G = c->nranks;
+    if (G == 1) return 0;   // an unsharded handle holds whole LowestAfter rows already
+    uint32_t wb = 4;
+    LXC(c->index(lx_shard_wire(c->ix, &wb), "lx_shard_wire"));
+    std::vector<size_t> sb(G, 0), rb(G, 0), so(G + 1, 0), ro(G + 1, 0);
+    for (uint32_t q = 0; q < G; q++) {
+        uint64_t n = 0;
+        if (q != r) {
+            LXC(c->index(lx_shard_block(c->ix, r, q, &n), "lx_shard_block"));
+            sb[q] = (size_t)n * wb;
+            LXC(c->index(lx_shard_block(c->ix, q, r, &n), "lx_shard_block"));
+            rb[q] = (size_t)n * wb;
+        }
+        so[q + 1] = so[q] + sb[q];
+        ro[q + 1] = ro[q] + rb[q];
+    }
+    LXC(c->grow(&c->send, &c->send_cap, std::max<size_t>(so[G], 1)));
+    LXC(c->grow(&c->recv, &c->recv_cap, std::max<size_t>(ro[G], 1)));
+    for (uint32_t q = 0; q < G; q++)
+        if (sb[q])
+            LXC(c->index(lx_la_pack_dev(c->ix, q, reinterpret_cast<uint32_t *>(c->send + so[q]), nullptr),
+                         "lx_la_pack_dev"));
+    if (G > 1) {
+        LXC(c->nccl(api.GroupStart(), "ncclGroupStart"));
+        for (uint32_t q = 0; q < G; q++) {
+            if (q == r) continue;
+            // blocks may be empty (a shard without rows yet): zero-byte send/recv keep the pairing
+            LXC(c->nccl(api.Send(c->send + so[q], sb[q], ncclUint8, (int)q, c->comm, c->stream), "ncclSend"));
+            LXC(c->nccl(api.Recv(c->recv + ro[q], rb[q], ncclUint8, (int)q, c->comm, c->stream), "ncclRecv"));
+        }
+        LXC(c->nccl(api.GroupEnd(), "ncclGroupEnd"));
+    }
+    // the unpacks below run on the same stream, after the received bytes landed
+    for (uint32_t q = 0; q < G; q++)
+        if (rb[q])
+            LXC(c->index(lx_la_unpack_dev(c->ix, q, reinterpret_cast<const uint32_t *>(c->recv + ro[q]), nullptr),
+                         "lx_la_unpack_dev"));
+    LXC(c->index(lx_la_own_dev(c->ix, nullptr), "lx_la_own_dev"));
+    return c->hip(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
+}
+
+int lx_forkless_cause_sharded_dev(lx_shard_comm *c, uint64_t n, const uint32_t *a, const uint32_t *b, uint8_t *out) {
+    if (!c || (n && (!a || !b || !out))) return LX_ERR_ARG;
+    if (!n) return 0;
+    RcclApi &api = rccl();
+    LXC(c->hip(hipSetDevice(c->device), "hipSetDevice"));
+    if (c->nranks == 1)
+        return c->index(lx_forkless_cause_batch_dev(c->ix, n, a, b, out, nullptr), "lx_forkless_cause_batch_dev");
+    if (n > c->part_cap) {
+        uint8_t *p = reinterpret_cast<uint8_t *>(c->part);
+        size_t cap = c->part_cap * 4;
+        LXC(c->grow(&p, &cap, n * 4));
+        c->part = reinterpret_cast<uint32_t *>(p);
+        c->part_cap = n;
+    }
+    LXC(c->index(lx_forkless_cause_partial_dev(c->ix, n, a, b, c->part, nullptr), "lx_forkless_cause_partial_dev"));
+    LXC(c->nccl(api.AllReduce(c->part, c->part, n, ncclUint32, ncclSum, c->comm, c->stream), "ncclAllReduce"));
+    LXC(c->index(lx_fc_combine_dev(c->ix, n, c->part, out, nullptr), "lx_fc_combine_dev"));
+    return 0;
+}
+
+}  // extern "C"

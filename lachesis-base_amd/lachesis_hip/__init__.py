@@ -19,7 +19,7 @@ There is no CPU fallback: importing this package on a machine without the
 built library raises, and every compute call goes to the GPU.
 """
 
-from .capi import Index, LxError, load_library  # noqa: F401
+from .capi import Index, LxError, ShardComm, load_library, shard_comm_unique_id  # noqa: F401
 from .vecfc import VecfcIndex, HighestBeforeSeq, LowestAfterSeq, BranchSeq  # noqa: F401
 from . import tools  # noqa: F401
 from . import abft  # noqa: F401

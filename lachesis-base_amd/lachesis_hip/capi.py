@@ -39,6 +39,7 @@ SIGNATURES = [
     ("lx_get_merged_highest_before", ctypes.c_int, [vp, ctypes.c_uint32, u8p, ctypes.c_uint32, u32p]),
     ("lx_get_event_branch_id", ctypes.c_int, [vp, ctypes.c_uint32, u32p]),
     ("lx_get_branches_info", ctypes.c_int, [vp, u32p, u32p, ctypes.c_uint32, u32p]),
+    ("lx_shard_of", ctypes.c_int, [vp, u32p, u32p]),
     ("lx_shard_range", ctypes.c_int, [vp, ctypes.c_uint32, u32p, u32p]),
     ("lx_shard_block", ctypes.c_int, [vp, ctypes.c_uint32, ctypes.c_uint32, u64p]),
     ("lx_shard_wire", ctypes.c_int, [vp, u32p]),
@@ -48,6 +49,12 @@ SIGNATURES = [
     ("lx_last_stats", ctypes.c_int, [vp, vp]),
     ("lx_device_planes", ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), u32p, ctypes.POINTER(vp)]),
     ("lx_sync", ctypes.c_int, [vp]),
+    ("lx_shard_comm_unique_id", ctypes.c_int, [u8p]),
+    ("lx_shard_comm_create", ctypes.c_int, [vp, u8p, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(vp)]),
+    ("lx_shard_comm_destroy", None, [vp]),
+    ("lx_shard_comm_last_error", ctypes.c_char_p, [vp]),
+    ("lx_shard_exchange", ctypes.c_int, [vp]),
+    ("lx_forkless_cause_sharded_dev", ctypes.c_int, [vp, ctypes.c_uint64, vp, vp, vp]),
     # include/lachesis_abft.h
     ("lx_abft_create", ctypes.c_int, [vp, ctypes.POINTER(vp)]),
     ("lx_abft_destroy", None, [vp]),
@@ -297,6 +304,11 @@ class Index:
         self._chk(self.L.lx_shard_block(self.h, src, dst, ctypes.byref(n)))
         return n.value
 
+    def shard_of(self):
+        r, c = ctypes.c_uint32(), ctypes.c_uint32()
+        self._chk(self.L.lx_shard_of(self.h, ctypes.byref(r), ctypes.byref(c)))
+        return r.value, c.value
+
     def shard_wire_bytes(self):
         """Bytes per LowestAfter entry in pack/unpack buffers (2 while every seq < 2^16, else 4)."""
         b = ctypes.c_uint32()
@@ -323,3 +335,49 @@ class Index:
         self._chk(self.L.lx_device_planes(self.h, ctypes.byref(hb), ctypes.byref(la), ctypes.byref(stride),
                                           ctypes.byref(st)))
         return hb.value, la.value, stride.value, st.value
+
+
+def shard_comm_unique_id():
+    """RCCL communicator id (128 bytes) for ShardComm; create on one rank, share with all."""
+    L = load_library()
+    buf = (ctypes.c_uint8 * 128)()
+    rc = L.lx_shard_comm_unique_id(buf)
+    if rc != 0:
+        raise LxError(rc, "ncclGetUniqueId failed (RCCL not loadable?)")
+    return bytes(buf)
+
+
+class ShardComm:
+    """lx_shard_comm: the column-shard collectives issued by the library itself
+    over RCCL on the index handle's stream (the path a Go caller binds;
+    lachesis_hip.shard.ShardedIndex does the same through torch.distributed)."""
+
+    def __init__(self, index, unique_id, nranks, rank):
+        self.L = index.L
+        self.ix = index
+        self.c = vp()
+        idb = (ctypes.c_uint8 * 128).from_buffer_copy(unique_id)
+        rc = self.L.lx_shard_comm_create(index.h, idb, nranks, rank, ctypes.byref(self.c))
+        if rc != 0:
+            raise LxError(rc, "lx_shard_comm_create: " + self.L.lx_shard_comm_last_error(None).decode())
+
+    def _chk(self, rc):
+        if rc != 0:
+            raise LxError(rc, self.L.lx_shard_comm_last_error(self.c).decode())
+
+    def exchange(self):
+        self._chk(self.L.lx_shard_exchange(self.c))
+
+    def forkless_cause_dev(self, n, a_ptr, b_ptr, out_ptr):
+        self._chk(self.L.lx_forkless_cause_sharded_dev(self.c, n, a_ptr, b_ptr, out_ptr))
+
+    def close(self):
+        if self.c:
+            self.L.lx_shard_comm_destroy(self.c)
+            self.c = vp()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
