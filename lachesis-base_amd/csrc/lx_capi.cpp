@@ -45,6 +45,10 @@ struct lx_index {
     uint64_t n_events = 0, n_flushed = 0, hwm = 0;
     uint32_t B = 0, B_flushed = 0;
     uint32_t max_seq = 0;
+    // LowestAfter tail zeroing (unsharded; TailArgs): per-(j, c) done-up-to seqs
+    bool la_tail = true;                   // LX_LA_MEMSET=1: zero the whole LA plane at reset instead
+    uint32_t *tail_zw = nullptr, *tail_lo = nullptr, *tail_cmin = nullptr;
+    uint32_t tail_cap = 0;
     uint32_t wire_force = 0;               // LX_SHARD_WIRE=4: LowestAfter blocks always uint32
     uint32_t pcols_used = 0;       // plane columns rows may hold non-zero values in (since the last zeroing)
     bool have_epoch = false;
@@ -168,6 +172,11 @@ void free_all(lx_index *h) {
                     h->q_a, h->q_b, h->q_out};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
+    void *tptrs[] = {h->tail_zw, h->tail_lo, h->tail_cmin};
+    for (void *p : tptrs)
+        if (p) (void)hipFree(p);
+    h->tail_zw = h->tail_lo = h->tail_cmin = nullptr;
+    h->tail_cap = 0;
     void *lptrs[] = {h->cheat_brl, h->cheat_crl, h->cmap, h->lap, h->wloc};
     for (void *p : lptrs)
         if (p) (void)hipFree(p);
@@ -243,6 +252,44 @@ int grow_events(lx_index *h, uint64_t need) {
         *p = n;
     }
     h->n_cap = cap;
+    return 0;
+}
+
+// LowestAfter tail state sized to the branch capacity; a new table starts at
+// zw = 0 (the next pass re-zeroes every unobserved tail: always correct)
+int ensure_tail(lx_index *h) {
+    if (h->tail_cap >= h->stride && h->tail_zw) return 0;
+    void *tptrs[] = {h->tail_zw, h->tail_lo, h->tail_cmin};
+    if (h->tail_zw) HIPCHK(h, hipStreamSynchronize(h->stream));
+    for (void *p : tptrs)
+        if (p) (void)hipFree(p);
+    h->tail_zw = h->tail_lo = h->tail_cmin = nullptr;
+    const uint64_t t = h->stride;
+    HIPCHK(h, dalloc(&h->tail_zw, t * t));
+    HIPCHK(h, dalloc(&h->tail_lo, t * t));
+    HIPCHK(h, dalloc(&h->tail_cmin, t));
+    HIPCHK(h, hipMemsetAsync(h->tail_zw, 0, t * t * 4, h->stream));
+    h->tail_cap = h->stride;
+    return 0;
+}
+
+int la_tail(lx_index *h, hipStream_t s) {
+    int rc;
+    if ((rc = ensure_tail(h))) return rc;
+    TailArgs t{};
+    t.la = h->la;
+    t.hb = h->hb;
+    t.stride = h->pstride;
+    t.brow = h->brow;
+    t.s_cap = h->s_cap;
+    t.branch_first = h->branch_first;
+    t.branch_len = h->branch_len;
+    t.B = h->B;
+    t.zw = h->tail_zw;
+    t.lo = h->tail_lo;
+    t.cmin = h->tail_cmin;
+    t.tcap = h->tail_cap;
+    HIPCHK(h, lx::launch_la_tail(t, s));
     return 0;
 }
 
@@ -591,6 +638,9 @@ int add_batch_dev(lx_index *h, uint32_t n, const uint32_t *creator, const uint32
         m.cheat_br = h->cheat_br;
         HIPCHK(h, lx::launch_marks(m, s));
     }
+    if (!h->sharded() && h->la_tail && !h->diag_nofill) {
+        if ((rc = la_tail(h, s))) return rc;
+    }
     HIPCHK(h, hipEventRecord(h->ev[3], s));
     h->n_events += n;
     h->hwm = std::max(h->hwm, h->n_events);
@@ -898,6 +948,7 @@ int lx_create(const lx_config *cfg, lx_index **out) {
     if (const char *d = getenv("LX_DIAG")) h->diag = (uint32_t)atoi(d);
     if (const char *d = getenv("LX_PROF")) h->prof = (d[0] == '1');
     if (const char *d = getenv("LX_SMALL")) h->small = (uint32_t)atoi(d);
+    if (const char *d = getenv("LX_LA_MEMSET")) h->la_tail = (d[0] != '1');
     if (const char *d = getenv("LX_SHARD_WIRE")) h->wire_force = (uint32_t)atoi(d);
     for (auto &e : h->ev)
         if (hipEventCreate(&e) != hipSuccess) {
@@ -972,8 +1023,17 @@ int lx_reset(lx_index *h, uint32_t nv, const uint32_t *w) {
             HIPCHK(h, hipMemset2DAsync(h->hb + no, (size_t)h->pstride * 4, 0, (size_t)(used - no) * 4, h->hwm, h->stream));
         // a shard's query plane is rewritten whole by the exchange (full blocks,
         // zeros included) before any ForklessCause: only its fill target needs zeroing
-        if (h->lap) HIPCHK(h, hipMemsetAsync(h->lap, 0, (uint64_t)h->pstride * h->s_cap * h->stride * 4, h->stream));
-        else HIPCHK(h, hipMemsetAsync(h->la, 0, h->hwm * h->pstride * 4, h->stream));
+        if (h->lap) {
+            HIPCHK(h, hipMemsetAsync(h->lap, 0, (uint64_t)h->pstride * h->s_cap * h->stride * 4, h->stream));
+        } else if (h->la_tail) {
+            // every entry (x, j < B) of a row is rewritten after its batch (fill or
+            // tail, la_tail): only fork-branch columns of old rows need zeroing
+            if (used > no)
+                HIPCHK(h, hipMemset2DAsync(h->la + no, (size_t)h->pstride * 4, 0, (size_t)(used - no) * 4, h->hwm, h->stream));
+            if (h->tail_zw) HIPCHK(h, hipMemsetAsync(h->tail_zw, 0, (uint64_t)h->tail_cap * h->tail_cap * 4, h->stream));
+        } else {
+            HIPCHK(h, hipMemsetAsync(h->la, 0, h->hwm * h->pstride * 4, h->stream));
+        }
         HIPCHK(h, lx::launch_fill_u32(h->first_child, h->hwm, LX_NONE, h->stream));
         h->hwm = 0;
     }
@@ -1063,6 +1123,9 @@ int lx_drop_not_flushed(lx_index *h) {
         HIPCHK(h, hipMemsetAsync(h->hb + h->n_flushed * h->pstride, 0, rows * h->pstride * 4, h->stream));
         HIPCHK(h, hipMemsetAsync(h->la + h->n_flushed * h->pstride, 0, rows * h->pstride * 4, h->stream));
     }
+    // re-added events may land on rows this epoch has not used yet (stale from an
+    // earlier epoch) with seqs the tail table already counts as done: start over
+    if (h->tail_zw) HIPCHK(h, hipMemsetAsync(h->tail_zw, 0, (uint64_t)h->tail_cap * h->tail_cap * 4, h->stream));
     HIPCHK(h, hipStreamSynchronize(h->stream));
     h->n_events = h->n_flushed;
     if (h->B != h->B_flushed) {

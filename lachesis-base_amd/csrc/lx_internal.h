@@ -184,6 +184,25 @@ struct XferArgs {
     uint32_t wire16;             // buf entries are uint16 (every seq of the epoch < 2^16)
 };
 
+// LowestAfter tail zeroing (unsharded planes; replaces the epoch-start memset of
+// the whole LA plane): after a batch, entry (x, j) of a row x = (c, s) that
+// branch j has not observed (s > RAW(last event of j)[c]) must read 0; the fill
+// wrote every observed entry.  zw[j][c] = seq up to which (c, .) x j is done.
+struct TailArgs {
+    uint32_t *la;
+    const uint32_t *hb;
+    uint64_t stride;             // plane stride (branches)
+    const uint32_t *brow;        // [branch][seq - first] -> event row
+    uint32_t s_cap;
+    const uint32_t *branch_first;
+    const uint32_t *branch_len;
+    uint32_t B;
+    uint32_t *zw;                // [j][c], tcap x tcap
+    uint32_t *lo;                // [j][c] scratch: first seq to zero
+    uint32_t *cmin;              // [c] min over j of lo
+    uint32_t tcap;
+};
+
 // ---- write-back to the reference's byte formats (lx_persist.hip)
 struct RowsArgs {
     const uint32_t *plane;       // hb or la
@@ -286,6 +305,7 @@ hipError_t launch_marks(const MarkArgs &a, hipStream_t s);
 hipError_t launch_fc(const FcArgs &a, uint32_t cols, bool forks, hipStream_t s);
 hipError_t launch_fc_combine(const uint32_t *sum, uint8_t *out, uint64_t n, uint32_t quorum, hipStream_t s);
 hipError_t launch_unfill(const UnfillArgs &a, hipStream_t s);
+hipError_t launch_la_tail(const TailArgs &a, hipStream_t s);
 hipError_t launch_fill_u32(uint32_t *p, uint64_t n, uint32_t v, hipStream_t s);
 hipError_t launch_shard_rows(const uint32_t *ev_branch, const uint32_t *branch_creator, uint32_t n, uint32_t lo,
                              uint32_t hi, uint32_t *flag, uint32_t *pos, void *scan_tmp, size_t scan_bytes,

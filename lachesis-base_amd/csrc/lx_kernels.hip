@@ -1032,6 +1032,71 @@ hipError_t launch_unfill(const UnfillArgs &a, hipStream_t s) {
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------- LowestAfter tail
+// The range fill writes LA[(c, s)][j] for every s <= RAW(last_j)[c] (the union
+// of (RAW(prev)[c], RAW(e)[c]] along branch j's chain), so instead of zeroing
+// the whole plane at epoch start only the unobserved tail (RAW(last_j)[c],
+// last(c)] of each (c, j) is zeroed after a batch; zw remembers how far, so a
+// later batch touches only new rows.  Typical tails are a few rows per (c, j)
+// (the last rounds), an idle validator j costs its column once.
+__global__ void k_tail_lo(TailArgs a) {
+    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= a.B) return;
+    const uint32_t lc = a.branch_len[c];
+    const uint32_t last = lc ? a.branch_first[c] + lc - 1 : 0;
+    const uint32_t f = lc ? a.branch_first[c] : 1u;
+    for (uint32_t j = blockIdx.y; j < a.B; j += gridDim.y) {
+        const uint32_t lj = a.branch_len[j];
+        uint32_t t = 0;   // RAW(last event of j)[c]; 0 if j has no event yet
+        if (lj) {
+            const uint32_t e = a.brow[(uint64_t)j * a.s_cap + (lj - 1)];
+            t = a.hb[(uint64_t)e * a.stride + c] & LX_SEQ_MASK;
+        }
+        const uint64_t o = (uint64_t)j * a.tcap + c;
+        const uint32_t z = a.zw[o];
+        const uint32_t lo = max(max(t, z) + 1u, f);
+        a.lo[o] = lo;
+        if (lc) a.zw[o] = max(z, last);
+        if (lc && lo <= last) atomicMin(&a.cmin[c], lo);
+    }
+}
+
+constexpr int kTailReg = 8;   // columns per thread cached in registers (B <= 2048)
+
+__global__ __launch_bounds__(256) void k_tail_zero(TailArgs a) {
+    const uint32_t c = blockIdx.x;
+    const uint32_t lc = a.branch_len[c];
+    const uint32_t s0 = a.cmin[c];
+    if (!lc || s0 == 0xFFFFFFFFu) return;
+    const uint32_t f = a.branch_first[c], last = f + lc - 1;
+    uint32_t lr[kTailReg];
+#pragma unroll
+    for (int k = 0; k < kTailReg; k++) {
+        const uint32_t j = threadIdx.x + 256u * k;
+        lr[k] = j < a.B ? a.lo[(uint64_t)j * a.tcap + c] : 0xFFFFFFFFu;
+    }
+    for (uint32_t s = s0; s <= last; s++) {
+        const uint64_t row = a.brow[(uint64_t)c * a.s_cap + (s - f)];
+        uint32_t *r = a.la + row * a.stride;
+#pragma unroll
+        for (int k = 0; k < kTailReg; k++) {
+            const uint32_t j = threadIdx.x + 256u * k;
+            if (s >= lr[k]) r[j] = 0u;
+        }
+        for (uint32_t j = threadIdx.x + 256u * kTailReg; j < a.B; j += 256u)
+            if (s >= a.lo[(uint64_t)j * a.tcap + c]) r[j] = 0u;
+    }
+}
+
+hipError_t launch_la_tail(const TailArgs &a, hipStream_t s) {
+    if (!a.B) return hipSuccess;
+    hipError_t e = hipMemsetAsync(a.cmin, 0xFF, (uint64_t)a.B * 4, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_tail_lo, dim3(nblk(a.B, 256), std::min<uint32_t>(a.B, 65535)), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_tail_zero, dim3(a.B), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
 // ---------------------------------------------------------------------------- column shards
 // Multi-GPU column sharding: rows whose branch belongs to
 // shard q carry complete LowestAfter rows only on q; shard r needs the columns

@@ -516,3 +516,60 @@ def test_random_forks_gpu(lx, i):
         ix.add_events(order)
         np.testing.assert_array_equal(fc_all(), fc)
         ix.drop_not_flushed()
+
+
+def _all_pairs_fc(ix, o, n):
+    a = np.repeat(np.arange(n, dtype=np.uint32), n)
+    b = np.tile(np.arange(n, dtype=np.uint32), n)
+    np.testing.assert_array_equal(ix.forkless_cause_batch(a, b), o.forkless_cause_batch(a, b))
+
+
+def test_la_tail_stale_rows(lx):
+    """The LowestAfter plane is not zeroed at reset: after each batch the
+    entries no branch has observed yet are zeroed (tail pass).  Epoch 1 dirties
+    every row; epoch 2 has idle validators (branches without events), arrives
+    in batches, is flushed, dropped and re-added with a longer stream that
+    reaches rows epoch 2 had not used yet -- rows, all-pairs FC equal the oracle
+    after every step."""
+    ix = lx.Index()
+    d1 = lx.tools.gen_dag(20, 60, 5, 0, 0, 51)
+    w1 = [3] * 20
+    ix.reset(w1)
+    ix.add_batch(d1.creator, d1.seq, d1.poff, d1.par)
+    _all_pairs_fc(ix, oracle_for(d1, w1), len(d1))
+
+    d2 = lx.tools.gen_dag(16, 40, 4, 3, 4, 52)      # creators 0..15 of 20: 16..19 idle
+    w2 = [5, 5, 4, 4, 4, 3, 3, 3, 3, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1, 1]
+    N = len(d2)
+    ix.reset(w2)
+    cuts = [0, 37, 150, 151, 300]
+    for lo, hi in zip(cuts, cuts[1:]):
+        ix.add_batch(d2.creator[lo:hi], d2.seq[lo:hi], d2.poff[lo:hi + 1], d2.par)
+        o = corc.OracleIndex(w2)
+        assert o.add_batch(d2.creator[:hi], d2.seq[:hi], d2.poff[:hi + 1], d2.par) == -1
+        compare_rows(ix, o, range(hi), check_merged=False)
+        _all_pairs_fc(ix, o, hi)
+    ix.flush()
+    ix.add_batch(d2.creator[300:420], d2.seq[300:420], d2.poff[300:421], d2.par)
+    ix.drop_not_flushed()
+    ix.add_batch(d2.creator[300:], d2.seq[300:], d2.poff[300:], d2.par)   # longer than the dropped part
+    o = oracle_for(d2, w2)
+    compare_rows(ix, o, range(N))
+    _all_pairs_fc(ix, o, N)
+    ix.close()
+
+
+def test_la_memset_mode_matches(lx, monkeypatch):
+    """LX_LA_MEMSET=1 (zero the whole LowestAfter plane at reset, no tail pass)
+    gives the same rows and FC as the default tail mode."""
+    monkeypatch.setenv("LX_LA_MEMSET", "1")
+    ix = lx.Index()
+    for (n, ev, p, ch, fk, seed) in [(20, 50, 5, 3, 4, 61), (12, 40, 4, 2, 3, 62)]:
+        d = lx.tools.gen_dag(n, ev, p, ch, fk, seed)
+        w = list(range(40, 40 - n, -1))
+        ix.reset(w)
+        ix.add_batch(d.creator, d.seq, d.poff, d.par)
+        o = oracle_for(d, w)
+        compare_rows(ix, o, range(len(d)))
+        _all_pairs_fc(ix, o, len(d))
+    ix.close()
