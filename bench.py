@@ -384,14 +384,14 @@ def main():
                            "note": "index step = walk of own columns + LowestAfter all-to-all (timed inside value)"}
 
     if not args.no_abft:
-        ab = abft_leg(lx, args.steps, args.warmup, local, args.cpu_budget, rank == 0 and not args.no_cpu)
+        ab = abft_leg(lx, args.steps, args.warmup, local, args.cpu_budget, rank == 0 and world == 1 and not args.no_cpu)
         barrier()
         ab["ms_per_step"] = max_over_ranks(ab["ms_per_step"])   # replicas: one epoch per rank
         ab["events_per_sec"] = ab["events"] * world / (ab["ms_per_step"] * 1e-3)
         ab["parallelism"] = "replica%d" % world
         result["abft"] = ab
 
-    if rank == 0 and not args.no_cpu:
+    if rank == 0 and world == 1 and not args.no_cpu:     # the CPU baseline is an N=1 figure
         sample_max = N
         done, t_add, nq, t_q, (nq_mt, t_mt, thr) = cpu_baseline(dag, weights, sample_max, 200_000, args.cpu_budget)
         result["cpu_baseline"] = {
