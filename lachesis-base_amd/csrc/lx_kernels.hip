@@ -381,6 +381,24 @@ __device__ __forceinline__ uint32_t lds_addr(const void *p) {
     return (uint32_t)(uintptr_t)p;
 }
 
+// The round tag and all four 16-B fields of a record in one LDS round trip:
+// DS instructions of a wave execute in order, so fields read after the tag
+// read are at least as new as the tag says (the loader stores the tag only
+// after its DMA landed); the caller discards them when the tag is not yet set.
+__device__ __forceinline__ void rec_read(uint32_t tag_addr, uint32_t rec_addr, uint32_t &tag, u4v q[4]) {
+    static_assert(LX_REC_Q == 4, "record = 4 fields of 16 B, 1 KB apart");
+    asm volatile(
+        "ds_read_b32 %0, %5\n\t"
+        "ds_read_b128 %1, %6\n\t"
+        "ds_read_b128 %2, %6 offset:1024\n\t"
+        "ds_read_b128 %3, %6 offset:2048\n\t"
+        "ds_read_b128 %4, %6 offset:3072\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(tag), "=&v"(q[0]), "=&v"(q[1]), "=&v"(q[2]), "=&v"(q[3])
+        : "v"(tag_addr), "v"(rec_addr)
+        : "memory");
+}
+
 // field q of the record in record-ring slot `slot` (round-blocked SoA)
 __device__ __forceinline__ uint32_t rec_off(uint32_t slot, uint32_t q) {
     return (slot & ~63u) * LX_REC_Q + q * 64u + (slot & 63u);
@@ -628,12 +646,14 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
         LX_WP(c_pass++;)
         if (!have) {
             const uint32_t slot = lp % RR;
-            if (__hip_atomic_load(&rtag[slot / 64], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != lp / 64 + 1) { LX_WP(c_norec++;) continue; }
-            const uint4 q0 = rrec[rec_off(slot, 0)];
-            br = q0.x; seq = q0.y; np = q0.z;
+            uint32_t tg;
+            u4v rq[LX_REC_Q];
+            rec_read(lds_addr(&rtag[slot / 64]), lds_addr(rrec) + rec_off(slot, 0) * 16u, tg, rq);
+            if (tg != lp / 64 + 1) { LX_WP(c_norec++;) continue; }
+            br = rq[0].x; seq = rq[0].y; np = rq[0].z;
 #pragma unroll
             for (int j = 0; j < LX_MAXP / 4; j++) {
-                const uint4 q = rrec[rec_off(slot, 1 + j)];
+                const u4v q = rq[1 + j];
                 par[4 * j] = q.x - bs; par[4 * j + 1] = q.y - bs; par[4 * j + 2] = q.z - bs; par[4 * j + 3] = q.w - bs;
             }
             todo = (np >= LX_MAXP) ? ((1u << LX_MAXP) - 1u) : ((1u << np) - 1u);
