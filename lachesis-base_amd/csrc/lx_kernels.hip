@@ -268,7 +268,7 @@ struct Ring {
     static constexpr int N = BYTES / (CPW == 1 ? 8 : CPW == 2 ? 16 : 32);
 };
 
-struct WalkShared {
+struct alignas(8) WalkShared {
     uint32_t copied[kND];    // rounds drained (ring and record data consumed) per drain wave
     uint32_t stored[kND];    // rounds whose global stores are complete per drain wave
     uint32_t req;            // a compute lane waits for `stored`: drains flush
@@ -288,6 +288,70 @@ struct Slot {
     uint32_t t0, t1;       // t1 = second unit's tag (CPW 4), else t0
     uint32_t v[CPW];
 };
+
+// read 4 slots (A = first-unit array, B = second-unit array) and the drains'
+// `copied` watermarks (W, 8 B; the completion check of the same pass uses them),
+// issue all, wait once
+template <int CPW>
+__device__ __forceinline__ void ring_read4w(uint32_t A, uint32_t B, const uint32_t s[4], Slot<CPW> o[4], uint32_t W,
+                                            u2v &wm) {
+    static_assert(kND == 2, "one 8-B read of both drains' watermarks");
+    if (CPW == 1) {
+        u2v x0, x1, x2, x3;
+        asm volatile(
+            "ds_read_b64 %0, %5\n\t"
+            "ds_read_b64 %1, %6\n\t"
+            "ds_read_b64 %2, %7\n\t"
+            "ds_read_b64 %3, %8\n\t"
+            "ds_read_b64 %4, %9\n\t"
+            "s_waitcnt lgkmcnt(0)"
+            : "=&v"(x0), "=&v"(x1), "=&v"(x2), "=&v"(x3), "=&v"(wm)
+            : "v"(A + s[0] * 8u), "v"(A + s[1] * 8u), "v"(A + s[2] * 8u), "v"(A + s[3] * 8u), "v"(W)
+            : "memory");
+        const u2v xs[4] = {x0, x1, x2, x3};
+#pragma unroll
+        for (int j = 0; j < 4; j++) { o[j].t0 = o[j].t1 = xs[j].x; o[j].v[0] = xs[j].y; }
+    } else if (CPW == 2) {
+        u4v x0, x1, x2, x3;
+        asm volatile(
+            "ds_read_b128 %0, %5\n\t"
+            "ds_read_b128 %1, %6\n\t"
+            "ds_read_b128 %2, %7\n\t"
+            "ds_read_b128 %3, %8\n\t"
+            "ds_read_b64 %4, %9\n\t"
+            "s_waitcnt lgkmcnt(0)"
+            : "=&v"(x0), "=&v"(x1), "=&v"(x2), "=&v"(x3), "=&v"(wm)
+            : "v"(A + s[0] * 16u), "v"(A + s[1] * 16u), "v"(A + s[2] * 16u), "v"(A + s[3] * 16u), "v"(W)
+            : "memory");
+        const u4v xs[4] = {x0, x1, x2, x3};
+#pragma unroll
+        for (int j = 0; j < 4; j++) { o[j].t0 = o[j].t1 = xs[j].x; o[j].v[0] = xs[j].y; o[j].v[1 % CPW] = xs[j].z; }
+    } else {
+        u4v x0, x1, x2, x3, y0, y1, y2, y3;
+        asm volatile(
+            "ds_read_b128 %0, %9\n\t"
+            "ds_read_b128 %4, %13\n\t"
+            "ds_read_b128 %1, %10\n\t"
+            "ds_read_b128 %5, %14\n\t"
+            "ds_read_b128 %2, %11\n\t"
+            "ds_read_b128 %6, %15\n\t"
+            "ds_read_b128 %3, %12\n\t"
+            "ds_read_b128 %7, %16\n\t"
+            "ds_read_b64 %8, %17\n\t"
+            "s_waitcnt lgkmcnt(0)"
+            : "=&v"(x0), "=&v"(x1), "=&v"(x2), "=&v"(x3), "=&v"(y0), "=&v"(y1), "=&v"(y2), "=&v"(y3), "=&v"(wm)
+            : "v"(A + s[0] * 16u), "v"(A + s[1] * 16u), "v"(A + s[2] * 16u), "v"(A + s[3] * 16u),
+              "v"(B + s[0] * 16u), "v"(B + s[1] * 16u), "v"(B + s[2] * 16u), "v"(B + s[3] * 16u), "v"(W)
+            : "memory");
+        const u4v xs[4] = {x0, x1, x2, x3};
+        const u4v ys[4] = {y0, y1, y2, y3};
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            o[j].t0 = xs[j].x; o[j].t1 = ys[j].x;
+            o[j].v[0] = xs[j].y; o[j].v[1 % CPW] = xs[j].z; o[j].v[2 % CPW] = xs[j].w; o[j].v[3 % CPW] = ys[j].y;
+        }
+    }
+}
 
 // read 4 slots (A = first-unit array, B = second-unit array), issue all, wait once
 template <int CPW>
@@ -641,6 +705,7 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
     uint32_t cc = 0;     // chunk folded next
     uint32_t r[CPW];
     uint32_t drained = 0;   // events < drained are known drained (slot reuse)
+    u2v cwm = {0u, 0u};     // drains' `copied` watermarks as of the last fold
 
     while (lp < n) {
         LX_WP(c_pass++;)
@@ -677,7 +742,7 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
             }
             const uint32_t tc = (todo >> (4 * cc)) & 15u;
             Slot<CPW> o[4];
-            ring_read4<CPW>(RA, RB, sl4, o);
+            ring_read4w<CPW>(RA, RB, sl4, o, lds_addr(&sh.copied[0]), cwm);
             // branch-free common case: fold the parents whose slot is valid
             uint32_t okm = 0, oldm = 0;
 #pragma unroll
@@ -753,7 +818,11 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
         {
             // complete: the slot's previous occupant (lp - RN) must be drained
             if (lp >= (uint32_t)RN && lp - RN >= drained) {
-                if (!round_done(sh.copied, lp - RN)) { LX_WP(c_wm++;) continue; }
+                // watermarks only grow: the copy read with this pass's fold (or an
+                // older one) answering "drained" is final; otherwise ask LDS now
+                const uint32_t rr = (lp - RN) / 64;
+                const uint32_t cw = (rr % kND) ? cwm.y : cwm.x;
+                if (cw <= rr / kND && !round_done(sh.copied, lp - RN)) { LX_WP(c_wm++;) continue; }
                 drained = ((lp - RN) | 63u) + 1;   // its whole round
             }
             const uint32_t e = bs + lp;
