@@ -379,7 +379,9 @@ def main():
         "host_gen_s": t_gen,
     }
     if shard or solo:
-        result["shard"] = {"columns": B, "wire_bytes_per_entry": ix.shard_wire_bytes(),
+        wire = sorted(set(w for w in sx.last_wire[0] if w)) if shard and getattr(sx, "last_wire", None) else \
+            [ix.shard_wire_bytes()]
+        result["shard"] = {"columns": B, "wire_bytes_per_entry": wire,
                            "exchange_ms": float(np.mean(st_x[-args.steps:])) if st_x else None,
                            "note": "index step = walk of own columns + LowestAfter all-to-all (timed inside value)"}
 

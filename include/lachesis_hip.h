@@ -170,6 +170,16 @@ int lx_shard_wire(lx_index *h, uint32_t *bytes_per_entry);
 int lx_la_pack_dev(lx_index *h, uint32_t dst_shard, uint32_t *out_dev, void *stream);
 int lx_la_unpack_dev(lx_index *h, uint32_t src_shard, const uint32_t *in_dev, void *stream);
 int lx_la_own_dev(lx_index *h, void *stream);
+/* Per-block byte wire: lx_shard_block_wire gives the narrowest width of this
+ * shard's outgoing block to dst -- 1 byte per entry when every entry is 0 or
+ * within 127 of its row event's own seq (stored as LA - seq + 128; typical: a
+ * branch observes an event a few seqs later), else lx_shard_wire's width
+ * (LX_SHARD_WIRE pins the latter).  The sender tells the receiver the width
+ * (e.g. a G-int all-to-all) and both sides move the block with the _wire_
+ * variants; the block occupies entries x width bytes. */
+int lx_shard_block_wire(lx_index *h, uint32_t dst_shard, uint32_t *bytes_per_entry);
+int lx_la_pack_wire_dev(lx_index *h, uint32_t dst_shard, void *out_dev, uint32_t bytes_per_entry);
+int lx_la_unpack_wire_dev(lx_index *h, uint32_t src_shard, const void *in_dev, uint32_t bytes_per_entry);
 
 /* Column shards over RCCL without a Python host (the Go caller): one
  * communicator per shard handle, built from a unique id that rank 0 creates

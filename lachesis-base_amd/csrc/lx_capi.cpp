@@ -1419,7 +1419,9 @@ int lx_shard_block(lx_index *h, uint32_t src, uint32_t dst, uint64_t *elems) {
 }
 
 // rows of shard `rows_of` x columns of shard `cols_of`, moved by `mode`
-static int la_xfer(lx_index *h, uint32_t rows_of, uint32_t cols_of, uint32_t *buf, int mode) {
+// (0 pack, 1 unpack, 2 own block, 3 byte-wire check into buf[0]); wire 0 = the
+// epoch's width (shard_wire_bytes)
+static int la_xfer(lx_index *h, uint32_t rows_of, uint32_t cols_of, uint32_t *buf, int mode, uint32_t wire = 0) {
     if (!h->sharded()) return h->fail(LX_ERR_STATE, "LowestAfter exchange needs a column-sharded handle");
     if (!h->have_epoch) return h->fail(LX_ERR_STATE, "exchange before lx_reset");
     HIPCHK(h, hipSetDevice(h->device));
@@ -1442,7 +1444,7 @@ static int la_xfer(lx_index *h, uint32_t rows_of, uint32_t cols_of, uint32_t *bu
     x.ncols = c1 - c0;
     x.buf = buf;
     x.mode = mode;
-    x.wire16 = shard_wire_bytes(h) == 2;
+    x.wire = wire ? wire : shard_wire_bytes(h);
     HIPCHK(h, lx::launch_la_xfer(x, h->stream));
     HIPCHK(h, hipStreamSynchronize(h->stream));
     return 0;
@@ -1458,6 +1460,43 @@ int lx_la_unpack_dev(lx_index *h, uint32_t src, const uint32_t *in, void *stream
     if (!h || src >= h->shard_count || src == h->shard_rank || !in) return LX_ERR_ARG;
     (void)stream;
     return la_xfer(h, src, h->shard_rank, const_cast<uint32_t *>(in), 1);
+}
+
+int lx_shard_block_wire(lx_index *h, uint32_t dst, uint32_t *bytes_per_entry) {
+    if (!h || !bytes_per_entry || dst >= h->shard_count || dst == h->shard_rank) return LX_ERR_ARG;
+    const uint32_t w = shard_wire_bytes(h);
+    *bytes_per_entry = w;
+    if (h->wire_force) return 0;               // LX_SHARD_WIRE pins the epoch width
+    int rc;
+    if (!h->sharded()) return h->fail(LX_ERR_STATE, "LowestAfter exchange needs a column-sharded handle");
+    if (!h->have_epoch) return h->fail(LX_ERR_STATE, "exchange before lx_reset");
+    if ((rc = ensure_shard_rows(h))) return rc;
+    uint32_t *flag = nullptr;
+    HIPCHK(h, hipSetDevice(h->device));
+    HIPCHK(h, hipMalloc(reinterpret_cast<void **>(&flag), 4));
+    uint32_t bad = 1;
+    hipError_t e = hipMemsetAsync(flag, 0, 4, h->stream);
+    if (e == hipSuccess && (rc = la_xfer(h, h->shard_rank, dst, flag, 3))) {
+        (void)hipFree(flag);
+        return rc;
+    }
+    if (e == hipSuccess) e = hipMemcpy(&bad, flag, 4, hipMemcpyDeviceToHost);
+    (void)hipFree(flag);
+    HIPCHK(h, e);
+    if (!bad) *bytes_per_entry = 1;
+    return 0;
+}
+
+int lx_la_pack_wire_dev(lx_index *h, uint32_t dst, void *out, uint32_t bytes_per_entry) {
+    if (!h || dst >= h->shard_count || dst == h->shard_rank || !out) return LX_ERR_ARG;
+    if (bytes_per_entry != 1 && bytes_per_entry != 2 && bytes_per_entry != 4) return LX_ERR_ARG;
+    return la_xfer(h, h->shard_rank, dst, static_cast<uint32_t *>(out), 0, bytes_per_entry);
+}
+
+int lx_la_unpack_wire_dev(lx_index *h, uint32_t src, const void *in, uint32_t bytes_per_entry) {
+    if (!h || src >= h->shard_count || src == h->shard_rank || !in) return LX_ERR_ARG;
+    if (bytes_per_entry != 1 && bytes_per_entry != 2 && bytes_per_entry != 4) return LX_ERR_ARG;
+    return la_xfer(h, src, h->shard_rank, static_cast<uint32_t *>(const_cast<void *>(in)), 1, bytes_per_entry);
 }
 
 int lx_la_own_dev(lx_index *h, void *stream) {

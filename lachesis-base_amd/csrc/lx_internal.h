@@ -181,7 +181,8 @@ struct XferArgs {
     uint32_t ncols;
     uint32_t *buf;
     int mode;
-    uint32_t wire16;             // buf entries are uint16 (every seq of the epoch < 2^16)
+    uint32_t wire;               // bytes per buf entry: 4, 2 (every seq < 2^16) or 1 (LA - seq(row) + 128,
+                                 // 0 = no entry; only when the whole block fits, see k_la_xfer mode 3)
 };
 
 // LowestAfter tail zeroing (unsharded planes; replaces the epoch-start memset of

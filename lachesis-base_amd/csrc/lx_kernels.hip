@@ -1214,12 +1214,21 @@ __global__ void k_compact(const uint32_t *flag, const uint32_t *pos, uint32_t n,
 // resolved once (event -> branch -> lap row, a chain of dependent loads) into
 // LDS, then every thread moves its column for all kXR rows with the loads
 // independent of each other -- the per-row lookups no longer serialise the copy.
+// byte wire: LA entries are 0 or seqs of a branch observing the row's event,
+// typically a few seqs above the row's own seq; a block travels as one byte
+// per entry when every entry of it fits (mode 3 checks), else 2 or 4 bytes
+__device__ __forceinline__ bool fits8(uint32_t v, uint32_t s) {
+    return v == 0u || (uint32_t)((int32_t)v - (int32_t)s + 127) < 255u;   // v - s in [-127, 127]
+}
+
 template <uint32_t kXR>
 __global__ __launch_bounds__(256) void k_la_xfer(XferArgs a) {
     __shared__ uint64_t s_src[kXR], s_dst[kXR];
+    __shared__ uint32_t s_seq[kXR];
     const uint32_t k = blockIdx.x * 256 + threadIdx.x;
     const uint32_t j = k < a.ncols ? a.cols[k] : 0u;
-    const uint32_t jl = (a.mode != 0 && k < a.ncols) ? a.cmap[j] : 0u;
+    const uint32_t jl = (a.mode == 1 || a.mode == 2) && k < a.ncols ? a.cmap[j] : 0u;
+    bool bad = false;
     for (uint32_t i0 = blockIdx.y * kXR; i0 < a.nrows; i0 += gridDim.y * kXR) {
         const uint32_t nr = min(kXR, a.nrows - i0);
         __syncthreads();
@@ -1232,27 +1241,48 @@ __global__ __launch_bounds__(256) void k_la_xfer(XferArgs a) {
                 s_src[threadIdx.x] = (uint64_t)i * a.ncols;
             }
             s_dst[threadIdx.x] = a.mode == 0 ? (uint64_t)i * a.ncols : (uint64_t)e * a.pstride;
+            s_seq[threadIdx.x] = a.ev_seq[e];
         }
         __syncthreads();
         if (k >= a.ncols) continue;
         uint32_t v[kXR];
         const uint16_t *in16 = reinterpret_cast<const uint16_t *>(a.buf);
-        uint16_t *out16 = reinterpret_cast<uint16_t *>(a.buf);
+        const uint8_t *in8 = reinterpret_cast<const uint8_t *>(a.buf);
 #pragma unroll
-        for (uint32_t r = 0; r < kXR; r++)
-            if (r < nr) v[r] = a.mode == 1 ? (a.wire16 ? (uint32_t)in16[s_src[r] + k] : a.buf[s_src[r] + k])
-                                           : a.lap[s_src[r] + j];
-#pragma unroll
-        for (uint32_t r = 0; r < kXR; r++)
-            if (r < nr) {
-                if (a.mode == 0) {
-                    if (a.wire16) out16[s_dst[r] + k] = (uint16_t)v[r];
-                    else a.buf[s_dst[r] + k] = v[r];
+        for (uint32_t r = 0; r < kXR; r++) {
+            if (r >= nr) continue;
+            if (a.mode == 1) {
+                const uint64_t o = s_src[r] + k;
+                if (a.wire == 1) {
+                    const uint32_t c = in8[o];
+                    v[r] = c ? c + s_seq[r] - 128u : 0u;
                 } else {
-                    a.la[s_dst[r] + jl] = v[r];
+                    v[r] = a.wire == 2 ? (uint32_t)in16[o] : a.buf[o];
                 }
+            } else {
+                v[r] = a.lap[s_src[r] + j];
             }
+        }
+        if (a.mode == 3) {
+#pragma unroll
+            for (uint32_t r = 0; r < kXR; r++)
+                if (r < nr) bad |= !fits8(v[r], s_seq[r]);
+            continue;
+        }
+#pragma unroll
+        for (uint32_t r = 0; r < kXR; r++) {
+            if (r >= nr) continue;
+            if (a.mode == 0) {
+                const uint64_t o = s_dst[r] + k;
+                if (a.wire == 1) reinterpret_cast<uint8_t *>(a.buf)[o] = v[r] ? (uint8_t)(v[r] - s_seq[r] + 128u) : 0u;
+                else if (a.wire == 2) reinterpret_cast<uint16_t *>(a.buf)[o] = (uint16_t)v[r];
+                else a.buf[o] = v[r];
+            } else {
+                a.la[s_dst[r] + jl] = v[r];
+            }
+        }
     }
+    if (a.mode == 3 && __any(bad) && (threadIdx.x % 64) == 0) atomicOr(a.buf, 1u);
 }
 
 template <uint32_t kXR>

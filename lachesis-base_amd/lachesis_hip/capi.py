@@ -46,6 +46,9 @@ SIGNATURES = [
     ("lx_la_pack_dev", ctypes.c_int, [vp, ctypes.c_uint32, vp, vp]),
     ("lx_la_unpack_dev", ctypes.c_int, [vp, ctypes.c_uint32, vp, vp]),
     ("lx_la_own_dev", ctypes.c_int, [vp, vp]),
+    ("lx_shard_block_wire", ctypes.c_int, [vp, ctypes.c_uint32, u32p]),
+    ("lx_la_pack_wire_dev", ctypes.c_int, [vp, ctypes.c_uint32, vp, ctypes.c_uint32]),
+    ("lx_la_unpack_wire_dev", ctypes.c_int, [vp, ctypes.c_uint32, vp, ctypes.c_uint32]),
     ("lx_last_stats", ctypes.c_int, [vp, vp]),
     ("lx_device_planes", ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), u32p, ctypes.POINTER(vp)]),
     ("lx_sync", ctypes.c_int, [vp]),
@@ -314,6 +317,18 @@ class Index:
         b = ctypes.c_uint32()
         self._chk(self.L.lx_shard_wire(self.h, ctypes.byref(b)))
         return b.value
+
+    def shard_block_wire(self, dst):
+        """Narrowest bytes per entry for this shard's outgoing block to ``dst`` (1, 2 or 4)."""
+        b = ctypes.c_uint32()
+        self._chk(self.L.lx_shard_block_wire(self.h, dst, ctypes.byref(b)))
+        return b.value
+
+    def la_pack_wire_dev(self, dst, out_ptr, width):
+        self._chk(self.L.lx_la_pack_wire_dev(self.h, dst, out_ptr, width))
+
+    def la_unpack_wire_dev(self, src, in_ptr, width):
+        self._chk(self.L.lx_la_unpack_wire_dev(self.h, src, in_ptr, width))
 
     def la_pack_dev(self, dst, out_ptr):
         self._chk(self.L.lx_la_pack_dev(self.h, dst, out_ptr, None))

@@ -61,20 +61,32 @@ class ShardedIndex:
     def exchange(self):
         """All-to-all of LowestAfter blocks; returns the entry counts sent.
 
-        Blocks travel as bytes: ``shard_wire_bytes()`` per entry (uint16 while
-        every seq of the epoch fits, which every rank decides identically)."""
+        Blocks travel as bytes.  With a library handle each block gets its
+        narrowest width (``shard_block_wire``: 1 byte per entry when every entry
+        is within 127 of its row's seq, else 2 while every seq < 2^16, else 4);
+        the widths go first in a G-int all-to-all so receivers know the sizes."""
         r, G = self.rank, self.world
-        wb = self.ix.shard_wire_bytes() if hasattr(self.ix, "shard_wire_bytes") else 4
         send_n = [self.ix.shard_block(r, t) if t != r else 0 for t in range(G)]
         recv_n = [self.ix.shard_block(s, r) if s != r else 0 for s in range(G)]
-        send_b = [wb * x for x in send_n]
-        recv_b = [wb * x for x in recv_n]
+        per_block = hasattr(self.ix, "shard_block_wire")
+        if per_block:
+            send_w = [self.ix.shard_block_wire(t) if t != r else 0 for t in range(G)]
+            recv_w = self._widths(send_w)
+        else:
+            wb = self.ix.shard_wire_bytes() if hasattr(self.ix, "shard_wire_bytes") else 4
+            send_w = [wb] * G
+            recv_w = [wb] * G
+        send_b = [w * x for w, x in zip(send_w, send_n)]
+        recv_b = [w * x for w, x in zip(recv_w, recv_n)]
         send = self._buf("send", sum(send_b))
         recv = self._buf("recv", sum(recv_b))
         off = 0
         for t in range(G):
             if send_b[t]:
-                self.ix.la_pack_dev(t, send.data_ptr() + off)
+                if per_block:
+                    self.ix.la_pack_wire_dev(t, send.data_ptr() + off, send_w[t])
+                else:
+                    self.ix.la_pack_dev(t, send.data_ptr() + off)
             off += send_b[t]
         self.ix.sync()   # packs run on the library stream; the collective on torch's
         if G > 1:
@@ -84,11 +96,26 @@ class ShardedIndex:
         off = 0
         for s in range(G):
             if recv_b[s]:
-                self.ix.la_unpack_dev(s, recv.data_ptr() + off)
+                if per_block:
+                    self.ix.la_unpack_wire_dev(s, recv.data_ptr() + off, recv_w[s])
+                else:
+                    self.ix.la_unpack_dev(s, recv.data_ptr() + off)
             off += recv_b[s]
         self.ix.la_own_dev()     # own rows x own columns, no communication
         self.ix.sync()
+        self.last_wire = (send_w, recv_w)
         return send_n
+
+    def _widths(self, send_w):
+        """Tell every rank the width of the block this rank sends it; returns recv widths."""
+        G = self.world
+        if G == 1:
+            return list(send_w)
+        dev = self.device if (self.device.type == "cuda" and not self.stage) else torch.device("cpu")
+        sw = torch.tensor(send_w, dtype=torch.int32, device=dev)
+        rw = torch.empty(G, dtype=torch.int32, device=dev)
+        dist.all_to_all_single(rw, sw, group=self.group)
+        return [int(x) for x in rw.tolist()]
 
     def _buf(self, name, nbytes):
         """Byte staging buffer for the exchange, kept between calls (grown on demand)."""

@@ -18,17 +18,24 @@ def exchange(shards):
     G = len(shards)
     wb = shards[0].shard_wire_bytes()
     assert all(ix.shard_wire_bytes() == wb for ix in shards)   # every shard picks the same width
+    widths = {}
     for s in range(G):
         for t in range(G):
             if s == t:
                 continue
             n = shards[s].shard_block(s, t)
             assert n == shards[t].shard_block(s, t)
-            buf = torch.zeros(max(n * wb, 1), dtype=torch.uint8, device=dev)
-            shards[s].la_pack_dev(t, buf.data_ptr())
-            shards[t].la_unpack_dev(s, buf.data_ptr())
+            w = shards[s].shard_block_wire(t)          # the sender picks, the receiver is told
+            assert w in (1, wb)
+            widths[(s, t)] = w
+            # torch fills on its own stream and the library runs on its own:
+            # no fill kernel may still be in flight when the pack writes
+            buf = torch.empty(max(n * w, 1), dtype=torch.uint8, device=dev)
+            shards[s].la_pack_wire_dev(t, buf.data_ptr(), w)
+            shards[t].la_unpack_wire_dev(s, buf.data_ptr(), w)
     for ix in shards:
         ix.la_own_dev()
+    return widths
 
 
 def fc(lx, shards, qa, qb):
@@ -39,13 +46,15 @@ def fc(lx, shards, qa, qb):
     b = torch.from_numpy(qb.view(np.int32)).to(dev)
     total = torch.zeros(len(qa), dtype=torch.int64, device=dev)
     for ix in shards:
-        part = torch.zeros(len(qa), dtype=torch.int32, device=dev)
+        part = torch.empty(len(qa), dtype=torch.int32, device=dev)
+        torch.cuda.synchronize(dev)      # inputs and `total` ready before the library stream runs
         ix.forkless_cause_partial_dev(len(qa), a.data_ptr(), b.data_ptr(), part.data_ptr())
         ix.sync()
         total += part.to(torch.int64) & 0xFFFFFFFF
     s32 = (total & 0xFFFFFFFF).to(torch.int64)
     s32 = torch.where(s32 >= 2 ** 31, s32 - 2 ** 32, s32).to(torch.int32)
-    out = torch.zeros(len(qa), dtype=torch.uint8, device=dev)
+    out = torch.empty(len(qa), dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize(dev)          # s32 is computed on torch's stream
     shards[0].fc_combine_dev(len(qa), s32.data_ptr(), out.data_ptr())
     shards[0].sync()
     return out.cpu().numpy()
@@ -58,7 +67,7 @@ def sharded_fc(lx, d, weights, G, qa, qb):
         ix.reset(weights)
         ix.add_batch(d.creator, d.seq, d.poff, d.par)
         shards.append(ix)
-    exchange(shards)
+    exchange.last = exchange(shards)
     return fc(lx, shards, qa, qb), shards
 
 
@@ -95,6 +104,8 @@ def test_sharded_wire_width(force, monkeypatch):
     qa, qb = lx.tools.fc_queries(d.lamport, 20_000, window=24, seed=9)
     got, shards = sharded_fc(lx, d, weights, 3, qa, qb)
     assert shards[0].shard_wire_bytes() == (4 if force else 2)
+    if force:
+        assert set(exchange.last.values()) == {4}
     np.testing.assert_array_equal(got, o.forkless_cause_batch(qa, qb))
 
 
@@ -110,6 +121,47 @@ def test_sharded_wire_long_branches():
     got, shards = sharded_fc(lx, d, weights, 2, qa, qb)
     assert shards[0].shard_wire_bytes() == 4
     np.testing.assert_array_equal(got, o.forkless_cause_batch(qa, qb))
+
+
+def test_sharded_byte_wire():
+    """Balanced DAG: every LowestAfter entry is within 127 of its row's seq, so
+    every block travels as one byte per entry; FC equals the oracle."""
+    import lachesis_hip as lx
+    d = lx.tools.gen_dag(16, 300, 5, 0, 0, 71)
+    w = [2] * 16
+    o = corc.OracleIndex(w)
+    assert o.add_batch(d.creator, d.seq, d.poff, d.par) == -1
+    qa, qb = lx.tools.fc_queries(d.lamport, 50_000, window=24, seed=71)
+    got, shards = sharded_fc(lx, d, w, 4, qa, qb)
+    assert set(exchange.last.values()) == {1}
+    np.testing.assert_array_equal(got, o.forkless_cause_batch(qa, qb))
+
+
+def test_sharded_byte_wire_fallback_on_skewed_progress():
+    """Validator 0 runs 300 events alone, then validators 1..7 join with their
+    first event on top of it, and 0's next event observes them: LowestAfter
+    entries lie far from their rows' seqs in both directions, so both blocks
+    fall back to the wider wire; all-pairs FC equals the oracle."""
+    import types
+    import lachesis_hip as lx
+    n0 = 300
+    creator = [0] * n0 + list(range(1, 8)) + [0]
+    seq = list(range(1, n0 + 1)) + [1] * 7 + [n0 + 1]
+    pars = [[]] + [[i - 1] for i in range(1, n0)] + [[n0 - 1]] * 7 + [[n0 - 1] + list(range(n0, n0 + 7))]
+    poff = np.cumsum([0] + [len(p) for p in pars]).astype(np.uint32)
+    d = types.SimpleNamespace(creator=np.array(creator, dtype=np.uint32), seq=np.array(seq, dtype=np.uint32),
+                              poff=poff, par=np.array([x for p in pars for x in p], dtype=np.uint32))
+    w = [1] * 8
+    o = corc.OracleIndex(w)
+    assert o.add_batch(d.creator, d.seq, d.poff, d.par) == -1
+    N = len(creator)
+    qa = np.repeat(np.arange(N, dtype=np.uint32), N)
+    qb = np.tile(np.arange(N, dtype=np.uint32), N)
+    got, shards = sharded_fc(lx, d, w, 2, qa, qb)
+    # (0 -> 1): LA(0, s)[j >= 4] = 1 for s up to 300; (1 -> 0): LA(k, 1)[0] = 301
+    assert exchange.last == {(0, 1): 2, (1, 0): 2}
+    np.testing.assert_array_equal(got, o.forkless_cause_batch(qa, qb))
+    assert got.sum() > 0
 
 
 def test_shard_planes_hold_own_columns():
