@@ -410,12 +410,34 @@ __device__ __forceinline__ void ring_read4(uint32_t A, uint32_t B, const uint32_
     }
 }
 
+// one slot (the drains' spin loop and the overflow path): a single access per
+// unit, so a spinning drain adds no redundant LDS traffic beside the compute waves
 template <int CPW>
 __device__ __forceinline__ void ring_read1(uint32_t A, uint32_t B, uint32_t s, Slot<CPW> &o) {
-    uint32_t ss[4] = {s, s, s, s};
-    Slot<CPW> t[4];
-    ring_read4<CPW>(A, B, ss, t);
-    o = t[0];
+    if (CPW == 1) {
+        u2v x;
+        asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=&v"(x) : "v"(A + s * 8u) : "memory");
+        o.t0 = o.t1 = x.x;
+        o.v[0] = x.y;
+    } else if (CPW == 2) {
+        u4v x;
+        asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=&v"(x) : "v"(A + s * 16u) : "memory");
+        o.t0 = o.t1 = x.x;
+        o.v[0] = x.y;
+        o.v[1 % CPW] = x.z;
+    } else {
+        u4v x, y;
+        asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %3\n\ts_waitcnt lgkmcnt(0)"
+                     : "=&v"(x), "=&v"(y)
+                     : "v"(A + s * 16u), "v"(B + s * 16u)
+                     : "memory");
+        o.t0 = x.x;
+        o.t1 = y.x;
+        o.v[0] = x.y;
+        o.v[1 % CPW] = x.z;
+        o.v[2 % CPW] = x.w;
+        o.v[3 % CPW] = y.y;
+    }
 }
 
 template <int CPW>
