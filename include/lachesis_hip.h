@@ -41,6 +41,7 @@ extern "C" {
 #define LX_ERR_STATE -4        /* inconsistent state (vecengine/index.go:107-126) */
 #define LX_ERR_HIP -5          /* HIP runtime / device error */
 #define LX_ERR_NOMEM -6        /* device memory exhausted */
+#define LX_ERR_WIRE -7         /* a LowestAfter block does not fit the 1-byte wire (pack it wider) */
 
 #define LX_NO_EVENT 0xFFFFFFFFu
 
@@ -176,7 +177,10 @@ int lx_la_own_dev(lx_index *h, void *stream);
  * branch observes an event a few seqs later), else lx_shard_wire's width
  * (LX_SHARD_WIRE pins the latter).  The sender tells the receiver the width
  * (e.g. a G-int all-to-all) and both sides move the block with the _wire_
- * variants; the block occupies entries x width bytes. */
+ * variants; the block occupies entries x width bytes.  Packing at width 1
+ * checks as it goes: LX_ERR_WIRE means some entry did not fit, and the caller
+ * packs the block again at lx_shard_wire's width (so a sender may skip
+ * lx_shard_block_wire and try the byte wire first). */
 int lx_shard_block_wire(lx_index *h, uint32_t dst_shard, uint32_t *bytes_per_entry);
 int lx_la_pack_wire_dev(lx_index *h, uint32_t dst_shard, void *out_dev, uint32_t bytes_per_entry);
 int lx_la_unpack_wire_dev(lx_index *h, uint32_t src_shard, const void *in_dev, uint32_t bytes_per_entry);

@@ -50,6 +50,7 @@ struct lx_index {
     uint32_t *tail_zw = nullptr, *tail_lo = nullptr, *tail_cmin = nullptr;
     uint32_t tail_cap = 0;
     uint32_t wire_force = 0;               // LX_SHARD_WIRE=4: LowestAfter blocks always uint32
+    uint32_t *wire_flag = nullptr;         // device flag of the byte-wire fit check (4 B)
     uint32_t pcols_used = 0;       // plane columns rows may hold non-zero values in (since the last zeroing)
     bool have_epoch = false;
 
@@ -172,10 +173,10 @@ void free_all(lx_index *h) {
                     h->q_a, h->q_b, h->q_out};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
-    void *tptrs[] = {h->tail_zw, h->tail_lo, h->tail_cmin};
+    void *tptrs[] = {h->tail_zw, h->tail_lo, h->tail_cmin, h->wire_flag};
     for (void *p : tptrs)
         if (p) (void)hipFree(p);
-    h->tail_zw = h->tail_lo = h->tail_cmin = nullptr;
+    h->tail_zw = h->tail_lo = h->tail_cmin = h->wire_flag = nullptr;
     h->tail_cap = 0;
     void *lptrs[] = {h->cheat_brl, h->cheat_crl, h->cmap, h->lap, h->wloc};
     for (void *p : lptrs)
@@ -1445,8 +1446,21 @@ static int la_xfer(lx_index *h, uint32_t rows_of, uint32_t cols_of, uint32_t *bu
     x.buf = buf;
     x.mode = mode;
     x.wire = wire ? wire : shard_wire_bytes(h);
+    const bool check = mode == 3 || (mode == 0 && x.wire == 1);
+    if (check) {
+        if (!h->wire_flag) HIPCHK(h, dalloc(&h->wire_flag, 1));
+        HIPCHK(h, hipMemsetAsync(h->wire_flag, 0, 4, h->stream));
+        x.flag = h->wire_flag;
+        if (mode == 3) x.buf = h->wire_flag;
+    }
     HIPCHK(h, lx::launch_la_xfer(x, h->stream));
     HIPCHK(h, hipStreamSynchronize(h->stream));
+    if (check) {
+        uint32_t bad = 0;
+        HIPCHK(h, hipMemcpy(&bad, h->wire_flag, 4, hipMemcpyDeviceToHost));
+        if (mode == 3) return bad ? 1 : 0;
+        if (bad) return h->fail(LX_ERR_WIRE, "LowestAfter block to shard %u does not fit the 1-byte wire", cols_of);
+    }
     return 0;
 }
 
@@ -1464,32 +1478,19 @@ int lx_la_unpack_dev(lx_index *h, uint32_t src, const uint32_t *in, void *stream
 
 int lx_shard_block_wire(lx_index *h, uint32_t dst, uint32_t *bytes_per_entry) {
     if (!h || !bytes_per_entry || dst >= h->shard_count || dst == h->shard_rank) return LX_ERR_ARG;
-    const uint32_t w = shard_wire_bytes(h);
-    *bytes_per_entry = w;
+    *bytes_per_entry = shard_wire_bytes(h);
     if (h->wire_force) return 0;               // LX_SHARD_WIRE pins the epoch width
-    int rc;
-    if (!h->sharded()) return h->fail(LX_ERR_STATE, "LowestAfter exchange needs a column-sharded handle");
-    if (!h->have_epoch) return h->fail(LX_ERR_STATE, "exchange before lx_reset");
-    if ((rc = ensure_shard_rows(h))) return rc;
-    uint32_t *flag = nullptr;
-    HIPCHK(h, hipSetDevice(h->device));
-    HIPCHK(h, hipMalloc(reinterpret_cast<void **>(&flag), 4));
-    uint32_t bad = 1;
-    hipError_t e = hipMemsetAsync(flag, 0, 4, h->stream);
-    if (e == hipSuccess && (rc = la_xfer(h, h->shard_rank, dst, flag, 3))) {
-        (void)hipFree(flag);
-        return rc;
-    }
-    if (e == hipSuccess) e = hipMemcpy(&bad, flag, 4, hipMemcpyDeviceToHost);
-    (void)hipFree(flag);
-    HIPCHK(h, e);
-    if (!bad) *bytes_per_entry = 1;
+    const int r = la_xfer(h, h->shard_rank, dst, nullptr, 3);
+    if (r < 0) return r;
+    if (r == 0) *bytes_per_entry = 1;
     return 0;
 }
 
 int lx_la_pack_wire_dev(lx_index *h, uint32_t dst, void *out, uint32_t bytes_per_entry) {
     if (!h || dst >= h->shard_count || dst == h->shard_rank || !out) return LX_ERR_ARG;
     if (bytes_per_entry != 1 && bytes_per_entry != 2 && bytes_per_entry != 4) return LX_ERR_ARG;
+    if (bytes_per_entry == 1 && h->wire_force)
+        return h->fail(LX_ERR_WIRE, "LX_SHARD_WIRE pins the wire to %u bytes", shard_wire_bytes(h));
     return la_xfer(h, h->shard_rank, dst, static_cast<uint32_t *>(out), 0, bytes_per_entry);
 }
 

@@ -181,6 +181,7 @@ struct XferArgs {
     uint32_t ncols;
     uint32_t *buf;
     int mode;
+    uint32_t *flag;              // set to 1 when a byte-wire pack meets an entry that does not fit
     uint32_t wire;               // bytes per buf entry: 4, 2 (every seq < 2^16) or 1 (LA - seq(row) + 128,
                                  // 0 = no entry; only when the whole block fits, see k_la_xfer mode 3)
 };

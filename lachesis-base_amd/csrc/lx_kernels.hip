@@ -1285,11 +1285,11 @@ __global__ __launch_bounds__(256) void k_la_xfer(XferArgs a) {
                 v[r] = a.lap[s_src[r] + j];
             }
         }
-        if (a.mode == 3) {
+        if (a.mode == 3 || (a.mode == 0 && a.wire == 1)) {
 #pragma unroll
             for (uint32_t r = 0; r < kXR; r++)
                 if (r < nr) bad |= !fits8(v[r], s_seq[r]);
-            continue;
+            if (a.mode == 3) continue;
         }
 #pragma unroll
         for (uint32_t r = 0; r < kXR; r++) {
@@ -1304,7 +1304,8 @@ __global__ __launch_bounds__(256) void k_la_xfer(XferArgs a) {
             }
         }
     }
-    if (a.mode == 3 && __any(bad) && (threadIdx.x % 64) == 0) atomicOr(a.buf, 1u);
+    // mode 3 checks into buf[0]; a byte-wire pack reports a misfit in flag[0]
+    if (__any(bad) && (threadIdx.x % 64) == 0) atomicOr(a.mode == 3 ? a.buf : a.flag, 1u);
 }
 
 template <uint32_t kXR>

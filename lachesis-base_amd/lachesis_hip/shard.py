@@ -27,6 +27,12 @@ exercised with gloo on CPU (tests/test_shard_protocol.py).
 import torch
 import torch.distributed as dist
 
+try:
+    from .capi import LxError
+except ImportError:          # the protocol tests load this module without the library
+    LxError = RuntimeError
+LX_ERR_WIRE = -7             # include/lachesis_hip.h
+
 
 class ShardedIndex:
     def __init__(self, index, group=None, device=None):
@@ -61,33 +67,38 @@ class ShardedIndex:
     def exchange(self):
         """All-to-all of LowestAfter blocks; returns the entry counts sent.
 
-        Blocks travel as bytes.  With a library handle each block gets its
-        narrowest width (``shard_block_wire``: 1 byte per entry when every entry
-        is within 127 of its row's seq, else 2 while every seq < 2^16, else 4);
-        the widths go first in a G-int all-to-all so receivers know the sizes."""
+        Blocks travel as bytes.  With a library handle each block is packed at
+        1 byte per entry when every entry is within 127 of its row's seq (the
+        pack checks as it goes and reports LX_ERR_WIRE otherwise), else at the
+        epoch width (2 while every seq < 2^16, else 4); a G-int all-to-all
+        tells the receivers the widths before the blocks move."""
         r, G = self.rank, self.world
         send_n = [self.ix.shard_block(r, t) if t != r else 0 for t in range(G)]
         recv_n = [self.ix.shard_block(s, r) if s != r else 0 for s in range(G)]
-        per_block = hasattr(self.ix, "shard_block_wire")
-        if per_block:
-            send_w = [self.ix.shard_block_wire(t) if t != r else 0 for t in range(G)]
-            recv_w = self._widths(send_w)
-        else:
-            wb = self.ix.shard_wire_bytes() if hasattr(self.ix, "shard_wire_bytes") else 4
-            send_w = [wb] * G
-            recv_w = [wb] * G
-        send_b = [w * x for w, x in zip(send_w, send_n)]
-        recv_b = [w * x for w, x in zip(recv_w, recv_n)]
-        send = self._buf("send", sum(send_b))
-        recv = self._buf("recv", sum(recv_b))
+        per_block = hasattr(self.ix, "la_pack_wire_dev")
+        wb = self.ix.shard_wire_bytes() if hasattr(self.ix, "shard_wire_bytes") else 4
+        send_w = [wb if t != r else 0 for t in range(G)]
+        send = self._buf("send", sum(wb * x for x in send_n))   # room for the widest case
         off = 0
         for t in range(G):
-            if send_b[t]:
-                if per_block:
-                    self.ix.la_pack_wire_dev(t, send.data_ptr() + off, send_w[t])
-                else:
-                    self.ix.la_pack_dev(t, send.data_ptr() + off)
-            off += send_b[t]
+            if not send_n[t]:
+                continue
+            if per_block:
+                # byte wire first; the pack itself reports a misfit (LX_ERR_WIRE)
+                try:
+                    self.ix.la_pack_wire_dev(t, send.data_ptr() + off, 1)
+                    send_w[t] = 1
+                except LxError as e:
+                    if e.code != LX_ERR_WIRE:
+                        raise
+                    self.ix.la_pack_wire_dev(t, send.data_ptr() + off, wb)
+            else:
+                self.ix.la_pack_dev(t, send.data_ptr() + off)
+            off += send_w[t] * send_n[t]
+        recv_w = self._widths(send_w) if per_block else [wb] * G
+        send_b = [w * x for w, x in zip(send_w, send_n)]
+        recv_b = [w * x for w, x in zip(recv_w, recv_n)]
+        recv = self._buf("recv", sum(recv_b))
         self.ix.sync()   # packs run on the library stream; the collective on torch's
         if G > 1:
             self.all_to_all(recv[:sum(recv_b)], send[:sum(send_b)], recv_b, send_b)

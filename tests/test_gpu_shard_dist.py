@@ -16,7 +16,20 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _worker(rank, world, port, q):
+def _skewed_dag():
+    """Validator 0 runs 300 events alone before 1..7 join on top of it: LowestAfter
+    entries far from their rows' seqs, so blocks fall back from the 1-byte wire."""
+    import types
+    n0 = 300
+    creator = [0] * n0 + list(range(1, 8)) + [0]
+    seq = list(range(1, n0 + 1)) + [1] * 7 + [n0 + 1]
+    pars = [[]] + [[i - 1] for i in range(1, n0)] + [[n0 - 1]] * 7 + [[n0 - 1] + list(range(n0, n0 + 7))]
+    poff = np.cumsum([0] + [len(p) for p in pars]).astype(np.uint32)
+    return types.SimpleNamespace(creator=np.array(creator, dtype=np.uint32), seq=np.array(seq, dtype=np.uint32),
+                                 poff=poff, par=np.array([x for p in pars for x in p], dtype=np.uint32))
+
+
+def _worker(rank, world, port, q, kind="tdag"):
     import sys
     sys.path[:0] = [ROOT, os.path.join(ROOT, "lachesis-base_amd")]
     import torch
@@ -27,16 +40,27 @@ def _worker(rank, world, port, q):
         import lachesis_hip as lx
         from lachesis_hip.shard import ShardedIndex
         from oracle import corc
-        d = lx.tools.gen_dag(28, 40, 6, 5, 6, 3)
-        rng = np.random.default_rng(3)
-        weights = sorted((int(x) for x in rng.integers(1, 40, 28)), reverse=True)
+        if kind == "skewed":
+            d = _skewed_dag()
+            weights = [1] * 8
+        else:
+            d = lx.tools.gen_dag(28, 40, 6, 5, 6, 3)
+            rng = np.random.default_rng(3)
+            weights = sorted((int(x) for x in rng.integers(1, 40, 28)), reverse=True)
         ix = lx.Index(device=0, shard_rank=rank, shard_count=world)
         ix.reset(weights)
         ix.add_batch(d.creator, d.seq, d.poff, d.par)
         dev = torch.device("cuda", 0)
         si = ShardedIndex(ix, device=dev)
         si.exchange()
-        qa, qb = lx.tools.fc_queries(d.lamport, 30_000, window=30, seed=5)
+        if kind == "skewed":
+            assert max(si.last_wire[0]) > 1 and max(si.last_wire[1]) > 1   # fell back from the byte wire
+            N = len(d.creator)
+            qa = np.repeat(np.arange(N, dtype=np.uint32), N)
+            qb = np.tile(np.arange(N, dtype=np.uint32), N)
+        else:
+            assert set(w for w in si.last_wire[0] if w) == {1}              # balanced DAG: byte wire
+            qa, qb = lx.tools.fc_queries(d.lamport, 30_000, window=30, seed=5)
         out = si.forkless_cause_dev(torch.from_numpy(qa.view(np.int32)).to(dev),
                                     torch.from_numpy(qb.view(np.int32)).to(dev)).cpu().numpy()
         o = corc.OracleIndex(weights)
@@ -54,12 +78,12 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_index_over_torch_distributed(world):
+@pytest.mark.parametrize("world,kind", [(2, "tdag"), (3, "tdag"), (2, "skewed")])
+def test_sharded_index_over_torch_distributed(world, kind):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, kind)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=150) for _ in range(world)]

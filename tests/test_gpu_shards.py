@@ -158,6 +158,11 @@ def test_sharded_byte_wire_fallback_on_skewed_progress():
     qa = np.repeat(np.arange(N, dtype=np.uint32), N)
     qb = np.tile(np.arange(N, dtype=np.uint32), N)
     got, shards = sharded_fc(lx, d, w, 2, qa, qb)
+    import torch
+    buf = torch.empty(shards[0].shard_block(0, 1), dtype=torch.uint8, device=torch.device("cuda", 0))
+    with pytest.raises(lx.LxError) as ei:
+        shards[0].la_pack_wire_dev(1, buf.data_ptr(), 1)   # the pack itself reports the misfit
+    assert ei.value.code == -7
     # (0 -> 1): LA(0, s)[j >= 4] = 1 for s up to 300; (1 -> 0): LA(k, 1)[0] = 301
     assert exchange.last == {(0, 1): 2, (1, 0): 2}
     np.testing.assert_array_equal(got, o.forkless_cause_batch(qa, qb))
