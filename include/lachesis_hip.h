@@ -188,8 +188,10 @@ int lx_la_unpack_wire_dev(lx_index *h, uint32_t src_shard, const void *in_dev, u
 /* Column shards over RCCL without a Python host (the Go caller): one
  * communicator per shard handle, built from a unique id that rank 0 creates
  * and the caller distributes (as ncclGetUniqueId / ncclCommInitRank).
- * lx_shard_exchange = the LowestAfter all-to-all (pack, grouped
- * ncclSend/ncclRecv of every block on the handle's stream, unpack, own block);
+ * lx_shard_exchange = the LowestAfter all-to-all (pack each block on the
+ * 1-byte wire when it fits, else at lx_shard_wire's width; the widths, then
+ * the blocks, as grouped ncclSend/ncclRecv on the handle's stream; unpack;
+ * own block);
  * lx_forkless_cause_sharded_dev = partial stake sums, an ncclAllReduce (sum,
  * uint32: exact, the true total fits 32 bits) and the quorum test, all
  * stream-ordered on the handle's stream.  Every rank must make the same calls

@@ -6,7 +6,8 @@
 // two collectives issued directly on the index handle's HIP stream:
 //   * exchange: every (src -> dst) LowestAfter block in one ncclGroupStart /
 //     ncclGroupEnd of ncclSend/ncclRecv (an all-to-all with uneven blocks),
-//     bytes on the wire = entries x lx_shard_wire;
+//     each block at 1 byte per entry when it fits, else lx_shard_wire's width,
+//     the widths announced first (one uint32 per peer);
 //   * ForklessCause: partial stake sums -> ncclAllReduce(sum, uint32) ->
 //     quorum test, stream-ordered (no host round trip).
 // RCCL is resolved with dlopen/dlsym on first use so that loading the index
@@ -211,39 +212,71 @@ int lx_shard_exchange(lx_shard_comm *c) {
     if (G == 1) return 0;   // an unsharded handle holds whole LowestAfter rows already
     uint32_t wb = 4;
     LXC(c->index(lx_shard_wire(c->ix, &wb), "lx_shard_wire"));
-    std::vector<size_t> sb(G, 0), rb(G, 0), so(G + 1, 0), ro(G + 1, 0);
+    // entry counts of every block, the send side laid out for the widest case
+    std::vector<uint64_t> sn(G, 0), rn(G, 0);
+    std::vector<size_t> so(G + 1, 0);
     for (uint32_t q = 0; q < G; q++) {
-        uint64_t n = 0;
         if (q != r) {
-            LXC(c->index(lx_shard_block(c->ix, r, q, &n), "lx_shard_block"));
-            sb[q] = (size_t)n * wb;
-            LXC(c->index(lx_shard_block(c->ix, q, r, &n), "lx_shard_block"));
-            rb[q] = (size_t)n * wb;
+            LXC(c->index(lx_shard_block(c->ix, r, q, &sn[q]), "lx_shard_block"));
+            LXC(c->index(lx_shard_block(c->ix, q, r, &rn[q]), "lx_shard_block"));
         }
-        so[q + 1] = so[q] + sb[q];
-        ro[q + 1] = ro[q] + rb[q];
+        so[q + 1] = so[q] + (size_t)sn[q] * wb;
     }
     LXC(c->grow(&c->send, &c->send_cap, std::max<size_t>(so[G], 1)));
-    LXC(c->grow(&c->recv, &c->recv_cap, std::max<size_t>(ro[G], 1)));
-    for (uint32_t q = 0; q < G; q++)
-        if (sb[q])
-            LXC(c->index(lx_la_pack_dev(c->ix, q, reinterpret_cast<uint32_t *>(c->send + so[q]), nullptr),
-                         "lx_la_pack_dev"));
-    if (G > 1) {
-        LXC(c->nccl(api.GroupStart(), "ncclGroupStart"));
-        for (uint32_t q = 0; q < G; q++) {
-            if (q == r) continue;
-            // blocks may be empty (a shard without rows yet): zero-byte send/recv keep the pairing
-            LXC(c->nccl(api.Send(c->send + so[q], sb[q], ncclUint8, (int)q, c->comm, c->stream), "ncclSend"));
-            LXC(c->nccl(api.Recv(c->recv + ro[q], rb[q], ncclUint8, (int)q, c->comm, c->stream), "ncclRecv"));
+    // pack each block at 1 byte per entry when it fits (the pack checks), else
+    // at the epoch width; blocks are laid out back to back at their own widths
+    std::vector<uint32_t> sw(G, 0), rw(G, 0);
+    std::vector<size_t> sb(G, 0), rb(G, 0), ro(G + 1, 0);
+    size_t off = 0;
+    for (uint32_t q = 0; q < G; q++) {
+        so[q] = off;
+        if (q == r || !sn[q]) continue;
+        int rc = lx_la_pack_wire_dev(c->ix, q, c->send + off, 1);
+        sw[q] = 1;
+        if (rc == LX_ERR_WIRE) {
+            rc = lx_la_pack_wire_dev(c->ix, q, c->send + off, wb);
+            sw[q] = wb;
         }
-        LXC(c->nccl(api.GroupEnd(), "ncclGroupEnd"));
+        LXC(c->index(rc, "lx_la_pack_wire_dev"));
+        sb[q] = (size_t)sn[q] * sw[q];
+        off += sb[q];
     }
+    // tell every peer the width of its block (one uint32 each way), then the blocks
+    uint8_t *wdev = nullptr;
+    size_t wcap = 0;
+    LXC(c->grow(&wdev, &wcap, 8ull * G));
+    LXC(c->hip(hipMemcpyAsync(wdev, sw.data(), 4ull * G, hipMemcpyHostToDevice, c->stream), "hipMemcpyAsync"));
+    int rc = c->nccl(api.GroupStart(), "ncclGroupStart");
+    for (uint32_t q = 0; q < G && !rc; q++) {
+        if (q == r) continue;
+        rc = c->nccl(api.Send(wdev + 4ull * q, 1, ncclUint32, (int)q, c->comm, c->stream), "ncclSend");
+        if (!rc) rc = c->nccl(api.Recv(wdev + 4ull * (G + q), 1, ncclUint32, (int)q, c->comm, c->stream), "ncclRecv");
+    }
+    if (!rc) rc = c->nccl(api.GroupEnd(), "ncclGroupEnd");
+    if (!rc) rc = c->hip(hipMemcpyAsync(rw.data(), wdev + 4ull * G, 4ull * G, hipMemcpyDeviceToHost, c->stream),
+                         "hipMemcpyAsync");
+    if (!rc) rc = c->hip(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
+    (void)hipFree(wdev);
+    if (rc) return rc;
+    for (uint32_t q = 0; q < G; q++) {
+        if (q != r && rn[q] && rw[q] != 1 && rw[q] != 2 && rw[q] != 4)
+            return c->fail(LX_ERR_STATE, "peer %u announced wire width %u", q, rw[q]);
+        rb[q] = q == r ? 0 : (size_t)rn[q] * rw[q];
+        ro[q + 1] = ro[q] + rb[q];
+    }
+    LXC(c->grow(&c->recv, &c->recv_cap, std::max<size_t>(ro[G], 1)));
+    LXC(c->nccl(api.GroupStart(), "ncclGroupStart"));
+    for (uint32_t q = 0; q < G; q++) {
+        if (q == r) continue;
+        // blocks may be empty (a shard without rows yet): zero-byte send/recv keep the pairing
+        LXC(c->nccl(api.Send(c->send + so[q], sb[q], ncclUint8, (int)q, c->comm, c->stream), "ncclSend"));
+        LXC(c->nccl(api.Recv(c->recv + ro[q], rb[q], ncclUint8, (int)q, c->comm, c->stream), "ncclRecv"));
+    }
+    LXC(c->nccl(api.GroupEnd(), "ncclGroupEnd"));
     // the unpacks below run on the same stream, after the received bytes landed
     for (uint32_t q = 0; q < G; q++)
         if (rb[q])
-            LXC(c->index(lx_la_unpack_dev(c->ix, q, reinterpret_cast<const uint32_t *>(c->recv + ro[q]), nullptr),
-                         "lx_la_unpack_dev"));
+            LXC(c->index(lx_la_unpack_wire_dev(c->ix, q, c->recv + ro[q], rw[q]), "lx_la_unpack_wire_dev"));
     LXC(c->index(lx_la_own_dev(c->ix, nullptr), "lx_la_own_dev"));
     return c->hip(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
 }
