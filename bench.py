@@ -99,6 +99,49 @@ def cpu_baseline(dag, weights, n_events_max, fc_n, budget_s):
     return done, t_add, fc_n, t_fc, (len(qa2), t_mt, threads)
 
 
+LAT_KINDS = ["add1_async", "add1_sync", "build1_add_drop_sync", "antichain_add_sync", "add1024_sync", "fc1", "fc667",
+             "get_hb", "get_la", "get_merged_hb", "get_merged_hb_x64"]
+
+
+def latency_leg(lx, dag, weights, device, history=200_000, reps=2000, feed=1_000_000):
+    """Per-call latency of the drop-in boundary at the granularity the
+    reference's callers use it (abft/indexed_lachesis.go:53-82 one Add per
+    event, Build = Add + DropNotFlushed; abft/event_processing.go:149-161 one
+    ForklessCause per (event, root); abft/lachesis.go:57 GetMergedHighestBefore
+    per event), timed from native code over the C ABI (tools/lx_latency.cpp:
+    wall clock around each call, p50/p99/mean in us) on an epoch of the bench
+    DAG with `history` events already indexed; then C3 events/s when the DAG is
+    fed antichain by antichain (events re-ordered by topological level, one
+    lx_add_batch + lx_flush per level), directly and through the level batcher."""
+    import ctypes
+    import numpy as np
+    path = os.path.join(PKG, "build", "liblx_bench.so")
+    L = ctypes.CDLL(path)
+    f = L.lx_bench_latency
+    f.restype = ctypes.c_int
+    u32p, u64p = ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint64)
+    f.argtypes = [ctypes.c_int, ctypes.c_uint32, u32p, ctypes.c_uint64, u32p, u32p, u64p, u32p, ctypes.c_uint64,
+                  ctypes.c_uint32, ctypes.c_uint64, ctypes.POINTER(ctypes.c_double), ctypes.c_char_p, ctypes.c_uint32]
+    n = min(len(dag), history + 2 * feed + 600_000)
+    w = np.ascontiguousarray(weights, dtype=np.uint32)
+    cr = np.ascontiguousarray(dag.creator[:n])
+    sq = np.ascontiguousarray(dag.seq[:n])
+    po = np.ascontiguousarray(dag.poff[:n + 1])
+    out = (ctypes.c_double * 64)()
+    err = ctypes.create_string_buffer(512)
+    rc = f(device, len(w), w.ctypes.data_as(u32p), n, cr.ctypes.data_as(u32p), sq.ctypes.data_as(u32p),
+           po.ctypes.data_as(u64p), dag.par.ctypes.data_as(u32p), history, reps, feed, out, err, 512)
+    if rc != 0:
+        raise RuntimeError("lx_bench_latency: " + err.value.decode())
+    res = {"unit": "us", "history_events": history, "reps": reps,
+           "calls": {k: {"p50": out[3 * i], "p99": out[3 * i + 1], "mean": out[3 * i + 2]} for i, k in enumerate(LAT_KINDS)},
+           "antichain_fed_events_per_sec": out[33], "batcher_fed_events_per_sec": out[36],
+           "fed_events": int(out[34]), "fed_levels": int(out[35]), "mean_events_per_level": out[37],
+           "note": "add1_async = host time of lx_add_batch(n=1) + lx_flush (the launch is not waited for); "
+                   "*_sync include lx_sync (completion); fc/getters are synchronous calls"}
+    return res
+
+
 ABFT_CONFIG = ("c5", 1000, 50, 10, "zipf")   # BASELINE configs[4]: V, events/validator, parents, stakes
 
 
@@ -174,6 +217,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--mode", default="shard", choices=["replica", "shard"])
     ap.add_argument("--no-abft", action="store_true", help="skip the configs[4] abft leg")
+    ap.add_argument("--no-latency", action="store_true", help="skip the per-call latency / antichain-fed leg")
     ap.add_argument("--shard-solo", type=int, default=0,
                     help="diagnostic: time rank 0 of a G-way column shard alone on this GPU (its index walk, "
                          "the packing of its outgoing LowestAfter blocks, its partial FC); no collectives")
@@ -384,6 +428,10 @@ def main():
         result["shard"] = {"columns": B, "wire_bytes_per_entry": wire,
                            "exchange_ms": float(np.mean(st_x[-args.steps:])) if st_x else None,
                            "note": "index step = walk of own columns + LowestAfter all-to-all (timed inside value)"}
+
+    if not args.no_latency and world == 1 and not solo:
+        ix.close()   # free the bench epoch's planes first
+        result["latency"] = latency_leg(lx, dag, weights, local)
 
     if not args.no_abft:
         ab = abft_leg(lx, args.steps, args.warmup, local, args.cpu_budget, rank == 0 and world == 1 and not args.no_cpu)

@@ -137,10 +137,23 @@ uint32_t lx_quorum(const lx_index *h);                 /* pos/validators.go:187-
 
 /* Getters.  *len receives the byte length; out may be NULL to query it.
  * GetHighestBefore / GetLowestAfter (vecfc/store_vectors.go:26-51),
- * GetMergedHighestBefore (vecengine/index.go:235-250). */
+ * GetMergedHighestBefore (vecengine/index.go:235-250 with GatherFrom,
+ * vecfc/vector_ops.go:81-96).  Rows are encoded on the device. */
 int lx_get_highest_before(lx_index *h, uint32_t ev, uint8_t *out, uint32_t cap, uint32_t *len);
 int lx_get_lowest_after(lx_index *h, uint32_t ev, uint8_t *out, uint32_t cap, uint32_t *len);
 int lx_get_merged_highest_before(lx_index *h, uint32_t ev, uint8_t *out, uint32_t cap, uint32_t *len);
+/* The same for n events in one call (applyAtropos, abft/lachesis.go:57, and the
+ * emitter's candidate loops call GetMergedHighestBefore per event): row i is
+ * written at out + off[i], off has n+1 entries (byte offsets, always filled);
+ * out may be NULL to query the sizes; a buffer smaller than off[n] gives
+ * LX_ERR_ARG (off still filled).  Unknown events: LX_ERR_ARG (the reference's
+ * getters return nil for them). */
+int lx_get_highest_before_batch(lx_index *h, uint32_t n, const uint32_t *ev, uint64_t *off, uint8_t *out,
+                                uint64_t cap);
+int lx_get_lowest_after_batch(lx_index *h, uint32_t n, const uint32_t *ev, uint64_t *off, uint8_t *out,
+                              uint64_t cap);
+int lx_get_merged_highest_before_batch(lx_index *h, uint32_t n, const uint32_t *ev, uint64_t *off, uint8_t *out,
+                                       uint64_t cap);
 int lx_get_event_branch_id(lx_index *h, uint32_t ev, uint32_t *out);
 
 /* BranchesInfo (vecengine/branches_info.go:9-14): per branch last seq and

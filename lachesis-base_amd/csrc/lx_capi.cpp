@@ -18,7 +18,8 @@
 
 namespace {
 
-constexpr uint32_t kStatusWords = 64;   // [1] fc bad flag, [2] max seq, [8..9] batch error u64, [16..47] jump flags
+constexpr uint32_t kStatusWords = 64;   // [1] fc bad flag, [2] max seq, [3] pinned-FC sink, [4] unresolved
+                                        // branch, [8..9] batch error u64, [16..47] jump flags
 
 template <typename T>
 hipError_t dalloc(T **p, uint64_t n) {
@@ -28,6 +29,14 @@ hipError_t dalloc(T **p, uint64_t n) {
 }
 
 inline uint32_t round_up(uint32_t x, uint32_t m) { return (x + m - 1) / m * m; }
+
+// hipSetDevice costs microseconds per call; every entry point makes sure the
+// handle's device is current, so switch only when it is not
+inline hipError_t set_dev(int device) {
+    int cur = -1;
+    if (hipGetDevice(&cur) == hipSuccess && cur == device) return hipSuccess;
+    return hipSetDevice(device);
+}
 
 }  // namespace
 
@@ -49,6 +58,7 @@ struct lx_index {
     bool la_tail = true;                   // LX_LA_MEMSET=1: zero the whole LA plane at reset instead
     uint32_t *tail_zw = nullptr, *tail_lo = nullptr, *tail_cmin = nullptr;
     uint32_t tail_cap = 0;
+    bool tail_dirty = false;               // zw holds progress (a tail pass ran since it was zeroed)
     uint32_t wire_force = 0;               // LX_SHARD_WIRE=4: LowestAfter blocks always uint32
     uint32_t *wire_flag = nullptr;         // device flag of the byte-wire fit check (4 B)
     uint32_t pcols_used = 0;       // plane columns rows may hold non-zero values in (since the last zeroing)
@@ -74,6 +84,8 @@ struct lx_index {
              *brow = nullptr, *wpad = nullptr, *col_list = nullptr;
     uint32_t *cheat_off = nullptr, *cheat_br = nullptr, *cheat_creator = nullptr;
     uint32_t *cheat_brl = nullptr, *cheat_crl = nullptr;   // the same as plane columns (shards)
+    int32_t *cheat_of = nullptr;           // creator -> index into the cheater CSR (-1: one branch)
+    uint32_t cheat_of_cap = 0;
     uint32_t n_cheat = 0, ncols = 0;
     // column shard (shard_count > 1): own columns only (lx_internal.h)
     std::vector<uint32_t> h_cmap;          // global branch -> plane column / LX_NONE
@@ -118,9 +130,33 @@ struct lx_index {
     lx_writeback wb{};
     std::string wb_bi;
 
+    // small-batch (latency) path, lx_small.hip: the host assigns branches in Add
+    // order from a mirror of the per-event metadata and stages the batch in
+    // pinned memory; one H2D copy + one launch, no sync
+    uint32_t small_max = kSmallMaxN;       // LX_SMALL_MAX: largest batch on this path (0: never)
+    bool hm_ok = false;                    // the mirror equals the device metadata
+    uint64_t hm_n = 0;                     // events whose (immutable) metadata the mirror holds
+    std::vector<uint32_t> hm_creator, hm_seq, hm_branch, hm_bbefore;
+    std::vector<uint32_t> hm_blen;         // per branch: events on it (= device branch_len)
+    std::vector<uint32_t> sm_level, sm_cnt, sm_touched;   // scratch
+    static constexpr int kSlots = 4;       // pinned staging images in flight
+    uint32_t *st_pin[kSlots] = {};
+    uint64_t st_pin_cap[kSlots] = {};
+    hipEvent_t st_done[kSlots] = {};       // the H2D copy of slot k has read it
+    bool st_used[kSlots] = {};
+    uint32_t st_next = 0;
+    uint32_t *st_dev = nullptr;            // device image (stream order serialises its reuse)
+    uint64_t st_dev_cap = 0;
+    // pinned, device-mapped query buffers (per-call ForklessCause, getters)
+    uint8_t *qp = nullptr;
+    uint64_t qp_cap = 0;
+    uint32_t *q_sink = nullptr;            // status word the pinned FC path lets the kernel flag into
+
     // timing (HIP events on `stream`)
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     lx_stats stats{};
+    bool stats_lazy = false;               // small path: ms_index from ev[1..2] on demand
+    bool small_timing = false;             // LX_TIMING=1: time small-path launches (two event records)
     uint32_t diag_nofill = 0;   // LX_DIAG_NOFILL=1: timing-only build of the walker (LA left empty)
     uint32_t cpw_hint = 0, ncw_hint = 0;   // LX_CPW / LX_NCW tuning overrides
     uint32_t rr_hint = 0, diag = 0;        // LX_RR record ring depth; LX_DIAG timing-only modes
@@ -178,10 +214,12 @@ void free_all(lx_index *h) {
         if (p) (void)hipFree(p);
     h->tail_zw = h->tail_lo = h->tail_cmin = h->wire_flag = nullptr;
     h->tail_cap = 0;
-    void *lptrs[] = {h->cheat_brl, h->cheat_crl, h->cmap, h->lap, h->wloc};
+    void *lptrs[] = {h->cheat_brl, h->cheat_crl, h->cmap, h->lap, h->wloc, h->cheat_of};
     for (void *p : lptrs)
         if (p) (void)hipFree(p);
     h->cheat_brl = h->cheat_crl = h->cmap = h->lap = h->wloc = nullptr;
+    h->cheat_of = nullptr;
+    h->cheat_of_cap = 0;
     h->cmap_cap = 0;
     for (uint32_t *p : h->sc_rows)
         if (p) (void)hipFree(p);
@@ -291,6 +329,7 @@ int la_tail(lx_index *h, hipStream_t s) {
     t.cmin = h->tail_cmin;
     t.tcap = h->tail_cap;
     HIPCHK(h, lx::launch_la_tail(t, s));
+    h->tail_dirty = true;
     return 0;
 }
 
@@ -439,6 +478,16 @@ int rebuild_columns(lx_index *h) {
         off.push_back((uint32_t)br.size());
     }
     h->n_cheat = (uint32_t)cr.size();
+    if (h->V > h->cheat_of_cap) {
+        if (h->cheat_of) (void)hipFree(h->cheat_of);
+        h->cheat_of = nullptr;
+        h->cheat_of_cap = 0;
+        HIPCHK(h, dalloc(&h->cheat_of, h->V));
+        h->cheat_of_cap = h->V;
+    }
+    std::vector<int32_t> co(h->V, -1);   // alive until the sync below
+    for (uint32_t k = 0; k < cr.size(); k++) co[cr[k]] = (int32_t)k;
+    HIPCHK(h, hipMemcpyAsync(h->cheat_of, co.data(), h->V * 4ull, hipMemcpyHostToDevice, h->stream));
     uint64_t need = std::max<uint64_t>({off.size(), br.size(), 1});
     if (need > h->cheat_cap) {
         uint64_t cap = std::max<uint64_t>(need * 2, 256);
@@ -502,6 +551,8 @@ int add_batch_dev(lx_index *h, uint32_t n, const uint32_t *creator, const uint32
     if (n == 0) return 0;
     h->wb_ready = false;
     if (h->n_events + n >= 0xFFFFFFF0ull) return h->fail(LX_ERR_ARG, "too many events in one epoch");
+    h->hm_ok = false;           // the device assigns this batch: the host mirror is refreshed on demand
+    h->stats_lazy = false;
     int rc;
     if ((rc = grow_events(h, h->n_events + n))) return rc;
     if ((rc = ensure_batch(h, n, 0))) return rc;
@@ -537,7 +588,12 @@ int add_batch_dev(lx_index *h, uint32_t n, const uint32_t *creator, const uint32
     h->max_seq = std::max(h->max_seq, bmax);
     if ((rc = grow_scap(h, h->max_seq))) return rc;
     a = batch_args(h, n, creator, seq, poff, par);   // pointers may have moved
-    HIPCHK(h, lx::launch_batch_finish(a, s));
+    // pointer jumping along in-batch self-parent chains: a chain has at most
+    // min(n, max seq) events, ceil(log2) + 1 rounds resolve it (k_finalize flags
+    // an unresolved event, checked below)
+    uint32_t rounds = 1;
+    while (rounds < 32 && (1ull << (rounds - 1)) < std::min<uint64_t>(n, bmax)) rounds++;
+    HIPCHK(h, lx::launch_batch_finish(a, rounds + 1, s));
     if (nforks) {
         std::vector<uint32_t> cr(nforks), fs(nforks);
         HIPCHK(h, hipMemcpyAsync(cr.data(), h->branch_creator + h->B, nforks * 4, hipMemcpyDeviceToHost, s));
@@ -646,6 +702,9 @@ int add_batch_dev(lx_index *h, uint32_t n, const uint32_t *creator, const uint32
     h->n_events += n;
     h->hwm = std::max(h->hwm, h->n_events);
     HIPCHK(h, hipStreamSynchronize(s));
+    uint32_t unresolved = 0;
+    HIPCHK(h, hipMemcpy(&unresolved, h->status + 4, 4, hipMemcpyDeviceToHost));
+    if (unresolved) return h->fail(LX_ERR_STATE, "branch assignment left %u events unresolved", unresolved);
     float t0 = 0, t1 = 0, t2 = 0;
     HIPCHK(h, hipEventElapsedTime(&t0, h->ev[0], h->ev[1]));
     HIPCHK(h, hipEventElapsedTime(&t1, h->ev[1], h->ev[2]));
@@ -921,6 +980,289 @@ int branches_info_rlp(lx_index *h, std::string *out) {
     return 0;
 }
 
+// ---- per-call queries: pinned, device-mapped host buffer (host and device pointer)
+constexpr uint64_t kFcPinnedMax = 1u << 16;
+
+int ensure_qp(lx_index *h, uint64_t bytes, uint8_t **host, uint8_t **dev) {
+    if (bytes > h->qp_cap) {
+        if (h->qp) {
+            HIPCHK(h, hipStreamSynchronize(h->stream));
+            (void)hipHostFree(h->qp);
+        }
+        h->qp = nullptr;
+        h->qp_cap = 0;
+        const uint64_t cap = std::max<uint64_t>(bytes, 1u << 16);
+        HIPCHK(h, hipHostMalloc((void **)&h->qp, cap, hipHostMallocMapped));
+        h->qp_cap = cap;
+    }
+    void *d = nullptr;
+    HIPCHK(h, hipHostGetDevicePointer(&d, h->qp, 0));
+    *host = h->qp;
+    *dev = static_cast<uint8_t *>(d);
+    return 0;
+}
+
+// ---- small-batch (latency) path (lx_small.hip)
+
+// Refresh the host mirror after batches the device assigned (big path): the
+// immutable per-event fields of the events not mirrored yet, branch lengths whole.
+int hm_sync(lx_index *h) {
+    if (h->hm_ok) return 0;
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    const uint64_t n = h->n_events, lo = std::min(h->hm_n, n);
+    std::vector<uint32_t> *v[] = {&h->hm_creator, &h->hm_seq, &h->hm_branch, &h->hm_bbefore};
+    const uint32_t *d[] = {h->ev_creator, h->ev_seq, h->ev_branch, h->ev_bbefore};
+    for (int k = 0; k < 4; k++) {
+        v[k]->resize(n);
+        if (n > lo) HIPCHK(h, hipMemcpy(v[k]->data() + lo, d[k] + lo, (n - lo) * 4, hipMemcpyDeviceToHost));
+    }
+    h->hm_blen.resize(h->B);
+    HIPCHK(h, hipMemcpy(h->hm_blen.data(), h->branch_len, h->B * 4ull, hipMemcpyDeviceToHost));
+    h->hm_n = n;
+    h->hm_ok = true;
+    return 0;
+}
+
+// pinned staging image of `words` uint32 (the slot's previous copy has finished
+// reading it) and a device image at least as large
+int stage_slot(lx_index *h, uint64_t words, uint32_t **out, int *slot) {
+    const int k = (int)h->st_next;
+    h->st_next = (h->st_next + 1) % lx_index::kSlots;
+    if (h->st_used[k]) HIPCHK(h, hipEventSynchronize(h->st_done[k]));
+    h->st_used[k] = false;
+    if (words > h->st_pin_cap[k]) {
+        if (h->st_pin[k]) (void)hipHostFree(h->st_pin[k]);
+        h->st_pin[k] = nullptr;
+        h->st_pin_cap[k] = 0;
+        const uint64_t cap = std::max<uint64_t>(words + words / 2, 16384);
+        HIPCHK(h, hipHostMalloc((void **)&h->st_pin[k], cap * 4, hipHostMallocDefault));
+        h->st_pin_cap[k] = cap;
+    }
+    if (words > h->st_dev_cap) {
+        if (h->st_dev) {
+            HIPCHK(h, hipStreamSynchronize(h->stream));
+            (void)hipFree(h->st_dev);
+        }
+        h->st_dev = nullptr;
+        h->st_dev_cap = 0;
+        const uint64_t cap = std::max<uint64_t>(words + words / 2, 16384);
+        HIPCHK(h, dalloc(&h->st_dev, cap));
+        h->st_dev_cap = cap;
+    }
+    *out = h->st_pin[k];
+    *slot = k;
+    return 0;
+}
+
+// Add for a batch of at most small_max events, host pointers, unsharded handle.
+// Validation and branch assignment run on the host in Add order -- the
+// reference's own sequential fillGlobalBranchID (vecengine/index.go:105-141:
+// a root continues the creator's branch iff its lastSeq is 0, a self-parented
+// event continues its self-parent's branch iff lastSeq + 1 == seq, otherwise a
+// new branch) over the mirrored metadata -- with the checks and error codes of
+// k_validate_claim; the device work is one copy and one launch (k_small), and
+// nothing waits for it: errors are known before anything is enqueued.
+int add_batch_small(lx_index *h, uint32_t n, const uint32_t *creator, const uint32_t *seq, const uint64_t *poff,
+                    const uint32_t *par, uint32_t *out_branch, uint32_t *err_index) {
+    int rc;
+    if ((rc = hm_sync(h))) return rc;
+    const uint64_t bs = h->n_events;
+    for (uint32_t i = 0; i < n; i++) {
+        const uint64_t g = bs + i;
+        const uint32_t c = creator[i], s = seq[i];
+        const uint64_t p0 = poff[i], p1 = poff[i + 1];
+        int code = 0;
+        if (c >= h->V) {
+            code = LX_ERR_ARG;
+        } else if (s == 0 || s >= 0x7FFFFFFEu) {
+            code = LX_ERR_EVENT;
+        } else {
+            for (uint64_t x = p0; x < p1; x++)
+                if (par[x] >= g) { code = LX_ERR_ORDER; break; }
+            if (!code && s > 1) {
+                if (p1 == p0) {
+                    code = LX_ERR_EVENT;
+                } else {
+                    const uint32_t sp = par[p0];
+                    const uint32_t cs = sp < bs ? h->hm_creator[sp] : creator[sp - bs];
+                    const uint32_t ss = sp < bs ? h->hm_seq[sp] : seq[sp - bs];
+                    if (cs != c || ss + 1 != s) code = LX_ERR_EVENT;
+                }
+            }
+        }
+        if (code) {
+            if (err_index) *err_index = i;
+            if (code == LX_ERR_ORDER) return h->fail(code, "event %u: processed out of order, parent not found", i);
+            if (code == LX_ERR_ARG) return h->fail(code, "event %u: creator idx out of range", i);
+            return h->fail(code, "event %u: violates seq/self-parent invariants (eventcheck)", i);
+        }
+    }
+
+    const uint64_t npar = poff[n] - poff[0];
+    // image: records, parents, perm, level offsets (<= n + 1), new branches' first
+    // seqs and creators (<= n each), touched branches' (branch, length) (<= 2n)
+    const uint64_t w_ev = 12ull * n;
+    const uint64_t words = w_ev + npar + n + (n + 1) + 2ull * n + 2ull * n;
+    uint32_t *img;
+    int slot;
+    if ((rc = stage_slot(h, words, &img, &slot))) return rc;
+    SmallEv *ev = reinterpret_cast<SmallEv *>(img);
+    uint32_t *ipar = img + w_ev;
+    if (npar) memcpy(ipar, par + poff[0], npar * 4);
+
+    h->wb_ready = false;
+    const uint32_t B0 = h->B;
+    uint32_t B = B0, max_level = 0, bmax = 0;
+    h->hm_creator.resize(bs + n);
+    h->hm_seq.resize(bs + n);
+    h->hm_branch.resize(bs + n);
+    h->hm_bbefore.resize(bs + n);
+    h->sm_level.resize(n);
+    h->sm_touched.clear();
+    for (uint32_t i = 0; i < n; i++) {
+        const uint64_t g = bs + i;
+        const uint32_t c = creator[i], s = seq[i];
+        const uint64_t p0 = poff[i], p1 = poff[i + 1];
+        const uint32_t sp = s > 1 ? par[p0] : LX_NONE;
+        uint32_t br = 0;
+        bool cont = false;
+        if (s > 1) {
+            const uint32_t bsp = h->hm_branch[sp];
+            const uint32_t len = h->hm_blen[bsp];
+            const uint32_t last = len ? h->h_branch_first[bsp] + len - 1 : 0;
+            if (last + 1 == s) { br = bsp; cont = true; }
+        } else if (h->hm_blen[c] == 0) {
+            br = c;
+            cont = true;
+        }
+        const uint32_t bb = B;
+        if (!cont) {
+            br = B++;
+            h->h_branch_first.push_back(s);
+            h->h_branch_creator.push_back(c);
+            h->by_creator[c].push_back(br);
+            h->hm_blen.push_back(0);
+        }
+        h->hm_blen[br] = s - h->h_branch_first[br] + 1;
+        h->hm_creator[g] = c;
+        h->hm_seq[g] = s;
+        h->hm_branch[g] = br;
+        h->hm_bbefore[g] = bb;
+        uint32_t lvl = 0;
+        for (uint64_t x = p0; x < p1; x++)
+            if (par[x] >= bs) lvl = std::max(lvl, h->sm_level[par[x] - bs] + 1);
+        h->sm_level[i] = lvl;
+        max_level = std::max(max_level, lvl);
+        bmax = std::max(bmax, s);
+        ev[i].q0 = make_uint4(br, s, (cont && s > 1) ? sp : LX_NONE, (uint32_t)(p1 - p0));
+        ev[i].q1 = make_uint4((uint32_t)(p0 - poff[0]), h->h_branch_first[br], sp, bb);
+        ev[i].q2 = make_uint4(c, cont ? kSmallCont : 0u, LX_NONE, 0u);
+        if (cont && sp != LX_NONE && sp >= bs) ev[sp - bs].q2.z = (uint32_t)g;
+        if (out_branch) out_branch[i] = br;
+        h->sm_touched.push_back(br);
+    }
+    // events by level (counting sort; batch order inside a level)
+    const uint32_t L = max_level + 1;
+    uint32_t *perm = ipar + npar, *loff = perm + n;
+    h->sm_cnt.assign(L + 1, 0);
+    for (uint32_t i = 0; i < n; i++) h->sm_cnt[h->sm_level[i] + 1]++;
+    for (uint32_t l = 0; l < L; l++) h->sm_cnt[l + 1] += h->sm_cnt[l];
+    for (uint32_t l = 0; l <= L; l++) loff[l] = h->sm_cnt[l];
+    for (uint32_t i = 0; i < n; i++) perm[h->sm_cnt[h->sm_level[i]]++] = i;
+    const uint32_t nf = B - B0;
+    uint32_t *nfirst = loff + L + 1, *ncreator = nfirst + nf, *blen = ncreator + nf;
+    for (uint32_t x = 0; x < nf; x++) {
+        nfirst[x] = h->h_branch_first[B0 + x];
+        ncreator[x] = h->h_branch_creator[B0 + x];
+    }
+    std::sort(h->sm_touched.begin(), h->sm_touched.end());
+    h->sm_touched.erase(std::unique(h->sm_touched.begin(), h->sm_touched.end()), h->sm_touched.end());
+    const uint32_t n_blen = (uint32_t)h->sm_touched.size();
+    for (uint32_t x = 0; x < n_blen; x++) {
+        blen[2 * x] = h->sm_touched[x];
+        blen[2 * x + 1] = h->hm_blen[h->sm_touched[x]];
+    }
+    const uint64_t used = (uint64_t)(blen + 2 * n_blen - img);
+
+    // capacity (rare re-layouts sync the stream); on failure the host mirror is rolled back
+    h->max_seq = std::max(h->max_seq, bmax);
+    if ((rc = grow_events(h, bs + n)) || (rc = grow_branches(h, B)) || (rc = grow_scap(h, h->max_seq))) {
+        h->h_branch_first.resize(B0);
+        h->h_branch_creator.resize(B0);
+        for (auto &l : h->by_creator)
+            while (!l.empty() && l.back() >= B0) l.pop_back();
+        h->hm_ok = false;
+        h->hm_n = std::min<uint64_t>(h->hm_n, bs);
+        return rc;
+    }
+    h->B = B;
+    h->pcols_used = std::max(h->pcols_used, B);
+    if (nf || h->ncols == 0)
+        if ((rc = rebuild_columns(h))) return rc;
+    hipStream_t s = h->stream;
+    HIPCHK(h, hipMemcpyAsync(h->st_dev, img, used * 4, hipMemcpyHostToDevice, s));
+    HIPCHK(h, hipEventRecord(h->st_done[slot], s));
+    h->st_used[slot] = true;
+
+    SmallArgs a{};
+    a.hb = h->hb;
+    a.la = h->la;
+    a.stride = h->pstride;
+    a.bs = (uint32_t)bs;
+    a.n = n;
+    a.B0 = B0;
+    a.B = B;
+    const uint32_t *d = h->st_dev;
+    a.ev = reinterpret_cast<const SmallEv *>(d);
+    a.par = d + w_ev;
+    a.perm = d + (perm - img);
+    a.lvl_off = d + (loff - img);
+    a.n_levels = L;
+    a.new_first = d + (nfirst - img);
+    a.new_creator = d + (ncreator - img);
+    a.blen = d + (blen - img);
+    a.n_blen = n_blen;
+    a.ev_creator = h->ev_creator;
+    a.ev_seq = h->ev_seq;
+    a.ev_branch = h->ev_branch;
+    a.ev_bbefore = h->ev_bbefore;
+    a.ev_sp = h->ev_sp;
+    a.first_child = h->first_child;
+    a.first_root = h->first_root;
+    a.branch_first = h->branch_first;
+    a.branch_creator = h->branch_creator;
+    a.branch_len = h->branch_len;
+    a.brow = h->brow;
+    a.s_cap = h->s_cap;
+    a.mask = B > h->V ? 1u : 0u;
+    if (h->small_timing) HIPCHK(h, hipEventRecord(h->ev[1], s));
+    HIPCHK(h, lx::launch_small(a, s));
+    if (h->small_timing) HIPCHK(h, hipEventRecord(h->ev[2], s));
+    if (B > h->V && h->n_cheat) {
+        MarkArgs m{};
+        m.hb = h->hb;
+        m.stride = h->pstride;
+        m.batch_start = (uint32_t)bs;
+        m.n = n;
+        m.V = h->V;
+        m.ev_branch = h->ev_branch;
+        m.ev_bbefore = h->ev_bbefore;
+        m.branch_first = h->branch_first;
+        m.n_cheat = h->n_cheat;
+        m.cheat_off = h->cheat_off;
+        m.cheat_br = h->cheat_br;
+        HIPCHK(h, lx::launch_marks(m, s));
+    }
+    h->n_events += n;
+    h->hwm = std::max(h->hwm, h->n_events);
+    h->hm_n = h->n_events;
+    h->last_npar = npar;
+    h->stats = lx_stats{};
+    h->stats.index_launches = 1;
+    h->stats_lazy = h->small_timing;
+    return 0;
+}
+
 }  // namespace
 
 // =============================================================================== C ABI
@@ -951,8 +1293,15 @@ int lx_create(const lx_config *cfg, lx_index **out) {
     if (const char *d = getenv("LX_SMALL")) h->small = (uint32_t)atoi(d);
     if (const char *d = getenv("LX_LA_MEMSET")) h->la_tail = (d[0] != '1');
     if (const char *d = getenv("LX_SHARD_WIRE")) h->wire_force = (uint32_t)atoi(d);
+    if (const char *d = getenv("LX_SMALL_MAX")) h->small_max = (uint32_t)atoi(d);
+    if (const char *d = getenv("LX_TIMING")) h->small_timing = (d[0] == '1');
     for (auto &e : h->ev)
         if (hipEventCreate(&e) != hipSuccess) {
+            delete h;
+            return LX_ERR_HIP;
+        }
+    for (auto &e : h->st_done)
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
             delete h;
             return LX_ERR_HIP;
         }
@@ -968,6 +1317,12 @@ void lx_destroy(lx_index *h) {
     if (h->status) (void)hipFree(h->status);
     for (auto &e : h->ev)
         if (e) (void)hipEventDestroy(e);
+    for (auto &e : h->st_done)
+        if (e) (void)hipEventDestroy(e);
+    for (auto *p : h->st_pin)
+        if (p) (void)hipHostFree(p);
+    if (h->st_dev) (void)hipFree(h->st_dev);
+    if (h->qp) (void)hipHostFree(h->qp);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
 }
@@ -983,7 +1338,7 @@ int lx_reset(lx_index *h, uint32_t nv, const uint32_t *w) {
         tot += w[i];
     }
     if (tot > 0x7FFFFFFFull) return h->fail(LX_ERR_ARG, "validators weight overflow");   // validators.go:101-110
-    HIPCHK(h, hipSetDevice(h->device));
+    HIPCHK(h, set_dev(h->device));
     HIPCHK(h, hipStreamSynchronize(h->stream));
     h->wb_ready = false;
     h->V = nv;
@@ -1031,7 +1386,9 @@ int lx_reset(lx_index *h, uint32_t nv, const uint32_t *w) {
             // tail, la_tail): only fork-branch columns of old rows need zeroing
             if (used > no)
                 HIPCHK(h, hipMemset2DAsync(h->la + no, (size_t)h->pstride * 4, 0, (size_t)(used - no) * 4, h->hwm, h->stream));
-            if (h->tail_zw) HIPCHK(h, hipMemsetAsync(h->tail_zw, 0, (uint64_t)h->tail_cap * h->tail_cap * 4, h->stream));
+            if (h->tail_zw && h->tail_dirty)
+                HIPCHK(h, hipMemsetAsync(h->tail_zw, 0, (uint64_t)h->tail_cap * h->tail_cap * 4, h->stream));
+            h->tail_dirty = false;
         } else {
             HIPCHK(h, hipMemsetAsync(h->la, 0, h->hwm * h->pstride * 4, h->stream));
         }
@@ -1067,6 +1424,11 @@ int lx_reset(lx_index *h, uint32_t nv, const uint32_t *w) {
     h->h_branch_first = ones;
     h->by_creator.assign(nv, {});
     for (uint32_t i = 0; i < nv; i++) h->by_creator[i].push_back(i);
+    h->hm_ok = true;
+    h->hm_n = 0;
+    for (auto *v : {&h->hm_creator, &h->hm_seq, &h->hm_branch, &h->hm_bbefore}) v->clear();
+    h->hm_blen.assign(nv, 0);
+    h->stats_lazy = false;
     h->have_epoch = true;
     h->ncols = 0;
     return rebuild_columns(h);
@@ -1077,7 +1439,7 @@ int lx_add_batch(lx_index *h, uint32_t n, const uint32_t *creator, const uint32_
     if (!h) return LX_ERR_ARG;
     if (n == 0) return 0;
     if (!creator || !seq || !poff) return h->fail(LX_ERR_ARG, "null input");
-    HIPCHK(h, hipSetDevice(h->device));
+    HIPCHK(h, set_dev(h->device));
     uint64_t base = poff[0], npar = poff[n] - poff[0];
     if (poff[n] < poff[0] || npar >= 0xFFFFFFFFull) return h->fail(LX_ERR_ARG, "bad parent offsets");
     std::vector<uint32_t> off(n + 1);
@@ -1086,6 +1448,8 @@ int lx_add_batch(lx_index *h, uint32_t n, const uint32_t *creator, const uint32_
         off[i] = (uint32_t)(poff[i] - base);
     }
     int rc;
+    if (h->have_epoch && !h->sharded() && n <= std::min(h->small_max, kSmallMaxN))
+        return add_batch_small(h, n, creator, seq, poff, par, out_branch, err_index);
     if ((rc = ensure_batch(h, n, npar))) return rc;
     HIPCHK(h, hipMemcpyAsync(h->b_creator, creator, n * 4ull, hipMemcpyHostToDevice, h->stream));
     HIPCHK(h, hipMemcpyAsync(h->b_seq, seq, n * 4ull, hipMemcpyHostToDevice, h->stream));
@@ -1100,7 +1464,7 @@ int lx_add_batch(lx_index *h, uint32_t n, const uint32_t *creator, const uint32_
 int lx_add_batch_dev(lx_index *h, uint32_t n, const uint32_t *creator, const uint32_t *seq, const uint32_t *poff,
                      const uint32_t *par, uint32_t *err_index) {
     if (!h) return LX_ERR_ARG;
-    HIPCHK(h, hipSetDevice(h->device));
+    HIPCHK(h, set_dev(h->device));
     return add_batch_dev(h, n, creator, seq, poff, par, err_index);
 }
 
@@ -1115,19 +1479,27 @@ int lx_flush(lx_index *h) {
 int lx_drop_not_flushed(lx_index *h) {
     if (!h) return LX_ERR_ARG;
     if (!h->have_epoch) return 0;
-    HIPCHK(h, hipSetDevice(h->device));
+    HIPCHK(h, set_dev(h->device));
     h->wb_ready = false;
     if (h->n_events == h->n_flushed && h->B == h->B_flushed) return 0;
     HIPCHK(h, lx::launch_unfill(unfill_args(h), h->stream));
-    uint64_t rows = h->n_events - h->n_flushed;
-    if (rows) {
-        HIPCHK(h, hipMemsetAsync(h->hb + h->n_flushed * h->pstride, 0, rows * h->pstride * 4, h->stream));
-        HIPCHK(h, hipMemsetAsync(h->la + h->n_flushed * h->pstride, 0, rows * h->pstride * 4, h->stream));
-    }
+    HIPCHK(h, lx::launch_zero_rows(h->hb, h->la, h->pstride, (uint32_t)h->n_flushed, (uint32_t)h->n_events, h->stream));
     // re-added events may land on rows this epoch has not used yet (stale from an
     // earlier epoch) with seqs the tail table already counts as done: start over
-    if (h->tail_zw) HIPCHK(h, hipMemsetAsync(h->tail_zw, 0, (uint64_t)h->tail_cap * h->tail_cap * 4, h->stream));
-    HIPCHK(h, hipStreamSynchronize(h->stream));
+    if (h->tail_zw && h->tail_dirty) {
+        HIPCHK(h, hipMemsetAsync(h->tail_zw, 0, (uint64_t)h->tail_cap * h->tail_cap * 4, h->stream));
+        h->tail_dirty = false;
+    }
+    // host mirror: the same rollback of the branch lengths (k_unclaim) and rows
+    if (h->hm_ok) {
+        for (uint64_t e = h->n_flushed; e < h->n_events; e++) {
+            const uint32_t br = h->hm_branch[e];
+            if (br < h->B_flushed) h->hm_blen[br] = std::min(h->hm_blen[br], h->hm_seq[e] - h->h_branch_first[br]);
+        }
+        h->hm_blen.resize(h->B_flushed);
+        for (auto *v : {&h->hm_creator, &h->hm_seq, &h->hm_branch, &h->hm_bbefore}) v->resize(h->n_flushed);
+    }
+    h->hm_n = std::min(h->hm_n, h->n_flushed);
     h->n_events = h->n_flushed;
     if (h->B != h->B_flushed) {
         h->B = h->B_flushed;
@@ -1152,7 +1524,7 @@ int lx_writeback_prepare(lx_index *h, lx_writeback *out) {
     if (!h || !out) return LX_ERR_ARG;
     if (!h->have_epoch) return h->fail(LX_ERR_STATE, "write-back before lx_reset");
     if (h->shard_count > 1) return h->fail(LX_ERR_STATE, "write-back needs an unsharded handle (shards hold partial rows)");
-    HIPCHK(h, hipSetDevice(h->device));
+    HIPCHK(h, set_dev(h->device));
     h->wb_ready = false;
     const uint32_t N = (uint32_t)h->n_events, lo = (uint32_t)h->n_flushed;
     int rc;
@@ -1194,7 +1566,7 @@ int lx_writeback_fetch(lx_index *h, uint64_t *hb_off, uint8_t *hb_bytes, uint32_
                        uint8_t *la_bytes, uint8_t *branch_be, uint8_t *bi_rlp) {
     if (!h) return LX_ERR_ARG;
     if (!h->wb_ready) return h->fail(LX_ERR_STATE, "lx_writeback_fetch without a current lx_writeback_prepare");
-    HIPCHK(h, hipSetDevice(h->device));
+    HIPCHK(h, set_dev(h->device));
     const lx_writeback &w = h->wb;
     const uint32_t n = (uint32_t)w.n_events, m = (uint32_t)w.n_la_rows;
     int rc;
@@ -1254,7 +1626,28 @@ int lx_fc_combine_dev(lx_index *h, uint64_t n, const uint32_t *sum, uint8_t *out
 int lx_forkless_cause_batch(lx_index *h, uint64_t n, const uint32_t *a, const uint32_t *b, uint8_t *out) {
     if (!h) return LX_ERR_ARG;
     if (!n) return 0;
-    HIPCHK(h, hipSetDevice(h->device));
+    HIPCHK(h, set_dev(h->device));
+    if (n <= kFcPinnedMax) {
+        // per-call sizes (calcFrameIdx asks ~2/3 V pairs, the election |roots|):
+        // the kernel reads the pairs from and writes the answers into pinned host
+        // memory -- one launch and one stream sync, no copies
+        int rc;
+        uint8_t *hp, *dp;
+        if ((rc = ensure_qp(h, n * 9 + 16, &hp, &dp))) return rc;
+        memcpy(hp, a, n * 4);
+        memcpy(hp + 4 * n, b, n * 4);
+        FcArgs f;
+        if ((rc = fc_args(h, n, reinterpret_cast<uint32_t *>(dp), reinterpret_cast<uint32_t *>(dp + 4 * n), dp + 8 * n,
+                          nullptr, &f)))
+            return rc;
+        f.status = h->status + 2;   // k_fc flags status[1] = word 3, the sink; unknown events answer 0xFF
+        HIPCHK(h, lx::launch_fc(f, h->ncols, h->B > h->V, h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        memcpy(out, hp + 8 * n, n);
+        for (uint64_t i = 0; i < n; i++)
+            if (out[i] > 1) return h->fail(LX_ERR_ARG, "ForklessCause on an unknown event");   // forkless_cause.go:43-61
+        return 0;
+    }
     if (n > h->q_cap) {
         uint64_t cap = std::max<uint64_t>(n, 4096);
         if (h->q_a) (void)hipFree(h->q_a);
@@ -1281,101 +1674,143 @@ int lx_forkless_cause_batch(lx_index *h, uint64_t n, const uint32_t *a, const ui
 int lx_get_event_branch_id(lx_index *h, uint32_t ev, uint32_t *out) {
     if (!h || !out) return LX_ERR_ARG;
     if (ev >= h->n_events) return h->fail(LX_ERR_ARG, "failed to read event's branch ID (unknown event %u)", ev);
-    HIPCHK(h, hipSetDevice(h->device));
+    if (h->hm_ok) {
+        *out = h->hm_branch[ev];
+        return 0;
+    }
+    HIPCHK(h, set_dev(h->device));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
     return read_u32(h, h->ev_branch + ev, out);
 }
 
-static int event_row(lx_index *h, const uint32_t *plane, uint32_t ev, std::vector<uint32_t> &row, uint32_t *bbefore,
-                     uint32_t *branch) {
-    if (ev >= h->n_events) return h->fail(LX_ERR_ARG, "unknown event %u", ev);
-    if (h->sharded()) return h->fail(LX_ERR_STATE, "vector getters need an unsharded handle (shards hold their own columns)");
-    HIPCHK(h, hipSetDevice(h->device));
-    HIPCHK(h, hipStreamSynchronize(h->stream));
-    row.resize(h->B);
-    HIPCHK(h, hipMemcpy(row.data(), plane + (uint64_t)ev * h->stride, h->B * 4ull, hipMemcpyDeviceToHost));
-    int rc;
-    if ((rc = read_u32(h, h->ev_bbefore + ev, bbefore))) return rc;
-    return read_u32(h, h->ev_branch + ev, branch);
-}
+}  // extern "C"
 
-static int put_bytes(uint8_t *out, uint32_t cap, uint32_t *len, const std::vector<uint32_t> &words) {
-    uint32_t nbytes = (uint32_t)words.size() * 4;
-    if (len) *len = nbytes;
-    if (out && cap) memcpy(out, words.data(), std::min(cap, nbytes));   // little-endian host
+namespace {
+
+// Rows of n events in the reference byte layout (mode 0 HighestBefore, 1
+// LowestAfter, 2 merged HighestBefore), encoded on the device by k_get_rows
+// straight into the pinned buffer: one launch and one stream sync per call
+// (rows of more than kGetChunk bytes go in several).  *rows: row i at
+// rows + i * slot; len[i] its byte length.
+constexpr uint64_t kGetChunk = 64ull << 20;
+
+int get_rows(lx_index *h, uint32_t mode, uint32_t n, const uint32_t *ev, uint8_t **rows, uint64_t *slot,
+             const uint32_t **len) {
+    const uint64_t sl = ((uint64_t)8 * std::max(h->B, h->V) + 15) / 16 * 16;
+    const uint64_t head = ((uint64_t)8 * n + 15) / 16 * 16;   // events + lengths
+    uint8_t *hp, *dp;
+    int rc;
+    if ((rc = ensure_qp(h, head + n * sl, &hp, &dp))) return rc;
+    memcpy(hp, ev, n * 4ull);
+    GetArgs a{};
+    a.plane = mode == 1 ? h->la : h->hb;
+    a.stride = h->stride;
+    a.ev = reinterpret_cast<const uint32_t *>(dp);
+    a.n = n;
+    a.B = h->B;
+    a.V = h->V;
+    a.mode = mode;
+    a.forks = h->B > h->V ? 1u : 0u;
+    a.ev_bbefore = h->ev_bbefore;
+    a.ev_branch = h->ev_branch;
+    a.branch_first = h->branch_first;
+    a.cheat_of = h->cheat_of;
+    a.cheat_off = h->cheat_off;
+    a.cheat_br = h->cheat_br;
+    a.len = reinterpret_cast<uint32_t *>(dp + 4ull * n);
+    a.out = dp + head;
+    a.slot = sl;
+    HIPCHK(h, lx::launch_get_rows(a, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    *rows = hp + head;
+    *slot = sl;
+    *len = reinterpret_cast<const uint32_t *>(hp + 4ull * n);
     return 0;
 }
 
-// HighestBeforeSeq bytes (vecfc/vector.go:63-102): length 8*max(B_before, last
-// non-empty + 1); MinSeq is the branch's first seq.
-static void encode_hb(lx_index *h, const std::vector<uint32_t> &row, uint32_t bb, uint32_t bafter,
-                      std::vector<uint32_t> &w) {
-    uint32_t n = bb;
-    for (uint32_t c = 0; c < bafter && c < row.size(); c++)
-        if (row[c]) n = std::max(n, c + 1);
-    w.assign(2 * n, 0);
-    for (uint32_t c = 0; c < n && c < bafter; c++) {
-        uint32_t v = row[c];
-        if (v & LX_MARK) { w[2 * c] = 0; w[2 * c + 1] = 0x7FFFFFFF; }
-        else if (v) { w[2 * c] = v; w[2 * c + 1] = h->h_branch_first[c]; }
-    }
+int get_check(lx_index *h, uint32_t n, const uint32_t *ev) {
+    if (h->sharded()) return h->fail(LX_ERR_STATE, "vector getters need an unsharded handle (shards hold their own columns)");
+    if (!h->have_epoch) return h->fail(LX_ERR_STATE, "getter before lx_reset");
+    for (uint32_t i = 0; i < n; i++)
+        if (ev[i] >= h->n_events) return h->fail(LX_ERR_ARG, "unknown event %u", ev[i]);
+    HIPCHK(h, set_dev(h->device));
+    return 0;
 }
 
-int lx_get_highest_before(lx_index *h, uint32_t ev, uint8_t *out, uint32_t cap, uint32_t *len) {
+int get_one(lx_index *h, uint32_t mode, uint32_t ev, uint8_t *out, uint32_t cap, uint32_t *len) {
     if (!h) return LX_ERR_ARG;
-    std::vector<uint32_t> row, w;
-    uint32_t bb, br;
-    int rc = event_row(h, h->hb, ev, row, &bb, &br);
-    if (rc) return rc;
-    encode_hb(h, row, bb, bb + (br == bb ? 1 : 0), w);
-    return put_bytes(out, cap, len, w);
+    int rc;
+    if ((rc = get_check(h, 1, &ev))) return rc;
+    uint8_t *rows;
+    uint64_t slot;
+    const uint32_t *ln;
+    if ((rc = get_rows(h, mode, 1, &ev, &rows, &slot, &ln))) return rc;
+    if (len) *len = ln[0];
+    if (out && cap) memcpy(out, rows, std::min(cap, ln[0]));   // little-endian host
+    return 0;
+}
+
+int get_batch(lx_index *h, uint32_t mode, uint32_t n, const uint32_t *ev, uint64_t *off, uint8_t *out, uint64_t cap) {
+    if (!h || (n && (!ev || !off))) return LX_ERR_ARG;
+    int rc;
+    if ((rc = get_check(h, n, ev))) return rc;
+    off[0] = 0;
+    const uint64_t sl = ((uint64_t)8 * std::max(h->B, h->V) + 15) / 16 * 16;
+    const uint32_t chunk = (uint32_t)std::max<uint64_t>(1, kGetChunk / sl);
+    for (uint32_t i0 = 0; i0 < n; i0 += chunk) {
+        const uint32_t m = std::min(chunk, n - i0);
+        uint8_t *rows;
+        uint64_t slot;
+        const uint32_t *ln;
+        if ((rc = get_rows(h, mode, m, ev + i0, &rows, &slot, &ln))) return rc;
+        for (uint32_t i = 0; i < m; i++) {
+            off[i0 + i + 1] = off[i0 + i] + ln[i];
+            if (out && off[i0 + i + 1] <= cap) memcpy(out + off[i0 + i], rows + i * slot, ln[i]);
+        }
+    }
+    if (out && off[n] > cap)
+        return h->fail(LX_ERR_ARG, "getter buffer too small: %llu bytes needed", (unsigned long long)off[n]);
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int lx_get_highest_before(lx_index *h, uint32_t ev, uint8_t *out, uint32_t cap, uint32_t *len) {
+    return get_one(h, 0, ev, out, cap, len);
 }
 
 int lx_get_lowest_after(lx_index *h, uint32_t ev, uint8_t *out, uint32_t cap, uint32_t *len) {
-    if (!h) return LX_ERR_ARG;
-    std::vector<uint32_t> row;
-    uint32_t bb, br;
-    int rc = event_row(h, h->la, ev, row, &bb, &br);
-    if (rc) return rc;
-    uint32_t n = bb;
-    for (uint32_t c = 0; c < row.size(); c++)
-        if (row[c]) n = std::max(n, c + 1);
-    row.resize(n, 0);
-    return put_bytes(out, cap, len, row);
+    return get_one(h, 1, ev, out, cap, len);
 }
 
-// GetMergedHighestBefore (vecengine/index.go:235-250) with GatherFrom
-// (vecfc/vector_ops.go:81-96): first marked branch wins, else strictly
-// greatest Seq (first max wins).
 int lx_get_merged_highest_before(lx_index *h, uint32_t ev, uint8_t *out, uint32_t cap, uint32_t *len) {
-    if (!h) return LX_ERR_ARG;
-    if (h->B <= h->V) return lx_get_highest_before(h, ev, out, cap, len);
-    std::vector<uint32_t> row, w, m(2 * h->V, 0);
-    uint32_t bb, br;
-    int rc = event_row(h, h->hb, ev, row, &bb, &br);
-    if (rc) return rc;
-    encode_hb(h, row, bb, bb + (br == bb ? 1 : 0), w);
-    uint32_t nb = (uint32_t)w.size() / 2;
-    for (uint32_t c = 0; c < h->V; c++) {
-        uint32_t bs = 0, bm = 0;
-        for (uint32_t b : h->by_creator[c]) {
-            uint32_t s = b < nb ? w[2 * b] : 0, mm = b < nb ? w[2 * b + 1] : 0;
-            if (s == 0 && mm == 0x7FFFFFFF) { bs = s; bm = mm; break; }
-            if (s > bs) { bs = s; bm = mm; }
-        }
-        m[2 * c] = bs;
-        m[2 * c + 1] = bm;
-    }
-    return put_bytes(out, cap, len, m);
+    return get_one(h, 2, ev, out, cap, len);
+}
+
+int lx_get_highest_before_batch(lx_index *h, uint32_t n, const uint32_t *ev, uint64_t *off, uint8_t *out,
+                                uint64_t cap) {
+    return get_batch(h, 0, n, ev, off, out, cap);
+}
+
+int lx_get_lowest_after_batch(lx_index *h, uint32_t n, const uint32_t *ev, uint64_t *off, uint8_t *out, uint64_t cap) {
+    return get_batch(h, 1, n, ev, off, out, cap);
+}
+
+int lx_get_merged_highest_before_batch(lx_index *h, uint32_t n, const uint32_t *ev, uint64_t *off, uint8_t *out,
+                                       uint64_t cap) {
+    return get_batch(h, 2, n, ev, off, out, cap);
 }
 
 int lx_get_branches_info(lx_index *h, uint32_t *last_seq, uint32_t *creator_idx, uint32_t cap, uint32_t *n_branches) {
     if (!h) return LX_ERR_ARG;
     if (n_branches) *n_branches = h->B;
     if (!cap) return 0;
-    HIPCHK(h, hipSetDevice(h->device));
-    HIPCHK(h, hipStreamSynchronize(h->stream));
-    std::vector<uint32_t> len(h->B);
-    HIPCHK(h, hipMemcpy(len.data(), h->branch_len, h->B * 4ull, hipMemcpyDeviceToHost));
+    HIPCHK(h, set_dev(h->device));
+    int rc;
+    if ((rc = hm_sync(h))) return rc;
+    const std::vector<uint32_t> &len = h->hm_blen;
     for (uint32_t b = 0; b < h->B && b < cap; b++) {
         if (last_seq) last_seq[b] = len[b] ? h->h_branch_first[b] + len[b] - 1 : 0;
         if (creator_idx) creator_idx[b] = h->h_branch_creator[b];
@@ -1412,7 +1847,7 @@ int lx_shard_wire(lx_index *h, uint32_t *bytes_per_entry) {
 
 int lx_shard_block(lx_index *h, uint32_t src, uint32_t dst, uint64_t *elems) {
     if (!h || !elems || src >= h->shard_count || dst >= h->shard_count) return LX_ERR_ARG;
-    HIPCHK(h, hipSetDevice(h->device));
+    HIPCHK(h, set_dev(h->device));
     int rc;
     if ((rc = ensure_shard_rows(h))) return rc;
     *elems = (uint64_t)h->sc_nrows[src] * (h->sc_col_off[dst + 1] - h->sc_col_off[dst]);
@@ -1425,7 +1860,7 @@ int lx_shard_block(lx_index *h, uint32_t src, uint32_t dst, uint64_t *elems) {
 static int la_xfer(lx_index *h, uint32_t rows_of, uint32_t cols_of, uint32_t *buf, int mode, uint32_t wire = 0) {
     if (!h->sharded()) return h->fail(LX_ERR_STATE, "LowestAfter exchange needs a column-sharded handle");
     if (!h->have_epoch) return h->fail(LX_ERR_STATE, "exchange before lx_reset");
-    HIPCHK(h, hipSetDevice(h->device));
+    HIPCHK(h, set_dev(h->device));
     int rc;
     if ((rc = ensure_shard_rows(h))) return rc;
     const uint32_t c0 = h->sc_col_off[cols_of], c1 = h->sc_col_off[cols_of + 1];
@@ -1509,6 +1944,12 @@ int lx_la_own_dev(lx_index *h, void *stream) {
 int lx_last_stats(const lx_index *h, lx_stats *out) {
     if (!h || !out) return LX_ERR_ARG;
     *out = h->stats;
+    if (h->stats_lazy) {
+        // small path: the launch is timed by ev[1..2]; wait for it only when asked
+        float t = 0;
+        if (hipEventSynchronize(h->ev[2]) == hipSuccess && hipEventElapsedTime(&t, h->ev[1], h->ev[2]) == hipSuccess)
+            out->ms_index = t;
+    }
     return 0;
 }
 
@@ -1523,7 +1964,7 @@ int lx_device_planes(lx_index *h, void **hb, void **la, uint32_t *stride, void *
 
 int lx_sync(lx_index *h) {
     if (!h) return LX_ERR_ARG;
-    HIPCHK(h, hipSetDevice(h->device));
+    HIPCHK(h, set_dev(h->device));
     HIPCHK(h, hipStreamSynchronize(h->stream));
     uint32_t bad = 0;
     HIPCHK(h, hipMemcpy(&bad, h->status + 1, 4, hipMemcpyDeviceToHost));

@@ -205,6 +205,42 @@ struct TailArgs {
     uint32_t tcap;
 };
 
+// ---- small-batch (latency) path (lx_small.hip): the host assigns branches in
+// Add order (vecengine/index.go:105-141, exactly the reference's lastSeq rule)
+// and stages the batch; one launch writes the metadata and computes HB + LA.
+// Per event: 3 x uint4
+//   q0 = {branch, seq, prev (previous event of the branch, global; NONE when the
+//         event opens its branch), number of parents}
+//   q1 = {parent offset (into par), first seq of the branch, self-parent (global
+//         or NONE), branches before Add}
+//   q2 = {creator, flags (kSmallCont: continues its branch), final first_child
+//         of this event (its continuing self-child in the batch, or NONE), 0}
+constexpr uint32_t kSmallCont = 1u;
+constexpr uint32_t kSmallCW = 4;     // columns per workgroup (256 threads = 4 columns x 64 event lanes)
+constexpr uint32_t kSmallMaxN = 3072;   // events per small batch (LDS: n x (kSmallCW + 1) x 4 B <= 64 KB)
+struct SmallEv {
+    uint4 q0, q1, q2;
+};
+struct SmallArgs {
+    uint32_t *hb, *la;
+    uint64_t stride;
+    uint32_t bs, n;              // first global index, events
+    uint32_t B0, B;              // branches before / after the batch
+    const SmallEv *ev;
+    const uint32_t *par;         // parents (global), by q1.x
+    const uint32_t *perm;        // batch positions ordered by level
+    const uint32_t *lvl_off;     // n_levels + 1 offsets into perm
+    uint32_t n_levels;
+    const uint32_t *new_first;   // first seq of branches B0 .. B-1
+    const uint32_t *new_creator;
+    const uint32_t *blen;        // (branch, events on it) pairs of the branches the batch touched
+    uint32_t n_blen;
+    uint32_t *ev_creator, *ev_seq, *ev_branch, *ev_bbefore, *ev_sp, *first_child, *first_root;
+    uint32_t *branch_first, *branch_creator, *branch_len, *brow;
+    uint32_t s_cap;
+    uint32_t mask;               // rows may carry fork marks (B > V)
+};
+
 // ---- write-back to the reference's byte formats (lx_persist.hip)
 struct RowsArgs {
     const uint32_t *plane;       // hb or la
@@ -216,6 +252,26 @@ struct RowsArgs {
     const uint32_t *ev_branch;
     const uint32_t *branch_first;
     uint32_t hb;                 // 1: HighestBefore (8 B per branch), 0: LowestAfter (4 B)
+};
+
+// batched getters (k_get_rows): mode 0 HighestBefore, 1 LowestAfter, 2 merged HighestBefore
+struct GetArgs {
+    const uint32_t *plane;       // hb (modes 0, 2) or la (mode 1)
+    uint64_t stride;
+    const uint32_t *ev;          // events (device-visible)
+    uint32_t n;
+    uint32_t B, V;
+    uint32_t mode;
+    uint32_t forks;              // B > V
+    const uint32_t *ev_bbefore;
+    const uint32_t *ev_branch;
+    const uint32_t *branch_first;
+    const int32_t *cheat_of;     // creator -> cheater index (-1: one branch)
+    const uint32_t *cheat_off;   // CSR over all branches of each cheater (original first)
+    const uint32_t *cheat_br;
+    uint8_t *out;                // row i at out + i * slot
+    uint64_t slot;
+    uint32_t *len;               // byte length of row i
 };
 
 // ---- emitter QuorumIndexer (lx_emitter.hip, lx_emitter.cpp)
@@ -299,7 +355,8 @@ struct VoteArgs {
 // kernel launchers (lx_kernels.hip); all enqueue on `s`
 namespace lx {
 hipError_t launch_batch_prepare(const BatchArgs &a, void *scan_tmp, size_t scan_tmp_bytes, hipStream_t s);
-hipError_t launch_batch_finish(const BatchArgs &a, hipStream_t s);
+hipError_t launch_batch_finish(const BatchArgs &a, uint32_t jump_rounds, hipStream_t s);
+hipError_t launch_small(const SmallArgs &a, hipStream_t s);
 hipError_t scan_tmp_bytes(uint32_t n, size_t *bytes);
 hipError_t launch_undo_claims(const BatchArgs &a, hipStream_t s);
 hipError_t launch_index(const IndexArgs &a, hipStream_t s);
@@ -307,6 +364,7 @@ hipError_t launch_marks(const MarkArgs &a, hipStream_t s);
 hipError_t launch_fc(const FcArgs &a, uint32_t cols, bool forks, hipStream_t s);
 hipError_t launch_fc_combine(const uint32_t *sum, uint8_t *out, uint64_t n, uint32_t quorum, hipStream_t s);
 hipError_t launch_unfill(const UnfillArgs &a, hipStream_t s);
+hipError_t launch_zero_rows(uint32_t *hb, uint32_t *la, uint64_t stride, uint32_t lo, uint32_t hi, hipStream_t s);
 hipError_t launch_la_tail(const TailArgs &a, hipStream_t s);
 hipError_t launch_fill_u32(uint32_t *p, uint64_t n, uint32_t v, hipStream_t s);
 hipError_t launch_shard_rows(const uint32_t *ev_branch, const uint32_t *branch_creator, uint32_t n, uint32_t lo,
@@ -321,6 +379,7 @@ hipError_t launch_iota(uint32_t *rows, uint32_t lo, uint32_t n, hipStream_t s);
 hipError_t launch_row_offsets(const RowsArgs &a, uint64_t *len, uint64_t *off, void *tmp, size_t tmp_bytes,
                               hipStream_t s);
 hipError_t launch_encode_rows(const RowsArgs &a, const uint64_t *off, uint64_t base, uint32_t *out, hipStream_t s);
+hipError_t launch_get_rows(const GetArgs &a, hipStream_t s);
 hipError_t launch_gather_u32(const uint32_t *src, const uint32_t *idx, uint32_t n, uint32_t *dst, hipStream_t s);
 hipError_t launch_qi_update(const QiArgs &a, const uint32_t *ev, const uint32_t *target, uint32_t n, hipStream_t s);
 hipError_t launch_qi_median(const QiArgs &a, hipStream_t s);

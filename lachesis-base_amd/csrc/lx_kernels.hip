@@ -36,24 +36,20 @@ __device__ __forceinline__ uint32_t ld_l2_now(const uint32_t *p) {
 }
 
 // ---------------------------------------------------------------------------- batch prepare
-__global__ void k_meta(BatchArgs a, unsigned long long *err) {
-    uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= a.n) return;
-    uint32_t g = a.batch_start + e;
-    uint32_t s = a.seq[e];
-    a.ev_creator[g] = a.creator[e];
-    a.ev_seq[g] = s;
-    a.first_child[g] = LX_NONE;
-    atomicMax(&a.status[2], s);
-}
-
-// eventcheck invariants the index relies on (parentscheck/parents_check.go:25-63,
-// basiccheck/basic_check.go:24-44) and claims of "first self-child" / "first root".
+// Per-event metadata, eventcheck invariants the index relies on
+// (parentscheck/parents_check.go:25-63, basiccheck/basic_check.go:24-44) and
+// claims of "first self-child" / "first root".  An in-batch self-parent's
+// creator and seq come from the batch inputs (the metadata of this launch's
+// other threads is not visible yet).  first_child of rows not yet added is
+// always NONE (reset, growth and rollback keep it so): claims land on it.
 __global__ void k_validate_claim(BatchArgs a, unsigned long long *err) {
     uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= a.n) return;
     uint32_t g = a.batch_start + e;
     uint32_t c = a.creator[e], s = a.seq[e];
+    a.ev_creator[g] = c;
+    a.ev_seq[g] = s;
+    atomicMax(&a.status[2], s);
     uint32_t p0 = a.poff[e], p1 = a.poff[e + 1];
     uint32_t code = 0;
     if (c >= a.V) {
@@ -69,8 +65,11 @@ __global__ void k_validate_claim(BatchArgs a, unsigned long long *err) {
             if (p1 == p0) {
                 code = E_EVENT;
             } else {
-                uint32_t sp = a.par[p0];
-                if (a.ev_creator[sp] != c || a.ev_seq[sp] + 1 != s) code = E_EVENT;
+                const uint32_t sp = a.par[p0];
+                const bool in = sp >= a.batch_start;
+                const uint32_t cs = in ? a.creator[sp - a.batch_start] : a.ev_creator[sp];
+                const uint32_t ss = in ? a.seq[sp - a.batch_start] : a.ev_seq[sp];
+                if (cs != c || ss + 1 != s) code = E_EVENT;
             }
         }
     }
@@ -118,7 +117,6 @@ static inline uint32_t nblk(uint64_t n, uint32_t t) { return (uint32_t)((n + t -
 
 hipError_t launch_batch_prepare(const BatchArgs &a, void *scan_tmp, size_t scan_tmp_bytes, hipStream_t s) {
     unsigned long long *err = (unsigned long long *)(a.status + 8);
-    hipLaunchKernelGGL(k_meta, dim3(nblk(a.n, 256)), dim3(256), 0, s, a, err);
     hipLaunchKernelGGL(k_validate_claim, dim3(nblk(a.n, 256)), dim3(256), 0, s, a, err);
     hipLaunchKernelGGL(k_isfork, dim3(nblk(a.n, 256)), dim3(256), 0, s, a);
     size_t tb = scan_tmp_bytes;
@@ -184,6 +182,10 @@ __global__ void k_finalize(BatchArgs a) {
     uint32_t g = a.batch_start + e;
     uint32_t br = a.tmp_br[e];
     uint32_t s = a.seq[e];
+    if (br == LX_NONE) {   // too few jump rounds: reported by the host, nothing written
+        atomicAdd(&a.status[4], 1u);
+        return;
+    }
     a.ev_branch[g] = br;
     uint32_t first = a.branch_first[br];
     a.brow[(uint64_t)br * a.s_cap + (s - first)] = g;
@@ -219,9 +221,10 @@ __global__ void k_finalize(BatchArgs a) {
     }
 }
 
-hipError_t launch_batch_finish(const BatchArgs &a, hipStream_t s) {
+hipError_t launch_batch_finish(const BatchArgs &a, uint32_t jump_rounds, hipStream_t s) {
     hipLaunchKernelGGL(k_assign, dim3(nblk(a.n, 256)), dim3(256), 0, s, a);
-    for (uint32_t r = 0; r < 32; r++) hipLaunchKernelGGL(k_jump, dim3(nblk(a.n, 256)), dim3(256), 0, s, a, r);
+    jump_rounds = std::min<uint32_t>(jump_rounds, 32);
+    for (uint32_t r = 0; r < jump_rounds; r++) hipLaunchKernelGGL(k_jump, dim3(nblk(a.n, 256)), dim3(256), 0, s, a, r);
     hipLaunchKernelGGL(k_finalize, dim3(nblk(a.n, 256)), dim3(256), 0, s, a);
     return hipGetLastError();
 }
@@ -1094,10 +1097,15 @@ hipError_t launch_fc_combine(const uint32_t *sum, uint8_t *out, uint64_t n, uint
 // ---------------------------------------------------------------------------- rollback
 // Zero exactly the LowestAfter entries the dropped events filled: the same
 // ranges (h0, h1] as k_index, recomputed from the still-intact HB rows.
+__device__ void unclaim_one(const UnfillArgs &a, uint32_t e);
+
 __global__ void k_unfill(UnfillArgs a) {
     uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint64_t total = (uint64_t)(a.hi - a.lo) * a.B;
     if (t >= total) return;
+    // claims and branch lengths of the dropped events (no other thread of this
+    // launch reads what this writes)
+    if (t < a.hi - a.lo) unclaim_one(a, a.lo + (uint32_t)t);
     uint32_t e = a.lo + (uint32_t)(t / a.B);
     uint32_t c = (uint32_t)(t % a.B);
     const uint32_t pcol = a.cmap ? a.cmap[c] : c;
@@ -1118,9 +1126,7 @@ __global__ void k_unfill(UnfillArgs a) {
     }
 }
 
-__global__ void k_unclaim(UnfillArgs a) {
-    uint32_t e = a.lo + blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= a.hi) return;
+__device__ void unclaim_one(const UnfillArgs &a, uint32_t e) {
     uint32_t sp = a.ev_sp[e];
     uint32_t br = a.ev_branch[e];
     uint32_t s = a.ev_seq[e];
@@ -1135,11 +1141,27 @@ __global__ void k_unclaim(UnfillArgs a) {
     if (br < a.B_keep) atomicMin(&a.branch_len[br], s - a.branch_first[br]);
 }
 
+// the dropped rows [lo, hi) of both planes, zeroed after k_unfill has read them
+__global__ void k_zero_rows(uint4 *hb, uint4 *la, uint64_t n16) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * blockDim.x) {
+        hb[i] = make_uint4(0, 0, 0, 0);
+        la[i] = make_uint4(0, 0, 0, 0);
+    }
+}
+
 hipError_t launch_unfill(const UnfillArgs &a, hipStream_t s) {
     if (a.hi <= a.lo) return hipSuccess;
     uint64_t total = (uint64_t)(a.hi - a.lo) * a.B;
     hipLaunchKernelGGL(k_unfill, dim3((uint32_t)((total + 255) / 256)), dim3(256), 0, s, a);
-    hipLaunchKernelGGL(k_unclaim, dim3(nblk(a.hi - a.lo, 256)), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_zero_rows(uint32_t *hb, uint32_t *la, uint64_t stride, uint32_t lo, uint32_t hi, hipStream_t s) {
+    if (hi <= lo) return hipSuccess;
+    const uint64_t n16 = (uint64_t)(hi - lo) * stride / 4;   // stride: a multiple of 16 words
+    const uint32_t grid = (uint32_t)std::min<uint64_t>((n16 + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_zero_rows, dim3(grid), dim3(256), 0, s, reinterpret_cast<uint4 *>(hb + (uint64_t)lo * stride),
+                       reinterpret_cast<uint4 *>(la + (uint64_t)lo * stride), n16);
     return hipGetLastError();
 }
 

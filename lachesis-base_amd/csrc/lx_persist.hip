@@ -136,4 +136,69 @@ hipError_t launch_encode_rows(const RowsArgs &a, const uint64_t *off, uint64_t b
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------- getters
+// GetHighestBefore / GetLowestAfter (vecfc/store_vectors.go:26-51) and
+// GetMergedHighestBefore (vecengine/index.go:235-250 with GatherFrom,
+// vecfc/vector_ops.go:81-96) for a batch of events, encoded on the device in the
+// reference byte layout: one wave per event, row i written at out + i * slot
+// (pinned host memory: one launch, no copies), its byte length in len[i].
+// Merged with forks: per creator the first fork-marked branch wins ({0,
+// MaxInt32}), else the strictly greatest Seq (first max wins) with its MinSeq
+// (the branch's first seq), else {0, 0}; 8 x V bytes.  Without forks the
+// reference returns the raw HighestBefore row.
+__global__ __launch_bounds__(256) void k_get_rows(GetArgs a) {
+    const uint32_t i = blockIdx.x * 4 + threadIdx.x / 64, lane = threadIdx.x % 64;
+    if (i >= a.n) return;
+    const uint32_t e = a.ev[i];
+    const uint32_t *row = a.plane + (uint64_t)e * a.stride;
+    uint32_t *o = reinterpret_cast<uint32_t *>(a.out + (uint64_t)i * a.slot);
+    if (a.mode == 2 && a.forks) {
+        for (uint32_t c = lane; c < a.V; c += 64) {
+            uint2 x = make_uint2(0u, 0u);
+            const int32_t k = a.cheat_of[c];
+            if (k < 0) {
+                const uint32_t v = row[c];
+                if (v) x = make_uint2(v & LX_SEQ_MASK, a.branch_first[c]);
+            } else {
+                for (uint32_t j = a.cheat_off[k]; j < a.cheat_off[k + 1]; j++) {
+                    const uint32_t b = a.cheat_br[j];
+                    const uint32_t v = row[b];
+                    if (v & LX_MARK) { x = make_uint2(0u, 0x7FFFFFFFu); break; }
+                    if (v > x.x) x = make_uint2(v, a.branch_first[b]);
+                }
+            }
+            *reinterpret_cast<uint2 *>(o + 2 * c) = x;
+        }
+        if (lane == 0) a.len[i] = 8u * a.V;
+        return;
+    }
+    const bool hb = a.mode != 1;
+    const uint32_t bb = a.ev_bbefore[e];
+    const uint32_t lim = hb ? bb + (a.ev_branch[e] == bb ? 1u : 0u) : a.B;
+    int last = -1;
+    for (uint32_t c = lane; c < lim; c += 64)
+        if (row[c]) last = (int)c;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) last = max(last, __shfl_xor(last, off, 64));
+    const uint32_t ent = max(bb, (uint32_t)(last + 1));
+    if (hb) {
+        for (uint32_t c = lane; c < ent; c += 64) {
+            const uint32_t v = c < lim ? row[c] : 0u;
+            uint2 x = make_uint2(0u, 0u);
+            if (v & LX_MARK) x.y = 0x7FFFFFFFu;
+            else if (v) x = make_uint2(v, a.branch_first[c]);
+            *reinterpret_cast<uint2 *>(o + 2 * c) = x;
+        }
+    } else {
+        for (uint32_t c = lane; c < ent; c += 64) o[c] = row[c];
+    }
+    if (lane == 0) a.len[i] = ent * (hb ? 8u : 4u);
+}
+
+hipError_t launch_get_rows(const GetArgs &a, hipStream_t s) {
+    if (!a.n) return hipSuccess;
+    hipLaunchKernelGGL(k_get_rows, dim3(nblk_p(a.n, 4)), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
 }  // namespace lx

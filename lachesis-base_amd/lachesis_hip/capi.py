@@ -37,6 +37,9 @@ SIGNATURES = [
     ("lx_get_highest_before", ctypes.c_int, [vp, ctypes.c_uint32, u8p, ctypes.c_uint32, u32p]),
     ("lx_get_lowest_after", ctypes.c_int, [vp, ctypes.c_uint32, u8p, ctypes.c_uint32, u32p]),
     ("lx_get_merged_highest_before", ctypes.c_int, [vp, ctypes.c_uint32, u8p, ctypes.c_uint32, u32p]),
+    ("lx_get_highest_before_batch", ctypes.c_int, [vp, ctypes.c_uint32, u32p, u64p, u8p, ctypes.c_uint64]),
+    ("lx_get_lowest_after_batch", ctypes.c_int, [vp, ctypes.c_uint32, u32p, u64p, u8p, ctypes.c_uint64]),
+    ("lx_get_merged_highest_before_batch", ctypes.c_int, [vp, ctypes.c_uint32, u32p, u64p, u8p, ctypes.c_uint64]),
     ("lx_get_event_branch_id", ctypes.c_int, [vp, ctypes.c_uint32, u32p]),
     ("lx_get_branches_info", ctypes.c_int, [vp, u32p, u32p, ctypes.c_uint32, u32p]),
     ("lx_shard_of", ctypes.c_int, [vp, u32p, u32p]),
@@ -282,6 +285,25 @@ class Index:
 
     def merged_highest_before(self, ev):
         return self._bytes(self.L.lx_get_merged_highest_before, ev)
+
+    def _rows(self, f, evs):
+        evs = _u32(evs)
+        n = len(evs)
+        off = np.zeros(n + 1, dtype=np.uint64)
+        buf = np.zeros(max(8 * n * self.num_branches(), 1), dtype=np.uint8)   # >= every row (B >= V)
+        self._chk(f(self.h, n, _p(evs, u32p), _p(off, u64p), _p(buf, u8p), len(buf)))
+        b = buf.tobytes()
+        return [b[off[i]:off[i + 1]] for i in range(n)]
+
+    def highest_before_batch(self, evs):
+        """lx_get_highest_before_batch: list of byte rows."""
+        return self._rows(self.L.lx_get_highest_before_batch, evs)
+
+    def lowest_after_batch(self, evs):
+        return self._rows(self.L.lx_get_lowest_after_batch, evs)
+
+    def merged_highest_before_batch(self, evs):
+        return self._rows(self.L.lx_get_merged_highest_before_batch, evs)
 
     def branch(self, ev):
         out = ctypes.c_uint32()

@@ -1,0 +1,321 @@
+// lx_latency.cpp -- per-call latency and antichain-fed throughput of the C ABI,
+// driven from native code the way the cgo shim drives it (bench tooling, not
+// part of the index library).
+//
+// The reference's callers use the index one event / one pair at a time:
+//   IndexedLachesis.Process: Add(e), ..., Flush            (abft/indexed_lachesis.go:69-82)
+//   IndexedLachesis.Build:   Add(e), ..., DropNotFlushed   (abft/indexed_lachesis.go:53-63)
+//   calcFrameIdx: ForklessCause(e, root) per root          (abft/event_processing.go:149-161)
+//   applyAtropos / emitter: GetMergedHighestBefore(id)     (abft/lachesis.go:57)
+// lx_bench_latency times those calls (wall clock around each C call; p50 / p99
+// / mean in microseconds) on a history-indexed epoch of the given DAG, then the
+// throughput of feeding the DAG antichain by antichain: the events re-ordered
+// by topological level (a valid Add order) and each level added as one
+// lx_add_batch + lx_flush, directly and through the level batcher.
+#include <algorithm>
+#include <chrono>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/lachesis_batcher.h"
+#include "../../include/lachesis_hip.h"
+
+namespace {
+
+using clk = std::chrono::steady_clock;
+inline double us_since(clk::time_point t0) {
+    return std::chrono::duration<double, std::micro>(clk::now() - t0).count();
+}
+
+struct Stat {
+    double p50 = 0, p99 = 0, mean = 0;
+};
+Stat stat_of(std::vector<double> v) {
+    Stat s;
+    if (v.empty()) return s;
+    std::sort(v.begin(), v.end());
+    s.p50 = v[v.size() / 2];
+    s.p99 = v[std::min(v.size() - 1, (size_t)(v.size() * 0.99))];
+    double t = 0;
+    for (double x : v) t += x;
+    s.mean = t / v.size();
+    return s;
+}
+
+// the DAG re-ordered by topological level (stable inside a level), parents remapped
+struct Leveled {
+    std::vector<uint32_t> creator, seq, par;
+    std::vector<uint64_t> poff;
+    std::vector<uint64_t> lvl_off;   // event offsets of the levels
+};
+
+Leveled by_level(uint64_t N, const uint32_t *creator, const uint32_t *seq, const uint64_t *poff, const uint32_t *par) {
+    std::vector<uint32_t> lvl(N);
+    uint32_t maxl = 0;
+    for (uint64_t i = 0; i < N; i++) {
+        uint32_t l = 0;
+        for (uint64_t k = poff[i]; k < poff[i + 1]; k++) l = std::max(l, lvl[par[k]] + 1);
+        lvl[i] = l;
+        maxl = std::max(maxl, l);
+    }
+    std::vector<uint64_t> cnt(maxl + 2, 0);
+    for (uint64_t i = 0; i < N; i++) cnt[lvl[i] + 1]++;
+    for (uint32_t l = 0; l <= maxl; l++) cnt[l + 1] += cnt[l];
+    Leveled o;
+    o.lvl_off.assign(cnt.begin(), cnt.end());
+    std::vector<uint32_t> pos(N), order(N);
+    for (uint64_t i = 0; i < N; i++) {
+        pos[i] = (uint32_t)cnt[lvl[i]]++;
+        order[pos[i]] = (uint32_t)i;
+    }
+    o.creator.resize(N);
+    o.seq.resize(N);
+    o.poff.resize(N + 1);
+    o.par.reserve(poff[N]);
+    o.poff[0] = 0;
+    for (uint64_t j = 0; j < N; j++) {
+        const uint32_t i = order[j];
+        o.creator[j] = creator[i];
+        o.seq[j] = seq[i];
+        for (uint64_t k = poff[i]; k < poff[i + 1]; k++) o.par.push_back(pos[par[k]]);
+        o.poff[j + 1] = o.par.size();
+    }
+    return o;
+}
+
+}  // namespace
+
+extern "C" {
+
+// out receives kLatOut doubles: for each of the 11 call kinds p50, p99, mean (us):
+//   0 add n=1 (Process: Add + Flush; host call time, the launch is not waited for)
+//   1 add n=1 + lx_sync (completion)
+//   2 Build: add n=1 + DropNotFlushed + lx_sync
+//   3 one antichain (a level, ~V/(1.6 P) events) add + flush + lx_sync
+//   4 add n=1024 + lx_sync
+//   5 ForklessCause n=1        6 ForklessCause n=667 (~2/3 V: calcFrameIdx)
+//   7 GetHighestBefore         8 GetLowestAfter       9 GetMergedHighestBefore
+//  10 getter batch of 64 merged HB rows (lx_get_merged_highest_before_batch)
+// then [33] antichain-fed events/s (levels added directly), [34] events fed,
+// [35] levels fed, [36] batcher-fed events/s (push a level, pop, add, flush),
+// [37] mean events per level.
+int lx_bench_latency(int device, uint32_t V, const uint32_t *weights, uint64_t N, const uint32_t *creator,
+                     const uint32_t *seq, const uint64_t *poff, const uint32_t *par, uint64_t history,
+                     uint32_t reps, uint64_t feed_events, double *out, char *err, uint32_t err_cap) {
+    auto fail = [&](const char *what, lx_index *h) {
+        snprintf(err, err_cap, "%s: %s", what, h ? lx_last_error(h) : "");
+        if (h) lx_destroy(h);
+        return -1;
+    };
+    Leveled d = by_level(N, creator, seq, poff, par);
+    // history = whole levels
+    uint64_t L0 = 0;
+    while (L0 + 1 < d.lvl_off.size() && d.lvl_off[L0 + 1] <= history) L0++;
+    const uint64_t H = d.lvl_off[L0];
+    lx_config cfg{};
+    cfg.device = device;
+    cfg.event_capacity = std::min<uint64_t>(N, H + 2 * feed_events + 2ull * reps + 400000);
+    lx_index *h = nullptr;
+    if (lx_create(&cfg, &h)) return fail("lx_create", nullptr);
+    if (lx_reset(h, V, weights)) return fail("lx_reset", h);
+    if (H && lx_add_batch(h, (uint32_t)H, d.creator.data(), d.seq.data(), d.poff.data(), d.par.data(), nullptr, nullptr))
+        return fail("history", h);
+    lx_flush(h);
+    if (lx_sync(h)) return fail("sync", h);
+    uint64_t next = H;   // next event (level order) to add
+    uint64_t lv = L0;    // its level
+    auto add = [&](uint64_t lo, uint64_t hi) {
+        return lx_add_batch(h, (uint32_t)(hi - lo), d.creator.data() + lo, d.seq.data() + lo, d.poff.data() + lo,
+                            d.par.data(), nullptr, nullptr);
+    };
+    std::vector<double> t[11];
+    // 0/1: single events, Process pattern (async; then with completion)
+    for (int mode = 0; mode < 2; mode++) {
+        for (uint32_t r = 0; r < reps && next < N; r++, next++) {
+            auto t0 = clk::now();
+            if (add(next, next + 1)) return fail("add1", h);
+            lx_flush(h);
+            if (mode == 1 && lx_sync(h)) return fail("sync", h);
+            t[mode].push_back(us_since(t0));
+        }
+        if (lx_sync(h)) return fail("sync", h);
+    }
+    while (lv + 1 < d.lvl_off.size() && d.lvl_off[lv + 1] <= next) lv++;
+    // 2: Build pattern on the next event, repeated (each Build is rolled back)
+    for (uint32_t r = 0; r < reps; r++) {
+        auto t0 = clk::now();
+        if (add(next, next + 1)) return fail("build", h);
+        if (lx_drop_not_flushed(h)) return fail("drop", h);
+        if (lx_sync(h)) return fail("sync", h);
+        t[2].push_back(us_since(t0));
+    }
+    // 3: antichains: finish the current level, then whole levels
+    if (next < d.lvl_off[lv + 1]) {
+        if (add(next, d.lvl_off[lv + 1])) return fail("level", h);
+        lx_flush(h);
+        next = d.lvl_off[++lv];
+    }
+    const uint32_t lreps = std::max<uint32_t>(reps / 4, 50);
+    for (uint32_t r = 0; r < lreps && lv + 1 < d.lvl_off.size(); r++, lv++) {
+        auto t0 = clk::now();
+        if (add(d.lvl_off[lv], d.lvl_off[lv + 1])) return fail("level", h);
+        lx_flush(h);
+        if (lx_sync(h)) return fail("sync", h);
+        t[3].push_back(us_since(t0));
+        next = d.lvl_off[lv + 1];
+    }
+    // 4: 1024-event batches (continuing in level order)
+    for (uint32_t r = 0; r < std::max<uint32_t>(reps / 20, 20) && next + 1024 <= N; r++) {
+        auto t0 = clk::now();
+        if (add(next, next + 1024)) return fail("add1024", h);
+        lx_flush(h);
+        if (lx_sync(h)) return fail("sync", h);
+        t[4].push_back(us_since(t0));
+        next += 1024;
+    }
+    while (lv + 1 < d.lvl_off.size() && d.lvl_off[lv + 1] <= next) lv++;
+    if (next < d.lvl_off[lv + 1] && lv + 1 < d.lvl_off.size()) {   // realign to a level boundary
+        if (add(next, d.lvl_off[lv + 1])) return fail("level", h);
+        lx_flush(h);
+        next = d.lvl_off[++lv];
+    }
+    // 5-10: queries over the indexed events (a among the newest, b anywhere older)
+    uint64_t rs = 0x9E3779B97F4A7C15ull;
+    auto rnd = [&](uint64_t m) {
+        rs ^= rs << 13;
+        rs ^= rs >> 7;
+        rs ^= rs << 17;
+        return rs % m;
+    };
+    std::vector<uint32_t> qa(667), qb(667);
+    std::vector<uint8_t> qo(667);
+    for (int kind = 5; kind <= 6; kind++) {
+        const uint32_t n = kind == 5 ? 1 : 667;
+        for (uint32_t r = 0; r < reps; r++) {
+            for (uint32_t i = 0; i < n; i++) {
+                qa[i] = (uint32_t)(next - 1 - rnd(std::min<uint64_t>(next, 5000)));
+                qb[i] = (uint32_t)rnd(next);
+            }
+            auto t0 = clk::now();
+            if (lx_forkless_cause_batch(h, n, qa.data(), qb.data(), qo.data())) return fail("fc", h);
+            t[kind].push_back(us_since(t0));
+        }
+    }
+    std::vector<uint8_t> row(16 * (V + 4096));
+    for (int kind = 7; kind <= 9; kind++) {
+        for (uint32_t r = 0; r < reps; r++) {
+            const uint32_t ev = (uint32_t)(next - 1 - rnd(std::min<uint64_t>(next, 5000)));
+            uint32_t len = 0;
+            auto t0 = clk::now();
+            int rc = kind == 7   ? lx_get_highest_before(h, ev, row.data(), (uint32_t)row.size(), &len)
+                     : kind == 8 ? lx_get_lowest_after(h, ev, row.data(), (uint32_t)row.size(), &len)
+                                 : lx_get_merged_highest_before(h, ev, row.data(), (uint32_t)row.size(), &len);
+            if (rc) return fail("getter", h);
+            t[kind].push_back(us_since(t0));
+        }
+    }
+    {
+        std::vector<uint32_t> evs(64);
+        std::vector<uint64_t> off(65);
+        std::vector<uint8_t> buf(64ull * 8 * V);
+        for (uint32_t r = 0; r < reps / 4 + 1; r++) {
+            for (auto &e : evs) e = (uint32_t)(next - 1 - rnd(std::min<uint64_t>(next, 5000)));
+            auto t0 = clk::now();
+            if (lx_get_merged_highest_before_batch(h, 64, evs.data(), off.data(), buf.data(), buf.size()))
+                return fail("getter batch", h);
+            t[10].push_back(us_since(t0));
+        }
+    }
+    for (int k = 0; k < 11; k++) {
+        Stat s = stat_of(t[k]);
+        out[3 * k] = s.p50;
+        out[3 * k + 1] = s.p99;
+        out[3 * k + 2] = s.mean;
+    }
+    // antichain-fed throughput: levels as batches, Add + Flush each, one sync at the end
+    {
+        const uint64_t lv0 = lv, e0 = next;
+        auto t0 = clk::now();
+        while (lv + 1 < d.lvl_off.size() && d.lvl_off[lv + 1] - e0 <= feed_events) {
+            if (add(d.lvl_off[lv], d.lvl_off[lv + 1])) return fail("feed", h);
+            lx_flush(h);
+            lv++;
+        }
+        if (lx_sync(h)) return fail("sync", h);
+        const double s = us_since(t0) * 1e-6;
+        next = d.lvl_off[lv];
+        out[33] = (next - e0) / s;
+        out[34] = (double)(next - e0);
+        out[35] = (double)(lv - lv0);
+        out[37] = (double)(next - e0) / std::max<double>(1, lv - lv0);
+    }
+    // batcher-fed: each level pushed by id, popped (parents-first release) and added
+    {
+        lx_batcher *b = nullptr;
+        if (lx_batcher_create(&b)) return fail("batcher", h);
+        // the batcher's dense indices must continue the epoch: replay the indexed
+        // prefix as released events (pushed and popped without adding)
+        std::vector<uint64_t> ids, pids, po;
+        auto push_range = [&](uint64_t lo, uint64_t hi) {
+            ids.resize(hi - lo);
+            po.assign(1, 0);
+            pids.clear();
+            for (uint64_t i = lo; i < hi; i++) {
+                ids[i - lo] = i + 1;
+                for (uint64_t k = d.poff[i]; k < d.poff[i + 1]; k++) pids.push_back((uint64_t)d.par[k] + 1);
+                po.push_back(pids.size());
+            }
+            return lx_batcher_push(b, (uint32_t)(hi - lo), ids.data(), d.creator.data() + lo, d.seq.data() + lo,
+                                   po.data(), pids.data(), nullptr);
+        };
+        std::vector<uint64_t> oid, opo;
+        std::vector<uint32_t> ocr, osq, opar, olv;
+        auto pop = [&](uint32_t *n_out) {
+            uint32_t ne = 0, nl = 0, nw = 0;
+            uint64_t npar = 0;
+            if (lx_batcher_peek(b, &ne, &npar, &nl, &nw)) return -1;
+            oid.resize(ne + 1);
+            ocr.resize(ne + 1);
+            osq.resize(ne + 1);
+            opo.resize(ne + 1);
+            opar.resize(npar + 1);
+            olv.resize(nl + 1);
+            *n_out = ne;
+            return lx_batcher_pop(b, oid.data(), ocr.data(), osq.data(), opo.data(), opar.data(), olv.data(), nullptr);
+        };
+        uint32_t ne = 0;
+        if (push_range(0, next) || pop(&ne) || ne != next) {
+            lx_batcher_destroy(b);
+            return fail("batcher replay", h);
+        }
+        const uint64_t lv0 = lv, e0 = next;
+        auto t0 = clk::now();
+        while (lv + 1 < d.lvl_off.size() && d.lvl_off[lv + 1] - e0 <= feed_events) {
+            if (push_range(d.lvl_off[lv], d.lvl_off[lv + 1]) || pop(&ne)) {
+                lx_batcher_destroy(b);
+                return fail("batcher feed", h);
+            }
+            if (ne && lx_add_batch(h, ne, ocr.data(), osq.data(), opo.data(), opar.data(), nullptr, nullptr)) {
+                lx_batcher_destroy(b);
+                return fail("batcher add", h);
+            }
+            lx_flush(h);
+            lv++;
+        }
+        if (lx_sync(h)) {
+            lx_batcher_destroy(b);
+            return fail("sync", h);
+        }
+        const double s = us_since(t0) * 1e-6;
+        out[36] = (d.lvl_off[lv] - e0) / s;
+        lx_batcher_destroy(b);
+    }
+    lx_destroy(h);
+    (void)lv;
+    return 0;
+}
+
+}  // extern "C"

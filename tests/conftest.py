@@ -13,6 +13,7 @@ for p in (ROOT, PKG, os.path.join(ROOT, "tests")):
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs under gpurun)")
     config.addinivalue_line("markers", "slow: long CPU test")
+    config.addinivalue_line("markers", "big_only: GPU parity test whose batches all exceed the small-batch path")
 
 
 @pytest.fixture(scope="session")

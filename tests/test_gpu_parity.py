@@ -20,6 +20,19 @@ def lx():
     return lachesis_hip
 
 
+@pytest.fixture(params=["small", "big"], autouse=True)
+def add_path(request, monkeypatch):
+    """Every test runs twice: host-pointer batches of <= 3072 events take the
+    small-batch path (host branch assignment + k_small, lx_small.hip) by
+    default; LX_SMALL_MAX=0 (read by lx_create) sends every batch through the
+    device-assigned walker path (k_index)."""
+    if request.param == "big":
+        monkeypatch.setenv("LX_SMALL_MAX", "0")
+    elif request.node.get_closest_marker("big_only"):
+        pytest.skip("every batch of this test is larger than the small path takes")
+    return request.param
+
+
 def oracle_for(dag, weights, flush_each=False):
     o = corc.OracleIndex(weights)
     r = o.add_batch(dag.creator, dag.seq, dag.poff, dag.par, flush_each=flush_each)
@@ -316,6 +329,7 @@ def test_config3_shape_skewed(lx):
     np.testing.assert_array_equal(ix.forkless_cause_batch(qa, qb), o.forkless_cause_batch(qa, qb))
 
 
+@pytest.mark.big_only
 def test_full_size_config3_prefix_vs_oracle(lx):
     """BASELINE configs[2] at full size (V=1000, Zipf stakes, 10M events, one
     batch -- the bench workload) against the C oracle on the first 120k events:
@@ -347,6 +361,7 @@ def test_full_size_config3_prefix_vs_oracle(lx):
     ix.close()
 
 
+@pytest.mark.big_only
 def test_full_size_properties_config2(lx):
     """BASELINE configs[1] at full size (V=100, 1M events): size-independent
     properties.  (i) HB of an event on branch j at seq s equals s on column j;
@@ -404,6 +419,7 @@ WALKER_VARIANTS = [
 ]
 
 
+@pytest.mark.big_only
 @pytest.mark.parametrize("env", WALKER_VARIANTS, ids=lambda e: "-".join("%s%s" % (k[3:].lower(), v) for k, v in e.items()))
 def test_walker_variants(lx, env, monkeypatch):
     """Every walker configuration (slot layouts, ring sizes, wave counts) is bit-exact;
