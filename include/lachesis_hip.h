@@ -104,9 +104,7 @@ int lx_drop_not_flushed(lx_index *h);
  * pointer may be NULL to skip that part; offsets have n+1 entries, in bytes).
  * lx_flush then commits.  Adding, dropping, flushing or resetting in between
  * invalidates the prepared set (LX_ERR_STATE).  Unsharded handles only.
- * Restart: replay the persisted epoch (lx_reset + lx_add_batch in the stored
- * Add order); a write-back prepared right after the replay equals the
- * persisted tables byte for byte. */
+ * Restart: lx_load_rows / lx_load_finish below. */
 typedef struct lx_writeback {
     uint64_t first_event, n_events;   /* rows of tables S and b */
     uint64_t n_la_rows;               /* rows of table s */
@@ -116,6 +114,29 @@ typedef struct lx_writeback {
 int lx_writeback_prepare(lx_index *h, lx_writeback *out);
 int lx_writeback_fetch(lx_index *h, uint64_t *hb_off, uint8_t *hb_bytes, uint32_t *la_ev, uint64_t *la_off,
                        uint8_t *la_bytes, uint8_t *branch_be, uint8_t *bi_rlp);
+
+/* Restart from the persisted tables without replay (abft/restart_test.go:156-188
+ * rebuilds a fresh index over a copy of the epoch DB; vecengine/index.go:56-68
+ * Reset + the lazy reads of vecfc/store_vectors.go:26-51 and
+ * vecengine/store_branches_info.go:57-88).  After lx_reset(V, weights):
+ *   lx_load_rows(...)  any number of times: the epoch's events in a parents-first
+ *                      order the caller chooses (dense indices continue: 0, 1, ...);
+ *                      per event its creator idx, seq, parents (self-parent
+ *                      first), table "b" value (4-B big-endian branch ID) and
+ *                      the bytes of tables "S" (HighestBefore) and "s"
+ *                      (LowestAfter); hb_off / la_off have n+1 absolute byte
+ *                      offsets into hb_bytes / la_bytes;
+ *   lx_load_finish(table "B" key "c": RLP(BranchesInfo)).
+ * The loaded epoch counts as flushed; Add, ForklessCause and the getters then
+ * continue exactly as in the reference after its restart.  Tables that do not
+ * form one consistent epoch (branch chains, creators, byte lengths, MinSeq,
+ * LastSeq, BranchesInfo, fork markers the vectors do not imply) return
+ * LX_ERR_STATE ("inconsistent DB", the reference's crit) and leave the handle
+ * needing lx_reset.  Unsharded handles only. */
+int lx_load_rows(lx_index *h, uint32_t n, const uint32_t *creator_idx, const uint32_t *seq,
+                 const uint64_t *parent_off, const uint32_t *parent_idx, const uint8_t *branch_be,
+                 const uint64_t *hb_off, const uint8_t *hb_bytes, const uint64_t *la_off, const uint8_t *la_bytes);
+int lx_load_finish(lx_index *h, const uint8_t *bi_rlp, uint32_t bi_len);
 
 uint64_t lx_num_events(const lx_index *h);
 uint32_t lx_num_branches(const lx_index *h);           /* len(BranchIDCreatorIdxs) */

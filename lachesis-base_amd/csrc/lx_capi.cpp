@@ -19,7 +19,7 @@
 namespace {
 
 constexpr uint32_t kStatusWords = 64;   // [1] fc bad flag, [2] max seq, [3] pinned-FC sink, [4] unresolved
-                                        // branch, [8..9] batch error u64, [16..47] jump flags
+                                        // branch, [5] load check flags, [8..9] batch error u64, [16..47] jump flags
 
 template <typename T>
 hipError_t dalloc(T **p, uint64_t n) {
@@ -147,6 +147,15 @@ struct lx_index {
     uint32_t st_next = 0;
     uint32_t *st_dev = nullptr;            // device image (stream order serialises its reuse)
     uint64_t st_dev_cap = 0;
+    // restart from the persisted tables (lx_load_rows / lx_load_finish)
+    bool loading = false;
+    std::vector<uint32_t> ld_first, ld_last, ld_count, ld_creator, ld_tail;   // per branch, as loaded
+    std::vector<uint32_t> ld_par;          // parents of every loaded event (dense)
+    std::vector<uint64_t> ld_poff;
+    uint32_t ld_B = 0;                     // branches seen so far (max ID + 1)
+    uint8_t *ld_buf = nullptr;             // device staging of a chunk's bytes and offsets
+    uint64_t ld_buf_cap = 0;
+
     // pinned, device-mapped query buffers (per-call ForklessCause, getters)
     uint8_t *qp = nullptr;
     uint64_t qp_cap = 0;
@@ -548,6 +557,7 @@ BatchArgs batch_args(lx_index *h, uint32_t n, const uint32_t *creator, const uin
 int add_batch_dev(lx_index *h, uint32_t n, const uint32_t *creator, const uint32_t *seq, const uint32_t *poff,
                   const uint32_t *par, uint32_t *err_index) {
     if (!h->have_epoch) return h->fail(LX_ERR_STATE, "lx_add_batch before lx_reset");
+    if (h->loading) return h->fail(LX_ERR_STATE, "lx_add_batch during a load (lx_load_finish first)");
     if (n == 0) return 0;
     h->wb_ready = false;
     if (h->n_events + n >= 0xFFFFFFF0ull) return h->fail(LX_ERR_ARG, "too many events in one epoch");
@@ -1323,6 +1333,7 @@ void lx_destroy(lx_index *h) {
         if (p) (void)hipHostFree(p);
     if (h->st_dev) (void)hipFree(h->st_dev);
     if (h->qp) (void)hipHostFree(h->qp);
+    if (h->ld_buf) (void)hipFree(h->ld_buf);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
 }
@@ -1429,6 +1440,7 @@ int lx_reset(lx_index *h, uint32_t nv, const uint32_t *w) {
     for (auto *v : {&h->hm_creator, &h->hm_seq, &h->hm_branch, &h->hm_bbefore}) v->clear();
     h->hm_blen.assign(nv, 0);
     h->stats_lazy = false;
+    h->loading = false;
     h->have_epoch = true;
     h->ncols = 0;
     return rebuild_columns(h);
@@ -1448,6 +1460,7 @@ int lx_add_batch(lx_index *h, uint32_t n, const uint32_t *creator, const uint32_
         off[i] = (uint32_t)(poff[i] - base);
     }
     int rc;
+    if (h->loading) return h->fail(LX_ERR_STATE, "lx_add_batch during a load (lx_load_finish first)");
     if (h->have_epoch && !h->sharded() && n <= std::min(h->small_max, kSmallMaxN))
         return add_batch_small(h, n, creator, seq, poff, par, out_branch, err_index);
     if ((rc = ensure_batch(h, n, npar))) return rc;
@@ -1972,6 +1985,385 @@ int lx_sync(lx_index *h) {
         HIPCHK(h, hipMemset(h->status + 1, 0, 4));
         return h->fail(LX_ERR_ARG, "ForklessCause on an unknown event");
     }
+    return 0;
+}
+
+// ---- restart from the persisted tables (abft/restart_test.go:156-188)
+
+// go-ethereum rlp (v1.9.22) reader for BranchesInfo: a list of three lists
+// (uint, uint, list of uint lists), uints minimal big-endian
+struct RlpIn {
+    const uint8_t *p, *end;
+    bool ok = true;
+    // header of the next item: list?, payload bounds
+    bool item(bool *list, const uint8_t **b, const uint8_t **e) {
+        if (p >= end) return ok = false;
+        const uint8_t x = *p;
+        uint64_t len = 0, hl = 1;
+        if (x < 0x80) { *list = false; *b = p; *e = p + 1; p++; return true; }
+        if (x <= 0xB7) { *list = false; len = x - 0x80; }
+        else if (x <= 0xBF) { *list = false; hl += x - 0xB7; }
+        else if (x <= 0xF7) { *list = true; len = x - 0xC0; }
+        else { *list = true; hl += x - 0xF7; }
+        if (hl > 1) {
+            if ((uint64_t)(end - p) < hl || hl > 9) return ok = false;
+            for (uint64_t k = 1; k < hl; k++) len = (len << 8) | p[k];
+        }
+        if ((uint64_t)(end - p) < hl + len) return ok = false;
+        *b = p + hl;
+        *e = p + hl + len;
+        p = *e;
+        return true;
+    }
+    bool uint_list(const uint8_t *b, const uint8_t *e, std::vector<uint32_t> &out) {
+        RlpIn r{b, e};
+        while (r.p < r.end) {
+            bool l;
+            const uint8_t *x, *y;
+            if (!r.item(&l, &x, &y) || l || y - x > 4) return ok = false;
+            uint32_t v = 0;
+            for (const uint8_t *q = x; q < y; q++) v = (v << 8) | *q;
+            out.push_back(v);
+        }
+        return true;
+    }
+};
+
+static bool decode_branches_info(const uint8_t *d, uint32_t n, std::vector<uint32_t> &last, std::vector<uint32_t> &cr,
+                                 std::vector<std::vector<uint32_t>> &by) {
+    RlpIn r{d, d + n};
+    bool l;
+    const uint8_t *b, *e;
+    if (!r.item(&l, &b, &e) || !l || r.p != r.end) return false;
+    RlpIn body{b, e};
+    const uint8_t *x, *y;
+    if (!body.item(&l, &x, &y) || !l || !body.uint_list(x, y, last)) return false;
+    if (!body.item(&l, &x, &y) || !l || !body.uint_list(x, y, cr)) return false;
+    if (!body.item(&l, &x, &y) || !l) return false;
+    RlpIn lists{x, y};
+    while (lists.p < lists.end) {
+        const uint8_t *u, *v;
+        if (!lists.item(&l, &u, &v) || !l) return false;
+        by.emplace_back();
+        if (!lists.uint_list(u, v, by.back())) return false;
+    }
+    return body.p == body.end && body.ok && lists.ok;
+}
+
+static int load_fail(lx_index *h, const char *fmt, uint64_t a = 0, uint64_t b = 0) {
+    char buf[256];
+    snprintf(buf, sizeof buf, fmt, (unsigned long long)a, (unsigned long long)b);
+    h->loading = false;
+    h->have_epoch = false;   // the handle needs lx_reset
+    return h->fail(LX_ERR_STATE, "inconsistent DB: %s", buf);
+}
+
+int lx_load_rows(lx_index *h, uint32_t n, const uint32_t *creator, const uint32_t *seq, const uint64_t *poff,
+                 const uint32_t *par, const uint8_t *branch_be, const uint64_t *hb_off, const uint8_t *hb_bytes,
+                 const uint64_t *la_off, const uint8_t *la_bytes) {
+    if (!h) return LX_ERR_ARG;
+    if (!h->have_epoch) return h->fail(LX_ERR_STATE, "lx_load_rows before lx_reset");
+    if (h->sharded()) return h->fail(LX_ERR_STATE, "lx_load_rows needs an unsharded handle");
+    if (!n) return 0;
+    if (!creator || !seq || !poff || !branch_be || !hb_off || !hb_bytes || !la_off || !la_bytes)
+        return h->fail(LX_ERR_ARG, "null input");
+    if (!h->loading) {
+        if (h->n_events) return h->fail(LX_ERR_STATE, "lx_load_rows needs a freshly reset handle");
+        h->loading = true;
+        h->ld_first.assign(h->V, 1);
+        h->ld_last.assign(h->V, 0);
+        h->ld_count.assign(h->V, 0);
+        h->ld_tail.assign(h->V, LX_NONE);
+        h->ld_creator.resize(h->V);
+        for (uint32_t c = 0; c < h->V; c++) h->ld_creator[c] = c;
+        h->ld_par.clear();
+        h->ld_poff.assign(1, 0);
+        h->ld_B = h->V;
+    }
+    HIPCHK(h, set_dev(h->device));
+    const uint64_t bs = h->n_events;
+    uint32_t max_hent = 0, max_lent = 0, bmax = h->max_seq;
+    for (uint32_t i = 0; i < n; i++) {
+        const uint64_t g = bs + i;
+        const uint32_t c = creator[i], s = seq[i];
+        const uint64_t p0 = poff[i], p1 = poff[i + 1];
+        const uint32_t br = ((uint32_t)branch_be[4 * i] << 24) | ((uint32_t)branch_be[4 * i + 1] << 16) |
+                            ((uint32_t)branch_be[4 * i + 2] << 8) | branch_be[4 * i + 3];
+        if (c >= h->V || s == 0 || s >= 0x7FFFFFFEu || p1 < p0) return load_fail(h, "event %llu: bad creator/seq", g);
+        for (uint64_t x = p0; x < p1; x++)
+            if (par[x] >= g) return load_fail(h, "event %llu: parent %llu not loaded before it", g, par[x]);
+        const uint32_t sp = s > 1 ? (p1 > p0 ? par[p0] : LX_NONE) : LX_NONE;
+        if (s > 1 && (sp == LX_NONE || h->hm_creator[sp] != c || h->hm_seq[sp] + 1 != s))
+            return load_fail(h, "event %llu: self-parent", g);
+        if (br < h->V && br != c) return load_fail(h, "event %llu: branch %llu of another creator", g, br);
+        if (br >= (1u << 24)) return load_fail(h, "event %llu: branch ID %llu", g, br);
+        if (br >= h->ld_first.size()) {
+            h->ld_first.resize(br + 1, 0);
+            h->ld_last.resize(br + 1, 0);
+            h->ld_count.resize(br + 1, 0);
+            h->ld_tail.resize(br + 1, LX_NONE);
+            h->ld_creator.resize(br + 1, LX_NONE);
+        }
+        const bool opens = h->ld_count[br] == 0;
+        if (opens) {
+            if (br < h->V && s != 1) return load_fail(h, "event %llu: first of branch %llu", g, br);
+            h->ld_first[br] = s;
+            h->ld_creator[br] = c;
+        } else if (h->ld_creator[br] != c || s != h->ld_last[br] + 1 || sp != h->ld_tail[br]) {
+            return load_fail(h, "event %llu: does not continue branch %llu", g, br);
+        }
+        h->ld_last[br] = s;
+        h->ld_tail[br] = (uint32_t)g;
+        h->ld_count[br]++;
+        h->ld_B = std::max(h->ld_B, br + 1);
+        // branches before its Add, from the HighestBefore byte length: 8 x (B
+        // before + 1) when it opened a fork branch, else 8 x B before
+        // (vecengine/index.go:147, vecfc/vector.go:82-89)
+        const uint64_t hl = hb_off[i + 1] - hb_off[i], ll = la_off[i + 1] - la_off[i];
+        if (hb_off[i + 1] < hb_off[i] || la_off[i + 1] < la_off[i] || hl % 8 || ll % 4 || hl / 8 > 0xFFFFFF || ll / 4 > 0xFFFFFF)
+            return load_fail(h, "event %llu: vector byte lengths", g);
+        const uint32_t hent = (uint32_t)(hl / 8), lent = (uint32_t)(ll / 4);
+        const bool fork_open = opens && br >= h->V;
+        const uint32_t bb = fork_open ? br : hent;
+        if ((fork_open ? hent != br + 1 : (hent < h->V || br >= hent)) || lent < bb + (fork_open ? 1u : 0u))
+            return load_fail(h, "event %llu: vector lengths disagree with branch %llu", g, br);
+        max_hent = std::max(max_hent, hent);
+        max_lent = std::max(max_lent, lent);
+        bmax = std::max(bmax, s);
+        h->hm_creator.push_back(c);
+        h->hm_seq.push_back(s);
+        h->hm_branch.push_back(br);
+        h->hm_bbefore.push_back(bb);
+        h->ld_par.insert(h->ld_par.end(), par + p0, par + p1);
+        h->ld_poff.push_back(h->ld_par.size());
+    }
+    h->max_seq = bmax;
+    int rc;
+    if ((rc = grow_events(h, bs + n)) || (rc = grow_branches(h, std::max({h->ld_B, max_hent, max_lent}))) ||
+        (rc = grow_scap(h, bmax)))
+        return rc;
+    hipStream_t st = h->stream;
+    // metadata of the chunk (the mirror vectors stay alive until the sync below)
+    std::vector<uint32_t> sp(n);
+    for (uint32_t i = 0; i < n; i++)
+        sp[i] = seq[i] > 1 ? par[poff[i]] : LX_NONE;
+    HIPCHK(h, hipMemcpyAsync(h->ev_creator + bs, h->hm_creator.data() + bs, n * 4ull, hipMemcpyHostToDevice, st));
+    HIPCHK(h, hipMemcpyAsync(h->ev_seq + bs, h->hm_seq.data() + bs, n * 4ull, hipMemcpyHostToDevice, st));
+    HIPCHK(h, hipMemcpyAsync(h->ev_branch + bs, h->hm_branch.data() + bs, n * 4ull, hipMemcpyHostToDevice, st));
+    HIPCHK(h, hipMemcpyAsync(h->ev_bbefore + bs, h->hm_bbefore.data() + bs, n * 4ull, hipMemcpyHostToDevice, st));
+    HIPCHK(h, hipMemcpyAsync(h->ev_sp + bs, sp.data(), n * 4ull, hipMemcpyHostToDevice, st));
+    HIPCHK(h, hipMemcpyAsync(h->branch_first, h->ld_first.data(), h->ld_B * 4ull, hipMemcpyHostToDevice, st));
+    // the chunk's table bytes and offsets
+    const uint64_t hb_n = hb_off[n] - hb_off[0], la_n = la_off[n] - la_off[0];
+    const uint64_t o_hoff = (hb_n + la_n + 15) / 16 * 16, o_loff = o_hoff + 8ull * (n + 1);
+    const uint64_t need = o_loff + 8ull * (n + 1);
+    if (need > h->ld_buf_cap) {
+        if (h->ld_buf) {
+            HIPCHK(h, hipStreamSynchronize(st));
+            (void)hipFree(h->ld_buf);
+        }
+        h->ld_buf = nullptr;
+        h->ld_buf_cap = 0;
+        HIPCHK(h, hipMalloc((void **)&h->ld_buf, need));
+        h->ld_buf_cap = need;
+    }
+    HIPCHK(h, hipMemcpyAsync(h->ld_buf, hb_bytes + hb_off[0], hb_n, hipMemcpyHostToDevice, st));
+    HIPCHK(h, hipMemcpyAsync(h->ld_buf + hb_n, la_bytes + la_off[0], la_n, hipMemcpyHostToDevice, st));
+    HIPCHK(h, hipMemcpyAsync(h->ld_buf + o_hoff, hb_off, 8ull * (n + 1), hipMemcpyHostToDevice, st));
+    HIPCHK(h, hipMemcpyAsync(h->ld_buf + o_loff, la_off, 8ull * (n + 1), hipMemcpyHostToDevice, st));
+    HIPCHK(h, hipMemsetAsync(h->status + 5, 0, 4, st));
+    LoadArgs a{};
+    a.hb = h->hb;
+    a.la = h->la;
+    a.stride = h->stride;
+    a.bs = (uint32_t)bs;
+    a.n = n;
+    a.B = h->ld_B;
+    a.hb_off = reinterpret_cast<const uint64_t *>(h->ld_buf + o_hoff);
+    a.la_off = reinterpret_cast<const uint64_t *>(h->ld_buf + o_loff);
+    a.hb_base = hb_off[0];
+    a.la_base = la_off[0] - hb_n;   // la bytes follow the hb bytes in the staging buffer
+    a.hb_bytes = h->ld_buf;
+    a.la_bytes = h->ld_buf;
+    a.ev_branch = h->ev_branch;
+    a.ev_seq = h->ev_seq;
+    a.branch_first = h->branch_first;
+    a.brow = h->brow;
+    a.s_cap = h->s_cap;
+    a.bad = h->status + 5;
+    HIPCHK(h, lx::launch_load_rows(a, st));
+    uint32_t bad = 0;
+    HIPCHK(h, hipMemcpyAsync(&bad, h->status + 5, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(h, hipStreamSynchronize(st));
+    if (bad) return load_fail(h, "HighestBefore entries (MinSeq, own seq or branch) in events %llu..%llu", bs, bs + n - 1);
+    h->n_events = bs + n;
+    h->hwm = std::max(h->hwm, h->n_events);
+    h->hm_n = h->n_events;
+    return 0;
+}
+
+int lx_load_finish(lx_index *h, const uint8_t *bi_rlp, uint32_t bi_len) {
+    if (!h) return LX_ERR_ARG;
+    if (!h->have_epoch) return h->fail(LX_ERR_STATE, "lx_load_finish before lx_reset");
+    if (!h->loading && h->n_events) return h->fail(LX_ERR_STATE, "lx_load_finish without lx_load_rows");
+    if (!bi_rlp) return h->fail(LX_ERR_ARG, "null BranchesInfo");
+    HIPCHK(h, set_dev(h->device));
+    if (!h->loading) {   // an empty epoch: the initial BranchesInfo
+        h->ld_first.assign(h->V, 1);
+        h->ld_last.assign(h->V, 0);
+        h->ld_count.assign(h->V, 0);
+        h->ld_creator.resize(h->V);
+        for (uint32_t c = 0; c < h->V; c++) h->ld_creator[c] = c;
+        h->ld_poff.assign(1, 0);
+        h->ld_B = h->V;
+        h->loading = true;
+    }
+    std::vector<uint32_t> last, cr;
+    std::vector<std::vector<uint32_t>> by;
+    if (!decode_branches_info(bi_rlp, bi_len, last, cr, by)) return load_fail(h, "RLP(BranchesInfo) malformed");
+    const uint32_t V = h->V, B = (uint32_t)last.size();
+    if (cr.size() != B || by.size() != V || B < V || B < h->ld_B) return load_fail(h, "BranchesInfo sizes (B %llu)", B);
+    h->ld_first.resize(B, 0);
+    h->ld_last.resize(B, 0);
+    h->ld_count.resize(B, 0);
+    h->ld_creator.resize(B, LX_NONE);
+    std::vector<std::vector<uint32_t>> want(V);
+    for (uint32_t b = 0; b < B; b++) {
+        if (cr[b] >= V || (b < V && cr[b] != b)) return load_fail(h, "branch %llu creator", b);
+        if (b >= V && !h->ld_count[b]) return load_fail(h, "fork branch %llu has no event", b);
+        if (h->ld_count[b] && h->ld_creator[b] != cr[b]) return load_fail(h, "branch %llu creator", b);
+        if (last[b] != h->ld_last[b]) return load_fail(h, "branch %llu last seq %llu", b, last[b]);   // branches_info.go:11
+        want[cr[b]].push_back(b);
+    }
+    for (uint32_t c = 0; c < V; c++)
+        if (by[c] != want[c]) return load_fail(h, "branches of creator %llu", c);
+    const uint64_t N = h->n_events;
+    int rc;
+    if ((rc = grow_branches(h, B))) return rc;
+    h->B = h->B_flushed = B;
+    h->h_branch_creator = cr;
+    h->h_branch_first.assign(B, 1);
+    std::vector<uint32_t> blen(B, 0);
+    for (uint32_t b = 0; b < B; b++) {
+        if (h->ld_count[b]) h->h_branch_first[b] = h->ld_first[b];
+        blen[b] = h->ld_count[b];
+    }
+    h->by_creator = by;
+    h->hm_blen = blen;
+    h->hm_ok = true;
+    h->hm_n = N;
+    // claims: the continuing self-child of each event, each creator's first root
+    std::vector<uint32_t> fchild(N, LX_NONE), froot(V, LX_NONE);
+    for (uint64_t e = 0; e < N; e++) {
+        const uint32_t s = h->hm_seq[e], br = h->hm_branch[e];
+        if (s > 1) {
+            const uint32_t sp = h->ld_par[h->ld_poff[e]];
+            if (h->hm_branch[sp] == br) fchild[sp] = (uint32_t)e;
+        } else if (br < V) {
+            froot[br] = (uint32_t)e;
+        }
+    }
+    hipStream_t st = h->stream;
+    HIPCHK(h, hipMemcpyAsync(h->branch_first, h->h_branch_first.data(), B * 4ull, hipMemcpyHostToDevice, st));
+    HIPCHK(h, hipMemcpyAsync(h->branch_creator, cr.data(), B * 4ull, hipMemcpyHostToDevice, st));
+    HIPCHK(h, hipMemcpyAsync(h->branch_len, blen.data(), B * 4ull, hipMemcpyHostToDevice, st));
+    if (N) HIPCHK(h, hipMemcpyAsync(h->first_child, fchild.data(), N * 4ull, hipMemcpyHostToDevice, st));
+    HIPCHK(h, hipMemcpyAsync(h->first_root, froot.data(), V * 4ull, hipMemcpyHostToDevice, st));
+    h->pcols_used = std::max(h->pcols_used, B);
+    if ((rc = rebuild_columns(h))) return rc;   // syncs the stream
+    if (B > V && h->n_cheat && N) {
+        // raw seqs behind the fork markers (cheaters' columns), then the markers
+        // re-derived from them must be exactly the loaded ones
+        std::vector<uint32_t> cols;
+        for (uint32_t c = 0; c < V; c++)
+            if (by[c].size() > 1) cols.insert(cols.end(), by[c].begin(), by[c].end());
+        const uint32_t ncc = (uint32_t)cols.size();
+        std::vector<uint32_t> lvl(N), perm(N);
+        uint32_t L = 0;
+        for (uint64_t e = 0; e < N; e++) {
+            uint32_t l = 0;
+            for (uint64_t k = h->ld_poff[e]; k < h->ld_poff[e + 1]; k++) l = std::max(l, lvl[h->ld_par[k]] + 1);
+            lvl[e] = l;
+            L = std::max(L, l + 1);
+        }
+        std::vector<uint32_t> off(L + 1, 0);
+        for (uint64_t e = 0; e < N; e++) off[lvl[e] + 1]++;
+        for (uint32_t l = 0; l < L; l++) off[l + 1] += off[l];
+        std::vector<uint32_t> cur(off.begin(), off.end() - 1);
+        for (uint64_t e = 0; e < N; e++) perm[cur[lvl[e]]++] = (uint32_t)e;
+        const uint64_t npar = h->ld_par.size();
+        uint8_t *scratch = nullptr;
+        const uint64_t o_perm = 4ull * ncc, o_off = o_perm + 4ull * N, o_poff = (o_off + 4ull * (L + 1) + 7) / 8 * 8,
+                       o_par = o_poff + 8ull * (N + 1), o_lm = o_par + 4ull * std::max<uint64_t>(npar, 1);
+        HIPCHK(h, hipMalloc((void **)&scratch, o_lm + N * ncc));
+        HIPCHK(h, hipMemcpyAsync(scratch, cols.data(), 4ull * ncc, hipMemcpyHostToDevice, st));
+        HIPCHK(h, hipMemcpyAsync(scratch + o_perm, perm.data(), 4ull * N, hipMemcpyHostToDevice, st));
+        HIPCHK(h, hipMemcpyAsync(scratch + o_off, off.data(), 4ull * (L + 1), hipMemcpyHostToDevice, st));
+        HIPCHK(h, hipMemcpyAsync(scratch + o_poff, h->ld_poff.data(), 8ull * (N + 1), hipMemcpyHostToDevice, st));
+        if (npar) HIPCHK(h, hipMemcpyAsync(scratch + o_par, h->ld_par.data(), 4ull * npar, hipMemcpyHostToDevice, st));
+        HIPCHK(h, hipMemsetAsync(h->status + 5, 0, 4, st));
+        LoadRawArgs r{};
+        r.hb = h->hb;
+        r.stride = h->stride;
+        r.cols = reinterpret_cast<const uint32_t *>(scratch);
+        r.ncc = ncc;
+        r.perm = reinterpret_cast<const uint32_t *>(scratch + o_perm);
+        r.lvl_off = reinterpret_cast<const uint32_t *>(scratch + o_off);
+        r.n_levels = L;
+        r.poff = reinterpret_cast<const uint64_t *>(scratch + o_poff);
+        r.par = reinterpret_cast<const uint32_t *>(scratch + o_par);
+        r.ev_branch = h->ev_branch;
+        r.ev_seq = h->ev_seq;
+        r.lm = scratch + o_lm;
+        r.bad = h->status + 5;
+        HIPCHK(h, lx::launch_load_raw(r, st));
+        MarkArgs m{};
+        m.hb = h->hb;
+        m.stride = h->pstride;
+        m.batch_start = 0;
+        m.n = (uint32_t)N;
+        m.V = V;
+        m.ev_branch = h->ev_branch;
+        m.ev_bbefore = h->ev_bbefore;
+        m.branch_first = h->branch_first;
+        m.n_cheat = h->n_cheat;
+        m.cheat_off = h->cheat_off;
+        m.cheat_br = h->cheat_br;
+        HIPCHK(h, lx::launch_marks(m, st));
+        HIPCHK(h, lx::launch_load_check(r, (uint32_t)N, st));
+        uint32_t bad = 0;
+        HIPCHK(h, hipMemcpyAsync(&bad, h->status + 5, 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(h, hipStreamSynchronize(st));
+        (void)hipFree(scratch);
+        if (bad) return load_fail(h, "fork markers / raw HighestBefore do not follow from the vectors (flags %llu)", bad);
+    }
+    if (N) {
+        LoadVerifyArgs v{};
+        v.hb = h->hb;
+        v.la = h->la;
+        v.stride = h->stride;
+        v.n = (uint32_t)N;
+        v.B = B;
+        v.ev_branch = h->ev_branch;
+        v.ev_seq = h->ev_seq;
+        v.branch_first = h->branch_first;
+        v.branch_len = h->branch_len;
+        v.brow = h->brow;
+        v.s_cap = h->s_cap;
+        v.bad = h->status + 5;
+        HIPCHK(h, hipMemsetAsync(h->status + 5, 0, 4, st));
+        HIPCHK(h, lx::launch_load_verify_la(v, st));
+        uint32_t bad = 0;
+        HIPCHK(h, hipMemcpyAsync(&bad, h->status + 5, 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(h, hipStreamSynchronize(st));
+        if (bad) return load_fail(h, "LowestAfter rows do not follow from the HighestBefore rows (flags %llu)", bad);
+    }
+    h->n_flushed = N;
+    h->loading = false;
+    h->ld_par.clear();
+    h->ld_par.shrink_to_fit();
+    h->ld_poff.clear();
+    h->ld_poff.shrink_to_fit();
     return 0;
 }
 

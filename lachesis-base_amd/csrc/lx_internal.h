@@ -254,6 +254,45 @@ struct RowsArgs {
     uint32_t hb;                 // 1: HighestBefore (8 B per branch), 0: LowestAfter (4 B)
 };
 
+// restart from the persisted tables (k_load_rows, k_load_raw, k_load_check)
+struct LoadArgs {
+    uint32_t *hb, *la;
+    uint64_t stride;
+    uint32_t bs, n;              // first dense index of the chunk, events
+    uint32_t B;                  // branches known so far (HB entries must lie below)
+    const uint64_t *hb_off, *la_off;   // n + 1 byte offsets (absolute)
+    uint64_t hb_base, la_base;   // offsets of the first byte of the chunk's buffers
+    const uint8_t *hb_bytes, *la_bytes;
+    const uint32_t *ev_branch, *ev_seq;
+    const uint32_t *branch_first;
+    uint32_t *brow;
+    uint32_t s_cap;
+    uint32_t *bad;               // |= 1: malformed entry
+};
+struct LoadRawArgs {
+    uint32_t *hb;
+    uint64_t stride;
+    const uint32_t *cols;        // the cheaters' branch columns
+    uint32_t ncc;
+    const uint32_t *perm, *lvl_off;   // events by topological level
+    uint32_t n_levels;
+    const uint64_t *poff;        // whole epoch: parents of event e at par[poff[e] .. poff[e+1])
+    const uint32_t *par;
+    const uint32_t *ev_branch, *ev_seq;
+    uint8_t *lm;                 // [e][k]: entry was loaded as a fork marker
+    uint32_t *bad;               // |= 2: raw value differs, 4: markers differ
+};
+
+struct LoadVerifyArgs {
+    const uint32_t *hb, *la;
+    uint64_t stride;
+    uint32_t n, B;
+    const uint32_t *ev_branch, *ev_seq;
+    const uint32_t *branch_first, *branch_len, *brow;
+    uint32_t s_cap;
+    uint32_t *bad;
+};
+
 // batched getters (k_get_rows): mode 0 HighestBefore, 1 LowestAfter, 2 merged HighestBefore
 struct GetArgs {
     const uint32_t *plane;       // hb (modes 0, 2) or la (mode 1)
@@ -380,6 +419,10 @@ hipError_t launch_row_offsets(const RowsArgs &a, uint64_t *len, uint64_t *off, v
                               hipStream_t s);
 hipError_t launch_encode_rows(const RowsArgs &a, const uint64_t *off, uint64_t base, uint32_t *out, hipStream_t s);
 hipError_t launch_get_rows(const GetArgs &a, hipStream_t s);
+hipError_t launch_load_rows(const LoadArgs &a, hipStream_t s);
+hipError_t launch_load_raw(const LoadRawArgs &a, hipStream_t s);
+hipError_t launch_load_check(const LoadRawArgs &a, uint32_t n, hipStream_t s);
+hipError_t launch_load_verify_la(const LoadVerifyArgs &a, hipStream_t s);
 hipError_t launch_gather_u32(const uint32_t *src, const uint32_t *idx, uint32_t n, uint32_t *dst, hipStream_t s);
 hipError_t launch_qi_update(const QiArgs &a, const uint32_t *ev, const uint32_t *target, uint32_t n, hipStream_t s);
 hipError_t launch_qi_median(const QiArgs &a, hipStream_t s);

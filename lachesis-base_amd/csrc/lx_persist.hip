@@ -195,6 +195,147 @@ __global__ __launch_bounds__(256) void k_get_rows(GetArgs a) {
     if (lane == 0) a.len[i] = ent * (hb ? 8u : 4u);
 }
 
+// ---------------------------------------------------------------------------- restart
+// Restart from the persisted tables (lx_load_rows / lx_load_finish): table-S
+// and table-s bytes of a chunk of events decoded into the planes, one wave per
+// event.  HighestBefore entries {Seq, MinSeq}: Seq as the plane value, the
+// marker {0, MaxInt32} as LX_MARK (its raw seq is rebuilt by k_load_raw);
+// every non-empty entry must carry its branch's first seq as MinSeq and the
+// event's own entry must be its seq (InitWithEvent) -- else bad[0] is set.
+__global__ __launch_bounds__(256) void k_load_rows(LoadArgs a) {
+    const uint32_t i = blockIdx.x * 4 + threadIdx.x / 64, lane = threadIdx.x % 64;
+    if (i >= a.n) return;
+    const uint32_t g = a.bs + i;
+    const uint64_t h0 = a.hb_off[i] - a.hb_base, la0 = a.la_off[i] - a.la_base;
+    const uint32_t hent = (uint32_t)((a.hb_off[i + 1] - a.hb_off[i]) / 8);
+    const uint32_t lent = (uint32_t)((a.la_off[i + 1] - a.la_off[i]) / 4);
+    const uint32_t br = a.ev_branch[g], seq = a.ev_seq[g];
+    uint32_t *hrow = a.hb + (uint64_t)g * a.stride;
+    uint32_t *lrow = a.la + (uint64_t)g * a.stride;
+    bool bad = false;
+    for (uint32_t c = lane; c < a.stride; c += 64) {
+        uint32_t v = 0;
+        if (c < hent) {
+            uint2 x;
+            memcpy(&x, a.hb_bytes + h0 + 8ull * c, 8);   // byte buffer: no alignment assumed
+            if (x.x == 0 && x.y == 0x7FFFFFFFu) {
+                v = LX_MARK;
+            } else if (x.x) {
+                v = x.x;
+                bad |= c >= a.B || x.y != a.branch_first[c] || x.x > 0x7FFFFFFDu;
+            } else {
+                bad |= x.y != 0;
+            }
+        }
+        if (c == br) bad |= !(v == seq || v == LX_MARK);
+        hrow[c] = v;
+        uint32_t l = 0;
+        if (c < lent) memcpy(&l, a.la_bytes + la0 + 4ull * c, 4);
+        lrow[c] = l;
+    }
+    if (lane == 0) a.brow[(uint64_t)br * a.s_cap + (seq - a.branch_first[br])] = g;
+    if (__any(bad) && lane == 0) atomicOr(a.bad, 1u);
+}
+
+hipError_t launch_load_rows(const LoadArgs &a, hipStream_t s) {
+    if (!a.n) return hipSuccess;
+    hipLaunchKernelGGL(k_load_rows, dim3(nblk_p(a.n, 4)), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+// Raw seqs behind the persisted fork markers: the max-join of HighestBefore
+// recomputed for the cheaters' branch columns (kSmallCW columns per workgroup,
+// 64 event lanes, level by level over the whole epoch; parents' values are read
+// back from the plane after the level barrier).  An entry loaded as a marker
+// takes the raw value and is noted in lm[e * ncc + k]; any other entry must
+// equal the recomputed value (else bad[0]).  k_marks then re-derives the
+// markers and k_load_check compares them with lm.
+__global__ __launch_bounds__(256) void k_load_raw(LoadRawArgs a) {
+    constexpr uint32_t CW = kSmallCW, NQ = 256 / CW;
+    const uint32_t k = threadIdx.x % CW, q = threadIdx.x / CW;
+    const uint32_t kc = blockIdx.x * CW + k;
+    const bool valid = kc < a.ncc;
+    const uint32_t col = valid ? a.cols[kc] : 0u;
+    bool bad = false;
+    for (uint32_t L = 0; L < a.n_levels; L++) {
+        const uint32_t lo = a.lvl_off[L], hi = a.lvl_off[L + 1];
+        for (uint32_t j = lo + q; j < hi && valid; j += NQ) {
+            const uint32_t e = a.perm[j];
+            uint32_t r = a.ev_branch[e] == col ? a.ev_seq[e] : 0u;
+            for (uint64_t p = a.poff[e]; p < a.poff[e + 1]; p++)
+                r = max(r, a.hb[(uint64_t)a.par[p] * a.stride + col] & LX_SEQ_MASK);
+            uint32_t *cell = a.hb + (uint64_t)e * a.stride + col;
+            const uint32_t old = *cell;
+            if (old & LX_MARK) {
+                a.lm[(uint64_t)e * a.ncc + kc] = 1;
+                *cell = r;
+            } else {
+                a.lm[(uint64_t)e * a.ncc + kc] = 0;
+                bad |= old != r;
+            }
+        }
+        __syncthreads();
+    }
+    if (bad) atomicOr(a.bad, 2u);
+}
+
+__global__ void k_load_check(LoadRawArgs a, uint32_t n) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (uint64_t)n * a.ncc) return;
+    const uint32_t e = (uint32_t)(t / a.ncc), kc = (uint32_t)(t % a.ncc);
+    const bool marked = (a.hb[(uint64_t)e * a.stride + a.cols[kc]] & LX_MARK) != 0;
+    if (marked != (a.lm[t] != 0)) atomicOr(a.bad, 4u);
+}
+
+hipError_t launch_load_raw(const LoadRawArgs &a, hipStream_t s) {
+    if (!a.ncc) return hipSuccess;
+    hipLaunchKernelGGL(k_load_raw, dim3((a.ncc + kSmallCW - 1) / kSmallCW), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_load_check(const LoadRawArgs &a, uint32_t n, hipStream_t s) {
+    const uint64_t t = (uint64_t)n * a.ncc;
+    if (!t) return hipSuccess;
+    hipLaunchKernelGGL(k_load_check, dim3((uint32_t)((t + 255) / 256)), dim3(256), 0, s, a, n);
+    return hipGetLastError();
+}
+
+// Every loaded LowestAfter entry must be what the range fill (DESIGN.md
+// section 3; the DFS of vecengine/index.go:212-225) gives from the loaded
+// HighestBefore rows: LA(x)[j] = s != 0 iff event (j, s) observes x and (j, s-1)
+// does not (or s is j's first seq); LA(x)[j] = 0 iff the last event of j does
+// not observe x.  One thread per (row, branch); bad |= 8.
+__global__ void k_load_verify_la(LoadVerifyArgs a) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (uint64_t)a.n * a.B) return;
+    const uint32_t x = (uint32_t)(t / a.B), j = (uint32_t)(t % a.B);
+    const uint32_t s = a.la[(uint64_t)x * a.stride + j];
+    const uint32_t bx = a.ev_branch[x], sx = a.ev_seq[x];
+    const uint32_t f = a.branch_first[j], len = a.branch_len[j];
+    bool bad;
+    if (s) {
+        bad = s < f || s - f >= len;
+        if (!bad) {
+            const uint32_t y = a.brow[(uint64_t)j * a.s_cap + (s - f)];
+            bad = (a.hb[(uint64_t)y * a.stride + bx] & LX_SEQ_MASK) < sx;
+            if (!bad && s > f) {
+                const uint32_t y0 = a.brow[(uint64_t)j * a.s_cap + (s - 1 - f)];
+                bad = (a.hb[(uint64_t)y0 * a.stride + bx] & LX_SEQ_MASK) >= sx;
+            }
+        }
+    } else {
+        bad = len && (a.hb[(uint64_t)a.brow[(uint64_t)j * a.s_cap + (len - 1)] * a.stride + bx] & LX_SEQ_MASK) >= sx;
+    }
+    if (bad) atomicOr(a.bad, 8u);
+}
+
+hipError_t launch_load_verify_la(const LoadVerifyArgs &a, hipStream_t s) {
+    const uint64_t t = (uint64_t)a.n * a.B;
+    if (!t) return hipSuccess;
+    hipLaunchKernelGGL(k_load_verify_la, dim3((uint32_t)((t + 255) / 256)), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
 hipError_t launch_get_rows(const GetArgs &a, hipStream_t s) {
     if (!a.n) return hipSuccess;
     hipLaunchKernelGGL(k_get_rows, dim3(nblk_p(a.n, 4)), dim3(256), 0, s, a);

@@ -26,6 +26,8 @@ SIGNATURES = [
     ("lx_drop_not_flushed", ctypes.c_int, [vp]),
     ("lx_writeback_prepare", ctypes.c_int, [vp, vp]),
     ("lx_writeback_fetch", ctypes.c_int, [vp, u64p, u8p, u32p, u64p, u8p, u8p, u8p]),
+    ("lx_load_rows", ctypes.c_int, [vp, ctypes.c_uint32, u32p, u32p, u64p, u32p, u8p, u64p, u8p, u64p, u8p]),
+    ("lx_load_finish", ctypes.c_int, [vp, u8p, ctypes.c_uint32]),
     ("lx_num_events", ctypes.c_uint64, [vp]),
     ("lx_num_branches", ctypes.c_uint32, [vp]),
     ("lx_at_least_one_fork", ctypes.c_int, [vp]),
@@ -233,6 +235,29 @@ class Index:
                 "s": {int(la_ev[k]): la_b[la_off[k]:la_off[k + 1]] for k in range(m)},
                 "b": {f + i: br_b[4 * i:4 * i + 4] for i in range(n)},
                 "B": bi.tobytes()[:wb.bi_bytes]}
+
+    def load_rows(self, creator_idx, seq, parent_off, parent_idx, branch_be, hb_rows, la_rows):
+        """lx_load_rows: events in a parents-first order with their persisted
+        table bytes (branch_be: 4 bytes per event; hb_rows / la_rows: lists of
+        bytes)."""
+        creator_idx = _u32(creator_idx)
+        seq = _u32(seq)
+        off = np.ascontiguousarray(parent_off, dtype=np.uint64)
+        par = _u32(parent_idx) if len(parent_idx) else np.zeros(1, dtype=np.uint32)
+        br = np.frombuffer(bytes(branch_be) or b"\0", dtype=np.uint8).copy()
+        hb_off = np.zeros(len(hb_rows) + 1, dtype=np.uint64)
+        hb_off[1:] = np.cumsum([len(r) for r in hb_rows])
+        la_off = np.zeros(len(la_rows) + 1, dtype=np.uint64)
+        la_off[1:] = np.cumsum([len(r) for r in la_rows])
+        hb = np.frombuffer(b"".join(hb_rows) or b"\0", dtype=np.uint8).copy()
+        la = np.frombuffer(b"".join(la_rows) or b"\0", dtype=np.uint8).copy()
+        self._chk(self.L.lx_load_rows(self.h, len(creator_idx), _p(creator_idx, u32p), _p(seq, u32p), _p(off, u64p),
+                                      _p(par, u32p), _p(br, u8p), _p(hb_off, u64p), _p(hb, u8p), _p(la_off, u64p),
+                                      _p(la, u8p)))
+
+    def load_finish(self, bi_rlp):
+        b = np.frombuffer(bytes(bi_rlp) or b"\0", dtype=np.uint8).copy()
+        self._chk(self.L.lx_load_finish(self.h, _p(b, u8p), len(bi_rlp)))
 
     def num_events(self):
         return self.L.lx_num_events(self.h)

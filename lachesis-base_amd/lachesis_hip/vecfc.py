@@ -130,48 +130,74 @@ class VecfcIndex:
         by event id -- db["S"] HighestBefore bytes, db["s"] LowestAfter
         bytes, db["b"] 4-B big-endian branch IDs, db["B"][b"c"]
         RLP(BranchesInfo) (vecfc/index.go:38-41, vecengine/index.go:39-42) --
-        plus db["i"], the shim's own table of Add-order positions that
-        ``restore`` replays from."""
+        and nothing else: ``restore`` works from exactly these tables."""
         if db is not None:
             wb = self.ix.writeback()
-            for t in ("S", "s", "b", "i", "B"):
+            for t in ("S", "s", "b", "B"):
                 db.setdefault(t, {})
             for k, v in wb["S"].items():
                 eid = self.ids[k]
                 db["S"][eid] = v
                 db["b"][eid] = wb["b"][k]
-                db["i"][eid] = k
             for k, v in wb["s"].items():
                 db["s"][self.ids[k]] = v
             db["B"][b"c"] = wb["B"]
         self.ix.flush()
         self.n_flushed = len(self.ids)
 
-    def restore(self, validators, db, get_event):
+    def restore(self, validators, db, get_event, chunk=4096):
         """Restart over persisted tables (abft/restart_test.go:156-188 builds a
-        fresh index over a copy of the DB): replays the stored events in their
-        Add order (db["i"]) and checks that the write-back of the replayed
-        epoch equals the persisted tables S, s, b and B byte for byte (crit
-        "inconsistent DB" otherwise, as vecengine/store_branches_info.go:83)."""
+        fresh index over a copy of the DB): the events of table "b" are loaded
+        in a parents-first order with their table S / s / b bytes and table B's
+        RLP(BranchesInfo) (lx_load_rows / lx_load_finish) -- no replay of Add.
+        Tables that do not form one consistent epoch call crit ("inconsistent
+        DB", as vecengine/store_branches_info.go:83)."""
+        from .capi import LxError
         self.reset(validators, get_event)
-        order = sorted(db.get("i", {}).items(), key=lambda kv: kv[1])
-        if [k for _, k in order] != list(range(len(order))):
-            self.crit(RuntimeError("inconsistent DB: Add-order table has gaps"))
+        ids = list(db.get("b", {}))
+        if not ids and not db.get("B"):
+            return                              # nothing flushed yet: an empty epoch
+        events = {eid: get_event(eid) for eid in ids}
+        order, state = [], {}
+        for root in sorted(ids, key=lambda x: (getattr(events[x], "lamport", 0), x)):
+            stack = [(root, False)]
+            while stack:
+                eid, done = stack.pop()
+                if done:
+                    if state.get(eid) != 2:
+                        state[eid] = 2
+                        order.append(eid)
+                    continue
+                if state.get(eid):
+                    continue
+                state[eid] = 1
+                stack.append((eid, True))
+                for p in reversed(events[eid].parents):
+                    if p not in events:
+                        self.crit(RuntimeError("inconsistent DB: parent %r of %r not persisted" % (p, eid)))
+                        return
+                    if not state.get(p):
+                        stack.append((p, False))
+        pos = {eid: k for k, eid in enumerate(order)}
+        try:
+            for lo in range(0, len(order), chunk):
+                part = order[lo:lo + chunk]
+                creator, seq, off, flat = [], [], [0], []
+                for eid in part:
+                    e = events[eid]
+                    creator.append(validators.idxs[e.creator])
+                    seq.append(e.seq)
+                    flat.extend(pos[p] for p in e.parents)
+                    off.append(len(flat))
+                self.ix.load_rows(creator, seq, off, flat, b"".join(db["b"][eid] for eid in part),
+                                  [db["S"][eid] for eid in part], [db["s"][eid] for eid in part])
+            self.ix.load_finish(db.get("B", {}).get(b"c", b""))
+        except (LxError, KeyError) as err:
+            self.crit(RuntimeError("inconsistent DB: %s" % (err,)))
             return
-        events = [get_event(eid) for eid, _ in order]
-        if events:
-            self.add_events(events)
-        wb = self.ix.writeback()
-        ok = (len(wb["S"]) == len(db.get("S", {})) and len(wb["s"]) == len(db.get("s", {})) and
-              all(db["S"].get(self.ids[k]) == v for k, v in wb["S"].items()) and
-              all(db["s"].get(self.ids[k]) == v for k, v in wb["s"].items()) and
-              all(db["b"].get(self.ids[k]) == v for k, v in wb["b"].items()) and
-              (not events or db.get("B", {}).get(b"c") == wb["B"]))
-        if not ok:
-            self.drop_not_flushed()
-            self.crit(RuntimeError("inconsistent DB: persisted vectors differ from the replayed epoch"))
-            return
-        self.flush()
+        self.ids = order
+        self.pos = pos
+        self.n_flushed = len(order)
 
     def drop_not_flushed(self):
         self.ix.drop_not_flushed()
