@@ -91,7 +91,7 @@ def cpu_baseline(dag, weights, n_events_max, fc_n, budget_s):
     o.forkless_cause_batch(qa, qb)
     t_fc = time.perf_counter() - t1
     # FC over all host cores given to this job (OpenMP)
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)   # the job's CPU share
     qa2, qb2 = tools.fc_queries(dag.lamport[:done], fc_n * threads, seed=4)
     t2 = time.perf_counter()
     o.forkless_cause_batch_mt(qa2, qb2, threads)
@@ -139,6 +139,124 @@ def latency_leg(lx, dag, weights, device, history=200_000, reps=2000, feed=1_000
            "fed_events": int(out[34]), "fed_levels": int(out[35]), "mean_events_per_level": out[37],
            "note": "add1_async = host time of lx_add_batch(n=1) + lx_flush (the launch is not waited for); "
                    "*_sync include lx_sync (completion); fc/getters are synchronous calls"}
+    return res
+
+
+def _bench_lib():
+    import ctypes
+    L = ctypes.CDLL(os.path.join(PKG, "build", "liblx_bench.so"))
+    u32p, u64p = ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint64)
+    L.lx_bench_feed.restype = ctypes.c_int
+    L.lx_bench_feed.argtypes = [ctypes.c_int, ctypes.c_uint32, u32p, ctypes.c_uint64, u32p, u32p, u64p, u32p,
+                                ctypes.c_uint32, ctypes.POINTER(ctypes.c_double), ctypes.c_char_p, ctypes.c_uint32]
+    return L
+
+
+def feed_rate(dag, weights, device, batch):
+    """Events/s adding the DAG in its Add order in batches of `batch` events
+    (lx_add_batch + lx_flush each; 1 = per-event Add), tools/lx_latency.cpp."""
+    import ctypes
+    import numpy as np
+    L = _bench_lib()
+    u32p, u64p = ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint64)
+    w = np.ascontiguousarray(weights, dtype=np.uint32)
+    out = (ctypes.c_double * 4)()
+    err = ctypes.create_string_buffer(512)
+    rc = L.lx_bench_feed(device, len(w), w.ctypes.data_as(u32p), len(dag), dag.creator.ctypes.data_as(u32p),
+                         dag.seq.ctypes.data_as(u32p), dag.poff.ctypes.data_as(u64p), dag.par.ctypes.data_as(u32p),
+                         batch, out, err, 512)
+    if rc != 0:
+        raise RuntimeError("lx_bench_feed: " + err.value.decode())
+    return out[0]
+
+
+def config_leg(lx, name, steps, warmup, device, want_cpu, cpu_budget, fc_n=1 << 22):
+    """Secondary line for another BASELINE config: the same
+    index step (reset + one lx_add_batch_dev of the epoch) and FC step as the
+    headline, with the k_fc roofline (8 B per branch per query) and the C
+    restatement's CPU baseline on a bounded sample; C1 also adds its events
+    one at a time (the reference's per-event Add)."""
+    import numpy as np
+    import torch
+    V, epv, P, ch, fk, wkind = CONFIGS[name]
+    weights = weights_for(V, wkind)
+    dag = lx.tools.gen_dag(V, epv, P, ch, fk, seed=1)
+    N = len(dag)
+    dev = torch.device("cuda", device)
+    to_dev = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int32)).to(dev)
+    d_c, d_s, d_p = to_dev(dag.creator), to_dev(dag.seq), to_dev(dag.par)
+    d_o = to_dev(dag.poff.astype(np.uint32))
+    qa, qb = lx.tools.fc_queries(dag.lamport, fc_n, window=64, seed=7)
+    d_qa, d_qb = to_dev(qa), to_dev(qb)
+    d_out = torch.empty(fc_n, dtype=torch.uint8, device=dev)
+    ix = lx.Index(device=device, event_capacity=N)
+
+    def step():
+        ix.reset(weights)
+        ix.add_batch_dev(N, d_c.data_ptr(), d_s.data_ptr(), d_o.data_ptr(), d_p.data_ptr())
+        return ix.last_stats()["ms_index"]
+
+    for _ in range(warmup):
+        step()
+    ix.sync()
+    t0 = time.perf_counter()
+    kms = [step() for _ in range(steps)]
+    ix.sync()
+    t_idx = (time.perf_counter() - t0) / steps
+    _, _, _, sp = ix.device_planes()
+    st = torch.cuda.ExternalStream(sp, device=dev)
+    for _ in range(warmup):
+        ix.forkless_cause_batch_dev(fc_n, d_qa.data_ptr(), d_qb.data_ptr(), d_out.data_ptr())
+    ix.sync()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    t1 = time.perf_counter()
+    for e0, e1 in evs:
+        e0.record(st)
+        ix.forkless_cause_batch_dev(fc_n, d_qa.data_ptr(), d_qb.data_ptr(), d_out.data_ptr())
+        e1.record(st)
+    ix.sync()
+    t_fc = (time.perf_counter() - t1) / steps
+    fc_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    B = ix.num_branches()
+    o = None
+    if want_cpu:
+        from oracle import corc
+        o = corc.OracleIndex(weights)
+    got = d_out[:4096].cpu().numpy()
+    ix.close()
+    fc_bytes = 8.0 * B * fc_n
+    p_mean = float(len(dag.par)) / N
+    res = {"workload": "%s: V=%d, %d events (%d/validator), P=%d, %s stakes, cheaters=%d x %d forks; FC 2^%d queries"
+                       % (name, V, N, epv, P, wkind, ch, fk, int(np.log2(fc_n))),
+           "events": N, "branches": B, "events_per_sec": N / t_idx, "ms_per_step": t_idx * 1e3,
+           "index_kernel_ms": float(np.mean(kms)), "fc_queries_per_sec": fc_n / t_fc,
+           "roofline": {"bound": "hbm", "kernel": "k_fc<%s>" % ("forks" if B > V else "no forks"),
+                        "achieved": fc_bytes / (fc_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": fc_bytes / (fc_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                        "algorithmic_bytes_per_launch": fc_bytes, "kernel_ms": fc_ms},
+           "roofline_index": {"kernel": "k_index", "algorithmic_bytes_per_launch":
+                              ((p_mean + 1) * 4 * B + 4 * B + 8) * N, "kernel_ms": float(np.mean(kms))}}
+    if name == "c1":
+        res["per_event_add_events_per_sec"] = feed_rate(dag, weights, device, 1)
+    if o is not None:
+        t2 = time.perf_counter()
+        done = 0
+        while done < N and time.perf_counter() - t2 < cpu_budget:
+            hi = min(N, done + 500)
+            assert o.add_batch(dag.creator[done:hi], dag.seq[done:hi], dag.poff[done:hi + 1], dag.par) == -1
+            done = hi
+        t_add = time.perf_counter() - t2
+        nq = 100_000
+        qa2, qb2 = lx.tools.fc_queries(dag.lamport[:done], nq, seed=3)
+        t3 = time.perf_counter()
+        want = o.forkless_cause_batch(qa2, qb2)
+        t_q = time.perf_counter() - t3
+        if done == N:   # whole epoch indexed on the CPU: this run's GPU answers must match
+            assert np.array_equal(got, o.forkless_cause_batch(qa[:4096], qb[:4096]))
+        res["cpu_baseline"] = {"value": done / t_add, "unit": "events/s", "cores": 1, "kind": "port",
+                               "sample": "first %d events indexed by the C restatement in %.1fs; FC %d queries in %.2fs"
+                                         % (done, t_add, nq, t_q), "fc_value": nq / t_q}
+        assert want.max() <= 1
     return res
 
 
@@ -218,6 +336,7 @@ def main():
     ap.add_argument("--mode", default="shard", choices=["replica", "shard"])
     ap.add_argument("--no-abft", action="store_true", help="skip the configs[4] abft leg")
     ap.add_argument("--no-latency", action="store_true", help="skip the per-call latency / antichain-fed leg")
+    ap.add_argument("--no-configs", action="store_true", help="skip the secondary C1/C2/C4 lines")
     ap.add_argument("--shard-solo", type=int, default=0,
                     help="diagnostic: time rank 0 of a G-way column shard alone on this GPU (its index walk, "
                          "the packing of its outgoing LowestAfter blocks, its partial FC); no collectives")
@@ -433,6 +552,12 @@ def main():
         ix.close()   # free the bench epoch's planes first
         result["latency"] = latency_leg(lx, dag, weights, local)
 
+    if not args.no_configs and world == 1 and not solo:
+        ix.close()
+        want_cpu = rank == 0 and not args.no_cpu
+        result["configs"] = {c: config_leg(lx, c, args.steps, args.warmup, local, want_cpu, min(args.cpu_budget, 4.0))
+                             for c in ("c2", "c4", "c1")}
+
     if not args.no_abft:
         ab = abft_leg(lx, args.steps, args.warmup, local, args.cpu_budget, rank == 0 and world == 1 and not args.no_cpu)
         barrier()
@@ -451,6 +576,10 @@ def main():
             "fc_value": nq / t_q, "fc_unit": "queries/s",
             "fc_value_mt": nq_mt / t_mt, "fc_threads": thr,
             "fc_sample_mt": "%d queries over the same prefix, OpenMP over queries, in %.2fs" % (nq_mt, t_mt),
+            "fc_value_all_cores_extrapolated": nq_mt / t_mt / thr * (os.cpu_count() or 1),
+            "fc_mt_note": "timed on the job's CPU share (OMP_NUM_THREADS=%d of %d logical CPUs on the box; the "
+                          "pool's rule is to stay within the share); the all-cores figure scales the measured "
+                          "per-thread rate linearly, an upper bound" % (thr, os.cpu_count() or 1),
             "host": "%s, %d logical cpus" % (platform.processor() or platform.machine(), os.cpu_count()),
         }
     if rank == 0:

@@ -146,6 +146,7 @@ struct lx_index {
     bool st_used[kSlots] = {};
     uint32_t st_next = 0;
     uint32_t *st_dev = nullptr;            // device image (stream order serialises its reuse)
+    SmallInlineArgs sm_inl{};              // arguments of the last launch; images of <= kSmallInline words inline
     uint64_t st_dev_cap = 0;
     // restart from the persisted tables (lx_load_rows / lx_load_finish)
     bool loading = false;
@@ -1114,8 +1115,10 @@ int add_batch_small(lx_index *h, uint32_t n, const uint32_t *creator, const uint
     const uint64_t w_ev = 12ull * n;
     const uint64_t words = w_ev + npar + n + (n + 1) + 2ull * n + 2ull * n;
     uint32_t *img;
-    int slot;
-    if ((rc = stage_slot(h, words, &img, &slot))) return rc;
+    int slot = -1;
+    const bool inl = words <= kSmallInline;   // small enough for the kernel arguments
+    if (inl) img = h->sm_inl.img;
+    else if ((rc = stage_slot(h, words, &img, &slot))) return rc;
     SmallEv *ev = reinterpret_cast<SmallEv *>(img);
     uint32_t *ipar = img + w_ev;
     if (npar) memcpy(ipar, par + poff[0], npar * 4);
@@ -1210,11 +1213,14 @@ int add_batch_small(lx_index *h, uint32_t n, const uint32_t *creator, const uint
     if (nf || h->ncols == 0)
         if ((rc = rebuild_columns(h))) return rc;
     hipStream_t s = h->stream;
-    HIPCHK(h, hipMemcpyAsync(h->st_dev, img, used * 4, hipMemcpyHostToDevice, s));
-    HIPCHK(h, hipEventRecord(h->st_done[slot], s));
-    h->st_used[slot] = true;
+    if (!inl) {
+        HIPCHK(h, hipMemcpyAsync(h->st_dev, img, used * 4, hipMemcpyHostToDevice, s));
+        HIPCHK(h, hipEventRecord(h->st_done[slot], s));
+        h->st_used[slot] = true;
+    }
 
-    SmallArgs a{};
+    SmallArgs &a = h->sm_inl.a;
+    a = SmallArgs{};
     a.hb = h->hb;
     a.la = h->la;
     a.stride = h->pstride;
@@ -1222,15 +1228,14 @@ int add_batch_small(lx_index *h, uint32_t n, const uint32_t *creator, const uint
     a.n = n;
     a.B0 = B0;
     a.B = B;
-    const uint32_t *d = h->st_dev;
-    a.ev = reinterpret_cast<const SmallEv *>(d);
-    a.par = d + w_ev;
-    a.perm = d + (perm - img);
-    a.lvl_off = d + (loff - img);
+    a.img = inl ? nullptr : h->st_dev;
+    a.o_par = (uint32_t)w_ev;
+    a.o_perm = (uint32_t)(perm - img);
+    a.o_loff = (uint32_t)(loff - img);
     a.n_levels = L;
-    a.new_first = d + (nfirst - img);
-    a.new_creator = d + (ncreator - img);
-    a.blen = d + (blen - img);
+    a.o_nfirst = (uint32_t)(nfirst - img);
+    a.o_ncreator = (uint32_t)(ncreator - img);
+    a.o_blen = (uint32_t)(blen - img);
     a.n_blen = n_blen;
     a.ev_creator = h->ev_creator;
     a.ev_seq = h->ev_seq;
@@ -1246,7 +1251,7 @@ int add_batch_small(lx_index *h, uint32_t n, const uint32_t *creator, const uint
     a.s_cap = h->s_cap;
     a.mask = B > h->V ? 1u : 0u;
     if (h->small_timing) HIPCHK(h, hipEventRecord(h->ev[1], s));
-    HIPCHK(h, lx::launch_small(a, s));
+    HIPCHK(h, inl ? lx::launch_small_inline(h->sm_inl, s) : lx::launch_small(a, s));
     if (h->small_timing) HIPCHK(h, hipEventRecord(h->ev[2], s));
     if (B > h->V && h->n_cheat) {
         MarkArgs m{};
@@ -1290,7 +1295,8 @@ int lx_create(const lx_config *cfg, lx_index **out) {
     }
     if (h->shard_rank >= h->shard_count) { delete h; return LX_ERR_ARG; }
     if (hipSetDevice(h->device) != hipSuccess || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipMalloc((void **)&h->status, kStatusWords * 4) != hipSuccess) {
+        hipMalloc((void **)&h->status, kStatusWords * 4) != hipSuccess ||
+        hipMemset(h->status, 0, kStatusWords * 4) != hipSuccess) {
         delete h;
         return LX_ERR_HIP;
     }

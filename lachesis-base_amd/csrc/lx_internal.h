@@ -226,19 +226,24 @@ struct SmallArgs {
     uint64_t stride;
     uint32_t bs, n;              // first global index, events
     uint32_t B0, B;              // branches before / after the batch
-    const SmallEv *ev;
-    const uint32_t *par;         // parents (global), by q1.x
-    const uint32_t *perm;        // batch positions ordered by level
-    const uint32_t *lvl_off;     // n_levels + 1 offsets into perm
+    // staged image (uint32 words; records first, 16-B aligned): SmallEv[n], then
+    // at word offsets: parents (global, by q1.x), perm (batch positions ordered by
+    // level), level offsets (n_levels + 1), first seqs and creators of branches
+    // B0 .. B-1, (branch, events on it) pairs of the branches the batch touched
+    const uint32_t *img;         // device copy (NULL: the image is in the kernel arguments)
+    uint32_t o_par, o_perm, o_loff, o_nfirst, o_ncreator, o_blen;
     uint32_t n_levels;
-    const uint32_t *new_first;   // first seq of branches B0 .. B-1
-    const uint32_t *new_creator;
-    const uint32_t *blen;        // (branch, events on it) pairs of the branches the batch touched
     uint32_t n_blen;
     uint32_t *ev_creator, *ev_seq, *ev_branch, *ev_bbefore, *ev_sp, *first_child, *first_root;
     uint32_t *branch_first, *branch_creator, *branch_len, *brow;
     uint32_t s_cap;
     uint32_t mask;               // rows may carry fork marks (B > V)
+};
+// Batches whose image fits travel in the kernel arguments (no staging copy)
+constexpr uint32_t kSmallInline = 768;   // words (3 KB; kernel arguments stay < 4 KB)
+struct SmallInlineArgs {
+    SmallArgs a;
+    alignas(16) uint32_t img[kSmallInline];
 };
 
 // ---- write-back to the reference's byte formats (lx_persist.hip)
@@ -396,6 +401,7 @@ namespace lx {
 hipError_t launch_batch_prepare(const BatchArgs &a, void *scan_tmp, size_t scan_tmp_bytes, hipStream_t s);
 hipError_t launch_batch_finish(const BatchArgs &a, uint32_t jump_rounds, hipStream_t s);
 hipError_t launch_small(const SmallArgs &a, hipStream_t s);
+hipError_t launch_small_inline(const SmallInlineArgs &a, hipStream_t s);
 hipError_t scan_tmp_bytes(uint32_t n, size_t *bytes);
 hipError_t launch_undo_claims(const BatchArgs &a, hipStream_t s);
 hipError_t launch_index(const IndexArgs &a, hipStream_t s);

@@ -26,8 +26,11 @@
 namespace lx {
 
 template <bool MASKED>
-__global__ __launch_bounds__(256) void k_small(SmallArgs a) {
+__device__ __forceinline__ void small_body(const SmallArgs &a, const uint32_t *img) {
     constexpr uint32_t CW = kSmallCW, NQ = 256 / CW;
+    const SmallEv *ev = reinterpret_cast<const SmallEv *>(img);
+    const uint32_t *par = img + a.o_par, *perm = img + a.o_perm, *lvl_off = img + a.o_loff;
+    const uint32_t *new_first = img + a.o_nfirst, *new_creator = img + a.o_ncreator, *blen = img + a.o_blen;
     extern __shared__ uint32_t smem[];
     uint32_t *val = smem;                  // [n][CW]: HB seqs of the batch's events in own columns
     uint32_t *own = smem + a.n * CW;       // batch positions of the events on own branches
@@ -38,7 +41,7 @@ __global__ __launch_bounds__(256) void k_small(SmallArgs a) {
     const uint32_t c0 = blockIdx.x * CW;
     const uint32_t col = c0 + k;
     const bool valid = col < a.B;
-    const uint32_t first = !valid ? 1u : col >= a.B0 ? a.new_first[col - a.B0] : a.branch_first[col];
+    const uint32_t first = !valid ? 1u : col >= a.B0 ? new_first[col - a.B0] : a.branch_first[col];
     constexpr uint32_t mask = MASKED ? LX_SEQ_MASK : 0xFFFFFFFFu;
     const uint32_t bs = a.bs, n = a.n;
     const uint64_t stride = a.stride;
@@ -46,7 +49,7 @@ __global__ __launch_bounds__(256) void k_small(SmallArgs a) {
     if (t == 0) n_own = 0;
     if (blockIdx.x == 0) {
         for (uint32_t i = t; i < n; i += 256) {
-            const SmallEv e = a.ev[i];
+            const SmallEv e = ev[i];
             const uint32_t g = bs + i;
             a.ev_creator[g] = e.q2.x;
             a.ev_seq[g] = e.q0.y;
@@ -60,16 +63,16 @@ __global__ __launch_bounds__(256) void k_small(SmallArgs a) {
             }
         }
         for (uint32_t b = t; b < a.B - a.B0; b += 256) {
-            a.branch_first[a.B0 + b] = a.new_first[b];
-            a.branch_creator[a.B0 + b] = a.new_creator[b];
+            a.branch_first[a.B0 + b] = new_first[b];
+            a.branch_creator[a.B0 + b] = new_creator[b];
         }
-        for (uint32_t i = t; i < a.n_blen; i += 256) a.branch_len[a.blen[2 * i]] = a.blen[2 * i + 1];
+        for (uint32_t i = t; i < a.n_blen; i += 256) a.branch_len[blen[2 * i]] = blen[2 * i + 1];
     }
     __syncthreads();
     for (uint32_t i = t; i < n; i += 256) {
-        const uint4 q0 = a.ev[i].q0;
+        const uint4 q0 = ev[i].q0;
         if (q0.x >= c0 && q0.x < c0 + CW) {
-            a.brow[(uint64_t)q0.x * a.s_cap + (q0.y - a.ev[i].q1.y)] = bs + i;
+            a.brow[(uint64_t)q0.x * a.s_cap + (q0.y - ev[i].q1.y)] = bs + i;
             own[atomicAdd(&n_own, 1u)] = i;
         }
     }
@@ -88,18 +91,18 @@ __global__ __launch_bounds__(256) void k_small(SmallArgs a) {
     __syncthreads();
 
     for (uint32_t L = 0; L < a.n_levels; L++) {
-        const uint32_t lo = a.lvl_off[L], hi = a.lvl_off[L + 1];
+        const uint32_t lo = lvl_off[L], hi = lvl_off[L + 1];
         for (uint32_t j = lo + q; j < hi && valid; j += NQ) {
-            const uint32_t i = a.perm[j];
-            const uint4 q0 = a.ev[i].q0;
-            const uint32_t po = a.ev[i].q1.x;
+            const uint32_t i = perm[j];
+            const uint4 q0 = ev[i].q0;
+            const uint32_t po = ev[i].q1.x;
             const uint32_t br = q0.x, seq = q0.y, prev = q0.z, np = q0.w;
             uint32_t r = (col == br) ? seq : 0u;
             uint32_t p = 0;
             for (; p + 4 <= np; p += 4) {
                 uint32_t x[4], v[4];
 #pragma unroll
-                for (int u = 0; u < 4; u++) x[u] = a.par[po + p + u];
+                for (int u = 0; u < 4; u++) x[u] = par[po + p + u];
 #pragma unroll
                 for (int u = 0; u < 4; u++)
                     v[u] = x[u] >= bs ? val[(x[u] - bs) * CW + k] : a.hb[(uint64_t)x[u] * stride + col];
@@ -107,7 +110,7 @@ __global__ __launch_bounds__(256) void k_small(SmallArgs a) {
                 for (int u = 0; u < 4; u++) r = max(r, v[u] & mask);
             }
             for (; p < np; p++) {
-                const uint32_t x = a.par[po + p];
+                const uint32_t x = par[po + p];
                 const uint32_t v = x >= bs ? val[(x - bs) * CW + k] : a.hb[(uint64_t)x * stride + col];
                 r = max(r, v & mask);
             }
@@ -127,12 +130,32 @@ __global__ __launch_bounds__(256) void k_small(SmallArgs a) {
     }
 }
 
+template <bool MASKED>
+__global__ __launch_bounds__(256) void k_small(SmallArgs a) {
+    small_body<MASKED>(a, a.img);
+}
+
+// the image read straight from the kernel arguments (kernarg segment)
+template <bool MASKED>
+__global__ __launch_bounds__(256) void k_small_inline(SmallInlineArgs a) {
+    small_body<MASKED>(a.a, a.img);
+}
+
 hipError_t launch_small(const SmallArgs &a, hipStream_t s) {
     if (!a.n || !a.B) return hipSuccess;
     const uint32_t grid = (a.B + kSmallCW - 1) / kSmallCW;
     const size_t lds = (size_t)a.n * (kSmallCW + 1) * 4;
     if (a.mask) hipLaunchKernelGGL(k_small<true>, dim3(grid), dim3(256), lds, s, a);
     else hipLaunchKernelGGL(k_small<false>, dim3(grid), dim3(256), lds, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_small_inline(const SmallInlineArgs &a, hipStream_t s) {
+    if (!a.a.n || !a.a.B) return hipSuccess;
+    const uint32_t grid = (a.a.B + kSmallCW - 1) / kSmallCW;
+    const size_t lds = (size_t)a.a.n * (kSmallCW + 1) * 4;
+    if (a.a.mask) hipLaunchKernelGGL(k_small_inline<true>, dim3(grid), dim3(256), lds, s, a);
+    else hipLaunchKernelGGL(k_small_inline<false>, dim3(grid), dim3(256), lds, s, a);
     return hipGetLastError();
 }
 

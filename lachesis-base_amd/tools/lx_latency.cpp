@@ -319,3 +319,46 @@ int lx_bench_latency(int device, uint32_t V, const uint32_t *weights, uint64_t N
 }
 
 }  // extern "C"
+
+extern "C" {
+
+// Events/s of adding the DAG (its own Add order) in batches of `batch` events
+// through lx_add_batch + lx_flush (batch 1 = the reference's per-event Add of
+// IndexedLachesis.Process), one lx_sync at the end.  out[0] events/s, out[1]
+// seconds.
+int lx_bench_feed(int device, uint32_t V, const uint32_t *weights, uint64_t N, const uint32_t *creator,
+                  const uint32_t *seq, const uint64_t *poff, const uint32_t *par, uint32_t batch, double *out,
+                  char *err, uint32_t err_cap) {
+    lx_config cfg{};
+    cfg.device = device;
+    cfg.event_capacity = N;
+    lx_index *h = nullptr;
+    if (lx_create(&cfg, &h) || lx_reset(h, V, weights)) {
+        snprintf(err, err_cap, "create/reset: %s", h ? lx_last_error(h) : "");
+        if (h) lx_destroy(h);
+        return -1;
+    }
+    batch = std::max<uint32_t>(batch, 1);
+    auto t0 = clk::now();
+    for (uint64_t lo = 0; lo < N; lo += batch) {
+        const uint64_t hi = std::min<uint64_t>(N, lo + batch);
+        if (lx_add_batch(h, (uint32_t)(hi - lo), creator + lo, seq + lo, poff + lo, par, nullptr, nullptr)) {
+            snprintf(err, err_cap, "add: %s", lx_last_error(h));
+            lx_destroy(h);
+            return -1;
+        }
+        lx_flush(h);
+    }
+    if (lx_sync(h)) {
+        snprintf(err, err_cap, "sync: %s", lx_last_error(h));
+        lx_destroy(h);
+        return -1;
+    }
+    const double s = us_since(t0) * 1e-6;
+    out[0] = N / s;
+    out[1] = s;
+    lx_destroy(h);
+    return 0;
+}
+
+}  // extern "C"
