@@ -223,9 +223,11 @@ int lx_la_unpack_wire_dev(lx_index *h, uint32_t src_shard, const void *in_dev, u
  * communicator per shard handle, built from a unique id that rank 0 creates
  * and the caller distributes (as ncclGetUniqueId / ncclCommInitRank).
  * lx_shard_exchange = the LowestAfter all-to-all (pack each block on the
- * 1-byte wire when it fits, else at lx_shard_wire's width; the widths, then
- * the blocks, as grouped ncclSend/ncclRecv on the handle's stream; unpack;
- * own block);
+ * 1-byte wire when it fits, else at lx_shard_wire's width -- a destination
+ * that needed the wide width starts there next time, the byte wire is retried
+ * every 8th exchange; the widths, then the blocks at 4-byte aligned offsets
+ * (lx_shard_exchange_layout), as grouped ncclSend/ncclRecv on the handle's
+ * stream; unpack; own block);
  * lx_forkless_cause_sharded_dev = partial stake sums, an ncclAllReduce (sum,
  * uint32: exact, the true total fits 32 bits) and the quorum test, all
  * stream-ordered on the handle's stream.  Every rank must make the same calls
@@ -240,6 +242,13 @@ int lx_shard_comm_create(lx_index *h, const uint8_t id[128], uint32_t nranks, ui
 void lx_shard_comm_destroy(lx_shard_comm *c);
 const char *lx_shard_comm_last_error(const lx_shard_comm *c);
 int lx_shard_exchange(lx_shard_comm *c);
+/* Layout of one rank's exchange buffer (send or receive side): block q of
+ * entries[q] x width[q] bytes starts at off[q], a multiple of 4 bytes (the own
+ * block, q == self, is empty); off[G] = buffer bytes.  Host-only: every
+ * implementation of the exchange (lx_shard_exchange, the Python ShardedIndex,
+ * a Go shim doing its own collectives) lays blocks out this way. */
+int lx_shard_exchange_layout(uint32_t G, uint32_t self, const uint64_t *entries, const uint32_t *width,
+                             uint64_t *off);
 int lx_forkless_cause_sharded_dev(lx_shard_comm *c, uint64_t n, const uint32_t *a_dev, const uint32_t *b_dev,
                                   uint8_t *out_dev);
 

@@ -22,11 +22,13 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <functional>
 #include <mutex>
 #include <string>
 #include <vector>
 
 #include "lachesis_hip.h"
+#include "lx_shard_exchange.h"
 
 namespace {
 
@@ -94,6 +96,8 @@ struct lx_shard_comm {
     size_t send_cap = 0, recv_cap = 0;
     uint32_t *part = nullptr;                    // FC partial sums, grown on demand
     uint64_t part_cap = 0;
+    uint32_t *wdev = nullptr;                    // wire widths: [0, G) sent, [G, 2G) received
+    lx::ExchangeState xs;                        // byte-wire fallbacks remembered per destination
     std::string err;
 
     int fail(int code, const char *fmt, ...) {
@@ -197,6 +201,7 @@ void lx_shard_comm_destroy(lx_shard_comm *c) {
     (void)hipFree(c->send);
     (void)hipFree(c->recv);
     (void)hipFree(c->part);
+    (void)hipFree(c->wdev);
     delete c;
 }
 
@@ -204,81 +209,91 @@ const char *lx_shard_comm_last_error(const lx_shard_comm *c) {
     return c ? c->err.c_str() : g_create_error.c_str();   // NULL: why the last create failed
 }
 
+// the index side of the exchange driver (lx_shard_exchange.h) over the shard ABI
+struct RcclOps {
+    lx_shard_comm *c;
+    int block(uint32_t s, uint32_t d, uint64_t *n) { return c->index(lx_shard_block(c->ix, s, d, n), "lx_shard_block"); }
+    int wire(uint32_t *w) { return c->index(lx_shard_wire(c->ix, w), "lx_shard_wire"); }
+    int pack(uint32_t d, uint8_t *buf, uint32_t w) {
+        const int rc = lx_la_pack_wire_dev(c->ix, d, buf, w);
+        return rc == LX_ERR_WIRE ? rc : c->index(rc, "lx_la_pack_wire_dev");
+    }
+    int unpack(uint32_t s, const uint8_t *buf, uint32_t w) {
+        return c->index(lx_la_unpack_wire_dev(c->ix, s, buf, w), "lx_la_unpack_wire_dev");
+    }
+    int own() { return c->index(lx_la_own_dev(c->ix, nullptr), "lx_la_own_dev"); }
+    uint8_t *send_buf(size_t n) { return c->grow(&c->send, &c->send_cap, std::max<size_t>(n, 1)) ? nullptr : c->send; }
+    uint8_t *recv_buf(size_t n) { return c->grow(&c->recv, &c->recv_cap, std::max<size_t>(n, 1)) ? nullptr : c->recv; }
+};
+
+// the collectives: grouped ncclSend / ncclRecv on the index stream; ncclGroupEnd
+// is called on every path once ncclGroupStart succeeded (an error inside the
+// group must not leave the thread in RCCL group mode)
+struct RcclNet {
+    lx_shard_comm *c;
+    int group(const std::function<int()> &body) {
+        RcclApi &api = rccl();
+        int rc = c->nccl(api.GroupStart(), "ncclGroupStart");
+        if (rc) return rc;
+        rc = body();
+        const int rc2 = c->nccl(api.GroupEnd(), "ncclGroupEnd");
+        return rc ? rc : rc2;
+    }
+    int widths(const uint32_t *sw, uint32_t *rw) {
+        RcclApi &api = rccl();
+        const uint32_t G = c->nranks, r = c->rank;
+        LXC(c->hip(hipMemcpyAsync(c->wdev, sw, 4ull * G, hipMemcpyHostToDevice, c->stream), "hipMemcpyAsync"));
+        LXC(group([&] {
+            for (uint32_t q = 0; q < G; q++) {
+                if (q == r) continue;
+                LXC(c->nccl(api.Send(c->wdev + q, 1, ncclUint32, (int)q, c->comm, c->stream), "ncclSend"));
+                LXC(c->nccl(api.Recv(c->wdev + G + q, 1, ncclUint32, (int)q, c->comm, c->stream), "ncclRecv"));
+            }
+            return 0;
+        }));
+        LXC(c->hip(hipMemcpyAsync(rw, c->wdev + G, 4ull * G, hipMemcpyDeviceToHost, c->stream), "hipMemcpyAsync"));
+        return c->hip(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
+    }
+    int blocks(const uint8_t *send, const uint64_t *so, const uint64_t *sb, uint8_t *recv, const uint64_t *ro,
+               const uint64_t *rb) {
+        RcclApi &api = rccl();
+        const uint32_t G = c->nranks, r = c->rank;
+        return group([&] {
+            for (uint32_t q = 0; q < G; q++) {
+                if (q == r) continue;
+                // blocks may be empty (a shard without rows yet): zero-byte send/recv keep the pairing
+                LXC(c->nccl(api.Send(send + so[q], sb[q], ncclUint8, (int)q, c->comm, c->stream), "ncclSend"));
+                LXC(c->nccl(api.Recv(recv + ro[q], rb[q], ncclUint8, (int)q, c->comm, c->stream), "ncclRecv"));
+            }
+            return 0;
+        });
+    }
+};
+
 int lx_shard_exchange(lx_shard_comm *c) {
     if (!c) return LX_ERR_ARG;
-    RcclApi &api = rccl();
     LXC(c->hip(hipSetDevice(c->device), "hipSetDevice"));
-    const uint32_t r = c->rank, G = c->nranks;
+    const uint32_t G = c->nranks;
     if (G == 1) return 0;   // an unsharded handle holds whole LowestAfter rows already
-    uint32_t wb = 4;
-    LXC(c->index(lx_shard_wire(c->ix, &wb), "lx_shard_wire"));
-    // entry counts of every block, the send side laid out for the widest case
-    std::vector<uint64_t> sn(G, 0), rn(G, 0);
-    std::vector<size_t> so(G + 1, 0);
-    for (uint32_t q = 0; q < G; q++) {
-        if (q != r) {
-            LXC(c->index(lx_shard_block(c->ix, r, q, &sn[q]), "lx_shard_block"));
-            LXC(c->index(lx_shard_block(c->ix, q, r, &rn[q]), "lx_shard_block"));
-        }
-        so[q + 1] = so[q] + (size_t)sn[q] * wb;
+    if (!c->wdev) LXC(c->hip(hipMalloc(reinterpret_cast<void **>(&c->wdev), 8ull * G), "hipMalloc"));
+    RcclOps ops{c};
+    RcclNet net{c};
+    c->err.clear();
+    const int rc = lx::shard_exchange_run(ops, net, c->rank, G, c->xs);
+    if (rc) {
+        if (c->err.empty()) c->fail(rc, "exchange failed (%d): block sizes or wire widths disagree between ranks", rc);
+        return rc;
     }
-    LXC(c->grow(&c->send, &c->send_cap, std::max<size_t>(so[G], 1)));
-    // pack each block at 1 byte per entry when it fits (the pack checks), else
-    // at the epoch width; blocks are laid out back to back at their own widths
-    std::vector<uint32_t> sw(G, 0), rw(G, 0);
-    std::vector<size_t> sb(G, 0), rb(G, 0), ro(G + 1, 0);
-    size_t off = 0;
-    for (uint32_t q = 0; q < G; q++) {
-        so[q] = off;
-        if (q == r || !sn[q]) continue;
-        int rc = lx_la_pack_wire_dev(c->ix, q, c->send + off, 1);
-        sw[q] = 1;
-        if (rc == LX_ERR_WIRE) {
-            rc = lx_la_pack_wire_dev(c->ix, q, c->send + off, wb);
-            sw[q] = wb;
-        }
-        LXC(c->index(rc, "lx_la_pack_wire_dev"));
-        sb[q] = (size_t)sn[q] * sw[q];
-        off += sb[q];
-    }
-    // tell every peer the width of its block (one uint32 each way), then the blocks
-    uint8_t *wdev = nullptr;
-    size_t wcap = 0;
-    LXC(c->grow(&wdev, &wcap, 8ull * G));
-    LXC(c->hip(hipMemcpyAsync(wdev, sw.data(), 4ull * G, hipMemcpyHostToDevice, c->stream), "hipMemcpyAsync"));
-    int rc = c->nccl(api.GroupStart(), "ncclGroupStart");
-    for (uint32_t q = 0; q < G && !rc; q++) {
-        if (q == r) continue;
-        rc = c->nccl(api.Send(wdev + 4ull * q, 1, ncclUint32, (int)q, c->comm, c->stream), "ncclSend");
-        if (!rc) rc = c->nccl(api.Recv(wdev + 4ull * (G + q), 1, ncclUint32, (int)q, c->comm, c->stream), "ncclRecv");
-    }
-    if (!rc) rc = c->nccl(api.GroupEnd(), "ncclGroupEnd");
-    if (!rc) rc = c->hip(hipMemcpyAsync(rw.data(), wdev + 4ull * G, 4ull * G, hipMemcpyDeviceToHost, c->stream),
-                         "hipMemcpyAsync");
-    if (!rc) rc = c->hip(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
-    (void)hipFree(wdev);
-    if (rc) return rc;
-    for (uint32_t q = 0; q < G; q++) {
-        if (q != r && rn[q] && rw[q] != 1 && rw[q] != 2 && rw[q] != 4)
-            return c->fail(LX_ERR_STATE, "peer %u announced wire width %u", q, rw[q]);
-        rb[q] = q == r ? 0 : (size_t)rn[q] * rw[q];
-        ro[q + 1] = ro[q] + rb[q];
-    }
-    LXC(c->grow(&c->recv, &c->recv_cap, std::max<size_t>(ro[G], 1)));
-    LXC(c->nccl(api.GroupStart(), "ncclGroupStart"));
-    for (uint32_t q = 0; q < G; q++) {
-        if (q == r) continue;
-        // blocks may be empty (a shard without rows yet): zero-byte send/recv keep the pairing
-        LXC(c->nccl(api.Send(c->send + so[q], sb[q], ncclUint8, (int)q, c->comm, c->stream), "ncclSend"));
-        LXC(c->nccl(api.Recv(c->recv + ro[q], rb[q], ncclUint8, (int)q, c->comm, c->stream), "ncclRecv"));
-    }
-    LXC(c->nccl(api.GroupEnd(), "ncclGroupEnd"));
-    // the unpacks below run on the same stream, after the received bytes landed
-    for (uint32_t q = 0; q < G; q++)
-        if (rb[q])
-            LXC(c->index(lx_la_unpack_wire_dev(c->ix, q, c->recv + ro[q], rw[q]), "lx_la_unpack_wire_dev"));
-    LXC(c->index(lx_la_own_dev(c->ix, nullptr), "lx_la_own_dev"));
+    // the unpacks ran on the handle's stream after the received bytes landed
     return c->hip(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
+}
+
+// Block layout shared by every implementation of the exchange (lx_shard_exchange.h).
+int lx_shard_exchange_layout(uint32_t G, uint32_t self, const uint64_t *entries, const uint32_t *width,
+                             uint64_t *off) {
+    if (!G || self >= G || !entries || !width || !off) return LX_ERR_ARG;
+    lx::shard_layout(G, self, entries, width, off);
+    return 0;
 }
 
 int lx_forkless_cause_sharded_dev(lx_shard_comm *c, uint64_t n, const uint32_t *a, const uint32_t *b, uint8_t *out) {

@@ -62,6 +62,7 @@ SIGNATURES = [
     ("lx_shard_comm_destroy", None, [vp]),
     ("lx_shard_comm_last_error", ctypes.c_char_p, [vp]),
     ("lx_shard_exchange", ctypes.c_int, [vp]),
+    ("lx_shard_exchange_layout", ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint32, u64p, u32p, u64p]),
     ("lx_forkless_cause_sharded_dev", ctypes.c_int, [vp, ctypes.c_uint64, vp, vp, vp]),
     # include/lachesis_abft.h
     ("lx_abft_create", ctypes.c_int, [vp, ctypes.POINTER(vp)]),

@@ -32,6 +32,20 @@ try:
 except ImportError:          # the protocol tests load this module without the library
     LxError = RuntimeError
 LX_ERR_WIRE = -7             # include/lachesis_hip.h
+WIRE_RETRY = 8               # csrc/lx_shard_exchange.h kWireRetry
+
+
+def shard_layout(G, self_rank, entries, widths):
+    """Offsets of the blocks in one rank's exchange buffer (G + 1 entries):
+    block q holds entries[q] x widths[q] bytes starting at a multiple of 4
+    (the own block is empty) -- lx_shard_exchange_layout."""
+    off, o = [], 0
+    for q in range(G):
+        off.append(o)
+        if q != self_rank:
+            o += (entries[q] * widths[q] + 3) & ~3
+    off.append(o)
+    return off
 
 
 class ShardedIndex:
@@ -46,6 +60,8 @@ class ShardedIndex:
         # (a rehearsal mode for several ranks sharing one GPU; RCCL is the product)
         self.stage = dist.get_backend(group) == "gloo" and self.device.type == "cuda"
         self._bufs = {}
+        self._last_w = []        # width each destination got last time (byte-wire fallbacks)
+        self._count = 0
 
     def all_to_all(self, recv, send, recv_n, send_n):
         if self.stage:
@@ -67,51 +83,68 @@ class ShardedIndex:
     def exchange(self):
         """All-to-all of LowestAfter blocks; returns the entry counts sent.
 
-        Blocks travel as bytes.  With a library handle each block is packed at
-        1 byte per entry when every entry is within 127 of its row's seq (the
-        pack checks as it goes and reports LX_ERR_WIRE otherwise), else at the
-        epoch width (2 while every seq < 2^16, else 4); a G-int all-to-all
-        tells the receivers the widths before the blocks move."""
+        The protocol of lx_shard_exchange (csrc/lx_shard_exchange.h): blocks
+        travel as bytes, each at 1 byte per entry when every entry is within
+        127 of its row's seq (the pack checks as it goes and reports
+        LX_ERR_WIRE otherwise), else at the epoch width (2 while every seq <
+        2^16, else 4); a destination that needed the wide width starts there
+        next time (the byte wire is retried every WIRE_RETRY exchanges); a
+        G-int all-to-all tells the receivers the widths; every block starts at
+        a multiple of 4 bytes on both sides (shard_layout)."""
         r, G = self.rank, self.world
         send_n = [self.ix.shard_block(r, t) if t != r else 0 for t in range(G)]
         recv_n = [self.ix.shard_block(s, r) if s != r else 0 for s in range(G)]
         per_block = hasattr(self.ix, "la_pack_wire_dev")
         wb = self.ix.shard_wire_bytes() if hasattr(self.ix, "shard_wire_bytes") else 4
-        send_w = [wb if t != r else 0 for t in range(G)]
-        send = self._buf("send", sum(wb * x for x in send_n))   # room for the widest case
-        off = 0
+        if len(self._last_w) != G:
+            self._last_w = [0] * G
+        retry = self._count % WIRE_RETRY == 0
+        send_w = [0] * G
         for t in range(G):
-            if not send_n[t]:
-                continue
-            if per_block:
-                # byte wire first; the pack itself reports a misfit (LX_ERR_WIRE)
-                try:
-                    self.ix.la_pack_wire_dev(t, send.data_ptr() + off, 1)
-                    send_w[t] = 1
-                except LxError as e:
-                    if e.code != LX_ERR_WIRE:
-                        raise
-                    self.ix.la_pack_wire_dev(t, send.data_ptr() + off, wb)
-            else:
-                self.ix.la_pack_dev(t, send.data_ptr() + off)
-            off += send_w[t] * send_n[t]
-        recv_w = self._widths(send_w) if per_block else [wb] * G
-        send_b = [w * x for w, x in zip(send_w, send_n)]
-        recv_b = [w * x for w, x in zip(recv_w, recv_n)]
-        recv = self._buf("recv", sum(recv_b))
+            if t != r and send_n[t]:
+                send_w[t] = 1 if per_block and (self._last_w[t] <= 1 or retry) else wb
+        send = self._buf("send", shard_layout(G, r, send_n, [wb] * G)[-1])   # room for the widest case
+        q0 = 0
+        while q0 < G:
+            so = shard_layout(G, r, send_n, send_w)
+            q = q0
+            while q < G:
+                if q != r and send_n[q]:
+                    if per_block:
+                        try:
+                            self.ix.la_pack_wire_dev(q, send.data_ptr() + so[q], send_w[q])
+                        except LxError as e:
+                            if e.code != LX_ERR_WIRE or send_w[q] != 1:
+                                raise
+                            send_w[q] = wb          # later blocks shift: resume packing here
+                            break
+                    else:
+                        self.ix.la_pack_dev(q, send.data_ptr() + so[q])
+                q += 1
+            q0 = q
+        for t in range(G):
+            if t != r and send_n[t]:
+                self._last_w[t] = send_w[t]
+        self._count += 1
+        recv_w = self._widths(send_w) if per_block else [wb if s != r else 0 for s in range(G)]
+        for s in range(G):
+            if s != r and recv_n[s] and recv_w[s] not in (1, 2, 4):
+                raise RuntimeError("rank %d announced wire width %d" % (s, recv_w[s]))
+        ro = shard_layout(G, r, recv_n, recv_w)
+        send_b = [so[t + 1] - so[t] for t in range(G)]
+        recv_b = [ro[s + 1] - ro[s] for s in range(G)]
+        recv = self._buf("recv", ro[-1])
         self.ix.sync()   # packs run on the library stream; the collective on torch's
         if G > 1:
-            self.all_to_all(recv[:sum(recv_b)], send[:sum(send_b)], recv_b, send_b)
+            self.all_to_all(recv[:ro[-1]], send[:so[-1]], recv_b, send_b)
         if self.device.type == "cuda":
             torch.cuda.current_stream(self.device).synchronize()
-        off = 0
         for s in range(G):
-            if recv_b[s]:
+            if s != r and recv_n[s]:
                 if per_block:
-                    self.ix.la_unpack_wire_dev(s, recv.data_ptr() + off, recv_w[s])
+                    self.ix.la_unpack_wire_dev(s, recv.data_ptr() + ro[s], recv_w[s])
                 else:
-                    self.ix.la_unpack_dev(s, recv.data_ptr() + off)
-            off += recv_b[s]
+                    self.ix.la_unpack_dev(s, recv.data_ptr() + ro[s])
         self.ix.la_own_dev()     # own rows x own columns, no communication
         self.ix.sync()
         self.last_wire = (send_w, recv_w)

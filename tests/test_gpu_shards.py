@@ -226,3 +226,26 @@ def test_sharded_drop_and_reexchange(G):
         ix.add_batch(d.creator[cut:], d.seq[cut:], d.poff[cut:], d.par)
     exchange(shards)
     np.testing.assert_array_equal(fc(lx, shards, qa, qb), o.forkless_cause_batch(qa, qb))
+
+
+@pytest.mark.parametrize("G", [5, 7, 8])
+def test_sharded_config3_shape_zipf_cheaters(G):
+    """BASELINE configs[2]'s split (V = 1000, Zipf stakes floor(2^20/(i+1)),
+    P = 10) at G = 8 and the uneven G = 5 / 7, with 20 double-signers: the
+    column shards' ForklessCause equals the oracle's; the shard ranges
+    partition the creators (multiples of 4)."""
+    import lachesis_hip as lx
+    V = 1000
+    w = [(1 << 20) // (i + 1) for i in range(V)]
+    d = lx.tools.gen_dag(V, 5, 10, cheaters=20, forks=3, seed=G)
+    o = corc.OracleIndex(w)
+    assert o.add_batch(d.creator, d.seq, d.poff, d.par) == -1
+    assert o.num_branches() > V
+    qa, qb = lx.tools.fc_queries(d.lamport, 100_000, window=24, seed=G)
+    got, shards = sharded_fc(lx, d, w, G, qa, qb)
+    np.testing.assert_array_equal(got, o.forkless_cause_batch(qa, qb))
+    ranges = [shards[0].shard_range(r) for r in range(G)]
+    assert ranges[0][0] == 0 and ranges[-1][1] == V
+    assert all(ranges[i][1] == ranges[i + 1][0] and ranges[i][1] % 4 == 0 for i in range(G - 1))
+    for ix in shards:
+        ix.close()
