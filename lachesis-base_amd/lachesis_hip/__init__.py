@@ -8,7 +8,10 @@ vecfc/forkless_cause_test.go:
 * :class:`Index`      -- dense-index handle (what a cgo shim binds 1:1)
 * :class:`VecfcIndex` -- hash-keyed facade: ``reset(validators, get_event)``,
   ``add(e)``, ``flush()``, ``drop_not_flushed()``, ``forkless_cause(a, b)``,
-  ``get_highest_before(id)`` ... (vecfc/index.go, vecfc/forkless_cause.go)
+  ``get_highest_before(id)``, ``dfs_subgraph``, ``branches_info`` ...
+  (vecfc/index.go, vecfc/forkless_cause.go); ``new_index``,
+  ``new_index_with_engine``, ``default_config``, ``lite_config`` as in
+  vecfc/index.go:52-89
 * :mod:`batcher`      -- level-synchronous DAG batcher (include/lachesis_batcher.h):
   parents-first buffering, bulk release in topological levels
 * :mod:`emitter`      -- emitter/ancestor.QuorumIndexer over include/lachesis_emitter.h
@@ -20,7 +23,8 @@ built library raises, and every compute call goes to the GPU.
 """
 
 from .capi import Index, LxError, ShardComm, load_library, shard_comm_unique_id  # noqa: F401
-from .vecfc import VecfcIndex, HighestBeforeSeq, LowestAfterSeq, BranchSeq  # noqa: F401
+from .vecfc import (VecfcIndex, HighestBeforeSeq, LowestAfterSeq, BranchSeq, IndexConfig,  # noqa: F401
+                    IndexCacheConfig, Ratio, default_config, lite_config, new_index, new_index_with_engine)
 from . import tools  # noqa: F401
 from . import abft  # noqa: F401
 from . import emitter  # noqa: F401

@@ -123,3 +123,35 @@ class LevelBatcher:
             index.ids.append(e.id)
         self.last_levels = lev
         return events
+
+    def drain_all(self, index, validators, on_reject=None):
+        """Index everything releasable, one lx_add_batch per pop.  A batch is
+        all-or-nothing, but the reference processes events one at a time and
+        rejects only the bad one (abft/indexed_lachesis.go:69-82): when the
+        index refuses a batch at event k (its first offending event), the batch
+        is un-popped, event k is handed to ``on_reject(event, error)`` and
+        every other event is pushed back -- the next pop releases them again,
+        except k's descendants, which stay pending like events with a missing
+        parent in dagordering.EventsBuffer.  Returns the events indexed."""
+        done = []
+        while True:
+            if self.peek()[0] == 0:
+                return done
+            events, cr, sq, off, par, lev, first = self.pop()
+            assert first == len(index.ids), "index and batcher out of step"
+            try:
+                index.ix.add_batch(cr, sq, off, par)
+            except LxError as err:
+                self.unpop(events)
+                k = getattr(err, "index", 0xFFFFFFFF)
+                if k >= len(events):
+                    raise
+                if on_reject:
+                    on_reject(events[k], err)
+                self.push(events[:k] + events[k + 1:], validators)
+                continue
+            for e in events:
+                index.pos[e.id] = len(index.ids)
+                index.ids.append(e.id)
+            self.last_levels = lev
+            done.extend(events)

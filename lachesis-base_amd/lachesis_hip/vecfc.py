@@ -68,16 +68,83 @@ class LowestAfterSeq:
         return self.raw
 
 
+class Ratio:
+    """cachescale.Ratio (utils/cachescale/ratio.go:8-44): v * Target / Base, rounded up."""
+
+    def __init__(self, base=1, target=1):
+        self.base, self.target = base, target
+
+    def U64(self, v):
+        m = v * self.target
+        return m // self.base + (1 if m % self.base else 0)
+
+    I = U = U32 = U64
+
+
+IDENTITY = Ratio(1, 1)
+
+
+class IndexCacheConfig:
+    """vecfc.IndexCacheConfig (vecfc/index.go:15-20)."""
+
+    def __init__(self, forkless_cause_pairs, highest_before_seq_size, lowest_after_seq_size):
+        self.forkless_cause_pairs = forkless_cause_pairs
+        self.highest_before_seq_size = highest_before_seq_size
+        self.lowest_after_seq_size = lowest_after_seq_size
+
+
+class IndexConfig:
+    """vecfc.IndexConfig (vecfc/index.go:22-25).  The reference sizes its LRU
+    caches from it; the device planes replace those caches (vectors live in
+    HBM, ForklessCause(a, b) is never recomputed wrongly because it is
+    immutable once a is indexed), so it changes nothing here -- it is kept so
+    callers written against vecfc construct the index unchanged."""
+
+    def __init__(self, caches):
+        self.caches = caches
+
+
+def default_config(scale=IDENTITY):
+    """vecfc.DefaultConfig (vecfc/index.go:52-61)."""
+    return IndexConfig(IndexCacheConfig(scale.I(20000), scale.U(160 * 1024), scale.U(160 * 1024)))
+
+
+def lite_config():
+    """vecfc.LiteConfig (vecfc/index.go:63-66): DefaultConfig scaled 1/100."""
+    return default_config(Ratio(100, 1))
+
+
+def new_index(crit, config=None, device=0, event_capacity=0):
+    """vecfc.NewIndex (vecfc/index.go:68-78)."""
+    return VecfcIndex(device=device, event_capacity=event_capacity, crit=crit, config=config)
+
+
+def new_index_with_engine(crit, config, engine):
+    """vecfc.NewIndexWithEngine (vecfc/index.go:80-89): an index over an
+    existing engine -- here a :class:`lachesis_hip.Index` handle, which the
+    new facade shares (its epoch state is the engine's)."""
+    return VecfcIndex(crit=crit, config=config, engine=engine)
+
+
 class VecfcIndex:
     """vecfc.Index over the HIP library.  ``validators`` needs ``ids``,
     ``weights`` (idx order) and ``idxs`` (ValidatorID -> idx)."""
 
-    def __init__(self, device=0, event_capacity=0, crit=None):
-        self.ix = Index(device=device, event_capacity=event_capacity)
+    def __init__(self, device=0, event_capacity=0, crit=None, config=None, engine=None):
         self.crit = crit or self._panic
+        self.cfg = config or default_config()
         self.pos = {}
         self.ids = []
         self.n_flushed = 0
+        self.validators = None
+        self.get_event_fn = None
+        if isinstance(engine, VecfcIndex):
+            # a second vecfc.Index over the same engine: the device handle and the
+            # epoch's event map are shared (the reference shares its Engine)
+            self.ix, self.pos, self.ids = engine.ix, engine.pos, engine.ids
+            self.validators, self.get_event_fn = engine.validators, engine.get_event_fn
+        else:
+            self.ix = engine if engine is not None else Index(device=device, event_capacity=event_capacity)
 
     @staticmethod
     def _panic(err):
@@ -241,9 +308,28 @@ class VecfcIndex:
     def at_least_one_fork(self):
         return self.ix.at_least_one_fork()
 
-    # vecengine/index.go:59-62 (InitBranchesInfo): the library keeps BranchesInfo live
+    # vecengine/branches_info.go:15-25 (InitBranchesInfo): the library keeps
+    # BranchesInfo live on the device and the host (restored by restore())
     def init_branches_info(self):
         pass
+
+    # vecfc/index.go:107-130: the callbacks the reference's Engine calls.  The
+    # GPU engine computes and stores the vectors itself, so the setters are
+    # not part of its contract (crit); getters and constructors behave as the
+    # reference's.
+    def get_engine_callbacks(self):
+        def unsupported(*_):
+            self.crit(RuntimeError("the GPU engine stores vectors itself (Set* callbacks are not used)"))
+        return {
+            "GetHighestBefore": self.get_highest_before,
+            "GetLowestAfter": self.get_lowest_after,
+            "SetHighestBefore": unsupported,
+            "SetLowestAfter": unsupported,
+            "NewHighestBefore": lambda size: HighestBeforeSeq(bytes(8 * size)),
+            "NewLowestAfter": lambda size: LowestAfterSeq(bytes(4 * size)),
+            "OnDbReset": lambda db: None,
+            "OnDropNotFlushed": lambda: None,
+        }
 
     def get_event(self, eid):
         return self.get_event_fn(eid) if self.get_event_fn else None

@@ -68,3 +68,16 @@ def test_fc_query_window():
     qa, qb = tools.fc_queries(d.lamport, 5000, window=16, seed=3)
     la, lb = d.lamport[qa].astype(np.int64), d.lamport[qb].astype(np.int64)
     assert np.all(lb <= la) and np.all(lb >= la - 16)
+
+
+def test_vecfc_config_api():
+    """vecfc.DefaultConfig / LiteConfig (vecfc/index.go:52-66) with cachescale
+    rounding (utils/cachescale/ratio.go:18-25): LiteConfig's HighestBefore
+    cache is 1639 bytes."""
+    import lachesis_hip as lx
+    c = lx.default_config()
+    assert (c.caches.forkless_cause_pairs, c.caches.highest_before_seq_size, c.caches.lowest_after_seq_size) == \
+        (20000, 160 * 1024, 160 * 1024)
+    c = lx.lite_config()
+    assert (c.caches.forkless_cause_pairs, c.caches.highest_before_seq_size) == (200, 1639)
+    assert lx.Ratio(3, 2).U64(10) == 7

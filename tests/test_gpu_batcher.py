@@ -43,3 +43,46 @@ def test_batched_ingest_matches_oracle(shape):
     lam = np.array([e.lamport for e in released], dtype=np.uint32)
     qa, qb = lx.tools.fc_queries(lam, 50_000, window=32, seed=seed)
     np.testing.assert_array_equal(ix.ix.forkless_cause_batch(qa, qb), o.forkless_cause_batch(qa, qb))
+
+
+def test_drain_isolates_a_rejected_event():
+    """One event violating the eventcheck invariants (seq != self-parent seq + 1)
+    arrives among valid ones: drain_all rejects exactly it (the reference's
+    Process returns an error for that event only), indexes every event that
+    does not descend from it, and leaves its descendants pending; the indexed
+    part equals the oracle fed the same release order."""
+    import lachesis_hip as lx
+    nodes, events = tdag.rand_fork_dag(12, 20, 4, 0, 0, seed=4)
+    validators = pos.Validators.equal(nodes)
+    k = 60
+    e = events[k]
+    events = list(events)
+    events[k] = tdag.Event(e.id, e.creator, e.seq + 7, e.lamport, e.parents, e.name)
+    desc, frontier = set(), {e.id}
+    for x in events[k + 1:]:
+        if any(p in frontier for p in x.parents):
+            desc.add(x.id)
+            frontier.add(x.id)
+    ix = lx.VecfcIndex()
+    ix.reset(validators)
+    b = lx.batcher.LevelBatcher()
+    rng = np.random.default_rng(4)
+    order = rng.permutation(len(events))
+    rejected = []
+    for i in range(0, len(order), 37):
+        b.push([events[j] for j in order[i:i + 37]], validators)
+        b.drain_all(ix, validators, lambda ev, err: rejected.append((ev.id, err.code)))
+    assert rejected == [(e.id, -3)]
+    assert set(ix.ids) == {x.id for x in events} - {e.id} - desc
+    assert b.peek()[3] == len(desc) > 0
+    by_id = {x.id: x for x in events}
+    released = [by_id[x] for x in ix.ids]
+    o = corc.OracleIndex(validators.weights)
+    assert o.add_batch(*tdag.to_dense(released, validators)) == -1
+    for d in range(len(released)):
+        assert ix.ix.highest_before(d) == o.hb(d), d
+        assert ix.ix.lowest_after(d) == o.la(d), d
+    N = len(released)
+    a = np.repeat(np.arange(N, dtype=np.uint32), N)
+    c = np.tile(np.arange(N, dtype=np.uint32), N)
+    np.testing.assert_array_equal(ix.ix.forkless_cause_batch(a, c), o.forkless_cause_batch(a, c))

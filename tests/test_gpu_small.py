@@ -258,3 +258,40 @@ def test_batched_getters(lx, shape):
     with pytest.raises(lx.LxError):
         ix.merged_highest_before_batch([0, N])
     ix.close()
+
+
+def test_vecfc_api_surface(lx):
+    """vecfc.NewIndex(crit, LiteConfig()), NewIndexWithEngine over the same
+    engine, GetEngineCallbacks, BranchesInfo and DfsSubgraph through the
+    facade (vecfc/index.go:52-130, vecengine/branches_info.go:15-53,
+    vecengine/traversal.go:10-37) agree with the Python reference restatement."""
+    from oracle import pos, tdag
+    from oracle import vecfc_oracle as vo
+    nodes, evs = tdag.rand_fork_dag(8, 15, 4, cheaters=2, forks_count=4, seed=6)
+    validators = pos.Validators.equal(nodes)
+    store = {e.id: e for e in evs}
+    crits = []
+    g = lx.new_index(crits.append, lx.lite_config())
+    g.reset(validators, store.get)
+    o = vo.Index()
+    o.reset(validators, store.get)
+    for e in evs:
+        g.add(e)
+        o.add(e)
+    g2 = lx.new_index_with_engine(crits.append, lx.lite_config(), g)
+    cb = g2.get_engine_callbacks()
+    for e in evs[::5]:
+        assert cb["GetHighestBefore"](e.id).to_bytes() == o.get_highest_before(e.id).to_bytes()
+        assert cb["GetLowestAfter"](e.id).to_bytes() == o.get_lowest_after(e.id).to_bytes()
+    assert cb["NewHighestBefore"](5).to_bytes() == bytes(40) and cb["NewLowestAfter"](5).to_bytes() == bytes(20)
+    cb["SetHighestBefore"](evs[0].id, None)
+    assert len(crits) == 1
+    last, creators, by = g2.branches_info()
+    bi = o.branches_info()
+    assert (last, creators, by) == (list(bi.last_seq), list(bi.creator_idxs), [list(x) for x in bi.by_creators])
+    g2.init_branches_info()
+    head = evs[-1]
+    seen_g, seen_o = [], []
+    g2.dfs_subgraph(head, lambda x: (seen_g.append(x), True)[1] if seen_g.count(x) == 0 else False)
+    o.dfs_subgraph(head, lambda x: (seen_o.append(x), True)[1] if seen_o.count(x) == 0 else False)
+    assert seen_g == seen_o and len(seen_g) > 10
