@@ -113,6 +113,39 @@ struct Frame {
     }
 };
 
+// The host-to-device uploads of one step (frame metadata, candidates,
+// cheater columns) go out together: data and descriptors are gathered on the
+// host, copied into a pinned, device-mapped staging slot, and one k_scatter
+// launch moves them (a hipMemcpyAsync from pageable memory per array cost
+// ~10 us each, ~250 per epoch at C5).
+struct Uploader {
+    static constexpr int kSlots = 4;
+    uint8_t *pin[kSlots] = {};
+    uint64_t cap[kSlots] = {};
+    hipEvent_t done[kSlots] = {};
+    bool used[kSlots] = {};
+    int next = 0;
+    std::vector<uint8_t> data;
+    std::vector<ScatterDesc> desc;
+    uint64_t launches = 0;
+    void add(void *dst, const void *src, uint64_t bytes) {
+        if (!bytes) return;
+        const uint64_t off = data.size();
+        data.resize(off + (bytes + 15) / 16 * 16);
+        memcpy(data.data() + off, src, bytes);
+        desc.push_back(ScatterDesc{dst, off, bytes});
+    }
+    bool pending() const { return !desc.empty(); }
+    void release() {
+        for (int k = 0; k < kSlots; k++) {
+            if (pin[k]) (void)hipHostFree(pin[k]);
+            if (done[k]) (void)hipEventDestroy(done[k]);
+            pin[k] = nullptr;
+            done[k] = nullptr;
+        }
+    }
+};
+
 }  // namespace
 
 struct lx_abft {
@@ -132,6 +165,11 @@ struct lx_abft {
     std::vector<uint32_t> par;
 
     BufPool pool;                       // recycled device buffers (all DVecs below)
+    Uploader up;                        // batched host-to-device uploads of a step
+    uint8_t *q_pin = nullptr;           // k_root_quorum answers, pinned and device-mapped
+    uint64_t q_pin_cap = 0;
+    uint32_t *rb_pin = nullptr;         // k_readback target (decisions + error word, atropos HB row)
+    uint64_t rb_cap = 0;
     std::vector<Frame> frames;          // [0] unused
     DVec<uint32_t> arena;               // bit rows (observed roots) of k_root_fc launches
     uint64_t arena_used = 0;
@@ -148,6 +186,7 @@ struct lx_abft {
     bool dec_dirty = true;
     uint32_t vw = 0;                    // subject window [0, vw) of the current election
     uint32_t spec_depth = kSpecDepth;
+    bool trace = getenv("LX_ABFT_TRACE") != nullptr;   // per-launch shapes on stderr (diagnostics)
 
     lx_abft_stats stats{};
 
@@ -183,9 +222,12 @@ struct lx_abft {
 
 namespace {
 
+int flush_uploads(lx_abft *a, hipStream_t s);
+
 template <typename T>
 int reserve(lx_abft *a, DVec<T> &v, uint64_t n, uint64_t keep, hipStream_t s) {
     if (n <= v.cap) return 0;
+    if (a->up.pending()) ARC(flush_uploads(a, s));   // their destinations may be about to move
     uint64_t cap = std::max<uint64_t>({n, v.cap + v.cap / 2, 256});
     uint64_t got = 0;
     T *p = static_cast<T *>(a->pool.take(cap * sizeof(T), &got));
@@ -202,8 +244,70 @@ int reserve(lx_abft *a, DVec<T> &v, uint64_t n, uint64_t keep, hipStream_t s) {
 template <typename T>
 int upload(lx_abft *a, DVec<T> &v, const std::vector<T> &h, uint64_t from, hipStream_t s) {
     ARC(reserve(a, v, h.size(), from, s));
-    if (h.size() > from)
-        AHIP(a, hipMemcpyAsync(v.p + from, h.data() + from, (h.size() - from) * sizeof(T), hipMemcpyHostToDevice, s));
+    if (h.size() > from) a->up.add(v.p + from, h.data() + from, (h.size() - from) * sizeof(T));
+    return 0;
+}
+
+// the step's uploads in one k_scatter launch (stream-ordered before the
+// kernels that read them)
+int flush_uploads(lx_abft *a, hipStream_t s) {
+    Uploader &u = a->up;
+    if (!u.pending()) return 0;
+    const int k = u.next;
+    u.next = (u.next + 1) % Uploader::kSlots;
+    if (!u.done[k]) AHIP(a, hipEventCreateWithFlags(&u.done[k], hipEventDisableTiming));
+    if (u.used[k]) AHIP(a, hipEventSynchronize(u.done[k]));
+    const uint64_t dbytes = u.desc.size() * sizeof(ScatterDesc);
+    const uint64_t need = dbytes + u.data.size();
+    if (need > u.cap[k]) {
+        if (u.pin[k]) (void)hipHostFree(u.pin[k]);
+        u.pin[k] = nullptr;
+        u.cap[k] = 0;
+        const uint64_t cap = std::max<uint64_t>(need * 2, 1u << 16);
+        AHIP(a, hipHostMalloc((void **)&u.pin[k], cap, hipHostMallocMapped));
+        u.cap[k] = cap;
+    }
+    uint64_t max_bytes = 0;
+    for (auto &d : u.desc) {
+        d.src_off += dbytes;
+        max_bytes = std::max<uint64_t>(max_bytes, d.bytes);
+    }
+    memcpy(u.pin[k], u.desc.data(), dbytes);
+    memcpy(u.pin[k] + dbytes, u.data.data(), u.data.size());
+    void *dp = nullptr;
+    AHIP(a, hipHostGetDevicePointer(&dp, u.pin[k], 0));
+    const uint8_t *base = static_cast<const uint8_t *>(dp);
+    AHIP(a, lx::launch_scatter(reinterpret_cast<const ScatterDesc *>(base), (uint32_t)u.desc.size(), max_bytes, base,
+                               s));
+    AHIP(a, hipEventRecord(u.done[k], s));
+    u.used[k] = true;
+    u.launches++;
+    u.desc.clear();
+    u.data.clear();
+    return 0;
+}
+
+// words [0, na) of a and [0, nb) of b (device) into a->rb_pin, then wait for
+// the stream: the host reads them at the returned pointer
+int readback(lx_abft *a, hipStream_t s, const uint32_t *x, uint32_t na, const uint32_t *y, uint32_t nb,
+             const uint32_t **out) {
+    const uint64_t need = (uint64_t)na + nb;
+    if (need > a->rb_cap) {
+        if (a->rb_pin) {
+            AHIP(a, hipStreamSynchronize(s));
+            (void)hipHostFree(a->rb_pin);
+        }
+        a->rb_pin = nullptr;
+        a->rb_cap = 0;
+        const uint64_t cap = std::max<uint64_t>(need * 2, 4096);
+        AHIP(a, hipHostMalloc((void **)&a->rb_pin, cap * 4, hipHostMallocMapped));
+        a->rb_cap = cap;
+    }
+    void *dp = nullptr;
+    AHIP(a, hipHostGetDevicePointer(&dp, a->rb_pin, 0));
+    AHIP(a, lx::launch_readback(static_cast<uint32_t *>(dp), x, na, y, nb, s));
+    AHIP(a, hipStreamSynchronize(s));
+    *out = a->rb_pin;
     return 0;
 }
 
@@ -303,10 +407,22 @@ int eval_frame(lx_abft *a, const IndexView &iv, uint32_t f, const std::vector<ui
     ARC(reserve(a, a->arena, a->arena_used + (uint64_t)n * words + 1, a->arena_used, s));
     ARC(reserve(a, a->d_cand, n, 0, s));
     ARC(reserve(a, a->d_q, n, 0, s));
-    AHIP(a, hipMemcpyAsync(a->d_cand.p, cand.data(), n * 4ull, hipMemcpyHostToDevice, s));
+    a->up.add(a->d_cand.p, cand.data(), n * 4ull);
     uint32_t *bits = a->arena.p + a->arena_used;
     if (words) {
         ARC(refresh_cheaters(a, iv));
+        if (n > a->q_pin_cap) {
+            if (a->q_pin) {
+                AHIP(a, hipStreamSynchronize(s));
+                (void)hipHostFree(a->q_pin);
+            }
+            a->q_pin = nullptr;
+            a->q_pin_cap = 0;
+            AHIP(a, hipHostMalloc((void **)&a->q_pin, std::max<uint64_t>(n, 4096), hipHostMallocMapped));
+            a->q_pin_cap = std::max<uint64_t>(n, 4096);
+        }
+        void *q_dev = nullptr;
+        AHIP(a, hipHostGetDevicePointer(&q_dev, a->q_pin, 0));
         // split the columns when the tiles alone cannot fill the chip
         const uint32_t ncols = (iv.V + 31) / 32 * 32;
         const uint32_t splits = lx::root_fc_splits(n, R, ncols);
@@ -334,6 +450,8 @@ int eval_frame(lx_abft *a, const IndexView &iv, uint32_t f, const std::vector<ui
         r.words = words;
         r.col_split = col_split;
         r.n_split = n_split;
+        ARC(flush_uploads(a, s));
+        if (a->trace) fprintf(stderr, "root_fc f=%u cand=%u roots=%u splits=%u col_split=%u\n", f, n, R, n_split, col_split);
         AHIP(a, lx::launch_root_fc(r, iv.B > iv.V, s));
         QuorumArgs qa{};
         qa.psum = a->d_psum.p;
@@ -348,11 +466,10 @@ int eval_frame(lx_abft *a, const IndexView &iv, uint32_t f, const std::vector<ui
         qa.dup = fr.d_dup.p;
         qa.wcreator = iv.wpad;
         qa.quorum = a->quorum;
-        qa.q = a->d_q.p;
+        qa.q = static_cast<uint8_t *>(q_dev);   // answers land in pinned host memory
         AHIP(a, lx::launch_root_quorum(qa, s));
-        q.resize(n);
-        AHIP(a, hipMemcpyAsync(q.data(), a->d_q.p, n, hipMemcpyDeviceToHost, s));
         AHIP(a, hipStreamSynchronize(s));
+        q.assign(a->q_pin, a->q_pin + n);
         a->stats.fc_launches++;
         a->stats.fc_pairs += (uint64_t)n * R;
     } else {
@@ -515,6 +632,7 @@ int vote_slots(lx_abft *a, const IndexView &iv, uint32_t F, uint32_t g, uint32_t
     v.votes = fg.votes.p + (uint64_t)from * a->V;
     v.dec = a->d_dec.p;
     v.err = a->d_err.p;
+    ARC(flush_uploads(a, s));
     AHIP(a, lx::launch_votes(v, to - from, g == F + 1, s));
     a->stats.vote_launches++;
     return 0;
@@ -544,11 +662,11 @@ int widen_window(lx_abft *a, const IndexView &iv, uint32_t F, uint32_t nw) {
 // decision of election F: 0 pending, 1 decided (*t, *atropos slot),
 // 2 every subject of the window decided "no" (widen it)
 int check_decision(lx_abft *a, const IndexView &iv, uint32_t F, uint64_t *t, uint32_t *obs, int *state) {
+    const uint32_t *rb = nullptr;
+    ARC(readback(a, iv.stream, reinterpret_cast<const uint32_t *>(a->d_dec.p), 2 * a->vw, a->d_err.p, 1, &rb));
     std::vector<unsigned long long> dec(a->vw);
-    uint32_t err = 0;
-    AHIP(a, hipMemcpyAsync(dec.data(), a->d_dec.p, a->vw * 8ull, hipMemcpyDeviceToHost, iv.stream));
-    AHIP(a, hipMemcpyAsync(&err, a->d_err.p, 4, hipMemcpyDeviceToHost, iv.stream));
-    AHIP(a, hipStreamSynchronize(iv.stream));
+    memcpy(dec.data(), rb, a->vw * 8ull);
+    const uint32_t err = rb[2 * a->vw];
     if (err & kVoteErrTwoRoots)
         return a->fail(LX_ERR_BYZANTINE, "forkless caused by 2 fork roots => more than 1/3W are Byzantine (election frame=%u)", F);
     if (err & kVoteErrQuorum)
@@ -589,10 +707,9 @@ int reset_election(lx_abft *a, const IndexView &iv) {
 int apply_block(lx_abft *a, const IndexView &iv, uint32_t F, uint32_t atropos, bool *sealed,
                 std::vector<uint32_t> *new_w) {
     *sealed = false;
-    std::vector<uint32_t> row(a->V), cheaters;
-    AHIP(a, hipMemcpyAsync(row.data(), iv.hb + (uint64_t)atropos * iv.stride, a->V * 4ull, hipMemcpyDeviceToHost,
-                           iv.stream));
-    AHIP(a, hipStreamSynchronize(iv.stream));
+    std::vector<uint32_t> cheaters;
+    const uint32_t *row = nullptr;
+    ARC(readback(a, iv.stream, iv.hb + (uint64_t)atropos * iv.stride, a->V, nullptr, 0, &row));
     for (uint32_t c = 0; c < a->V; c++)
         if (row[c] & LX_MARK) cheaters.push_back(c);   // GetMergedHighestBefore(atropos)[c].IsForkDetected()
     if (!a->cb.begin_block) return 0;   // BeginBlock == nil: no confirmation, no seal (lachesis.go:69-71)
@@ -812,6 +929,9 @@ void lx_abft_destroy(lx_abft *a) {
     a->d_kflag.release();
     a->d_kw.release();
     (void)hipDeviceSynchronize();   // queued work may still use pooled buffers
+    a->up.release();
+    if (a->q_pin) (void)hipHostFree(a->q_pin);
+    if (a->rb_pin) (void)hipHostFree(a->rb_pin);
     a->pool.drain();
     delete a;
 }

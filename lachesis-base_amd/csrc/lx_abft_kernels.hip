@@ -363,4 +363,55 @@ hipError_t launch_votes(const VoteArgs &a, uint32_t n_voters, bool round1, hipSt
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------- k_scatter
+// The host-to-device uploads of one abft step in one launch: descriptors and
+// data sit in one pinned, device-mapped staging slot (read once over the bus);
+// workgroup (i, c) copies words [c*1024, c*1024+1024) of segment i (4-byte
+// words; every upload is a uint32 or uint64 array).  Every word is read by its
+// own load and the four loads of a thread are issued before any store, so the
+// whole launch waits about one bus round trip, not one per 256 words.
+constexpr uint32_t kScatterChunk = 1024;
+
+__global__ __launch_bounds__(256) void k_scatter(const ScatterDesc *d, const uint8_t *base) {
+    const ScatterDesc x = d[blockIdx.x];
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(base + x.src_off);
+    uint32_t *dst = reinterpret_cast<uint32_t *>(x.dst);
+    const uint64_t nw = x.bytes / 4, w0 = (uint64_t)blockIdx.y * kScatterChunk + threadIdx.x;
+    if (w0 >= nw) return;
+    uint32_t v[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) v[u] = w0 + u * 256 < nw ? src[w0 + u * 256] : 0u;
+#pragma unroll
+    for (int u = 0; u < 4; u++)
+        if (w0 + u * 256 < nw) dst[w0 + u * 256] = v[u];
+}
+
+hipError_t launch_scatter(const ScatterDesc *desc, uint32_t n, uint64_t max_bytes, const uint8_t *base,
+                          hipStream_t s) {
+    if (!n || !max_bytes) return hipSuccess;
+    const uint64_t chunks = (max_bytes / 4 + kScatterChunk - 1) / kScatterChunk;
+    if (chunks > 65535) return hipErrorInvalidValue;   // 256 MB per upload: far beyond any abft step
+    hipLaunchKernelGGL(k_scatter, dim3(n, (uint32_t)chunks), dim3(256), 0, s, desc, base);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------- k_readback
+// Small device results (decision words, error flags, one HB row) written
+// straight into pinned, device-mapped host memory: one launch instead of a
+// blit copy per array through a pageable staging buffer.
+__global__ __launch_bounds__(256) void k_readback(uint32_t *dst, const uint32_t *a, uint32_t na, const uint32_t *b,
+                                                  uint32_t nb) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i < na) dst[i] = a[i];
+    else if (i < na + nb) dst[i] = b[i - na];
+}
+
+hipError_t launch_readback(uint32_t *dst, const uint32_t *a, uint32_t na, const uint32_t *b, uint32_t nb,
+                           hipStream_t s) {
+    const uint32_t n = na + nb;
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_readback, dim3((n + 255) / 256), dim3(256), 0, s, dst, a, na, b, nb);
+    return hipGetLastError();
+}
+
 }  // namespace lx

@@ -378,6 +378,13 @@ constexpr uint32_t kVoteVoted = 0x80000000u, kVoteYes = 0x40000000u, kVoteDecide
                    kVoteNoRoot = 0x1FFFFFFFu;
 constexpr uint32_t kVoteErrMissing = 1, kVoteErrTwoRoots = 2, kVoteErrQuorum = 4;
 
+// one host-to-device segment of an abft step's batched upload (k_scatter)
+struct ScatterDesc {
+    void *dst;
+    uint64_t src_off;            // into the staging slot
+    uint64_t bytes;              // a multiple of 4
+};
+
 struct VoteArgs {
     uint32_t V;
     const uint32_t *voter_ev;    // per voter slot (NONE = skip)
@@ -438,6 +445,10 @@ uint32_t root_fc_splits(uint32_t n_cand, uint32_t n_roots, uint32_t ncols);
 hipError_t launch_root_fc(const RootFcArgs &a, bool forks, hipStream_t s);
 hipError_t launch_root_quorum(const QuorumArgs &a, hipStream_t s);
 hipError_t launch_votes(const VoteArgs &a, uint32_t n_voters, bool round1, hipStream_t s);
+hipError_t launch_scatter(const ScatterDesc *desc, uint32_t n, uint64_t max_bytes, const uint8_t *base,
+                          hipStream_t s);
+hipError_t launch_readback(uint32_t *dst, const uint32_t *a, uint32_t na, const uint32_t *b, uint32_t nb,
+                           hipStream_t s);
 hipError_t launch_copy_rows(uint32_t *dst, uint64_t dst_stride, const uint32_t *src, uint64_t src_stride,
                             uint64_t rows, uint64_t cols, hipStream_t s);
 }  // namespace lx
