@@ -104,6 +104,8 @@ typedef struct lx_abft_stats {
     float ms_blocks;     /* cheaters, confirmation DFS, callbacks */
     uint32_t frame_steps, fc_launches, vote_launches, blocks;
     uint64_t fc_pairs;   /* (event, root) pairs evaluated */
+    uint64_t fc_pair_cols;   /* pairs x validator columns compared by k_root_fc */
+    float ms_root_fc_gpu;    /* k_root_fc time on the stream (HIP events around each launch) */
 } lx_abft_stats;
 int lx_abft_last_stats(const lx_abft *a, lx_abft_stats *out);
 

@@ -170,6 +170,7 @@ struct lx_abft {
     uint64_t q_pin_cap = 0;
     uint32_t *rb_pin = nullptr;         // k_readback target (decisions + error word, atropos HB row)
     uint64_t rb_cap = 0;
+    hipEvent_t ev_fc[2] = {};           // around each k_root_fc launch (stats.ms_root_fc_gpu)
     std::vector<Frame> frames;          // [0] unused
     DVec<uint32_t> arena;               // bit rows (observed roots) of k_root_fc launches
     uint64_t arena_used = 0;
@@ -452,7 +453,13 @@ int eval_frame(lx_abft *a, const IndexView &iv, uint32_t f, const std::vector<ui
         r.n_split = n_split;
         ARC(flush_uploads(a, s));
         if (a->trace) fprintf(stderr, "root_fc f=%u cand=%u roots=%u splits=%u col_split=%u\n", f, n, R, n_split, col_split);
+        if (!a->ev_fc[0]) {
+            AHIP(a, hipEventCreate(&a->ev_fc[0]));
+            AHIP(a, hipEventCreate(&a->ev_fc[1]));
+        }
+        AHIP(a, hipEventRecord(a->ev_fc[0], s));
         AHIP(a, lx::launch_root_fc(r, iv.B > iv.V, s));
+        AHIP(a, hipEventRecord(a->ev_fc[1], s));
         QuorumArgs qa{};
         qa.psum = a->d_psum.p;
         qa.n_split = n_split;
@@ -470,8 +477,12 @@ int eval_frame(lx_abft *a, const IndexView &iv, uint32_t f, const std::vector<ui
         AHIP(a, lx::launch_root_quorum(qa, s));
         AHIP(a, hipStreamSynchronize(s));
         q.assign(a->q_pin, a->q_pin + n);
+        float ms = 0;
+        AHIP(a, hipEventElapsedTime(&ms, a->ev_fc[0], a->ev_fc[1]));
+        a->stats.ms_root_fc_gpu += ms;
         a->stats.fc_launches++;
         a->stats.fc_pairs += (uint64_t)n * R;
+        a->stats.fc_pair_cols += (uint64_t)n * R * iv.V;
     } else {
         q.assign(n, 0);   // no roots in frame f: no quorum (WeightCounter of nothing)
     }
@@ -932,6 +943,8 @@ void lx_abft_destroy(lx_abft *a) {
     a->up.release();
     if (a->q_pin) (void)hipHostFree(a->q_pin);
     if (a->rb_pin) (void)hipHostFree(a->rb_pin);
+    for (hipEvent_t e : a->ev_fc)
+        if (e) (void)hipEventDestroy(e);
     a->pool.drain();
     delete a;
 }

@@ -159,7 +159,8 @@ __global__ __launch_bounds__(256) void k_root_fc(RootFcArgs a) {
 uint32_t root_fc_splits(uint32_t n_cand, uint32_t n_roots, uint32_t ncols) {
     // enough workgroups to fill 256 CUs x 4, at least 4 LDS chunks per split
     const uint32_t tiles = ((n_roots + kTile - 1) / kTile) * ((n_cand + kTile - 1) / kTile);
-    uint32_t s = tiles ? (1024 + tiles - 1) / tiles : 1;
+    static const uint32_t target = getenv("LX_ROOTFC_WGS") ? (uint32_t)atoi(getenv("LX_ROOTFC_WGS")) : 1024u;
+    uint32_t s = tiles ? (target + tiles - 1) / tiles : 1;
     const uint32_t max_s = ncols / (4 * kKc) ? ncols / (4 * kKc) : 1;
     return s < 1 ? 1 : (s > max_s ? max_s : s);
 }

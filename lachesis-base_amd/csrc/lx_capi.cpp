@@ -169,6 +169,7 @@ struct lx_index {
     bool small_timing = false;             // LX_TIMING=1: time small-path launches (two event records)
     uint32_t diag_nofill = 0;   // LX_DIAG_NOFILL=1: timing-only build of the walker (LA left empty)
     uint32_t cpw_hint = 0, ncw_hint = 0;   // LX_CPW / LX_NCW tuning overrides
+    uint32_t lean = 0, lean_ncw = 4;       // LX_WALKER=lean: quad-per-event compute waves (LX_LEAN_NCW)
     uint32_t rr_hint = 0, diag = 0;        // LX_RR record ring depth; LX_DIAG timing-only modes
     bool prof = false;                     // LX_PROF=1: per-wave walker counters to stderr
     uint32_t small = 0;                    // LX_SMALL=1: small-LDS walker (several workgroups per CU)
@@ -651,6 +652,8 @@ int add_batch_dev(lx_index *h, uint32_t n, const uint32_t *creator, const uint32
     ia.diag = h->diag;
     ia.small = h->small;
     ia.ncw_hint = h->ncw_hint;
+    ia.lean = h->lean;
+    ia.lean_ncw = h->lean_ncw;
     // antichain width of tdag-like DAGs ~ V / (1.6 P); P from the batch
     {
         uint32_t pbar = std::max<uint32_t>(1, (uint32_t)((h->last_npar + n - 1) / n));
@@ -686,8 +689,8 @@ int add_batch_dev(lx_index *h, uint32_t n, const uint32_t *creator, const uint32
                     w, q[9] / nb / 100.0, q[8] / nb, q[0] / nb, q[1] / nb, q[2] / nb, q[3] / nb, q[4] / nb, q[5] / nb, q[6] / nb,
                     q[7] / nb, q[9] * 10.0 / (q[8] > 0 ? q[8] : 1));
             if (q[14] > 0)
-                fprintf(stderr, "[lx_prof] wave %d cycles/pass: fetch=%.0f fold=%.0f ovf=%.0f complete=%.0f total=%.0f\n", w,
-                        q[10] / q[8], q[11] / q[8], q[12] / q[8], q[13] / q[8], q[14] / q[8]);
+                fprintf(stderr, "[lx_prof] wave %d cycles/pass: fetch=%.0f (record rt %.0f) fold=%.0f (ring rt %.0f) ovf=%.0f complete=%.0f total=%.0f\n", w,
+                        q[10] / q[8], q[5] / q[8], q[11] / q[8], q[15] / q[8], q[12] / q[8], q[13] / q[8], q[14] / q[8]);
         }
     }
     if (h->B > h->V && h->n_cheat) {
@@ -1303,6 +1306,8 @@ int lx_create(const lx_config *cfg, lx_index **out) {
     if (const char *d = getenv("LX_DIAG_NOFILL")) h->diag_nofill = (d[0] == '1');
     if (const char *d = getenv("LX_CPW")) h->cpw_hint = (uint32_t)atoi(d);
     if (const char *d = getenv("LX_NCW")) h->ncw_hint = (uint32_t)atoi(d);
+    if (const char *d = getenv("LX_WALKER")) h->lean = strcmp(d, "lean") == 0;
+    if (const char *d = getenv("LX_LEAN_NCW")) h->lean_ncw = (uint32_t)atoi(d);
     if (const char *d = getenv("LX_RR")) h->rr_hint = (uint32_t)atoi(d);
     if (const char *d = getenv("LX_DIAG")) h->diag = (uint32_t)atoi(d);
     if (const char *d = getenv("LX_PROF")) h->prof = (d[0] == '1');

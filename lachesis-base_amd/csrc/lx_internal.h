@@ -66,6 +66,8 @@ struct IndexArgs {
     const uint32_t *cmap;        // sharded: global branch -> plane column (NULL = identity)
     uint32_t *lap;               // sharded: LowestAfter rows of own branches (fill target)
     uint64_t lap_stride;         // = global branch capacity
+    uint32_t lean;               // quad-per-event compute waves (CPW 4; LX_WALKER=lean)
+    uint32_t lean_ncw;           // their compute waves (4 or 8)
 };
 constexpr int kProfSlots = 16;   // see k_index: passes, spin misses, chunk folds, completes, ...
 

@@ -504,18 +504,41 @@ __device__ __forceinline__ uint32_t rec_off(uint32_t slot, uint32_t q) {
 
 // MASKED: older rows may carry fork marks in bit 31 (B > V); without forks
 // the seq values are used unmasked.
-template <int CPW, int NCW, int RR, bool FILL, bool SMALL, bool MASKED>
+constexpr uint32_t kNullTag = 0xFFFFFFFFu;   // lean null slot: never an event tag (tags are lp + 1 <= n)
+// DPP quad permutations (lanes 4q..4q+3): swap neighbours, swap pairs
+constexpr int kQuadSwap1 = 0xB1;   // quad_perm [1,0,3,2]
+constexpr int kQuadSwap2 = 0x4E;   // quad_perm [2,3,0,1]
+__device__ __forceinline__ uint32_t quad_max(uint32_t v) {
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kQuadSwap1, 0xF, 0xF, false));
+    return max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kQuadSwap2, 0xF, 0xF, false));
+}
+__device__ __forceinline__ uint32_t quad_and(uint32_t v) {
+    v &= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kQuadSwap1, 0xF, 0xF, false);
+    return v & (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kQuadSwap2, 0xF, 0xF, false);
+}
+
+// LEAN (CPW 4 only): the compute waves give each event a quad of lanes; lane j
+// of the quad folds the inline parents j, j+4, j+8 into all four columns
+// (straight-line, one LDS round trip for all of them), the quad merges its
+// partial maxima and its readiness by DPP, and lane 0 publishes.  A pass costs
+// a fraction of the one-lane-per-event pass (no chunk scheduling, ~1/4 of the
+// instructions), and the walk is bound by pass latency x DAG depth.
+template <int CPW, int NCW, int RR, bool FILL, bool SMALL, bool MASKED, bool LEAN = false>
 __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
     static_assert(CPW == 1 || CPW == 2 || CPW == 4, "slot layout");
+    static_assert(!LEAN || (CPW == 4 && LX_MAXP == 12), "lean walker: quads over 4 columns, 12 inline parents");
     constexpr int NT = 64 * (NCW + 1 + kND);
     constexpr int E = 64 * NCW;
     constexpr int RQ = LX_REC_Q;
     constexpr int KB = (SMALL ? 512 : 1024) / CPW;   // recent (seq -> event) entries per owned branch
     constexpr int RN = Ring<CPW, SMALL>::N;
     constexpr int RB16 = Ring<CPW, SMALL>::BYTES / 16;
-    static_assert(RN % E == 0 && RN / E >= 4, "ring slot reuse must stay within one lane");
-    static_assert(RR % 64 == 0 && RR / 64 >= 4 && RR >= 2 * E, "record ring");
-    __shared__ uint4 ring[RB16];                 // slot units (A array, then B array for CPW 4)
+    // (the lean layout checks slot reuse explicitly at completion, any quad)
+    static_assert(LEAN || (RN % E == 0 && RN / E >= 4), "ring slot reuse must stay within one lane");
+    static_assert(RR % 64 == 0 && RR / 64 >= 4 && RR >= 2 * (LEAN ? 16 * NCW : E), "record ring");
+    // slot units (A array, then B array for CPW 4); the lean layout keeps a
+    // null slot after each array (tag kNullTag, values 0)
+    __shared__ uint4 ring[RB16 + (LEAN ? 2 : 0)];
     __shared__ uint4 rrec[RR * RQ];              // event records
     __shared__ uint32_t rtag[RR / 64];           // per record round: batch round index + 1
     __shared__ uint2 brc[CPW * KB];              // {seq, event} of recent events of owned branches
@@ -525,7 +548,8 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
     const uint32_t slice = (w % 8) * a.slices_per_xcd + (w / 8);   // XCD-aware: neighbouring slices share an L2
     if (slice >= a.n_slices) return;
 
-    for (int i = threadIdx.x; i < RB16; i += NT) ring[i] = make_uint4(0, 0, 0, 0);
+    for (int i = threadIdx.x; i < RB16 + (LEAN ? 2 : 0); i += NT)
+        ring[i] = make_uint4(LEAN && (i == RN || i == 2 * RN + 1) ? kNullTag : 0u, 0, 0, 0);
     for (int i = threadIdx.x; i < RR / 64; i += NT) rtag[i] = 0;
     for (int i = threadIdx.x; i < CPW * KB; i += NT) brc[i] = make_uint2(0, LX_NONE);
     if (threadIdx.x < kND) { sh.copied[threadIdx.x] = 0; sh.stored[threadIdx.x] = 0; }
@@ -539,7 +563,7 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
     const uint64_t stride = a.stride;
     constexpr uint32_t mask = MASKED ? LX_SEQ_MASK : 0xFFFFFFFFu;
     const uint32_t RA = lds_addr(ring);
-    const uint32_t RB = RA + (uint32_t)(RN * 16);   // second units (CPW 4 only)
+    const uint32_t RB = RA + (uint32_t)((RN + (LEAN ? 1 : 0)) * 16);   // second units (CPW 4 only)
 
     // col = global branch (semantics), pc = plane column (addressing; differs
     // from col only in a column-sharded handle, which stores its own columns)
@@ -594,7 +618,7 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
                 if (lane == 0) __hip_atomic_store(&rtag[done % (RR / 64)], done + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                 done++;
             } else if (!progressed) {
-                __builtin_amdgcn_s_sleep(1);
+                if (a.diag & 32) __builtin_amdgcn_s_sleep(4); else __builtin_amdgcn_s_sleep(1);
             }
         }
         return;
@@ -621,7 +645,7 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     if (lane == 0) __hip_atomic_store(&sh.stored[d], nd, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
-                __builtin_amdgcn_s_sleep(1);
+                if (a.diag & 32) __builtin_amdgcn_s_sleep(4); else __builtin_amdgcn_s_sleep(1);
             }
             uint32_t h0[CPW];
             uint32_t prev = LX_NONE, br = 0, seq = 0;
@@ -716,10 +740,220 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
         return;
     }
 
+    if constexpr (LEAN) {
+        // ------------------------------------------------------------ compute (lean)
+        // Per lane: its three parents as (expected tag, LDS address of the
+        // slot's unit A; unit B is LEAN_BOFF further).  An absent (or already
+        // folded) parent points at the null slot, whose tag kNullTag matches
+        // and whose values are 0, so the fold needs no presence masks.  The
+        // loop body has no `continue`: flat if/else regions keep the exec-mask
+        // bookkeeping per pass small.
+        constexpr uint32_t GE = 16 * NCW;            // events in flight: one per quad
+        constexpr uint32_t kLeanStuck = 64;          // passes before a waiting event checks for reused slots
+        constexpr uint32_t LEAN_BOFF = (RN + 1) * 16;   // unit B of a slot, from its unit A (= RB - RA)
+        static_assert(LEAN_BOFF < 65536, "ds offset field");
+        const uint32_t ANULL = RA + (uint32_t)(RN * 16);
+        const uint32_t j = lane & 3;
+        const uint32_t mycol = col[j & (CPW - 1)];
+        const bool myvalid = valid[j & (CPW - 1)];
+        uint32_t lp = wave * 16 + (lane >> 2);
+        bool have = false;
+        uint32_t br = 0, seq = 0, np = 0, xi = 0, stuck = 0;
+        uint32_t px[3] = {kNullTag, kNullTag, kNullTag};
+        uint32_t pa[3] = {ANULL, ANULL, ANULL};
+        uint32_t r[CPW];
+#pragma unroll
+        for (int k = 0; k < CPW; k++) r[k] = 0;
+        uint32_t drained = 0;
+        u2v cwm = {0u, 0u};
+#ifdef LX_WALKER_PROF
+        uint32_t c_pass = 0, c_done = 0, c_slow = 0, c_wm = 0, c_norec = 0;
+        const unsigned long long t_start = wall_clock64();
+#endif
+        while (lp < n) {
+            LX_WP(c_pass++;)
+            if (!have) {
+                // record: tag, field 0 {branch, seq, #parents, prev}, and this
+                // lane's three inline parents (field 1+k, component j)
+                const uint32_t slot = lp % RR;
+                const uint32_t ra = lds_addr(rrec) + rec_off(slot, 0) * 16u;
+                uint32_t tg, w0, w1, w2;
+                u4v q0;
+                asm volatile(
+                    "ds_read_b32 %0, %5\n\t"
+                    "ds_read_b128 %1, %6\n\t"
+                    "ds_read_b32 %2, %7 offset:1024\n\t"
+                    "ds_read_b32 %3, %7 offset:2048\n\t"
+                    "ds_read_b32 %4, %7 offset:3072\n\t"
+                    "s_waitcnt lgkmcnt(0)"
+                    : "=&v"(tg), "=&v"(q0), "=&v"(w0), "=&v"(w1), "=&v"(w2)
+                    : "v"(lds_addr(&rtag[slot / 64])), "v"(ra), "v"(ra + j * 4u)
+                    : "memory");
+                if (tg == lp / 64 + 1) {
+                    br = q0.x; seq = q0.y; np = q0.z;
+                    const uint32_t w[3] = {w0, w1, w2};
+#pragma unroll
+                    for (int k = 0; k < 3; k++) {
+                        const uint32_t pl = w[k] - bs;
+                        const bool in = j + 4 * k < np;
+                        px[k] = in ? pl + 1u : kNullTag;
+                        pa[k] = in ? RA + (pl % RN) * 16u : ANULL;
+                    }
+#pragma unroll
+                    for (int k = 0; k < CPW; k++) r[k] = (col[k] == br) ? seq : 0u;
+                    // parents from earlier batches (sorted oldest first: parent j
+                    // is this lane's oldest): their rows are final, fold them now
+                    if (j < np && w0 - bs >= n) {
+#pragma unroll
+                        for (int k = 0; k < 3; k++) {
+                            if (j + 4 * k >= np || w[k] - bs < n) continue;
+                            LX_WP(c_slow++;)
+                            const uint32_t *row = a.hb + (uint64_t)w[k] * stride;
+#pragma unroll
+                            for (int c = 0; c < CPW; c++)
+                                if (valid[c]) r[c] = max(r[c], ld_l2_now(row + pc[c]) & mask);
+                            px[k] = kNullTag;
+                            pa[k] = ANULL;
+                        }
+                    }
+                    xi = LX_MAXP;
+                    stuck = 0;
+                    have = true;
+                } else {
+                    LX_WP(c_norec++;)
+                }
+            }
+            // fold this lane's parents: both slot units of each, plus the
+            // drains' watermarks, in one round trip (lanes without an event read
+            // the null slot)
+            u4v xa0, xb0, xa1, xb1, xa2, xb2;
+            asm volatile(
+                "ds_read_b128 %0, %7\n\t"
+                "ds_read_b128 %1, %7 offset:%10\n\t"
+                "ds_read_b128 %2, %8\n\t"
+                "ds_read_b128 %3, %8 offset:%10\n\t"
+                "ds_read_b128 %4, %9\n\t"
+                "ds_read_b128 %5, %9 offset:%10\n\t"
+                "ds_read_b64 %6, %11\n\t"
+                "s_waitcnt lgkmcnt(0)"
+                : "=&v"(xa0), "=&v"(xb0), "=&v"(xa1), "=&v"(xb1), "=&v"(xa2), "=&v"(xb2), "=&v"(cwm)
+                : "v"(pa[0]), "v"(pa[1]), "v"(pa[2]), "i"(LEAN_BOFF), "v"(lds_addr(&sh.copied[0]))
+                : "memory");
+            const u4v xa[3] = {xa0, xa1, xa2};
+            const u4v xb[3] = {xb0, xb1, xb2};
+            bool all = true;
+#pragma unroll
+            for (int k = 0; k < 3; k++) {
+                const bool ok = (xa[k].x == px[k]) & (xb[k].x == px[k]);
+                const uint32_t v[4] = {xa[k].y, xa[k].z, xa[k].w, xb[k].y};
+#pragma unroll
+                for (int c = 0; c < CPW; c++) r[c] = max(r[c], ok ? v[c] : 0u);
+                all &= ok;
+            }
+#pragma unroll
+            for (int c = 0; c < CPW; c++) r[c] = quad_max(r[c]);
+            const bool rdy = have && quad_and(all ? 1u : 0u);
+            if (!rdy) {
+                if (have && ++stuck >= kLeanStuck) {
+                    // waiting long: a parent's slot may have been reused by a
+                    // newer event; its HB row from L2 once its drain stored it
+#pragma unroll
+                    for (int k = 0; k < 3; k++) {
+                        const uint32_t x = px[k];
+                        if (x == kNullTag || (xa[k].x == x && xb[k].x == x) || max(xa[k].x, xb[k].x) <= x) continue;
+                        if (!round_done(sh.stored, x - 1u)) {
+                            LX_WP(c_wm++;)
+                            __hip_atomic_store(&sh.req, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            continue;
+                        }
+                        LX_WP(c_slow++;)
+                        const uint32_t *row = a.hb + (uint64_t)(x - 1u + bs) * stride;
+#pragma unroll
+                        for (int c = 0; c < CPW; c++)
+                            if (valid[c]) r[c] = max(r[c], ld_l2_now(row + pc[c]) & mask);
+                        px[k] = kNullTag;
+                        pa[k] = ANULL;
+                    }
+                }
+            } else if (xi < np) {
+                // parents beyond the inline twelve (rare): one per pass, the same on every lane of the quad
+                const uint32_t pg = ld_l2_now(a.par_in + a.poff_in[lp] + xi);
+                const uint32_t lpp = pg - bs;
+                bool ok = false, old = lpp >= n;
+                if (!old) {
+                    Slot<CPW> ps;
+                    ring_read1<CPW>(RA, RB, lpp % RN, ps);
+                    if (ps.t0 == lpp + 1 && ps.t1 == lpp + 1) {
+#pragma unroll
+                        for (int c = 0; c < CPW; c++) r[c] = max(r[c], ps.v[c]);
+                        ok = true;
+                    } else if (max(ps.t0, ps.t1) > lpp + 1) {
+                        if (round_done(sh.stored, lpp)) old = true;
+                        else __hip_atomic_store(&sh.req, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
+                }
+                if (old) {
+                    const uint32_t *row = a.hb + (uint64_t)pg * stride;
+#pragma unroll
+                    for (int c = 0; c < CPW; c++)
+                        if (valid[c]) r[c] = max(r[c], ld_l2_now(row + pc[c]) & mask);
+                    ok = true;
+                }
+                if (quad_and(ok ? 1u : 0u)) xi++;
+            } else {
+                // complete once the slot's previous occupant (lp - RN) is drained
+                bool free = true;
+                if (lp >= (uint32_t)RN && lp - RN >= drained) {
+                    const uint32_t rr = (lp - RN) / 64;
+                    const uint32_t cw = (rr % kND) ? cwm.y : cwm.x;
+                    free = cw > rr / kND || round_done(sh.copied, lp - RN);
+                    if (free) drained = ((lp - RN) | 63u) + 1;
+                    LX_WP(if (!free) c_wm++;)
+                }
+                if (free) {
+                    const uint32_t e = bs + lp;
+                    if (myvalid && mycol == br)
+                        __hip_atomic_store(reinterpret_cast<uint64_t *>(brc + (j & (CPW - 1)) * KB + seq % KB),
+                                           ((uint64_t)e << 32) | seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    if (j == 0) ring_publish<CPW>(RA, RB, lp % RN, lp + 1, r);
+                    lp += GE;
+                    have = false;
+#pragma unroll
+                    for (int k = 0; k < 3; k++) { px[k] = kNullTag; pa[k] = ANULL; }
+                    LX_WP(c_done++;)
+                }
+            }
+        }
+#ifdef LX_WALKER_PROF
+        if (a.prof) {
+            unsigned long long *pw = a.prof + ((uint64_t)blockIdx.x * 8 + wave) * kProfSlots;
+            const uint32_t cs[8] = {c_pass, 0u, 0u, c_done, c_slow, 0u, c_wm, c_norec};
+#pragma unroll
+            for (int i = 0; i < 8; i++) atomicAdd(pw + i, (unsigned long long)cs[i]);
+            atomicMax(pw + 8, (unsigned long long)c_pass);
+            if (lane == 0) atomicMax(pw + 9, wall_clock64() - t_start);
+        }
+#endif
+        return;
+    } else {
     // ---------------------------------------------------------------- compute
 #ifdef LX_WALKER_PROF
     uint32_t c_pass = 0, c_chunk = 0, c_done = 0, c_slow = 0, c_wm = 0, c_norec = 0;
     const unsigned long long t_start = wall_clock64();
+    // shader cycles per pass segment (wave-uniform; lane 0 reports):
+    // 0 record fetch, 1 fold, 2 parents beyond the inline ones, 3 completion,
+    // 4 the fold's ring-read round trip, 5 the fetch's record round trip
+    unsigned long long cyc[6] = {0, 0, 0, 0, 0, 0}, t_last = clock64();
+    uint32_t seg = 0;
+#define LX_SEG(k)                                  \
+    do {                                           \
+        const unsigned long long t_ = clock64();   \
+        cyc[seg] += t_ - t_last;                   \
+        t_last = t_;                               \
+        seg = (k);                                 \
+    } while (0)
+#else
+#define LX_SEG(k)
 #endif
 
     uint32_t lp = threadIdx.x;
@@ -734,11 +968,14 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
 
     while (lp < n) {
         LX_WP(c_pass++;)
+        LX_SEG(0);
         if (!have) {
             const uint32_t slot = lp % RR;
             uint32_t tg;
             u4v rq[LX_REC_Q];
+            LX_SEG(5);
             rec_read(lds_addr(&rtag[slot / 64]), lds_addr(rrec) + rec_off(slot, 0) * 16u, tg, rq);
+            LX_SEG(0);
             if (tg != lp / 64 + 1) { LX_WP(c_norec++;) continue; }
             br = rq[0].x; seq = rq[0].y; np = rq[0].z;
 #pragma unroll
@@ -753,6 +990,7 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
             for (int k = 0; k < CPW; k++) r[k] = (col[k] == br) ? seq : 0u;
             have = true;
         }
+        LX_SEG(1);
         if (todo) {
             // fold chunk cc (parents 4cc..4cc+3)
             LX_WP(c_chunk++;)
@@ -767,7 +1005,9 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
             }
             const uint32_t tc = (todo >> (4 * cc)) & 15u;
             Slot<CPW> o[4];
+            LX_SEG(4);
             ring_read4w<CPW>(RA, RB, sl4, o, lds_addr(&sh.copied[0]), cwm);
+            LX_SEG(1);
             // branch-free common case: fold the parents whose slot is valid
             uint32_t okm = 0, oldm = 0;
 #pragma unroll
@@ -813,6 +1053,7 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
             cc = rot ? (cc + 1 + (uint32_t)__builtin_ctz(rot)) % NCH : cc;
             if (todo) continue;
         }
+        LX_SEG(2);
         if (xi < np) {
             // parents beyond the inline LX_MAXP (rare): one per pass, from the ring or L2
             const uint32_t p = ld_l2_now(a.par_in + a.poff_in[lp] + xi);
@@ -840,6 +1081,7 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
             if (ok) xi++;
             continue;
         }
+        LX_SEG(3);
         {
             // complete: the slot's previous occupant (lp - RN) must be drained
             if (lp >= (uint32_t)RN && lp - RN >= drained) {
@@ -870,20 +1112,32 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
         for (int i = 0; i < 8; i++) atomicAdd(pw + i, (unsigned long long)cs[i]);
         atomicMax(pw + 8, (unsigned long long)c_pass);               // wave passes = max over lanes
         if (lane == 0) atomicMax(pw + 9, wall_clock64() - t_start);  // wall ticks (100 MHz)
+        LX_SEG(0);
+        if (lane == 0) {
+#pragma unroll
+            for (int i = 0; i < 4; i++) atomicAdd(pw + 10 + i, cyc[i]);
+            atomicAdd(pw + 14, cyc[0] + cyc[1] + cyc[2] + cyc[3] + cyc[4] + cyc[5]);
+            atomicAdd(pw + 10, cyc[5]);   // fetch includes its LDS round trip ...
+            atomicAdd(pw + 11, cyc[4]);   // ... and fold its ring reads
+            atomicAdd(pw + 15, cyc[4]);   // ring-read round trip alone
+            atomicAdd(pw + 5, cyc[5]);    // record round trip alone (slot 5 unused otherwise)
+        }
     }
 #endif
+#undef LX_SEG
+    }
 }
 
-template <int CPW, int NCW, int RR, bool SMALL>
+template <int CPW, int NCW, int RR, bool SMALL, bool LEAN = false>
 static hipError_t launch_index_t(const IndexArgs &a0, hipStream_t s) {
     IndexArgs a = a0;
     a.n_slices = (a.ncols + CPW - 1) / CPW;
     a.slices_per_xcd = (a.n_slices + 7) / 8;
     uint32_t grid = a.slices_per_xcd * 8;
     const dim3 blk(64 * (NCW + 1 + kND));
-    if (a.diag_nofill) hipLaunchKernelGGL((k_index<CPW, NCW, RR, false, SMALL, true>), dim3(grid), blk, 0, s, a);
-    else if (a.mask) hipLaunchKernelGGL((k_index<CPW, NCW, RR, true, SMALL, true>), dim3(grid), blk, 0, s, a);
-    else hipLaunchKernelGGL((k_index<CPW, NCW, RR, true, SMALL, false>), dim3(grid), blk, 0, s, a);
+    if (a.diag_nofill) hipLaunchKernelGGL((k_index<CPW, NCW, RR, false, SMALL, true, LEAN>), dim3(grid), blk, 0, s, a);
+    else if (a.mask) hipLaunchKernelGGL((k_index<CPW, NCW, RR, true, SMALL, true, LEAN>), dim3(grid), blk, 0, s, a);
+    else hipLaunchKernelGGL((k_index<CPW, NCW, RR, true, SMALL, false, LEAN>), dim3(grid), blk, 0, s, a);
     return hipGetLastError();
 }
 
@@ -902,6 +1156,14 @@ static hipError_t launch_index_c(const IndexArgs &a, uint32_t ncw, hipStream_t s
             if (ncw <= 1) return launch_index_t<CPW, 1, 512, false>(a, s);
             if (ncw <= 2) return launch_index_t<CPW, 2, 512, false>(a, s);
             return launch_index_t<CPW, 4, 512, false>(a, s);
+        }
+    }
+    if constexpr (CPW == 4) {
+        if (a.lean) {
+            // quads: 16 events in flight per compute wave
+            if (a.lean_ncw <= 4) return launch_index_t<CPW, 4, 1024, false, true>(a, s);
+            if (a.lean_ncw <= 8) return launch_index_t<CPW, 8, 1024, false, true>(a, s);
+            return launch_index_t<CPW, 12, 1024, false, true>(a, s);
         }
     }
     if (ncw <= 1) return launch_index_t<CPW, 1, 1024, false>(a, s);

@@ -6,7 +6,8 @@ import os
 import numpy as np
 
 _PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(_PKG, "build", "liblachesis_hip.so")
+# LX_LIB: another build of the same library (diagnostics: make wprof)
+LIB_PATH = os.environ.get("LX_LIB") or os.path.join(_PKG, "build", "liblachesis_hip.so")
 _lib = None
 
 u8p = ctypes.POINTER(ctypes.c_uint8)

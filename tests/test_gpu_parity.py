@@ -416,6 +416,8 @@ WALKER_VARIANTS = [
     {"LX_CPW": "4", "LX_NCW": "1"}, {"LX_CPW": "1", "LX_NCW": "4"},
     {"LX_SMALL": "1", "LX_CPW": "1", "LX_NCW": "1"}, {"LX_SMALL": "1", "LX_CPW": "2", "LX_NCW": "2"},
     {"LX_RR": "512", "LX_CPW": "2", "LX_NCW": "4"}, {"LX_RR": "512", "LX_CPW": "2", "LX_NCW": "2"},
+    # quad-per-event compute waves (CPW 4), 4 and 8 compute waves
+    {"LX_CPW": "4", "LX_WALKER": "lean"}, {"LX_CPW": "4", "LX_WALKER": "lean", "LX_LEAN_NCW": "8"},
 ]
 
 
@@ -437,6 +439,27 @@ def test_walker_variants(lx, env, monkeypatch):
     rng = np.random.default_rng(5)
     compare_rows(ix, o, rng.choice(len(d), 1500, replace=False))
     qa, qb = lx.tools.fc_queries(d.lamport, 200_000, window=32, seed=4)
+    np.testing.assert_array_equal(ix.forkless_cause_batch(qa, qb), o.forkless_cause_batch(qa, qb))
+    ix.close()
+
+
+@pytest.mark.big_only
+@pytest.mark.parametrize("walker", ["", "lean"])
+def test_walker_many_parents(lx, walker, monkeypatch):
+    """Events with more parents than a record holds inline (16 > 12) take the
+    overflow path of the walker; CPW 4 with both compute layouts."""
+    monkeypatch.setenv("LX_CPW", "4")
+    monkeypatch.setenv("LX_WALKER", walker)
+    d = lx.tools.gen_dag(30, 120, 16, 3, 4, 77)
+    assert int(np.max(np.diff(d.poff))) > 12
+    weights = list(range(70, 40, -1))
+    o = oracle_for(d, weights)
+    ix = lx.Index()
+    ix.reset(weights)
+    br = ix.add_batch(d.creator, d.seq, d.poff, d.par, want_branches=True)
+    assert [int(x) for x in br] == [o.branch(i) for i in range(len(d))]
+    compare_rows(ix, o, range(len(d)))
+    qa, qb = lx.tools.fc_queries(d.lamport, 100_000, window=32, seed=8)
     np.testing.assert_array_equal(ix.forkless_cause_batch(qa, qb), o.forkless_cause_batch(qa, qb))
     ix.close()
 
