@@ -170,6 +170,7 @@ struct lx_index {
     uint32_t diag_nofill = 0;   // LX_DIAG_NOFILL=1: timing-only build of the walker (LA left empty)
     uint32_t cpw_hint = 0, ncw_hint = 0;   // LX_CPW / LX_NCW tuning overrides
     uint32_t lean = 0, lean_ncw = 4;       // LX_WALKER=lean: quad-per-event compute waves (LX_LEAN_NCW)
+    uint32_t drains = 2;                   // LX_DRAINS: drain waves of the block walker (2 or 4)
     uint32_t rr_hint = 0, diag = 0;        // LX_RR record ring depth; LX_DIAG timing-only modes
     bool prof = false;                     // LX_PROF=1: per-wave walker counters to stderr
     uint32_t small = 0;                    // LX_SMALL=1: small-LDS walker (several workgroups per CU)
@@ -654,12 +655,13 @@ int add_batch_dev(lx_index *h, uint32_t n, const uint32_t *creator, const uint32
     ia.ncw_hint = h->ncw_hint;
     ia.lean = h->lean;
     ia.lean_ncw = h->lean_ncw;
+    ia.drains = h->drains;
     // antichain width of tdag-like DAGs ~ V / (1.6 P); P from the batch
     {
         uint32_t pbar = std::max<uint32_t>(1, (uint32_t)((h->last_npar + n - 1) / n));
         ia.width_hint = std::max<uint32_t>(1, (uint32_t)(h->V * 10 / (16 * pbar)));
     }
-    const size_t prof_n = (size_t)65536 * 8 * kProfSlots;
+    const size_t prof_n = (size_t)kProfBlocks * kProfWaves * kProfSlots;
     if (h->prof) {
         HIPCHK(h, hipMalloc(&ia.prof, prof_n * 8));
         HIPCHK(h, hipMemsetAsync(ia.prof, 0, prof_n * 8, s));
@@ -672,25 +674,34 @@ int add_batch_dev(lx_index *h, uint32_t n, const uint32_t *creator, const uint32
         HIPCHK(h, hipMemcpyAsync(pv.data(), ia.prof, prof_n * 8, hipMemcpyDeviceToHost, s));
         HIPCHK(h, hipStreamSynchronize(s));
         HIPCHK(h, hipFree(ia.prof));
-        // summary over workgroups: per compute wave (lane sums), wave passes, wall time
-        double sum[8 * kProfSlots] = {0};
+        // summary over workgroups: compute waves (lane sums), loader, drains
+        double sum[kProfWaves * kProfSlots] = {0};
         uint32_t nb = 0;
-        for (uint32_t b = 0; b < 65536; b++) {
-            const unsigned long long *pb = pv.data() + (size_t)b * 8 * kProfSlots;
+        for (uint32_t b = 0; b < (uint32_t)kProfBlocks; b++) {
+            const unsigned long long *pb = pv.data() + (size_t)b * kProfWaves * kProfSlots;
             if (!pb[9]) continue;
             nb++;
-            for (int i = 0; i < 8 * kProfSlots; i++) sum[i] += (double)pb[i];
+            for (int i = 0; i < kProfWaves * kProfSlots; i++) sum[i] += (double)pb[i];
         }
         fprintf(stderr, "[lx_prof] n=%u blocks=%u (means per block)\n", n, nb);
-        for (int w = 0; w < 8; w++) {
+        for (int w = 0; w < kProfWaves; w++) {
             const double *q = sum + w * kProfSlots;
             if (!q[9]) continue;
-            fprintf(stderr, "[lx_prof] wave %d: wall_us=%.0f wave_passes=%.0f lane: pass=%.0f spin=%.0f chunk=%.0f done=%.0f slow=%.0f fill=%.0f wm=%.0f norec=%.0f  ns/pass=%.1f\n",
-                    w, q[9] / nb / 100.0, q[8] / nb, q[0] / nb, q[1] / nb, q[2] / nb, q[3] / nb, q[4] / nb, q[5] / nb, q[6] / nb,
-                    q[7] / nb, q[9] * 10.0 / (q[8] > 0 ? q[8] : 1));
-            if (q[14] > 0)
-                fprintf(stderr, "[lx_prof] wave %d cycles/pass: fetch=%.0f (record rt %.0f) fold=%.0f (ring rt %.0f) ovf=%.0f complete=%.0f total=%.0f\n", w,
-                        q[10] / q[8], q[5] / q[8], q[11] / q[8], q[15] / q[8], q[12] / q[8], q[13] / q[8], q[14] / q[8]);
+            const double role = q[10] / (nb ? nb : 1);
+            if (role > 1.5) {
+                fprintf(stderr, "[lx_prof] wave %d drain: wall_us=%.0f rounds=%.0f spin=%.0f busy_us=%.0f fills=%.0f brc_miss=%.0f\n",
+                        w, q[9] / nb / 100.0, q[3] / nb, q[0] / nb, q[6] / nb / 100.0, q[4] / nb, q[5] / nb);
+            } else if (role > 0.5) {
+                fprintf(stderr, "[lx_prof] wave %d loader: wall_us=%.0f rounds=%.0f iter=%.0f slot_wait=%.0f sleeps=%.0f\n", w,
+                        q[9] / nb / 100.0, q[3] / nb, q[0] / nb, q[1] / nb, q[2] / nb);
+            } else {
+                fprintf(stderr, "[lx_prof] wave %d: wall_us=%.0f wave_passes=%.0f lane: pass=%.0f spin=%.0f chunk=%.0f done=%.0f slow=%.0f fill=%.0f wm=%.0f norec=%.0f  ns/pass=%.1f\n",
+                        w, q[9] / nb / 100.0, q[8] / nb, q[0] / nb, q[1] / nb, q[2] / nb, q[3] / nb, q[4] / nb, q[5] / nb, q[6] / nb,
+                        q[7] / nb, q[9] * 10.0 / (q[8] > 0 ? q[8] : 1));
+                if (q[14] > 0)
+                    fprintf(stderr, "[lx_prof] wave %d cycles/pass: fetch=%.0f (record rt %.0f) fold=%.0f (ring rt %.0f) ovf=%.0f complete=%.0f total=%.0f\n", w,
+                            q[10] / q[8], q[5] / q[8], q[11] / q[8], q[15] / q[8], q[12] / q[8], q[13] / q[8], q[14] / q[8]);
+            }
         }
     }
     if (h->B > h->V && h->n_cheat) {
@@ -1306,8 +1317,9 @@ int lx_create(const lx_config *cfg, lx_index **out) {
     if (const char *d = getenv("LX_DIAG_NOFILL")) h->diag_nofill = (d[0] == '1');
     if (const char *d = getenv("LX_CPW")) h->cpw_hint = (uint32_t)atoi(d);
     if (const char *d = getenv("LX_NCW")) h->ncw_hint = (uint32_t)atoi(d);
-    if (const char *d = getenv("LX_WALKER")) h->lean = strcmp(d, "lean") == 0;
+    if (const char *d = getenv("LX_WALKER")) h->lean = strcmp(d, "lean") == 0 ? 1 : strcmp(d, "block") == 0 ? 2 : 0;
     if (const char *d = getenv("LX_LEAN_NCW")) h->lean_ncw = (uint32_t)atoi(d);
+    if (const char *d = getenv("LX_DRAINS")) h->drains = (uint32_t)atoi(d);
     if (const char *d = getenv("LX_RR")) h->rr_hint = (uint32_t)atoi(d);
     if (const char *d = getenv("LX_DIAG")) h->diag = (uint32_t)atoi(d);
     if (const char *d = getenv("LX_PROF")) h->prof = (d[0] == '1');

@@ -68,8 +68,11 @@ struct IndexArgs {
     uint64_t lap_stride;         // = global branch capacity
     uint32_t lean;               // quad-per-event compute waves (CPW 4; LX_WALKER=lean)
     uint32_t lean_ncw;           // their compute waves (4 or 8)
+    uint32_t drains;             // drain waves of the block layout (2 or 4; LX_DRAINS)
 };
 constexpr int kProfSlots = 16;   // see k_index: passes, spin misses, chunk folds, completes, ...
+constexpr int kProfWaves = 16;   // waves per workgroup in the counter layout
+constexpr int kProfBlocks = 4096;
 
 struct BatchArgs {
     uint32_t n;

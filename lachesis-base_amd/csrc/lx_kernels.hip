@@ -260,7 +260,8 @@ hipError_t launch_batch_finish(const BatchArgs &a, uint32_t jump_rounds, hipStre
 // from an earlier batch).  Lanes never block inside a pass, so dependencies
 // between lanes of one wave cannot deadlock; drains wait only for older events
 // and keep publishing their own progress.
-constexpr int kND = 2;               // drain waves
+constexpr int kND = 2;               // drain waves (the classic compute layout reads both watermarks as 8 B)
+constexpr int kNDMax = 4;            // drain waves of the quad / block layouts (LX_DRAINS)
 
 template <int CPW, bool SMALL>
 struct Ring {
@@ -271,15 +272,16 @@ struct Ring {
     static constexpr int N = BYTES / (CPW == 1 ? 8 : CPW == 2 ? 16 : 32);
 };
 
-struct alignas(8) WalkShared {
-    uint32_t copied[kND];    // rounds drained (ring and record data consumed) per drain wave
-    uint32_t stored[kND];    // rounds whose global stores are complete per drain wave
+struct alignas(16) WalkShared {
+    uint32_t copied[kNDMax];    // rounds drained (ring and record data consumed) per drain wave
+    uint32_t stored[kNDMax];    // rounds whose global stores are complete per drain wave
     uint32_t req;            // a compute lane waits for `stored`: drains flush
 };
 
+template <int ND = kND>
 __device__ __forceinline__ bool round_done(const uint32_t *cnt, uint32_t ev) {
     const uint32_t r = ev / 64;
-    return __hip_atomic_load(cnt + (r % kND), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) > r / kND;
+    return __hip_atomic_load(cnt + (r % ND), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) > r / ND;
 }
 
 typedef uint32_t u4v __attribute__((ext_vector_type(4)));
@@ -505,6 +507,9 @@ __device__ __forceinline__ uint32_t rec_off(uint32_t slot, uint32_t q) {
 // MASKED: older rows may carry fork marks in bit 31 (B > V); without forks
 // the seq values are used unmasked.
 constexpr uint32_t kNullTag = 0xFFFFFFFFu;   // lean null slot: never an event tag (tags are lp + 1 <= n)
+__device__ __forceinline__ uint32_t wm_pick(const u4v &w, uint32_t i) {
+    return i == 0 ? w.x : i == 1 ? w.y : i == 2 ? w.z : w.w;
+}
 // DPP quad permutations (lanes 4q..4q+3): swap neighbours, swap pairs
 constexpr int kQuadSwap1 = 0xB1;   // quad_perm [1,0,3,2]
 constexpr int kQuadSwap2 = 0x4E;   // quad_perm [2,3,0,1]
@@ -523,11 +528,12 @@ __device__ __forceinline__ uint32_t quad_and(uint32_t v) {
 // partial maxima and its readiness by DPP, and lane 0 publishes.  A pass costs
 // a fraction of the one-lane-per-event pass (no chunk scheduling, ~1/4 of the
 // instructions), and the walk is bound by pass latency x DAG depth.
-template <int CPW, int NCW, int RR, bool FILL, bool SMALL, bool MASKED, bool LEAN = false>
-__global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
+template <int CPW, int NCW, int RR, bool FILL, bool SMALL, bool MASKED, int LEAN = 0, int ND = kND>
+__global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
+    static_assert(ND == kND || (LEAN && ND <= kNDMax), "drain waves: 2, or up to 4 with the quad / block layouts");
     static_assert(CPW == 1 || CPW == 2 || CPW == 4, "slot layout");
     static_assert(!LEAN || (CPW == 4 && LX_MAXP == 12), "lean walker: quads over 4 columns, 12 inline parents");
-    constexpr int NT = 64 * (NCW + 1 + kND);
+    constexpr int NT = 64 * (NCW + 1 + ND);
     constexpr int E = 64 * NCW;
     constexpr int RQ = LX_REC_Q;
     constexpr int KB = (SMALL ? 512 : 1024) / CPW;   // recent (seq -> event) entries per owned branch
@@ -542,6 +548,7 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
     __shared__ uint4 rrec[RR * RQ];              // event records
     __shared__ uint32_t rtag[RR / 64];           // per record round: batch round index + 1
     __shared__ uint2 brc[CPW * KB];              // {seq, event} of recent events of owned branches
+    __shared__ uint4 dummy[LEAN == 2 ? 128 : 1];  // block walker: per-lane targets of suppressed writes
     __shared__ WalkShared sh;
 
     const uint32_t w = blockIdx.x;
@@ -552,7 +559,7 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
         ring[i] = make_uint4(LEAN && (i == RN || i == 2 * RN + 1) ? kNullTag : 0u, 0, 0, 0);
     for (int i = threadIdx.x; i < RR / 64; i += NT) rtag[i] = 0;
     for (int i = threadIdx.x; i < CPW * KB; i += NT) brc[i] = make_uint2(0, LX_NONE);
-    if (threadIdx.x < kND) { sh.copied[threadIdx.x] = 0; sh.stored[threadIdx.x] = 0; }
+    if (threadIdx.x < kNDMax) { sh.copied[threadIdx.x] = 0; sh.stored[threadIdx.x] = 0; }
     if (threadIdx.x == 0) sh.req = 0;
     __syncthreads();
 
@@ -586,13 +593,19 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
         const uint32_t nrounds = (n + 63) / 64;
         constexpr uint32_t D = RR / 64 < 8 ? RR / 64 : 8;
         uint32_t issued = 0, done = 0;
+#ifdef LX_WALKER_PROF
+        uint32_t l_iter = 0, l_slot = 0, l_sleep = 0;
+        const unsigned long long lt0 = wall_clock64();
+#endif
         const char *recb = reinterpret_cast<const char *>(a.rec);
         while (done < nrounds) {
             bool progressed = false;
+            LX_WP(l_iter++;)
+            LX_WP(if (issued < nrounds && issued - done < D && !(issued * 64 < (uint32_t)RR || round_done<ND>(sh.copied, issued * 64 - RR))) l_slot++;)
             // a round's record slots are free once the drain consumed their
             // previous occupants (events ev - RR: same round offset)
             if (issued < nrounds && issued - done < D &&
-                (issued * 64 < (uint32_t)RR || round_done(sh.copied, issued * 64 - RR))) {
+                (issued * 64 < (uint32_t)RR || round_done<ND>(sh.copied, issued * 64 - RR))) {
                 const uint32_t s0 = (issued * 64) % RR;
                 char *dst = reinterpret_cast<char *>(rrec) + (uint64_t)s0 * sizeof(EventRec);
                 const uint64_t base = (uint64_t)issued * 64 * sizeof(EventRec);
@@ -618,9 +631,21 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
                 if (lane == 0) __hip_atomic_store(&rtag[done % (RR / 64)], done + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                 done++;
             } else if (!progressed) {
+                LX_WP(l_sleep++;)
                 if (a.diag & 32) __builtin_amdgcn_s_sleep(4); else __builtin_amdgcn_s_sleep(1);
             }
         }
+#ifdef LX_WALKER_PROF
+        if (a.prof && lane == 0) {
+            unsigned long long *pw = a.prof + ((uint64_t)blockIdx.x * kProfWaves + wave) * kProfSlots;
+            atomicAdd(pw + 0, (unsigned long long)l_iter);
+            atomicAdd(pw + 1, (unsigned long long)l_slot);
+            atomicAdd(pw + 2, (unsigned long long)l_sleep);
+            atomicAdd(pw + 3, (unsigned long long)nrounds);
+            atomicMax(pw + 9, wall_clock64() - lt0);
+            atomicAdd(pw + 10, 1ull);   // role: loader
+        }
+#endif
         return;
     }
 
@@ -628,7 +653,12 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
         // ------------------------------------------------------------ drain
         const uint32_t d = wave - NCW - 1;
         uint32_t nd = 0;                 // rounds of this wave completed
-        for (uint32_t R = d; R * 64 < n; R += kND, nd++) {
+#ifdef LX_WALKER_PROF
+        uint32_t d_spin = 0, d_fill = 0, d_miss = 0;
+        const unsigned long long dt0 = wall_clock64();
+        unsigned long long d_busy = 0;
+#endif
+        for (uint32_t R = d; R * 64 < n; R += ND, nd++) {
             const uint32_t ev = R * 64 + lane;
             const uint32_t sl = ev % RN;
             Slot<CPW> me;
@@ -641,12 +671,16 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
                     ready = me.t0 == ev + 1 && me.t1 == ev + 1;
                 }
                 if (__all(ready)) break;
+                LX_WP(d_spin++;)
                 if (__hip_atomic_load(&sh.req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     if (lane == 0) __hip_atomic_store(&sh.stored[d], nd, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
                 if (a.diag & 32) __builtin_amdgcn_s_sleep(4); else __builtin_amdgcn_s_sleep(1);
             }
+#ifdef LX_WALKER_PROF
+            const unsigned long long tb0 = wall_clock64();
+#endif
             uint32_t h0[CPW];
             uint32_t prev = LX_NONE, br = 0, seq = 0;
             if (ev < n) {
@@ -667,11 +701,11 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
                         } else {
                             // reused slot: prev's row is (being) stored by a drain
                             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                            if ((pl / 64) % kND != d) {
+                            if ((pl / 64) % ND != d) {
                                 // the other drain may in turn wait for this one: keep
                                 // publishing our completed rounds (divergent: every active lane)
                                 __hip_atomic_store(&sh.stored[d], nd, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                                while (!round_done(sh.stored, pl)) {
+                                while (!round_done<ND>(sh.stored, pl)) {
                                     __hip_atomic_store(&sh.req, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                                     __builtin_amdgcn_s_sleep(1);
                                 }
@@ -705,23 +739,38 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
                 if (FILL) {
                     // LowestAfter range fill: events (col, s), s in (h0, r], are first
                     // observed from branch `br` by this event.
+                    uint32_t lo[CPW], hi[CPW];
 #pragma unroll
                     for (int k = 0; k < CPW; k++) {
-                        if (!valid[k]) continue;
-                        const uint32_t lo = max(h0[k] + 1u, first[k]);
-                        const uint32_t hi = r[k] & mask;
-                        if (a.lap) {
-                            // sharded: rows of own branches addressed by (column, seq)
-                            for (uint32_t s = lo; s <= hi; s++)
+                        lo[k] = max(h0[k] + 1u, first[k]);
+                        hi[k] = valid[k] ? (r[k] & mask) : 0u;
+                    }
+                    if (a.lap) {
+                        // sharded: rows of own branches addressed by (column, seq)
+#pragma unroll
+                        for (int k = 0; k < CPW; k++)
+                            for (uint32_t s = lo[k]; s <= hi[k]; s++)
                                 a.lap[((uint64_t)pc[k] * a.s_cap + (s - first[k])) * a.lap_stride + br] = seq;
-                            continue;
-                        }
-                        for (uint32_t s = lo; s <= hi; s++) {
-                            const uint64_t cc = __hip_atomic_load(reinterpret_cast<const uint64_t *>(brc + k * KB + s % KB),
-                                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                            uint32_t row = (uint32_t)(cc >> 32);
-                            if ((uint32_t)cc != s) row = ld_l2_now(a.brow + (uint64_t)col[k] * a.s_cap + (s - first[k]));
-                            a.la[(uint64_t)row * stride + br] = seq;
+                    } else {
+                        // the first (usually only) seq of every column's range: all
+                        // the recent-event lookups in one LDS round trip
+                        uint64_t c0[CPW];
+#pragma unroll
+                        for (int k = 0; k < CPW; k++)
+                            c0[k] = __hip_atomic_load(reinterpret_cast<const uint64_t *>(brc + k * KB + lo[k] % KB),
+                                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#pragma unroll
+                        for (int k = 0; k < CPW; k++) {
+                            for (uint32_t s = lo[k]; s <= hi[k]; s++) {
+                                const uint64_t cc = s == lo[k] ? c0[k]
+                                                               : __hip_atomic_load(reinterpret_cast<const uint64_t *>(brc + k * KB + s % KB),
+                                                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                                uint32_t row = (uint32_t)(cc >> 32);
+                                LX_WP(d_fill++;)
+                                LX_WP(if ((uint32_t)cc != s) d_miss++;)
+                                if ((uint32_t)cc != s) row = ld_l2_now(a.brow + (uint64_t)col[k] * a.s_cap + (s - first[k]));
+                                a.la[(uint64_t)row * stride + br] = seq;
+                            }
                         }
                     }
                 }
@@ -733,14 +782,29 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
                     __hip_atomic_store(&sh.req, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
             }
+            LX_WP(d_busy += wall_clock64() - tb0;)
         }
         // every store of this wave complete; a compute lane or the other drain may wait for it
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (lane == 0) __hip_atomic_store(&sh.stored[d], 0xFFFFFFFFu, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+#ifdef LX_WALKER_PROF
+        if (a.prof) {
+            unsigned long long *pw = a.prof + ((uint64_t)blockIdx.x * kProfWaves + wave) * kProfSlots;
+            atomicAdd(pw + 4, (unsigned long long)d_fill);
+            atomicAdd(pw + 5, (unsigned long long)d_miss);
+            if (lane == 0) {
+                atomicAdd(pw + 0, (unsigned long long)d_spin);
+                atomicAdd(pw + 3, (unsigned long long)nd);
+                atomicAdd(pw + 6, d_busy);
+                atomicMax(pw + 9, wall_clock64() - dt0);
+                atomicAdd(pw + 10, 2ull);   // role: drain
+            }
+        }
+#endif
         return;
     }
 
-    if constexpr (LEAN) {
+    if constexpr (LEAN == 1) {
         // ------------------------------------------------------------ compute (lean)
         // Per lane: its three parents as (expected tag, LDS address of the
         // slot's unit A; unit B is LEAN_BOFF further).  An absent (or already
@@ -765,7 +829,7 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
 #pragma unroll
         for (int k = 0; k < CPW; k++) r[k] = 0;
         uint32_t drained = 0;
-        u2v cwm = {0u, 0u};
+        u4v cwm = {0u, 0u, 0u, 0u};   // all drains' `copied` watermarks (16 B)
 #ifdef LX_WALKER_PROF
         uint32_t c_pass = 0, c_done = 0, c_slow = 0, c_wm = 0, c_norec = 0;
         const unsigned long long t_start = wall_clock64();
@@ -834,7 +898,7 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
                 "ds_read_b128 %3, %8 offset:%10\n\t"
                 "ds_read_b128 %4, %9\n\t"
                 "ds_read_b128 %5, %9 offset:%10\n\t"
-                "ds_read_b64 %6, %11\n\t"
+                "ds_read_b128 %6, %11\n\t"
                 "s_waitcnt lgkmcnt(0)"
                 : "=&v"(xa0), "=&v"(xb0), "=&v"(xa1), "=&v"(xb1), "=&v"(xa2), "=&v"(xb2), "=&v"(cwm)
                 : "v"(pa[0]), "v"(pa[1]), "v"(pa[2]), "i"(LEAN_BOFF), "v"(lds_addr(&sh.copied[0]))
@@ -861,7 +925,7 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
                     for (int k = 0; k < 3; k++) {
                         const uint32_t x = px[k];
                         if (x == kNullTag || (xa[k].x == x && xb[k].x == x) || max(xa[k].x, xb[k].x) <= x) continue;
-                        if (!round_done(sh.stored, x - 1u)) {
+                        if (!round_done<ND>(sh.stored, x - 1u)) {
                             LX_WP(c_wm++;)
                             __hip_atomic_store(&sh.req, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                             continue;
@@ -888,7 +952,7 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
                         for (int c = 0; c < CPW; c++) r[c] = max(r[c], ps.v[c]);
                         ok = true;
                     } else if (max(ps.t0, ps.t1) > lpp + 1) {
-                        if (round_done(sh.stored, lpp)) old = true;
+                        if (round_done<ND>(sh.stored, lpp)) old = true;
                         else __hip_atomic_store(&sh.req, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     }
                 }
@@ -905,8 +969,8 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
                 bool free = true;
                 if (lp >= (uint32_t)RN && lp - RN >= drained) {
                     const uint32_t rr = (lp - RN) / 64;
-                    const uint32_t cw = (rr % kND) ? cwm.y : cwm.x;
-                    free = cw > rr / kND || round_done(sh.copied, lp - RN);
+                    const uint32_t cw = wm_pick(cwm, rr % ND);
+                    free = cw > rr / ND || round_done<ND>(sh.copied, lp - RN);
                     if (free) drained = ((lp - RN) | 63u) + 1;
                     LX_WP(if (!free) c_wm++;)
                 }
@@ -926,7 +990,206 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
         }
 #ifdef LX_WALKER_PROF
         if (a.prof) {
-            unsigned long long *pw = a.prof + ((uint64_t)blockIdx.x * 8 + wave) * kProfSlots;
+            unsigned long long *pw = a.prof + ((uint64_t)blockIdx.x * kProfWaves + wave) * kProfSlots;
+            const uint32_t cs[8] = {c_pass, 0u, 0u, c_done, c_slow, 0u, c_wm, c_norec};
+#pragma unroll
+            for (int i = 0; i < 8; i++) atomicAdd(pw + i, (unsigned long long)cs[i]);
+            atomicMax(pw + 8, (unsigned long long)c_pass);
+            if (lane == 0) atomicMax(pw + 9, wall_clock64() - t_start);
+        }
+#endif
+        return;
+    } else if constexpr (LEAN == 2) {
+        // ------------------------------------------------------------ compute (block)
+        // As the quad layout, but a wave's 16 quads own 16 consecutive events
+        // (a block) and the wave moves to its next block (+NCW blocks) only
+        // when all 16 have published: record fetch and block advance are
+        // wave-uniform branches; per pass only the publish of newly ready
+        // quads is divergent.
+        constexpr uint32_t kLeanStuck = 64;
+        constexpr uint32_t LEAN_BOFF = (RN + 1) * 16;
+        static_assert(LEAN_BOFF < 65536, "ds offset field");
+        const uint32_t ANULL = RA + (uint32_t)(RN * 16);
+        const uint32_t j = lane & 3, quad = lane >> 2;
+        const uint32_t mycol = col[j & (CPW - 1)];
+        const bool myvalid = valid[j & (CPW - 1)];
+        uint32_t blk = wave;
+        bool loaded = false, done = true;
+        uint32_t br = 0, seq = 0, np = 0, xi = 0, stuck = 0;
+        uint32_t px[3] = {kNullTag, kNullTag, kNullTag};
+        uint32_t pa[3] = {ANULL, ANULL, ANULL};
+        uint32_t r[CPW];
+#pragma unroll
+        for (int k = 0; k < CPW; k++) r[k] = 0;
+        uint32_t drained = 0;
+        u4v cwm = {0u, 0u, 0u, 0u};   // all drains' `copied` watermarks (16 B)
+#ifdef LX_WALKER_PROF
+        uint32_t c_pass = 0, c_done = 0, c_slow = 0, c_wm = 0, c_norec = 0;
+        const unsigned long long t_start = wall_clock64();
+#endif
+        while (blk * 16 < n) {
+            LX_WP(c_pass++;)
+            const uint32_t lp = blk * 16 + quad;
+            const bool live = lp < n;
+            if (!loaded) {
+                const uint32_t slot = lp % RR;
+                const uint32_t ra = lds_addr(rrec) + rec_off(slot, 0) * 16u;
+                uint32_t tg, w0, w1, w2;
+                u4v q0;
+                asm volatile(
+                    "ds_read_b32 %0, %5\n\t"
+                    "ds_read_b128 %1, %6\n\t"
+                    "ds_read_b32 %2, %7 offset:1024\n\t"
+                    "ds_read_b32 %3, %7 offset:2048\n\t"
+                    "ds_read_b32 %4, %7 offset:3072\n\t"
+                    "s_waitcnt lgkmcnt(0)"
+                    : "=&v"(tg), "=&v"(q0), "=&v"(w0), "=&v"(w1), "=&v"(w2)
+                    : "v"(lds_addr(&rtag[slot / 64])), "v"(ra), "v"(ra + j * 4u)
+                    : "memory");
+                if (!__all(!live || tg == lp / 64 + 1)) {
+                    LX_WP(c_norec++;)
+                    continue;   // wave-uniform: the loader is behind
+                }
+                br = q0.x; seq = q0.y; np = live ? q0.z : 0u;
+                const uint32_t w[3] = {w0, w1, w2};
+#pragma unroll
+                for (int k = 0; k < 3; k++) {
+                    const uint32_t pl = w[k] - bs;
+                    const bool in = j + 4 * k < np;
+                    px[k] = in ? pl + 1u : kNullTag;
+                    pa[k] = in ? RA + (pl % RN) * 16u : ANULL;
+                }
+#pragma unroll
+                for (int k = 0; k < CPW; k++) r[k] = (col[k] == br) ? seq : 0u;
+                if (j < np && w0 - bs >= n) {
+                    // parents from earlier batches (sorted oldest first): final rows
+#pragma unroll
+                    for (int k = 0; k < 3; k++) {
+                        if (j + 4 * k >= np || w[k] - bs < n) continue;
+                        LX_WP(c_slow++;)
+                        const uint32_t *row = a.hb + (uint64_t)w[k] * stride;
+#pragma unroll
+                        for (int c = 0; c < CPW; c++)
+                            if (valid[c]) r[c] = max(r[c], ld_l2_now(row + pc[c]) & mask);
+                        px[k] = kNullTag;
+                        pa[k] = ANULL;
+                    }
+                }
+                xi = LX_MAXP;
+                stuck = 0;
+                done = !live;
+                loaded = true;
+            }
+            // fold (published quads read the null slot)
+            u4v xa0, xb0, xa1, xb1, xa2, xb2;
+            asm volatile(
+                "ds_read_b128 %0, %7\n\t"
+                "ds_read_b128 %1, %7 offset:%10\n\t"
+                "ds_read_b128 %2, %8\n\t"
+                "ds_read_b128 %3, %8 offset:%10\n\t"
+                "ds_read_b128 %4, %9\n\t"
+                "ds_read_b128 %5, %9 offset:%10\n\t"
+                "ds_read_b128 %6, %11\n\t"
+                "s_waitcnt lgkmcnt(0)"
+                : "=&v"(xa0), "=&v"(xb0), "=&v"(xa1), "=&v"(xb1), "=&v"(xa2), "=&v"(xb2), "=&v"(cwm)
+                : "v"(pa[0]), "v"(pa[1]), "v"(pa[2]), "i"(LEAN_BOFF), "v"(lds_addr(&sh.copied[0]))
+                : "memory");
+            const u4v xa[3] = {xa0, xa1, xa2};
+            const u4v xb[3] = {xb0, xb1, xb2};
+            bool all = true;
+#pragma unroll
+            for (int k = 0; k < 3; k++) {
+                const bool ok = (xa[k].x == px[k]) & (xb[k].x == px[k]);
+                const uint32_t v[4] = {xa[k].y, xa[k].z, xa[k].w, xb[k].y};
+#pragma unroll
+                for (int c = 0; c < CPW; c++) r[c] = max(r[c], ok ? v[c] : 0u);
+                all &= ok;
+            }
+#pragma unroll
+            for (int c = 0; c < CPW; c++) r[c] = quad_max(r[c]);
+            const bool rdy = quad_and(all ? 1u : 0u) != 0;
+            if (rdy && !done && xi < np) {
+                // parents beyond the inline twelve (rare): one per pass, the same on every lane of the quad
+                const uint32_t pg = ld_l2_now(a.par_in + a.poff_in[lp] + xi);
+                const uint32_t lpp = pg - bs;
+                bool ok = false, old = lpp >= n;
+                if (!old) {
+                    Slot<CPW> ps;
+                    ring_read1<CPW>(RA, RB, lpp % RN, ps);
+                    if (ps.t0 == lpp + 1 && ps.t1 == lpp + 1) {
+#pragma unroll
+                        for (int c = 0; c < CPW; c++) r[c] = max(r[c], ps.v[c]);
+                        ok = true;
+                    } else if (max(ps.t0, ps.t1) > lpp + 1) {
+                        if (round_done<ND>(sh.stored, lpp)) old = true;
+                        else __hip_atomic_store(&sh.req, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
+                }
+                if (old) {
+                    const uint32_t *row = a.hb + (uint64_t)pg * stride;
+#pragma unroll
+                    for (int c = 0; c < CPW; c++)
+                        if (valid[c]) r[c] = max(r[c], ld_l2_now(row + pc[c]) & mask);
+                    ok = true;
+                }
+                if (quad_and(ok ? 1u : 0u)) xi++;
+            }
+            {
+                // publish, branch-free: a ready quad whose slot's previous
+                // occupant (lp - RN) is drained (as of this pass's watermark
+                // copy) writes unit A from lane 0 and unit B from lane 1; every
+                // other lane writes the same instruction into its own dummy slot
+                const bool chk = lp >= (uint32_t)RN && lp - RN >= drained;
+                const uint32_t rr = (lp - RN) / 64;
+                const uint32_t cw = wm_pick(cwm, rr % ND);
+                const bool fin = rdy && !done && xi >= np && (!chk || cw > rr / ND);
+                drained = (fin && chk) ? ((lp - RN) | 63u) + 1 : drained;
+                const uint32_t rs = (lp % RN) * 16u;
+                const uint32_t dmy = lds_addr(dummy) + lane * 16u;
+                const uint32_t wa = (fin && j < 2) ? (j == 0 ? RA : RB) + rs : dmy;
+                u4v x;
+                x.x = lp + 1; x.y = j == 0 ? r[0] : r[3 % CPW]; x.z = j == 0 ? r[1 % CPW] : 0u; x.w = j == 0 ? r[2 % CPW] : 0u;
+                // recent-event table of the owned branch (the drains' LowestAfter rows)
+                const bool own = fin && myvalid && mycol == br;
+                const uint32_t wb = own ? lds_addr(brc) + ((j & (CPW - 1)) * KB + seq % KB) * 8u : dmy + 1024u;
+                u2v y;
+                y.x = seq; y.y = bs + lp;
+                asm volatile("ds_write_b64 %2, %3\n\tds_write_b128 %0, %1" : : "v"(wa), "v"(x), "v"(wb), "v"(y) : "memory");
+                done = done || fin;
+#pragma unroll
+                for (int k = 0; k < 3; k++) { px[k] = fin ? kNullTag : px[k]; pa[k] = fin ? ANULL : pa[k]; }
+                LX_WP(c_done += fin ? 1u : 0u;)
+                LX_WP(c_wm += (rdy && !done && !fin) ? 1u : 0u;)
+            }
+            if (!rdy && ++stuck >= kLeanStuck) {
+                // waiting long: a parent's slot may have been reused by a newer
+                // event; its HB row from L2 once its drain stored it
+#pragma unroll
+                for (int k = 0; k < 3; k++) {
+                    const uint32_t x = px[k];
+                    if (x == kNullTag || (xa[k].x == x && xb[k].x == x) || max(xa[k].x, xb[k].x) <= x) continue;
+                    if (!round_done<ND>(sh.stored, x - 1u)) {
+                        LX_WP(c_wm++;)
+                        __hip_atomic_store(&sh.req, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        continue;
+                    }
+                    LX_WP(c_slow++;)
+                    const uint32_t *row = a.hb + (uint64_t)(x - 1u + bs) * stride;
+#pragma unroll
+                    for (int c = 0; c < CPW; c++)
+                        if (valid[c]) r[c] = max(r[c], ld_l2_now(row + pc[c]) & mask);
+                    px[k] = kNullTag;
+                    pa[k] = ANULL;
+                }
+            }
+            if (__all(done)) {
+                blk += NCW;
+                loaded = false;
+            }
+        }
+#ifdef LX_WALKER_PROF
+        if (a.prof) {
+            unsigned long long *pw = a.prof + ((uint64_t)blockIdx.x * kProfWaves + wave) * kProfSlots;
             const uint32_t cs[8] = {c_pass, 0u, 0u, c_done, c_slow, 0u, c_wm, c_norec};
 #pragma unroll
             for (int i = 0; i < 8; i++) atomicAdd(pw + i, (unsigned long long)cs[i]);
@@ -940,20 +1203,6 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
 #ifdef LX_WALKER_PROF
     uint32_t c_pass = 0, c_chunk = 0, c_done = 0, c_slow = 0, c_wm = 0, c_norec = 0;
     const unsigned long long t_start = wall_clock64();
-    // shader cycles per pass segment (wave-uniform; lane 0 reports):
-    // 0 record fetch, 1 fold, 2 parents beyond the inline ones, 3 completion,
-    // 4 the fold's ring-read round trip, 5 the fetch's record round trip
-    unsigned long long cyc[6] = {0, 0, 0, 0, 0, 0}, t_last = clock64();
-    uint32_t seg = 0;
-#define LX_SEG(k)                                  \
-    do {                                           \
-        const unsigned long long t_ = clock64();   \
-        cyc[seg] += t_ - t_last;                   \
-        t_last = t_;                               \
-        seg = (k);                                 \
-    } while (0)
-#else
-#define LX_SEG(k)
 #endif
 
     uint32_t lp = threadIdx.x;
@@ -968,14 +1217,11 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
 
     while (lp < n) {
         LX_WP(c_pass++;)
-        LX_SEG(0);
         if (!have) {
             const uint32_t slot = lp % RR;
             uint32_t tg;
             u4v rq[LX_REC_Q];
-            LX_SEG(5);
             rec_read(lds_addr(&rtag[slot / 64]), lds_addr(rrec) + rec_off(slot, 0) * 16u, tg, rq);
-            LX_SEG(0);
             if (tg != lp / 64 + 1) { LX_WP(c_norec++;) continue; }
             br = rq[0].x; seq = rq[0].y; np = rq[0].z;
 #pragma unroll
@@ -990,7 +1236,6 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
             for (int k = 0; k < CPW; k++) r[k] = (col[k] == br) ? seq : 0u;
             have = true;
         }
-        LX_SEG(1);
         if (todo) {
             // fold chunk cc (parents 4cc..4cc+3)
             LX_WP(c_chunk++;)
@@ -1005,9 +1250,7 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
             }
             const uint32_t tc = (todo >> (4 * cc)) & 15u;
             Slot<CPW> o[4];
-            LX_SEG(4);
             ring_read4w<CPW>(RA, RB, sl4, o, lds_addr(&sh.copied[0]), cwm);
-            LX_SEG(1);
             // branch-free common case: fold the parents whose slot is valid
             uint32_t okm = 0, oldm = 0;
 #pragma unroll
@@ -1030,7 +1273,7 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
                 for (int j = 0; j < 4; j++) {
                     if (!((oldm >> j) & 1u)) continue;
                     const uint32_t lpp = p4[j];
-                    if (lpp < n && !round_done(sh.stored, lpp)) {
+                    if (lpp < n && !round_done<ND>(sh.stored, lpp)) {
                         LX_WP(c_wm++;)
                         __hip_atomic_store(&sh.req, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     } else {
@@ -1053,7 +1296,6 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
             cc = rot ? (cc + 1 + (uint32_t)__builtin_ctz(rot)) % NCH : cc;
             if (todo) continue;
         }
-        LX_SEG(2);
         if (xi < np) {
             // parents beyond the inline LX_MAXP (rare): one per pass, from the ring or L2
             const uint32_t p = ld_l2_now(a.par_in + a.poff_in[lp] + xi);
@@ -1067,7 +1309,7 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
                     for (int k = 0; k < CPW; k++) r[k] = max(r[k], ps.v[k] & mask);
                     ok = true;
                 } else if (max(ps.t0, ps.t1) > lpp + 1) {
-                    if (round_done(sh.stored, lpp)) old = true;
+                    if (round_done<ND>(sh.stored, lpp)) old = true;
                     else __hip_atomic_store(&sh.req, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
             }
@@ -1081,7 +1323,6 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
             if (ok) xi++;
             continue;
         }
-        LX_SEG(3);
         {
             // complete: the slot's previous occupant (lp - RN) must be drained
             if (lp >= (uint32_t)RN && lp - RN >= drained) {
@@ -1089,7 +1330,7 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
                 // older one) answering "drained" is final; otherwise ask LDS now
                 const uint32_t rr = (lp - RN) / 64;
                 const uint32_t cw = (rr % kND) ? cwm.y : cwm.x;
-                if (cw <= rr / kND && !round_done(sh.copied, lp - RN)) { LX_WP(c_wm++;) continue; }
+                if (cw <= rr / kND && !round_done<ND>(sh.copied, lp - RN)) { LX_WP(c_wm++;) continue; }
                 drained = ((lp - RN) | 63u) + 1;   // its whole round
             }
             const uint32_t e = bs + lp;
@@ -1106,38 +1347,27 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
     }
 #ifdef LX_WALKER_PROF
     if (a.prof) {
-        unsigned long long *pw = a.prof + ((uint64_t)blockIdx.x * 8 + wave) * kProfSlots;
+        unsigned long long *pw = a.prof + ((uint64_t)blockIdx.x * kProfWaves + wave) * kProfSlots;
         const uint32_t cs[8] = {c_pass, 0u, c_chunk, c_done, c_slow, 0u, c_wm, c_norec};
 #pragma unroll
         for (int i = 0; i < 8; i++) atomicAdd(pw + i, (unsigned long long)cs[i]);
         atomicMax(pw + 8, (unsigned long long)c_pass);               // wave passes = max over lanes
         if (lane == 0) atomicMax(pw + 9, wall_clock64() - t_start);  // wall ticks (100 MHz)
-        LX_SEG(0);
-        if (lane == 0) {
-#pragma unroll
-            for (int i = 0; i < 4; i++) atomicAdd(pw + 10 + i, cyc[i]);
-            atomicAdd(pw + 14, cyc[0] + cyc[1] + cyc[2] + cyc[3] + cyc[4] + cyc[5]);
-            atomicAdd(pw + 10, cyc[5]);   // fetch includes its LDS round trip ...
-            atomicAdd(pw + 11, cyc[4]);   // ... and fold its ring reads
-            atomicAdd(pw + 15, cyc[4]);   // ring-read round trip alone
-            atomicAdd(pw + 5, cyc[5]);    // record round trip alone (slot 5 unused otherwise)
-        }
     }
 #endif
-#undef LX_SEG
     }
 }
 
-template <int CPW, int NCW, int RR, bool SMALL, bool LEAN = false>
+template <int CPW, int NCW, int RR, bool SMALL, int LEAN = 0, int ND = kND>
 static hipError_t launch_index_t(const IndexArgs &a0, hipStream_t s) {
     IndexArgs a = a0;
     a.n_slices = (a.ncols + CPW - 1) / CPW;
     a.slices_per_xcd = (a.n_slices + 7) / 8;
     uint32_t grid = a.slices_per_xcd * 8;
-    const dim3 blk(64 * (NCW + 1 + kND));
-    if (a.diag_nofill) hipLaunchKernelGGL((k_index<CPW, NCW, RR, false, SMALL, true, LEAN>), dim3(grid), blk, 0, s, a);
-    else if (a.mask) hipLaunchKernelGGL((k_index<CPW, NCW, RR, true, SMALL, true, LEAN>), dim3(grid), blk, 0, s, a);
-    else hipLaunchKernelGGL((k_index<CPW, NCW, RR, true, SMALL, false, LEAN>), dim3(grid), blk, 0, s, a);
+    const dim3 blk(64 * (NCW + 1 + ND));
+    if (a.diag_nofill) hipLaunchKernelGGL((k_index<CPW, NCW, RR, false, SMALL, true, LEAN, ND>), dim3(grid), blk, 0, s, a);
+    else if (a.mask) hipLaunchKernelGGL((k_index<CPW, NCW, RR, true, SMALL, true, LEAN, ND>), dim3(grid), blk, 0, s, a);
+    else hipLaunchKernelGGL((k_index<CPW, NCW, RR, true, SMALL, false, LEAN, ND>), dim3(grid), blk, 0, s, a);
     return hipGetLastError();
 }
 
@@ -1159,11 +1389,20 @@ static hipError_t launch_index_c(const IndexArgs &a, uint32_t ncw, hipStream_t s
         }
     }
     if constexpr (CPW == 4) {
-        if (a.lean) {
+        if (a.lean == 1) {
             // quads: 16 events in flight per compute wave
-            if (a.lean_ncw <= 4) return launch_index_t<CPW, 4, 1024, false, true>(a, s);
-            if (a.lean_ncw <= 8) return launch_index_t<CPW, 8, 1024, false, true>(a, s);
-            return launch_index_t<CPW, 12, 1024, false, true>(a, s);
+            if (a.lean_ncw <= 4) return launch_index_t<CPW, 4, 1024, false, 1>(a, s);
+            if (a.lean_ncw <= 8) return launch_index_t<CPW, 8, 1024, false, 1>(a, s);
+            return launch_index_t<CPW, 12, 1024, false, 1>(a, s);
+        }
+        if (a.lean == 2) {
+            if (a.drains >= 4) {
+                if (a.lean_ncw <= 8) return launch_index_t<CPW, 8, 1024, false, 2, 4>(a, s);
+                return launch_index_t<CPW, 11, 1024, false, 2, 4>(a, s);
+            }
+            if (a.lean_ncw <= 4) return launch_index_t<CPW, 4, 1024, false, 2>(a, s);
+            if (a.lean_ncw <= 8) return launch_index_t<CPW, 8, 1024, false, 2>(a, s);
+            return launch_index_t<CPW, 12, 1024, false, 2>(a, s);
         }
     }
     if (ncw <= 1) return launch_index_t<CPW, 1, 1024, false>(a, s);
