@@ -169,8 +169,12 @@ struct lx_index {
     bool small_timing = false;             // LX_TIMING=1: time small-path launches (two event records)
     uint32_t diag_nofill = 0;   // LX_DIAG_NOFILL=1: timing-only build of the walker (LA left empty)
     uint32_t cpw_hint = 0, ncw_hint = 0;   // LX_CPW / LX_NCW tuning overrides
-    uint32_t lean = 0, lean_ncw = 4;       // LX_WALKER=lean: quad-per-event compute waves (LX_LEAN_NCW)
-    uint32_t drains = 2;                   // LX_DRAINS: drain waves of the block walker (2 or 4)
+    // walker compute layout: 2 = blocks of 16 events per wave, quad of lanes
+    // per event (default), 1 = independent quads, 0 = one lane per event
+    // (LX_WALKER=block/lean/classic); LX_LEAN_NCW compute waves, LX_DRAINS
+    // drain waves of the block layout
+    uint32_t lean = 2, lean_ncw = 8;
+    uint32_t drains = 4;
     uint32_t rr_hint = 0, diag = 0;        // LX_RR record ring depth; LX_DIAG timing-only modes
     bool prof = false;                     // LX_PROF=1: per-wave walker counters to stderr
     uint32_t small = 0;                    // LX_SMALL=1: small-LDS walker (several workgroups per CU)
@@ -1317,7 +1321,7 @@ int lx_create(const lx_config *cfg, lx_index **out) {
     if (const char *d = getenv("LX_DIAG_NOFILL")) h->diag_nofill = (d[0] == '1');
     if (const char *d = getenv("LX_CPW")) h->cpw_hint = (uint32_t)atoi(d);
     if (const char *d = getenv("LX_NCW")) h->ncw_hint = (uint32_t)atoi(d);
-    if (const char *d = getenv("LX_WALKER")) h->lean = strcmp(d, "lean") == 0 ? 1 : strcmp(d, "block") == 0 ? 2 : 0;
+    if (const char *d = getenv("LX_WALKER")) h->lean = strcmp(d, "lean") == 0 ? 1 : strcmp(d, "classic") == 0 ? 0 : 2;
     if (const char *d = getenv("LX_LEAN_NCW")) h->lean_ncw = (uint32_t)atoi(d);
     if (const char *d = getenv("LX_DRAINS")) h->drains = (uint32_t)atoi(d);
     if (const char *d = getenv("LX_RR")) h->rr_hint = (uint32_t)atoi(d);

@@ -1396,7 +1396,7 @@ static hipError_t launch_index_c(const IndexArgs &a, uint32_t ncw, hipStream_t s
             return launch_index_t<CPW, 12, 1024, false, 1>(a, s);
         }
         if (a.lean == 2) {
-            if (a.drains >= 4) {
+            if (a.drains != 2) {
                 if (a.lean_ncw <= 8) return launch_index_t<CPW, 8, 1024, false, 2, 4>(a, s);
                 return launch_index_t<CPW, 11, 1024, false, 2, 4>(a, s);
             }
@@ -1414,7 +1414,9 @@ hipError_t launch_index(const IndexArgs &a, hipStream_t s) {
     if (a.n == 0 || a.ncols == 0) return hipSuccess;
     // columns per workgroup: aim at ~256 workgroups; compute waves: enough
     // events in flight for the DAG's antichain width (~V / (1.6 P))
-    uint32_t cpw = a.cpw_hint ? a.cpw_hint : (a.ncols <= 256 ? 1 : a.ncols <= 512 ? 2 : 4);
+    // (the quad / block layouts exist for 4-column slices; the walk time is
+    // levels x pass latency whatever the number of workgroups)
+    uint32_t cpw = a.cpw_hint ? a.cpw_hint : a.lean ? 4 : (a.ncols <= 256 ? 1 : a.ncols <= 512 ? 2 : 4);
     uint32_t ncw = a.ncw_hint ? a.ncw_hint : (a.width_hint <= 24 ? 1 : a.width_hint <= 48 ? 2 : 4);
     if (cpw <= 1) return launch_index_c<1>(a, ncw, s);
     if (cpw <= 2) return launch_index_c<2>(a, ncw, s);

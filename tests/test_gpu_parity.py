@@ -411,17 +411,22 @@ def test_full_size_properties_config2(lx):
 
 # ---------------------------------------------------------------- walker variants
 WALKER_VARIANTS = [
-    # environment read by lx_create: columns per workgroup, compute waves, small-LDS ring
-    {"LX_CPW": "1", "LX_NCW": "1"}, {"LX_CPW": "2", "LX_NCW": "2"}, {"LX_CPW": "4", "LX_NCW": "4"},
-    {"LX_CPW": "4", "LX_NCW": "1"}, {"LX_CPW": "1", "LX_NCW": "4"},
-    {"LX_SMALL": "1", "LX_CPW": "1", "LX_NCW": "1"}, {"LX_SMALL": "1", "LX_CPW": "2", "LX_NCW": "2"},
-    {"LX_RR": "512", "LX_CPW": "2", "LX_NCW": "4"}, {"LX_RR": "512", "LX_CPW": "2", "LX_NCW": "2"},
+    # environment read by lx_create: the one-lane-per-event layout (columns per
+    # workgroup, compute waves, small-LDS ring, record ring)
+    {"LX_WALKER": "classic", "LX_CPW": "1", "LX_NCW": "1"}, {"LX_WALKER": "classic", "LX_CPW": "2", "LX_NCW": "2"},
+    {"LX_WALKER": "classic", "LX_CPW": "4", "LX_NCW": "4"}, {"LX_WALKER": "classic", "LX_CPW": "4", "LX_NCW": "1"},
+    {"LX_WALKER": "classic", "LX_CPW": "1", "LX_NCW": "4"},
+    {"LX_WALKER": "classic", "LX_SMALL": "1", "LX_CPW": "1", "LX_NCW": "1"},
+    {"LX_WALKER": "classic", "LX_SMALL": "1", "LX_CPW": "2", "LX_NCW": "2"},
+    {"LX_WALKER": "classic", "LX_RR": "512", "LX_CPW": "2", "LX_NCW": "4"},
+    {"LX_WALKER": "classic", "LX_RR": "512", "LX_CPW": "2", "LX_NCW": "2"},
     # quad-per-event compute waves (CPW 4), 4 and 8 compute waves
     {"LX_CPW": "4", "LX_WALKER": "lean"}, {"LX_CPW": "4", "LX_WALKER": "lean", "LX_LEAN_NCW": "8"},
     # the same with wave-uniform blocks of 16 events
-    {"LX_CPW": "4", "LX_WALKER": "block"}, {"LX_CPW": "4", "LX_WALKER": "block", "LX_LEAN_NCW": "8"},
-    {"LX_CPW": "4", "LX_WALKER": "block", "LX_LEAN_NCW": "12"},
-    {"LX_CPW": "4", "LX_WALKER": "block", "LX_LEAN_NCW": "8", "LX_DRAINS": "4"},
+    {"LX_CPW": "4", "LX_WALKER": "block", "LX_LEAN_NCW": "4", "LX_DRAINS": "2"},
+    {"LX_CPW": "4", "LX_WALKER": "block", "LX_LEAN_NCW": "8", "LX_DRAINS": "2"},
+    {"LX_CPW": "4", "LX_WALKER": "block", "LX_LEAN_NCW": "12", "LX_DRAINS": "2"},
+    {"LX_WALKER": "block"},   # the default: 8 compute waves, 4 drains
     {"LX_CPW": "4", "LX_WALKER": "block", "LX_LEAN_NCW": "11", "LX_DRAINS": "4"},
 ]
 
@@ -449,7 +454,7 @@ def test_walker_variants(lx, env, monkeypatch):
 
 
 @pytest.mark.big_only
-@pytest.mark.parametrize("walker", ["", "lean", "block"])
+@pytest.mark.parametrize("walker", ["classic", "lean", "block"])
 def test_walker_many_parents(lx, walker, monkeypatch):
     """Events with more parents than a record holds inline (16 > 12) take the
     overflow path of the walker; CPW 4 with both compute layouts."""
