@@ -50,9 +50,10 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
 
 
 def measured_traffic(config, fc_queries):
-    """HBM bytes per launch from the committed PMC profile of this workload
-    (profiles/r*/traffic_<config>.json, made by scripts/prof_traffic.sh: separate
-    FETCH_SIZE / WRITE_SIZE passes, gfx950 FETCH_SIZE doubled), or None."""
+    """HBM bytes per launch from the newest committed PMC profile of this
+    workload (profiles/r*/traffic_<config>.json; round 2: scripts/prof_r02.sh,
+    reads from the L2's memory-side read requests by size, writes from
+    WRITE_SIZE, separate passes), or None."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "traffic_%s.json" % config)))
     if not files:

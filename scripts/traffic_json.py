@@ -1,9 +1,12 @@
-"""Convert the FETCH_SIZE / WRITE_SIZE passes of scripts/prof_round.sh into
-per-launch HBM bytes of k_index and k_fc (mean over dispatches).
+"""Per-launch HBM bytes of k_index and k_fc from the --pmc passes of
+scripts/prof_r02.sh (mean over dispatches, summed over TCC instances).
 
-FETCH_SIZE and WRITE_SIZE are in KiB.  Per MI355X_MICROARCH.md, gfx950's
-FETCH_SIZE counts half of the bytes of 16-B-per-lane streaming reads, so it is
-doubled (both kernels read with 16-B vector loads on their streaming paths).
+Reads: the L2's memory-side read requests by size, TCC_EA0_RDREQ_{32B,64B,128B}
+(bytes = 32 n32 + 64 n64 + 128 n128), which needs no assumption about the
+access pattern.  FETCH_SIZE, the older figure, is kept for reference: gfx950
+tallies a 128-B request at 64 B (MI355X_MICROARCH.md), so it undercounts wide
+streaming reads by 2x and is exact for narrow ones.  Writes: WRITE_SIZE (KiB)
+and the request counts TCC_EA0_WRREQ / _64B.
 """
 import csv
 import glob
@@ -12,40 +15,43 @@ import os
 import sys
 
 
-def per_kernel(root, counter):
+def per_kernel(root, counters):
     files = glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True)
     acc = {}
     for f in files:
         with open(f) as fh:
             for row in csv.DictReader(fh):
-                if row.get("Counter_Name") != counter:
+                c = row.get("Counter_Name")
+                if c not in counters:
                     continue
                 name = row["Kernel_Name"]
                 key = "k_fc" if "k_fc<" in name else "k_index" if "k_index<" in name else None
                 if key is None:
                     continue
-                d = acc.setdefault(key, {})
-                # one value per (dispatch, dimension instance): sum per dispatch
                 disp = row.get("Dispatch_Id") or row.get("Correlation_Id")
+                d = acc.setdefault(key, {}).setdefault(c, {})
                 d[disp] = d.get(disp, 0.0) + float(row["Counter_Value"])
-    return {k: sum(v.values()) / len(v) for k, v in acc.items() if v}
+    return {k: {c: sum(v.values()) / len(v) for c, v in cs.items()} for k, cs in acc.items()}
 
 
 def main():
     root = sys.argv[1]
-    fetch = per_kernel(os.path.join(root, "fetch"), "FETCH_SIZE")
-    write = per_kernel(os.path.join(root, "write"), "WRITE_SIZE")
-    out = {"workload": "c3", "fc_queries": 1 << 24,
-           "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes "
-                     "(scripts/prof_round.sh); mean over dispatches; FETCH_SIZE (KiB) doubled per "
-                     "MI355X_MICROARCH.md (gfx950 halves 16-B/lane streaming reads); WRITE_SIZE exact "
-                     "for 16-B stores, uncalibrated for the 1-B FC outputs and 4-B LA fills",
+    rd = per_kernel(os.path.join(root, "rdreq"), {"TCC_EA0_RDREQ_32B", "TCC_EA0_RDREQ_64B", "TCC_EA0_RDREQ_128B",
+                                                   "TCC_EA0_RDREQ"})
+    wr = per_kernel(os.path.join(root, "write"), {"WRITE_SIZE", "TCC_EA0_WRREQ", "TCC_EA0_WRREQ_64B"})
+    fe = per_kernel(os.path.join(root, "fetch"), {"FETCH_SIZE"})
+    out = {"workload": os.environ.get("CFG", "c3"), "fc_queries": 1 << 24,
+           "method": "rocprofv3 --pmc passes of scripts/prof_r02.sh (one TCC group per pass): reads = "
+                     "32*TCC_EA0_RDREQ_32B + 64*TCC_EA0_RDREQ_64B + 128*TCC_EA0_RDREQ_128B, writes = WRITE_SIZE "
+                     "(KiB); mean over dispatches, summed over TCC instances",
            "kernels": {}}
-    for k in sorted(set(fetch) | set(write)):
-        r = 2.0 * 1024 * fetch.get(k, 0.0)
-        w = 1024 * write.get(k, 0.0)
-        out["kernels"][k] = {"hbm_read_bytes": r, "hbm_write_bytes": w, "hbm_bytes": r + w,
-                             "FETCH_SIZE_KiB_mean": fetch.get(k), "WRITE_SIZE_KiB_mean": write.get(k)}
+    for k in sorted(set(rd) | set(wr)):
+        r = rd.get(k, {})
+        w = wr.get(k, {})
+        rb = 32 * r.get("TCC_EA0_RDREQ_32B", 0) + 64 * r.get("TCC_EA0_RDREQ_64B", 0) + 128 * r.get("TCC_EA0_RDREQ_128B", 0)
+        wb = 1024 * w.get("WRITE_SIZE", 0)
+        out["kernels"][k] = {"hbm_read_bytes": rb, "hbm_write_bytes": wb, "hbm_bytes": rb + wb, "counters": {**r, **w},
+                             "FETCH_SIZE_KiB_mean": fe.get(k, {}).get("FETCH_SIZE")}
     json.dump(out, sys.stdout, indent=1)
 
 
