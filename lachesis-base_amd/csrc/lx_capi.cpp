@@ -773,6 +773,7 @@ int fc_args(lx_index *h, uint64_t n, const uint32_t *a, const uint32_t *b, uint8
     f.cheat_crl = h->cheat_crl;
     f.quorum = h->quorum;
     f.ev_branch = h->ev_branch;
+    f.ev_creator = h->ev_creator;
     f.n_cheat = h->n_cheat;
     f.cheat_off = h->cheat_off;
     f.cheat_br = h->cheat_br;

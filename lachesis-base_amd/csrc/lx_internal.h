@@ -117,6 +117,7 @@ struct FcArgs {
     uint32_t vlo4, vhi4;         // column range in uint4 units
     uint32_t quorum;
     const uint32_t *ev_branch;
+    const uint32_t *ev_creator;  // creator per event (= creator of its branch)
     // cheaters of this shard: CSR over all their branches (first = original)
     uint32_t n_cheat;
     const uint32_t *cheat_off;

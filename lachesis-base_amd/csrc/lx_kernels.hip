@@ -1014,6 +1014,7 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
         const uint32_t mycol = col[j & (CPW - 1)];
         const bool myvalid = valid[j & (CPW - 1)];
         uint32_t blk = wave;
+        if (a.diag & 16) __builtin_amdgcn_s_setprio(2);   // diagnostic: compute waves first
         bool loaded = false, done = true;
         uint32_t br = 0, seq = 0, np = 0, xi = 0, stuck = 0;
         uint32_t px[3] = {kNullTag, kNullTag, kNullTag};
@@ -1498,6 +1499,12 @@ __global__ __launch_bounds__(256) void k_fc(FcArgs a) {
         uint32_t A = a.qa[q], Bq = a.qb[q];
         const bool bad = (A >= a.n_events) | (Bq >= a.n_events);
         if (bad) { A = 0; Bq = 0; }
+        // FORKS, lane 0: the early-false inputs first (their loads overlap the rows')
+        uint32_t e_bb = 0, e_cb = 0;
+        if (FORKS && lane == 0) {
+            e_bb = a.ev_branch[Bq];
+            e_cb = a.ev_creator[Bq];
+        }
         const uint4 *ha = reinterpret_cast<const uint4 *>(a.hb + (uint64_t)A * a.stride) + a.vlo4;
         const uint4 *lb = reinterpret_cast<const uint4 *>(a.la + (uint64_t)Bq * a.stride) + a.vlo4;
         uint4 h[kR], l[kR];
@@ -1531,6 +1538,11 @@ __global__ __launch_bounds__(256) void k_fc(FcArgs a) {
         if (FORKS) {
             const uint32_t *hrow = a.hb + (uint64_t)A * a.stride;
             const uint32_t *lrow = a.la + (uint64_t)Bq * a.stride;
+            uint32_t hm = 0;
+            if (lane == 0) {
+                const uint32_t hc = a.cmap ? a.cmap[e_bb] : e_bb;   // NONE: another shard's branch
+                hm = hc != LX_NONE ? hrow[hc] : 0u;
+            }
             // plane columns (cheat_crl / cheat_brl): the creator's original
             // branch and its fork branches
             for (uint32_t c = lane; c < a.n_cheat; c += LPQ) {
@@ -1544,11 +1556,8 @@ __global__ __launch_bounds__(256) void k_fc(FcArgs a) {
                 }
                 if (!cn && hit) sum += a.wpad[n];
             }
-            if (lane == 0) {
-                const uint32_t bb = a.ev_branch[Bq];
-                const uint32_t cb = a.branch_creator[bb];
-                if (cb >= a.own_lo && cb < a.own_hi && (hrow[a.cmap ? a.cmap[bb] : bb] & LX_MARK)) early = 1;
-            }
+            // early false (forkless_cause.go:49-54); creator(branch(b)) = creator(b)
+            if (lane == 0 && e_cb >= a.own_lo && e_cb < a.own_hi && (hm & LX_MARK)) early = 1;
         }
 #pragma unroll
         for (int off = LPQ / 2; off > 0; off >>= 1) sum += __shfl_xor(sum, off, LPQ);
