@@ -510,6 +510,14 @@ constexpr uint32_t kNullTag = 0xFFFFFFFFu;   // lean null slot: never an event t
 __device__ __forceinline__ uint32_t wm_pick(const u4v &w, uint32_t i) {
     return i == 0 ? w.x : i == 1 ? w.y : i == 2 ? w.z : w.w;
 }
+// any of a lane's three parents (expected tag = local index + 1, or kNullTag)
+// at least `reach` events before event lp
+__device__ __forceinline__ bool far_parent(const uint32_t px[3], uint32_t lp, uint32_t reach) {
+    bool f = false;
+#pragma unroll
+    for (int k = 0; k < 3; k++) f |= px[k] != kNullTag && lp - (px[k] - 1u) >= reach;
+    return f;
+}
 // DPP quad permutations (lanes 4q..4q+3): swap neighbours, swap pairs
 constexpr int kQuadSwap1 = 0xB1;   // quad_perm [1,0,3,2]
 constexpr int kQuadSwap2 = 0x4E;   // quad_perm [2,3,0,1]
@@ -814,6 +822,7 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
         // bookkeeping per pass small.
         constexpr uint32_t GE = 16 * NCW;            // events in flight: one per quad
         constexpr uint32_t kLeanStuck = 64;          // passes before a waiting event checks for reused slots
+        constexpr uint32_t kLeanFar = 512;           // parents this close to the ring's reach: checked at once
         constexpr uint32_t LEAN_BOFF = (RN + 1) * 16;   // unit B of a slot, from its unit A (= RB - RA)
         static_assert(LEAN_BOFF < 65536, "ds offset field");
         const uint32_t ANULL = RA + (uint32_t)(RN * 16);
@@ -881,7 +890,9 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
                         }
                     }
                     xi = LX_MAXP;
-                    stuck = 0;
+                    // a parent far enough back that its slot may already hold a newer event
+                    // is checked against the L2 path from the first pass on
+                    stuck = far_parent(px, lp, (uint32_t)RN - kLeanFar) ? kLeanStuck : 0u;
                     have = true;
                 } else {
                     LX_WP(c_norec++;)
@@ -1007,6 +1018,7 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
         // wave-uniform branches; per pass only the publish of newly ready
         // quads is divergent.
         constexpr uint32_t kLeanStuck = 64;
+        constexpr uint32_t kLeanFar = 512;
         constexpr uint32_t LEAN_BOFF = (RN + 1) * 16;
         static_assert(LEAN_BOFF < 65536, "ds offset field");
         const uint32_t ANULL = RA + (uint32_t)(RN * 16);
@@ -1077,7 +1089,9 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
                     }
                 }
                 xi = LX_MAXP;
-                stuck = 0;
+                // a parent far enough back that its slot may already hold a newer event
+                // is checked against the L2 path from the first pass on
+                stuck = far_parent(px, lp, (uint32_t)RN - kLeanFar) ? kLeanStuck : 0u;
                 done = !live;
                 loaded = true;
             }

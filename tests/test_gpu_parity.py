@@ -474,6 +474,58 @@ def test_walker_many_parents(lx, walker, monkeypatch):
     ix.close()
 
 
+def far_parent_dag(lx, n_nodes, n, seed):
+    """A valid DAG whose non-self parents are uniform over ALL earlier events:
+    many parents lie thousands of events back, beyond the walker's LDS ring, so
+    their slots are reused while their children wait (the L2 fallback paths)."""
+    rng = np.random.default_rng(seed)
+    creator = np.zeros(n, dtype=np.uint32)
+    seq = np.zeros(n, dtype=np.uint32)
+    lam = np.zeros(n, dtype=np.uint32)
+    poff = [0]
+    par = []
+    last = [-1] * n_nodes
+    for i in range(n):
+        c = int(rng.integers(n_nodes))
+        ps = [last[c]] if last[c] >= 0 else []
+        if i:
+            for x in rng.integers(0, i, size=int(rng.integers(0, 5))):
+                if int(x) not in ps and creator[int(x)] != c:
+                    ps.append(int(x))
+        creator[i] = c
+        seq[i] = (seq[last[c]] + 1) if last[c] >= 0 else 1
+        lam[i] = 1 + max([int(lam[p]) for p in ps], default=0)
+        last[c] = i
+        par.extend(ps)
+        poff.append(len(par))
+    return lx.tools.Dag(creator, seq, lam, np.array(poff, dtype=np.uint64), np.array(par or [0], dtype=np.uint32),
+                        n_nodes)
+
+
+@pytest.mark.big_only
+@pytest.mark.parametrize("walker", ["classic", "lean", "block"])
+def test_walker_far_parents(lx, walker, monkeypatch):
+    """Parents far older than the ring (slot reuse while an event waits) in
+    one batch and across batches, for each compute layout, bit-exact."""
+    monkeypatch.setenv("LX_CPW", "4")
+    monkeypatch.setenv("LX_WALKER", walker)
+    d = far_parent_dag(lx, 16, 12000, 91)
+    weights = list(range(50, 34, -1))
+    o = oracle_for(d, weights)
+    for chunks in (1, 3):
+        ix = lx.Index()
+        ix.reset(weights)
+        cuts = np.linspace(0, len(d), chunks + 1).astype(int)
+        for lo, hi in zip(cuts[:-1], cuts[1:]):
+            p0, p1 = int(d.poff[lo]), int(d.poff[hi])
+            ix.add_batch(d.creator[lo:hi], d.seq[lo:hi], d.poff[lo:hi + 1] - p0, d.par[p0:p1])
+        rng = np.random.default_rng(chunks)
+        compare_rows(ix, o, rng.choice(len(d), 1500, replace=False))
+        qa, qb = lx.tools.fc_queries(d.lamport, 100_000, window=64, seed=4)
+        np.testing.assert_array_equal(ix.forkless_cause_batch(qa, qb), o.forkless_cause_batch(qa, qb))
+        ix.close()
+
+
 def test_reset_reuses_planes(lx):
     """lx_reset on a used handle (same layout) clears exactly what the next epoch
     may read: epoch 1 dirties fork-branch columns, epoch 2 (different V, new
