@@ -1035,7 +1035,13 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
 #pragma unroll
         for (int k = 0; k < CPW; k++) r[k] = 0;
         uint32_t drained = 0;
-        u4v cwm = {0u, 0u, 0u, 0u};   // all drains' `copied` watermarks (16 B)
+        // per-event publish constants, set at the block fetch: LDS targets of
+        // this lane's slot unit and recent-event entry (dummy when not its
+        // role), the drain watermark that frees the event's slot
+        const uint32_t dmy = lds_addr(dummy) + lane * 16u;
+        uint32_t wa_pub = dmy, wb_pub = dmy + 1024u, wm_addr = lds_addr(&sh.copied[0]), rrq = 0;
+        bool chk0 = false;
+        uint32_t cw = 0;   // that watermark, read with the parents every pass
 #ifdef LX_WALKER_PROF
         uint32_t c_pass = 0, c_done = 0, c_slow = 0, c_wm = 0, c_norec = 0;
         const unsigned long long t_start = wall_clock64();
@@ -1092,6 +1098,16 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
                 // a parent far enough back that its slot may already hold a newer event
                 // is checked against the L2 path from the first pass on
                 stuck = far_parent(px, lp, (uint32_t)RN - kLeanFar) ? kLeanStuck : 0u;
+                {
+                    const uint32_t rs = (lp % RN) * 16u;
+                    wa_pub = j == 0 ? RA + rs : j == 1 ? RB + rs : dmy;
+                    wb_pub = (myvalid && mycol == br) ? lds_addr(brc) + ((j & (CPW - 1)) * KB + seq % KB) * 8u
+                                                      : dmy + 1024u;
+                    chk0 = lp >= (uint32_t)RN;
+                    const uint32_t rr = (lp - RN) / 64;
+                    rrq = rr / ND;
+                    wm_addr = lds_addr(&sh.copied[rr % ND]);
+                }
                 done = !live;
                 loaded = true;
             }
@@ -1104,10 +1120,10 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
                 "ds_read_b128 %3, %8 offset:%10\n\t"
                 "ds_read_b128 %4, %9\n\t"
                 "ds_read_b128 %5, %9 offset:%10\n\t"
-                "ds_read_b128 %6, %11\n\t"
+                "ds_read_b32 %6, %11\n\t"
                 "s_waitcnt lgkmcnt(0)"
-                : "=&v"(xa0), "=&v"(xb0), "=&v"(xa1), "=&v"(xb1), "=&v"(xa2), "=&v"(xb2), "=&v"(cwm)
-                : "v"(pa[0]), "v"(pa[1]), "v"(pa[2]), "i"(LEAN_BOFF), "v"(lds_addr(&sh.copied[0]))
+                : "=&v"(xa0), "=&v"(xb0), "=&v"(xa1), "=&v"(xb1), "=&v"(xa2), "=&v"(xb2), "=&v"(cw)
+                : "v"(pa[0]), "v"(pa[1]), "v"(pa[2]), "i"(LEAN_BOFF), "v"(wm_addr)
                 : "memory");
             const u4v xa[3] = {xa0, xa1, xa2};
             const u4v xb[3] = {xb0, xb1, xb2};
@@ -1151,32 +1167,25 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
             }
             {
                 // publish, branch-free: a ready quad whose slot's previous
-                // occupant (lp - RN) is drained (as of this pass's watermark
-                // copy) writes unit A from lane 0 and unit B from lane 1; every
-                // other lane writes the same instruction into its own dummy slot
-                const bool chk = lp >= (uint32_t)RN && lp - RN >= drained;
-                const uint32_t rr = (lp - RN) / 64;
-                const uint32_t cw = wm_pick(cwm, rr % ND);
-                const bool fin = rdy && !done && xi >= np && (!chk || cw > rr / ND);
+                // occupant (lp - RN) is drained (as of this pass's watermark)
+                // writes unit A from lane 0 and unit B from lane 1, and its
+                // recent-event entry; every other lane writes the same
+                // instructions into its own dummy slot
+                const bool chk = chk0 && lp - RN >= drained;
+                const bool fin = rdy && !done && xi >= np && (!chk || cw > rrq);
                 drained = (fin && chk) ? ((lp - RN) | 63u) + 1 : drained;
-                const uint32_t rs = (lp % RN) * 16u;
-                const uint32_t dmy = lds_addr(dummy) + lane * 16u;
-                const uint32_t wa = (fin && j < 2) ? (j == 0 ? RA : RB) + rs : dmy;
+                const uint32_t wa = fin ? wa_pub : dmy;
+                const uint32_t wb = fin ? wb_pub : dmy + 1024u;
                 u4v x;
                 x.x = lp + 1; x.y = j == 0 ? r[0] : r[3 % CPW]; x.z = j == 0 ? r[1 % CPW] : 0u; x.w = j == 0 ? r[2 % CPW] : 0u;
-                // recent-event table of the owned branch (the drains' LowestAfter rows)
-                const bool own = fin && myvalid && mycol == br;
-                const uint32_t wb = own ? lds_addr(brc) + ((j & (CPW - 1)) * KB + seq % KB) * 8u : dmy + 1024u;
                 u2v y;
                 y.x = seq; y.y = bs + lp;
                 asm volatile("ds_write_b64 %2, %3\n\tds_write_b128 %0, %1" : : "v"(wa), "v"(x), "v"(wb), "v"(y) : "memory");
-                done = done || fin;
-#pragma unroll
-                for (int k = 0; k < 3; k++) { px[k] = fin ? kNullTag : px[k]; pa[k] = fin ? ANULL : pa[k]; }
                 LX_WP(c_done += fin ? 1u : 0u;)
                 LX_WP(c_wm += (rdy && !done && !fin) ? 1u : 0u;)
+                done = done || fin;
             }
-            if (!rdy && ++stuck >= kLeanStuck) {
+            if (!rdy && !done && ++stuck >= kLeanStuck) {
                 // waiting long: a parent's slot may have been reused by a newer
                 // event; its HB row from L2 once its drain stored it
 #pragma unroll
