@@ -599,7 +599,9 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
     if (wave == NCW) {
         // ------------------------------------------------------------ loader
         const uint32_t nrounds = (n + 63) / 64;
-        constexpr uint32_t D = RR / 64 < 8 ? RR / 64 : 8;
+        // rounds in flight: the DMA round trip is long while the CU's memory
+        // queue also carries the drains' stores (the block walker starved at 8)
+        constexpr uint32_t D = LEAN ? (RR / 64 - 1 < 15 ? RR / 64 - 1 : 15) : (RR / 64 < 8 ? RR / 64 : 8);
         uint32_t issued = 0, done = 0;
 #ifdef LX_WALKER_PROF
         uint32_t l_iter = 0, l_slot = 0, l_sleep = 0;
@@ -626,6 +628,7 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
             }
             if (!progressed && issued > done) {
                 // the oldest round landed once at most RQ DMAs per younger round remain
+                static_assert(D <= 15 && RQ == 4, "vmcnt field (6 bits): at most 14 younger rounds of 4 DMAs");
                 switch (issued - done - 1) {
                     case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
                     case 1: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
@@ -634,7 +637,14 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
                     case 4: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
                     case 5: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
                     case 6: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
-                    default: asm volatile("s_waitcnt vmcnt(28)" ::: "memory"); break;
+                    case 7: asm volatile("s_waitcnt vmcnt(28)" ::: "memory"); break;
+                    case 8: asm volatile("s_waitcnt vmcnt(32)" ::: "memory"); break;
+                    case 9: asm volatile("s_waitcnt vmcnt(36)" ::: "memory"); break;
+                    case 10: asm volatile("s_waitcnt vmcnt(40)" ::: "memory"); break;
+                    case 11: asm volatile("s_waitcnt vmcnt(44)" ::: "memory"); break;
+                    case 12: asm volatile("s_waitcnt vmcnt(48)" ::: "memory"); break;
+                    case 13: asm volatile("s_waitcnt vmcnt(52)" ::: "memory"); break;
+                    default: asm volatile("s_waitcnt vmcnt(56)" ::: "memory"); break;
                 }
                 if (lane == 0) __hip_atomic_store(&rtag[done % (RR / 64)], done + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                 done++;
