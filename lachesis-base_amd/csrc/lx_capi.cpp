@@ -87,6 +87,13 @@ struct lx_index {
     int32_t *cheat_of = nullptr;           // creator -> index into the cheater CSR (-1: one branch)
     uint32_t cheat_of_cap = 0;
     uint32_t n_cheat = 0, ncols = 0;
+    // fork-path ForklessCause tables per plane column (k_fc_fk; valid when
+    // fk_hi4 != 0): weight of a non-cheater's original, cheater index of a
+    // cheater's branches, the cheaters' weights
+    uint32_t *fk_w = nullptr, *fk_c = nullptr, *fk_wch = nullptr;
+    uint64_t fk_cap = 0;
+    uint32_t fk_hi4 = 0;
+    bool fc_fk = true;                     // LX_FC_FK=0: the fix-up loop kernel instead (A/B)
     // column shard (shard_count > 1): own columns only (lx_internal.h)
     std::vector<uint32_t> h_cmap;          // global branch -> plane column / LX_NONE
     uint32_t nloc = 0;                     // plane columns in use
@@ -230,10 +237,13 @@ void free_all(lx_index *h) {
         if (p) (void)hipFree(p);
     h->tail_zw = h->tail_lo = h->tail_cmin = h->wire_flag = nullptr;
     h->tail_cap = 0;
-    void *lptrs[] = {h->cheat_brl, h->cheat_crl, h->cmap, h->lap, h->wloc, h->cheat_of};
+    void *lptrs[] = {h->cheat_brl, h->cheat_crl, h->cmap, h->lap, h->wloc, h->cheat_of, h->fk_w, h->fk_c, h->fk_wch};
     for (void *p : lptrs)
         if (p) (void)hipFree(p);
     h->cheat_brl = h->cheat_crl = h->cmap = h->lap = h->wloc = nullptr;
+    h->fk_w = h->fk_c = h->fk_wch = nullptr;
+    h->fk_cap = 0;
+    h->fk_hi4 = 0;
     h->cheat_of = nullptr;
     h->cheat_of_cap = 0;
     h->cmap_cap = 0;
@@ -494,6 +504,7 @@ int rebuild_columns(lx_index *h) {
         off.push_back((uint32_t)br.size());
     }
     h->n_cheat = (uint32_t)cr.size();
+    const std::vector<uint32_t> cr_glob = cr;   // cr becomes plane columns below (shards)
     if (h->V > h->cheat_of_cap) {
         if (h->cheat_of) (void)hipFree(h->cheat_of);
         h->cheat_of = nullptr;
@@ -524,6 +535,40 @@ int rebuild_columns(lx_index *h) {
         }
         HIPCHK(h, hipMemcpyAsync(h->cheat_brl, br.data(), br.size() * 4, hipMemcpyHostToDevice, h->stream));
         HIPCHK(h, hipMemcpyAsync(h->cheat_crl, cr.data(), cr.size() * 4, hipMemcpyHostToDevice, h->stream));
+    }
+    // fork-path FC tables (k_fc_fk streams every plane column; <= 64 cheaters
+    // per handle, beyond that the cheater fix-up loop of k_fc<.., true>)
+    std::vector<uint32_t> fw, fc, wch;   // alive until the sync below
+    h->fk_hi4 = 0;
+    if (h->fc_fk && h->n_cheat && h->n_cheat <= kFcFkMaxCheaters) {
+        const uint32_t npc = h->sharded() ? h->nloc : h->B;
+        const uint64_t cap = round_up(npc, 4);
+        if (cap > h->fk_cap) {
+            uint32_t **arrs[] = {&h->fk_w, &h->fk_c};
+            for (uint32_t **a : arrs) {
+                if (*a) (void)hipFree(*a);
+                *a = nullptr;
+            }
+            h->fk_cap = 0;
+            for (uint32_t **a : arrs) HIPCHK(h, dalloc(a, cap + cap / 2));
+            h->fk_cap = cap + cap / 2;
+        }
+        if (!h->fk_wch) HIPCHK(h, dalloc(&h->fk_wch, kFcFkMaxCheaters));
+        fw.assign(cap, 0);
+        fc.assign(cap, LX_NONE);
+        for (uint32_t b : cols) {
+            const uint32_t c = h->h_branch_creator[b];
+            const uint32_t pc = h->sharded() ? h->h_cmap[b] : b;
+            if (pc >= cap) return h->fail(LX_ERR_STATE, "fork FC table: plane column %u past %u", pc, npc);
+            if (co[c] >= 0) fc[pc] = (uint32_t)co[c];
+            else fw[pc] = b < h->V ? h->weights[c] : 0u;
+        }
+        wch.assign(kFcFkMaxCheaters, 0);
+        for (uint32_t k = 0; k < h->n_cheat; k++) wch[k] = h->weights[cr_glob[k]];
+        HIPCHK(h, hipMemcpyAsync(h->fk_w, fw.data(), cap * 4, hipMemcpyHostToDevice, h->stream));
+        HIPCHK(h, hipMemcpyAsync(h->fk_c, fc.data(), cap * 4, hipMemcpyHostToDevice, h->stream));
+        HIPCHK(h, hipMemcpyAsync(h->fk_wch, wch.data(), wch.size() * 4, hipMemcpyHostToDevice, h->stream));
+        h->fk_hi4 = (uint32_t)(cap / 4);
     }
     HIPCHK(h, hipStreamSynchronize(h->stream));
     return 0;
@@ -771,6 +816,10 @@ int fc_args(lx_index *h, uint64_t n, const uint32_t *a, const uint32_t *b, uint8
     }
     f.cheat_brl = h->cheat_brl;
     f.cheat_crl = h->cheat_crl;
+    f.fk_w = h->fk_w;
+    f.fk_c = h->fk_c;
+    f.fk_wch = h->fk_wch;
+    f.fk_hi4 = h->fk_hi4;
     f.quorum = h->quorum;
     f.ev_branch = h->ev_branch;
     f.ev_creator = h->ev_creator;
@@ -1320,6 +1369,7 @@ int lx_create(const lx_config *cfg, lx_index **out) {
         return LX_ERR_HIP;
     }
     if (const char *d = getenv("LX_DIAG_NOFILL")) h->diag_nofill = (d[0] == '1');
+    if (const char *d = getenv("LX_FC_FK")) h->fc_fk = (d[0] != '0');
     if (const char *d = getenv("LX_CPW")) h->cpw_hint = (uint32_t)atoi(d);
     if (const char *d = getenv("LX_NCW")) h->ncw_hint = (uint32_t)atoi(d);
     if (const char *d = getenv("LX_WALKER")) h->lean = strcmp(d, "lean") == 0 ? 1 : strcmp(d, "classic") == 0 ? 0 : 2;

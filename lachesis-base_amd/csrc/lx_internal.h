@@ -129,7 +129,16 @@ struct FcArgs {
     uint32_t own_lo, own_hi;     // creator range owned by this shard
     const uint32_t *branch_creator;
     uint32_t *status;            // status[1] |= bad-event flag
+    // fork DAGs with <= kFcFkMaxCheaters cheaters (fk_hi4 != 0): per plane
+    // column [0, 4 fk_hi4) the weight of a non-cheater's original branch
+    // (fk_w) and the cheater index of a cheater's branches (fk_c, LX_NONE
+    // otherwise); the cheaters' weights (fk_wch)
+    const uint32_t *fk_w;
+    const uint32_t *fk_c;
+    const uint32_t *fk_wch;
+    uint32_t fk_hi4;
 };
+constexpr uint32_t kFcFkMaxCheaters = 64;   // one 64-bit mask per query
 
 struct MarkArgs {
     uint32_t *hb;

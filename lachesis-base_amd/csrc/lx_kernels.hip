@@ -1605,13 +1605,140 @@ __global__ __launch_bounds__(256) void k_fc(FcArgs a) {
     }
 }
 
+// Fork DAGs (few cheaters): every plane column is streamed -- originals and
+// fork branches alike -- instead of re-reading the cheaters' columns with
+// dependent scalar loads after the stream.  A non-cheater's original counts
+// its weight directly (fk_w); a counting branch of cheater k sets bit k of the
+// query's 64-bit mask (fk_c), the mask is OR-reduced over the query's lanes and
+// each set bit adds cheater k's weight once: WeightCounter.CountByIdx's
+// per-creator dedupe (inter/pos/stake.go:47-55) over all branches of the
+// creator, vecfc/forkless_cause.go:63-78.  Marked branches count 0 (fc_term),
+// the early false of forkless_cause.go:49-54 as in k_fc.
+template <int LPQ, typename M>   // M: the cheater mask, uint32_t (<= 32 cheaters) or uint64_t
+__global__ __launch_bounds__(256) void k_fc_fk(FcArgs a) {
+    constexpr uint32_t MB = 8 * sizeof(M);
+    const int lane = threadIdx.x % LPQ;
+    const uint64_t qpb = 256 / LPQ;
+    const uint32_t nv = a.fk_hi4;
+    constexpr int kR = 4;
+    constexpr int kW = (int)MB / LPQ > 0 ? (int)MB / LPQ : 1;
+    const uint4 *wv = reinterpret_cast<const uint4 *>(a.fk_w);
+    const uint4 *cv = reinterpret_cast<const uint4 *>(a.fk_c);
+    // per lane, its columns' weights and cheater bits stay in registers
+    uint4 wr[kR];
+    M cm[kR][4];
+    auto cbit = [](uint32_t k) -> M { return k < MB ? ((M)1 << k) : (M)0; };
+#pragma unroll
+    for (int t = 0; t < kR; t++) {
+        const uint32_t i = lane + t * LPQ;
+        const bool in = i < nv;
+        wr[t] = in ? wv[i] : make_uint4(0, 0, 0, 0);
+        const uint4 c = in ? cv[i] : make_uint4(LX_NONE, LX_NONE, LX_NONE, LX_NONE);
+        cm[t][0] = cbit(c.x); cm[t][1] = cbit(c.y); cm[t][2] = cbit(c.z); cm[t][3] = cbit(c.w);
+    }
+    // this lane's share of the cheaters' weights: cheater lane + t * LPQ
+    uint32_t wch[kW];
+#pragma unroll
+    for (int t = 0; t < kW; t++) {
+        const uint32_t k = lane + t * LPQ;
+        wch[t] = k < a.n_cheat ? a.fk_wch[k] : 0u;
+    }
+    for (uint64_t q = blockIdx.x * qpb + threadIdx.x / LPQ; q < a.n; q += (uint64_t)gridDim.x * qpb) {
+        uint32_t A = a.qa[q], Bq = a.qb[q];
+        const bool bad = (A >= a.n_events) | (Bq >= a.n_events);
+        if (bad) { A = 0; Bq = 0; }
+        uint32_t e_bb = 0, e_cb = 0;
+        if (lane == 0) {
+            e_bb = a.ev_branch[Bq];
+            e_cb = a.ev_creator[Bq];
+        }
+        const uint4 *ha = reinterpret_cast<const uint4 *>(a.hb + (uint64_t)A * a.stride);
+        const uint4 *lb = reinterpret_cast<const uint4 *>(a.la + (uint64_t)Bq * a.stride);
+        uint4 h[kR], l[kR];
+#pragma unroll
+        for (int t = 0; t < kR; t++) {
+            const uint32_t i = min((uint32_t)(lane + t * LPQ), nv - 1u);
+            if (LPQ == 64) {
+                const u4v hv = __builtin_nontemporal_load(reinterpret_cast<const u4v *>(ha + i));
+                const u4v lv = __builtin_nontemporal_load(reinterpret_cast<const u4v *>(lb + i));
+                h[t] = make_uint4(hv.x, hv.y, hv.z, hv.w);
+                l[t] = make_uint4(lv.x, lv.y, lv.z, lv.w);
+            } else {
+                h[t] = ha[i];
+                l[t] = lb[i];
+            }
+        }
+        uint32_t sum = 0;
+        M m = 0;
+#pragma unroll
+        for (int t = 0; t < kR; t++) {   // wr[t] / cm[t] are zero past the row
+            const uint32_t hh[4] = {h[t].x, h[t].y, h[t].z, h[t].w};
+            const uint32_t ll[4] = {l[t].x, l[t].y, l[t].z, l[t].w};
+            const uint32_t ww[4] = {wr[t].x, wr[t].y, wr[t].z, wr[t].w};
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                const bool on = fc_term(ll[c], hh[c], 1u, true) != 0;
+                sum += on ? ww[c] : 0u;
+                m |= on ? cm[t][c] : (M)0;
+            }
+        }
+        for (uint32_t i = lane + kR * LPQ; i < nv; i += LPQ) {   // rows longer than kR*LPQ uint4
+            const uint4 hv = ha[i], lv = lb[i], w = wv[i], cc = cv[i];
+            const uint32_t hh[4] = {hv.x, hv.y, hv.z, hv.w};
+            const uint32_t ll[4] = {lv.x, lv.y, lv.z, lv.w};
+            const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
+            const uint32_t ck[4] = {cc.x, cc.y, cc.z, cc.w};
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                const bool on = fc_term(ll[c], hh[c], 1u, true) != 0;
+                sum += on ? ww[c] : 0u;
+                m |= on ? cbit(ck[c]) : (M)0;
+            }
+        }
+        uint32_t early = 0;
+        if (lane == 0) {
+            const uint32_t hc = a.cmap ? a.cmap[e_bb] : e_bb;   // NONE: another shard's branch
+            const uint32_t hm = hc != LX_NONE ? a.hb[(uint64_t)A * a.stride + hc] : 0u;
+            if (e_cb >= a.own_lo && e_cb < a.own_hi && (hm & LX_MARK)) early = 1;
+        }
+        // cheaters with a counting branch: OR over the query's lanes, then each
+        // lane adds the weights of its share of them
+        if constexpr (MB == 64) {
+            uint32_t mlo = (uint32_t)m, mhi = (uint32_t)((uint64_t)m >> 32);
+#pragma unroll
+            for (int off = LPQ / 2; off > 0; off >>= 1) {
+                mlo |= __shfl_xor(mlo, off, LPQ);
+                mhi |= __shfl_xor(mhi, off, LPQ);
+            }
+            m = (M)(((uint64_t)mhi << 32) | mlo);
+        } else {
+#pragma unroll
+            for (int off = LPQ / 2; off > 0; off >>= 1) m |= (M)__shfl_xor((uint32_t)m, off, LPQ);
+        }
+#pragma unroll
+        for (int t = 0; t < kW; t++) sum += (lane + t * LPQ < MB && ((m >> (lane + t * LPQ)) & 1u)) ? wch[t] : 0u;
+#pragma unroll
+        for (int off = LPQ / 2; off > 0; off >>= 1) sum += __shfl_xor(sum, off, LPQ);
+        if (lane == 0) {
+            if (a.partial) {
+                a.partial[q] = sum + (early ? LX_MARK : 0u);
+            } else {
+                a.out[q] = bad ? 0xFF : (uint8_t)(!early && sum >= a.quorum);
+            }
+            if (bad) atomicOr(&a.status[1], 1u);
+        }
+    }
+}
+
 template <int LPQ>
 static hipError_t launch_fc_t(const FcArgs &a, bool forks, hipStream_t s) {
     const uint64_t qpb = 256 / LPQ;
     uint64_t blocks = (a.n + qpb - 1) / qpb;
     if (blocks > 256 * 32) blocks = 256 * 32;
     if (blocks == 0) return hipSuccess;
-    if (forks) hipLaunchKernelGGL((k_fc<LPQ, true>), dim3((uint32_t)blocks), dim3(256), 0, s, a);
+    if (forks && a.fk_hi4 && a.n_cheat <= 32) hipLaunchKernelGGL((k_fc_fk<LPQ, uint32_t>), dim3((uint32_t)blocks), dim3(256), 0, s, a);
+    else if (forks && a.fk_hi4) hipLaunchKernelGGL((k_fc_fk<LPQ, uint64_t>), dim3((uint32_t)blocks), dim3(256), 0, s, a);
+    else if (forks) hipLaunchKernelGGL((k_fc<LPQ, true>), dim3((uint32_t)blocks), dim3(256), 0, s, a);
     else hipLaunchKernelGGL((k_fc<LPQ, false>), dim3((uint32_t)blocks), dim3(256), 0, s, a);
     return hipGetLastError();
 }
@@ -1620,7 +1747,8 @@ static hipError_t launch_fc_t(const FcArgs &a, bool forks, hipStream_t s) {
 // (HB and LA) whatever the row length -- short rows (few validators, or a
 // column shard) would otherwise leave one load pair per lane and stay latency-bound
 hipError_t launch_fc(const FcArgs &a, uint32_t cols, bool forks, hipStream_t s) {
-    const uint32_t nv = a.vhi4 - a.vlo4;
+    if (forks && !a.fk_hi4 && !a.n_cheat) forks = false;   // no cheater among this handle's creators
+    const uint32_t nv = forks && a.fk_hi4 ? a.fk_hi4 : a.vhi4 - a.vlo4;
     if (nv <= 16) return launch_fc_t<4>(a, forks, s);
     if (nv <= 32) return launch_fc_t<8>(a, forks, s);
     if (nv <= 64) return launch_fc_t<16>(a, forks, s);

@@ -123,6 +123,30 @@ def test_fork_dag_rows_and_fc(lx, shape):
     assert len(ls) == o.num_branches()
 
 
+@pytest.mark.parametrize("cheaters", [20, 40, 70])
+@pytest.mark.parametrize("fk", ["1", "0"])
+def test_fork_fc_paths(lx, cheaters, fk, monkeypatch):
+    """The fork-path ForklessCause kernels: every plane column streamed with a
+    32-bit (<= 32 cheaters) or 64-bit cheater mask (k_fc_fk), and the cheater
+    fix-up loop (k_fc<.., true>: > 64 cheaters, or LX_FC_FK=0), all equal to
+    the oracle; Zipf stakes so the per-creator dedupe weighs differently."""
+    monkeypatch.setenv("LX_FC_FK", fk)
+    n = 100
+    d = lx.tools.gen_dag(n, 14, 10, cheaters=cheaters, forks=4, seed=cheaters)
+    weights = [(1 << 20) // (i + 1) for i in range(n)]
+    o = oracle_for(d, weights)
+    ix = lx.Index()
+    ix.reset(weights)
+    ix.add_batch(d.creator, d.seq, d.poff, d.par)
+    assert ix.num_branches() == o.num_branches() > n
+    N = len(d)
+    rng = np.random.default_rng(cheaters)
+    a = rng.integers(0, N, 300_000, dtype=np.uint32)
+    b = np.minimum(a, rng.integers(0, N, 300_000, dtype=np.uint32))
+    b = np.where(rng.random(300_000) < 0.5, np.maximum(a.astype(np.int64) - rng.integers(0, 400, 300_000), 0), b).astype(np.uint32)
+    np.testing.assert_array_equal(ix.forkless_cause_batch(a, b), o.forkless_cause_batch(a, b))
+
+
 @pytest.mark.parametrize("chunk", [1, 7, 64, 1000])
 def test_batching_is_bit_exact(lx, chunk):
     """lx_add_batch over any split equals per-event Add (fork-heavy DAG)."""
