@@ -530,6 +530,67 @@ __device__ __forceinline__ uint32_t quad_and(uint32_t v) {
     return v & (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kQuadSwap2, 0xF, 0xF, false);
 }
 
+// Block walker fold: the slot units of a lane's three parents (unit A at pa[k];
+// unit B, CPW 4 only, in the B array (RN + 1) * 16 bytes further) and the drain
+// watermark at W, one LDS round trip.  tg[k] = the units' tags (equal for one
+// unit), pv[k] = the parent's CPW seqs.
+template <int CPW, int RN>
+__device__ __forceinline__ void blk_fold(const uint32_t pa[3], uint32_t W, uint32_t tg[3][2], uint32_t pv[3][CPW],
+                                         uint32_t &cw) {
+    if constexpr (CPW == 4) {
+        constexpr uint32_t BOFF = (RN + 1) * 16;
+        static_assert(BOFF < 65536, "ds offset field");
+        u4v xa0, xb0, xa1, xb1, xa2, xb2;
+        asm volatile(
+            "ds_read_b128 %0, %7\n\t"
+            "ds_read_b128 %1, %7 offset:%10\n\t"
+            "ds_read_b128 %2, %8\n\t"
+            "ds_read_b128 %3, %8 offset:%10\n\t"
+            "ds_read_b128 %4, %9\n\t"
+            "ds_read_b128 %5, %9 offset:%10\n\t"
+            "ds_read_b32 %6, %11\n\t"
+            "s_waitcnt lgkmcnt(0)"
+            : "=&v"(xa0), "=&v"(xb0), "=&v"(xa1), "=&v"(xb1), "=&v"(xa2), "=&v"(xb2), "=&v"(cw)
+            : "v"(pa[0]), "v"(pa[1]), "v"(pa[2]), "i"(BOFF), "v"(W)
+            : "memory");
+        const u4v xa[3] = {xa0, xa1, xa2};
+        const u4v xb[3] = {xb0, xb1, xb2};
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            tg[k][0] = xa[k].x; tg[k][1] = xb[k].x;
+            pv[k][0] = xa[k].y; pv[k][1 % CPW] = xa[k].z; pv[k][2 % CPW] = xa[k].w; pv[k][3 % CPW] = xb[k].y;
+        }
+    } else if constexpr (CPW == 2) {
+        u4v x0, x1, x2;
+        asm volatile(
+            "ds_read_b128 %0, %4\n\t"
+            "ds_read_b128 %1, %5\n\t"
+            "ds_read_b128 %2, %6\n\t"
+            "ds_read_b32 %3, %7\n\t"
+            "s_waitcnt lgkmcnt(0)"
+            : "=&v"(x0), "=&v"(x1), "=&v"(x2), "=&v"(cw)
+            : "v"(pa[0]), "v"(pa[1]), "v"(pa[2]), "v"(W)
+            : "memory");
+        const u4v x[3] = {x0, x1, x2};
+#pragma unroll
+        for (int k = 0; k < 3; k++) { tg[k][0] = tg[k][1] = x[k].x; pv[k][0] = x[k].y; pv[k][1 % CPW] = x[k].z; }
+    } else {
+        u2v x0, x1, x2;
+        asm volatile(
+            "ds_read_b64 %0, %4\n\t"
+            "ds_read_b64 %1, %5\n\t"
+            "ds_read_b64 %2, %6\n\t"
+            "ds_read_b32 %3, %7\n\t"
+            "s_waitcnt lgkmcnt(0)"
+            : "=&v"(x0), "=&v"(x1), "=&v"(x2), "=&v"(cw)
+            : "v"(pa[0]), "v"(pa[1]), "v"(pa[2]), "v"(W)
+            : "memory");
+        const u2v x[3] = {x0, x1, x2};
+#pragma unroll
+        for (int k = 0; k < 3; k++) { tg[k][0] = tg[k][1] = x[k].x; pv[k][0] = x[k].y; }
+    }
+}
+
 // LEAN (CPW 4 only): the compute waves give each event a quad of lanes; lane j
 // of the quad folds the inline parents j, j+4, j+8 into all four columns
 // (straight-line, one LDS round trip for all of them), the quad merges its
@@ -540,7 +601,8 @@ template <int CPW, int NCW, int RR, bool FILL, bool SMALL, bool MASKED, int LEAN
 __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
     static_assert(ND == kND || (LEAN && ND <= kNDMax), "drain waves: 2, or up to 4 with the quad / block layouts");
     static_assert(CPW == 1 || CPW == 2 || CPW == 4, "slot layout");
-    static_assert(!LEAN || (CPW == 4 && LX_MAXP == 12), "lean walker: quads over 4 columns, 12 inline parents");
+    static_assert(!LEAN || LX_MAXP == 12, "quad / block walkers: 12 inline parents, three per lane of a quad");
+    static_assert(LEAN != 1 || CPW == 4, "quad walker: 4-column slices (the block walker takes 1, 2 or 4)");
     constexpr int NT = 64 * (NCW + 1 + ND);
     constexpr int E = 64 * NCW;
     constexpr int RQ = LX_REC_Q;
@@ -563,8 +625,11 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
     const uint32_t slice = (w % 8) * a.slices_per_xcd + (w / 8);   // XCD-aware: neighbouring slices share an L2
     if (slice >= a.n_slices) return;
 
+    // null slot: unit A right after the A array (uint4 index RN, or RN / 2 for
+    // 8-B units), unit B (CPW 4) after the B array
+    constexpr int kNullA = CPW == 1 ? RN / 2 : RN;
     for (int i = threadIdx.x; i < RB16 + (LEAN ? 2 : 0); i += NT)
-        ring[i] = make_uint4(LEAN && (i == RN || i == 2 * RN + 1) ? kNullTag : 0u, 0, 0, 0);
+        ring[i] = make_uint4(LEAN && (i == kNullA || (CPW == 4 && i == 2 * RN + 1)) ? kNullTag : 0u, 0, 0, 0);
     for (int i = threadIdx.x; i < RR / 64; i += NT) rtag[i] = 0;
     for (int i = threadIdx.x; i < CPW * KB; i += NT) brc[i] = make_uint2(0, LX_NONE);
     if (threadIdx.x < kNDMax) { sh.copied[threadIdx.x] = 0; sh.stored[threadIdx.x] = 0; }
@@ -1027,14 +1092,15 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
         // when all 16 have published: record fetch and block advance are
         // wave-uniform branches; per pass only the publish of newly ready
         // quads is divergent.
+        // (1- and 2-column slices: one slot unit of 8 / 16 B per event, lane 0
+        // of the quad publishes it; 4 columns: units A and B from lanes 0, 1)
         constexpr uint32_t kLeanStuck = 64;
         constexpr uint32_t kLeanFar = 512;
-        constexpr uint32_t LEAN_BOFF = (RN + 1) * 16;
-        static_assert(LEAN_BOFF < 65536, "ds offset field");
-        const uint32_t ANULL = RA + (uint32_t)(RN * 16);
+        constexpr uint32_t UA = CPW == 1 ? 8u : 16u;   // bytes of unit A
+        const uint32_t ANULL = RA + (uint32_t)RN * UA;
         const uint32_t j = lane & 3, quad = lane >> 2;
         const uint32_t mycol = col[j & (CPW - 1)];
-        const bool myvalid = valid[j & (CPW - 1)];
+        const bool myvalid = j < (uint32_t)CPW && valid[j & (CPW - 1)];
         uint32_t blk = wave;
         if (a.diag & 16) __builtin_amdgcn_s_setprio(2);   // diagnostic: compute waves first
         bool loaded = false, done = true;
@@ -1086,7 +1152,7 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
                     const uint32_t pl = w[k] - bs;
                     const bool in = j + 4 * k < np;
                     px[k] = in ? pl + 1u : kNullTag;
-                    pa[k] = in ? RA + (pl % RN) * 16u : ANULL;
+                    pa[k] = in ? RA + (pl % RN) * UA : ANULL;
                 }
 #pragma unroll
                 for (int k = 0; k < CPW; k++) r[k] = (col[k] == br) ? seq : 0u;
@@ -1109,8 +1175,8 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
                 // is checked against the L2 path from the first pass on
                 stuck = far_parent(px, lp, (uint32_t)RN - kLeanFar) ? kLeanStuck : 0u;
                 {
-                    const uint32_t rs = (lp % RN) * 16u;
-                    wa_pub = j == 0 ? RA + rs : j == 1 ? RB + rs : dmy;
+                    const uint32_t rs = (lp % RN) * UA;
+                    wa_pub = j == 0 ? RA + rs : (CPW == 4 && j == 1) ? RB + (lp % RN) * 16u : dmy;
                     wb_pub = (myvalid && mycol == br) ? lds_addr(brc) + ((j & (CPW - 1)) * KB + seq % KB) * 8u
                                                       : dmy + 1024u;
                     chk0 = lp >= (uint32_t)RN;
@@ -1121,29 +1187,16 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
                 done = !live;
                 loaded = true;
             }
+            bool prog = false;
             // fold (published quads read the null slot)
-            u4v xa0, xb0, xa1, xb1, xa2, xb2;
-            asm volatile(
-                "ds_read_b128 %0, %7\n\t"
-                "ds_read_b128 %1, %7 offset:%10\n\t"
-                "ds_read_b128 %2, %8\n\t"
-                "ds_read_b128 %3, %8 offset:%10\n\t"
-                "ds_read_b128 %4, %9\n\t"
-                "ds_read_b128 %5, %9 offset:%10\n\t"
-                "ds_read_b32 %6, %11\n\t"
-                "s_waitcnt lgkmcnt(0)"
-                : "=&v"(xa0), "=&v"(xb0), "=&v"(xa1), "=&v"(xb1), "=&v"(xa2), "=&v"(xb2), "=&v"(cw)
-                : "v"(pa[0]), "v"(pa[1]), "v"(pa[2]), "i"(LEAN_BOFF), "v"(wm_addr)
-                : "memory");
-            const u4v xa[3] = {xa0, xa1, xa2};
-            const u4v xb[3] = {xb0, xb1, xb2};
+            uint32_t tg[3][2], pv[3][CPW];
+            blk_fold<CPW, RN>(pa, wm_addr, tg, pv, cw);
             bool all = true;
 #pragma unroll
             for (int k = 0; k < 3; k++) {
-                const bool ok = (xa[k].x == px[k]) & (xb[k].x == px[k]);
-                const uint32_t v[4] = {xa[k].y, xa[k].z, xa[k].w, xb[k].y};
+                const bool ok = (tg[k][0] == px[k]) & (tg[k][1] == px[k]);
 #pragma unroll
-                for (int c = 0; c < CPW; c++) r[c] = max(r[c], ok ? v[c] : 0u);
+                for (int c = 0; c < CPW; c++) r[c] = max(r[c], ok ? pv[k][c] : 0u);
                 all &= ok;
             }
 #pragma unroll
@@ -1186,11 +1239,21 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
                 drained = (fin && chk) ? ((lp - RN) | 63u) + 1 : drained;
                 const uint32_t wa = fin ? wa_pub : dmy;
                 const uint32_t wb = fin ? wb_pub : dmy + 1024u;
-                u4v x;
-                x.x = lp + 1; x.y = j == 0 ? r[0] : r[3 % CPW]; x.z = j == 0 ? r[1 % CPW] : 0u; x.w = j == 0 ? r[2 % CPW] : 0u;
-                u2v y;
-                y.x = seq; y.y = bs + lp;
-                asm volatile("ds_write_b64 %2, %3\n\tds_write_b128 %0, %1" : : "v"(wa), "v"(x), "v"(wb), "v"(y) : "memory");
+                prog = __any(fin);
+                if (!(a.diag & 128) || prog) {
+                    u2v y;
+                    y.x = seq; y.y = bs + lp;
+                    if constexpr (CPW == 1) {
+                        u2v x;
+                        x.x = lp + 1; x.y = r[0];
+                        asm volatile("ds_write_b64 %2, %3\n\tds_write_b64 %0, %1" : : "v"(wa), "v"(x), "v"(wb), "v"(y) : "memory");
+                    } else {
+                        u4v x;
+                        x.x = lp + 1; x.y = j == 0 ? r[0] : r[3 % CPW]; x.z = j == 0 ? r[1 % CPW] : 0u;
+                        x.w = (CPW == 4 && j == 0) ? r[2 % CPW] : 0u;
+                        asm volatile("ds_write_b64 %2, %3\n\tds_write_b128 %0, %1" : : "v"(wa), "v"(x), "v"(wb), "v"(y) : "memory");
+                    }
+                }
                 LX_WP(c_done += fin ? 1u : 0u;)
                 LX_WP(c_wm += (rdy && !done && !fin) ? 1u : 0u;)
                 done = done || fin;
@@ -1201,7 +1264,7 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
 #pragma unroll
                 for (int k = 0; k < 3; k++) {
                     const uint32_t x = px[k];
-                    if (x == kNullTag || (xa[k].x == x && xb[k].x == x) || max(xa[k].x, xb[k].x) <= x) continue;
+                    if (x == kNullTag || (tg[k][0] == x && tg[k][1] == x) || max(tg[k][0], tg[k][1]) <= x) continue;
                     if (!round_done<ND>(sh.stored, x - 1u)) {
                         LX_WP(c_wm++;)
                         __hip_atomic_store(&sh.req, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1219,6 +1282,8 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
             if (__all(done)) {
                 blk += NCW;
                 loaded = false;
+            } else if ((a.diag & 64) && !prog) {
+                __builtin_amdgcn_s_sleep(1);   // diagnostic: yield issue slots after a pass without progress
             }
         }
 #ifdef LX_WALKER_PROF
@@ -1408,6 +1473,18 @@ static hipError_t launch_index_t(const IndexArgs &a0, hipStream_t s) {
 template <int CPW>
 static hipError_t launch_index_c(const IndexArgs &a, uint32_t ncw, hipStream_t s) {
     if constexpr (CPW <= 2) {
+        if (a.lean == 2) {
+            // block walker on 1- / 2-column slices (few columns: small V, or a column shard)
+            if constexpr (CPW == 2) {
+                // 512-record ring (~74 KB of LDS): two workgroups per CU
+                if (a.rr_hint == 512) {
+                    if (a.drains != 2) return launch_index_t<CPW, 8, 512, false, 2, 4>(a, s);
+                    return launch_index_t<CPW, 8, 512, false, 2>(a, s);
+                }
+            }
+            if (a.drains != 2) return launch_index_t<CPW, 8, 1024, false, 2, 4>(a, s);
+            return launch_index_t<CPW, 8, 1024, false, 2>(a, s);
+        }
         if (a.small) {
             // small-LDS variant (~37 KB): several workgroups share a CU
             if (ncw <= 1) return launch_index_t<CPW, 1, 256, true>(a, s);
@@ -1448,9 +1525,11 @@ hipError_t launch_index(const IndexArgs &a, hipStream_t s) {
     if (a.n == 0 || a.ncols == 0) return hipSuccess;
     // columns per workgroup: aim at ~256 workgroups; compute waves: enough
     // events in flight for the DAG's antichain width (~V / (1.6 P))
-    // (the quad / block layouts exist for 4-column slices; the walk time is
-    // levels x pass latency whatever the number of workgroups)
-    uint32_t cpw = a.cpw_hint ? a.cpw_hint : a.lean ? 4 : (a.ncols <= 256 ? 1 : a.ncols <= 512 ? 2 : 4);
+    // (the walk time is levels x pass latency whatever the number of
+    // workgroups, and the block walker's pass gets shorter with fewer columns
+    // per slice: 1 or 2 columns while that leaves at most ~256 workgroups,
+    // one per CU; the quad layout exists for 4-column slices only)
+    uint32_t cpw = a.cpw_hint ? a.cpw_hint : a.lean == 1 ? 4 : (a.ncols <= 256 ? 1 : a.ncols <= 512 ? 2 : 4);
     uint32_t ncw = a.ncw_hint ? a.ncw_hint : (a.width_hint <= 24 ? 1 : a.width_hint <= 48 ? 2 : 4);
     if (cpw <= 1) return launch_index_c<1>(a, ncw, s);
     if (cpw <= 2) return launch_index_c<2>(a, ncw, s);

@@ -450,7 +450,10 @@ WALKER_VARIANTS = [
     {"LX_CPW": "4", "LX_WALKER": "block", "LX_LEAN_NCW": "4", "LX_DRAINS": "2"},
     {"LX_CPW": "4", "LX_WALKER": "block", "LX_LEAN_NCW": "8", "LX_DRAINS": "2"},
     {"LX_CPW": "4", "LX_WALKER": "block", "LX_LEAN_NCW": "12", "LX_DRAINS": "2"},
-    {"LX_WALKER": "block"},   # the default: 8 compute waves, 4 drains
+    {"LX_WALKER": "block"},   # the default: 8 compute waves, 4 drains (1-column slices at this V)
+    # block walker on 1- and 2-column slices (small V, column shards)
+    {"LX_CPW": "1", "LX_WALKER": "block"}, {"LX_CPW": "2", "LX_WALKER": "block"},
+    {"LX_CPW": "1", "LX_WALKER": "block", "LX_DRAINS": "2"}, {"LX_CPW": "2", "LX_WALKER": "block", "LX_DRAINS": "2"},
     {"LX_CPW": "4", "LX_WALKER": "block", "LX_LEAN_NCW": "11", "LX_DRAINS": "4"},
 ]
 
@@ -478,11 +481,12 @@ def test_walker_variants(lx, env, monkeypatch):
 
 
 @pytest.mark.big_only
-@pytest.mark.parametrize("walker", ["classic", "lean", "block"])
+@pytest.mark.parametrize("walker", ["classic", "lean", "block", "block-1", "block-2"])
 def test_walker_many_parents(lx, walker, monkeypatch):
     """Events with more parents than a record holds inline (16 > 12) take the
     overflow path of the walker; CPW 4 with both compute layouts."""
-    monkeypatch.setenv("LX_CPW", "4")
+    walker, _, cpw = walker.partition("-")
+    monkeypatch.setenv("LX_CPW", cpw or "4")
     monkeypatch.setenv("LX_WALKER", walker)
     d = lx.tools.gen_dag(30, 120, 16, 3, 4, 77)
     assert int(np.max(np.diff(d.poff))) > 12
@@ -527,11 +531,12 @@ def far_parent_dag(lx, n_nodes, n, seed):
 
 
 @pytest.mark.big_only
-@pytest.mark.parametrize("walker", ["classic", "lean", "block"])
+@pytest.mark.parametrize("walker", ["classic", "lean", "block", "block-1", "block-2"])
 def test_walker_far_parents(lx, walker, monkeypatch):
     """Parents far older than the ring (slot reuse while an event waits) in
     one batch and across batches, for each compute layout, bit-exact."""
-    monkeypatch.setenv("LX_CPW", "4")
+    walker, _, cpw = walker.partition("-")
+    monkeypatch.setenv("LX_CPW", cpw or "4")
     monkeypatch.setenv("LX_WALKER", walker)
     d = far_parent_dag(lx, 16, 12000, 91)
     weights = list(range(50, 34, -1))
