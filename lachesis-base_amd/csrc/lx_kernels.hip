@@ -1191,13 +1191,19 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
             // fold (published quads read the null slot)
             uint32_t tg[3][2], pv[3][CPW];
             blk_fold<CPW, RN>(pa, wm_addr, tg, pv, cw);
-            bool all = true;
+            bool ok[3], all = true;
 #pragma unroll
             for (int k = 0; k < 3; k++) {
-                const bool ok = (tg[k][0] == px[k]) & (tg[k][1] == px[k]);
+                ok[k] = (tg[k][0] == px[k]) & (tg[k][1] == px[k]);
+                all &= ok[k];
+            }
+            // three selects and two maxima per column (v_max3)
 #pragma unroll
-                for (int c = 0; c < CPW; c++) r[c] = max(r[c], ok ? pv[k][c] : 0u);
-                all &= ok;
+            for (int c = 0; c < CPW; c++) {
+                const uint32_t t0 = ok[0] ? pv[0][c] : 0u, t1 = ok[1] ? pv[1][c] : 0u, t2 = ok[2] ? pv[2][c] : 0u;
+                uint32_t m;
+                asm("v_max3_u32 %0, %1, %2, %3" : "=v"(m) : "v"(r[c]), "v"(t0), "v"(t1));
+                r[c] = max(m, t2);
             }
 #pragma unroll
             for (int c = 0; c < CPW; c++) r[c] = quad_max(r[c]);
