@@ -1101,23 +1101,24 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
         const uint32_t j = lane & 3, quad = lane >> 2;
         const uint32_t mycol = col[j & (CPW - 1)];
         const bool myvalid = j < (uint32_t)CPW && valid[j & (CPW - 1)];
-        uint32_t blk = wave;
+        uint32_t blk = __builtin_amdgcn_readfirstlane(wave);   // wave-uniform: scalar loop control
         if (a.diag & 16) __builtin_amdgcn_s_setprio(2);   // diagnostic: compute waves first
         bool loaded = false, done = true;
-        uint32_t br = 0, seq = 0, np = 0, xi = 0, stuck = 0;
+        uint32_t br = 0, seq = 0, np = 0, xi = 0;
+        uint32_t wstuck = 0;   // passes since the block fetch (wave-uniform)
         uint32_t px[3] = {kNullTag, kNullTag, kNullTag};
         uint32_t pa[3] = {ANULL, ANULL, ANULL};
         uint32_t r[CPW];
 #pragma unroll
         for (int k = 0; k < CPW; k++) r[k] = 0;
-        uint32_t drained = 0;
         // per-event publish constants, set at the block fetch: LDS targets of
         // this lane's slot unit and recent-event entry (dummy when not its
-        // role), the drain watermark that frees the event's slot
+        // role), the drain watermark that frees the event's slot and the value
+        // it must exceed (wneed: rounds of that drain, 0 while the slot is fresh)
         const uint32_t dmy = lds_addr(dummy) + lane * 16u;
-        uint32_t wa_pub = dmy, wb_pub = dmy + 1024u, wm_addr = lds_addr(&sh.copied[0]), rrq = 0;
-        bool chk0 = false;
+        uint32_t wa_pub = dmy, wb_pub = dmy + 1024u, wm_addr = lds_addr(&sh.copied[0]), wneed = 0;
         uint32_t cw = 0;   // that watermark, read with the parents every pass
+        const uint32_t qbase = lane & ~3u;   // lane 0 of this lane's quad
 #ifdef LX_WALKER_PROF
         uint32_t c_pass = 0, c_done = 0, c_slow = 0, c_wm = 0, c_norec = 0;
         const unsigned long long t_start = wall_clock64();
@@ -1173,21 +1174,21 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
                 xi = LX_MAXP;
                 // a parent far enough back that its slot may already hold a newer event
                 // is checked against the L2 path from the first pass on
-                stuck = far_parent(px, lp, (uint32_t)RN - kLeanFar) ? kLeanStuck : 0u;
+                wstuck = __any(far_parent(px, lp, (uint32_t)RN - kLeanFar)) ? kLeanStuck : 0u;
                 {
                     const uint32_t rs = (lp % RN) * UA;
                     wa_pub = j == 0 ? RA + rs : (CPW == 4 && j == 1) ? RB + (lp % RN) * 16u : dmy;
                     wb_pub = (myvalid && mycol == br) ? lds_addr(brc) + ((j & (CPW - 1)) * KB + seq % KB) * 8u
                                                       : dmy + 1024u;
-                    chk0 = lp >= (uint32_t)RN;
+                    // the slot's previous occupant lp - RN is drained once its
+                    // drain wave's `copied` count exceeds its round / ND
                     const uint32_t rr = (lp - RN) / 64;
-                    rrq = rr / ND;
+                    wneed = lp >= (uint32_t)RN ? rr / ND + 1 : 0u;
                     wm_addr = lds_addr(&sh.copied[rr % ND]);
                 }
                 done = !live;
                 loaded = true;
             }
-            bool prog = false;
             // fold (published quads read the null slot)
             uint32_t tg[3][2], pv[3][CPW];
             blk_fold<CPW, RN>(pa, wm_addr, tg, pv, cw);
@@ -1207,7 +1208,11 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
             }
 #pragma unroll
             for (int c = 0; c < CPW; c++) r[c] = quad_max(r[c]);
-            const bool rdy = quad_and(all ? 1u : 0u) != 0;
+            // the quad's readiness: AND of its four lanes on the scalar unit
+            uint64_t qm = __builtin_amdgcn_ballot_w64(all);
+            qm &= qm >> 1;
+            qm &= qm >> 2;   // bit 4q: all four lanes of quad q
+            const bool rdy = (qm >> qbase) & 1u;
             if (rdy && !done && xi < np) {
                 // parents beyond the inline twelve (rare): one per pass, the same on every lane of the quad
                 const uint32_t pg = ld_l2_now(a.par_in + a.poff_in[lp] + xi);
@@ -1240,33 +1245,29 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
                 // writes unit A from lane 0 and unit B from lane 1, and its
                 // recent-event entry; every other lane writes the same
                 // instructions into its own dummy slot
-                const bool chk = chk0 && lp - RN >= drained;
-                const bool fin = rdy && !done && xi >= np && (!chk || cw > rrq);
-                drained = (fin && chk) ? ((lp - RN) | 63u) + 1 : drained;
+                const bool fin = rdy && !done && xi >= np && cw >= wneed;
                 const uint32_t wa = fin ? wa_pub : dmy;
                 const uint32_t wb = fin ? wb_pub : dmy + 1024u;
-                prog = __any(fin);
-                if (!(a.diag & 128) || prog) {
-                    u2v y;
-                    y.x = seq; y.y = bs + lp;
-                    if constexpr (CPW == 1) {
-                        u2v x;
-                        x.x = lp + 1; x.y = r[0];
-                        asm volatile("ds_write_b64 %2, %3\n\tds_write_b64 %0, %1" : : "v"(wa), "v"(x), "v"(wb), "v"(y) : "memory");
-                    } else {
-                        u4v x;
-                        x.x = lp + 1; x.y = j == 0 ? r[0] : r[3 % CPW]; x.z = j == 0 ? r[1 % CPW] : 0u;
-                        x.w = (CPW == 4 && j == 0) ? r[2 % CPW] : 0u;
-                        asm volatile("ds_write_b64 %2, %3\n\tds_write_b128 %0, %1" : : "v"(wa), "v"(x), "v"(wb), "v"(y) : "memory");
-                    }
+                u2v y;
+                y.x = seq; y.y = bs + lp;
+                if constexpr (CPW == 1) {
+                    u2v x;
+                    x.x = lp + 1; x.y = r[0];
+                    asm volatile("ds_write_b64 %2, %3\n\tds_write_b64 %0, %1" : : "v"(wa), "v"(x), "v"(wb), "v"(y) : "memory");
+                } else {
+                    u4v x;
+                    x.x = lp + 1; x.y = j == 0 ? r[0] : r[3 % CPW]; x.z = j == 0 ? r[1 % CPW] : 0u;
+                    x.w = (CPW == 4 && j == 0) ? r[2 % CPW] : 0u;
+                    asm volatile("ds_write_b64 %2, %3\n\tds_write_b128 %0, %1" : : "v"(wa), "v"(x), "v"(wb), "v"(y) : "memory");
                 }
                 LX_WP(c_done += fin ? 1u : 0u;)
                 LX_WP(c_wm += (rdy && !done && !fin) ? 1u : 0u;)
                 done = done || fin;
             }
-            if (!rdy && !done && ++stuck >= kLeanStuck) {
-                // waiting long: a parent's slot may have been reused by a newer
-                // event; its HB row from L2 once its drain stored it
+            if (++wstuck >= kLeanStuck && !rdy && !done) {
+                // waiting long (the wave's block fetched >= 64 passes ago): a
+                // parent's slot may have been reused by a newer event; its HB
+                // row from L2 once its drain stored it
 #pragma unroll
                 for (int k = 0; k < 3; k++) {
                     const uint32_t x = px[k];
@@ -1288,8 +1289,6 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
             if (__all(done)) {
                 blk += NCW;
                 loaded = false;
-            } else if ((a.diag & 64) && !prog) {
-                __builtin_amdgcn_s_sleep(1);   // diagnostic: yield issue slots after a pass without progress
             }
         }
 #ifdef LX_WALKER_PROF
