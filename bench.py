@@ -348,6 +348,9 @@ def main():
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--fc-queries", type=int, default=1 << 24)
     ap.add_argument("--batch", type=int, default=0, help="events per lx_add_batch_dev call (0 = whole epoch)")
+    ap.add_argument("--order", default="add", choices=["add", "level"],
+                    help="event order of the batch: generator (Add) order, or level order as a "
+                         "level-synchronous batcher releases the epoch (same DAG, renumbered)")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--mode", default="shard", choices=["replica", "shard"])
@@ -386,6 +389,8 @@ def main():
     weights = weights_for(V, wkind)
     t_gen = time.perf_counter()
     dag = lx.tools.gen_dag(V, epv, P, cheaters, forks, seed=1)
+    if args.order == "level":
+        dag = lx.tools.level_order(dag)
     qa, qb = lx.tools.fc_queries(dag.lamport, args.fc_queries, window=64, seed=7)
     t_gen = time.perf_counter() - t_gen
     N = len(dag)

@@ -747,6 +747,9 @@ int add_batch_dev(lx_index *h, uint32_t n, const uint32_t *creator, const uint32
                 fprintf(stderr, "[lx_prof] wave %d: wall_us=%.0f wave_passes=%.0f lane: pass=%.0f spin=%.0f chunk=%.0f done=%.0f slow=%.0f fill=%.0f wm=%.0f norec=%.0f  ns/pass=%.1f\n",
                         w, q[9] / nb / 100.0, q[8] / nb, q[0] / nb, q[1] / nb, q[2] / nb, q[3] / nb, q[4] / nb, q[5] / nb, q[6] / nb,
                         q[7] / nb, q[9] * 10.0 / (q[8] > 0 ? q[8] : 1));
+                if (q[14] == 0 && q[15] > 0)
+                    fprintf(stderr, "[lx_prof] wave %d blocks ahead of the fetched one: landed records %.1f, issued %.1f; behind it: drained %.1f\n",
+                            w, q[11] / q[15], q[12] / q[15], q[13] / q[15]);
                 if (q[14] > 0)
                     fprintf(stderr, "[lx_prof] wave %d cycles/pass: fetch=%.0f (record rt %.0f) fold=%.0f (ring rt %.0f) ovf=%.0f complete=%.0f total=%.0f\n", w,
                             q[10] / q[8], q[5] / q[8], q[11] / q[8], q[15] / q[8], q[12] / q[8], q[13] / q[8], q[14] / q[8]);

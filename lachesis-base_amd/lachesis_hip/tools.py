@@ -61,6 +61,27 @@ def gen_dag(n_nodes, events_per_node, parent_count, cheaters=0, forks=0, seed=1)
     return Dag(creator, seq, lam, poff, par[:max(np_, 1)], n_nodes)
 
 
+def level_order(dag):
+    """The same DAG in level order: events sorted by Lamport time (= 1 + the
+    longest parent chain, which is the DAG level for tdag-structured DAGs),
+    ties kept in Add order -- the order a level-synchronous batcher
+    (lx_batcher_pop) releases a whole epoch in.  Parents are renumbered; each
+    event keeps its parent list order (self-parent first)."""
+    n = len(dag)
+    perm = np.argsort(dag.lamport, kind="stable")
+    inv = np.empty(n, dtype=np.uint32)
+    inv[perm] = np.arange(n, dtype=np.uint32)
+    counts = np.diff(dag.poff).astype(np.int64)
+    new_counts = counts[perm]
+    poff = np.zeros(n + 1, dtype=np.uint64)
+    np.cumsum(new_counts, out=poff[1:])
+    total = int(poff[-1])
+    idx = np.repeat(dag.poff[:-1][perm].astype(np.int64) - poff[:-1].astype(np.int64), new_counts) + \
+        np.arange(total, dtype=np.int64)
+    par = inv[dag.par[idx]] if total else dag.par[:1].copy()
+    return Dag(dag.creator[perm].copy(), dag.seq[perm].copy(), dag.lamport[perm].copy(), poff, par, dag.n_nodes)
+
+
 def fc_queries(lamport, nq, window=64, seed=7):
     L = _lib()
     lamport = np.ascontiguousarray(lamport, dtype=np.uint32)
