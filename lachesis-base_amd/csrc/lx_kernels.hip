@@ -288,6 +288,20 @@ __device__ __forceinline__ bool round_done(const uint32_t *cnt, uint32_t ev) {
 typedef uint32_t u4v __attribute__((ext_vector_type(4)));
 typedef uint32_t u2v __attribute__((ext_vector_type(2)));
 
+#ifndef LX_PIPE
+#define LX_PIPE 1
+#endif
+#ifndef LX_IDLE_SLEEP
+#define LX_IDLE_SLEEP 0
+#endif
+// LDS read in inline asm: the compiler orders a plain LDS load after every
+// LDS-DMA (global_load_lds) still in flight (an s_waitcnt vmcnt(0))
+__device__ __forceinline__ uint32_t lds_ld32(uint32_t addr) {
+    uint32_t x;
+    asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(x) : "v"(addr) : "memory");
+    return x;
+}
+
 // a slot as read: tag(s) and seqs
 template <int CPW>
 struct Slot {
@@ -677,11 +691,19 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
         while (done < nrounds) {
             bool progressed = false;
             LX_WP(l_iter++;)
-            LX_WP(if (issued < nrounds && issued - done < D && !(issued * 64 < (uint32_t)RR || round_done<ND>(sh.copied, issued * 64 - RR))) l_slot++;)
             // a round's record slots are free once the drain consumed their
             // previous occupants (events ev - RR: same round offset)
-            if (issued < nrounds && issued - done < D &&
-                (issued * 64 < (uint32_t)RR || round_done<ND>(sh.copied, issued * 64 - RR))) {
+            bool free = issued * 64 < (uint32_t)RR;
+            if (!free && issued < nrounds && issued - done < D) {
+                if (LX_PIPE) {
+                    const uint32_t r = (issued * 64 - RR) / 64;
+                    free = __builtin_amdgcn_readfirstlane(lds_ld32(lds_addr(&sh.copied[r % ND]))) > r / ND;
+                } else {
+                    free = round_done<ND>(sh.copied, issued * 64 - RR);
+                }
+            }
+            LX_WP(if (issued < nrounds && issued - done < D && !free) l_slot++;)
+            if (issued < nrounds && issued - done < D && free) {
                 const uint32_t s0 = (issued * 64) % RR;
                 char *dst = reinterpret_cast<char *>(rrec) + (uint64_t)s0 * sizeof(EventRec);
                 const uint64_t base = (uint64_t)issued * 64 * sizeof(EventRec);
@@ -713,7 +735,10 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
                     case 13: asm volatile("s_waitcnt vmcnt(52)" ::: "memory"); break;
                     default: asm volatile("s_waitcnt vmcnt(56)" ::: "memory"); break;
                 }
-                if (lane == 0) __hip_atomic_store(&rtag[done % (RR / 64)], done + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (LX_PIPE)   // (the vmcnt wait above landed the round; a release store waits for all)
+                    asm volatile("ds_write_b32 %0, %1" : : "v"(lds_addr(&rtag[done % (RR / 64)])), "v"(done + 1) : "memory");
+                else if (lane == 0)
+                    __hip_atomic_store(&rtag[done % (RR / 64)], done + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                 done++;
                 LX_WP(asm volatile("ds_write_b32 %0, %1" : : "v"(lds_addr(&sh.p_done)), "v"(done) : "memory");)
             } else if (!progressed) {
@@ -1281,6 +1306,7 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
                 LX_WP(c_done += fin ? 1u : 0u;)
                 LX_WP(c_wm += (rdy && !done && !fin) ? 1u : 0u;)
                 done = done || fin;
+                if (LX_IDLE_SLEEP && !__any(fin) && !__all(done)) __builtin_amdgcn_s_sleep(LX_IDLE_SLEEP);
             }
             if (++wstuck >= kLeanStuck && !rdy && !done) {
                 // waiting long (the wave's block fetched >= 64 passes ago): a
