@@ -180,7 +180,7 @@ struct lx_index {
     // per event (default), 1 = independent quads, 0 = one lane per event
     // (LX_WALKER=block/lean/classic); LX_LEAN_NCW compute waves, LX_DRAINS
     // drain waves of the block layout
-    uint32_t lean = 2, lean_ncw = 8;
+    uint32_t lean = 2, lean_ncw = 0;   // 0: the walker picks (8, or 11 on 4-column slices)
     uint32_t drains = 4;
     uint32_t rr_hint = 0, diag = 0;        // LX_RR record ring depth; LX_DIAG timing-only modes
     bool prof = false;                     // LX_PROF=1: per-wave walker counters to stderr

@@ -1537,7 +1537,11 @@ static hipError_t launch_index_c(const IndexArgs &a, uint32_t ncw, hipStream_t s
                     return launch_index_t<CPW, 8, 512, false, 2>(a, s);
                 }
             }
-            if (a.drains != 2) return launch_index_t<CPW, 8, 1024, false, 2, 4>(a, s);
+            // (lean_ncw 0 = auto: 8 compute waves; 11 slowed C2 by 7 %)
+            if (a.drains != 2) {
+                if (a.lean_ncw <= 8) return launch_index_t<CPW, 8, 1024, false, 2, 4>(a, s);
+                return launch_index_t<CPW, 11, 1024, false, 2, 4>(a, s);
+            }
             return launch_index_t<CPW, 8, 1024, false, 2>(a, s);
         }
         if (a.small) {
@@ -1556,18 +1560,21 @@ static hipError_t launch_index_c(const IndexArgs &a, uint32_t ncw, hipStream_t s
     }
     if constexpr (CPW == 4) {
         if (a.lean == 1) {
-            // quads: 16 events in flight per compute wave
-            if (a.lean_ncw <= 4) return launch_index_t<CPW, 4, 1024, false, 1>(a, s);
+            // quads: 16 events in flight per compute wave (lean_ncw 0 = 8)
+            if (a.lean_ncw && a.lean_ncw <= 4) return launch_index_t<CPW, 4, 1024, false, 1>(a, s);
             if (a.lean_ncw <= 8) return launch_index_t<CPW, 8, 1024, false, 1>(a, s);
             return launch_index_t<CPW, 12, 1024, false, 1>(a, s);
         }
         if (a.lean == 2) {
+            // lean_ncw 0 = auto: 11 compute waves with 4 drains (16 waves, the
+            // workgroup limit): C3 walk -1.8 % against 8 once the loader kept
+            // its record DMAs in flight
             if (a.drains != 2) {
-                if (a.lean_ncw <= 8) return launch_index_t<CPW, 8, 1024, false, 2, 4>(a, s);
+                if (a.lean_ncw && a.lean_ncw <= 8) return launch_index_t<CPW, 8, 1024, false, 2, 4>(a, s);
                 return launch_index_t<CPW, 11, 1024, false, 2, 4>(a, s);
             }
-            if (a.lean_ncw <= 4) return launch_index_t<CPW, 4, 1024, false, 2>(a, s);
-            if (a.lean_ncw <= 8) return launch_index_t<CPW, 8, 1024, false, 2>(a, s);
+            if (a.lean_ncw && a.lean_ncw <= 4) return launch_index_t<CPW, 4, 1024, false, 2>(a, s);
+            if (!a.lean_ncw || a.lean_ncw <= 8) return launch_index_t<CPW, 8, 1024, false, 2>(a, s);
             return launch_index_t<CPW, 12, 1024, false, 2>(a, s);
         }
     }
