@@ -182,6 +182,7 @@ struct lx_index {
     // drain waves of the block layout
     uint32_t lean = 2, lean_ncw = 0;   // 0: the walker picks (8, or 11 on 4-column slices)
     uint32_t drains = 4;
+    bool pack16 = true;                    // LX_PACK16=0: two slot units per event even for small seqs
     uint32_t rr_hint = 0, diag = 0;        // LX_RR record ring depth; LX_DIAG timing-only modes
     bool prof = false;                     // LX_PROF=1: per-wave walker counters to stderr
     uint32_t small = 0;                    // LX_SMALL=1: small-LDS walker (several workgroups per CU)
@@ -705,6 +706,7 @@ int add_batch_dev(lx_index *h, uint32_t n, const uint32_t *creator, const uint32
     ia.lean = h->lean;
     ia.lean_ncw = h->lean_ncw;
     ia.drains = h->drains;
+    ia.pack16 = h->pack16 && h->max_seq <= 0xFFFFu;
     // antichain width of tdag-like DAGs ~ V / (1.6 P); P from the batch
     {
         uint32_t pbar = std::max<uint32_t>(1, (uint32_t)((h->last_npar + n - 1) / n));
@@ -1383,6 +1385,7 @@ int lx_create(const lx_config *cfg, lx_index **out) {
     if (const char *d = getenv("LX_PROF")) h->prof = (d[0] == '1');
     if (const char *d = getenv("LX_SMALL")) h->small = (uint32_t)atoi(d);
     if (const char *d = getenv("LX_LA_MEMSET")) h->la_tail = (d[0] != '1');
+    if (const char *d = getenv("LX_PACK16")) h->pack16 = (d[0] != '0');
     if (const char *d = getenv("LX_SHARD_WIRE")) h->wire_force = (uint32_t)atoi(d);
     if (const char *d = getenv("LX_SMALL_MAX")) h->small_max = (uint32_t)atoi(d);
     if (const char *d = getenv("LX_TIMING")) h->small_timing = (d[0] == '1');

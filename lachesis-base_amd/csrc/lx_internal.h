@@ -69,6 +69,7 @@ struct IndexArgs {
     uint32_t lean;               // quad-per-event compute waves (CPW 4; LX_WALKER=lean)
     uint32_t lean_ncw;           // their compute waves (4 or 8)
     uint32_t drains;             // drain waves of the block layout (2 or 4; LX_DRAINS)
+    uint32_t pack16;             // every seq of the epoch <= 0xFFFF: 16-B packed slots (4-column block walker)
 };
 constexpr int kProfSlots = 16;   // see k_index: passes, spin misses, chunk folds, completes, ...
 constexpr int kProfWaves = 16;   // waves per workgroup in the counter layout

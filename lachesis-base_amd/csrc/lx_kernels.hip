@@ -432,8 +432,24 @@ __device__ __forceinline__ void ring_read4(uint32_t A, uint32_t B, const uint32_
 
 // one slot (the drains' spin loop and the overflow path): a single access per
 // unit, so a spinning drain adds no redundant LDS traffic beside the compute waves
-template <int CPW>
+// PK (4-column slices, every seq of the epoch <= 0xFFFF): one 16-B unit
+// {tag, s0 | s1 << 16, s2 | s3 << 16, 0} per slot instead of two
+__device__ __forceinline__ void unpack16(const u4v &x, uint32_t *v) {
+    v[0] = x.y & 0xFFFFu; v[1] = x.y >> 16; v[2] = x.z & 0xFFFFu; v[3] = x.z >> 16;
+}
+template <int CPW, bool PK = false>
 __device__ __forceinline__ void ring_read1(uint32_t A, uint32_t B, uint32_t s, Slot<CPW> &o) {
+    if constexpr (PK) {
+        static_assert(CPW == 4, "packed slots: 4-column slices");
+        u4v x;
+        asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=&v"(x) : "v"(A + s * 16u) : "memory");
+        o.t0 = o.t1 = x.x;
+        uint32_t v[4];
+        unpack16(x, v);
+#pragma unroll
+        for (int k = 0; k < CPW; k++) o.v[k] = v[k % 4];
+        return;
+    }
     if (CPW == 1) {
         u2v x;
         asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=&v"(x) : "v"(A + s * 8u) : "memory");
@@ -549,9 +565,73 @@ __device__ __forceinline__ uint32_t quad_and(uint32_t v) {
 // unit B, CPW 4 only, in the B array (RN + 1) * 16 bytes further) and the drain
 // watermark at W, one LDS round trip.  tg[k] = the units' tags (equal for one
 // unit), pv[k] = the parent's CPW seqs.
-template <int CPW, int RN>
+template <int CPW, int RN, bool PK = false>
 __device__ __forceinline__ void blk_fold(const uint32_t pa[3], uint32_t W, uint32_t tg[3][2], uint32_t pv[3][CPW],
                                          uint32_t &cw) {
+    if constexpr (PK) {
+        static_assert(CPW == 4, "packed slots: 4-column slices");
+        u4v x0, x1, x2;
+        asm volatile(
+            "ds_read_b128 %0, %4\n\t"
+            "ds_read_b128 %1, %5\n\t"
+            "ds_read_b128 %2, %6\n\t"
+            "ds_read_b32 %3, %7\n\t"
+            "s_waitcnt lgkmcnt(0)"
+            : "=&v"(x0), "=&v"(x1), "=&v"(x2), "=&v"(cw)
+            : "v"(pa[0]), "v"(pa[1]), "v"(pa[2]), "v"(W)
+            : "memory");
+        const u4v x[3] = {x0, x1, x2};
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            tg[k][0] = tg[k][1] = x[k].x;
+            uint32_t v[4];
+            unpack16(x[k], v);
+#pragma unroll
+            for (int c = 0; c < CPW; c++) pv[k][c] = v[c % 4];
+        }
+        return;
+    }
+#ifdef LX_EXP_NARROW
+    if constexpr (CPW == 4) {
+        // timing experiment only (wrong values): LX_EXP_NARROW bytes of unit A per parent
+        if constexpr (LX_EXP_NARROW == 8) {
+            u2v x0, x1, x2;
+            asm volatile(
+                "ds_read_b64 %0, %4\n\t"
+                "ds_read_b64 %1, %5\n\t"
+                "ds_read_b64 %2, %6\n\t"
+                "ds_read_b32 %3, %7\n\t"
+                "s_waitcnt lgkmcnt(0)"
+                : "=&v"(x0), "=&v"(x1), "=&v"(x2), "=&v"(cw)
+                : "v"(pa[0]), "v"(pa[1]), "v"(pa[2]), "v"(W)
+                : "memory");
+            const u2v x[3] = {x0, x1, x2};
+#pragma unroll
+            for (int k = 0; k < 3; k++) {
+                tg[k][0] = tg[k][1] = x[k].x;
+#pragma unroll
+                for (int c = 0; c < CPW; c++) pv[k][c] = x[k].y;
+            }
+        } else {
+            u4v x0, x1, x2;
+            asm volatile(
+                "ds_read_b128 %0, %4\n\t"
+                "ds_read_b128 %1, %5\n\t"
+                "ds_read_b128 %2, %6\n\t"
+                "ds_read_b32 %3, %7\n\t"
+                "s_waitcnt lgkmcnt(0)"
+                : "=&v"(x0), "=&v"(x1), "=&v"(x2), "=&v"(cw)
+                : "v"(pa[0]), "v"(pa[1]), "v"(pa[2]), "v"(W)
+                : "memory");
+            const u4v x[3] = {x0, x1, x2};
+#pragma unroll
+            for (int k = 0; k < 3; k++) {
+                tg[k][0] = tg[k][1] = x[k].x;
+                pv[k][0] = x[k].y; pv[k][1] = x[k].z; pv[k][2] = x[k].w; pv[k][3] = x[k].y;
+            }
+        }
+    } else
+#endif
     if constexpr (CPW == 4) {
         constexpr uint32_t BOFF = (RN + 1) * 16;
         static_assert(BOFF < 65536, "ds offset field");
@@ -612,8 +692,9 @@ __device__ __forceinline__ void blk_fold(const uint32_t pa[3], uint32_t W, uint3
 // partial maxima and its readiness by DPP, and lane 0 publishes.  A pass costs
 // a fraction of the one-lane-per-event pass (no chunk scheduling, ~1/4 of the
 // instructions), and the walk is bound by pass latency x DAG depth.
-template <int CPW, int NCW, int RR, bool FILL, bool SMALL, bool MASKED, int LEAN = 0, int ND = kND>
+template <int CPW, int NCW, int RR, bool FILL, bool SMALL, bool MASKED, int LEAN = 0, int ND = kND, bool PK = false>
 __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
+    static_assert(!PK || (CPW == 4 && LEAN == 2), "packed slots: block walker on 4-column slices");
     static_assert(ND == kND || (LEAN && ND <= kNDMax), "drain waves: 2, or up to 4 with the quad / block layouts");
     static_assert(CPW == 1 || CPW == 2 || CPW == 4, "slot layout");
     static_assert(!LEAN || LX_MAXP == 12, "quad / block walkers: 12 inline parents, three per lane of a quad");
@@ -778,7 +859,7 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
             while (true) {
                 bool ready = true;
                 if (ev < n) {
-                    ring_read1<CPW>(RA, RB, sl, me);
+                    ring_read1<CPW, PK>(RA, RB, sl, me);
                     ready = me.t0 == ev + 1 && me.t1 == ev + 1;
                 }
                 if (__all(ready)) break;
@@ -804,7 +885,7 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
                     bool got = false;
                     if (pl < n) {
                         Slot<CPW> ps;
-                        ring_read1<CPW>(RA, RB, pl % RN, ps);
+                        ring_read1<CPW, PK>(RA, RB, pl % RN, ps);
                         if (ps.t0 == pl + 1 && ps.t1 == pl + 1) {
 #pragma unroll
                             for (int k = 0; k < CPW; k++) h0[k] = ps.v[k];
@@ -1060,7 +1141,7 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
                 bool ok = false, old = lpp >= n;
                 if (!old) {
                     Slot<CPW> ps;
-                    ring_read1<CPW>(RA, RB, lpp % RN, ps);
+                    ring_read1<CPW, PK>(RA, RB, lpp % RN, ps);
                     if (ps.t0 == lpp + 1 && ps.t1 == lpp + 1) {
 #pragma unroll
                         for (int c = 0; c < CPW; c++) r[c] = max(r[c], ps.v[c]);
@@ -1206,7 +1287,7 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
                 wstuck = __any(far_parent(px, lp, (uint32_t)RN - kLeanFar)) ? kLeanStuck : 0u;
                 {
                     const uint32_t rs = (lp % RN) * UA;
-                    wa_pub = j == 0 ? RA + rs : (CPW == 4 && j == 1) ? RB + (lp % RN) * 16u : dmy;
+                    wa_pub = j == 0 ? RA + rs : (CPW == 4 && !PK && j == 1) ? RB + (lp % RN) * 16u : dmy;
                     wb_pub = (myvalid && mycol == br) ? lds_addr(brc) + ((j & (CPW - 1)) * KB + seq % KB) * 8u
                                                       : dmy + 1024u;
                     // the slot's previous occupant lp - RN is drained once its
@@ -1237,7 +1318,7 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
             // max over them is the event's value; r holds only what does not
             // come from the ring (own seq, L2 rows of old / overflow parents)
             uint32_t tg[3][2], pv[3][CPW];
-            blk_fold<CPW, RN>(pa, wm_addr, tg, pv, cw);
+            blk_fold<CPW, RN, PK>(pa, wm_addr, tg, pv, cw);
             bool all = true;
 #pragma unroll
             for (int k = 0; k < 3; k++) all &= (tg[k][0] == px[k]) & (tg[k][1] == px[k]);
@@ -1260,7 +1341,7 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
                 bool ok = false, old = lpp >= n;
                 if (!old) {
                     Slot<CPW> ps;
-                    ring_read1<CPW>(RA, RB, lpp % RN, ps);
+                    ring_read1<CPW, PK>(RA, RB, lpp % RN, ps);
                     if (ps.t0 == lpp + 1 && ps.t1 == lpp + 1) {
 #pragma unroll
                         for (int c = 0; c < CPW; c++) r[c] = max(r[c], ps.v[c]);
@@ -1297,6 +1378,10 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
                     u2v x;
                     x.x = lp + 1; x.y = m[0];
                     asm volatile("ds_write_b64 %2, %3\n\tds_write_b64 %0, %1" : : "v"(wa), "v"(x), "v"(wb), "v"(y) : "memory");
+                } else if constexpr (PK) {
+                    u4v x;   // lane 0: {tag, s0 | s1 << 16, s2 | s3 << 16, 0}
+                    x.x = lp + 1; x.y = m[0] | (m[1 % CPW] << 16); x.z = m[2 % CPW] | (m[3 % CPW] << 16); x.w = 0u;
+                    asm volatile("ds_write_b64 %2, %3\n\tds_write_b128 %0, %1" : : "v"(wa), "v"(x), "v"(wb), "v"(y) : "memory");
                 } else {
                     u4v x;
                     x.x = lp + 1; x.y = j == 0 ? m[0] : m[3 % CPW]; x.z = j == 0 ? m[1 % CPW] : 0u;
@@ -1457,7 +1542,7 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
             bool ok = false, old = lpp >= n;
             if (!old) {
                 Slot<CPW> ps;
-                ring_read1<CPW>(RA, RB, lpp % RN, ps);
+                ring_read1<CPW, PK>(RA, RB, lpp % RN, ps);
                 if (ps.t0 == lpp + 1 && ps.t1 == lpp + 1) {
 #pragma unroll
                     for (int k = 0; k < CPW; k++) r[k] = max(r[k], ps.v[k] & mask);
@@ -1519,6 +1604,14 @@ static hipError_t launch_index_t(const IndexArgs &a0, hipStream_t s) {
     a.slices_per_xcd = (a.n_slices + 7) / 8;
     uint32_t grid = a.slices_per_xcd * 8;
     const dim3 blk(64 * (NCW + 1 + ND));
+    if constexpr (CPW == 4 && LEAN == 2) {
+        if (a.pack16) {   // every seq of the epoch fits 16 bits: one 16-B slot unit
+            if (a.diag_nofill) hipLaunchKernelGGL((k_index<CPW, NCW, RR, false, SMALL, true, LEAN, ND, true>), dim3(grid), blk, 0, s, a);
+            else if (a.mask) hipLaunchKernelGGL((k_index<CPW, NCW, RR, true, SMALL, true, LEAN, ND, true>), dim3(grid), blk, 0, s, a);
+            else hipLaunchKernelGGL((k_index<CPW, NCW, RR, true, SMALL, false, LEAN, ND, true>), dim3(grid), blk, 0, s, a);
+            return hipGetLastError();
+        }
+    }
     if (a.diag_nofill) hipLaunchKernelGGL((k_index<CPW, NCW, RR, false, SMALL, true, LEAN, ND>), dim3(grid), blk, 0, s, a);
     else if (a.mask) hipLaunchKernelGGL((k_index<CPW, NCW, RR, true, SMALL, true, LEAN, ND>), dim3(grid), blk, 0, s, a);
     else hipLaunchKernelGGL((k_index<CPW, NCW, RR, true, SMALL, false, LEAN, ND>), dim3(grid), blk, 0, s, a);

@@ -455,6 +455,9 @@ WALKER_VARIANTS = [
     {"LX_CPW": "1", "LX_WALKER": "block"}, {"LX_CPW": "2", "LX_WALKER": "block"},
     {"LX_CPW": "1", "LX_WALKER": "block", "LX_DRAINS": "2"}, {"LX_CPW": "2", "LX_WALKER": "block", "LX_DRAINS": "2"},
     {"LX_CPW": "4", "LX_WALKER": "block", "LX_LEAN_NCW": "11", "LX_DRAINS": "4"},
+    # 4-column slices with two slot units per event (the layout for seqs > 0xFFFF)
+    {"LX_CPW": "4", "LX_WALKER": "block", "LX_PACK16": "0"},
+    {"LX_CPW": "4", "LX_WALKER": "block", "LX_LEAN_NCW": "8", "LX_PACK16": "0"},
 ]
 
 
@@ -481,11 +484,15 @@ def test_walker_variants(lx, env, monkeypatch):
 
 
 @pytest.mark.big_only
-@pytest.mark.parametrize("walker", ["classic", "lean", "block", "block-1", "block-2"])
+@pytest.mark.parametrize("walker", ["classic", "lean", "block", "block-4u", "block-1", "block-2"])
 def test_walker_many_parents(lx, walker, monkeypatch):
     """Events with more parents than a record holds inline (16 > 12) take the
-    overflow path of the walker; CPW 4 with both compute layouts."""
+    overflow path of the walker; CPW 4 with both compute layouts (block-4u:
+    two slot units per event instead of the packed 16-bit one)."""
     walker, _, cpw = walker.partition("-")
+    if cpw.endswith("u"):
+        cpw = cpw[:-1]
+        monkeypatch.setenv("LX_PACK16", "0")
     monkeypatch.setenv("LX_CPW", cpw or "4")
     monkeypatch.setenv("LX_WALKER", walker)
     d = lx.tools.gen_dag(30, 120, 16, 3, 4, 77)
@@ -498,6 +505,25 @@ def test_walker_many_parents(lx, walker, monkeypatch):
     assert [int(x) for x in br] == [o.branch(i) for i in range(len(d))]
     compare_rows(ix, o, range(len(d)))
     qa, qb = lx.tools.fc_queries(d.lamport, 100_000, window=32, seed=8)
+    np.testing.assert_array_equal(ix.forkless_cause_batch(qa, qb), o.forkless_cause_batch(qa, qb))
+    ix.close()
+
+
+@pytest.mark.big_only
+def test_walker_seqs_beyond_16_bits(lx, monkeypatch):
+    """4-column slices with seqs above 0xFFFF: the walker must not use the
+    packed 16-bit slot units (rows and FC still equal the oracle)."""
+    monkeypatch.setenv("LX_CPW", "4")
+    weights = [3, 2]
+    big = lx.tools.gen_dag(2, 66000, 2, 0, 0, 6)
+    assert int(big.seq.max()) > 0xFFFF
+    o = oracle_for(big, weights)
+    ix = lx.Index()
+    ix.reset(weights)
+    ix.add_batch(big.creator, big.seq, big.poff, big.par)
+    rng = np.random.default_rng(9)
+    compare_rows(ix, o, np.concatenate([rng.choice(len(big), 2000, replace=False), np.arange(len(big) - 300, len(big))]))
+    qa, qb = lx.tools.fc_queries(big.lamport, 100_000, window=32, seed=3)
     np.testing.assert_array_equal(ix.forkless_cause_batch(qa, qb), o.forkless_cause_batch(qa, qb))
     ix.close()
 
