@@ -1381,7 +1381,12 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
                 } else if constexpr (PK) {
                     u4v x;   // lane 0: {tag, s0 | s1 << 16, s2 | s3 << 16, 0}
                     x.x = lp + 1; x.y = m[0] | (m[1 % CPW] << 16); x.z = m[2 % CPW] | (m[3 % CPW] << 16); x.w = 0u;
+#ifdef LX_EXP_PUBMASK
+                    if (fin && wa != dmy) asm volatile("ds_write_b128 %0, %1" : : "v"(wa), "v"(x) : "memory");
+                    if (fin && wb != dmy + 1024u) asm volatile("ds_write_b64 %0, %1" : : "v"(wb), "v"(y) : "memory");
+#else
                     asm volatile("ds_write_b64 %2, %3\n\tds_write_b128 %0, %1" : : "v"(wa), "v"(x), "v"(wb), "v"(y) : "memory");
+#endif
                 } else {
                     u4v x;
                     x.x = lp + 1; x.y = j == 0 ? m[0] : m[3 % CPW]; x.z = j == 0 ? m[1 % CPW] : 0u;
