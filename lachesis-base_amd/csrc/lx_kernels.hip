@@ -556,6 +556,16 @@ __device__ __forceinline__ uint32_t quad_max(uint32_t v) {
     v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kQuadSwap1, 0xF, 0xF, false));
     return max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kQuadSwap2, 0xF, 0xF, false));
 }
+// packed 16-bit maxima (two columns per dword) and their quad reduction
+__device__ __forceinline__ uint32_t pk_max(uint32_t a, uint32_t b) {
+    uint32_t d;
+    asm("v_pk_max_u16 %0, %1, %2" : "=v"(d) : "v"(a), "v"(b));
+    return d;
+}
+__device__ __forceinline__ uint32_t quad_pk_max(uint32_t v) {
+    v = pk_max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, kQuadSwap1, 0xF, 0xF, true));
+    return pk_max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, kQuadSwap2, 0xF, 0xF, true));
+}
 __device__ __forceinline__ uint32_t quad_and(uint32_t v) {
     v &= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kQuadSwap1, 0xF, 0xF, false);
     return v & (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kQuadSwap2, 0xF, 0xF, false);
@@ -583,11 +593,10 @@ __device__ __forceinline__ void blk_fold(const uint32_t pa[3], uint32_t W, uint3
         const u4v x[3] = {x0, x1, x2};
 #pragma unroll
         for (int k = 0; k < 3; k++) {
+            // packed: pv[k][0] = s0 | s1 << 16, pv[k][1] = s2 | s3 << 16 (the
+            // fold takes packed 16-bit maxima)
             tg[k][0] = tg[k][1] = x[k].x;
-            uint32_t v[4];
-            unpack16(x[k], v);
-#pragma unroll
-            for (int c = 0; c < CPW; c++) pv[k][c] = v[c % 4];
+            pv[k][0] = x[k].y; pv[k][1 % CPW] = x[k].z; pv[k][2 % CPW] = 0u; pv[k][3 % CPW] = 0u;
         }
         return;
     }
@@ -1323,11 +1332,23 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
 #pragma unroll
             for (int k = 0; k < 3; k++) all &= (tg[k][0] == px[k]) & (tg[k][1] == px[k]);
             uint32_t m[CPW];
+            if constexpr (PK) {
+                // two columns per dword: three packed maxima per dword, the quad
+                // reduction on packed words
 #pragma unroll
-            for (int c = 0; c < CPW; c++) {
-                uint32_t t;
-                asm("v_max3_u32 %0, %1, %2, %3" : "=v"(t) : "v"(r[c]), "v"(pv[0][c]), "v"(pv[1][c]));
-                m[c] = quad_max(max(t, pv[2][c]));
+                for (int h = 0; h < 2; h++) {
+                    const uint32_t rp = r[(2 * h) % CPW] | (r[(2 * h + 1) % CPW] << 16);
+                    const uint32_t t = quad_pk_max(pk_max(pk_max(rp, pv[0][h % CPW]), pk_max(pv[1][h % CPW], pv[2][h % CPW])));
+                    m[(2 * h) % CPW] = t & 0xFFFFu;
+                    m[(2 * h + 1) % CPW] = t >> 16;
+                }
+            } else {
+#pragma unroll
+                for (int c = 0; c < CPW; c++) {
+                    uint32_t t;
+                    asm("v_max3_u32 %0, %1, %2, %3" : "=v"(t) : "v"(r[c]), "v"(pv[0][c]), "v"(pv[1][c]));
+                    m[c] = quad_max(max(t, pv[2][c]));
+                }
             }
             // the quad's readiness: AND of its four lanes on the scalar unit
             uint64_t qm = __builtin_amdgcn_ballot_w64(all);
