@@ -651,12 +651,13 @@ int add_batch_dev(lx_index *h, uint32_t n, const uint32_t *creator, const uint32
     h->max_seq = std::max(h->max_seq, bmax);
     if ((rc = grow_scap(h, h->max_seq))) return rc;
     a = batch_args(h, n, creator, seq, poff, par);   // pointers may have moved
+    a.nofork = (nforks == 0 && B_new == h->V) ? 1u : 0u;
     // pointer jumping along in-batch self-parent chains: a chain has at most
     // min(n, max seq) events, ceil(log2) + 1 rounds resolve it (k_finalize flags
-    // an unresolved event, checked below)
+    // an unresolved event, checked below); none without forks
     uint32_t rounds = 1;
     while (rounds < 32 && (1ull << (rounds - 1)) < std::min<uint64_t>(n, bmax)) rounds++;
-    HIPCHK(h, lx::launch_batch_finish(a, rounds + 1, s));
+    HIPCHK(h, lx::launch_batch_finish(a, a.nofork ? 0u : rounds + 1, s));
     if (nforks) {
         std::vector<uint32_t> cr(nforks), fs(nforks);
         HIPCHK(h, hipMemcpyAsync(cr.data(), h->branch_creator + h->B, nforks * 4, hipMemcpyDeviceToHost, s));

@@ -102,6 +102,7 @@ struct BatchArgs {
     uint32_t *jmp;
     EventRec *rec;
     uint32_t *status;            // [0] err index, [1] err code, [2] max seq, [3..] jump flags
+    uint32_t nofork;             // no fork branch in the epoch nor in the batch: branch = creator
 };
 
 struct FcArgs {

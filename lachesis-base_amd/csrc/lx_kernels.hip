@@ -140,7 +140,13 @@ __global__ void k_assign(BatchArgs a) {
     a.ev_bbefore[g] = a.B0 + rk - f;
     uint32_t sp = (s > 1) ? a.par[a.poff[e]] : LX_NONE;
     a.ev_sp[g] = sp;
-    if (f) {
+    if (a.nofork) {
+        // no fork branch anywhere (B = V before and after the batch): every
+        // event continues its creator's original branch (fillGlobalBranchID,
+        // vecengine/index.go:105-141), no pointer jumping needed
+        a.tmp_br[e] = c;
+        a.jmp[e] = e;
+    } else if (f) {
         uint32_t br = a.B0 + rk - 1;
         a.branch_first[br] = s;
         a.branch_creator[br] = c;
