@@ -297,9 +297,6 @@ typedef uint32_t u2v __attribute__((ext_vector_type(2)));
 #ifndef LX_PIPE
 #define LX_PIPE 1
 #endif
-#ifndef LX_IDLE_SLEEP
-#define LX_IDLE_SLEEP 0
-#endif
 // LDS read in inline asm: the compiler orders a plain LDS load after every
 // LDS-DMA (global_load_lds) still in flight (an s_waitcnt vmcnt(0))
 __device__ __forceinline__ uint32_t lds_ld32(uint32_t addr) {
@@ -606,47 +603,6 @@ __device__ __forceinline__ void blk_fold(const uint32_t pa[3], uint32_t W, uint3
         }
         return;
     }
-#ifdef LX_EXP_NARROW
-    if constexpr (CPW == 4) {
-        // timing experiment only (wrong values): LX_EXP_NARROW bytes of unit A per parent
-        if constexpr (LX_EXP_NARROW == 8) {
-            u2v x0, x1, x2;
-            asm volatile(
-                "ds_read_b64 %0, %4\n\t"
-                "ds_read_b64 %1, %5\n\t"
-                "ds_read_b64 %2, %6\n\t"
-                "ds_read_b32 %3, %7\n\t"
-                "s_waitcnt lgkmcnt(0)"
-                : "=&v"(x0), "=&v"(x1), "=&v"(x2), "=&v"(cw)
-                : "v"(pa[0]), "v"(pa[1]), "v"(pa[2]), "v"(W)
-                : "memory");
-            const u2v x[3] = {x0, x1, x2};
-#pragma unroll
-            for (int k = 0; k < 3; k++) {
-                tg[k][0] = tg[k][1] = x[k].x;
-#pragma unroll
-                for (int c = 0; c < CPW; c++) pv[k][c] = x[k].y;
-            }
-        } else {
-            u4v x0, x1, x2;
-            asm volatile(
-                "ds_read_b128 %0, %4\n\t"
-                "ds_read_b128 %1, %5\n\t"
-                "ds_read_b128 %2, %6\n\t"
-                "ds_read_b32 %3, %7\n\t"
-                "s_waitcnt lgkmcnt(0)"
-                : "=&v"(x0), "=&v"(x1), "=&v"(x2), "=&v"(cw)
-                : "v"(pa[0]), "v"(pa[1]), "v"(pa[2]), "v"(W)
-                : "memory");
-            const u4v x[3] = {x0, x1, x2};
-#pragma unroll
-            for (int k = 0; k < 3; k++) {
-                tg[k][0] = tg[k][1] = x[k].x;
-                pv[k][0] = x[k].y; pv[k][1] = x[k].z; pv[k][2] = x[k].w; pv[k][3] = x[k].y;
-            }
-        }
-    } else
-#endif
     if constexpr (CPW == 4) {
         constexpr uint32_t BOFF = (RN + 1) * 16;
         static_assert(BOFF < 65536, "ds offset field");
@@ -1425,7 +1381,6 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
                 LX_WP(c_done += fin ? 1u : 0u;)
                 LX_WP(c_wm += (rdy && !done && !fin) ? 1u : 0u;)
                 done = done || fin;
-                if (LX_IDLE_SLEEP && !__any(fin) && !__all(done)) __builtin_amdgcn_s_sleep(LX_IDLE_SLEEP);
             }
             if (++wstuck >= kLeanStuck && !rdy && !done) {
                 // waiting long (the wave's block fetched >= 64 passes ago): a
