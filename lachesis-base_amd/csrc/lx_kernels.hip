@@ -1289,9 +1289,12 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
             // come from the ring (own seq, L2 rows of old / overflow parents)
             uint32_t tg[3][2], pv[3][CPW];
             blk_fold<CPW, RN, PK>(pa, wm_addr, tg, pv, cw);
-            bool all = true;
+            // tag mismatches OR-ed on the VALU: no compare masks and no mask
+            // ANDs on the scalar unit, which the CU's waves share (C3 -1.9 %,
+            // C2 -5.2 % against v_cmp + s_and)
+            uint32_t tx = 0;
 #pragma unroll
-            for (int k = 0; k < 3; k++) all &= (tg[k][0] == px[k]) & (tg[k][1] == px[k]);
+            for (int k = 0; k < 3; k++) tx |= (tg[k][0] ^ px[k]) | (PK || CPW < 4 ? 0u : (tg[k][1] ^ px[k]));
             uint32_t m[CPW];
             uint32_t mp[2] = {0u, 0u};   // PK: the quad's maxima, two columns per dword
             if constexpr (PK) {
@@ -1314,10 +1317,9 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
             // the quad's readiness: AND of its four lanes by DPP (two VALU
             // steps; the ballot / scalar-shift / per-lane bit test it replaced
             // cost 7 VALU and 3 SALU: C3 walk -3.4 %)
-            uint32_t qa = all ? 1u : 0u;
-            qa &= (uint32_t)__builtin_amdgcn_mov_dpp((int)qa, kQuadSwap1, 0xF, 0xF, true);
-            qa &= (uint32_t)__builtin_amdgcn_mov_dpp((int)qa, kQuadSwap2, 0xF, 0xF, true);
-            const bool rdy = qa != 0u;
+            tx |= (uint32_t)__builtin_amdgcn_mov_dpp((int)tx, kQuadSwap1, 0xF, 0xF, true);
+            tx |= (uint32_t)__builtin_amdgcn_mov_dpp((int)tx, kQuadSwap2, 0xF, 0xF, true);
+            const bool rdy = tx == 0u;   // all twelve slot tags of the quad as expected
             if (rdy && !done && xi < np) {
                 // parents beyond the inline twelve (rare): one per pass, the same on every lane of the quad
                 const uint32_t pg = ld_l2_now(a.par_in + a.poff_in[lp] + xi);
