@@ -1314,9 +1314,9 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
                 }
             }
             // the quad's readiness: AND of its four lanes on the scalar unit
-            // the quad's readiness: AND of its four lanes by DPP (two VALU
-            // steps; the ballot / scalar-shift / per-lane bit test it replaced
-            // cost 7 VALU and 3 SALU: C3 walk -3.4 %)
+            // the quad's readiness: its four lanes' mismatches OR-ed by DPP
+            // (two VALU steps; the ballot / scalar-shift / per-lane bit test it
+            // replaced cost 7 VALU and 3 SALU: C3 walk -3.4 %)
             tx |= (uint32_t)__builtin_amdgcn_mov_dpp((int)tx, kQuadSwap1, 0xF, 0xF, true);
             tx |= (uint32_t)__builtin_amdgcn_mov_dpp((int)tx, kQuadSwap2, 0xF, 0xF, true);
             const bool rdy = tx == 0u;   // all twelve slot tags of the quad as expected
