@@ -62,6 +62,20 @@ int lx_create(const lx_config *cfg, lx_index **out);
 void lx_destroy(lx_index *h);
 const char *lx_last_error(const lx_index *h);
 
+/* Path selection for tests and tuning; no reference counterpart.  Every
+ * option picks between implementations that give identical results (the
+ * parity tests run each of them), so no setting changes an answer:
+ *   "small_max"  largest host-pointer batch on the latency path (lx_small; 0 = never)
+ *   "fc_fk"      0: ForklessCause on fork DAGs by the fix-up loop instead of the cheater-mask kernel
+ *   "cpw"        walker columns per workgroup: 0 (auto), 1, 2 or 4
+ *   "pack16"     0: two slot units per event even when every seq fits 16 bits
+ *   "la_memset"  1: zero the whole LowestAfter plane at lx_reset instead of the tail pass (before lx_reset)
+ *   "shard_wire" LowestAfter exchange width: 0 (auto), 2 or 4 bytes
+ *   "timing"     1: HIP-event timing of latency-path launches (lx_last_stats)
+ *   "fc_cache"   working set of lx_forkless_cause in events (0: no cache; default 4 V, 512..8192)
+ * The library reads no environment variables. */
+int lx_set_option(lx_index *h, const char *name, int64_t value);
+
 /* Reset (vecfc/index.go:98-105, vecengine/index.go:56-68): new epoch with
  * `n_validators` validators whose weights are given in idx order. */
 int lx_reset(lx_index *h, uint32_t n_validators, const uint32_t *weights_by_idx);
@@ -148,6 +162,30 @@ int lx_forkless_cause_batch(lx_index *h, uint64_t n, const uint32_t *a, const ui
  * events yield 0xFF in out and LX_ERR_ARG from the next lx_sync(). */
 int lx_forkless_cause_batch_dev(lx_index *h, uint64_t n, const uint32_t *a_dev, const uint32_t *b_dev,
                                 uint8_t *out_dev, void *stream);
+/* ForklessCause for one pair, as the unchanged caller asks it
+ * (vecfc/forkless_cause.go:28-38; per pair from forklessCausedByQuorumOn,
+ * abft/event_processing.go:149-161, and the election's observedRoots,
+ * abft/election/election.go:101-123).  Answered from the index's result
+ * cache -- the counterpart of the reference's ForklessCause LRU -- over a
+ * working set of the events recently asking and asked about; a miss fills a
+ * whole row (the asking event against the working set) or, for an older row,
+ * the whole working set in one launch, so a caller looping over a frame's
+ * roots waits for the GPU once per asking event.  Exact: FC(a, b) never
+ * changes once a is indexed; DropNotFlushed evicts the dropped events.  Option
+ * "fc_cache" sets the working set (0: every call evaluates its pair).
+ * Unknown events: LX_ERR_ARG. */
+int lx_forkless_cause(lx_index *h, uint32_t a, uint32_t b, uint8_t *out);
+typedef struct lx_fc_stats {
+    uint64_t calls;         /* lx_forkless_cause calls */
+    uint64_t hits;          /* answered from the cache without a launch */
+    uint64_t row_fills;     /* misses answered by one row launch (asking event x working set) */
+    uint64_t tile_fills;    /* misses answered by one working set x working set launch */
+    uint64_t pairs;         /* pairs evaluated on the GPU by the fills */
+    uint32_t slots;         /* working set capacity (events) */
+    uint32_t slots_used;
+} lx_fc_stats;
+int lx_fc_cache_stats(const lx_index *h, lx_fc_stats *out);
+
 /* Column-sharded partial: stake sum over this shard's creators, plus
  * 0x80000000 when this shard owns branch(b) and A observes it as forked.
  * Sum the partials of all shards (uint32) and apply lx_fc_combine. */
@@ -209,7 +247,7 @@ int lx_la_own_dev(lx_index *h, void *stream);
  * shard's outgoing block to dst -- 1 byte per entry when every entry is 0 or
  * within 127 of its row event's own seq (stored as LA - seq + 128; typical: a
  * branch observes an event a few seqs later), else lx_shard_wire's width
- * (LX_SHARD_WIRE pins the latter).  The sender tells the receiver the width
+ * (option shard_wire pins the latter).  The sender tells the receiver the width
  * (e.g. a G-int all-to-all) and both sides move the block with the _wire_
  * variants; the block occupies entries x width bytes.  Packing at width 1
  * checks as it goes: LX_ERR_WIRE means some entry did not fit, and the caller

@@ -187,7 +187,6 @@ struct lx_abft {
     bool dec_dirty = true;
     uint32_t vw = 0;                    // subject window [0, vw) of the current election
     uint32_t spec_depth = kSpecDepth;
-    bool trace = getenv("LX_ABFT_TRACE") != nullptr;   // per-launch shapes on stderr (diagnostics)
 
     lx_abft_stats stats{};
 
@@ -408,9 +407,12 @@ int eval_frame(lx_abft *a, const IndexView &iv, uint32_t f, const std::vector<ui
     ARC(reserve(a, a->arena, a->arena_used + (uint64_t)n * words + 1, a->arena_used, s));
     ARC(reserve(a, a->d_cand, n, 0, s));
     ARC(reserve(a, a->d_q, n, 0, s));
-    a->up.add(a->d_cand.p, cand.data(), n * 4ull);
     uint32_t *bits = a->arena.p + a->arena_used;
     if (words) {
+        // queued only when this step launches (flush_uploads below): a frame
+        // without roots must not leave a pending descriptor for d_cand that a
+        // later step's upload of the same range could race with
+        a->up.add(a->d_cand.p, cand.data(), n * 4ull);
         ARC(refresh_cheaters(a, iv));
         if (n > a->q_pin_cap) {
             if (a->q_pin) {
@@ -452,7 +454,6 @@ int eval_frame(lx_abft *a, const IndexView &iv, uint32_t f, const std::vector<ui
         r.col_split = col_split;
         r.n_split = n_split;
         ARC(flush_uploads(a, s));
-        if (a->trace) fprintf(stderr, "root_fc f=%u cand=%u roots=%u splits=%u col_split=%u\n", f, n, R, n_split, col_split);
         if (!a->ev_fc[0]) {
             AHIP(a, hipEventCreate(&a->ev_fc[0]));
             AHIP(a, hipEventCreate(&a->ev_fc[1]));
@@ -922,7 +923,6 @@ int lx_abft_create(lx_index *index, lx_abft **out) {
     if (!index || !out) return LX_ERR_ARG;
     lx_abft *a = new lx_abft();
     a->ix = index;
-    if (const char *e = getenv("LX_SPEC")) a->spec_depth = (uint32_t)atoi(e);
     *out = a;
     return 0;
 }

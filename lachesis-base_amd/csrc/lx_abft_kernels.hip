@@ -159,7 +159,7 @@ __global__ __launch_bounds__(256) void k_root_fc(RootFcArgs a) {
 uint32_t root_fc_splits(uint32_t n_cand, uint32_t n_roots, uint32_t ncols) {
     // enough workgroups to fill 256 CUs x 4, at least 4 LDS chunks per split
     const uint32_t tiles = ((n_roots + kTile - 1) / kTile) * ((n_cand + kTile - 1) / kTile);
-    static const uint32_t target = getenv("LX_ROOTFC_WGS") ? (uint32_t)atoi(getenv("LX_ROOTFC_WGS")) : 1024u;
+    constexpr uint32_t target = 1024u;
     uint32_t s = tiles ? (target + tiles - 1) / tiles : 1;
     const uint32_t max_s = ncols / (4 * kKc) ? ncols / (4 * kKc) : 1;
     return s < 1 ? 1 : (s > max_s ? max_s : s);
@@ -224,6 +224,29 @@ __global__ __launch_bounds__(256) void k_root_quorum(QuorumArgs a) {
 hipError_t launch_root_quorum(const QuorumArgs &a, hipStream_t s) {
     if (!a.n_cand) return hipSuccess;
     hipLaunchKernelGGL(k_root_quorum, dim3((a.n_cand + 3) / 4), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------- k_fc_tile_out
+// ForklessCause answers of a whole k_root_fc launch as bytes (the per-pair
+// result cache, lx_fccache.cpp): out[c * pitch + r] = tag[r] << 1 | FC(cand c,
+// root r), FC = (sum over the column splits >= quorum, no early-false flag).
+__global__ __launch_bounds__(256) void k_fc_tile_out(const uint32_t *psum, uint32_t n_split, uint32_t n_cand,
+                                                     uint32_t rp, uint32_t n_roots, uint32_t quorum, const uint8_t *tag,
+                                                     uint8_t *out, uint64_t pitch) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x, c = blockIdx.y;
+    if (r >= n_roots || c >= n_cand) return;
+    uint32_t sum = 0;
+    for (uint32_t z = 0; z < n_split; z++) sum += psum[((uint64_t)z * n_cand + c) * rp + r];
+    const uint32_t ok = !(sum >> 31) && sum >= quorum;
+    out[(uint64_t)c * pitch + r] = (uint8_t)(tag[r] << 1 | ok);
+}
+
+hipError_t launch_fc_tile_out(const uint32_t *psum, uint32_t n_split, uint32_t n_cand, uint32_t rp, uint32_t n_roots,
+                              uint32_t quorum, const uint8_t *tag, uint8_t *out, uint64_t pitch, hipStream_t s) {
+    if (!n_cand || !n_roots) return hipSuccess;
+    hipLaunchKernelGGL(k_fc_tile_out, dim3((n_roots + 255) / 256, n_cand), dim3(256), 0, s, psum, n_split, n_cand, rp,
+                       n_roots, quorum, tag, out, pitch);
     return hipGetLastError();
 }
 

@@ -5,208 +5,20 @@
 // lx_internal.h.  Host state is O(branches); all per-event work is on the GPU.
 #include <hip/hip_runtime.h>
 
-#include <algorithm>
-#include <cstdarg>
-#include <cstdio>
 #include <cstdlib>
 #include <cstring>
-#include <string>
-#include <vector>
 
-#include "../../include/lachesis_hip.h"
-#include "lx_internal.h"
 
-namespace {
+#include "lx_index.h"
 
-constexpr uint32_t kStatusWords = 64;   // [1] fc bad flag, [2] max seq, [3] pinned-FC sink, [4] unresolved
-                                        // branch, [5] load check flags, [8..9] batch error u64, [16..47] jump flags
+using namespace lxi;
 
-template <typename T>
-hipError_t dalloc(T **p, uint64_t n) {
-    *p = nullptr;
-    if (!n) n = 1;
-    return hipMalloc((void **)p, n * sizeof(T));
-}
-
-inline uint32_t round_up(uint32_t x, uint32_t m) { return (x + m - 1) / m * m; }
-
-// hipSetDevice costs microseconds per call; every entry point makes sure the
-// handle's device is current, so switch only when it is not
-inline hipError_t set_dev(int device) {
-    int cur = -1;
-    if (hipGetDevice(&cur) == hipSuccess && cur == device) return hipSuccess;
-    return hipSetDevice(device);
-}
-
-}  // namespace
-
-struct lx_index {
-    int device = 0;
-    hipStream_t stream = nullptr;
-    uint32_t shard_rank = 0, shard_count = 1;
-    std::string err;
-
-    // epoch
-    uint32_t V = 0;
-    std::vector<uint32_t> weights;
-    uint32_t quorum = 0;
-    uint32_t own_lo = 0, own_hi = 0;
-    uint64_t n_events = 0, n_flushed = 0, hwm = 0;
-    uint32_t B = 0, B_flushed = 0;
-    uint32_t max_seq = 0;
-    // LowestAfter tail zeroing (unsharded; TailArgs): per-(j, c) done-up-to seqs
-    bool la_tail = true;                   // LX_LA_MEMSET=1: zero the whole LA plane at reset instead
-    uint32_t *tail_zw = nullptr, *tail_lo = nullptr, *tail_cmin = nullptr;
-    uint32_t tail_cap = 0;
-    bool tail_dirty = false;               // zw holds progress (a tail pass ran since it was zeroed)
-    uint32_t wire_force = 0;               // LX_SHARD_WIRE=4: LowestAfter blocks always uint32
-    uint32_t *wire_flag = nullptr;         // device flag of the byte-wire fit check (4 B)
-    uint32_t pcols_used = 0;       // plane columns rows may hold non-zero values in (since the last zeroing)
-    bool have_epoch = false;
-
-    // host mirror of BranchesInfo (creator / first seq per branch; by creator)
-    std::vector<uint32_t> h_branch_creator, h_branch_first;
-    std::vector<std::vector<uint32_t>> by_creator;
-
-    // capacities
-    uint64_t n_cap = 0;
-    uint32_t stride = 0;   // == branch capacity
-    uint32_t pstride = 0;  // row stride of hb / la (= stride; a shard's local column capacity)
-    uint32_t s_cap = 0;
-    uint64_t cap_hint = 0;
-    uint32_t reserve = 0;
-
-    // device state
-    uint32_t *hb = nullptr, *la = nullptr;
-    uint32_t *ev_creator = nullptr, *ev_seq = nullptr, *ev_branch = nullptr, *ev_bbefore = nullptr,
-             *ev_sp = nullptr, *first_child = nullptr;
-    uint32_t *first_root = nullptr, *branch_first = nullptr, *branch_creator = nullptr, *branch_len = nullptr,
-             *brow = nullptr, *wpad = nullptr, *col_list = nullptr;
-    uint32_t *cheat_off = nullptr, *cheat_br = nullptr, *cheat_creator = nullptr;
-    uint32_t *cheat_brl = nullptr, *cheat_crl = nullptr;   // the same as plane columns (shards)
-    int32_t *cheat_of = nullptr;           // creator -> index into the cheater CSR (-1: one branch)
-    uint32_t cheat_of_cap = 0;
-    uint32_t n_cheat = 0, ncols = 0;
-    // fork-path ForklessCause tables per plane column (k_fc_fk; valid when
-    // fk_hi4 != 0): weight of a non-cheater's original, cheater index of a
-    // cheater's branches, the cheaters' weights
-    uint32_t *fk_w = nullptr, *fk_c = nullptr, *fk_wch = nullptr;
-    uint64_t fk_cap = 0;
-    uint32_t fk_hi4 = 0;
-    bool fc_fk = true;                     // LX_FC_FK=0: the fix-up loop kernel instead (A/B)
-    // column shard (shard_count > 1): own columns only (lx_internal.h)
-    std::vector<uint32_t> h_cmap;          // global branch -> plane column / LX_NONE
-    uint32_t nloc = 0;                     // plane columns in use
-    uint32_t *cmap = nullptr, *lap = nullptr, *wloc = nullptr;
-    uint32_t cmap_cap = 0;
-    bool sharded() const { return shard_count > 1; }
-    uint64_t cheat_cap = 0;
-    uint32_t *status = nullptr;
-
-    // batch scratch
-    uint64_t batch_cap = 0, par_cap = 0;
-    uint32_t *b_creator = nullptr, *b_seq = nullptr, *b_poff = nullptr, *b_par = nullptr;
-    uint32_t *b_isfork = nullptr, *b_rank = nullptr, *b_tmpbr = nullptr, *b_jmp = nullptr;
-    EventRec *b_rec = nullptr;
-    void *scan_tmp = nullptr;
-    size_t scan_bytes = 0;
-
-    // query scratch
-    uint64_t q_cap = 0;
-    uint32_t *q_a = nullptr, *q_b = nullptr;
-    uint8_t *q_out = nullptr;
-
-    // column-shard exchange cache (rows per shard at sc_events)
-    uint64_t sc_events = ~0ull;
-    uint32_t sc_B = 0;
-    std::vector<uint32_t *> sc_rows;
-    std::vector<uint32_t> sc_nrows;
-    uint32_t *sc_flag = nullptr, *sc_pos = nullptr, *sc_cols = nullptr;
-    std::vector<uint32_t> sc_col_off;    // shard q's columns: sc_cols[sc_col_off[q] .. sc_col_off[q+1])
-    uint64_t sc_cap = 0;
-    void *sc_tmp = nullptr;
-    size_t sc_tmp_bytes = 0;
-
-    // write-back (lx_writeback_*): dirty-row flags, row lists, byte offsets
-    uint64_t wb_cap = 0, wb_buf_cap = 0;
-    uint32_t *wb_flag = nullptr, *wb_pos = nullptr, *wb_la_rows = nullptr, *wb_hb_rows = nullptr, *wb_buf = nullptr;
-    uint64_t *wb_len = nullptr, *wb_la_off = nullptr, *wb_hb_off = nullptr;
-    void *wb_tmp = nullptr;
-    size_t wb_tmp_bytes = 0;
-    bool wb_ready = false;
-    lx_writeback wb{};
-    std::string wb_bi;
-
-    // small-batch (latency) path, lx_small.hip: the host assigns branches in Add
-    // order from a mirror of the per-event metadata and stages the batch in
-    // pinned memory; one H2D copy + one launch, no sync
-    uint32_t small_max = kSmallMaxN;       // LX_SMALL_MAX: largest batch on this path (0: never)
-    bool hm_ok = false;                    // the mirror equals the device metadata
-    uint64_t hm_n = 0;                     // events whose (immutable) metadata the mirror holds
-    std::vector<uint32_t> hm_creator, hm_seq, hm_branch, hm_bbefore;
-    std::vector<uint32_t> hm_blen;         // per branch: events on it (= device branch_len)
-    std::vector<uint32_t> sm_level, sm_cnt, sm_touched;   // scratch
-    static constexpr int kSlots = 4;       // pinned staging images in flight
-    uint32_t *st_pin[kSlots] = {};
-    uint64_t st_pin_cap[kSlots] = {};
-    hipEvent_t st_done[kSlots] = {};       // the H2D copy of slot k has read it
-    bool st_used[kSlots] = {};
-    uint32_t st_next = 0;
-    uint32_t *st_dev = nullptr;            // device image (stream order serialises its reuse)
-    SmallInlineArgs sm_inl{};              // arguments of the last launch; images of <= kSmallInline words inline
-    uint64_t st_dev_cap = 0;
-    // restart from the persisted tables (lx_load_rows / lx_load_finish)
-    bool loading = false;
-    std::vector<uint32_t> ld_first, ld_last, ld_count, ld_creator, ld_tail;   // per branch, as loaded
-    std::vector<uint32_t> ld_par;          // parents of every loaded event (dense)
-    std::vector<uint64_t> ld_poff;
-    uint32_t ld_B = 0;                     // branches seen so far (max ID + 1)
-    uint8_t *ld_buf = nullptr;             // device staging of a chunk's bytes and offsets
-    uint64_t ld_buf_cap = 0;
-
-    // pinned, device-mapped query buffers (per-call ForklessCause, getters)
-    uint8_t *qp = nullptr;
-    uint64_t qp_cap = 0;
-    uint32_t *q_sink = nullptr;            // status word the pinned FC path lets the kernel flag into
-
-    // timing (HIP events on `stream`)
-    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-    lx_stats stats{};
-    bool stats_lazy = false;               // small path: ms_index from ev[1..2] on demand
-    bool small_timing = false;             // LX_TIMING=1: time small-path launches (two event records)
-    uint32_t diag_nofill = 0;   // LX_DIAG_NOFILL=1: timing-only build of the walker (LA left empty)
-    uint32_t cpw_hint = 0, ncw_hint = 0;   // LX_CPW / LX_NCW tuning overrides
-    // walker compute layout: 2 = blocks of 16 events per wave, quad of lanes
-    // per event (default), 1 = independent quads, 0 = one lane per event
-    // (LX_WALKER=block/lean/classic); LX_LEAN_NCW compute waves, LX_DRAINS
-    // drain waves of the block layout
-    uint32_t lean = 2, lean_ncw = 0;   // 0: the walker picks (8, or 11 on 4-column slices)
-    uint32_t drains = 4;
-    bool pack16 = true;                    // LX_PACK16=0: two slot units per event even for small seqs
-    uint32_t rr_hint = 0, diag = 0;        // LX_RR record ring depth; LX_DIAG timing-only modes
-    bool prof = false;                     // LX_PROF=1: per-wave walker counters to stderr
-    uint32_t small = 0;                    // LX_SMALL=1: small-LDS walker (several workgroups per CU)
-    uint64_t last_npar = 0;                // parents in the current batch
-
-    int fail(int code, const char *fmt, ...) {
-        char buf[512];
-        va_list ap;
-        va_start(ap, fmt);
-        vsnprintf(buf, sizeof buf, fmt, ap);
-        va_end(ap);
-        err = buf;
-        return code;
-    }
-    int hip(hipError_t e, const char *what) {
-        if (e == hipSuccess) return 0;
-        return fail(e == hipErrorOutOfMemory ? LX_ERR_NOMEM : LX_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
-    }
-};
-
-#define HIPCHK(h, expr)                                  \
-    do {                                                 \
-        int _rc = (h)->hip((expr), #expr);               \
-        if (_rc) return _rc;                             \
+// Between lx_load_rows and lx_load_finish the branch table, B, the cheater
+// tables and the branch lengths are not rebuilt yet: every entry point that
+// reads or changes the epoch refuses (the load is finished or reset first).
+#define NOT_LOADING(h)                                                                            \
+    do {                                                                                          \
+        if ((h)->loading) return (h)->fail(LX_ERR_STATE, "index is loading (lx_load_finish first)"); \
     } while (0)
 
 namespace {
@@ -698,21 +510,8 @@ int add_batch_dev(lx_index *h, uint32_t n, const uint32_t *creator, const uint32
     ia.brow = h->brow;
     ia.s_cap = h->s_cap;
     ia.mask = (h->B > h->V) ? 1u : 0u;
-    ia.diag_nofill = h->diag_nofill;
     ia.cpw_hint = h->cpw_hint;
-    ia.rr_hint = h->rr_hint;
-    ia.diag = h->diag;
-    ia.small = h->small;
-    ia.ncw_hint = h->ncw_hint;
-    ia.lean = h->lean;
-    ia.lean_ncw = h->lean_ncw;
-    ia.drains = h->drains;
     ia.pack16 = h->pack16 && h->max_seq <= 0xFFFFu;
-    // antichain width of tdag-like DAGs ~ V / (1.6 P); P from the batch
-    {
-        uint32_t pbar = std::max<uint32_t>(1, (uint32_t)((h->last_npar + n - 1) / n));
-        ia.width_hint = std::max<uint32_t>(1, (uint32_t)(h->V * 10 / (16 * pbar)));
-    }
     const size_t prof_n = (size_t)kProfBlocks * kProfWaves * kProfSlots;
     if (h->prof) {
         HIPCHK(h, hipMalloc(&ia.prof, prof_n * 8));
@@ -775,7 +574,7 @@ int add_batch_dev(lx_index *h, uint32_t n, const uint32_t *creator, const uint32
         m.cheat_br = h->cheat_br;
         HIPCHK(h, lx::launch_marks(m, s));
     }
-    if (!h->sharded() && h->la_tail && !h->diag_nofill) {
+    if (!h->sharded() && h->la_tail) {
         if ((rc = la_tail(h, s))) return rc;
     }
     HIPCHK(h, hipEventRecord(h->ev[3], s));
@@ -796,9 +595,12 @@ int add_batch_dev(lx_index *h, uint32_t n, const uint32_t *creator, const uint32
     return 0;
 }
 
-int fc_args(lx_index *h, uint64_t n, const uint32_t *a, const uint32_t *b, uint8_t *out, uint32_t *partial,
-            FcArgs *fa) {
+}  // namespace
+
+int lx_fc_args(lx_index *h, uint64_t n, const uint32_t *a, const uint32_t *b, uint8_t *out, uint32_t *partial,
+               FcArgs *fa) {
     if (!h->have_epoch) return h->fail(LX_ERR_STATE, "ForklessCause before lx_reset");
+    NOT_LOADING(h);
     FcArgs f{};
     f.hb = h->hb;
     f.la = h->la;
@@ -840,6 +642,8 @@ int fc_args(lx_index *h, uint64_t n, const uint32_t *a, const uint32_t *b, uint8
     *fa = f;
     return 0;
 }
+
+namespace {
 
 void shard_bounds(const lx_index *h, uint32_t r, uint32_t *lo, uint32_t *hi) {
     auto bound = [&](uint32_t q) {
@@ -1374,22 +1178,9 @@ int lx_create(const lx_config *cfg, lx_index **out) {
         delete h;
         return LX_ERR_HIP;
     }
-    if (const char *d = getenv("LX_DIAG_NOFILL")) h->diag_nofill = (d[0] == '1');
-    if (const char *d = getenv("LX_FC_FK")) h->fc_fk = (d[0] != '0');
-    if (const char *d = getenv("LX_CPW")) h->cpw_hint = (uint32_t)atoi(d);
-    if (const char *d = getenv("LX_NCW")) h->ncw_hint = (uint32_t)atoi(d);
-    if (const char *d = getenv("LX_WALKER")) h->lean = strcmp(d, "lean") == 0 ? 1 : strcmp(d, "classic") == 0 ? 0 : 2;
-    if (const char *d = getenv("LX_LEAN_NCW")) h->lean_ncw = (uint32_t)atoi(d);
-    if (const char *d = getenv("LX_DRAINS")) h->drains = (uint32_t)atoi(d);
-    if (const char *d = getenv("LX_RR")) h->rr_hint = (uint32_t)atoi(d);
-    if (const char *d = getenv("LX_DIAG")) h->diag = (uint32_t)atoi(d);
-    if (const char *d = getenv("LX_PROF")) h->prof = (d[0] == '1');
-    if (const char *d = getenv("LX_SMALL")) h->small = (uint32_t)atoi(d);
-    if (const char *d = getenv("LX_LA_MEMSET")) h->la_tail = (d[0] != '1');
-    if (const char *d = getenv("LX_PACK16")) h->pack16 = (d[0] != '0');
-    if (const char *d = getenv("LX_SHARD_WIRE")) h->wire_force = (uint32_t)atoi(d);
-    if (const char *d = getenv("LX_SMALL_MAX")) h->small_max = (uint32_t)atoi(d);
-    if (const char *d = getenv("LX_TIMING")) h->small_timing = (d[0] == '1');
+#ifdef LX_WALKER_PROF
+    if (const char *d = getenv("LX_PROF")) h->prof = (d[0] == '1');   // counters build only (make WPROF=1)
+#endif
     for (auto &e : h->ev)
         if (hipEventCreate(&e) != hipSuccess) {
             delete h;
@@ -1408,6 +1199,7 @@ void lx_destroy(lx_index *h) {
     if (!h) return;
     (void)hipSetDevice(h->device);
     (void)hipStreamSynchronize(h->stream);
+    fcc_destroy(h);
     free_all(h);
     if (h->status) (void)hipFree(h->status);
     for (auto &e : h->ev)
@@ -1424,6 +1216,38 @@ void lx_destroy(lx_index *h) {
 }
 
 const char *lx_last_error(const lx_index *h) { return h ? h->err.c_str() : "null handle"; }
+
+int lx_set_option(lx_index *h, const char *name, int64_t value) {
+    if (!h || !name) return LX_ERR_ARG;
+    const std::string k(name);
+    if (k == "small_max") {
+        if (value < 0) return h->fail(LX_ERR_ARG, "small_max < 0");
+        h->small_max = (uint32_t)std::min<int64_t>(value, kSmallMaxN);
+    } else if (k == "fc_fk") {
+        h->fc_fk = value != 0;
+    } else if (k == "cpw") {
+        if (value != 0 && value != 1 && value != 2 && value != 4) return h->fail(LX_ERR_ARG, "cpw must be 0, 1, 2 or 4");
+        h->cpw_hint = (uint32_t)value;
+    } else if (k == "pack16") {
+        h->pack16 = value != 0;
+    } else if (k == "la_memset") {
+        if (h->have_epoch) return h->fail(LX_ERR_STATE, "la_memset must be set before lx_reset");
+        h->la_tail = value == 0;
+    } else if (k == "shard_wire") {
+        if (value != 0 && value != 2 && value != 4) return h->fail(LX_ERR_ARG, "shard_wire must be 0, 2 or 4");
+        h->wire_force = (uint32_t)value;
+    } else if (k == "timing") {
+        h->small_timing = value != 0;
+    } else if (k == "fc_cache") {
+        if (value < 0 || value > 16384) return h->fail(LX_ERR_ARG, "fc_cache must be 0..16384");
+        fcc_destroy(h);
+        h->fcc_slots = value ? round_up((uint32_t)value, 64) : 0;
+        h->fcc_slots_set = true;
+    } else {
+        return h->fail(LX_ERR_ARG, "unknown option %s", name);
+    }
+    return 0;
+}
 
 int lx_reset(lx_index *h, uint32_t nv, const uint32_t *w) {
     if (!h || (nv && !w)) return LX_ERR_ARG;
@@ -1527,6 +1351,12 @@ int lx_reset(lx_index *h, uint32_t nv, const uint32_t *w) {
     h->stats_lazy = false;
     h->loading = false;
     h->have_epoch = true;
+    if (!h->fcc_slots_set) {
+        const uint32_t w = std::min<uint32_t>(8192, std::max<uint32_t>(512, round_up(4 * nv, 64)));
+        if (w != h->fcc_slots) fcc_destroy(h);
+        h->fcc_slots = w;
+    }
+    fcc_clear(h);
     h->ncols = 0;
     return rebuild_columns(h);
 }
@@ -1568,6 +1398,7 @@ int lx_add_batch_dev(lx_index *h, uint32_t n, const uint32_t *creator, const uin
 
 int lx_flush(lx_index *h) {
     if (!h) return LX_ERR_ARG;
+    NOT_LOADING(h);
     h->wb_ready = false;
     h->n_flushed = h->n_events;
     h->B_flushed = h->B;
@@ -1576,6 +1407,7 @@ int lx_flush(lx_index *h) {
 
 int lx_drop_not_flushed(lx_index *h) {
     if (!h) return LX_ERR_ARG;
+    NOT_LOADING(h);
     if (!h->have_epoch) return 0;
     HIPCHK(h, set_dev(h->device));
     h->wb_ready = false;
@@ -1599,6 +1431,7 @@ int lx_drop_not_flushed(lx_index *h) {
     }
     h->hm_n = std::min(h->hm_n, h->n_flushed);
     h->n_events = h->n_flushed;
+    fcc_forget_from(h, h->n_flushed);
     if (h->B != h->B_flushed) {
         h->B = h->B_flushed;
         h->h_branch_creator.resize(h->B);
@@ -1621,6 +1454,7 @@ int lx_drop_not_flushed(lx_index *h) {
 int lx_writeback_prepare(lx_index *h, lx_writeback *out) {
     if (!h || !out) return LX_ERR_ARG;
     if (!h->have_epoch) return h->fail(LX_ERR_STATE, "write-back before lx_reset");
+    NOT_LOADING(h);
     if (h->shard_count > 1) return h->fail(LX_ERR_STATE, "write-back needs an unsharded handle (shards hold partial rows)");
     HIPCHK(h, set_dev(h->device));
     h->wb_ready = false;
@@ -1695,7 +1529,7 @@ int lx_forkless_cause_batch_dev(lx_index *h, uint64_t n, const uint32_t *a, cons
     if (!h) return LX_ERR_ARG;
     if (!n) return 0;
     FcArgs f;
-    int rc = fc_args(h, n, a, b, out, nullptr, &f);
+    int rc = lx_fc_args(h, n, a, b, out, nullptr, &f);
     if (rc) return rc;
     hipStream_t s = stream ? (hipStream_t)stream : h->stream;
     HIPCHK(h, lx::launch_fc(f, h->ncols, h->B > h->V, s));
@@ -1707,7 +1541,7 @@ int lx_forkless_cause_partial_dev(lx_index *h, uint64_t n, const uint32_t *a, co
     if (!h) return LX_ERR_ARG;
     if (!n) return 0;
     FcArgs f;
-    int rc = fc_args(h, n, a, b, nullptr, partial, &f);
+    int rc = lx_fc_args(h, n, a, b, nullptr, partial, &f);
     if (rc) return rc;
     hipStream_t s = stream ? (hipStream_t)stream : h->stream;
     HIPCHK(h, lx::launch_fc(f, h->ncols, h->B > h->V, s));
@@ -1735,7 +1569,7 @@ int lx_forkless_cause_batch(lx_index *h, uint64_t n, const uint32_t *a, const ui
         memcpy(hp, a, n * 4);
         memcpy(hp + 4 * n, b, n * 4);
         FcArgs f;
-        if ((rc = fc_args(h, n, reinterpret_cast<uint32_t *>(dp), reinterpret_cast<uint32_t *>(dp + 4 * n), dp + 8 * n,
+        if ((rc = lx_fc_args(h, n, reinterpret_cast<uint32_t *>(dp), reinterpret_cast<uint32_t *>(dp + 4 * n), dp + 8 * n,
                           nullptr, &f)))
             return rc;
         f.status = h->status + 2;   // k_fc flags status[1] = word 3, the sink; unknown events answer 0xFF
@@ -1771,6 +1605,7 @@ int lx_forkless_cause_batch(lx_index *h, uint64_t n, const uint32_t *a, const ui
 
 int lx_get_event_branch_id(lx_index *h, uint32_t ev, uint32_t *out) {
     if (!h || !out) return LX_ERR_ARG;
+    NOT_LOADING(h);
     if (ev >= h->n_events) return h->fail(LX_ERR_ARG, "failed to read event's branch ID (unknown event %u)", ev);
     if (h->hm_ok) {
         *out = h->hm_branch[ev];
@@ -1829,6 +1664,7 @@ int get_rows(lx_index *h, uint32_t mode, uint32_t n, const uint32_t *ev, uint8_t
 int get_check(lx_index *h, uint32_t n, const uint32_t *ev) {
     if (h->sharded()) return h->fail(LX_ERR_STATE, "vector getters need an unsharded handle (shards hold their own columns)");
     if (!h->have_epoch) return h->fail(LX_ERR_STATE, "getter before lx_reset");
+    NOT_LOADING(h);
     for (uint32_t i = 0; i < n; i++)
         if (ev[i] >= h->n_events) return h->fail(LX_ERR_ARG, "unknown event %u", ev[i]);
     HIPCHK(h, set_dev(h->device));
@@ -1903,6 +1739,7 @@ int lx_get_merged_highest_before_batch(lx_index *h, uint32_t n, const uint32_t *
 
 int lx_get_branches_info(lx_index *h, uint32_t *last_seq, uint32_t *creator_idx, uint32_t cap, uint32_t *n_branches) {
     if (!h) return LX_ERR_ARG;
+    NOT_LOADING(h);
     if (n_branches) *n_branches = h->B;
     if (!cap) return 0;
     HIPCHK(h, set_dev(h->device));
@@ -1932,7 +1769,7 @@ int lx_shard_range(const lx_index *h, uint32_t shard, uint32_t *lo, uint32_t *hi
 // Wire width of a LowestAfter block entry: LA entries are seqs or 0, so while
 // every seq of the epoch is < 2^16 they travel as uint16 (half the all-to-all
 // bytes).  max_seq follows the event stream, which every shard indexes whole,
-// so all shards agree on the width.  LX_SHARD_WIRE=4 forces uint32.
+// so all shards agree on the width.  Option shard_wire=4 forces uint32.
 static uint32_t shard_wire_bytes(const lx_index *h) {
     return (h->wire_force != 4 && h->max_seq <= 0xFFFFu) ? 2u : 4u;
 }
@@ -2012,7 +1849,7 @@ int lx_la_unpack_dev(lx_index *h, uint32_t src, const uint32_t *in, void *stream
 int lx_shard_block_wire(lx_index *h, uint32_t dst, uint32_t *bytes_per_entry) {
     if (!h || !bytes_per_entry || dst >= h->shard_count || dst == h->shard_rank) return LX_ERR_ARG;
     *bytes_per_entry = shard_wire_bytes(h);
-    if (h->wire_force) return 0;               // LX_SHARD_WIRE pins the epoch width
+    if (h->wire_force) return 0;               // option shard_wire pins the epoch width
     const int r = la_xfer(h, h->shard_rank, dst, nullptr, 3);
     if (r < 0) return r;
     if (r == 0) *bytes_per_entry = 1;
@@ -2023,7 +1860,7 @@ int lx_la_pack_wire_dev(lx_index *h, uint32_t dst, void *out, uint32_t bytes_per
     if (!h || dst >= h->shard_count || dst == h->shard_rank || !out) return LX_ERR_ARG;
     if (bytes_per_entry != 1 && bytes_per_entry != 2 && bytes_per_entry != 4) return LX_ERR_ARG;
     if (bytes_per_entry == 1 && h->wire_force)
-        return h->fail(LX_ERR_WIRE, "LX_SHARD_WIRE pins the wire to %u bytes", shard_wire_bytes(h));
+        return h->fail(LX_ERR_WIRE, "option shard_wire pins the wire to %u bytes", shard_wire_bytes(h));
     return la_xfer(h, h->shard_rank, dst, static_cast<uint32_t *>(out), 0, bytes_per_entry);
 }
 
@@ -2356,6 +2193,22 @@ int lx_load_finish(lx_index *h, const uint8_t *bi_rlp, uint32_t bi_len) {
     HIPCHK(h, hipMemcpyAsync(h->first_root, froot.data(), V * 4ull, hipMemcpyHostToDevice, st));
     h->pcols_used = std::max(h->pcols_used, B);
     if ((rc = rebuild_columns(h))) return rc;   // syncs the stream
+    if (N) {
+        // fork markers only in cheaters' columns (k_load_raw / k_load_check
+        // below verify those); a marker anywhere else is corrupt
+        std::vector<uint32_t> cheat_col(B, 0);
+        for (uint32_t b = 0; b < B; b++) cheat_col[b] = by[cr[b]].size() > 1 ? 1u : 0u;
+        uint32_t *d_cc = nullptr;
+        HIPCHK(h, hipMalloc((void **)&d_cc, 4ull * B));
+        HIPCHK(h, hipMemcpyAsync(d_cc, cheat_col.data(), 4ull * B, hipMemcpyHostToDevice, st));
+        HIPCHK(h, hipMemsetAsync(h->status + 5, 0, 4, st));
+        HIPCHK(h, lx::launch_load_marks_ok(h->hb, h->stride, (uint32_t)N, B, d_cc, h->status + 5, st));
+        uint32_t bad = 0;
+        HIPCHK(h, hipMemcpyAsync(&bad, h->status + 5, 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(h, hipStreamSynchronize(st));
+        (void)hipFree(d_cc);
+        if (bad) return load_fail(h, "fork marker in a column of a creator with one branch");
+    }
     if (B > V && h->n_cheat && N) {
         // raw seqs behind the fork markers (cheaters' columns), then the markers
         // re-derived from them must be exactly the loaded ones

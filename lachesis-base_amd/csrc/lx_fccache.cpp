@@ -1,0 +1,385 @@
+// lx_fccache.cpp -- lx_forkless_cause: ForklessCause for one (a, b) pair, the
+// way the unchanged caller asks it.
+//
+// The reference's callers ask one pair per call: forklessCausedByQuorumOn
+// loops over GetFrameRoots(f) (abft/event_processing.go:149-161), the
+// election's observedRoots over the previous frame's roots
+// (abft/election/election.go:101-123), processKnownRoots replays them after
+// every decided frame (abft/event_processing.go:102-146).  vecfc keeps an LRU
+// of answers (vecfc/forkless_cause.go:28-38, vecfc/index.go:91-95); here the
+// index keeps a result matrix over a working set of events and fills it a
+// row at a time on the GPU:
+//
+//  * working set: up to W events, each in a slot; every event that asks (a)
+//    or is asked about (b) joins it, and a newly asked b brings the next
+//    kWindow events of its Add order with it (the roots of a frame are asked
+//    in insertion order, most of them for the first time by the same event);
+//  * M[W][W] bytes in pinned, device-mapped host memory: M[sa][sb] =
+//    g7[sb] << 1 | FC(ev[sa], ev[sb]), valid while the column's generation
+//    g7[sb] (1..127, bumped when the slot gets a new event) matches -- a slot's
+//    reuse invalidates its column without touching W rows;
+//  * a miss on a row that was just created (a new asking event) or on the last
+//    asking event's row evaluates a against every slot in one k_fc launch
+//    (FcArgs.qa_bcast) whose answers land in M directly; a miss on an older
+//    row -- processKnownRoots replaying the roots of several frames -- fills
+//    the whole matrix with one k_root_fc tile launch (every row and column
+//    staged through LDS once per 64 x 64 tile) and k_fc_tile_out.
+//
+// Exactness: FC(a, b) is immutable once a is indexed (SURVEY Appendix A.5:
+// a later LowestAfter entry of b on branch j is the seq of an event a does
+// not observe), which is why the reference never invalidates its LRU except
+// at Reset; here DropNotFlushed also evicts the dropped events, because dense
+// indices are reused afterwards (hashes are not).
+#include "lx_index.h"
+
+#include <cstring>
+
+using namespace lxi;
+
+namespace {
+
+constexpr uint32_t kWindow = 64;   // events after a newly asked b that join the working set with it
+
+}  // namespace
+
+struct FcCache {
+    uint32_t W = 0, used = 0;
+    // pinned, device-mapped (the fill kernels read slot events and generations)
+    uint32_t *evk = nullptr, *evk_dev = nullptr;   // event per slot (free: a valid fallback, 0)
+    uint8_t *g7 = nullptr, *g7_dev = nullptr;       // column generation per slot, 1..127
+    uint8_t *M = nullptr, *M_dev = nullptr;         // [W][W]
+    uint32_t *qa = nullptr, *qa_dev = nullptr;      // the row's a
+    std::vector<uint32_t> ev;                       // slot -> event (LX_NONE: free)
+    std::vector<uint8_t> ref;                       // clock reference bits
+    std::vector<uint32_t> free_slots;
+    uint32_t hand = 0;
+    // event -> slot: open addressing, linear probing, backward-shift deletion
+    std::vector<uint32_t> hk, hv;
+    uint32_t hmask = 0;
+    uint32_t last_a = LX_NONE, last_sa = LX_NONE;
+    // tile fills: partial sums and the cheaters' branch columns (k_root_fc)
+    uint32_t *d_psum = nullptr;
+    uint64_t psum_cap = 0;
+    uint32_t *d_k = nullptr;                         // kcol | kflag | kw, k_cap entries each
+    uint32_t n_k = 0, k_B = 0, k_cap = 0;
+    lx_fc_stats st{};
+
+    uint32_t hash(uint32_t e) const { return (uint32_t)((e * 0x9E3779B97F4A7C15ull) >> 40) & hmask; }
+    uint32_t find(uint32_t e) const {
+        for (uint32_t i = hash(e);; i = (i + 1) & hmask) {
+            const uint32_t k = hk[i];
+            if (k == e) return hv[i];
+            if (k == LX_NONE) return LX_NONE;
+        }
+    }
+    void map_put(uint32_t e, uint32_t s) {
+        uint32_t i = hash(e);
+        while (hk[i] != LX_NONE) i = (i + 1) & hmask;
+        hk[i] = e;
+        hv[i] = s;
+    }
+    void map_erase(uint32_t e) {
+        uint32_t i = hash(e);
+        while (hk[i] != e) {
+            if (hk[i] == LX_NONE) return;
+            i = (i + 1) & hmask;
+        }
+        hk[i] = LX_NONE;
+        for (uint32_t j = (i + 1) & hmask; hk[j] != LX_NONE; j = (j + 1) & hmask) {
+            const uint32_t want = hash(hk[j]);
+            if (((j - want) & hmask) >= ((j - i) & hmask)) {   // backward shift
+                hk[i] = hk[j];
+                hv[i] = hv[j];
+                hk[j] = LX_NONE;
+                i = j;
+            }
+        }
+    }
+    void free_slot(uint32_t s) {
+        map_erase(ev[s]);
+        ev[s] = LX_NONE;
+        evk[s] = 0;
+        free_slots.push_back(s);
+        if (last_sa == s) last_a = last_sa = LX_NONE;
+    }
+    // a slot for event e (clock replacement; never p0 or p1)
+    uint32_t insert(uint32_t e, uint32_t p0, uint32_t p1) {
+        uint32_t s;
+        if (!free_slots.empty()) {
+            s = free_slots.back();
+            free_slots.pop_back();
+        } else if (used < W) {
+            s = used++;
+        } else {
+            for (;;) {
+                const uint32_t x = hand;
+                hand = (hand + 1) % W;
+                if (x == p0 || x == p1) continue;
+                if (ref[x]) { ref[x] = 0; continue; }
+                s = x;
+                break;
+            }
+            free_slot(s);
+            free_slots.pop_back();
+        }
+        ev[s] = e;
+        evk[s] = e;
+        map_put(e, s);
+        g7[s] = (uint8_t)(g7[s] % 127u + 1u);
+        if (g7[s] == 1)   // the generation wrapped: entries of an old occupant could match again
+            for (uint32_t r = 0; r < W; r++) M[(uint64_t)r * W + s] = 0;
+        memset(M + (uint64_t)s * W, 0, W);
+        ref[s] = 1;
+        return s;
+    }
+    void clear() {
+        std::fill(hk.begin(), hk.end(), LX_NONE);
+        std::fill(ev.begin(), ev.end(), LX_NONE);
+        for (uint32_t s = 0; s < W; s++) evk[s] = 0;
+        std::fill(ref.begin(), ref.end(), 0);
+        free_slots.clear();
+        used = 0;
+        hand = 0;
+        last_a = last_sa = LX_NONE;
+        k_B = 0;
+    }
+};
+
+namespace {
+
+void fcc_free(FcCache *c) {
+    if (!c) return;
+    for (void *p : {(void *)c->evk, (void *)c->g7, (void *)c->M, (void *)c->qa})
+        if (p) (void)hipHostFree(p);
+    if (c->d_psum) (void)hipFree(c->d_psum);
+    if (c->d_k) (void)hipFree(c->d_k);
+    delete c;
+}
+
+int fcc_make(lx_index *h) {
+    if (h->fcc) return 0;
+    const uint32_t W = h->fcc_slots;
+    FcCache *c = new FcCache();
+    c->W = W;
+    void *d = nullptr;
+    auto pin = [&](void **host, void **dev, uint64_t bytes) -> hipError_t {
+        hipError_t e = hipHostMalloc(host, bytes, hipHostMallocMapped);
+        if (e != hipSuccess) return e;
+        return hipHostGetDevicePointer(dev, *host, 0);
+    };
+    hipError_t e = pin((void **)&c->evk, &d, 4ull * W);
+    c->evk_dev = static_cast<uint32_t *>(d);
+    if (e == hipSuccess) { e = pin((void **)&c->g7, &d, W); c->g7_dev = static_cast<uint8_t *>(d); }
+    if (e == hipSuccess) { e = pin((void **)&c->M, &d, (uint64_t)W * W); c->M_dev = static_cast<uint8_t *>(d); }
+    if (e == hipSuccess) { e = pin((void **)&c->qa, &d, 64); c->qa_dev = static_cast<uint32_t *>(d); }
+    if (e != hipSuccess) {
+        fcc_free(c);
+        return h->hip(e, "ForklessCause cache (pinned memory)");
+    }
+    memset(c->g7, 0, W);
+    memset(c->M, 0, (uint64_t)W * W);
+    c->ev.assign(W, LX_NONE);
+    c->ref.assign(W, 0);
+    uint32_t m = 1;
+    while (m < 2 * W) m <<= 1;
+    c->hmask = m - 1;
+    c->hk.assign(m, LX_NONE);
+    c->hv.assign(m, 0);
+    c->clear();
+    c->st.slots = W;
+    h->fcc = c;
+    return 0;
+}
+
+// the cheaters' branch columns for k_root_fc, grouped by creator, original first
+int fcc_cheaters(lx_index *h, FcCache *c) {
+    if (c->k_B == h->B) return 0;
+    std::vector<uint32_t> col, flag, kw;
+    for (uint32_t v = 0; v < h->V; v++) {
+        const auto &l = h->by_creator[v];
+        if (l.size() < 2) continue;
+        for (size_t i = 0; i < l.size(); i++) {
+            col.push_back(l[i]);
+            flag.push_back((i == 0 ? 1u : 0u) | (i + 1 == l.size() ? 2u : 0u));
+            kw.push_back(i + 1 == l.size() ? h->weights[v] : 0u);
+        }
+    }
+    c->n_k = (uint32_t)col.size();
+    if (c->n_k > c->k_cap) {
+        if (c->d_k) {
+            HIPCHK(h, hipStreamSynchronize(h->stream));
+            (void)hipFree(c->d_k);
+        }
+        c->d_k = nullptr;
+        c->k_cap = 0;
+        HIPCHK(h, hipMalloc((void **)&c->d_k, 12ull * c->n_k));
+        c->k_cap = c->n_k;
+    }
+    if (c->n_k) {
+        std::vector<uint32_t> all(col);
+        all.insert(all.end(), flag.begin(), flag.end());
+        all.insert(all.end(), kw.begin(), kw.end());
+        // sized for this B: the copy runs before any tile launch on the stream
+        HIPCHK(h, hipMemcpyAsync(c->d_k, all.data(), 4ull * all.size(), hipMemcpyHostToDevice, h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+    }
+    c->k_B = h->B;
+    return 0;
+}
+
+// a against every slot in use: one k_fc launch, answers into M's row sa
+int fcc_row(lx_index *h, FcCache *c, uint32_t a, uint32_t sa) {
+    c->qa[0] = a;
+    FcArgs f;
+    int rc = lx_fc_args(h, c->used, c->qa_dev, c->evk_dev, c->M_dev + (uint64_t)sa * c->W, nullptr, &f);
+    if (rc) return rc;
+    f.qa_bcast = 1;
+    f.out_tag = c->g7_dev;
+    f.status = h->status + 2;   // the pinned-path sink: every slot holds a known event
+    HIPCHK(h, lx::launch_fc(f, h->ncols, h->B > h->V, h->stream));
+    c->st.row_fills++;
+    c->st.pairs += c->used;
+    return 0;
+}
+
+// every slot against every slot: k_root_fc tiles + k_fc_tile_out into M
+int fcc_tile(lx_index *h, FcCache *c) {
+    int rc;
+    if ((rc = fcc_cheaters(h, c))) return rc;
+    const uint32_t n = c->used, words = (n + 31) / 32, rp = words * 32;
+    const uint32_t ncols = (h->V + 31) / 32 * 32;
+    const uint32_t splits = lx::root_fc_splits(n, n, ncols);
+    const uint32_t col_split = ((ncols + splits - 1) / splits + 31) / 32 * 32;
+    const uint32_t n_split = (ncols + col_split - 1) / col_split;
+    const uint64_t need = (uint64_t)n_split * n * rp;
+    if (need > c->psum_cap) {
+        if (c->d_psum) {
+            HIPCHK(h, hipStreamSynchronize(h->stream));
+            (void)hipFree(c->d_psum);
+        }
+        c->d_psum = nullptr;
+        c->psum_cap = 0;
+        HIPCHK(h, dalloc(&c->d_psum, need));
+        c->psum_cap = need;
+    }
+    RootFcArgs r{};
+    r.hb = h->hb;
+    r.la = h->la;
+    r.stride = h->pstride;
+    r.cand = c->evk_dev;
+    r.n_cand = n;
+    r.roots = c->evk_dev;
+    r.n_roots = n;
+    r.roots_fallback = c->evk[0];
+    r.ncols = ncols;
+    r.wpad = h->wpad;
+    r.quorum = h->quorum;
+    r.n_k = c->n_k;
+    r.kcol = c->d_k;
+    r.kflag = c->d_k + c->n_k;
+    r.kw = c->d_k + 2ull * c->n_k;
+    r.ev_branch = h->ev_branch;
+    r.psum = c->d_psum;
+    r.words = words;
+    r.col_split = col_split;
+    r.n_split = n_split;
+    HIPCHK(h, lx::launch_root_fc(r, h->B > h->V, h->stream));
+    HIPCHK(h, lx::launch_fc_tile_out(c->d_psum, n_split, n, rp, n, h->quorum, c->g7_dev, c->M_dev, c->W, h->stream));
+    c->st.tile_fills++;
+    c->st.pairs += (uint64_t)n * n;
+    return 0;
+}
+
+inline bool fcc_hit(FcCache *c, uint32_t a, uint32_t b, uint8_t *out) {
+    const uint32_t sa = a == c->last_a ? c->last_sa : c->find(a);
+    if (sa == LX_NONE) return false;
+    const uint32_t sb = c->find(b);
+    if (sb == LX_NONE) return false;
+    const uint8_t m = c->M[(uint64_t)sa * c->W + sb];
+    if ((m >> 1) != c->g7[sb]) return false;
+    c->ref[sa] = c->ref[sb] = 1;
+    c->last_a = a;
+    c->last_sa = sa;
+    *out = m & 1u;
+    return true;
+}
+
+int fcc_query(lx_index *h, uint32_t a, uint32_t b, uint8_t *out) {
+    FcCache *c = h->fcc;
+    c->st.calls++;
+    if (fcc_hit(c, a, b, out)) {
+        c->st.hits++;
+        return 0;
+    }
+    HIPCHK(h, set_dev(h->device));
+    uint32_t sa = c->find(a);
+    const bool a_new = sa == LX_NONE;
+    if (a_new) sa = c->insert(a, LX_NONE, LX_NONE);
+    uint32_t sb = c->find(b);
+    if (sb == LX_NONE) {
+        sb = c->insert(b, sa, LX_NONE);
+        for (uint64_t e = (uint64_t)b + 1; e < (uint64_t)b + kWindow && e < h->n_events; e++)
+            if (c->find((uint32_t)e) == LX_NONE) c->insert((uint32_t)e, sa, sb);
+    }
+    int rc;
+    if (a_new || a == c->last_a) rc = fcc_row(h, c, a, sa);
+    else rc = fcc_tile(h, c);
+    if (rc) return rc;
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    const uint8_t m = c->M[(uint64_t)sa * c->W + sb];
+    if ((m >> 1) != c->g7[sb]) return h->fail(LX_ERR_STATE, "ForklessCause cache: fill left (%u, %u) unanswered", a, b);
+    c->ref[sa] = c->ref[sb] = 1;
+    c->last_a = a;
+    c->last_sa = sa;
+    *out = m & 1u;
+    return 0;
+}
+
+}  // namespace
+
+void fcc_destroy(lx_index *h) {
+    if (h->fcc) (void)hipStreamSynchronize(h->stream);
+    fcc_free(h->fcc);
+    h->fcc = nullptr;
+}
+
+void fcc_clear(lx_index *h) {
+    if (h->fcc) h->fcc->clear();
+}
+
+void fcc_forget_from(lx_index *h, uint64_t n) {
+    FcCache *c = h->fcc;
+    if (!c) return;
+    for (uint32_t s = 0; s < c->used; s++)
+        if (c->ev[s] != LX_NONE && c->ev[s] >= n) c->free_slot(s);
+}
+
+extern "C" {
+
+int lx_forkless_cause(lx_index *h, uint32_t a, uint32_t b, uint8_t *out) {
+    if (!h || !out) return LX_ERR_ARG;
+    if (!h->have_epoch) return h->fail(LX_ERR_STATE, "ForklessCause before lx_reset");
+    if (h->loading) return h->fail(LX_ERR_STATE, "index is loading (lx_load_finish first)");
+    if (a >= h->n_events || b >= h->n_events)
+        return h->fail(LX_ERR_ARG, "ForklessCause on an unknown event");   // forkless_cause.go:43-61 (crit)
+    if (h->sharded() || !h->fcc_slots) return lx_forkless_cause_batch(h, 1, &a, &b, out);
+    if (!h->fcc) {
+        int rc = fcc_make(h);
+        if (rc) return rc;
+    }
+    return fcc_query(h, a, b, out);
+}
+
+int lx_fc_cache_stats(const lx_index *h, lx_fc_stats *out) {
+    if (!h || !out) return LX_ERR_ARG;
+    if (h->fcc) {
+        *out = h->fcc->st;
+        out->slots_used = h->fcc->used - (uint32_t)h->fcc->free_slots.size();
+    } else {
+        *out = lx_fc_stats{};
+        out->slots = h->fcc_slots;
+    }
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,211 @@
+// lx_index.h -- the index handle behind the C ABI (include/lachesis_hip.h),
+// shared by the host engine (lx_capi.cpp) and the ForklessCause result cache
+// (lx_fccache.cpp).  Internal: not part of the ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#include "../../include/lachesis_hip.h"
+#include "lx_internal.h"
+
+struct FcCache;   // lx_fccache.cpp
+
+namespace lxi {
+
+constexpr uint32_t kStatusWords = 64;   // [1] fc bad flag, [2] max seq, [3] pinned-FC sink, [4] unresolved
+                                        // branch, [5] load check flags, [8..9] batch error u64, [16..47] jump flags
+
+template <typename T>
+hipError_t dalloc(T **p, uint64_t n) {
+    *p = nullptr;
+    if (!n) n = 1;
+    return hipMalloc((void **)p, n * sizeof(T));
+}
+
+inline uint32_t round_up(uint32_t x, uint32_t m) { return (x + m - 1) / m * m; }
+
+// hipSetDevice costs microseconds per call; every entry point makes sure the
+// handle's device is current, so switch only when it is not
+inline hipError_t set_dev(int device) {
+    int cur = -1;
+    if (hipGetDevice(&cur) == hipSuccess && cur == device) return hipSuccess;
+    return hipSetDevice(device);
+}
+
+}  // namespace lxi
+
+struct lx_index {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    uint32_t shard_rank = 0, shard_count = 1;
+    std::string err;
+
+    // epoch
+    uint32_t V = 0;
+    std::vector<uint32_t> weights;
+    uint32_t quorum = 0;
+    uint32_t own_lo = 0, own_hi = 0;
+    uint64_t n_events = 0, n_flushed = 0, hwm = 0;
+    uint32_t B = 0, B_flushed = 0;
+    uint32_t max_seq = 0;
+    // LowestAfter tail zeroing (unsharded; TailArgs): per-(j, c) done-up-to seqs
+    bool la_tail = true;                   // option la_memset=1: zero the whole LA plane at reset instead
+    uint32_t *tail_zw = nullptr, *tail_lo = nullptr, *tail_cmin = nullptr;
+    uint32_t tail_cap = 0;
+    bool tail_dirty = false;               // zw holds progress (a tail pass ran since it was zeroed)
+    uint32_t wire_force = 0;               // option shard_wire=4: LowestAfter blocks always uint32
+    uint32_t *wire_flag = nullptr;         // device flag of the byte-wire fit check (4 B)
+    uint32_t pcols_used = 0;       // plane columns rows may hold non-zero values in (since the last zeroing)
+    bool have_epoch = false;
+
+    // host mirror of BranchesInfo (creator / first seq per branch; by creator)
+    std::vector<uint32_t> h_branch_creator, h_branch_first;
+    std::vector<std::vector<uint32_t>> by_creator;
+
+    // capacities
+    uint64_t n_cap = 0;
+    uint32_t stride = 0;   // == branch capacity
+    uint32_t pstride = 0;  // row stride of hb / la (= stride; a shard's local column capacity)
+    uint32_t s_cap = 0;
+    uint64_t cap_hint = 0;
+    uint32_t reserve = 0;
+
+    // device state
+    uint32_t *hb = nullptr, *la = nullptr;
+    uint32_t *ev_creator = nullptr, *ev_seq = nullptr, *ev_branch = nullptr, *ev_bbefore = nullptr,
+             *ev_sp = nullptr, *first_child = nullptr;
+    uint32_t *first_root = nullptr, *branch_first = nullptr, *branch_creator = nullptr, *branch_len = nullptr,
+             *brow = nullptr, *wpad = nullptr, *col_list = nullptr;
+    uint32_t *cheat_off = nullptr, *cheat_br = nullptr, *cheat_creator = nullptr;
+    uint32_t *cheat_brl = nullptr, *cheat_crl = nullptr;   // the same as plane columns (shards)
+    int32_t *cheat_of = nullptr;           // creator -> index into the cheater CSR (-1: one branch)
+    uint32_t cheat_of_cap = 0;
+    uint32_t n_cheat = 0, ncols = 0;
+    // fork-path ForklessCause tables per plane column (k_fc_fk; valid when
+    // fk_hi4 != 0): weight of a non-cheater's original, cheater index of a
+    // cheater's branches, the cheaters' weights
+    uint32_t *fk_w = nullptr, *fk_c = nullptr, *fk_wch = nullptr;
+    uint64_t fk_cap = 0;
+    uint32_t fk_hi4 = 0;
+    bool fc_fk = true;                     // option fc_fk=0: the fix-up loop kernel instead
+    // column shard (shard_count > 1): own columns only (lx_internal.h)
+    std::vector<uint32_t> h_cmap;          // global branch -> plane column / LX_NONE
+    uint32_t nloc = 0;                     // plane columns in use
+    uint32_t *cmap = nullptr, *lap = nullptr, *wloc = nullptr;
+    uint32_t cmap_cap = 0;
+    bool sharded() const { return shard_count > 1; }
+    uint64_t cheat_cap = 0;
+    uint32_t *status = nullptr;
+
+    // batch scratch
+    uint64_t batch_cap = 0, par_cap = 0;
+    uint32_t *b_creator = nullptr, *b_seq = nullptr, *b_poff = nullptr, *b_par = nullptr;
+    uint32_t *b_isfork = nullptr, *b_rank = nullptr, *b_tmpbr = nullptr, *b_jmp = nullptr;
+    EventRec *b_rec = nullptr;
+    void *scan_tmp = nullptr;
+    size_t scan_bytes = 0;
+
+    // query scratch
+    uint64_t q_cap = 0;
+    uint32_t *q_a = nullptr, *q_b = nullptr;
+    uint8_t *q_out = nullptr;
+
+    // column-shard exchange cache (rows per shard at sc_events)
+    uint64_t sc_events = ~0ull;
+    uint32_t sc_B = 0;
+    std::vector<uint32_t *> sc_rows;
+    std::vector<uint32_t> sc_nrows;
+    uint32_t *sc_flag = nullptr, *sc_pos = nullptr, *sc_cols = nullptr;
+    std::vector<uint32_t> sc_col_off;    // shard q's columns: sc_cols[sc_col_off[q] .. sc_col_off[q+1])
+    uint64_t sc_cap = 0;
+    void *sc_tmp = nullptr;
+    size_t sc_tmp_bytes = 0;
+
+    // write-back (lx_writeback_*): dirty-row flags, row lists, byte offsets
+    uint64_t wb_cap = 0, wb_buf_cap = 0;
+    uint32_t *wb_flag = nullptr, *wb_pos = nullptr, *wb_la_rows = nullptr, *wb_hb_rows = nullptr, *wb_buf = nullptr;
+    uint64_t *wb_len = nullptr, *wb_la_off = nullptr, *wb_hb_off = nullptr;
+    void *wb_tmp = nullptr;
+    size_t wb_tmp_bytes = 0;
+    bool wb_ready = false;
+    lx_writeback wb{};
+    std::string wb_bi;
+
+    // small-batch (latency) path, lx_small.hip: the host assigns branches in Add
+    // order from a mirror of the per-event metadata and stages the batch in
+    // pinned memory; one H2D copy + one launch, no sync
+    uint32_t small_max = kSmallMaxN;       // option small_max: largest batch on this path (0: never)
+    bool hm_ok = false;                    // the mirror equals the device metadata
+    uint64_t hm_n = 0;                     // events whose (immutable) metadata the mirror holds
+    std::vector<uint32_t> hm_creator, hm_seq, hm_branch, hm_bbefore;
+    std::vector<uint32_t> hm_blen;         // per branch: events on it (= device branch_len)
+    std::vector<uint32_t> sm_level, sm_cnt, sm_touched;   // scratch
+    static constexpr int kSlots = 4;       // pinned staging images in flight
+    uint32_t *st_pin[kSlots] = {};
+    uint64_t st_pin_cap[kSlots] = {};
+    hipEvent_t st_done[kSlots] = {};       // the H2D copy of slot k has read it
+    bool st_used[kSlots] = {};
+    uint32_t st_next = 0;
+    uint32_t *st_dev = nullptr;            // device image (stream order serialises its reuse)
+    SmallInlineArgs sm_inl{};              // arguments of the last launch; images of <= kSmallInline words inline
+    uint64_t st_dev_cap = 0;
+    // restart from the persisted tables (lx_load_rows / lx_load_finish)
+    bool loading = false;
+    std::vector<uint32_t> ld_first, ld_last, ld_count, ld_creator, ld_tail;   // per branch, as loaded
+    std::vector<uint32_t> ld_par;          // parents of every loaded event (dense)
+    std::vector<uint64_t> ld_poff;
+    uint32_t ld_B = 0;                     // branches seen so far (max ID + 1)
+    uint8_t *ld_buf = nullptr;             // device staging of a chunk's bytes and offsets
+    uint64_t ld_buf_cap = 0;
+
+    // pinned, device-mapped query buffers (per-call ForklessCause, getters)
+    uint8_t *qp = nullptr;
+    uint64_t qp_cap = 0;
+    uint32_t *q_sink = nullptr;            // status word the pinned FC path lets the kernel flag into
+
+    // timing (HIP events on `stream`)
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    lx_stats stats{};
+    bool stats_lazy = false;               // small path: ms_index from ev[1..2] on demand
+    bool small_timing = false;             // option timing=1: time small-path launches (two event records)
+    uint32_t cpw_hint = 0;                 // option cpw: walker columns per workgroup (0 = auto)
+    bool pack16 = true;                    // option pack16=0: two slot units per event even for small seqs
+    bool prof = false;                     // LX_PROF=1 in make WPROF=1 builds: per-wave walker counters
+    uint64_t last_npar = 0;                // parents in the current batch
+    FcCache *fcc = nullptr;                // per-pair ForklessCause result cache (lx_fccache.cpp)
+    uint32_t fcc_slots = 4096;             // option fc_cache: its working set (0 = no cache)
+    bool fcc_slots_set = false;            // set by the option (else sized at lx_reset from V)
+
+    int fail(int code, const char *fmt, ...) {
+        char buf[512];
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(buf, sizeof buf, fmt, ap);
+        va_end(ap);
+        err = buf;
+        return code;
+    }
+    int hip(hipError_t e, const char *what) {
+        if (e == hipSuccess) return 0;
+        return fail(e == hipErrorOutOfMemory ? LX_ERR_NOMEM : LX_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
+    }
+};
+
+#define HIPCHK(h, expr)                                  \
+    do {                                                 \
+        int _rc = (h)->hip((expr), #expr);               \
+        if (_rc) return _rc;                             \
+    } while (0)
+
+
+// internal entry points shared by lx_capi.cpp and lx_fccache.cpp
+int lx_fc_args(lx_index *h, uint64_t n, const uint32_t *a, const uint32_t *b, uint8_t *out, uint32_t *partial,
+               FcArgs *fa);
+void fcc_destroy(lx_index *h);
+void fcc_clear(lx_index *h);                    // Reset: a new epoch
+void fcc_forget_from(lx_index *h, uint64_t n);  // DropNotFlushed: events >= n are gone

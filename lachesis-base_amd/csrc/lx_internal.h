@@ -55,20 +55,11 @@ struct IndexArgs {
     const uint32_t *brow;
     uint32_t s_cap;
     uint32_t mask;               // older rows may carry fork marks
-    uint32_t diag_nofill;        // diagnostic timing build: skip the LA fill (LX_DIAG_NOFILL=1)
-    uint32_t cpw_hint;           // columns per workgroup (0 = auto; LX_CPW)
-    uint32_t ncw_hint;           // compute waves per workgroup (0 = auto; LX_NCW)
-    uint32_t width_hint;         // expected antichain width of the batch
-    uint32_t rr_hint;            // record ring depth (LX_RR; 0 = auto)
-    uint32_t diag;               // timing-only diagnostics (LX_DIAG): 2 no deps, 3 no global stores
-    unsigned long long *prof;    // optional per-wave counters (LX_PROF=1), kProfSlots per wave
-    uint32_t small;              // small-LDS walker variant (LX_SMALL=1)
+    uint32_t cpw_hint;           // columns per workgroup (0 = auto; lx_set_option "cpw", tests)
+    unsigned long long *prof;    // per-wave counters (make WPROF=1 builds only), kProfSlots per wave
     const uint32_t *cmap;        // sharded: global branch -> plane column (NULL = identity)
     uint32_t *lap;               // sharded: LowestAfter rows of own branches (fill target)
     uint64_t lap_stride;         // = global branch capacity
-    uint32_t lean;               // quad-per-event compute waves (CPW 4; LX_WALKER=lean)
-    uint32_t lean_ncw;           // their compute waves (4 or 8)
-    uint32_t drains;             // drain waves of the block layout (2 or 4; LX_DRAINS)
     uint32_t pack16;             // every seq of the epoch <= 0xFFFF: 16-B packed slots (4-column block walker)
 };
 constexpr int kProfSlots = 16;   // see k_index: passes, spin misses, chunk folds, completes, ...
@@ -114,6 +105,8 @@ struct FcArgs {
     const uint32_t *qa;
     const uint32_t *qb;
     uint8_t *out;                // bool result (or NULL)
+    const uint8_t *out_tag;      // optional: out[q] = out_tag[q] << 1 | result (FC cache generations)
+    uint32_t qa_bcast;           // 1: every query's a is qa[0] (a row of the FC cache)
     uint32_t *partial;           // partial sum (or NULL)
     const uint32_t *wpad;        // weight per column (0 outside [vlo, vhi) originals)
     uint32_t vlo4, vhi4;         // column range in uint4 units
@@ -452,6 +445,8 @@ hipError_t launch_get_rows(const GetArgs &a, hipStream_t s);
 hipError_t launch_load_rows(const LoadArgs &a, hipStream_t s);
 hipError_t launch_load_raw(const LoadRawArgs &a, hipStream_t s);
 hipError_t launch_load_check(const LoadRawArgs &a, uint32_t n, hipStream_t s);
+hipError_t launch_load_marks_ok(const uint32_t *hb, uint64_t stride, uint32_t n, uint32_t B, const uint32_t *cheat_col,
+                                uint32_t *bad, hipStream_t s);
 hipError_t launch_load_verify_la(const LoadVerifyArgs &a, hipStream_t s);
 hipError_t launch_gather_u32(const uint32_t *src, const uint32_t *idx, uint32_t n, uint32_t *dst, hipStream_t s);
 hipError_t launch_qi_update(const QiArgs &a, const uint32_t *ev, const uint32_t *target, uint32_t n, hipStream_t s);
@@ -461,6 +456,8 @@ hipError_t launch_qi_metric(const QiArgs &a, const uint32_t *ev, uint32_t n, uin
 uint32_t root_fc_splits(uint32_t n_cand, uint32_t n_roots, uint32_t ncols);
 hipError_t launch_root_fc(const RootFcArgs &a, bool forks, hipStream_t s);
 hipError_t launch_root_quorum(const QuorumArgs &a, hipStream_t s);
+hipError_t launch_fc_tile_out(const uint32_t *psum, uint32_t n_split, uint32_t n_cand, uint32_t rp, uint32_t n_roots,
+                              uint32_t quorum, const uint8_t *tag, uint8_t *out, uint64_t pitch, hipStream_t s);
 hipError_t launch_votes(const VoteArgs &a, uint32_t n_voters, bool round1, hipStream_t s);
 hipError_t launch_scatter(const ScatterDesc *desc, uint32_t n, uint64_t max_bytes, const uint8_t *base,
                           hipStream_t s);

@@ -248,55 +248,49 @@ hipError_t launch_batch_finish(const BatchArgs &a, uint32_t jump_rounds, hipStre
 // Roles (NCW compute waves + 1 loader + kND drain waves):
 //  * loader: streams 64-B event records (round-blocked SoA, one 4-KB block per
 //    64 events) into an LDS record ring by LDS-DMA (global_load_lds_dwordx4,
-//    up to 8 rounds in flight) and publishes each round with a tag after its
+//    up to 15 rounds in flight) and publishes each round with a tag after its
 //    own vmcnt wait;
-//  * compute lane g handles events g, g+E, ... (E = 64*NCW).  Each pass it
-//    folds ONE chunk of 4 parents, cycling over the chunks that still have
-//    pending parents (a parent that completes late stalls only its own
-//    chunk), then publishes its CPW seqs into a slot of the LDS event ring.
-//    No global access on the hot path;
+//  * compute waves (block layout): a wave's 16 quads own 16 consecutive
+//    events; lane j of a quad folds the inline parents j, j+4, j+8 from their
+//    LDS ring slots, the quad merges maxima and readiness by DPP and publishes
+//    the event's CPW seqs into its slot.  No global access on the hot path;
 //  * drain waves (rounds of 64 events, round r on wave r % kND): store the HB
 //    row and do the LowestAfter range fill, reading RAW(prev) from the ring.
 // Slots carry their event tag next to the seqs in one 8-B (CPW 1) or 16-B
 // (CPW 2) unit, or two 16-B units in separate arrays (CPW 4: {tag, s0, s1, s2},
-// {tag, s3}); one lane's ds_read/ds_write of such a unit is a single LDS
-// access, so a unit whose tag matches is consistent.  A tag above the
-// expected one means the slot was reused: that parent's HB row is read from
-// L2 once its drain reports it stored (rare: parents older than the ring, or
-// from an earlier batch).  Lanes never block inside a pass, so dependencies
-// between lanes of one wave cannot deadlock; drains wait only for older events
-// and keep publishing their own progress.
-constexpr int kND = 2;               // drain waves (the classic compute layout reads both watermarks as 8 B)
-constexpr int kNDMax = 4;            // drain waves of the quad / block layouts (LX_DRAINS)
+// {tag, s3}; one unit {tag, s0 | s1 << 16, s2 | s3 << 16, 0} when every seq of
+// the epoch fits 16 bits); one lane's ds_read/ds_write of such a unit is a
+// single LDS access, so a unit whose tag matches is consistent.  A tag above
+// the expected one means the slot was reused: that parent's HB row is read
+// from L2 once its drain reports it stored (rare: parents older than the ring,
+// or from an earlier batch).  Lanes never block inside a pass, so
+// dependencies between lanes of one wave cannot deadlock; drains wait only for
+// older events and keep publishing their own progress.
+constexpr int kND = 4;               // drain waves
+constexpr int kRR = 1024;            // record ring (events)
 
-template <int CPW, bool SMALL>
+template <int CPW>
 struct Ring {
-    // slots: 64 KB of units, or 16 KB in the small-LDS variant (several
-    // workgroups per CU when each owns few columns)
-    // (CPW 2 uses one 16-B unit per slot: 2048 slots in 32 KB)
-    static constexpr int BYTES = SMALL ? 16384 : (CPW == 2 ? 32768 : 65536);
+    // slots: 64 KB of units (CPW 2 uses one 16-B unit per slot: 2048 slots in 32 KB)
+    static constexpr int BYTES = CPW == 2 ? 32768 : 65536;
     static constexpr int N = BYTES / (CPW == 1 ? 8 : CPW == 2 ? 16 : 32);
 };
 
 struct alignas(16) WalkShared {
-    uint32_t copied[kNDMax];    // rounds drained (ring and record data consumed) per drain wave
-    uint32_t stored[kNDMax];    // rounds whose global stores are complete per drain wave
+    uint32_t copied[kND];    // rounds drained (ring and record data consumed) per drain wave
+    uint32_t stored[kND];    // rounds whose global stores are complete per drain wave
     uint32_t req;            // a compute lane waits for `stored`: drains flush
     uint32_t p_issued, p_done;   // LX_WALKER_PROF: loader progress (rounds issued / landed)
 };
 
-template <int ND = kND>
 __device__ __forceinline__ bool round_done(const uint32_t *cnt, uint32_t ev) {
     const uint32_t r = ev / 64;
-    return __hip_atomic_load(cnt + (r % ND), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) > r / ND;
+    return __hip_atomic_load(cnt + (r % kND), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) > r / kND;
 }
 
 typedef uint32_t u4v __attribute__((ext_vector_type(4)));
 typedef uint32_t u2v __attribute__((ext_vector_type(2)));
 
-#ifndef LX_PIPE
-#define LX_PIPE 1
-#endif
 // LDS read in inline asm: the compiler orders a plain LDS load after every
 // LDS-DMA (global_load_lds) still in flight (an s_waitcnt vmcnt(0))
 __device__ __forceinline__ uint32_t lds_ld32(uint32_t addr) {
@@ -311,127 +305,6 @@ struct Slot {
     uint32_t t0, t1;       // t1 = second unit's tag (CPW 4), else t0
     uint32_t v[CPW];
 };
-
-// read 4 slots (A = first-unit array, B = second-unit array) and the drains'
-// `copied` watermarks (W, 8 B; the completion check of the same pass uses them),
-// issue all, wait once
-template <int CPW>
-__device__ __forceinline__ void ring_read4w(uint32_t A, uint32_t B, const uint32_t s[4], Slot<CPW> o[4], uint32_t W,
-                                            u2v &wm) {
-    static_assert(kND == 2, "one 8-B read of both drains' watermarks");
-    if (CPW == 1) {
-        u2v x0, x1, x2, x3;
-        asm volatile(
-            "ds_read_b64 %0, %5\n\t"
-            "ds_read_b64 %1, %6\n\t"
-            "ds_read_b64 %2, %7\n\t"
-            "ds_read_b64 %3, %8\n\t"
-            "ds_read_b64 %4, %9\n\t"
-            "s_waitcnt lgkmcnt(0)"
-            : "=&v"(x0), "=&v"(x1), "=&v"(x2), "=&v"(x3), "=&v"(wm)
-            : "v"(A + s[0] * 8u), "v"(A + s[1] * 8u), "v"(A + s[2] * 8u), "v"(A + s[3] * 8u), "v"(W)
-            : "memory");
-        const u2v xs[4] = {x0, x1, x2, x3};
-#pragma unroll
-        for (int j = 0; j < 4; j++) { o[j].t0 = o[j].t1 = xs[j].x; o[j].v[0] = xs[j].y; }
-    } else if (CPW == 2) {
-        u4v x0, x1, x2, x3;
-        asm volatile(
-            "ds_read_b128 %0, %5\n\t"
-            "ds_read_b128 %1, %6\n\t"
-            "ds_read_b128 %2, %7\n\t"
-            "ds_read_b128 %3, %8\n\t"
-            "ds_read_b64 %4, %9\n\t"
-            "s_waitcnt lgkmcnt(0)"
-            : "=&v"(x0), "=&v"(x1), "=&v"(x2), "=&v"(x3), "=&v"(wm)
-            : "v"(A + s[0] * 16u), "v"(A + s[1] * 16u), "v"(A + s[2] * 16u), "v"(A + s[3] * 16u), "v"(W)
-            : "memory");
-        const u4v xs[4] = {x0, x1, x2, x3};
-#pragma unroll
-        for (int j = 0; j < 4; j++) { o[j].t0 = o[j].t1 = xs[j].x; o[j].v[0] = xs[j].y; o[j].v[1 % CPW] = xs[j].z; }
-    } else {
-        u4v x0, x1, x2, x3, y0, y1, y2, y3;
-        asm volatile(
-            "ds_read_b128 %0, %9\n\t"
-            "ds_read_b128 %4, %13\n\t"
-            "ds_read_b128 %1, %10\n\t"
-            "ds_read_b128 %5, %14\n\t"
-            "ds_read_b128 %2, %11\n\t"
-            "ds_read_b128 %6, %15\n\t"
-            "ds_read_b128 %3, %12\n\t"
-            "ds_read_b128 %7, %16\n\t"
-            "ds_read_b64 %8, %17\n\t"
-            "s_waitcnt lgkmcnt(0)"
-            : "=&v"(x0), "=&v"(x1), "=&v"(x2), "=&v"(x3), "=&v"(y0), "=&v"(y1), "=&v"(y2), "=&v"(y3), "=&v"(wm)
-            : "v"(A + s[0] * 16u), "v"(A + s[1] * 16u), "v"(A + s[2] * 16u), "v"(A + s[3] * 16u),
-              "v"(B + s[0] * 16u), "v"(B + s[1] * 16u), "v"(B + s[2] * 16u), "v"(B + s[3] * 16u), "v"(W)
-            : "memory");
-        const u4v xs[4] = {x0, x1, x2, x3};
-        const u4v ys[4] = {y0, y1, y2, y3};
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            o[j].t0 = xs[j].x; o[j].t1 = ys[j].x;
-            o[j].v[0] = xs[j].y; o[j].v[1 % CPW] = xs[j].z; o[j].v[2 % CPW] = xs[j].w; o[j].v[3 % CPW] = ys[j].y;
-        }
-    }
-}
-
-// read 4 slots (A = first-unit array, B = second-unit array), issue all, wait once
-template <int CPW>
-__device__ __forceinline__ void ring_read4(uint32_t A, uint32_t B, const uint32_t s[4], Slot<CPW> o[4]) {
-    if (CPW == 1) {
-        u2v x0, x1, x2, x3;
-        asm volatile(
-            "ds_read_b64 %0, %4\n\t"
-            "ds_read_b64 %1, %5\n\t"
-            "ds_read_b64 %2, %6\n\t"
-            "ds_read_b64 %3, %7\n\t"
-            "s_waitcnt lgkmcnt(0)"
-            : "=&v"(x0), "=&v"(x1), "=&v"(x2), "=&v"(x3)
-            : "v"(A + s[0] * 8u), "v"(A + s[1] * 8u), "v"(A + s[2] * 8u), "v"(A + s[3] * 8u)
-            : "memory");
-        const u2v xs[4] = {x0, x1, x2, x3};
-#pragma unroll
-        for (int j = 0; j < 4; j++) { o[j].t0 = o[j].t1 = xs[j].x; o[j].v[0] = xs[j].y; }
-    } else if (CPW == 2) {
-        u4v x0, x1, x2, x3;
-        asm volatile(
-            "ds_read_b128 %0, %4\n\t"
-            "ds_read_b128 %1, %5\n\t"
-            "ds_read_b128 %2, %6\n\t"
-            "ds_read_b128 %3, %7\n\t"
-            "s_waitcnt lgkmcnt(0)"
-            : "=&v"(x0), "=&v"(x1), "=&v"(x2), "=&v"(x3)
-            : "v"(A + s[0] * 16u), "v"(A + s[1] * 16u), "v"(A + s[2] * 16u), "v"(A + s[3] * 16u)
-            : "memory");
-        const u4v xs[4] = {x0, x1, x2, x3};
-#pragma unroll
-        for (int j = 0; j < 4; j++) { o[j].t0 = o[j].t1 = xs[j].x; o[j].v[0] = xs[j].y; o[j].v[1 % CPW] = xs[j].z; }
-    } else {
-        u4v x0, x1, x2, x3, y0, y1, y2, y3;
-        asm volatile(
-            "ds_read_b128 %0, %8\n\t"
-            "ds_read_b128 %4, %12\n\t"
-            "ds_read_b128 %1, %9\n\t"
-            "ds_read_b128 %5, %13\n\t"
-            "ds_read_b128 %2, %10\n\t"
-            "ds_read_b128 %6, %14\n\t"
-            "ds_read_b128 %3, %11\n\t"
-            "ds_read_b128 %7, %15\n\t"
-            "s_waitcnt lgkmcnt(0)"
-            : "=&v"(x0), "=&v"(x1), "=&v"(x2), "=&v"(x3), "=&v"(y0), "=&v"(y1), "=&v"(y2), "=&v"(y3)
-            : "v"(A + s[0] * 16u), "v"(A + s[1] * 16u), "v"(A + s[2] * 16u), "v"(A + s[3] * 16u),
-              "v"(B + s[0] * 16u), "v"(B + s[1] * 16u), "v"(B + s[2] * 16u), "v"(B + s[3] * 16u)
-            : "memory");
-        const u4v xs[4] = {x0, x1, x2, x3};
-        const u4v ys[4] = {y0, y1, y2, y3};
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            o[j].t0 = xs[j].x; o[j].t1 = ys[j].x;
-            o[j].v[0] = xs[j].y; o[j].v[1 % CPW] = xs[j].z; o[j].v[2 % CPW] = xs[j].w; o[j].v[3 % CPW] = ys[j].y;
-        }
-    }
-}
 
 // one slot (the drains' spin loop and the overflow path): a single access per
 // unit, so a spinning drain adds no redundant LDS traffic beside the compute waves
@@ -479,49 +352,8 @@ __device__ __forceinline__ void ring_read1(uint32_t A, uint32_t B, uint32_t s, S
     }
 }
 
-template <int CPW>
-__device__ __forceinline__ void ring_publish(uint32_t A, uint32_t B, uint32_t s, uint32_t tag, const uint32_t *r) {
-    if (CPW == 1) {
-        u2v x;
-        x.x = tag; x.y = r[0];
-        asm volatile("ds_write_b64 %0, %1" : : "v"(A + s * 8u), "v"(x) : "memory");
-    } else if (CPW == 2) {
-        u4v x;
-        x.x = tag; x.y = r[0]; x.z = r[1 % CPW]; x.w = 0u;
-        asm volatile("ds_write_b128 %0, %1" : : "v"(A + s * 16u), "v"(x) : "memory");
-    } else {
-        u4v x, y;
-        x.x = tag; x.y = r[0]; x.z = r[1 % CPW]; x.w = r[2 % CPW];
-        y.x = tag; y.y = r[3 % CPW]; y.z = 0u; y.w = 0u;
-        asm volatile(
-            "ds_write_b128 %0, %2\n\t"
-            "ds_write_b128 %1, %3"
-            :
-            : "v"(A + s * 16u), "v"(B + s * 16u), "v"(x), "v"(y)
-            : "memory");
-    }
-}
-
 __device__ __forceinline__ uint32_t lds_addr(const void *p) {
     return (uint32_t)(uintptr_t)p;
-}
-
-// The round tag and all four 16-B fields of a record in one LDS round trip:
-// DS instructions of a wave execute in order, so fields read after the tag
-// read are at least as new as the tag says (the loader stores the tag only
-// after its DMA landed); the caller discards them when the tag is not yet set.
-__device__ __forceinline__ void rec_read(uint32_t tag_addr, uint32_t rec_addr, uint32_t &tag, u4v q[4]) {
-    static_assert(LX_REC_Q == 4, "record = 4 fields of 16 B, 1 KB apart");
-    asm volatile(
-        "ds_read_b32 %0, %5\n\t"
-        "ds_read_b128 %1, %6\n\t"
-        "ds_read_b128 %2, %6 offset:1024\n\t"
-        "ds_read_b128 %3, %6 offset:2048\n\t"
-        "ds_read_b128 %4, %6 offset:3072\n\t"
-        "s_waitcnt lgkmcnt(0)"
-        : "=&v"(tag), "=&v"(q[0]), "=&v"(q[1]), "=&v"(q[2]), "=&v"(q[3])
-        : "v"(tag_addr), "v"(rec_addr)
-        : "memory");
 }
 
 // field q of the record in record-ring slot `slot` (round-blocked SoA)
@@ -540,10 +372,7 @@ __device__ __forceinline__ uint32_t rec_off(uint32_t slot, uint32_t q) {
 
 // MASKED: older rows may carry fork marks in bit 31 (B > V); without forks
 // the seq values are used unmasked.
-constexpr uint32_t kNullTag = 0xFFFFFFFFu;   // lean null slot: never an event tag (tags are lp + 1 <= n)
-__device__ __forceinline__ uint32_t wm_pick(const u4v &w, uint32_t i) {
-    return i == 0 ? w.x : i == 1 ? w.y : i == 2 ? w.z : w.w;
-}
+constexpr uint32_t kNullTag = 0xFFFFFFFFu;   // null slot: never an event tag (tags are lp + 1 <= n)
 // any of a lane's three parents (expected tag = local index + 1, or kNullTag)
 // at least `reach` events before event lp
 __device__ __forceinline__ bool far_parent(const uint32_t px[3], uint32_t lp, uint32_t reach) {
@@ -657,35 +486,29 @@ __device__ __forceinline__ void blk_fold(const uint32_t pa[3], uint32_t W, uint3
     }
 }
 
-// LEAN (CPW 4 only): the compute waves give each event a quad of lanes; lane j
-// of the quad folds the inline parents j, j+4, j+8 into all four columns
-// (straight-line, one LDS round trip for all of them), the quad merges its
-// partial maxima and its readiness by DPP, and lane 0 publishes.  A pass costs
-// a fraction of the one-lane-per-event pass (no chunk scheduling, ~1/4 of the
-// instructions), and the walk is bound by pass latency x DAG depth.
-template <int CPW, int NCW, int RR, bool FILL, bool SMALL, bool MASKED, int LEAN = 0, int ND = kND, bool PK = false>
-__global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
-    static_assert(!PK || (CPW == 4 && LEAN == 2), "packed slots: block walker on 4-column slices");
-    static_assert(ND == kND || (LEAN && ND <= kNDMax), "drain waves: 2, or up to 4 with the quad / block layouts");
+// The walker kernel.  MASKED: older rows may carry fork marks in bit 31
+// (B > V); PK: 4-column slices with 16-bit packed slot units (every seq of the
+// epoch <= 0xFFFF).
+template <int CPW, int NCW, bool MASKED, bool PK>
+__global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
+    static_assert(!PK || CPW == 4, "packed slots: 4-column slices");
     static_assert(CPW == 1 || CPW == 2 || CPW == 4, "slot layout");
-    static_assert(!LEAN || LX_MAXP == 12, "quad / block walkers: 12 inline parents, three per lane of a quad");
-    static_assert(LEAN != 1 || CPW == 4, "quad walker: 4-column slices (the block walker takes 1, 2 or 4)");
+    static_assert(LX_MAXP == 12, "block walker: 12 inline parents, three per lane of a quad");
+    constexpr int ND = kND;
+    constexpr int RR = kRR;
     constexpr int NT = 64 * (NCW + 1 + ND);
-    constexpr int E = 64 * NCW;
     constexpr int RQ = LX_REC_Q;
-    constexpr int KB = (SMALL ? 512 : 1024) / CPW;   // recent (seq -> event) entries per owned branch
-    constexpr int RN = Ring<CPW, SMALL>::N;
-    constexpr int RB16 = Ring<CPW, SMALL>::BYTES / 16;
-    // (the lean layout checks slot reuse explicitly at completion, any quad)
-    static_assert(LEAN || (RN % E == 0 && RN / E >= 4), "ring slot reuse must stay within one lane");
-    static_assert(RR % 64 == 0 && RR / 64 >= 4 && RR >= 2 * (LEAN ? 16 * NCW : E), "record ring");
-    // slot units (A array, then B array for CPW 4); the lean layout keeps a
-    // null slot after each array (tag kNullTag, values 0)
-    __shared__ uint4 ring[RB16 + (LEAN ? 2 : 0)];
+    constexpr int KB = 1024 / CPW;               // recent (seq -> event) entries per owned branch
+    constexpr int RN = Ring<CPW>::N;
+    constexpr int RB16 = Ring<CPW>::BYTES / 16;
+    static_assert(RR % 64 == 0 && RR / 64 >= 4 && RR >= 2 * 16 * NCW, "record ring");
+    // slot units (A array, then B array for CPW 4), each followed by a null
+    // slot (tag kNullTag, values 0) that absent parents point at
+    __shared__ uint4 ring[RB16 + 2];
     __shared__ uint4 rrec[RR * RQ];              // event records
     __shared__ uint32_t rtag[RR / 64];           // per record round: batch round index + 1
     __shared__ uint2 brc[CPW * KB];              // {seq, event} of recent events of owned branches
-    __shared__ uint4 dummy[LEAN == 2 ? 128 : 1];  // block walker: per-lane targets of suppressed writes
+    __shared__ uint4 dummy[128];                 // per-lane targets of suppressed writes
     __shared__ WalkShared sh;
 
     const uint32_t w = blockIdx.x;
@@ -695,11 +518,11 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
     // null slot: unit A right after the A array (uint4 index RN, or RN / 2 for
     // 8-B units), unit B (CPW 4) after the B array
     constexpr int kNullA = CPW == 1 ? RN / 2 : RN;
-    for (int i = threadIdx.x; i < RB16 + (LEAN ? 2 : 0); i += NT)
-        ring[i] = make_uint4(LEAN && (i == kNullA || (CPW == 4 && i == 2 * RN + 1)) ? kNullTag : 0u, 0, 0, 0);
+    for (int i = threadIdx.x; i < RB16 + 2; i += NT)
+        ring[i] = make_uint4((i == kNullA || (CPW == 4 && i == 2 * RN + 1)) ? kNullTag : 0u, 0, 0, 0);
     for (int i = threadIdx.x; i < RR / 64; i += NT) rtag[i] = 0;
     for (int i = threadIdx.x; i < CPW * KB; i += NT) brc[i] = make_uint2(0, LX_NONE);
-    if (threadIdx.x < kNDMax) { sh.copied[threadIdx.x] = 0; sh.stored[threadIdx.x] = 0; }
+    if (threadIdx.x < kND) { sh.copied[threadIdx.x] = 0; sh.stored[threadIdx.x] = 0; }
     if (threadIdx.x == 0) { sh.req = 0; sh.p_issued = 0; sh.p_done = 0; }
     __syncthreads();
 
@@ -710,7 +533,7 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
     const uint64_t stride = a.stride;
     constexpr uint32_t mask = MASKED ? LX_SEQ_MASK : 0xFFFFFFFFu;
     const uint32_t RA = lds_addr(ring);
-    const uint32_t RB = RA + (uint32_t)((RN + (LEAN ? 1 : 0)) * 16);   // second units (CPW 4 only)
+    const uint32_t RB = RA + (uint32_t)((RN + 1) * 16);   // second units (CPW 4 only)
 
     // col = global branch (semantics), pc = plane column (addressing; differs
     // from col only in a column-sharded handle, which stores its own columns)
@@ -733,7 +556,7 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
         const uint32_t nrounds = (n + 63) / 64;
         // rounds in flight: the DMA round trip is long while the CU's memory
         // queue also carries the drains' stores (the block walker starved at 8)
-        constexpr uint32_t D = LEAN ? (RR / 64 - 1 < 15 ? RR / 64 - 1 : 15) : (RR / 64 < 8 ? RR / 64 : 8);
+        constexpr uint32_t D = RR / 64 - 1 < 15 ? RR / 64 - 1 : 15;
         uint32_t issued = 0, done = 0;
 #ifdef LX_WALKER_PROF
         uint32_t l_iter = 0, l_slot = 0, l_sleep = 0;
@@ -747,12 +570,8 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
             // previous occupants (events ev - RR: same round offset)
             bool free = issued * 64 < (uint32_t)RR;
             if (!free && issued < nrounds && issued - done < D) {
-                if (LX_PIPE) {
-                    const uint32_t r = (issued * 64 - RR) / 64;
-                    free = __builtin_amdgcn_readfirstlane(lds_ld32(lds_addr(&sh.copied[r % ND]))) > r / ND;
-                } else {
-                    free = round_done<ND>(sh.copied, issued * 64 - RR);
-                }
+                const uint32_t r = (issued * 64 - RR) / 64;
+                free = __builtin_amdgcn_readfirstlane(lds_ld32(lds_addr(&sh.copied[r % ND]))) > r / ND;
             }
             LX_WP(if (issued < nrounds && issued - done < D && !free) l_slot++;)
             if (issued < nrounds && issued - done < D && free) {
@@ -787,15 +606,13 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
                     case 13: asm volatile("s_waitcnt vmcnt(52)" ::: "memory"); break;
                     default: asm volatile("s_waitcnt vmcnt(56)" ::: "memory"); break;
                 }
-                if (LX_PIPE)   // (the vmcnt wait above landed the round; a release store waits for all)
-                    asm volatile("ds_write_b32 %0, %1" : : "v"(lds_addr(&rtag[done % (RR / 64)])), "v"(done + 1) : "memory");
-                else if (lane == 0)
-                    __hip_atomic_store(&rtag[done % (RR / 64)], done + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                // (the vmcnt wait above landed the round; a release store would wait for all)
+                asm volatile("ds_write_b32 %0, %1" : : "v"(lds_addr(&rtag[done % (RR / 64)])), "v"(done + 1) : "memory");
                 done++;
                 LX_WP(asm volatile("ds_write_b32 %0, %1" : : "v"(lds_addr(&sh.p_done)), "v"(done) : "memory");)
             } else if (!progressed) {
                 LX_WP(l_sleep++;)
-                if (a.diag & 32) __builtin_amdgcn_s_sleep(4); else __builtin_amdgcn_s_sleep(1);
+                __builtin_amdgcn_s_sleep(1);
             }
         }
 #ifdef LX_WALKER_PROF
@@ -839,7 +656,7 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     if (lane == 0) __hip_atomic_store(&sh.stored[d], nd, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
-                if (a.diag & 32) __builtin_amdgcn_s_sleep(4); else __builtin_amdgcn_s_sleep(1);
+                __builtin_amdgcn_s_sleep(1);
             }
 #ifdef LX_WALKER_PROF
             const unsigned long long tb0 = wall_clock64();
@@ -868,7 +685,7 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
                                 // the other drain may in turn wait for this one: keep
                                 // publishing our completed rounds (divergent: every active lane)
                                 __hip_atomic_store(&sh.stored[d], nd, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                                while (!round_done<ND>(sh.stored, pl)) {
+                                while (!round_done(sh.stored, pl)) {
                                     __hip_atomic_store(&sh.req, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                                     __builtin_amdgcn_s_sleep(1);
                                 }
@@ -899,7 +716,7 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
                     for (int k = 0; k < CPW; k++)
                         if (valid[k]) hrow[pc[k]] = r[k];
                 }
-                if (FILL) {
+                {
                     // LowestAfter range fill: events (col, s), s in (h0, r], are first
                     // observed from branch `br` by this event.
                     uint32_t lo[CPW], hi[CPW];
@@ -967,205 +784,7 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
         return;
     }
 
-    if constexpr (LEAN == 1) {
-        // ------------------------------------------------------------ compute (lean)
-        // Per lane: its three parents as (expected tag, LDS address of the
-        // slot's unit A; unit B is LEAN_BOFF further).  An absent (or already
-        // folded) parent points at the null slot, whose tag kNullTag matches
-        // and whose values are 0, so the fold needs no presence masks.  The
-        // loop body has no `continue`: flat if/else regions keep the exec-mask
-        // bookkeeping per pass small.
-        constexpr uint32_t GE = 16 * NCW;            // events in flight: one per quad
-        constexpr uint32_t kLeanStuck = 64;          // passes before a waiting event checks for reused slots
-        constexpr uint32_t kLeanFar = 512;           // parents this close to the ring's reach: checked at once
-        constexpr uint32_t LEAN_BOFF = (RN + 1) * 16;   // unit B of a slot, from its unit A (= RB - RA)
-        static_assert(LEAN_BOFF < 65536, "ds offset field");
-        const uint32_t ANULL = RA + (uint32_t)(RN * 16);
-        const uint32_t j = lane & 3;
-        const uint32_t mycol = col[j & (CPW - 1)];
-        const bool myvalid = valid[j & (CPW - 1)];
-        uint32_t lp = wave * 16 + (lane >> 2);
-        bool have = false;
-        uint32_t br = 0, seq = 0, np = 0, xi = 0, stuck = 0;
-        uint32_t px[3] = {kNullTag, kNullTag, kNullTag};
-        uint32_t pa[3] = {ANULL, ANULL, ANULL};
-        uint32_t r[CPW];
-#pragma unroll
-        for (int k = 0; k < CPW; k++) r[k] = 0;
-        uint32_t drained = 0;
-        u4v cwm = {0u, 0u, 0u, 0u};   // all drains' `copied` watermarks (16 B)
-#ifdef LX_WALKER_PROF
-        uint32_t c_pass = 0, c_done = 0, c_slow = 0, c_wm = 0, c_norec = 0;
-        const unsigned long long t_start = wall_clock64();
-#endif
-        while (lp < n) {
-            LX_WP(c_pass++;)
-            if (!have) {
-                // record: tag, field 0 {branch, seq, #parents, prev}, and this
-                // lane's three inline parents (field 1+k, component j)
-                const uint32_t slot = lp % RR;
-                const uint32_t ra = lds_addr(rrec) + rec_off(slot, 0) * 16u;
-                uint32_t tg, w0, w1, w2;
-                u4v q0;
-                asm volatile(
-                    "ds_read_b32 %0, %5\n\t"
-                    "ds_read_b128 %1, %6\n\t"
-                    "ds_read_b32 %2, %7 offset:1024\n\t"
-                    "ds_read_b32 %3, %7 offset:2048\n\t"
-                    "ds_read_b32 %4, %7 offset:3072\n\t"
-                    "s_waitcnt lgkmcnt(0)"
-                    : "=&v"(tg), "=&v"(q0), "=&v"(w0), "=&v"(w1), "=&v"(w2)
-                    : "v"(lds_addr(&rtag[slot / 64])), "v"(ra), "v"(ra + j * 4u)
-                    : "memory");
-                if (tg == lp / 64 + 1) {
-                    br = q0.x; seq = q0.y; np = q0.z;
-                    const uint32_t w[3] = {w0, w1, w2};
-#pragma unroll
-                    for (int k = 0; k < 3; k++) {
-                        const uint32_t pl = w[k] - bs;
-                        const bool in = j + 4 * k < np;
-                        px[k] = in ? pl + 1u : kNullTag;
-                        pa[k] = in ? RA + (pl % RN) * 16u : ANULL;
-                    }
-#pragma unroll
-                    for (int k = 0; k < CPW; k++) r[k] = (col[k] == br) ? seq : 0u;
-                    // parents from earlier batches (sorted oldest first: parent j
-                    // is this lane's oldest): their rows are final, fold them now
-                    if (j < np && w0 - bs >= n) {
-#pragma unroll
-                        for (int k = 0; k < 3; k++) {
-                            if (j + 4 * k >= np || w[k] - bs < n) continue;
-                            LX_WP(c_slow++;)
-                            const uint32_t *row = a.hb + (uint64_t)w[k] * stride;
-#pragma unroll
-                            for (int c = 0; c < CPW; c++)
-                                if (valid[c]) r[c] = max(r[c], ld_l2_now(row + pc[c]) & mask);
-                            px[k] = kNullTag;
-                            pa[k] = ANULL;
-                        }
-                    }
-                    xi = LX_MAXP;
-                    // a parent far enough back that its slot may already hold a newer event
-                    // is checked against the L2 path from the first pass on
-                    stuck = far_parent(px, lp, (uint32_t)RN - kLeanFar) ? kLeanStuck : 0u;
-                    have = true;
-                } else {
-                    LX_WP(c_norec++;)
-                }
-            }
-            // fold this lane's parents: both slot units of each, plus the
-            // drains' watermarks, in one round trip (lanes without an event read
-            // the null slot)
-            u4v xa0, xb0, xa1, xb1, xa2, xb2;
-            asm volatile(
-                "ds_read_b128 %0, %7\n\t"
-                "ds_read_b128 %1, %7 offset:%10\n\t"
-                "ds_read_b128 %2, %8\n\t"
-                "ds_read_b128 %3, %8 offset:%10\n\t"
-                "ds_read_b128 %4, %9\n\t"
-                "ds_read_b128 %5, %9 offset:%10\n\t"
-                "ds_read_b128 %6, %11\n\t"
-                "s_waitcnt lgkmcnt(0)"
-                : "=&v"(xa0), "=&v"(xb0), "=&v"(xa1), "=&v"(xb1), "=&v"(xa2), "=&v"(xb2), "=&v"(cwm)
-                : "v"(pa[0]), "v"(pa[1]), "v"(pa[2]), "i"(LEAN_BOFF), "v"(lds_addr(&sh.copied[0]))
-                : "memory");
-            const u4v xa[3] = {xa0, xa1, xa2};
-            const u4v xb[3] = {xb0, xb1, xb2};
-            bool all = true;
-#pragma unroll
-            for (int k = 0; k < 3; k++) {
-                const bool ok = (xa[k].x == px[k]) & (xb[k].x == px[k]);
-                const uint32_t v[4] = {xa[k].y, xa[k].z, xa[k].w, xb[k].y};
-#pragma unroll
-                for (int c = 0; c < CPW; c++) r[c] = max(r[c], ok ? v[c] : 0u);
-                all &= ok;
-            }
-#pragma unroll
-            for (int c = 0; c < CPW; c++) r[c] = quad_max(r[c]);
-            const bool rdy = have && quad_and(all ? 1u : 0u);
-            if (!rdy) {
-                if (have && ++stuck >= kLeanStuck) {
-                    // waiting long: a parent's slot may have been reused by a
-                    // newer event; its HB row from L2 once its drain stored it
-#pragma unroll
-                    for (int k = 0; k < 3; k++) {
-                        const uint32_t x = px[k];
-                        if (x == kNullTag || (xa[k].x == x && xb[k].x == x) || max(xa[k].x, xb[k].x) <= x) continue;
-                        if (!round_done<ND>(sh.stored, x - 1u)) {
-                            LX_WP(c_wm++;)
-                            __hip_atomic_store(&sh.req, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                            continue;
-                        }
-                        LX_WP(c_slow++;)
-                        const uint32_t *row = a.hb + (uint64_t)(x - 1u + bs) * stride;
-#pragma unroll
-                        for (int c = 0; c < CPW; c++)
-                            if (valid[c]) r[c] = max(r[c], ld_l2_now(row + pc[c]) & mask);
-                        px[k] = kNullTag;
-                        pa[k] = ANULL;
-                    }
-                }
-            } else if (xi < np) {
-                // parents beyond the inline twelve (rare): one per pass, the same on every lane of the quad
-                const uint32_t pg = ld_l2_now(a.par_in + a.poff_in[lp] + xi);
-                const uint32_t lpp = pg - bs;
-                bool ok = false, old = lpp >= n;
-                if (!old) {
-                    Slot<CPW> ps;
-                    ring_read1<CPW, PK>(RA, RB, lpp % RN, ps);
-                    if (ps.t0 == lpp + 1 && ps.t1 == lpp + 1) {
-#pragma unroll
-                        for (int c = 0; c < CPW; c++) r[c] = max(r[c], ps.v[c]);
-                        ok = true;
-                    } else if (max(ps.t0, ps.t1) > lpp + 1) {
-                        if (round_done<ND>(sh.stored, lpp)) old = true;
-                        else __hip_atomic_store(&sh.req, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    }
-                }
-                if (old) {
-                    const uint32_t *row = a.hb + (uint64_t)pg * stride;
-#pragma unroll
-                    for (int c = 0; c < CPW; c++)
-                        if (valid[c]) r[c] = max(r[c], ld_l2_now(row + pc[c]) & mask);
-                    ok = true;
-                }
-                if (quad_and(ok ? 1u : 0u)) xi++;
-            } else {
-                // complete once the slot's previous occupant (lp - RN) is drained
-                bool free = true;
-                if (lp >= (uint32_t)RN && lp - RN >= drained) {
-                    const uint32_t rr = (lp - RN) / 64;
-                    const uint32_t cw = wm_pick(cwm, rr % ND);
-                    free = cw > rr / ND || round_done<ND>(sh.copied, lp - RN);
-                    if (free) drained = ((lp - RN) | 63u) + 1;
-                    LX_WP(if (!free) c_wm++;)
-                }
-                if (free) {
-                    const uint32_t e = bs + lp;
-                    if (myvalid && mycol == br)
-                        __hip_atomic_store(reinterpret_cast<uint64_t *>(brc + (j & (CPW - 1)) * KB + seq % KB),
-                                           ((uint64_t)e << 32) | seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    if (j == 0) ring_publish<CPW>(RA, RB, lp % RN, lp + 1, r);
-                    lp += GE;
-                    have = false;
-#pragma unroll
-                    for (int k = 0; k < 3; k++) { px[k] = kNullTag; pa[k] = ANULL; }
-                    LX_WP(c_done++;)
-                }
-            }
-        }
-#ifdef LX_WALKER_PROF
-        if (a.prof) {
-            unsigned long long *pw = a.prof + ((uint64_t)blockIdx.x * kProfWaves + wave) * kProfSlots;
-            const uint32_t cs[8] = {c_pass, 0u, 0u, c_done, c_slow, 0u, c_wm, c_norec};
-#pragma unroll
-            for (int i = 0; i < 8; i++) atomicAdd(pw + i, (unsigned long long)cs[i]);
-            atomicMax(pw + 8, (unsigned long long)c_pass);
-            if (lane == 0) atomicMax(pw + 9, wall_clock64() - t_start);
-        }
-#endif
-        return;
-    } else if constexpr (LEAN == 2) {
+    {
         // ------------------------------------------------------------ compute (block)
         // As the quad layout, but a wave's 16 quads own 16 consecutive events
         // (a block) and the wave moves to its next block (+NCW blocks) only
@@ -1182,7 +801,6 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
         const uint32_t mycol = col[j & (CPW - 1)];
         const bool myvalid = j < (uint32_t)CPW && valid[j & (CPW - 1)];
         uint32_t blk = __builtin_amdgcn_readfirstlane(wave);   // wave-uniform: scalar loop control
-        if (a.diag & 16) __builtin_amdgcn_s_setprio(2);   // diagnostic: compute waves first
         bool loaded = false, done = true;
         uint32_t br = 0, seq = 0, np = 0, xi = 0;
         uint32_t wstuck = 0;   // passes since the block fetch (wave-uniform)
@@ -1333,7 +951,7 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
                         for (int c = 0; c < CPW; c++) r[c] = max(r[c], ps.v[c]);
                         ok = true;
                     } else if (max(ps.t0, ps.t1) > lpp + 1) {
-                        if (round_done<ND>(sh.stored, lpp)) old = true;
+                        if (round_done(sh.stored, lpp)) old = true;
                         else __hip_atomic_store(&sh.req, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     }
                 }
@@ -1392,7 +1010,7 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
                 for (int k = 0; k < 3; k++) {
                     const uint32_t x = px[k];
                     if (x == kNullTag || (tg[k][0] == x && tg[k][1] == x) || max(tg[k][0], tg[k][1]) <= x) continue;
-                    if (!round_done<ND>(sh.stored, x - 1u)) {
+                    if (!round_done(sh.stored, x - 1u)) {
                         LX_WP(c_wm++;)
                         __hip_atomic_store(&sh.req, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                         continue;
@@ -1428,258 +1046,40 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
         }
 #endif
         return;
-    } else {
-    // ---------------------------------------------------------------- compute
-#ifdef LX_WALKER_PROF
-    uint32_t c_pass = 0, c_chunk = 0, c_done = 0, c_slow = 0, c_wm = 0, c_norec = 0;
-    const unsigned long long t_start = wall_clock64();
-#endif
-
-    uint32_t lp = threadIdx.x;
-    bool have = false;
-    uint32_t br = 0, seq = 0, np = 0, xi = 0;
-    uint32_t par[LX_MAXP];
-    uint32_t todo = 0;   // pending parents (bit j = par[j])
-    uint32_t cc = 0;     // chunk folded next
-    uint32_t r[CPW];
-    uint32_t drained = 0;   // events < drained are known drained (slot reuse)
-    u2v cwm = {0u, 0u};     // drains' `copied` watermarks as of the last fold
-
-    while (lp < n) {
-        LX_WP(c_pass++;)
-        if (!have) {
-            const uint32_t slot = lp % RR;
-            uint32_t tg;
-            u4v rq[LX_REC_Q];
-            rec_read(lds_addr(&rtag[slot / 64]), lds_addr(rrec) + rec_off(slot, 0) * 16u, tg, rq);
-            if (tg != lp / 64 + 1) { LX_WP(c_norec++;) continue; }
-            br = rq[0].x; seq = rq[0].y; np = rq[0].z;
-#pragma unroll
-            for (int j = 0; j < LX_MAXP / 4; j++) {
-                const u4v q = rq[1 + j];
-                par[4 * j] = q.x - bs; par[4 * j + 1] = q.y - bs; par[4 * j + 2] = q.z - bs; par[4 * j + 3] = q.w - bs;
-            }
-            todo = (np >= LX_MAXP) ? ((1u << LX_MAXP) - 1u) : ((1u << np) - 1u);
-            cc = 0;
-            xi = LX_MAXP;
-#pragma unroll
-            for (int k = 0; k < CPW; k++) r[k] = (col[k] == br) ? seq : 0u;
-            have = true;
-        }
-        if (todo) {
-            // fold chunk cc (parents 4cc..4cc+3)
-            LX_WP(c_chunk++;)
-            uint32_t p4[4], sl4[4];
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                uint32_t x = par[j];
-#pragma unroll
-                for (int c = 1; c < LX_MAXP / 4; c++) x = (cc == (uint32_t)c) ? par[4 * c + j] : x;
-                p4[j] = x;
-                sl4[j] = x % RN;
-            }
-            const uint32_t tc = (todo >> (4 * cc)) & 15u;
-            Slot<CPW> o[4];
-            ring_read4w<CPW>(RA, RB, sl4, o, lds_addr(&sh.copied[0]), cwm);
-            // branch-free common case: fold the parents whose slot is valid
-            uint32_t okm = 0, oldm = 0;
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const uint32_t x = p4[j] + 1u;
-                const uint32_t pend = (tc >> j) & 1u;
-                const uint32_t inb = (uint32_t)(p4[j] < n);
-                const uint32_t ok = pend & inb & (uint32_t)(o[j].t0 == x) & (uint32_t)(o[j].t1 == x);
-                const uint32_t newer = (uint32_t)(max(o[j].t0, o[j].t1) > x);
-                const uint32_t old = pend & ((inb ^ 1u) | newer);
-#pragma unroll
-                for (int k = 0; k < CPW; k++) r[k] = max(r[k], ok ? (o[j].v[k] & mask) : 0u);
-                okm |= ok << j;
-                oldm |= old << j;
-            }
-            uint32_t tn = tc & ~okm;
-            if (oldm) {
-                // older than the ring or an earlier batch: HB row from L2 once stored
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    if (!((oldm >> j) & 1u)) continue;
-                    const uint32_t lpp = p4[j];
-                    if (lpp < n && !round_done<ND>(sh.stored, lpp)) {
-                        LX_WP(c_wm++;)
-                        __hip_atomic_store(&sh.req, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    } else {
-                        LX_WP(c_slow++;)
-                        const uint32_t *row = a.hb + (uint64_t)(lpp + bs) * stride;
-#pragma unroll
-                        for (int k = 0; k < CPW; k++)
-                            if (valid[k]) r[k] = max(r[k], ld_l2_now(row + pc[k]) & mask);
-                        tn &= ~(1u << j);
-                    }
-                }
-            }
-            todo = (todo & ~(15u << (4 * cc))) | (tn << (4 * cc));
-            // next chunk: cyclically after cc, among the chunks still pending
-            constexpr uint32_t NCH = LX_MAXP / 4;
-            uint32_t pm = 0;
-#pragma unroll
-            for (int c = 0; c < (int)NCH; c++) pm |= (uint32_t)(((todo >> (4 * c)) & 15u) != 0) << c;
-            const uint32_t rot = ((pm | (pm << NCH)) >> (cc + 1)) & ((1u << NCH) - 1u);
-            cc = rot ? (cc + 1 + (uint32_t)__builtin_ctz(rot)) % NCH : cc;
-            if (todo) continue;
-        }
-        if (xi < np) {
-            // parents beyond the inline LX_MAXP (rare): one per pass, from the ring or L2
-            const uint32_t p = ld_l2_now(a.par_in + a.poff_in[lp] + xi);
-            const uint32_t lpp = p - bs;
-            bool ok = false, old = lpp >= n;
-            if (!old) {
-                Slot<CPW> ps;
-                ring_read1<CPW, PK>(RA, RB, lpp % RN, ps);
-                if (ps.t0 == lpp + 1 && ps.t1 == lpp + 1) {
-#pragma unroll
-                    for (int k = 0; k < CPW; k++) r[k] = max(r[k], ps.v[k] & mask);
-                    ok = true;
-                } else if (max(ps.t0, ps.t1) > lpp + 1) {
-                    if (round_done<ND>(sh.stored, lpp)) old = true;
-                    else __hip_atomic_store(&sh.req, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                }
-            }
-            if (old) {
-                const uint32_t *row = a.hb + (uint64_t)p * stride;
-#pragma unroll
-                for (int k = 0; k < CPW; k++)
-                    if (valid[k]) r[k] = max(r[k], ld_l2_now(row + pc[k]) & mask);
-                ok = true;
-            }
-            if (ok) xi++;
-            continue;
-        }
-        {
-            // complete: the slot's previous occupant (lp - RN) must be drained
-            if (lp >= (uint32_t)RN && lp - RN >= drained) {
-                // watermarks only grow: the copy read with this pass's fold (or an
-                // older one) answering "drained" is final; otherwise ask LDS now
-                const uint32_t rr = (lp - RN) / 64;
-                const uint32_t cw = (rr % kND) ? cwm.y : cwm.x;
-                if (cw <= rr / kND && !round_done<ND>(sh.copied, lp - RN)) { LX_WP(c_wm++;) continue; }
-                drained = ((lp - RN) | 63u) + 1;   // its whole round
-            }
-            const uint32_t e = bs + lp;
-#pragma unroll
-            for (int k = 0; k < CPW; k++)
-                if (valid[k] && col[k] == br)
-                    __hip_atomic_store(reinterpret_cast<uint64_t *>(brc + k * KB + seq % KB),
-                                       ((uint64_t)e << 32) | seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            ring_publish<CPW>(RA, RB, lp % RN, lp + 1, r);
-            lp += E;
-            have = false;
-            LX_WP(c_done++;)
-        }
-    }
-#ifdef LX_WALKER_PROF
-    if (a.prof) {
-        unsigned long long *pw = a.prof + ((uint64_t)blockIdx.x * kProfWaves + wave) * kProfSlots;
-        const uint32_t cs[8] = {c_pass, 0u, c_chunk, c_done, c_slow, 0u, c_wm, c_norec};
-#pragma unroll
-        for (int i = 0; i < 8; i++) atomicAdd(pw + i, (unsigned long long)cs[i]);
-        atomicMax(pw + 8, (unsigned long long)c_pass);               // wave passes = max over lanes
-        if (lane == 0) atomicMax(pw + 9, wall_clock64() - t_start);  // wall ticks (100 MHz)
-    }
-#endif
     }
 }
 
-template <int CPW, int NCW, int RR, bool SMALL, int LEAN = 0, int ND = kND>
+template <int CPW, int NCW>
 static hipError_t launch_index_t(const IndexArgs &a0, hipStream_t s) {
     IndexArgs a = a0;
     a.n_slices = (a.ncols + CPW - 1) / CPW;
     a.slices_per_xcd = (a.n_slices + 7) / 8;
-    uint32_t grid = a.slices_per_xcd * 8;
-    const dim3 blk(64 * (NCW + 1 + ND));
-    if constexpr (CPW == 4 && LEAN == 2) {
+    const uint32_t grid = a.slices_per_xcd * 8;
+    const dim3 blk(64 * (NCW + 1 + kND));
+    if constexpr (CPW == 4) {
         if (a.pack16) {   // every seq of the epoch fits 16 bits: one 16-B slot unit
-            if (a.diag_nofill) hipLaunchKernelGGL((k_index<CPW, NCW, RR, false, SMALL, true, LEAN, ND, true>), dim3(grid), blk, 0, s, a);
-            else if (a.mask) hipLaunchKernelGGL((k_index<CPW, NCW, RR, true, SMALL, true, LEAN, ND, true>), dim3(grid), blk, 0, s, a);
-            else hipLaunchKernelGGL((k_index<CPW, NCW, RR, true, SMALL, false, LEAN, ND, true>), dim3(grid), blk, 0, s, a);
+            if (a.mask) hipLaunchKernelGGL((k_index<CPW, NCW, true, true>), dim3(grid), blk, 0, s, a);
+            else hipLaunchKernelGGL((k_index<CPW, NCW, false, true>), dim3(grid), blk, 0, s, a);
             return hipGetLastError();
         }
     }
-    if (a.diag_nofill) hipLaunchKernelGGL((k_index<CPW, NCW, RR, false, SMALL, true, LEAN, ND>), dim3(grid), blk, 0, s, a);
-    else if (a.mask) hipLaunchKernelGGL((k_index<CPW, NCW, RR, true, SMALL, true, LEAN, ND>), dim3(grid), blk, 0, s, a);
-    else hipLaunchKernelGGL((k_index<CPW, NCW, RR, true, SMALL, false, LEAN, ND>), dim3(grid), blk, 0, s, a);
+    if (a.mask) hipLaunchKernelGGL((k_index<CPW, NCW, true, false>), dim3(grid), blk, 0, s, a);
+    else hipLaunchKernelGGL((k_index<CPW, NCW, false, false>), dim3(grid), blk, 0, s, a);
     return hipGetLastError();
-}
-
-template <int CPW>
-static hipError_t launch_index_c(const IndexArgs &a, uint32_t ncw, hipStream_t s) {
-    if constexpr (CPW <= 2) {
-        if (a.lean == 2) {
-            // block walker on 1- / 2-column slices (few columns: small V, or a column shard)
-            if constexpr (CPW == 2) {
-                // 512-record ring (~74 KB of LDS): two workgroups per CU
-                if (a.rr_hint == 512) {
-                    if (a.drains != 2) return launch_index_t<CPW, 8, 512, false, 2, 4>(a, s);
-                    return launch_index_t<CPW, 8, 512, false, 2>(a, s);
-                }
-            }
-            // (lean_ncw 0 = auto: 8 compute waves; 11 slowed C2 by 7 %)
-            if (a.drains != 2) {
-                if (a.lean_ncw <= 8) return launch_index_t<CPW, 8, 1024, false, 2, 4>(a, s);
-                return launch_index_t<CPW, 11, 1024, false, 2, 4>(a, s);
-            }
-            return launch_index_t<CPW, 8, 1024, false, 2>(a, s);
-        }
-        if (a.small) {
-            // small-LDS variant (~37 KB): several workgroups share a CU
-            if (ncw <= 1) return launch_index_t<CPW, 1, 256, true>(a, s);
-            return launch_index_t<CPW, 2, 256, true>(a, s);
-        }
-    }
-    if constexpr (CPW == 2) {
-        // 512-record ring: ~72 KB of LDS, two workgroups per CU
-        if (a.rr_hint == 512) {
-            if (ncw <= 1) return launch_index_t<CPW, 1, 512, false>(a, s);
-            if (ncw <= 2) return launch_index_t<CPW, 2, 512, false>(a, s);
-            return launch_index_t<CPW, 4, 512, false>(a, s);
-        }
-    }
-    if constexpr (CPW == 4) {
-        if (a.lean == 1) {
-            // quads: 16 events in flight per compute wave (lean_ncw 0 = 8)
-            if (a.lean_ncw && a.lean_ncw <= 4) return launch_index_t<CPW, 4, 1024, false, 1>(a, s);
-            if (a.lean_ncw <= 8) return launch_index_t<CPW, 8, 1024, false, 1>(a, s);
-            return launch_index_t<CPW, 12, 1024, false, 1>(a, s);
-        }
-        if (a.lean == 2) {
-            // lean_ncw 0 = auto: 11 compute waves with 4 drains (16 waves, the
-            // workgroup limit): C3 walk -1.8 % against 8 once the loader kept
-            // its record DMAs in flight
-            if (a.drains != 2) {
-                if (a.lean_ncw && a.lean_ncw <= 8) return launch_index_t<CPW, 8, 1024, false, 2, 4>(a, s);
-                return launch_index_t<CPW, 11, 1024, false, 2, 4>(a, s);
-            }
-            if (a.lean_ncw && a.lean_ncw <= 4) return launch_index_t<CPW, 4, 1024, false, 2>(a, s);
-            if (!a.lean_ncw || a.lean_ncw <= 8) return launch_index_t<CPW, 8, 1024, false, 2>(a, s);
-            return launch_index_t<CPW, 12, 1024, false, 2>(a, s);
-        }
-    }
-    if (ncw <= 1) return launch_index_t<CPW, 1, 1024, false>(a, s);
-    if (ncw <= 2) return launch_index_t<CPW, 2, 1024, false>(a, s);
-    return launch_index_t<CPW, 4, 1024, false>(a, s);
 }
 
 hipError_t launch_index(const IndexArgs &a, hipStream_t s) {
     if (a.n == 0 || a.ncols == 0) return hipSuccess;
-    // columns per workgroup: aim at ~256 workgroups; compute waves: enough
-    // events in flight for the DAG's antichain width (~V / (1.6 P))
-    // (the walk time is levels x pass latency whatever the number of
-    // workgroups, and the block walker's pass gets shorter with fewer columns
-    // per slice: 1 or 2 columns while that leaves at most ~256 workgroups,
-    // one per CU; the quad layout exists for 4-column slices only)
-    uint32_t cpw = a.cpw_hint ? a.cpw_hint : a.lean == 1 ? 4 : (a.ncols <= 256 ? 1 : a.ncols <= 512 ? 2 : 4);
-    uint32_t ncw = a.ncw_hint ? a.ncw_hint : (a.width_hint <= 24 ? 1 : a.width_hint <= 48 ? 2 : 4);
-    if (cpw <= 1) return launch_index_c<1>(a, ncw, s);
-    if (cpw <= 2) return launch_index_c<2>(a, ncw, s);
-    return launch_index_c<4>(a, ncw, s);
+    // columns per workgroup: the fewest that still leave at most ~256
+    // workgroups (one per CU); the pass gets shorter with fewer columns per
+    // slice, and the walk time is levels x pass latency whatever the number of
+    // workgroups.  Compute waves: 8 on 1- / 2-column slices (11 slowed C2 by
+    // 7 %), 11 on 4-column slices (16 waves with the loader and 4 drains, the
+    // workgroup limit: C3 walk -1.8 % against 8).
+    const uint32_t cpw = a.cpw_hint ? a.cpw_hint : (a.ncols <= 256 ? 1 : a.ncols <= 512 ? 2 : 4);
+    if (cpw <= 1) return launch_index_t<1, 8>(a, s);
+    if (cpw <= 2) return launch_index_t<2, 8>(a, s);
+    return launch_index_t<4, 11>(a, s);
 }
 
 // ---------------------------------------------------------------------------- fork marks
@@ -1754,7 +1154,7 @@ __global__ __launch_bounds__(256) void k_fc(FcArgs a) {
         wr[t] = i < nv ? wv[i] : make_uint4(0, 0, 0, 0);
     }
     for (uint64_t q = blockIdx.x * qpb + threadIdx.x / LPQ; q < a.n; q += (uint64_t)gridDim.x * qpb) {
-        uint32_t A = a.qa[q], Bq = a.qb[q];
+        uint32_t A = a.qa[a.qa_bcast ? 0 : q], Bq = a.qb[q];
         const bool bad = (A >= a.n_events) | (Bq >= a.n_events);
         if (bad) { A = 0; Bq = 0; }
         // FORKS, lane 0: the early-false inputs first (their loads overlap the rows')
@@ -1823,7 +1223,8 @@ __global__ __launch_bounds__(256) void k_fc(FcArgs a) {
             if (a.partial) {
                 a.partial[q] = sum + (early ? LX_MARK : 0u);
             } else {
-                a.out[q] = bad ? 0xFF : (uint8_t)(!early && sum >= a.quorum);
+                const uint8_t r = bad ? 0xFF : (uint8_t)(!early && sum >= a.quorum);
+                a.out[q] = a.out_tag && !bad ? (uint8_t)(a.out_tag[q] << 1 | r) : r;
             }
             if (bad) atomicOr(&a.status[1], 1u);
         }
@@ -1869,7 +1270,7 @@ __global__ __launch_bounds__(256) void k_fc_fk(FcArgs a) {
         wch[t] = k < a.n_cheat ? a.fk_wch[k] : 0u;
     }
     for (uint64_t q = blockIdx.x * qpb + threadIdx.x / LPQ; q < a.n; q += (uint64_t)gridDim.x * qpb) {
-        uint32_t A = a.qa[q], Bq = a.qb[q];
+        uint32_t A = a.qa[a.qa_bcast ? 0 : q], Bq = a.qb[q];
         const bool bad = (A >= a.n_events) | (Bq >= a.n_events);
         if (bad) { A = 0; Bq = 0; }
         uint32_t e_bb = 0, e_cb = 0;
@@ -1948,7 +1349,8 @@ __global__ __launch_bounds__(256) void k_fc_fk(FcArgs a) {
             if (a.partial) {
                 a.partial[q] = sum + (early ? LX_MARK : 0u);
             } else {
-                a.out[q] = bad ? 0xFF : (uint8_t)(!early && sum >= a.quorum);
+                const uint8_t r = bad ? 0xFF : (uint8_t)(!early && sum >= a.quorum);
+                a.out[q] = a.out_tag && !bad ? (uint8_t)(a.out_tag[q] << 1 | r) : r;
             }
             if (bad) atomicOr(&a.status[1], 1u);
         }

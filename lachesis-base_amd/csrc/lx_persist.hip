@@ -287,6 +287,27 @@ __global__ void k_load_check(LoadRawArgs a, uint32_t n) {
     if (marked != (a.lm[t] != 0)) atomicOr(a.bad, 4u);
 }
 
+// A fork marker is only valid in a column of a creator with more than one
+// branch (vecengine/index.go:173-209 marks cheaters' branches only): any
+// other marker cell -- a non-cheater's column, or anywhere in an epoch without
+// fork branches -- is a corrupt row.  One thread per (row, column); bad |= 16.
+__global__ void k_load_marks_ok(const uint32_t *hb, uint64_t stride, uint32_t n, uint32_t B,
+                                const uint32_t *cheat_col, uint32_t *bad) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (uint64_t)n * B) return;
+    const uint32_t e = (uint32_t)(t / B), c = (uint32_t)(t % B);
+    if ((hb[(uint64_t)e * stride + c] & LX_MARK) && !cheat_col[c]) atomicOr(bad, 16u);
+}
+
+hipError_t launch_load_marks_ok(const uint32_t *hb, uint64_t stride, uint32_t n, uint32_t B, const uint32_t *cheat_col,
+                                uint32_t *bad, hipStream_t s) {
+    const uint64_t t = (uint64_t)n * B;
+    if (!t) return hipSuccess;
+    hipLaunchKernelGGL(k_load_marks_ok, dim3((uint32_t)((t + 255) / 256)), dim3(256), 0, s, hb, stride, n, B, cheat_col,
+                       bad);
+    return hipGetLastError();
+}
+
 hipError_t launch_load_raw(const LoadRawArgs &a, hipStream_t s) {
     if (!a.ncc) return hipSuccess;
     hipLaunchKernelGGL(k_load_raw, dim3((a.ncc + kSmallCW - 1) / kSmallCW), dim3(256), 0, s, a);

@@ -20,6 +20,7 @@ SIGNATURES = [
     ("lx_create", ctypes.c_int, [vp, ctypes.POINTER(vp)]),
     ("lx_destroy", None, [vp]),
     ("lx_last_error", ctypes.c_char_p, [vp]),
+    ("lx_set_option", ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_int64]),
     ("lx_reset", ctypes.c_int, [vp, ctypes.c_uint32, u32p]),
     ("lx_add_batch", ctypes.c_int, [vp, ctypes.c_uint32, u32p, u32p, u64p, u32p, u32p, u32p]),
     ("lx_add_batch_dev", ctypes.c_int, [vp, ctypes.c_uint32, vp, vp, vp, vp, u32p]),
@@ -33,6 +34,8 @@ SIGNATURES = [
     ("lx_num_branches", ctypes.c_uint32, [vp]),
     ("lx_at_least_one_fork", ctypes.c_int, [vp]),
     ("lx_forkless_cause_batch", ctypes.c_int, [vp, ctypes.c_uint64, u32p, u32p, u8p]),
+    ("lx_forkless_cause", ctypes.c_int, [vp, ctypes.c_uint32, ctypes.c_uint32, u8p]),
+    ("lx_fc_cache_stats", ctypes.c_int, [vp, vp]),
     ("lx_forkless_cause_batch_dev", ctypes.c_int, [vp, ctypes.c_uint64, vp, vp, vp, vp]),
     ("lx_forkless_cause_partial_dev", ctypes.c_int, [vp, ctypes.c_uint64, vp, vp, vp, vp]),
     ("lx_fc_combine_dev", ctypes.c_int, [vp, ctypes.c_uint64, vp, vp, vp]),
@@ -113,6 +116,12 @@ class LxStats(ctypes.Structure):
                 ("ms_marks", ctypes.c_float), ("index_launches", ctypes.c_uint32)]
 
 
+class LxFcStats(ctypes.Structure):
+    _fields_ = [("calls", ctypes.c_uint64), ("hits", ctypes.c_uint64), ("row_fills", ctypes.c_uint64),
+                ("tile_fills", ctypes.c_uint64), ("pairs", ctypes.c_uint64), ("slots", ctypes.c_uint32),
+                ("slots_used", ctypes.c_uint32)]
+
+
 class LxWriteback(ctypes.Structure):
     _fields_ = [("first_event", ctypes.c_uint64), ("n_events", ctypes.c_uint64), ("n_la_rows", ctypes.c_uint64),
                 ("hb_bytes", ctypes.c_uint64), ("la_bytes", ctypes.c_uint64), ("bi_bytes", ctypes.c_uint32)]
@@ -155,10 +164,15 @@ def _u32(a):
     return np.ascontiguousarray(a, dtype=np.uint32)
 
 
+# lx_set_option values applied to every new Index (tests select implementation
+# paths this way, e.g. {"small_max": 0}; every option gives identical results)
+DEFAULT_OPTIONS = {}
+
+
 class Index:
     """Dense-index handle over lx_* (one GPU, one epoch at a time)."""
 
-    def __init__(self, device=0, event_capacity=0, branch_reserve=0, shard_rank=0, shard_count=1):
+    def __init__(self, device=0, event_capacity=0, branch_reserve=0, shard_rank=0, shard_count=1, options=None):
         self.L = load_library()
         cfg = LxConfig(device, event_capacity, branch_reserve, shard_rank, shard_count)
         h = vp()
@@ -166,6 +180,12 @@ class Index:
         if rc != 0:
             raise LxError(rc, "lx_create failed (device %d)" % device)
         self.h = h
+        for k, v in dict(DEFAULT_OPTIONS, **(options or {})).items():
+            self.set_option(k, v)
+
+    def set_option(self, name, value):
+        """lx_set_option (path selection; results never change)."""
+        self._chk(self.L.lx_set_option(self.h, name.encode(), int(value)))
 
     def close(self):
         if getattr(self, "h", None):
@@ -283,7 +303,16 @@ class Index:
         return out
 
     def forkless_cause(self, a, b):
-        return bool(self.forkless_cause_batch([a], [b])[0])
+        """lx_forkless_cause: one pair, as the reference's callers ask it (the
+        index's result cache answers repeated questions)."""
+        out = ctypes.c_uint8()
+        self._chk(self.L.lx_forkless_cause(self.h, int(a), int(b), ctypes.byref(out)))
+        return bool(out.value)
+
+    def fc_cache_stats(self):
+        st = LxFcStats()
+        self._chk(self.L.lx_fc_cache_stats(self.h, ctypes.byref(st)))
+        return {k: getattr(st, k) for k, _ in LxFcStats._fields_}
 
     def forkless_cause_batch_dev(self, n, a_ptr, b_ptr, out_ptr, stream=None):
         self._chk(self.L.lx_forkless_cause_batch_dev(self.h, n, a_ptr, b_ptr, out_ptr, stream))

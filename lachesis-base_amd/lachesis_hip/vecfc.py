@@ -126,25 +126,45 @@ def new_index_with_engine(crit, config, engine):
     return VecfcIndex(crit=crit, config=config, engine=engine)
 
 
-class VecfcIndex:
-    """vecfc.Index over the HIP library.  ``validators`` needs ``ids``,
-    ``weights`` (idx order) and ``idxs`` (ValidatorID -> idx)."""
+class _EngineState:
+    """The epoch state a vecengine.Engine owns: the device handle, the event-ID
+    <-> dense-index map, the flush point, validators and the getEvent
+    callback.  Every vecfc.Index over one engine (NewIndexWithEngine) shares
+    this object, so a Reset / Flush / DropNotFlushed / restore through one
+    facade is what the others see (vecfc/index.go:80-89 shares its Engine)."""
 
-    def __init__(self, device=0, event_capacity=0, crit=None, config=None, engine=None):
-        self.crit = crit or self._panic
-        self.cfg = config or default_config()
+    def __init__(self, ix):
+        self.ix = ix
         self.pos = {}
         self.ids = []
         self.n_flushed = 0
         self.validators = None
         self.get_event_fn = None
+
+
+def _shared(name):
+    return property(lambda self: getattr(self._st, name), lambda self, v: setattr(self._st, name, v))
+
+
+class VecfcIndex:
+    """vecfc.Index over the HIP library.  ``validators`` needs ``ids``,
+    ``weights`` (idx order) and ``idxs`` (ValidatorID -> idx)."""
+
+    ix = _shared("ix")
+    pos = _shared("pos")
+    ids = _shared("ids")
+    n_flushed = _shared("n_flushed")
+    validators = _shared("validators")
+    get_event_fn = _shared("get_event_fn")
+
+    def __init__(self, device=0, event_capacity=0, crit=None, config=None, engine=None):
+        self.crit = crit or self._panic
+        self.cfg = config or default_config()
         if isinstance(engine, VecfcIndex):
-            # a second vecfc.Index over the same engine: the device handle and the
-            # epoch's event map are shared (the reference shares its Engine)
-            self.ix, self.pos, self.ids = engine.ix, engine.pos, engine.ids
-            self.validators, self.get_event_fn = engine.validators, engine.get_event_fn
+            # a second vecfc.Index over the same engine: one shared epoch state
+            self._st = engine._st
         else:
-            self.ix = engine if engine is not None else Index(device=device, event_capacity=event_capacity)
+            self._st = _EngineState(engine if engine is not None else Index(device=device, event_capacity=event_capacity))
 
     @staticmethod
     def _panic(err):

@@ -57,6 +57,11 @@ def lib():
             f.argtypes = [ctypes.c_void_p]
         L.abo_event_frame.restype = ctypes.c_uint32
         L.abo_event_frame.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
+        L.abo_trace.argtypes = [ctypes.c_void_p, u64p]
+        L.abo_set_timing.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.abo_fc_seconds.restype = ctypes.c_double
+        L.abo_fc_seconds.argtypes = [ctypes.c_void_p]
+        L.abo_set_fc_cache.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
         L.abo_frame_roots.restype = ctypes.c_uint32
         L.abo_frame_roots.argtypes = [ctypes.c_void_p, ctypes.c_uint32, u32p, ctypes.c_uint32]
         _lib = L
@@ -205,6 +210,23 @@ class AbftOracle:
         rc = self.L.abo_process_batch(self.h, n, _p(creator, u32p), _p(seq, u32p), _p(poff, u64p), _p(par, u32p),
                                       None if cl is None else _p(cl, u32p), _p(out, u32p), ctypes.byref(consumed))
         return rc, consumed.value, out
+
+    def trace(self):
+        """The caller's call sequence on the index so far: {"hash", "fc_calls",
+        "fc_lru_hits", "adds", "flushes", "drops"} (abo_trace)."""
+        out = np.zeros(6, dtype=np.uint64)
+        self.L.abo_trace(self.h, _p(out, u64p))
+        return dict(zip(("hash", "fc_calls", "fc_lru_hits", "adds", "flushes", "drops"), map(int, out)))
+
+    def set_fc_cache(self, pairs):
+        """The reference's ForklessCause LRU (DefaultConfig: 20000 pairs); 0 = none."""
+        self.L.abo_set_fc_cache(self.h, pairs)
+
+    def set_timing(self, on=True):
+        self.L.abo_set_timing(self.h, int(on))
+
+    def fc_seconds(self):
+        return self.L.abo_fc_seconds(self.h)
 
     def epoch(self):
         return self.L.abo_epoch(self.h)

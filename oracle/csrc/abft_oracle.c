@@ -23,6 +23,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #define NONE 0xFFFFFFFFu
 
@@ -82,12 +83,135 @@ typedef struct {
     uint32_t *stack;
     uint64_t stack_cap;
     int err;                 /* sticky election error */
+    /* the caller's call sequence on the index (IndexedLachesis.Process,
+     * abft/indexed_lachesis.go:69-82): counts and a running hash, see abo_trace */
+    uint64_t tr_hash, tr_fc, tr_add, tr_flush, tr_drop, tr_fc_hits;
+    int timing;
+    double t_fc;             /* seconds inside ForklessCause (LRU included) */
+    /* the reference's ForklessCause LRU (vecfc/forkless_cause.go:28-38, a
+     * simplewlru of IndexCacheConfig.ForklessCausePairs entries of weight 1,
+     * vecfc/index.go:52-61); 0 entries = none */
+    uint32_t lru_cap, lru_n, lru_head, lru_tail, lru_mask;
+    uint64_t *lru_key;
+    uint8_t *lru_val;
+    uint32_t *lru_prev, *lru_next, *lru_slot;   /* lru_slot: hash slot -> node + 1 */
 } abo_t;
 
 static void *xr(void *p, size_t n) {
     void *q = realloc(p, n ? n : 1);
     if (!q) abort();
     return q;
+}
+
+/* ---- call-sequence trace: h = splitmix64(h ^ record); records
+ *   Add(e) (1 << 62 | e), ForklessCause(a, b) (a << 32 | b), Flush (2 << 62 |
+ *   events), DropNotFlushed (3 << 62 | events after it) -- the same definition
+ *   as tools/lx_dropin.cpp */
+static uint64_t tr_mix(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+static void tr(abo_t *a, uint64_t rec) { a->tr_hash = tr_mix(a->tr_hash ^ rec); }
+
+/* ---- simplewlru restated for (a, b) -> bool: hash (linear probing,
+ * backward-shift deletion) + recency list */
+static uint32_t lru_h(uint64_t k, uint32_t mask) { return (uint32_t)(tr_mix(k) & mask); }
+static void lru_unlink(abo_t *a, uint32_t i) {
+    uint32_t p = a->lru_prev[i], n = a->lru_next[i];
+    if (p != NONE) a->lru_next[p] = n; else a->lru_head = n;
+    if (n != NONE) a->lru_prev[n] = p; else a->lru_tail = p;
+}
+static void lru_front(abo_t *a, uint32_t i) {
+    a->lru_prev[i] = NONE;
+    a->lru_next[i] = a->lru_head;
+    if (a->lru_head != NONE) a->lru_prev[a->lru_head] = i;
+    a->lru_head = i;
+    if (a->lru_tail == NONE) a->lru_tail = i;
+}
+static uint32_t lru_find(abo_t *a, uint64_t k, uint32_t *slot) {
+    uint32_t h = lru_h(k, a->lru_mask);
+    for (;; h = (h + 1) & a->lru_mask) {
+        uint32_t v = a->lru_slot[h];
+        if (!v) { *slot = h; return NONE; }
+        if (a->lru_key[v - 1] == k) { *slot = h; return v - 1; }
+    }
+}
+static void lru_erase_slot(abo_t *a, uint32_t h) {
+    uint32_t i = (h + 1) & a->lru_mask;
+    a->lru_slot[h] = 0;
+    while (a->lru_slot[i]) {          /* backward shift */
+        uint32_t v = a->lru_slot[i], want = lru_h(a->lru_key[v - 1], a->lru_mask);
+        if (((i - want) & a->lru_mask) >= ((i - h) & a->lru_mask)) {
+            a->lru_slot[h] = v;
+            a->lru_slot[i] = 0;
+            h = i;
+        }
+        i = (i + 1) & a->lru_mask;
+    }
+}
+static void lru_clear(abo_t *a) {
+    if (!a->lru_cap) return;
+    memset(a->lru_slot, 0, (size_t)(a->lru_mask + 1) * 4u);
+    a->lru_n = 0;
+    a->lru_head = a->lru_tail = NONE;
+}
+void abo_set_fc_cache(void *h, uint32_t pairs) {
+    abo_t *a = h;
+    free(a->lru_key); free(a->lru_val); free(a->lru_prev); free(a->lru_next); free(a->lru_slot);
+    a->lru_key = NULL; a->lru_val = NULL; a->lru_prev = a->lru_next = a->lru_slot = NULL;
+    a->lru_cap = pairs;
+    if (!pairs) return;
+    uint32_t m = 1;
+    while (m < 2 * pairs) m <<= 1;
+    a->lru_mask = m - 1;
+    a->lru_key = xr(NULL, (size_t)pairs * 8u);
+    a->lru_val = xr(NULL, pairs);
+    a->lru_prev = xr(NULL, (size_t)pairs * 4u);
+    a->lru_next = xr(NULL, (size_t)pairs * 4u);
+    a->lru_slot = xr(NULL, (size_t)m * 4u);
+    lru_clear(a);
+}
+
+/* ForklessCause as the caller asks it (vecfc/forkless_cause.go:28-38) */
+static int fc_call(abo_t *a, uint32_t x, uint32_t y) {
+    const uint64_t k = ((uint64_t)x << 32) | y;
+    struct timespec t0, t1;
+    if (a->timing) clock_gettime(CLOCK_MONOTONIC, &t0);
+    tr(a, k);
+    a->tr_fc++;
+    int r;
+    uint32_t slot, i = a->lru_cap ? lru_find(a, k, &slot) : NONE;
+    if (i != NONE) {
+        lru_unlink(a, i);
+        lru_front(a, i);
+        r = a->lru_val[i];
+        a->tr_fc_hits++;
+    } else {
+        r = orc_forkless_cause(a->ix, x, y);
+        if (a->lru_cap) {
+            if (a->lru_n == a->lru_cap) {     /* evict the oldest */
+                uint32_t o = a->lru_tail, os;
+                lru_find(a, a->lru_key[o], &os);
+                lru_erase_slot(a, os);
+                lru_unlink(a, o);
+                i = o;
+                lru_find(a, k, &slot);        /* the slot may have moved */
+            } else {
+                i = a->lru_n++;
+            }
+            a->lru_key[i] = k;
+            a->lru_val[i] = (uint8_t)(r == 1);
+            a->lru_slot[slot] = i + 1;
+            lru_front(a, i);
+        }
+    }
+    if (a->timing) {
+        clock_gettime(CLOCK_MONOTONIC, &t1);
+        a->t_fc += (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+    }
+    return r;
 }
 
 static uint32_t quorum_of(const uint32_t *w, uint32_t V) {
@@ -105,6 +229,7 @@ static void free_epoch(abo_t *a) {
     a->npar = 0;
     if (a->ix) orc_destroy(a->ix);
     a->ix = NULL;
+    lru_clear(a);          /* Reset purges the ForklessCause cache (vecfc/index.go:103) */
 }
 
 static void election_reset(abo_t *a, uint32_t frame_to_decide) {   /* election.go:87-93 */
@@ -139,6 +264,7 @@ static void new_epoch(abo_t *a, uint32_t epoch, uint32_t V, const uint32_t *w) {
 void *abo_create(uint32_t epoch, uint32_t V, const uint32_t *w, const abo_callbacks *cb) {
     abo_t *a = calloc(1, sizeof(abo_t));
     if (cb) a->cb = *cb;
+    a->lru_head = a->lru_tail = NONE;
     new_epoch(a, epoch, V, w);
     election_reset(a, 1);
     return a;
@@ -150,6 +276,7 @@ void abo_destroy(void *h) {
     free(a->w); free(a->frame); free(a->sp); free(a->confirmed); free(a->poff); free(a->par);
     free(a->dec_has); free(a->dec); free(a->cnt_yes); free(a->cnt_no); free(a->cnt_all);
     free(a->map_slot); free(a->map_stamp); free(a->obs); free(a->stack);
+    abo_set_fc_cache(a, 0);
     free(a);
 }
 
@@ -214,7 +341,7 @@ static int process_root(abo_t *a, uint32_t f, uint32_t k, uint32_t *atropos) {
     uint32_t nobs = 0;
     a->cnt_stamp++;                                   /* observedRootsMap stamp */
     for (uint32_t j = 0; j < prev->n; j++) {
-        if (orc_forkless_cause(a->ix, root, prev->ev[j]) != 1) continue;
+        if (fc_call(a, root, prev->ev[j]) != 1) continue;
         if (round == 1) { a->map_slot[prev->creator[j]] = j; a->map_stamp[prev->creator[j]] = a->cnt_stamp; }
         else obs_push(a, &nobs, j);
     }
@@ -260,7 +387,7 @@ static int forkless_caused_by_quorum_on(abo_t *a, uint32_t e, uint32_t f) {   /*
     const uint32_t cs = ++a->cnt_stamp;
     uint32_t sum = 0;
     for (uint32_t j = 0; j < r->n; j++) {
-        if (orc_forkless_cause(a->ix, e, r->ev[j]) == 1) {
+        if (fc_call(a, e, r->ev[j]) == 1) {
             uint32_t c = r->creator[j];
             if (a->cnt_all[c] != cs) { a->cnt_all[c] = cs; sum += a->w[c]; }
         }
@@ -278,6 +405,8 @@ static uint32_t calc_frame(abo_t *a, uint32_t e, uint32_t claimed, int check_onl
 }
 
 static int add_event(abo_t *a, uint32_t creator, uint32_t seq, uint32_t np, const uint32_t *parents) {
+    tr(a, (1ull << 62) | a->n);
+    a->tr_add++;
     int rc = orc_add(a->ix, creator, seq, np, parents);
     if (rc) return rc == -1 ? ABO_ERR_ORDER : ABO_ERR_ARG;
     if (a->n == a->cap) {
@@ -303,6 +432,13 @@ static void drop_event(abo_t *a) {     /* DropNotFlushed of the last Add */
     orc_drop_not_flushed(a->ix);
     a->n--;
     a->npar = a->poff[a->n];
+    lru_clear(a);          /* dense indices are reused after a rollback (hashes are not) */
+}
+
+/* the deferred DropNotFlushed of Process / Build, as a call (a no-op after Flush) */
+static void tr_drop(abo_t *a) {
+    tr(a, (3ull << 62) | a->n);
+    a->tr_drop++;
 }
 
 /* applyAtropos (lachesis.go:57-86) + onFrameDecided (frame_decide.go:11-35);
@@ -381,7 +517,7 @@ int abo_process(void *h, uint32_t creator, uint32_t seq, uint32_t np, const uint
     uint32_t sp_frame;
     if (claimed == NONE) claimed = calc_frame(a, e, 0, 0, &sp_frame);   /* Build */
     uint32_t f = calc_frame(a, e, claimed, 1, &sp_frame);
-    if (f != claimed) { drop_event(a); return ABO_ERR_FRAME; }
+    if (f != claimed) { drop_event(a); tr_drop(a); return ABO_ERR_FRAME; }
     a->frame[e] = f;
     if (out_frame) *out_frame = f;
     if (sp_frame != f) add_root(a, sp_frame, e, f, creator);
@@ -400,6 +536,9 @@ int abo_process(void *h, uint32_t creator, uint32_t seq, uint32_t np, const uint
         if (rc == 1) { sealed = 1; break; }
     }
     if (!sealed) orc_flush(a->ix);
+    tr(a, (2ull << 62) | a->n);           /* IndexedLachesis.Process: Flush, then the deferred drop */
+    a->tr_flush++;
+    tr_drop(a);
     return sealed;
 }
 
@@ -410,6 +549,7 @@ int abo_build(void *h, uint32_t creator, uint32_t seq, uint32_t np, const uint32
     uint32_t sp_frame;
     *out_frame = calc_frame(a, a->n - 1, 0, 0, &sp_frame);
     drop_event(a);
+    tr_drop(a);
     return 0;
 }
 
@@ -426,6 +566,16 @@ int abo_process_batch(void *h, uint32_t n, const uint32_t *creator, const uint32
     }
     return 0;
 }
+
+/* out[0] call-sequence hash, [1] ForklessCause calls, [2] of them LRU hits,
+ * [3] Adds, [4] Flushes, [5] DropNotFlushed calls */
+void abo_trace(void *h, uint64_t out[6]) {
+    abo_t *a = h;
+    out[0] = a->tr_hash; out[1] = a->tr_fc; out[2] = a->tr_fc_hits;
+    out[3] = a->tr_add; out[4] = a->tr_flush; out[5] = a->tr_drop;
+}
+void abo_set_timing(void *h, int on) { ((abo_t *)h)->timing = on; }
+double abo_fc_seconds(void *h) { return ((abo_t *)h)->t_fc; }
 
 uint32_t abo_epoch(void *h) { return ((abo_t *)h)->epoch; }
 uint32_t abo_last_decided_frame(void *h) { return ((abo_t *)h)->last_decided; }

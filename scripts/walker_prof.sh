@@ -1,6 +1,6 @@
 #!/bin/bash
 # k_index per-wave counters and per-segment cycles (make wprof build).
-#   OUT=gpurun_out/wprof CFGS="c3 c2" bash scripts/walker_prof.sh   (extra env, e.g. LX_WALKER=lean, passes through)
+#   OUT=gpurun_out/wprof CFGS="c3 c2" bash scripts/walker_prof.sh   
 cd "$(dirname "$0")/.."
 O=${OUT:-gpurun_out/wprof}
 mkdir -p $O

@@ -1,0 +1,150 @@
+"""lx_forkless_cause: the per-pair ForklessCause of the unchanged caller
+(vecfc/forkless_cause.go:28-38), answered from the index's result cache
+(lachesis-base_amd/csrc/lx_fccache.cpp), bit-exact against the C oracle under
+the access patterns of abft -- the newest event against a frame's roots
+(abft/event_processing.go:149-161), a root against the previous frame's roots
+(abft/election/election.go:101-123), old roots replayed after a decided frame
+(abft/event_processing.go:102-146) -- with Build-style rollbacks
+(abft/indexed_lachesis.go:53-63), evictions and slot reuse."""
+
+import numpy as np
+import pytest
+
+from oracle import corc
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def lx():
+    import lachesis_hip
+    return lachesis_hip
+
+
+def _oracle(d, w, n):
+    o = corc.OracleIndex(w)
+    assert o.add_batch(d.creator[:n], d.seq[:n], d.poff[:n + 1], d.par) == -1
+    return o
+
+
+@pytest.mark.parametrize("slots", [0, 64, 256, 4096])
+@pytest.mark.parametrize("cheaters", [0, 3])
+def test_caller_pattern_matches_oracle(lx, slots, cheaters):
+    """Events added one at a time; after each Add the newest event asks about
+    a window of older "roots" in order, then an older event replays its
+    questions (the election / processKnownRoots pattern).  Every answer equals
+    the oracle's; a small working set forces evictions, slot reuse past the
+    127 column generations, and tile fills."""
+    V = 12
+    d = lx.tools.gen_dag(V, 40, 4, cheaters=cheaters, forks=4, seed=5 + cheaters)
+    w = list(range(30, 30 - V, -1))
+    N = len(d)
+    o = _oracle(d, w, N)
+    ix = lx.Index(options={"fc_cache": slots})
+    ix.reset(w)
+    rng = np.random.default_rng(slots + cheaters)
+    asked = 0
+    for e in range(N):
+        ix.add_batch(d.creator[e:e + 1], d.seq[e:e + 1], d.poff[e:e + 2], d.par)
+        ix.flush()
+        if e < 8:
+            continue
+        lo = max(0, e - 3 * V)
+        for b in range(lo, e, 2):                      # newest event vs a frame's roots, in order
+            assert ix.forkless_cause(e, b) == bool(o.forkless_cause(e, b)), (e, b)
+            asked += 1
+        if e % 7 == 0:                                 # an older root replays its questions
+            a = int(rng.integers(max(0, e - 4 * V), e))
+            for b in range(max(0, a - 2 * V), a, 3):
+                assert ix.forkless_cause(a, b) == bool(o.forkless_cause(a, b)), (a, b)
+                asked += 1
+    st = ix.fc_cache_stats()
+    if slots:
+        assert st["calls"] == asked and st["hits"] > asked // 2
+        assert st["row_fills"] > 0 and st["tile_fills"] > 0
+    ix.close()
+
+
+def test_rollback_evicts_dropped_events(lx):
+    """Add, ask, DropNotFlushed of several unflushed events, re-Add: the
+    dropped events leave the working set, the re-added ones (same dense
+    indices) are answered afresh."""
+    V = 8
+    d = lx.tools.gen_dag(V, 30, 3, cheaters=2, forks=3, seed=3)
+    w = [3, 3, 2, 2, 2, 1, 1, 1]
+    N = len(d)
+    o = corc.OracleIndex(w)
+    ix = lx.Index(options={"fc_cache": 128})
+    ix.reset(w)
+    for e in range(N):
+        ix.add_batch(d.creator[e:e + 1], d.seq[e:e + 1], d.poff[e:e + 2], d.par)
+        o.add(int(d.creator[e]), int(d.seq[e]), d.par[d.poff[e]:d.poff[e + 1]])
+        for b in range(max(0, e - 12), e + 1):
+            assert ix.forkless_cause(e, b) == bool(o.forkless_cause(e, b))
+        if e % 4 == 3:
+            ix.drop_not_flushed()                       # rolls back e - 2 .. e
+            o.drop_not_flushed()
+            # re-add the same events: the same dense indices, recomputed answers
+            lo = int(o.num_events())
+            for x in range(lo, e + 1):
+                ix.add_batch(d.creator[x:x + 1], d.seq[x:x + 1], d.poff[x:x + 2], d.par)
+                o.add(int(d.creator[x]), int(d.seq[x]), d.par[d.poff[x]:d.poff[x + 1]])
+                for b in range(max(0, x - 12), x + 1):
+                    assert ix.forkless_cause(x, b) == bool(o.forkless_cause(x, b))
+        if e % 2 == 1:
+            ix.flush()
+            o.flush()
+    ix.close()
+
+
+def test_reused_index_after_drop_gets_fresh_answers(lx):
+    """A dropped event's dense index taken by a different event (another
+    validator's): answers for that index are recomputed, not served from the
+    dropped event's row or column."""
+    d = lx.tools.gen_dag(6, 30, 3, seed=4)
+    w = [1] * 6
+    N = len(d)
+    ix = lx.Index(options={"fc_cache": 64})
+    ix.reset(w)
+    cut = N - 20
+    ix.add_batch(d.creator[:cut], d.seq[:cut], d.poff[:cut + 1], d.par)
+    ix.flush()
+    o = _oracle(d, w, cut)
+    # event `cut` of the DAG, asked about, then dropped
+    x = cut
+    ix.add_batch(d.creator[x:x + 1], d.seq[x:x + 1], d.poff[x:x + 2], d.par)
+    first = [ix.forkless_cause(x, b) for b in range(cut - 30, cut + 1)] + \
+            [ix.forkless_cause(a, x) for a in range(cut - 30, cut + 1)]
+    ix.drop_not_flushed()
+    # a different event lands on index `cut`: the next event of another creator
+    y = next(i for i in range(cut + 1, N) if d.creator[i] != d.creator[x]
+             and all(p < cut for p in d.par[d.poff[i]:d.poff[i + 1]]))
+    par = d.par[d.poff[y]:d.poff[y + 1]]
+    ix.add(int(d.creator[y]), int(d.seq[y]), par)
+    o.add(int(d.creator[y]), int(d.seq[y]), par)
+    for b in range(cut - 30, cut + 1):
+        assert ix.forkless_cause(cut, b) == bool(o.forkless_cause(cut, b))
+        assert ix.forkless_cause(b, cut) == bool(o.forkless_cause(b, cut))
+    assert len(first) == 62
+    ix.close()
+
+
+def test_unknown_events_and_reset(lx):
+    d = lx.tools.gen_dag(5, 10, 3, seed=2)
+    ix = lx.Index()
+    ix.reset([1] * 5)
+    ix.add_batch(d.creator, d.seq, d.poff, d.par)
+    N = len(d)
+    with pytest.raises(lx.LxError) as ei:
+        ix.forkless_cause(N, 0)
+    assert ei.value.code == -1
+    assert ix.forkless_cause(N - 1, 0) in (True, False)
+    ix.reset([1] * 5)                                    # a new epoch: nothing cached survives
+    with pytest.raises(lx.LxError):
+        ix.forkless_cause(0, 0)
+    ix.add_batch(d.creator, d.seq, d.poff, d.par)
+    o = _oracle(d, [1] * 5, N)
+    for a in range(N - 10, N):
+        for b in range(N):
+            assert ix.forkless_cause(a, b) == bool(o.forkless_cause(a, b))
+    ix.close()

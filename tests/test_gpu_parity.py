@@ -20,14 +20,25 @@ def lx():
     return lachesis_hip
 
 
+@pytest.fixture
+def opts(monkeypatch):
+    """Set lx_set_option values for every Index this test creates."""
+    from lachesis_hip import capi
+
+    def set_(**kw):
+        for k, v in kw.items():
+            monkeypatch.setitem(capi.DEFAULT_OPTIONS, k, v)
+    return set_
+
+
 @pytest.fixture(params=["small", "big"], autouse=True)
-def add_path(request, monkeypatch):
+def add_path(request, opts):
     """Every test runs twice: host-pointer batches of <= 3072 events take the
     small-batch path (host branch assignment + k_small, lx_small.hip) by
-    default; LX_SMALL_MAX=0 (read by lx_create) sends every batch through the
-    device-assigned walker path (k_index)."""
+    default; option small_max=0 sends every batch through the device-assigned
+    walker path (k_index)."""
     if request.param == "big":
-        monkeypatch.setenv("LX_SMALL_MAX", "0")
+        opts(small_max=0)
     elif request.node.get_closest_marker("big_only"):
         pytest.skip("every batch of this test is larger than the small path takes")
     return request.param
@@ -125,12 +136,12 @@ def test_fork_dag_rows_and_fc(lx, shape):
 
 @pytest.mark.parametrize("cheaters", [20, 40, 70])
 @pytest.mark.parametrize("fk", ["1", "0"])
-def test_fork_fc_paths(lx, cheaters, fk, monkeypatch):
+def test_fork_fc_paths(lx, cheaters, fk, opts):
     """The fork-path ForklessCause kernels: every plane column streamed with a
     32-bit (<= 32 cheaters) or 64-bit cheater mask (k_fc_fk), and the cheater
     fix-up loop (k_fc<.., true>: > 64 cheaters, or LX_FC_FK=0), all equal to
     the oracle; Zipf stakes so the per-creator dedupe weighs differently."""
-    monkeypatch.setenv("LX_FC_FK", fk)
+    opts(fc_fk=int(fk))
     n = 100
     d = lx.tools.gen_dag(n, 14, 10, cheaters=cheaters, forks=4, seed=cheaters)
     weights = [(1 << 20) // (i + 1) for i in range(n)]
@@ -434,41 +445,19 @@ def test_full_size_properties_config2(lx):
 
 
 # ---------------------------------------------------------------- walker variants
-WALKER_VARIANTS = [
-    # environment read by lx_create: the one-lane-per-event layout (columns per
-    # workgroup, compute waves, small-LDS ring, record ring)
-    {"LX_WALKER": "classic", "LX_CPW": "1", "LX_NCW": "1"}, {"LX_WALKER": "classic", "LX_CPW": "2", "LX_NCW": "2"},
-    {"LX_WALKER": "classic", "LX_CPW": "4", "LX_NCW": "4"}, {"LX_WALKER": "classic", "LX_CPW": "4", "LX_NCW": "1"},
-    {"LX_WALKER": "classic", "LX_CPW": "1", "LX_NCW": "4"},
-    {"LX_WALKER": "classic", "LX_SMALL": "1", "LX_CPW": "1", "LX_NCW": "1"},
-    {"LX_WALKER": "classic", "LX_SMALL": "1", "LX_CPW": "2", "LX_NCW": "2"},
-    {"LX_WALKER": "classic", "LX_RR": "512", "LX_CPW": "2", "LX_NCW": "4"},
-    {"LX_WALKER": "classic", "LX_RR": "512", "LX_CPW": "2", "LX_NCW": "2"},
-    # quad-per-event compute waves (CPW 4), 4 and 8 compute waves
-    {"LX_CPW": "4", "LX_WALKER": "lean"}, {"LX_CPW": "4", "LX_WALKER": "lean", "LX_LEAN_NCW": "8"},
-    # the same with wave-uniform blocks of 16 events
-    {"LX_CPW": "4", "LX_WALKER": "block", "LX_LEAN_NCW": "4", "LX_DRAINS": "2"},
-    {"LX_CPW": "4", "LX_WALKER": "block", "LX_LEAN_NCW": "8", "LX_DRAINS": "2"},
-    {"LX_CPW": "4", "LX_WALKER": "block", "LX_LEAN_NCW": "12", "LX_DRAINS": "2"},
-    {"LX_WALKER": "block"},   # the default: 8 compute waves, 4 drains (1-column slices at this V)
-    # block walker on 1- and 2-column slices (small V, column shards)
-    {"LX_CPW": "1", "LX_WALKER": "block"}, {"LX_CPW": "2", "LX_WALKER": "block"},
-    {"LX_CPW": "1", "LX_WALKER": "block", "LX_DRAINS": "2"}, {"LX_CPW": "2", "LX_WALKER": "block", "LX_DRAINS": "2"},
-    {"LX_CPW": "4", "LX_WALKER": "block", "LX_LEAN_NCW": "11", "LX_DRAINS": "4"},
-    # 4-column slices with two slot units per event (the layout for seqs > 0xFFFF)
-    {"LX_CPW": "4", "LX_WALKER": "block", "LX_PACK16": "0"},
-    {"LX_CPW": "4", "LX_WALKER": "block", "LX_LEAN_NCW": "8", "LX_PACK16": "0"},
-]
+# The shipped walker (block layout: 16-event blocks per wave, a quad of lanes
+# per event, 4 drain waves) on 1-, 2- and 4-column slices, the last with the
+# 16-bit packed slot unit (default while every seq fits) and with two units.
+WALKER_VARIANTS = [{"cpw": 0}, {"cpw": 1}, {"cpw": 2}, {"cpw": 4}, {"cpw": 4, "pack16": 0}]
 
 
 @pytest.mark.big_only
-@pytest.mark.parametrize("env", WALKER_VARIANTS, ids=lambda e: "-".join("%s%s" % (k[3:].lower(), v) for k, v in e.items()))
-def test_walker_variants(lx, env, monkeypatch):
-    """Every walker configuration (slot layouts, ring sizes, wave counts) is bit-exact;
-    the DAG is long enough (6000 events, cheaters) that ring slots are reused and
-    parents older than the ring take the L2 path."""
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
+@pytest.mark.parametrize("env", WALKER_VARIANTS, ids=lambda e: "-".join("%s%s" % (k, v) for k, v in e.items()))
+def test_walker_variants(lx, env, opts):
+    """Every shipped walker configuration (slice widths, slot layouts) is
+    bit-exact; the DAG is long enough (6000 events, cheaters) that ring slots
+    are reused and parents older than the ring take the L2 path."""
+    opts(**env)
     d = lx.tools.gen_dag(24, 250, 6, 4, 6, 21)
     weights = list(range(40, 16, -1))
     o = oracle_for(d, weights)
@@ -484,17 +473,15 @@ def test_walker_variants(lx, env, monkeypatch):
 
 
 @pytest.mark.big_only
-@pytest.mark.parametrize("walker", ["classic", "lean", "block", "block-4u", "block-1", "block-2"])
-def test_walker_many_parents(lx, walker, monkeypatch):
+@pytest.mark.parametrize("cpw", ["4", "4u", "1", "2"])
+def test_walker_many_parents(lx, cpw, opts):
     """Events with more parents than a record holds inline (16 > 12) take the
-    overflow path of the walker; CPW 4 with both compute layouts (block-4u:
-    two slot units per event instead of the packed 16-bit one)."""
-    walker, _, cpw = walker.partition("-")
+    overflow path of the walker, on each slice width (4u: two slot units per
+    event instead of the packed 16-bit one)."""
     if cpw.endswith("u"):
         cpw = cpw[:-1]
-        monkeypatch.setenv("LX_PACK16", "0")
-    monkeypatch.setenv("LX_CPW", cpw or "4")
-    monkeypatch.setenv("LX_WALKER", walker)
+        opts(pack16=0)
+    opts(cpw=int(cpw))
     d = lx.tools.gen_dag(30, 120, 16, 3, 4, 77)
     assert int(np.max(np.diff(d.poff))) > 12
     weights = list(range(70, 40, -1))
@@ -510,10 +497,10 @@ def test_walker_many_parents(lx, walker, monkeypatch):
 
 
 @pytest.mark.big_only
-def test_walker_seqs_beyond_16_bits(lx, monkeypatch):
+def test_walker_seqs_beyond_16_bits(lx, opts):
     """4-column slices with seqs above 0xFFFF: the walker must not use the
     packed 16-bit slot units (rows and FC still equal the oracle)."""
-    monkeypatch.setenv("LX_CPW", "4")
+    opts(cpw=4)
     weights = [3, 2]
     big = lx.tools.gen_dag(2, 66000, 2, 0, 0, 6)
     assert int(big.seq.max()) > 0xFFFF
@@ -557,13 +544,11 @@ def far_parent_dag(lx, n_nodes, n, seed):
 
 
 @pytest.mark.big_only
-@pytest.mark.parametrize("walker", ["classic", "lean", "block", "block-1", "block-2"])
-def test_walker_far_parents(lx, walker, monkeypatch):
+@pytest.mark.parametrize("cpw", [4, 1, 2])
+def test_walker_far_parents(lx, cpw, opts):
     """Parents far older than the ring (slot reuse while an event waits) in
-    one batch and across batches, for each compute layout, bit-exact."""
-    walker, _, cpw = walker.partition("-")
-    monkeypatch.setenv("LX_CPW", cpw or "4")
-    monkeypatch.setenv("LX_WALKER", walker)
+    one batch and across batches, for each slice width, bit-exact."""
+    opts(cpw=cpw)
     d = far_parent_dag(lx, 16, 12000, 91)
     weights = list(range(50, 34, -1))
     o = oracle_for(d, weights)
@@ -715,10 +700,10 @@ def test_la_tail_stale_rows(lx):
     ix.close()
 
 
-def test_la_memset_mode_matches(lx, monkeypatch):
-    """LX_LA_MEMSET=1 (zero the whole LowestAfter plane at reset, no tail pass)
-    gives the same rows and FC as the default tail mode."""
-    monkeypatch.setenv("LX_LA_MEMSET", "1")
+def test_la_memset_mode_matches(lx, opts):
+    """Option la_memset=1 (zero the whole LowestAfter plane at reset, no tail
+    pass) gives the same rows and FC as the default tail mode."""
+    opts(la_memset=1)
     ix = lx.Index()
     for (n, ev, p, ch, fk, seed) in [(20, 50, 5, 3, 4, 61), (12, 40, 4, 2, 3, 62)]:
         d = lx.tools.gen_dag(n, ev, p, ch, fk, seed)

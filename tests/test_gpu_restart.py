@@ -147,14 +147,15 @@ def _flip(b, k, x=1):
 
 
 CORRUPTIONS = ["la_entry", "hb_seq", "hb_minseq", "branch_id", "hb_length", "bi_last_seq", "bi_creator", "marker",
-               "missing_parent"]
+               "missing_parent", "marker_honest", "marker_nofork"]
+MARKER = bytes(4) + (0x7FFFFFFF).to_bytes(4, "little")
 
 
 @pytest.mark.parametrize("kind", CORRUPTIONS)
 def test_load_refuses_inconsistent_tables(lx, kind):
     """Each kind of table damage is refused with crit("inconsistent DB"); the
     undamaged tables load (and a handle refused once loads fine after reset)."""
-    evs, validators, store, o, db = _base_db(lx)
+    evs, validators, store, o, db = _base_db(lx, cheaters=0 if kind == "marker_nofork" else 3)
     bad = {t: dict(v) for t, v in db.items()}
     e = evs[len(evs) // 2]
     if kind == "la_entry":
@@ -193,6 +194,16 @@ def test_load_refuses_inconsistent_tables(lx, kind):
         row = bytearray(bad["S"][k.id])
         row[8 * j:8 * j + 8] = bytes(8)
         bad["S"][k.id] = bytes(row)
+    elif kind in ("marker_honest", "marker_nofork"):
+        # a fork marker in the column of a creator with one branch (in a fork-free
+        # epoch: anywhere) -- the reference marks cheaters' branches only
+        # (vecengine/index.go:173-209); loading it would feed 0x80000000 to the walker
+        by = o.tbl_binfo.flushed[b"c"].by_creators
+        honest = [bs[0] for bs in by if len(bs) == 1]
+        row = bytearray(bad["S"][e.id])
+        j = next(k for k in honest if k != o.get_event_branch_id(e.id) and 8 * k < len(row) and row[8 * k])
+        row[8 * j:8 * j + 8] = MARKER
+        bad["S"][e.id] = bytes(row)
     else:
         del bad["b"][evs[3].id]
     h = lx.VecfcIndex()
@@ -237,6 +248,37 @@ def test_load_full_size_config4(lx):
     assert R.lowest_after_batch(ev) == A.lowest_after_batch(ev)
     assert R.merged_highest_before_batch(ev) == A.merged_highest_before_batch(ev)
     qa, qb = lx.tools.fc_queries(d.lamport, 200_000, seed=8)
+    np.testing.assert_array_equal(R.forkless_cause_batch(qa, qb), A.forkless_cause_batch(qa, qb))
+    A.close()
+    R.close()
+
+
+def test_entry_points_refused_while_loading(lx):
+    """Between lx_load_rows and lx_load_finish the branch table is not rebuilt:
+    ForklessCause, the getters, Flush, DropNotFlushed and the write-back return
+    LX_ERR_STATE; after lx_load_finish they answer as the writing handle."""
+    d = lx.tools.gen_dag(10, 30, 4, cheaters=2, forks=3, seed=13)
+    w = [1] * 10
+    A = lx.Index()
+    A.reset(w)
+    A.add_batch(d.creator, d.seq, d.poff, d.par)
+    wb = A.writeback()
+    A.flush()
+    N = len(d)
+    R = lx.Index()
+    R.reset(w)
+    R.load_rows(d.creator, d.seq, d.poff, d.par, b"".join(wb["b"][k] for k in range(N)),
+                [wb["S"][k] for k in range(N)], [wb["s"][k] for k in range(N)])
+    for call in (lambda: R.forkless_cause(N - 1, 0), lambda: R.highest_before(0), lambda: R.lowest_after(0),
+                 lambda: R.merged_highest_before(0), lambda: R.branch(0), R.flush, R.drop_not_flushed,
+                 R.writeback, R.branches_info):
+        with pytest.raises(lx.LxError) as ei:
+            call()
+        assert ei.value.code == -4
+    R.load_finish(wb["B"])
+    for i in range(0, N, 5):
+        assert R.highest_before(i) == A.highest_before(i) and R.lowest_after(i) == A.lowest_after(i)
+    qa, qb = lx.tools.fc_queries(d.lamport, 5000, seed=2)
     np.testing.assert_array_equal(R.forkless_cause_batch(qa, qb), A.forkless_cause_batch(qa, qb))
     A.close()
     R.close()

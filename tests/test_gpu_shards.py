@@ -93,10 +93,10 @@ def test_sharded_fc_matches_oracle(G, shape):
 @pytest.mark.parametrize("force", [None, "4"])
 def test_sharded_wire_width(force, monkeypatch):
     """LowestAfter blocks travel as uint16 while every seq < 2^16, else (or
-    with LX_SHARD_WIRE=4) as uint32; FC equals the oracle either way."""
+    with option shard_wire=4) as uint32; FC equals the oracle either way."""
     import lachesis_hip as lx
     if force:
-        monkeypatch.setenv("LX_SHARD_WIRE", force)
+        monkeypatch.setitem(lx.capi.DEFAULT_OPTIONS, "shard_wire", int(force))
     d = lx.tools.gen_dag(12, 30, 4, 3, 4, 9)
     weights = [3, 3, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1]
     o = corc.OracleIndex(weights)

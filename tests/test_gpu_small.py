@@ -79,8 +79,7 @@ def test_random_chunks_vs_oracle_and_walker(lx, seed, monkeypatch):
         lo = hi
     assert br == [o.branch(i) for i in range(N)]
     rows_equal(ix, o, range(N))
-    monkeypatch.setenv("LX_SMALL_MAX", "0")
-    wk = lx.Index()
+    wk = lx.Index(options={"small_max": 0})
     wk.reset(w)
     wk.add_batch(d.creator, d.seq, d.poff, d.par)
     qa, qb = lx.tools.fc_queries(d.lamport, 100_000, window=32, seed=seed)
@@ -295,3 +294,42 @@ def test_vecfc_api_surface(lx):
     g2.dfs_subgraph(head, lambda x: (seen_g.append(x), True)[1] if seen_g.count(x) == 0 else False)
     o.dfs_subgraph(head, lambda x: (seen_o.append(x), True)[1] if seen_o.count(x) == 0 else False)
     assert seen_g == seen_o and len(seen_g) > 10
+
+
+def test_vecfc_engine_shared_state(lx):
+    """Two vecfc.Index facades over one engine (NewIndexWithEngine) share the
+    epoch state: a flush, a drop and a reset through one are what the other
+    sees -- its Adds resolve parents and its queries resolve events through the
+    same map (the reference shares its Engine, vecfc/index.go:80-89)."""
+    from oracle import pos, tdag
+    from oracle import vecfc_oracle as vo
+    nodes, evs = tdag.rand_fork_dag(6, 12, 3, cheaters=1, forks_count=3, seed=8)
+    validators = pos.Validators.equal(nodes)
+    store = {e.id: e for e in evs}
+    g = lx.new_index(None, lx.lite_config())
+    g.reset(validators, store.get)
+    g2 = lx.new_index_with_engine(None, lx.lite_config(), g)
+    o = vo.Index()
+    o.reset(validators, store.get)
+    half = len(evs) // 2
+    for e in evs[:half]:
+        g.add(e)
+        o.add(e)
+    g.flush()
+    o.flush()
+    for e in evs[half:half + 5]:          # unflushed, dropped through the other facade
+        g2.add(e)
+    g2.drop_not_flushed()
+    assert g.get_highest_before(evs[half].id) is None
+    for e in evs[half:]:                  # re-added through the first, queried through the second
+        g.add(e)
+        o.add(e)
+    for a in evs[::3]:
+        assert g2.get_highest_before(a.id).to_bytes() == o.get_highest_before(a.id).to_bytes()
+        for b in evs[::4]:
+            assert g2.forkless_cause(a.id, b.id) == o.forkless_cause(a.id, b.id)
+    g2.reset(validators, store.get)       # a reset through the second empties the first
+    assert g.get_highest_before(evs[0].id) is None
+    for e in evs[:4]:
+        g.add(e)
+    assert g2.get_lowest_after(evs[0].id) is not None
