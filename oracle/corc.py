@@ -142,6 +142,16 @@ class OracleIndex:
         self.L.orc_forkless_cause_batch(self.h, len(a), _p(a, u32p), _p(b, u32p), _p(out, u8p))
         return out
 
+    def c_funcs(self):
+        """This index as C function pointers (handle, add, flush, drop, fc,
+        merged_hb) for lachesis_hip.dropin.replay(kind="cpu") -- the bench's
+        cpu_baseline leg and the tests drive the same caller restatement over
+        this CPU index."""
+        f = lambda fn: ctypes.cast(fn, ctypes.c_void_p).value
+        L = self.L
+        return {"owner": self, "h": self.h, "add": f(L.orc_add), "flush": f(L.orc_flush), "drop": f(L.orc_drop_not_flushed),
+                "fc": f(L.orc_forkless_cause), "merged_hb": f(L.orc_get_merged_hb)}
+
     def forkless_cause_batch_mt(self, a, b, threads):
         """The same over OpenMP threads (CPU baseline; results identical)."""
         a = np.ascontiguousarray(a, dtype=np.uint32)
