@@ -137,9 +137,12 @@ def latency_leg(lx, dag, weights, device, history=200_000, reps=2000, feed=1_000
     res = {"unit": "us", "history_events": history, "reps": reps,
            "calls": {k: {"p50": out[3 * i], "p99": out[3 * i + 1], "mean": out[3 * i + 2]} for i, k in enumerate(LAT_KINDS)},
            "antichain_fed_events_per_sec": out[33], "batcher_fed_events_per_sec": out[36],
+           "fc_pair_cached": {"first_call_miss": {"p50": out[40], "p99": out[41], "mean": out[42]},
+                              "next_calls_hit": {"p50": out[43], "p99": out[44], "mean": out[45]}},
            "fed_events": int(out[34]), "fed_levels": int(out[35]), "mean_events_per_level": out[37],
            "note": "add1_async = host time of lx_add_batch(n=1) + lx_flush (the launch is not waited for); "
-                   "*_sync include lx_sync (completion); fc/getters are synchronous calls"}
+                   "*_sync include lx_sync (completion); fc/getters are synchronous calls; fc1 / fc667 = "
+                   "lx_forkless_cause_batch (no cache); fc_pair_cached = lx_forkless_cause (the drop-in path)"}
     return res
 
 
@@ -340,6 +343,65 @@ def abft_leg(lx, steps, warmup, device, cpu_budget, want_cpu):
     return res
 
 
+def dropin_leg(lx, device, want_cpu, cpu_events=4000):
+    """BASELINE configs[4] through the UNCHANGED caller: IndexedLachesis.Process
+    restated in C++ (tools/lx_dropin.cpp) makes the reference's index calls one
+    by one -- Add per event, ForklessCause per (event, root) pair from
+    calcFrameIdx, the election and processKnownRoots, Flush, DropNotFlushed,
+    GetMergedHighestBefore per decided frame (abft/indexed_lachesis.go:69-82,
+    abft/event_processing.go:102-189, abft/election/election.go:101-123) --
+    on the HIP library's C ABI (lx_forkless_cause and its result cache, the
+    path a cgo shim binds).  The same driver replaying the recorded answers
+    gives the caller's own time; the CPU baseline is the same driver over the
+    C restatement of the index behind the reference's ForklessCause LRU
+    (20000 pairs, vecfc/index.go:52-61) on a prefix of the epoch."""
+    import numpy as np
+    from lachesis_hip import dropin
+    name, V, epv, P, wkind = ABFT_CONFIG
+    weights = weights_for(V, wkind)
+    dag = lx.tools.gen_dag(V, epv, P, 0, 0, seed=1)
+    N = len(dag)
+    lch = lx.abft.DenseLachesis(weights, device=device, event_capacity=N, apply_events=False)
+    rc, consumed, claimed = lch.process_batch(dag.creator, dag.seq, dag.poff, dag.par)   # claimed frames (Build)
+    assert rc == 0 and consumed == N
+    blocks = [(int(b[1]), int(b[2])) for b in lch.blocks]
+    lch.close()
+    rec = dropin.Recording(60_000_000, V)
+    r = dropin.replay(dag, weights, claimed, kind="hip", device=device, record=rec)
+    assert np.array_equal(r["frames"], claimed)
+    assert [(int(f), int(a)) for f, a in zip(r["block_frame"], r["block_atropos"])] == blocks
+    q = dropin.replay(dag, weights, claimed, kind="recorded", record=rec)
+    assert q["trace_hash"] == r["trace_hash"]
+    st = r["fc_cache"]
+    t_idx = r["seconds"] - q["seconds"]
+    res = {"workload": "%s: V=%d, %d events, P=%d, %s stakes; IndexedLachesis.Process per event with the claimed "
+                       "frames, every index call made one at a time as the reference's caller makes it" % (
+                           name, V, N, P, wkind),
+           "events": N, "events_per_sec": N / r["seconds"], "ms_per_epoch": r["seconds"] * 1e3,
+           "caller_ms": q["seconds"] * 1e3, "index_ms": t_idx * 1e3, "index_events_per_sec": N / t_idx,
+           "add_ms": r["add_seconds"] * 1e3,
+           "fc_calls": r["fc_calls"], "fc_calls_per_sec": r["fc_calls"] / r["seconds"],
+           "fc_cache_hit_rate": st["hits"] / max(1, st["calls"]), "fc_row_fills": st["row_fills"],
+           "fc_tile_fills": st["tile_fills"], "fc_pairs_evaluated": st["pairs"], "fc_cache_slots": st["slots"],
+           "blocks": len(blocks), "trace_hash": str(r["trace_hash"]),
+           "note": "caller_ms = the same driver replaying the recorded answers without an index; "
+                   "index_ms = the rest (Add, ForklessCause incl. cache hits, Flush, DropNotFlushed, merged HB)"}
+    if want_cpu:
+        from oracle import corc
+        ix = corc.OracleIndex(weights)
+        c = dropin.replay(dag, weights, claimed, kind="cpu", cpu=ix.c_funcs(), lru_pairs=20000, max_events=cpu_events)
+        assert np.array_equal(c["frames"], claimed[:cpu_events])
+        g = float(r["checkpoint_s"][cpu_events // 1000 - 1])
+        res["cpu_baseline"] = {
+            "value": c["events"] / c["seconds"], "unit": "events/s", "cores": 1, "kind": "port",
+            "sample": "first %d events of the epoch through the same caller driver over the C restatement of the "
+                      "index (oracle/csrc/oracle.c: per-event Add with DFS LowestAfter) behind the reference's "
+                      "ForklessCause LRU of 20000 pairs, in %.1fs (%d ForklessCause calls, %d LRU hits)"
+                      % (c["events"], c["seconds"], c["fc_calls"], c["lru_hits"]),
+            "gpu_seconds_same_prefix": g, "speedup_same_prefix": c["seconds"] / g}
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -355,6 +417,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--mode", default="shard", choices=["replica", "shard"])
     ap.add_argument("--no-abft", action="store_true", help="skip the configs[4] abft leg")
+    ap.add_argument("--no-dropin", action="store_true", help="skip the configs[4] drop-in (unchanged caller) leg")
     ap.add_argument("--no-latency", action="store_true", help="skip the per-call latency / antichain-fed leg")
     ap.add_argument("--no-configs", action="store_true", help="skip the secondary C1/C2/C4 lines")
     ap.add_argument("--shard-solo", type=int, default=0,
@@ -587,6 +650,9 @@ def main():
         ab["events_per_sec"] = ab["events"] * world / (ab["ms_per_step"] * 1e-3)
         ab["parallelism"] = "replica%d" % world
         result["abft"] = ab
+
+    if not args.no_dropin and world == 1 and not solo:
+        result["dropin_c5"] = dropin_leg(lx, local, rank == 0 and not args.no_cpu)
 
     if rank == 0 and world == 1 and not args.no_cpu:     # the CPU baseline is an N=1 figure
         sample_max = N

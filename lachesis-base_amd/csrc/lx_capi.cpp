@@ -943,160 +943,60 @@ int stage_slot(lx_index *h, uint64_t words, uint32_t **out, int *slot) {
     return 0;
 }
 
-// Add for a batch of at most small_max events, host pointers, unsharded handle.
-// Validation and branch assignment run on the host in Add order -- the
-// reference's own sequential fillGlobalBranchID (vecengine/index.go:105-141:
-// a root continues the creator's branch iff its lastSeq is 0, a self-parented
-// event continues its self-parent's branch iff lastSeq + 1 == seq, otherwise a
-// new branch) over the mirrored metadata -- with the checks and error codes of
-// k_validate_claim; the device work is one copy and one launch (k_small), and
-// nothing waits for it: errors are known before anything is enqueued.
-int add_batch_small(lx_index *h, uint32_t n, const uint32_t *creator, const uint32_t *seq, const uint64_t *poff,
-                    const uint32_t *par, uint32_t *out_branch, uint32_t *err_index) {
-    int rc;
-    if ((rc = hm_sync(h))) return rc;
-    const uint64_t bs = h->n_events;
-    for (uint32_t i = 0; i < n; i++) {
-        const uint64_t g = bs + i;
-        const uint32_t c = creator[i], s = seq[i];
-        const uint64_t p0 = poff[i], p1 = poff[i + 1];
-        int code = 0;
-        if (c >= h->V) {
-            code = LX_ERR_ARG;
-        } else if (s == 0 || s >= 0x7FFFFFFEu) {
-            code = LX_ERR_EVENT;
-        } else {
-            for (uint64_t x = p0; x < p1; x++)
-                if (par[x] >= g) { code = LX_ERR_ORDER; break; }
-            if (!code && s > 1) {
-                if (p1 == p0) {
-                    code = LX_ERR_EVENT;
-                } else {
-                    const uint32_t sp = par[p0];
-                    const uint32_t cs = sp < bs ? h->hm_creator[sp] : creator[sp - bs];
-                    const uint32_t ss = sp < bs ? h->hm_seq[sp] : seq[sp - bs];
-                    if (cs != c || ss + 1 != s) code = LX_ERR_EVENT;
-                }
-            }
-        }
-        if (code) {
-            if (err_index) *err_index = i;
-            if (code == LX_ERR_ORDER) return h->fail(code, "event %u: processed out of order, parent not found", i);
-            if (code == LX_ERR_ARG) return h->fail(code, "event %u: creator idx out of range", i);
-            return h->fail(code, "event %u: violates seq/self-parent invariants (eventcheck)", i);
-        }
-    }
+}  // namespace
 
-    const uint64_t npar = poff[n] - poff[0];
-    // image: records, parents, perm, level offsets (<= n + 1), new branches' first
-    // seqs and creators (<= n each), touched branches' (branch, length) (<= 2n)
+// Launch the pending run of small-path events [pend_bs, pend_bs + pend_n): the
+// staged image (records, parents, the run's topological levels, new branches,
+// touched branch lengths), one k_small, then the fork marks.  Every entry point
+// that reads the device state or enqueues after it calls this first.
+int flush_pending(lx_index *h) {
+    if (!h->pend_n) return 0;
+    const uint32_t n = h->pend_n;
+    const uint64_t bs = h->pend_bs;
+    const uint32_t B0 = h->pend_B0, B = h->B;
+    const uint64_t npar = h->pend_par.size();
+    const uint32_t L = h->pend_maxlvl + 1, nf = B - B0;
+    // branches the run touched (each once)
+    h->sm_touched.clear();
+    if (h->touch_mark.size() < B) h->touch_mark.resize(B, 0);
+    const uint32_t tm = ++h->touch_stamp;
+    for (uint32_t i = 0; i < n; i++) {
+        const uint32_t br = h->pend_ev[i].q0.x;
+        if (h->touch_mark[br] != tm) { h->touch_mark[br] = tm; h->sm_touched.push_back(br); }
+    }
+    const uint32_t n_blen = (uint32_t)h->sm_touched.size();
     const uint64_t w_ev = 12ull * n;
-    const uint64_t words = w_ev + npar + n + (n + 1) + 2ull * n + 2ull * n;
+    const uint64_t words = w_ev + npar + n + (L + 1) + 2ull * nf + 2ull * n_blen;
     uint32_t *img;
-    int slot = -1;
+    int slot = -1, rc;
     const bool inl = words <= kSmallInline;   // small enough for the kernel arguments
     if (inl) img = h->sm_inl.img;
     else if ((rc = stage_slot(h, words, &img, &slot))) return rc;
-    SmallEv *ev = reinterpret_cast<SmallEv *>(img);
+    memcpy(img, h->pend_ev.data(), w_ev * 4);
     uint32_t *ipar = img + w_ev;
-    if (npar) memcpy(ipar, par + poff[0], npar * 4);
-
-    h->wb_ready = false;
-    const uint32_t B0 = h->B;
-    uint32_t B = B0, max_level = 0, bmax = 0;
-    h->hm_creator.resize(bs + n);
-    h->hm_seq.resize(bs + n);
-    h->hm_branch.resize(bs + n);
-    h->hm_bbefore.resize(bs + n);
-    h->sm_level.resize(n);
-    h->sm_touched.clear();
-    for (uint32_t i = 0; i < n; i++) {
-        const uint64_t g = bs + i;
-        const uint32_t c = creator[i], s = seq[i];
-        const uint64_t p0 = poff[i], p1 = poff[i + 1];
-        const uint32_t sp = s > 1 ? par[p0] : LX_NONE;
-        uint32_t br = 0;
-        bool cont = false;
-        if (s > 1) {
-            const uint32_t bsp = h->hm_branch[sp];
-            const uint32_t len = h->hm_blen[bsp];
-            const uint32_t last = len ? h->h_branch_first[bsp] + len - 1 : 0;
-            if (last + 1 == s) { br = bsp; cont = true; }
-        } else if (h->hm_blen[c] == 0) {
-            br = c;
-            cont = true;
-        }
-        const uint32_t bb = B;
-        if (!cont) {
-            br = B++;
-            h->h_branch_first.push_back(s);
-            h->h_branch_creator.push_back(c);
-            h->by_creator[c].push_back(br);
-            h->hm_blen.push_back(0);
-        }
-        h->hm_blen[br] = s - h->h_branch_first[br] + 1;
-        h->hm_creator[g] = c;
-        h->hm_seq[g] = s;
-        h->hm_branch[g] = br;
-        h->hm_bbefore[g] = bb;
-        uint32_t lvl = 0;
-        for (uint64_t x = p0; x < p1; x++)
-            if (par[x] >= bs) lvl = std::max(lvl, h->sm_level[par[x] - bs] + 1);
-        h->sm_level[i] = lvl;
-        max_level = std::max(max_level, lvl);
-        bmax = std::max(bmax, s);
-        ev[i].q0 = make_uint4(br, s, (cont && s > 1) ? sp : LX_NONE, (uint32_t)(p1 - p0));
-        ev[i].q1 = make_uint4((uint32_t)(p0 - poff[0]), h->h_branch_first[br], sp, bb);
-        ev[i].q2 = make_uint4(c, cont ? kSmallCont : 0u, LX_NONE, 0u);
-        if (cont && sp != LX_NONE && sp >= bs) ev[sp - bs].q2.z = (uint32_t)g;
-        if (out_branch) out_branch[i] = br;
-        h->sm_touched.push_back(br);
-    }
-    // events by level (counting sort; batch order inside a level)
-    const uint32_t L = max_level + 1;
+    if (npar) memcpy(ipar, h->pend_par.data(), npar * 4);
+    // events by level (counting sort; Add order inside a level)
     uint32_t *perm = ipar + npar, *loff = perm + n;
     h->sm_cnt.assign(L + 1, 0);
-    for (uint32_t i = 0; i < n; i++) h->sm_cnt[h->sm_level[i] + 1]++;
+    for (uint32_t i = 0; i < n; i++) h->sm_cnt[h->pend_lvl[i] + 1]++;
     for (uint32_t l = 0; l < L; l++) h->sm_cnt[l + 1] += h->sm_cnt[l];
     for (uint32_t l = 0; l <= L; l++) loff[l] = h->sm_cnt[l];
-    for (uint32_t i = 0; i < n; i++) perm[h->sm_cnt[h->sm_level[i]]++] = i;
-    const uint32_t nf = B - B0;
+    for (uint32_t i = 0; i < n; i++) perm[h->sm_cnt[h->pend_lvl[i]]++] = i;
     uint32_t *nfirst = loff + L + 1, *ncreator = nfirst + nf, *blen = ncreator + nf;
     for (uint32_t x = 0; x < nf; x++) {
         nfirst[x] = h->h_branch_first[B0 + x];
         ncreator[x] = h->h_branch_creator[B0 + x];
     }
-    std::sort(h->sm_touched.begin(), h->sm_touched.end());
-    h->sm_touched.erase(std::unique(h->sm_touched.begin(), h->sm_touched.end()), h->sm_touched.end());
-    const uint32_t n_blen = (uint32_t)h->sm_touched.size();
     for (uint32_t x = 0; x < n_blen; x++) {
         blen[2 * x] = h->sm_touched[x];
         blen[2 * x + 1] = h->hm_blen[h->sm_touched[x]];
     }
-    const uint64_t used = (uint64_t)(blen + 2 * n_blen - img);
-
-    // capacity (rare re-layouts sync the stream); on failure the host mirror is rolled back
-    h->max_seq = std::max(h->max_seq, bmax);
-    if ((rc = grow_events(h, bs + n)) || (rc = grow_branches(h, B)) || (rc = grow_scap(h, h->max_seq))) {
-        h->h_branch_first.resize(B0);
-        h->h_branch_creator.resize(B0);
-        for (auto &l : h->by_creator)
-            while (!l.empty() && l.back() >= B0) l.pop_back();
-        h->hm_ok = false;
-        h->hm_n = std::min<uint64_t>(h->hm_n, bs);
-        return rc;
-    }
-    h->B = B;
-    h->pcols_used = std::max(h->pcols_used, B);
-    if (nf || h->ncols == 0)
-        if ((rc = rebuild_columns(h))) return rc;
     hipStream_t s = h->stream;
     if (!inl) {
-        HIPCHK(h, hipMemcpyAsync(h->st_dev, img, used * 4, hipMemcpyHostToDevice, s));
+        HIPCHK(h, hipMemcpyAsync(h->st_dev, img, words * 4, hipMemcpyHostToDevice, s));
         HIPCHK(h, hipEventRecord(h->st_done[slot], s));
         h->st_used[slot] = true;
     }
-
     SmallArgs &a = h->sm_inl.a;
     a = SmallArgs{};
     a.hb = h->hb;
@@ -1146,13 +1046,164 @@ int add_batch_small(lx_index *h, uint32_t n, const uint32_t *creator, const uint
         m.cheat_br = h->cheat_br;
         HIPCHK(h, lx::launch_marks(m, s));
     }
-    h->n_events += n;
-    h->hwm = std::max(h->hwm, h->n_events);
-    h->hm_n = h->n_events;
-    h->last_npar = npar;
+    h->pend_n = 0;
     h->stats = lx_stats{};
     h->stats.index_launches = 1;
     h->stats_lazy = h->small_timing;
+    return 0;
+}
+
+namespace {
+
+// flush_pending for a launch on stream s: a foreign stream is not ordered after
+// the handle's, so it waits for the run to finish
+int flush_before(lx_index *h, hipStream_t s) {
+    if (!h->pend_n) return 0;
+    int rc = flush_pending(h);
+    if (rc) return rc;
+    if (s != h->stream) HIPCHK(h, hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+// Add for a batch of at most small_max events, host pointers, unsharded handle.
+// Validation and branch assignment run on the host in Add order -- the
+// reference's own sequential fillGlobalBranchID (vecengine/index.go:105-141:
+// a root continues the creator's branch iff its lastSeq is 0, a self-parented
+// event continues its self-parent's branch iff lastSeq + 1 == seq, otherwise a
+// new branch) over the mirrored metadata -- with the checks and error codes of
+// k_validate_claim.  The batch joins the pending run of small-path events
+// (pend_*); the run is launched as one k_small (level by level inside the
+// kernel) when it reaches kPendLaunch events, or before anything reads or
+// orders after the device state (flush_pending).  Nothing waits: errors are
+// known before anything is enqueued, and a DropNotFlushed of events that are
+// still pending costs no device work at all.
+int add_batch_small(lx_index *h, uint32_t n, const uint32_t *creator, const uint32_t *seq, const uint64_t *poff,
+                    const uint32_t *par, uint32_t *out_branch, uint32_t *err_index) {
+    int rc;
+    if ((rc = hm_sync(h))) return rc;
+    const uint64_t bs = h->n_events;
+    for (uint32_t i = 0; i < n; i++) {
+        const uint64_t g = bs + i;
+        const uint32_t c = creator[i], s = seq[i];
+        const uint64_t p0 = poff[i], p1 = poff[i + 1];
+        int code = 0;
+        if (c >= h->V) {
+            code = LX_ERR_ARG;
+        } else if (s == 0 || s >= 0x7FFFFFFEu) {
+            code = LX_ERR_EVENT;
+        } else {
+            for (uint64_t x = p0; x < p1; x++)
+                if (par[x] >= g) { code = LX_ERR_ORDER; break; }
+            if (!code && s > 1) {
+                if (p1 == p0) {
+                    code = LX_ERR_EVENT;
+                } else {
+                    const uint32_t sp = par[p0];
+                    const uint32_t cs = sp < bs ? h->hm_creator[sp] : creator[sp - bs];
+                    const uint32_t ss = sp < bs ? h->hm_seq[sp] : seq[sp - bs];
+                    if (cs != c || ss + 1 != s) code = LX_ERR_EVENT;
+                }
+            }
+        }
+        if (code) {
+            if (err_index) *err_index = i;
+            if (code == LX_ERR_ORDER) return h->fail(code, "event %u: processed out of order, parent not found", i);
+            if (code == LX_ERR_ARG) return h->fail(code, "event %u: creator idx out of range", i);
+            return h->fail(code, "event %u: violates seq/self-parent invariants (eventcheck)", i);
+        }
+    }
+    // the run launches before it would outgrow one k_small (LDS: kSmallMaxN events)
+    if (h->pend_n && h->pend_n + n > kSmallMaxN && (rc = flush_pending(h))) return rc;
+    if (!h->pend_n) {
+        h->pend_bs = bs;
+        h->pend_B0 = h->B;
+        h->pend_maxlvl = 0;
+        h->pend_ev.clear();
+        h->pend_par.clear();
+        h->pend_lvl.clear();
+    }
+    const uint64_t pbs = h->pend_bs;
+    const uint32_t B0 = h->B, pn0 = h->pend_n;
+    const size_t par0 = h->pend_par.size();
+    uint32_t B = B0, bmax = 0;
+    h->hm_creator.resize(bs + n);
+    h->hm_seq.resize(bs + n);
+    h->hm_branch.resize(bs + n);
+    h->hm_bbefore.resize(bs + n);
+    h->pend_ev.resize(pn0 + n);
+    h->pend_lvl.resize(pn0 + n);
+    h->pend_par.insert(h->pend_par.end(), par + poff[0], par + poff[n]);
+    for (uint32_t i = 0; i < n; i++) {
+        const uint64_t g = bs + i;
+        const uint32_t c = creator[i], s = seq[i];
+        const uint64_t p0 = poff[i], p1 = poff[i + 1];
+        const uint32_t sp = s > 1 ? par[p0] : LX_NONE;
+        uint32_t br = 0;
+        bool cont = false;
+        if (s > 1) {
+            const uint32_t bsp = h->hm_branch[sp];
+            const uint32_t len = h->hm_blen[bsp];
+            const uint32_t last = len ? h->h_branch_first[bsp] + len - 1 : 0;
+            if (last + 1 == s) { br = bsp; cont = true; }
+        } else if (h->hm_blen[c] == 0) {
+            br = c;
+            cont = true;
+        }
+        const uint32_t bb = B;
+        if (!cont) {
+            br = B++;
+            h->h_branch_first.push_back(s);
+            h->h_branch_creator.push_back(c);
+            h->by_creator[c].push_back(br);
+            h->hm_blen.push_back(0);
+        }
+        h->hm_blen[br] = s - h->h_branch_first[br] + 1;
+        h->hm_creator[g] = c;
+        h->hm_seq[g] = s;
+        h->hm_branch[g] = br;
+        h->hm_bbefore[g] = bb;
+        uint32_t lvl = 0;
+        for (uint64_t x = p0; x < p1; x++)
+            if (par[x] >= pbs) lvl = std::max(lvl, h->pend_lvl[par[x] - pbs] + 1);
+        const uint32_t pi = pn0 + i;
+        h->pend_lvl[pi] = lvl;
+        h->pend_maxlvl = std::max(h->pend_maxlvl, lvl);
+        bmax = std::max(bmax, s);
+        SmallEv &e = h->pend_ev[pi];
+        e.q0 = make_uint4(br, s, (cont && s > 1) ? sp : LX_NONE, (uint32_t)(p1 - p0));
+        e.q1 = make_uint4((uint32_t)(par0 + (p0 - poff[0])), h->h_branch_first[br], sp, bb);
+        e.q2 = make_uint4(c, cont ? kSmallCont : 0u, LX_NONE, 0u);
+        if (cont && sp != LX_NONE && sp >= pbs) h->pend_ev[sp - pbs].q2.z = (uint32_t)g;
+        if (out_branch) out_branch[i] = br;
+    }
+    // capacity (rare re-layouts sync the stream; the pending run is not on the
+    // device yet); on failure the host mirror and the run are rolled back
+    h->max_seq = std::max(h->max_seq, bmax);
+    if ((rc = grow_events(h, bs + n)) || (rc = grow_branches(h, B)) || (rc = grow_scap(h, h->max_seq))) {
+        h->h_branch_first.resize(B0);
+        h->h_branch_creator.resize(B0);
+        for (auto &l : h->by_creator)
+            while (!l.empty() && l.back() >= B0) l.pop_back();
+        h->hm_ok = false;
+        h->hm_n = std::min<uint64_t>(h->hm_n, bs);
+        h->pend_ev.resize(pn0);
+        h->pend_lvl.resize(pn0);
+        h->pend_par.resize(par0);
+        for (uint32_t i = 0; i < pn0; i++)
+            if (h->pend_ev[i].q2.z != LX_NONE && h->pend_ev[i].q2.z >= bs) h->pend_ev[i].q2.z = LX_NONE;
+        return rc;
+    }
+    h->wb_ready = false;
+    h->B = B;
+    h->pcols_used = std::max(h->pcols_used, B);
+    if (B != B0 || h->ncols == 0)
+        if ((rc = rebuild_columns(h))) return rc;
+    h->n_events += n;
+    h->hwm = std::max(h->hwm, h->n_events);
+    h->hm_n = h->n_events;
+    h->last_npar = poff[n] - poff[0];
+    h->pend_n = pn0 + n;
+    if (h->pend_n >= kPendLaunch) return flush_pending(h);
     return 0;
 }
 
@@ -1260,6 +1311,7 @@ int lx_reset(lx_index *h, uint32_t nv, const uint32_t *w) {
     if (tot > 0x7FFFFFFFull) return h->fail(LX_ERR_ARG, "validators weight overflow");   // validators.go:101-110
     HIPCHK(h, set_dev(h->device));
     HIPCHK(h, hipStreamSynchronize(h->stream));
+    h->pend_n = 0;     // a pending run of the old epoch is simply forgotten
     h->wb_ready = false;
     h->V = nv;
     h->weights.assign(w, w + nv);
@@ -1378,6 +1430,7 @@ int lx_add_batch(lx_index *h, uint32_t n, const uint32_t *creator, const uint32_
     if (h->loading) return h->fail(LX_ERR_STATE, "lx_add_batch during a load (lx_load_finish first)");
     if (h->have_epoch && !h->sharded() && n <= std::min(h->small_max, kSmallMaxN))
         return add_batch_small(h, n, creator, seq, poff, par, out_branch, err_index);
+    if ((rc = flush_pending(h))) return rc;
     if ((rc = ensure_batch(h, n, npar))) return rc;
     HIPCHK(h, hipMemcpyAsync(h->b_creator, creator, n * 4ull, hipMemcpyHostToDevice, h->stream));
     HIPCHK(h, hipMemcpyAsync(h->b_seq, seq, n * 4ull, hipMemcpyHostToDevice, h->stream));
@@ -1393,6 +1446,10 @@ int lx_add_batch_dev(lx_index *h, uint32_t n, const uint32_t *creator, const uin
                      const uint32_t *par, uint32_t *err_index) {
     if (!h) return LX_ERR_ARG;
     HIPCHK(h, set_dev(h->device));
+    {
+        const int rc = flush_pending(h);
+        if (rc) return rc;
+    }
     return add_batch_dev(h, n, creator, seq, poff, par, err_index);
 }
 
@@ -1412,13 +1469,31 @@ int lx_drop_not_flushed(lx_index *h) {
     HIPCHK(h, set_dev(h->device));
     h->wb_ready = false;
     if (h->n_events == h->n_flushed && h->B == h->B_flushed) return 0;
-    HIPCHK(h, lx::launch_unfill(unfill_args(h), h->stream));
-    HIPCHK(h, lx::launch_zero_rows(h->hb, h->la, h->pstride, (uint32_t)h->n_flushed, (uint32_t)h->n_events, h->stream));
-    // re-added events may land on rows this epoch has not used yet (stale from an
-    // earlier epoch) with seqs the tail table already counts as done: start over
-    if (h->tail_zw && h->tail_dirty) {
-        HIPCHK(h, hipMemsetAsync(h->tail_zw, 0, (uint64_t)h->tail_cap * h->tail_cap * 4, h->stream));
-        h->tail_dirty = false;
+    if (h->pend_n && h->n_flushed >= h->pend_bs) {
+        // every dropped event is still in the pending run: it never reached the
+        // device, so the rollback is host-only (Build = Add + DropNotFlushed
+        // costs no launch)
+        const uint32_t keep = (uint32_t)(h->n_flushed - h->pend_bs);
+        h->pend_par.resize(h->pend_ev[keep].q1.x);
+        h->pend_ev.resize(keep);
+        h->pend_lvl.resize(keep);
+        h->pend_maxlvl = 0;
+        for (uint32_t i = 0; i < keep; i++) {
+            if (h->pend_ev[i].q2.z != LX_NONE && h->pend_ev[i].q2.z >= h->n_flushed) h->pend_ev[i].q2.z = LX_NONE;
+            h->pend_maxlvl = std::max(h->pend_maxlvl, h->pend_lvl[i]);
+        }
+        h->pend_n = keep;
+    } else {
+        int rc;
+        if ((rc = flush_pending(h))) return rc;
+        HIPCHK(h, lx::launch_unfill(unfill_args(h), h->stream));
+        HIPCHK(h, lx::launch_zero_rows(h->hb, h->la, h->pstride, (uint32_t)h->n_flushed, (uint32_t)h->n_events, h->stream));
+        // re-added events may land on rows this epoch has not used yet (stale from an
+        // earlier epoch) with seqs the tail table already counts as done: start over
+        if (h->tail_zw && h->tail_dirty) {
+            HIPCHK(h, hipMemsetAsync(h->tail_zw, 0, (uint64_t)h->tail_cap * h->tail_cap * 4, h->stream));
+            h->tail_dirty = false;
+        }
     }
     // host mirror: the same rollback of the branch lengths (k_unclaim) and rows
     if (h->hm_ok) {
@@ -1455,6 +1530,10 @@ int lx_writeback_prepare(lx_index *h, lx_writeback *out) {
     if (!h || !out) return LX_ERR_ARG;
     if (!h->have_epoch) return h->fail(LX_ERR_STATE, "write-back before lx_reset");
     NOT_LOADING(h);
+    {
+        const int rc = flush_pending(h);
+        if (rc) return rc;
+    }
     if (h->shard_count > 1) return h->fail(LX_ERR_STATE, "write-back needs an unsharded handle (shards hold partial rows)");
     HIPCHK(h, set_dev(h->device));
     h->wb_ready = false;
@@ -1532,6 +1611,7 @@ int lx_forkless_cause_batch_dev(lx_index *h, uint64_t n, const uint32_t *a, cons
     int rc = lx_fc_args(h, n, a, b, out, nullptr, &f);
     if (rc) return rc;
     hipStream_t s = stream ? (hipStream_t)stream : h->stream;
+    if ((rc = flush_before(h, s))) return rc;
     HIPCHK(h, lx::launch_fc(f, h->ncols, h->B > h->V, s));
     return 0;
 }
@@ -1544,6 +1624,7 @@ int lx_forkless_cause_partial_dev(lx_index *h, uint64_t n, const uint32_t *a, co
     int rc = lx_fc_args(h, n, a, b, nullptr, partial, &f);
     if (rc) return rc;
     hipStream_t s = stream ? (hipStream_t)stream : h->stream;
+    if ((rc = flush_before(h, s))) return rc;
     HIPCHK(h, lx::launch_fc(f, h->ncols, h->B > h->V, s));
     return 0;
 }
@@ -1559,6 +1640,10 @@ int lx_forkless_cause_batch(lx_index *h, uint64_t n, const uint32_t *a, const ui
     if (!h) return LX_ERR_ARG;
     if (!n) return 0;
     HIPCHK(h, set_dev(h->device));
+    {
+        const int rc = flush_pending(h);
+        if (rc) return rc;
+    }
     if (n <= kFcPinnedMax) {
         // per-call sizes (calcFrameIdx asks ~2/3 V pairs, the election |roots|):
         // the kernel reads the pairs from and writes the answers into pinned host
@@ -1665,6 +1750,10 @@ int get_check(lx_index *h, uint32_t n, const uint32_t *ev) {
     if (h->sharded()) return h->fail(LX_ERR_STATE, "vector getters need an unsharded handle (shards hold their own columns)");
     if (!h->have_epoch) return h->fail(LX_ERR_STATE, "getter before lx_reset");
     NOT_LOADING(h);
+    {
+        const int rc = flush_pending(h);
+        if (rc) return rc;
+    }
     for (uint32_t i = 0; i < n; i++)
         if (ev[i] >= h->n_events) return h->fail(LX_ERR_ARG, "unknown event %u", ev[i]);
     HIPCHK(h, set_dev(h->device));
@@ -1890,6 +1979,11 @@ int lx_last_stats(const lx_index *h, lx_stats *out) {
 
 int lx_device_planes(lx_index *h, void **hb, void **la, uint32_t *stride, void **stream) {
     if (!h) return LX_ERR_ARG;
+    HIPCHK(h, set_dev(h->device));
+    {
+        const int rc = flush_pending(h);   // the caller reads the planes in stream order after this
+        if (rc) return rc;
+    }
     if (hb) *hb = h->hb;
     if (la) *la = h->la;
     if (stride) *stride = h->pstride;
@@ -1900,6 +1994,10 @@ int lx_device_planes(lx_index *h, void **hb, void **la, uint32_t *stride, void *
 int lx_sync(lx_index *h) {
     if (!h) return LX_ERR_ARG;
     HIPCHK(h, set_dev(h->device));
+    {
+        const int rc = flush_pending(h);
+        if (rc) return rc;
+    }
     HIPCHK(h, hipStreamSynchronize(h->stream));
     uint32_t bad = 0;
     HIPCHK(h, hipMemcpy(&bad, h->status + 1, 4, hipMemcpyDeviceToHost));
@@ -2311,6 +2409,10 @@ int lx_load_finish(lx_index *h, const uint8_t *bi_rlp, uint32_t bi_len) {
 int lx_index_view(lx_index *h, IndexView *o) {
     if (!h || !o) return LX_ERR_ARG;
     if (!h->have_epoch) return h->fail(LX_ERR_STATE, "index has no epoch (lx_reset first)");
+    {
+        const int rc = flush_pending(h);   // abft and the emitter enqueue after the index's work
+        if (rc) return rc;
+    }
     o->stream = h->stream;
     o->device = h->device;
     o->hb = h->hb;

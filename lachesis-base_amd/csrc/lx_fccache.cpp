@@ -312,6 +312,8 @@ int fcc_query(lx_index *h, uint32_t a, uint32_t b, uint8_t *out) {
         return 0;
     }
     HIPCHK(h, set_dev(h->device));
+    int rc;
+    if ((rc = flush_pending(h))) return rc;   // the fills read rows of events the pending run adds
     uint32_t sa = c->find(a);
     const bool a_new = sa == LX_NONE;
     if (a_new) sa = c->insert(a, LX_NONE, LX_NONE);
@@ -321,7 +323,6 @@ int fcc_query(lx_index *h, uint32_t a, uint32_t b, uint8_t *out) {
         for (uint64_t e = (uint64_t)b + 1; e < (uint64_t)b + kWindow && e < h->n_events; e++)
             if (c->find((uint32_t)e) == LX_NONE) c->insert((uint32_t)e, sa, sb);
     }
-    int rc;
     if (a_new || a == c->last_a) rc = fcc_row(h, c, a, sa);
     else rc = fcc_tile(h, c);
     if (rc) return rc;

@@ -145,6 +145,15 @@ struct lx_index {
     std::vector<uint32_t> hm_creator, hm_seq, hm_branch, hm_bbefore;
     std::vector<uint32_t> hm_blen;         // per branch: events on it (= device branch_len)
     std::vector<uint32_t> sm_level, sm_cnt, sm_touched;   // scratch
+    // the pending run: small-path events assigned on the host but not launched
+    // yet, [pend_bs, pend_bs + pend_n), branches from pend_B0 (flush_pending)
+    uint32_t pend_n = 0, pend_B0 = 0, pend_maxlvl = 0;
+    uint64_t pend_bs = 0;
+    std::vector<SmallEv> pend_ev;          // records (q1.x = offset into pend_par)
+    std::vector<uint32_t> pend_par;        // parents, global indices
+    std::vector<uint32_t> pend_lvl;        // topological level inside the run
+    std::vector<uint32_t> touch_mark;      // per branch: stamp of the last run that touched it
+    uint32_t touch_stamp = 0;
     static constexpr int kSlots = 4;       // pinned staging images in flight
     uint32_t *st_pin[kSlots] = {};
     uint64_t st_pin_cap[kSlots] = {};
@@ -206,6 +215,7 @@ struct lx_index {
 // internal entry points shared by lx_capi.cpp and lx_fccache.cpp
 int lx_fc_args(lx_index *h, uint64_t n, const uint32_t *a, const uint32_t *b, uint8_t *out, uint32_t *partial,
                FcArgs *fa);
+int flush_pending(lx_index *h);                 // launch the pending small-path run (lx_capi.cpp)
 void fcc_destroy(lx_index *h);
 void fcc_clear(lx_index *h);                    // Reset: a new epoch
 void fcc_forget_from(lx_index *h, uint64_t n);  // DropNotFlushed: events >= n are gone

@@ -228,6 +228,7 @@ struct TailArgs {
 constexpr uint32_t kSmallCont = 1u;
 constexpr uint32_t kSmallCW = 4;     // columns per workgroup (256 threads = 4 columns x 64 event lanes)
 constexpr uint32_t kSmallMaxN = 3072;   // events per small batch (LDS: n x (kSmallCW + 1) x 4 B <= 64 KB)
+constexpr uint32_t kPendLaunch = 2048;  // a pending run of small batches launches at this size
 struct SmallEv {
     uint4 q0, q1, q2;
 };

@@ -101,7 +101,9 @@ extern "C" {
 //  10 getter batch of 64 merged HB rows (lx_get_merged_highest_before_batch)
 // then [33] antichain-fed events/s (levels added directly), [34] events fed,
 // [35] levels fed, [36] batcher-fed events/s (push a level, pop, add, flush),
-// [37] mean events per level.
+// [37] mean events per level; [40..42] lx_forkless_cause of a new event's
+// first pair (a cache miss: pending Add + row fill), [43..45] its next pairs
+// (hits).
 int lx_bench_latency(int device, uint32_t V, const uint32_t *weights, uint64_t N, const uint32_t *creator,
                      const uint32_t *seq, const uint64_t *poff, const uint32_t *par, uint64_t history,
                      uint32_t reps, uint64_t feed_events, double *out, char *err, uint32_t err_cap) {
@@ -227,6 +229,36 @@ int lx_bench_latency(int device, uint32_t V, const uint32_t *weights, uint64_t N
             if (lx_get_merged_highest_before_batch(h, 64, evs.data(), off.data(), buf.data(), buf.size()))
                 return fail("getter batch", h);
             t[10].push_back(us_since(t0));
+        }
+    }
+    // ForklessCause of one pair through lx_forkless_cause (the drop-in path):
+    // a new event's first question fills its row of the result cache (a miss:
+    // the pending Add and one row launch, waited for), the next ones are hits
+    {
+        std::vector<double> tm, th;
+        uint8_t o = 0;
+        for (uint32_t r = 0; r < reps && next < N; r++, next++) {
+            if (add(next, next + 1)) return fail("add (fc)", h);
+            lx_flush(h);
+            const uint32_t a = (uint32_t)next;
+            auto t0 = clk::now();
+            if (lx_forkless_cause(h, a, (uint32_t)rnd(next), &o)) return fail("fc pair", h);
+            tm.push_back(us_since(t0));
+            for (int k = 0; k < 8; k++) {
+                const uint32_t b = (uint32_t)rnd(next);
+                auto t1 = clk::now();
+                if (lx_forkless_cause(h, a, b, &o)) return fail("fc pair", h);
+                th.push_back(us_since(t1));
+            }
+        }
+        Stat sm = stat_of(tm), sh = stat_of(th);
+        out[40] = sm.p50; out[41] = sm.p99; out[42] = sm.mean;
+        out[43] = sh.p50; out[44] = sh.p99; out[45] = sh.mean;
+        while (lv + 1 < d.lvl_off.size() && d.lvl_off[lv + 1] <= next) lv++;
+        if (next < d.lvl_off[lv + 1] && lv + 1 < d.lvl_off.size()) {   // realign to a level boundary
+            if (add(next, d.lvl_off[lv + 1])) return fail("level", h);
+            lx_flush(h);
+            next = d.lvl_off[++lv];
         }
     }
     for (int k = 0; k < 11; k++) {

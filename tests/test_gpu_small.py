@@ -333,3 +333,47 @@ def test_vecfc_engine_shared_state(lx):
     for e in evs[:4]:
         g.add(e)
     assert g2.get_lowest_after(evs[0].id) is not None
+
+
+def test_pending_run_flush_drop_readd(lx):
+    """Small batches coalesce into a pending run that reaches the device only
+    when it grows to 2048 events or something reads the index: flushes in
+    between, DropNotFlushed of events still pending (host-only rollback,
+    including fork branches they opened), of events partly launched (a query
+    launched the run), and re-adds at the same dense indices -- rows, branch
+    IDs and FC equal the oracle's at every step."""
+    d = lx.tools.gen_dag(12, 80, 4, cheaters=3, forks=6, seed=17)
+    w = [3, 3, 3, 2, 2, 2, 2, 1, 1, 1, 1, 1]
+    N = len(d)
+    o = corc.OracleIndex(w)
+    ix = lx.Index()
+    ix.reset(w)
+    rng = np.random.default_rng(3)
+    e = 0
+    while e < N:
+        k = min(N - e, int(rng.integers(1, 40)))
+        br = ix.add_batch(d.creator[e:e + k], d.seq[e:e + k], d.poff[e:e + k + 1], d.par, want_branches=True)
+        for i in range(e, e + k):
+            assert o.add(int(d.creator[i]), int(d.seq[i]), d.par[d.poff[i]:d.poff[i + 1]]) == 0
+        assert [int(x) for x in br] == [o.branch(i) for i in range(e, e + k)]
+        r = rng.random()
+        if r < 0.25:                                  # drop what is not flushed (pending or launched)
+            if rng.random() < 0.5:
+                ix.highest_before(e)                  # a read launches the pending run first
+            ix.drop_not_flushed()
+            o.drop_not_flushed()
+            e = int(o.num_events())
+            assert ix.num_events() == e and ix.num_branches() == o.num_branches()
+            continue
+        if r < 0.7:
+            ix.flush()
+            o.flush()
+        e += k
+        if rng.random() < 0.2:
+            j = int(rng.integers(0, e))
+            assert ix.highest_before(j) == o.hb(j) and ix.lowest_after(j) == o.la(j)
+    ix.flush()
+    rows_equal(ix, o, range(N))
+    qa, qb = lx.tools.fc_queries(d.lamport, 50_000, window=24, seed=5)
+    np.testing.assert_array_equal(ix.forkless_cause_batch(qa, qb), o.forkless_cause_batch(qa, qb))
+    ix.close()
