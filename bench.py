@@ -153,7 +153,36 @@ def _bench_lib():
     L.lx_bench_feed.restype = ctypes.c_int
     L.lx_bench_feed.argtypes = [ctypes.c_int, ctypes.c_uint32, u32p, ctypes.c_uint64, u32p, u32p, u64p, u32p,
                                 ctypes.c_uint32, ctypes.POINTER(ctypes.c_double), ctypes.c_char_p, ctypes.c_uint32]
+    L.lx_bench_feed_levels.restype = ctypes.c_int
+    L.lx_bench_feed_levels.argtypes = [ctypes.c_int, ctypes.c_uint32, u32p, ctypes.c_uint64, u32p, u32p, u64p, u32p,
+                                       ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
+                                       ctypes.c_char_p, ctypes.c_uint32]
     return L
+
+
+def feed_levels(dag, weights, device, history=200_000, feed=1_000_000):
+    """C3 fed antichain by antichain (the DAG renumbered by topological level,
+    one lx_add_batch + lx_flush per level; or each level pushed into and popped
+    from lx_batcher first), after 100 untimed levels; one lx_sync at the end
+    (tools/lx_latency.cpp lx_bench_feed_levels).  Host seconds split between
+    the Adds and the batcher."""
+    import ctypes
+    import numpy as np
+    L = _bench_lib()
+    u32p, u64p = ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint64)
+    w = np.ascontiguousarray(weights, dtype=np.uint32)
+    res = {}
+    for mode, name in ((0, "direct"), (1, "batcher")):
+        out = (ctypes.c_double * 8)()
+        err = ctypes.create_string_buffer(512)
+        rc = L.lx_bench_feed_levels(device, len(w), w.ctypes.data_as(u32p), len(dag), dag.creator.ctypes.data_as(u32p),
+                                    dag.seq.ctypes.data_as(u32p), dag.poff.ctypes.data_as(u64p),
+                                    dag.par.ctypes.data_as(u32p), history, feed, mode, out, err, 512)
+        if rc != 0:
+            raise RuntimeError("lx_bench_feed_levels: " + err.value.decode())
+        res[name] = {"events_per_sec": out[0], "events": int(out[1]), "levels": int(out[2]), "add_s": out[3],
+                     "batcher_s": out[4], "final_sync_s": out[5]}
+    return res
 
 
 def feed_rate(dag, weights, device, batch):
@@ -636,6 +665,10 @@ def main():
     if not args.no_latency and world == 1 and not solo:
         ix.close()   # free the bench epoch's planes first
         result["latency"] = latency_leg(lx, dag, weights, local)
+        fl = feed_levels(dag, weights, local)
+        result["latency"]["antichain_fed_events_per_sec"] = fl["direct"]["events_per_sec"]
+        result["latency"]["batcher_fed_events_per_sec"] = fl["batcher"]["events_per_sec"]
+        result["latency"]["fed"] = fl
 
     if not args.no_configs and world == 1 and not solo:
         ix.close()

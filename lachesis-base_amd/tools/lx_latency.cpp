@@ -394,3 +394,128 @@ int lx_bench_feed(int device, uint32_t V, const uint32_t *weights, uint64_t N, c
 }
 
 }  // extern "C"
+
+extern "C" {
+
+// Level-fed throughput alone (for profiling): the DAG re-ordered by level,
+// `history` events added in one batch, 100 levels fed untimed, then levels fed one lx_add_batch +
+// lx_flush each (mode 0) or pushed / popped through lx_batcher (mode 1) for
+// up to feed_events events, one lx_sync at the end.  out[0] events/s, [1]
+// events, [2] levels, [3] seconds in lx_add_batch, [4] seconds in the batcher,
+// [5] seconds in the final lx_sync.
+int lx_bench_feed_levels(int device, uint32_t V, const uint32_t *weights, uint64_t N, const uint32_t *creator,
+                         const uint32_t *seq, const uint64_t *poff, const uint32_t *par, uint64_t history,
+                         uint64_t feed_events, int mode, double *out, char *err, uint32_t err_cap) {
+    Leveled d = by_level(N, creator, seq, poff, par);
+    uint64_t L0 = 0;
+    while (L0 + 1 < d.lvl_off.size() && d.lvl_off[L0 + 1] <= history) L0++;
+    const uint64_t H = d.lvl_off[L0];
+    lx_config cfg{};
+    cfg.device = device;
+    cfg.event_capacity = std::min<uint64_t>(N, H + feed_events + 100000);
+    lx_index *h = nullptr;
+    auto fail = [&](const char *what) {
+        snprintf(err, err_cap, "%s: %s", what, h ? lx_last_error(h) : "");
+        if (h) lx_destroy(h);
+        return -1;
+    };
+    if (lx_create(&cfg, &h) || lx_reset(h, V, weights)) return fail("create");
+    if (H && lx_add_batch(h, (uint32_t)H, d.creator.data(), d.seq.data(), d.poff.data(), d.par.data(), nullptr, nullptr))
+        return fail("history");
+    lx_flush(h);
+    if (lx_sync(h)) return fail("sync");
+    lx_batcher *b = nullptr;
+    std::vector<uint64_t> ids, pids, po, oid, opo;
+    std::vector<uint32_t> ocr, osq, opar, olv;
+    if (mode == 1) {
+        if (lx_batcher_create(&b)) return fail("batcher");
+        // the batcher's dense indices continue the epoch: the history as released events
+        ids.resize(H);
+        po.assign(1, 0);
+        for (uint64_t i = 0; i < H; i++) {
+            ids[i] = i + 1;
+            for (uint64_t k = d.poff[i]; k < d.poff[i + 1]; k++) pids.push_back((uint64_t)d.par[k] + 1);
+            po.push_back(pids.size());
+        }
+        uint32_t ne = 0, nl = 0, nw = 0;
+        uint64_t np = 0;
+        if (H) {
+            if (lx_batcher_push(b, (uint32_t)H, ids.data(), d.creator.data(), d.seq.data(), po.data(), pids.data(), nullptr) ||
+                lx_batcher_peek(b, &ne, &np, &nl, &nw))
+                return fail("batcher history");
+            oid.resize(ne + 1); ocr.resize(ne + 1); osq.resize(ne + 1); opo.resize(ne + 1);
+            opar.resize(np + 1); olv.resize(nl + 1);
+            if (lx_batcher_pop(b, oid.data(), ocr.data(), osq.data(), opo.data(), opar.data(), olv.data(), nullptr))
+                return fail("batcher history pop");
+        }
+    }
+    std::vector<uint64_t> lv_ids, lv_po, lv_pids;
+    uint64_t lv = L0;
+    uint64_t e0 = H;
+    double t_add = 0, t_bat = 0;
+    auto t0 = clk::now();
+    const uint64_t warm = 100;   // levels fed untimed first (kernel code objects, allocations)
+    for (uint64_t round = 0; round < 2; round++) {
+    if (round == 1) {
+        if (lx_sync(h)) return fail("sync");
+        e0 = d.lvl_off[lv];
+        t_add = t_bat = 0;
+        t0 = clk::now();
+    }
+    const uint64_t lv_end = round == 0 ? std::min<uint64_t>(lv + warm, d.lvl_off.size() - 1) : d.lvl_off.size() - 1;
+    while (lv < lv_end && d.lvl_off[lv + 1] - e0 <= feed_events) {
+        const uint64_t lo = d.lvl_off[lv], hi = d.lvl_off[lv + 1];
+        if (mode == 0) {
+            auto a0 = clk::now();
+            if (lx_add_batch(h, (uint32_t)(hi - lo), d.creator.data() + lo, d.seq.data() + lo, d.poff.data() + lo,
+                             d.par.data(), nullptr, nullptr))
+                return fail("feed");
+            lx_flush(h);
+            t_add += us_since(a0) * 1e-6;
+        } else {
+            lv_ids.resize(hi - lo);
+            lv_po.assign(1, 0);
+            lv_pids.clear();
+            for (uint64_t i = lo; i < hi; i++) {
+                lv_ids[i - lo] = i + 1;
+                for (uint64_t k = d.poff[i]; k < d.poff[i + 1]; k++) lv_pids.push_back((uint64_t)d.par[k] + 1);
+                lv_po.push_back(lv_pids.size());
+            }
+            auto a0 = clk::now();
+            uint32_t ne = 0, nl = 0, nw = 0;
+            uint64_t np = 0;
+            if (lx_batcher_push(b, (uint32_t)(hi - lo), lv_ids.data(), d.creator.data() + lo, d.seq.data() + lo,
+                                lv_po.data(), lv_pids.data(), nullptr) ||
+                lx_batcher_peek(b, &ne, &np, &nl, &nw))
+                return fail("batcher push");
+            if (oid.size() < ne + 1) { oid.resize(ne + 1); ocr.resize(ne + 1); osq.resize(ne + 1); opo.resize(ne + 1); }
+            if (opar.size() < np + 1) opar.resize(np + 1);
+            if (olv.size() < nl + 1) olv.resize(nl + 1);
+            if (lx_batcher_pop(b, oid.data(), ocr.data(), osq.data(), opo.data(), opar.data(), olv.data(), nullptr))
+                return fail("batcher pop");
+            auto a1 = clk::now();
+            if (ne && lx_add_batch(h, ne, ocr.data(), osq.data(), opo.data(), opar.data(), nullptr, nullptr))
+                return fail("batcher add");
+            lx_flush(h);
+            auto a2 = clk::now();
+            t_bat += std::chrono::duration<double>(a1 - a0).count();
+            t_add += std::chrono::duration<double>(a2 - a1).count();
+        }
+        lv++;
+    }
+    }
+    auto ts = clk::now();
+    if (lx_sync(h)) return fail("sync");
+    const double s = us_since(t0) * 1e-6;
+    out[0] = (d.lvl_off[lv] - e0) / s;
+    out[1] = (double)(d.lvl_off[lv] - e0);
+    out[2] = (double)(lv - L0);
+    out[3] = t_add;
+    out[4] = t_bat;
+    out[5] = us_since(ts) * 1e-6;
+    if (b) lx_batcher_destroy(b);
+    lx_destroy(h);
+    return 0;
+}
+
+}  // extern "C"
