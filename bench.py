@@ -185,6 +185,73 @@ def feed_levels(dag, weights, device, history=200_000, feed=1_000_000):
     return res
 
 
+def qi_leg(dag, weights, device, want_cpu, history=20_000, reps=2000, every=50, cands=64):
+    """The emitter's QuorumIndexer at V=1000 (emitter/ancestor/quorum_indexer.go:
+    86-136) on the HIP index, per call as the emitter makes them
+    (tools/lx_latency.cpp lx_bench_qi): after `history` events, each next event
+    is Added and handed to ProcessEvent alone; every `every`-th event
+    GetMetricOf for `cands` candidate parents (medians recomputed lazily, as
+    recacheState does).  The CPU line is the numpy port
+    (oracle/emitter_oracle.DenseQuorumIndexerNp over the C restatement's
+    merged rows) making the same calls; the last metric batch must agree."""
+    import ctypes
+    import numpy as np
+    L = _bench_lib()
+    u32p, u64p = ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint64)
+    L.lx_bench_qi.restype = ctypes.c_int
+    L.lx_bench_qi.argtypes = [ctypes.c_int, ctypes.c_uint32, u32p, ctypes.c_uint64, u32p, u32p, u64p, u32p,
+                              ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                              ctypes.POINTER(ctypes.c_double), u64p, ctypes.c_char_p, ctypes.c_uint32]
+    w = np.ascontiguousarray(weights, dtype=np.uint32)
+    out = (ctypes.c_double * 8)()
+    mo = np.zeros(cands, dtype=np.uint64)
+    err = ctypes.create_string_buffer(512)
+    rc = L.lx_bench_qi(device, len(w), w.ctypes.data_as(u32p), len(dag), dag.creator.ctypes.data_as(u32p),
+                       dag.seq.ctypes.data_as(u32p), dag.poff.ctypes.data_as(u64p), dag.par.ctypes.data_as(u32p),
+                       history, reps, every, cands, out, mo.ctypes.data_as(u64p), err, 512)
+    if rc != 0:
+        raise RuntimeError("lx_bench_qi: " + err.value.decode())
+    nlast = int(out[6])
+    res = {"unit": "us", "validators": len(w), "history_events": history, "events": reps, "metric_every": every,
+           "candidates": cands,
+           "process_event": {"p50": out[0], "p99": out[1], "mean": out[2]},
+           "metric_batch": {"p50": out[3], "p99": out[4], "mean": out[5]}}
+    if want_cpu:
+        from oracle import corc
+        from oracle.emitter_oracle import DenseQuorumIndexerNp
+        n = history + reps
+        ix = corc.OracleIndex(weights)
+        assert ix.add_batch(dag.creator[:n], dag.seq[:n], dag.poff[:n + 1], dag.par) == -1
+        ix.flush()
+        qi = DenseQuorumIndexerNp(weights, ix, cap=2)
+        for e in range(history):
+            qi.process_event(e, int(dag.creator[e]), dag.creator[e] == 0)
+        last = {}
+        for e in range(history):
+            last[int(dag.creator[e])] = e
+        tp, tm, got = [], [], None
+        for r in range(reps):
+            e = history + r
+            last[int(dag.creator[e])] = e
+            t0 = time.perf_counter()
+            qi.process_event(e, int(dag.creator[e]), dag.creator[e] == 0)
+            tp.append(time.perf_counter() - t0)
+            if every and r % every == every - 1:
+                cv = [last[c] for c in range(len(w)) if c in last][:cands]
+                t1 = time.perf_counter()
+                got = qi.metric_of(cv)
+                tm.append(time.perf_counter() - t1)
+        assert got is not None and np.array_equal(got, mo[:nlast]), "QuorumIndexer metric mismatch vs the CPU port"
+        res["metrics_checked"] = nlast
+        res["cpu_baseline"] = {"kind": "port", "cores": 1,
+                               "process_event_mean_us": float(np.mean(tp)) * 1e6,
+                               "metric_batch_mean_us": float(np.mean(tm)) * 1e6,
+                               "sample": "the same %d ProcessEvent and %d GetMetricOf batches on the numpy port "
+                                         "over oracle.c merged rows (same DAG prefix, already indexed)"
+                                         % (len(tp), len(tm))}
+    return res
+
+
 def feed_rate(dag, weights, device, batch):
     """Events/s adding the DAG in its Add order in batches of `batch` events
     (lx_add_batch + lx_flush each; 1 = per-event Add), tools/lx_latency.cpp."""
@@ -600,9 +667,25 @@ def main():
     t_fc = max_over_ranks(time.perf_counter() - t1)
     fc_kernel_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
 
-    # correctness spot check of this run's FC output against the index getters
-    out_host = d_out[:2000].cpu().numpy()
-    assert out_host.max() <= 1
+    # correctness spot check: this run's first 4096 ForklessCause answers
+    # recomputed on the host from the index's own HighestBefore / LowestAfter
+    # rows (reference byte layouts through the batched getters):
+    # sum of stakes over branches j with 0 < LA(b)[j] <= HB(a)[j].Seq >= quorum
+    # (vecfc/forkless_cause.go:63-82; the bench DAG has no forks)
+    spot_n = 0
+    if not (shard or solo):
+        import numpy as np
+        qa_s, qb_s = qa[:4096], qb[:4096]
+        got = d_out[:4096].cpu().numpy()
+        _, hbb = ix.rows_np(0, qa_s)
+        _, lab = ix.rows_np(1, qb_s)
+        hbs = hbb.view(np.uint32).reshape(len(qa_s), -1, 2)[:, :V, 0].astype(np.int64)
+        las = lab.view(np.uint32).reshape(len(qb_s), -1)[:, :V].astype(np.int64)
+        wv = np.asarray(weights, dtype=np.int64)
+        stake = (((las > 0) & (las <= hbs)) * wv).sum(axis=1)
+        want = (stake >= ix.quorum()).astype(np.uint8)
+        assert np.array_equal(got, want), "ForklessCause spot check failed"
+        spot_n = len(got)
 
     units = 1 if shard else world          # shard: the ranks share one epoch
     events_per_s = N * args.steps * units / t_index
@@ -654,6 +737,7 @@ def main():
                            "traffic": traffic["k_index"]["hbm_bytes"] if traffic else None,
                            "algorithmic_bytes_per_launch": idx_bytes, "kernel_ms": kidx},
         "host_gen_s": t_gen,
+        "fc_spot_checked": spot_n,
     }
     if shard or solo:
         wire = sorted(set(w for w in sx.last_wire[0] if w)) if shard and getattr(sx, "last_wire", None) else \
@@ -669,6 +753,7 @@ def main():
         result["latency"]["antichain_fed_events_per_sec"] = fl["direct"]["events_per_sec"]
         result["latency"]["batcher_fed_events_per_sec"] = fl["batcher"]["events_per_sec"]
         result["latency"]["fed"] = fl
+        result["quorum_indexer"] = qi_leg(dag, weights, local, rank == 0 and not args.no_cpu)
 
     if not args.no_configs and world == 1 and not solo:
         ix.close()
@@ -697,10 +782,8 @@ def main():
             "fc_value": nq / t_q, "fc_unit": "queries/s",
             "fc_value_mt": nq_mt / t_mt, "fc_threads": thr,
             "fc_sample_mt": "%d queries over the same prefix, OpenMP over queries, in %.2fs" % (nq_mt, t_mt),
-            "fc_value_all_cores_extrapolated": nq_mt / t_mt / thr * (os.cpu_count() or 1),
             "fc_mt_note": "timed on the job's CPU share (OMP_NUM_THREADS=%d of %d logical CPUs on the box; the "
-                          "pool's rule is to stay within the share); the all-cores figure scales the measured "
-                          "per-thread rate linearly, an upper bound" % (thr, os.cpu_count() or 1),
+                          "pool's rule is to stay within the share)" % (thr, os.cpu_count() or 1),
             "host": "%s, %d logical cpus" % (platform.processor() or platform.machine(), os.cpu_count()),
         }
     if rank == 0:

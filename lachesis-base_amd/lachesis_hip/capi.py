@@ -351,6 +351,19 @@ class Index:
         b = buf.tobytes()
         return [b[off[i]:off[i + 1]] for i in range(n)]
 
+    def rows_np(self, mode, evs):
+        """Rows of many events in one call, as numpy arrays (offsets[n + 1],
+        bytes): mode 0 HighestBefore, 1 LowestAfter, 2 merged HighestBefore."""
+        f = (self.L.lx_get_highest_before_batch, self.L.lx_get_lowest_after_batch,
+             self.L.lx_get_merged_highest_before_batch)[mode]
+        evs = _u32(evs)
+        n = len(evs)
+        off = np.zeros(n + 1, dtype=np.uint64)
+        self._chk(f(self.h, n, _p(evs, u32p), _p(off, u64p), None, 0))
+        buf = np.zeros(max(int(off[-1]), 1), dtype=np.uint8)
+        self._chk(f(self.h, n, _p(evs, u32p), _p(off, u64p), _p(buf, u8p), len(buf)))
+        return off, buf[:int(off[-1])]
+
     def highest_before_batch(self, evs):
         """lx_get_highest_before_batch: list of byte rows."""
         return self._rows(self.L.lx_get_highest_before_batch, evs)

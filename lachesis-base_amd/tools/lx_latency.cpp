@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "../../include/lachesis_batcher.h"
+#include "../../include/lachesis_emitter.h"
 #include "../../include/lachesis_hip.h"
 
 namespace {
@@ -514,6 +515,80 @@ int lx_bench_feed_levels(int device, uint32_t V, const uint32_t *weights, uint64
     out[4] = t_bat;
     out[5] = us_since(ts) * 1e-6;
     if (b) lx_batcher_destroy(b);
+    lx_destroy(h);
+    return 0;
+}
+
+}  // extern "C"
+
+extern "C" {
+
+// The emitter's QuorumIndexer (emitter/ancestor/quorum_indexer.go:86-136) on
+// the index, per call as the emitter uses it: the first `history` events
+// indexed, then for each of `reps` next events Add + ProcessEvent of that one
+// event (lx_qi_process_events n = 1; every event reaches the emitter), and
+// every `every`-th event GetMetricOf for `cands` candidate parents (the newest
+// event of `cands` validators; lx_qi_metric_of, the medians recomputed lazily
+// after the updates as recacheState does).  Validator 0 is the emitter (its
+// events are self events).  out[0..2] ProcessEvent p50 / p99 / mean us, [3..5]
+// metric batch p50 / p99 / mean us, [6] candidates in the last batch, whose
+// metrics land in last_metrics[cands] (the bench checks them on the CPU port).
+int lx_bench_qi(int device, uint32_t V, const uint32_t *weights, uint64_t N, const uint32_t *creator,
+                const uint32_t *seq, const uint64_t *poff, const uint32_t *par, uint64_t history, uint32_t reps,
+                uint32_t every, uint32_t cands, double *out, uint64_t *last_metrics, char *err,
+                uint32_t err_cap) {
+    lx_config cfg{};
+    cfg.device = device;
+    cfg.event_capacity = N;
+    lx_index *h = nullptr;
+    lx_qi *q = nullptr;
+    auto fail = [&](const char *what) {
+        snprintf(err, err_cap, "%s: %s", what, q ? lx_qi_last_error(q) : h ? lx_last_error(h) : "");
+        if (q) lx_qi_destroy(q);
+        if (h) lx_destroy(h);
+        return -1;
+    };
+    if (lx_create(&cfg, &h) || lx_reset(h, V, weights)) return fail("create");
+    if (lx_add_batch(h, (uint32_t)history, creator, seq, poff, par, nullptr, nullptr)) return fail("history");
+    lx_flush(h);
+    if (lx_qi_create(h, &q)) return fail("qi create");
+    {   // the emitter has seen the history (one batched call)
+        std::vector<uint32_t> ev(history);
+        std::vector<uint8_t> self(history);
+        for (uint64_t i = 0; i < history; i++) ev[i] = (uint32_t)i, self[i] = creator[i] == 0;
+        if (lx_qi_process_events(q, (uint32_t)history, ev.data(), self.data())) return fail("qi history");
+    }
+    std::vector<int64_t> last(V, -1);
+    for (uint64_t i = 0; i < history; i++) last[creator[i]] = (int64_t)i;
+    std::vector<double> tp, tm;
+    std::vector<uint32_t> cv;
+    std::vector<uint64_t> mo(cands);
+    for (uint32_t r = 0; r < reps && history + r < N; r++) {
+        const uint64_t e = history + r;
+        if (lx_add_batch(h, 1, creator + e, seq + e, poff + e, par, nullptr, nullptr)) return fail("add");
+        lx_flush(h);
+        last[creator[e]] = (int64_t)e;
+        const uint32_t ev = (uint32_t)e;
+        const uint8_t self = creator[e] == 0 ? 1 : 0;   // validator 0 is the emitter
+        auto t0 = clk::now();
+        if (lx_qi_process_events(q, 1, &ev, &self)) return fail("process event");
+        tp.push_back(us_since(t0));
+        if (every && r % every == every - 1) {
+            cv.clear();
+            for (uint32_t c = 0; c < V && cv.size() < cands; c++)
+                if (last[c] >= 0) cv.push_back((uint32_t)last[c]);
+            auto t1 = clk::now();
+            if (lx_qi_metric_of(q, (uint32_t)cv.size(), cv.data(), 2, mo.data())) return fail("metric");
+            tm.push_back(us_since(t1));
+            std::copy(mo.begin(), mo.begin() + cv.size(), last_metrics);
+            out[6] = (double)cv.size();
+        }
+    }
+    Stat a = stat_of(tp), b = stat_of(tm);
+    if (tm.empty()) out[6] = 0;
+    out[0] = a.p50; out[1] = a.p99; out[2] = a.mean;
+    out[3] = b.p50; out[4] = b.p99; out[5] = b.mean;
+    lx_qi_destroy(q);
     lx_destroy(h);
     return 0;
 }

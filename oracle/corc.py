@@ -44,6 +44,7 @@ def lib():
         for f in (L.orc_get_hb, L.orc_get_la, L.orc_get_merged_hb):
             f.argtypes = [ctypes.c_void_p, ctypes.c_uint32, u8p, ctypes.c_uint32, u32p]
         L.orc_forkless_cause.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32]
+        L.orc_get_rows.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64, u32p, u64p, u8p, ctypes.c_uint64]
         L.orc_forkless_cause_batch.argtypes = [ctypes.c_void_p, ctypes.c_uint64, u32p, u32p, u8p]
         L.orc_forkless_cause_batch_mt.argtypes = [ctypes.c_void_p, ctypes.c_uint64, u32p, u32p, u8p, ctypes.c_int]
         # abft_oracle.c
@@ -131,6 +132,16 @@ class OracleIndex:
 
     def merged_hb(self, ev):
         return self._row(self.L.orc_get_merged_hb, ev)
+
+    def rows(self, mode, evs):
+        """Rows of many events at once (mode 0 HighestBefore, 1 LowestAfter):
+        (offsets[n + 1], bytes) as numpy arrays."""
+        evs = np.ascontiguousarray(evs, dtype=np.uint32)
+        off = np.zeros(len(evs) + 1, dtype=np.uint64)
+        assert self.L.orc_get_rows(self.h, mode, len(evs), _p(evs, u32p), _p(off, u64p), None, 0) == 0
+        buf = np.zeros(max(int(off[-1]), 1), dtype=np.uint8)
+        assert self.L.orc_get_rows(self.h, mode, len(evs), _p(evs, u32p), _p(off, u64p), _p(buf, u8p), len(buf)) == 0
+        return off, buf[:int(off[-1])]
 
     def forkless_cause(self, a, b):
         return self.L.orc_forkless_cause(self.h, a, b)

@@ -387,6 +387,27 @@ int orc_get_la(void *h, uint32_t id, uint8_t *out, uint32_t cap, uint32_t *len) 
     return copy_row(tbl_get(&o->la, id), out, cap, len);
 }
 
+/* rows of n events (mode 0 HighestBefore, 1 LowestAfter) back to back:
+ * off[n + 1] byte offsets (always filled); out may be NULL to size; returns
+ * -1 on an unknown event or a short buffer */
+int orc_get_rows(void *h, int mode, uint64_t n, const uint32_t *ev, uint64_t *off, uint8_t *out, uint64_t cap) {
+    orc_t *o = h;
+    uint64_t k = 0;
+    off[0] = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        if (ev[i] >= o->n_events) return -1;
+        const row_t *r = tbl_get(mode ? &o->la : &o->hb, ev[i]);
+        const uint32_t len = r ? r->len : 0;
+        if (out) {
+            if (k + len > cap) return -1;
+            if (len) memcpy(out + k, r->p, len);
+        }
+        k += len;
+        off[i + 1] = k;
+    }
+    return 0;
+}
+
 /* GetMergedHighestBefore (index.go:235-250) + GatherFrom (vector_ops.go:81-96) */
 int orc_get_merged_hb(void *h, uint32_t id, uint8_t *out, uint32_t cap, uint32_t *len) {
     orc_t *o = h;

@@ -160,3 +160,67 @@ def parents_to_string(pp, name_of=str):
     if len(names) >= 3:
         names = names[:1] + sorted(names[1:])
     return "[" + ", ".join(names) + "]"
+
+
+class DenseQuorumIndexerNp:
+    """The same QuorumIndexer over a dense-index C oracle (``corc.OracleIndex``)
+    with numpy arrays and the capped metric built in -- the CPU timing baseline
+    of bench.py (a vectorised port: ProcessEvent writes one matrix column,
+    recacheState sorts every row at once, GetMetricOf evaluates the capped
+    difference over all validators).  ``weights`` in idx order; events are
+    dense indices.  Checked against ``QuorumIndexer`` by
+    tests/test_emitter_oracle.py."""
+
+    def __init__(self, weights, index, cap=2):
+        import numpy as np
+        self.np = np
+        self.w = np.asarray(weights, dtype=np.int64)
+        self.V = len(weights)
+        self.ix = index
+        self.cap = cap
+        self.quorum = int(self.w.sum()) * 2 // 3 + 1
+        self.matrix = np.zeros((self.V, self.V), dtype=np.int64)   # [validator, creator]
+        self.sp = np.zeros(self.V, dtype=np.int64)
+        self.median = np.zeros(self.V, dtype=np.int64)
+        self.dirty = True
+
+    def _seqs(self, ev):
+        """seqOf of the merged HighestBefore row (quorum_indexer.go:70-75)."""
+        np = self.np
+        r = np.frombuffer(self.ix.merged_hb(ev), dtype=np.uint32).reshape(-1, 2)[:self.V].astype(np.int64)
+        s = np.zeros(self.V, dtype=np.int64)
+        s[:len(r)] = r[:, 0]
+        fork = (r[:, 0] == 0) & (r[:, 1] == 0x7FFFFFFF)
+        s[:len(r)][fork] = FORK_SEQ
+        return s
+
+    def process_event(self, ev, creator, self_event):
+        s = self._seqs(ev)
+        self.matrix[:, creator] = s
+        if self_event:
+            self.sp[:] = s
+        self.dirty = True
+
+    def recache(self):
+        np = self.np
+        order = np.argsort(-self.matrix, axis=1, kind="stable")
+        ws = np.cumsum(self.w[order], axis=1)
+        k = np.argmax(ws >= self.quorum, axis=1)
+        self.median = np.take_along_axis(self.matrix, order, axis=1)[np.arange(self.V), k]
+        self.dirty = False
+
+    def metric_of(self, evs):
+        np = self.np
+        if self.dirty:
+            self.recache()
+        out = np.zeros(len(evs), dtype=np.uint64)
+        cap = self.cap
+        for i, ev in enumerate(evs):
+            u = self._seqs(ev)
+            m, cur = self.median, self.sp
+            d_um = np.minimum(u - m, cap) * self.w
+            d_cm = np.minimum(cur - m, cap) * self.w
+            val = np.where(m < cur, d_um - d_cm, d_um)
+            val = np.where((u <= m) | (u <= cur), 0, val)
+            out[i] = np.uint64(int(val.sum()) & 0xFFFFFFFFFFFFFFFF)
+        return out

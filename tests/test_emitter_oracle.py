@@ -61,3 +61,46 @@ def test_capped_metric_cases():
     assert fn(1, 0, 2, 1) == 5            # diff 1 * w
     assert fn(1, 0, 9, 1) == 10           # capped at 2 * w
     assert fn(1, 2, 9, 0) == 6 - 3        # median < current: cap(8) - cap(1)
+
+
+@pytest.mark.parametrize("forks", [0, 3])
+def test_numpy_quorum_indexer_matches_restatement(forks):
+    """The bench's CPU baseline (DenseQuorumIndexerNp) against the scalar
+    restatement's median / metric functions on the same merged rows."""
+    import numpy as np
+    from lachesis_hip import tools
+    from oracle import corc
+    V = 12
+    d = tools.gen_dag(V, 30, 4, cheaters=2 if forks else 0, forks=forks, seed=5)
+    w = [1 + (i % 4) * 3 for i in range(V)]
+    ix = corc.OracleIndex(w)
+    assert ix.add_batch(d.creator, d.seq, d.poff, d.par) == -1
+    ix.flush()
+    qi = eo.DenseQuorumIndexerNp(w, ix, cap=2)
+    quorum = sum(w) * 2 // 3 + 1
+    fn = eo.capped_metric(w, 2)
+    matrix = [[0] * V for _ in range(V)]
+    sp = [0] * V
+
+    def seqs(e):
+        r = np.frombuffer(ix.merged_hb(e), dtype=np.uint32).reshape(-1, 2)
+        return [eo.seq_of((int(r[i, 0]), int(r[i, 1]))) for i in range(V)]
+
+    checked = 0
+    for e in range(len(d)):
+        c = int(d.creator[e])
+        qi.process_event(e, c, c == 0)
+        s = seqs(e)
+        for i in range(V):
+            matrix[i][c] = s[i]
+            if c == 0:
+                sp[i] = s[i]
+        if e % 37 == 36:
+            med = [eo.wmedian_of(sorted(((matrix[i][k], w[k]) for k in range(V)), key=lambda p: -p[0]), quorum)[0]
+                   for i in range(V)]
+            cand = list(range(max(0, e - 20), e + 1))
+            want = [sum(fn(med[i], sp[i], seqs(x)[i], i) for i in range(V)) & 0xFFFFFFFFFFFFFFFF for x in cand]
+            assert list(qi.metric_of(cand)) == want
+            assert list(qi.median) == med
+            checked += len(cand)
+    assert checked > 100

@@ -364,15 +364,24 @@ def test_config3_shape_skewed(lx):
     np.testing.assert_array_equal(ix.forkless_cause_batch(qa, qb), o.forkless_cause_batch(qa, qb))
 
 
+def _rows_in_chunks(ix, o, mode, events, chunk):
+    """GPU and oracle rows of `events` (mode 0 HighestBefore, 1 LowestAfter),
+    chunk by chunk: yields (offsets, bytes) pairs of both."""
+    for lo in range(0, len(events), chunk):
+        ev = events[lo:lo + chunk]
+        yield ix.rows_np(mode, ev), o.rows(mode, ev)
+
+
 @pytest.mark.big_only
 def test_full_size_config3_prefix_vs_oracle(lx):
     """BASELINE configs[2] at full size (V=1000, Zipf stakes, 10M events, one
-    batch -- the bench workload) against the C oracle on the first 120k events:
-    HighestBefore rows of prefix events are final, so they must be identical;
-    a LowestAfter entry the oracle has already set can never change, so every
-    non-zero oracle entry must be identical; ForklessCause between prefix
-    events must be identical (an entry set after the prefix is larger than any
-    prefix seq of its branch, so it never counts)."""
+    batch -- the bench workload) against the C oracle on the first 500k
+    events, EVERY row: HighestBefore rows of prefix events are final, so they
+    must be byte-identical; LowestAfter: every entry the oracle has set is
+    final and must be identical, and an entry the oracle has not set must be 0
+    or come from an event after the prefix (a seq beyond the prefix's last seq
+    of that branch); ForklessCause of 1M pairs between prefix events must be
+    identical (an entry set after the prefix never counts for a prefix a)."""
     V = 1000
     w = [(1 << 20) // (i + 1) for i in range(V)]
     d = lx.tools.gen_dag(V, 10_000, 10, seed=1)
@@ -380,19 +389,48 @@ def test_full_size_config3_prefix_vs_oracle(lx):
     ix = lx.Index(event_capacity=N)
     ix.reset(w)
     ix.add_batch(d.creator, d.seq, d.poff, d.par)
-    P = 120_000
+    P = 500_000
     o = corc.OracleIndex(w)
     assert o.add_batch(d.creator[:P], d.seq[:P], d.poff[:P + 1], d.par) == -1
-    rng = np.random.default_rng(3)
-    for x in rng.choice(P, 300, replace=False):
-        x = int(x)
-        assert ix.highest_before(x) == o.hb(x), x
-        want = np.frombuffer(o.la(x), dtype=np.uint32)
-        got = np.frombuffer(ix.lowest_after(x), dtype=np.uint32)
-        nz = np.nonzero(want)[0]
-        assert np.array_equal(got[nz], want[nz]), x
-    qa, qb = lx.tools.fc_queries(d.lamport[:P], 200_000, seed=5)
-    np.testing.assert_array_equal(ix.forkless_cause_batch(qa, qb), o.forkless_cause_batch_mt(qa, qb, 8))
+    last = np.zeros(V, dtype=np.uint32)                    # last seq of each branch inside the prefix
+    np.maximum.at(last, d.creator[:P], d.seq[:P])
+    ev = np.arange(P, dtype=np.uint32)
+    for (go, gb), (oo, ob) in _rows_in_chunks(ix, o, 0, ev, 50_000):
+        np.testing.assert_array_equal(go, oo)
+        assert np.array_equal(gb, ob)
+    for (go, gb), (oo, ob) in _rows_in_chunks(ix, o, 1, ev, 50_000):
+        np.testing.assert_array_equal(go, oo)              # no forks: every LA row is 4 V bytes on both sides
+        g = gb.view(np.uint32).reshape(-1, V)
+        want = ob.view(np.uint32).reshape(-1, V)
+        set_ = want != 0
+        assert np.array_equal(g[set_], want[set_])
+        later = g[~set_]
+        assert np.all((later == 0) | (later > np.broadcast_to(last, g.shape)[~set_]))
+    qa, qb = lx.tools.fc_queries(d.lamport[:P], 1_000_000, seed=5)
+    np.testing.assert_array_equal(ix.forkless_cause_batch(qa, qb), o.forkless_cause_batch_mt(qa, qb, 16))
+    ix.close()
+
+
+@pytest.mark.big_only
+def test_full_size_config2_vs_oracle(lx):
+    """BASELINE configs[1] at full size (V=100, 1M events) against the C
+    oracle over the whole epoch: every HighestBefore row, every LowestAfter row
+    (byte-identical, lengths included) and 1M ForklessCause answers."""
+    V = 100
+    d = lx.tools.gen_dag(V, 10_000, 10, seed=1)
+    N = len(d)
+    ix = lx.Index(event_capacity=N)
+    ix.reset([1] * V)
+    ix.add_batch(d.creator, d.seq, d.poff, d.par)
+    o = corc.OracleIndex([1] * V)
+    assert o.add_batch(d.creator, d.seq, d.poff, d.par) == -1
+    ev = np.arange(N, dtype=np.uint32)
+    for mode in (0, 1):
+        for (go, gb), (oo, ob) in _rows_in_chunks(ix, o, mode, ev, 250_000):
+            np.testing.assert_array_equal(go, oo)
+            assert np.array_equal(gb, ob), mode
+    qa, qb = lx.tools.fc_queries(d.lamport, 1_000_000, window=64, seed=9)
+    np.testing.assert_array_equal(ix.forkless_cause_batch(qa, qb), o.forkless_cause_batch_mt(qa, qb, 16))
     ix.close()
 
 
