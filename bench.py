@@ -516,6 +516,9 @@ def main():
     ap.add_argument("--no-dropin", action="store_true", help="skip the configs[4] drop-in (unchanged caller) leg")
     ap.add_argument("--no-latency", action="store_true", help="skip the per-call latency / antichain-fed leg")
     ap.add_argument("--no-configs", action="store_true", help="skip the secondary C1/C2/C4 lines")
+    ap.add_argument("--segments", type=int, default=0,
+                    help="single GPU: walk the epoch as G Add-order segments + fix-up (option segments, the "
+                         "per-rank work of the row-segment multi-GPU mode timed segment by segment)")
     ap.add_argument("--shard-solo", type=int, default=0,
                     help="diagnostic: time rank 0 of a G-way column shard alone on this GPU (its index walk, "
                          "the packing of its outgoing LowestAfter blocks, its partial FC); no collectives")
@@ -582,7 +585,7 @@ def main():
         sx = ShardedIndex(ix, device=dev)
         d_part = torch.empty(args.fc_queries, dtype=torch.int32, device=dev)
     else:
-        ix = lx.Index(device=local, event_capacity=N)
+        ix = lx.Index(device=local, event_capacity=N, options={"segments": args.segments} if args.segments > 1 else None)
 
     st_x = []   # shard mode: LowestAfter all-to-all (pack + collective + unpack) per step, ms
 
@@ -739,6 +742,14 @@ def main():
         "host_gen_s": t_gen,
         "fc_spot_checked": spot_n,
     }
+    if args.segments > 1 and world == 1:
+        sg = ix.segment_stats()
+        rest = sg["partial_ms"] + sg["la_ms"]
+        sg["per_rank_estimate_ms"] = {"walk_max": max(sg["walk_ms"]), "fixup_share": rest / sg["segments"],
+                                      "assign_and_marks": float(np.mean(k_assign_ms))}
+        sg["note"] = ("one GPU, the segments walked one after another; a rank of the row-segment mode walks one "
+                      "segment and does 1/G of the fix-up and LowestAfter passes")
+        result["segments"] = sg
     if shard or solo:
         wire = sorted(set(w for w in sx.last_wire[0] if w)) if shard and getattr(sx, "last_wire", None) else \
             [ix.shard_wire_bytes()]

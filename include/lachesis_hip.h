@@ -73,6 +73,9 @@ const char *lx_last_error(const lx_index *h);
  *   "shard_wire" LowestAfter exchange width: 0 (auto), 2 or 4 bytes
  *   "timing"     1: HIP-event timing of latency-path launches (lx_last_stats)
  *   "fc_cache"   working set of lx_forkless_cause in events (0: no cache; default 4 V, 512..8192)
+ *   "segments"   G in 2..64: a batch of >= 64 G events is walked as G Add-order segments
+ *                and fixed up (the single-GPU form of the row-segment multi-GPU
+ *                protocol; results identical); 0/1 off
  * The library reads no environment variables. */
 int lx_set_option(lx_index *h, const char *name, int64_t value);
 
@@ -300,6 +303,18 @@ typedef struct lx_stats {
     uint32_t index_launches;
 } lx_stats;
 int lx_last_stats(const lx_index *h, lx_stats *out);
+
+/* Timings of the last segmented batch (option "segments"): per segment its
+ * first event, walk time and number of "partial" events (rows that needed
+ * the gathered fix-up); then the gathered fix-up and the LowestAfter pass. */
+typedef struct lx_seg_stats {
+    uint32_t segments;
+    uint32_t first_event[65];
+    uint32_t partial[64];
+    float walk_ms[64];
+    float partial_ms, la_ms;
+} lx_seg_stats;
+int lx_last_segment_stats(const lx_index *h, lx_seg_stats *out);
 
 /* Device views for benchmarks/tests (valid until the next add/reset). */
 int lx_device_planes(lx_index *h, void **hb, void **la, uint32_t *stride, void **stream);

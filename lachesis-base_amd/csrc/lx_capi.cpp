@@ -54,6 +54,11 @@ void free_all(lx_index *h) {
     for (void *p : lptrs)
         if (p) (void)hipFree(p);
     h->cheat_brl = h->cheat_crl = h->cmap = h->lap = h->wloc = nullptr;
+    void *gptrs[] = {h->seg_jt, h->seg_cnt, h->seg_mf, h->seg_plist};
+    for (void *p : gptrs)
+        if (p) (void)hipFree(p);
+    h->seg_jt = h->seg_cnt = h->seg_mf = h->seg_plist = nullptr;
+    h->seg_jt_cap = h->seg_cnt_cap = h->seg_mf_cap = h->seg_plist_cap = 0;
     h->fk_w = h->fk_c = h->fk_wch = nullptr;
     h->fk_cap = 0;
     h->fk_hi4 = 0;
@@ -419,6 +424,101 @@ BatchArgs batch_args(lx_index *h, uint32_t n, const uint32_t *creator, const uin
     return a;
 }
 
+template <typename T>
+int seg_grow(lx_index *h, T **p, uint64_t *cap, uint64_t need) {
+    if (*cap >= need && *p) return 0;
+    if (*p) {
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        (void)hipFree(*p);
+    }
+    HIPCHK(h, dalloc(p, need));
+    *cap = need;
+    return 0;
+}
+
+// The batch walked as h->segments Add-order segments, the partial events'
+// rows gathered, LowestAfter filled from the final rows (lx_segment.hip,
+// DESIGN.md section 6b).  `ia` is the batch's ordinary walk; timings into
+// seg_stats.
+int seg_walk(lx_index *h, IndexArgs ia, const uint32_t *poff, hipStream_t s) {
+    const uint32_t G = h->segments, n = ia.n, bs = ia.batch_start;
+    SegArgs a{};
+    a.hb = h->hb;
+    a.la = h->la;
+    a.stride = h->pstride;
+    a.B = h->B;
+    a.bs = bs;
+    a.n = n;
+    a.G = G;
+    for (uint32_t k = 0; k < G; k++) a.seg_lo[k] = bs + (uint32_t)((uint64_t)n * k / G / 64 * 64);
+    a.seg_lo[G] = bs + n;
+    a.ev_branch = h->ev_branch;
+    a.ev_seq = h->ev_seq;
+    a.branch_first = h->branch_first;
+    a.branch_len = h->branch_len;
+    a.brow = h->brow;
+    a.s_cap = h->s_cap;
+    int rc;
+    if ((rc = seg_grow(h, &h->seg_jt, &h->seg_jt_cap, (uint64_t)(G + 1) * h->B)) ||
+        (rc = seg_grow(h, &h->seg_cnt, &h->seg_cnt_cap, (uint64_t)h->B + kMaxSegments + 2)) ||
+        (rc = seg_grow(h, &h->seg_mf, &h->seg_mf_cap, (uint64_t)n)) ||
+        (rc = seg_grow(h, &h->seg_plist, &h->seg_plist_cap, (uint64_t)n)))
+        return rc;
+    a.jt = h->seg_jt;
+    a.cnt = h->seg_cnt;
+    a.pcount = h->seg_cnt + h->B;
+    a.pflag = h->seg_mf;
+    a.plist = h->seg_plist;
+    while (h->seg_ev.size() < 2 * G + 3) {
+        hipEvent_t e;
+        HIPCHK(h, hipEventCreate(&e));
+        h->seg_ev.push_back(e);
+    }
+    hipEvent_t *ev = h->seg_ev.data();
+    HIPCHK(h, lx::launch_seg_tables(a, s));
+    ia.seg = 1;
+    ia.ev_branch = h->ev_branch;
+    ia.ev_seq = h->ev_seq;
+    for (uint32_t k = 0; k < G; k++) {
+        IndexArgs sk = ia;
+        sk.batch_start = a.seg_lo[k];
+        sk.n = a.seg_lo[k + 1] - a.seg_lo[k];
+        sk.rec = ia.rec + (a.seg_lo[k] - bs);
+        sk.poff_in = poff + (a.seg_lo[k] - bs);
+        sk.seg_j = a.jt + (uint64_t)k * a.B;
+        sk.seg_flag = a.pflag + (a.seg_lo[k] - bs);
+        sk.seg_list = a.plist + (a.seg_lo[k] - bs);
+        sk.seg_count = a.pcount + k;
+        HIPCHK(h, hipEventRecord(ev[2 * k], s));
+        HIPCHK(h, lx::launch_index(sk, s));
+        HIPCHK(h, hipEventRecord(ev[2 * k + 1], s));
+    }
+    uint32_t pc[kMaxSegments + 2];
+    HIPCHK(h, hipMemcpyAsync(pc, a.pcount, (G + 2) * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(h, hipStreamSynchronize(s));
+    for (uint32_t k = 0; k < G; k++) HIPCHK(h, lx::launch_seg_partial(a, k, pc[k], s));
+    HIPCHK(h, hipEventRecord(ev[2 * G], s));
+    a.ev_lo = bs;
+    a.ev_hi = bs + n;
+    a.k_lo = pc[G];
+    a.k_hi = pc[G + 1];
+    HIPCHK(h, lx::launch_seg_la(a, s));
+    HIPCHK(h, hipEventRecord(ev[2 * G + 1], s));
+    HIPCHK(h, hipStreamSynchronize(s));
+    lx_seg_stats &st = h->seg_stats;
+    st = lx_seg_stats{};
+    st.segments = G;
+    for (uint32_t k = 0; k < G; k++) {
+        st.first_event[k] = a.seg_lo[k];
+        st.partial[k] = pc[k];
+        HIPCHK(h, hipEventElapsedTime(&st.walk_ms[k], ev[2 * k], ev[2 * k + 1]));
+    }
+    st.first_event[G] = a.seg_lo[G];
+    HIPCHK(h, hipEventElapsedTime(&st.partial_ms, ev[2 * G - 1], ev[2 * G]));
+    HIPCHK(h, hipEventElapsedTime(&st.la_ms, ev[2 * G], ev[2 * G + 1]));
+    return 0;
+}
+
 int add_batch_dev(lx_index *h, uint32_t n, const uint32_t *creator, const uint32_t *seq, const uint32_t *poff,
                   const uint32_t *par, uint32_t *err_index) {
     if (!h->have_epoch) return h->fail(LX_ERR_STATE, "lx_add_batch before lx_reset");
@@ -518,7 +618,11 @@ int add_batch_dev(lx_index *h, uint32_t n, const uint32_t *creator, const uint32
         HIPCHK(h, hipMemsetAsync(ia.prof, 0, prof_n * 8, s));
     }
     HIPCHK(h, hipEventRecord(h->ev[1], s));
-    HIPCHK(h, lx::launch_index(ia, s));
+    if (h->segments > 1 && !h->sharded() && n >= 64ull * h->segments) {
+        if ((rc = seg_walk(h, ia, poff, s))) return rc;
+    } else {
+        HIPCHK(h, lx::launch_index(ia, s));
+    }
     HIPCHK(h, hipEventRecord(h->ev[2], s));
     if (h->prof) {
         std::vector<unsigned long long> pv(prof_n);
@@ -1257,6 +1361,7 @@ void lx_destroy(lx_index *h) {
         if (e) (void)hipEventDestroy(e);
     for (auto &e : h->st_done)
         if (e) (void)hipEventDestroy(e);
+    for (auto &e : h->seg_ev) (void)hipEventDestroy(e);
     for (auto *p : h->st_pin)
         if (p) (void)hipHostFree(p);
     if (h->st_dev) (void)hipFree(h->st_dev);
@@ -1289,6 +1394,10 @@ int lx_set_option(lx_index *h, const char *name, int64_t value) {
         h->wire_force = (uint32_t)value;
     } else if (k == "timing") {
         h->small_timing = value != 0;
+    } else if (k == "segments") {
+        if (value < 0 || value > (int64_t)kMaxSegments) return h->fail(LX_ERR_ARG, "segments must be 0..%u", kMaxSegments);
+        if (value > 1 && h->sharded()) return h->fail(LX_ERR_STATE, "segments on a column shard");
+        h->segments = (uint32_t)value;
     } else if (k == "fc_cache") {
         if (value < 0 || value > 16384) return h->fail(LX_ERR_ARG, "fc_cache must be 0..16384");
         fcc_destroy(h);
@@ -1988,6 +2097,12 @@ int lx_device_planes(lx_index *h, void **hb, void **la, uint32_t *stride, void *
     if (la) *la = h->la;
     if (stride) *stride = h->pstride;
     if (stream) *stream = h->stream;
+    return 0;
+}
+
+int lx_last_segment_stats(const lx_index *h, lx_seg_stats *out) {
+    if (!h || !out) return LX_ERR_ARG;
+    *out = h->seg_stats;
     return 0;
 }
 

@@ -189,6 +189,12 @@ struct lx_index {
     FcCache *fcc = nullptr;                // per-pair ForklessCause result cache (lx_fccache.cpp)
     uint32_t fcc_slots = 4096;             // option fc_cache: its working set (0 = no cache)
     bool fcc_slots_set = false;            // set by the option (else sized at lx_reset from V)
+    // segmented walk (option segments, lx_segment.hip): scratch and timings of the last batch
+    uint32_t segments = 0;
+    uint32_t *seg_jt = nullptr, *seg_cnt = nullptr, *seg_mf = nullptr, *seg_plist = nullptr;   // seg_mf: partial flags
+    uint64_t seg_jt_cap = 0, seg_cnt_cap = 0, seg_mf_cap = 0, seg_plist_cap = 0;
+    std::vector<hipEvent_t> seg_ev;
+    lx_seg_stats seg_stats{};
 
     int fail(int code, const char *fmt, ...) {
         char buf[512];

@@ -61,6 +61,15 @@ struct IndexArgs {
     uint32_t *lap;               // sharded: LowestAfter rows of own branches (fill target)
     uint64_t lap_stride;         // = global branch capacity
     uint32_t pack16;             // every seq of the epoch <= 0xFFFF: 16-B packed slots (4-column block walker)
+    // segment walk (lx_segment.hip): parents before batch_start contribute only
+    // their own (branch, seq) entry, and no LowestAfter is filled
+    uint32_t seg;
+    const uint32_t *ev_branch;
+    const uint32_t *ev_seq;
+    const uint32_t *seg_j;       // J_k: last seq of each branch before the segment
+    uint32_t *seg_flag;          // per segment event: set when its row misses some J_k (a "partial" event)
+    uint32_t *seg_list;          // partial events (global index), appended
+    uint32_t *seg_count;
 };
 constexpr int kProfSlots = 16;   // see k_index: passes, spin misses, chunk folds, completes, ...
 constexpr int kProfWaves = 16;   // waves per workgroup in the counter layout
@@ -414,8 +423,43 @@ struct VoteArgs {
     uint32_t *err;
 };
 
+// Segmented walk of one batch (lx_segment.hip): the
+// batch [bs, bs + n) split into G Add-order segments seg_lo[k] .. seg_lo[k+1],
+// each walked with its boundary parents as own entries only (IndexArgs::seg),
+// then fixed up to the reference's rows.
+constexpr uint32_t kMaxSegments = 64;
+struct SegArgs {
+    uint32_t *hb;
+    uint32_t *la;
+    uint64_t stride;
+    uint32_t B;                  // branches after the batch
+    uint32_t bs, n, G;
+    uint32_t seg_lo[kMaxSegments + 1];
+    const uint32_t *ev_branch;
+    const uint32_t *ev_seq;
+    const uint32_t *branch_first;
+    const uint32_t *branch_len;
+    const uint32_t *brow;
+    uint32_t s_cap;
+    uint32_t *jt;                // [(G + 1) * B]: row k = J_k, last seq of each branch before segment k
+    uint32_t *cnt;               // [B] batch events per branch, then [G] partial counts
+    uint32_t *pflag;             // [n] partial flags (k_index drains)
+    uint32_t *plist;             // partial events of segment k at plist[seg_lo[k] - bs ..]
+    uint32_t *pcount;            // [G]
+    // LowestAfter pass (k_seg_la): events [ev_lo, ev_hi) fill, at chain positions [k_lo, k_hi)
+    uint32_t ev_lo, ev_hi;
+    uint32_t k_lo, k_hi;
+    uint32_t own_lo;             // rows below it are another rank's: their entries go to `out` as (row, column, seq)
+    uint32_t *out;
+    uint32_t *out_count;
+    uint64_t out_cap;            // triples
+};
+
 // kernel launchers (lx_kernels.hip); all enqueue on `s`
 namespace lx {
+hipError_t launch_seg_tables(const SegArgs &a, hipStream_t s);
+hipError_t launch_seg_partial(const SegArgs &a, uint32_t k, uint32_t count, hipStream_t s);
+hipError_t launch_seg_la(const SegArgs &a, hipStream_t s);
 hipError_t launch_batch_prepare(const BatchArgs &a, void *scan_tmp, size_t scan_tmp_bytes, hipStream_t s);
 hipError_t launch_batch_finish(const BatchArgs &a, uint32_t jump_rounds, hipStream_t s);
 hipError_t launch_small(const SmallArgs &a, hipStream_t s);

@@ -633,6 +633,9 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
         // ------------------------------------------------------------ drain
         const uint32_t d = wave - NCW - 1;
         uint32_t nd = 0;                 // rounds of this wave completed
+        uint32_t sj[CPW];                // segment walk: J_k of the slice's columns
+#pragma unroll
+        for (int k = 0; k < CPW; k++) sj[k] = a.seg && valid[k] ? a.seg_j[col[k]] : 0u;
 #ifdef LX_WALKER_PROF
         uint32_t d_spin = 0, d_fill = 0, d_miss = 0;
         const unsigned long long dt0 = wall_clock64();
@@ -705,6 +708,14 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
             if (lane == 0) __hip_atomic_store(&sh.copied[d], nd + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             if (ev < n) {
                 const uint32_t *r = me.v;
+                if (a.seg) {
+                    // segment walk: an event whose row misses the last pre-segment
+                    // event of some branch is "partial" (lx_segment.hip fixes it up)
+                    bool unc = false;
+#pragma unroll
+                    for (int k = 0; k < CPW; k++) unc |= valid[k] && (r[k] & mask) < sj[k];
+                    if (unc && atomicOr(a.seg_flag + ev, 1u) == 0u) a.seg_list[atomicAdd(a.seg_count, 1u)] = bs + ev;
+                }
                 // HB row (raw values incl. fork bits as published)
                 uint32_t *hrow = a.hb + (uint64_t)(bs + ev) * stride;
                 if (contig) {
@@ -723,7 +734,7 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
 #pragma unroll
                     for (int k = 0; k < CPW; k++) {
                         lo[k] = max(h0[k] + 1u, first[k]);
-                        hi[k] = valid[k] ? (r[k] & mask) : 0u;
+                        hi[k] = valid[k] && !a.seg ? (r[k] & mask) : 0u;
                     }
                     if (a.lap) {
                         // sharded: rows of own branches addressed by (column, seq)
@@ -861,10 +872,18 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
                     for (int k = 0; k < 3; k++) {
                         if (j + 4 * k >= np || w[k] - bs < n) continue;
                         LX_WP(c_slow++;)
-                        const uint32_t *row = a.hb + (uint64_t)w[k] * stride;
+                        if (a.seg) {
+                            // segment walk: a boundary parent is its own entry only
+                            const uint32_t pb = a.ev_branch[w[k]], ps = a.ev_seq[w[k]];
 #pragma unroll
-                        for (int c = 0; c < CPW; c++)
-                            if (valid[c]) r[c] = max(r[c], ld_l2_now(row + pc[c]) & mask);
+                            for (int c = 0; c < CPW; c++)
+                                if (valid[c] && col[c] == pb) r[c] = max(r[c], ps);
+                        } else {
+                            const uint32_t *row = a.hb + (uint64_t)w[k] * stride;
+#pragma unroll
+                            for (int c = 0; c < CPW; c++)
+                                if (valid[c]) r[c] = max(r[c], ld_l2_now(row + pc[c]) & mask);
+                        }
                         px[k] = kNullTag;
                         pa[k] = ANULL;
                     }
@@ -955,7 +974,13 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
                         else __hip_atomic_store(&sh.req, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     }
                 }
-                if (old) {
+                if (old && a.seg && lpp >= n) {
+                    const uint32_t pb = a.ev_branch[pg], ps = a.ev_seq[pg];
+#pragma unroll
+                    for (int c = 0; c < CPW; c++)
+                        if (valid[c] && col[c] == pb) r[c] = max(r[c], ps);
+                    ok = true;
+                } else if (old) {
                     const uint32_t *row = a.hb + (uint64_t)pg * stride;
 #pragma unroll
                     for (int c = 0; c < CPW; c++)

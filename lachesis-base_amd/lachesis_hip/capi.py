@@ -59,6 +59,7 @@ SIGNATURES = [
     ("lx_la_pack_wire_dev", ctypes.c_int, [vp, ctypes.c_uint32, vp, ctypes.c_uint32]),
     ("lx_la_unpack_wire_dev", ctypes.c_int, [vp, ctypes.c_uint32, vp, ctypes.c_uint32]),
     ("lx_last_stats", ctypes.c_int, [vp, vp]),
+    ("lx_last_segment_stats", ctypes.c_int, [vp, vp]),
     ("lx_device_planes", ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), u32p, ctypes.POINTER(vp)]),
     ("lx_sync", ctypes.c_int, [vp]),
     ("lx_shard_comm_unique_id", ctypes.c_int, [u8p]),
@@ -120,6 +121,11 @@ class LxFcStats(ctypes.Structure):
     _fields_ = [("calls", ctypes.c_uint64), ("hits", ctypes.c_uint64), ("row_fills", ctypes.c_uint64),
                 ("tile_fills", ctypes.c_uint64), ("pairs", ctypes.c_uint64), ("slots", ctypes.c_uint32),
                 ("slots_used", ctypes.c_uint32)]
+
+
+class LxSegStats(ctypes.Structure):
+    _fields_ = [("segments", ctypes.c_uint32), ("first_event", ctypes.c_uint32 * 65), ("partial", ctypes.c_uint32 * 64),
+                ("walk_ms", ctypes.c_float * 64), ("partial_ms", ctypes.c_float), ("la_ms", ctypes.c_float)]
 
 
 class LxWriteback(ctypes.Structure):
@@ -434,6 +440,14 @@ class Index:
         st = LxStats()
         self._chk(self.L.lx_last_stats(self.h, ctypes.byref(st)))
         return {"ms_assign": st.ms_assign, "ms_index": st.ms_index, "ms_marks": st.ms_marks}
+
+    def segment_stats(self):
+        """Timings of the last segmented batch (option "segments")."""
+        st = LxSegStats()
+        self._chk(self.L.lx_last_segment_stats(self.h, ctypes.byref(st)))
+        G = st.segments
+        return {"segments": G, "first_event": list(st.first_event[:G + 1]), "partial": list(st.partial[:G]),
+                "walk_ms": list(st.walk_ms[:G]), "partial_ms": st.partial_ms, "la_ms": st.la_ms}
 
     def device_planes(self):
         hb, la, st = vp(), vp(), vp()
