@@ -73,6 +73,8 @@ const char *lx_last_error(const lx_index *h);
  *   "shard_wire" LowestAfter exchange width: 0 (auto), 2 or 4 bytes
  *   "timing"     1: HIP-event timing of latency-path launches (lx_last_stats)
  *   "fc_cache"   working set of lx_forkless_cause in events (0: no cache; default 4 V, 512..8192)
+ *   "seg_count", "seg_rank"  G in 2..64 and r < G, before lx_reset: a row-segment rank
+ *                (lx_rowseg_*, below); 0 = off
  *   "segments"   G in 2..64: a batch of >= 64 G events is walked as G Add-order segments
  *                and fixed up (the single-GPU form of the row-segment multi-GPU
  *                protocol; results identical); 0/1 off
@@ -315,6 +317,39 @@ typedef struct lx_seg_stats {
     float partial_ms, la_ms;
 } lx_seg_stats;
 int lx_last_segment_stats(const lx_index *h, lx_seg_stats *out);
+
+/* Row segments: the segmented walk spread over G ranks, one GPU each
+ * (DESIGN.md section 6b).  A handle with options seg_count = G, seg_rank = r
+ * takes the epoch as ONE lx_add_batch(_dev) of n >= 64 G events; it assigns
+ * every event's branch (replicated metadata) but walks and owns only the rows
+ * of segment r, [lo, hi) (lx_rowseg_range).  The caller then runs two
+ * exchanges with its collectives (lachesis_hip/rowseg.py):
+ *   rows, in rounds until no rank has requests left:
+ *     lx_rowseg_requests  -> the ids of the rows this rank still needs into a
+ *                            device buffer (lx_rowseg_request_cap ids),
+ *                            grouped by owner rank, counts[G];
+ *     (ids to their owners) lx_rowseg_serve -> rows (lx_rowseg_row_words
+ *                            words each) and ready flags (0: not final yet);
+ *     (rows back)          lx_rowseg_receive -> *remaining;
+ *   LowestAfter: lx_rowseg_la -> counts[G] of (row, column, seq) triples for
+ *     each owner rank, lx_rowseg_la_fetch copies them (grouped by owner) to a
+ *     device buffer; each owner lx_rowseg_la_apply's what it gets;
+ * then lx_rowseg_finish.  After it, ForklessCause answers queries between own
+ * events (others are LX_ERR_ARG); getters, write-back, DropNotFlushed and the
+ * abft / emitter views need a whole index (LX_ERR_STATE).  Every call has
+ * completed on the device when it returns. */
+int lx_rowseg_range(const lx_index *h, uint32_t *lo, uint32_t *hi);
+int lx_rowseg_bounds(const lx_index *h, uint32_t *lo /* G + 1 */);
+int lx_rowseg_row_words(const lx_index *h, uint32_t *words);
+int lx_rowseg_request_cap(const lx_index *h, uint32_t *cap);
+int lx_rowseg_requests(lx_index *h, uint32_t *ids_dev, uint32_t cap, uint32_t *counts);
+int lx_rowseg_serve(lx_index *h, uint32_t n, const uint32_t *ids_dev, uint32_t *rows_dev, uint32_t *ready_dev);
+int lx_rowseg_receive(lx_index *h, uint32_t n, const uint32_t *ids_dev, const uint32_t *rows_dev,
+                      const uint32_t *ready_dev, uint32_t *remaining);
+int lx_rowseg_la(lx_index *h, uint64_t *counts);
+int lx_rowseg_la_fetch(lx_index *h, uint32_t *triples_dev);
+int lx_rowseg_la_apply(lx_index *h, uint64_t n, const uint32_t *triples_dev);
+int lx_rowseg_finish(lx_index *h);
 
 /* Device views for benchmarks/tests (valid until the next add/reset). */
 int lx_device_planes(lx_index *h, void **hb, void **la, uint32_t *stride, void **stream);

@@ -20,6 +20,11 @@ using namespace lxi;
     do {                                                                                          \
         if ((h)->loading) return (h)->fail(LX_ERR_STATE, "index is loading (lx_load_finish first)"); \
     } while (0)
+// entry points that read whole rows of any event: not on a row-segment rank
+#define WHOLE_INDEX(h)                                                                            \
+    do {                                                                                          \
+        if ((h)->rowseg()) return (h)->fail(LX_ERR_STATE, "needs a whole index (a row-segment rank holds its own rows)"); \
+    } while (0)
 
 namespace {
 
@@ -59,6 +64,7 @@ void free_all(lx_index *h) {
         if (p) (void)hipFree(p);
     h->seg_jt = h->seg_cnt = h->seg_mf = h->seg_plist = nullptr;
     h->seg_jt_cap = h->seg_cnt_cap = h->seg_mf_cap = h->seg_plist_cap = 0;
+    rs_free(h);
     h->fk_w = h->fk_c = h->fk_wch = nullptr;
     h->fk_cap = 0;
     h->fk_hi4 = 0;
@@ -424,18 +430,6 @@ BatchArgs batch_args(lx_index *h, uint32_t n, const uint32_t *creator, const uin
     return a;
 }
 
-template <typename T>
-int seg_grow(lx_index *h, T **p, uint64_t *cap, uint64_t need) {
-    if (*cap >= need && *p) return 0;
-    if (*p) {
-        HIPCHK(h, hipStreamSynchronize(h->stream));
-        (void)hipFree(*p);
-    }
-    HIPCHK(h, dalloc(p, need));
-    *cap = need;
-    return 0;
-}
-
 // The batch walked as h->segments Add-order segments, the partial events'
 // rows gathered, LowestAfter filled from the final rows (lx_segment.hip,
 // DESIGN.md section 6b).  `ia` is the batch's ordinary walk; timings into
@@ -458,11 +452,12 @@ int seg_walk(lx_index *h, IndexArgs ia, const uint32_t *poff, hipStream_t s) {
     a.branch_len = h->branch_len;
     a.brow = h->brow;
     a.s_cap = h->s_cap;
+    a.own_seg = LX_NONE;
     int rc;
-    if ((rc = seg_grow(h, &h->seg_jt, &h->seg_jt_cap, (uint64_t)(G + 1) * h->B)) ||
-        (rc = seg_grow(h, &h->seg_cnt, &h->seg_cnt_cap, (uint64_t)h->B + kMaxSegments + 2)) ||
-        (rc = seg_grow(h, &h->seg_mf, &h->seg_mf_cap, (uint64_t)n)) ||
-        (rc = seg_grow(h, &h->seg_plist, &h->seg_plist_cap, (uint64_t)n)))
+    if ((rc = grow_scratch(h, &h->seg_jt, &h->seg_jt_cap, (uint64_t)(G + 1) * h->B)) ||
+        (rc = grow_scratch(h, &h->seg_cnt, &h->seg_cnt_cap, (uint64_t)h->B + kMaxSegments + 2)) ||
+        (rc = grow_scratch(h, &h->seg_mf, &h->seg_mf_cap, (uint64_t)n)) ||
+        (rc = grow_scratch(h, &h->seg_plist, &h->seg_plist_cap, (uint64_t)n)))
         return rc;
     a.jt = h->seg_jt;
     a.cnt = h->seg_cnt;
@@ -524,6 +519,11 @@ int add_batch_dev(lx_index *h, uint32_t n, const uint32_t *creator, const uint32
     if (!h->have_epoch) return h->fail(LX_ERR_STATE, "lx_add_batch before lx_reset");
     if (h->loading) return h->fail(LX_ERR_STATE, "lx_add_batch during a load (lx_load_finish first)");
     if (n == 0) return 0;
+    if (h->rowseg()) {
+        if (h->n_events || h->rs_state) return h->fail(LX_ERR_STATE, "a row-segment rank takes one batch per epoch");
+        if (h->rs_rank >= h->rs_count) return h->fail(LX_ERR_ARG, "seg_rank %u >= seg_count %u", h->rs_rank, h->rs_count);
+        if (n < 64ull * h->rs_count) return h->fail(LX_ERR_ARG, "row segments need >= 64 events per rank");
+    }
     h->wb_ready = false;
     if (h->n_events + n >= 0xFFFFFFF0ull) return h->fail(LX_ERR_ARG, "too many events in one epoch");
     h->hm_ok = false;           // the device assigns this batch: the host mirror is refreshed on demand
@@ -618,7 +618,9 @@ int add_batch_dev(lx_index *h, uint32_t n, const uint32_t *creator, const uint32
         HIPCHK(h, hipMemsetAsync(ia.prof, 0, prof_n * 8, s));
     }
     HIPCHK(h, hipEventRecord(h->ev[1], s));
-    if (h->segments > 1 && !h->sharded() && n >= 64ull * h->segments) {
+    if (h->rowseg()) {
+        if ((rc = rs_begin(h, ia, poff, s))) return rc;
+    } else if (h->segments > 1 && !h->sharded() && n >= 64ull * h->segments) {
         if ((rc = seg_walk(h, ia, poff, s))) return rc;
     } else {
         HIPCHK(h, lx::launch_index(ia, s));
@@ -662,7 +664,7 @@ int add_batch_dev(lx_index *h, uint32_t n, const uint32_t *creator, const uint32
             }
         }
     }
-    if (h->B > h->V && h->n_cheat) {
+    if (h->B > h->V && h->n_cheat && !h->rowseg()) {   // a row-segment rank marks its rows at lx_rowseg_finish
         MarkArgs m{};
         m.hb = h->hb;
         m.stride = h->pstride;
@@ -678,7 +680,7 @@ int add_batch_dev(lx_index *h, uint32_t n, const uint32_t *creator, const uint32
         m.cheat_br = h->cheat_br;
         HIPCHK(h, lx::launch_marks(m, s));
     }
-    if (!h->sharded() && h->la_tail) {
+    if (!h->sharded() && !h->rowseg() && h->la_tail) {
         if ((rc = la_tail(h, s))) return rc;
     }
     HIPCHK(h, hipEventRecord(h->ev[3], s));
@@ -705,11 +707,14 @@ int lx_fc_args(lx_index *h, uint64_t n, const uint32_t *a, const uint32_t *b, ui
                FcArgs *fa) {
     if (!h->have_epoch) return h->fail(LX_ERR_STATE, "ForklessCause before lx_reset");
     NOT_LOADING(h);
+    if (h->rowseg() && h->rs_state != 4)
+        return h->fail(LX_ERR_STATE, "row-segment rank: ForklessCause before lx_rowseg_finish");
     FcArgs f{};
     f.hb = h->hb;
     f.la = h->la;
     f.stride = h->pstride;
-    f.n_events = (uint32_t)h->n_events;
+    f.n_events = h->rowseg() ? h->rs_hi : (uint32_t)h->n_events;
+    f.ev_lo = h->rowseg() ? h->rs_lo : 0u;
     f.n = n;
     f.qa = a;
     f.qb = b;
@@ -1394,6 +1399,11 @@ int lx_set_option(lx_index *h, const char *name, int64_t value) {
         h->wire_force = (uint32_t)value;
     } else if (k == "timing") {
         h->small_timing = value != 0;
+    } else if (k == "seg_count" || k == "seg_rank") {
+        if (h->have_epoch) return h->fail(LX_ERR_STATE, "%s must be set before lx_reset", name);
+        if (h->sharded()) return h->fail(LX_ERR_STATE, "row segments on a column shard");
+        if (value < 0 || value > (int64_t)kMaxSegments) return h->fail(LX_ERR_ARG, "%s must be 0..%u", name, kMaxSegments);
+        (k == "seg_count" ? h->rs_count : h->rs_rank) = (uint32_t)value;
     } else if (k == "segments") {
         if (value < 0 || value > (int64_t)kMaxSegments) return h->fail(LX_ERR_ARG, "segments must be 0..%u", kMaxSegments);
         if (value > 1 && h->sharded()) return h->fail(LX_ERR_STATE, "segments on a column shard");
@@ -1498,6 +1508,7 @@ int lx_reset(lx_index *h, uint32_t nv, const uint32_t *w) {
     HIPCHK(h, hipMemcpyAsync(h->branch_creator, idx.data(), nv * 4, hipMemcpyHostToDevice, h->stream));
     HIPCHK(h, hipMemcpyAsync(h->wpad, wp.data(), (uint64_t)h->stride * 4, hipMemcpyHostToDevice, h->stream));
     h->n_events = h->n_flushed = 0;
+    h->rs_state = 0;
     h->pcols_used = h->sharded() ? norig : nv;
     h->B = h->B_flushed = nv;
     h->max_seq = 0;
@@ -1537,7 +1548,7 @@ int lx_add_batch(lx_index *h, uint32_t n, const uint32_t *creator, const uint32_
     }
     int rc;
     if (h->loading) return h->fail(LX_ERR_STATE, "lx_add_batch during a load (lx_load_finish first)");
-    if (h->have_epoch && !h->sharded() && n <= std::min(h->small_max, kSmallMaxN))
+    if (h->have_epoch && !h->sharded() && !h->rowseg() && n <= std::min(h->small_max, kSmallMaxN))
         return add_batch_small(h, n, creator, seq, poff, par, out_branch, err_index);
     if ((rc = flush_pending(h))) return rc;
     if ((rc = ensure_batch(h, n, npar))) return rc;
@@ -1574,6 +1585,7 @@ int lx_flush(lx_index *h) {
 int lx_drop_not_flushed(lx_index *h) {
     if (!h) return LX_ERR_ARG;
     NOT_LOADING(h);
+    WHOLE_INDEX(h);
     if (!h->have_epoch) return 0;
     HIPCHK(h, set_dev(h->device));
     h->wb_ready = false;
@@ -1637,6 +1649,7 @@ int lx_drop_not_flushed(lx_index *h) {
 
 int lx_writeback_prepare(lx_index *h, lx_writeback *out) {
     if (!h || !out) return LX_ERR_ARG;
+    WHOLE_INDEX(h);
     if (!h->have_epoch) return h->fail(LX_ERR_STATE, "write-back before lx_reset");
     NOT_LOADING(h);
     {
@@ -1857,6 +1870,7 @@ int get_rows(lx_index *h, uint32_t mode, uint32_t n, const uint32_t *ev, uint8_t
 
 int get_check(lx_index *h, uint32_t n, const uint32_t *ev) {
     if (h->sharded()) return h->fail(LX_ERR_STATE, "vector getters need an unsharded handle (shards hold their own columns)");
+    WHOLE_INDEX(h);
     if (!h->have_epoch) return h->fail(LX_ERR_STATE, "getter before lx_reset");
     NOT_LOADING(h);
     {
@@ -2197,6 +2211,7 @@ int lx_load_rows(lx_index *h, uint32_t n, const uint32_t *creator, const uint32_
                  const uint32_t *par, const uint8_t *branch_be, const uint64_t *hb_off, const uint8_t *hb_bytes,
                  const uint64_t *la_off, const uint8_t *la_bytes) {
     if (!h) return LX_ERR_ARG;
+    WHOLE_INDEX(h);
     if (!h->have_epoch) return h->fail(LX_ERR_STATE, "lx_load_rows before lx_reset");
     if (h->sharded()) return h->fail(LX_ERR_STATE, "lx_load_rows needs an unsharded handle");
     if (!n) return 0;
@@ -2523,6 +2538,7 @@ int lx_load_finish(lx_index *h, const uint8_t *bi_rlp, uint32_t bi_len) {
 // view for the abft engine (lx_abft.cpp); see lx_internal.h
 int lx_index_view(lx_index *h, IndexView *o) {
     if (!h || !o) return LX_ERR_ARG;
+    WHOLE_INDEX(h);
     if (!h->have_epoch) return h->fail(LX_ERR_STATE, "index has no epoch (lx_reset first)");
     {
         const int rc = flush_pending(h);   // abft and the emitter enqueue after the index's work

@@ -363,7 +363,7 @@ int lx_forkless_cause(lx_index *h, uint32_t a, uint32_t b, uint8_t *out) {
     if (h->loading) return h->fail(LX_ERR_STATE, "index is loading (lx_load_finish first)");
     if (a >= h->n_events || b >= h->n_events)
         return h->fail(LX_ERR_ARG, "ForklessCause on an unknown event");   // forkless_cause.go:43-61 (crit)
-    if (h->sharded() || !h->fcc_slots) return lx_forkless_cause_batch(h, 1, &a, &b, out);
+    if (h->sharded() || h->rowseg() || !h->fcc_slots) return lx_forkless_cause_batch(h, 1, &a, &b, out);
     if (!h->fcc) {
         int rc = fcc_make(h);
         if (rc) return rc;

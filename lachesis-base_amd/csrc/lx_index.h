@@ -29,6 +29,21 @@ hipError_t dalloc(T **p, uint64_t n) {
 
 inline uint32_t round_up(uint32_t x, uint32_t m) { return (x + m - 1) / m * m; }
 
+// device scratch grown to `need` elements (contents not kept)
+template <typename H, typename T>
+int grow_scratch(H *h, T **p, uint64_t *cap, uint64_t need) {
+    if (*cap >= need && *p) return 0;
+    if (*p) {
+        if (int rc = h->hip(hipStreamSynchronize(h->stream), "grow_scratch sync")) return rc;
+        (void)hipFree(*p);
+        *p = nullptr;
+        *cap = 0;
+    }
+    if (int rc = h->hip(dalloc(p, need), "grow_scratch")) return rc;
+    *cap = need;
+    return 0;
+}
+
 // hipSetDevice costs microseconds per call; every entry point makes sure the
 // handle's device is current, so switch only when it is not
 inline hipError_t set_dev(int device) {
@@ -195,6 +210,18 @@ struct lx_index {
     uint64_t seg_jt_cap = 0, seg_cnt_cap = 0, seg_mf_cap = 0, seg_plist_cap = 0;
     std::vector<hipEvent_t> seg_ev;
     lx_seg_stats seg_stats{};
+    // row-segment rank (options seg_rank / seg_count, lx_rowseg.cpp): one batch
+    // per epoch, this rank walks and owns the rows of segment rs_rank
+    uint32_t rs_rank = 0, rs_count = 0;
+    int rs_state = 0;                      // 0 idle, 1 rows needed, 2 rows final, 3 LowestAfter sent, 4 ready
+    uint32_t rs_lo = 0, rs_hi = 0, rs_npartial = 0, rs_nreq = 0, rs_klo = 0, rs_khi = 0;
+    uint32_t rs_seg_lo[kMaxSegments + 1] = {};
+    uint32_t *rs_need = nullptr, *rs_req = nullptr, *rs_ctr = nullptr, *rs_ids = nullptr, *rs_out = nullptr,
+             *rs_send = nullptr;
+    uint64_t rs_need_cap = 0, rs_req_cap = 0, rs_ids_cap = 0, rs_out_cap = 0, rs_send_cap = 0, rs_ctr_cap = 0;
+    uint64_t rs_out_per = 0;               // triples per destination in rs_out
+    uint64_t rs_nsend = 0;                 // triples packed in rs_send (lx_rowseg_la)
+    bool rowseg() const { return rs_count > 1; }
 
     int fail(int code, const char *fmt, ...) {
         char buf[512];
@@ -222,6 +249,8 @@ struct lx_index {
 int lx_fc_args(lx_index *h, uint64_t n, const uint32_t *a, const uint32_t *b, uint8_t *out, uint32_t *partial,
                FcArgs *fa);
 int flush_pending(lx_index *h);                 // launch the pending small-path run (lx_capi.cpp)
+int rs_begin(lx_index *h, IndexArgs ia, const uint32_t *poff, hipStream_t s);   // lx_rowseg.cpp
+void rs_free(lx_index *h);
 void fcc_destroy(lx_index *h);
 void fcc_clear(lx_index *h);                    // Reset: a new epoch
 void fcc_forget_from(lx_index *h, uint64_t n);  // DropNotFlushed: events >= n are gone

@@ -110,6 +110,7 @@ struct FcArgs {
     const uint32_t *la;
     uint64_t stride;
     uint32_t n_events;
+    uint32_t ev_lo;              // row-segment rank: queries must lie in [ev_lo, n_events)
     uint64_t n;
     const uint32_t *qa;
     const uint32_t *qb;
@@ -449,10 +450,27 @@ struct SegArgs {
     // LowestAfter pass (k_seg_la): events [ev_lo, ev_hi) fill, at chain positions [k_lo, k_hi)
     uint32_t ev_lo, ev_hi;
     uint32_t k_lo, k_hi;
-    uint32_t own_lo;             // rows below it are another rank's: their entries go to `out` as (row, column, seq)
-    uint32_t *out;
-    uint32_t *out_count;
-    uint64_t out_cap;            // triples
+    uint32_t own_seg;            // row-segment rank: its segment (k range of k_seg_prefix_j); LX_NONE: the batch
+    uint32_t own_lo;             // rows below it are another rank's: their entries go to out[seg_of(row)]
+    uint32_t *out;               // per destination segment d: out_cap triples (row, column, seq) at out + 3 d out_cap
+    uint32_t *out_count;         // [G]
+    uint64_t out_cap;
+};
+
+// Row-segment multi-GPU exchange (lx_rowseg.cpp): rows a rank needs from the
+// others, and the moves of rows and LowestAfter entries between ranks
+struct RsArgs {
+    uint32_t *hb;
+    uint32_t *la;
+    uint64_t stride;
+    uint32_t B;
+    uint32_t lo, hi;             // own events
+    const uint32_t *pflag;       // own partial flags (index e - lo)
+    uint32_t partials_done;
+    uint32_t *need;              // [n_events]: 1 = requested and not received
+    uint32_t *req;               // requested rows (appended)
+    uint32_t *req_count;
+    uint32_t *remaining;
 };
 
 // kernel launchers (lx_kernels.hip); all enqueue on `s`
@@ -460,6 +478,14 @@ namespace lx {
 hipError_t launch_seg_tables(const SegArgs &a, hipStream_t s);
 hipError_t launch_seg_partial(const SegArgs &a, uint32_t k, uint32_t count, hipStream_t s);
 hipError_t launch_seg_la(const SegArgs &a, hipStream_t s);
+hipError_t launch_rs_refs(const SegArgs &a, const RsArgs &r, uint32_t n_partial, hipStream_t s);
+hipError_t launch_rs_bucket(const SegArgs &a, const RsArgs &r, uint32_t n_req, uint32_t *out, uint32_t *counts,
+                            hipStream_t s);
+hipError_t launch_rs_gather(const RsArgs &r, const uint32_t *ids, uint32_t n, uint32_t *rows, uint32_t *ready,
+                            hipStream_t s);
+hipError_t launch_rs_scatter(const RsArgs &r, const uint32_t *ids, uint32_t n, const uint32_t *rows,
+                             const uint32_t *ready, hipStream_t s);
+hipError_t launch_rs_la_apply(const RsArgs &r, const uint32_t *triples, uint64_t n, hipStream_t s);
 hipError_t launch_batch_prepare(const BatchArgs &a, void *scan_tmp, size_t scan_tmp_bytes, hipStream_t s);
 hipError_t launch_batch_finish(const BatchArgs &a, uint32_t jump_rounds, hipStream_t s);
 hipError_t launch_small(const SmallArgs &a, hipStream_t s);

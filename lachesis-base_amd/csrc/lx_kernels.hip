@@ -1180,7 +1180,7 @@ __global__ __launch_bounds__(256) void k_fc(FcArgs a) {
     }
     for (uint64_t q = blockIdx.x * qpb + threadIdx.x / LPQ; q < a.n; q += (uint64_t)gridDim.x * qpb) {
         uint32_t A = a.qa[a.qa_bcast ? 0 : q], Bq = a.qb[q];
-        const bool bad = (A >= a.n_events) | (Bq >= a.n_events);
+        const bool bad = (A >= a.n_events) | (Bq >= a.n_events) | (A < a.ev_lo) | (Bq < a.ev_lo);
         if (bad) { A = 0; Bq = 0; }
         // FORKS, lane 0: the early-false inputs first (their loads overlap the rows')
         uint32_t e_bb = 0, e_cb = 0;
@@ -1296,7 +1296,7 @@ __global__ __launch_bounds__(256) void k_fc_fk(FcArgs a) {
     }
     for (uint64_t q = blockIdx.x * qpb + threadIdx.x / LPQ; q < a.n; q += (uint64_t)gridDim.x * qpb) {
         uint32_t A = a.qa[a.qa_bcast ? 0 : q], Bq = a.qb[q];
-        const bool bad = (A >= a.n_events) | (Bq >= a.n_events);
+        const bool bad = (A >= a.n_events) | (Bq >= a.n_events) | (A < a.ev_lo) | (Bq < a.ev_lo);
         if (bad) { A = 0; Bq = 0; }
         uint32_t e_bb = 0, e_cb = 0;
         if (lane == 0) {

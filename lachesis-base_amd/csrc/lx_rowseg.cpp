@@ -1,0 +1,344 @@
+// lx_rowseg.cpp -- row segments: the segmented walk (lx_segment.hip) spread
+// over ranks, one GPU each.
+//
+// Every rank takes the same epoch as one batch (branch assignment and the
+// J_k tables are replicated metadata work) but walks, fixes up and owns only
+// the rows of its segment [lo, hi).  Two exchanges connect the ranks, both
+// driven by the caller's collectives (lachesis_hip/rowseg.py over
+// torch.distributed / RCCL):
+//   rows   -- a partial event's fix-up reads final rows of earlier segments
+//             (and the LowestAfter pass needs the row before each branch's
+//             first own event): lx_rowseg_requests groups the ids by owner,
+//             owners answer with lx_rowseg_serve, lx_rowseg_receive stores
+//             them; a row that is not final yet (a partial event whose owner
+//             still waits) is answered "not ready" and asked again next
+//             round -- at most G - 1 rounds, one when segments are longer
+//             than the DAG's observation depth.
+//   LowestAfter -- an own event's range fill reaches rows of earlier
+//             segments: those entries leave as (row, column, seq) triples
+//             per owner (lx_rowseg_la) and are written there
+//             (lx_rowseg_la_apply).
+// lx_rowseg_finish sets the own rows' fork marks; then ForklessCause answers
+// queries between own events.
+#include "lx_index.h"
+
+using namespace lxi;
+
+namespace {
+
+SegArgs rs_seg_args(lx_index *h) {
+    SegArgs a{};
+    a.hb = h->hb;
+    a.la = h->la;
+    a.stride = h->pstride;
+    a.B = h->B;
+    a.bs = 0;
+    a.n = h->rs_seg_lo[h->rs_count];
+    a.G = h->rs_count;
+    for (uint32_t k = 0; k <= h->rs_count; k++) a.seg_lo[k] = h->rs_seg_lo[k];
+    a.ev_branch = h->ev_branch;
+    a.ev_seq = h->ev_seq;
+    a.branch_first = h->branch_first;
+    a.branch_len = h->branch_len;
+    a.brow = h->brow;
+    a.s_cap = h->s_cap;
+    a.jt = h->seg_jt;
+    a.cnt = h->seg_cnt;
+    a.pcount = h->seg_cnt + h->B;
+    a.pflag = h->seg_mf;
+    a.plist = h->seg_plist;
+    a.own_seg = h->rs_rank;
+    a.own_lo = h->rs_lo;
+    return a;
+}
+
+RsArgs rs_args(lx_index *h) {
+    RsArgs r{};
+    r.hb = h->hb;
+    r.la = h->la;
+    r.stride = h->pstride;
+    r.B = h->B;
+    r.lo = h->rs_lo;
+    r.hi = h->rs_hi;
+    r.pflag = h->seg_mf + h->rs_lo;
+    r.partials_done = h->rs_state >= 2 ? 1u : 0u;
+    r.need = h->rs_need;
+    r.req = h->rs_req;
+    r.req_count = h->rs_ctr;
+    r.remaining = h->rs_ctr + 1;
+    return r;
+}
+
+int rs_check(lx_index *h, int state) {
+    if (!h) return LX_ERR_ARG;
+    if (!h->rowseg()) return h->fail(LX_ERR_STATE, "not a row-segment rank (options seg_count / seg_rank)");
+    if (state >= 0 && h->rs_state != state)
+        return h->fail(LX_ERR_STATE, "row-segment step out of order (state %d, expected %d)", h->rs_state, state);
+    return h->hip(set_dev(h->device), "set device");
+}
+
+// the own partial events' rows from the rows they reference (every one final
+// and present by now)
+int rs_fix_partials(lx_index *h) {
+    if (h->rs_npartial) {
+        SegArgs a = rs_seg_args(h);
+        HIPCHK(h, hipEventRecord(h->seg_ev[2], h->stream));
+        HIPCHK(h, lx::launch_seg_partial(a, h->rs_rank, h->rs_npartial, h->stream));
+        HIPCHK(h, hipEventRecord(h->seg_ev[3], h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        HIPCHK(h, hipEventElapsedTime(&h->seg_stats.partial_ms, h->seg_ev[2], h->seg_ev[3]));
+    }
+    h->rs_state = 2;
+    return 0;
+}
+
+}  // namespace
+
+void rs_free(lx_index *h) {
+    void *p[] = {h->rs_need, h->rs_req, h->rs_ctr, h->rs_ids, h->rs_out, h->rs_send};
+    for (void *q : p)
+        if (q) (void)hipFree(q);
+    h->rs_need = h->rs_req = h->rs_ctr = h->rs_ids = h->rs_out = h->rs_send = nullptr;
+    h->rs_need_cap = h->rs_req_cap = h->rs_ids_cap = h->rs_out_cap = h->rs_send_cap = h->rs_ctr_cap = 0;
+    h->rs_state = 0;
+}
+
+// lx_add_batch on a row-segment rank (the epoch's only batch, assigned): walk
+// the own segment, list the rows its partial events and its LowestAfter pass
+// need from the other ranks
+int rs_begin(lx_index *h, IndexArgs ia, const uint32_t *poff, hipStream_t s) {
+    const uint32_t G = h->rs_count, k = h->rs_rank, n = ia.n;
+    for (uint32_t q = 0; q < G; q++) h->rs_seg_lo[q] = (uint32_t)((uint64_t)n * q / G / 64 * 64);
+    h->rs_seg_lo[G] = n;
+    h->rs_lo = h->rs_seg_lo[k];
+    h->rs_hi = h->rs_seg_lo[k + 1];
+    int rc;
+    if ((rc = grow_scratch(h, &h->seg_jt, &h->seg_jt_cap, (uint64_t)(G + 1) * h->B)) ||
+        (rc = grow_scratch(h, &h->seg_cnt, &h->seg_cnt_cap, (uint64_t)h->B + kMaxSegments + 2)) ||
+        (rc = grow_scratch(h, &h->seg_mf, &h->seg_mf_cap, (uint64_t)n)) ||
+        (rc = grow_scratch(h, &h->seg_plist, &h->seg_plist_cap, (uint64_t)n)) ||
+        (rc = grow_scratch(h, &h->rs_need, &h->rs_need_cap, (uint64_t)n)) ||
+        (rc = grow_scratch(h, &h->rs_ctr, &h->rs_ctr_cap, (uint64_t)2 + 2 * kMaxSegments)))
+        return rc;
+    while (h->seg_ev.size() < 6) {
+        hipEvent_t e;
+        HIPCHK(h, hipEventCreate(&e));
+        h->seg_ev.push_back(e);
+    }
+    h->rs_state = 0;
+    SegArgs a = rs_seg_args(h);
+    HIPCHK(h, lx::launch_seg_tables(a, s));
+    // the own rows' LowestAfter is written by the own pass and the others' triples only
+    HIPCHK(h, hipMemsetAsync(h->la + (uint64_t)h->rs_lo * h->pstride, 0,
+                             (uint64_t)(h->rs_hi - h->rs_lo) * h->pstride * 4, s));
+    ia.seg = 1;
+    ia.ev_branch = h->ev_branch;
+    ia.ev_seq = h->ev_seq;
+    ia.batch_start = h->rs_lo;
+    ia.n = h->rs_hi - h->rs_lo;
+    ia.rec = ia.rec + h->rs_lo;
+    ia.poff_in = poff + h->rs_lo;
+    ia.seg_j = a.jt + (uint64_t)k * a.B;
+    ia.seg_flag = a.pflag + h->rs_lo;
+    ia.seg_list = a.plist + h->rs_lo;
+    ia.seg_count = a.pcount + k;
+    HIPCHK(h, hipEventRecord(h->seg_ev[0], s));
+    HIPCHK(h, lx::launch_index(ia, s));
+    HIPCHK(h, hipEventRecord(h->seg_ev[1], s));
+    uint32_t pc[kMaxSegments + 2];
+    HIPCHK(h, hipMemcpyAsync(pc, a.pcount, (G + 2) * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(h, hipStreamSynchronize(s));
+    h->rs_npartial = pc[k];
+    h->rs_klo = pc[G];
+    h->rs_khi = pc[G + 1];
+    // the rows to ask for: at most every referenced branch of every partial
+    // event plus one per branch, and never more than the events before lo
+    const uint64_t want = std::min<uint64_t>((uint64_t)h->rs_npartial * h->B + h->B, (uint64_t)h->rs_lo + 1);
+    if ((rc = grow_scratch(h, &h->rs_req, &h->rs_req_cap, want)) ||
+        (rc = grow_scratch(h, &h->rs_ids, &h->rs_ids_cap, want)))
+        return rc;
+    HIPCHK(h, hipMemsetAsync(h->rs_need, 0, (uint64_t)n * 4, s));
+    HIPCHK(h, hipMemsetAsync(h->rs_ctr, 0, (2 + 2 * kMaxSegments) * 4, s));
+    RsArgs r = rs_args(h);
+    SegArgs ap = a;
+    ap.plist = a.plist + h->rs_lo;
+    HIPCHK(h, lx::launch_rs_refs(ap, r, h->rs_npartial, s));
+    HIPCHK(h, hipMemcpyAsync(h->rs_ctr + 1, h->rs_ctr, 4, hipMemcpyDeviceToDevice, s));
+    uint32_t nreq = 0;
+    HIPCHK(h, hipMemcpyAsync(&nreq, h->rs_ctr, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(h, hipStreamSynchronize(s));
+    h->rs_nreq = nreq;
+    lx_seg_stats &st = h->seg_stats;
+    st = lx_seg_stats{};
+    st.segments = G;
+    for (uint32_t q = 0; q <= G; q++) st.first_event[q] = h->rs_seg_lo[q];
+    st.partial[k] = h->rs_npartial;
+    HIPCHK(h, hipEventElapsedTime(&st.walk_ms[k], h->seg_ev[0], h->seg_ev[1]));
+    h->rs_state = 1;
+    if (!nreq) return rs_fix_partials(h);
+    return 0;
+}
+
+extern "C" {
+
+int lx_rowseg_bounds(const lx_index *h, uint32_t *lo) {
+    if (!h || !lo) return LX_ERR_ARG;
+    if (!h->rowseg() || !h->rs_state) return LX_ERR_STATE;
+    for (uint32_t q = 0; q <= h->rs_count; q++) lo[q] = h->rs_seg_lo[q];
+    return 0;
+}
+
+int lx_rowseg_row_words(const lx_index *h, uint32_t *words) {
+    if (!h || !words) return LX_ERR_ARG;
+    *words = h->B;
+    return 0;
+}
+
+int lx_rowseg_requests(lx_index *h, uint32_t *ids, uint32_t cap, uint32_t *counts) {
+    int rc;
+    if ((rc = rs_check(h, -1))) return rc;
+    if (!counts) return LX_ERR_ARG;
+    if (h->rs_state < 1 || h->rs_state > 2) return h->fail(LX_ERR_STATE, "row-segment requests outside the row exchange");
+    for (uint32_t q = 0; q < h->rs_count; q++) counts[q] = 0;
+    if (h->rs_state == 2 || !h->rs_nreq) return 0;
+    if (ids && cap < h->rs_nreq) return h->fail(LX_ERR_ARG, "request buffer of %u ids < %u", cap, h->rs_nreq);
+    SegArgs a = rs_seg_args(h);
+    RsArgs r = rs_args(h);
+    HIPCHK(h, lx::launch_rs_bucket(a, r, h->rs_nreq, ids ? ids : h->rs_ids, h->rs_ctr + 2, h->stream));
+    HIPCHK(h, hipMemcpyAsync(counts, h->rs_ctr + 2, h->rs_count * 4, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+int lx_rowseg_request_cap(const lx_index *h, uint32_t *cap) {
+    if (!h || !cap) return LX_ERR_ARG;
+    *cap = h->rowseg() ? h->rs_nreq : 0u;
+    return 0;
+}
+
+int lx_rowseg_serve(lx_index *h, uint32_t n, const uint32_t *ids, uint32_t *rows, uint32_t *ready) {
+    int rc;
+    if ((rc = rs_check(h, -1))) return rc;
+    if (h->rs_state < 1 || h->rs_state > 2) return h->fail(LX_ERR_STATE, "row-segment serve outside the row exchange");
+    RsArgs r = rs_args(h);
+    HIPCHK(h, lx::launch_rs_gather(r, ids, n, rows, ready, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+int lx_rowseg_receive(lx_index *h, uint32_t n, const uint32_t *ids, const uint32_t *rows, const uint32_t *ready,
+                      uint32_t *remaining) {
+    int rc;
+    if ((rc = rs_check(h, -1))) return rc;
+    if (h->rs_state < 1 || h->rs_state > 2) return h->fail(LX_ERR_STATE, "row-segment receive outside the row exchange");
+    uint32_t left = 0;
+    if (h->rs_state == 1) {
+        RsArgs r = rs_args(h);
+        HIPCHK(h, lx::launch_rs_scatter(r, ids, n, rows, ready, h->stream));
+        HIPCHK(h, hipMemcpyAsync(&left, h->rs_ctr + 1, 4, hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        if (!left && (rc = rs_fix_partials(h))) return rc;
+    }
+    if (remaining) *remaining = left;
+    return 0;
+}
+
+int lx_rowseg_la(lx_index *h, uint64_t *counts) {
+    int rc;
+    if ((rc = rs_check(h, 2))) return rc;
+    if (!counts) return LX_ERR_ARG;
+    const uint32_t G = h->rs_count;
+    if (!h->rs_out_per) h->rs_out_per = 1u << 18;
+    std::vector<uint32_t> c(G);
+    for (int attempt = 0; attempt < 2; attempt++) {
+        if ((rc = grow_scratch(h, &h->rs_out, &h->rs_out_cap, 3ull * G * h->rs_out_per))) return rc;
+        SegArgs a = rs_seg_args(h);
+        a.ev_lo = h->rs_lo;
+        a.ev_hi = h->rs_hi;
+        a.k_lo = h->rs_klo;
+        a.k_hi = h->rs_khi;
+        a.out = h->rs_out;
+        a.out_count = h->rs_ctr + 2 + kMaxSegments;
+        a.out_cap = h->rs_out_per;
+        HIPCHK(h, hipMemsetAsync(a.out_count, 0, G * 4, h->stream));
+        HIPCHK(h, hipEventRecord(h->seg_ev[4], h->stream));
+        HIPCHK(h, lx::launch_seg_la(a, h->stream));
+        HIPCHK(h, hipEventRecord(h->seg_ev[5], h->stream));
+        HIPCHK(h, hipMemcpyAsync(c.data(), a.out_count, G * 4, hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        const uint32_t mx = *std::max_element(c.begin(), c.end());
+        if (mx <= h->rs_out_per) break;
+        // too many entries for a destination: larger buckets, the same pass
+        // again (its own stores are idempotent)
+        h->rs_out_per = (uint64_t)mx + mx / 4;
+        if (attempt) return h->fail(LX_ERR_STATE, "row-segment LowestAfter buckets overflowed twice");
+    }
+    HIPCHK(h, hipEventElapsedTime(&h->seg_stats.la_ms, h->seg_ev[4], h->seg_ev[5]));
+    uint64_t tot = 0;
+    for (uint32_t q = 0; q < G; q++) tot += c[q];
+    if ((rc = grow_scratch(h, &h->rs_send, &h->rs_send_cap, 3 * tot + 3))) return rc;
+    uint64_t o = 0;
+    for (uint32_t q = 0; q < G; q++) {
+        counts[q] = c[q];
+        if (c[q])
+            HIPCHK(h, hipMemcpyAsync(h->rs_send + 3 * o, h->rs_out + 3ull * q * h->rs_out_per, 12ull * c[q],
+                                     hipMemcpyDeviceToDevice, h->stream));
+        o += c[q];
+    }
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    h->rs_nsend = o;
+    h->rs_state = 3;
+    return 0;
+}
+
+int lx_rowseg_la_fetch(lx_index *h, uint32_t *triples) {
+    int rc;
+    if ((rc = rs_check(h, 3))) return rc;
+    if (h->rs_nsend)
+        HIPCHK(h, hipMemcpyAsync(triples, h->rs_send, 12ull * h->rs_nsend, hipMemcpyDeviceToDevice, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+int lx_rowseg_la_apply(lx_index *h, uint64_t n, const uint32_t *triples) {
+    int rc;
+    if ((rc = rs_check(h, 3))) return rc;
+    RsArgs r = rs_args(h);
+    HIPCHK(h, lx::launch_rs_la_apply(r, triples, n, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+int lx_rowseg_finish(lx_index *h) {
+    int rc;
+    if ((rc = rs_check(h, 3))) return rc;
+    if (h->B > h->V && h->n_cheat) {
+        MarkArgs m{};
+        m.hb = h->hb;
+        m.stride = h->pstride;
+        m.cmap = nullptr;
+        m.batch_start = h->rs_lo;
+        m.n = h->rs_hi - h->rs_lo;
+        m.V = h->V;
+        m.ev_branch = h->ev_branch;
+        m.ev_bbefore = h->ev_bbefore;
+        m.branch_first = h->branch_first;
+        m.n_cheat = h->n_cheat;
+        m.cheat_off = h->cheat_off;
+        m.cheat_br = h->cheat_br;
+        HIPCHK(h, lx::launch_marks(m, h->stream));
+    }
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    h->rs_state = 4;
+    return 0;
+}
+
+int lx_rowseg_range(const lx_index *h, uint32_t *lo, uint32_t *hi) {
+    if (!h || !lo || !hi) return LX_ERR_ARG;
+    if (!h->rowseg() || !h->rs_state) return LX_ERR_STATE;
+    *lo = h->rs_lo;
+    *hi = h->rs_hi;
+    return 0;
+}
+
+}  // extern "C"

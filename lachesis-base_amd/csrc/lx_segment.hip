@@ -63,9 +63,19 @@ __global__ void k_seg_prefix_j(SegArgs a) {
         j = max(j, *p);
         *p = j;
     }
-    if (a.cnt[c]) {
-        atomicMin(a.cnt + a.B + a.G, before);
-        atomicMax(a.cnt + a.B + a.G + 1, a.branch_len[c]);
+    if (a.own_seg == LX_NONE) {
+        if (a.cnt[c]) {
+            atomicMin(a.cnt + a.B + a.G, before);
+            atomicMax(a.cnt + a.B + a.G + 1, a.branch_len[c]);
+        }
+    } else {
+        // chain positions of the own segment's events of branch c
+        const uint32_t j0 = a.jt[(uint64_t)a.own_seg * a.B + c], j1 = a.jt[(uint64_t)(a.own_seg + 1) * a.B + c];
+        if (j1 > j0) {
+            const uint32_t f = a.branch_first[c];
+            atomicMin(a.cnt + a.B + a.G, j0 ? j0 - f + 1 : 0u);
+            atomicMax(a.cnt + a.B + a.G + 1, j1 - f + 1);
+        }
     }
 }
 
@@ -158,21 +168,36 @@ __global__ void __launch_bounds__(256) k_seg_la(SegArgs a, uint32_t nkc, uint32_
             const uint32_t y = yrow[kk + 1][lane];
             if (y != LX_NONE && y >= a.ev_lo && y < a.ev_hi) {
                 const uint32_t sq = fj + (uint32_t)(k0 + kk);
-                for (uint32_t ci = wave; ci < (uint32_t)kLC; ci += 4) {
-                    const uint32_t c = c0 + ci;
-                    if (c >= a.B) break;
-                    const uint32_t hi = R[lane][ci];
-                    const uint32_t lo = max(P[lane][ci] + 1u, a.branch_first[c]);
-                    for (uint32_t s = lo; s <= hi; s++) {
-                        const uint32_t x = row_of(a, c, s);
-                        if (x >= a.own_lo) {
-                            a.la[(uint64_t)x * a.stride + j] = sq;
+                // the wave's 16 columns: ranges first, then every first row
+                // lookup in flight at once (the lookups were the pass's
+                // critical path when issued one column at a time)
+                constexpr int T = kLC / 4;
+                uint32_t lo[T], hi[T], x[T];
+#pragma unroll
+                for (int t = 0; t < T; t++) {
+                    const uint32_t ci = wave + 4 * t, c = c0 + ci;
+                    const bool v = c < a.B;
+                    const uint32_t f = v ? a.branch_first[c] : 1u;
+                    hi[t] = v ? R[lane][ci] : 0u;
+                    lo[t] = max(P[lane][ci] + 1u, f);
+                    x[t] = lo[t] <= hi[t] ? a.brow[(uint64_t)c * a.s_cap + (lo[t] - f)] : 0u;
+                }
+#pragma unroll
+                for (int t = 0; t < T; t++) {
+                    const uint32_t c = c0 + wave + 4 * t;
+                    for (uint32_t s = lo[t]; s <= hi[t]; s++) {
+                        const uint32_t xr = s == lo[t] ? x[t] : row_of(a, c, s);
+                        if (xr >= a.own_lo) {
+                            a.la[(uint64_t)xr * a.stride + j] = sq;
                         } else {
-                            const uint32_t p = atomicAdd(a.out_count, 1u);
+                            // another rank's row: to the owner of its segment
+                            const uint32_t d = seg_of(a, xr);
+                            const uint32_t p = atomicAdd(a.out_count + d, 1u);
                             if (p < a.out_cap) {
-                                a.out[3ull * p] = x;
-                                a.out[3ull * p + 1] = j;
-                                a.out[3ull * p + 2] = sq;
+                                uint32_t *o = a.out + 3ull * (d * a.out_cap + p);
+                                o[0] = xr;
+                                o[1] = j;
+                                o[2] = sq;
                             }
                         }
                     }
@@ -183,6 +208,90 @@ __global__ void __launch_bounds__(256) k_seg_la(SegArgs a, uint32_t nkc, uint32_
             pk = (int)kk + 1;
         }
     }
+}
+
+// ------------------------------------------------------------------ row segments (lx_rowseg.cpp)
+__device__ __forceinline__ void rs_want(const RsArgs &r, uint32_t x) {
+    if (atomicOr(r.need + x, 1u) == 0u) r.req[atomicAdd(r.req_count, 1u)] = x;
+}
+
+// the rows the own partial events reference (one workgroup per partial event)
+__global__ void __launch_bounds__(256) k_rs_refs(SegArgs a, RsArgs r) {
+    const uint32_t e = a.plist[blockIdx.x];
+    const uint32_t *J = a.jt + (uint64_t)a.own_seg * a.B;
+    const uint32_t *row = a.hb + (uint64_t)e * a.stride;
+    for (uint32_t c = threadIdx.x; c < a.B; c += blockDim.x) {
+        const uint32_t m = min(row[c], J[c]);
+        if (m) rs_want(r, row_of(a, c, m));
+    }
+}
+
+// the previous event of every branch's first own event (k_seg_la's first prev)
+__global__ void k_rs_frontier(SegArgs a, RsArgs r) {
+    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= a.B) return;
+    const uint32_t j0 = a.jt[(uint64_t)a.own_seg * a.B + c], j1 = a.jt[(uint64_t)(a.own_seg + 1) * a.B + c];
+    if (j1 > j0 && j0) rs_want(r, row_of(a, c, j0));
+}
+
+// the still-needed requests grouped by owner segment: out = [d0 ids][d1 ids]...,
+// counts[G] (one workgroup)
+__global__ void __launch_bounds__(1024) k_rs_bucket(SegArgs a, RsArgs r, uint32_t n_req, uint32_t *out,
+                                                    uint32_t *counts) {
+    __shared__ uint32_t cnt[kMaxSegments], off[kMaxSegments];
+    if (threadIdx.x < a.G) cnt[threadIdx.x] = 0;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < n_req; i += blockDim.x) {
+        const uint32_t x = r.req[i];
+        if (r.need[x]) atomicAdd(&cnt[seg_of(a, x)], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t o = 0;
+        for (uint32_t d = 0; d < a.G; d++) {
+            off[d] = o;
+            o += cnt[d];
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < a.G) counts[threadIdx.x] = cnt[threadIdx.x];
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < n_req; i += blockDim.x) {
+        const uint32_t x = r.req[i];
+        if (r.need[x]) out[atomicAdd(&off[seg_of(a, x)], 1u)] = x;
+    }
+}
+
+// serve: own final rows (B words each) of the requested ids; ready[i] = 0 for
+// a row that is not final yet (a partial event before its fix-up) or not own
+__global__ void __launch_bounds__(256) k_rs_gather(RsArgs r, const uint32_t *ids, uint32_t *rows, uint32_t *ready) {
+    const uint32_t x = ids[blockIdx.x];
+    const bool own = x >= r.lo && x < r.hi;
+    const bool ok = own && (r.partials_done || !r.pflag[x - r.lo]);
+    if (threadIdx.x == 0) ready[blockIdx.x] = ok ? 1u : 0u;
+    if (!ok) return;
+    const uint32_t *src = r.hb + (uint64_t)x * r.stride;
+    uint32_t *dst = rows + (uint64_t)blockIdx.x * r.B;
+    for (uint32_t c = threadIdx.x; c < r.B; c += blockDim.x) dst[c] = src[c];
+}
+
+// receive: ready rows into the plane; each newly received requested row
+// counts down `remaining`
+__global__ void __launch_bounds__(256) k_rs_scatter(RsArgs r, const uint32_t *ids, const uint32_t *rows,
+                                                    const uint32_t *ready) {
+    if (!ready[blockIdx.x]) return;
+    const uint32_t x = ids[blockIdx.x];
+    uint32_t *dst = r.hb + (uint64_t)x * r.stride;
+    const uint32_t *src = rows + (uint64_t)blockIdx.x * r.B;
+    for (uint32_t c = threadIdx.x; c < r.B; c += blockDim.x) dst[c] = src[c];
+    if (threadIdx.x == 0 && atomicExch(r.need + x, 0u) == 1u) atomicSub(r.remaining, 1u);
+}
+
+__global__ void k_rs_la_apply(RsArgs r, const uint32_t *t, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t x = t[3 * i], j = t[3 * i + 1];
+    if (x >= r.lo && x < r.hi && j < r.B) r.la[(uint64_t)x * r.stride + j] = t[3 * i + 2];
 }
 
 inline uint32_t nb(uint64_t n, uint32_t t) { return (uint32_t)((n + t - 1) / t); }
@@ -204,6 +313,38 @@ hipError_t launch_seg_tables(const SegArgs &a, hipStream_t s) {
 hipError_t launch_seg_partial(const SegArgs &a, uint32_t k, uint32_t count, hipStream_t s) {
     if (!count) return hipSuccess;
     hipLaunchKernelGGL(k_seg_partial, dim3(count), dim3(256), (size_t)a.B * 4, s, a, k);
+    return hipGetLastError();
+}
+
+hipError_t launch_rs_refs(const SegArgs &a, const RsArgs &r, uint32_t n_partial, hipStream_t s) {
+    if (n_partial) hipLaunchKernelGGL(k_rs_refs, dim3(n_partial), dim3(256), 0, s, a, r);
+    hipLaunchKernelGGL(k_rs_frontier, dim3(nb(a.B, 256)), dim3(256), 0, s, a, r);
+    return hipGetLastError();
+}
+
+hipError_t launch_rs_bucket(const SegArgs &a, const RsArgs &r, uint32_t n_req, uint32_t *out, uint32_t *counts,
+                            hipStream_t s) {
+    hipLaunchKernelGGL(k_rs_bucket, dim3(1), dim3(1024), 0, s, a, r, n_req, out, counts);
+    return hipGetLastError();
+}
+
+hipError_t launch_rs_gather(const RsArgs &r, const uint32_t *ids, uint32_t n, uint32_t *rows, uint32_t *ready,
+                            hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_rs_gather, dim3(n), dim3(256), 0, s, r, ids, rows, ready);
+    return hipGetLastError();
+}
+
+hipError_t launch_rs_scatter(const RsArgs &r, const uint32_t *ids, uint32_t n, const uint32_t *rows,
+                             const uint32_t *ready, hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_rs_scatter, dim3(n), dim3(256), 0, s, r, ids, rows, ready);
+    return hipGetLastError();
+}
+
+hipError_t launch_rs_la_apply(const RsArgs &r, const uint32_t *triples, uint64_t n, hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_rs_la_apply, dim3(nb(n, 256)), dim3(256), 0, s, r, triples, n);
     return hipGetLastError();
 }
 

@@ -60,6 +60,17 @@ SIGNATURES = [
     ("lx_la_unpack_wire_dev", ctypes.c_int, [vp, ctypes.c_uint32, vp, ctypes.c_uint32]),
     ("lx_last_stats", ctypes.c_int, [vp, vp]),
     ("lx_last_segment_stats", ctypes.c_int, [vp, vp]),
+    ("lx_rowseg_range", ctypes.c_int, [vp, u32p, u32p]),
+    ("lx_rowseg_bounds", ctypes.c_int, [vp, u32p]),
+    ("lx_rowseg_row_words", ctypes.c_int, [vp, u32p]),
+    ("lx_rowseg_request_cap", ctypes.c_int, [vp, u32p]),
+    ("lx_rowseg_requests", ctypes.c_int, [vp, vp, ctypes.c_uint32, u32p]),
+    ("lx_rowseg_serve", ctypes.c_int, [vp, ctypes.c_uint32, vp, vp, vp]),
+    ("lx_rowseg_receive", ctypes.c_int, [vp, ctypes.c_uint32, vp, vp, vp, u32p]),
+    ("lx_rowseg_la", ctypes.c_int, [vp, u64p]),
+    ("lx_rowseg_la_fetch", ctypes.c_int, [vp, vp]),
+    ("lx_rowseg_la_apply", ctypes.c_int, [vp, ctypes.c_uint64, vp]),
+    ("lx_rowseg_finish", ctypes.c_int, [vp]),
     ("lx_device_planes", ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), u32p, ctypes.POINTER(vp)]),
     ("lx_sync", ctypes.c_int, [vp]),
     ("lx_shard_comm_unique_id", ctypes.c_int, [u8p]),
@@ -440,6 +451,54 @@ class Index:
         st = LxStats()
         self._chk(self.L.lx_last_stats(self.h, ctypes.byref(st)))
         return {"ms_assign": st.ms_assign, "ms_index": st.ms_index, "ms_marks": st.ms_marks}
+
+    # ---- row-segment rank (options seg_count / seg_rank; lachesis_hip.rowseg drives the exchange)
+    def rowseg_range(self):
+        lo, hi = ctypes.c_uint32(), ctypes.c_uint32()
+        self._chk(self.L.lx_rowseg_range(self.h, ctypes.byref(lo), ctypes.byref(hi)))
+        return lo.value, hi.value
+
+    def rowseg_bounds(self, G):
+        b = np.zeros(G + 1, dtype=np.uint32)
+        self._chk(self.L.lx_rowseg_bounds(self.h, _p(b, u32p)))
+        return [int(x) for x in b]
+
+    def rowseg_row_words(self):
+        w = ctypes.c_uint32()
+        self._chk(self.L.lx_rowseg_row_words(self.h, ctypes.byref(w)))
+        return w.value
+
+    def rowseg_request_cap(self):
+        c = ctypes.c_uint32()
+        self._chk(self.L.lx_rowseg_request_cap(self.h, ctypes.byref(c)))
+        return c.value
+
+    def rowseg_requests(self, ids_ptr, cap, G):
+        c = np.zeros(G, dtype=np.uint32)
+        self._chk(self.L.lx_rowseg_requests(self.h, ids_ptr, cap, _p(c, u32p)))
+        return [int(x) for x in c]
+
+    def rowseg_serve(self, n, ids_ptr, rows_ptr, ready_ptr):
+        self._chk(self.L.lx_rowseg_serve(self.h, n, ids_ptr, rows_ptr, ready_ptr))
+
+    def rowseg_receive(self, n, ids_ptr, rows_ptr, ready_ptr):
+        left = ctypes.c_uint32()
+        self._chk(self.L.lx_rowseg_receive(self.h, n, ids_ptr, rows_ptr, ready_ptr, ctypes.byref(left)))
+        return left.value
+
+    def rowseg_la(self, G):
+        c = np.zeros(G, dtype=np.uint64)
+        self._chk(self.L.lx_rowseg_la(self.h, _p(c, u64p)))
+        return [int(x) for x in c]
+
+    def rowseg_la_fetch(self, ptr):
+        self._chk(self.L.lx_rowseg_la_fetch(self.h, ptr))
+
+    def rowseg_la_apply(self, n, ptr):
+        self._chk(self.L.lx_rowseg_la_apply(self.h, n, ptr))
+
+    def rowseg_finish(self):
+        self._chk(self.L.lx_rowseg_finish(self.h))
 
     def segment_stats(self):
         """Timings of the last segmented batch (option "segments")."""

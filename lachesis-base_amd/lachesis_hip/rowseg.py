@@ -1,0 +1,104 @@
+"""Row segments across GPUs.
+
+One process per GPU; rank r holds an :class:`~lachesis_hip.Index` with
+options ``seg_count=world, seg_rank=r`` and adds the epoch as one batch.
+Every rank assigns every event's branch (replicated metadata), but walks and
+owns only the rows of its Add-order segment (``rowseg_range``): the walk of
+an epoch of D DAG levels takes ~D/G levels per rank.  :meth:`RowSegments.exchange`
+then connects the segments:
+
+* rows -- a segment's first levels ("partial" events, whose rows miss the
+  last event of some branch before the segment) take the max of the final
+  rows they reference, which live on earlier ranks; the LowestAfter pass also
+  needs the row before each branch's first own event.  Each round: the ids
+  go to their owners (``all_to_all_single``), the owners answer with the rows
+  and a ready flag (a partial row of an owner still waiting is not final),
+  the rows come back; rounds repeat until no rank waits (one round when a
+  segment is longer than the DAG's observation depth);
+* LowestAfter -- a rank's range fill reaches rows of earlier segments: those
+  entries travel as (row, column, seq) triples to their owners.
+
+Afterwards each rank answers ForklessCause between its own events.  The
+reference has no multi-process index (vecfc/index.go is single-node): this
+is the MI355X scale-out of the same computation, bit-exact to the single
+index (tests/test_gpu_rowseg.py).
+"""
+
+import torch
+import torch.distributed as dist
+
+
+class RowSegments:
+    def __init__(self, index, group=None, device=None):
+        """``index``: this rank's handle (options seg_count = world, seg_rank = rank)."""
+        self.ix = index
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+        # gloo moves host tensors only: stage device buffers through the host
+        # (a rehearsal mode for several ranks sharing one GPU; RCCL is the product)
+        self.stage = dist.get_backend(group) == "gloo" and self.device.type == "cuda"
+        self.last = {}
+
+    def _a2a(self, recv, send, recv_n, send_n):
+        if self.stage:
+            r = recv.cpu()
+            dist.all_to_all_single(r, send.cpu(), output_split_sizes=recv_n, input_split_sizes=send_n, group=self.group)
+            recv.copy_(r)
+        else:
+            dist.all_to_all_single(recv, send, output_split_sizes=recv_n, input_split_sizes=send_n, group=self.group)
+
+    def _counts(self, send_n):
+        s = torch.tensor(send_n, dtype=torch.int64, device="cpu" if self.stage else self.device)
+        r = torch.empty_like(s)
+        dist.all_to_all_single(r, s, group=self.group)
+        return [int(x) for x in r.cpu()]
+
+    def _sum(self, x):
+        t = torch.tensor([x], dtype=torch.int64, device="cpu" if self.stage else self.device)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+        return int(t.item())
+
+    def exchange(self):
+        """Both exchanges and lx_rowseg_finish, after this rank's add_batch."""
+        ix, G, dev = self.ix, self.world, self.device
+        W = ix.rowseg_row_words()
+        cap = max(1, ix.rowseg_request_cap())
+        ids = torch.empty(cap, dtype=torch.int32, device=dev)
+        rounds = 0
+        rows_moved = 0
+        while True:
+            counts = ix.rowseg_requests(ids.data_ptr(), cap, G)
+            if self._sum(sum(counts)) == 0:
+                break
+            rounds += 1
+            total = sum(counts)
+            recv_n = self._counts(counts)
+            asked = torch.empty(max(1, sum(recv_n)), dtype=torch.int32, device=dev)
+            self._a2a(asked[:sum(recv_n)], ids[:total], recv_n, counts)
+            m = sum(recv_n)
+            out_rows = torch.empty(max(1, m) * W, dtype=torch.int32, device=dev)
+            out_ready = torch.empty(max(1, m), dtype=torch.int32, device=dev)
+            ix.rowseg_serve(m, asked.data_ptr(), out_rows.data_ptr(), out_ready.data_ptr())
+            got_rows = torch.empty(max(1, total) * W, dtype=torch.int32, device=dev)
+            got_ready = torch.empty(max(1, total), dtype=torch.int32, device=dev)
+            self._a2a(got_rows[:total * W], out_rows[:m * W], [c * W for c in counts], [c * W for c in recv_n])
+            self._a2a(got_ready[:total], out_ready[:m], counts, recv_n)
+            ix.rowseg_receive(total, ids.data_ptr(), got_rows.data_ptr(), got_ready.data_ptr())
+            rows_moved += total
+            if rounds > G + 1:
+                raise RuntimeError("row-segment row exchange did not converge")
+        la_counts = ix.rowseg_la(G)
+        n_send = sum(la_counts)
+        send = torch.empty(max(1, 3 * n_send), dtype=torch.int32, device=dev)
+        ix.rowseg_la_fetch(send.data_ptr())
+        recv_n = self._counts(la_counts)
+        n_recv = sum(recv_n)
+        recv = torch.empty(max(1, 3 * n_recv), dtype=torch.int32, device=dev)
+        self._a2a(recv[:3 * n_recv], send[:3 * n_send], [3 * c for c in recv_n], [3 * c for c in la_counts])
+        ix.rowseg_la_apply(n_recv, recv.data_ptr())
+        ix.rowseg_finish()
+        self.last = {"row_rounds": rounds, "rows_received": rows_moved, "la_entries_sent": n_send,
+                     "la_entries_received": n_recv}
+        return self.last
