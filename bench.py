@@ -287,6 +287,13 @@ def config_leg(lx, name, steps, warmup, device, want_cpu, cpu_budget, fc_n=1 << 
     d_c, d_s, d_p = to_dev(dag.creator), to_dev(dag.seq), to_dev(dag.par)
     d_o = to_dev(dag.poff.astype(np.uint32))
     qa, qb = lx.tools.fc_queries(dag.lamport, fc_n, window=64, seed=7)
+    if rowseg:
+        # ForklessCause between this rank's own rows: the same query shape
+        # (a uniform, b at most 64 Lamport before it) mapped into [lo, hi)
+        lo_r = N * rank // world // 64 * 64
+        hi_r = N if rank == world - 1 else N * (rank + 1) // world // 64 * 64
+        qa = (lo_r + qa.astype(np.int64) % (hi_r - lo_r)).astype(np.uint32)
+        qb = np.maximum(qa.astype(np.int64) - np.abs(qa.astype(np.int64) - qb.astype(np.int64)) % 4096, lo_r).astype(np.uint32)
     d_qa, d_qb = to_dev(qa), to_dev(qb)
     d_out = torch.empty(fc_n, dtype=torch.uint8, device=dev)
     ix = lx.Index(device=device, event_capacity=N)
@@ -511,7 +518,9 @@ def main():
                          "level-synchronous batcher releases the epoch (same DAG, renumbered)")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--mode", default="shard", choices=["replica", "shard"])
+    ap.add_argument("--mode", default="rowseg", choices=["replica", "shard", "rowseg"],
+                    help="N > 1: rowseg = the epoch split into N Add-order row segments, one walk per rank "
+                         "(DESIGN.md 6b, the default); shard = column shards; replica = independent epochs")
     ap.add_argument("--no-abft", action="store_true", help="skip the configs[4] abft leg")
     ap.add_argument("--no-dropin", action="store_true", help="skip the configs[4] drop-in (unchanged caller) leg")
     ap.add_argument("--no-latency", action="store_true", help="skip the per-call latency / antichain-fed leg")
@@ -532,6 +541,7 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     backend = os.environ.get("LX_DIST_BACKEND", "nccl")
+    rowseg = args.mode == "rowseg" and world > 1
     if backend != "nccl":
         local = local % max(1, torch.cuda.device_count())   # rehearsal: ranks may share a GPU
     if world > 1:
@@ -570,6 +580,13 @@ def main():
         hi = min(N, lo + batch)
         off = (dag.poff[lo:hi + 1] - dag.poff[lo]).astype(np.uint32)
         batches.append((lo, hi, to_dev(off), int(dag.poff[lo])))
+    if rowseg:
+        # ForklessCause between this rank's own rows: the same query shape
+        # (a uniform, b at most 64 Lamport before it) mapped into [lo, hi)
+        lo_r = N * rank // world // 64 * 64
+        hi_r = N if rank == world - 1 else N * (rank + 1) // world // 64 * 64
+        qa = (lo_r + qa.astype(np.int64) % (hi_r - lo_r)).astype(np.uint32)
+        qb = np.maximum(qa.astype(np.int64) - np.abs(qa.astype(np.int64) - qb.astype(np.int64)) % 4096, lo_r).astype(np.uint32)
     d_qa, d_qb = to_dev(qa), to_dev(qb)
     d_out = torch.empty(args.fc_queries, dtype=torch.uint8, device=dev)
 
@@ -579,6 +596,10 @@ def main():
         ix = lx.Index(device=local, event_capacity=N, shard_rank=0, shard_count=solo)
         d_part = torch.empty(args.fc_queries, dtype=torch.int32, device=dev)
         d_blk = None
+    elif rowseg:
+        ix = lx.Index(device=local, event_capacity=N, options={"seg_count": world, "seg_rank": rank})
+        from lachesis_hip.rowseg import RowSegments
+        rsx = RowSegments(ix, device=dev)
     elif shard:
         ix = lx.Index(device=local, event_capacity=N, shard_rank=rank, shard_count=world)
         from lachesis_hip.shard import ShardedIndex
@@ -602,6 +623,10 @@ def main():
         if shard:
             tx = time.perf_counter()
             sx.exchange()
+            st_x.append((time.perf_counter() - tx) * 1e3)
+        if rowseg:
+            tx = time.perf_counter()
+            rsx.exchange()
             st_x.append((time.perf_counter() - tx) * 1e3)
         if solo:
             nonlocal d_blk
@@ -676,7 +701,7 @@ def main():
     # sum of stakes over branches j with 0 < LA(b)[j] <= HB(a)[j].Seq >= quorum
     # (vecfc/forkless_cause.go:63-82; the bench DAG has no forks)
     spot_n = 0
-    if not (shard or solo):
+    if not (shard or solo or rowseg):
         import numpy as np
         qa_s, qb_s = qa[:4096], qb[:4096]
         got = d_out[:4096].cpu().numpy()
@@ -690,9 +715,10 @@ def main():
         assert np.array_equal(got, want), "ForklessCause spot check failed"
         spot_n = len(got)
 
-    units = 1 if shard else world          # shard: the ranks share one epoch
+    units = 1 if (shard or rowseg) else world          # shard / rowseg: the ranks share one epoch
+    fc_units = 1 if shard else world                   # rowseg: every rank answers its own batch of queries
     events_per_s = N * args.steps * units / t_index
-    fc_per_s = args.fc_queries * args.steps * units / t_fc
+    fc_per_s = args.fc_queries * args.steps * fc_units / t_fc
     B = ix.num_branches()
     if shard or solo:
         lo, hi = ix.shard_range(rank)
@@ -717,7 +743,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": t_index / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "strong" if shard else "weak",
+        "scaling": "strong" if (shard or rowseg) else "weak",
         "vs_baseline": None,
         "dtype": "u32",
         "data": "synthetic tdag-structured DAG (splitmix64 seed 1), no forks",
@@ -725,7 +751,8 @@ def main():
                    % (args.config, V, N, epv, P, wkind, cheaters, int(np.log2(args.fc_queries)), ),
                    "validators": V, "events": N, "parents": P, "fc_queries": args.fc_queries,
                    "parallelism": ("solo-shard0-of-%d" % solo) if solo else
-                                  ("colshard%d" if shard else "replica%d") % world, "batch": batch},
+                                  ("colshard%d" if shard else "rowseg%d" if rowseg else "replica%d") % world,
+                   "batch": batch},
         "fc_queries_per_sec": fc_per_s,
         "fc_ms_per_step": t_fc / args.steps * 1e3,
         "index_kernel_ms": kidx,
@@ -750,6 +777,15 @@ def main():
         sg["note"] = ("one GPU, the segments walked one after another; a rank of the row-segment mode walks one "
                       "segment and does 1/G of the fix-up and LowestAfter passes")
         result["segments"] = sg
+    if rowseg:
+        sg = ix.segment_stats()
+        result["rowseg"] = {"rows": [int(x) for x in ix.rowseg_range()], "walk_ms": sg["walk_ms"][rank],
+                            "partial_events": sg["partial"][rank], "partial_ms": sg["partial_ms"], "la_ms": sg["la_ms"],
+                            "exchange_ms": float(np.mean(st_x[-args.steps:])) if st_x else None,
+                            "exchange": rsx.last,
+                            "note": "index step = assignment of every event + walk of the own segment + row "
+                                    "requests, partial fix-up, LowestAfter pass and triples (exchange_ms), timed "
+                                    "inside value; FC: 2^k queries per rank between its own rows"}
     if shard or solo:
         wire = sorted(set(w for w in sx.last_wire[0] if w)) if shard and getattr(sx, "last_wire", None) else \
             [ix.shard_wire_bytes()]

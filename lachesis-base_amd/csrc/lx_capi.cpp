@@ -59,11 +59,11 @@ void free_all(lx_index *h) {
     for (void *p : lptrs)
         if (p) (void)hipFree(p);
     h->cheat_brl = h->cheat_crl = h->cmap = h->lap = h->wloc = nullptr;
-    void *gptrs[] = {h->seg_jt, h->seg_cnt, h->seg_mf, h->seg_plist};
+    void *gptrs[] = {h->seg_jt, h->seg_cnt, h->seg_mf, h->seg_plist, h->seg_elist};
     for (void *p : gptrs)
         if (p) (void)hipFree(p);
-    h->seg_jt = h->seg_cnt = h->seg_mf = h->seg_plist = nullptr;
-    h->seg_jt_cap = h->seg_cnt_cap = h->seg_mf_cap = h->seg_plist_cap = 0;
+    h->seg_jt = h->seg_cnt = h->seg_mf = h->seg_plist = h->seg_elist = nullptr;
+    h->seg_jt_cap = h->seg_cnt_cap = h->seg_mf_cap = h->seg_plist_cap = h->seg_elist_cap = 0;
     rs_free(h);
     h->fk_w = h->fk_c = h->fk_wch = nullptr;
     h->fk_cap = 0;
@@ -455,15 +455,18 @@ int seg_walk(lx_index *h, IndexArgs ia, const uint32_t *poff, hipStream_t s) {
     a.own_seg = LX_NONE;
     int rc;
     if ((rc = grow_scratch(h, &h->seg_jt, &h->seg_jt_cap, (uint64_t)(G + 1) * h->B)) ||
-        (rc = grow_scratch(h, &h->seg_cnt, &h->seg_cnt_cap, (uint64_t)h->B + kMaxSegments + 2)) ||
+        (rc = grow_scratch(h, &h->seg_cnt, &h->seg_cnt_cap, (uint64_t)h->B + 2 * kMaxSegments)) ||
         (rc = grow_scratch(h, &h->seg_mf, &h->seg_mf_cap, (uint64_t)n)) ||
-        (rc = grow_scratch(h, &h->seg_plist, &h->seg_plist_cap, (uint64_t)n)))
+        (rc = grow_scratch(h, &h->seg_plist, &h->seg_plist_cap, (uint64_t)n)) ||
+        (rc = grow_scratch(h, &h->seg_elist, &h->seg_elist_cap, (uint64_t)n)))
         return rc;
     a.jt = h->seg_jt;
     a.cnt = h->seg_cnt;
     a.pcount = h->seg_cnt + h->B;
     a.pflag = h->seg_mf;
     a.plist = h->seg_plist;
+    a.elist = h->seg_elist;
+    a.ecount = a.pcount + G;
     while (h->seg_ev.size() < 2 * G + 3) {
         hipEvent_t e;
         HIPCHK(h, hipEventCreate(&e));
@@ -488,16 +491,15 @@ int seg_walk(lx_index *h, IndexArgs ia, const uint32_t *poff, hipStream_t s) {
         HIPCHK(h, lx::launch_index(sk, s));
         HIPCHK(h, hipEventRecord(ev[2 * k + 1], s));
     }
-    uint32_t pc[kMaxSegments + 2];
-    HIPCHK(h, hipMemcpyAsync(pc, a.pcount, (G + 2) * 4, hipMemcpyDeviceToHost, s));
+    uint32_t pc[kMaxSegments], ec[kMaxSegments];
+    HIPCHK(h, hipMemcpyAsync(pc, a.pcount, G * 4, hipMemcpyDeviceToHost, s));
     HIPCHK(h, hipStreamSynchronize(s));
     for (uint32_t k = 0; k < G; k++) HIPCHK(h, lx::launch_seg_partial(a, k, pc[k], s));
     HIPCHK(h, hipEventRecord(ev[2 * G], s));
-    a.ev_lo = bs;
-    a.ev_hi = bs + n;
-    a.k_lo = pc[G];
-    a.k_hi = pc[G + 1];
-    HIPCHK(h, lx::launch_seg_la(a, s));
+    for (uint32_t k = 0; k < G; k++) HIPCHK(h, lx::launch_seg_edges(a, k, pc[k], s));
+    HIPCHK(h, hipMemcpyAsync(ec, a.ecount, G * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(h, hipStreamSynchronize(s));
+    for (uint32_t k = 0; k < G; k++) HIPCHK(h, lx::launch_seg_la_edge(a, k, ec[k], s));
     HIPCHK(h, hipEventRecord(ev[2 * G + 1], s));
     HIPCHK(h, hipStreamSynchronize(s));
     lx_seg_stats &st = h->seg_stats;

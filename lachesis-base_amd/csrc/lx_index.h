@@ -206,15 +206,15 @@ struct lx_index {
     bool fcc_slots_set = false;            // set by the option (else sized at lx_reset from V)
     // segmented walk (option segments, lx_segment.hip): scratch and timings of the last batch
     uint32_t segments = 0;
-    uint32_t *seg_jt = nullptr, *seg_cnt = nullptr, *seg_mf = nullptr, *seg_plist = nullptr;   // seg_mf: partial flags
-    uint64_t seg_jt_cap = 0, seg_cnt_cap = 0, seg_mf_cap = 0, seg_plist_cap = 0;
+    uint32_t *seg_jt = nullptr, *seg_cnt = nullptr, *seg_mf = nullptr, *seg_plist = nullptr, *seg_elist = nullptr;
+    uint64_t seg_jt_cap = 0, seg_cnt_cap = 0, seg_mf_cap = 0, seg_plist_cap = 0, seg_elist_cap = 0;   // seg_mf: flags
     std::vector<hipEvent_t> seg_ev;
     lx_seg_stats seg_stats{};
     // row-segment rank (options seg_rank / seg_count, lx_rowseg.cpp): one batch
     // per epoch, this rank walks and owns the rows of segment rs_rank
     uint32_t rs_rank = 0, rs_count = 0;
     int rs_state = 0;                      // 0 idle, 1 rows needed, 2 rows final, 3 LowestAfter sent, 4 ready
-    uint32_t rs_lo = 0, rs_hi = 0, rs_npartial = 0, rs_nreq = 0, rs_klo = 0, rs_khi = 0;
+    uint32_t rs_lo = 0, rs_hi = 0, rs_npartial = 0, rs_nreq = 0;
     uint32_t rs_seg_lo[kMaxSegments + 1] = {};
     uint32_t *rs_need = nullptr, *rs_req = nullptr, *rs_ctr = nullptr, *rs_ids = nullptr, *rs_out = nullptr,
              *rs_send = nullptr;

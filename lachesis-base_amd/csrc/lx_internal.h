@@ -443,14 +443,16 @@ struct SegArgs {
     const uint32_t *brow;
     uint32_t s_cap;
     uint32_t *jt;                // [(G + 1) * B]: row k = J_k, last seq of each branch before segment k
-    uint32_t *cnt;               // [B] batch events per branch, then [G] partial counts
+    uint32_t *cnt;               // [B] batch events per branch, then [G] partial counts, [G] edge counts
     uint32_t *pflag;             // [n] partial flags (k_index drains)
     uint32_t *plist;             // partial events of segment k at plist[seg_lo[k] - bs ..]
     uint32_t *pcount;            // [G]
-    // LowestAfter pass (k_seg_la): events [ev_lo, ev_hi) fill, at chain positions [k_lo, k_hi)
-    uint32_t ev_lo, ev_hi;
-    uint32_t k_lo, k_hi;
-    uint32_t own_seg;            // row-segment rank: its segment (k range of k_seg_prefix_j); LX_NONE: the batch
+    // LowestAfter of the rows up to J_k (k_seg_la_edge): the events whose
+    // range reaches them -- partial events, their successors on their
+    // branch, every branch's first event in the segment
+    uint32_t *elist;
+    uint32_t *ecount;
+    uint32_t own_seg;            // row-segment rank: its segment; LX_NONE: every segment of the batch
     uint32_t own_lo;             // rows below it are another rank's: their entries go to out[seg_of(row)]
     uint32_t *out;               // per destination segment d: out_cap triples (row, column, seq) at out + 3 d out_cap
     uint32_t *out_count;         // [G]
@@ -477,7 +479,8 @@ struct RsArgs {
 namespace lx {
 hipError_t launch_seg_tables(const SegArgs &a, hipStream_t s);
 hipError_t launch_seg_partial(const SegArgs &a, uint32_t k, uint32_t count, hipStream_t s);
-hipError_t launch_seg_la(const SegArgs &a, hipStream_t s);
+hipError_t launch_seg_edges(const SegArgs &a, uint32_t k, uint32_t n_partial, hipStream_t s);
+hipError_t launch_seg_la_edge(const SegArgs &a, uint32_t k, uint32_t count, hipStream_t s);
 hipError_t launch_rs_refs(const SegArgs &a, const RsArgs &r, uint32_t n_partial, hipStream_t s);
 hipError_t launch_rs_bucket(const SegArgs &a, const RsArgs &r, uint32_t n_req, uint32_t *out, uint32_t *counts,
                             hipStream_t s);

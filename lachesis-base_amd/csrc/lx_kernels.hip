@@ -695,7 +695,7 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
                             }
                         }
                     }
-                    if (!got) {
+                    if (!got && !(a.seg && pl >= n)) {   // (segment walk: a prev before the segment counts below as J_k)
                         const uint32_t *row = a.hb + (uint64_t)prev * stride;
 #pragma unroll
                         for (int k = 0; k < CPW; k++) h0[k] = valid[k] ? ld_l2_now(row + pc[k]) : 0u;
@@ -733,8 +733,11 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
                     uint32_t lo[CPW], hi[CPW];
 #pragma unroll
                     for (int k = 0; k < CPW; k++) {
-                        lo[k] = max(h0[k] + 1u, first[k]);
-                        hi[k] = valid[k] && !a.seg ? (r[k] & mask) : 0u;
+                        // segment walk: the rows after J_k only; L is RAW there for this
+                        // event and its prev (lx_segment.hip), the rows up to J_k are
+                        // filled by k_seg_la_edge
+                        lo[k] = max(max(h0[k], sj[k]) + 1u, first[k]);
+                        hi[k] = valid[k] ? (r[k] & mask) : 0u;
                     }
                     if (a.lap) {
                         // sharded: rows of own branches addressed by (column, seq)

@@ -47,6 +47,8 @@ SegArgs rs_seg_args(lx_index *h) {
     a.pcount = h->seg_cnt + h->B;
     a.pflag = h->seg_mf;
     a.plist = h->seg_plist;
+    a.elist = h->seg_elist;
+    a.ecount = a.pcount + h->rs_count;
     a.own_seg = h->rs_rank;
     a.own_lo = h->rs_lo;
     return a;
@@ -114,9 +116,10 @@ int rs_begin(lx_index *h, IndexArgs ia, const uint32_t *poff, hipStream_t s) {
     h->rs_hi = h->rs_seg_lo[k + 1];
     int rc;
     if ((rc = grow_scratch(h, &h->seg_jt, &h->seg_jt_cap, (uint64_t)(G + 1) * h->B)) ||
-        (rc = grow_scratch(h, &h->seg_cnt, &h->seg_cnt_cap, (uint64_t)h->B + kMaxSegments + 2)) ||
+        (rc = grow_scratch(h, &h->seg_cnt, &h->seg_cnt_cap, (uint64_t)h->B + 2 * kMaxSegments)) ||
         (rc = grow_scratch(h, &h->seg_mf, &h->seg_mf_cap, (uint64_t)n)) ||
         (rc = grow_scratch(h, &h->seg_plist, &h->seg_plist_cap, (uint64_t)n)) ||
+        (rc = grow_scratch(h, &h->seg_elist, &h->seg_elist_cap, (uint64_t)n)) ||
         (rc = grow_scratch(h, &h->rs_need, &h->rs_need_cap, (uint64_t)n)) ||
         (rc = grow_scratch(h, &h->rs_ctr, &h->rs_ctr_cap, (uint64_t)2 + 2 * kMaxSegments)))
         return rc;
@@ -145,12 +148,10 @@ int rs_begin(lx_index *h, IndexArgs ia, const uint32_t *poff, hipStream_t s) {
     HIPCHK(h, hipEventRecord(h->seg_ev[0], s));
     HIPCHK(h, lx::launch_index(ia, s));
     HIPCHK(h, hipEventRecord(h->seg_ev[1], s));
-    uint32_t pc[kMaxSegments + 2];
-    HIPCHK(h, hipMemcpyAsync(pc, a.pcount, (G + 2) * 4, hipMemcpyDeviceToHost, s));
+    uint32_t pc = 0;
+    HIPCHK(h, hipMemcpyAsync(&pc, a.pcount + k, 4, hipMemcpyDeviceToHost, s));
     HIPCHK(h, hipStreamSynchronize(s));
-    h->rs_npartial = pc[k];
-    h->rs_klo = pc[G];
-    h->rs_khi = pc[G + 1];
+    h->rs_npartial = pc;
     // the rows to ask for: at most every referenced branch of every partial
     // event plus one per branch, and never more than the events before lo
     const uint64_t want = std::min<uint64_t>((uint64_t)h->rs_npartial * h->B + h->B, (uint64_t)h->rs_lo + 1);
@@ -250,26 +251,27 @@ int lx_rowseg_la(lx_index *h, uint64_t *counts) {
     const uint32_t G = h->rs_count;
     if (!h->rs_out_per) h->rs_out_per = 1u << 18;
     std::vector<uint32_t> c(G);
+    // the own events whose LowestAfter range reaches rows before the segment
+    SegArgs a = rs_seg_args(h);
+    uint32_t ne = 0;
+    HIPCHK(h, hipEventRecord(h->seg_ev[4], h->stream));
+    HIPCHK(h, lx::launch_seg_edges(a, h->rs_rank, h->rs_npartial, h->stream));
+    HIPCHK(h, hipMemcpyAsync(&ne, a.ecount + h->rs_rank, 4, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
     for (int attempt = 0; attempt < 2; attempt++) {
         if ((rc = grow_scratch(h, &h->rs_out, &h->rs_out_cap, 3ull * G * h->rs_out_per))) return rc;
-        SegArgs a = rs_seg_args(h);
-        a.ev_lo = h->rs_lo;
-        a.ev_hi = h->rs_hi;
-        a.k_lo = h->rs_klo;
-        a.k_hi = h->rs_khi;
         a.out = h->rs_out;
         a.out_count = h->rs_ctr + 2 + kMaxSegments;
         a.out_cap = h->rs_out_per;
         HIPCHK(h, hipMemsetAsync(a.out_count, 0, G * 4, h->stream));
-        HIPCHK(h, hipEventRecord(h->seg_ev[4], h->stream));
-        HIPCHK(h, lx::launch_seg_la(a, h->stream));
+        HIPCHK(h, lx::launch_seg_la_edge(a, h->rs_rank, ne, h->stream));
         HIPCHK(h, hipEventRecord(h->seg_ev[5], h->stream));
         HIPCHK(h, hipMemcpyAsync(c.data(), a.out_count, G * 4, hipMemcpyDeviceToHost, h->stream));
         HIPCHK(h, hipStreamSynchronize(h->stream));
         const uint32_t mx = *std::max_element(c.begin(), c.end());
         if (mx <= h->rs_out_per) break;
         // too many entries for a destination: larger buckets, the same pass
-        // again (its own stores are idempotent)
+        // again (it writes only these buckets)
         h->rs_out_per = (uint64_t)mx + mx / 4;
         if (attempt) return h->fail(LX_ERR_STATE, "row-segment LowestAfter buckets overflowed twice");
     }

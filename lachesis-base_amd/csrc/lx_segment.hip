@@ -15,8 +15,15 @@
 // a branch-c event after J_k[c], so every term of the max is <= J_k <= L(e).
 // The walk's drains flag the others ("partial": the first levels of a
 // segment); k_seg_partial gathers their referenced rows, segment by segment
-// (a reference always lies in an earlier segment, final by then).  LowestAfter
-// is then the walker's range fill computed from the final rows (k_seg_la), and
+// (a reference always lies in an earlier segment, final by then).
+//
+// LowestAfter: event e (prev p on its branch) fills (RAW(p)[c], RAW(e)[c]].
+// The part above J_k[c] (rows of the segment) is (max(L(p)[c], J_k[c]),
+// L(e)[c]] exactly -- above J_k a column of L is RAW -- so the walker's
+// drains fill it as in an ordinary walk.  The part up to J_k[c] (rows before
+// the segment) is empty unless p misses (c, J_k[c]): p partial, or p before
+// the segment (e is its branch's first event in it); k_seg_la_edge fills it
+// from the final rows for exactly those events and their partial ones.  Then
 // the batch's tail zeroing and fork marks run as after an ordinary walk.
 #include "lx_internal.h"
 
@@ -49,9 +56,7 @@ __global__ void k_seg_scan(SegArgs a) {
     atomicAdd(a.cnt + b, 1u);
 }
 
-// J_0 from the branch lengths before the batch, then J_{k+1} = max(J_k, last
-// in k); the chain positions of the batch's events: [min before, max length)
-// into cnt[B + G], cnt[B + G + 1]
+// J_0 from the branch lengths before the batch, then J_{k+1} = max(J_k, last in k)
 __global__ void k_seg_prefix_j(SegArgs a) {
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= a.B) return;
@@ -62,20 +67,6 @@ __global__ void k_seg_prefix_j(SegArgs a) {
         uint32_t *p = a.jt + (uint64_t)k * a.B + c;
         j = max(j, *p);
         *p = j;
-    }
-    if (a.own_seg == LX_NONE) {
-        if (a.cnt[c]) {
-            atomicMin(a.cnt + a.B + a.G, before);
-            atomicMax(a.cnt + a.B + a.G + 1, a.branch_len[c]);
-        }
-    } else {
-        // chain positions of the own segment's events of branch c
-        const uint32_t j0 = a.jt[(uint64_t)a.own_seg * a.B + c], j1 = a.jt[(uint64_t)(a.own_seg + 1) * a.B + c];
-        if (j1 > j0) {
-            const uint32_t f = a.branch_first[c];
-            atomicMin(a.cnt + a.B + a.G, j0 ? j0 - f + 1 : 0u);
-            atomicMax(a.cnt + a.B + a.G + 1, j1 - f + 1);
-        }
     }
 }
 
@@ -106,106 +97,54 @@ __global__ void __launch_bounds__(256) k_seg_partial(SegArgs a, uint32_t k) {
     }
 }
 
-// LowestAfter from the final rows: event y = (j, k) (the k-th event of
-// branch j's chain) first observes the events (c, s), s in
-// (RAW(prev)[c], RAW(y)[c]], prev = (j, k - 1) (the
-// walker's range fill).  A task is 64 consecutive branches x kLK chain
-// positions; it stages the rows of (j, k - 1 .. k + kLK - 1) 64 columns at a
-// time through LDS, then a wave's lanes are the 64 branches of one column, so
-// the stores of one seq s land in one 256-B run of row (c, s).  Tasks are
-// dealt to XCDs in contiguous ranges (branch block major): the LowestAfter
-// columns of a branch block are written through one XCD's L2, where the runs
-// written by tasks at neighbouring chain positions merge into whole lines.
-constexpr int kLJ = 64, kLC = 64, kLK = 16;
+// the events of segment k whose LowestAfter range reaches rows before the
+// segment: partial events and their successors, every branch's first event
+// (bit 1 of pflag dedupes; the list at elist[seg_lo[k] - bs ..])
+__device__ __forceinline__ void edge_want(const SegArgs &a, uint32_t k, uint32_t e) {
+    if (!(atomicOr(a.pflag + (e - a.bs), 2u) & 2u))
+        a.elist[a.seg_lo[k] - a.bs + atomicAdd(a.ecount + k, 1u)] = e;
+}
 
-__global__ void __launch_bounds__(256) k_seg_la(SegArgs a, uint32_t nkc, uint32_t ntask) {
-    __shared__ uint32_t buf[2][kLJ][kLC + 1];
-    __shared__ uint32_t yrow[kLK + 1][kLJ];
-    __shared__ uint32_t yany[kLK + 1];
-    const uint32_t per = (ntask + 7) / 8;
-    const uint32_t task = (blockIdx.x % 8) * per + blockIdx.x / 8;
-    if (task >= ntask) return;
-    const uint32_t jb = task / nkc, kc = task % nkc;
-    const int64_t k0 = (int64_t)a.k_lo + (int64_t)kc * kLK;
-    const uint32_t tid = threadIdx.x, wave = tid / 64, lane = tid % 64;
-    if (tid <= kLK) yany[tid] = 0;
-    __syncthreads();
-    for (uint32_t i = tid; i < (kLK + 1) * kLJ; i += 256) {
-        const uint32_t kk = i / kLJ, j = jb * kLJ + i % kLJ;
-        const int64_t k = k0 - 1 + kk;
-        uint32_t r = LX_NONE;
-        if (j < a.B && k >= 0 && k < (int64_t)a.branch_len[j]) r = a.brow[(uint64_t)j * a.s_cap + k];
-        yrow[kk][i % kLJ] = r;
-        if (kk && r != LX_NONE && r >= a.ev_lo && r < a.ev_hi) yany[kk] = 1;
+__global__ void k_seg_edges(SegArgs a, uint32_t k, uint32_t n_partial) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t *J0 = a.jt + (uint64_t)k * a.B, *J1 = a.jt + (uint64_t)(k + 1) * a.B;
+    if (t < n_partial) {
+        const uint32_t e = a.plist[a.seg_lo[k] - a.bs + t];
+        edge_want(a, k, e);
+        const uint32_t j = a.ev_branch[e], s = a.ev_seq[e];
+        if (s < J1[j]) edge_want(a, k, row_of(a, j, s + 1));
+    } else if (t - n_partial < a.B) {
+        const uint32_t j = t - n_partial;
+        if (J1[j] > J0[j]) edge_want(a, k, row_of(a, j, J0[j] ? J0[j] + 1 : a.branch_first[j]));
     }
-    __syncthreads();
-    const uint32_t j = jb * kLJ + lane;
-    const uint32_t fj = j < a.B ? a.branch_first[j] : 0u;
-    const uint32_t ncc = (a.B + kLC - 1) / kLC;
-    for (uint32_t cc = 0; cc < ncc; cc++) {
-        const uint32_t c0 = cc * kLC;
-        auto load = [&](uint32_t kk, uint32_t (*dst)[kLC + 1]) {
-            for (uint32_t i = tid; i < kLJ * kLC / 4; i += 256) {
-                const uint32_t r = i / (kLC / 4), q = i % (kLC / 4);
-                const uint32_t y = yrow[kk][r];
-                uint4 v = make_uint4(0, 0, 0, 0);
-                if (y != LX_NONE) v = *reinterpret_cast<const uint4 *>(a.hb + (uint64_t)y * a.stride + c0 + q * 4);
-                dst[r][q * 4 + 0] = v.x & LX_SEQ_MASK;
-                dst[r][q * 4 + 1] = v.y & LX_SEQ_MASK;
-                dst[r][q * 4 + 2] = v.z & LX_SEQ_MASK;
-                dst[r][q * 4 + 3] = v.w & LX_SEQ_MASK;
-            }
-        };
-        int pk = -1;        // chain offset whose rows buf[pb] holds (uniform)
-        uint32_t pb = 0;
-        for (uint32_t kk = 0; kk < (uint32_t)kLK; kk++) {
-            if (!yany[kk + 1]) continue;   // no event of this pass at kk + 1 (uniform)
-            if (pk != (int)kk) load(kk, buf[pb]);
-            uint32_t (*P)[kLC + 1] = buf[pb];
-            uint32_t (*R)[kLC + 1] = buf[pb ^ 1];
-            load(kk + 1, R);
-            __syncthreads();
-            const uint32_t y = yrow[kk + 1][lane];
-            if (y != LX_NONE && y >= a.ev_lo && y < a.ev_hi) {
-                const uint32_t sq = fj + (uint32_t)(k0 + kk);
-                // the wave's 16 columns: ranges first, then every first row
-                // lookup in flight at once (the lookups were the pass's
-                // critical path when issued one column at a time)
-                constexpr int T = kLC / 4;
-                uint32_t lo[T], hi[T], x[T];
-#pragma unroll
-                for (int t = 0; t < T; t++) {
-                    const uint32_t ci = wave + 4 * t, c = c0 + ci;
-                    const bool v = c < a.B;
-                    const uint32_t f = v ? a.branch_first[c] : 1u;
-                    hi[t] = v ? R[lane][ci] : 0u;
-                    lo[t] = max(P[lane][ci] + 1u, f);
-                    x[t] = lo[t] <= hi[t] ? a.brow[(uint64_t)c * a.s_cap + (lo[t] - f)] : 0u;
-                }
-#pragma unroll
-                for (int t = 0; t < T; t++) {
-                    const uint32_t c = c0 + wave + 4 * t;
-                    for (uint32_t s = lo[t]; s <= hi[t]; s++) {
-                        const uint32_t xr = s == lo[t] ? x[t] : row_of(a, c, s);
-                        if (xr >= a.own_lo) {
-                            a.la[(uint64_t)xr * a.stride + j] = sq;
-                        } else {
-                            // another rank's row: to the owner of its segment
-                            const uint32_t d = seg_of(a, xr);
-                            const uint32_t p = atomicAdd(a.out_count + d, 1u);
-                            if (p < a.out_cap) {
-                                uint32_t *o = a.out + 3ull * (d * a.out_cap + p);
-                                o[0] = xr;
-                                o[1] = j;
-                                o[2] = sq;
-                            }
-                        }
-                    }
+}
+
+// one workgroup per listed event e = (j, s) of segment k: the entries
+// (c, s'), s' in (RAW(p)[c], min(RAW(e)[c], J_k[c])], from the final rows
+__global__ void __launch_bounds__(256) k_seg_la_edge(SegArgs a, uint32_t k) {
+    const uint32_t e = a.elist[a.seg_lo[k] - a.bs + blockIdx.x];
+    const uint32_t j = a.ev_branch[e], sq = a.ev_seq[e];
+    const uint32_t *J = a.jt + (uint64_t)k * a.B;
+    const uint32_t *re = a.hb + (uint64_t)e * a.stride;
+    const uint32_t *rp = sq > a.branch_first[j] ? a.hb + (uint64_t)row_of(a, j, sq - 1) * a.stride : nullptr;
+    for (uint32_t c = threadIdx.x; c < a.B; c += blockDim.x) {
+        const uint32_t hi = min(re[c] & LX_SEQ_MASK, J[c]);
+        const uint32_t lo = max(rp ? (rp[c] & LX_SEQ_MASK) + 1u : 1u, a.branch_first[c]);
+        for (uint32_t s = lo; s <= hi; s++) {
+            const uint32_t x = row_of(a, c, s);
+            if (x >= a.own_lo) {
+                a.la[(uint64_t)x * a.stride + j] = sq;
+            } else {
+                // another rank's row: to the owner of its segment
+                const uint32_t d = seg_of(a, x);
+                const uint32_t p = atomicAdd(a.out_count + d, 1u);
+                if (p < a.out_cap) {
+                    uint32_t *o = a.out + 3ull * (d * a.out_cap + p);
+                    o[0] = x;
+                    o[1] = j;
+                    o[2] = sq;
                 }
             }
-            __syncthreads();
-            pb ^= 1;
-            pk = (int)kk + 1;
         }
     }
 }
@@ -267,7 +206,7 @@ __global__ void __launch_bounds__(1024) k_rs_bucket(SegArgs a, RsArgs r, uint32_
 __global__ void __launch_bounds__(256) k_rs_gather(RsArgs r, const uint32_t *ids, uint32_t *rows, uint32_t *ready) {
     const uint32_t x = ids[blockIdx.x];
     const bool own = x >= r.lo && x < r.hi;
-    const bool ok = own && (r.partials_done || !r.pflag[x - r.lo]);
+    const bool ok = own && (r.partials_done || !(r.pflag[x - r.lo] & 1u));
     if (threadIdx.x == 0) ready[blockIdx.x] = ok ? 1u : 0u;
     if (!ok) return;
     const uint32_t *src = r.hb + (uint64_t)x * r.stride;
@@ -301,9 +240,7 @@ inline uint32_t nb(uint64_t n, uint32_t t) { return (uint32_t)((n + t - 1) / t);
 hipError_t launch_seg_tables(const SegArgs &a, hipStream_t s) {
     hipError_t e;
     if ((e = hipMemsetAsync(a.jt, 0, (uint64_t)(a.G + 1) * a.B * 4, s)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(a.cnt, 0, (uint64_t)(a.B + a.G) * 4, s)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(a.cnt + a.B + a.G, 0xFF, 4, s)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(a.cnt + a.B + a.G + 1, 0, 4, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(a.cnt, 0, (uint64_t)(a.B + 2 * a.G) * 4, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(a.pflag, 0, (uint64_t)a.n * 4, s)) != hipSuccess) return e;
     hipLaunchKernelGGL(k_seg_scan, dim3(nb(a.n, 256)), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_seg_prefix_j, dim3(nb(a.B, 256)), dim3(256), 0, s, a);
@@ -348,11 +285,14 @@ hipError_t launch_rs_la_apply(const RsArgs &r, const uint32_t *triples, uint64_t
     return hipGetLastError();
 }
 
-hipError_t launch_seg_la(const SegArgs &a, hipStream_t s) {
-    if (a.k_hi <= a.k_lo || !a.B) return hipSuccess;
-    const uint32_t nkc = nb(a.k_hi - a.k_lo, kLK), njb = nb(a.B, kLJ);
-    const uint32_t ntask = nkc * njb;
-    hipLaunchKernelGGL(k_seg_la, dim3(8 * nb(ntask, 8)), dim3(256), 0, s, a, nkc, ntask);
+hipError_t launch_seg_edges(const SegArgs &a, uint32_t k, uint32_t n_partial, hipStream_t s) {
+    hipLaunchKernelGGL(k_seg_edges, dim3(nb((uint64_t)n_partial + a.B, 256)), dim3(256), 0, s, a, k, n_partial);
+    return hipGetLastError();
+}
+
+hipError_t launch_seg_la_edge(const SegArgs &a, uint32_t k, uint32_t count, hipStream_t s) {
+    if (!count) return hipSuccess;
+    hipLaunchKernelGGL(k_seg_la_edge, dim3(count), dim3(256), 0, s, a, k);
     return hipGetLastError();
 }
 
