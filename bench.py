@@ -287,13 +287,6 @@ def config_leg(lx, name, steps, warmup, device, want_cpu, cpu_budget, fc_n=1 << 
     d_c, d_s, d_p = to_dev(dag.creator), to_dev(dag.seq), to_dev(dag.par)
     d_o = to_dev(dag.poff.astype(np.uint32))
     qa, qb = lx.tools.fc_queries(dag.lamport, fc_n, window=64, seed=7)
-    if rowseg:
-        # ForklessCause between this rank's own rows: the same query shape
-        # (a uniform, b at most 64 Lamport before it) mapped into [lo, hi)
-        lo_r = N * rank // world // 64 * 64
-        hi_r = N if rank == world - 1 else N * (rank + 1) // world // 64 * 64
-        qa = (lo_r + qa.astype(np.int64) % (hi_r - lo_r)).astype(np.uint32)
-        qb = np.maximum(qa.astype(np.int64) - np.abs(qa.astype(np.int64) - qb.astype(np.int64)) % 4096, lo_r).astype(np.uint32)
     d_qa, d_qb = to_dev(qa), to_dev(qb)
     d_out = torch.empty(fc_n, dtype=torch.uint8, device=dev)
     ix = lx.Index(device=device, event_capacity=N)

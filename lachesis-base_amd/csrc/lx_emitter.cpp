@@ -32,6 +32,11 @@ struct lx_qi {
     uint32_t *cheat_off = nullptr, *cheat_br = nullptr;
     uint32_t *d_ev = nullptr, *d_tg = nullptr;
     unsigned long long *d_out = nullptr;
+    unsigned long long *lastk = nullptr;   // [V + 1] last batch position per creator / self (k_qi_mark)
+    uint32_t gen = 0;
+    std::vector<uint32_t> stage;           // host image of a large batch: events, then self flags
+    hipEvent_t staged = nullptr;           // its copy has read `stage`
+    hipEvent_t done = nullptr;             // the last ProcessEvent launch finished (freeing waits for it)
     uint64_t cap = 0;
 
     int fail(int code, const char *fmt, ...) {
@@ -64,7 +69,7 @@ namespace {
 
 void qi_free(lx_qi *q) {
     void *p[] = {q->mt, q->sp, q->median, q->weights, q->cheat_of, q->cheat_off, q->cheat_br, q->d_ev, q->d_tg,
-                 q->d_out};
+                 q->d_out, q->lastk};
     for (void *x : p)
         if (x) (void)hipFree(x);
     q->mt = q->sp = q->median = q->weights = nullptr;
@@ -72,6 +77,7 @@ void qi_free(lx_qi *q) {
     q->cheat_off = q->cheat_br = nullptr;
     q->d_ev = q->d_tg = nullptr;
     q->d_out = nullptr;
+    q->lastk = nullptr;
     q->cap = 0;
     q->B = 0;
 }
@@ -127,12 +133,15 @@ QiArgs qi_args(lx_qi *q, const IndexView &iv) {
     a.mt = q->mt;
     a.sp = q->sp;
     a.median = q->median;
+    a.ev_creator = iv.ev_creator;
+    a.lastk = q->lastk;
     return a;
 }
 
-int ensure_cap(lx_qi *q, uint64_t n) {
+int ensure_cap(lx_qi *q, uint64_t n, hipStream_t s) {
     if (n <= q->cap) return 0;
     const uint64_t cap = std::max<uint64_t>(n, 1024);
+    QHIP(q, hipStreamSynchronize(s));   // ProcessEvent launches may still read the old buffers
     if (q->d_ev) (void)hipFree(q->d_ev);
     if (q->d_tg) (void)hipFree(q->d_tg);
     if (q->d_out) (void)hipFree(q->d_out);
@@ -184,7 +193,10 @@ int lx_qi_create(lx_index *index, lx_qi **out) {
 
 void lx_qi_destroy(lx_qi *q) {
     if (!q) return;
+    if (q->done) (void)hipEventSynchronize(q->done);   // ProcessEvent launches in flight
     qi_free(q);
+    if (q->staged) (void)hipEventDestroy(q->staged);
+    if (q->done) (void)hipEventDestroy(q->done);
     delete q;
 }
 
@@ -201,6 +213,7 @@ int lx_qi_reset(lx_qi *q) {
     if (iv.shard_count > 1) return q->fail(LX_ERR_STATE, "QuorumIndexer needs an unsharded index");
     if (iv.V > kQiMaxV) return q->fail(LX_ERR_ARG, "QuorumIndexer supports up to %u validators", kQiMaxV);
     QHIP(q, hipSetDevice(iv.device));
+    if (q->done) QHIP(q, hipEventSynchronize(q->done));   // ProcessEvent launches in flight read the old buffers
     qi_free(q);
     q->V = iv.V;
     q->quorum = iv.quorum;
@@ -210,6 +223,9 @@ int lx_qi_reset(lx_qi *q) {
     QHIP(q, hipMalloc((void **)&q->median, V * 4));
     QHIP(q, hipMalloc((void **)&q->weights, V * 4));
     QHIP(q, hipMalloc((void **)&q->cheat_of, V * 4));
+    QHIP(q, hipMalloc((void **)&q->lastk, (V + 1) * 8));
+    QHIP(q, hipMemsetAsync(q->lastk, 0, (V + 1) * 8, iv.stream));
+    q->gen = 0;
     QHIP(q, hipMemsetAsync(q->mt, 0, V * V * 4, iv.stream));
     QHIP(q, hipMemsetAsync(q->sp, 0, V * 4, iv.stream));
     QHIP(q, hipMemsetAsync(q->median, 0, V * 4, iv.stream));
@@ -227,33 +243,37 @@ int lx_qi_process_events(lx_qi *q, uint32_t n, const uint32_t *ev, const uint8_t
     QRC(view(q, &iv));
     QRC(check_events(q, iv, n, ev));
     QRC(refresh_cheaters(q, iv));
-    QRC(ensure_cap(q, (uint64_t)n + 1));
-    // creators of the batch's events
-    std::vector<uint32_t> cr(n);
-    QHIP(q, hipMemcpyAsync(q->d_ev, ev, n * 4ull, hipMemcpyHostToDevice, iv.stream));
-    QHIP(q, lx::launch_gather_u32(iv.ev_creator, q->d_ev, n, q->d_tg, iv.stream));
-    QRC(copy_out(q, iv, cr.data(), q->d_tg, n * 4ull));
-    // whole columns are overwritten: the last event per creator, the last self event
-    std::vector<uint32_t> last(q->V, LX_NONE), pe, pt;
-    uint32_t self_last = LX_NONE;
-    for (uint32_t i = 0; i < n; i++) {
-        last[cr[i]] = ev[i];
-        if (self_event && self_event[i]) self_last = ev[i];
+    // no host round trip: the device reduces the batch to the last event per
+    // creator and the last self event (k_qi_mark / k_qi_apply); nothing to wait for
+    QiBatch b{};
+    b.n = n;
+    if (++q->gen == 0) {   // stamps wrapped: start over
+        QHIP(q, hipMemsetAsync(q->lastk, 0, (q->V + 1ull) * 8, iv.stream));
+        q->gen = 1;
     }
-    for (uint32_t c = 0; c < q->V; c++)
-        if (last[c] != LX_NONE) {
-            pe.push_back(last[c]);
-            pt.push_back(c);
+    b.gen = q->gen;
+    if (n <= kQiInline) {
+        for (uint32_t i = 0; i < n; i++) {
+            b.iev[i] = ev[i];
+            if (self_event && self_event[i]) b.iself |= 1u << i;
         }
-    if (self_last != LX_NONE) {
-        pe.push_back(self_last);
-        pt.push_back(q->V);
+    } else {
+        QRC(ensure_cap(q, (uint64_t)2 * n, iv.stream));
+        if (!q->staged) QHIP(q, hipEventCreateWithFlags(&q->staged, hipEventDisableTiming));
+        else QHIP(q, hipEventSynchronize(q->staged));
+        q->stage.resize(2ull * n);
+        for (uint32_t i = 0; i < n; i++) {
+            q->stage[i] = ev[i];
+            q->stage[n + i] = self_event && self_event[i] ? 1u : 0u;
+        }
+        QHIP(q, hipMemcpyAsync(q->d_ev, q->stage.data(), 8ull * n, hipMemcpyHostToDevice, iv.stream));
+        QHIP(q, hipEventRecord(q->staged, iv.stream));
+        b.ev = q->d_ev;
+        b.self = q->d_ev + n;
     }
-    QRC(ensure_cap(q, pe.size()));
-    QHIP(q, hipMemcpyAsync(q->d_ev, pe.data(), pe.size() * 4, hipMemcpyHostToDevice, iv.stream));
-    QHIP(q, hipMemcpyAsync(q->d_tg, pt.data(), pt.size() * 4, hipMemcpyHostToDevice, iv.stream));
-    QHIP(q, lx::launch_qi_update(qi_args(q, iv), q->d_ev, q->d_tg, (uint32_t)pe.size(), iv.stream));
-    QHIP(q, hipStreamSynchronize(iv.stream));   // pe/pt are host temporaries
+    QHIP(q, lx::launch_qi_apply(qi_args(q, iv), b, iv.stream));
+    if (!q->done) QHIP(q, hipEventCreateWithFlags(&q->done, hipEventDisableTiming));
+    QHIP(q, hipEventRecord(q->done, iv.stream));
     q->dirty = true;
     return 0;
 }
@@ -293,7 +313,7 @@ int lx_qi_metric_of(lx_qi *q, uint32_t n, const uint32_t *ev, uint32_t cap, uint
     QRC(check_events(q, iv, n, ev));
     QRC(refresh_cheaters(q, iv));
     QRC(recache(q, iv));
-    QRC(ensure_cap(q, n));
+    QRC(ensure_cap(q, n, iv.stream));
     QHIP(q, hipMemcpyAsync(q->d_ev, ev, n * 4ull, hipMemcpyHostToDevice, iv.stream));
     QHIP(q, lx::launch_qi_metric(qi_args(q, iv), q->d_ev, n, cap, q->d_out, iv.stream));
     return copy_out(q, iv, out, q->d_out, n * 8ull);

@@ -1,7 +1,7 @@
 // lx_emitter.hip -- CDNA4 (gfx950) kernels of the emitter's QuorumIndexer
 // (emitter/ancestor/quorum_indexer.go:20-158) on the index's HighestBefore plane.
 //
-//   k_qi_update : ProcessEvent (:86-98) -- the merged-HighestBefore seqs of an
+//   k_qi_apply  : ProcessEvent (:86-98) -- the merged-HighestBefore seqs of an
 //                 event (GetMergedHighestBefore, vecengine/index.go:235-250,
 //                 mapped by seqOf :70-75) into the matrix column of its
 //                 creator, or into the self-parent seqs.  The matrix is kept
@@ -49,19 +49,45 @@ hipError_t launch_gather_u32(const uint32_t *src, const uint32_t *idx, uint32_t 
     return hipGetLastError();
 }
 
-// one workgroup per (event, target): target < V = matrix column, V = self-parent seqs
-__global__ __launch_bounds__(256) void k_qi_update(QiArgs a, const uint32_t *ev, const uint32_t *target, uint32_t n) {
-    const uint32_t i = blockIdx.x;
-    if (i >= n) return;
-    const uint32_t *row = a.hb + (uint64_t)ev[i] * a.stride;
-    const uint32_t t = target[i];
-    uint32_t *dst = t < a.V ? a.mt + (uint64_t)t * a.V : a.sp;
-    for (uint32_t v = threadIdx.x; v < a.V; v += blockDim.x) dst[v] = merged_seq(a, row, v);
+// ProcessEvent of a batch without a host round trip: only the last event of
+// each creator (and the last self event) writes, so every event stamps its
+// batch position into its creator's slot (gen << 32 | i, atomicMax: no reset
+// between batches), then the events that won write their whole column
+// (the matrix is transposed: one coalesced row) and / or the self row
+__device__ __forceinline__ uint32_t qb_ev(const QiBatch &b, uint32_t i) { return b.ev ? b.ev[i] : b.iev[i]; }
+__device__ __forceinline__ bool qb_self(const QiBatch &b, uint32_t i) {
+    return b.ev ? b.self[i] != 0u : ((b.iself >> i) & 1u) != 0u;
 }
 
-hipError_t launch_qi_update(const QiArgs &a, const uint32_t *ev, const uint32_t *target, uint32_t n, hipStream_t s) {
-    if (!n) return hipSuccess;
-    hipLaunchKernelGGL(k_qi_update, dim3(n), dim3(256), 0, s, a, ev, target, n);
+__global__ void k_qi_mark(QiArgs a, QiBatch b) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= b.n) return;
+    const unsigned long long key = (unsigned long long)b.gen << 32 | i;
+    atomicMax(a.lastk + a.ev_creator[qb_ev(b, i)], key);
+    if (qb_self(b, i)) atomicMax(a.lastk + a.V, key);
+}
+
+__global__ __launch_bounds__(256) void k_qi_apply(QiArgs a, QiBatch b) {
+    const uint32_t i = blockIdx.x;
+    const uint32_t e = qb_ev(b, i);
+    const unsigned long long key = (unsigned long long)b.gen << 32 | i;
+    const uint32_t c = a.ev_creator[e];
+    const bool col = a.lastk[c] == key;
+    const bool self = qb_self(b, i) && a.lastk[a.V] == key;
+    if (!col && !self) return;
+    const uint32_t *row = a.hb + (uint64_t)e * a.stride;
+    uint32_t *dc = a.mt + (uint64_t)c * a.V;
+    for (uint32_t v = threadIdx.x; v < a.V; v += blockDim.x) {
+        const uint32_t m = merged_seq(a, row, v);
+        if (col) dc[v] = m;
+        if (self) a.sp[v] = m;
+    }
+}
+
+hipError_t launch_qi_apply(const QiArgs &a, const QiBatch &b, hipStream_t s) {
+    if (!b.n) return hipSuccess;
+    hipLaunchKernelGGL(k_qi_mark, dim3((b.n + 255) / 256), dim3(256), 0, s, a, b);
+    hipLaunchKernelGGL(k_qi_apply, dim3(b.n), dim3(256), 0, s, a, b);
     return hipGetLastError();
 }
 

@@ -353,6 +353,18 @@ struct QiArgs {
     uint32_t *mt;                // matrix, transposed: mt[creator * V + validator]
     uint32_t *sp;                // self-parent seqs
     uint32_t *median;            // global median seqs
+    const uint32_t *ev_creator;
+    unsigned long long *lastk;   // [V + 1]: per creator (and [V]: self) the last batch position, gen << 32 | i
+};
+
+// a ProcessEvent batch: events inline (n <= kQiInline) or in device memory
+constexpr uint32_t kQiInline = 16;
+struct QiBatch {
+    uint32_t n, gen;
+    const uint32_t *ev;          // NULL: inline
+    const uint32_t *self;        // per event 0/1 (device, with ev)
+    uint32_t iev[kQiInline];
+    uint32_t iself;              // inline self flags, bit i
 };
 
 // ---- batched abft caller (lx_abft_kernels.hip, lx_abft.cpp)
@@ -523,7 +535,7 @@ hipError_t launch_load_marks_ok(const uint32_t *hb, uint64_t stride, uint32_t n,
                                 uint32_t *bad, hipStream_t s);
 hipError_t launch_load_verify_la(const LoadVerifyArgs &a, hipStream_t s);
 hipError_t launch_gather_u32(const uint32_t *src, const uint32_t *idx, uint32_t n, uint32_t *dst, hipStream_t s);
-hipError_t launch_qi_update(const QiArgs &a, const uint32_t *ev, const uint32_t *target, uint32_t n, hipStream_t s);
+hipError_t launch_qi_apply(const QiArgs &a, const QiBatch &b, hipStream_t s);
 hipError_t launch_qi_median(const QiArgs &a, hipStream_t s);
 hipError_t launch_qi_metric(const QiArgs &a, const uint32_t *ev, uint32_t n, uint32_t cap, unsigned long long *out,
                             hipStream_t s);

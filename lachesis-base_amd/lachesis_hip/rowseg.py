@@ -48,6 +48,8 @@ class RowSegments:
             recv.copy_(r)
         else:
             dist.all_to_all_single(recv, send, output_split_sizes=recv_n, input_split_sizes=send_n, group=self.group)
+            # the library reads `recv` on its own stream
+            torch.cuda.current_stream(self.device).synchronize()
 
     def _counts(self, send_n):
         s = torch.tensor(send_n, dtype=torch.int64, device="cpu" if self.stage else self.device)
