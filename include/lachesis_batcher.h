@@ -44,6 +44,11 @@ const char *lx_batcher_last_error(const lx_batcher *b);
  * as after lx_reset). */
 int lx_batcher_reset(lx_batcher *b);
 
+/* Capacity hint: room for the ids of n events in this epoch (as
+ * lx_config.event_capacity for the index); the id table otherwise grows, and
+ * rehashes, as the epoch fills.  No effect on results. */
+int lx_batcher_reserve(lx_batcher *b, uint64_t n_events);
+
 /* Push n events: id, creator idx, seq, parents by id (parent_off has n+1
  * entries into parent_id; self-parent first).  out_status (optional, n
  * entries) receives LX_PUSH_*. */

@@ -95,7 +95,7 @@ struct IdMap {
     void grow() {
         std::vector<Ent> old;
         old.swap(t);
-        init(std::max<uint64_t>(2 * (mask + 1), 2 * live));
+        init(std::max<uint64_t>(2 * (mask + 1), 2 * live));   // init doubles again: 4x the slots
         for (const Ent &e : old)
             if (e.st == 1) put(e.key, e.val);
     }
@@ -274,6 +274,20 @@ int lx_batcher_reset(lx_batcher *b) {
     if (!b) return LX_ERR_ARG;
     lx_batcher fresh;
     std::swap(*b, fresh);
+    return 0;
+}
+
+int lx_batcher_reserve(lx_batcher *b, uint64_t n_events) {
+    if (!b) return LX_ERR_ARG;
+    if (2 * (n_events + b->ids.live) > b->ids.mask + 1) {
+        // rebuild at the larger size (ids are kept)
+        std::vector<IdMap::Ent> old;
+        old.swap(b->ids.t);
+        b->ids.init(n_events + b->ids.live);
+        for (const IdMap::Ent &e : old)
+            if (e.st == 1) b->ids.put(e.key, e.val);
+    }
+    b->released.reserve(n_events);
     return 0;
 }
 

@@ -1191,12 +1191,16 @@ int flush_before(lx_index *h, hipStream_t s) {
 int add_batch_small(lx_index *h, uint32_t n, const uint32_t *creator, const uint32_t *seq, const uint64_t *poff,
                     const uint32_t *par, uint32_t *out_branch, uint32_t *err_index) {
     int rc;
-    if ((rc = hm_sync(h))) return rc;
+    if (!h->hm_ok) {
+        HIPCHK(h, set_dev(h->device));
+        if ((rc = hm_sync(h))) return rc;
+    }
     const uint64_t bs = h->n_events;
     for (uint32_t i = 0; i < n; i++) {
         const uint64_t g = bs + i;
         const uint32_t c = creator[i], s = seq[i];
         const uint64_t p0 = poff[i], p1 = poff[i + 1];
+        if (p1 < p0) return h->fail(LX_ERR_ARG, "parent offsets not monotone");
         int code = 0;
         if (c >= h->V) {
             code = LX_ERR_ARG;
@@ -1224,7 +1228,9 @@ int add_batch_small(lx_index *h, uint32_t n, const uint32_t *creator, const uint
         }
     }
     // the run launches before it would outgrow one k_small (LDS: kSmallMaxN events)
-    if (h->pend_n && h->pend_n + n > kSmallMaxN && (rc = flush_pending(h))) return rc;
+    if (h->pend_n && h->pend_n + n > kSmallMaxN && ((rc = h->hip(set_dev(h->device), "set device")) ||
+                                                    (rc = flush_pending(h))))
+        return rc;
     if (!h->pend_n) {
         h->pend_bs = bs;
         h->pend_B0 = h->B;
@@ -1237,6 +1243,11 @@ int add_batch_small(lx_index *h, uint32_t n, const uint32_t *creator, const uint
     const uint32_t B0 = h->B, pn0 = h->pend_n;
     const size_t par0 = h->pend_par.size();
     uint32_t B = B0, bmax = 0;
+    if (h->hm_creator.capacity() < bs + n) {
+        // the mirror grows with the epoch: reserve for the device capacity at once
+        const uint64_t c = std::max<uint64_t>(2 * (bs + n), h->n_cap);
+        for (auto *v : {&h->hm_creator, &h->hm_seq, &h->hm_branch, &h->hm_bbefore}) v->reserve(c);
+    }
     h->hm_creator.resize(bs + n);
     h->hm_seq.resize(bs + n);
     h->hm_branch.resize(bs + n);
@@ -1290,6 +1301,9 @@ int add_batch_small(lx_index *h, uint32_t n, const uint32_t *creator, const uint
     // capacity (rare re-layouts sync the stream; the pending run is not on the
     // device yet); on failure the host mirror and the run are rolled back
     h->max_seq = std::max(h->max_seq, bmax);
+    const bool grows = bs + n > h->n_cap || B > h->stride || h->max_seq > h->s_cap;
+    if (grows || B != B0 || h->ncols == 0 || h->pend_n + n >= kPendLaunch)
+        if ((rc = h->hip(set_dev(h->device), "set device"))) return rc;
     if ((rc = grow_events(h, bs + n)) || (rc = grow_branches(h, B)) || (rc = grow_scap(h, h->max_seq))) {
         h->h_branch_first.resize(B0);
         h->h_branch_creator.resize(B0);
@@ -1540,18 +1554,19 @@ int lx_add_batch(lx_index *h, uint32_t n, const uint32_t *creator, const uint32_
     if (!h) return LX_ERR_ARG;
     if (n == 0) return 0;
     if (!creator || !seq || !poff) return h->fail(LX_ERR_ARG, "null input");
-    HIPCHK(h, set_dev(h->device));
     uint64_t base = poff[0], npar = poff[n] - poff[0];
     if (poff[n] < poff[0] || npar >= 0xFFFFFFFFull) return h->fail(LX_ERR_ARG, "bad parent offsets");
+    if (h->loading) return h->fail(LX_ERR_STATE, "lx_add_batch during a load (lx_load_finish first)");
+    // the small path makes no HIP call unless it launches or grows (it sets the device then)
+    if (h->have_epoch && !h->sharded() && !h->rowseg() && n <= std::min(h->small_max, kSmallMaxN))
+        return add_batch_small(h, n, creator, seq, poff, par, out_branch, err_index);
+    HIPCHK(h, set_dev(h->device));
     std::vector<uint32_t> off(n + 1);
     for (uint32_t i = 0; i <= n; i++) {
         if (i && poff[i] < poff[i - 1]) return h->fail(LX_ERR_ARG, "parent offsets not monotone");
         off[i] = (uint32_t)(poff[i] - base);
     }
     int rc;
-    if (h->loading) return h->fail(LX_ERR_STATE, "lx_add_batch during a load (lx_load_finish first)");
-    if (h->have_epoch && !h->sharded() && !h->rowseg() && n <= std::min(h->small_max, kSmallMaxN))
-        return add_batch_small(h, n, creator, seq, poff, par, out_branch, err_index);
     if ((rc = flush_pending(h))) return rc;
     if ((rc = ensure_batch(h, n, npar))) return rc;
     HIPCHK(h, hipMemcpyAsync(h->b_creator, creator, n * 4ull, hipMemcpyHostToDevice, h->stream));

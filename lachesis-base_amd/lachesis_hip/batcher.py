@@ -21,13 +21,16 @@ PUSH_QUEUED, PUSH_DUPLICATE, PUSH_CONNECTED = 0, 1, 2
 
 
 class LevelBatcher:
-    def __init__(self):
+    def __init__(self, capacity=0):
+        """``capacity``: expected events per epoch (lx_batcher_reserve; a hint)."""
         self.L = load_library()
         h = vp()
         rc = self.L.lx_batcher_create(ctypes.byref(h))
         if rc != 0:
             raise LxError(rc, "lx_batcher_create failed")
         self.h = h
+        if capacity:
+            self._chk(self.L.lx_batcher_reserve(h, capacity))
         self._handle = {}      # event id -> uint64 handle
         self._event = {}       # uint64 handle -> event
 

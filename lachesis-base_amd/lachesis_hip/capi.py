@@ -109,6 +109,7 @@ SIGNATURES = [
     ("lx_batcher_destroy", None, [vp]),
     ("lx_batcher_last_error", ctypes.c_char_p, [vp]),
     ("lx_batcher_reset", ctypes.c_int, [vp]),
+    ("lx_batcher_reserve", ctypes.c_int, [vp, ctypes.c_uint64]),
     ("lx_batcher_push", ctypes.c_int, [vp, ctypes.c_uint32, u64p, u32p, u32p, u64p, u64p, u8p]),
     ("lx_batcher_peek", ctypes.c_int, [vp, u32p, u64p, u32p, u32p]),
     ("lx_batcher_pop", ctypes.c_int, [vp, u64p, u32p, u32p, u64p, u32p, u32p, u64p]),

@@ -291,7 +291,7 @@ int lx_bench_latency(int device, uint32_t V, const uint32_t *weights, uint64_t N
     // batcher-fed: each level pushed by id, popped (parents-first release) and added
     {
         lx_batcher *b = nullptr;
-        if (lx_batcher_create(&b)) return fail("batcher", h);
+        if (lx_batcher_create(&b) || lx_batcher_reserve(b, N)) return fail("batcher", h);
         // the batcher's dense indices must continue the epoch: replay the indexed
         // prefix as released events (pushed and popped without adding)
         std::vector<uint64_t> ids, pids, po;
@@ -432,7 +432,7 @@ int lx_bench_feed_levels(int device, uint32_t V, const uint32_t *weights, uint64
     std::vector<uint64_t> ids, pids, po, oid, opo;
     std::vector<uint32_t> ocr, osq, opar, olv;
     if (mode == 1) {
-        if (lx_batcher_create(&b)) return fail("batcher");
+        if (lx_batcher_create(&b) || lx_batcher_reserve(b, N)) return fail("batcher");
         // the batcher's dense indices continue the epoch: the history as released events
         ids.resize(H);
         po.assign(1, 0);

@@ -18,10 +18,10 @@ def lx():
     return lachesis_hip
 
 
-def drain(lx, events, validators, seed, chunk_max=40):
+def drain(lx, events, validators, seed, chunk_max=40, capacity=0):
     rng = np.random.default_rng(seed)
     order = list(rng.permutation(len(events)))
-    b = lx.batcher.LevelBatcher()
+    b = lx.batcher.LevelBatcher(capacity)
     released, batches = [], []
     i = 0
     while i < len(order):
@@ -98,3 +98,15 @@ def test_duplicates_unpop_and_reset(lx):
     assert b.peek() == (0, 0, 0, 0)
     b.push(events, validators)
     assert b.peek()[0] == len(events)
+
+
+def test_reserve_changes_nothing(lx):
+    """lx_batcher_reserve is a capacity hint: the same pops with and without it
+    (and the id table rebuilt mid-epoch keeps the released ids)."""
+    nodes, events = tdag.rand_fork_dag(16, 30, 4, 3, 4, seed=7)
+    validators = pos.Validators.equal(nodes, 1)
+    _, rel0, bat0 = drain(lx, events, validators, seed=5)
+    _, rel1, bat1 = drain(lx, events, validators, seed=5, capacity=100_000)
+    assert [e.id for e in rel0] == [e.id for e in rel1]
+    for x, y in zip(bat0, bat1):
+        assert [e.id for e in x[0]] == [e.id for e in y[0]] and list(x[2]) == list(y[2]) and list(x[3]) == list(y[3])
