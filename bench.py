@@ -521,8 +521,6 @@ def main():
     ap.add_argument("--segments", type=int, default=0,
                     help="single GPU: walk the epoch as G Add-order segments + fix-up (option segments, the "
                          "per-rank work of the row-segment multi-GPU mode timed segment by segment)")
-    ap.add_argument("--seg-concurrent", action="store_true",
-                    help="with --segments: two segment walks side by side (half-LDS walkers, two per CU)")
     ap.add_argument("--shard-solo", type=int, default=0,
                     help="diagnostic: time rank 0 of a G-way column shard alone on this GPU (its index walk, "
                          "the packing of its outgoing LowestAfter blocks, its partial FC); no collectives")
@@ -601,9 +599,7 @@ def main():
         sx = ShardedIndex(ix, device=dev)
         d_part = torch.empty(args.fc_queries, dtype=torch.int32, device=dev)
     else:
-        ix = lx.Index(device=local, event_capacity=N,
-                      options={"segments": args.segments, "seg_concurrent": int(args.seg_concurrent)}
-                      if args.segments > 1 else None)
+        ix = lx.Index(device=local, event_capacity=N, options={"segments": args.segments} if args.segments > 1 else None)
 
     st_x = []   # shard mode: LowestAfter all-to-all (pack + collective + unpack) per step, ms
 

@@ -472,25 +472,11 @@ int seg_walk(lx_index *h, IndexArgs ia, const uint32_t *poff, hipStream_t s) {
         HIPCHK(h, hipEventCreate(&e));
         h->seg_ev.push_back(e);
     }
-    for (auto &e : h->seg_join)
-        if (!e) HIPCHK(h, hipEventCreateWithFlags(&e, hipEventDisableTiming));
     hipEvent_t *ev = h->seg_ev.data();
     HIPCHK(h, lx::launch_seg_tables(a, s));
     ia.seg = 1;
     ia.ev_branch = h->ev_branch;
     ia.ev_seq = h->ev_seq;
-    // side by side: two streams, two half-LDS walkers per CU (option seg_concurrent)
-    const uint32_t NS = h->seg_conc ? 2u : 1u;
-    hipStream_t ws[2] = {s, s};
-    if (NS > 1) {
-        for (uint32_t q = 0; q < NS; q++) {
-            if (!h->seg_side[q]) HIPCHK(h, hipStreamCreateWithFlags(&h->seg_side[q], hipStreamNonBlocking));
-            ws[q] = h->seg_side[q];
-        }
-        HIPCHK(h, hipEventRecord(ev[2 * G + 2], s));
-        for (uint32_t q = 0; q < NS; q++) HIPCHK(h, hipStreamWaitEvent(ws[q], ev[2 * G + 2], 0));
-        ia.co = 1;
-    }
     for (uint32_t k = 0; k < G; k++) {
         IndexArgs sk = ia;
         sk.batch_start = a.seg_lo[k];
@@ -501,16 +487,10 @@ int seg_walk(lx_index *h, IndexArgs ia, const uint32_t *poff, hipStream_t s) {
         sk.seg_flag = a.pflag + (a.seg_lo[k] - bs);
         sk.seg_list = a.plist + (a.seg_lo[k] - bs);
         sk.seg_count = a.pcount + k;
-        hipStream_t q = ws[k % NS];
-        HIPCHK(h, hipEventRecord(ev[2 * k], q));
-        HIPCHK(h, lx::launch_index(sk, q));
-        HIPCHK(h, hipEventRecord(ev[2 * k + 1], q));
+        HIPCHK(h, hipEventRecord(ev[2 * k], s));
+        HIPCHK(h, lx::launch_index(sk, s));
+        HIPCHK(h, hipEventRecord(ev[2 * k + 1], s));
     }
-    if (NS > 1)
-        for (uint32_t q = 0; q < NS; q++) {
-            HIPCHK(h, hipEventRecord(h->seg_join[q], ws[q]));
-            HIPCHK(h, hipStreamWaitEvent(s, h->seg_join[q], 0));
-        }
     uint32_t pc[kMaxSegments], ec[kMaxSegments];
     HIPCHK(h, hipMemcpyAsync(pc, a.pcount, G * 4, hipMemcpyDeviceToHost, s));
     HIPCHK(h, hipStreamSynchronize(s));
@@ -1403,10 +1383,6 @@ void lx_destroy(lx_index *h) {
     for (auto &e : h->st_done)
         if (e) (void)hipEventDestroy(e);
     for (auto &e : h->seg_ev) (void)hipEventDestroy(e);
-    for (auto &e : h->seg_join)
-        if (e) (void)hipEventDestroy(e);
-    for (auto &q : h->seg_side)
-        if (q) (void)hipStreamDestroy(q);
     for (auto *p : h->st_pin)
         if (p) (void)hipHostFree(p);
     if (h->st_dev) (void)hipFree(h->st_dev);
@@ -1444,8 +1420,6 @@ int lx_set_option(lx_index *h, const char *name, int64_t value) {
         if (h->sharded()) return h->fail(LX_ERR_STATE, "row segments on a column shard");
         if (value < 0 || value > (int64_t)kMaxSegments) return h->fail(LX_ERR_ARG, "%s must be 0..%u", name, kMaxSegments);
         (k == "seg_count" ? h->rs_count : h->rs_rank) = (uint32_t)value;
-    } else if (k == "seg_concurrent") {
-        h->seg_conc = value != 0;
     } else if (k == "segments") {
         if (value < 0 || value > (int64_t)kMaxSegments) return h->fail(LX_ERR_ARG, "segments must be 0..%u", kMaxSegments);
         if (value > 1 && h->sharded()) return h->fail(LX_ERR_STATE, "segments on a column shard");

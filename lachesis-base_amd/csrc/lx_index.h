@@ -209,9 +209,6 @@ struct lx_index {
     uint32_t *seg_jt = nullptr, *seg_cnt = nullptr, *seg_mf = nullptr, *seg_plist = nullptr, *seg_elist = nullptr;
     uint64_t seg_jt_cap = 0, seg_cnt_cap = 0, seg_mf_cap = 0, seg_plist_cap = 0, seg_elist_cap = 0;   // seg_mf: flags
     std::vector<hipEvent_t> seg_ev;
-    bool seg_conc = false;                 // option seg_concurrent: two segment walks side by side
-    hipStream_t seg_side[2] = {nullptr, nullptr};
-    hipEvent_t seg_join[2] = {nullptr, nullptr};
     lx_seg_stats seg_stats{};
     // row-segment rank (options seg_rank / seg_count, lx_rowseg.cpp): one batch
     // per epoch, this rank walks and owns the rows of segment rs_rank

@@ -70,7 +70,6 @@ struct IndexArgs {
     uint32_t *seg_flag;          // per segment event: set when its row misses some J_k (a "partial" event)
     uint32_t *seg_list;          // partial events (global index), appended
     uint32_t *seg_count;
-    uint32_t co;                 // half-LDS walker (two per CU; 4-column packed slices only)
 };
 constexpr int kProfSlots = 16;   // see k_index: passes, spin misses, chunk folds, completes, ...
 constexpr int kProfWaves = 16;   // waves per workgroup in the counter layout

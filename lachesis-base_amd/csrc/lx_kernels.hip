@@ -269,11 +269,10 @@ hipError_t launch_batch_finish(const BatchArgs &a, uint32_t jump_rounds, hipStre
 constexpr int kND = 4;               // drain waves
 constexpr int kRR = 1024;            // record ring (events)
 
-template <int CPW, bool CO = false>
+template <int CPW>
 struct Ring {
-    // slots: 64 KB of units (CPW 2 uses one 16-B unit per slot: 2048 slots in
-    // 32 KB); CO (two co-resident walkers per CU, segment walks): half
-    static constexpr int BYTES = (CPW == 2 ? 32768 : 65536) / (CO ? 2 : 1);
+    // slots: 64 KB of units (CPW 2 uses one 16-B unit per slot: 2048 slots in 32 KB)
+    static constexpr int BYTES = CPW == 2 ? 32768 : 65536;
     static constexpr int N = BYTES / (CPW == 1 ? 8 : CPW == 2 ? 16 : 32);
 };
 
@@ -490,20 +489,18 @@ __device__ __forceinline__ void blk_fold(const uint32_t pa[3], uint32_t W, uint3
 // The walker kernel.  MASKED: older rows may carry fork marks in bit 31
 // (B > V); PK: 4-column slices with 16-bit packed slot units (every seq of the
 // epoch <= 0xFFFF).
-// CO: half the LDS rings (74 KB instead of 141 KB for 4-column slices), so two
-// walkers share a CU -- two segments of a segmented walk run side by side.
-template <int CPW, int NCW, bool MASKED, bool PK, bool CO = false>
+template <int CPW, int NCW, bool MASKED, bool PK>
 __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
     static_assert(!PK || CPW == 4, "packed slots: 4-column slices");
     static_assert(CPW == 1 || CPW == 2 || CPW == 4, "slot layout");
     static_assert(LX_MAXP == 12, "block walker: 12 inline parents, three per lane of a quad");
     constexpr int ND = kND;
-    constexpr int RR = CO ? kRR / 2 : kRR;
+    constexpr int RR = kRR;
     constexpr int NT = 64 * (NCW + 1 + ND);
     constexpr int RQ = LX_REC_Q;
     constexpr int KB = 1024 / CPW;               // recent (seq -> event) entries per owned branch
-    constexpr int RN = Ring<CPW, CO>::N;
-    constexpr int RB16 = Ring<CPW, CO>::BYTES / 16;
+    constexpr int RN = Ring<CPW>::N;
+    constexpr int RB16 = Ring<CPW>::BYTES / 16;
     static_assert(RR % 64 == 0 && RR / 64 >= 4 && RR >= 2 * 16 * NCW, "record ring");
     // slot units (A array, then B array for CPW 4), each followed by a null
     // slot (tag kNullTag, values 0) that absent parents point at
@@ -811,7 +808,7 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
         // (1- and 2-column slices: one slot unit of 8 / 16 B per event, lane 0
         // of the quad publishes it; 4 columns: units A and B from lanes 0, 1)
         constexpr uint32_t kLeanStuck = 64;
-        constexpr uint32_t kLeanFar = RN / 2 < 512 ? RN / 2 : 512;
+        constexpr uint32_t kLeanFar = 512;
         constexpr uint32_t UA = CPW == 1 ? 8u : 16u;   // bytes of unit A
         const uint32_t ANULL = RA + (uint32_t)RN * UA;
         const uint32_t j = lane & 3, quad = lane >> 2;
@@ -1088,11 +1085,6 @@ static hipError_t launch_index_t(const IndexArgs &a0, hipStream_t s) {
     const uint32_t grid = a.slices_per_xcd * 8;
     const dim3 blk(64 * (NCW + 1 + kND));
     if constexpr (CPW == 4) {
-        if (a.pack16 && a.co) {   // a segment walk sharing the CUs with another
-            if (a.mask) hipLaunchKernelGGL((k_index<CPW, NCW, true, true, true>), dim3(grid), blk, 0, s, a);
-            else hipLaunchKernelGGL((k_index<CPW, NCW, false, true, true>), dim3(grid), blk, 0, s, a);
-            return hipGetLastError();
-        }
         if (a.pack16) {   // every seq of the epoch fits 16 bits: one 16-B slot unit
             if (a.mask) hipLaunchKernelGGL((k_index<CPW, NCW, true, true>), dim3(grid), blk, 0, s, a);
             else hipLaunchKernelGGL((k_index<CPW, NCW, false, true>), dim3(grid), blk, 0, s, a);

@@ -53,10 +53,9 @@ SHAPES = [
 ]
 
 
-@pytest.mark.parametrize("conc", [0, 1])
 @pytest.mark.parametrize("G", [2, 3, 8, 32])
 @pytest.mark.parametrize("shape", SHAPES)
-def test_segmented_batch_vs_oracle(lx, monkeypatch, shape, G, conc):
+def test_segmented_batch_vs_oracle(lx, monkeypatch, shape, G):
     V, epv, P, ch, fk, seed = shape
     d = lx.tools.gen_dag(V, epv, P, ch, fk, seed)
     if len(d) < 64 * G:
@@ -64,7 +63,7 @@ def test_segmented_batch_vs_oracle(lx, monkeypatch, shape, G, conc):
     w = [1 + (i * 7) % 5 for i in range(V)]
     o = corc.OracleIndex(w)
     assert o.add_batch(d.creator, d.seq, d.poff, d.par) == -1
-    ix = make_index(lx, monkeypatch, G, seg_concurrent=conc, cpw=4 if conc else 0)
+    ix = make_index(lx, monkeypatch, G)
     ix.reset(w)
     br = ix.add_batch(d.creator, d.seq, d.poff, d.par, want_branches=True)
     st = ix.segment_stats()
@@ -112,8 +111,8 @@ def _plane(ptr, rows, stride, cols):
     return out[:, :cols]
 
 
-@pytest.mark.parametrize("G,conc", [(4, 0), (8, 0), (2, 1), (8, 1)])
-def test_segmented_config3_shape_planes(lx, monkeypatch, G, conc):
+@pytest.mark.parametrize("G", [4, 8])
+def test_segmented_config3_shape_planes(lx, monkeypatch, G):
     """V = 1000 with Zipf stakes (BASELINE configs[2]'s shape), 150k events:
     both planes byte-identical to the ordinary walk's, which the parity tests
     pin to the oracle; a prefix of rows against the oracle directly."""
@@ -123,7 +122,7 @@ def test_segmented_config3_shape_planes(lx, monkeypatch, G, conc):
     N = len(d)
     planes = []
     for g in (0, G):
-        ix = make_index(lx, monkeypatch, g, cap=N, seg_concurrent=conc if g else 0)
+        ix = make_index(lx, monkeypatch, g, cap=N)
         ix.reset(w)
         ix.add_batch(d.creator, d.seq, d.poff, d.par)
         ix.sync()
