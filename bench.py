@@ -51,7 +51,7 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
 
 def measured_traffic(config, fc_queries):
     """HBM bytes per launch from the newest committed PMC profile of this
-    workload (profiles/r*/traffic_<config>.json; round 2: scripts/prof_r02.sh,
+    workload (profiles/r*/traffic_<config>.json; round 2: scripts/prof_round.sh,
     reads from the L2's memory-side read requests by size, writes from
     WRITE_SIZE, separate passes), or None."""
     import glob

@@ -1065,7 +1065,6 @@ int flush_pending(lx_index *h) {
     const uint32_t n = h->pend_n;
     const uint64_t bs = h->pend_bs;
     const uint32_t B0 = h->pend_B0, B = h->B;
-    const uint64_t npar = h->pend_par.size();
     const uint32_t L = h->pend_maxlvl + 1, nf = B - B0;
     // branches the run touched (each once)
     h->sm_touched.clear();
@@ -1076,23 +1075,56 @@ int flush_pending(lx_index *h) {
         if (h->touch_mark[br] != tm) { h->touch_mark[br] = tm; h->sm_touched.push_back(br); }
     }
     const uint32_t n_blen = (uint32_t)h->sm_touched.size();
-    const uint64_t w_ev = 12ull * n;
-    const uint64_t words = w_ev + npar + n + (L + 1) + 2ull * nf + 2ull * n_blen;
+    // in-run parents (batch positions) and "old" entries: parents older than the
+    // run, and the older previous branch event of a branch's first event in it
+    h->sm_pl.clear();
+    h->sm_old.clear();
+    h->sm_meta.resize(n);
+    uint32_t nh = 0;
+    const uint32_t *pp = h->pend_par.data();
+    for (uint32_t i = 0; i < n; i++) {
+        // in-run parents in chunks of 4, padded with the event itself (k_small)
+        const SmallEv &e = h->pend_ev[i];
+        const uint32_t off = (uint32_t)h->sm_pl.size();
+        for (uint32_t x = e.q1.x, xe = e.q1.x + e.q0.w; x < xe; x++) {
+            const uint32_t g = pp[x];
+            if (g >= bs) h->sm_pl.push_back((uint16_t)(g - bs));
+            else h->sm_old.push_back(make_uint2(i, g));
+        }
+        while (h->sm_pl.size() & 3) h->sm_pl.push_back((uint16_t)i);
+        h->sm_meta[i] = make_uint2(i | ((uint32_t)h->sm_pl.size() - off) / 4 << 16, off / 4);
+        if (e.q0.z != LX_NONE && e.q0.z < bs) h->sm_old.push_back(make_uint2(0x80000000u | nh++, e.q0.z));
+    }
+    const uint32_t n_pl = (uint32_t)h->sm_pl.size(), n_old = (uint32_t)h->sm_old.size();
+    if (small_lds_bytes(n, nh, L, n_pl) > kSmallLds)   // add_batch_small keeps runs within it
+        return h->fail(LX_ERR_STATE, "pending run exceeds the k_small LDS budget");
+    // regions 16-B aligned: the kernel copies meta and the in-run list to LDS as uint4
+    const uint64_t w_ev = 12ull * n, w_meta = (2ull * n + 3) & ~3ull, w_pl = ((n_pl + 7ull) & ~7ull) / 2;
+    const uint64_t words = w_ev + w_meta + w_pl + 2ull * n_old + (L + 1) + 2ull * nf + 2ull * n_blen;
     uint32_t *img;
     int slot = -1, rc;
     const bool inl = words <= kSmallInline;   // small enough for the kernel arguments
     if (inl) img = h->sm_inl.img;
     else if ((rc = stage_slot(h, words, &img, &slot))) return rc;
     memcpy(img, h->pend_ev.data(), w_ev * 4);
-    uint32_t *ipar = img + w_ev;
-    if (npar) memcpy(ipar, h->pend_par.data(), npar * 4);
-    // events by level (counting sort; Add order inside a level)
-    uint32_t *perm = ipar + npar, *loff = perm + n;
+    {   // h0 slots of the events whose prev is older than the run (same order as above)
+        SmallEv *iev = reinterpret_cast<SmallEv *>(img);
+        uint32_t k = 0;
+        for (uint32_t i = 0; i < n; i++)
+            iev[i].q2.w = (iev[i].q0.z != LX_NONE && iev[i].q0.z < bs) ? k++ : LX_NONE;
+    }
+    // meta in level order (counting sort; Add order inside a level), level offsets
+    uint2 *meta = reinterpret_cast<uint2 *>(img + w_ev);
+    uint32_t *ipl = img + w_ev + w_meta;
+    uint2 *iold = reinterpret_cast<uint2 *>(ipl + w_pl);
+    uint32_t *loff = reinterpret_cast<uint32_t *>(iold + n_old);
     h->sm_cnt.assign(L + 1, 0);
     for (uint32_t i = 0; i < n; i++) h->sm_cnt[h->pend_lvl[i] + 1]++;
     for (uint32_t l = 0; l < L; l++) h->sm_cnt[l + 1] += h->sm_cnt[l];
     for (uint32_t l = 0; l <= L; l++) loff[l] = h->sm_cnt[l];
-    for (uint32_t i = 0; i < n; i++) perm[h->sm_cnt[h->pend_lvl[i]]++] = i;
+    for (uint32_t i = 0; i < n; i++) meta[h->sm_cnt[h->pend_lvl[i]]++] = h->sm_meta[i];
+    if (n_pl) memcpy(ipl, h->sm_pl.data(), n_pl * 2ull);
+    if (n_old) memcpy(iold, h->sm_old.data(), n_old * 8ull);
     uint32_t *nfirst = loff + L + 1, *ncreator = nfirst + nf, *blen = ncreator + nf;
     for (uint32_t x = 0; x < nf; x++) {
         nfirst[x] = h->h_branch_first[B0 + x];
@@ -1118,9 +1150,13 @@ int flush_pending(lx_index *h) {
     a.B0 = B0;
     a.B = B;
     a.img = inl ? nullptr : h->st_dev;
-    a.o_par = (uint32_t)w_ev;
-    a.o_perm = (uint32_t)(perm - img);
+    a.o_meta = (uint32_t)w_ev;
+    a.o_pl = (uint32_t)(w_ev + w_meta);
+    a.o_old = (uint32_t)(w_ev + w_meta + w_pl);
     a.o_loff = (uint32_t)(loff - img);
+    a.n_pl = n_pl;
+    a.n_old = n_old;
+    a.n_h0 = nh;
     a.n_levels = L;
     a.o_nfirst = (uint32_t)(nfirst - img);
     a.o_ncreator = (uint32_t)(ncreator - img);
@@ -1176,6 +1212,13 @@ int flush_before(lx_index *h, hipStream_t s) {
     return 0;
 }
 
+// A run of n events with npar parents fits one k_small workgroup's LDS (the h0
+// slots are at most one per branch existing before the run, and levels <= n).
+inline bool small_fits(const lx_index *h, uint64_t n, uint64_t npar) {
+    return n <= kSmallMaxN && npar <= 0xFFFF &&
+           small_lds_bytes(n, std::min<uint64_t>(n, h->B), n, npar + 3 * n) <= kSmallLds;
+}
+
 // Add for a batch of at most small_max events, host pointers, unsharded handle.
 // Validation and branch assignment run on the host in Add order -- the
 // reference's own sequential fillGlobalBranchID (vecengine/index.go:105-141:
@@ -1227,9 +1270,9 @@ int add_batch_small(lx_index *h, uint32_t n, const uint32_t *creator, const uint
             return h->fail(code, "event %u: violates seq/self-parent invariants (eventcheck)", i);
         }
     }
-    // the run launches before it would outgrow one k_small (LDS: kSmallMaxN events)
-    if (h->pend_n && h->pend_n + n > kSmallMaxN && ((rc = h->hip(set_dev(h->device), "set device")) ||
-                                                    (rc = flush_pending(h))))
+    // the run launches before it would outgrow one k_small (LDS, small_fits)
+    if (h->pend_n && !small_fits(h, h->pend_n + n, h->pend_par.size() + (poff[n] - poff[0])) &&
+        ((rc = h->hip(set_dev(h->device), "set device")) || (rc = flush_pending(h))))
         return rc;
     if (!h->pend_n) {
         h->pend_bs = bs;
@@ -1558,7 +1601,8 @@ int lx_add_batch(lx_index *h, uint32_t n, const uint32_t *creator, const uint32_
     if (poff[n] < poff[0] || npar >= 0xFFFFFFFFull) return h->fail(LX_ERR_ARG, "bad parent offsets");
     if (h->loading) return h->fail(LX_ERR_STATE, "lx_add_batch during a load (lx_load_finish first)");
     // the small path makes no HIP call unless it launches or grows (it sets the device then)
-    if (h->have_epoch && !h->sharded() && !h->rowseg() && n <= std::min(h->small_max, kSmallMaxN))
+    if (h->have_epoch && !h->sharded() && !h->rowseg() && n <= std::min(h->small_max, kSmallMaxN) &&
+        small_fits(h, n, npar))
         return add_batch_small(h, n, creator, seq, poff, par, out_branch, err_index);
     HIPCHK(h, set_dev(h->device));
     std::vector<uint32_t> off(n + 1);

@@ -32,6 +32,7 @@
 // indices are reused afterwards (hashes are not).
 #include "lx_index.h"
 
+#include <algorithm>
 #include <cstring>
 
 using namespace lxi;
@@ -53,9 +54,8 @@ struct FcCache {
     std::vector<uint8_t> ref;                       // clock reference bits
     std::vector<uint32_t> free_slots;
     uint32_t hand = 0;
-    // event -> slot: open addressing, linear probing, backward-shift deletion
-    std::vector<uint32_t> hk, hv;
-    uint32_t hmask = 0;
+    // event -> slot, indexed by the dense event index (LX_NONE: not in the set)
+    std::vector<uint32_t> slot_of;
     uint32_t last_a = LX_NONE, last_sa = LX_NONE;
     // tile fills: partial sums and the cheaters' branch columns (k_root_fc)
     uint32_t *d_psum = nullptr;
@@ -64,36 +64,13 @@ struct FcCache {
     uint32_t n_k = 0, k_B = 0, k_cap = 0;
     lx_fc_stats st{};
 
-    uint32_t hash(uint32_t e) const { return (uint32_t)((e * 0x9E3779B97F4A7C15ull) >> 40) & hmask; }
-    uint32_t find(uint32_t e) const {
-        for (uint32_t i = hash(e);; i = (i + 1) & hmask) {
-            const uint32_t k = hk[i];
-            if (k == e) return hv[i];
-            if (k == LX_NONE) return LX_NONE;
-        }
-    }
+    uint32_t find(uint32_t e) const { return e < slot_of.size() ? slot_of[e] : LX_NONE; }
     void map_put(uint32_t e, uint32_t s) {
-        uint32_t i = hash(e);
-        while (hk[i] != LX_NONE) i = (i + 1) & hmask;
-        hk[i] = e;
-        hv[i] = s;
+        if (e >= slot_of.size()) slot_of.resize(std::max<size_t>(2 * slot_of.size(), (size_t)e + 1024), LX_NONE);
+        slot_of[e] = s;
     }
     void map_erase(uint32_t e) {
-        uint32_t i = hash(e);
-        while (hk[i] != e) {
-            if (hk[i] == LX_NONE) return;
-            i = (i + 1) & hmask;
-        }
-        hk[i] = LX_NONE;
-        for (uint32_t j = (i + 1) & hmask; hk[j] != LX_NONE; j = (j + 1) & hmask) {
-            const uint32_t want = hash(hk[j]);
-            if (((j - want) & hmask) >= ((j - i) & hmask)) {   // backward shift
-                hk[i] = hk[j];
-                hv[i] = hv[j];
-                hk[j] = LX_NONE;
-                i = j;
-            }
-        }
+        if (e < slot_of.size()) slot_of[e] = LX_NONE;
     }
     void free_slot(uint32_t s) {
         map_erase(ev[s]);
@@ -133,7 +110,7 @@ struct FcCache {
         return s;
     }
     void clear() {
-        std::fill(hk.begin(), hk.end(), LX_NONE);
+        std::fill(slot_of.begin(), slot_of.end(), LX_NONE);
         std::fill(ev.begin(), ev.end(), LX_NONE);
         for (uint32_t s = 0; s < W; s++) evk[s] = 0;
         std::fill(ref.begin(), ref.end(), 0);
@@ -180,11 +157,6 @@ int fcc_make(lx_index *h) {
     memset(c->M, 0, (uint64_t)W * W);
     c->ev.assign(W, LX_NONE);
     c->ref.assign(W, 0);
-    uint32_t m = 1;
-    while (m < 2 * W) m <<= 1;
-    c->hmask = m - 1;
-    c->hk.assign(m, LX_NONE);
-    c->hv.assign(m, 0);
     c->clear();
     c->st.slots = W;
     h->fcc = c;

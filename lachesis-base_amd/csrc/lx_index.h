@@ -160,6 +160,8 @@ struct lx_index {
     std::vector<uint32_t> hm_creator, hm_seq, hm_branch, hm_bbefore;
     std::vector<uint32_t> hm_blen;         // per branch: events on it (= device branch_len)
     std::vector<uint32_t> sm_level, sm_cnt, sm_touched;   // scratch
+    std::vector<uint16_t> sm_pl;            // scratch: in-run parents of the run being staged
+    std::vector<uint2> sm_old, sm_meta;     // scratch: "old" entries, meta by Add order
     // the pending run: small-path events assigned on the host but not launched
     // yet, [pend_bs, pend_bs + pend_n), branches from pend_B0 (flush_pending)
     uint32_t pend_n = 0, pend_B0 = 0, pend_maxlvl = 0;

@@ -231,28 +231,43 @@ struct TailArgs {
 // Per event: 3 x uint4
 //   q0 = {branch, seq, prev (previous event of the branch, global; NONE when the
 //         event opens its branch), number of parents}
-//   q1 = {parent offset (into par), first seq of the branch, self-parent (global
+//   q1 = {parent offset (host only), first seq of the branch, self-parent (global
 //         or NONE), branches before Add}
 //   q2 = {creator, flags (kSmallCont: continues its branch), final first_child
-//         of this event (its continuing self-child in the batch, or NONE), 0}
+//         of this event (its continuing self-child in the batch, or NONE),
+//         h0 slot: index of prev's HB row among the "old" entries when prev is
+//         older than the batch (else NONE; set in the staged image)}
 constexpr uint32_t kSmallCont = 1u;
 constexpr uint32_t kSmallCW = 4;     // columns per workgroup (256 threads = 4 columns x 64 event lanes)
-constexpr uint32_t kSmallMaxN = 3072;   // events per small batch (LDS: n x (kSmallCW + 1) x 4 B <= 64 KB)
+constexpr uint32_t kSmallMaxN = 2048;   // events per small batch (positions are 16-bit; LDS below)
 constexpr uint32_t kPendLaunch = 2048;  // a pending run of small batches launches at this size
+constexpr uint32_t kSmallLds = 160 * 1024 - 256;   // dynamic LDS of one k_small workgroup
 struct SmallEv {
     uint4 q0, q1, q2;
 };
+// dynamic LDS of k_small: val[n] + h0v[nh] (uint4), lmeta (uint2, n rounded to
+// even), in-run parents (uint16, rounded to 8), level offsets (L + 1), own
+// events (uint16)
+__host__ __device__ inline uint64_t small_lds_bytes(uint64_t n, uint64_t nh, uint64_t L, uint64_t npl) {
+    return 16 * (n + nh) + 8 * ((n + 1) & ~1ull) + 2 * ((npl + 7) & ~7ull) + 4 * (L + 1) + 2 * n;
+}
 struct SmallArgs {
     uint32_t *hb, *la;
     uint64_t stride;
     uint32_t bs, n;              // first global index, events
     uint32_t B0, B;              // branches before / after the batch
-    // staged image (uint32 words; records first, 16-B aligned): SmallEv[n], then
-    // at word offsets: parents (global, by q1.x), perm (batch positions ordered by
-    // level), level offsets (n_levels + 1), first seqs and creators of branches
-    // B0 .. B-1, (branch, events on it) pairs of the branches the batch touched
+    // staged image (uint32 words; records first, 16-B aligned): SmallEv[n] in
+    // Add order, then at word offsets: meta (level order, uint2 {batch position
+    // | chunks of 4 in-run parents << 16, offset into the in-run list in chunks};
+    // padded to 16 B), the in-run parents (batch positions, uint16, each event's
+    // list padded to a chunk with its own position; padded to 16 B), the "old" entries (uint2
+    // {target, global event}: target = batch position for a parent older than
+    // the batch, 0x80000000 | h0 slot for an older prev), level offsets
+    // (n_levels + 1), first seqs and creators of branches B0 .. B-1, (branch,
+    // events on it) pairs of the branches the batch touched
     const uint32_t *img;         // device copy (NULL: the image is in the kernel arguments)
-    uint32_t o_par, o_perm, o_loff, o_nfirst, o_ncreator, o_blen;
+    uint32_t o_meta, o_pl, o_old, o_loff, o_nfirst, o_ncreator, o_blen;
+    uint32_t n_pl, n_old, n_h0;
     uint32_t n_levels;
     uint32_t n_blen;
     uint32_t *ev_creator, *ev_seq, *ev_branch, *ev_bbefore, *ev_sp, *first_child, *first_root;

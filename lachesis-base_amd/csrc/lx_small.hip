@@ -6,34 +6,76 @@
 // (branch assignment kernels, the persistent column walker, the LowestAfter
 // tail pass) costs far more in launches and syncs than the work itself.  Here
 // the host has already assigned branches in Add order (lx_capi.cpp,
-// add_batch_small: the lastSeq rule of vecengine/index.go:105-141) and staged
-// the batch as SmallEv records; one launch then does everything else:
-//   * workgroup 0 writes the per-event metadata, the branch claims and the new
-//     branches (read only by later launches);
-//   * every workgroup owns kSmallCW columns (branches) and, as k_index, works
-//     column by column with no inter-workgroup communication:
-//       - for the batch's events on its own branches: the branch-row entry and
-//         a zeroed LowestAfter row (the range fill below writes the observed
-//         entries; nothing else may be left from an earlier epoch),
-//       - level by level (the host sorts the batch into topological levels),
-//         64 event lanes x kSmallCW columns: HighestBefore = max-join of the
-//         parents' seqs (in-batch parents from LDS, older ones from the plane;
-//         CollectFrom, vecfc/vector_ops.go:49-79) and the LowestAfter range fill
-//         of DESIGN.md section 3 (the DFS of vecengine/index.go:212-225).
+// add_batch_small: the lastSeq rule of vecengine/index.go:105-141), sorted the
+// run into topological levels and split every event's parents into the ones
+// inside the run (batch positions) and the older ones (flush_pending); one
+// launch does everything else.  Every workgroup owns kSmallCW = 4 columns
+// (branches) and, as k_index, works column by column with no inter-workgroup
+// communication, in four phases:
+//   0. metadata, branch claims and new branches (workgroup 0, read only by
+//      later launches); branch-row entries and zeroed LowestAfter rows of the
+//      events on own branches; the level schedule and the in-run parent lists
+//      copied to LDS;
+//   1. the older parents' HB rows (final in the plane; 16 B = the 4 own
+//      columns per parent, many loads in flight) max-ed into each event's LDS
+//      value, which starts as its own seq in its own column;
+//   2. level by level, LDS only: HighestBefore = the max-join with the in-run
+//      parents' values (CollectFrom, vecfc/vector_ops.go:49-79), one barrier per
+//      level that waits for LDS operations only;
+//   3. HB rows out and the LowestAfter range fill of DESIGN.md section 3 (the
+//      DFS of vecengine/index.go:212-225), every event at once.
+// A 2048-event run of C3 (~40 levels) used to pay three dependent global
+// loads per level (record, parent list, parent value) plus the fill's branch
+// row; now a level costs a few LDS round trips.
 // Fork marks (k_marks) run after it when the epoch has forks.
 #include "lx_internal.h"
 
 namespace lx {
 
+// LDS-only barrier: waits for this wave's LDS operations, not for its global
+// stores (on gfx950 vmcnt also counts stores; __syncthreads' workgroup-scope
+// release would wait for them).  The memory clobber keeps the compiler from
+// moving LDS accesses across it.
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// global -> LDS copy of n16 uint4, four loads in flight per thread
+__device__ __forceinline__ void copy_to_lds(uint4 *dst, const uint4 *src, uint32_t n16, uint32_t t) {
+    for (uint32_t x0 = t; x0 < n16; x0 += 256 * 4) {
+        uint4 v[4];
+#pragma unroll
+        for (uint32_t u = 0; u < 4; u++) v[u] = src[min(x0 + u * 256, n16 - 1)];
+#pragma unroll
+        for (uint32_t u = 0; u < 4; u++)
+            if (x0 + u * 256 < n16) dst[x0 + u * 256] = v[u];
+    }
+}
+
 template <bool MASKED>
 __device__ __forceinline__ void small_body(const SmallArgs &a, const uint32_t *img) {
-    constexpr uint32_t CW = kSmallCW, NQ = 256 / CW;
+    constexpr uint32_t CW = kSmallCW, NQ = 256 / CW, U = 8;
+    static_assert(CW == 4, "one uint4 of HB per event and workgroup");
     const SmallEv *ev = reinterpret_cast<const SmallEv *>(img);
-    const uint32_t *par = img + a.o_par, *perm = img + a.o_perm, *lvl_off = img + a.o_loff;
+    const uint2 *meta = reinterpret_cast<const uint2 *>(img + a.o_meta);
+    const uint32_t *pl = img + a.o_pl;
+    const uint2 *old = reinterpret_cast<const uint2 *>(img + a.o_old);
+    const uint32_t *lvl_off = img + a.o_loff;
     const uint32_t *new_first = img + a.o_nfirst, *new_creator = img + a.o_ncreator, *blen = img + a.o_blen;
-    extern __shared__ uint32_t smem[];
-    uint32_t *val = smem;                  // [n][CW]: HB seqs of the batch's events in own columns
-    uint32_t *own = smem + a.n * CW;       // batch positions of the events on own branches
+    const uint32_t n = a.n, nh = a.n_h0, L = a.n_levels;
+    // LDS (small_lds_bytes): val[n] (HB seqs of the 4 own columns), h0v[nh]
+    // (HB of an older previous branch event), lmeta[n rounded to even], lpl[n_pl
+    // rounded to 8], lloff[L + 1], own[n]
+    extern __shared__ uint4 smem4[];
+    const uint32_t n2 = (n + 1) & ~1u, npl8 = (a.n_pl + 7) & ~7u;
+    uint4 *val = smem4;
+    uint4 *h0v = val + n;
+    uint2 *lmeta = reinterpret_cast<uint2 *>(h0v + nh);
+    uint16_t *lpl = reinterpret_cast<uint16_t *>(lmeta + n2);
+    uint32_t *lloff = reinterpret_cast<uint32_t *>(lpl + npl8);
+    uint16_t *own = reinterpret_cast<uint16_t *>(lloff + L + 1);
+    uint32_t *val32 = reinterpret_cast<uint32_t *>(val);
+    uint32_t *h0v32 = reinterpret_cast<uint32_t *>(h0v);
     __shared__ uint32_t n_own;
 
     const uint32_t t = threadIdx.x;
@@ -43,10 +85,13 @@ __device__ __forceinline__ void small_body(const SmallArgs &a, const uint32_t *i
     const bool valid = col < a.B;
     const uint32_t first = !valid ? 1u : col >= a.B0 ? new_first[col - a.B0] : a.branch_first[col];
     constexpr uint32_t mask = MASKED ? LX_SEQ_MASK : 0xFFFFFFFFu;
-    const uint32_t bs = a.bs, n = a.n;
+    const uint32_t bs = a.bs;
     const uint64_t stride = a.stride;
 
+    // ---- phase 0: metadata (workgroup 0), branch rows and the list of own
+    // events, LDS images
     if (t == 0) n_own = 0;
+    __syncthreads();
     if (blockIdx.x == 0) {
         for (uint32_t i = t; i < n; i += 256) {
             const SmallEv e = ev[i];
@@ -68,21 +113,64 @@ __device__ __forceinline__ void small_body(const SmallArgs &a, const uint32_t *i
         }
         for (uint32_t i = t; i < a.n_blen; i += 256) a.branch_len[blen[2 * i]] = blen[2 * i + 1];
     }
-    __syncthreads();
-    for (uint32_t i = t; i < n; i += 256) {
-        const uint4 q0 = ev[i].q0;
-        if (q0.x >= c0 && q0.x < c0 + CW) {
-            a.brow[(uint64_t)q0.x * a.s_cap + (q0.y - ev[i].q1.y)] = bs + i;
-            own[atomicAdd(&n_own, 1u)] = i;
+    copy_to_lds(reinterpret_cast<uint4 *>(lmeta), reinterpret_cast<const uint4 *>(meta), n2 / 2, t);
+    copy_to_lds(reinterpret_cast<uint4 *>(lpl), reinterpret_cast<const uint4 *>(pl), npl8 / 8, t);
+    for (uint32_t j = t; j <= L; j += 256) lloff[j] = lvl_off[j];
+    for (uint32_t x = t; x < nh; x += 256) h0v[x] = make_uint4(0, 0, 0, 0);
+    for (uint32_t i0 = t; i0 < n; i0 += 256 * 4) {
+        // own seq in its own column (the parents are folded in below); branch
+        // rows and the list of the events on own branches
+        uint4 q0[4];
+        uint32_t f[4];
+#pragma unroll
+        for (uint32_t u = 0; u < 4; u++) {
+            const uint32_t i = min(i0 + u * 256, n - 1);
+            q0[u] = ev[i].q0;
+            f[u] = ev[i].q1.y;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < 4; u++) {
+            const uint32_t i = i0 + u * 256;
+            if (i >= n) continue;
+            const uint32_t d = q0[u].x - c0, s = q0[u].y;
+            val[i] = make_uint4(d == 0 ? s : 0u, d == 1 ? s : 0u, d == 2 ? s : 0u, d == 3 ? s : 0u);
+            if (d < CW) {
+                a.brow[(uint64_t)q0[u].x * a.s_cap + (s - f[u])] = bs + i;
+                own[atomicAdd(&n_own, 1u)] = (uint16_t)i;
+            }
         }
     }
     __syncthreads();
     {
-        // zero the LowestAfter rows of own events (whole 16-B groups; stride is a multiple of 64)
+        // zero the LowestAfter rows of own events (whole 16-B groups; stride is a
+        // multiple of 64); the range fill of phase 3 writes the observed entries,
+        // ordered after these stores by the barrier that ends phase 1
         const uint32_t no = n_own, B4 = (a.B + 3) / 4;
         for (uint32_t x = t; x < no * B4; x += 256) {
             uint4 *row = reinterpret_cast<uint4 *>(a.la + (uint64_t)(bs + own[x / B4]) * stride);
             row[x % B4] = make_uint4(0, 0, 0, 0);
+        }
+    }
+    // ---- phase 1: parents older than the run (HB rows final in the plane) and
+    // the older previous branch events, 16 B (the 4 own columns) per entry,
+    // folded into LDS; every entry independent, U loads in flight per thread
+    for (uint32_t e0 = t; e0 < a.n_old; e0 += 256 * U) {
+        // loads without conditions (clamped to the last entry), so that all U
+        // are in flight before the first is used
+        uint2 o[U];
+        uint4 v[U];
+#pragma unroll
+        for (uint32_t u = 0; u < U; u++) o[u] = old[min(e0 + u * 256, a.n_old - 1)];
+#pragma unroll
+        for (uint32_t u = 0; u < U; u++) v[u] = *reinterpret_cast<const uint4 *>(a.hb + (uint64_t)o[u].y * stride + c0);
+#pragma unroll
+        for (uint32_t u = 0; u < U; u++) {
+            if (e0 + u * 256 >= a.n_old) continue;
+            uint32_t *dst = (o[u].x & 0x80000000u) ? h0v32 + 4 * (o[u].x & 0x7FFFFFFFu) : val32 + 4 * o[u].x;
+            atomicMax(dst + 0, v[u].x & mask);
+            atomicMax(dst + 1, v[u].y & mask);
+            atomicMax(dst + 2, v[u].z & mask);
+            atomicMax(dst + 3, v[u].w & mask);
         }
     }
     // branch rows and zeroed rows are read / overwritten below only by this
@@ -90,43 +178,81 @@ __device__ __forceinline__ void small_body(const SmallArgs &a, const uint32_t *i
     // agent-scope fence would write back the XCD's whole L2 on this part)
     __syncthreads();
 
-    for (uint32_t L = 0; L < a.n_levels; L++) {
-        const uint32_t lo = lvl_off[L], hi = lvl_off[L + 1];
-        for (uint32_t j = lo + q; j < hi && valid; j += NQ) {
-            const uint32_t i = perm[j];
-            const uint4 q0 = ev[i].q0;
-            const uint32_t po = ev[i].q1.x;
-            const uint32_t br = q0.x, seq = q0.y, prev = q0.z, np = q0.w;
-            uint32_t r = (col == br) ? seq : 0u;
-            uint32_t p = 0;
-            for (; p + 4 <= np; p += 4) {
-                uint32_t x[4], v[4];
+    // ---- phase 2: HighestBefore level by level, LDS only (CollectFrom,
+    // vecfc/vector_ops.go:49-79): the max-join of the in-run parents' values
+    // into the value phase 1 left (own seq, older parents).  An event's in-run
+    // parents come in chunks of 4 (padded with the event itself, whose value
+    // does not change a max); up to 16 parents cost two LDS round trips.  The
+    // next level's bounds and first meta entry are read ahead.
+    {
+        const uint2 *lpl2 = reinterpret_cast<const uint2 *>(lpl);
+        uint32_t lo = lloff[0], hi = L ? lloff[1] : 0u;
+        uint2 m_next = lo + q < hi ? lmeta[lo + q] : make_uint2(0, 0);
+        for (uint32_t l = 0; l < L; l++) {
+            const uint32_t hn = l + 2 <= L ? lloff[l + 2] : hi;
+            uint2 m = m_next;
+            m_next = hi + q < hn ? lmeta[hi + q] : make_uint2(0, 0);
+            for (uint32_t j = lo + q; j < hi; j += NQ) {
+                if (j != lo + q) m = lmeta[j];
+                const uint32_t i = m.x & 0xFFFFu, cnt4 = m.x >> 16, off4 = m.y;
+                uint32_t r = val32[4 * i + k];
+                for (uint32_t c = 0; c < cnt4; c += 4) {
+                    uint2 w[4];
 #pragma unroll
-                for (int u = 0; u < 4; u++) x[u] = par[po + p + u];
+                    for (uint32_t u = 0; u < 4; u++) w[u] = lpl2[off4 + min(c + u, cnt4 - 1)];
 #pragma unroll
-                for (int u = 0; u < 4; u++)
-                    v[u] = x[u] >= bs ? val[(x[u] - bs) * CW + k] : a.hb[(uint64_t)x[u] * stride + col];
-#pragma unroll
-                for (int u = 0; u < 4; u++) r = max(r, v[u] & mask);
+                    for (uint32_t u = 0; u < 4; u++)
+                        r = max(max(r, max(val32[4 * (w[u].x & 0xFFFFu) + k], val32[4 * (w[u].x >> 16) + k])),
+                                max(val32[4 * (w[u].y & 0xFFFFu) + k], val32[4 * (w[u].y >> 16) + k]));
+                }
+                val32[4 * i + k] = r;
             }
-            for (; p < np; p++) {
-                const uint32_t x = par[po + p];
-                const uint32_t v = x >= bs ? val[(x - bs) * CW + k] : a.hb[(uint64_t)x * stride + col];
-                r = max(r, v & mask);
-            }
-            a.hb[(uint64_t)(bs + i) * stride + col] = r;
-            val[i * CW + k] = r;
-            // LowestAfter range fill: events (col, s), s in (HB(prev)[col], r], are first
-            // observed from branch br by this event
-            uint32_t h0 = 0;
-            if (prev != LX_NONE)
-                h0 = (prev >= bs ? val[(prev - bs) * CW + k] : a.hb[(uint64_t)prev * stride + col]) & mask;
-            for (uint32_t s = max(h0 + 1u, first); s <= r; s++) {
-                const uint32_t row = a.brow[(uint64_t)col * a.s_cap + (s - first)];
-                a.la[(uint64_t)row * stride + br] = seq;
-            }
+            lds_barrier();
+            lo = hi;
+            hi = hn;
         }
-        __syncthreads();
+    }
+
+    // ---- phase 3: HB rows out, LowestAfter range fill (the
+    // DFS of vecengine/index.go:212-225): events (col, s), s in (HB(prev)[col],
+    // HB(e)[col]], are first observed from branch(e) by e.  Every event is
+    // final; U events per thread at a time keep U branch-row loads in flight.
+    if (!valid) return;
+    for (uint32_t x0 = q; x0 < n; x0 += NQ * U) {
+        // records and branch rows loaded without conditions (clamped), U in flight
+        uint32_t br[U], sq[U], lo[U], hi[U], row[U], pv[U], sl[U];
+#pragma unroll
+        for (uint32_t u = 0; u < U; u++) {
+            const uint32_t i = min(x0 + u * NQ, n - 1);
+            const uint4 q0 = ev[i].q0, q2 = ev[i].q2;
+            br[u] = q0.x;
+            sq[u] = q0.y;
+            pv[u] = q0.z;
+            sl[u] = q2.w;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < U; u++) {
+            const uint32_t i = x0 + u * NQ, ic = min(i, n - 1);
+            const uint32_t r = val32[4 * ic + k];
+            // HB(prev) from the run (val) or from phase 1 (h0v): one LDS read at a
+            // computed address, no branch (a branch would sink the record loads)
+            const uint32_t prev = pv[u];
+            const uint32_t *hp = prev == LX_NONE ? val32 + 4 * ic : prev >= bs ? val32 + 4 * (prev - bs) : h0v32 + 4 * sl[u];
+            const uint32_t h0 = prev == LX_NONE ? 0u : hp[k];
+            lo[u] = max(h0 + 1u, first);
+            hi[u] = i < n ? r : 0u;
+            if (i < n) a.hb[(uint64_t)(bs + i) * stride + col] = r;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < U; u++)
+            row[u] = a.brow[(uint64_t)col * a.s_cap + min(lo[u] - first, hi[u] >= lo[u] ? hi[u] - first : 0u)];
+#pragma unroll
+        for (uint32_t u = 0; u < U; u++)
+            if (lo[u] <= hi[u]) a.la[(uint64_t)row[u] * stride + br[u]] = sq[u];
+#pragma unroll
+        for (uint32_t u = 0; u < U; u++)
+            for (uint32_t s = lo[u] + 1; s <= hi[u]; s++)
+                a.la[(uint64_t)a.brow[(uint64_t)col * a.s_cap + (s - first)] * stride + br[u]] = sq[u];
     }
 }
 
@@ -144,7 +270,7 @@ __global__ __launch_bounds__(256) void k_small_inline(SmallInlineArgs a) {
 hipError_t launch_small(const SmallArgs &a, hipStream_t s) {
     if (!a.n || !a.B) return hipSuccess;
     const uint32_t grid = (a.B + kSmallCW - 1) / kSmallCW;
-    const size_t lds = (size_t)a.n * (kSmallCW + 1) * 4;
+    const size_t lds = small_lds_bytes(a.n, a.n_h0, a.n_levels, a.n_pl);
     if (a.mask) hipLaunchKernelGGL(k_small<true>, dim3(grid), dim3(256), lds, s, a);
     else hipLaunchKernelGGL(k_small<false>, dim3(grid), dim3(256), lds, s, a);
     return hipGetLastError();
@@ -153,7 +279,7 @@ hipError_t launch_small(const SmallArgs &a, hipStream_t s) {
 hipError_t launch_small_inline(const SmallInlineArgs &a, hipStream_t s) {
     if (!a.a.n || !a.a.B) return hipSuccess;
     const uint32_t grid = (a.a.B + kSmallCW - 1) / kSmallCW;
-    const size_t lds = (size_t)a.a.n * (kSmallCW + 1) * 4;
+    const size_t lds = small_lds_bytes(a.a.n, a.a.n_h0, a.a.n_levels, a.a.n_pl);
     if (a.a.mask) hipLaunchKernelGGL(k_small_inline<true>, dim3(grid), dim3(256), lds, s, a);
     else hipLaunchKernelGGL(k_small_inline<false>, dim3(grid), dim3(256), lds, s, a);
     return hipGetLastError();

@@ -1,18 +1,20 @@
 #!/bin/bash
-# Profile evidence for profiles/<round>/: rocprofv3 kernel stats of the default
-# bench line, then HBM traffic of k_fc / k_index from PMC counters collected
-# as MI355X_MICROARCH.md prescribes (FETCH_SIZE and WRITE_SIZE in separate
-# --pmc passes), converted by scripts/traffic_json.py.
-#   OUT=gpurun_out/prof_r01 bash scripts/prof_round.sh
+# Profile evidence for profiles/<round>/: rocprofv3 kernel stats of the
+# default bench run (all legs but the CPU baselines), then k_index / k_fc HBM
+# traffic of the headline config alone from PMC passes (one TCC counter group
+# per pass, as MI355X_MICROARCH.md prescribes), converted by
+# scripts/traffic_json.py.
+#   OUT=gpurun_out/prof_r03 bash scripts/prof_round.sh
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 O=${OUT:-gpurun_out/prof_round}
 mkdir -p $O
-ARGS="${ARGS:---config c3 --steps 3 --warmup 1 --no-cpu}"
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o kt -- python3 bench.py $ARGS --no-abft > $O/kt.log 2>&1 || exit $?
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_abft -o kt_abft -- python3 scripts/bench_abft_only.py > $O/kt_abft.log 2>&1 || exit $?
+timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o kt -- python3 bench.py --no-cpu > $O/kt.log 2>&1 || exit $?
+A="--config ${CFG:-c3} --steps 2 --warmup 1 --no-cpu --no-abft --no-latency --no-configs"
 P="rocprofv3 --kernel-include-regex k_fc|k_index --output-format csv"
-timeout -k 10 400 $P --pmc FETCH_SIZE -d $O/fetch -o fetch -- python3 bench.py $ARGS --no-abft > $O/fetch.log 2>&1 || exit $?
-timeout -k 10 400 $P --pmc WRITE_SIZE -d $O/write -o write -- python3 bench.py $ARGS --no-abft > $O/write.log 2>&1 || exit $?
-python3 scripts/traffic_json.py $O > $O/traffic_c3.json || exit $?
+timeout -k 10 300 $P --pmc TCC_EA0_RDREQ_32B TCC_EA0_RDREQ_64B TCC_EA0_RDREQ_128B TCC_EA0_RDREQ -d $O/rdreq -o rdreq -- python3 bench.py $A > $O/rdreq.log 2>&1 || exit $?
+timeout -k 10 300 $P --pmc WRITE_SIZE TCC_EA0_WRREQ TCC_EA0_WRREQ_64B -d $O/write -o write -- python3 bench.py $A > $O/write.log 2>&1 || exit $?
+timeout -k 10 300 $P --pmc FETCH_SIZE -d $O/fetch -o fetch -- python3 bench.py $A > $O/fetch.log 2>&1 || exit $?
+python3 scripts/traffic_json.py $O > $O/traffic_${CFG:-c3}.json || exit $?
+find $O -name "*trace*.csv" -delete
 echo done

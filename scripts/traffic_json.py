@@ -1,5 +1,5 @@
 """Per-launch HBM bytes of k_index and k_fc from the --pmc passes of
-scripts/prof_r02.sh (mean over dispatches, summed over TCC instances).
+scripts/prof_round.sh (mean over dispatches, summed over TCC instances).
 
 Reads: the L2's memory-side read requests by size, TCC_EA0_RDREQ_{32B,64B,128B}
 (bytes = 32 n32 + 64 n64 + 128 n128), which needs no assumption about the
@@ -41,7 +41,7 @@ def main():
     wr = per_kernel(os.path.join(root, "write"), {"WRITE_SIZE", "TCC_EA0_WRREQ", "TCC_EA0_WRREQ_64B"})
     fe = per_kernel(os.path.join(root, "fetch"), {"FETCH_SIZE"})
     out = {"workload": os.environ.get("CFG", "c3"), "fc_queries": 1 << 24,
-           "method": "rocprofv3 --pmc passes of scripts/prof_r02.sh (one TCC group per pass): reads = "
+           "method": "rocprofv3 --pmc passes of scripts/prof_round.sh (one TCC group per pass): reads = "
                      "32*TCC_EA0_RDREQ_32B + 64*TCC_EA0_RDREQ_64B + 128*TCC_EA0_RDREQ_128B, writes = WRITE_SIZE "
                      "(KiB); mean over dispatches, summed over TCC instances",
            "kernels": {}}

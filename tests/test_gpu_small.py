@@ -3,8 +3,9 @@
 abft calls Add once per event (abft/indexed_lachesis.go:53-82) and
 ForklessCause once per (event, root) pair (abft/event_processing.go:149-161);
 the level batcher hands over one antichain at a time.  lx_add_batch routes
-host-pointer batches of up to 3072 events through host branch assignment +
-one k_small launch (lx_small.hip); these tests check that path bit-exactly
+host-pointer batches of up to 2048 events (that fit one workgroup's LDS)
+through host branch assignment + one k_small launch per pending run
+(lx_small.hip); these tests check that path bit-exactly
 against the C oracle and against the device-assigned walker path (k_index),
 including mixed sequences of both, rollbacks, errors and deep batches.
 """
@@ -132,9 +133,9 @@ def test_mixed_small_and_device_batches(lx):
 
 
 def test_deep_chain_one_batch(lx):
-    """3000 levels in one small batch: a single validator's chain plus a second
+    """2000 levels in one small batch: a single validator's chain plus a second
     validator that references it (every event its own level)."""
-    d = lx.tools.gen_dag(2, 1500, 2, seed=5)
+    d = lx.tools.gen_dag(2, 1000, 2, seed=5)
     w = [2, 1]
     o = oracle_for(d, w)
     ix = lx.Index()
@@ -142,6 +143,26 @@ def test_deep_chain_one_batch(lx):
     ix.add_batch(d.creator, d.seq, d.poff, d.par)
     assert levels_of(d).max() > 1000
     rows_equal(ix, o, range(len(d)))
+    ix.close()
+
+
+@pytest.mark.parametrize("chunk", [1, 37, 400, 2048])
+def test_many_parents_lds_budget(lx, chunk):
+    """Events with 40 parents: pending runs launch early when the next batch
+    would not fit one k_small workgroup's LDS, and a 2048-event batch (80k
+    parents) takes the device-assigned path; results equal the oracle either way."""
+    d = lx.tools.gen_dag(64, 40, 40, cheaters=3, forks=4, seed=23)
+    w = [1 + (i % 7) for i in range(64)]
+    N = len(d)
+    o = oracle_for(d, w)
+    ix = lx.Index()
+    ix.reset(w)
+    for lo in range(0, N, chunk):
+        hi = min(N, lo + chunk)
+        ix.add_batch(d.creator[lo:hi], d.seq[lo:hi], d.poff[lo:hi + 1], d.par)
+    rows_equal(ix, o, range(0, N, 5))
+    qa, qb = lx.tools.fc_queries(d.lamport, 50_000, window=16, seed=3)
+    np.testing.assert_array_equal(ix.forkless_cause_batch(qa, qb), o.forkless_cause_batch(qa, qb))
     ix.close()
 
 
