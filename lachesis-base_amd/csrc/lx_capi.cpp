@@ -1075,27 +1075,10 @@ int flush_pending(lx_index *h) {
         if (h->touch_mark[br] != tm) { h->touch_mark[br] = tm; h->sm_touched.push_back(br); }
     }
     const uint32_t n_blen = (uint32_t)h->sm_touched.size();
-    // in-run parents (batch positions) and "old" entries: parents older than the
+    // in-run parents (run positions) and "old" entries -- parents older than the
     // run, and the older previous branch event of a branch's first event in it
-    h->sm_pl.clear();
-    h->sm_old.clear();
-    h->sm_meta.resize(n);
-    uint32_t nh = 0;
-    const uint32_t *pp = h->pend_par.data();
-    for (uint32_t i = 0; i < n; i++) {
-        // in-run parents in chunks of 4, padded with the event itself (k_small)
-        const SmallEv &e = h->pend_ev[i];
-        const uint32_t off = (uint32_t)h->sm_pl.size();
-        for (uint32_t x = e.q1.x, xe = e.q1.x + e.q0.w; x < xe; x++) {
-            const uint32_t g = pp[x];
-            if (g >= bs) h->sm_pl.push_back((uint16_t)(g - bs));
-            else h->sm_old.push_back(make_uint2(i, g));
-        }
-        while (h->sm_pl.size() & 3) h->sm_pl.push_back((uint16_t)i);
-        h->sm_meta[i] = make_uint2(i | ((uint32_t)h->sm_pl.size() - off) / 4 << 16, off / 4);
-        if (e.q0.z != LX_NONE && e.q0.z < bs) h->sm_old.push_back(make_uint2(0x80000000u | nh++, e.q0.z));
-    }
-    const uint32_t n_pl = (uint32_t)h->sm_pl.size(), n_old = (uint32_t)h->sm_old.size();
+    // -- were split as the events were added (add_batch_small)
+    const uint32_t n_pl = (uint32_t)h->pend_pl.size(), n_old = (uint32_t)h->pend_old.size(), nh = h->pend_nh;
     if (small_lds_bytes(n, nh, L, n_pl) > kSmallLds)   // add_batch_small keeps runs within it
         return h->fail(LX_ERR_STATE, "pending run exceeds the k_small LDS budget");
     // regions 16-B aligned: the kernel copies meta and the in-run list to LDS as uint4
@@ -1107,12 +1090,6 @@ int flush_pending(lx_index *h) {
     if (inl) img = h->sm_inl.img;
     else if ((rc = stage_slot(h, words, &img, &slot))) return rc;
     memcpy(img, h->pend_ev.data(), w_ev * 4);
-    {   // h0 slots of the events whose prev is older than the run (same order as above)
-        SmallEv *iev = reinterpret_cast<SmallEv *>(img);
-        uint32_t k = 0;
-        for (uint32_t i = 0; i < n; i++)
-            iev[i].q2.w = (iev[i].q0.z != LX_NONE && iev[i].q0.z < bs) ? k++ : LX_NONE;
-    }
     // meta in level order (counting sort; Add order inside a level), level offsets
     uint2 *meta = reinterpret_cast<uint2 *>(img + w_ev);
     uint32_t *ipl = img + w_ev + w_meta;
@@ -1122,9 +1099,9 @@ int flush_pending(lx_index *h) {
     for (uint32_t i = 0; i < n; i++) h->sm_cnt[h->pend_lvl[i] + 1]++;
     for (uint32_t l = 0; l < L; l++) h->sm_cnt[l + 1] += h->sm_cnt[l];
     for (uint32_t l = 0; l <= L; l++) loff[l] = h->sm_cnt[l];
-    for (uint32_t i = 0; i < n; i++) meta[h->sm_cnt[h->pend_lvl[i]]++] = h->sm_meta[i];
-    if (n_pl) memcpy(ipl, h->sm_pl.data(), n_pl * 2ull);
-    if (n_old) memcpy(iold, h->sm_old.data(), n_old * 8ull);
+    for (uint32_t i = 0; i < n; i++) meta[h->sm_cnt[h->pend_lvl[i]]++] = h->pend_meta[i];
+    if (n_pl) memcpy(ipl, h->pend_pl.data(), n_pl * 2ull);
+    if (n_old) memcpy(iold, h->pend_old.data(), n_old * 8ull);
     uint32_t *nfirst = loff + L + 1, *ncreator = nfirst + nf, *blen = ncreator + nf;
     for (uint32_t x = 0; x < nf; x++) {
         nfirst[x] = h->h_branch_first[B0 + x];
@@ -1271,7 +1248,7 @@ int add_batch_small(lx_index *h, uint32_t n, const uint32_t *creator, const uint
         }
     }
     // the run launches before it would outgrow one k_small (LDS, small_fits)
-    if (h->pend_n && !small_fits(h, h->pend_n + n, h->pend_par.size() + (poff[n] - poff[0])) &&
+    if (h->pend_n && !small_fits(h, h->pend_n + n, h->pend_npar + (poff[n] - poff[0])) &&
         ((rc = h->hip(set_dev(h->device), "set device")) || (rc = flush_pending(h))))
         return rc;
     if (!h->pend_n) {
@@ -1279,12 +1256,16 @@ int add_batch_small(lx_index *h, uint32_t n, const uint32_t *creator, const uint
         h->pend_B0 = h->B;
         h->pend_maxlvl = 0;
         h->pend_ev.clear();
-        h->pend_par.clear();
         h->pend_lvl.clear();
+        h->pend_meta.clear();
+        h->pend_pl.clear();
+        h->pend_old.clear();
+        h->pend_npar = 0;
+        h->pend_nh = 0;
     }
     const uint64_t pbs = h->pend_bs;
-    const uint32_t B0 = h->B, pn0 = h->pend_n;
-    const size_t par0 = h->pend_par.size();
+    const uint32_t B0 = h->B, pn0 = h->pend_n, nh0 = h->pend_nh;
+    const size_t pl0 = h->pend_pl.size(), old0 = h->pend_old.size();
     uint32_t B = B0, bmax = 0;
     if (h->hm_creator.capacity() < bs + n) {
         // the mirror grows with the epoch: reserve for the device capacity at once
@@ -1297,7 +1278,7 @@ int add_batch_small(lx_index *h, uint32_t n, const uint32_t *creator, const uint
     h->hm_bbefore.resize(bs + n);
     h->pend_ev.resize(pn0 + n);
     h->pend_lvl.resize(pn0 + n);
-    h->pend_par.insert(h->pend_par.end(), par + poff[0], par + poff[n]);
+    h->pend_meta.resize(pn0 + n);
     for (uint32_t i = 0; i < n; i++) {
         const uint64_t g = bs + i;
         const uint32_t c = creator[i], s = seq[i];
@@ -1327,17 +1308,35 @@ int add_batch_small(lx_index *h, uint32_t n, const uint32_t *creator, const uint
         h->hm_seq[g] = s;
         h->hm_branch[g] = br;
         h->hm_bbefore[g] = bb;
-        uint32_t lvl = 0;
-        for (uint64_t x = p0; x < p1; x++)
-            if (par[x] >= pbs) lvl = std::max(lvl, h->pend_lvl[par[x] - pbs] + 1);
+        // level inside the run; parents split into in-run positions (chunks of
+        // 4, padded with the event's own position) and older events (k_small)
         const uint32_t pi = pn0 + i;
+        const uint32_t e_pl = (uint32_t)h->pend_pl.size(), e_old = (uint32_t)h->pend_old.size();
+        uint32_t lvl = 0;
+        for (uint64_t x = p0; x < p1; x++) {
+            const uint32_t gp = par[x];
+            if (gp >= pbs) {
+                lvl = std::max(lvl, h->pend_lvl[gp - pbs] + 1);
+                h->pend_pl.push_back((uint16_t)(gp - pbs));
+            } else {
+                h->pend_old.push_back(make_uint2(pi, gp));
+            }
+        }
+        while (h->pend_pl.size() & 3) h->pend_pl.push_back((uint16_t)pi);
+        h->pend_meta[pi] = make_uint2(pi | ((uint32_t)h->pend_pl.size() - e_pl) / 4 << 16, e_pl / 4);
+        const uint32_t prev = (cont && s > 1) ? sp : LX_NONE;
+        uint32_t hslot = LX_NONE;
+        if (prev != LX_NONE && prev < pbs) {
+            hslot = h->pend_nh++;
+            h->pend_old.push_back(make_uint2(0x80000000u | hslot, prev));
+        }
         h->pend_lvl[pi] = lvl;
         h->pend_maxlvl = std::max(h->pend_maxlvl, lvl);
         bmax = std::max(bmax, s);
         SmallEv &e = h->pend_ev[pi];
-        e.q0 = make_uint4(br, s, (cont && s > 1) ? sp : LX_NONE, (uint32_t)(p1 - p0));
-        e.q1 = make_uint4((uint32_t)(par0 + (p0 - poff[0])), h->h_branch_first[br], sp, bb);
-        e.q2 = make_uint4(c, cont ? kSmallCont : 0u, LX_NONE, 0u);
+        e.q0 = make_uint4(br, s, prev, (uint32_t)(p1 - p0));
+        e.q1 = make_uint4(e_old, h->h_branch_first[br], sp, bb);
+        e.q2 = make_uint4(c, cont ? kSmallCont : 0u, LX_NONE, hslot);
         if (cont && sp != LX_NONE && sp >= pbs) h->pend_ev[sp - pbs].q2.z = (uint32_t)g;
         if (out_branch) out_branch[i] = br;
     }
@@ -1356,7 +1355,10 @@ int add_batch_small(lx_index *h, uint32_t n, const uint32_t *creator, const uint
         h->hm_n = std::min<uint64_t>(h->hm_n, bs);
         h->pend_ev.resize(pn0);
         h->pend_lvl.resize(pn0);
-        h->pend_par.resize(par0);
+        h->pend_meta.resize(pn0);
+        h->pend_pl.resize(pl0);
+        h->pend_old.resize(old0);
+        h->pend_nh = nh0;
         for (uint32_t i = 0; i < pn0; i++)
             if (h->pend_ev[i].q2.z != LX_NONE && h->pend_ev[i].q2.z >= bs) h->pend_ev[i].q2.z = LX_NONE;
         return rc;
@@ -1370,6 +1372,7 @@ int add_batch_small(lx_index *h, uint32_t n, const uint32_t *creator, const uint
     h->hwm = std::max(h->hwm, h->n_events);
     h->hm_n = h->n_events;
     h->last_npar = poff[n] - poff[0];
+    h->pend_npar += poff[n] - poff[0];
     h->pend_n = pn0 + n;
     if (h->pend_n >= kPendLaunch) return flush_pending(h);
     return 0;
@@ -1583,7 +1586,9 @@ int lx_reset(lx_index *h, uint32_t nv, const uint32_t *w) {
     h->loading = false;
     h->have_epoch = true;
     if (!h->fcc_slots_set) {
-        const uint32_t w = std::min<uint32_t>(8192, std::max<uint32_t>(512, round_up(4 * nv, 64)));
+        // two frames of roots (C5, V = 1000: 2048 slots miss as often as 4032 and
+        // fill rows half as long; profiles/r03/dropin)
+        const uint32_t w = std::min<uint32_t>(8192, std::max<uint32_t>(512, round_up(2 * nv, 64)));
         if (w != h->fcc_slots) fcc_destroy(h);
         h->fcc_slots = w;
     }
@@ -1656,12 +1661,19 @@ int lx_drop_not_flushed(lx_index *h) {
         // device, so the rollback is host-only (Build = Add + DropNotFlushed
         // costs no launch)
         const uint32_t keep = (uint32_t)(h->n_flushed - h->pend_bs);
-        h->pend_par.resize(h->pend_ev[keep].q1.x);
+        h->pend_old.resize(h->pend_ev[keep].q1.x);
+        h->pend_pl.resize(4ull * h->pend_meta[keep].y);
         h->pend_ev.resize(keep);
         h->pend_lvl.resize(keep);
+        h->pend_meta.resize(keep);
         h->pend_maxlvl = 0;
+        h->pend_nh = 0;
+        h->pend_npar = 0;
         for (uint32_t i = 0; i < keep; i++) {
-            if (h->pend_ev[i].q2.z != LX_NONE && h->pend_ev[i].q2.z >= h->n_flushed) h->pend_ev[i].q2.z = LX_NONE;
+            SmallEv &e = h->pend_ev[i];
+            if (e.q2.z != LX_NONE && e.q2.z >= h->n_flushed) e.q2.z = LX_NONE;
+            if (e.q2.w != LX_NONE) h->pend_nh = e.q2.w + 1;
+            h->pend_npar += e.q0.w;
             h->pend_maxlvl = std::max(h->pend_maxlvl, h->pend_lvl[i]);
         }
         h->pend_n = keep;

@@ -33,6 +33,7 @@
 #include "lx_index.h"
 
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 
 using namespace lxi;
@@ -50,6 +51,12 @@ struct FcCache {
     uint8_t *g7 = nullptr, *g7_dev = nullptr;       // column generation per slot, 1..127
     uint8_t *M = nullptr, *M_dev = nullptr;         // [W][W]
     uint32_t *qa = nullptr, *qa_dev = nullptr;      // the row's a
+    // completion of the last fill: the stream writes fill_seq into done[0] after
+    // it (hipStreamWriteValue32); the host spins on the answer it needs, and
+    // waits for done before it changes slots, generations or qa again
+    uint32_t *done = nullptr, *done_dev = nullptr;
+    uint32_t fill_seq = 0;
+    bool inflight = false;
     std::vector<uint32_t> ev;                       // slot -> event (LX_NONE: free)
     std::vector<uint8_t> ref;                       // clock reference bits
     std::vector<uint32_t> free_slots;
@@ -126,7 +133,7 @@ namespace {
 
 void fcc_free(FcCache *c) {
     if (!c) return;
-    for (void *p : {(void *)c->evk, (void *)c->g7, (void *)c->M, (void *)c->qa})
+    for (void *p : {(void *)c->evk, (void *)c->g7, (void *)c->M, (void *)c->qa, (void *)c->done})
         if (p) (void)hipHostFree(p);
     if (c->d_psum) (void)hipFree(c->d_psum);
     if (c->d_k) (void)hipFree(c->d_k);
@@ -149,12 +156,14 @@ int fcc_make(lx_index *h) {
     if (e == hipSuccess) { e = pin((void **)&c->g7, &d, W); c->g7_dev = static_cast<uint8_t *>(d); }
     if (e == hipSuccess) { e = pin((void **)&c->M, &d, (uint64_t)W * W); c->M_dev = static_cast<uint8_t *>(d); }
     if (e == hipSuccess) { e = pin((void **)&c->qa, &d, 64); c->qa_dev = static_cast<uint32_t *>(d); }
+    if (e == hipSuccess) { e = pin((void **)&c->done, &d, 64); c->done_dev = static_cast<uint32_t *>(d); }
     if (e != hipSuccess) {
         fcc_free(c);
         return h->hip(e, "ForklessCause cache (pinned memory)");
     }
     memset(c->g7, 0, W);
     memset(c->M, 0, (uint64_t)W * W);
+    c->done[0] = 0;
     c->ev.assign(W, LX_NONE);
     c->ref.assign(W, 0);
     c->clear();
@@ -262,6 +271,38 @@ int fcc_tile(lx_index *h, FcCache *c) {
     return 0;
 }
 
+// the last fill has finished (its kernels no longer read evk / g7 / qa or write
+// M): spin on the stream's completion word, or synchronize the stream (errors)
+int fcc_quiesce(lx_index *h, FcCache *c) {
+    if (!c->inflight) return 0;
+    const volatile uint32_t *dn = c->done;
+    for (int k = 0; k < 1 << 22; k++)
+        if (*dn == c->fill_seq) {
+            c->inflight = false;
+            return 0;
+        }
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    c->inflight = false;
+    return 0;
+}
+
+// wait for M[sa][sb] to carry the column's generation (the answer of the fill
+// just enqueued): a spin on pinned memory returns ~5 us sooner than a stream
+// synchronization (scripts/probes/sync_latency.hip); on timeout the stream is
+// synchronized, which also reports a failed launch
+int fcc_wait_answer(lx_index *h, FcCache *c, uint32_t sa, uint32_t sb) {
+    const volatile uint8_t *m = c->M + (uint64_t)sa * c->W + sb;
+    const uint8_t want = c->g7[sb];
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t k = 0;; k++) {
+        if ((*m >> 1) == want) return 0;
+        if ((k & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(200)) break;
+    }
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    c->inflight = false;
+    return 0;
+}
+
 inline bool fcc_hit(FcCache *c, uint32_t a, uint32_t b, uint8_t *out) {
     const uint32_t sa = a == c->last_a ? c->last_sa : c->find(a);
     if (sa == LX_NONE) return false;
@@ -283,8 +324,17 @@ int fcc_query(lx_index *h, uint32_t a, uint32_t b, uint8_t *out) {
         c->st.hits++;
         return 0;
     }
-    HIPCHK(h, set_dev(h->device));
     int rc;
+    if (c->inflight) {
+        // the last fill may still be writing the entry (the caller returned as
+        // soon as its own answer landed): let it finish, then look again
+        if ((rc = fcc_quiesce(h, c))) return rc;
+        if (fcc_hit(c, a, b, out)) {
+            c->st.hits++;
+            return 0;
+        }
+    }
+    HIPCHK(h, set_dev(h->device));
     if ((rc = flush_pending(h))) return rc;   // the fills read rows of events the pending run adds
     uint32_t sa = c->find(a);
     const bool a_new = sa == LX_NONE;
@@ -298,7 +348,9 @@ int fcc_query(lx_index *h, uint32_t a, uint32_t b, uint8_t *out) {
     if (a_new || a == c->last_a) rc = fcc_row(h, c, a, sa);
     else rc = fcc_tile(h, c);
     if (rc) return rc;
-    HIPCHK(h, hipStreamSynchronize(h->stream));
+    HIPCHK(h, hipStreamWriteValue32(h->stream, c->done_dev, ++c->fill_seq, 0));
+    c->inflight = true;
+    if ((rc = fcc_wait_answer(h, c, sa, sb))) return rc;
     const uint8_t m = c->M[(uint64_t)sa * c->W + sb];
     if ((m >> 1) != c->g7[sb]) return h->fail(LX_ERR_STATE, "ForklessCause cache: fill left (%u, %u) unanswered", a, b);
     c->ref[sa] = c->ref[sb] = 1;
@@ -311,18 +363,21 @@ int fcc_query(lx_index *h, uint32_t a, uint32_t b, uint8_t *out) {
 }  // namespace
 
 void fcc_destroy(lx_index *h) {
-    if (h->fcc) (void)hipStreamSynchronize(h->stream);
+    if (h->fcc) (void)hipStreamSynchronize(h->stream);   // no fill in flight afterwards
     fcc_free(h->fcc);
     h->fcc = nullptr;
 }
 
 void fcc_clear(lx_index *h) {
-    if (h->fcc) h->fcc->clear();
+    if (!h->fcc) return;
+    (void)fcc_quiesce(h, h->fcc);
+    h->fcc->clear();
 }
 
 void fcc_forget_from(lx_index *h, uint64_t n) {
     FcCache *c = h->fcc;
     if (!c) return;
+    (void)fcc_quiesce(h, c);
     for (uint32_t s = 0; s < c->used; s++)
         if (c->ev[s] != LX_NONE && c->ev[s] >= n) c->free_slot(s);
 }

@@ -160,15 +160,17 @@ struct lx_index {
     std::vector<uint32_t> hm_creator, hm_seq, hm_branch, hm_bbefore;
     std::vector<uint32_t> hm_blen;         // per branch: events on it (= device branch_len)
     std::vector<uint32_t> sm_level, sm_cnt, sm_touched;   // scratch
-    std::vector<uint16_t> sm_pl;            // scratch: in-run parents of the run being staged
-    std::vector<uint2> sm_old, sm_meta;     // scratch: "old" entries, meta by Add order
     // the pending run: small-path events assigned on the host but not launched
     // yet, [pend_bs, pend_bs + pend_n), branches from pend_B0 (flush_pending)
     uint32_t pend_n = 0, pend_B0 = 0, pend_maxlvl = 0;
     uint64_t pend_bs = 0;
-    std::vector<SmallEv> pend_ev;          // records (q1.x = offset into pend_par)
-    std::vector<uint32_t> pend_par;        // parents, global indices
+    std::vector<SmallEv> pend_ev;          // records (q1.x = offset into pend_old, q2.w = h0 slot)
     std::vector<uint32_t> pend_lvl;        // topological level inside the run
+    std::vector<uint2> pend_meta;          // per event {position | chunks << 16, chunk offset into pend_pl}
+    std::vector<uint16_t> pend_pl;         // in-run parents (run positions), chunks of 4 (k_small)
+    std::vector<uint2> pend_old;           // {target, global event}: parents older than the run, older prevs
+    uint64_t pend_npar = 0;                // parents of the run (LDS budget, small_fits)
+    uint32_t pend_nh = 0;                  // h0 slots of the run
     std::vector<uint32_t> touch_mark;      // per branch: stamp of the last run that touched it
     uint32_t touch_stamp = 0;
     static constexpr int kSlots = 4;       // pinned staging images in flight

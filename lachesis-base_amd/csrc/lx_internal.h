@@ -231,12 +231,12 @@ struct TailArgs {
 // Per event: 3 x uint4
 //   q0 = {branch, seq, prev (previous event of the branch, global; NONE when the
 //         event opens its branch), number of parents}
-//   q1 = {parent offset (host only), first seq of the branch, self-parent (global
-//         or NONE), branches before Add}
+//   q1 = {offset of its entries in the run's "old" list (host only), first seq of
+//         the branch, self-parent (global or NONE), branches before Add}
 //   q2 = {creator, flags (kSmallCont: continues its branch), final first_child
 //         of this event (its continuing self-child in the batch, or NONE),
 //         h0 slot: index of prev's HB row among the "old" entries when prev is
-//         older than the batch (else NONE; set in the staged image)}
+//         older than the batch (else NONE)}
 constexpr uint32_t kSmallCont = 1u;
 constexpr uint32_t kSmallCW = 4;     // columns per workgroup (256 threads = 4 columns x 64 event lanes)
 constexpr uint32_t kSmallMaxN = 2048;   // events per small batch (positions are 16-bit; LDS below)

@@ -140,7 +140,9 @@ __device__ __forceinline__ void small_body(const SmallArgs &a, const uint32_t *i
             }
         }
     }
-    __syncthreads();
+    // LDS only: the global stores above are ordered before phase 3 by the
+    // barrier that ends phase 1, and phase 1 reads only rows older than the run
+    lds_barrier();
     {
         // zero the LowestAfter rows of own events (whole 16-B groups; stride is a
         // multiple of 64); the range fill of phase 3 writes the observed entries,
@@ -151,6 +153,21 @@ __device__ __forceinline__ void small_body(const SmallArgs &a, const uint32_t *i
             row[x % B4] = make_uint4(0, 0, 0, 0);
         }
     }
+    // phase 3's first records, loaded now so that they are in registers when
+    // the levels are done (one dependent global round trip less per launch)
+    uint32_t br[U], sq[U], pv[U], sl[U];
+    auto load_recs = [&](uint32_t x0) {
+#pragma unroll
+        for (uint32_t u = 0; u < U; u++) {
+            const uint32_t i = min(x0 + u * NQ, n - 1);
+            const uint4 q0 = ev[i].q0, q2 = ev[i].q2;
+            br[u] = q0.x;
+            sq[u] = q0.y;
+            pv[u] = q0.z;
+            sl[u] = q2.w;
+        }
+    };
+    load_recs(q);
     // ---- phase 1: parents older than the run (HB rows final in the plane) and
     // the older previous branch events, 16 B (the 4 own columns) per entry,
     // folded into LDS; every entry independent, U loads in flight per thread
@@ -219,17 +236,10 @@ __device__ __forceinline__ void small_body(const SmallArgs &a, const uint32_t *i
     // final; U events per thread at a time keep U branch-row loads in flight.
     if (!valid) return;
     for (uint32_t x0 = q; x0 < n; x0 += NQ * U) {
-        // records and branch rows loaded without conditions (clamped), U in flight
-        uint32_t br[U], sq[U], lo[U], hi[U], row[U], pv[U], sl[U];
-#pragma unroll
-        for (uint32_t u = 0; u < U; u++) {
-            const uint32_t i = min(x0 + u * NQ, n - 1);
-            const uint4 q0 = ev[i].q0, q2 = ev[i].q2;
-            br[u] = q0.x;
-            sq[u] = q0.y;
-            pv[u] = q0.z;
-            sl[u] = q2.w;
-        }
+        // records (the first iteration's were loaded before phase 1) and
+        // branch rows loaded without conditions (clamped), U in flight
+        uint32_t lo[U], hi[U], row[U];
+        if (x0 != q) load_recs(x0);
 #pragma unroll
         for (uint32_t u = 0; u < U; u++) {
             const uint32_t i = x0 + u * NQ, ic = min(i, n - 1);
