@@ -188,6 +188,8 @@ typedef struct lx_fc_stats {
     uint64_t pairs;         /* pairs evaluated on the GPU by the fills */
     uint32_t slots;         /* working set capacity (events) */
     uint32_t slots_used;
+    uint64_t miss_ns;       /* host time inside misses (launch + wait), ns */
+    uint64_t wait_ns;       /* ... of which waiting for the answer to land */
 } lx_fc_stats;
 int lx_fc_cache_stats(const lx_index *h, lx_fc_stats *out);
 

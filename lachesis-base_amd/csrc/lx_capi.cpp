@@ -1177,6 +1177,60 @@ int flush_pending(lx_index *h) {
     return 0;
 }
 
+// The pending run is one fork-free event a: add it and fill the FC cache row
+// of a against the n_slots events of evk in one k_add1_row launch (the
+// unchanged caller's Add-then-ForklessCause miss; lx_fccache.cpp).  Returns 1
+// (nothing enqueued) when the run is not of that shape; the caller then
+// flushes and fills separately.
+int flush_add1_row(lx_index *h, uint32_t a, const uint32_t *evk_dev, uint32_t n_slots, const uint8_t *tag_dev,
+                   uint8_t *out_dev, uint32_t *psum_dev) {
+    if (h->pend_n != 1 || h->pend_bs != a || h->B != h->V || h->pend_B0 != h->B || h->n_cheat || h->small_timing ||
+        h->sharded() || h->rowseg() || !n_slots)
+        return 1;
+    const SmallEv &e = h->pend_ev[0];
+    // parents: all older than the run (one event), in its "old" entries
+    Add1RowArgs r{};
+    uint32_t np = 0;
+    for (const uint2 &o : h->pend_old)
+        if (!(o.x & 0x80000000u)) {
+            if (np == kAdd1MaxPar) return 1;
+            r.par[np++] = o.y;
+        }
+    if (np != e.q0.w) return 1;
+    r.hb = h->hb;
+    r.la = h->la;
+    r.stride = h->pstride;
+    r.a = a;
+    r.e = e;
+    r.blen = h->hm_blen[e.q0.x];
+    r.B = h->B;
+    r.w_br = h->weights[e.q0.x];
+    r.ev_creator = h->ev_creator;
+    r.ev_seq = h->ev_seq;
+    r.ev_branch = h->ev_branch;
+    r.ev_bbefore = h->ev_bbefore;
+    r.ev_sp = h->ev_sp;
+    r.first_child = h->first_child;
+    r.first_root = h->first_root;
+    r.branch_len = h->branch_len;
+    r.brow = h->brow;
+    r.branch_first = h->branch_first;
+    r.s_cap = h->s_cap;
+    r.evk = evk_dev;
+    r.n_slots = n_slots;
+    r.tag = tag_dev;
+    r.out = out_dev;
+    r.wpad = h->wpad;
+    r.quorum = h->quorum;
+    r.psum = psum_dev;
+    HIPCHK(h, lx::launch_add1_row(r, h->stream));
+    h->pend_n = 0;
+    h->stats = lx_stats{};
+    h->stats.index_launches = 1;
+    h->stats_lazy = false;
+    return 0;
+}
+
 namespace {
 
 // flush_pending for a launch on stream s: a foreign stream is not ordered after

@@ -51,12 +51,18 @@ struct FcCache {
     uint8_t *g7 = nullptr, *g7_dev = nullptr;       // column generation per slot, 1..127
     uint8_t *M = nullptr, *M_dev = nullptr;         // [W][W]
     uint32_t *qa = nullptr, *qa_dev = nullptr;      // the row's a
-    // completion of the last fill: the stream writes fill_seq into done[0] after
-    // it (hipStreamWriteValue32); the host spins on the answer it needs, and
-    // waits for done before it changes slots, generations or qa again
-    uint32_t *done = nullptr, *done_dev = nullptr;
-    uint32_t fill_seq = 0;
+    // completion of the last fill: an event recorded after it; the host spins on
+    // the answer it needs, and waits for the event before it changes slots,
+    // generations or qa again
+    hipEvent_t filled = nullptr;
     bool inflight = false;
+    // a k_add1_row fill is complete once every entry of its row carries its
+    // column's generation (each entry is written after that slot's reads): no
+    // event is recorded for it
+    bool inflight_row = false;
+    uint32_t inflight_sa = 0, inflight_n = 0;
+    // k_add1_row's per-slot {count, sum} words (W x uint64), zero between launches
+    uint32_t *d_rsum = nullptr;
     std::vector<uint32_t> ev;                       // slot -> event (LX_NONE: free)
     std::vector<uint8_t> ref;                       // clock reference bits
     std::vector<uint32_t> free_slots;
@@ -133,8 +139,10 @@ namespace {
 
 void fcc_free(FcCache *c) {
     if (!c) return;
-    for (void *p : {(void *)c->evk, (void *)c->g7, (void *)c->M, (void *)c->qa, (void *)c->done})
+    for (void *p : {(void *)c->evk, (void *)c->g7, (void *)c->M, (void *)c->qa})
         if (p) (void)hipHostFree(p);
+    if (c->filled) (void)hipEventDestroy(c->filled);
+    if (c->d_rsum) (void)hipFree(c->d_rsum);
     if (c->d_psum) (void)hipFree(c->d_psum);
     if (c->d_k) (void)hipFree(c->d_k);
     delete c;
@@ -156,14 +164,15 @@ int fcc_make(lx_index *h) {
     if (e == hipSuccess) { e = pin((void **)&c->g7, &d, W); c->g7_dev = static_cast<uint8_t *>(d); }
     if (e == hipSuccess) { e = pin((void **)&c->M, &d, (uint64_t)W * W); c->M_dev = static_cast<uint8_t *>(d); }
     if (e == hipSuccess) { e = pin((void **)&c->qa, &d, 64); c->qa_dev = static_cast<uint32_t *>(d); }
-    if (e == hipSuccess) { e = pin((void **)&c->done, &d, 64); c->done_dev = static_cast<uint32_t *>(d); }
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->filled, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipMalloc((void **)&c->d_rsum, 8ull * W);
+    if (e == hipSuccess) e = hipMemsetAsync(c->d_rsum, 0, 8ull * W, h->stream);
     if (e != hipSuccess) {
         fcc_free(c);
         return h->hip(e, "ForklessCause cache (pinned memory)");
     }
     memset(c->g7, 0, W);
     memset(c->M, 0, (uint64_t)W * W);
-    c->done[0] = 0;
     c->ev.assign(W, LX_NONE);
     c->ref.assign(W, 0);
     c->clear();
@@ -272,16 +281,26 @@ int fcc_tile(lx_index *h, FcCache *c) {
 }
 
 // the last fill has finished (its kernels no longer read evk / g7 / qa or write
-// M): spin on the stream's completion word, or synchronize the stream (errors)
+// M; by the time the caller asks again it normally has)
 int fcc_quiesce(lx_index *h, FcCache *c) {
     if (!c->inflight) return 0;
-    const volatile uint32_t *dn = c->done;
-    for (int k = 0; k < 1 << 22; k++)
-        if (*dn == c->fill_seq) {
-            c->inflight = false;
-            return 0;
+    if (c->inflight_row) {
+        const volatile uint8_t *row = c->M + (uint64_t)c->inflight_sa * c->W;
+        const auto t0 = std::chrono::steady_clock::now();
+        uint32_t s = 0;
+        for (uint32_t k = 0; s < c->inflight_n; k++) {
+            if ((row[s] >> 1) == c->g7[s]) {
+                s++;
+                continue;
+            }
+            if ((k & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(200)) {
+                HIPCHK(h, hipStreamSynchronize(h->stream));
+                break;
+            }
         }
-    HIPCHK(h, hipStreamSynchronize(h->stream));
+    } else {
+        HIPCHK(h, hipEventSynchronize(c->filled));
+    }
     c->inflight = false;
     return 0;
 }
@@ -320,11 +339,8 @@ inline bool fcc_hit(FcCache *c, uint32_t a, uint32_t b, uint8_t *out) {
 int fcc_query(lx_index *h, uint32_t a, uint32_t b, uint8_t *out) {
     FcCache *c = h->fcc;
     c->st.calls++;
-    if (fcc_hit(c, a, b, out)) {
-        c->st.hits++;
-        return 0;
-    }
     int rc;
+    const auto t_miss = std::chrono::steady_clock::now();
     if (c->inflight) {
         // the last fill may still be writing the entry (the caller returned as
         // soon as its own answer landed): let it finish, then look again
@@ -335,7 +351,8 @@ int fcc_query(lx_index *h, uint32_t a, uint32_t b, uint8_t *out) {
         }
     }
     HIPCHK(h, set_dev(h->device));
-    if ((rc = flush_pending(h))) return rc;   // the fills read rows of events the pending run adds
+    // (the pending run is launched with or before the fill below: the fills read
+    // rows of the events it adds; the slot bookkeeping here is host-only)
     uint32_t sa = c->find(a);
     const bool a_new = sa == LX_NONE;
     if (a_new) sa = c->insert(a, LX_NONE, LX_NONE);
@@ -345,12 +362,29 @@ int fcc_query(lx_index *h, uint32_t a, uint32_t b, uint8_t *out) {
         for (uint64_t e = (uint64_t)b + 1; e < (uint64_t)b + kWindow && e < h->n_events; e++)
             if (c->find((uint32_t)e) == LX_NONE) c->insert((uint32_t)e, sa, sb);
     }
-    if (a_new || a == c->last_a) rc = fcc_row(h, c, a, sa);
-    else rc = fcc_tile(h, c);
+    // a new asking event that is the pending run's only event (Add, then the
+    // caller's first ForklessCause): one launch adds it and fills its row
+    rc = a_new ? flush_add1_row(h, a, c->evk_dev, c->used, c->g7_dev, c->M_dev + (uint64_t)sa * c->W, c->d_rsum) : 1;
+    const bool fused = rc == 0;
+    if (rc == 1) {
+        if ((rc = flush_pending(h))) return rc;
+        if (a_new || a == c->last_a) rc = fcc_row(h, c, a, sa);
+        else rc = fcc_tile(h, c);
+    } else if (!rc) {
+        c->st.row_fills++;
+        c->st.pairs += c->used;
+    }
     if (rc) return rc;
-    HIPCHK(h, hipStreamWriteValue32(h->stream, c->done_dev, ++c->fill_seq, 0));
     c->inflight = true;
+    c->inflight_row = fused;
+    c->inflight_sa = sa;
+    c->inflight_n = c->used;
+    if (!fused) HIPCHK(h, hipEventRecord(c->filled, h->stream));
+    const auto t_wait = std::chrono::steady_clock::now();
     if ((rc = fcc_wait_answer(h, c, sa, sb))) return rc;
+    const auto t_end = std::chrono::steady_clock::now();
+    c->st.miss_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t_end - t_miss).count();
+    c->st.wait_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t_end - t_wait).count();
     const uint8_t m = c->M[(uint64_t)sa * c->W + sb];
     if ((m >> 1) != c->g7[sb]) return h->fail(LX_ERR_STATE, "ForklessCause cache: fill left (%u, %u) unanswered", a, b);
     c->ref[sa] = c->ref[sb] = 1;
@@ -386,6 +420,14 @@ extern "C" {
 
 int lx_forkless_cause(lx_index *h, uint32_t a, uint32_t b, uint8_t *out) {
     if (!h || !out) return LX_ERR_ARG;
+    // hit path first: the cache exists only for whole, non-segmented handles, and
+    // holds only events < n_events (dropped ones are forgotten), so an unknown
+    // event misses here and is reported below
+    if (FcCache *c = h->fcc; c && !h->loading && fcc_hit(c, a, b, out)) {
+        c->st.calls++;
+        c->st.hits++;
+        return 0;
+    }
     if (!h->have_epoch) return h->fail(LX_ERR_STATE, "ForklessCause before lx_reset");
     if (h->loading) return h->fail(LX_ERR_STATE, "index is loading (lx_load_finish first)");
     if (a >= h->n_events || b >= h->n_events)
@@ -394,6 +436,7 @@ int lx_forkless_cause(lx_index *h, uint32_t a, uint32_t b, uint8_t *out) {
     if (!h->fcc) {
         int rc = fcc_make(h);
         if (rc) return rc;
+        if (fcc_hit(h->fcc, a, b, out)) return h->fail(LX_ERR_STATE, "ForklessCause cache: hit in an empty cache");
     }
     return fcc_query(h, a, b, out);
 }

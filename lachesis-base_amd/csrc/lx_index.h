@@ -253,6 +253,8 @@ struct lx_index {
 int lx_fc_args(lx_index *h, uint64_t n, const uint32_t *a, const uint32_t *b, uint8_t *out, uint32_t *partial,
                FcArgs *fa);
 int flush_pending(lx_index *h);                 // launch the pending small-path run (lx_capi.cpp)
+int flush_add1_row(lx_index *h, uint32_t a, const uint32_t *evk_dev, uint32_t n_slots, const uint8_t *tag_dev,
+                   uint8_t *out_dev, uint32_t *psum_dev);   // 1: not applicable
 int rs_begin(lx_index *h, IndexArgs ia, const uint32_t *poff, hipStream_t s);   // lx_rowseg.cpp
 void rs_free(lx_index *h);
 void fcc_destroy(lx_index *h);

@@ -275,6 +275,33 @@ struct SmallArgs {
     uint32_t s_cap;
     uint32_t mask;               // rows may carry fork marks (B > V)
 };
+// One pending event added and its ForklessCause row of the FC cache filled in
+// one launch (lx_small.hip k_add1_row; the unchanged caller's miss path: Add(e)
+// then ForklessCause(e, root) for the roots of a frame).  Fork-free epochs only.
+constexpr uint32_t kAdd1MaxPar = 32;
+struct Add1RowArgs {
+    uint32_t *hb, *la;
+    uint64_t stride;
+    uint32_t a;                  // global index of the event
+    SmallEv e;                   // its record (q0 = {branch, seq, prev, #parents}, ...)
+    uint32_t blen;               // branch_len of its branch afterwards
+    uint32_t B;                  // branches (= validators: no forks)
+    uint32_t w_br;               // weight of its branch
+    uint32_t par[kAdd1MaxPar];   // parents, global indices
+    uint32_t *ev_creator, *ev_seq, *ev_branch, *ev_bbefore, *ev_sp, *first_child, *first_root;
+    uint32_t *branch_len, *brow;
+    const uint32_t *branch_first;
+    uint32_t s_cap;
+    // the row: out[s] = tag[s] << 1 | ForklessCause(a, evk[s]) for s < n_slots
+    const uint32_t *evk;
+    uint32_t n_slots;
+    const uint8_t *tag;
+    uint8_t *out;
+    const uint32_t *wpad;
+    uint32_t quorum;
+    uint32_t *psum;              // [n_slots] x uint64 {column groups, sum}, zero between launches
+};
+
 // Batches whose image fits travel in the kernel arguments (no staging copy)
 constexpr uint32_t kSmallInline = 768;   // words (3 KB; kernel arguments stay < 4 KB)
 struct SmallInlineArgs {
@@ -520,6 +547,7 @@ hipError_t launch_batch_prepare(const BatchArgs &a, void *scan_tmp, size_t scan_
 hipError_t launch_batch_finish(const BatchArgs &a, uint32_t jump_rounds, hipStream_t s);
 hipError_t launch_small(const SmallArgs &a, hipStream_t s);
 hipError_t launch_small_inline(const SmallInlineArgs &a, hipStream_t s);
+hipError_t launch_add1_row(const Add1RowArgs &a, hipStream_t s);
 hipError_t scan_tmp_bytes(uint32_t n, size_t *bytes);
 hipError_t launch_undo_claims(const BatchArgs &a, hipStream_t s);
 hipError_t launch_index(const IndexArgs &a, hipStream_t s);

@@ -277,6 +277,120 @@ __global__ __launch_bounds__(256) void k_small_inline(SmallInlineArgs a) {
     small_body<MASKED>(a.a, a.img);
 }
 
+// ---- k_add1_row: the unchanged caller's FC-cache miss (lx_fccache.cpp) --
+// Add of ONE pending event a and ForklessCause(a, b) for every slot b of the
+// cache, one launch.  Workgroup (cg, sg) owns columns [64 cg, 64 cg + 64) and
+// slots [256 sg, 256 sg + 256):
+//   * wave 0 computes HB(a) on its 64 columns (max over the parents' rows; each
+//     workgroup recomputes it, no communication); the sg == 0 workgroups store it
+//     and do a's LowestAfter range fill, workgroup (0, 0)
+//     writes the metadata and a's own LowestAfter row;
+//   * every thread sums, for one slot b, w_c [0 < LA(b)[c] <= HB(a)[c]] over the
+//     workgroup's columns except c = branch(a) -- the only LowestAfter column
+//     a's Add writes, in other workgroups -- for which it adds w instead when the
+//     column holds branch(b) and a reaches b: in a fork-free epoch LA(b)[br(a)]
+//     is set and <= seq(a) iff a reaches b (vecfc/forkless_cause.go:63-82);
+//   * per slot the partial sums meet in one 64-bit word by atomics: {number of
+//     column groups so far, sum}; the thread whose add completes the count
+//     compares the sum with the quorum, writes the answer and clears the word
+//     (no last-workgroup pass, no fence).
+__global__ __launch_bounds__(256) void k_add1_row(Add1RowArgs a) {
+    __shared__ uint32_t hbv[64], wv[64];
+    const uint32_t t = threadIdx.x, cg = blockIdx.x, sg = blockIdx.y;
+    // this thread's slot: its event and tag live in pinned host memory, so they
+    // are fetched first, under the HB computation
+    const uint32_t s = sg * 256 + t;
+    const bool has = s < a.n_slots;
+    const uint32_t b = has ? a.evk[s] : 0u;
+    const uint32_t tg = has ? a.tag[s] : 0u;
+    const uint32_t c0 = cg * 64;
+    const uint32_t br = a.e.q0.x, seq = a.e.q0.y, prev = a.e.q0.z, np = a.e.q0.w;
+    const uint64_t stride = a.stride;
+    const uint32_t c = c0 + t;
+    const bool valid = t < 64 && c < a.B;
+    uint32_t r = c == br ? seq : 0u, h0 = 0;
+    if (t < 64) {
+        const uint32_t cc = valid ? c : 0u;
+        for (uint32_t p = 0; p < np; p += 8) {
+            uint32_t v[8];
+#pragma unroll
+            for (uint32_t u = 0; u < 8; u++) v[u] = a.hb[(uint64_t)a.par[min(p + u, np - 1)] * stride + cc];
+#pragma unroll
+            for (uint32_t u = 0; u < 8; u++) r = max(r, v[u]);
+        }
+        h0 = prev != LX_NONE ? a.hb[(uint64_t)prev * stride + cc] : 0u;
+        hbv[t] = valid ? r : 0u;
+        wv[t] = valid && c != br ? a.wpad[c] : 0u;
+    } else if (sg == 0 && cg == 0) {
+        const uint32_t u = t - 64;
+        if (u == 0) {
+            const uint32_t g = a.a, sp = a.e.q1.z, creator = a.e.q2.x;
+            a.ev_creator[g] = creator;
+            a.ev_seq[g] = seq;
+            a.ev_branch[g] = br;
+            a.ev_bbefore[g] = a.e.q1.w;
+            a.ev_sp[g] = sp;
+            a.first_child[g] = a.e.q2.z;
+            if (a.e.q2.y & kSmallCont) {
+                if (sp == LX_NONE) a.first_root[creator] = g;
+                else a.first_child[sp] = g;
+            }
+            a.branch_len[br] = a.blen;
+            a.brow[(uint64_t)br * a.s_cap + (seq - a.e.q1.y)] = g;
+        }
+        // a's LowestAfter row: its own branch observes it at its own seq
+        uint4 *row = reinterpret_cast<uint4 *>(a.la + (uint64_t)a.a * stride);
+        for (uint32_t x = u; x < (a.B + 3) / 4; x += 192)
+            row[x] = make_uint4(4 * x == br ? seq : 0u, 4 * x + 1 == br ? seq : 0u, 4 * x + 2 == br ? seq : 0u,
+                                4 * x + 3 == br ? seq : 0u);
+    }
+    __syncthreads();
+    if (has) {
+        uint32_t part = 0;
+        uint32_t bbr = br, bseq = seq;
+        if (b != a.a) {
+            const uint4 *lr = reinterpret_cast<const uint4 *>(a.la + (uint64_t)b * stride + c0);
+            uint4 l[16];
+#pragma unroll
+            for (uint32_t i = 0; i < 16; i++) l[i] = lr[i];
+            bbr = a.ev_branch[b];
+            bseq = a.ev_seq[b];
+#pragma unroll
+            for (uint32_t i = 0; i < 16; i++) {
+                part += (l[i].x - 1u) < hbv[4 * i] ? wv[4 * i] : 0u;
+                part += (l[i].y - 1u) < hbv[4 * i + 1] ? wv[4 * i + 1] : 0u;
+                part += (l[i].z - 1u) < hbv[4 * i + 2] ? wv[4 * i + 2] : 0u;
+                part += (l[i].w - 1u) < hbv[4 * i + 3] ? wv[4 * i + 3] : 0u;
+            }
+        }
+        if (bbr - c0 < 64 && hbv[bbr - c0] >= bseq) part += a.w_br;
+        unsigned long long *w = reinterpret_cast<unsigned long long *>(a.psum) + s;
+        // every read of pinned memory (evk, tag) has returned before the count
+        // moves: once the row's last entry lands, the host may reuse the slots
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned long long old = atomicAdd(w, (1ull << 32) | part);
+        if ((uint32_t)(old >> 32) == gridDim.x - 1) {
+            a.out[s] = (uint8_t)(tg << 1 | ((uint32_t)old + part >= a.quorum ? 1u : 0u));
+            *w = 0;
+        }
+    }
+    // HB(a) out and a's LowestAfter range fill, off the row's critical path
+    if (sg == 0 && valid) {
+        a.hb[(uint64_t)a.a * stride + c] = r;
+        const uint32_t first = a.branch_first[c];
+        // (br, seq) is a itself: its own LowestAfter row is written above
+        const uint32_t hi = c == br ? seq - 1 : r;
+        for (uint32_t x = max(h0 + 1u, first); x <= hi; x++)
+            a.la[(uint64_t)a.brow[(uint64_t)c * a.s_cap + (x - first)] * stride + br] = seq;
+    }
+}
+
+hipError_t launch_add1_row(const Add1RowArgs &a, hipStream_t s) {
+    if (!a.n_slots || !a.B || a.e.q0.w > kAdd1MaxPar) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_add1_row, dim3((a.B + 63) / 64, (a.n_slots + 255) / 256), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
 hipError_t launch_small(const SmallArgs &a, hipStream_t s) {
     if (!a.n || !a.B) return hipSuccess;
     const uint32_t grid = (a.B + kSmallCW - 1) / kSmallCW;
