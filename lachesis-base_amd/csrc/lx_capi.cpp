@@ -1333,6 +1333,16 @@ int add_batch_small(lx_index *h, uint32_t n, const uint32_t *creator, const uint
     h->pend_ev.resize(pn0 + n);
     h->pend_lvl.resize(pn0 + n);
     h->pend_meta.resize(pn0 + n);
+    // the split lists sized for the worst case once, written through raw
+    // pointers, trimmed after the loop (the per-parent push_backs of round 3's
+    // first version cost a capacity check each)
+    const uint64_t npar_b = poff[n] - poff[0];
+    h->pend_pl.resize(pl0 + npar_b + 3ull * n);
+    h->pend_old.resize(old0 + npar_b + n);
+    uint16_t *const plb = h->pend_pl.data();
+    uint2 *const ob = h->pend_old.data();
+    uint32_t *const lvlb = h->pend_lvl.data();
+    size_t npl = pl0, nold = old0;
     for (uint32_t i = 0; i < n; i++) {
         const uint64_t g = bs + i;
         const uint32_t c = creator[i], s = seq[i];
@@ -1365,26 +1375,26 @@ int add_batch_small(lx_index *h, uint32_t n, const uint32_t *creator, const uint
         // level inside the run; parents split into in-run positions (chunks of
         // 4, padded with the event's own position) and older events (k_small)
         const uint32_t pi = pn0 + i;
-        const uint32_t e_pl = (uint32_t)h->pend_pl.size(), e_old = (uint32_t)h->pend_old.size();
+        const uint32_t e_pl = (uint32_t)npl, e_old = (uint32_t)nold;
         uint32_t lvl = 0;
         for (uint64_t x = p0; x < p1; x++) {
             const uint32_t gp = par[x];
             if (gp >= pbs) {
-                lvl = std::max(lvl, h->pend_lvl[gp - pbs] + 1);
-                h->pend_pl.push_back((uint16_t)(gp - pbs));
+                lvl = std::max(lvl, lvlb[gp - pbs] + 1);
+                plb[npl++] = (uint16_t)(gp - pbs);
             } else {
-                h->pend_old.push_back(make_uint2(pi, gp));
+                ob[nold++] = make_uint2(pi, gp);
             }
         }
-        while (h->pend_pl.size() & 3) h->pend_pl.push_back((uint16_t)pi);
-        h->pend_meta[pi] = make_uint2(pi | ((uint32_t)h->pend_pl.size() - e_pl) / 4 << 16, e_pl / 4);
+        while (npl & 3) plb[npl++] = (uint16_t)pi;
+        h->pend_meta[pi] = make_uint2(pi | ((uint32_t)npl - e_pl) / 4 << 16, e_pl / 4);
         const uint32_t prev = (cont && s > 1) ? sp : LX_NONE;
         uint32_t hslot = LX_NONE;
         if (prev != LX_NONE && prev < pbs) {
             hslot = h->pend_nh++;
-            h->pend_old.push_back(make_uint2(0x80000000u | hslot, prev));
+            ob[nold++] = make_uint2(0x80000000u | hslot, prev);
         }
-        h->pend_lvl[pi] = lvl;
+        lvlb[pi] = lvl;
         h->pend_maxlvl = std::max(h->pend_maxlvl, lvl);
         bmax = std::max(bmax, s);
         SmallEv &e = h->pend_ev[pi];
@@ -1394,6 +1404,8 @@ int add_batch_small(lx_index *h, uint32_t n, const uint32_t *creator, const uint
         if (cont && sp != LX_NONE && sp >= pbs) h->pend_ev[sp - pbs].q2.z = (uint32_t)g;
         if (out_branch) out_branch[i] = br;
     }
+    h->pend_pl.resize(npl);
+    h->pend_old.resize(nold);
     // capacity (rare re-layouts sync the stream; the pending run is not on the
     // device yet); on failure the host mirror and the run are rolled back
     h->max_seq = std::max(h->max_seq, bmax);
