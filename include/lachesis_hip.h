@@ -341,6 +341,18 @@ int lx_last_segment_stats(const lx_index *h, lx_seg_stats *out);
  * abft / emitter views need a whole index (LX_ERR_STATE).  Every call has
  * completed on the device when it returns. */
 int lx_rowseg_range(const lx_index *h, uint32_t *lo, uint32_t *hi);
+int lx_rowseg_of(const lx_index *h, uint32_t *rank, uint32_t *count);   /* options seg_rank / seg_count (1: whole) */
+
+/* Row segments over RCCL for callers without a Python host (the Go shim): the
+ * exchanges above (the protocol of lachesis_hip/rowseg.py) issued by the library
+ * on the handle's stream -- ids, rows and LowestAfter triples by grouped
+ * ncclSend / ncclRecv, the termination test by ncclAllReduce -- then
+ * lx_rowseg_finish.  Create the communicator with the handle's seg_rank /
+ * seg_count (an lx_shard_comm; every rank calls collectively, after its
+ * lx_add_batch_dev of the epoch).  stats (optional): rounds of the row
+ * exchange, rows received, LowestAfter triples sent, received. */
+int lx_rowseg_comm_create(lx_index *h, const uint8_t id[128], uint32_t nranks, uint32_t rank, lx_shard_comm **out);
+int lx_rowseg_exchange(lx_shard_comm *c, uint64_t stats[4]);
 int lx_rowseg_bounds(const lx_index *h, uint32_t *lo /* G + 1 */);
 int lx_rowseg_row_words(const lx_index *h, uint32_t *words);
 int lx_rowseg_request_cap(const lx_index *h, uint32_t *cap);

@@ -335,6 +335,13 @@ int lx_rowseg_finish(lx_index *h) {
     return 0;
 }
 
+int lx_rowseg_of(const lx_index *h, uint32_t *rank, uint32_t *count) {
+    if (!h || !rank || !count) return LX_ERR_ARG;
+    *rank = h->rowseg() ? h->rs_rank : 0u;
+    *count = h->rowseg() ? h->rs_count : 1u;
+    return 0;
+}
+
 int lx_rowseg_range(const lx_index *h, uint32_t *lo, uint32_t *hi) {
     if (!h || !lo || !hi) return LX_ERR_ARG;
     if (!h->rowseg() || !h->rs_state) return LX_ERR_STATE;

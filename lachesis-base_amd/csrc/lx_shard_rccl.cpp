@@ -1,4 +1,6 @@
-// Column shards over RCCL for callers without a Python host (the Go shim).
+// Column shards and row segments over RCCL for callers without a Python host
+// (the Go shim).  Row segments: lx_rowseg_exchange at the end of this file,
+// the driver of lx_rowseg_exchange.h over grouped ncclSend / ncclRecv.
 //
 // The multi-GPU protocol of DESIGN.md section 6, written against the public
 // shard ABI (lx_shard_block / lx_shard_wire / lx_la_pack_dev / lx_la_unpack_dev /
@@ -28,6 +30,7 @@
 #include <vector>
 
 #include "lachesis_hip.h"
+#include "lx_rowseg_exchange.h"
 #include "lx_shard_exchange.h"
 
 namespace {
@@ -98,6 +101,10 @@ struct lx_shard_comm {
     uint64_t part_cap = 0;
     uint32_t *wdev = nullptr;                    // wire widths: [0, G) sent, [G, 2G) received
     lx::ExchangeState xs;                        // byte-wire fallbacks remembered per destination
+    bool rowseg = false;                         // a row-segment rank (lx_rowseg_comm_create)
+    uint8_t *rbuf[lx::kRsBufs] = {};             // row-segment exchange buffers, grown on demand
+    size_t rcap[lx::kRsBufs] = {};
+    uint64_t *udev = nullptr;                    // row segments: [0, G) counts sent, [G, 2G) received, [2G] sum
     std::string err;
 
     int fail(int code, const char *fmt, ...) {
@@ -153,21 +160,24 @@ int lx_shard_comm_unique_id(uint8_t id[128]) {
     return 0;
 }
 
-int lx_shard_comm_create(lx_index *h, const uint8_t id[128], uint32_t nranks, uint32_t rank, lx_shard_comm **out) {
+static int comm_create(lx_index *h, const uint8_t id[128], uint32_t nranks, uint32_t rank, bool rowseg,
+                       lx_shard_comm **out) {
     if (!h || !id || !out || rank >= nranks) return create_fail(LX_ERR_ARG, "bad argument");
     *out = nullptr;
     uint32_t srank = 0, scount = 1;
-    if (lx_shard_of(h, &srank, &scount)) return create_fail(LX_ERR_ARG, "bad index handle");
+    if ((rowseg ? lx_rowseg_of(h, &srank, &scount) : lx_shard_of(h, &srank, &scount)))
+        return create_fail(LX_ERR_ARG, "bad index handle");
     if (scount != nranks || srank != rank)
         return create_fail(LX_ERR_ARG, "rank " + std::to_string(rank) + " of " + std::to_string(nranks) +
-                                           " does not match the handle's shard " + std::to_string(srank) + " of " +
-                                           std::to_string(scount));
+                                           " does not match the handle's " + (rowseg ? "row segment " : "shard ") +
+                                           std::to_string(srank) + " of " + std::to_string(scount));
     RcclApi &api = rccl();
     if (!api.ok) return create_fail(LX_ERR_HIP, api.error);
     auto *c = new lx_shard_comm();
     c->ix = h;
     c->rank = rank;
     c->nranks = nranks;
+    c->rowseg = rowseg;
     void *stream = nullptr;
     std::string why;
     int rc = lx_device_planes(h, nullptr, nullptr, nullptr, &stream);
@@ -193,6 +203,14 @@ int lx_shard_comm_create(lx_index *h, const uint8_t id[128], uint32_t nranks, ui
     return 0;
 }
 
+int lx_shard_comm_create(lx_index *h, const uint8_t id[128], uint32_t nranks, uint32_t rank, lx_shard_comm **out) {
+    return comm_create(h, id, nranks, rank, false, out);
+}
+
+int lx_rowseg_comm_create(lx_index *h, const uint8_t id[128], uint32_t nranks, uint32_t rank, lx_shard_comm **out) {
+    return comm_create(h, id, nranks, rank, true, out);
+}
+
 void lx_shard_comm_destroy(lx_shard_comm *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
@@ -202,6 +220,8 @@ void lx_shard_comm_destroy(lx_shard_comm *c) {
     (void)hipFree(c->recv);
     (void)hipFree(c->part);
     (void)hipFree(c->wdev);
+    for (uint8_t *p : c->rbuf) (void)hipFree(p);
+    (void)hipFree(c->udev);
     delete c;
 }
 
@@ -272,6 +292,7 @@ struct RcclNet {
 
 int lx_shard_exchange(lx_shard_comm *c) {
     if (!c) return LX_ERR_ARG;
+    if (c->rowseg) return c->fail(LX_ERR_STATE, "a row-segment communicator (lx_rowseg_exchange)");
     LXC(c->hip(hipSetDevice(c->device), "hipSetDevice"));
     const uint32_t G = c->nranks;
     if (G == 1) return 0;   // an unsharded handle holds whole LowestAfter rows already
@@ -298,6 +319,7 @@ int lx_shard_exchange_layout(uint32_t G, uint32_t self, const uint64_t *entries,
 
 int lx_forkless_cause_sharded_dev(lx_shard_comm *c, uint64_t n, const uint32_t *a, const uint32_t *b, uint8_t *out) {
     if (!c || (n && (!a || !b || !out))) return LX_ERR_ARG;
+    if (c->rowseg) return c->fail(LX_ERR_STATE, "row segments answer ForklessCause through the index");
     if (!n) return 0;
     RcclApi &api = rccl();
     LXC(c->hip(hipSetDevice(c->device), "hipSetDevice"));
@@ -313,6 +335,104 @@ int lx_forkless_cause_sharded_dev(lx_shard_comm *c, uint64_t n, const uint32_t *
     LXC(c->index(lx_forkless_cause_partial_dev(c->ix, n, a, b, c->part, nullptr), "lx_forkless_cause_partial_dev"));
     LXC(c->nccl(api.AllReduce(c->part, c->part, n, ncclUint32, ncclSum, c->comm, c->stream), "ncclAllReduce"));
     LXC(c->index(lx_fc_combine_dev(c->ix, n, c->part, out, nullptr), "lx_fc_combine_dev"));
+    return 0;
+}
+
+// ---- row segments: the driver of lx_rowseg_exchange.h over the rowseg ABI
+struct RcclRowOps {
+    lx_shard_comm *c;
+    int row_words(uint32_t *w) { return c->index(lx_rowseg_row_words(c->ix, w), "lx_rowseg_row_words"); }
+    int request_cap(uint32_t *cap) { return c->index(lx_rowseg_request_cap(c->ix, cap), "lx_rowseg_request_cap"); }
+    int requests(uint32_t *ids, uint32_t cap, uint32_t *counts) {
+        return c->index(lx_rowseg_requests(c->ix, ids, cap, counts), "lx_rowseg_requests");
+    }
+    int serve(uint32_t n, const uint32_t *ids, uint32_t *rows, uint32_t *ready) {
+        return c->index(lx_rowseg_serve(c->ix, n, ids, rows, ready), "lx_rowseg_serve");
+    }
+    int receive(uint32_t n, const uint32_t *ids, const uint32_t *rows, const uint32_t *ready) {
+        return c->index(lx_rowseg_receive(c->ix, n, ids, rows, ready, nullptr), "lx_rowseg_receive");
+    }
+    int la(uint64_t *counts) { return c->index(lx_rowseg_la(c->ix, counts), "lx_rowseg_la"); }
+    int la_fetch(uint32_t *buf) { return c->index(lx_rowseg_la_fetch(c->ix, buf), "lx_rowseg_la_fetch"); }
+    int la_apply(uint64_t n, const uint32_t *buf) { return c->index(lx_rowseg_la_apply(c->ix, n, buf), "lx_rowseg_la_apply"); }
+    int finish() { return c->index(lx_rowseg_finish(c->ix), "lx_rowseg_finish"); }
+    void *buf(int k, size_t bytes) { return c->grow(&c->rbuf[k], &c->rcap[k], bytes) ? nullptr : c->rbuf[k]; }
+};
+
+// the collectives on the handle's stream; the own block moves by a local copy
+struct RcclRowNet {
+    lx_shard_comm *c;
+    RcclNet group_net{c};
+    int sum(uint64_t x, uint64_t *all) {
+        const uint32_t G = c->nranks;
+        LXC(c->hip(hipMemcpyAsync(c->udev + 2 * G, &x, 8, hipMemcpyHostToDevice, c->stream), "hipMemcpyAsync"));
+        LXC(c->nccl(rccl().AllReduce(c->udev + 2 * G, c->udev + 2 * G, 1, ncclUint64, ncclSum, c->comm, c->stream),
+                    "ncclAllReduce"));
+        LXC(c->hip(hipMemcpyAsync(all, c->udev + 2 * G, 8, hipMemcpyDeviceToHost, c->stream), "hipMemcpyAsync"));
+        return c->hip(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
+    }
+    int counts(const uint64_t *send, uint64_t *recv) {
+        RcclApi &api = rccl();
+        const uint32_t G = c->nranks, r = c->rank;
+        LXC(c->hip(hipMemcpyAsync(c->udev, send, 8ull * G, hipMemcpyHostToDevice, c->stream), "hipMemcpyAsync"));
+        LXC(group_net.group([&] {
+            for (uint32_t q = 0; q < G; q++) {
+                if (q == r) continue;
+                LXC(c->nccl(api.Send(c->udev + q, 1, ncclUint64, (int)q, c->comm, c->stream), "ncclSend"));
+                LXC(c->nccl(api.Recv(c->udev + G + q, 1, ncclUint64, (int)q, c->comm, c->stream), "ncclRecv"));
+            }
+            return 0;
+        }));
+        LXC(c->hip(hipMemcpyAsync(recv, c->udev + G, 8ull * G, hipMemcpyDeviceToHost, c->stream), "hipMemcpyAsync"));
+        LXC(c->hip(hipStreamSynchronize(c->stream), "hipStreamSynchronize"));
+        recv[r] = send[r];
+        return 0;
+    }
+    int move(const void *send, const uint64_t *sb, void *recv, const uint64_t *rb) {
+        RcclApi &api = rccl();
+        const uint32_t G = c->nranks, r = c->rank;
+        std::vector<uint64_t> so(G + 1, 0), ro(G + 1, 0);
+        for (uint32_t q = 0; q < G; q++) so[q + 1] = so[q] + sb[q], ro[q + 1] = ro[q] + rb[q];
+        const uint8_t *s = static_cast<const uint8_t *>(send);
+        uint8_t *d = static_cast<uint8_t *>(recv);
+        if (sb[r] != rb[r]) return c->fail(LX_ERR_STATE, "row-segment exchange: own block %llu != %llu bytes",
+                                          (unsigned long long)sb[r], (unsigned long long)rb[r]);
+        if (sb[r])
+            LXC(c->hip(hipMemcpyAsync(d + ro[r], s + so[r], sb[r], hipMemcpyDeviceToDevice, c->stream),
+                       "hipMemcpyAsync"));
+        return group_net.group([&] {
+            for (uint32_t q = 0; q < G; q++) {
+                if (q == r) continue;
+                LXC(c->nccl(api.Send(s + so[q], sb[q], ncclUint8, (int)q, c->comm, c->stream), "ncclSend"));
+                LXC(c->nccl(api.Recv(d + ro[q], rb[q], ncclUint8, (int)q, c->comm, c->stream), "ncclRecv"));
+            }
+            return 0;
+        });
+    }
+};
+
+int lx_rowseg_exchange(lx_shard_comm *c, uint64_t stats[4]) {
+    if (!c) return LX_ERR_ARG;
+    if (!c->rowseg) return c->fail(LX_ERR_STATE, "not a row-segment communicator (lx_rowseg_comm_create)");
+    LXC(c->hip(hipSetDevice(c->device), "hipSetDevice"));
+    const uint32_t G = c->nranks;
+    if (G == 1) return 0;   // a whole index: nothing to join
+    if (!c->udev) LXC(c->hip(hipMalloc(reinterpret_cast<void **>(&c->udev), 8ull * (2 * G + 1)), "hipMalloc"));
+    RcclRowOps ops{c};
+    RcclRowNet net{c};
+    c->err.clear();
+    lx::RowsegExchangeStats st;
+    const int rc = lx::rowseg_exchange_run(ops, net, G, st);
+    if (rc) {
+        if (c->err.empty()) c->fail(rc, "row-segment exchange failed (%d)", rc);
+        return rc;
+    }
+    if (stats) {
+        stats[0] = st.rounds;
+        stats[1] = st.rows_received;
+        stats[2] = st.la_sent;
+        stats[3] = st.la_received;
+    }
     return 0;
 }
 

@@ -22,7 +22,7 @@ There is no CPU fallback: importing this package on a machine without the
 built library raises, and every compute call goes to the GPU.
 """
 
-from .capi import Index, LxError, ShardComm, load_library, shard_comm_unique_id  # noqa: F401
+from .capi import Index, LxError, RowsegComm, ShardComm, load_library, shard_comm_unique_id  # noqa: F401
 from .vecfc import (VecfcIndex, HighestBeforeSeq, LowestAfterSeq, BranchSeq, IndexConfig,  # noqa: F401
                     IndexCacheConfig, Ratio, default_config, lite_config, new_index, new_index_with_engine)
 from . import tools  # noqa: F401

@@ -78,6 +78,9 @@ SIGNATURES = [
     ("lx_shard_comm_destroy", None, [vp]),
     ("lx_shard_comm_last_error", ctypes.c_char_p, [vp]),
     ("lx_shard_exchange", ctypes.c_int, [vp]),
+    ("lx_rowseg_of", ctypes.c_int, [vp, u32p, u32p]),
+    ("lx_rowseg_comm_create", ctypes.c_int, [vp, u8p, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(vp)]),
+    ("lx_rowseg_exchange", ctypes.c_int, [vp, u64p]),
     ("lx_shard_exchange_layout", ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint32, u64p, u32p, u64p]),
     ("lx_forkless_cause_sharded_dev", ctypes.c_int, [vp, ctypes.c_uint64, vp, vp, vp]),
     # include/lachesis_abft.h
@@ -459,6 +462,12 @@ class Index:
         self._chk(self.L.lx_rowseg_range(self.h, ctypes.byref(lo), ctypes.byref(hi)))
         return lo.value, hi.value
 
+    def rowseg_of(self):
+        """(seg_rank, seg_count) of the handle; (0, 1) for a whole index."""
+        r, g = ctypes.c_uint32(), ctypes.c_uint32()
+        self._chk(self.L.lx_rowseg_of(self.h, ctypes.byref(r), ctypes.byref(g)))
+        return r.value, g.value
+
     def rowseg_bounds(self, G):
         b = np.zeros(G + 1, dtype=np.uint32)
         self._chk(self.L.lx_rowseg_bounds(self.h, _p(b, u32p)))
@@ -561,3 +570,28 @@ class ShardComm:
             self.close()
         except Exception:
             pass
+
+
+class RowsegComm(ShardComm):
+    """lx_rowseg_comm_create / lx_rowseg_exchange: the row-segment exchanges
+    issued by the library over RCCL (the Go path; lachesis_hip.rowseg runs the
+    same protocol through torch.distributed).  The index has seg_count =
+    nranks, seg_rank = rank."""
+
+    def __init__(self, index, unique_id, nranks, rank):
+        self.L = index.L
+        self.ix = index
+        self.c = vp()
+        idb = (ctypes.c_uint8 * 128).from_buffer_copy(unique_id)
+        rc = self.L.lx_rowseg_comm_create(index.h, idb, nranks, rank, ctypes.byref(self.c))
+        if rc != 0:
+            raise LxError(rc, "lx_rowseg_comm_create: " + self.L.lx_shard_comm_last_error(None).decode())
+
+    def exchange(self):
+        st = np.zeros(4, dtype=np.uint64)
+        self._chk(self.L.lx_rowseg_exchange(self.c, _p(st, u64p)))
+        return {"row_rounds": int(st[0]), "rows_received": int(st[1]), "la_sent": int(st[2]),
+                "la_received": int(st[3])}
+
+    def forkless_cause_dev(self, n, a_ptr, b_ptr, out_ptr):
+        raise LxError(-1, "row segments answer ForklessCause through the index (own rows)")
