@@ -13,6 +13,24 @@
 
 using namespace lxi;
 
+// Host-time counters of the small Add path (make hprof: build_hprof/, read by
+// lx_host_prof; absent from the default build)
+#ifdef LX_HOST_PROF
+#include <x86intrin.h>
+static uint64_t g_hprof[16];
+#define HP_T(v) const uint64_t v = __rdtsc()
+#define HP_ADD(k, t0) (g_hprof[k] += __rdtsc() - (t0))
+#define HP_CNT(k, x) (g_hprof[k] += (x))
+extern "C" void lx_host_prof(uint64_t out[16], int reset) {
+    memcpy(out, g_hprof, sizeof g_hprof);
+    if (reset) memset(g_hprof, 0, sizeof g_hprof);
+}
+#else
+#define HP_T(v)
+#define HP_ADD(k, t0)
+#define HP_CNT(k, x)
+#endif
+
 // Between lx_load_rows and lx_load_finish the branch table, B, the cheater
 // tables and the branch lengths are not rebuilt yet: every entry point that
 // reads or changes the epoch refuses (the load is finished or reset first).
@@ -1010,7 +1028,7 @@ int hm_sync(lx_index *h) {
     if (h->hm_ok) return 0;
     HIPCHK(h, hipStreamSynchronize(h->stream));
     const uint64_t n = h->n_events, lo = std::min(h->hm_n, n);
-    std::vector<uint32_t> *v[] = {&h->hm_creator, &h->hm_seq, &h->hm_branch, &h->hm_bbefore};
+    rawvec<uint32_t> *v[] = {&h->hm_creator, &h->hm_seq, &h->hm_branch, &h->hm_bbefore};
     const uint32_t *d[] = {h->ev_creator, h->ev_seq, h->ev_branch, h->ev_bbefore};
     for (int k = 0; k < 4; k++) {
         v[k]->resize(n);
@@ -1028,8 +1046,7 @@ int hm_sync(lx_index *h) {
 int stage_slot(lx_index *h, uint64_t words, uint32_t **out, int *slot) {
     const int k = (int)h->st_next;
     h->st_next = (h->st_next + 1) % lx_index::kSlots;
-    if (h->st_used[k]) HIPCHK(h, hipEventSynchronize(h->st_done[k]));
-    h->st_used[k] = false;
+    if (h->st_used[k]) HIPCHK(h, hipEventSynchronize(h->st_copied[k]));
     if (words > h->st_pin_cap[k]) {
         if (h->st_pin[k]) (void)hipHostFree(h->st_pin[k]);
         h->st_pin[k] = nullptr;
@@ -1038,16 +1055,16 @@ int stage_slot(lx_index *h, uint64_t words, uint32_t **out, int *slot) {
         HIPCHK(h, hipHostMalloc((void **)&h->st_pin[k], cap * 4, hipHostMallocDefault));
         h->st_pin_cap[k] = cap;
     }
-    if (words > h->st_dev_cap) {
-        if (h->st_dev) {
-            HIPCHK(h, hipStreamSynchronize(h->stream));
-            (void)hipFree(h->st_dev);
+    if (words > h->st_dev_cap[k]) {
+        if (h->st_dev[k]) {
+            if (h->st_used[k]) HIPCHK(h, hipEventSynchronize(h->st_done[k]));
+            (void)hipFree(h->st_dev[k]);
         }
-        h->st_dev = nullptr;
-        h->st_dev_cap = 0;
+        h->st_dev[k] = nullptr;
+        h->st_dev_cap[k] = 0;
         const uint64_t cap = std::max<uint64_t>(words + words / 2, 16384);
-        HIPCHK(h, dalloc(&h->st_dev, cap));
-        h->st_dev_cap = cap;
+        HIPCHK(h, dalloc(&h->st_dev[k], cap));
+        h->st_dev_cap[k] = cap;
     }
     *out = h->st_pin[k];
     *slot = k;
@@ -1062,6 +1079,7 @@ int stage_slot(lx_index *h, uint64_t words, uint32_t **out, int *slot) {
 // that reads the device state or enqueues after it calls this first.
 int flush_pending(lx_index *h) {
     if (!h->pend_n) return 0;
+    HP_T(f0);
     const uint32_t n = h->pend_n;
     const uint64_t bs = h->pend_bs;
     const uint32_t B0 = h->pend_B0, B = h->B;
@@ -1087,9 +1105,14 @@ int flush_pending(lx_index *h) {
     uint32_t *img;
     int slot = -1, rc;
     const bool inl = words <= kSmallInline;   // small enough for the kernel arguments
+    HP_T(g0);
     if (inl) img = h->sm_inl.img;
     else if ((rc = stage_slot(h, words, &img, &slot))) return rc;
+    HP_ADD(12, g0);
+    HP_T(g1);
     memcpy(img, h->pend_ev.data(), w_ev * 4);
+    HP_ADD(13, g1);
+    HP_T(g2);
     // meta in level order (counting sort; Add order inside a level), level offsets
     uint2 *meta = reinterpret_cast<uint2 *>(img + w_ev);
     uint32_t *ipl = img + w_ev + w_meta;
@@ -1100,6 +1123,8 @@ int flush_pending(lx_index *h) {
     for (uint32_t l = 0; l < L; l++) h->sm_cnt[l + 1] += h->sm_cnt[l];
     for (uint32_t l = 0; l <= L; l++) loff[l] = h->sm_cnt[l];
     for (uint32_t i = 0; i < n; i++) meta[h->sm_cnt[h->pend_lvl[i]]++] = h->pend_meta[i];
+    HP_ADD(14, g2);
+    HP_T(g3);
     if (n_pl) memcpy(ipl, h->pend_pl.data(), n_pl * 2ull);
     if (n_old) memcpy(iold, h->pend_old.data(), n_old * 8ull);
     uint32_t *nfirst = loff + L + 1, *ncreator = nfirst + nf, *blen = ncreator + nf;
@@ -1111,11 +1136,16 @@ int flush_pending(lx_index *h) {
         blen[2 * x] = h->sm_touched[x];
         blen[2 * x + 1] = h->hm_blen[h->sm_touched[x]];
     }
+    HP_ADD(15, g3);
+    HP_ADD(4, f0);
+    HP_T(f1);
     hipStream_t s = h->stream;
     if (!inl) {
-        HIPCHK(h, hipMemcpyAsync(h->st_dev, img, words * 4, hipMemcpyHostToDevice, s));
-        HIPCHK(h, hipEventRecord(h->st_done[slot], s));
-        h->st_used[slot] = true;
+        // device image `slot` is free once the kernel that read it finished
+        if (h->st_used[slot]) HIPCHK(h, hipStreamWaitEvent(h->cstream, h->st_done[slot], 0));
+        HIPCHK(h, hipMemcpyAsync(h->st_dev[slot], img, words * 4, hipMemcpyHostToDevice, h->cstream));
+        HIPCHK(h, hipEventRecord(h->st_copied[slot], h->cstream));
+        HIPCHK(h, hipStreamWaitEvent(s, h->st_copied[slot], 0));
     }
     SmallArgs &a = h->sm_inl.a;
     a = SmallArgs{};
@@ -1126,7 +1156,7 @@ int flush_pending(lx_index *h) {
     a.n = n;
     a.B0 = B0;
     a.B = B;
-    a.img = inl ? nullptr : h->st_dev;
+    a.img = inl ? nullptr : h->st_dev[slot];
     a.o_meta = (uint32_t)w_ev;
     a.o_pl = (uint32_t)(w_ev + w_meta);
     a.o_old = (uint32_t)(w_ev + w_meta + w_pl);
@@ -1154,6 +1184,10 @@ int flush_pending(lx_index *h) {
     a.mask = B > h->V ? 1u : 0u;
     if (h->small_timing) HIPCHK(h, hipEventRecord(h->ev[1], s));
     HIPCHK(h, inl ? lx::launch_small_inline(h->sm_inl, s) : lx::launch_small(a, s));
+    if (!inl) {
+        HIPCHK(h, hipEventRecord(h->st_done[slot], s));
+        h->st_used[slot] = true;
+    }
     if (h->small_timing) HIPCHK(h, hipEventRecord(h->ev[2], s));
     if (B > h->V && h->n_cheat) {
         MarkArgs m{};
@@ -1174,6 +1208,8 @@ int flush_pending(lx_index *h) {
     h->stats = lx_stats{};
     h->stats.index_launches = 1;
     h->stats_lazy = h->small_timing;
+    HP_ADD(5, f1);
+    HP_CNT(9, 1);
     return 0;
 }
 
@@ -1269,42 +1305,19 @@ int add_batch_small(lx_index *h, uint32_t n, const uint32_t *creator, const uint
         HIPCHK(h, set_dev(h->device));
         if ((rc = hm_sync(h))) return rc;
     }
+    HP_T(a0);
     const uint64_t bs = h->n_events;
-    for (uint32_t i = 0; i < n; i++) {
-        const uint64_t g = bs + i;
-        const uint32_t c = creator[i], s = seq[i];
-        const uint64_t p0 = poff[i], p1 = poff[i + 1];
-        if (p1 < p0) return h->fail(LX_ERR_ARG, "parent offsets not monotone");
-        int code = 0;
-        if (c >= h->V) {
-            code = LX_ERR_ARG;
-        } else if (s == 0 || s >= 0x7FFFFFFEu) {
-            code = LX_ERR_EVENT;
-        } else {
-            for (uint64_t x = p0; x < p1; x++)
-                if (par[x] >= g) { code = LX_ERR_ORDER; break; }
-            if (!code && s > 1) {
-                if (p1 == p0) {
-                    code = LX_ERR_EVENT;
-                } else {
-                    const uint32_t sp = par[p0];
-                    const uint32_t cs = sp < bs ? h->hm_creator[sp] : creator[sp - bs];
-                    const uint32_t ss = sp < bs ? h->hm_seq[sp] : seq[sp - bs];
-                    if (cs != c || ss + 1 != s) code = LX_ERR_EVENT;
-                }
-            }
-        }
-        if (code) {
-            if (err_index) *err_index = i;
-            if (code == LX_ERR_ORDER) return h->fail(code, "event %u: processed out of order, parent not found", i);
-            if (code == LX_ERR_ARG) return h->fail(code, "event %u: creator idx out of range", i);
-            return h->fail(code, "event %u: violates seq/self-parent invariants (eventcheck)", i);
-        }
-    }
+    // events [0, m) have monotone parent offsets (the error at m, if any, is
+    // reported after those before it, in Add order)
+    uint32_t m = 0;
+    while (m < n && poff[m + 1] >= poff[m]) m++;
+    const uint64_t npar_b = poff[m] - poff[0];
+    HP_ADD(0, a0);
     // the run launches before it would outgrow one k_small (LDS, small_fits)
-    if (h->pend_n && !small_fits(h, h->pend_n + n, h->pend_npar + (poff[n] - poff[0])) &&
+    if (h->pend_n && !small_fits(h, h->pend_n + n, h->pend_npar + npar_b) &&
         ((rc = h->hip(set_dev(h->device), "set device")) || (rc = flush_pending(h))))
         return rc;
+    HP_T(a1);
     if (!h->pend_n) {
         h->pend_bs = bs;
         h->pend_B0 = h->B;
@@ -1318,7 +1331,7 @@ int add_batch_small(lx_index *h, uint32_t n, const uint32_t *creator, const uint
         h->pend_nh = 0;
     }
     const uint64_t pbs = h->pend_bs;
-    const uint32_t B0 = h->B, pn0 = h->pend_n, nh0 = h->pend_nh;
+    const uint32_t B0 = h->B, pn0 = h->pend_n, nh0 = h->pend_nh, maxlvl0 = h->pend_maxlvl;
     const size_t pl0 = h->pend_pl.size(), old0 = h->pend_old.size();
     uint32_t B = B0, bmax = 0;
     if (h->hm_creator.capacity() < bs + n) {
@@ -1333,29 +1346,67 @@ int add_batch_small(lx_index *h, uint32_t n, const uint32_t *creator, const uint
     h->pend_ev.resize(pn0 + n);
     h->pend_lvl.resize(pn0 + n);
     h->pend_meta.resize(pn0 + n);
+    h->sm_undo.resize(n);
     // the split lists sized for the worst case once, written through raw
     // pointers, trimmed after the loop (the per-parent push_backs of round 3's
     // first version cost a capacity check each)
-    const uint64_t npar_b = poff[n] - poff[0];
     h->pend_pl.resize(pl0 + npar_b + 3ull * n);
     h->pend_old.resize(old0 + npar_b + n);
     uint16_t *const plb = h->pend_pl.data();
     uint2 *const ob = h->pend_old.data();
     uint32_t *const lvlb = h->pend_lvl.data();
+    uint2 *const metab = h->pend_meta.data();
+    SmallEv *const evb = h->pend_ev.data();
+    uint32_t *const mc = h->hm_creator.data(), *const ms = h->hm_seq.data(), *const mb = h->hm_branch.data(),
+                   *const mbb = h->hm_bbefore.data();
+    uint2 *const undo = h->sm_undo.data();   // {branch, length before} per event, for a rollback
+    uint32_t *blen = h->hm_blen.data(), *bfirst = h->h_branch_first.data();
+    const uint32_t V = h->V;
     size_t npl = pl0, nold = old0;
+    uint32_t maxlvl = maxlvl0, nh = nh0;
+    int code = 0;
+    bool nonmono = false;
+    uint32_t bad = 0;
+    HP_ADD(1, a1);
+    HP_T(a2);
+    // validation (the checks and error codes of k_validate_claim), branch
+    // assignment and the parent split in one pass; an error rolls the batch
+    // back below (nothing of it was enqueued)
     for (uint32_t i = 0; i < n; i++) {
         const uint64_t g = bs + i;
         const uint32_t c = creator[i], s = seq[i];
+        if (i == m) { nonmono = true; bad = i; break; }
         const uint64_t p0 = poff[i], p1 = poff[i + 1];
-        const uint32_t sp = s > 1 ? par[p0] : LX_NONE;
+        if (c >= V) { code = LX_ERR_ARG; bad = i; break; }
+        if (s == 0 || s >= 0x7FFFFFFEu) { code = LX_ERR_EVENT; bad = i; break; }
+        // level inside the run; parents split into in-run positions (chunks of
+        // 4, padded with the event's own position) and older events (k_small)
+        const uint32_t pi = pn0 + i;
+        const uint32_t e_pl = (uint32_t)npl, e_old = (uint32_t)nold;
+        uint32_t lvl = 0;
+        for (uint64_t x = p0; x < p1; x++) {
+            const uint32_t gp = par[x];
+            if (gp >= g) { code = LX_ERR_ORDER; break; }
+            if (gp >= pbs) {
+                lvl = std::max(lvl, lvlb[gp - pbs] + 1);
+                plb[npl++] = (uint16_t)(gp - pbs);
+            } else {
+                ob[nold++] = make_uint2(pi, gp);
+            }
+        }
+        if (code) { bad = i; break; }
+        const uint32_t sp = s > 1 ? (p1 > p0 ? par[p0] : LX_NONE) : LX_NONE;
         uint32_t br = 0;
         bool cont = false;
         if (s > 1) {
-            const uint32_t bsp = h->hm_branch[sp];
-            const uint32_t len = h->hm_blen[bsp];
-            const uint32_t last = len ? h->h_branch_first[bsp] + len - 1 : 0;
+            // eventcheck: a self-parent of the same creator with seq - 1 (in the
+            // mirror already, this batch's earlier events included)
+            if (sp == LX_NONE || mc[sp] != c || ms[sp] + 1 != s) { code = LX_ERR_EVENT; bad = i; break; }
+            const uint32_t bsp = mb[sp];
+            const uint32_t len = blen[bsp];
+            const uint32_t last = len ? bfirst[bsp] + len - 1 : 0;
             if (last + 1 == s) { br = bsp; cont = true; }
-        } else if (h->hm_blen[c] == 0) {
+        } else if (blen[c] == 0) {
             br = c;
             cont = true;
         }
@@ -1366,46 +1417,67 @@ int add_batch_small(lx_index *h, uint32_t n, const uint32_t *creator, const uint
             h->h_branch_creator.push_back(c);
             h->by_creator[c].push_back(br);
             h->hm_blen.push_back(0);
+            blen = h->hm_blen.data();
+            bfirst = h->h_branch_first.data();
         }
-        h->hm_blen[br] = s - h->h_branch_first[br] + 1;
-        h->hm_creator[g] = c;
-        h->hm_seq[g] = s;
-        h->hm_branch[g] = br;
-        h->hm_bbefore[g] = bb;
-        // level inside the run; parents split into in-run positions (chunks of
-        // 4, padded with the event's own position) and older events (k_small)
-        const uint32_t pi = pn0 + i;
-        const uint32_t e_pl = (uint32_t)npl, e_old = (uint32_t)nold;
-        uint32_t lvl = 0;
-        for (uint64_t x = p0; x < p1; x++) {
-            const uint32_t gp = par[x];
-            if (gp >= pbs) {
-                lvl = std::max(lvl, lvlb[gp - pbs] + 1);
-                plb[npl++] = (uint16_t)(gp - pbs);
-            } else {
-                ob[nold++] = make_uint2(pi, gp);
-            }
-        }
+        undo[i] = make_uint2(br, blen[br]);
+        blen[br] = s - bfirst[br] + 1;
+        mc[g] = c;
+        ms[g] = s;
+        mb[g] = br;
+        mbb[g] = bb;
         while (npl & 3) plb[npl++] = (uint16_t)pi;
-        h->pend_meta[pi] = make_uint2(pi | ((uint32_t)npl - e_pl) / 4 << 16, e_pl / 4);
+        metab[pi] = make_uint2(pi | ((uint32_t)npl - e_pl) / 4 << 16, e_pl / 4);
         const uint32_t prev = (cont && s > 1) ? sp : LX_NONE;
         uint32_t hslot = LX_NONE;
         if (prev != LX_NONE && prev < pbs) {
-            hslot = h->pend_nh++;
+            hslot = nh++;
             ob[nold++] = make_uint2(0x80000000u | hslot, prev);
         }
         lvlb[pi] = lvl;
-        h->pend_maxlvl = std::max(h->pend_maxlvl, lvl);
+        maxlvl = std::max(maxlvl, lvl);
         bmax = std::max(bmax, s);
-        SmallEv &e = h->pend_ev[pi];
+        SmallEv &e = evb[pi];
         e.q0 = make_uint4(br, s, prev, (uint32_t)(p1 - p0));
-        e.q1 = make_uint4(e_old, h->h_branch_first[br], sp, bb);
+        e.q1 = make_uint4(e_old, bfirst[br], sp, bb);
         e.q2 = make_uint4(c, cont ? kSmallCont : 0u, LX_NONE, hslot);
-        if (cont && sp != LX_NONE && sp >= pbs) h->pend_ev[sp - pbs].q2.z = (uint32_t)g;
+        if (cont && sp != LX_NONE && sp >= pbs) evb[sp - pbs].q2.z = (uint32_t)g;
         if (out_branch) out_branch[i] = br;
+    }
+    HP_ADD(2, a2);
+    HP_T(a3);
+    // the batch rolled back: the host mirror as before it, the run without it
+    auto rollback = [&](uint32_t done) {
+        for (uint32_t i = done; i-- > 0;)
+            if (undo[i].x < B0) h->hm_blen[undo[i].x] = undo[i].y;
+        h->hm_blen.resize(B0);
+        h->h_branch_first.resize(B0);
+        h->h_branch_creator.resize(B0);
+        for (auto &l : h->by_creator)
+            while (!l.empty() && l.back() >= B0) l.pop_back();
+        for (auto *v : {&h->hm_creator, &h->hm_seq, &h->hm_branch, &h->hm_bbefore}) v->resize(bs);
+        h->pend_ev.resize(pn0);
+        h->pend_lvl.resize(pn0);
+        h->pend_meta.resize(pn0);
+        h->pend_pl.resize(pl0);
+        h->pend_old.resize(old0);
+        h->pend_nh = nh0;
+        h->pend_maxlvl = maxlvl0;
+        for (uint32_t i = 0; i < pn0; i++)
+            if (h->pend_ev[i].q2.z != LX_NONE && h->pend_ev[i].q2.z >= bs) h->pend_ev[i].q2.z = LX_NONE;
+    };
+    if (code || nonmono) {
+        rollback(bad);
+        if (err_index) *err_index = bad;
+        if (nonmono) return h->fail(LX_ERR_ARG, "parent offsets not monotone");
+        if (code == LX_ERR_ORDER) return h->fail(code, "event %u: processed out of order, parent not found", bad);
+        if (code == LX_ERR_ARG) return h->fail(code, "event %u: creator idx out of range", bad);
+        return h->fail(code, "event %u: violates seq/self-parent invariants (eventcheck)", bad);
     }
     h->pend_pl.resize(npl);
     h->pend_old.resize(nold);
+    h->pend_nh = nh;
+    h->pend_maxlvl = maxlvl;
     // capacity (rare re-layouts sync the stream; the pending run is not on the
     // device yet); on failure the host mirror and the run are rolled back
     h->max_seq = std::max(h->max_seq, bmax);
@@ -1413,20 +1485,7 @@ int add_batch_small(lx_index *h, uint32_t n, const uint32_t *creator, const uint
     if (grows || B != B0 || h->ncols == 0 || h->pend_n + n >= kPendLaunch)
         if ((rc = h->hip(set_dev(h->device), "set device"))) return rc;
     if ((rc = grow_events(h, bs + n)) || (rc = grow_branches(h, B)) || (rc = grow_scap(h, h->max_seq))) {
-        h->h_branch_first.resize(B0);
-        h->h_branch_creator.resize(B0);
-        for (auto &l : h->by_creator)
-            while (!l.empty() && l.back() >= B0) l.pop_back();
-        h->hm_ok = false;
-        h->hm_n = std::min<uint64_t>(h->hm_n, bs);
-        h->pend_ev.resize(pn0);
-        h->pend_lvl.resize(pn0);
-        h->pend_meta.resize(pn0);
-        h->pend_pl.resize(pl0);
-        h->pend_old.resize(old0);
-        h->pend_nh = nh0;
-        for (uint32_t i = 0; i < pn0; i++)
-            if (h->pend_ev[i].q2.z != LX_NONE && h->pend_ev[i].q2.z >= bs) h->pend_ev[i].q2.z = LX_NONE;
+        rollback(n);
         return rc;
     }
     h->wb_ready = false;
@@ -1440,6 +1499,7 @@ int add_batch_small(lx_index *h, uint32_t n, const uint32_t *creator, const uint
     h->last_npar = poff[n] - poff[0];
     h->pend_npar += poff[n] - poff[0];
     h->pend_n = pn0 + n;
+    HP_ADD(3, a3);
     if (h->pend_n >= kPendLaunch) return flush_pending(h);
     return 0;
 }
@@ -1474,11 +1534,16 @@ int lx_create(const lx_config *cfg, lx_index **out) {
             delete h;
             return LX_ERR_HIP;
         }
-    for (auto &e : h->st_done)
-        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
-            delete h;
-            return LX_ERR_HIP;
-        }
+    for (auto *ev : {h->st_done, h->st_copied})
+        for (int k = 0; k < lx_index::kSlots; k++)
+            if (hipEventCreateWithFlags(&ev[k], hipEventDisableTiming) != hipSuccess) {
+                delete h;
+                return LX_ERR_HIP;
+            }
+    if (hipStreamCreateWithFlags(&h->cstream, hipStreamNonBlocking) != hipSuccess) {
+        delete h;
+        return LX_ERR_HIP;
+    }
     *out = h;
     return 0;
 }
@@ -1492,12 +1557,16 @@ void lx_destroy(lx_index *h) {
     if (h->status) (void)hipFree(h->status);
     for (auto &e : h->ev)
         if (e) (void)hipEventDestroy(e);
-    for (auto &e : h->st_done)
-        if (e) (void)hipEventDestroy(e);
+    if (h->cstream) (void)hipStreamSynchronize(h->cstream);
+    for (auto *ev : {h->st_done, h->st_copied})
+        for (int k = 0; k < lx_index::kSlots; k++)
+            if (ev[k]) (void)hipEventDestroy(ev[k]);
     for (auto &e : h->seg_ev) (void)hipEventDestroy(e);
     for (auto *p : h->st_pin)
         if (p) (void)hipHostFree(p);
-    if (h->st_dev) (void)hipFree(h->st_dev);
+    for (auto *p : h->st_dev)
+        if (p) (void)hipFree(p);
+    if (h->cstream) (void)hipStreamDestroy(h->cstream);
     if (h->qp) (void)hipHostFree(h->qp);
     if (h->ld_buf) (void)hipFree(h->ld_buf);
     if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -1666,6 +1735,7 @@ int lx_reset(lx_index *h, uint32_t nv, const uint32_t *w) {
 int lx_add_batch(lx_index *h, uint32_t n, const uint32_t *creator, const uint32_t *seq, const uint64_t *poff,
                  const uint32_t *par, uint32_t *out_branch, uint32_t *err_index) {
     if (!h) return LX_ERR_ARG;
+    HP_T(e0);
     if (n == 0) return 0;
     if (!creator || !seq || !poff) return h->fail(LX_ERR_ARG, "null input");
     uint64_t base = poff[0], npar = poff[n] - poff[0];
@@ -1673,8 +1743,13 @@ int lx_add_batch(lx_index *h, uint32_t n, const uint32_t *creator, const uint32_
     if (h->loading) return h->fail(LX_ERR_STATE, "lx_add_batch during a load (lx_load_finish first)");
     // the small path makes no HIP call unless it launches or grows (it sets the device then)
     if (h->have_epoch && !h->sharded() && !h->rowseg() && n <= std::min(h->small_max, kSmallMaxN) &&
-        small_fits(h, n, npar))
-        return add_batch_small(h, n, creator, seq, poff, par, out_branch, err_index);
+        small_fits(h, n, npar)) {
+        const int rs = add_batch_small(h, n, creator, seq, poff, par, out_branch, err_index);
+        HP_ADD(6, e0);
+        HP_CNT(10, n);
+        HP_CNT(11, 1);
+        return rs;
+    }
     HIPCHK(h, set_dev(h->device));
     std::vector<uint32_t> off(n + 1);
     for (uint32_t i = 0; i <= n; i++) {

@@ -29,6 +29,30 @@ hipError_t dalloc(T **p, uint64_t n) {
 
 inline uint32_t round_up(uint32_t x, uint32_t m) { return (x + m - 1) / m * m; }
 
+// std::vector whose resize leaves new elements default-initialised (no zero
+// fill): the small Add path sizes its lists for the worst case per batch and
+// writes every element it keeps
+template <class T>
+struct NoInitAlloc : std::allocator<T> {
+    NoInitAlloc() = default;
+    template <class U>
+    NoInitAlloc(const NoInitAlloc<U> &) noexcept {}
+    template <class U>
+    struct rebind {
+        using other = NoInitAlloc<U>;
+    };
+    template <class U>
+    void construct(U *p) noexcept {
+        ::new (static_cast<void *>(p)) U;
+    }
+    template <class U, class... A>
+    void construct(U *p, A &&...a) {
+        ::new (static_cast<void *>(p)) U(std::forward<A>(a)...);
+    }
+};
+template <class T>
+using rawvec = std::vector<T, NoInitAlloc<T>>;
+
 // device scratch grown to `need` elements (contents not kept)
 template <typename H, typename T>
 int grow_scratch(H *h, T **p, uint64_t *cap, uint64_t need) {
@@ -157,31 +181,38 @@ struct lx_index {
     uint32_t small_max = kSmallMaxN;       // option small_max: largest batch on this path (0: never)
     bool hm_ok = false;                    // the mirror equals the device metadata
     uint64_t hm_n = 0;                     // events whose (immutable) metadata the mirror holds
-    std::vector<uint32_t> hm_creator, hm_seq, hm_branch, hm_bbefore;
+    lxi::rawvec<uint32_t> hm_creator, hm_seq, hm_branch, hm_bbefore;
     std::vector<uint32_t> hm_blen;         // per branch: events on it (= device branch_len)
     std::vector<uint32_t> sm_level, sm_cnt, sm_touched;   // scratch
+    lxi::rawvec<uint2> sm_undo;            // add_batch_small: {branch, length before} per event
     // the pending run: small-path events assigned on the host but not launched
     // yet, [pend_bs, pend_bs + pend_n), branches from pend_B0 (flush_pending)
     uint32_t pend_n = 0, pend_B0 = 0, pend_maxlvl = 0;
     uint64_t pend_bs = 0;
-    std::vector<SmallEv> pend_ev;          // records (q1.x = offset into pend_old, q2.w = h0 slot)
-    std::vector<uint32_t> pend_lvl;        // topological level inside the run
-    std::vector<uint2> pend_meta;          // per event {position | chunks << 16, chunk offset into pend_pl}
-    std::vector<uint16_t> pend_pl;         // in-run parents (run positions), chunks of 4 (k_small)
-    std::vector<uint2> pend_old;           // {target, global event}: parents older than the run, older prevs
+    lxi::rawvec<SmallEv> pend_ev;          // records (q1.x = offset into pend_old, q2.w = h0 slot)
+    lxi::rawvec<uint32_t> pend_lvl;        // topological level inside the run
+    lxi::rawvec<uint2> pend_meta;          // per event {position | chunks << 16, chunk offset into pend_pl}
+    lxi::rawvec<uint16_t> pend_pl;         // in-run parents (run positions), chunks of 4 (k_small)
+    lxi::rawvec<uint2> pend_old;           // {target, global event}: parents older than the run, older prevs
     uint64_t pend_npar = 0;                // parents of the run (LDS budget, small_fits)
     uint32_t pend_nh = 0;                  // h0 slots of the run
     std::vector<uint32_t> touch_mark;      // per branch: stamp of the last run that touched it
     uint32_t touch_stamp = 0;
-    static constexpr int kSlots = 4;       // pinned staging images in flight
+    // staging images in flight: slot k = a pinned image and its device copy.
+    // The H2D copy runs on cstream, so the copy of run k + 1 overlaps the
+    // kernel of run k (on one stream it waited for that kernel, and the copy
+    // engine's hand-off to the compute queue sat between every two runs)
+    static constexpr int kSlots = 4;
     uint32_t *st_pin[kSlots] = {};
     uint64_t st_pin_cap[kSlots] = {};
-    hipEvent_t st_done[kSlots] = {};       // the H2D copy of slot k has read it
+    hipEvent_t st_copied[kSlots] = {};     // cstream: the H2D copy of slot k finished (pinned image free)
+    hipEvent_t st_done[kSlots] = {};       // stream: the kernel that read device image k finished
     bool st_used[kSlots] = {};
     uint32_t st_next = 0;
-    uint32_t *st_dev = nullptr;            // device image (stream order serialises its reuse)
+    uint32_t *st_dev[kSlots] = {};
+    uint64_t st_dev_cap[kSlots] = {};
+    hipStream_t cstream = nullptr;
     SmallInlineArgs sm_inl{};              // arguments of the last launch; images of <= kSmallInline words inline
-    uint64_t st_dev_cap = 0;
     // restart from the persisted tables (lx_load_rows / lx_load_finish)
     bool loading = false;
     std::vector<uint32_t> ld_first, ld_last, ld_count, ld_creator, ld_tail;   // per branch, as loaded

@@ -189,16 +189,19 @@ def test_level_fed_config3_prefix(lx):
     ix.close()
 
 
-@pytest.mark.parametrize("case", ["creator", "seq0", "selfparent", "order"])
+@pytest.mark.parametrize("case", ["creator", "seq0", "selfparent", "order", "offsets"])
 def test_small_path_errors(lx, case):
     """Errors of the small path: code, offending batch position, state unchanged
-    (the checks of k_validate_claim; vecengine/index.go:159-161, eventcheck)."""
+    (the checks of k_validate_claim; vecengine/index.go:159-161, eventcheck).
+    The events before the offending one were assigned (new fork branches
+    among them) and are rolled back: the re-added batch must index as if the
+    failed one never happened."""
     d = lx.tools.gen_dag(4, 10, 3, cheaters=1, forks=2, seed=3)
     w = [1, 1, 1, 1]
     ix = lx.Index()
     ix.reset(w)
     ix.add_batch(d.creator[:20], d.seq[:20], d.poff[:21], d.par)
-    cr, sq, par = d.creator.copy(), d.seq.copy(), d.par.copy()
+    cr, sq, par, poff = d.creator.copy(), d.seq.copy(), d.par.copy(), d.poff.copy()
     bad = 24
     if case == "creator":
         cr[bad] = 9
@@ -209,11 +212,14 @@ def test_small_path_errors(lx, case):
     elif case == "selfparent":
         sq[bad] += 1
         code = -3
-    else:
+    elif case == "order":
         par[d.poff[bad]] = bad + 3
         code = -2
+    else:
+        poff[bad + 1] = poff[bad] - 1
+        code = -1
     with pytest.raises(lx.LxError) as ei:
-        ix.add_batch(cr[20:], sq[20:], d.poff[20:], par)
+        ix.add_batch(cr[20:], sq[20:], poff[20:], par)
     assert ei.value.code == code and ei.value.index == bad - 20
     assert ix.num_events() == 20
     ix.add_batch(d.creator[20:], d.seq[20:], d.poff[20:], d.par)
