@@ -642,6 +642,26 @@ int add_batch_dev(lx_index *h, uint32_t n, const uint32_t *creator, const uint32
         if ((rc = rs_begin(h, ia, poff, s))) return rc;
     } else if (h->segments > 1 && !h->sharded() && n >= 64ull * h->segments) {
         if ((rc = seg_walk(h, ia, poff, s))) return rc;
+    } else if (h->dbl && !ia.mask && !h->sharded() && h->B <= kDblMaxB && n >= 16ull * h->B && n <= 0xFFFFu &&
+               dbl_lds_bytes(n, h->B) <= kDblLds) {
+        // few branches, no forks: HB by frontier doubling in one workgroup
+        // (the walker's time is levels x pass, and such epochs are deep chains)
+        DblArgs da{};
+        da.hb = h->hb;
+        da.la = h->la;
+        da.stride = h->pstride;
+        da.bs = (uint32_t)h->n_events;
+        da.n = n;
+        da.B = h->B;
+        da.rec = h->b_rec;
+        da.par = par;
+        da.poff = poff;
+        da.ev_branch = h->ev_branch;
+        da.ev_seq = h->ev_seq;
+        da.branch_first = h->branch_first;
+        da.brow = h->brow;
+        da.s_cap = h->s_cap;
+        HIPCHK(h, lx::launch_dbl(da, s));
     } else {
         HIPCHK(h, lx::launch_index(ia, s));
     }
@@ -1588,6 +1608,8 @@ int lx_set_option(lx_index *h, const char *name, int64_t value) {
         h->cpw_hint = (uint32_t)value;
     } else if (k == "pack16") {
         h->pack16 = value != 0;
+    } else if (k == "dbl") {
+        h->dbl = value != 0;
     } else if (k == "la_memset") {
         if (h->have_epoch) return h->fail(LX_ERR_STATE, "la_memset must be set before lx_reset");
         h->la_tail = value == 0;

@@ -131,6 +131,7 @@ struct lx_index {
     uint32_t *fk_w = nullptr, *fk_c = nullptr, *fk_wch = nullptr;
     uint64_t fk_cap = 0;
     uint32_t fk_hi4 = 0;
+    bool dbl = true;                       // option dbl=0: the column walker for small fork-free batches too
     bool fc_fk = true;                     // option fc_fk=0: the fix-up loop kernel instead
     // column shard (shard_count > 1): own columns only (lx_internal.h)
     std::vector<uint32_t> h_cmap;          // global branch -> plane column / LX_NONE

@@ -71,6 +71,29 @@ struct IndexArgs {
     uint32_t *seg_list;          // partial events (global index), appended
     uint32_t *seg_count;
 };
+// k_dbl (lx_dbl.hip): HighestBefore by frontier doubling in one workgroup's
+// LDS, for fork-free batches with few branches
+struct DblArgs {
+    uint32_t *hb;
+    uint32_t *la;
+    uint64_t stride;
+    uint32_t bs;                 // first event of the batch
+    uint32_t n;
+    uint32_t B;                  // branches (= validators: no forks)
+    const EventRec *rec;
+    const uint32_t *par;         // batch parent array (global indices), batch-local offsets
+    const uint32_t *poff;
+    const uint32_t *ev_branch;
+    const uint32_t *ev_seq;
+    const uint32_t *branch_first;
+    const uint32_t *brow;
+    uint32_t s_cap;
+};
+constexpr uint32_t kDblLds = 160 * 1024 - 256;
+constexpr uint32_t kDblMaxB = 16;
+__host__ __device__ inline uint64_t dbl_lds_bytes(uint64_t n, uint64_t B) {
+    return 4 * (n * B + 3 * B + 3) + 2 * ((n + 1) & ~1ull);
+}
 constexpr int kProfSlots = 16;   // see k_index: passes, spin misses, chunk folds, completes, ...
 constexpr int kProfWaves = 16;   // waves per workgroup in the counter layout
 constexpr int kProfBlocks = 4096;
@@ -551,6 +574,7 @@ hipError_t launch_add1_row(const Add1RowArgs &a, hipStream_t s);
 hipError_t scan_tmp_bytes(uint32_t n, size_t *bytes);
 hipError_t launch_undo_claims(const BatchArgs &a, hipStream_t s);
 hipError_t launch_index(const IndexArgs &a, hipStream_t s);
+hipError_t launch_dbl(const DblArgs &a, hipStream_t s);
 hipError_t launch_marks(const MarkArgs &a, hipStream_t s);
 hipError_t launch_fc(const FcArgs &a, uint32_t cols, bool forks, hipStream_t s);
 hipError_t launch_fc_combine(const uint32_t *sum, uint8_t *out, uint64_t n, uint32_t quorum, hipStream_t s);
