@@ -69,6 +69,8 @@ const char *lx_last_error(const lx_index *h);
  *   "fc_fk"      0: ForklessCause on fork DAGs by the fix-up loop instead of the cheater-mask kernel
  *   "cpw"        walker columns per workgroup: 0 (auto), 1, 2 or 4
  *   "pack16"     0: two slot units per event even when every seq fits 16 bits
+ *   "dbl"        0: the column walker also for fork-free batches of <= 16 branches
+ *                (default: HighestBefore by frontier doubling in one workgroup, lx_dbl.hip)
  *   "la_memset"  1: zero the whole LowestAfter plane at lx_reset instead of the tail pass (before lx_reset)
  *   "shard_wire" LowestAfter exchange width: 0 (auto), 2 or 4 bytes
  *   "timing"     1: HIP-event timing of latency-path launches (lx_last_stats)
