@@ -452,8 +452,29 @@ BatchArgs batch_args(lx_index *h, uint32_t n, const uint32_t *creator, const uin
 // rows gathered, LowestAfter filled from the final rows (lx_segment.hip,
 // DESIGN.md section 6b).  `ia` is the batch's ordinary walk; timings into
 // seg_stats.
-int seg_walk(lx_index *h, IndexArgs ia, const uint32_t *poff, hipStream_t s) {
-    const uint32_t G = h->segments, n = ia.n, bs = ia.batch_start;
+// Workgroups of one walk of the batch's columns (launch_index's slice choice,
+// rounded to the 8 XCDs)
+uint32_t walk_grid(const lx_index *h) {
+    const uint32_t nc = h->ncols, cpw = h->cpw_hint ? h->cpw_hint : (nc <= 256 ? 1 : nc <= 512 ? 2 : 4);
+    const uint32_t slices = (nc + cpw - 1) / cpw;
+    return (slices + 7) / 8 * 8;
+}
+
+// Segments walked at once on idle compute units: a walk of few columns leaves
+// most CUs idle (C2: 100 columns, 104 workgroups on 256 CUs), and its time is
+// the batch's DAG depth x pass latency, so G concurrent Add-order segments
+// walk ~1/G of the levels each.  0 when the batch stays one walk.
+uint32_t auto_segments(const lx_index *h, uint64_t n) {
+    if (!h->seg_auto || h->sharded() || h->rowseg() || h->segments > 1) return 0;
+    const uint32_t grid = walk_grid(h);
+    if (!grid) return 0;
+    uint32_t G = std::min<uint32_t>(h->n_cus / grid, kSegLaunchMax);
+    while (G >= 2 && n < (uint64_t)G * kAutoSegEvents) G--;
+    return G >= 2 ? G : 0;
+}
+
+int seg_walk(lx_index *h, IndexArgs ia, const uint32_t *poff, hipStream_t s, uint32_t G) {
+    const uint32_t n = ia.n, bs = ia.batch_start;
     SegArgs a{};
     a.hb = h->hb;
     a.la = h->la;
@@ -492,10 +513,26 @@ int seg_walk(lx_index *h, IndexArgs ia, const uint32_t *poff, hipStream_t s) {
     }
     hipEvent_t *ev = h->seg_ev.data();
     HIPCHK(h, lx::launch_seg_tables(a, s));
+    // one launch for all G when they fit the CUs side by side (one workgroup
+    // per CU each: k_index_segs); otherwise one walk after the other
+    const bool conc = G <= kSegLaunchMax && G * walk_grid(h) <= h->n_cus;
     ia.seg = 1;
     ia.ev_branch = h->ev_branch;
     ia.ev_seq = h->ev_seq;
-    for (uint32_t k = 0; k < G; k++) {
+    if (conc) {
+        IndexArgs sk = ia;
+        sk.seg_g = G;
+        sk.seg_B = a.B;
+        for (uint32_t k = 0; k <= G; k++) sk.seg_lo[k] = a.seg_lo[k];
+        sk.seg_j = a.jt;
+        sk.seg_flag = a.pflag;
+        sk.seg_list = a.plist;
+        sk.seg_count = a.pcount;
+        HIPCHK(h, hipEventRecord(ev[0], s));
+        HIPCHK(h, lx::launch_index(sk, s));
+        for (uint32_t k = 0; k < G; k++) HIPCHK(h, hipEventRecord(ev[2 * k + 1], s));
+    }
+    for (uint32_t k = 0; k < G && !conc; k++) {
         IndexArgs sk = ia;
         sk.batch_start = a.seg_lo[k];
         sk.n = a.seg_lo[k + 1] - a.seg_lo[k];
@@ -526,7 +563,7 @@ int seg_walk(lx_index *h, IndexArgs ia, const uint32_t *poff, hipStream_t s) {
     for (uint32_t k = 0; k < G; k++) {
         st.first_event[k] = a.seg_lo[k];
         st.partial[k] = pc[k];
-        HIPCHK(h, hipEventElapsedTime(&st.walk_ms[k], ev[2 * k], ev[2 * k + 1]));
+        HIPCHK(h, hipEventElapsedTime(&st.walk_ms[k], ev[conc ? 0 : 2 * k], ev[2 * k + 1]));
     }
     st.first_event[G] = a.seg_lo[G];
     HIPCHK(h, hipEventElapsedTime(&st.partial_ms, ev[2 * G - 1], ev[2 * G]));
@@ -641,7 +678,7 @@ int add_batch_dev(lx_index *h, uint32_t n, const uint32_t *creator, const uint32
     if (h->rowseg()) {
         if ((rc = rs_begin(h, ia, poff, s))) return rc;
     } else if (h->segments > 1 && !h->sharded() && n >= 64ull * h->segments) {
-        if ((rc = seg_walk(h, ia, poff, s))) return rc;
+        if ((rc = seg_walk(h, ia, poff, s, h->segments))) return rc;
     } else if (h->dbl && !ia.mask && !h->sharded() && h->B <= kDblMaxB && n >= 16ull * h->B && n <= 0xFFFFu &&
                dbl_lds_bytes(n, h->B) <= kDblLds) {
         // few branches, no forks: HB by frontier doubling in one workgroup
@@ -662,6 +699,8 @@ int add_batch_dev(lx_index *h, uint32_t n, const uint32_t *creator, const uint32
         da.brow = h->brow;
         da.s_cap = h->s_cap;
         HIPCHK(h, lx::launch_dbl(da, s));
+    } else if (const uint32_t G = auto_segments(h, n)) {
+        if ((rc = seg_walk(h, ia, poff, s, G))) return rc;
     } else {
         HIPCHK(h, lx::launch_index(ia, s));
     }
@@ -1564,6 +1603,11 @@ int lx_create(const lx_config *cfg, lx_index **out) {
         delete h;
         return LX_ERR_HIP;
     }
+    {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device) == hipSuccess && cus > 0)
+            h->n_cus = (uint32_t)cus;
+    }
     *out = h;
     return 0;
 }
@@ -1610,6 +1654,8 @@ int lx_set_option(lx_index *h, const char *name, int64_t value) {
         h->pack16 = value != 0;
     } else if (k == "dbl") {
         h->dbl = value != 0;
+    } else if (k == "seg_auto") {
+        h->seg_auto = value != 0;
     } else if (k == "la_memset") {
         if (h->have_epoch) return h->fail(LX_ERR_STATE, "la_memset must be set before lx_reset");
         h->la_tail = value == 0;

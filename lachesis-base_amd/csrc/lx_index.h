@@ -242,6 +242,8 @@ struct lx_index {
     bool fcc_slots_set = false;            // set by the option (else sized at lx_reset from V)
     // segmented walk (option segments, lx_segment.hip): scratch and timings of the last batch
     uint32_t segments = 0;
+    bool seg_auto = true;                  // option seg_auto=0: never split a batch on its own
+    uint32_t n_cus = 256;                  // compute units of the device (auto segments)
     uint32_t *seg_jt = nullptr, *seg_cnt = nullptr, *seg_mf = nullptr, *seg_plist = nullptr, *seg_elist = nullptr;
     uint64_t seg_jt_cap = 0, seg_cnt_cap = 0, seg_mf_cap = 0, seg_plist_cap = 0, seg_elist_cap = 0;   // seg_mf: flags
     std::vector<hipEvent_t> seg_ev;

@@ -38,6 +38,7 @@ struct EventRec {
     uint4 q[LX_REC_Q];
 };
 
+constexpr uint32_t kSegLaunchMax = 32;   // segments of one k_index_segs launch
 struct IndexArgs {
     uint32_t *hb;
     uint32_t *la;
@@ -70,6 +71,12 @@ struct IndexArgs {
     uint32_t *seg_flag;          // per segment event: set when its row misses some J_k (a "partial" event)
     uint32_t *seg_list;          // partial events (global index), appended
     uint32_t *seg_count;
+    // > 0: one launch walks seg_g segments side by side (k_index_segs): segment
+    // k = [seg_lo[k], seg_lo[k + 1]), its J table at seg_j + k * seg_B, its
+    // partial-event flags / list at the batch offset, its count at seg_count + k
+    uint32_t seg_g;
+    uint32_t seg_B;
+    uint32_t seg_lo[kSegLaunchMax + 1];
 };
 // k_dbl (lx_dbl.hip): HighestBefore by frontier doubling in one workgroup's
 // LDS, for fork-free batches with few branches
@@ -506,6 +513,7 @@ struct VoteArgs {
 // each walked with its boundary parents as own entries only (IndexArgs::seg),
 // then fixed up to the reference's rows.
 constexpr uint32_t kMaxSegments = 64;
+constexpr uint64_t kAutoSegEvents = 32768;   // events per segment at least, for a batch split on its own
 struct SegArgs {
     uint32_t *hb;
     uint32_t *la;

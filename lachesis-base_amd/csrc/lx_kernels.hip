@@ -533,7 +533,7 @@ __device__ __forceinline__ void blk_fold(const uint32_t pa[3], uint32_t W, uint3
 // (B > V); PK: 4-column slices with 16-bit packed slot units (every seq of the
 // epoch <= 0xFFFF).
 template <int CPW, int NCW, bool MASKED, bool PK>
-__global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
+__device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t w) {
     static_assert(!PK || CPW == 4, "packed slots: 4-column slices");
     static_assert(CPW == 1 || CPW == 2 || CPW == 4, "slot layout");
     static_assert(LX_MAXP == 12, "block walker: 12 inline parents, three per lane of a quad");
@@ -554,7 +554,6 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
     __shared__ uint4 dummy[128];                 // per-lane targets of suppressed writes
     __shared__ WalkShared sh;
 
-    const uint32_t w = blockIdx.x;
     const uint32_t slice = (w % 8) * a.slices_per_xcd + (w / 8);   // XCD-aware: neighbouring slices share an L2
     if (slice >= a.n_slices) return;
 
@@ -1120,6 +1119,31 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
     }
 }
 
+template <int CPW, int NCW, bool MASKED, bool PK>
+__global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
+    index_body<CPW, NCW, MASKED, PK>(a, blockIdx.x);
+}
+
+// seg_g Add-order segments of a batch walked by one launch, side by side on
+// idle CUs (a walk of few columns leaves most of them idle): workgroup
+// blockIdx.x walks segment blockIdx.x / (gridDim.x / seg_g) with the
+// segment's own batch window, J table and partial-event lists (lx_segment.hip)
+template <int CPW, int NCW, bool MASKED, bool PK>
+__global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index_segs(IndexArgs a0) {
+    const uint32_t per = gridDim.x / a0.seg_g, k = blockIdx.x / per;
+    IndexArgs a = a0;
+    const uint32_t lo = a0.seg_lo[k], off = lo - a0.batch_start;
+    a.batch_start = lo;
+    a.n = a0.seg_lo[k + 1] - lo;
+    a.rec = a0.rec + off;
+    a.poff_in = a0.poff_in + off;
+    a.seg_j = a0.seg_j + (uint64_t)k * a0.seg_B;
+    a.seg_flag = a0.seg_flag + off;
+    a.seg_list = a0.seg_list + off;
+    a.seg_count = a0.seg_count + k;
+    index_body<CPW, NCW, MASKED, PK>(a, blockIdx.x - k * per);
+}
+
 template <int CPW, int NCW>
 static hipError_t launch_index_t(const IndexArgs &a0, hipStream_t s) {
     IndexArgs a = a0;
@@ -1127,6 +1151,19 @@ static hipError_t launch_index_t(const IndexArgs &a0, hipStream_t s) {
     a.slices_per_xcd = (a.n_slices + 7) / 8;
     const uint32_t grid = a.slices_per_xcd * 8;
     const dim3 blk(64 * (NCW + 1 + kND));
+    if (a.seg_g) {   // segments side by side (walk_grid-sized blocks of workgroups)
+        const dim3 g(grid * a.seg_g);
+        if constexpr (CPW == 4) {
+            if (a.pack16) {
+                if (a.mask) hipLaunchKernelGGL((k_index_segs<CPW, NCW, true, true>), g, blk, 0, s, a);
+                else hipLaunchKernelGGL((k_index_segs<CPW, NCW, false, true>), g, blk, 0, s, a);
+                return hipGetLastError();
+            }
+        }
+        if (a.mask) hipLaunchKernelGGL((k_index_segs<CPW, NCW, true, false>), g, blk, 0, s, a);
+        else hipLaunchKernelGGL((k_index_segs<CPW, NCW, false, false>), g, blk, 0, s, a);
+        return hipGetLastError();
+    }
     if constexpr (CPW == 4) {
         if (a.pack16) {   // every seq of the epoch fits 16 bits: one 16-B slot unit
             if (a.mask) hipLaunchKernelGGL((k_index<CPW, NCW, true, true>), dim3(grid), blk, 0, s, a);
