@@ -80,6 +80,9 @@ const char *lx_last_error(const lx_index *h);
  *   "segments"   G in 2..64: a batch of >= 64 G events is walked as G Add-order segments
  *                and fixed up (the single-GPU form of the row-segment multi-GPU
  *                protocol; results identical); 0/1 off
+ *   "seg_auto"   0: never split a batch on its own (default 1: a batch whose walk
+ *                leaves CUs idle -- few columns -- is walked as G segments side by
+ *                side in one launch, G = CUs / walk workgroups, >= 32k events each)
  * The library reads no environment variables. */
 int lx_set_option(lx_index *h, const char *name, int64_t value);
 

@@ -141,3 +141,37 @@ def test_segmented_config3_shape_planes(lx, monkeypatch, G):
         ix.close()
     np.testing.assert_array_equal(planes[0][0], planes[1][0])
     np.testing.assert_array_equal(planes[0][1], planes[1][1])
+
+
+@pytest.mark.parametrize("shape", [(60, 2500, 8, 3, 4), (100, 1400, 10, 0, 0)])
+def test_auto_segments_side_by_side(lx, monkeypatch, shape):
+    """A walk of few columns leaves CUs idle: the batch is split on its own
+    (seg_auto, the default) into Add-order segments walked by one launch side
+    by side.  Both planes byte-identical to the single walk (seg_auto = 0),
+    HighestBefore rows of a prefix and ForklessCause against the oracle."""
+    V, epv, P, ch, fk = shape
+    d = lx.tools.gen_dag(V, epv, P, ch, fk, seed=17)
+    N = len(d)
+    w = [1 + (i * 7) % 11 for i in range(V)]
+    planes = []
+    for auto in (0, 1):
+        ix = lx.Index(event_capacity=N, options={"seg_auto": auto})
+        ix.reset(w)
+        ix.add_batch(d.creator, d.seq, d.poff, d.par)
+        ix.sync()
+        B = ix.num_branches()
+        hb, la, stride, _ = ix.device_planes()
+        planes.append((_plane(hb, N, stride, B), _plane(la, N, stride, B)))
+        if auto:
+            st = ix.segment_stats()
+            assert st["segments"] >= 2, st
+            o = corc.OracleIndex(w)
+            Pn = 20_000
+            assert o.add_batch(d.creator[:Pn], d.seq[:Pn], d.poff[:Pn + 1], d.par) == -1
+            ev = np.arange(0, Pn, 9, dtype=np.uint32)
+            # HighestBefore of a prefix (its LowestAfter rows fill from later events)
+            assert np.array_equal(ix.rows_np(0, ev)[1], o.rows(0, ev)[1])
+            fc_sample(ix, o, Pn, 50_000, 3)
+        ix.close()
+    np.testing.assert_array_equal(planes[0][0], planes[1][0])
+    np.testing.assert_array_equal(planes[0][1], planes[1][1])
