@@ -1116,7 +1116,7 @@ int stage_slot(lx_index *h, uint64_t words, uint32_t **out, int *slot) {
     }
     if (words > h->st_dev_cap[k]) {
         if (h->st_dev[k]) {
-            if (h->st_used[k]) HIPCHK(h, hipEventSynchronize(h->st_done[k]));
+            if (h->st_used[k]) HIPCHK(h, hipStreamSynchronize(h->stream));   // the kernel that read it
             (void)hipFree(h->st_dev[k]);
         }
         h->st_dev[k] = nullptr;
@@ -1201,10 +1201,11 @@ int flush_pending(lx_index *h) {
     hipStream_t s = h->stream;
     if (!inl) {
         // device image `slot` is free once the kernel that read it finished
-        if (h->st_used[slot]) HIPCHK(h, hipStreamWaitEvent(h->cstream, h->st_done[slot], 0));
-        HIPCHK(h, hipMemcpyAsync(h->st_dev[slot], img, words * 4, hipMemcpyHostToDevice, h->cstream));
-        HIPCHK(h, hipEventRecord(h->st_copied[slot], h->cstream));
-        HIPCHK(h, hipStreamWaitEvent(s, h->st_copied[slot], 0));
+        // the copy is a kernel on this stream (a copy-engine transfer waited
+        // for the previous run's kernel and then handed over to the compute
+        // queue, tens of us between every two runs of a level-fed stream)
+        HIPCHK(h, lx::launch_stage(h->st_dev[slot], img, words, s));
+        HIPCHK(h, hipEventRecord(h->st_copied[slot], s));
     }
     SmallArgs &a = h->sm_inl.a;
     a = SmallArgs{};
@@ -1243,10 +1244,7 @@ int flush_pending(lx_index *h) {
     a.mask = B > h->V ? 1u : 0u;
     if (h->small_timing) HIPCHK(h, hipEventRecord(h->ev[1], s));
     HIPCHK(h, inl ? lx::launch_small_inline(h->sm_inl, s) : lx::launch_small(a, s));
-    if (!inl) {
-        HIPCHK(h, hipEventRecord(h->st_done[slot], s));
-        h->st_used[slot] = true;
-    }
+    if (!inl) h->st_used[slot] = true;
     if (h->small_timing) HIPCHK(h, hipEventRecord(h->ev[2], s));
     if (B > h->V && h->n_cheat) {
         MarkArgs m{};
@@ -1593,16 +1591,11 @@ int lx_create(const lx_config *cfg, lx_index **out) {
             delete h;
             return LX_ERR_HIP;
         }
-    for (auto *ev : {h->st_done, h->st_copied})
-        for (int k = 0; k < lx_index::kSlots; k++)
-            if (hipEventCreateWithFlags(&ev[k], hipEventDisableTiming) != hipSuccess) {
-                delete h;
-                return LX_ERR_HIP;
-            }
-    if (hipStreamCreateWithFlags(&h->cstream, hipStreamNonBlocking) != hipSuccess) {
-        delete h;
-        return LX_ERR_HIP;
-    }
+    for (auto &e : h->st_copied)
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+            delete h;
+            return LX_ERR_HIP;
+        }
     {
         int cus = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device) == hipSuccess && cus > 0)
@@ -1621,16 +1614,13 @@ void lx_destroy(lx_index *h) {
     if (h->status) (void)hipFree(h->status);
     for (auto &e : h->ev)
         if (e) (void)hipEventDestroy(e);
-    if (h->cstream) (void)hipStreamSynchronize(h->cstream);
-    for (auto *ev : {h->st_done, h->st_copied})
-        for (int k = 0; k < lx_index::kSlots; k++)
-            if (ev[k]) (void)hipEventDestroy(ev[k]);
+    for (auto &e : h->st_copied)
+        if (e) (void)hipEventDestroy(e);
     for (auto &e : h->seg_ev) (void)hipEventDestroy(e);
     for (auto *p : h->st_pin)
         if (p) (void)hipHostFree(p);
     for (auto *p : h->st_dev)
         if (p) (void)hipFree(p);
-    if (h->cstream) (void)hipStreamDestroy(h->cstream);
     if (h->qp) (void)hipHostFree(h->qp);
     if (h->ld_buf) (void)hipFree(h->ld_buf);
     if (h->stream) (void)hipStreamDestroy(h->stream);

@@ -199,20 +199,16 @@ struct lx_index {
     uint32_t pend_nh = 0;                  // h0 slots of the run
     std::vector<uint32_t> touch_mark;      // per branch: stamp of the last run that touched it
     uint32_t touch_stamp = 0;
-    // staging images in flight: slot k = a pinned image and its device copy.
-    // The H2D copy runs on cstream, so the copy of run k + 1 overlaps the
-    // kernel of run k (on one stream it waited for that kernel, and the copy
-    // engine's hand-off to the compute queue sat between every two runs)
+    // staging images in flight: slot k = a pinned image and its device copy,
+    // copied by a kernel on the handle's stream (k_stage)
     static constexpr int kSlots = 4;
     uint32_t *st_pin[kSlots] = {};
     uint64_t st_pin_cap[kSlots] = {};
-    hipEvent_t st_copied[kSlots] = {};     // cstream: the H2D copy of slot k finished (pinned image free)
-    hipEvent_t st_done[kSlots] = {};       // stream: the kernel that read device image k finished
+    hipEvent_t st_copied[kSlots] = {};     // the copy of slot k finished (its pinned image is free)
     bool st_used[kSlots] = {};
     uint32_t st_next = 0;
     uint32_t *st_dev[kSlots] = {};
     uint64_t st_dev_cap[kSlots] = {};
-    hipStream_t cstream = nullptr;
     SmallInlineArgs sm_inl{};              // arguments of the last launch; images of <= kSmallInline words inline
     // restart from the persisted tables (lx_load_rows / lx_load_finish)
     bool loading = false;

@@ -583,6 +583,7 @@ hipError_t scan_tmp_bytes(uint32_t n, size_t *bytes);
 hipError_t launch_undo_claims(const BatchArgs &a, hipStream_t s);
 hipError_t launch_index(const IndexArgs &a, hipStream_t s);
 hipError_t launch_dbl(const DblArgs &a, hipStream_t s);
+hipError_t launch_stage(uint32_t *dst, const uint32_t *src, uint64_t words, hipStream_t s);
 hipError_t launch_marks(const MarkArgs &a, hipStream_t s);
 hipError_t launch_fc(const FcArgs &a, uint32_t cols, bool forks, hipStream_t s);
 hipError_t launch_fc_combine(const uint32_t *sum, uint8_t *out, uint64_t n, uint32_t quorum, hipStream_t s);

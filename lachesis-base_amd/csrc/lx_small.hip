@@ -28,6 +28,8 @@
 // loads per level (record, parent list, parent value) plus the fill's branch
 // row; now a level costs a few LDS round trips.
 // Fork marks (k_marks) run after it when the epoch has forks.
+#include <algorithm>
+
 #include "lx_internal.h"
 
 namespace lx {
@@ -388,6 +390,21 @@ __global__ __launch_bounds__(256) void k_add1_row(Add1RowArgs a) {
 hipError_t launch_add1_row(const Add1RowArgs &a, hipStream_t s) {
     if (!a.n_slots || !a.B || a.e.q0.w > kAdd1MaxPar) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_add1_row, dim3((a.B + 63) / 64, (a.n_slots + 255) / 256), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+// The pending run's staged image, pinned host memory -> its device copy, on
+// the kernel's own stream: no copy-engine hand-off between the runs of a
+// level-fed stream (flush_pending)
+__global__ __launch_bounds__(256) void k_stage(uint4 *dst, const uint4 *src, uint32_t n16) {
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n16; i += gridDim.x * 256) dst[i] = src[i];
+}
+
+hipError_t launch_stage(uint32_t *dst, const uint32_t *src, uint64_t words, hipStream_t s) {
+    const uint32_t n16 = (uint32_t)((words + 3) / 4);
+    if (!n16) return hipSuccess;
+    hipLaunchKernelGGL(k_stage, dim3(std::min<uint32_t>((n16 + 255) / 256, 64)), dim3(256), 0, s,
+                       reinterpret_cast<uint4 *>(dst), reinterpret_cast<const uint4 *>(src), n16);
     return hipGetLastError();
 }
 
