@@ -47,6 +47,7 @@ struct IdMap {
         t.assign(m, Ent{0, 0, 0});
         mask = m - 1;
         used = live = 0;
+        gen++;
     }
     uint32_t find(uint64_t k) const {
         for (uint64_t i = h(k) & mask;; i = (i + 1) & mask) {
@@ -62,22 +63,25 @@ struct IdMap {
             if (e.key == k && e.st == 1) return &e.val;
         }
     }
-    // the value of k, or (k absent) insert v and return kNone: one probe sequence
-    uint32_t find_or_put(uint64_t k, uint32_t v) {
+    // the value of k, or (k absent) insert v and return kNone: one probe
+    // sequence; *at = the entry's position (valid until the table grows)
+    uint32_t find_or_put(uint64_t k, uint32_t v, uint64_t *at) {
         if ((used + 1) * 2 > mask + 1) grow();
         uint64_t i = h(k) & mask, tomb = ~0ull;
         for (;; i = (i + 1) & mask) {
             Ent &e = t[i];
             if (e.st == 0) break;
-            if (e.st == 1 && e.key == k) return e.val;
+            if (e.st == 1 && e.key == k) { *at = i; return e.val; }
             if (e.st == 2 && tomb == ~0ull) tomb = i;
         }
         if (tomb != ~0ull) i = tomb;
         else used++;
         t[i] = Ent{k, v, 1};
         live++;
+        *at = i;
         return kNone;
     }
+    uint64_t gen = 0;   // bumped when the table is rebuilt: remembered positions are stale
     void put(uint64_t k, uint32_t v) {   // k not present
         if ((used + 1) * 2 > mask + 1) grow();
         uint64_t i = h(k) & mask;
@@ -103,6 +107,7 @@ struct IdMap {
 
 struct Pending {
     uint64_t id = 0, order = 0;
+    uint64_t at = 0, at_gen = 0;    // its ids entry (position, table generation)
     uint32_t creator = 0, seq = 0;
     uint32_t par_off = 0, np = 0;   // into par_id / par_res
     uint32_t missing = 0;           // parents not released yet
@@ -310,7 +315,8 @@ int lx_batcher_push(lx_batcher *b, uint32_t n, const uint64_t *id, const uint32_
     for (uint32_t i = 0; i < n; i++) {
         // the slot this event would take (the table holds it only if the id is new)
         const uint32_t s = b->free_slots.empty() ? (uint32_t)b->pend.size() : b->free_slots.back();
-        const uint32_t v = b->ids.find_or_put(id[i], kPend | s);
+        uint64_t at = 0;
+        const uint32_t v = b->ids.find_or_put(id[i], kPend | s, &at);
         uint8_t st = LX_PUSH_QUEUED;
         if (v != kNone) st = (v & kPend) ? LX_PUSH_DUPLICATE : LX_PUSH_CONNECTED;   // ErrDuplicateEvent / ErrAlreadyConnectedEvent
         if (out_status) out_status[i] = st;
@@ -318,6 +324,8 @@ int lx_batcher_push(lx_batcher *b, uint32_t n, const uint64_t *id, const uint32_
         if (b->alloc_slot() != s) return b->fail(LX_ERR_STATE, "batcher slot bookkeeping");
         Pending &p = b->pend[s];
         p.id = id[i];
+        p.at = at;
+        p.at_gen = b->ids.gen;
         p.creator = creator_idx[i];
         p.seq = seq[i];
         p.order = b->next_order++;
@@ -368,7 +376,9 @@ int lx_batcher_pop(lx_batcher *b, uint64_t *out_id, uint32_t *out_creator, uint3
         const uint32_t s = b->plan[i];
         Pending &p = b->pend[s];
         const uint32_t dense = base + i;
-        *b->ids.ref(p.id) = dense;
+        // its table entry as remembered at push (one probe less per event)
+        if (p.at_gen == b->ids.gen && b->ids.t[p.at].key == p.id && b->ids.t[p.at].st == 1) b->ids.t[p.at].val = dense;
+        else *b->ids.ref(p.id) = dense;
         b->released.push_back(p.id);
         out_id[i] = p.id;
         out_creator[i] = p.creator;
