@@ -454,8 +454,8 @@ BatchArgs batch_args(lx_index *h, uint32_t n, const uint32_t *creator, const uin
 // seg_stats.
 // Workgroups of one walk of the batch's columns (launch_index's slice choice,
 // rounded to the 8 XCDs)
-uint32_t walk_grid(const lx_index *h) {
-    const uint32_t nc = h->ncols, cpw = h->cpw_hint ? h->cpw_hint : (nc <= 256 ? 1 : nc <= 512 ? 2 : 4);
+uint32_t walk_grid(const lx_index *h, uint32_t cpw_hint) {
+    const uint32_t nc = h->ncols, cpw = cpw_hint ? cpw_hint : (nc <= 256 ? 1 : nc <= 512 ? 2 : 4);
     const uint32_t slices = (nc + cpw - 1) / cpw;
     return (slices + 7) / 8 * 8;
 }
@@ -463,17 +463,29 @@ uint32_t walk_grid(const lx_index *h) {
 // Segments walked at once on idle compute units: a walk of few columns leaves
 // most CUs idle (C2: 100 columns, 104 workgroups on 256 CUs), and its time is
 // the batch's DAG depth x pass latency, so G concurrent Add-order segments
-// walk ~1/G of the levels each.  0 when the batch stays one walk.
-uint32_t auto_segments(const lx_index *h, uint64_t n) {
-    if (!h->seg_auto || h->sharded() || h->rowseg() || h->segments > 1) return 0;
-    const uint32_t grid = walk_grid(h);
-    if (!grid) return 0;
-    uint32_t G = std::min<uint32_t>(h->n_cus / grid, kSegLaunchMax);
-    while (G >= 2 && n < (uint64_t)G * kAutoSegEvents) G--;
-    return G >= 2 ? G : 0;
+// walk ~1/G of the levels each.  Wider slices free more CUs for more
+// segments at a longer pass (relative pass costs of 1-, 2- and 4-column
+// slices as measured on C2: 1, 1.15, 1.28): the slice width with the
+// smallest pass / G wins.  0 when the batch stays one walk; *cpw = the width.
+uint32_t auto_segments(const lx_index *h, uint64_t n, uint32_t *cpw) {
+    if (!h->seg_auto || h->sharded() || h->rowseg() || h->segments > 1 || !h->ncols) return 0;
+    static const float kPass[5] = {0, 1.0f, 1.15f, 0, 1.28f};
+    uint32_t best_g = 0;
+    float best = 1.0f;   // one walk at the default width
+    for (uint32_t c : {1u, 2u, 4u}) {
+        if (h->cpw_hint && c != h->cpw_hint) continue;
+        uint32_t G = std::min<uint32_t>(h->n_cus / walk_grid(h, c), kSegLaunchMax);
+        while (G >= 2 && n < (uint64_t)G * kAutoSegEvents) G--;
+        if (G >= 2 && kPass[c] / G < best) {
+            best = kPass[c] / G;
+            best_g = G;
+            *cpw = c;
+        }
+    }
+    return best_g;
 }
 
-int seg_walk(lx_index *h, IndexArgs ia, const uint32_t *poff, hipStream_t s, uint32_t G) {
+int seg_walk(lx_index *h, IndexArgs ia, const uint32_t *poff, hipStream_t s, uint32_t G, uint32_t cpw) {
     const uint32_t n = ia.n, bs = ia.batch_start;
     SegArgs a{};
     a.hb = h->hb;
@@ -515,7 +527,8 @@ int seg_walk(lx_index *h, IndexArgs ia, const uint32_t *poff, hipStream_t s, uin
     HIPCHK(h, lx::launch_seg_tables(a, s));
     // one launch for all G when they fit the CUs side by side (one workgroup
     // per CU each: k_index_segs); otherwise one walk after the other
-    const bool conc = G <= kSegLaunchMax && G * walk_grid(h) <= h->n_cus;
+    ia.cpw_hint = cpw;
+    const bool conc = G <= kSegLaunchMax && G * walk_grid(h, cpw) <= h->n_cus;
     ia.seg = 1;
     ia.ev_branch = h->ev_branch;
     ia.ev_seq = h->ev_seq;
@@ -678,7 +691,7 @@ int add_batch_dev(lx_index *h, uint32_t n, const uint32_t *creator, const uint32
     if (h->rowseg()) {
         if ((rc = rs_begin(h, ia, poff, s))) return rc;
     } else if (h->segments > 1 && !h->sharded() && n >= 64ull * h->segments) {
-        if ((rc = seg_walk(h, ia, poff, s, h->segments))) return rc;
+        if ((rc = seg_walk(h, ia, poff, s, h->segments, h->cpw_hint))) return rc;
     } else if (h->dbl && !ia.mask && !h->sharded() && h->B <= kDblMaxB && n >= 16ull * h->B && n <= 0xFFFFu &&
                dbl_lds_bytes(n, h->B) <= kDblLds) {
         // few branches, no forks: HB by frontier doubling in one workgroup
@@ -699,8 +712,8 @@ int add_batch_dev(lx_index *h, uint32_t n, const uint32_t *creator, const uint32
         da.brow = h->brow;
         da.s_cap = h->s_cap;
         HIPCHK(h, lx::launch_dbl(da, s));
-    } else if (const uint32_t G = auto_segments(h, n)) {
-        if ((rc = seg_walk(h, ia, poff, s, G))) return rc;
+    } else if (uint32_t cpw = 0, G = auto_segments(h, n, &cpw); G) {
+        if ((rc = seg_walk(h, ia, poff, s, G, cpw))) return rc;
     } else {
         HIPCHK(h, lx::launch_index(ia, s));
     }

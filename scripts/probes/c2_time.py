@@ -12,7 +12,9 @@ import numpy as np  # noqa: E402
 import lachesis_hip as lx  # noqa: E402
 
 V = int(os.environ.get("V", "100"))
-d = lx.tools.gen_dag(V, 1_000_000 // V, 10, seed=1)
+EPV = int(os.environ.get("EPV", str(1_000_000 // V)))
+CH, FK = int(os.environ.get("CH", "0")), int(os.environ.get("FK", "0"))
+d = lx.tools.gen_dag(V, EPV, 10, CH, FK, seed=1)
 w = [1] * V
 res = {}
 for auto in (1, 0):
