@@ -469,11 +469,13 @@ uint32_t walk_grid(const lx_index *h, uint32_t cpw_hint) {
 // smallest pass / G wins.  0 when the batch stays one walk; *cpw = the width.
 uint32_t auto_segments(const lx_index *h, uint64_t n, uint32_t *cpw) {
     if (!h->seg_auto || h->sharded() || h->rowseg() || h->segments > 1 || !h->ncols) return 0;
-    static const float kPass[5] = {0, 1.0f, 1.15f, 0, 1.28f};
+    static const float kPass[9] = {0, 1.0f, 1.15f, 0, 1.28f, 0, 0, 0, kPass8};
+    // 8-column slices: packed 16-bit slots only (every seq <= 0xFFFF, no forks)
+    const bool w8 = h->pack16 && h->max_seq <= 0xFFFFu && h->B <= h->V;
     uint32_t best_g = 0;
     float best = 1.0f;   // one walk at the default width
-    for (uint32_t c : {1u, 2u, 4u}) {
-        if (h->cpw_hint && c != h->cpw_hint) continue;
+    for (uint32_t c : {1u, 2u, 4u, 8u}) {
+        if ((h->cpw_hint && c != h->cpw_hint) || (c == 8 && !w8)) continue;
         uint32_t G = std::min<uint32_t>(h->n_cus / walk_grid(h, c), kSegLaunchMax);
         while (G >= 2 && n < (uint64_t)G * kAutoSegEvents) G--;
         if (G >= 2 && kPass[c] / G < best) {
@@ -527,7 +529,8 @@ int seg_walk(lx_index *h, IndexArgs ia, const uint32_t *poff, hipStream_t s, uin
     HIPCHK(h, lx::launch_seg_tables(a, s));
     // one launch for all G when they fit the CUs side by side (one workgroup
     // per CU each: k_index_segs); otherwise one walk after the other
-    ia.cpw_hint = cpw;
+    ia.cpw_hint = cpw == 8 && (!ia.pack16 || ia.mask) ? 4 : cpw;
+    cpw = ia.cpw_hint;
     const bool conc = G <= kSegLaunchMax && G * walk_grid(h, cpw) <= h->n_cus;
     ia.seg = 1;
     ia.ev_branch = h->ev_branch;
@@ -682,6 +685,7 @@ int add_batch_dev(lx_index *h, uint32_t n, const uint32_t *creator, const uint32
     ia.mask = (h->B > h->V) ? 1u : 0u;
     ia.cpw_hint = h->cpw_hint;
     ia.pack16 = h->pack16 && h->max_seq <= 0xFFFFu;
+    if (ia.cpw_hint == 8 && (!ia.pack16 || ia.mask)) ia.cpw_hint = 4;   // 8-column slots: packed, fork-free
     const size_t prof_n = (size_t)kProfBlocks * kProfWaves * kProfSlots;
     if (h->prof) {
         HIPCHK(h, hipMalloc(&ia.prof, prof_n * 8));
@@ -1651,7 +1655,8 @@ int lx_set_option(lx_index *h, const char *name, int64_t value) {
     } else if (k == "fc_fk") {
         h->fc_fk = value != 0;
     } else if (k == "cpw") {
-        if (value != 0 && value != 1 && value != 2 && value != 4) return h->fail(LX_ERR_ARG, "cpw must be 0, 1, 2 or 4");
+        if (value != 0 && value != 1 && value != 2 && value != 4 && value != 8)
+            return h->fail(LX_ERR_ARG, "cpw must be 0, 1, 2, 4 or 8 (8: fork-free epochs with seqs <= 0xFFFF)");
         h->cpw_hint = (uint32_t)value;
     } else if (k == "pack16") {
         h->pack16 = value != 0;

@@ -513,7 +513,8 @@ struct VoteArgs {
 // each walked with its boundary parents as own entries only (IndexArgs::seg),
 // then fixed up to the reference's rows.
 constexpr uint32_t kMaxSegments = 64;
-constexpr uint64_t kAutoSegEvents = 32768;   // events per segment at least, for a batch split on its own
+constexpr uint64_t kAutoSegEvents = 32768;
+constexpr float kPass8 = 4.0f;   // pass cost of 8- vs 1-column slices for auto segments (4: not picked until measured)
 struct SegArgs {
     uint32_t *hb;
     uint32_t *la;

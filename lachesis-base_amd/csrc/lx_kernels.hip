@@ -358,8 +358,21 @@ __device__ __forceinline__ void unpack16(const u4v &x, uint32_t *v) {
 }
 template <int CPW, bool PK = false>
 __device__ __forceinline__ void ring_read1(uint32_t A, uint32_t B, uint32_t s, Slot<CPW> &o) {
-    if constexpr (PK) {
-        static_assert(CPW == 4, "packed slots: 4-column slices");
+    if constexpr (PK && CPW == 8) {
+        // two units {tag, s0 | s1 << 16, s2 | s3 << 16, s4 | s5 << 16}, {tag, s6 | s7 << 16, 0, 0}
+        u4v x, y;
+        asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %3\n\ts_waitcnt lgkmcnt(0)"
+                     : "=&v"(x), "=&v"(y)
+                     : "v"(A + s * 16u), "v"(B + s * 16u)
+                     : "memory");
+        o.t0 = x.x;
+        o.t1 = y.x;
+        const uint32_t w[4] = {x.y, x.z, x.w, y.y};
+#pragma unroll
+        for (int k = 0; k < CPW; k++) o.v[k] = (k & 1) ? w[(k / 2) % 4] >> 16 : w[(k / 2) % 4] & 0xFFFFu;
+        return;
+    } else if constexpr (PK) {
+        static_assert(CPW == 4, "packed slots: 4- or 8-column slices");
         u4v x;
         asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=&v"(x) : "v"(A + s * 16u) : "memory");
         o.t0 = o.t1 = x.x;
@@ -453,8 +466,7 @@ __device__ __forceinline__ uint32_t quad_and(uint32_t v) {
 template <int CPW, int RN, bool PK = false>
 __device__ __forceinline__ void blk_fold(const uint32_t pa[3], uint32_t W, uint32_t tg[3][2], uint32_t pv[3][CPW],
                                          uint32_t &cw) {
-    if constexpr (PK) {
-        static_assert(CPW == 4, "packed slots: 4-column slices");
+    if constexpr (PK && CPW == 4) {
         u4v x0, x1, x2;
         asm volatile(
             "ds_read_b128 %0, %4\n\t"
@@ -475,7 +487,8 @@ __device__ __forceinline__ void blk_fold(const uint32_t pa[3], uint32_t W, uint3
         }
         return;
     }
-    if constexpr (CPW == 4) {
+    if constexpr (CPW == 4 || CPW == 8) {
+        // two units per slot; CPW 8 (packed): pv[k][0..3] = packed column pairs
         constexpr uint32_t BOFF = (RN + 1) * 16;
         static_assert(BOFF < 65536, "ds offset field");
         u4v xa0, xb0, xa1, xb1, xa2, xb2;
@@ -534,8 +547,8 @@ __device__ __forceinline__ void blk_fold(const uint32_t pa[3], uint32_t W, uint3
 // epoch <= 0xFFFF).
 template <int CPW, int NCW, bool MASKED, bool PK>
 __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t w) {
-    static_assert(!PK || CPW == 4, "packed slots: 4-column slices");
-    static_assert(CPW == 1 || CPW == 2 || CPW == 4, "slot layout");
+    static_assert(!PK || CPW >= 4, "packed slots: 4- or 8-column slices");
+    static_assert(CPW == 1 || CPW == 2 || CPW == 4 || (CPW == 8 && PK && !MASKED), "slot layout");
     static_assert(LX_MAXP == 12, "block walker: 12 inline parents, three per lane of a quad");
     constexpr int ND = kND;
     constexpr int RR = kRR;
@@ -561,7 +574,7 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t w)
     // 8-B units), unit B (CPW 4) after the B array
     constexpr int kNullA = CPW == 1 ? RN / 2 : RN;
     for (int i = threadIdx.x; i < RB16 + 2; i += NT)
-        ring[i] = make_uint4((i == kNullA || (CPW == 4 && i == 2 * RN + 1)) ? kNullTag : 0u, 0, 0, 0);
+        ring[i] = make_uint4((i == kNullA || (CPW >= 4 && i == 2 * RN + 1)) ? kNullTag : 0u, 0, 0, 0);
     for (int i = threadIdx.x; i < RR / 64; i += NT) rtag[i] = 0;
     for (int i = threadIdx.x; i < CPW * KB; i += NT) brc[i] = make_uint2(0, LX_NONE);
     if (threadIdx.x < kND) { sh.copied[threadIdx.x] = 0; sh.stored[threadIdx.x] = 0; }
@@ -763,7 +776,11 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t w)
                 if (contig) {
                     if (CPW == 1) hrow[pc[0]] = r[0];
                     else if (CPW == 2) *reinterpret_cast<uint2 *>(hrow + pc[0]) = make_uint2(r[0], r[1 % CPW]);
-                    else *reinterpret_cast<uint4 *>(hrow + pc[0]) = make_uint4(r[0], r[1 % CPW], r[2 % CPW], r[3 % CPW]);
+                    else if (CPW == 4) *reinterpret_cast<uint4 *>(hrow + pc[0]) = make_uint4(r[0], r[1 % CPW], r[2 % CPW], r[3 % CPW]);
+                    else {
+                        *reinterpret_cast<uint4 *>(hrow + pc[0]) = make_uint4(r[0], r[1 % CPW], r[2 % CPW], r[3 % CPW]);
+                        *reinterpret_cast<uint4 *>(hrow + pc[0] + 4) = make_uint4(r[4 % CPW], r[5 % CPW], r[6 % CPW], r[7 % CPW]);
+                    }
                 } else {
 #pragma unroll
                     for (int k = 0; k < CPW; k++)
@@ -856,6 +873,14 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t w)
         const uint32_t j = lane & 3, quad = lane >> 2;
         const uint32_t mycol = col[j & (CPW - 1)];
         const bool myvalid = j < (uint32_t)CPW && valid[j & (CPW - 1)];
+        // CPW 8: lane j of a quad also owns column j + 4 (recent-event entries)
+        uint32_t mycol2 = 0;
+        bool myvalid2 = false;
+        if constexpr (CPW == 8) {
+#pragma unroll
+            for (int k = 4; k < CPW; k++)
+                if ((uint32_t)k == j + 4) { mycol2 = col[k]; myvalid2 = valid[k]; }
+        }
         uint32_t blk = __builtin_amdgcn_readfirstlane(wave);   // wave-uniform: scalar loop control
         bool loaded = false, done = true;
         uint32_t br = 0, seq = 0, np = 0, xi = 0;
@@ -939,9 +964,10 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t w)
                 wstuck = __any(far_parent(px, lp, (uint32_t)RN - kLeanFar)) ? kLeanStuck : 0u;
                 {
                     const uint32_t rs = (lp % RN) * UA;
-                    wa_pub = j == 0 ? RA + rs : (CPW == 4 && !PK && j == 1) ? RB + (lp % RN) * 16u : dmy;
+                    wa_pub = j == 0 ? RA + rs : (((CPW == 4 && !PK) || CPW == 8) && j == 1) ? RB + (lp % RN) * 16u : dmy;
                     wb_pub = (myvalid && mycol == br) ? lds_addr(brc) + ((j & (CPW - 1)) * KB + seq % KB) * 8u
-                                                      : dmy + 1024u;
+                             : (CPW == 8 && myvalid2 && mycol2 == br) ? lds_addr(brc) + (((j + 4) & (CPW - 1)) * KB + seq % KB) * 8u
+                                                                       : dmy + 1024u;
                     // the slot's previous occupant lp - RN is drained once its
                     // drain wave's `copied` count exceeds its round / ND
                     const uint32_t rr = (lp - RN) / 64;
@@ -976,14 +1002,17 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t w)
             // C2 -5.2 % against v_cmp + s_and)
             uint32_t tx = 0;
 #pragma unroll
-            for (int k = 0; k < 3; k++) tx |= (tg[k][0] ^ px[k]) | (PK || CPW < 4 ? 0u : (tg[k][1] ^ px[k]));
+            for (int k = 0; k < 3; k++) tx |= (tg[k][0] ^ px[k]) | ((PK && CPW == 4) || CPW < 4 ? 0u : (tg[k][1] ^ px[k]));
             uint32_t m[CPW];
-            uint32_t mp[2] = {0u, 0u};   // PK: the quad's maxima, two columns per dword
+            constexpr int NH = CPW / 2 > 0 ? CPW / 2 : 1;
+            uint32_t mp[NH];   // PK: the quad's maxima, two columns per dword
+#pragma unroll
+            for (int h = 0; h < NH; h++) mp[h] = 0u;
             if constexpr (PK) {
                 // two columns per dword: three packed maxima per dword, the quad
                 // reduction on packed words
 #pragma unroll
-                for (int h = 0; h < 2; h++) {
+                for (int h = 0; h < NH; h++) {
                     const uint32_t rp = r[(2 * h) % CPW] | (r[(2 * h + 1) % CPW] << 16);
                     mp[h] = quad_pk_max(pk_max(pk_max(rp, pv[0][h % CPW]), pk_max(pv[1][h % CPW], pv[2][h % CPW])));
                 }
@@ -1035,7 +1064,7 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t w)
                 // the same parent on every lane of the quad: m stays the quad's value
                 if constexpr (PK) {
 #pragma unroll
-                    for (int h = 0; h < 2; h++)
+                    for (int h = 0; h < NH; h++)
                         mp[h] = pk_max(mp[h], r[(2 * h) % CPW] | (r[(2 * h + 1) % CPW] << 16));
                 } else {
 #pragma unroll
@@ -1058,9 +1087,14 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t w)
                     u2v x;
                     x.x = lp + 1; x.y = m[0];
                     asm volatile("ds_write_b64 %2, %3\n\tds_write_b64 %0, %1" : : "v"(wa), "v"(x), "v"(wb), "v"(y) : "memory");
+                } else if constexpr (PK && CPW == 8) {
+                    u4v x;   // lane 0: {tag, s01, s23, s45}, lane 1: {tag, s67, 0, 0}
+                    x.x = lp + 1; x.y = j == 0 ? mp[0] : mp[3 % NH]; x.z = j == 0 ? mp[1 % NH] : 0u;
+                    x.w = j == 0 ? mp[2 % NH] : 0u;
+                    asm volatile("ds_write_b64 %2, %3\n\tds_write_b128 %0, %1" : : "v"(wa), "v"(x), "v"(wb), "v"(y) : "memory");
                 } else if constexpr (PK) {
                     u4v x;   // lane 0: {tag, s0 | s1 << 16, s2 | s3 << 16, 0}
-                    x.x = lp + 1; x.y = mp[0]; x.z = mp[1]; x.w = 0u;
+                    x.x = lp + 1; x.y = mp[0]; x.z = mp[1 % NH]; x.w = 0u;
                     asm volatile("ds_write_b64 %2, %3\n\tds_write_b128 %0, %1" : : "v"(wa), "v"(x), "v"(wb), "v"(y) : "memory");
                 } else {
                     u4v x;
@@ -1151,6 +1185,12 @@ static hipError_t launch_index_t(const IndexArgs &a0, hipStream_t s) {
     a.slices_per_xcd = (a.n_slices + 7) / 8;
     const uint32_t grid = a.slices_per_xcd * 8;
     const dim3 blk(64 * (NCW + 1 + kND));
+    if constexpr (CPW == 8) {   // packed fork-free epochs only
+        if (!a.pack16 || a.mask) return hipErrorInvalidValue;
+        if (a.seg_g) hipLaunchKernelGGL((k_index_segs<CPW, NCW, false, true>), dim3(grid * a.seg_g), blk, 0, s, a);
+        else hipLaunchKernelGGL((k_index<CPW, NCW, false, true>), dim3(grid), blk, 0, s, a);
+        return hipGetLastError();
+    } else {
     if (a.seg_g) {   // segments side by side (walk_grid-sized blocks of workgroups)
         const dim3 g(grid * a.seg_g);
         if constexpr (CPW == 4) {
@@ -1174,6 +1214,7 @@ static hipError_t launch_index_t(const IndexArgs &a0, hipStream_t s) {
     if (a.mask) hipLaunchKernelGGL((k_index<CPW, NCW, true, false>), dim3(grid), blk, 0, s, a);
     else hipLaunchKernelGGL((k_index<CPW, NCW, false, false>), dim3(grid), blk, 0, s, a);
     return hipGetLastError();
+    }
 }
 
 hipError_t launch_index(const IndexArgs &a, hipStream_t s) {
@@ -1187,6 +1228,7 @@ hipError_t launch_index(const IndexArgs &a, hipStream_t s) {
     const uint32_t cpw = a.cpw_hint ? a.cpw_hint : (a.ncols <= 256 ? 1 : a.ncols <= 512 ? 2 : 4);
     if (cpw <= 1) return launch_index_t<1, 8>(a, s);
     if (cpw <= 2) return launch_index_t<2, 8>(a, s);
+    if (cpw == 8) return launch_index_t<8, 11>(a, s);
     return launch_index_t<4, 11>(a, s);
 }
 

@@ -1,0 +1,93 @@
+"""The walker on 8-column slices (packed 16-bit slot units in two 16-B units:
+fork-free epochs whose seqs fit 16 bits), alone and as side-by-side segments:
+rows and ForklessCause against the C oracle, planes byte-identical to the
+4-column walk."""
+
+import ctypes
+
+import numpy as np
+import pytest
+
+from oracle import corc
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def lx():
+    import lachesis_hip
+    return lachesis_hip
+
+
+def _plane(ptr, rows, stride, cols):
+    hip = ctypes.CDLL("libamdhip64.so.7")
+    hip.hipMemcpy.restype = ctypes.c_int
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    out = np.empty((rows, stride), dtype=np.uint32)
+    assert hip.hipMemcpy(out.ctypes.data, ptr, out.nbytes, 2) == 0
+    return out[:, :cols]
+
+
+def planes_of(lx, d, w, opts):
+    ix = lx.Index(event_capacity=len(d), options=dict(small_max=0, dbl=0, **opts))
+    ix.reset(w)
+    ix.add_batch(d.creator, d.seq, d.poff, d.par)
+    ix.sync()
+    hb, la, stride, _ = ix.device_planes()
+    B = ix.num_branches()
+    out = (_plane(hb, len(d), stride, B), _plane(la, len(d), stride, B))
+    return ix, out
+
+
+@pytest.mark.parametrize("shape", [(24, 250, 6), (13, 400, 5), (30, 120, 16), (200, 60, 10)])
+def test_cpw8_walk_vs_oracle_and_cpw4(lx, shape):
+    """One walk on 8-column slices (ring slots reused, parents beyond the
+    inline twelve, a partly filled last slice, many slices)."""
+    V, epv, P = shape
+    d = lx.tools.gen_dag(V, epv, P, seed=31 + V)
+    w = [1 + (i * 5) % 9 for i in range(V)]
+    N = len(d)
+    o = corc.OracleIndex(w)
+    assert o.add_batch(d.creator, d.seq, d.poff, d.par) == -1
+    ix8, p8 = planes_of(lx, d, w, {"cpw": 8, "seg_auto": 0})
+    ix4, p4 = planes_of(lx, d, w, {"cpw": 4, "seg_auto": 0})
+    np.testing.assert_array_equal(p8[0], p4[0])
+    np.testing.assert_array_equal(p8[1], p4[1])
+    ev = np.arange(0, N, 5, dtype=np.uint32)
+    for mode in (0, 1):
+        assert np.array_equal(ix8.rows_np(mode, ev)[1], o.rows(mode, ev)[1]), mode
+    qa, qb = lx.tools.fc_queries(d.lamport, 100_000, window=32, seed=V)
+    np.testing.assert_array_equal(ix8.forkless_cause_batch(qa, qb), o.forkless_cause_batch(qa, qb))
+    ix8.close()
+    ix4.close()
+
+
+@pytest.mark.parametrize("shape", [(64, 2100, 10), (100, 1400, 8)])
+def test_cpw8_side_by_side_segments(lx, shape):
+    """Auto segments on 8-column slices (the width auto picks for few columns)
+    byte-identical to one 4-column walk."""
+    V, epv, P = shape
+    d = lx.tools.gen_dag(V, epv, P, seed=5)
+    w = [1] * V
+    ix8, p8 = planes_of(lx, d, w, {"cpw": 8})
+    st = ix8.segment_stats()
+    assert st["segments"] >= 2, st
+    ix1, p1 = planes_of(lx, d, w, {"seg_auto": 0})
+    np.testing.assert_array_equal(p8[0], p1[0])
+    np.testing.assert_array_equal(p8[1], p1[1])
+    ix8.close()
+    ix1.close()
+
+
+def test_cpw8_falls_back_with_forks(lx):
+    """cpw = 8 on a fork epoch walks 4-column slices (8-column slots need
+    packed fork-free values): rows still equal the oracle."""
+    d = lx.tools.gen_dag(20, 150, 6, 3, 4, seed=9)
+    w = [2] * 20
+    o = corc.OracleIndex(w)
+    assert o.add_batch(d.creator, d.seq, d.poff, d.par) == -1
+    ix, _ = planes_of(lx, d, w, {"cpw": 8})
+    ev = np.arange(0, len(d), 3, dtype=np.uint32)
+    for mode in (0, 1):
+        assert np.array_equal(ix.rows_np(mode, ev)[1], o.rows(mode, ev)[1]), mode
+    ix.close()
