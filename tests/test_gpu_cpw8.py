@@ -64,14 +64,14 @@ def test_cpw8_walk_vs_oracle_and_cpw4(lx, shape):
 
 @pytest.mark.parametrize("shape", [(64, 2100, 10), (100, 1400, 8)])
 def test_cpw8_side_by_side_segments(lx, shape):
-    """Auto segments on 8-column slices (the width auto picks for few columns)
-    byte-identical to one 4-column walk."""
+    """Segments side by side on 8-column slices (one k_index_segs launch)
+    byte-identical to one walk."""
     V, epv, P = shape
     d = lx.tools.gen_dag(V, epv, P, seed=5)
     w = [1] * V
-    ix8, p8 = planes_of(lx, d, w, {"cpw": 8})
+    ix8, p8 = planes_of(lx, d, w, {"cpw": 8, "segments": 4})
     st = ix8.segment_stats()
-    assert st["segments"] >= 2, st
+    assert st["segments"] == 4, st
     ix1, p1 = planes_of(lx, d, w, {"seg_auto": 0})
     np.testing.assert_array_equal(p8[0], p1[0])
     np.testing.assert_array_equal(p8[1], p1[1])
