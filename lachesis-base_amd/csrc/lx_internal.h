@@ -514,7 +514,7 @@ struct VoteArgs {
 // then fixed up to the reference's rows.
 constexpr uint32_t kMaxSegments = 64;
 constexpr uint64_t kAutoSegEvents = 32768;
-constexpr float kPass8 = 2.1f;   // pass cost of 8- vs 1-column slices (C3 one walk: 151 ms at 8 columns, 91.5 at 4 = 1.28)
+constexpr float kPass8 = 1.7f;   // pass cost of 8- vs 1-column slices (8 compute + 7 drain waves; C3 one walk: 121.7 ms at 8 columns, 91.4 at 4 = 1.28)
 struct SegArgs {
     uint32_t *hb;
     uint32_t *la;

@@ -320,15 +320,16 @@ struct Ring {
 };
 
 struct alignas(16) WalkShared {
-    uint32_t copied[kND];    // rounds drained (ring and record data consumed) per drain wave
-    uint32_t stored[kND];    // rounds whose global stores are complete per drain wave
+    uint32_t copied[8];      // rounds drained (ring and record data consumed) per drain wave (<= 8 drains)
+    uint32_t stored[8];      // rounds whose global stores are complete per drain wave
     uint32_t req;            // a compute lane waits for `stored`: drains flush
     uint32_t p_issued, p_done;   // LX_WALKER_PROF: loader progress (rounds issued / landed)
 };
 
+template <int ND = kND>
 __device__ __forceinline__ bool round_done(const uint32_t *cnt, uint32_t ev) {
     const uint32_t r = ev / 64;
-    return __hip_atomic_load(cnt + (r % kND), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) > r / kND;
+    return __hip_atomic_load(cnt + (r % ND), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) > r / ND;
 }
 
 typedef uint32_t u4v __attribute__((ext_vector_type(4)));
@@ -545,12 +546,13 @@ __device__ __forceinline__ void blk_fold(const uint32_t pa[3], uint32_t W, uint3
 // The walker kernel.  MASKED: older rows may carry fork marks in bit 31
 // (B > V); PK: 4-column slices with 16-bit packed slot units (every seq of the
 // epoch <= 0xFFFF).
-template <int CPW, int NCW, bool MASKED, bool PK>
+template <int CPW, int NCW, bool MASKED, bool PK, int ND_ = kND>
 __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t w) {
     static_assert(!PK || CPW >= 4, "packed slots: 4- or 8-column slices");
     static_assert(CPW == 1 || CPW == 2 || CPW == 4 || (CPW == 8 && PK && !MASKED), "slot layout");
     static_assert(LX_MAXP == 12, "block walker: 12 inline parents, three per lane of a quad");
-    constexpr int ND = kND;
+    constexpr int ND = ND_;
+    static_assert(ND >= 1 && ND <= 8, "drain waves");
     constexpr int RR = kRR;
     constexpr int NT = 64 * (NCW + 1 + ND);
     constexpr int RQ = LX_REC_Q;
@@ -577,7 +579,7 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t w)
         ring[i] = make_uint4((i == kNullA || (CPW >= 4 && i == 2 * RN + 1)) ? kNullTag : 0u, 0, 0, 0);
     for (int i = threadIdx.x; i < RR / 64; i += NT) rtag[i] = 0;
     for (int i = threadIdx.x; i < CPW * KB; i += NT) brc[i] = make_uint2(0, LX_NONE);
-    if (threadIdx.x < kND) { sh.copied[threadIdx.x] = 0; sh.stored[threadIdx.x] = 0; }
+    if (threadIdx.x < ND) { sh.copied[threadIdx.x] = 0; sh.stored[threadIdx.x] = 0; }
     if (threadIdx.x == 0) { sh.req = 0; sh.p_issued = 0; sh.p_done = 0; }
     __syncthreads();
 
@@ -743,7 +745,7 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t w)
                                 // the other drain may in turn wait for this one: keep
                                 // publishing our completed rounds (divergent: every active lane)
                                 __hip_atomic_store(&sh.stored[d], nd, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                                while (!round_done(sh.stored, pl)) {
+                                while (!round_done<ND>(sh.stored, pl)) {
                                     __hip_atomic_store(&sh.req, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                                     __builtin_amdgcn_s_sleep(1);
                                 }
@@ -1044,7 +1046,7 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t w)
                         for (int c = 0; c < CPW; c++) r[c] = max(r[c], ps.v[c]);
                         ok = true;
                     } else if (max(ps.t0, ps.t1) > lpp + 1) {
-                        if (round_done(sh.stored, lpp)) old = true;
+                        if (round_done<ND>(sh.stored, lpp)) old = true;
                         else __hip_atomic_store(&sh.req, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     }
                 }
@@ -1114,7 +1116,7 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t w)
                 for (int k = 0; k < 3; k++) {
                     const uint32_t x = px[k];
                     if (x == kNullTag || (tg[k][0] == x && tg[k][1] == x) || max(tg[k][0], tg[k][1]) <= x) continue;
-                    if (!round_done(sh.stored, x - 1u)) {
+                    if (!round_done<ND>(sh.stored, x - 1u)) {
                         LX_WP(c_wm++;)
                         __hip_atomic_store(&sh.req, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                         continue;
@@ -1153,17 +1155,17 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t w)
     }
 }
 
-template <int CPW, int NCW, bool MASKED, bool PK>
-__global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index(IndexArgs a) {
-    index_body<CPW, NCW, MASKED, PK>(a, blockIdx.x);
+template <int CPW, int NCW, bool MASKED, bool PK, int ND = kND>
+__global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
+    index_body<CPW, NCW, MASKED, PK, ND>(a, blockIdx.x);
 }
 
 // seg_g Add-order segments of a batch walked by one launch, side by side on
 // idle CUs (a walk of few columns leaves most of them idle): workgroup
 // blockIdx.x walks segment blockIdx.x / (gridDim.x / seg_g) with the
 // segment's own batch window, J table and partial-event lists (lx_segment.hip)
-template <int CPW, int NCW, bool MASKED, bool PK>
-__global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index_segs(IndexArgs a0) {
+template <int CPW, int NCW, bool MASKED, bool PK, int ND = kND>
+__global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index_segs(IndexArgs a0) {
     const uint32_t per = gridDim.x / a0.seg_g, k = blockIdx.x / per;
     IndexArgs a = a0;
     const uint32_t lo = a0.seg_lo[k], off = lo - a0.batch_start;
@@ -1175,20 +1177,20 @@ __global__ __launch_bounds__(64 * (NCW + 1 + kND)) void k_index_segs(IndexArgs a
     a.seg_flag = a0.seg_flag + off;
     a.seg_list = a0.seg_list + off;
     a.seg_count = a0.seg_count + k;
-    index_body<CPW, NCW, MASKED, PK>(a, blockIdx.x - k * per);
+    index_body<CPW, NCW, MASKED, PK, ND>(a, blockIdx.x - k * per);
 }
 
-template <int CPW, int NCW>
+template <int CPW, int NCW, int ND = kND>
 static hipError_t launch_index_t(const IndexArgs &a0, hipStream_t s) {
     IndexArgs a = a0;
     a.n_slices = (a.ncols + CPW - 1) / CPW;
     a.slices_per_xcd = (a.n_slices + 7) / 8;
     const uint32_t grid = a.slices_per_xcd * 8;
-    const dim3 blk(64 * (NCW + 1 + kND));
+    const dim3 blk(64 * (NCW + 1 + ND));
     if constexpr (CPW == 8) {   // packed fork-free epochs only
         if (!a.pack16 || a.mask) return hipErrorInvalidValue;
-        if (a.seg_g) hipLaunchKernelGGL((k_index_segs<CPW, NCW, false, true>), dim3(grid * a.seg_g), blk, 0, s, a);
-        else hipLaunchKernelGGL((k_index<CPW, NCW, false, true>), dim3(grid), blk, 0, s, a);
+        if (a.seg_g) hipLaunchKernelGGL((k_index_segs<CPW, NCW, false, true, ND>), dim3(grid * a.seg_g), blk, 0, s, a);
+        else hipLaunchKernelGGL((k_index<CPW, NCW, false, true, ND>), dim3(grid), blk, 0, s, a);
         return hipGetLastError();
     } else {
     if (a.seg_g) {   // segments side by side (walk_grid-sized blocks of workgroups)
@@ -1228,7 +1230,9 @@ hipError_t launch_index(const IndexArgs &a, hipStream_t s) {
     const uint32_t cpw = a.cpw_hint ? a.cpw_hint : (a.ncols <= 256 ? 1 : a.ncols <= 512 ? 2 : 4);
     if (cpw <= 1) return launch_index_t<1, 8>(a, s);
     if (cpw <= 2) return launch_index_t<2, 8>(a, s);
-    if (cpw == 8) return launch_index_t<8, 11>(a, s);
+    // 8 columns: twice the drains' work per event (HB row, range fills), so
+    // 7 drain waves beside 8 compute waves
+    if (cpw == 8) return launch_index_t<8, 8, 7>(a, s);
     return launch_index_t<4, 11>(a, s);
 }
 
