@@ -25,7 +25,7 @@ def per_kernel(root, counters):
                 if c not in counters:
                     continue
                 name = row["Kernel_Name"]
-                key = "k_fc" if "k_fc<" in name else "k_index" if "k_index<" in name else None
+                key = "k_fc" if "k_fc<" in name else "k_index" if ("k_index<" in name or "k_index_segs<" in name) else None
                 if key is None:
                     continue
                 disp = row.get("Dispatch_Id") or row.get("Correlation_Id")
