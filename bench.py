@@ -725,8 +725,22 @@ def main():
     idx_achieved = idx_bytes / (kidx * 1e-3) / 1e9
 
     traffic, traffic_src = measured_traffic(args.config, args.fc_queries)
-    if shard:
-        traffic = None   # the committed profile is of the single-GPU run
+    if shard or rowseg or solo or args.segments > 1 or args.batch:
+        traffic = None   # the committed profile is of the default single-GPU run
+    # the walk kernel this run timed: one k_index_segs launch when the batch was
+    # walked as side-by-side segments (every segment then reports
+    # the same launch's time), else k_index; the traffic figure must be that
+    # kernel's own, or null
+    walk_kernel = "k_index"
+    if not (shard or rowseg or solo):
+        sg0 = ix.segment_stats()
+        if sg0["segments"] >= 2 and len(set(sg0["walk_ms"])) == 1:
+            walk_kernel = "k_index_segs"
+    idx_traffic = traffic.get(walk_kernel) if traffic else None
+    # compulsory HBM bytes of the walk: every HB and LA row of the epoch written
+    # once at the plane's row stride (8 * stride bytes per event)
+    plane_stride = ix.device_planes()[2]
+    idx_compulsory = 8.0 * plane_stride * N
     result = {
         "metric": "events indexed/sec + ForklessCause queries/sec at 1000 validators, 1/2/4/8 GPU",
         "value": events_per_s,
@@ -752,13 +766,21 @@ def main():
         "assign_and_marks_ms": float(np.mean(k_assign_ms)),
         "roofline": {"bound": "hbm", "kernel": "k_fc (ForklessCause)", "achieved": fc_achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": fc_achieved / HBM_PEAK_GBS,
-                     "traffic": traffic["k_fc"]["hbm_bytes"] if traffic else None,
+                     "traffic": traffic["k_fc"]["hbm_bytes"] if traffic and "k_fc" in traffic else None,
                      "traffic_source": traffic_src,
                      "algorithmic_bytes_per_launch": fc_bytes, "kernel_ms": fc_kernel_ms},
-        "roofline_index": {"bound": "latency (DAG depth); hbm ceiling", "kernel": "k_index", "achieved": idx_achieved,
-                           "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": idx_achieved / HBM_PEAK_GBS,
-                           "traffic": traffic["k_index"]["hbm_bytes"] if traffic else None,
-                           "algorithmic_bytes_per_launch": idx_bytes, "kernel_ms": kidx},
+        "roofline_index": {"bound": "latency (DAG depth x pass latency); hbm ceiling", "kernel": walk_kernel,
+                           "achieved": idx_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                           "frac": idx_achieved / HBM_PEAK_GBS,
+                           "traffic": idx_traffic["hbm_bytes"] if idx_traffic else None,
+                           "traffic_kernel_names": idx_traffic.get("kernel_names") if idx_traffic else None,
+                           "traffic_source": traffic_src if idx_traffic else None,
+                           "algorithmic_bytes_per_launch": idx_bytes, "kernel_ms": kidx,
+                           "compulsory_bytes_per_launch": idx_compulsory,
+                           "compulsory_frac": idx_compulsory / (kidx * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                           "note": "frac follows SURVEY 8d's formula, which counts every parent-row read; the walker "
+                                   "serves those from LDS, so compulsory_frac (HB + LA rows written once, 8 x row "
+                                   "stride bytes per event) is the HBM load: the walk is latency-bound"},
         "host_gen_s": t_gen,
         "fc_spot_checked": spot_n,
     }

@@ -75,7 +75,10 @@ const char *lx_last_error(const lx_index *h);
  *   "la_memset"  1: zero the whole LowestAfter plane at lx_reset instead of the tail pass (before lx_reset)
  *   "shard_wire" LowestAfter exchange width: 0 (auto), 2 or 4 bytes
  *   "timing"     1: HIP-event timing of latency-path launches (lx_last_stats)
- *   "fc_cache"   working set of lx_forkless_cause in events (0: no cache; default 2 V, 512..8192)
+ *   "fc_cache"   working set of lx_forkless_cause in events (0: no cache; default 2 V, 512..8192).
+ *                The result matrix is W^2 bytes of PINNED host memory per handle (64 MiB at
+ *                8192, 256 MiB at the 16384 maximum), allocated on the first lx_forkless_cause;
+ *                if it cannot be pinned the handle answers through lx_forkless_cause_batch
  *   "seg_count", "seg_rank"  G in 2..64 and r < G, before lx_reset: a row-segment rank
  *                (lx_rowseg_*, below); 0 = off
  *   "segments"   G in 2..64: a batch of >= 64 G events is walked as G Add-order segments

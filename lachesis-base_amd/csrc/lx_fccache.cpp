@@ -16,7 +16,7 @@
 //    in insertion order, most of them for the first time by the same event);
 //  * M[W][W] bytes in pinned, device-mapped host memory: M[sa][sb] =
 //    g7[sb] << 1 | FC(ev[sa], ev[sb]), valid while the column's generation
-//    g7[sb] (1..127, bumped when the slot gets a new event) matches -- a slot's
+//    g7[sb] (1..126, bumped when the slot gets a new event) matches -- a slot's
 //    reuse invalidates its column without touching W rows;
 //  * a miss on a row that was just created (a new asking event) or on the last
 //    asking event's row evaluates a against every slot in one k_fc launch
@@ -74,6 +74,9 @@ struct FcCache {
     uint32_t *d_psum = nullptr;
     uint64_t psum_cap = 0;
     uint32_t *d_k = nullptr;                         // kcol | kflag | kw, k_cap entries each
+    // k_B: the branch count the columns were built for; 0 = stale.  A drop can
+    // remove one creator's fork branch and a later Add give the same branch
+    // number to another creator's fork, so every DropNotFlushed clears it
     uint32_t n_k = 0, k_B = 0, k_cap = 0;
     lx_fc_stats st{};
 
@@ -115,7 +118,9 @@ struct FcCache {
         ev[s] = e;
         evk[s] = e;
         map_put(e, s);
-        g7[s] = (uint8_t)(g7[s] % 127u + 1u);
+        // 1..126: a row fill writes 0xFF for a query it cannot answer, and
+        // 0xFF >> 1 = 127 must never equal a valid generation
+        g7[s] = (uint8_t)(g7[s] % 126u + 1u);
         if (g7[s] == 1)   // the generation wrapped: entries of an old occupant could match again
             for (uint32_t r = 0; r < W; r++) M[(uint64_t)r * W + s] = 0;
         memset(M + (uint64_t)s * W, 0, W);
@@ -414,6 +419,7 @@ void fcc_forget_from(lx_index *h, uint64_t n) {
     (void)fcc_quiesce(h, c);
     for (uint32_t s = 0; s < c->used; s++)
         if (c->ev[s] != LX_NONE && c->ev[s] >= n) c->free_slot(s);
+    c->k_B = 0;   // the branch -> creator map may change under the same B
 }
 
 extern "C" {
@@ -434,7 +440,13 @@ int lx_forkless_cause(lx_index *h, uint32_t a, uint32_t b, uint8_t *out) {
         return h->fail(LX_ERR_ARG, "ForklessCause on an unknown event");   // forkless_cause.go:43-61 (crit)
     if (h->sharded() || h->rowseg() || !h->fcc_slots) return lx_forkless_cause_batch(h, 1, &a, &b, out);
     if (!h->fcc) {
+        // W^2 bytes of pinned host memory (64 MiB at the default 8192 slots):
+        // when the host cannot pin them, the handle answers without the cache
         int rc = fcc_make(h);
+        if (rc == LX_ERR_NOMEM) {
+            h->fcc_slots = 0;
+            return lx_forkless_cause_batch(h, 1, &a, &b, out);
+        }
         if (rc) return rc;
         if (fcc_hit(h->fcc, a, b, out)) return h->fail(LX_ERR_STATE, "ForklessCause cache: hit in an empty cache");
     }

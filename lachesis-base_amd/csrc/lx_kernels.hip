@@ -421,6 +421,16 @@ __device__ __forceinline__ uint32_t rec_off(uint32_t slot, uint32_t q) {
 // Per-wave walker counters (LX_PROF=1) are compiled in only with
 // -DLX_WALKER_PROF (make WPROF=1): the increments cost the compute pass
 // several VALU instructions.
+// `make nofill` (build_nofill/, never loaded by the tests or bench.py): the
+// drains skip the LowestAfter range fill, so the LA plane is WRONG; the build
+// exists only to time the walk with and without the 4-B scatter
+// (scripts/probes/nofill_ab.sh)
+#ifdef LX_TIMING_NO_LA_FILL
+constexpr bool kTimingNoLaFill = true;
+#else
+constexpr bool kTimingNoLaFill = false;
+#endif
+
 #ifdef LX_WALKER_PROF
 #define LX_WP(x) x
 #else
@@ -788,7 +798,7 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t w)
                     for (int k = 0; k < CPW; k++)
                         if (valid[k]) hrow[pc[k]] = r[k];
                 }
-                {
+                if (!kTimingNoLaFill) {
                     // LowestAfter range fill: events (col, s), s in (h0, r], are first
                     // observed from branch `br` by this event.
                     uint32_t lo[CPW], hi[CPW];

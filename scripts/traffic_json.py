@@ -15,6 +15,9 @@ import os
 import sys
 
 
+names = {}   # key -> full kernel names seen (template arguments included)
+
+
 def per_kernel(root, counters):
     files = glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True)
     acc = {}
@@ -25,9 +28,14 @@ def per_kernel(root, counters):
                 if c not in counters:
                     continue
                 name = row["Kernel_Name"]
-                key = "k_fc" if "k_fc<" in name else "k_index" if ("k_index<" in name or "k_index_segs<" in name) else None
+                # keyed by the kernel's own name (k_fc, k_index, k_index_segs):
+                # bench.py takes the figure of the kernel it timed, never a
+                # neighbour's
+                key = next((k for k in ("k_index_segs", "k_index", "k_fc") if name.startswith("void lx::" + k + "<")
+                            or name.startswith(k + "<") or ("lx::" + k + "<") in name), None)
                 if key is None:
                     continue
+                names.setdefault(key, set()).add(name.split("(")[0])
                 disp = row.get("Dispatch_Id") or row.get("Correlation_Id")
                 d = acc.setdefault(key, {}).setdefault(c, {})
                 d[disp] = d.get(disp, 0.0) + float(row["Counter_Value"])
@@ -51,7 +59,8 @@ def main():
         rb = 32 * r.get("TCC_EA0_RDREQ_32B", 0) + 64 * r.get("TCC_EA0_RDREQ_64B", 0) + 128 * r.get("TCC_EA0_RDREQ_128B", 0)
         wb = 1024 * w.get("WRITE_SIZE", 0)
         out["kernels"][k] = {"hbm_read_bytes": rb, "hbm_write_bytes": wb, "hbm_bytes": rb + wb, "counters": {**r, **w},
-                             "FETCH_SIZE_KiB_mean": fe.get(k, {}).get("FETCH_SIZE")}
+                             "FETCH_SIZE_KiB_mean": fe.get(k, {}).get("FETCH_SIZE"),
+                             "kernel_names": sorted(names.get(k, ()))}
     json.dump(out, sys.stdout, indent=1)
 
 

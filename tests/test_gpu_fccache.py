@@ -148,3 +148,127 @@ def test_unknown_events_and_reset(lx):
         for b in range(N):
             assert ix.forkless_cause(a, b) == bool(o.forkless_cause(a, b))
     ix.close()
+
+
+def _grid_dag(V, rounds):
+    """Round-robin DAG: e(v, s) has parents [e(v, s-1)] + e(u, s-1) of every
+    other u.  Returns (events as (creator, seq, parents), index of e(v, s))."""
+    evs, at = [], {}
+    for s in range(1, rounds + 1):
+        for v in range(V):
+            par = [] if s == 1 else [at[v, s - 1]] + [at[u, s - 1] for u in range(V) if u != v]
+            at[v, s] = len(evs)
+            evs.append((v, s, par))
+    return evs, at
+
+
+def test_drop_then_other_creators_fork_same_branch_count(lx):
+    """fork of creator 1 (branch V), a tile fill that builds
+    the cheater columns for it, DropNotFlushed, then a fork of creator 3 gets
+    the same branch number V.  The next tile fill must count branch V for
+    creator 3, not creator 1.  Hand-built so the answer depends on it:
+    g = e(0, R+1) observes only creator 3's fork branch (not its original
+    e(3, R)) and e(2, R); FC(g, e(3, R-1)) holds with creators 0, 2 and 3
+    (1 + 1 + 2 >= quorum 4) and fails if branch V is credited to creator 1."""
+    V, R = 4, 4
+    w = [1, 1, 1, 2]
+    evs, at = _grid_dag(V, R)
+    o = corc.OracleIndex(w)
+    ix = lx.Index(options={"fc_cache": 512})
+    ix.reset(w)
+
+    def add(c, s, par):
+        ix.add(c, s, par)
+        o.add(c, s, par)
+        return int(o.num_events()) - 1
+
+    for c, s, par in evs:
+        add(c, s, par)
+    ix.flush()
+    o.flush()
+    n0 = len(evs)
+    # rows of the base events filled before the fork exists
+    for a in range(n0 - V, n0):
+        for b in range(n0):
+            assert ix.forkless_cause(a, b) == bool(o.forkless_cause(a, b))
+    # creator 1 forks at seq R: branch V
+    f1 = add(1, R, [at[1, R - 1]])
+    assert o.num_branches() == V + 1
+    assert ix.forkless_cause(f1, at[0, 1]) == bool(o.forkless_cause(f1, at[0, 1]))   # row fill of f1
+    old = n0 - V
+    assert ix.forkless_cause(old, f1) == bool(o.forkless_cause(old, f1))             # older row: tile fill
+    tiles0 = ix.fc_cache_stats()["tile_fills"]
+    assert tiles0 >= 1
+    ix.drop_not_flushed()
+    o.drop_not_flushed()
+    # creator 3 forks at seq R: the same branch number V, another creator
+    f3 = add(3, R, [at[3, R - 1]])
+    assert o.num_branches() == V + 1 and o.branch(f3) == V
+    g = add(0, R + 1, [at[0, R], f3, at[2, R]])
+    b = at[3, R - 1]
+    assert bool(o.forkless_cause(g, b))                                              # the case the test is about
+    assert ix.forkless_cause(g, b)                                                   # row fill of g (new a)
+    assert ix.forkless_cause(old, g) == bool(o.forkless_cause(old, g))               # older row again: tile fill
+    assert ix.fc_cache_stats()["tile_fills"] > tiles0
+    N = int(o.num_events())
+    for a in range(N):                                                               # all answers from the tile
+        for b2 in range(N):
+            assert ix.forkless_cause(a, b2) == bool(o.forkless_cause(a, b2)), (a, b2)
+    ix.close()
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_drop_readd_different_fork_suffix(lx, seed):
+    """after each DropNotFlushed a DIFFERENT suffix is added,
+    whose forks belong to other creators, with older-row questions
+    interleaved so the cache refills by tiles; every answer equals the oracle."""
+    V = 8
+    w = [5, 4, 3, 3, 2, 2, 1, 1]
+    base = lx.tools.gen_dag(V, 12, 3, seed=40 + seed)
+    nb = len(base)
+    o = corc.OracleIndex(w)
+    ix = lx.Index(options={"fc_cache": 256})
+    ix.reset(w)
+    ix.add_batch(base.creator, base.seq, base.poff, base.par)
+    o.add_batch(base.creator, base.seq, base.poff, base.par)
+    ix.flush()
+    o.flush()
+    rng = np.random.default_rng(seed)
+    last = {}                                 # creator -> last event of the base
+    for e in range(nb):
+        last[int(base.creator[e])] = e
+    seqs = {v: int(base.seq[last[v]]) for v in range(V)}
+    for trial in range(4):
+        forkers = rng.choice(V, size=2, replace=False)
+        n_before = int(o.num_events())
+        tip = dict(last)
+        tipseq = dict(seqs)
+        added = []
+        for step in range(3 * V):
+            v = int(rng.integers(V))
+            par = [tip[v]] + [tip[u] for u in rng.choice(V, size=3, replace=False) if u != v]
+            s = tipseq[v] + 1
+            if v in forkers and step < V and rng.random() < 0.7:
+                # fork: another event on the same self-parent
+                par = [last[v]] + par[1:]
+                s = seqs[v] + 1
+            ix.add(v, s, par)
+            o.add(v, s, par)
+            x = int(o.num_events()) - 1
+            added.append(x)
+            tip[v], tipseq[v] = x, s
+            for b in range(max(0, x - 10), x + 1):
+                assert ix.forkless_cause(x, b) == bool(o.forkless_cause(x, b)), (trial, x, b)
+            if step % 4 == 3:                   # older rows against the new events: tile fills
+                a = int(rng.integers(max(0, n_before - 20), x))
+                for b in added[-4:]:
+                    assert ix.forkless_cause(a, b) == bool(o.forkless_cause(a, b)), (trial, a, b)
+        N = int(o.num_events())
+        for a in range(max(0, N - 40), N):
+            for b in range(max(0, N - 60), N):
+                assert ix.forkless_cause(a, b) == bool(o.forkless_cause(a, b)), (trial, a, b)
+        ix.drop_not_flushed()
+        o.drop_not_flushed()
+        assert int(o.num_events()) == n_before
+    assert ix.fc_cache_stats()["tile_fills"] > 0
+    ix.close()

@@ -412,6 +412,110 @@ def test_full_size_config3_prefix_vs_oracle(lx):
 
 
 @pytest.mark.big_only
+def test_config3_shape_1m_default_two_segments_vs_oracle(lx):
+    """The headline walk as shipped, pinned end to end: BASELINE configs[2]'s
+    shape (V=1000, Zipf stakes, P=10) at 1,000 events per validator (1M
+    events), indexed as one batch with DEFAULT options.  seg_auto then walks
+    it as two side-by-side Add-order segments of 8-column slices (the 10M
+    headline's exact configuration: k_index_segs<8 columns, 7 drains>), so the
+    second segment -- its boundary parents, its partial-event fix-up
+    (k_seg_partial) and its edge LowestAfter pass (k_seg_la_edge) -- lies
+    inside the oracle's coverage.  EVERY HighestBefore and LowestAfter row of
+    the epoch byte-identical, branch IDs, and 1M ForklessCause pairs of which
+    most span the segment boundary (vecengine/index.go:144-233,
+    vecengine/traversal.go:13-37, vecfc/forkless_cause.go:40-82)."""
+    V = 1000
+    w = [(1 << 20) // (i + 1) for i in range(V)]
+    d = lx.tools.gen_dag(V, 1000, 10, seed=11)
+    N = len(d)
+    ix = lx.Index(event_capacity=N)
+    ix.reset(w)
+    br = ix.add_batch(d.creator, d.seq, d.poff, d.par, want_branches=True)
+    st = ix.segment_stats()
+    assert st["segments"] == 2, st                        # the side-by-side form of the headline
+    cut = st["first_event"][1]
+    assert cut == N // 2 // 64 * 64 and st["partial"][1] > 0, st
+    assert np.array_equal(np.asarray(br, dtype=np.uint32), d.creator)   # fork-free: branch = creator
+    o = corc.OracleIndex(w)
+    assert o.add_batch(d.creator, d.seq, d.poff, d.par) == -1
+    ev = np.arange(N, dtype=np.uint32)
+    for mode in (0, 1):
+        for (go, gb), (oo, ob) in _rows_in_chunks(ix, o, mode, ev, 50_000):
+            np.testing.assert_array_equal(go, oo)
+            assert np.array_equal(gb, ob), mode
+    # 1M pairs: 3/4 with a in the first 40k events of segment 1 and b within
+    # 64 Lamport of a (b mostly in segment 0), 1/4 uniform over the epoch
+    lo, hi = cut - 40_000, cut + 40_000
+    qa1, qb1 = lx.tools.fc_queries(d.lamport[lo:hi], 750_000, window=64, seed=12)
+    qa1, qb1 = qa1 + lo, qb1 + lo
+    keep = qa1 >= cut
+    qa2, qb2 = lx.tools.fc_queries(d.lamport, 1_000_000 - int(keep.sum()), window=64, seed=13)
+    qa = np.concatenate([qa1[keep], qa2]).astype(np.uint32)
+    qb = np.concatenate([qb1[keep], qb2]).astype(np.uint32)
+    assert int(((qa >= cut) & (qb < cut)).sum()) > 100_000
+    got = ix.forkless_cause_batch(qa, qb)
+    want = o.forkless_cause_batch_mt(qa, qb, 16)
+    np.testing.assert_array_equal(got, want)
+    assert 0.05 < want.mean() < 0.95                     # both answers occur
+    ix.close()
+
+
+def _planes_equal_on_device(ixs, n, cols, chunk_rows=1 << 18):
+    """Both planes of two handles compared on the GPU, chunk by chunk: the
+    rows are copied device to device into torch buffers (hipMemcpy) and
+    compared there, so 2 x 87 GB never crosses PCIe."""
+    import ctypes
+    import torch
+    hip = ctypes.CDLL("libamdhip64.so.7")
+    hip.hipMemcpy.restype = ctypes.c_int
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    planes = [ix.device_planes() for ix in ixs]
+    strides = {p[2] for p in planes}
+    assert len(strides) == 1
+    stride = strides.pop()
+    bufs = [torch.empty((chunk_rows, stride), dtype=torch.int32, device="cuda") for _ in ixs]
+    for k in (0, 1):                                       # 0: hb, 1: la
+        for lo in range(0, n, chunk_rows):
+            m = min(chunk_rows, n - lo)
+            for buf, p in zip(bufs, planes):
+                src = p[k] + lo * stride * 4
+                assert hip.hipMemcpy(buf.data_ptr(), src, m * stride * 4, 3) == 0
+            torch.cuda.synchronize()
+            if not torch.equal(bufs[0][:m, :cols], bufs[1][:m, :cols]):
+                bad = (bufs[0][:m, :cols] != bufs[1][:m, :cols]).nonzero()[:5].tolist()
+                raise AssertionError(f"plane {k} rows {lo}..{lo + m}: first mismatches {bad}")
+
+
+@pytest.mark.big_only
+def test_full_size_config3_segments_equal_single_walk(lx):
+    """BASELINE configs[2] at full size (10M events, the bench workload): the
+    default handle (two side-by-side segments of 8-column slices) and a
+    seg_auto=0 handle (ONE 4-column walk of the batch) hold byte-identical
+    HighestBefore and LowestAfter planes, every row -- the half of the
+    shipped walk after event 5M included.  The single walk is the one pinned
+    to the oracle at full size on its 500k prefix (above) and in every
+    smaller configs[2]-shaped test."""
+    V = 1000
+    w = [(1 << 20) // (i + 1) for i in range(V)]
+    d = lx.tools.gen_dag(V, 10_000, 10, seed=1)
+    N = len(d)
+    ixs = []
+    for auto in (1, 0):
+        ix = lx.Index(event_capacity=N, options={"seg_auto": auto})
+        ix.reset(w)
+        ix.add_batch(d.creator, d.seq, d.poff, d.par)
+        ix.sync()
+        st = ix.segment_stats()
+        assert st["segments"] == (2 if auto else 0), st
+        ixs.append(ix)
+    _planes_equal_on_device(ixs, N, V)
+    qa, qb = lx.tools.fc_queries(d.lamport, 1 << 22, seed=21)
+    np.testing.assert_array_equal(ixs[0].forkless_cause_batch(qa, qb), ixs[1].forkless_cause_batch(qa, qb))
+    for ix in ixs:
+        ix.close()
+
+
+@pytest.mark.big_only
 def test_full_size_config2_vs_oracle(lx):
     """BASELINE configs[1] at full size (V=100, 1M events) against the C
     oracle over the whole epoch: every HighestBefore row, every LowestAfter row

@@ -114,18 +114,22 @@ def _plane(ptr, rows, stride, cols):
 @pytest.mark.parametrize("G", [4, 8])
 def test_segmented_config3_shape_planes(lx, monkeypatch, G):
     """V = 1000 with Zipf stakes (BASELINE configs[2]'s shape), 150k events:
-    both planes byte-identical to the ordinary walk's, which the parity tests
-    pin to the oracle; a prefix of rows against the oracle directly."""
+    both planes byte-identical to the ordinary walk's (g = 0 with seg_auto = 0:
+    ONE walk of the batch, not the side-by-side segments seg_auto would pick at
+    this size), which the parity tests pin to the oracle; a prefix of rows
+    against the oracle directly."""
     V = 1000
     w = [(1 << 20) // (i + 1) for i in range(V)]
     d = lx.tools.gen_dag(V, 150, 10, seed=1)
     N = len(d)
     planes = []
     for g in (0, G):
-        ix = make_index(lx, monkeypatch, g, cap=N)
+        ix = make_index(lx, monkeypatch, g, cap=N, seg_auto=0 if g == 0 else 1)
         ix.reset(w)
         ix.add_batch(d.creator, d.seq, d.poff, d.par)
         ix.sync()
+        if g == 0:
+            assert ix.segment_stats()["segments"] == 0      # really the single walk
         hb, la, stride, _ = ix.device_planes()
         planes.append((_plane(hb, N, stride, V), _plane(la, N, stride, V)))
         if g:
