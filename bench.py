@@ -556,7 +556,9 @@ def main():
     dag = lx.tools.gen_dag(V, epv, P, cheaters, forks, seed=1)
     if args.order == "level":
         dag = lx.tools.level_order(dag)
-    qa, qb = lx.tools.fc_queries(dag.lamport, args.fc_queries, window=64, seed=7)
+    # every rank asks 2^k queries of the same shape (a uniform over the epoch, b
+    # within 64 Lamport of a); rank 0's are the N=1 set, the others draw their own
+    qa, qb = lx.tools.fc_queries(dag.lamport, args.fc_queries, window=64, seed=7 + rank)
     t_gen = time.perf_counter() - t_gen
     N = len(dag)
     batch = args.batch if args.batch > 0 else N
@@ -573,13 +575,6 @@ def main():
         hi = min(N, lo + batch)
         off = (dag.poff[lo:hi + 1] - dag.poff[lo]).astype(np.uint32)
         batches.append((lo, hi, to_dev(off), int(dag.poff[lo])))
-    if rowseg:
-        # ForklessCause between this rank's own rows: the same query shape
-        # (a uniform, b at most 64 Lamport before it) mapped into [lo, hi)
-        lo_r = N * rank // world // 64 * 64
-        hi_r = N if rank == world - 1 else N * (rank + 1) // world // 64 * 64
-        qa = (lo_r + qa.astype(np.int64) % (hi_r - lo_r)).astype(np.uint32)
-        qb = np.maximum(qa.astype(np.int64) - np.abs(qa.astype(np.int64) - qb.astype(np.int64)) % 4096, lo_r).astype(np.uint32)
     d_qa, d_qb = to_dev(qa), to_dev(qb)
     d_out = torch.empty(args.fc_queries, dtype=torch.uint8, device=dev)
 
@@ -639,6 +634,10 @@ def main():
             evs[0].record(lib_stream)
         if shard or solo:
             ix.forkless_cause_partial_dev(args.fc_queries, d_qa.data_ptr(), d_qb.data_ptr(), d_part.data_ptr())
+        elif rowseg:
+            # any pair: queries to owner(a), remote LowestAfter rows to it, answers
+            # back; the HIP events then bracket the whole protocol
+            rsx.forkless_cause_dev(args.fc_queries, d_qa, d_qb, d_out)
         else:
             ix.forkless_cause_batch_dev(args.fc_queries, d_qa.data_ptr(), d_qb.data_ptr(), d_out.data_ptr())
         if evs is not None:
@@ -709,7 +708,7 @@ def main():
         spot_n = len(got)
 
     units = 1 if (shard or rowseg) else world          # shard / rowseg: the ranks share one epoch
-    fc_units = 1 if shard else world                   # rowseg: every rank answers its own batch of queries
+    fc_units = 1 if shard else world                   # rowseg / replica: every rank asks its own 2^k queries
     events_per_s = N * args.steps * units / t_index
     fc_per_s = args.fc_queries * args.steps * fc_units / t_fc
     B = ix.num_branches()
@@ -797,10 +796,12 @@ def main():
         result["rowseg"] = {"rows": [int(x) for x in ix.rowseg_range()], "walk_ms": sg["walk_ms"][rank],
                             "partial_events": sg["partial"][rank], "partial_ms": sg["partial_ms"], "la_ms": sg["la_ms"],
                             "exchange_ms": float(np.mean(st_x[-args.steps:])) if st_x else None,
-                            "exchange": rsx.last,
+                            "exchange": rsx.last, "fc": rsx.last_fc,
                             "note": "index step = assignment of every event + walk of the own segment + row "
                                     "requests, partial fix-up, LowestAfter pass and triples (exchange_ms), timed "
-                                    "inside value; FC: 2^k queries per rank between its own rows"}
+                                    "inside value; FC: every rank asks 2^k queries of the N=1 shape over the whole "
+                                    "epoch, routed to owner(a) with the LowestAfter rows of remote b shipped to it "
+                                    "(DESIGN.md 6c), timed inside fc_queries_per_sec"}
     if shard or solo:
         wire = sorted(set(w for w in sx.last_wire[0] if w)) if shard and getattr(sx, "last_wire", None) else \
             [ix.shard_wire_bytes()]

@@ -346,9 +346,10 @@ int lx_last_segment_stats(const lx_index *h, lx_seg_stats *out);
  *     each owner rank, lx_rowseg_la_fetch copies them (grouped by owner) to a
  *     device buffer; each owner lx_rowseg_la_apply's what it gets;
  * then lx_rowseg_finish.  After it, ForklessCause answers queries between own
- * events (others are LX_ERR_ARG); getters, write-back, DropNotFlushed and the
- * abft / emitter views need a whole index (LX_ERR_STATE).  Every call has
- * completed on the device when it returns. */
+ * events, and any pair of the epoch through the cross-rank protocol below;
+ * getters, write-back, DropNotFlushed and the abft / emitter views need a whole
+ * index (LX_ERR_STATE).  Every call has completed on the device when it
+ * returns. */
 int lx_rowseg_range(const lx_index *h, uint32_t *lo, uint32_t *hi);
 int lx_rowseg_of(const lx_index *h, uint32_t *rank, uint32_t *count);   /* options seg_rank / seg_count (1: whole) */
 
@@ -373,6 +374,34 @@ int lx_rowseg_la(lx_index *h, uint64_t *counts);
 int lx_rowseg_la_fetch(lx_index *h, uint32_t *triples_dev);
 int lx_rowseg_la_apply(lx_index *h, uint64_t n, const uint32_t *triples_dev);
 int lx_rowseg_finish(lx_index *h);
+
+/* ForklessCause(a, b) of ANY pair of a row-segmented epoch
+ * (vecfc/forkless_cause.go:40-82): answered on owner(a)
+ * -- HB(a) is there -- with LA(b) shipped from owner(b) when b lies in another
+ * segment.  Every rank calls collectively, after lx_rowseg_finish, with its own
+ * batch of n queries (device arrays):
+ *   lx_rowseg_fc_route   -> the queries grouped by owner(a) into ra / rb, the
+ *                           permutation perm (n each), counts[G];
+ *   (ra, rb to their owners: m received pairs)
+ *   lx_rowseg_fc_need    -> the distinct b of the received pairs outside this
+ *                           rank's rows, grouped by owner, into ids (capacity >=
+ *                           min(m, events)), counts[G];
+ *   (ids to their owners) lx_rowseg_la_serve -> their LA rows (lx_rowseg_row_words
+ *                           words each); (rows back) lx_rowseg_la_store;
+ *   lx_forkless_cause_batch_dev over the m received pairs (b may now be any
+ *                           stored row; lx_sync before moving the answers);
+ *   (answers back)        lx_rowseg_fc_unroute -> out[i] for the caller's query i.
+ * lx_rowseg_forkless_cause runs the same over RCCL (lx_rowseg_comm_create). */
+int lx_rowseg_fc_route(lx_index *h, uint64_t n, const uint32_t *qa_dev, const uint32_t *qb_dev, uint32_t *ra_dev,
+                       uint32_t *rb_dev, uint32_t *perm_dev, uint64_t *counts);
+int lx_rowseg_fc_need(lx_index *h, uint64_t m, const uint32_t *ra_dev, const uint32_t *rb_dev, uint32_t *ids_dev,
+                      uint64_t cap, uint64_t *counts);
+int lx_rowseg_la_serve(lx_index *h, uint64_t n, const uint32_t *ids_dev, uint32_t *rows_dev);
+int lx_rowseg_la_store(lx_index *h, uint64_t n, const uint32_t *ids_dev, const uint32_t *rows_dev);
+int lx_rowseg_fc_unroute(lx_index *h, uint64_t n, const uint32_t *perm_dev, const uint8_t *ans_dev, uint8_t *out_dev);
+/* stats (optional): queries routed away, pairs answered here, LA rows received, sent */
+int lx_rowseg_forkless_cause(lx_shard_comm *c, uint64_t n, const uint32_t *qa_dev, const uint32_t *qb_dev,
+                             uint8_t *out_dev, uint64_t stats[4]);
 
 /* Device views for benchmarks/tests (valid until the next add/reset). */
 int lx_device_planes(lx_index *h, void **hb, void **la, uint32_t *stride, void **stream);

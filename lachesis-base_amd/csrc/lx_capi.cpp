@@ -811,6 +811,8 @@ int lx_fc_args(lx_index *h, uint64_t n, const uint32_t *a, const uint32_t *b, ui
     f.stride = h->pstride;
     f.n_events = h->rowseg() ? h->rs_hi : (uint32_t)h->n_events;
     f.ev_lo = h->rowseg() ? h->rs_lo : 0u;
+    f.b_stamp = h->rowseg() ? h->rs_stamp : nullptr;
+    f.n_all = (uint32_t)h->n_events;
     f.n = n;
     f.qa = a;
     f.qb = b;

@@ -255,6 +255,17 @@ struct lx_index {
     uint64_t rs_need_cap = 0, rs_req_cap = 0, rs_ids_cap = 0, rs_out_cap = 0, rs_send_cap = 0, rs_ctr_cap = 0;
     uint64_t rs_out_per = 0;               // triples per destination in rs_out
     uint64_t rs_nsend = 0;                 // triples packed in rs_send (lx_rowseg_la)
+    // ForklessCause across ranks (lx_rowseg_fc_*): per event the stamp of its LA
+    // row (2 gen: asked in batch gen, 2 gen + 1: received), the batch counter,
+    // route / sort scratch
+    uint32_t *rs_stamp = nullptr;
+    uint64_t rs_stamp_cap = 0;
+    uint32_t rs_gen = 0;
+    uint32_t *rsq_scratch = nullptr, *rsq_list = nullptr, *rsq_ctr = nullptr;
+    uint64_t rsq_scratch_cap = 0, rsq_list_cap = 0, rsq_ctr_cap = 0;
+    void *rsq_tmp = nullptr;
+    size_t rsq_tmp_bytes = 0;
+    uint32_t rsq_nlist = 0;                // distinct remote rows of the last lx_rowseg_fc_need
     bool rowseg() const { return rs_count > 1; }
 
     int fail(int code, const char *fmt, ...) {

@@ -141,6 +141,10 @@ struct FcArgs {
     uint64_t stride;
     uint32_t n_events;
     uint32_t ev_lo;              // row-segment rank: queries must lie in [ev_lo, n_events)
+    // row-segment rank: b may also be another segment's event whose final LA
+    // row was received (b_stamp[b] odd; lx_rowseg_fc.hip); NULL elsewhere
+    const uint32_t *b_stamp;
+    uint32_t n_all;              // events of the epoch (b_stamp's length)
     uint64_t n;
     const uint32_t *qa;
     const uint32_t *qb;
@@ -561,6 +565,15 @@ struct RsArgs {
     uint32_t *remaining;
 };
 
+// ForklessCause across row-segment ranks (lx_rowseg_fc.hip)
+struct RsqArgs {
+    uint32_t G, self;            // ranks, this rank
+    uint32_t n_all;              // events of the epoch
+    uint32_t lo, hi;             // own rows
+    uint32_t B;                  // words per shipped LA row
+    uint32_t seg_lo[kMaxSegments + 1];
+};
+
 // kernel launchers (lx_kernels.hip); all enqueue on `s`
 namespace lx {
 hipError_t launch_seg_tables(const SegArgs &a, hipStream_t s);
@@ -568,6 +581,19 @@ hipError_t launch_seg_partial(const SegArgs &a, uint32_t k, uint32_t count, hipS
 hipError_t launch_seg_edges(const SegArgs &a, uint32_t k, uint32_t n_partial, hipStream_t s);
 hipError_t launch_seg_la_edge(const SegArgs &a, uint32_t k, uint32_t count, hipStream_t s);
 hipError_t launch_rs_refs(const SegArgs &a, const RsArgs &r, uint32_t n_partial, hipStream_t s);
+hipError_t rsq_tmp_bytes(uint64_t n, uint32_t G, size_t *bytes);
+hipError_t launch_rsq_route(const RsqArgs &a, const uint32_t *qa, const uint32_t *qb, uint64_t n, uint32_t *scratch,
+                            void *tmp, size_t tmp_bytes, uint32_t *ra, uint32_t *rb, uint32_t *perm, uint32_t *counts,
+                            hipStream_t s);
+hipError_t launch_rsq_need(const RsqArgs &a, const uint32_t *ra, const uint32_t *rb, uint64_t m, uint32_t *stamp,
+                           uint32_t want, uint32_t *list, uint32_t *count, hipStream_t s);
+hipError_t launch_rsq_group(const RsqArgs &a, const uint32_t *list, uint32_t n, void *tmp, size_t tmp_bytes,
+                            uint32_t *ids, uint32_t *counts, hipStream_t s);
+hipError_t launch_rsq_la_gather(const RsqArgs &a, const uint32_t *la, uint64_t stride, const uint32_t *ids,
+                                uint32_t n, uint32_t *rows, hipStream_t s);
+hipError_t launch_rsq_la_store(const RsqArgs &a, uint32_t *la, uint64_t stride, const uint32_t *ids, uint32_t n,
+                               const uint32_t *rows, uint32_t *stamp, uint32_t arrived, hipStream_t s);
+hipError_t launch_rsq_unroute(const uint32_t *perm, const uint8_t *ans, uint64_t n, uint8_t *out, hipStream_t s);
 hipError_t launch_rs_bucket(const SegArgs &a, const RsArgs &r, uint32_t n_req, uint32_t *out, uint32_t *counts,
                             hipStream_t s);
 hipError_t launch_rs_gather(const RsArgs &r, const uint32_t *ids, uint32_t n, uint32_t *rows, uint32_t *ready,

@@ -1300,6 +1300,16 @@ __device__ __forceinline__ uint32_t fc_term(uint32_t l, uint32_t h, uint32_t w, 
     return ((l - 1u) < h) ? w : 0u;               // l != 0 && l <= h
 }
 
+// a query the handle cannot answer: a outside [ev_lo, n_events); b too,
+// unless a row-segment rank received b's final LowestAfter row (b_stamp odd)
+__device__ __forceinline__ bool fc_bad(const FcArgs &a, uint32_t A, uint32_t Bq) {
+    const bool b_out = (Bq >= a.n_events) | (Bq < a.ev_lo);
+    bool bad = (A >= a.n_events) | (A < a.ev_lo);
+    if (a.b_stamp) bad |= b_out && (Bq >= a.n_all || !(a.b_stamp[Bq] & 1u));
+    else bad |= b_out;
+    return bad;
+}
+
 template <int LPQ, bool FORKS>
 __global__ __launch_bounds__(256) void k_fc(FcArgs a) {
     const int lane = threadIdx.x % LPQ;
@@ -1319,7 +1329,7 @@ __global__ __launch_bounds__(256) void k_fc(FcArgs a) {
     }
     for (uint64_t q = blockIdx.x * qpb + threadIdx.x / LPQ; q < a.n; q += (uint64_t)gridDim.x * qpb) {
         uint32_t A = a.qa[a.qa_bcast ? 0 : q], Bq = a.qb[q];
-        const bool bad = (A >= a.n_events) | (Bq >= a.n_events) | (A < a.ev_lo) | (Bq < a.ev_lo);
+        const bool bad = fc_bad(a, A, Bq);
         if (bad) { A = 0; Bq = 0; }
         // FORKS, lane 0: the early-false inputs first (their loads overlap the rows')
         uint32_t e_bb = 0, e_cb = 0;
@@ -1435,7 +1445,7 @@ __global__ __launch_bounds__(256) void k_fc_fk(FcArgs a) {
     }
     for (uint64_t q = blockIdx.x * qpb + threadIdx.x / LPQ; q < a.n; q += (uint64_t)gridDim.x * qpb) {
         uint32_t A = a.qa[a.qa_bcast ? 0 : q], Bq = a.qb[q];
-        const bool bad = (A >= a.n_events) | (Bq >= a.n_events) | (A < a.ev_lo) | (Bq < a.ev_lo);
+        const bool bad = fc_bad(a, A, Bq);
         if (bad) { A = 0; Bq = 0; }
         uint32_t e_bb = 0, e_cb = 0;
         if (lane == 0) {

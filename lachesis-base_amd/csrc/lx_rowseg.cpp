@@ -26,6 +26,8 @@ using namespace lxi;
 
 namespace {
 
+
+
 SegArgs rs_seg_args(lx_index *h) {
     SegArgs a{};
     a.hb = h->hb;
@@ -71,6 +73,33 @@ RsArgs rs_args(lx_index *h) {
     return r;
 }
 
+RsqArgs rsq_args(const lx_index *h) {
+    RsqArgs a{};
+    a.G = h->rs_count;
+    a.self = h->rs_rank;
+    a.n_all = (uint32_t)h->n_events;
+    a.lo = h->rs_lo;
+    a.hi = h->rs_hi;
+    a.B = h->B;
+    for (uint32_t q = 0; q <= h->rs_count; q++) a.seg_lo[q] = h->rs_seg_lo[q];
+    return a;
+}
+
+int rsq_tmp(lx_index *h, uint64_t n) {
+    size_t need = 0;
+    HIPCHK(h, lx::rsq_tmp_bytes(n ? n : 1, h->rs_count, &need));
+    if (need <= h->rsq_tmp_bytes && h->rsq_tmp) return 0;
+    if (h->rsq_tmp) {
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        (void)hipFree(h->rsq_tmp);
+        h->rsq_tmp = nullptr;
+        h->rsq_tmp_bytes = 0;
+    }
+    HIPCHK(h, hipMalloc(&h->rsq_tmp, need ? need : 1));
+    h->rsq_tmp_bytes = need;
+    return 0;
+}
+
 int rs_check(lx_index *h, int state) {
     if (!h) return LX_ERR_ARG;
     if (!h->rowseg()) return h->fail(LX_ERR_STATE, "not a row-segment rank (options seg_count / seg_rank)");
@@ -97,11 +126,17 @@ int rs_fix_partials(lx_index *h) {
 }  // namespace
 
 void rs_free(lx_index *h) {
-    void *p[] = {h->rs_need, h->rs_req, h->rs_ctr, h->rs_ids, h->rs_out, h->rs_send};
+    void *p[] = {h->rs_need, h->rs_req, h->rs_ctr, h->rs_ids, h->rs_out, h->rs_send,
+                 h->rs_stamp, h->rsq_scratch, h->rsq_list, h->rsq_ctr, h->rsq_tmp};
     for (void *q : p)
         if (q) (void)hipFree(q);
     h->rs_need = h->rs_req = h->rs_ctr = h->rs_ids = h->rs_out = h->rs_send = nullptr;
     h->rs_need_cap = h->rs_req_cap = h->rs_ids_cap = h->rs_out_cap = h->rs_send_cap = h->rs_ctr_cap = 0;
+    h->rs_stamp = h->rsq_scratch = h->rsq_list = h->rsq_ctr = nullptr;
+    h->rsq_tmp = nullptr;
+    h->rs_stamp_cap = h->rsq_scratch_cap = h->rsq_list_cap = h->rsq_ctr_cap = 0;
+    h->rsq_tmp_bytes = 0;
+    h->rs_gen = 0;
     h->rs_state = 0;
 }
 
@@ -129,6 +164,10 @@ int rs_begin(lx_index *h, IndexArgs ia, const uint32_t *poff, hipStream_t s) {
         h->seg_ev.push_back(e);
     }
     h->rs_state = 0;
+    // no LowestAfter row of another segment has been received in this epoch
+    if ((rc = grow_scratch(h, &h->rs_stamp, &h->rs_stamp_cap, (uint64_t)n))) return rc;
+    HIPCHK(h, hipMemsetAsync(h->rs_stamp, 0, (uint64_t)n * 4, s));
+    h->rs_gen = 0;
     SegArgs a = rs_seg_args(h);
     HIPCHK(h, lx::launch_seg_tables(a, s));
     // the own rows' LowestAfter is written by the own pass and the others' triples only
@@ -332,6 +371,90 @@ int lx_rowseg_finish(lx_index *h) {
     }
     HIPCHK(h, hipStreamSynchronize(h->stream));
     h->rs_state = 4;
+    return 0;
+}
+
+// ---- ForklessCause of any pair of the epoch (lx_rowseg_fc.hip)
+
+int lx_rowseg_fc_route(lx_index *h, uint64_t n, const uint32_t *qa, const uint32_t *qb, uint32_t *ra, uint32_t *rb,
+                       uint32_t *perm, uint64_t *counts) {
+    int rc;
+    if ((rc = rs_check(h, 4))) return rc;
+    if (!counts || (n && (!qa || !qb || !ra || !rb || !perm))) return LX_ERR_ARG;
+    if (n >= 0x7FFFFFFFull) return h->fail(LX_ERR_ARG, "too many queries in one batch");
+    const uint32_t G = h->rs_count;
+    if ((rc = grow_scratch(h, &h->rsq_scratch, &h->rsq_scratch_cap, 3 * n + 3)) ||
+        (rc = grow_scratch(h, &h->rsq_ctr, &h->rsq_ctr_cap, (uint64_t)2 * kMaxSegments + 2)) || (rc = rsq_tmp(h, n)))
+        return rc;
+    const RsqArgs a = rsq_args(h);
+    HIPCHK(h, lx::launch_rsq_route(a, qa, qb, n, h->rsq_scratch, h->rsq_tmp, h->rsq_tmp_bytes, ra, rb, perm, h->rsq_ctr,
+                                   h->stream));
+    uint32_t c[kMaxSegments];
+    HIPCHK(h, hipMemcpyAsync(c, h->rsq_ctr, 4ull * G, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    for (uint32_t q = 0; q < G; q++) counts[q] = c[q];
+    return 0;
+}
+
+int lx_rowseg_fc_need(lx_index *h, uint64_t m, const uint32_t *ra, const uint32_t *rb, uint32_t *ids, uint64_t cap,
+                      uint64_t *counts) {
+    int rc;
+    if ((rc = rs_check(h, 4))) return rc;
+    if (!counts || (m && (!ra || !rb))) return LX_ERR_ARG;
+    const uint32_t G = h->rs_count;
+    if (h->rs_gen >= 0x7FFFFFF0u) {   // stamps about to wrap: forget every received row
+        HIPCHK(h, hipMemsetAsync(h->rs_stamp, 0, h->n_events * 4, h->stream));
+        h->rs_gen = 0;
+    }
+    h->rs_gen++;
+    const uint64_t lim = std::min<uint64_t>(m, h->n_events);
+    if ((rc = grow_scratch(h, &h->rsq_list, &h->rsq_list_cap, lim + 1)) ||
+        (rc = grow_scratch(h, &h->rsq_ctr, &h->rsq_ctr_cap, (uint64_t)2 * kMaxSegments + 2)))
+        return rc;
+    const RsqArgs a = rsq_args(h);
+    uint32_t *cnt = h->rsq_ctr + kMaxSegments;
+    HIPCHK(h, hipMemsetAsync(cnt, 0, 4, h->stream));
+    HIPCHK(h, lx::launch_rsq_need(a, ra, rb, m, h->rs_stamp, 2 * h->rs_gen, h->rsq_list, cnt, h->stream));
+    uint32_t nl = 0;
+    HIPCHK(h, hipMemcpyAsync(&nl, cnt, 4, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    h->rsq_nlist = nl;
+    if (nl && (!ids || cap < nl)) return h->fail(LX_ERR_ARG, "id buffer of %llu < %u rows", (unsigned long long)cap, nl);
+    if ((rc = rsq_tmp(h, nl))) return rc;
+    HIPCHK(h, lx::launch_rsq_group(a, h->rsq_list, nl, h->rsq_tmp, h->rsq_tmp_bytes, ids, h->rsq_ctr, h->stream));
+    uint32_t c[kMaxSegments];
+    HIPCHK(h, hipMemcpyAsync(c, h->rsq_ctr, 4ull * G, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    for (uint32_t q = 0; q < G; q++) counts[q] = c[q];
+    return 0;
+}
+
+int lx_rowseg_la_serve(lx_index *h, uint64_t n, const uint32_t *ids, uint32_t *rows) {
+    int rc;
+    if ((rc = rs_check(h, 4))) return rc;
+    if (n && (!ids || !rows)) return LX_ERR_ARG;
+    if (n > 0xFFFFFFFFull) return LX_ERR_ARG;
+    HIPCHK(h, lx::launch_rsq_la_gather(rsq_args(h), h->la, h->pstride, ids, (uint32_t)n, rows, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+int lx_rowseg_la_store(lx_index *h, uint64_t n, const uint32_t *ids, const uint32_t *rows) {
+    int rc;
+    if ((rc = rs_check(h, 4))) return rc;
+    if (n && (!ids || !rows)) return LX_ERR_ARG;
+    if (n > 0xFFFFFFFFull) return LX_ERR_ARG;
+    HIPCHK(h, lx::launch_rsq_la_store(rsq_args(h), h->la, h->pstride, ids, (uint32_t)n, rows, h->rs_stamp,
+                                      2 * h->rs_gen + 1, h->stream));
+    return 0;
+}
+
+int lx_rowseg_fc_unroute(lx_index *h, uint64_t n, const uint32_t *perm, const uint8_t *ans, uint8_t *out) {
+    int rc;
+    if ((rc = rs_check(h, 4))) return rc;
+    if (n && (!perm || !ans || !out)) return LX_ERR_ARG;
+    HIPCHK(h, lx::launch_rsq_unroute(perm, ans, n, out, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
     return 0;
 }
 

@@ -34,7 +34,12 @@ struct RowsegExchangeStats {
     uint64_t rows_received = 0, la_sent = 0, la_received = 0;
 };
 
-enum RowsegBuf : int { kRsIds = 0, kRsAsked, kRsOutRows, kRsOutReady, kRsGotRows, kRsGotReady, kRsLaSend, kRsLaRecv, kRsBufs };
+enum RowsegBuf : int {
+    kRsIds = 0, kRsAsked, kRsOutRows, kRsOutReady, kRsGotRows, kRsGotReady, kRsLaSend, kRsLaRecv,
+    // ForklessCause across ranks (rowseg_fc_run)
+    kRqA, kRqB, kRqPerm, kRqRecvA, kRqRecvB, kRqIds, kRqAsked, kRqRows, kRqGotRows, kRqAns, kRqAnsBack,
+    kRsBufs
+};
 
 template <class Ops, class Net>
 int rowseg_exchange_run(Ops &ops, Net &net, uint32_t G, RowsegExchangeStats &st) {
@@ -92,6 +97,70 @@ int rowseg_exchange_run(Ops &ops, Net &net, uint32_t G, RowsegExchangeStats &st)
     st.la_sent = ns;
     st.la_received = nr;
     return ops.finish();
+}
+
+struct RowsegFcStats {
+    uint64_t routed_away = 0, answered = 0, rows_received = 0, rows_sent = 0;
+};
+
+// ForklessCause of any pair of the epoch (lx_rowseg_fc_* in lachesis_hip.h,
+// DESIGN.md section 6c): queries to owner(a), LA rows of remote b to owner(a),
+// answers back.  More Ops: fc_route(n, qa, qb, ra, rb, perm, counts[G]),
+// fc_need(m, ra, rb, ids, cap, counts[G]), la_serve(n, ids, rows),
+// la_store(n, ids, rows), fc_pairs(m, ra, rb, ans) (completed on return),
+// fc_unroute(n, perm, ans, out), rank().
+template <class Ops, class Net>
+int rowseg_fc_run(Ops &ops, Net &net, uint32_t G, uint64_t n, const uint32_t *qa, const uint32_t *qb, uint8_t *out,
+                  RowsegFcStats &st) {
+    st = RowsegFcStats{};
+    int rc;
+    uint32_t W = 0;
+    if ((rc = ops.row_words(&W))) return rc;
+    const uint32_t me = ops.rank();
+    std::vector<uint64_t> send_n(G), recv_n(G), sb(G), rb(G);
+    uint32_t *ra = static_cast<uint32_t *>(ops.buf(kRqA, 4 * (n + 1)));
+    uint32_t *rbq = static_cast<uint32_t *>(ops.buf(kRqB, 4 * (n + 1)));
+    uint32_t *perm = static_cast<uint32_t *>(ops.buf(kRqPerm, 4 * (n + 1)));
+    if (!ra || !rbq || !perm) return LX_ERR_NOMEM;
+    if ((rc = ops.fc_route(n, qa, qb, ra, rbq, perm, send_n.data()))) return rc;
+    for (uint32_t q = 0; q < G; q++)
+        if (q != me) st.routed_away += send_n[q];
+    if ((rc = net.counts(send_n.data(), recv_n.data()))) return rc;
+    uint64_t m = 0;
+    for (uint32_t q = 0; q < G; q++) m += recv_n[q];
+    uint32_t *xa = static_cast<uint32_t *>(ops.buf(kRqRecvA, 4 * (m + 1)));
+    uint32_t *xb = static_cast<uint32_t *>(ops.buf(kRqRecvB, 4 * (m + 1)));
+    uint8_t *ans = static_cast<uint8_t *>(ops.buf(kRqAns, m + 1));
+    uint8_t *back = static_cast<uint8_t *>(ops.buf(kRqAnsBack, n + 1));
+    if (!xa || !xb || !ans || !back) return LX_ERR_NOMEM;
+    for (uint32_t q = 0; q < G; q++) sb[q] = 4 * send_n[q], rb[q] = 4 * recv_n[q];
+    if ((rc = net.move(ra, sb.data(), xa, rb.data())) || (rc = net.move(rbq, sb.data(), xb, rb.data()))) return rc;
+    // LA rows of the remote b
+    std::vector<uint64_t> need_n(G), ask_n(G);
+    uint32_t *ids = static_cast<uint32_t *>(ops.buf(kRqIds, 4 * (m + 1)));
+    if (!ids) return LX_ERR_NOMEM;
+    if ((rc = ops.fc_need(m, xa, xb, ids, m, need_n.data()))) return rc;
+    if ((rc = net.counts(need_n.data(), ask_n.data()))) return rc;
+    uint64_t nn = 0, na = 0;
+    for (uint32_t q = 0; q < G; q++) nn += need_n[q], na += ask_n[q];
+    uint32_t *asked = static_cast<uint32_t *>(ops.buf(kRqAsked, 4 * (na + 1)));
+    uint32_t *rows = static_cast<uint32_t *>(ops.buf(kRqRows, 4 * (na * W + 1)));
+    uint32_t *got = static_cast<uint32_t *>(ops.buf(kRqGotRows, 4 * (nn * W + 1)));
+    if (!asked || !rows || !got) return LX_ERR_NOMEM;
+    for (uint32_t q = 0; q < G; q++) sb[q] = 4 * need_n[q], rb[q] = 4 * ask_n[q];
+    if ((rc = net.move(ids, sb.data(), asked, rb.data()))) return rc;
+    if ((rc = ops.la_serve(na, asked, rows))) return rc;
+    for (uint32_t q = 0; q < G; q++) sb[q] = 4ull * W * ask_n[q], rb[q] = 4ull * W * need_n[q];
+    if ((rc = net.move(rows, sb.data(), got, rb.data()))) return rc;
+    if ((rc = ops.la_store(nn, ids, got))) return rc;
+    st.rows_received = nn;
+    st.rows_sent = na;
+    // the pairs, then the answers back in the order they came
+    if ((rc = ops.fc_pairs(m, xa, xb, ans))) return rc;
+    st.answered = m;
+    for (uint32_t q = 0; q < G; q++) sb[q] = recv_n[q], rb[q] = send_n[q];
+    if ((rc = net.move(ans, sb.data(), back, rb.data()))) return rc;
+    return ops.fc_unroute(n, perm, back, out);
 }
 
 }  // namespace lx

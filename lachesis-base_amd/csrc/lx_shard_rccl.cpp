@@ -357,6 +357,28 @@ struct RcclRowOps {
     int la_apply(uint64_t n, const uint32_t *buf) { return c->index(lx_rowseg_la_apply(c->ix, n, buf), "lx_rowseg_la_apply"); }
     int finish() { return c->index(lx_rowseg_finish(c->ix), "lx_rowseg_finish"); }
     void *buf(int k, size_t bytes) { return c->grow(&c->rbuf[k], &c->rcap[k], bytes) ? nullptr : c->rbuf[k]; }
+    // ForklessCause across ranks (rowseg_fc_run)
+    uint32_t rank() const { return c->rank; }
+    int fc_route(uint64_t n, const uint32_t *qa, const uint32_t *qb, uint32_t *ra, uint32_t *rb, uint32_t *perm,
+                 uint64_t *counts) {
+        return c->index(lx_rowseg_fc_route(c->ix, n, qa, qb, ra, rb, perm, counts), "lx_rowseg_fc_route");
+    }
+    int fc_need(uint64_t m, const uint32_t *ra, const uint32_t *rb, uint32_t *ids, uint64_t cap, uint64_t *counts) {
+        return c->index(lx_rowseg_fc_need(c->ix, m, ra, rb, ids, cap, counts), "lx_rowseg_fc_need");
+    }
+    int la_serve(uint64_t n, const uint32_t *ids, uint32_t *rows) {
+        return c->index(lx_rowseg_la_serve(c->ix, n, ids, rows), "lx_rowseg_la_serve");
+    }
+    int la_store(uint64_t n, const uint32_t *ids, const uint32_t *rows) {
+        return c->index(lx_rowseg_la_store(c->ix, n, ids, rows), "lx_rowseg_la_store");
+    }
+    int fc_pairs(uint64_t m, const uint32_t *a, const uint32_t *b, uint8_t *ans) {
+        LXC(c->index(lx_forkless_cause_batch_dev(c->ix, m, a, b, ans, nullptr), "lx_forkless_cause_batch_dev"));
+        return c->index(lx_sync(c->ix), "lx_sync");
+    }
+    int fc_unroute(uint64_t n, const uint32_t *perm, const uint8_t *ans, uint8_t *out) {
+        return c->index(lx_rowseg_fc_unroute(c->ix, n, perm, ans, out), "lx_rowseg_fc_unroute");
+    }
 };
 
 // the collectives on the handle's stream; the own block moves by a local copy
@@ -432,6 +454,35 @@ int lx_rowseg_exchange(lx_shard_comm *c, uint64_t stats[4]) {
         stats[1] = st.rows_received;
         stats[2] = st.la_sent;
         stats[3] = st.la_received;
+    }
+    return 0;
+}
+
+int lx_rowseg_forkless_cause(lx_shard_comm *c, uint64_t n, const uint32_t *qa, const uint32_t *qb, uint8_t *out,
+                             uint64_t stats[4]) {
+    if (!c) return LX_ERR_ARG;
+    if (!c->rowseg) return c->fail(LX_ERR_STATE, "not a row-segment communicator (lx_rowseg_comm_create)");
+    LXC(c->hip(hipSetDevice(c->device), "hipSetDevice"));
+    const uint32_t G = c->nranks;
+    if (G == 1) {   // a whole index
+        LXC(c->index(lx_forkless_cause_batch_dev(c->ix, n, qa, qb, out, nullptr), "lx_forkless_cause_batch_dev"));
+        return c->index(lx_sync(c->ix), "lx_sync");
+    }
+    if (!c->udev) LXC(c->hip(hipMalloc(reinterpret_cast<void **>(&c->udev), 8ull * (2 * G + 1)), "hipMalloc"));
+    RcclRowOps ops{c};
+    RcclRowNet net{c};
+    c->err.clear();
+    lx::RowsegFcStats st;
+    const int rc = lx::rowseg_fc_run(ops, net, G, n, qa, qb, out, st);
+    if (rc) {
+        if (c->err.empty()) c->fail(rc, "row-segment ForklessCause failed (%d)", rc);
+        return rc;
+    }
+    if (stats) {
+        stats[0] = st.routed_away;
+        stats[1] = st.answered;
+        stats[2] = st.rows_received;
+        stats[3] = st.rows_sent;
     }
     return 0;
 }

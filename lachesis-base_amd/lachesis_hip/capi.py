@@ -71,6 +71,12 @@ SIGNATURES = [
     ("lx_rowseg_la_fetch", ctypes.c_int, [vp, vp]),
     ("lx_rowseg_la_apply", ctypes.c_int, [vp, ctypes.c_uint64, vp]),
     ("lx_rowseg_finish", ctypes.c_int, [vp]),
+    ("lx_rowseg_fc_route", ctypes.c_int, [vp, ctypes.c_uint64, vp, vp, vp, vp, vp, u64p]),
+    ("lx_rowseg_fc_need", ctypes.c_int, [vp, ctypes.c_uint64, vp, vp, vp, ctypes.c_uint64, u64p]),
+    ("lx_rowseg_la_serve", ctypes.c_int, [vp, ctypes.c_uint64, vp, vp]),
+    ("lx_rowseg_la_store", ctypes.c_int, [vp, ctypes.c_uint64, vp, vp]),
+    ("lx_rowseg_fc_unroute", ctypes.c_int, [vp, ctypes.c_uint64, vp, vp, vp]),
+    ("lx_rowseg_forkless_cause", ctypes.c_int, [vp, ctypes.c_uint64, vp, vp, vp, u64p]),
     ("lx_device_planes", ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), u32p, ctypes.POINTER(vp)]),
     ("lx_sync", ctypes.c_int, [vp]),
     ("lx_shard_comm_unique_id", ctypes.c_int, [u8p]),
@@ -510,6 +516,26 @@ class Index:
     def rowseg_finish(self):
         self._chk(self.L.lx_rowseg_finish(self.h))
 
+    # ForklessCause of any pair across row-segment ranks (lachesis_hip.rowseg.RowSegments.forkless_cause_dev)
+    def rowseg_fc_route(self, n, qa_ptr, qb_ptr, ra_ptr, rb_ptr, perm_ptr, G):
+        c = np.zeros(G, dtype=np.uint64)
+        self._chk(self.L.lx_rowseg_fc_route(self.h, n, qa_ptr, qb_ptr, ra_ptr, rb_ptr, perm_ptr, _p(c, u64p)))
+        return [int(x) for x in c]
+
+    def rowseg_fc_need(self, m, ra_ptr, rb_ptr, ids_ptr, cap, G):
+        c = np.zeros(G, dtype=np.uint64)
+        self._chk(self.L.lx_rowseg_fc_need(self.h, m, ra_ptr, rb_ptr, ids_ptr, cap, _p(c, u64p)))
+        return [int(x) for x in c]
+
+    def rowseg_la_serve(self, n, ids_ptr, rows_ptr):
+        self._chk(self.L.lx_rowseg_la_serve(self.h, n, ids_ptr, rows_ptr))
+
+    def rowseg_la_store(self, n, ids_ptr, rows_ptr):
+        self._chk(self.L.lx_rowseg_la_store(self.h, n, ids_ptr, rows_ptr))
+
+    def rowseg_fc_unroute(self, n, perm_ptr, ans_ptr, out_ptr):
+        self._chk(self.L.lx_rowseg_fc_unroute(self.h, n, perm_ptr, ans_ptr, out_ptr))
+
     def segment_stats(self):
         """Timings of the last segmented batch (option "segments")."""
         st = LxSegStats()
@@ -594,4 +620,9 @@ class RowsegComm(ShardComm):
                 "la_received": int(st[3])}
 
     def forkless_cause_dev(self, n, a_ptr, b_ptr, out_ptr):
-        raise LxError(-1, "row segments answer ForklessCause through the index (own rows)")
+        """ForklessCause of any pairs of the epoch (lx_rowseg_forkless_cause):
+        queries to owner(a), remote LowestAfter rows to it, answers back."""
+        st = np.zeros(4, dtype=np.uint64)
+        self._chk(self.L.lx_rowseg_forkless_cause(self.c, n, a_ptr, b_ptr, out_ptr, _p(st, u64p)))
+        return {"routed_away": int(st[0]), "answered": int(st[1]), "rows_received": int(st[2]),
+                "rows_sent": int(st[3])}

@@ -18,10 +18,13 @@ then connects the segments:
 * LowestAfter -- a rank's range fill reaches rows of earlier segments: those
   entries travel as (row, column, seq) triples to their owners.
 
-Afterwards each rank answers ForklessCause between its own events.  The
-reference has no multi-process index (vecfc/index.go is single-node): this
-is the MI355X scale-out of the same computation, bit-exact to the single
-index (tests/test_gpu_rowseg.py).
+Afterwards :meth:`RowSegments.forkless_cause_dev` answers ForklessCause of ANY
+pair of the epoch (vecfc/forkless_cause.go:40-82): each rank's queries go to
+owner(a), which holds HB(a); the LowestAfter rows of the b outside its
+segment come from their owners; the answers go back in the caller's order
+(DESIGN.md section 6c).  The reference has no multi-process index
+(vecfc/index.go is single-node): this is the MI355X scale-out of the same
+computation, bit-exact to the single index (tests/test_gpu_rowseg.py).
 """
 
 import torch
@@ -40,6 +43,8 @@ class RowSegments:
         # (a rehearsal mode for several ranks sharing one GPU; RCCL is the product)
         self.stage = dist.get_backend(group) == "gloo" and self.device.type == "cuda"
         self.last = {}
+        self.last_fc = {}
+        self._bufs = {}   # device buffers of forkless_cause_dev, grown on demand
 
     def _a2a(self, recv, send, recv_n, send_n):
         if self.stage:
@@ -104,3 +109,43 @@ class RowSegments:
         self.last = {"row_rounds": rounds, "rows_received": rows_moved, "la_entries_sent": n_send,
                      "la_entries_received": n_recv}
         return self.last
+
+    def _buf(self, name, n, dtype=torch.int32):
+        b = self._bufs.get(name)
+        if b is None or b.numel() < n:
+            b = torch.empty(max(1, n), dtype=dtype, device=self.device)
+            self._bufs[name] = b
+        return b
+
+    def forkless_cause_dev(self, n, qa, qb, out):
+        """ForklessCause of this rank's n queries (device tensors qa, qb of
+        int32 event ids, out uint8), collectively with every rank."""
+        ix, G = self.ix, self.world
+        ra, rb = self._buf("ra", n), self._buf("rb", n)
+        perm = self._buf("perm", n)
+        send_n = ix.rowseg_fc_route(n, qa.data_ptr(), qb.data_ptr(), ra.data_ptr(), rb.data_ptr(), perm.data_ptr(), G)
+        recv_n = self._counts(send_n)
+        m = sum(recv_n)
+        xa, xb = self._buf("xa", m), self._buf("xb", m)
+        self._a2a(xa[:m], ra[:n], recv_n, send_n)
+        self._a2a(xb[:m], rb[:n], recv_n, send_n)
+        ids = self._buf("ids", m)
+        need_n = ix.rowseg_fc_need(m, xa.data_ptr(), xb.data_ptr(), ids.data_ptr(), max(1, m), G)
+        ask_n = self._counts(need_n)
+        nn, na = sum(need_n), sum(ask_n)
+        W = ix.rowseg_row_words()
+        asked = self._buf("asked", na)
+        self._a2a(asked[:na], ids[:nn], ask_n, need_n)
+        rows = self._buf("rows", na * W)
+        ix.rowseg_la_serve(na, asked.data_ptr(), rows.data_ptr())
+        got = self._buf("got", nn * W)
+        self._a2a(got[:nn * W], rows[:na * W], [c * W for c in need_n], [c * W for c in ask_n])
+        ix.rowseg_la_store(nn, ids.data_ptr(), got.data_ptr())
+        ans = self._buf("ans", m, torch.uint8)
+        ix.forkless_cause_batch_dev(m, xa.data_ptr(), xb.data_ptr(), ans.data_ptr())
+        ix.sync()
+        back = self._buf("back", n, torch.uint8)
+        self._a2a(back[:n], ans[:m], send_n, recv_n)
+        ix.rowseg_fc_unroute(n, perm.data_ptr(), back.data_ptr(), out.data_ptr())
+        self.last_fc = {"routed_away": n - send_n[self.rank], "answered": m, "rows_received": nn, "rows_sent": na}
+        return self.last_fc

@@ -71,6 +71,25 @@ struct Ops {
     int la_fetch(uint32_t *buf) { return lx_rowseg_la_fetch(h, buf); }
     int la_apply(uint64_t n, const uint32_t *buf) { return lx_rowseg_la_apply(h, n, buf); }
     int finish() { return lx_rowseg_finish(h); }
+    // ForklessCause across ranks (rowseg_fc_run)
+    uint32_t r = 0;
+    uint32_t rank() const { return r; }
+    int fc_route(uint64_t n, const uint32_t *qa, const uint32_t *qb, uint32_t *ra, uint32_t *rb, uint32_t *perm,
+                 uint64_t *counts) {
+        return lx_rowseg_fc_route(h, n, qa, qb, ra, rb, perm, counts);
+    }
+    int fc_need(uint64_t m, const uint32_t *ra, const uint32_t *rb, uint32_t *ids, uint64_t cap, uint64_t *counts) {
+        return lx_rowseg_fc_need(h, m, ra, rb, ids, cap, counts);
+    }
+    int la_serve(uint64_t n, const uint32_t *ids, uint32_t *rows) { return lx_rowseg_la_serve(h, n, ids, rows); }
+    int la_store(uint64_t n, const uint32_t *ids, const uint32_t *rows) { return lx_rowseg_la_store(h, n, ids, rows); }
+    int fc_pairs(uint64_t m, const uint32_t *a, const uint32_t *b, uint8_t *ans) {
+        int rc = lx_forkless_cause_batch_dev(h, m, a, b, ans, nullptr);
+        return rc ? rc : lx_sync(h);
+    }
+    int fc_unroute(uint64_t n, const uint32_t *perm, const uint8_t *ans, uint8_t *out) {
+        return lx_rowseg_fc_unroute(h, n, perm, ans, out);
+    }
     void *buf(int k, size_t bytes) {
         if (bytes > caps[k]) {
             (void)hipFree(bufs[k]);
@@ -148,6 +167,40 @@ extern "C" int lx_fake_rowseg_exchange(void **handles, uint32_t G, uint64_t *sta
             stats[4 * r + 1] = st.rows_received;
             stats[4 * r + 2] = st.la_sent;
             stats[4 * r + 3] = st.la_received;
+        });
+    for (auto &t : th) t.join();
+    snprintf(err, err_cap, "%s", w.err.c_str());
+    for (int rc : rcs)
+        if (rc) return rc;
+    return 0;
+}
+
+// ForklessCause across ranks: rank r asks its n[r] queries (device arrays),
+// stats[4 r ..] = routed away, answered, LA rows received, sent
+extern "C" int lx_fake_rowseg_fc(void **handles, uint32_t G, const uint64_t *n, void **qa, void **qb, void **out,
+                                 uint64_t *stats, char *err, uint32_t err_cap) {
+    World w(G);
+    std::vector<int> rcs(G, 0);
+    std::vector<std::thread> th;
+    for (uint32_t r = 0; r < G; r++)
+        th.emplace_back([&, r] {
+            (void)hipSetDevice(0);
+            Ops ops{static_cast<lx_index *>(handles[r])};
+            ops.r = r;
+            Net net{w, r};
+            lx::RowsegFcStats st;
+            rcs[r] = lx::rowseg_fc_run(ops, net, G, n[r], static_cast<const uint32_t *>(qa[r]),
+                                       static_cast<const uint32_t *>(qb[r]), static_cast<uint8_t *>(out[r]), st);
+            if (rcs[r]) {
+                w.fail("rank " + std::to_string(r) + ": " + lx_last_error(ops.h));
+                std::lock_guard<std::mutex> l(w.m);
+                w.broken = true;
+                w.cv.notify_all();
+            }
+            stats[4 * r] = st.routed_away;
+            stats[4 * r + 1] = st.answered;
+            stats[4 * r + 2] = st.rows_received;
+            stats[4 * r + 3] = st.rows_sent;
         });
     for (auto &t : th) t.join();
     snprintf(err, err_cap, "%s", w.err.c_str());

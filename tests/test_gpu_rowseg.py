@@ -81,6 +81,18 @@ def _worker(rank, world, port, q, shape):
             ok = False
         except Exception:
             pass
+        # ForklessCause of ANY pair across ranks (RowSegments.forkless_cause_dev):
+        # a uniform over the epoch, b up to 300 events before it
+        N = len(d)
+        k = 20_000 + 500 * rank
+        qa2 = rng.integers(0, N, k).astype(np.uint32)
+        qb2 = np.clip(qa2.astype(np.int64) - rng.integers(0, 300, k), 0, N - 1).astype(np.uint32)
+        ta = torch.from_numpy(qa2.view(np.int32)).to(dev)
+        tb = torch.from_numpy(qb2.view(np.int32)).to(dev)
+        out = torch.full((k,), 7, dtype=torch.uint8, device=dev)
+        fc = rs.forkless_cause_dev(k, ta, tb, out)
+        ok = ok and bool(np.array_equal(out.cpu().numpy(), o.forkless_cause_batch(qa2, qb2)))
+        info = dict(info, fc=fc)
         q.put((rank, ok, info))
     except Exception as e:   # report instead of hanging the other ranks' queue reads
         q.put((rank, False, repr(e)))
@@ -107,5 +119,6 @@ def test_row_segments_over_torch_distributed(world, shape):
         p.join(timeout=60)
         assert p.exitcode == 0
     assert all(ok for _, ok, _ in res), res
+    assert sum(r[2]["fc"]["rows_received"] for r in res) > 0, res     # LA rows crossed ranks
     if shape == "short":
         assert max(r[2]["row_rounds"] for r in res) >= 2, res    # not-ready rows asked again

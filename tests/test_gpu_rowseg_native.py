@@ -40,6 +40,10 @@ def fake(lx):
     L.lx_fake_rowseg_exchange.restype = ctypes.c_int
     L.lx_fake_rowseg_exchange.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint32,
                                           ctypes.POINTER(ctypes.c_uint64), ctypes.c_char_p, ctypes.c_uint32]
+    vpp = ctypes.POINTER(ctypes.c_void_p)
+    L.lx_fake_rowseg_fc.restype = ctypes.c_int
+    L.lx_fake_rowseg_fc.argtypes = [vpp, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64), vpp, vpp, vpp,
+                                    ctypes.POINTER(ctypes.c_uint64), ctypes.c_char_p, ctypes.c_uint32]
     return L
 
 
@@ -99,6 +103,59 @@ def test_native_row_segment_exchange(lx, fake, world, shape):
     ref.close()
 
 
+@pytest.mark.parametrize("world,shape", [(2, "forks"), (3, "forks"), (4, "parents"), (8, "wide")])
+def test_native_row_segment_forkless_cause_any_pair(lx, fake, world, shape):
+    """ForklessCause of ANY pair of the epoch across row-segment ranks
+    (lx_rowseg_forkless_cause's driver, csrc/lx_rowseg_exchange.h
+    rowseg_fc_run, over the in-process transport): every rank asks queries
+    with a uniform over the whole epoch and b up to 300 events before it --
+    most pairs leave the asking rank, many cross a segment boundary -- and
+    gets the C oracle's answers in its own order (vecfc/forkless_cause.go:40-82)."""
+    import torch
+    V, epv, P, ch, fk, seed = SHAPES[shape]
+    d = lx.tools.gen_dag(V, epv, P, ch, fk, seed)
+    N = len(d)
+    rng = np.random.default_rng(seed + 100)
+    weights = [int(x) for x in rng.integers(1, 40, V)]
+    ranks = []
+    for r in range(world):
+        ix = lx.Index(device=0, options={"seg_count": world, "seg_rank": r, "small_max": 0})
+        ix.reset(weights)
+        ix.add_batch(d.creator, d.seq, d.poff, d.par)
+        ranks.append(ix)
+    hs = (ctypes.c_void_p * world)(*[ix.h for ix in ranks])
+    stats = (ctypes.c_uint64 * (4 * world))()
+    err = ctypes.create_string_buffer(512)
+    assert fake.lx_fake_rowseg_exchange(hs, world, stats, err, 512) == 0, err.value.decode()
+    o = corc.OracleIndex(weights)
+    assert o.add_batch(d.creator, d.seq, d.poff, d.par) == -1
+    dev = torch.device("cuda", 0)
+    qs, bufs = [], []
+    for r in range(world):
+        k = 30_000 + 1000 * r                          # ranks ask different numbers of queries
+        qa = rng.integers(0, N, k).astype(np.uint32)
+        qb = np.clip(qa.astype(np.int64) - rng.integers(0, 300, k), 0, N - 1).astype(np.uint32)
+        qs.append((qa, qb))
+        t = lambda x: torch.from_numpy(x.view(np.int32)).to(dev)
+        bufs.append((t(qa), t(qb), torch.full((k,), 7, dtype=torch.uint8, device=dev)))
+    torch.cuda.synchronize()
+    ns = (ctypes.c_uint64 * world)(*[len(q[0]) for q in qs])
+    P_ = lambda i: (ctypes.c_void_p * world)(*[b[i].data_ptr() for b in bufs])
+    fst = (ctypes.c_uint64 * (4 * world))()
+    for rep in range(2):                               # a second batch re-asks (and re-ships) its rows
+        rc = fake.lx_fake_rowseg_fc(hs, world, ns, P_(0), P_(1), P_(2), fst, err, 512)
+        assert rc == 0, err.value.decode()
+        for r in range(world):
+            qa, qb = qs[r]
+            np.testing.assert_array_equal(bufs[r][2].cpu().numpy(), o.forkless_cause_batch(qa, qb), err_msg=str(r))
+    st = np.array(fst[:], dtype=np.uint64).reshape(world, 4)
+    assert st[:, 0].sum() > 0 and st[:, 2].sum() > 0, st      # pairs left their rank, rows crossed
+    assert st[:, 1].sum() == sum(len(q[0]) for q in qs)        # every query answered exactly once
+    assert st[:, 2].sum() == st[:, 3].sum()                    # every LA row sent was received
+    for ix in ranks:
+        ix.close()
+
+
 def test_rowseg_comm_one_rank_and_mismatch(lx):
     """lx_rowseg_comm_create over real RCCL with one rank (the 1-GPU box): a
     whole index has nothing to join; a handle whose seg_rank / seg_count do not
@@ -110,8 +167,18 @@ def test_rowseg_comm_one_rank_and_mismatch(lx):
     assert ix.rowseg_of() == (0, 1)
     c = lx.RowsegComm(ix, lx.shard_comm_unique_id(), 1, 0)
     assert c.exchange() == {"row_rounds": 0, "rows_received": 0, "la_sent": 0, "la_received": 0}
-    with pytest.raises(lx.LxError):
-        c.forkless_cause_dev(0, 0, 0, 0)
+    # one rank: lx_rowseg_forkless_cause is the whole index's batch call
+    import torch
+    N = len(d)
+    qa, qb = lx.tools.fc_queries(d.lamport, 5000, seed=3)
+    dev = torch.device("cuda", 0)
+    ta = torch.from_numpy(qa.view(np.int32)).to(dev)
+    tb = torch.from_numpy(qb.view(np.int32)).to(dev)
+    out = torch.empty(len(qa), dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    c.forkless_cause_dev(len(qa), ta.data_ptr(), tb.data_ptr(), out.data_ptr())
+    np.testing.assert_array_equal(out.cpu().numpy(), ix.forkless_cause_batch(qa, qb))
+    assert N > 0
     c.close()
     seg = lx.Index(device=0, options={"seg_count": 2, "seg_rank": 1, "small_max": 0})
     assert seg.rowseg_of() == (1, 2)
