@@ -272,6 +272,20 @@ int lx_la_own_dev(lx_index *h, void *stream);
 int lx_shard_block_wire(lx_index *h, uint32_t dst_shard, uint32_t *bytes_per_entry);
 int lx_la_pack_wire_dev(lx_index *h, uint32_t dst_shard, void *out_dev, uint32_t bytes_per_entry);
 int lx_la_unpack_wire_dev(lx_index *h, uint32_t src_shard, const void *in_dev, uint32_t bytes_per_entry);
+/* Incremental exchange (the reference's per-event Add -> Flush cadence,
+ * abft/indexed_lachesis.go:69-82, vecengine/index.go:78-96): blocks hold only
+ * the rows whose LowestAfter entries can have changed since the last committed
+ * exchange.  lx_shard_dirty writes, for each of this shard's branches, the
+ * first such seq into dmin[branch] (LX_NONE for the other shards' branches and
+ * for unchanged ones; nb >= lx_num_branches); the ranks combine their arrays
+ * by an element-wise min (e.g. an all_reduce MIN) and pass the result to
+ * lx_shard_dirty_set, after which lx_shard_block / pack / unpack / own move the
+ * dirty rows only (every rank lists the same rows, branch by branch in seq
+ * order); lx_shard_dirty_commit after the unpacks ends it.  After lx_reset, a
+ * DropNotFlushed or a branch-capacity growth the next exchange is whole. */
+int lx_shard_dirty(lx_index *h, uint32_t nb, uint32_t *dmin);
+int lx_shard_dirty_set(lx_index *h, uint32_t nb, const uint32_t *dmin);
+int lx_shard_dirty_commit(lx_index *h);
 
 /* Column shards over RCCL without a Python host (the Go caller): one
  * communicator per shard handle, built from a unique id that rank 0 creates

@@ -101,6 +101,14 @@ void free_all(lx_index *h) {
     h->sc_cap = 0;
     h->sc_tmp_bytes = 0;
     h->sc_events = ~0ull;
+    h->sc_cols_B = 0;
+    for (void *p : {(void *)h->sx_len, (void *)h->sx_dmin, (void *)h->sx_rows, (void *)h->sx_meta})
+        if (p) (void)hipFree(p);
+    h->sx_len = h->sx_dmin = h->sx_rows = h->sx_meta = nullptr;
+    h->sx_cap = 0;
+    h->sx_rows_cap = h->sx_meta_cap = 0;
+    h->sx_full = true;
+    h->sx_active = false;
     h->hb = h->la = nullptr;
     h->ev_creator = h->ev_seq = h->ev_branch = h->ev_bbefore = h->ev_sp = h->first_child = nullptr;
     h->first_root = h->branch_first = h->branch_creator = h->branch_len = h->brow = h->wpad = h->col_list = nullptr;
@@ -870,6 +878,7 @@ std::vector<uint32_t> shard_cols(const lx_index *h, uint32_t q) {
 }
 
 int upload_cols(lx_index *h);
+int ensure_shard_cols(lx_index *h);
 
 // rows (events) whose branch belongs to each shard, at the current event count
 // (and every shard's column list)
@@ -910,6 +919,14 @@ int ensure_shard_rows(lx_index *h) {
     return 0;
 }
 
+// the column lists alone (the incremental exchange lists its rows itself)
+int ensure_shard_cols(lx_index *h) {
+    if (h->sc_cols && h->sc_cols_B == h->B) return 0;
+    if (int rc = upload_cols(h)) return rc;
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return 0;
+}
+
 // every shard's column list on the device (rebuilt with the shard rows, when
 // the event count or the branch set changed)
 int upload_cols(lx_index *h) {
@@ -920,10 +937,14 @@ int upload_cols(lx_index *h) {
         all.insert(all.end(), c.begin(), c.end());
         h->sc_col_off.push_back((uint32_t)all.size());
     }
-    if (h->sc_cols) (void)hipFree(h->sc_cols);
+    if (h->sc_cols) {
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        (void)hipFree(h->sc_cols);
+    }
     HIPCHK(h, dalloc(&h->sc_cols, all.size()));
     if (!all.empty())
         HIPCHK(h, hipMemcpyAsync(h->sc_cols, all.data(), all.size() * 4, hipMemcpyHostToDevice, h->stream));
+    h->sc_cols_B = h->B;
     return 0;
 }
 
@@ -1712,6 +1733,8 @@ int lx_reset(lx_index *h, uint32_t nv, const uint32_t *w) {
     h->quorum = (uint32_t)(tot * 2 / 3 + 1);
     shard_bounds(h, h->shard_rank, &h->own_lo, &h->own_hi);
     h->sc_events = ~0ull;
+    h->sx_full = true;      // a new epoch: the next LowestAfter exchange is whole
+    h->sx_active = false;
     uint32_t reserve = h->reserve ? h->reserve : std::max<uint32_t>(64, nv / 16);
     uint32_t want_stride = round_up(nv + reserve, 64);
     // a shard stores its own columns: originals + a share of the fork reserve
@@ -1920,6 +1943,8 @@ int lx_drop_not_flushed(lx_index *h) {
     h->hm_n = std::min(h->hm_n, h->n_flushed);
     h->n_events = h->n_flushed;
     fcc_forget_from(h, h->n_flushed);
+    h->sx_full = true;      // receivers may hold entries of the dropped events
+    h->sx_active = false;
     if (h->B != h->B_flushed) {
         h->B = h->B_flushed;
         h->h_branch_creator.resize(h->B);
@@ -2288,8 +2313,9 @@ int lx_shard_block(lx_index *h, uint32_t src, uint32_t dst, uint64_t *elems) {
     if (!h || !elems || src >= h->shard_count || dst >= h->shard_count) return LX_ERR_ARG;
     HIPCHK(h, set_dev(h->device));
     int rc;
-    if ((rc = ensure_shard_rows(h))) return rc;
-    *elems = (uint64_t)h->sc_nrows[src] * (h->sc_col_off[dst + 1] - h->sc_col_off[dst]);
+    if ((rc = h->sx_active ? ensure_shard_cols(h) : ensure_shard_rows(h))) return rc;
+    const uint64_t nrows = h->sx_active ? h->sx_roff[src + 1] - h->sx_roff[src] : h->sc_nrows[src];
+    *elems = nrows * (h->sc_col_off[dst + 1] - h->sc_col_off[dst]);
     return 0;
 }
 
@@ -2301,7 +2327,7 @@ static int la_xfer(lx_index *h, uint32_t rows_of, uint32_t cols_of, uint32_t *bu
     if (!h->have_epoch) return h->fail(LX_ERR_STATE, "exchange before lx_reset");
     HIPCHK(h, set_dev(h->device));
     int rc;
-    if ((rc = ensure_shard_rows(h))) return rc;
+    if ((rc = h->sx_active ? ensure_shard_cols(h) : ensure_shard_rows(h))) return rc;
     const uint32_t c0 = h->sc_col_off[cols_of], c1 = h->sc_col_off[cols_of + 1];
     XferArgs x{};
     x.lap = h->lap;
@@ -2313,8 +2339,9 @@ static int la_xfer(lx_index *h, uint32_t rows_of, uint32_t cols_of, uint32_t *bu
     x.ev_branch = h->ev_branch;
     x.ev_seq = h->ev_seq;
     x.branch_first = h->branch_first;
-    x.rows = h->sc_rows[rows_of];
-    x.nrows = h->sc_nrows[rows_of];
+    // the dirty rows of an incremental exchange (lx_shard_dirty_set), else every row
+    x.rows = h->sx_active ? h->sx_rows + h->sx_roff[rows_of] : h->sc_rows[rows_of];
+    x.nrows = h->sx_active ? (uint32_t)(h->sx_roff[rows_of + 1] - h->sx_roff[rows_of]) : h->sc_nrows[rows_of];
     x.cols = h->sc_cols + c0;
     x.ncols = c1 - c0;
     x.buf = buf;
@@ -2378,6 +2405,114 @@ int lx_la_own_dev(lx_index *h, void *stream) {
     if (!h) return LX_ERR_ARG;
     (void)stream;
     return la_xfer(h, h->shard_rank, h->shard_rank, nullptr, 2);
+}
+
+// ---- incremental LowestAfter exchange ("streaming")
+//
+// An entry LA[(c, s)][j] is written when an event e of branch j first reaches
+// (c, s): s in (RAW(prev(e))[c], RAW(e)[c]].  RAW grows
+// along a branch, so every entry written since the last exchange lies at
+// s > RAW(p_j)[c], p_j = branch j's last event at that exchange (none: from
+// the branch's first seq).  dmin[c] = min over the branches with new events
+// of RAW(p_j)[c] + 1 is therefore the first row of branch c that can have
+// changed; rows below it are unchanged on every receiver.  Only the owner of
+// column c holds RAW(.)[c]: each rank reports its own columns, the ranks
+// combine them by an element-wise min, and every rank lists the same dirty
+// rows for every shard (branch order, then seq).  A DropNotFlushed, reset or
+// load makes the next exchange a full one.
+
+int lx_shard_dirty(lx_index *h, uint32_t nb, uint32_t *dmin) {
+    if (!h || !dmin) return LX_ERR_ARG;
+    if (!h->sharded()) return h->fail(LX_ERR_STATE, "the incremental exchange needs a column-sharded handle");
+    if (!h->have_epoch) return h->fail(LX_ERR_STATE, "exchange before lx_reset");
+    if (nb < h->B) return h->fail(LX_ERR_ARG, "dmin holds %u branches < %u", nb, h->B);
+    HIPCHK(h, set_dev(h->device));
+    int rc;
+    if ((rc = flush_pending(h)) || (rc = ensure_shard_cols(h))) return rc;
+    for (uint32_t b = 0; b < nb; b++) dmin[b] = LX_NONE;
+    const uint32_t c0 = h->sc_col_off[h->shard_rank], c1 = h->sc_col_off[h->shard_rank + 1];
+    if (h->sx_cap < h->stride || !h->sx_len) {
+        for (void *p : {(void *)h->sx_len, (void *)h->sx_dmin})
+            if (p) (void)hipFree(p);
+        h->sx_len = h->sx_dmin = nullptr;
+        h->sx_cap = 0;
+        HIPCHK(h, dalloc(&h->sx_len, h->stride));
+        HIPCHK(h, dalloc(&h->sx_dmin, h->stride));
+        HIPCHK(h, hipMemsetAsync(h->sx_len, 0, (uint64_t)h->stride * 4, h->stream));
+        h->sx_cap = h->stride;
+        h->sx_full = true;
+    }
+    if (h->sx_full) {
+        // whole blocks: every row of every own branch
+        const std::vector<uint32_t> own = shard_cols(h, h->shard_rank);
+        for (uint32_t c : own) dmin[c] = h->h_branch_first[c];
+        return 0;
+    }
+    if (!h->B || c1 == c0) return 0;
+    HIPCHK(h, lx::launch_fill_u32(h->sx_dmin, h->B, LX_NONE, h->stream));
+    HIPCHK(h, lx::launch_shard_dmin(h->hb, h->pstride, h->cmap, h->branch_len, h->brow, h->s_cap, h->branch_first,
+                                    h->sx_len, h->B, h->sc_cols + c0, c1 - c0, h->sx_dmin, h->stream));
+    HIPCHK(h, hipMemcpyAsync(dmin, h->sx_dmin, 4ull * h->B, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+int lx_shard_dirty_set(lx_index *h, uint32_t nb, const uint32_t *dmin) {
+    if (!h || !dmin) return LX_ERR_ARG;
+    if (!h->sharded()) return h->fail(LX_ERR_STATE, "the incremental exchange needs a column-sharded handle");
+    if (nb < h->B) return h->fail(LX_ERR_ARG, "dmin holds %u branches < %u", nb, h->B);
+    HIPCHK(h, set_dev(h->device));
+    int rc;
+    if ((rc = ensure_shard_cols(h))) return rc;
+    const uint32_t B = h->B, G = h->shard_count;
+    std::vector<uint32_t> len(B);
+    if (B) HIPCHK(h, hipMemcpyAsync(len.data(), h->branch_len, 4ull * B, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    // per shard, its branches in order: {branch, first dirty index, row offset}
+    std::vector<uint32_t> meta;
+    std::vector<uint64_t> moff;
+    h->sx_roff.assign(G + 1, 0);
+    uint64_t total = 0;
+    for (uint32_t q = 0; q < G; q++) {
+        h->sx_roff[q] = total;
+        for (uint32_t c : shard_cols(h, q)) {
+            const uint32_t first = h->h_branch_first[c];
+            uint32_t start = len[c];
+            if (dmin[c] != LX_NONE) start = dmin[c] <= first ? 0u : std::min(dmin[c] - first, len[c]);
+            if (start == len[c]) continue;
+            meta.push_back(c);
+            meta.push_back(start);
+            meta.push_back((uint32_t)total);
+            meta.push_back(len[c] - start);
+            total += len[c] - start;
+        }
+    }
+    h->sx_roff[G] = total;
+    if (total > 0xFFFFFFFFull) return h->fail(LX_ERR_ARG, "too many dirty rows");
+    if ((rc = grow_scratch(h, &h->sx_rows, &h->sx_rows_cap, total + 1)) ||
+        (rc = grow_scratch(h, &h->sx_meta, &h->sx_meta_cap, (uint64_t)meta.size() + 4)))
+        return rc;
+    if (!meta.empty()) {
+        HIPCHK(h, hipMemcpyAsync(h->sx_meta, meta.data(), meta.size() * 4, hipMemcpyHostToDevice, h->stream));
+        HIPCHK(h, lx::launch_shard_dirty_rows(h->brow, h->s_cap, h->sx_meta, (uint32_t)(meta.size() / 4), h->sx_rows,
+                                              h->stream));
+    }
+    HIPCHK(h, hipStreamSynchronize(h->stream));   // `meta` is a host temporary
+    h->sx_active = true;
+    return 0;
+}
+
+int lx_shard_dirty_commit(lx_index *h) {
+    if (!h) return LX_ERR_ARG;
+    if (!h->sharded()) return h->fail(LX_ERR_STATE, "the incremental exchange needs a column-sharded handle");
+    HIPCHK(h, set_dev(h->device));
+    if (h->sx_len && h->B) {
+        HIPCHK(h, hipMemcpyAsync(h->sx_len, h->branch_len, 4ull * h->B, hipMemcpyDeviceToDevice, h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        h->sx_full = false;
+    }
+    h->sx_active = false;
+    return 0;
 }
 
 int lx_last_stats(const lx_index *h, lx_stats *out) {

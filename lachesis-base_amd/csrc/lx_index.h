@@ -165,6 +165,16 @@ struct lx_index {
     uint64_t sc_cap = 0;
     void *sc_tmp = nullptr;
     size_t sc_tmp_bytes = 0;
+    uint32_t sc_cols_B = 0;               // branch count sc_cols was built for
+    // incremental LowestAfter exchange (lx_shard_dirty*): per branch the events it
+    // had at the last committed exchange; the dirty row lists of every shard
+    uint32_t *sx_len = nullptr, *sx_dmin = nullptr;
+    uint32_t sx_cap = 0;
+    bool sx_full = true;                  // the next exchange sends whole blocks (reset, drop, load)
+    bool sx_active = false;               // pack / unpack / lx_shard_block use the dirty lists
+    uint32_t *sx_rows = nullptr, *sx_meta = nullptr;
+    uint64_t sx_rows_cap = 0, sx_meta_cap = 0;
+    std::vector<uint64_t> sx_roff;        // shard q's dirty rows: sx_rows[sx_roff[q] .. sx_roff[q + 1])
 
     // write-back (lx_writeback_*): dirty-row flags, row lists, byte offsets
     uint64_t wb_cap = 0, wb_buf_cap = 0;

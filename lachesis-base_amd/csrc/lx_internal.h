@@ -618,6 +618,11 @@ hipError_t launch_unfill(const UnfillArgs &a, hipStream_t s);
 hipError_t launch_zero_rows(uint32_t *hb, uint32_t *la, uint64_t stride, uint32_t lo, uint32_t hi, hipStream_t s);
 hipError_t launch_la_tail(const TailArgs &a, hipStream_t s);
 hipError_t launch_fill_u32(uint32_t *p, uint64_t n, uint32_t v, hipStream_t s);
+hipError_t launch_shard_dmin(const uint32_t *hb, uint64_t pstride, const uint32_t *cmap, const uint32_t *branch_len,
+                             const uint32_t *brow, uint32_t s_cap, const uint32_t *branch_first, const uint32_t *sx_len,
+                             uint32_t B, const uint32_t *cols, uint32_t ncols, uint32_t *dmin, hipStream_t s);
+hipError_t launch_shard_dirty_rows(const uint32_t *brow, uint32_t s_cap, const uint32_t *meta, uint32_t nmeta,
+                                   uint32_t *rows, hipStream_t s);
 hipError_t launch_shard_rows(const uint32_t *ev_branch, const uint32_t *branch_creator, uint32_t n, uint32_t lo,
                              uint32_t hi, uint32_t *flag, uint32_t *pos, void *scan_tmp, size_t scan_bytes,
                              uint32_t *rows, hipStream_t s);

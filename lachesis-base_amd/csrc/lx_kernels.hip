@@ -1820,6 +1820,48 @@ hipError_t launch_la_xfer(const XferArgs &a, hipStream_t s) {
     return launch_la_xfer_t<16>(a, s);
 }
 
+// incremental exchange (lx_shard_dirty): for each branch j with events since
+// the last exchange, its last event then p_j, and every own column c:
+// dmin[c] = min(RAW(p_j)[c] + 1) (p_j none: the branch's first seq)
+__global__ __launch_bounds__(256) void k_shard_dmin(const uint32_t *hb, uint64_t pstride, const uint32_t *cmap,
+                                                    const uint32_t *branch_len, const uint32_t *brow, uint32_t s_cap,
+                                                    const uint32_t *branch_first, const uint32_t *sx_len,
+                                                    const uint32_t *cols, uint32_t ncols, uint32_t *dmin) {
+    const uint32_t j = blockIdx.x;
+    const uint32_t x = sx_len[j];
+    if (branch_len[j] <= x) return;   // nothing new on branch j (a drop makes the exchange full instead)
+    const uint32_t p0 = x ? brow[(uint64_t)j * s_cap + x - 1] : LX_NONE;
+    for (uint32_t k = threadIdx.x; k < ncols; k += blockDim.x) {
+        const uint32_t c = cols[k];
+        const uint32_t raw = p0 != LX_NONE ? (hb[(uint64_t)p0 * pstride + cmap[c]] & ~LX_MARK) : 0u;
+        atomicMin(dmin + c, max(raw + 1u, branch_first[c]));
+    }
+}
+
+// the dirty rows: per listed branch {c, first index, row offset, count}
+__global__ __launch_bounds__(256) void k_shard_dirty_rows(const uint32_t *brow, uint32_t s_cap, const uint32_t *meta,
+                                                          uint32_t *rows) {
+    const uint32_t *m = meta + 4ull * blockIdx.x;
+    const uint32_t c = m[0], start = m[1], off = m[2], cnt = m[3];
+    for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) rows[off + i] = brow[(uint64_t)c * s_cap + start + i];
+}
+
+hipError_t launch_shard_dmin(const uint32_t *hb, uint64_t pstride, const uint32_t *cmap, const uint32_t *branch_len,
+                             const uint32_t *brow, uint32_t s_cap, const uint32_t *branch_first, const uint32_t *sx_len,
+                             uint32_t B, const uint32_t *cols, uint32_t ncols, uint32_t *dmin, hipStream_t s) {
+    if (!B || !ncols) return hipSuccess;
+    hipLaunchKernelGGL(k_shard_dmin, dim3(B), dim3(256), 0, s, hb, pstride, cmap, branch_len, brow, s_cap,
+                       branch_first, sx_len, cols, ncols, dmin);
+    return hipGetLastError();
+}
+
+hipError_t launch_shard_dirty_rows(const uint32_t *brow, uint32_t s_cap, const uint32_t *meta, uint32_t nmeta,
+                                   uint32_t *rows, hipStream_t s) {
+    if (!nmeta) return hipSuccess;
+    hipLaunchKernelGGL(k_shard_dirty_rows, dim3(nmeta), dim3(256), 0, s, brow, s_cap, meta, rows);
+    return hipGetLastError();
+}
+
 hipError_t launch_shard_rows(const uint32_t *ev_branch, const uint32_t *branch_creator, uint32_t n, uint32_t lo,
                              uint32_t hi, uint32_t *flag, uint32_t *pos, void *scan_tmp, size_t scan_bytes,
                              uint32_t *rows, hipStream_t s) {

@@ -6,10 +6,18 @@
 //   Ops (one rank's index): block(src, dst, &entries), wire(&bytes),
 //       pack(dst, buf, width) -> 0 | LX_ERR_WIRE (width 1 and an entry does not
 //       fit) | error, unpack(src, buf, width), own(), send_buf(bytes),
-//       recv_buf(bytes)
+//       recv_buf(bytes); the incremental exchange: branches(&B) (0: whole
+//       blocks always), dirty(B, dmin), dirty_set(B, dmin), commit()
 //   Net (the collectives): widths(send_w[G], recv_w[G]) -- every rank tells
 //       every peer the width of the block it sends it; blocks(send, so, sb,
-//       recv, ro, rb) -- grouped point-to-point moves of the blocks
+//       recv, ro, rb) -- grouped point-to-point moves of the blocks;
+//       min_u32(v, n) -- element-wise minimum over the ranks, in place
+//
+// Incremental: each rank reports, for its own branches, the first row whose
+// LowestAfter entries can have changed since the last exchange
+// (lx_shard_dirty); the element-wise min over the ranks gives every rank the
+// same dirty row lists (lx_shard_dirty_set), so blocks hold only the rows
+// written since then -- bytes scale with the events added, not the epoch.
 //
 // Wire widths: a block goes at 1 byte per entry when it fits, else at the
 // epoch width (2 while every seq < 2^16, else 4).  A sender that had to fall
@@ -56,6 +64,13 @@ int shard_exchange_run(Ops &ops, Net &net, uint32_t r, uint32_t G, ExchangeState
     if ((rc = ops.wire(&wb))) return rc;
     std::vector<uint64_t> sn(G, 0), rn(G, 0), so(G + 1), ro(G + 1), sb(G, 0), rb(G, 0);
     std::vector<uint32_t> sw(G, 0), rw(G, 0), wide(G, wb);
+    uint32_t nb = 0;
+    if ((rc = ops.branches(&nb))) return rc;
+    if (nb) {
+        std::vector<uint32_t> dm(nb);
+        if ((rc = ops.dirty(nb, dm.data())) || (rc = net.min_u32(dm.data(), nb)) || (rc = ops.dirty_set(nb, dm.data())))
+            return rc;
+    }
     for (uint32_t q = 0; q < G; q++) {
         if (q == r) continue;
         if ((rc = ops.block(r, q, &sn[q])) || (rc = ops.block(q, r, &rn[q]))) return rc;
@@ -104,6 +119,7 @@ int shard_exchange_run(Ops &ops, Net &net, uint32_t r, uint32_t G, ExchangeState
     for (uint32_t q = 0; q < G; q++)
         if (rb[q] && (rc = ops.unpack(q, recv + ro[q], rw[q]))) return rc;
     if ((rc = ops.own())) return rc;
+    if (nb && (rc = ops.commit())) return rc;
     st.count++;
     return 0;
 }

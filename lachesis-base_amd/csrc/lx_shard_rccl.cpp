@@ -97,6 +97,8 @@ struct lx_shard_comm {
     uint32_t rank = 0, nranks = 1;
     uint8_t *send = nullptr, *recv = nullptr;    // exchange staging (bytes), grown on demand
     size_t send_cap = 0, recv_cap = 0;
+    uint8_t *mbuf = nullptr;                     // element-wise min of the dirty rows (incremental exchange)
+    size_t mbuf_cap = 0;
     uint32_t *part = nullptr;                    // FC partial sums, grown on demand
     uint64_t part_cap = 0;
     uint32_t *wdev = nullptr;                    // wire widths: [0, G) sent, [G, 2G) received
@@ -218,6 +220,7 @@ void lx_shard_comm_destroy(lx_shard_comm *c) {
     if (c->comm) rccl().CommDestroy(c->comm);
     (void)hipFree(c->send);
     (void)hipFree(c->recv);
+    (void)hipFree(c->mbuf);
     (void)hipFree(c->part);
     (void)hipFree(c->wdev);
     for (uint8_t *p : c->rbuf) (void)hipFree(p);
@@ -242,6 +245,15 @@ struct RcclOps {
         return c->index(lx_la_unpack_wire_dev(c->ix, s, buf, w), "lx_la_unpack_wire_dev");
     }
     int own() { return c->index(lx_la_own_dev(c->ix, nullptr), "lx_la_own_dev"); }
+    int branches(uint32_t *nb) {
+        *nb = lx_num_branches(c->ix);
+        return 0;
+    }
+    int dirty(uint32_t nb, uint32_t *dmin) { return c->index(lx_shard_dirty(c->ix, nb, dmin), "lx_shard_dirty"); }
+    int dirty_set(uint32_t nb, const uint32_t *dmin) {
+        return c->index(lx_shard_dirty_set(c->ix, nb, dmin), "lx_shard_dirty_set");
+    }
+    int commit() { return c->index(lx_shard_dirty_commit(c->ix), "lx_shard_dirty_commit"); }
     uint8_t *send_buf(size_t n) { return c->grow(&c->send, &c->send_cap, std::max<size_t>(n, 1)) ? nullptr : c->send; }
     uint8_t *recv_buf(size_t n) { return c->grow(&c->recv, &c->recv_cap, std::max<size_t>(n, 1)) ? nullptr : c->recv; }
 };
@@ -272,6 +284,13 @@ struct RcclNet {
             return 0;
         }));
         LXC(c->hip(hipMemcpyAsync(rw, c->wdev + G, 4ull * G, hipMemcpyDeviceToHost, c->stream), "hipMemcpyAsync"));
+        return c->hip(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
+    }
+    int min_u32(uint32_t *v, uint32_t n) {
+        LXC(c->grow(&c->mbuf, &c->mbuf_cap, 4ull * n));
+        LXC(c->hip(hipMemcpyAsync(c->mbuf, v, 4ull * n, hipMemcpyHostToDevice, c->stream), "hipMemcpyAsync"));
+        LXC(c->nccl(rccl().AllReduce(c->mbuf, c->mbuf, n, ncclUint32, ncclMin, c->comm, c->stream), "ncclAllReduce"));
+        LXC(c->hip(hipMemcpyAsync(v, c->mbuf, 4ull * n, hipMemcpyDeviceToHost, c->stream), "hipMemcpyAsync"));
         return c->hip(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
     }
     int blocks(const uint8_t *send, const uint64_t *so, const uint64_t *sb, uint8_t *recv, const uint64_t *ro,

@@ -55,6 +55,9 @@ SIGNATURES = [
     ("lx_la_pack_dev", ctypes.c_int, [vp, ctypes.c_uint32, vp, vp]),
     ("lx_la_unpack_dev", ctypes.c_int, [vp, ctypes.c_uint32, vp, vp]),
     ("lx_la_own_dev", ctypes.c_int, [vp, vp]),
+    ("lx_shard_dirty", ctypes.c_int, [vp, ctypes.c_uint32, u32p]),
+    ("lx_shard_dirty_set", ctypes.c_int, [vp, ctypes.c_uint32, u32p]),
+    ("lx_shard_dirty_commit", ctypes.c_int, [vp]),
     ("lx_shard_block_wire", ctypes.c_int, [vp, ctypes.c_uint32, u32p]),
     ("lx_la_pack_wire_dev", ctypes.c_int, [vp, ctypes.c_uint32, vp, ctypes.c_uint32]),
     ("lx_la_unpack_wire_dev", ctypes.c_int, [vp, ctypes.c_uint32, vp, ctypes.c_uint32]),
@@ -456,6 +459,22 @@ class Index:
 
     def la_own_dev(self):
         self._chk(self.L.lx_la_own_dev(self.h, None))
+
+    # incremental LowestAfter exchange (lachesis_hip.shard.ShardedIndex.exchange)
+    def shard_dirty(self):
+        """Per branch the first seq of this shard's rows changed since the last
+        committed exchange (LX_NONE: other shards' branches, unchanged ones)."""
+        nb = self.num_branches()
+        d = np.zeros(max(nb, 1), dtype=np.uint32)
+        self._chk(self.L.lx_shard_dirty(self.h, nb, _p(d, u32p)))
+        return d[:nb]
+
+    def shard_dirty_set(self, dmin):
+        d = np.ascontiguousarray(dmin, dtype=np.uint32)
+        self._chk(self.L.lx_shard_dirty_set(self.h, len(d), _p(d, u32p)))
+
+    def shard_dirty_commit(self):
+        self._chk(self.L.lx_shard_dirty_commit(self.h))
 
     def last_stats(self):
         st = LxStats()

@@ -62,6 +62,7 @@ class ShardedIndex:
         self._bufs = {}
         self._last_w = []        # width each destination got last time (byte-wire fallbacks)
         self._count = 0
+        self.last_bytes = 0      # bytes this rank sent in the last exchange
 
     def all_to_all(self, recv, send, recv_n, send_n):
         if self.stage:
@@ -92,6 +93,12 @@ class ShardedIndex:
         G-int all-to-all tells the receivers the widths; every block starts at
         a multiple of 4 bytes on both sides (shard_layout)."""
         r, G = self.rank, self.world
+        incr = hasattr(self.ix, "shard_dirty")
+        if incr:
+            # only the rows written since the last exchange (lx_shard_dirty): each
+            # rank knows the first changed row of its own branches, the
+            # element-wise min over the ranks gives everyone every branch's
+            self.ix.shard_dirty_set(self._min(self.ix.shard_dirty()))
         send_n = [self.ix.shard_block(r, t) if t != r else 0 for t in range(G)]
         recv_n = [self.ix.shard_block(s, r) if s != r else 0 for s in range(G)]
         per_block = hasattr(self.ix, "la_pack_wire_dev")
@@ -147,8 +154,21 @@ class ShardedIndex:
                     self.ix.la_unpack_dev(s, recv.data_ptr() + ro[s])
         self.ix.la_own_dev()     # own rows x own columns, no communication
         self.ix.sync()
+        if incr:
+            self.ix.shard_dirty_commit()
         self.last_wire = (send_w, recv_w)
+        self.last_bytes = so[-1]
         return send_n
+
+    def _min(self, v):
+        """Element-wise minimum over the ranks of a uint32 numpy vector."""
+        import numpy as np
+        if self.world == 1 or len(v) == 0:
+            return v
+        dev = self.device if (self.device.type == "cuda" and not self.stage) else torch.device("cpu")
+        t = torch.from_numpy(np.asarray(v, dtype=np.int64)).to(dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.group)
+        return t.cpu().numpy().astype(np.uint32)
 
     def _widths(self, send_w):
         """Tell every rank the width of the block this rank sends it; returns recv widths."""

@@ -71,6 +71,7 @@ struct FakeNet {
         w->barrier();
         return 0;
     }
+    int min_u32(uint32_t *, uint32_t) { return 0; }
     int blocks(const uint8_t *send, const uint64_t *so, const uint64_t *sb, uint8_t *recv, const uint64_t *ro,
                const uint64_t *rb) {
         w->sendp[r] = send;
@@ -155,6 +156,14 @@ struct FakeOps {
             for (uint32_t c : t->cols[r]) got[(uint64_t)i * t->V + c] = t->la[(uint64_t)i * t->V + c];
         return 0;
     }
+    // no incremental exchange in the model: whole blocks every time
+    int branches(uint32_t *nb) {
+        *nb = 0;
+        return 0;
+    }
+    int dirty(uint32_t, uint32_t *) { return 0; }
+    int dirty_set(uint32_t, const uint32_t *) { return 0; }
+    int commit() { return 0; }
     // aligned staging (the device buffers are 256-B aligned)
     uint8_t *send_buf(size_t n) {
         sbuf.assign(n + 256, 0);
