@@ -5,9 +5,10 @@
 // lx_internal.h.  Host state is O(branches); all per-event work is on the GPU.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
-
 
 #include "lx_index.h"
 
@@ -1101,21 +1102,22 @@ int branches_info_rlp(lx_index *h, std::string *out) {
 constexpr uint64_t kFcPinnedMax = 1u << 16;
 
 int ensure_qp(lx_index *h, uint64_t bytes, uint8_t **host, uint8_t **dev) {
-    if (bytes > h->qp_cap) {
+    if (bytes > h->qp_cap || !h->qp) {
         if (h->qp) {
             HIPCHK(h, hipStreamSynchronize(h->stream));
             (void)hipHostFree(h->qp);
         }
-        h->qp = nullptr;
+        h->qp = h->qp_dev = nullptr;
         h->qp_cap = 0;
         const uint64_t cap = std::max<uint64_t>(bytes, 1u << 16);
         HIPCHK(h, hipHostMalloc((void **)&h->qp, cap, hipHostMallocMapped));
+        void *d = nullptr;
+        HIPCHK(h, hipHostGetDevicePointer(&d, h->qp, 0));   // once per buffer, not per call
+        h->qp_dev = static_cast<uint8_t *>(d);
         h->qp_cap = cap;
     }
-    void *d = nullptr;
-    HIPCHK(h, hipHostGetDevicePointer(&d, h->qp, 0));
     *host = h->qp;
-    *dev = static_cast<uint8_t *>(d);
+    *dev = h->qp_dev;
     return 0;
 }
 
@@ -1315,8 +1317,8 @@ int flush_pending(lx_index *h) {
 // unchanged caller's Add-then-ForklessCause miss; lx_fccache.cpp).  Returns 1
 // (nothing enqueued) when the run is not of that shape; the caller then
 // flushes and fills separately.
-int flush_add1_row(lx_index *h, uint32_t a, const uint32_t *evk_dev, uint32_t n_slots, const uint8_t *tag_dev,
-                   uint8_t *out_dev, uint32_t *psum_dev) {
+int flush_add1_row(lx_index *h, uint32_t a, uint32_t *evk_dev, uint32_t n_slots, uint8_t *tag_dev, uint8_t *out_dev,
+                   uint32_t *psum_dev, const Add1Delta *delta) {
     if (h->pend_n != 1 || h->pend_bs != a || h->B != h->V || h->pend_B0 != h->B || h->n_cheat || h->small_timing ||
         h->sharded() || h->rowseg() || !n_slots)
         return 1;
@@ -1356,6 +1358,14 @@ int flush_add1_row(lx_index *h, uint32_t a, const uint32_t *evk_dev, uint32_t n_
     r.wpad = h->wpad;
     r.quorum = h->quorum;
     r.psum = psum_dev;
+    if (delta) {
+        r.nd = delta->n;
+        for (uint32_t i = 0; i < delta->n; i++) {
+            r.d_slot[i] = delta->slot[i];
+            r.d_ev[i] = delta->ev[i];
+            r.d_tag[i] = delta->tag[i];
+        }
+    }
     HIPCHK(h, lx::launch_add1_row(r, h->stream));
     h->pend_n = 0;
     h->stats = lx_stats{};
@@ -2154,7 +2164,7 @@ constexpr uint64_t kGetChunk = 64ull << 20;
 int get_rows(lx_index *h, uint32_t mode, uint32_t n, const uint32_t *ev, uint8_t **rows, uint64_t *slot,
              const uint32_t **len) {
     const uint64_t sl = ((uint64_t)8 * std::max(h->B, h->V) + 15) / 16 * 16;
-    const uint64_t head = ((uint64_t)8 * n + 15) / 16 * 16;   // events + lengths
+    const uint64_t head = ((uint64_t)8 * n + 4 + 15) / 16 * 16;   // events + lengths + completion tag
     uint8_t *hp, *dp;
     int rc;
     if ((rc = ensure_qp(h, head + n * sl, &hp, &dp))) return rc;
@@ -2177,8 +2187,27 @@ int get_rows(lx_index *h, uint32_t mode, uint32_t n, const uint32_t *ev, uint8_t
     a.len = reinterpret_cast<uint32_t *>(dp + 4ull * n);
     a.out = dp + head;
     a.slot = sl;
-    HIPCHK(h, lx::launch_get_rows(a, h->stream));
-    HIPCHK(h, hipStreamSynchronize(h->stream));
+    if (n == 1) {
+        // one row (the reference's per-call getters): the kernel publishes a tag
+        // after the row, the host spins on it (a stream synchronization costs
+        // ~5 us more, scripts/probes/sync_latency.hip); a launch that never
+        // lands is caught by the timeout's synchronization
+        a.tag = ++h->get_tag ? h->get_tag : ++h->get_tag;
+        a.done = reinterpret_cast<uint32_t *>(dp + 8ull * n);
+        HIPCHK(h, lx::launch_get_rows(a, h->stream));
+        const volatile uint32_t *done = reinterpret_cast<const volatile uint32_t *>(hp + 8ull * n);
+        const auto t0 = std::chrono::steady_clock::now();
+        for (uint32_t k = 0; *done != a.tag; k++) {
+            if ((k & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(200)) {
+                HIPCHK(h, hipStreamSynchronize(h->stream));
+                if (*done != a.tag) return h->fail(LX_ERR_STATE, "getter: the row kernel did not complete");
+            }
+        }
+        std::atomic_thread_fence(std::memory_order_acquire);
+    } else {
+        HIPCHK(h, lx::launch_get_rows(a, h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+    }
     *rows = hp + head;
     *slot = sl;
     *len = reinterpret_cast<const uint32_t *>(hp + 4ull * n);

@@ -42,25 +42,37 @@ namespace {
 
 constexpr uint32_t kWindow = 64;   // events after a newly asked b that join the working set with it
 
+int fcc_quiesce(lx_index *h, FcCache *c);
+
 }  // namespace
 
 struct FcCache {
     uint32_t W = 0, used = 0;
-    // pinned, device-mapped (the fill kernels read slot events and generations)
-    uint32_t *evk = nullptr, *evk_dev = nullptr;   // event per slot (free: a valid fallback, 0)
-    uint8_t *g7 = nullptr, *g7_dev = nullptr;       // column generation per slot, 1..127
-    uint8_t *M = nullptr, *M_dev = nullptr;         // [W][W]
+    // slot events and generations: written by the host (pinned), read by the
+    // fill kernels from a device mirror -- a fill never reads host memory over
+    // the bus; the slots changed since the mirror was written are `dirty`
+    // (k_add1_row takes up to kAdd1Delta of them in its arguments, else the
+    // mirror is copied before the fill)
+    uint32_t *evk = nullptr;                        // event per slot (free: a valid fallback, 0)
+    uint8_t *g7 = nullptr;                          // column generation per slot, 1..126
+    uint32_t *evk_d = nullptr;                      // device mirrors
+    uint8_t *g7_d = nullptr;
+    std::vector<uint32_t> dirty;
+    std::vector<uint8_t> dmark;
+    bool dirty_all = true;
+    uint8_t *M = nullptr, *M_dev = nullptr;         // [W][W], pinned and device-mapped: answers land here
     uint32_t *qa = nullptr, *qa_dev = nullptr;      // the row's a
-    // completion of the last fill: an event recorded after it; the host spins on
-    // the answer it needs, and waits for the event before it changes slots,
-    // generations or qa again
+    // the last fill: it writes row inflight_sa of M (a tile fill: every row)
+    // while the host goes on as soon as its own answer landed; a row is reused
+    // (cleared for a new occupant) only after that fill has finished: an event
+    // recorded after k_fc / tile fills, the row's entries for k_add1_row
     hipEvent_t filled = nullptr;
     bool inflight = false;
-    // a k_add1_row fill is complete once every entry of its row carries its
-    // column's generation (each entry is written after that slot's reads): no
-    // event is recorded for it
-    bool inflight_row = false;
+    bool inflight_row = false;                      // k_add1_row (no event recorded)
+    bool inflight_tile = false;
     uint32_t inflight_sa = 0, inflight_n = 0;
+    std::vector<uint8_t> g7_launch;                 // the column generations the in-flight row fill writes
+    lx_index *h = nullptr;
     // k_add1_row's per-slot {count, sum} words (W x uint64), zero between launches
     uint32_t *d_rsum = nullptr;
     std::vector<uint32_t> ev;                       // slot -> event (LX_NONE: free)
@@ -88,10 +100,17 @@ struct FcCache {
     void map_erase(uint32_t e) {
         if (e < slot_of.size()) slot_of[e] = LX_NONE;
     }
+    void mark(uint32_t s) {
+        if (!dmark[s]) {
+            dmark[s] = 1;
+            dirty.push_back(s);
+        }
+    }
     void free_slot(uint32_t s) {
         map_erase(ev[s]);
         ev[s] = LX_NONE;
         evk[s] = 0;
+        mark(s);
         free_slots.push_back(s);
         if (last_sa == s) last_a = last_sa = LX_NONE;
     }
@@ -117,10 +136,15 @@ struct FcCache {
         }
         ev[s] = e;
         evk[s] = e;
+        mark(s);
         map_put(e, s);
         // 1..126: a row fill writes 0xFF for a query it cannot answer, and
         // 0xFF >> 1 = 127 must never equal a valid generation
         g7[s] = (uint8_t)(g7[s] % 126u + 1u);
+        // row s is cleared for its new occupant (and, when the generation
+        // wraps, column s in every row): the fill in flight must not be
+        // writing them any more
+        if (inflight && (inflight_tile || s == inflight_sa || g7[s] == 1)) (void)fcc_quiesce(h, this);
         if (g7[s] == 1)   // the generation wrapped: entries of an old occupant could match again
             for (uint32_t r = 0; r < W; r++) M[(uint64_t)r * W + s] = 0;
         memset(M + (uint64_t)s * W, 0, W);
@@ -131,6 +155,7 @@ struct FcCache {
         std::fill(slot_of.begin(), slot_of.end(), LX_NONE);
         std::fill(ev.begin(), ev.end(), LX_NONE);
         for (uint32_t s = 0; s < W; s++) evk[s] = 0;
+        dirty_all = true;
         std::fill(ref.begin(), ref.end(), 0);
         free_slots.clear();
         used = 0;
@@ -146,6 +171,8 @@ void fcc_free(FcCache *c) {
     if (!c) return;
     for (void *p : {(void *)c->evk, (void *)c->g7, (void *)c->M, (void *)c->qa})
         if (p) (void)hipHostFree(p);
+    if (c->evk_d) (void)hipFree(c->evk_d);
+    if (c->g7_d) (void)hipFree(c->g7_d);
     if (c->filled) (void)hipEventDestroy(c->filled);
     if (c->d_rsum) (void)hipFree(c->d_rsum);
     if (c->d_psum) (void)hipFree(c->d_psum);
@@ -158,15 +185,17 @@ int fcc_make(lx_index *h) {
     const uint32_t W = h->fcc_slots;
     FcCache *c = new FcCache();
     c->W = W;
+    c->h = h;
     void *d = nullptr;
     auto pin = [&](void **host, void **dev, uint64_t bytes) -> hipError_t {
         hipError_t e = hipHostMalloc(host, bytes, hipHostMallocMapped);
         if (e != hipSuccess) return e;
         return hipHostGetDevicePointer(dev, *host, 0);
     };
-    hipError_t e = pin((void **)&c->evk, &d, 4ull * W);
-    c->evk_dev = static_cast<uint32_t *>(d);
-    if (e == hipSuccess) { e = pin((void **)&c->g7, &d, W); c->g7_dev = static_cast<uint8_t *>(d); }
+    hipError_t e = hipHostMalloc((void **)&c->evk, 4ull * W, hipHostMallocDefault);
+    if (e == hipSuccess) e = hipHostMalloc((void **)&c->g7, W, hipHostMallocDefault);
+    if (e == hipSuccess) e = hipMalloc((void **)&c->evk_d, 4ull * W);
+    if (e == hipSuccess) e = hipMalloc((void **)&c->g7_d, W);
     if (e == hipSuccess) { e = pin((void **)&c->M, &d, (uint64_t)W * W); c->M_dev = static_cast<uint8_t *>(d); }
     if (e == hipSuccess) { e = pin((void **)&c->qa, &d, 64); c->qa_dev = static_cast<uint32_t *>(d); }
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->filled, hipEventDisableTiming);
@@ -178,6 +207,8 @@ int fcc_make(lx_index *h) {
     }
     memset(c->g7, 0, W);
     memset(c->M, 0, (uint64_t)W * W);
+    c->dmark.assign(W, 0);
+    c->g7_launch.assign(W, 0);
     c->ev.assign(W, LX_NONE);
     c->ref.assign(W, 0);
     c->clear();
@@ -222,14 +253,27 @@ int fcc_cheaters(lx_index *h, FcCache *c) {
     return 0;
 }
 
+// the device mirror of the slots brought up to date (stream-ordered before the
+// fill that follows; the host waits for that fill's answer, so the copy has
+// read the pinned arrays before the host changes them again)
+int fcc_sync_mirror(lx_index *h, FcCache *c) {
+    if (!c->dirty_all && c->dirty.empty()) return 0;
+    HIPCHK(h, hipMemcpyAsync(c->evk_d, c->evk, 4ull * c->W, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(h, hipMemcpyAsync(c->g7_d, c->g7, c->W, hipMemcpyHostToDevice, h->stream));
+    for (uint32_t s : c->dirty) c->dmark[s] = 0;
+    c->dirty.clear();
+    c->dirty_all = false;
+    return 0;
+}
+
 // a against every slot in use: one k_fc launch, answers into M's row sa
 int fcc_row(lx_index *h, FcCache *c, uint32_t a, uint32_t sa) {
     c->qa[0] = a;
     FcArgs f;
-    int rc = lx_fc_args(h, c->used, c->qa_dev, c->evk_dev, c->M_dev + (uint64_t)sa * c->W, nullptr, &f);
+    int rc = lx_fc_args(h, c->used, c->qa_dev, c->evk_d, c->M_dev + (uint64_t)sa * c->W, nullptr, &f);
     if (rc) return rc;
     f.qa_bcast = 1;
-    f.out_tag = c->g7_dev;
+    f.out_tag = c->g7_d;
     f.status = h->status + 2;   // the pinned-path sink: every slot holds a known event
     HIPCHK(h, lx::launch_fc(f, h->ncols, h->B > h->V, h->stream));
     c->st.row_fills++;
@@ -261,9 +305,9 @@ int fcc_tile(lx_index *h, FcCache *c) {
     r.hb = h->hb;
     r.la = h->la;
     r.stride = h->pstride;
-    r.cand = c->evk_dev;
+    r.cand = c->evk_d;
     r.n_cand = n;
-    r.roots = c->evk_dev;
+    r.roots = c->evk_d;
     r.n_roots = n;
     r.roots_fallback = c->evk[0];
     r.ncols = ncols;
@@ -279,22 +323,23 @@ int fcc_tile(lx_index *h, FcCache *c) {
     r.col_split = col_split;
     r.n_split = n_split;
     HIPCHK(h, lx::launch_root_fc(r, h->B > h->V, h->stream));
-    HIPCHK(h, lx::launch_fc_tile_out(c->d_psum, n_split, n, rp, n, h->quorum, c->g7_dev, c->M_dev, c->W, h->stream));
+    HIPCHK(h, lx::launch_fc_tile_out(c->d_psum, n_split, n, rp, n, h->quorum, c->g7_d, c->M_dev, c->W, h->stream));
     c->st.tile_fills++;
     c->st.pairs += (uint64_t)n * n;
     return 0;
 }
 
-// the last fill has finished (its kernels no longer read evk / g7 / qa or write
-// M; by the time the caller asks again it normally has)
+// the last fill has finished writing M (by the time the caller asks again it
+// normally has): a row fill once every entry of its row carries the generation
+// it was launched with, a tile fill by its event
 int fcc_quiesce(lx_index *h, FcCache *c) {
     if (!c->inflight) return 0;
-    if (c->inflight_row) {
+    if (!c->inflight_tile) {
         const volatile uint8_t *row = c->M + (uint64_t)c->inflight_sa * c->W;
         const auto t0 = std::chrono::steady_clock::now();
         uint32_t s = 0;
         for (uint32_t k = 0; s < c->inflight_n; k++) {
-            if ((row[s] >> 1) == c->g7[s]) {
+            if ((row[s] >> 1) == c->g7_launch[s]) {
                 s++;
                 continue;
             }
@@ -307,6 +352,7 @@ int fcc_quiesce(lx_index *h, FcCache *c) {
         HIPCHK(h, hipEventSynchronize(c->filled));
     }
     c->inflight = false;
+    c->inflight_row = c->inflight_tile = false;
     return 0;
 }
 
@@ -346,8 +392,8 @@ int fcc_query(lx_index *h, uint32_t a, uint32_t b, uint8_t *out) {
     c->st.calls++;
     int rc;
     const auto t_miss = std::chrono::steady_clock::now();
-    if (c->inflight) {
-        // the last fill may still be writing the entry (the caller returned as
+    if (c->inflight && (c->inflight_tile || c->find(a) == c->inflight_sa)) {
+        // the last fill may still be writing this entry (the caller returned as
         // soon as its own answer landed): let it finish, then look again
         if ((rc = fcc_quiesce(h, c))) return rc;
         if (fcc_hit(c, a, b, out)) {
@@ -368,23 +414,47 @@ int fcc_query(lx_index *h, uint32_t a, uint32_t b, uint8_t *out) {
             if (c->find((uint32_t)e) == LX_NONE) c->insert((uint32_t)e, sa, sb);
     }
     // a new asking event that is the pending run's only event (Add, then the
-    // caller's first ForklessCause): one launch adds it and fills its row
-    rc = a_new ? flush_add1_row(h, a, c->evk_dev, c->used, c->g7_dev, c->M_dev + (uint64_t)sa * c->W, c->d_rsum) : 1;
+    // caller's first ForklessCause): one launch adds it and fills its row; the
+    // slots changed since the mirror was written travel in its arguments
+    rc = 1;
+    if (a_new && !c->dirty_all && c->dirty.size() <= kAdd1Delta) {
+        Add1Delta d{};
+        d.n = (uint32_t)c->dirty.size();
+        for (uint32_t i = 0; i < d.n; i++) {
+            const uint32_t x = c->dirty[i];
+            d.slot[i] = x;
+            d.ev[i] = c->evk[x];
+            d.tag[i] = c->g7[x];
+        }
+        rc = flush_add1_row(h, a, c->evk_d, c->used, c->g7_d, c->M_dev + (uint64_t)sa * c->W, c->d_rsum, &d);
+        if (rc == 0) {   // the kernel stores them into the mirror
+            for (uint32_t x : c->dirty) c->dmark[x] = 0;
+            c->dirty.clear();
+        }
+    }
     const bool fused = rc == 0;
+    bool tile = false;
     if (rc == 1) {
-        if ((rc = flush_pending(h))) return rc;
-        if (a_new || a == c->last_a) rc = fcc_row(h, c, a, sa);
-        else rc = fcc_tile(h, c);
+        if ((rc = flush_pending(h)) || (rc = fcc_sync_mirror(h, c))) return rc;
+        if (a_new || a == c->last_a) {
+            rc = fcc_row(h, c, a, sa);
+        } else {
+            rc = fcc_tile(h, c);
+            tile = true;
+        }
     } else if (!rc) {
         c->st.row_fills++;
         c->st.pairs += c->used;
     }
     if (rc) return rc;
     c->inflight = true;
-    c->inflight_row = fused;
+    c->inflight_row = !tile;
+    c->inflight_tile = tile;
     c->inflight_sa = sa;
     c->inflight_n = c->used;
-    if (!fused) HIPCHK(h, hipEventRecord(c->filled, h->stream));
+    if (!tile) memcpy(c->g7_launch.data(), c->g7, c->used);
+    else HIPCHK(h, hipEventRecord(c->filled, h->stream));
+    (void)fused;
     const auto t_wait = std::chrono::steady_clock::now();
     if ((rc = fcc_wait_answer(h, c, sa, sb))) return rc;
     const auto t_end = std::chrono::steady_clock::now();

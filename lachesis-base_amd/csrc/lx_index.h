@@ -230,8 +230,9 @@ struct lx_index {
     uint64_t ld_buf_cap = 0;
 
     // pinned, device-mapped query buffers (per-call ForklessCause, getters)
-    uint8_t *qp = nullptr;
+    uint8_t *qp = nullptr, *qp_dev = nullptr;
     uint64_t qp_cap = 0;
+    uint32_t get_tag = 0;                  // completion tag of the last single-row getter
     uint32_t *q_sink = nullptr;            // status word the pinned FC path lets the kernel flag into
 
     // timing (HIP events on `stream`)
@@ -304,8 +305,14 @@ struct lx_index {
 int lx_fc_args(lx_index *h, uint64_t n, const uint32_t *a, const uint32_t *b, uint8_t *out, uint32_t *partial,
                FcArgs *fa);
 int flush_pending(lx_index *h);                 // launch the pending small-path run (lx_capi.cpp)
-int flush_add1_row(lx_index *h, uint32_t a, const uint32_t *evk_dev, uint32_t n_slots, const uint8_t *tag_dev,
-                   uint8_t *out_dev, uint32_t *psum_dev);   // 1: not applicable
+// slots of the FC cache changed since its device mirror was written
+struct Add1Delta {
+    uint32_t n;
+    uint32_t slot[kAdd1Delta], ev[kAdd1Delta];
+    uint8_t tag[kAdd1Delta];
+};
+int flush_add1_row(lx_index *h, uint32_t a, uint32_t *evk_dev, uint32_t n_slots, uint8_t *tag_dev, uint8_t *out_dev,
+                   uint32_t *psum_dev, const Add1Delta *delta);   // 1: not applicable
 int rs_begin(lx_index *h, IndexArgs ia, const uint32_t *poff, hipStream_t s);   // lx_rowseg.cpp
 void rs_free(lx_index *h);
 void fcc_destroy(lx_index *h);

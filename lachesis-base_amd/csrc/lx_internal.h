@@ -313,6 +313,8 @@ struct SmallArgs {
 // one launch (lx_small.hip k_add1_row; the unchanged caller's miss path: Add(e)
 // then ForklessCause(e, root) for the roots of a frame).  Fork-free epochs only.
 constexpr uint32_t kAdd1MaxPar = 32;
+constexpr uint32_t kAdd1Delta = 8;      // slot changes carried in k_add1_row's arguments
+constexpr uint32_t kAdd1Slots = 128;    // slots (threads) per k_add1_row workgroup
 struct Add1RowArgs {
     uint32_t *hb, *la;
     uint64_t stride;
@@ -327,13 +329,19 @@ struct Add1RowArgs {
     const uint32_t *branch_first;
     uint32_t s_cap;
     // the row: out[s] = tag[s] << 1 | ForklessCause(a, evk[s]) for s < n_slots
-    const uint32_t *evk;
+    // (evk / tag: the device mirror of the cache's slots)
+    uint32_t *evk;
     uint32_t n_slots;
-    const uint8_t *tag;
+    uint8_t *tag;
     uint8_t *out;
     const uint32_t *wpad;
     uint32_t quorum;
     uint32_t *psum;              // [n_slots] x uint64 {column groups, sum}, zero between launches
+    // slots the host changed since the mirror was last written: applied by
+    // every reader, stored into the mirror by the column-group-0 workgroups
+    uint32_t nd;
+    uint32_t d_slot[kAdd1Delta], d_ev[kAdd1Delta];
+    uint8_t d_tag[kAdd1Delta];
 };
 
 // Batches whose image fits travel in the kernel arguments (no staging copy)
@@ -413,6 +421,10 @@ struct GetArgs {
     uint8_t *out;                // row i at out + i * slot
     uint64_t slot;
     uint32_t *len;               // byte length of row i
+    // single-row call (n = 1): `tag` into pinned *done after the row and its
+    // length, so the host spins on it instead of synchronizing the stream
+    uint32_t *done;
+    uint32_t tag;
 };
 
 // ---- emitter QuorumIndexer (lx_emitter.hip, lx_emitter.cpp)

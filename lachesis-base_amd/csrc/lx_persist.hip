@@ -146,6 +146,14 @@ hipError_t launch_encode_rows(const RowsArgs &a, const uint64_t *off, uint64_t b
 // MaxInt32}), else the strictly greatest Seq (first max wins) with its MinSeq
 // (the branch's first seq), else {0, 0}; 8 x V bytes.  Without forks the
 // reference returns the raw HighestBefore row.
+// the completion tag of a single-row call: every lane's row stores are made
+// visible system-wide before lane 0 publishes the tag (pinned host memory)
+__device__ __forceinline__ void get_done(const GetArgs &a, uint32_t lane) {
+    if (!a.done) return;
+    __threadfence_system();
+    if (lane == 0) __hip_atomic_store(a.done, a.tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __global__ __launch_bounds__(256) void k_get_rows(GetArgs a) {
     const uint32_t i = blockIdx.x * 4 + threadIdx.x / 64, lane = threadIdx.x % 64;
     if (i >= a.n) return;
@@ -170,6 +178,7 @@ __global__ __launch_bounds__(256) void k_get_rows(GetArgs a) {
             *reinterpret_cast<uint2 *>(o + 2 * c) = x;
         }
         if (lane == 0) a.len[i] = 8u * a.V;
+        get_done(a, lane);
         return;
     }
     const bool hb = a.mode != 1;
@@ -193,6 +202,7 @@ __global__ __launch_bounds__(256) void k_get_rows(GetArgs a) {
         for (uint32_t c = lane; c < ent; c += 64) o[c] = row[c];
     }
     if (lane == 0) a.len[i] = ent * (hb ? 8u : 4u);
+    get_done(a, lane);
 }
 
 // ---------------------------------------------------------------------------- restart

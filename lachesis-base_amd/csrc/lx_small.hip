@@ -282,12 +282,17 @@ __global__ __launch_bounds__(256) void k_small_inline(SmallInlineArgs a) {
 // ---- k_add1_row: the unchanged caller's FC-cache miss (lx_fccache.cpp) --
 // Add of ONE pending event a and ForklessCause(a, b) for every slot b of the
 // cache, one launch.  Workgroup (cg, sg) owns columns [64 cg, 64 cg + 64) and
-// slots [256 sg, 256 sg + 256):
-//   * wave 0 computes HB(a) on its 64 columns (max over the parents' rows; each
-//     workgroup recomputes it, no communication); the sg == 0 workgroups store it
-//     and do a's LowestAfter range fill, workgroup (0, 0)
-//     writes the metadata and a's own LowestAfter row;
-//   * every thread sums, for one slot b, w_c [0 < LA(b)[c] <= HB(a)[c]] over the
+// slots [128 sg, 128 sg + 128) (>= 256 workgroups at V = 1000, W = 2000: one
+// per CU streams its slots' LowestAfter rows):
+//   * every thread first issues its slot's loads -- the slot's event and tag
+//     from the cache's device mirror (plus the host's changes since, carried
+//     in the arguments), then LA(b) on the workgroup's columns and b's branch
+//     and seq -- so they are in flight together with wave 0's HB(a) loads;
+//   * wave 0 computes HB(a) on its 64 columns (max over the parents' rows, all
+//     in flight at once; each workgroup recomputes it, no communication); the
+//     sg == 0 workgroups store it and do a's LowestAfter range fill (DESIGN.md
+//     section 3), workgroup (0, 0) writes the metadata and a's own LA row;
+//   * every thread sums, for its slot b, w_c [0 < LA(b)[c] <= HB(a)[c]] over the
 //     workgroup's columns except c = branch(a) -- the only LowestAfter column
 //     a's Add writes, in other workgroups -- for which it adds w instead when the
 //     column holds branch(b) and a reaches b: in a fork-free epoch LA(b)[br(a)]
@@ -296,31 +301,47 @@ __global__ __launch_bounds__(256) void k_small_inline(SmallInlineArgs a) {
 //     column groups so far, sum}; the thread whose add completes the count
 //     compares the sum with the quorum, writes the answer and clears the word
 //     (no last-workgroup pass, no fence).
-__global__ __launch_bounds__(256) void k_add1_row(Add1RowArgs a) {
+__global__ __launch_bounds__(kAdd1Slots) void k_add1_row(Add1RowArgs a) {
     __shared__ uint32_t hbv[64], wv[64];
     const uint32_t t = threadIdx.x, cg = blockIdx.x, sg = blockIdx.y;
-    // this thread's slot: its event and tag live in pinned host memory, so they
-    // are fetched first, under the HB computation
-    const uint32_t s = sg * 256 + t;
+    const uint32_t s = sg * kAdd1Slots + t;
     const bool has = s < a.n_slots;
-    const uint32_t b = has ? a.evk[s] : 0u;
-    const uint32_t tg = has ? a.tag[s] : 0u;
+    uint32_t b = has ? a.evk[s] : 0u;
+    uint32_t tg = has ? a.tag[s] : 0u;
+    for (uint32_t u = 0; u < a.nd; u++)      // kernel arguments: scalar loads
+        if (a.d_slot[u] == s) {
+            b = a.d_ev[u];
+            tg = a.d_tag[u];
+            if (cg == 0) {
+                a.evk[s] = b;
+                a.tag[s] = (uint8_t)tg;
+            }
+        }
     const uint32_t c0 = cg * 64;
     const uint32_t br = a.e.q0.x, seq = a.e.q0.y, prev = a.e.q0.z, np = a.e.q0.w;
     const uint64_t stride = a.stride;
+    // the slot's row and metadata, in flight under the HB computation
+    const bool other = has && b != a.a;
+    const uint32_t bq = other ? b : 0u;
+    const uint4 *lr = reinterpret_cast<const uint4 *>(a.la + (uint64_t)bq * stride + c0);
+    uint4 l[16];
+#pragma unroll
+    for (uint32_t i = 0; i < 16; i++) l[i] = lr[i];
+    const uint32_t bbr0 = a.ev_branch[bq], bseq0 = a.ev_seq[bq];
     const uint32_t c = c0 + t;
     const bool valid = t < 64 && c < a.B;
     uint32_t r = c == br ? seq : 0u, h0 = 0;
     if (t < 64) {
         const uint32_t cc = valid ? c : 0u;
-        for (uint32_t p = 0; p < np; p += 8) {
-            uint32_t v[8];
+        uint32_t v[kAdd1MaxPar / 2];
 #pragma unroll
-            for (uint32_t u = 0; u < 8; u++) v[u] = a.hb[(uint64_t)a.par[min(p + u, np - 1)] * stride + cc];
+        for (uint32_t u = 0; u < kAdd1MaxPar / 2; u++)
+            v[u] = np ? a.hb[(uint64_t)a.par[min(u, np - 1)] * stride + cc] : 0u;   // a root has no parents
+        const uint32_t hp = prev != LX_NONE ? a.hb[(uint64_t)prev * stride + cc] : 0u;
+        for (uint32_t p = kAdd1MaxPar / 2; p < np; p++) r = max(r, a.hb[(uint64_t)a.par[p] * stride + cc]);   // rare
 #pragma unroll
-            for (uint32_t u = 0; u < 8; u++) r = max(r, v[u]);
-        }
-        h0 = prev != LX_NONE ? a.hb[(uint64_t)prev * stride + cc] : 0u;
+        for (uint32_t u = 0; u < kAdd1MaxPar / 2; u++) r = max(r, v[u]);
+        h0 = hp;
         hbv[t] = valid ? r : 0u;
         wv[t] = valid && c != br ? a.wpad[c] : 0u;
     } else if (sg == 0 && cg == 0) {
@@ -342,7 +363,7 @@ __global__ __launch_bounds__(256) void k_add1_row(Add1RowArgs a) {
         }
         // a's LowestAfter row: its own branch observes it at its own seq
         uint4 *row = reinterpret_cast<uint4 *>(a.la + (uint64_t)a.a * stride);
-        for (uint32_t x = u; x < (a.B + 3) / 4; x += 192)
+        for (uint32_t x = u; x < (a.B + 3) / 4; x += kAdd1Slots - 64)
             row[x] = make_uint4(4 * x == br ? seq : 0u, 4 * x + 1 == br ? seq : 0u, 4 * x + 2 == br ? seq : 0u,
                                 4 * x + 3 == br ? seq : 0u);
     }
@@ -350,13 +371,9 @@ __global__ __launch_bounds__(256) void k_add1_row(Add1RowArgs a) {
     if (has) {
         uint32_t part = 0;
         uint32_t bbr = br, bseq = seq;
-        if (b != a.a) {
-            const uint4 *lr = reinterpret_cast<const uint4 *>(a.la + (uint64_t)b * stride + c0);
-            uint4 l[16];
-#pragma unroll
-            for (uint32_t i = 0; i < 16; i++) l[i] = lr[i];
-            bbr = a.ev_branch[b];
-            bseq = a.ev_seq[b];
+        if (other) {
+            bbr = bbr0;
+            bseq = bseq0;
 #pragma unroll
             for (uint32_t i = 0; i < 16; i++) {
                 part += (l[i].x - 1u) < hbv[4 * i] ? wv[4 * i] : 0u;
@@ -367,9 +384,6 @@ __global__ __launch_bounds__(256) void k_add1_row(Add1RowArgs a) {
         }
         if (bbr - c0 < 64 && hbv[bbr - c0] >= bseq) part += a.w_br;
         unsigned long long *w = reinterpret_cast<unsigned long long *>(a.psum) + s;
-        // every read of pinned memory (evk, tag) has returned before the count
-        // moves: once the row's last entry lands, the host may reuse the slots
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const unsigned long long old = atomicAdd(w, (1ull << 32) | part);
         if ((uint32_t)(old >> 32) == gridDim.x - 1) {
             a.out[s] = (uint8_t)(tg << 1 | ((uint32_t)old + part >= a.quorum ? 1u : 0u));
@@ -388,8 +402,9 @@ __global__ __launch_bounds__(256) void k_add1_row(Add1RowArgs a) {
 }
 
 hipError_t launch_add1_row(const Add1RowArgs &a, hipStream_t s) {
-    if (!a.n_slots || !a.B || a.e.q0.w > kAdd1MaxPar) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_add1_row, dim3((a.B + 63) / 64, (a.n_slots + 255) / 256), dim3(256), 0, s, a);
+    if (!a.n_slots || !a.B || a.e.q0.w > kAdd1MaxPar || a.nd > kAdd1Delta) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_add1_row, dim3((a.B + 63) / 64, (a.n_slots + kAdd1Slots - 1) / kAdd1Slots), dim3(kAdd1Slots),
+                       0, s, a);
     return hipGetLastError();
 }
 

@@ -443,16 +443,16 @@ def test_config3_shape_1m_default_two_segments_vs_oracle(lx):
         for (go, gb), (oo, ob) in _rows_in_chunks(ix, o, mode, ev, 50_000):
             np.testing.assert_array_equal(go, oo)
             assert np.array_equal(gb, ob), mode
-    # 1M pairs: 3/4 with a in the first 40k events of segment 1 and b within
-    # 64 Lamport of a (b mostly in segment 0), 1/4 uniform over the epoch
-    lo, hi = cut - 40_000, cut + 40_000
-    qa1, qb1 = lx.tools.fc_queries(d.lamport[lo:hi], 750_000, window=64, seed=12)
-    qa1, qb1 = qa1 + lo, qb1 + lo
-    keep = qa1 >= cut
-    qa2, qb2 = lx.tools.fc_queries(d.lamport, 1_000_000 - int(keep.sum()), window=64, seed=13)
-    qa = np.concatenate([qa1[keep], qa2]).astype(np.uint32)
-    qb = np.concatenate([qb1[keep], qb2]).astype(np.uint32)
-    assert int(((qa >= cut) & (qb < cut)).sum()) > 100_000
+    # 1M pairs: half with a among the first 20k events of segment 1 and b up to
+    # 25k events before it (most of them in segment 0), half of the bench's
+    # shape (a uniform, b within 64 Lamport of a)
+    rng = np.random.default_rng(12)
+    qa1 = (cut + rng.integers(0, 20_000, 500_000)).astype(np.int64)
+    qb1 = qa1 - rng.integers(1, 25_000, 500_000)
+    qa2, qb2 = lx.tools.fc_queries(d.lamport, 500_000, window=64, seed=13)
+    qa = np.concatenate([qa1, qa2]).astype(np.uint32)
+    qb = np.concatenate([qb1, qb2]).astype(np.uint32)
+    assert int(((qa >= cut) & (qb < cut)).sum()) > 250_000
     got = ix.forkless_cause_batch(qa, qb)
     want = o.forkless_cause_batch_mt(qa, qb, 16)
     np.testing.assert_array_equal(got, want)
