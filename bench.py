@@ -267,7 +267,7 @@ def feed_rate(dag, weights, device, batch):
                          batch, out, err, 512)
     if rc != 0:
         raise RuntimeError("lx_bench_feed: " + err.value.decode())
-    return out[0]
+    return out[0], {"seconds": out[1], "host_calls_s": out[2], "final_sync_s": out[3]}
 
 
 def config_leg(lx, name, steps, warmup, device, want_cpu, cpu_budget, fc_n=1 << 22):
@@ -337,7 +337,7 @@ def config_leg(lx, name, steps, warmup, device, want_cpu, cpu_budget, fc_n=1 << 
            "roofline_index": {"kernel": "k_index", "algorithmic_bytes_per_launch":
                               ((p_mean + 1) * 4 * B + 4 * B + 8) * N, "kernel_ms": float(np.mean(kms))}}
     if name == "c1":
-        res["per_event_add_events_per_sec"] = feed_rate(dag, weights, device, 1)
+        res["per_event_add_events_per_sec"], res["per_event_add_split"] = feed_rate(dag, weights, device, 1)
     if o is not None:
         t2 = time.perf_counter()
         done = 0
@@ -727,13 +727,12 @@ def main():
     if shard or rowseg or solo or args.segments > 1 or args.batch:
         traffic = None   # the committed profile is of the default single-GPU run
     # the walk kernel this run timed: one k_index_segs launch when the batch was
-    # walked as side-by-side segments (every segment then reports
-    # the same launch's time), else k_index; the traffic figure must be that
-    # kernel's own, or null
+    # walked as side-by-side segments, else k_index; the traffic
+    # figure must be that kernel's own, or null
     walk_kernel = "k_index"
     if not (shard or rowseg or solo):
         sg0 = ix.segment_stats()
-        if sg0["segments"] >= 2 and len(set(sg0["walk_ms"])) == 1:
+        if sg0["segments"] >= 2 and sg0["one_launch"]:
             walk_kernel = "k_index_segs"
     idx_traffic = traffic.get(walk_kernel) if traffic else None
     # compulsory HBM bytes of the walk: every HB and LA row of the epoch written

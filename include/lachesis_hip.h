@@ -340,6 +340,7 @@ typedef struct lx_seg_stats {
     uint32_t partial[64];
     float walk_ms[64];
     float partial_ms, la_ms;
+    uint32_t one_launch;    /* 1: the segments were walked side by side by one k_index_segs launch */
 } lx_seg_stats;
 int lx_last_segment_stats(const lx_index *h, lx_seg_stats *out);
 

@@ -585,6 +585,7 @@ int seg_walk(lx_index *h, IndexArgs ia, const uint32_t *poff, hipStream_t s, uin
     lx_seg_stats &st = h->seg_stats;
     st = lx_seg_stats{};
     st.segments = G;
+    st.one_launch = conc ? 1u : 0u;
     for (uint32_t k = 0; k < G; k++) {
         st.first_event[k] = a.seg_lo[k];
         st.partial[k] = pc[k];

@@ -161,21 +161,35 @@ __global__ __launch_bounds__(256) void k_get_rows(GetArgs a) {
     const uint32_t *row = a.plane + (uint64_t)e * a.stride;
     uint32_t *o = reinterpret_cast<uint32_t *>(a.out + (uint64_t)i * a.slot);
     if (a.mode == 2 && a.forks) {
-        for (uint32_t c = lane; c < a.V; c += 64) {
-            uint2 x = make_uint2(0u, 0u);
-            const int32_t k = a.cheat_of[c];
-            if (k < 0) {
-                const uint32_t v = row[c];
-                if (v) x = make_uint2(v & LX_SEQ_MASK, a.branch_first[c]);
-            } else {
-                for (uint32_t j = a.cheat_off[k]; j < a.cheat_off[k + 1]; j++) {
-                    const uint32_t b = a.cheat_br[j];
-                    const uint32_t v = row[b];
-                    if (v & LX_MARK) { x = make_uint2(0u, 0x7FFFFFFFu); break; }
-                    if (v > x.x) x = make_uint2(v, a.branch_first[b]);
+        // 8 creators per lane computed before their stores (loads after a store
+        // to host memory would wait for it, see below)
+        for (uint32_t c0 = 0; c0 < a.V; c0 += 64 * 8) {
+            uint2 xs[8];
+#pragma unroll
+            for (uint32_t u = 0; u < 8; u++) {
+                const uint32_t c = c0 + lane + 64 * u;
+                uint2 x = make_uint2(0u, 0u);
+                if (c < a.V) {
+                    const int32_t k = a.cheat_of[c];
+                    if (k < 0) {
+                        const uint32_t v = row[c];
+                        if (v) x = make_uint2(v & LX_SEQ_MASK, a.branch_first[c]);
+                    } else {
+                        for (uint32_t j = a.cheat_off[k]; j < a.cheat_off[k + 1]; j++) {
+                            const uint32_t b = a.cheat_br[j];
+                            const uint32_t v = row[b];
+                            if (v & LX_MARK) { x = make_uint2(0u, 0x7FFFFFFFu); break; }
+                            if (v > x.x) x = make_uint2(v, a.branch_first[b]);
+                        }
+                    }
                 }
+                xs[u] = x;
             }
-            *reinterpret_cast<uint2 *>(o + 2 * c) = x;
+#pragma unroll
+            for (uint32_t u = 0; u < 8; u++) {
+                const uint32_t c = c0 + lane + 64 * u;
+                if (c < a.V) *reinterpret_cast<uint2 *>(o + 2 * c) = xs[u];
+            }
         }
         if (lane == 0) a.len[i] = 8u * a.V;
         get_done(a, lane);
@@ -184,22 +198,52 @@ __global__ __launch_bounds__(256) void k_get_rows(GetArgs a) {
     const bool hb = a.mode != 1;
     const uint32_t bb = a.ev_bbefore[e];
     const uint32_t lim = hb ? bb + (a.ev_branch[e] == bb ? 1u : 0u) : a.B;
+    // the first kGetR x 64 columns (B <= 1024: the whole row) are loaded into
+    // registers before any store: gfx950 counts stores in vmcnt, so a load
+    // issued after a store to host memory would wait for that store's PCIe
+    // round trip -- interleaved, a 1000-column row took 16 of them
+    constexpr uint32_t kGetR = 16;
+    uint32_t v[kGetR], f[kGetR];
+#pragma unroll
+    for (uint32_t u = 0; u < kGetR; u++) {
+        const uint32_t c = lane + 64 * u;
+        v[u] = c < lim ? row[c] : 0u;
+        f[u] = hb && c < lim ? a.branch_first[c] : 0u;
+    }
     int last = -1;
-    for (uint32_t c = lane; c < lim; c += 64)
+#pragma unroll
+    for (uint32_t u = 0; u < kGetR; u++)
+        if (v[u]) last = (int)(lane + 64 * u);
+    for (uint32_t c = lane + 64 * kGetR; c < lim; c += 64)   // rows wider than 1024 columns
         if (row[c]) last = (int)c;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) last = max(last, __shfl_xor(last, off, 64));
     const uint32_t ent = max(bb, (uint32_t)(last + 1));
-    if (hb) {
-        for (uint32_t c = lane; c < ent; c += 64) {
-            const uint32_t v = c < lim ? row[c] : 0u;
-            uint2 x = make_uint2(0u, 0u);
-            if (v & LX_MARK) x.y = 0x7FFFFFFFu;
-            else if (v) x = make_uint2(v, a.branch_first[c]);
-            *reinterpret_cast<uint2 *>(o + 2 * c) = x;
+    auto enc = [](uint32_t x, uint32_t first) {
+        if (x & LX_MARK) return make_uint2(0u, 0x7FFFFFFFu);   // forkDetectedSeq
+        return x ? make_uint2(x, first) : make_uint2(0u, 0u);  // {Seq, MinSeq}
+    };
+#pragma unroll
+    for (uint32_t u = 0; u < kGetR; u++) {
+        const uint32_t c = lane + 64 * u;
+        if (c >= ent) continue;
+        if (hb) *reinterpret_cast<uint2 *>(o + 2 * c) = enc(v[u], f[u]);
+        else o[c] = v[u];
+    }
+    for (uint32_t c0 = 64 * kGetR; c0 < ent; c0 += 64 * kGetR) {   // wider rows: chunks, loads first
+#pragma unroll
+        for (uint32_t u = 0; u < kGetR; u++) {
+            const uint32_t c = c0 + lane + 64 * u;
+            v[u] = c < lim ? row[c] : 0u;
+            f[u] = hb && c < lim ? a.branch_first[c] : 0u;
         }
-    } else {
-        for (uint32_t c = lane; c < ent; c += 64) o[c] = row[c];
+#pragma unroll
+        for (uint32_t u = 0; u < kGetR; u++) {
+            const uint32_t c = c0 + lane + 64 * u;
+            if (c >= ent) continue;
+            if (hb) *reinterpret_cast<uint2 *>(o + 2 * c) = enc(v[u], f[u]);
+            else o[c] = v[u];
+        }
     }
     if (lane == 0) a.len[i] = ent * (hb ? 8u : 4u);
     get_done(a, lane);

@@ -149,7 +149,8 @@ class LxFcStats(ctypes.Structure):
 
 class LxSegStats(ctypes.Structure):
     _fields_ = [("segments", ctypes.c_uint32), ("first_event", ctypes.c_uint32 * 65), ("partial", ctypes.c_uint32 * 64),
-                ("walk_ms", ctypes.c_float * 64), ("partial_ms", ctypes.c_float), ("la_ms", ctypes.c_float)]
+                ("walk_ms", ctypes.c_float * 64), ("partial_ms", ctypes.c_float), ("la_ms", ctypes.c_float),
+                ("one_launch", ctypes.c_uint32)]
 
 
 class LxWriteback(ctypes.Structure):
@@ -561,7 +562,8 @@ class Index:
         self._chk(self.L.lx_last_segment_stats(self.h, ctypes.byref(st)))
         G = st.segments
         return {"segments": G, "first_event": list(st.first_event[:G + 1]), "partial": list(st.partial[:G]),
-                "walk_ms": list(st.walk_ms[:G]), "partial_ms": st.partial_ms, "la_ms": st.la_ms}
+                "walk_ms": list(st.walk_ms[:G]), "partial_ms": st.partial_ms, "la_ms": st.la_ms,
+                "one_launch": bool(st.one_launch)}
 
     def device_planes(self):
         hb, la, st = vp(), vp(), vp()

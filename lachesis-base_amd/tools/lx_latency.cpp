@@ -385,6 +385,7 @@ int lx_bench_feed(int device, uint32_t V, const uint32_t *weights, uint64_t N, c
         }
         lx_flush(h);
     }
+    const double s_host = us_since(t0) * 1e-6;
     if (lx_sync(h)) {
         snprintf(err, err_cap, "sync: %s", lx_last_error(h));
         lx_destroy(h);
@@ -393,6 +394,8 @@ int lx_bench_feed(int device, uint32_t V, const uint32_t *weights, uint64_t N, c
     const double s = us_since(t0) * 1e-6;
     out[0] = N / s;
     out[1] = s;
+    out[2] = s_host;       // the Add / Flush calls alone
+    out[3] = s - s_host;   // the final lx_sync (device work left when the last call returned)
     lx_destroy(h);
     return 0;
 }
