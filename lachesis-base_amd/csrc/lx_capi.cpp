@@ -1286,7 +1286,11 @@ int flush_pending(lx_index *h) {
     a.s_cap = h->s_cap;
     a.mask = B > h->V ? 1u : 0u;
     if (h->small_timing) HIPCHK(h, hipEventRecord(h->ev[1], s));
-    HIPCHK(h, inl ? lx::launch_small_inline(h->sm_inl, s) : lx::launch_small(a, s));
+    // a deep run of few fork-free branches (per-event Adds of configs[0]: every
+    // event its own level) by frontier doubling instead of level by level
+    const bool dbl = h->dbl && !inl && !a.mask && B <= kDblMaxB && L >= kSmallDblLevels &&
+                     small_dbl_lds_bytes(n, B, nh) <= kDblLds;
+    HIPCHK(h, inl ? lx::launch_small_inline(h->sm_inl, s) : dbl ? lx::launch_small_dbl(a, s) : lx::launch_small(a, s));
     if (!inl) h->st_used[slot] = true;
     if (h->small_timing) HIPCHK(h, hipEventRecord(h->ev[2], s));
     if (B > h->V && h->n_cheat) {

@@ -275,6 +275,7 @@ constexpr uint32_t kSmallCont = 1u;
 constexpr uint32_t kSmallCW = 4;     // columns per workgroup (256 threads = 4 columns x 64 event lanes)
 constexpr uint32_t kSmallMaxN = 2048;   // events per small batch (positions are 16-bit; LDS below)
 constexpr uint32_t kPendLaunch = 2048;  // a pending run of small batches launches at this size
+constexpr uint32_t kSmallDblLevels = 128;   // runs this deep (and <= kDblMaxB branches) go to k_small_dbl
 constexpr uint32_t kSmallLds = 160 * 1024 - 256;   // dynamic LDS of one k_small workgroup
 struct SmallEv {
     uint4 q0, q1, q2;
@@ -284,6 +285,11 @@ struct SmallEv {
 // events (uint16)
 __host__ __device__ inline uint64_t small_lds_bytes(uint64_t n, uint64_t nh, uint64_t L, uint64_t npl) {
     return 16 * (n + nh) + 8 * ((n + 1) & ~1ull) + 2 * ((npl + 7) & ~7ull) + 4 * (L + 1) + 2 * n;
+}
+// dynamic LDS of k_small_dbl: the run's rows and the older previous events'
+// rows (B words each), per-branch tables, chain positions (uint16)
+__host__ __device__ inline uint64_t small_dbl_lds_bytes(uint64_t n, uint64_t B, uint64_t nh) {
+    return 4 * ((n + nh) * B + 4 * B + 3) + 2 * ((n + 1) & ~1ull);
 }
 struct SmallArgs {
     uint32_t *hb, *la;
@@ -616,6 +622,7 @@ hipError_t launch_rs_la_apply(const RsArgs &r, const uint32_t *triples, uint64_t
 hipError_t launch_batch_prepare(const BatchArgs &a, void *scan_tmp, size_t scan_tmp_bytes, hipStream_t s);
 hipError_t launch_batch_finish(const BatchArgs &a, uint32_t jump_rounds, hipStream_t s);
 hipError_t launch_small(const SmallArgs &a, hipStream_t s);
+hipError_t launch_small_dbl(const SmallArgs &a, hipStream_t s);   // needs the image on the device
 hipError_t launch_small_inline(const SmallInlineArgs &a, hipStream_t s);
 hipError_t launch_add1_row(const Add1RowArgs &a, hipStream_t s);
 hipError_t scan_tmp_bytes(uint32_t n, size_t *bytes);

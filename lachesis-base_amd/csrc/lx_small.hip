@@ -423,6 +423,172 @@ hipError_t launch_stage(uint32_t *dst, const uint32_t *src, uint64_t words, hipS
     return hipGetLastError();
 }
 
+// ---- k_small_dbl: a deep, narrow pending run (the reference's per-event Add
+// on configs[0]: 5 validators, every event its own DAG level) -- k_small pays
+// one LDS barrier per level, so a 2048-event chain is 2048 dependent steps.
+// One workgroup holds the run's whole rows (B <= kDblMaxB columns, fork-free)
+// in LDS and iterates them to the fixpoint of k_dbl (lx_dbl.hip: compose
+// through the in-run event J(e, c') that HB[e][c'] names, chain prefix max
+// per branch), ~log2(depth) rounds; the metadata, branch rows, older parents
+// and the LowestAfter range fill are those of k_small, on the same staged
+// image.  Every value is the seq of an ancestor and the fixpoint folds in
+// every parent, so the rows are CollectFrom's max-join (vecfc/vector_ops.go:49-79).
+constexpr uint32_t kSdThreads = 1024;
+
+__global__ __launch_bounds__(kSdThreads) void k_small_dbl(SmallArgs a) {
+    extern __shared__ uint32_t sm[];
+    const uint32_t *img = a.img;
+    const SmallEv *ev = reinterpret_cast<const SmallEv *>(img);
+    const uint2 *meta = reinterpret_cast<const uint2 *>(img + a.o_meta);
+    const uint16_t *pl = reinterpret_cast<const uint16_t *>(img + a.o_pl);
+    const uint2 *old = reinterpret_cast<const uint2 *>(img + a.o_old);
+    const uint32_t *new_first = img + a.o_nfirst, *new_creator = img + a.o_ncreator, *blen = img + a.o_blen;
+    const uint32_t n = a.n, B = a.B, B0 = a.B0, nh = a.n_h0, bs = a.bs;
+    const uint64_t stride = a.stride;
+    uint32_t *hbl = sm;              // n * B: the run's HB rows
+    uint32_t *h0v = hbl + n * B;     // nh * B: rows of older previous branch events
+    uint32_t *s0 = h0v + nh * B;     // B: first seq of the branch in the run (~0: none)
+    uint32_t *cnt = s0 + B;          // B: events of the branch in the run
+    uint32_t *start = cnt + B;       // B + 1: chain offsets into posl
+    uint32_t *first = start + B + 1; // B: the branch's first seq (epoch)
+    uint32_t *flag = first + B;      // [0] changed in this round
+    uint16_t *posl = reinterpret_cast<uint16_t *>(flag + 2);   // run positions, chain (seq) order per branch
+    const uint32_t t = threadIdx.x, lane = t % 64, wave = t / 64;
+
+    // ---- metadata, new branches, branch lengths (k_small phase 0)
+    for (uint32_t i = t; i < n; i += kSdThreads) {
+        const SmallEv e = ev[i];
+        const uint32_t g = bs + i;
+        a.ev_creator[g] = e.q2.x;
+        a.ev_seq[g] = e.q0.y;
+        a.ev_branch[g] = e.q0.x;
+        a.ev_bbefore[g] = e.q1.w;
+        a.ev_sp[g] = e.q1.z;
+        a.first_child[g] = e.q2.z;
+        if (e.q2.y & kSmallCont) {
+            if (e.q1.z == LX_NONE) a.first_root[e.q2.x] = g;
+            else if (e.q1.z < bs) a.first_child[e.q1.z] = g;
+        }
+        a.brow[(uint64_t)e.q0.x * a.s_cap + (e.q0.y - e.q1.y)] = g;
+    }
+    for (uint32_t b = t; b < B - B0; b += kSdThreads) {
+        a.branch_first[B0 + b] = new_first[b];
+        a.branch_creator[B0 + b] = new_creator[b];
+    }
+    for (uint32_t i = t; i < a.n_blen; i += kSdThreads) a.branch_len[blen[2 * i]] = blen[2 * i + 1];
+    for (uint32_t c = t; c < B; c += kSdThreads) {
+        s0[c] = 0xFFFFFFFFu;
+        cnt[c] = 0;
+        first[c] = c >= B0 ? new_first[c - B0] : a.branch_first[c];
+    }
+    for (uint32_t x = t; x < (n + nh) * B; x += kSdThreads) hbl[x] = 0;   // hbl and h0v
+    // zeroed LowestAfter rows of the run's events (whole 16-B groups)
+    const uint32_t B4 = (B + 3) / 4;
+    for (uint32_t x = t; x < n * B4; x += kSdThreads)
+        reinterpret_cast<uint4 *>(a.la + (uint64_t)(bs + x / B4) * stride)[x % B4] = make_uint4(0, 0, 0, 0);
+    if (t == 0) flag[0] = 0;
+    __syncthreads();
+    for (uint32_t i = t; i < n; i += kSdThreads) {
+        const uint4 q0 = ev[i].q0;
+        atomicMin(&s0[q0.x], q0.y);
+        atomicAdd(&cnt[q0.x], 1u);
+        hbl[i * B + q0.x] = q0.y;   // own seq in its own column
+    }
+    __syncthreads();
+    if (t == 0) {
+        start[0] = 0;
+        for (uint32_t c = 0; c < B; c++) start[c + 1] = start[c] + cnt[c];
+    }
+    __syncthreads();
+    // chain order; the direct in-run parents by (branch, seq); the older
+    // parents and older previous branch events by their final rows
+    for (uint32_t i = t; i < n; i += kSdThreads) {
+        const uint4 q0 = ev[i].q0;
+        posl[start[q0.x] + (q0.y - s0[q0.x])] = (uint16_t)i;   // seqs of a branch in the run are consecutive
+    }
+    for (uint32_t j = t; j < n; j += kSdThreads) {
+        const uint2 m = meta[j];
+        const uint32_t i = m.x & 0xFFFFu, cnt4 = m.x >> 16, off4 = m.y;
+        for (uint32_t x = 4 * off4; x < 4 * (off4 + cnt4); x++) {
+            const uint32_t p = pl[x];
+            if (p == i) continue;   // padding
+            const uint4 pq = ev[p].q0;
+            atomicMax(&hbl[i * B + pq.x], pq.y);
+        }
+    }
+    for (uint32_t x = t; x < a.n_old * B; x += kSdThreads) {
+        const uint2 o = old[x / B];
+        const uint32_t c = x % B;
+        const uint32_t v = a.hb[(uint64_t)o.y * stride + c];
+        if (o.x & 0x80000000u) h0v[(o.x & 0x7FFFFFFFu) * B + c] = v;
+        else atomicMax(&hbl[o.x * B + c], v);
+    }
+    __syncthreads();
+
+    // ---- the fixpoint (k_dbl): compose, then chain prefix max, until nothing changes
+    for (;;) {
+        bool ch = false;
+        for (uint32_t x = t; x < n * B; x += kSdThreads) {
+            const uint32_t i = x / B, c = x - i * B;
+            const uint32_t *row = hbl + i * B;
+            uint32_t v = row[c];
+            for (uint32_t c2 = 0; c2 < B; c2++) {
+                const uint32_t d = row[c2] - s0[c2];
+                if (d < cnt[c2]) v = max(v, hbl[(uint32_t)posl[start[c2] + d] * B + c]);
+            }
+            if (v != hbl[x]) { hbl[x] = v; ch = true; }
+        }
+        __syncthreads();
+        for (uint32_t pr = wave; pr < B * B; pr += kSdThreads / 64) {
+            const uint32_t c2 = pr / B, k = pr - c2 * B, m = cnt[c2], o = start[c2];
+            uint32_t carry = 0;
+            for (uint32_t off = 0; off < m; off += 64) {
+                const uint32_t idx = off + lane;
+                const uint32_t cell = idx < m ? (uint32_t)posl[o + idx] * B + k : 0u;
+                const uint32_t old_v = idx < m ? hbl[cell] : 0u;
+                uint32_t v = old_v;
+#pragma unroll
+                for (uint32_t dd = 1; dd < 64; dd <<= 1) {
+                    const uint32_t u = __shfl_up(v, dd, 64);
+                    if (lane >= dd) v = max(v, u);
+                }
+                v = max(v, carry);
+                if (idx < m && v != old_v) { hbl[cell] = v; ch = true; }
+                carry = __shfl(v, 63, 64);
+            }
+        }
+        if (ch) flag[0] = 1;
+        __syncthreads();
+        const bool more = flag[0] != 0;
+        __syncthreads();
+        if (!more) break;
+        if (t == 0) flag[0] = 0;
+        __syncthreads();
+    }
+
+    // ---- HB rows out, then the LowestAfter range fill (k_small phase 3)
+    for (uint32_t x = t; x < n * B; x += kSdThreads) {
+        const uint32_t i = x / B, c = x - i * B;
+        a.hb[(uint64_t)(bs + i) * stride + c] = hbl[x];
+    }
+    for (uint32_t x = t; x < n * B; x += kSdThreads) {
+        const uint32_t i = x / B, c = x - i * B;
+        const uint4 q0 = ev[i].q0;
+        const uint32_t prev = q0.z;
+        const uint32_t h0 = prev == LX_NONE ? 0u : prev >= bs ? hbl[(prev - bs) * B + c] : h0v[ev[i].q2.w * B + c];
+        const uint32_t f = first[c];
+        for (uint32_t sq = max(h0 + 1u, f); sq <= hbl[x]; sq++)
+            a.la[(uint64_t)a.brow[(uint64_t)c * a.s_cap + (sq - f)] * stride + q0.x] = q0.y;
+    }
+}
+
+hipError_t launch_small_dbl(const SmallArgs &a, hipStream_t s) {
+    if (!a.n || !a.B) return hipSuccess;
+    if (a.mask || a.B > kDblMaxB || !a.img || small_dbl_lds_bytes(a.n, a.B, a.n_h0) > kDblLds) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_small_dbl, dim3(1), dim3(kSdThreads), small_dbl_lds_bytes(a.n, a.B, a.n_h0), s, a);
+    return hipGetLastError();
+}
+
 hipError_t launch_small(const SmallArgs &a, hipStream_t s) {
     if (!a.n || !a.B) return hipSuccess;
     const uint32_t grid = (a.B + kSmallCW - 1) / kSmallCW;

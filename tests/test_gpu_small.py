@@ -404,3 +404,36 @@ def test_pending_run_flush_drop_readd(lx):
     qa, qb = lx.tools.fc_queries(d.lamport, 50_000, window=24, seed=5)
     np.testing.assert_array_equal(ix.forkless_cause_batch(qa, qb), o.forkless_cause_batch(qa, qb))
     ix.close()
+
+
+@pytest.mark.parametrize("V,epv,P,batch", [(5, 1000, 5, 1), (5, 600, 3, 7), (16, 300, 6, 1), (3, 900, 2, 33)])
+def test_deep_runs_by_frontier_doubling(lx, V, epv, P, batch):
+    """BASELINE configs[0]'s regime, Add by Add (vecengine/index.go:71-75): a
+    few validators, every event its own DAG level, so each 2048-event pending
+    run is ~2048 levels deep and is indexed by k_small_dbl (frontier doubling
+    in one workgroup) instead of level by level.  Every row, branch and merged
+    row equals the oracle's, and FC of all recent pairs; the same stream with
+    option dbl=0 (k_small, level by level) gives identical answers."""
+    d = lx.tools.gen_dag(V, epv, P, seed=V + epv)
+    N = len(d)
+    w = [1 + (i * 3) % 7 for i in range(V)]
+    o = oracle_for(d, w)
+    outs = []
+    for dbl in (1, 0):
+        ix = lx.Index(options={"dbl": dbl})
+        ix.reset(w)
+        for lo in range(0, N, batch):
+            hi = min(N, lo + batch)
+            ix.add_batch(d.creator[lo:hi], d.seq[lo:hi], d.poff[lo:hi + 1] - d.poff[lo], d.par[d.poff[lo]:])
+            ix.flush()
+        ev = np.arange(0, N, 1 if N <= 3000 else 3)
+        if dbl:
+            rows_equal(ix, o, ev)
+        qa = np.repeat(np.arange(N - 300, N, dtype=np.uint32), 300)
+        qb = np.tile(np.arange(N - 600, N - 300, dtype=np.uint32), 300)
+        got = ix.forkless_cause_batch(qa, qb)
+        np.testing.assert_array_equal(got, o.forkless_cause_batch(qa, qb))
+        outs.append((got, ix.rows_np(0, np.arange(N, dtype=np.uint32))[1], ix.rows_np(1, np.arange(N, dtype=np.uint32))[1]))
+        ix.close()
+    for a, b in zip(outs[0], outs[1]):
+        assert np.array_equal(a, b)
