@@ -199,6 +199,9 @@ typedef struct lx_fc_stats {
     uint32_t slots_used;
     uint64_t miss_ns;       /* host time inside misses (launch + wait), ns */
     uint64_t wait_ns;       /* ... of which waiting for the answer to land */
+    uint64_t launch_ns;     /* ... of which inside the fill's enqueue calls (flush, copies, launch) */
+    uint64_t quiesce_ns;    /* ... of which waiting for an earlier fill to finish writing */
+    uint64_t fused;         /* row fills that were also the asking event's Add (k_add1_row) */
 } lx_fc_stats;
 int lx_fc_cache_stats(const lx_index *h, lx_fc_stats *out);
 

@@ -334,6 +334,7 @@ int fcc_tile(lx_index *h, FcCache *c) {
 // it was launched with, a tile fill by its event
 int fcc_quiesce(lx_index *h, FcCache *c) {
     if (!c->inflight) return 0;
+    const auto tq = std::chrono::steady_clock::now();
     if (!c->inflight_tile) {
         const volatile uint8_t *row = c->M + (uint64_t)c->inflight_sa * c->W;
         const auto t0 = std::chrono::steady_clock::now();
@@ -353,6 +354,8 @@ int fcc_quiesce(lx_index *h, FcCache *c) {
     }
     c->inflight = false;
     c->inflight_row = c->inflight_tile = false;
+    c->st.quiesce_ns +=
+        (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - tq).count();
     return 0;
 }
 
@@ -416,6 +419,7 @@ int fcc_query(lx_index *h, uint32_t a, uint32_t b, uint8_t *out) {
     // a new asking event that is the pending run's only event (Add, then the
     // caller's first ForklessCause): one launch adds it and fills its row; the
     // slots changed since the mirror was written travel in its arguments
+    const auto t_launch = std::chrono::steady_clock::now();
     rc = 1;
     if (a_new && !c->dirty_all && c->dirty.size() <= kAdd1Delta) {
         Add1Delta d{};
@@ -433,6 +437,7 @@ int fcc_query(lx_index *h, uint32_t a, uint32_t b, uint8_t *out) {
         }
     }
     const bool fused = rc == 0;
+    if (fused) c->st.fused++;
     bool tile = false;
     if (rc == 1) {
         if ((rc = flush_pending(h)) || (rc = fcc_sync_mirror(h, c))) return rc;
@@ -454,8 +459,8 @@ int fcc_query(lx_index *h, uint32_t a, uint32_t b, uint8_t *out) {
     c->inflight_n = c->used;
     if (!tile) memcpy(c->g7_launch.data(), c->g7, c->used);
     else HIPCHK(h, hipEventRecord(c->filled, h->stream));
-    (void)fused;
     const auto t_wait = std::chrono::steady_clock::now();
+    c->st.launch_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t_wait - t_launch).count();
     if ((rc = fcc_wait_answer(h, c, sa, sb))) return rc;
     const auto t_end = std::chrono::steady_clock::now();
     c->st.miss_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t_end - t_miss).count();

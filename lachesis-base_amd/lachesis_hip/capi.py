@@ -144,7 +144,8 @@ class LxStats(ctypes.Structure):
 class LxFcStats(ctypes.Structure):
     _fields_ = [("calls", ctypes.c_uint64), ("hits", ctypes.c_uint64), ("row_fills", ctypes.c_uint64),
                 ("tile_fills", ctypes.c_uint64), ("pairs", ctypes.c_uint64), ("slots", ctypes.c_uint32),
-                ("slots_used", ctypes.c_uint32), ("miss_ns", ctypes.c_uint64), ("wait_ns", ctypes.c_uint64)]
+                ("slots_used", ctypes.c_uint32), ("miss_ns", ctypes.c_uint64), ("wait_ns", ctypes.c_uint64),
+                ("launch_ns", ctypes.c_uint64), ("quiesce_ns", ctypes.c_uint64), ("fused", ctypes.c_uint64)]
 
 
 class LxSegStats(ctypes.Structure):

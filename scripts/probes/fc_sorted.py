@@ -20,8 +20,8 @@ dev = torch.device("cuda", 0)
 to_dev = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int32)).to(dev)
 ix = lx.Index(event_capacity=N)
 ix.reset(w)
-ix.add_batch_dev(N, to_dev(d.creator).data_ptr(), to_dev(d.seq).data_ptr(), to_dev(d.poff.astype(np.uint32)).data_ptr(),
-                 to_dev(d.par).data_ptr())
+keep = [to_dev(d.creator), to_dev(d.seq), to_dev(d.poff.astype(np.uint32)), to_dev(d.par)]   # alive until the add
+ix.add_batch_dev(N, *[t.data_ptr() for t in keep])
 ix.sync()
 nq = 1 << 24
 qa, qb = lx.tools.fc_queries(d.lamport, nq, window=64, seed=7)
