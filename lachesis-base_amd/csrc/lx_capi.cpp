@@ -2173,11 +2173,13 @@ int get_rows(lx_index *h, uint32_t mode, uint32_t n, const uint32_t *ev, uint8_t
     uint8_t *hp, *dp;
     int rc;
     if ((rc = ensure_qp(h, head + n * sl, &hp, &dp))) return rc;
-    memcpy(hp, ev, n * 4ull);
+    if (n > 1) memcpy(hp, ev, n * 4ull);
     GetArgs a{};
     a.plane = mode == 1 ? h->la : h->hb;
     a.stride = h->stride;
-    a.ev = reinterpret_cast<const uint32_t *>(dp);
+    // one row: the event travels in the arguments (no read of host memory)
+    a.ev = n > 1 ? reinterpret_cast<const uint32_t *>(dp) : nullptr;
+    a.ev0 = ev[0];
     a.n = n;
     a.B = h->B;
     a.V = h->V;

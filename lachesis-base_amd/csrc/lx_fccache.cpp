@@ -73,7 +73,7 @@ struct FcCache {
     uint32_t inflight_sa = 0, inflight_n = 0;
     std::vector<uint8_t> g7_launch;                 // the column generations the in-flight row fill writes
     lx_index *h = nullptr;
-    // k_add1_row's per-slot {count, sum} words (W x uint64), zero between launches
+    // k_add1_row's per-slot {count, sum} words (one per 128-B line), zero between launches
     uint32_t *d_rsum = nullptr;
     std::vector<uint32_t> ev;                       // slot -> event (LX_NONE: free)
     std::vector<uint8_t> ref;                       // clock reference bits
@@ -199,8 +199,8 @@ int fcc_make(lx_index *h) {
     if (e == hipSuccess) { e = pin((void **)&c->M, &d, (uint64_t)W * W); c->M_dev = static_cast<uint8_t *>(d); }
     if (e == hipSuccess) { e = pin((void **)&c->qa, &d, 64); c->qa_dev = static_cast<uint32_t *>(d); }
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->filled, hipEventDisableTiming);
-    if (e == hipSuccess) e = hipMalloc((void **)&c->d_rsum, 8ull * W);
-    if (e == hipSuccess) e = hipMemsetAsync(c->d_rsum, 0, 8ull * W, h->stream);
+    if (e == hipSuccess) e = hipMalloc((void **)&c->d_rsum, 8ull * kAdd1PsumStride * W);
+    if (e == hipSuccess) e = hipMemsetAsync(c->d_rsum, 0, 8ull * kAdd1PsumStride * W, h->stream);
     if (e != hipSuccess) {
         fcc_free(c);
         return h->hip(e, "ForklessCause cache (pinned memory)");

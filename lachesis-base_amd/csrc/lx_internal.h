@@ -321,6 +321,7 @@ struct SmallArgs {
 constexpr uint32_t kAdd1MaxPar = 32;
 constexpr uint32_t kAdd1Delta = 8;      // slot changes carried in k_add1_row's arguments
 constexpr uint32_t kAdd1Slots = 128;    // slots (threads) per k_add1_row workgroup
+constexpr uint32_t kAdd1PsumStride = 16;   // uint64 words between two slots' partial-sum words (128 B)
 struct Add1RowArgs {
     uint32_t *hb, *la;
     uint64_t stride;
@@ -342,7 +343,7 @@ struct Add1RowArgs {
     uint8_t *out;
     const uint32_t *wpad;
     uint32_t quorum;
-    uint32_t *psum;              // [n_slots] x uint64 {column groups, sum}, zero between launches
+    uint32_t *psum;              // [n_slots] x kAdd1PsumStride x uint64: {column groups, sum}, zero between launches
     // slots the host changed since the mirror was last written: applied by
     // every reader, stored into the mirror by the column-group-0 workgroups
     uint32_t nd;
@@ -413,7 +414,8 @@ struct LoadVerifyArgs {
 struct GetArgs {
     const uint32_t *plane;       // hb (modes 0, 2) or la (mode 1)
     uint64_t stride;
-    const uint32_t *ev;          // events (device-visible)
+    const uint32_t *ev;          // events (device-visible; NULL: the one event ev0, n = 1)
+    uint32_t ev0;
     uint32_t n;
     uint32_t B, V;
     uint32_t mode;

@@ -157,7 +157,7 @@ __device__ __forceinline__ void get_done(const GetArgs &a, uint32_t lane) {
 __global__ __launch_bounds__(256) void k_get_rows(GetArgs a) {
     const uint32_t i = blockIdx.x * 4 + threadIdx.x / 64, lane = threadIdx.x % 64;
     if (i >= a.n) return;
-    const uint32_t e = a.ev[i];
+    const uint32_t e = a.ev ? a.ev[i] : a.ev0;
     const uint32_t *row = a.plane + (uint64_t)e * a.stride;
     uint32_t *o = reinterpret_cast<uint32_t *>(a.out + (uint64_t)i * a.slot);
     if (a.mode == 2 && a.forks) {
@@ -204,12 +204,17 @@ __global__ __launch_bounds__(256) void k_get_rows(GetArgs a) {
     // round trip -- interleaved, a 1000-column row took 16 of them
     constexpr uint32_t kGetR = 16;
     uint32_t v[kGetR], f[kGetR];
+    // (the loads do not wait for lim: entries of branches created after the
+    // event's Add are 0 in its HighestBefore row, and masked below anyway)
 #pragma unroll
     for (uint32_t u = 0; u < kGetR; u++) {
         const uint32_t c = lane + 64 * u;
-        v[u] = c < lim ? row[c] : 0u;
-        f[u] = hb && c < lim ? a.branch_first[c] : 0u;
+        v[u] = c < a.B ? row[c] : 0u;
+        f[u] = hb && c < a.B ? a.branch_first[c] : 0u;
     }
+#pragma unroll
+    for (uint32_t u = 0; u < kGetR; u++)
+        if (lane + 64 * u >= lim) v[u] = 0u;
     int last = -1;
 #pragma unroll
     for (uint32_t u = 0; u < kGetR; u++)
