@@ -383,8 +383,7 @@ __global__ __launch_bounds__(kAdd1Slots) void k_add1_row(Add1RowArgs a) {
             }
         }
         if (bbr - c0 < 64 && hbv[bbr - c0] >= bseq) part += a.w_br;
-        // one 128-B line per slot: the 16+ column groups' atomics on a slot meet
-        // in its own line instead of queueing behind 15 other slots' at L2
+        // (kAdd1PsumStride 1: one 128-B line per slot measured slower)
         unsigned long long *w = reinterpret_cast<unsigned long long *>(a.psum) + (uint64_t)s * kAdd1PsumStride;
         const unsigned long long old = atomicAdd(w, (1ull << 32) | part);
         if ((uint32_t)(old >> 32) == gridDim.x - 1) {
