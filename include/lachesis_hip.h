@@ -81,6 +81,9 @@ const char *lx_last_error(const lx_index *h);
  *                if it cannot be pinned the handle answers through lx_forkless_cause_batch
  *   "seg_count", "seg_rank"  G in 2..64 and r < G, before lx_reset: a row-segment rank
  *                (lx_rowseg_*, below); 0 = off
+ *   "seg_sub"    row-segment rank: its own segment walked as this many side-by-side
+ *                sub-segments (0: auto, as "seg_auto" would split the rank's share; the
+ *                same value on every rank of a job)
  *   "segments"   G in 2..64: a batch of >= 64 G events is walked as G Add-order segments
  *                and fixed up (the single-GPU form of the row-segment multi-GPU
  *                protocol; results identical); 0/1 off

@@ -478,6 +478,14 @@ uint32_t walk_grid(const lx_index *h, uint32_t cpw_hint) {
 // smallest pass / G wins.  0 when the batch stays one walk; *cpw = the width.
 uint32_t auto_segments(const lx_index *h, uint64_t n, uint32_t *cpw) {
     if (!h->seg_auto || h->sharded() || h->rowseg() || h->segments > 1 || !h->ncols) return 0;
+    return seg_pick(h, n, cpw);
+}
+
+}  // namespace
+
+// the segment count and slice width auto_segments would pick for n events
+// (row-segment ranks split their own segment by it too, lx_rowseg.cpp)
+uint32_t seg_pick(const lx_index *h, uint64_t n, uint32_t *cpw) {
     static const float kPass[9] = {0, 1.0f, 1.15f, 0, 1.28f, 0, 0, 0, kPass8};
     // 8-column slices: packed 16-bit slots only (every seq <= 0xFFFF, no forks)
     const bool w8 = h->pack16 && h->max_seq <= 0xFFFFu && h->B <= h->V;
@@ -495,6 +503,10 @@ uint32_t auto_segments(const lx_index *h, uint64_t n, uint32_t *cpw) {
     }
     return best_g;
 }
+
+uint32_t seg_walk_grid(const lx_index *h, uint32_t cpw) { return walk_grid(h, cpw); }
+
+namespace {
 
 int seg_walk(lx_index *h, IndexArgs ia, const uint32_t *poff, hipStream_t s, uint32_t G, uint32_t cpw) {
     const uint32_t n = ia.n, bs = ia.batch_start;
@@ -515,6 +527,7 @@ int seg_walk(lx_index *h, IndexArgs ia, const uint32_t *poff, hipStream_t s, uin
     a.brow = h->brow;
     a.s_cap = h->s_cap;
     a.own_seg = LX_NONE;
+    a.per_rank = 1;
     int rc;
     if ((rc = grow_scratch(h, &h->seg_jt, &h->seg_jt_cap, (uint64_t)(G + 1) * h->B)) ||
         (rc = grow_scratch(h, &h->seg_cnt, &h->seg_cnt_cap, (uint64_t)h->B + 2 * kMaxSegments)) ||
@@ -1719,6 +1732,11 @@ int lx_set_option(lx_index *h, const char *name, int64_t value) {
         if (value < 0 || value > (int64_t)kMaxSegments) return h->fail(LX_ERR_ARG, "segments must be 0..%u", kMaxSegments);
         if (value > 1 && h->sharded()) return h->fail(LX_ERR_STATE, "segments on a column shard");
         h->segments = (uint32_t)value;
+    } else if (k == "seg_sub") {
+        // row-segment ranks: sub-segments each rank walks side by side (0: auto);
+        // every rank of a job must use the same value
+        if (value < 0 || value > (int64_t)kSegLaunchMax) return h->fail(LX_ERR_ARG, "seg_sub must be 0..%u", kSegLaunchMax);
+        h->rs_sub_opt = (uint32_t)value;
     } else if (k == "fc_cache") {
         if (value < 0 || value > 16384) return h->fail(LX_ERR_ARG, "fc_cache must be 0..16384");
         fcc_destroy(h);

@@ -260,6 +260,10 @@ struct lx_index {
     uint32_t rs_rank = 0, rs_count = 0;
     int rs_state = 0;                      // 0 idle, 1 rows needed, 2 rows final, 3 LowestAfter sent, 4 ready
     uint32_t rs_lo = 0, rs_hi = 0, rs_npartial = 0, rs_nreq = 0;
+    // the rank's own segment walked as rs_sub side-by-side sub-segments (option
+    // seg_sub, 0: auto); rs_seg_lo then holds rs_count x rs_sub segments
+    uint32_t rs_sub = 1, rs_sub_opt = 0;
+    uint32_t rs_npart[kMaxSegments] = {};   // partial events per own sub-segment
     uint32_t rs_seg_lo[kMaxSegments + 1] = {};
     uint32_t *rs_need = nullptr, *rs_req = nullptr, *rs_ctr = nullptr, *rs_ids = nullptr, *rs_out = nullptr,
              *rs_send = nullptr;
@@ -314,6 +318,8 @@ struct Add1Delta {
 int flush_add1_row(lx_index *h, uint32_t a, uint32_t *evk_dev, uint32_t n_slots, uint8_t *tag_dev, uint8_t *out_dev,
                    uint32_t *psum_dev, const Add1Delta *delta);   // 1: not applicable
 int rs_begin(lx_index *h, IndexArgs ia, const uint32_t *poff, hipStream_t s);   // lx_rowseg.cpp
+uint32_t seg_pick(const lx_index *h, uint64_t n, uint32_t *cpw);    // lx_capi.cpp (auto_segments)
+uint32_t seg_walk_grid(const lx_index *h, uint32_t cpw);
 void rs_free(lx_index *h);
 void fcc_destroy(lx_index *h);
 void fcc_clear(lx_index *h);                    // Reset: a new epoch

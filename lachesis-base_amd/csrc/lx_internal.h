@@ -562,11 +562,14 @@ struct SegArgs {
     // branch, every branch's first event in the segment
     uint32_t *elist;
     uint32_t *ecount;
-    uint32_t own_seg;            // row-segment rank: its segment; LX_NONE: every segment of the batch
-    uint32_t own_lo;             // rows below it are another rank's: their entries go to out[seg_of(row)]
-    uint32_t *out;               // per destination segment d: out_cap triples (row, column, seq) at out + 3 d out_cap
-    uint32_t *out_count;         // [G]
+    uint32_t own_seg;            // row-segment rank: its first segment; LX_NONE: every segment of the batch
+    uint32_t own_lo;             // rows below it are another rank's: their entries go to out[owner rank]
+    uint32_t *out;               // per destination rank d: out_cap triples (row, column, seq) at out + 3 d out_cap
+    uint32_t *out_count;         // [ranks]
     uint64_t out_cap;
+    // row-segment rank: segments per rank (its own segment walked as per_rank
+    // side-by-side sub-segments); the owner rank of segment k is k / per_rank
+    uint32_t per_rank;
 };
 
 // Row-segment multi-GPU exchange (lx_rowseg.cpp): rows a rank needs from the
@@ -600,7 +603,8 @@ hipError_t launch_seg_tables(const SegArgs &a, hipStream_t s);
 hipError_t launch_seg_partial(const SegArgs &a, uint32_t k, uint32_t count, hipStream_t s);
 hipError_t launch_seg_edges(const SegArgs &a, uint32_t k, uint32_t n_partial, hipStream_t s);
 hipError_t launch_seg_la_edge(const SegArgs &a, uint32_t k, uint32_t count, hipStream_t s);
-hipError_t launch_rs_refs(const SegArgs &a, const RsArgs &r, uint32_t n_partial, hipStream_t s);
+hipError_t launch_rs_refs(const SegArgs &a, const RsArgs &r, const uint32_t *n_partial /* per own segment */,
+                          hipStream_t s);
 hipError_t rsq_tmp_bytes(uint64_t n, uint32_t G, size_t *bytes);
 hipError_t launch_rsq_route(const RsqArgs &a, const uint32_t *qa, const uint32_t *qb, uint64_t n, uint32_t *scratch,
                             void *tmp, size_t tmp_bytes, uint32_t *ra, uint32_t *rb, uint32_t *perm, uint32_t *counts,

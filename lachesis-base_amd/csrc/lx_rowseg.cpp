@@ -35,9 +35,10 @@ SegArgs rs_seg_args(lx_index *h) {
     a.stride = h->pstride;
     a.B = h->B;
     a.bs = 0;
-    a.n = h->rs_seg_lo[h->rs_count];
-    a.G = h->rs_count;
-    for (uint32_t k = 0; k <= h->rs_count; k++) a.seg_lo[k] = h->rs_seg_lo[k];
+    const uint32_t GS = h->rs_count * h->rs_sub;   // segments: rs_sub per rank
+    a.n = h->rs_seg_lo[GS];
+    a.G = GS;
+    for (uint32_t k = 0; k <= GS; k++) a.seg_lo[k] = h->rs_seg_lo[k];
     a.ev_branch = h->ev_branch;
     a.ev_seq = h->ev_seq;
     a.branch_first = h->branch_first;
@@ -50,9 +51,10 @@ SegArgs rs_seg_args(lx_index *h) {
     a.pflag = h->seg_mf;
     a.plist = h->seg_plist;
     a.elist = h->seg_elist;
-    a.ecount = a.pcount + h->rs_count;
-    a.own_seg = h->rs_rank;
+    a.ecount = a.pcount + GS;
+    a.own_seg = h->rs_rank * h->rs_sub;
     a.own_lo = h->rs_lo;
+    a.per_rank = h->rs_sub;
     return a;
 }
 
@@ -81,7 +83,7 @@ RsqArgs rsq_args(const lx_index *h) {
     a.lo = h->rs_lo;
     a.hi = h->rs_hi;
     a.B = h->B;
-    for (uint32_t q = 0; q <= h->rs_count; q++) a.seg_lo[q] = h->rs_seg_lo[q];
+    for (uint32_t q = 0; q <= h->rs_count; q++) a.seg_lo[q] = h->rs_seg_lo[q * h->rs_sub];   // rank bounds
     return a;
 }
 
@@ -108,13 +110,15 @@ int rs_check(lx_index *h, int state) {
     return h->hip(set_dev(h->device), "set device");
 }
 
-// the own partial events' rows from the rows they reference (every one final
-// and present by now)
+// the own partial events' rows from the rows they reference (every other
+// rank's one final and present by now), own sub-segment by own sub-segment:
+// a later one may reference rows of an earlier one, final after its fix-up
 int rs_fix_partials(lx_index *h) {
     if (h->rs_npartial) {
         SegArgs a = rs_seg_args(h);
         HIPCHK(h, hipEventRecord(h->seg_ev[2], h->stream));
-        HIPCHK(h, lx::launch_seg_partial(a, h->rs_rank, h->rs_npartial, h->stream));
+        for (uint32_t t = 0; t < h->rs_sub; t++)
+            HIPCHK(h, lx::launch_seg_partial(a, a.own_seg + t, h->rs_npart[t], h->stream));
         HIPCHK(h, hipEventRecord(h->seg_ev[3], h->stream));
         HIPCHK(h, hipStreamSynchronize(h->stream));
         HIPCHK(h, hipEventElapsedTime(&h->seg_stats.partial_ms, h->seg_ev[2], h->seg_ev[3]));
@@ -145,12 +149,28 @@ void rs_free(lx_index *h) {
 // need from the other ranks
 int rs_begin(lx_index *h, IndexArgs ia, const uint32_t *poff, hipStream_t s) {
     const uint32_t G = h->rs_count, k = h->rs_rank, n = ia.n;
-    for (uint32_t q = 0; q < G; q++) h->rs_seg_lo[q] = (uint32_t)((uint64_t)n * q / G / 64 * 64);
-    h->rs_seg_lo[G] = n;
-    h->rs_lo = h->rs_seg_lo[k];
-    h->rs_hi = h->rs_seg_lo[k + 1];
+    // sub-segments per rank: the segment count auto_segments would pick for a
+    // rank's share of the epoch (the same on every rank: it depends only on
+    // the epoch and the device), or option seg_sub; each >= 64 events
+    uint32_t S = h->rs_sub_opt, cpw = ia.cpw_hint;
+    if (!S) {
+        uint32_t c = 0;
+        S = seg_pick(h, (uint64_t)n / G, &c);
+        if (S >= 2) cpw = c;
+        else S = 1;
+    }
+    S = std::max<uint32_t>(1, std::min<uint32_t>({S, kMaxSegments / G, kSegLaunchMax}));
+    while (S > 1 && (uint64_t)n / G < 128ull * S) S--;
+    h->rs_sub = S;
+    for (uint32_t q = 0; q < G; q++) {
+        const uint64_t r0 = (uint64_t)n * q / G / 64 * 64, r1 = q + 1 == G ? n : (uint64_t)n * (q + 1) / G / 64 * 64;
+        for (uint32_t t = 0; t < S; t++) h->rs_seg_lo[q * S + t] = (uint32_t)(r0 + (r1 - r0) * t / S / 64 * 64);
+    }
+    h->rs_seg_lo[G * S] = n;
+    h->rs_lo = h->rs_seg_lo[k * S];
+    h->rs_hi = h->rs_seg_lo[(k + 1) * S];
     int rc;
-    if ((rc = grow_scratch(h, &h->seg_jt, &h->seg_jt_cap, (uint64_t)(G + 1) * h->B)) ||
+    if ((rc = grow_scratch(h, &h->seg_jt, &h->seg_jt_cap, (uint64_t)(G * S + 1) * h->B)) ||
         (rc = grow_scratch(h, &h->seg_cnt, &h->seg_cnt_cap, (uint64_t)h->B + 2 * kMaxSegments)) ||
         (rc = grow_scratch(h, &h->seg_mf, &h->seg_mf_cap, (uint64_t)n)) ||
         (rc = grow_scratch(h, &h->seg_plist, &h->seg_plist_cap, (uint64_t)n)) ||
@@ -176,21 +196,37 @@ int rs_begin(lx_index *h, IndexArgs ia, const uint32_t *poff, hipStream_t s) {
     ia.seg = 1;
     ia.ev_branch = h->ev_branch;
     ia.ev_seq = h->ev_seq;
-    ia.batch_start = h->rs_lo;
-    ia.n = h->rs_hi - h->rs_lo;
-    ia.rec = ia.rec + h->rs_lo;
-    ia.poff_in = poff + h->rs_lo;
-    ia.seg_j = a.jt + (uint64_t)k * a.B;
-    ia.seg_flag = a.pflag + h->rs_lo;
-    ia.seg_list = a.plist + h->rs_lo;
-    ia.seg_count = a.pcount + k;
+    const IndexArgs ib = ia;   // the batch's walk arguments (records from event 0)
+    const uint32_t k0 = a.own_seg;
+    // the own sub-segments: one k_index_segs launch side by side when they fit
+    // the CUs (as a single-GPU batch), else one walk each
+    if (S > 1) ia.cpw_hint = cpw == 8 && (!ia.pack16 || ia.mask) ? 4 : cpw;
+    const bool conc = S > 1 && S * seg_walk_grid(h, ia.cpw_hint) <= h->n_cus;
     HIPCHK(h, hipEventRecord(h->seg_ev[0], s));
-    HIPCHK(h, lx::launch_index(ia, s));
+    for (uint32_t t = 0; t < S; t++) {
+        if (conc && t) break;
+        IndexArgs sk = ia;
+        const uint32_t b0 = h->rs_seg_lo[k0 + t];
+        sk.batch_start = conc ? h->rs_lo : b0;
+        sk.n = conc ? h->rs_hi - h->rs_lo : h->rs_seg_lo[k0 + t + 1] - b0;
+        sk.rec = ib.rec + sk.batch_start;
+        sk.poff_in = poff + sk.batch_start;
+        sk.seg_j = a.jt + (uint64_t)(k0 + t) * a.B;
+        sk.seg_flag = a.pflag + sk.batch_start;
+        sk.seg_list = a.plist + sk.batch_start;
+        sk.seg_count = a.pcount + k0 + t;
+        if (conc) {
+            sk.seg_g = S;
+            sk.seg_B = a.B;
+            for (uint32_t u = 0; u <= S; u++) sk.seg_lo[u] = h->rs_seg_lo[k0 + u];
+        }
+        HIPCHK(h, lx::launch_index(sk, s));
+    }
     HIPCHK(h, hipEventRecord(h->seg_ev[1], s));
-    uint32_t pc = 0;
-    HIPCHK(h, hipMemcpyAsync(&pc, a.pcount + k, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(h, hipMemcpyAsync(h->rs_npart, a.pcount + k0, 4ull * S, hipMemcpyDeviceToHost, s));
     HIPCHK(h, hipStreamSynchronize(s));
-    h->rs_npartial = pc;
+    h->rs_npartial = 0;
+    for (uint32_t t = 0; t < S; t++) h->rs_npartial += h->rs_npart[t];
     // the rows to ask for: at most every referenced branch of every partial
     // event plus one per branch, and never more than the events before lo
     const uint64_t want = std::min<uint64_t>((uint64_t)h->rs_npartial * h->B + h->B, (uint64_t)h->rs_lo + 1);
@@ -200,9 +236,7 @@ int rs_begin(lx_index *h, IndexArgs ia, const uint32_t *poff, hipStream_t s) {
     HIPCHK(h, hipMemsetAsync(h->rs_need, 0, (uint64_t)n * 4, s));
     HIPCHK(h, hipMemsetAsync(h->rs_ctr, 0, (2 + 2 * kMaxSegments) * 4, s));
     RsArgs r = rs_args(h);
-    SegArgs ap = a;
-    ap.plist = a.plist + h->rs_lo;
-    HIPCHK(h, lx::launch_rs_refs(ap, r, h->rs_npartial, s));
+    HIPCHK(h, lx::launch_rs_refs(a, r, h->rs_npart, s));
     HIPCHK(h, hipMemcpyAsync(h->rs_ctr + 1, h->rs_ctr, 4, hipMemcpyDeviceToDevice, s));
     uint32_t nreq = 0;
     HIPCHK(h, hipMemcpyAsync(&nreq, h->rs_ctr, 4, hipMemcpyDeviceToHost, s));
@@ -211,8 +245,9 @@ int rs_begin(lx_index *h, IndexArgs ia, const uint32_t *poff, hipStream_t s) {
     lx_seg_stats &st = h->seg_stats;
     st = lx_seg_stats{};
     st.segments = G;
-    for (uint32_t q = 0; q <= G; q++) st.first_event[q] = h->rs_seg_lo[q];
+    for (uint32_t q = 0; q <= G; q++) st.first_event[q] = h->rs_seg_lo[q * S];
     st.partial[k] = h->rs_npartial;
+    st.one_launch = conc ? 1u : 0u;
     HIPCHK(h, hipEventElapsedTime(&st.walk_ms[k], h->seg_ev[0], h->seg_ev[1]));
     h->rs_state = 1;
     if (!nreq) return rs_fix_partials(h);
@@ -224,7 +259,7 @@ extern "C" {
 int lx_rowseg_bounds(const lx_index *h, uint32_t *lo) {
     if (!h || !lo) return LX_ERR_ARG;
     if (!h->rowseg() || !h->rs_state) return LX_ERR_STATE;
-    for (uint32_t q = 0; q <= h->rs_count; q++) lo[q] = h->rs_seg_lo[q];
+    for (uint32_t q = 0; q <= h->rs_count; q++) lo[q] = h->rs_seg_lo[q * h->rs_sub];
     return 0;
 }
 
@@ -291,11 +326,14 @@ int lx_rowseg_la(lx_index *h, uint64_t *counts) {
     if (!h->rs_out_per) h->rs_out_per = 1u << 18;
     std::vector<uint32_t> c(G);
     // the own events whose LowestAfter range reaches rows before the segment
+    // (per own sub-segment: rows up to its J, in earlier own sub-segments or
+    // other ranks' segments)
     SegArgs a = rs_seg_args(h);
-    uint32_t ne = 0;
+    const uint32_t S = h->rs_sub, k0 = a.own_seg;
+    uint32_t ne[kMaxSegments] = {};
     HIPCHK(h, hipEventRecord(h->seg_ev[4], h->stream));
-    HIPCHK(h, lx::launch_seg_edges(a, h->rs_rank, h->rs_npartial, h->stream));
-    HIPCHK(h, hipMemcpyAsync(&ne, a.ecount + h->rs_rank, 4, hipMemcpyDeviceToHost, h->stream));
+    for (uint32_t t = 0; t < S; t++) HIPCHK(h, lx::launch_seg_edges(a, k0 + t, h->rs_npart[t], h->stream));
+    HIPCHK(h, hipMemcpyAsync(ne, a.ecount + k0, 4ull * S, hipMemcpyDeviceToHost, h->stream));
     HIPCHK(h, hipStreamSynchronize(h->stream));
     for (int attempt = 0; attempt < 2; attempt++) {
         if ((rc = grow_scratch(h, &h->rs_out, &h->rs_out_cap, 3ull * G * h->rs_out_per))) return rc;
@@ -303,7 +341,7 @@ int lx_rowseg_la(lx_index *h, uint64_t *counts) {
         a.out_count = h->rs_ctr + 2 + kMaxSegments;
         a.out_cap = h->rs_out_per;
         HIPCHK(h, hipMemsetAsync(a.out_count, 0, G * 4, h->stream));
-        HIPCHK(h, lx::launch_seg_la_edge(a, h->rs_rank, ne, h->stream));
+        for (uint32_t t = 0; t < S; t++) HIPCHK(h, lx::launch_seg_la_edge(a, k0 + t, ne[t], h->stream));
         HIPCHK(h, hipEventRecord(h->seg_ev[5], h->stream));
         HIPCHK(h, hipMemcpyAsync(c.data(), a.out_count, G * 4, hipMemcpyDeviceToHost, h->stream));
         HIPCHK(h, hipStreamSynchronize(h->stream));

@@ -41,6 +41,11 @@ __device__ __forceinline__ uint32_t seg_of(const SegArgs &a, uint32_t e) {
     return lo;
 }
 
+// the row-segment rank owning row e
+__device__ __forceinline__ uint32_t rank_of(const SegArgs &a, uint32_t e) {
+    return seg_of(a, e) / (a.per_rank ? a.per_rank : 1u);
+}
+
 __device__ __forceinline__ uint32_t row_of(const SegArgs &a, uint32_t c, uint32_t s) {
     return a.brow[(uint64_t)c * a.s_cap + (s - a.branch_first[c])];
 }
@@ -136,7 +141,7 @@ __global__ void __launch_bounds__(256) k_seg_la_edge(SegArgs a, uint32_t k) {
                 a.la[(uint64_t)x * a.stride + j] = sq;
             } else {
                 // another rank's row: to the owner of its segment
-                const uint32_t d = seg_of(a, x);
+                const uint32_t d = rank_of(a, x);
                 const uint32_t p = atomicAdd(a.out_count + d, 1u);
                 if (p < a.out_cap) {
                     uint32_t *o = a.out + 3ull * (d * a.out_cap + p);
@@ -154,14 +159,19 @@ __device__ __forceinline__ void rs_want(const RsArgs &r, uint32_t x) {
     if (atomicOr(r.need + x, 1u) == 0u) r.req[atomicAdd(r.req_count, 1u)] = x;
 }
 
-// the rows the own partial events reference (one workgroup per partial event)
-__global__ void __launch_bounds__(256) k_rs_refs(SegArgs a, RsArgs r) {
-    const uint32_t e = a.plist[blockIdx.x];
-    const uint32_t *J = a.jt + (uint64_t)a.own_seg * a.B;
+// the rows the partial events of own segment k reference (one workgroup per
+// partial event); rows of the rank's own earlier sub-segments are final after
+// their own fix-up and are not asked for
+__global__ void __launch_bounds__(256) k_rs_refs(SegArgs a, RsArgs r, uint32_t k) {
+    const uint32_t e = a.plist[a.seg_lo[k] - a.bs + blockIdx.x];
+    const uint32_t *J = a.jt + (uint64_t)k * a.B;
     const uint32_t *row = a.hb + (uint64_t)e * a.stride;
     for (uint32_t c = threadIdx.x; c < a.B; c += blockDim.x) {
         const uint32_t m = min(row[c], J[c]);
-        if (m) rs_want(r, row_of(a, c, m));
+        if (m) {
+            const uint32_t x = row_of(a, c, m);
+            if (x < r.lo) rs_want(r, x);
+        }
     }
 }
 
@@ -169,7 +179,8 @@ __global__ void __launch_bounds__(256) k_rs_refs(SegArgs a, RsArgs r) {
 __global__ void k_rs_frontier(SegArgs a, RsArgs r) {
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= a.B) return;
-    const uint32_t j0 = a.jt[(uint64_t)a.own_seg * a.B + c], j1 = a.jt[(uint64_t)(a.own_seg + 1) * a.B + c];
+    const uint32_t per = a.per_rank ? a.per_rank : 1u;
+    const uint32_t j0 = a.jt[(uint64_t)a.own_seg * a.B + c], j1 = a.jt[(uint64_t)(a.own_seg + per) * a.B + c];
     if (j1 > j0 && j0) rs_want(r, row_of(a, c, j0));
 }
 
@@ -178,26 +189,27 @@ __global__ void k_rs_frontier(SegArgs a, RsArgs r) {
 __global__ void __launch_bounds__(1024) k_rs_bucket(SegArgs a, RsArgs r, uint32_t n_req, uint32_t *out,
                                                     uint32_t *counts) {
     __shared__ uint32_t cnt[kMaxSegments], off[kMaxSegments];
-    if (threadIdx.x < a.G) cnt[threadIdx.x] = 0;
+    const uint32_t R = a.G / (a.per_rank ? a.per_rank : 1u);   // ranks
+    if (threadIdx.x < R) cnt[threadIdx.x] = 0;
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < n_req; i += blockDim.x) {
         const uint32_t x = r.req[i];
-        if (r.need[x]) atomicAdd(&cnt[seg_of(a, x)], 1u);
+        if (r.need[x]) atomicAdd(&cnt[rank_of(a, x)], 1u);
     }
     __syncthreads();
     if (threadIdx.x == 0) {
         uint32_t o = 0;
-        for (uint32_t d = 0; d < a.G; d++) {
+        for (uint32_t d = 0; d < R; d++) {
             off[d] = o;
             o += cnt[d];
         }
     }
     __syncthreads();
-    if (threadIdx.x < a.G) counts[threadIdx.x] = cnt[threadIdx.x];
+    if (threadIdx.x < R) counts[threadIdx.x] = cnt[threadIdx.x];
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < n_req; i += blockDim.x) {
         const uint32_t x = r.req[i];
-        if (r.need[x]) out[atomicAdd(&off[seg_of(a, x)], 1u)] = x;
+        if (r.need[x]) out[atomicAdd(&off[rank_of(a, x)], 1u)] = x;
     }
 }
 
@@ -253,8 +265,10 @@ hipError_t launch_seg_partial(const SegArgs &a, uint32_t k, uint32_t count, hipS
     return hipGetLastError();
 }
 
-hipError_t launch_rs_refs(const SegArgs &a, const RsArgs &r, uint32_t n_partial, hipStream_t s) {
-    if (n_partial) hipLaunchKernelGGL(k_rs_refs, dim3(n_partial), dim3(256), 0, s, a, r);
+hipError_t launch_rs_refs(const SegArgs &a, const RsArgs &r, const uint32_t *n_partial, hipStream_t s) {
+    const uint32_t per = a.per_rank ? a.per_rank : 1u;
+    for (uint32_t k = 0; k < per; k++)
+        if (n_partial[k]) hipLaunchKernelGGL(k_rs_refs, dim3(n_partial[k]), dim3(256), 0, s, a, r, a.own_seg + k);
     hipLaunchKernelGGL(k_rs_frontier, dim3(nb(a.B, 256)), dim3(256), 0, s, a, r);
     return hipGetLastError();
 }

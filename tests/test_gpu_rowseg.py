@@ -40,7 +40,7 @@ def _planes(ix, lo, hi):
     return out
 
 
-def _worker(rank, world, port, q, shape):
+def _worker(rank, world, port, q, shape, sub=0):
     import sys
     sys.path[:0] = [ROOT, os.path.join(ROOT, "lachesis-base_amd")]
     import torch
@@ -55,7 +55,7 @@ def _worker(rank, world, port, q, shape):
         d = lx.tools.gen_dag(V, epv, P, ch, fk, seed)
         rng = np.random.default_rng(seed)
         weights = [int(x) for x in rng.integers(1, 40, V)]
-        ix = lx.Index(device=0, options={"seg_count": world, "seg_rank": rank, "small_max": 0})
+        ix = lx.Index(device=0, options={"seg_count": world, "seg_rank": rank, "small_max": 0, "seg_sub": sub})
         ix.reset(weights)
         ix.add_batch(d.creator, d.seq, d.poff, d.par)
         dev = torch.device("cuda", 0)
@@ -106,12 +106,13 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("world,shape", [(2, "forks"), (3, "forks"), (4, "parents"), (4, "short"), (3, "wide")])
-def test_row_segments_over_torch_distributed(world, shape):
+@pytest.mark.parametrize("world,shape,sub", [(2, "forks", 0), (3, "forks", 0), (4, "parents", 0), (4, "short", 0),
+                                             (3, "wide", 0), (2, "forks", 3)])
+def test_row_segments_over_torch_distributed(world, shape, sub):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, shape)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, shape, sub)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=150) for _ in range(world)]

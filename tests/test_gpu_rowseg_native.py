@@ -61,16 +61,20 @@ def _planes(ix, lo, hi):
     return out
 
 
-@pytest.mark.parametrize("world,shape", [(2, "forks"), (3, "forks"), (4, "parents"), (4, "short"), (3, "wide"),
-                                         (8, "wide")])
-def test_native_row_segment_exchange(lx, fake, world, shape):
+@pytest.mark.parametrize("world,shape,sub", [(2, "forks", 0), (3, "forks", 0), (4, "parents", 0), (4, "short", 0),
+                                             (3, "wide", 0), (8, "wide", 0),
+                                             (2, "forks", 2), (3, "wide", 3), (4, "parents", 2), (2, "wide", 5)])
+def test_native_row_segment_exchange(lx, fake, world, shape, sub):
+    """sub > 1: every rank walks its own segment as `sub` side-by-side
+    sub-segments (option seg_sub; auto picks it for large epochs), fixed up in
+    order after the rows of the other ranks arrive."""
     V, epv, P, ch, fk, seed = SHAPES[shape]
     d = lx.tools.gen_dag(V, epv, P, ch, fk, seed)
     rng = np.random.default_rng(seed)
     weights = [int(x) for x in rng.integers(1, 40, V)]
     ranks = []
     for r in range(world):
-        ix = lx.Index(device=0, options={"seg_count": world, "seg_rank": r, "small_max": 0})
+        ix = lx.Index(device=0, options={"seg_count": world, "seg_rank": r, "small_max": 0, "seg_sub": sub})
         ix.reset(weights)
         ix.add_batch(d.creator, d.seq, d.poff, d.par)
         ranks.append(ix)
@@ -103,8 +107,9 @@ def test_native_row_segment_exchange(lx, fake, world, shape):
     ref.close()
 
 
-@pytest.mark.parametrize("world,shape", [(2, "forks"), (3, "forks"), (4, "parents"), (8, "wide")])
-def test_native_row_segment_forkless_cause_any_pair(lx, fake, world, shape):
+@pytest.mark.parametrize("world,shape,sub", [(2, "forks", 0), (3, "forks", 0), (4, "parents", 0), (8, "wide", 0),
+                                             (3, "wide", 2)])
+def test_native_row_segment_forkless_cause_any_pair(lx, fake, world, shape, sub):
     """ForklessCause of ANY pair of the epoch across row-segment ranks
     (lx_rowseg_forkless_cause's driver, csrc/lx_rowseg_exchange.h
     rowseg_fc_run, over the in-process transport): every rank asks queries
@@ -119,7 +124,7 @@ def test_native_row_segment_forkless_cause_any_pair(lx, fake, world, shape):
     weights = [int(x) for x in rng.integers(1, 40, V)]
     ranks = []
     for r in range(world):
-        ix = lx.Index(device=0, options={"seg_count": world, "seg_rank": r, "small_max": 0})
+        ix = lx.Index(device=0, options={"seg_count": world, "seg_rank": r, "small_max": 0, "seg_sub": sub})
         ix.reset(weights)
         ix.add_batch(d.creator, d.seq, d.poff, d.par)
         ranks.append(ix)
