@@ -139,6 +139,12 @@ struct Net {
             }
             ro += rb[p];
         }
+        // a device-to-device hipMemcpy may return before the copy is done, and
+        // the handles' streams do not wait for the null stream
+        if (!rc && hipDeviceSynchronize() != hipSuccess) {
+            w.fail("hipDeviceSynchronize");
+            rc = LX_ERR_HIP;
+        }
         if (!w.barrier()) return LX_ERR_STATE;   // every copy done before a sender reuses its buffer
         return rc;
     }
