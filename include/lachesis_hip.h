@@ -90,6 +90,8 @@ const char *lx_last_error(const lx_index *h);
  *   "seg_auto"   0: never split a batch on its own (default 1: a batch whose walk
  *                leaves CUs idle -- few columns -- is walked as G segments side by
  *                side in one launch, G = CUs / walk workgroups, >= 32k events each)
+ *   "get_server" 0: every single-row getter launches its kernel (default 1: the resident
+ *                row server answers them while the stream is idle, lx_get_server_stats)
  * The library reads no environment variables. */
 int lx_set_option(lx_index *h, const char *name, int64_t value);
 
@@ -223,6 +225,14 @@ uint32_t lx_quorum(const lx_index *h);                 /* pos/validators.go:187-
 int lx_get_highest_before(lx_index *h, uint32_t ev, uint8_t *out, uint32_t cap, uint32_t *len);
 int lx_get_lowest_after(lx_index *h, uint32_t ev, uint8_t *out, uint32_t cap, uint32_t *len);
 int lx_get_merged_highest_before(lx_index *h, uint32_t ev, uint8_t *out, uint32_t cap, uint32_t *len);
+/* The single-row getters above are answered by a resident one-wave kernel
+ * (the row server) when the handle's stream is idle: no launch per call, the
+ * row and a completion tag land in pinned memory.  It leaves after 250 us
+ * without a request (and after 0.5 s in all), so a device-wide synchronization
+ * right after a getter may wait that long; option get_server = 0 turns it off
+ * (every call launches).  out[0] rows it served, out[1] its launches, out[2]
+ * single-row calls that launched instead (stream busy or option off). */
+int lx_get_server_stats(const lx_index *h, uint64_t out[3]);
 /* The same for n events in one call (applyAtropos, abft/lachesis.go:57, and the
  * emitter's candidate loops call GetMergedHighestBefore per event): row i is
  * written at out + off[i], off has n+1 entries (byte offsets, always filled);

@@ -1676,6 +1676,9 @@ int lx_create(const lx_config *cfg, lx_index **out) {
 void lx_destroy(lx_index *h) {
     if (!h) return;
     (void)hipSetDevice(h->device);
+    srv_stop(h);
+    if (h->srv_stream) (void)hipStreamDestroy(h->srv_stream);
+    if (h->srv_host) (void)hipHostFree(h->srv_host);
     (void)hipStreamSynchronize(h->stream);
     fcc_destroy(h);
     free_all(h);
@@ -1737,6 +1740,10 @@ int lx_set_option(lx_index *h, const char *name, int64_t value) {
         // every rank of a job must use the same value
         if (value < 0 || value > (int64_t)kSegLaunchMax) return h->fail(LX_ERR_ARG, "seg_sub must be 0..%u", kSegLaunchMax);
         h->rs_sub_opt = (uint32_t)value;
+    } else if (k == "get_server") {
+        // single-row getters through the resident row server (default 1)
+        h->srv_opt = value != 0;
+        if (!h->srv_opt) srv_stop(h);
     } else if (k == "fc_cache") {
         if (value < 0 || value > 16384) return h->fail(LX_ERR_ARG, "fc_cache must be 0..16384");
         fcc_destroy(h);
@@ -2184,6 +2191,94 @@ namespace {
 // rows + i * slot; len[i] its byte length.
 constexpr uint64_t kGetChunk = 64ull << 20;
 
+// single-row tags: 30 bits (the server's request word), never 0 or kGetSrvStop
+uint32_t next_get_tag(lx_index *h) {
+    h->get_tag = h->get_tag + 1 >= kGetSrvStop ? 1u : h->get_tag + 1;
+    return h->get_tag;
+}
+
+// the server's arguments for a single-row GetArgs (memcmp-comparable)
+GetSrvArgs srv_args_of(const lx_index *h, const GetArgs &a) {
+    GetSrvArgs s;
+    memset(&s, 0, sizeof s);
+    s.g = a;
+    s.g.plane = nullptr;
+    s.g.ev = nullptr;
+    s.g.ev0 = 0;
+    s.g.mode = 0;
+    s.g.tag = 0;
+    s.hb = h->hb;
+    s.la = h->la;
+    s.req = h->srv_dev;
+    s.exited = reinterpret_cast<uint32_t *>(h->srv_dev + 1);
+    return s;
+}
+
+// (re)launch the server with the arguments of `a`; it ignores request tags up
+// to seen0
+int srv_launch(lx_index *h, const GetArgs &a, uint32_t seen0) {
+    GetSrvArgs s = srv_args_of(h, a);
+    h->srv_args = s;
+    s.gen = ++h->srv_gen;
+    s.seen0 = seen0;
+    s.idle_ticks = 250 * h->srv_ticks_us;          // leave after 250 us without a request
+    s.budget_ticks = 500000 * h->srv_ticks_us;     // and after 0.5 s in all
+    HIPCHK(h, lx::launch_get_server(s, h->srv_stream));
+    h->srv_live = true;
+    h->srv_launches++;
+    return 0;
+}
+
+}  // namespace
+
+// stop a live server (the stop tag, then its stream): it reads nothing but
+// the request word between requests
+void srv_stop(lx_index *h) {
+    if (!h || !h->srv_live) return;
+    reinterpret_cast<volatile uint64_t *>(h->srv_host)[0] = kGetSrvStop;
+    (void)hipStreamSynchronize(h->srv_stream);
+    h->srv_live = false;
+}
+
+namespace {
+
+// post one row request to the server when the handle's stream is idle (every
+// row the request reads is final); *posted = false: the caller launches
+int srv_post(lx_index *h, const GetArgs &a, bool *posted) {
+    *posted = false;
+    if (!h->srv_opt || a.n != 1 || a.ev) return 0;
+    if (hipStreamQuery(h->stream) != hipSuccess) return 0;
+    if (!h->srv_host) {
+        int lo = 0, hi = 0, khz = 0;
+        HIPCHK(h, hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, h->device));
+        if (khz < 1000) {   // no usable wall clock: never resident
+            h->srv_opt = false;
+            return 0;
+        }
+        h->srv_ticks_us = (uint64_t)khz / 1000;
+        HIPCHK(h, hipDeviceGetStreamPriorityRange(&lo, &hi));
+        HIPCHK(h, hipStreamCreateWithPriority(&h->srv_stream, hipStreamNonBlocking, hi));
+        void *p = nullptr, *d = nullptr;
+        HIPCHK(h, hipHostMalloc(&p, 64, hipHostMallocMapped));
+        HIPCHK(h, hipHostGetDevicePointer(&d, p, 0));
+        memset(p, 0, 64);
+        h->srv_host = static_cast<uint64_t *>(p);
+        h->srv_dev = static_cast<uint64_t *>(d);
+    }
+    volatile uint64_t *req = h->srv_host;
+    const GetSrvArgs want = srv_args_of(h, a);
+    if (h->srv_live && (uint32_t)reinterpret_cast<volatile uint64_t *>(h->srv_host)[1] == h->srv_gen) {
+        (void)hipStreamSynchronize(h->srv_stream);   // it left (idle or deadline): its launch has ended
+        h->srv_live = false;
+    }
+    if (h->srv_live && memcmp(&want, &h->srv_args, sizeof want) != 0) srv_stop(h);
+    int rc;
+    if (!h->srv_live && (rc = srv_launch(h, a, (uint32_t)(req[0] & kGetSrvStop)))) return rc;
+    req[0] = (uint64_t)a.ev0 << 32 | (uint64_t)(a.mode & 3u) << 30 | a.tag;
+    *posted = true;
+    return 0;
+}
+
 int get_rows(lx_index *h, uint32_t mode, uint32_t n, const uint32_t *ev, uint8_t **rows, uint64_t *slot,
              const uint32_t **len) {
     const uint64_t sl = ((uint64_t)8 * std::max(h->B, h->V) + 15) / 16 * 16;
@@ -2213,21 +2308,38 @@ int get_rows(lx_index *h, uint32_t mode, uint32_t n, const uint32_t *ev, uint8_t
     a.out = dp + head;
     a.slot = sl;
     if (n == 1) {
-        // one row (the reference's per-call getters): the kernel publishes a tag
-        // after the row, the host spins on it (a stream synchronization costs
-        // ~5 us more, scripts/probes/sync_latency.hip); a launch that never
-        // lands is caught by the timeout's synchronization
-        a.tag = ++h->get_tag ? h->get_tag : ++h->get_tag;
+        // one row (the reference's per-call getters): the resident server
+        // answers it when the handle's stream is idle (no launch); otherwise a
+        // launch on the stream.  Either publishes a tag after the row and the
+        // host spins on it (a stream synchronization costs ~5 us more,
+        // scripts/probes/sync_latency.hip); a launch that never lands is caught
+        // by the timeout's synchronization
+        a.tag = next_get_tag(h);
         a.done = reinterpret_cast<uint32_t *>(dp + 8ull * n);
-        HIPCHK(h, lx::launch_get_rows(a, h->stream));
         const volatile uint32_t *done = reinterpret_cast<const volatile uint32_t *>(hp + 8ull * n);
+        bool posted = false;
+        if ((rc = srv_post(h, a, &posted))) return rc;
+        if (!posted) {
+            h->srv_fallbacks++;
+            HIPCHK(h, lx::launch_get_rows(a, h->stream));
+        }
         const auto t0 = std::chrono::steady_clock::now();
+        bool relaunched = false;
         for (uint32_t k = 0; *done != a.tag; k++) {
+            if ((k & 63) != 63) continue;
+            if (posted && !relaunched && (uint32_t)h->srv_host[1] == h->srv_gen && *done != a.tag) {
+                // the server left (idle or its deadline) before it saw the request
+                h->srv_live = false;
+                if ((rc = srv_launch(h, a, a.tag == 1 ? kGetSrvStop - 1 : a.tag - 1))) return rc;
+                relaunched = true;
+            }
             if ((k & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(200)) {
+                if (posted) srv_stop(h);
                 HIPCHK(h, hipStreamSynchronize(h->stream));
                 if (*done != a.tag) return h->fail(LX_ERR_STATE, "getter: the row kernel did not complete");
             }
         }
+        if (posted) h->srv_served++;
         std::atomic_thread_fence(std::memory_order_acquire);
     } else {
         HIPCHK(h, lx::launch_get_rows(a, h->stream));
@@ -2293,6 +2405,14 @@ int get_batch(lx_index *h, uint32_t mode, uint32_t n, const uint32_t *ev, uint64
 }  // namespace
 
 extern "C" {
+
+int lx_get_server_stats(const lx_index *h, uint64_t out[3]) {
+    if (!h || !out) return LX_ERR_ARG;
+    out[0] = h->srv_served;
+    out[1] = h->srv_launches;
+    out[2] = h->srv_fallbacks;
+    return 0;
+}
 
 int lx_get_highest_before(lx_index *h, uint32_t ev, uint8_t *out, uint32_t cap, uint32_t *len) {
     return get_one(h, 0, ev, out, cap, len);

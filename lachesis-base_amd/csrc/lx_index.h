@@ -233,6 +233,15 @@ struct lx_index {
     uint8_t *qp = nullptr, *qp_dev = nullptr;
     uint64_t qp_cap = 0;
     uint32_t get_tag = 0;                  // completion tag of the last single-row getter
+    // the resident single-row server (k_get_server, option get_server)
+    bool srv_opt = true;
+    hipStream_t srv_stream = nullptr;      // its own (high-priority) stream
+    uint64_t *srv_host = nullptr, *srv_dev = nullptr;   // pinned: [0] request word, [1] exited gen
+    bool srv_live = false;                 // launched and not known to have left
+    uint32_t srv_gen = 0;
+    GetSrvArgs srv_args{};                 // the live server's arguments (ticks, seen0, gen aside)
+    uint64_t srv_ticks_us = 0;             // wall clock ticks per microsecond
+    uint64_t srv_served = 0, srv_launches = 0, srv_fallbacks = 0;
     uint32_t *q_sink = nullptr;            // status word the pinned FC path lets the kernel flag into
 
     // timing (HIP events on `stream`)
@@ -321,6 +330,7 @@ int rs_begin(lx_index *h, IndexArgs ia, const uint32_t *poff, hipStream_t s);   
 uint32_t seg_pick(const lx_index *h, uint64_t n, uint32_t *cpw);    // lx_capi.cpp (auto_segments)
 uint32_t seg_walk_grid(const lx_index *h, uint32_t cpw);
 void rs_free(lx_index *h);
+void srv_stop(lx_index *h);   // lx_capi.cpp: the resident row server leaves
 void fcc_destroy(lx_index *h);
 void fcc_clear(lx_index *h);                    // Reset: a new epoch
 void fcc_forget_from(lx_index *h, uint64_t n);  // DropNotFlushed: events >= n are gone

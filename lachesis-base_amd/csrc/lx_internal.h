@@ -435,6 +435,19 @@ struct GetArgs {
     uint32_t tag;
 };
 
+// the resident single-row server (k_get_server): `g` with plane / ev0 / mode /
+// tag filled per request from the request word *req
+constexpr uint32_t kGetSrvStop = 0x3FFFFFFFu;   // request tag: leave
+struct GetSrvArgs {
+    GetArgs g;
+    const uint32_t *hb, *la;
+    const uint64_t *req;         // pinned: {tag : 30, mode : 2, event : 32}
+    uint32_t *exited;            // pinned: gen on leaving
+    uint32_t gen;
+    uint32_t seen0;              // the last tag answered before this launch
+    uint64_t idle_ticks, budget_ticks;   // wall clock (hipDeviceAttributeWallClockRate)
+};
+
 // ---- emitter QuorumIndexer (lx_emitter.hip, lx_emitter.cpp)
 struct QiArgs {
     const uint32_t *hb;
@@ -661,6 +674,7 @@ hipError_t launch_row_offsets(const RowsArgs &a, uint64_t *len, uint64_t *off, v
                               hipStream_t s);
 hipError_t launch_encode_rows(const RowsArgs &a, const uint64_t *off, uint64_t base, uint32_t *out, hipStream_t s);
 hipError_t launch_get_rows(const GetArgs &a, hipStream_t s);
+hipError_t launch_get_server(const GetSrvArgs &a, hipStream_t s);
 hipError_t launch_load_rows(const LoadArgs &a, hipStream_t s);
 hipError_t launch_load_raw(const LoadRawArgs &a, hipStream_t s);
 hipError_t launch_load_check(const LoadRawArgs &a, uint32_t n, hipStream_t s);

@@ -154,10 +154,8 @@ __device__ __forceinline__ void get_done(const GetArgs &a, uint32_t lane) {
     if (lane == 0) __hip_atomic_store(a.done, a.tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-__global__ __launch_bounds__(256) void k_get_rows(GetArgs a) {
-    const uint32_t i = blockIdx.x * 4 + threadIdx.x / 64, lane = threadIdx.x % 64;
-    if (i >= a.n) return;
-    const uint32_t e = a.ev ? a.ev[i] : a.ev0;
+// row i (event e) by one wave
+__device__ __forceinline__ void get_row(const GetArgs &a, uint32_t i, uint32_t e, uint32_t lane) {
     const uint32_t *row = a.plane + (uint64_t)e * a.stride;
     uint32_t *o = reinterpret_cast<uint32_t *>(a.out + (uint64_t)i * a.slot);
     if (a.mode == 2 && a.forks) {
@@ -252,6 +250,56 @@ __global__ __launch_bounds__(256) void k_get_rows(GetArgs a) {
     }
     if (lane == 0) a.len[i] = ent * (hb ? 8u : 4u);
     get_done(a, lane);
+}
+
+__global__ __launch_bounds__(256) void k_get_rows(GetArgs a) {
+    const uint32_t i = blockIdx.x * 4 + threadIdx.x / 64, lane = threadIdx.x % 64;
+    if (i >= a.n) return;
+    get_row(a, i, a.ev ? a.ev[i] : a.ev0, lane);
+}
+
+// The resident single-row server: one wave polls the request
+// word in pinned memory -- {tag : 30, mode : 2, event : 32}, tag kGetSrvStop =
+// leave -- and answers each new tag like k_get_rows answers one row (row,
+// length, then the tag into *done).  It leaves after idle_ticks without a
+// request or budget_ticks in all (wall clock), publishing `gen` into *exited,
+// so the host can tell a server that left from one still coming.  It reads
+// only the request word until a request arrives, and the host posts one only
+// when the handle's stream is idle and the arguments it was launched with
+// still hold (lx_capi.cpp get_rows).
+__global__ __launch_bounds__(64) void k_get_server(GetSrvArgs s) {
+    const uint32_t lane = threadIdx.x;
+    uint32_t seen = s.seen0;
+    uint64_t last = wall_clock64();
+    const uint64_t deadline = last + s.budget_ticks;
+    for (;;) {
+        uint64_t w;
+        uint32_t q;
+        bool go = false;
+        for (;;) {
+            w = __hip_atomic_load(s.req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            q = __builtin_amdgcn_readfirstlane((uint32_t)w & kGetSrvStop);
+            if (q != seen) {
+                go = q != kGetSrvStop;
+                break;
+            }
+            const uint64_t now = wall_clock64();
+            if (now - last > s.idle_ticks || now > deadline) break;
+            __builtin_amdgcn_s_sleep(1);
+        }
+        if (!go) break;
+        // rows written by kernels on other queues (and XCDs) since the last request
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        GetArgs a = s.g;
+        a.mode = __builtin_amdgcn_readfirstlane((uint32_t)w >> 30);
+        a.plane = a.mode == 1 ? s.la : s.hb;
+        a.tag = q;
+        get_row(a, 0, __builtin_amdgcn_readfirstlane((uint32_t)(w >> 32)), lane);
+        seen = q;
+        last = wall_clock64();
+    }
+    __threadfence_system();
+    if (lane == 0) __hip_atomic_store(s.exited, s.gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // ---------------------------------------------------------------------------- restart
@@ -413,6 +461,11 @@ hipError_t launch_load_verify_la(const LoadVerifyArgs &a, hipStream_t s) {
     const uint64_t t = (uint64_t)a.n * a.B;
     if (!t) return hipSuccess;
     hipLaunchKernelGGL(k_load_verify_la, dim3((uint32_t)((t + 255) / 256)), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_get_server(const GetSrvArgs &a, hipStream_t s) {
+    hipLaunchKernelGGL(k_get_server, dim3(1), dim3(64), 0, s, a);
     return hipGetLastError();
 }
 

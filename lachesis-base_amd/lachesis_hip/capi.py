@@ -47,6 +47,7 @@ SIGNATURES = [
     ("lx_get_lowest_after_batch", ctypes.c_int, [vp, ctypes.c_uint32, u32p, u64p, u8p, ctypes.c_uint64]),
     ("lx_get_merged_highest_before_batch", ctypes.c_int, [vp, ctypes.c_uint32, u32p, u64p, u8p, ctypes.c_uint64]),
     ("lx_get_event_branch_id", ctypes.c_int, [vp, ctypes.c_uint32, u32p]),
+    ("lx_get_server_stats", ctypes.c_int, [vp, u64p]),
     ("lx_get_branches_info", ctypes.c_int, [vp, u32p, u32p, ctypes.c_uint32, u32p]),
     ("lx_shard_of", ctypes.c_int, [vp, u32p, u32p]),
     ("lx_shard_range", ctypes.c_int, [vp, ctypes.c_uint32, u32p, u32p]),
@@ -345,6 +346,13 @@ class Index:
         st = LxFcStats()
         self._chk(self.L.lx_fc_cache_stats(self.h, ctypes.byref(st)))
         return {k: getattr(st, k) for k, _ in LxFcStats._fields_}
+
+    def get_server_stats(self):
+        """Single-row getters: rows the resident row server served, its
+        launches, and calls that launched their own kernel instead."""
+        out = np.zeros(3, dtype=np.uint64)
+        self._chk(self.L.lx_get_server_stats(self.h, _p(out, u64p)))
+        return {"served": int(out[0]), "launches": int(out[1]), "fallbacks": int(out[2])}
 
     def forkless_cause_batch_dev(self, n, a_ptr, b_ptr, out_ptr, stream=None):
         self._chk(self.L.lx_forkless_cause_batch_dev(self.h, n, a_ptr, b_ptr, out_ptr, stream))
