@@ -193,3 +193,74 @@ def test_rowseg_comm_one_rank_and_mismatch(lx):
         lx.ShardComm(seg, bytes(128), 2, 1)   # not a column-shard handle
     seg.close()
     ix.close()
+
+
+def _planes_equal(ix, ref, lo, hi, B, chunk=50_000):
+    for r0 in range(lo, hi, chunk):
+        r1 = min(hi, r0 + chunk)
+        mine, theirs = _planes(ix, r0, r1), _planes(ref, r0, r1)
+        for k in range(2):
+            if not np.array_equal(mine[k][:, :B], theirs[k][:, :B]):
+                bad = np.argwhere(mine[k][:, :B] != theirs[k][:, :B])[:5]
+                return ("hb", "la")[k], r0, bad.tolist()
+    return None
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_native_row_segments_c3_shape_auto_sub(lx, fake, world):
+    """The multi-GPU default at the headline shape (V = 1000, Zipf stakes, 10
+    parents; 1M events here): every rank walks its segment as the side-by-side
+    sub-segments it picks on its own (seg_sub auto, 8-column slices, one
+    launch), and every own HB / LA row equals the single walk's byte for byte;
+    ForklessCause of pairs across the rank boundaries equals the whole index's."""
+    import torch
+    V = 1000
+    d = lx.tools.gen_dag(V, 1000, 10, seed=1)
+    N = len(d)
+    w = [(1 << 20) // (i + 1) for i in range(V)]
+    ranks = []
+    for r in range(world):
+        ix = lx.Index(device=0, event_capacity=N, options={"seg_count": world, "seg_rank": r, "small_max": 0})
+        ix.reset(w)
+        ix.add_batch(d.creator, d.seq, d.poff, d.par)
+        st = ix.segment_stats()
+        assert st["one_launch"], st            # sub-segments side by side in one launch
+        ranks.append(ix)
+    hs = (ctypes.c_void_p * world)(*[ix.h for ix in ranks])
+    stats = (ctypes.c_uint64 * (4 * world))()
+    err = ctypes.create_string_buffer(512)
+    assert fake.lx_fake_rowseg_exchange(hs, world, stats, err, 512) == 0, err.value.decode()
+    ref = lx.Index(device=0, event_capacity=N, options={"small_max": 0, "seg_auto": 0})
+    ref.reset(w)
+    ref.add_batch(d.creator, d.seq, d.poff, d.par)
+    B = ref.num_branches()
+    for r, ix in enumerate(ranks):
+        lo, hi = ix.rowseg_range()
+        assert _planes_equal(ix, ref, lo, hi, B) is None, r
+    # pairs that cross every rank boundary: a just after it, b up to 3000 before
+    rng = np.random.default_rng(5)
+    dev = torch.device("cuda", 0)
+    bounds = [ix.rowseg_range()[0] for ix in ranks[1:]]
+    qs, bufs = [], []
+    for r in range(world):
+        k = 40_000
+        at = np.array(bounds, dtype=np.int64)[rng.integers(0, len(bounds), k)]
+        qa = (at + rng.integers(0, 20_000, k)).astype(np.uint32)
+        qb = np.clip(qa.astype(np.int64) - rng.integers(1, 23_000, k), 0, N - 1).astype(np.uint32)
+        qs.append((qa, qb))
+        t = lambda x: torch.from_numpy(x.view(np.int32)).to(dev)
+        bufs.append((t(qa), t(qb), torch.full((k,), 7, dtype=torch.uint8, device=dev)))
+    torch.cuda.synchronize()
+    ns = (ctypes.c_uint64 * world)(*[len(q[0]) for q in qs])
+    P_ = lambda i: (ctypes.c_void_p * world)(*[b[i].data_ptr() for b in bufs])
+    fst = (ctypes.c_uint64 * (4 * world))()
+    assert fake.lx_fake_rowseg_fc(hs, world, ns, P_(0), P_(1), P_(2), fst, err, 512) == 0, err.value.decode()
+    crossing = 0
+    for r in range(world):
+        qa, qb = qs[r]
+        np.testing.assert_array_equal(bufs[r][2].cpu().numpy(), ref.forkless_cause_batch(qa, qb), err_msg=str(r))
+        crossing += int(sum(((qb < b) & (qa >= b)).sum() for b in bounds))
+    assert crossing > 10_000, crossing
+    for ix in ranks:
+        ix.close()
+    ref.close()
