@@ -2249,19 +2249,22 @@ int srv_post(lx_index *h, const GetArgs &a, bool *posted) {
     if (!h->srv_opt || a.n != 1 || a.ev) return 0;
     if (hipStreamQuery(h->stream) != hipSuccess) return 0;
     if (!h->srv_host) {
+        // what the server needs; without any of it the getters launch as before
         int lo = 0, hi = 0, khz = 0;
-        HIPCHK(h, hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, h->device));
-        if (khz < 1000) {   // no usable wall clock: never resident
+        void *p = nullptr, *d = nullptr;
+        bool ok = hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, h->device) == hipSuccess && khz >= 1000 &&
+                  hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess;
+        if (ok && !h->srv_stream) ok = hipStreamCreateWithPriority(&h->srv_stream, hipStreamNonBlocking, hi) == hipSuccess;
+        if (ok) ok = hipHostMalloc(&p, 64, hipHostMallocMapped) == hipSuccess;
+        if (ok) ok = hipHostGetDevicePointer(&d, p, 0) == hipSuccess;
+        if (!ok) {
+            if (p) (void)hipHostFree(p);
+            (void)hipGetLastError();
             h->srv_opt = false;
             return 0;
         }
-        h->srv_ticks_us = (uint64_t)khz / 1000;
-        HIPCHK(h, hipDeviceGetStreamPriorityRange(&lo, &hi));
-        HIPCHK(h, hipStreamCreateWithPriority(&h->srv_stream, hipStreamNonBlocking, hi));
-        void *p = nullptr, *d = nullptr;
-        HIPCHK(h, hipHostMalloc(&p, 64, hipHostMallocMapped));
-        HIPCHK(h, hipHostGetDevicePointer(&d, p, 0));
         memset(p, 0, 64);
+        h->srv_ticks_us = (uint64_t)khz / 1000;
         h->srv_host = static_cast<uint64_t *>(p);
         h->srv_dev = static_cast<uint64_t *>(d);
     }
