@@ -60,7 +60,7 @@ VARS = [int(x) for x in os.environ.get("WV", "0 3 4 5").split()]
 res = {v: [] for v in VARS}
 for rnd in range(2):
     for v in VARS:
-        other.set_option("walk_var", v)
+        other.set_option(os.environ.get("WOPT", "walk_var"), v)
         step(other)
         res[v] += [step(other), step(other)]
         print(json.dumps({"round": rnd, "walk_var": v, "walk_ms": res[v][-2:]}), flush=True)
