@@ -2330,14 +2330,23 @@ int get_rows(lx_index *h, uint32_t mode, uint32_t n, const uint32_t *ev, uint8_t
         bool relaunched = false;
         for (uint32_t k = 0; *done != a.tag; k++) {
             if ((k & 63) != 63) continue;
-            if (posted && !relaunched && (uint32_t)h->srv_host[1] == h->srv_gen && *done != a.tag) {
+            if (posted && !relaunched && (uint32_t)reinterpret_cast<volatile uint64_t *>(h->srv_host)[1] == h->srv_gen &&
+                *done != a.tag) {
                 // the server left (idle or its deadline) before it saw the request
                 h->srv_live = false;
                 if ((rc = srv_launch(h, a, a.tag == 1 ? kGetSrvStop - 1 : a.tag - 1))) return rc;
                 relaunched = true;
             }
             if ((k & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(200)) {
-                if (posted) srv_stop(h);
+                if (posted && *done != a.tag) {
+                    // the server did not answer: stop it and take the launch path
+                    srv_stop(h);
+                    if (*done != a.tag) {
+                        posted = false;
+                        h->srv_fallbacks++;
+                        HIPCHK(h, lx::launch_get_rows(a, h->stream));
+                    }
+                }
                 HIPCHK(h, hipStreamSynchronize(h->stream));
                 if (*done != a.tag) return h->fail(LX_ERR_STATE, "getter: the row kernel did not complete");
             }
