@@ -126,3 +126,26 @@ def test_server_leaves_for_device_sync(lx):
         worst = max(worst, time.perf_counter() - t0)
     assert worst < 0.05, worst
     ix.close()
+
+
+def test_server_idle_boundary_race(lx):
+    """Requests spaced around the server's 250 us idle limit: some arrive as
+    it decides to leave; each is still answered (a relaunch or the launch
+    path), with the oracle's bytes."""
+    d = lx.tools.gen_dag(30, 20, 5, 0, 0, 4)
+    w = [1 + (i % 3) for i in range(30)]
+    o = _oracle(d, w)
+    ix = lx.Index()
+    ix.reset(w)
+    ix.add_batch(d.creator, d.seq, d.poff, d.par)
+    ix.sync()
+    N = len(d)
+    for i in range(300):
+        e = (i * 37) % N
+        assert ix.highest_before(e) == o.hb(e), e
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < 0.00018 + 0.00002 * (i % 7):   # 180-300 us
+            pass
+    st = ix.get_server_stats()
+    assert st["served"] + st["fallbacks"] >= 300 and st["launches"] >= 2, st
+    ix.close()
