@@ -9,7 +9,7 @@ L=lachesis-base_amd/build/liblachesis_hip.so
 cp $L $O/a.so || exit 1
 for i in 1 2; do
   cp $O/a.so $L && timeout -k 10 200 python3 scripts/dropin_probe.py > $O/a_$i.json 2> $O/a_$i.err || { cp $O/a.so $L; exit 1; }
-  cp lachesis-base_amd/build_ab/liblachesis_hip.so $L && timeout -k 10 200 python3 scripts/dropin_probe.py > $O/b_$i.json 2> $O/b_$i.err || { cp $O/a.so $L; exit 1; }
+  cp ${BLIB:-lachesis-base_amd/build_ab/liblachesis_hip.so} $L && timeout -k 10 200 python3 scripts/dropin_probe.py > $O/b_$i.json 2> $O/b_$i.err || { cp $O/a.so $L; exit 1; }
 done
 cp $O/a.so $L
 rm -f $O/a.so
