@@ -1550,6 +1550,9 @@ static hipError_t launch_fc_t(const FcArgs &a, bool forks, hipStream_t s) {
 hipError_t launch_fc(const FcArgs &a, uint32_t cols, bool forks, hipStream_t s) {
     if (forks && !a.fk_hi4 && !a.n_cheat) forks = false;   // no cheater among this handle's creators
     const uint32_t nv = forks && a.fk_hi4 ? a.fk_hi4 : a.vhi4 - a.vlo4;
+    // (rows of <= 8 branches: 2 lanes, twice the queries per wave -- C1's
+    // 20-B rows 0.078 -> 0.072 ms per 2^22 queries, profiles/r04/fc_small_rows_r04y.jsonl)
+    if (nv <= 2) return launch_fc_t<2>(a, forks, s);
     if (nv <= 16) return launch_fc_t<4>(a, forks, s);
     if (nv <= 32) return launch_fc_t<8>(a, forks, s);
     if (nv <= 64) return launch_fc_t<16>(a, forks, s);
