@@ -76,23 +76,46 @@ __global__ void k_seg_prefix_j(SegArgs a) {
 }
 
 // one workgroup per partial event of segment k (every earlier row final):
-// the max of the rows it references, one per branch
+// the max of the rows it references, one per branch.  The row indices go to
+// LDS first (one pass over the branches, in parallel), then every thread
+// streams its columns of those rows eight at a time -- the loads of a group
+// in flight together instead of one brow -> row -> max chain per branch
 __global__ void __launch_bounds__(256) k_seg_partial(SegArgs a, uint32_t k) {
-    extern __shared__ uint32_t lrow[];
+    extern __shared__ uint32_t refs[];   // <= B referenced rows
+    __shared__ uint32_t n_refs;
     const uint32_t e = a.plist[a.seg_lo[k] - a.bs + blockIdx.x];
     const uint32_t *J = a.jt + (uint64_t)k * a.B;
     uint32_t *row = a.hb + (uint64_t)e * a.stride;
-    for (uint32_t c = threadIdx.x; c < a.B; c += blockDim.x) lrow[c] = row[c];
+    if (threadIdx.x == 0) n_refs = 0;
     __syncthreads();
+    for (uint32_t c = threadIdx.x; c < a.B; c += blockDim.x) {
+        const uint32_t m = min(row[c], J[c]);
+        if (m) refs[atomicAdd(&n_refs, 1u)] = row_of(a, c, m);
+    }
+    __syncthreads();
+    const uint32_t n = n_refs;
     constexpr int W = 4;   // columns per thread per step
+    constexpr uint32_t U = 8;   // referenced rows in flight per thread
     for (uint32_t c0 = threadIdx.x * W; c0 < a.stride; c0 += blockDim.x * W) {
         uint32_t acc[W];
 #pragma unroll
         for (int i = 0; i < W; i++) acc[i] = row[c0 + i];
-        for (uint32_t b = 0; b < a.B; b++) {
-            const uint32_t m = min(lrow[b], J[b]);
-            if (!m) continue;
-            const uint4 v = *reinterpret_cast<const uint4 *>(a.hb + (uint64_t)row_of(a, b, m) * a.stride + c0);
+        uint32_t i = 0;
+        for (; i + U <= n; i += U) {
+            uint4 v[U];
+#pragma unroll
+            for (uint32_t u = 0; u < U; u++)
+                v[u] = *reinterpret_cast<const uint4 *>(a.hb + (uint64_t)refs[i + u] * a.stride + c0);
+#pragma unroll
+            for (uint32_t u = 0; u < U; u++) {
+                acc[0] = max(acc[0], v[u].x & LX_SEQ_MASK);
+                acc[1] = max(acc[1], v[u].y & LX_SEQ_MASK);
+                acc[2] = max(acc[2], v[u].z & LX_SEQ_MASK);
+                acc[3] = max(acc[3], v[u].w & LX_SEQ_MASK);
+            }
+        }
+        for (; i < n; i++) {
+            const uint4 v = *reinterpret_cast<const uint4 *>(a.hb + (uint64_t)refs[i] * a.stride + c0);
             acc[0] = max(acc[0], v.x & LX_SEQ_MASK);
             acc[1] = max(acc[1], v.y & LX_SEQ_MASK);
             acc[2] = max(acc[2], v.z & LX_SEQ_MASK);
