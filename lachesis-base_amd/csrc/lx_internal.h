@@ -566,7 +566,7 @@ struct SegArgs {
     const uint32_t *brow;
     uint32_t s_cap;
     uint32_t *jt;                // [(G + 1) * B]: row k = J_k, last seq of each branch before segment k
-    uint32_t *cnt;               // [B] batch events per branch, then [G] partial counts, [G] edge counts
+    uint32_t *cnt;               // [B] seq of each branch's first batch event (0: none), then [G] partial counts, [G] edge counts
     uint32_t *pflag;             // [n] partial flags (k_index drains)
     uint32_t *plist;             // partial events of segment k at plist[seg_lo[k] - bs ..]
     uint32_t *pcount;            // [G]

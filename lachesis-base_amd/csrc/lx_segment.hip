@@ -50,22 +50,29 @@ __device__ __forceinline__ uint32_t row_of(const SegArgs &a, uint32_t c, uint32_
     return a.brow[(uint64_t)c * a.s_cap + (s - a.branch_first[c])];
 }
 
-// per batch event: the last seq of its branch in its segment, and the number
-// of batch events per branch
+// per batch event, without atomics (a branch is a seq-consecutive chain in
+// Add order, so each entry has exactly one writer): the last event of its
+// branch in its segment writes its seq as that segment's entry, the branch's
+// first batch event writes its own seq into cnt
 __global__ void k_seg_scan(SegArgs a) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= a.n) return;
     const uint32_t e = a.bs + i;
-    const uint32_t b = a.ev_branch[e];
-    atomicMax(a.jt + (uint64_t)(seg_of(a, e) + 1) * a.B + b, a.ev_seq[e]);
-    atomicAdd(a.cnt + b, 1u);
+    const uint32_t b = a.ev_branch[e], s = a.ev_seq[e], first = a.branch_first[b];
+    const uint32_t k = seg_of(a, e);
+    // the branch's next event: none, or its row (a later segment ends this one's run)
+    const bool last_of_branch = s + 1 - first >= a.branch_len[b];
+    if (last_of_branch || a.brow[(uint64_t)b * a.s_cap + (s + 1 - first)] >= a.seg_lo[k + 1])
+        a.jt[(uint64_t)(k + 1) * a.B + b] = s;
+    if (s == first || a.brow[(uint64_t)b * a.s_cap + (s - 1 - first)] < a.bs) a.cnt[b] = s;
 }
 
 // J_0 from the branch lengths before the batch, then J_{k+1} = max(J_k, last in k)
 __global__ void k_seg_prefix_j(SegArgs a) {
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= a.B) return;
-    const uint32_t before = a.branch_len[c] - a.cnt[c];
+    // cnt[c]: the seq of the branch's first batch event (0: none in the batch)
+    const uint32_t before = a.cnt[c] ? a.cnt[c] - a.branch_first[c] : a.branch_len[c];
     uint32_t j = before ? a.branch_first[c] + before - 1 : 0u;
     a.jt[c] = j;
     for (uint32_t k = 1; k <= a.G; k++) {
