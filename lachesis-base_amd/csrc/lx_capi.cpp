@@ -869,6 +869,7 @@ int lx_fc_args(lx_index *h, uint64_t n, const uint32_t *a, const uint32_t *b, ui
     f.own_hi = h->own_hi;
     f.branch_creator = h->branch_creator;
     f.status = h->status;
+    h->fc_unchecked = true;   // a query it cannot answer flags status[1]; lx_sync reports it
     *fa = f;
     return 0;
 }
@@ -2741,6 +2742,11 @@ int lx_sync(lx_index *h) {
         if (rc) return rc;
     }
     HIPCHK(h, hipStreamSynchronize(h->stream));
+    // the unknown-event flag of asynchronous ForklessCause batches: read only
+    // when one ran since the last check (a blocking 4-byte copy costs ~10 us,
+    // the whole of an Add-and-sync otherwise)
+    if (!h->fc_unchecked) return 0;
+    h->fc_unchecked = false;
     uint32_t bad = 0;
     HIPCHK(h, hipMemcpy(&bad, h->status + 1, 4, hipMemcpyDeviceToHost));
     if (bad) {

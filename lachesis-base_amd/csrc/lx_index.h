@@ -233,6 +233,7 @@ struct lx_index {
     uint8_t *qp = nullptr, *qp_dev = nullptr;
     uint64_t qp_cap = 0;
     uint32_t get_tag = 0;                  // completion tag of the last single-row getter
+    bool fc_unchecked = false;             // a ForklessCause launch may have flagged status[1] since lx_sync looked
     // the resident single-row server (k_get_server, option get_server)
     bool srv_opt = true;
     hipStream_t srv_stream = nullptr;      // its own (high-priority) stream
