@@ -463,10 +463,13 @@ BatchArgs batch_args(lx_index *h, uint32_t n, const uint32_t *creator, const uin
 // seg_stats.
 // Workgroups of one walk of the batch's columns (launch_index's slice choice,
 // rounded to the 8 XCDs)
+// -- the CUs a walk holds: 12-column slices count only the real slices (the
+// launch's rounding workgroups leave at once and free their CUs for the next
+// walk's: V = 1000, 84 slices, three walks side by side)
 uint32_t walk_grid(const lx_index *h, uint32_t cpw_hint) {
     const uint32_t nc = h->ncols, cpw = cpw_hint ? cpw_hint : (nc <= 256 ? 1 : nc <= 512 ? 2 : 4);
     const uint32_t slices = (nc + cpw - 1) / cpw;
-    return (slices + 7) / 8 * 8;
+    return cpw == 12 ? slices : (slices + 7) / 8 * 8;
 }
 
 // Segments walked at once on idle compute units: a walk of few columns leaves
@@ -486,13 +489,14 @@ uint32_t auto_segments(const lx_index *h, uint64_t n, uint32_t *cpw) {
 // the segment count and slice width auto_segments would pick for n events
 // (row-segment ranks split their own segment by it too, lx_rowseg.cpp)
 uint32_t seg_pick(const lx_index *h, uint64_t n, uint32_t *cpw) {
-    static const float kPass[9] = {0, 1.0f, 1.15f, 0, 1.28f, 0, 0, 0, kPass8};
-    // 8-column slices: packed 16-bit slots only (every seq <= 0xFFFF, no forks)
+    static const float kPass[13] = {0, 1.0f, 1.15f, 0, 1.28f, 0, 0, 0, kPass8, 0, 0, 0, kPass12};
+    // 8- and 12-column slices: packed 16-bit slots only (every seq <= 0xFFFF, no forks)
     const bool w8 = h->pack16 && h->max_seq <= 0xFFFFu && h->B <= h->V;
     uint32_t best_g = 0;
     float best = 1.0f;   // one walk at the default width
-    for (uint32_t c : {1u, 2u, 4u, 8u}) {
-        if ((h->cpw_hint && c != h->cpw_hint) || (c == 8 && !w8)) continue;
+    for (uint32_t c : {1u, 2u, 4u, 8u, 12u}) {
+        if ((h->cpw_hint && c != h->cpw_hint) || (c >= 8 && !w8)) continue;
+        if (c == 12 && !h->cpw_hint && h->ncols <= 512) continue;   // few columns: 8-column slices already give >= 4 walks
         uint32_t G = std::min<uint32_t>(h->n_cus / walk_grid(h, c), kSegLaunchMax);
         while (G >= 2 && n < (uint64_t)G * kAutoSegEvents) G--;
         if (G >= 2 && kPass[c] / G < best) {
@@ -551,7 +555,7 @@ int seg_walk(lx_index *h, IndexArgs ia, const uint32_t *poff, hipStream_t s, uin
     HIPCHK(h, lx::launch_seg_tables(a, s));
     // one launch for all G when they fit the CUs side by side (one workgroup
     // per CU each: k_index_segs); otherwise one walk after the other
-    ia.cpw_hint = cpw == 8 && (!ia.pack16 || ia.mask) ? 4 : cpw;
+    ia.cpw_hint = cpw >= 8 && (!ia.pack16 || ia.mask) ? 4 : cpw;
     cpw = ia.cpw_hint;
     const bool conc = G <= kSegLaunchMax && G * walk_grid(h, cpw) <= h->n_cus;
     ia.seg = 1;
@@ -708,7 +712,7 @@ int add_batch_dev(lx_index *h, uint32_t n, const uint32_t *creator, const uint32
     ia.mask = (h->B > h->V) ? 1u : 0u;
     ia.cpw_hint = h->cpw_hint;
     ia.pack16 = h->pack16 && h->max_seq <= 0xFFFFu;
-    if (ia.cpw_hint == 8 && (!ia.pack16 || ia.mask)) ia.cpw_hint = 4;   // 8-column slots: packed, fork-free
+    if (ia.cpw_hint >= 8 && (!ia.pack16 || ia.mask)) ia.cpw_hint = 4;   // 8- / 12-column slots: packed, fork-free
     const size_t prof_n = (size_t)kProfBlocks * kProfWaves * kProfSlots;
     if (h->prof) {
         HIPCHK(h, hipMalloc(&ia.prof, prof_n * 8));
@@ -1710,8 +1714,8 @@ int lx_set_option(lx_index *h, const char *name, int64_t value) {
     } else if (k == "fc_fk") {
         h->fc_fk = value != 0;
     } else if (k == "cpw") {
-        if (value != 0 && value != 1 && value != 2 && value != 4 && value != 8)
-            return h->fail(LX_ERR_ARG, "cpw must be 0, 1, 2, 4 or 8 (8: fork-free epochs with seqs <= 0xFFFF)");
+        if (value != 0 && value != 1 && value != 2 && value != 4 && value != 8 && value != 12)
+            return h->fail(LX_ERR_ARG, "cpw must be 0, 1, 2, 4, 8 or 12 (8, 12: fork-free epochs with seqs <= 0xFFFF)");
         h->cpw_hint = (uint32_t)value;
     } else if (k == "pack16") {
         h->pack16 = value != 0;

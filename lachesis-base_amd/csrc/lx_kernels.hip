@@ -359,8 +359,9 @@ __device__ __forceinline__ void unpack16(const u4v &x, uint32_t *v) {
 }
 template <int CPW, bool PK = false>
 __device__ __forceinline__ void ring_read1(uint32_t A, uint32_t B, uint32_t s, Slot<CPW> &o) {
-    if constexpr (PK && CPW == 8) {
+    if constexpr (PK && (CPW == 8 || CPW == 12)) {
         // two units {tag, s0 | s1 << 16, s2 | s3 << 16, s4 | s5 << 16}, {tag, s6 | s7 << 16, 0, 0}
+        // (12 columns: {tag, s6 | s7 << 16, s8 | s9 << 16, s10 | s11 << 16})
         u4v x, y;
         asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %3\n\ts_waitcnt lgkmcnt(0)"
                      : "=&v"(x), "=&v"(y)
@@ -368,12 +369,12 @@ __device__ __forceinline__ void ring_read1(uint32_t A, uint32_t B, uint32_t s, S
                      : "memory");
         o.t0 = x.x;
         o.t1 = y.x;
-        const uint32_t w[4] = {x.y, x.z, x.w, y.y};
+        const uint32_t w[6] = {x.y, x.z, x.w, y.y, y.z, y.w};
 #pragma unroll
-        for (int k = 0; k < CPW; k++) o.v[k] = (k & 1) ? w[(k / 2) % 4] >> 16 : w[(k / 2) % 4] & 0xFFFFu;
+        for (int k = 0; k < CPW; k++) o.v[k] = (k & 1) ? w[(k / 2) % 6] >> 16 : w[(k / 2) % 6] & 0xFFFFu;
         return;
     } else if constexpr (PK) {
-        static_assert(CPW == 4, "packed slots: 4- or 8-column slices");
+        static_assert(CPW == 4, "packed slots: 4-, 8- or 12-column slices");
         u4v x;
         asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=&v"(x) : "v"(A + s * 16u) : "memory");
         o.t0 = o.t1 = x.x;
@@ -498,8 +499,8 @@ __device__ __forceinline__ void blk_fold(const uint32_t pa[3], uint32_t W, uint3
         }
         return;
     }
-    if constexpr (CPW == 4 || CPW == 8) {
-        // two units per slot; CPW 8 (packed): pv[k][0..3] = packed column pairs
+    if constexpr (CPW == 4 || CPW == 8 || CPW == 12) {
+        // two units per slot; CPW 8 / 12 (packed): pv[k][0..3 / 5] = packed column pairs
         constexpr uint32_t BOFF = (RN + 1) * 16;
         static_assert(BOFF < 65536, "ds offset field");
         u4v xa0, xb0, xa1, xb1, xa2, xb2;
@@ -521,6 +522,7 @@ __device__ __forceinline__ void blk_fold(const uint32_t pa[3], uint32_t W, uint3
         for (int k = 0; k < 3; k++) {
             tg[k][0] = xa[k].x; tg[k][1] = xb[k].x;
             pv[k][0] = xa[k].y; pv[k][1 % CPW] = xa[k].z; pv[k][2 % CPW] = xa[k].w; pv[k][3 % CPW] = xb[k].y;
+            if constexpr (CPW == 12) { pv[k][4] = xb[k].z; pv[k][5] = xb[k].w; }
         }
     } else if constexpr (CPW == 2) {
         u4v x0, x1, x2;
@@ -557,16 +559,16 @@ __device__ __forceinline__ void blk_fold(const uint32_t pa[3], uint32_t W, uint3
 // (B > V); PK: 4-column slices with 16-bit packed slot units (every seq of the
 // epoch <= 0xFFFF).
 template <int CPW, int NCW, bool MASKED, bool PK, int ND_ = kND>
-__device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t w) {
-    static_assert(!PK || CPW >= 4, "packed slots: 4- or 8-column slices");
-    static_assert(CPW == 1 || CPW == 2 || CPW == 4 || (CPW == 8 && PK && !MASKED), "slot layout");
+__device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t slice) {
+    static_assert(!PK || CPW >= 4, "packed slots: 4-, 8- or 12-column slices");
+    static_assert(CPW == 1 || CPW == 2 || CPW == 4 || ((CPW == 8 || CPW == 12) && PK && !MASKED), "slot layout");
     static_assert(LX_MAXP == 12, "block walker: 12 inline parents, three per lane of a quad");
     constexpr int ND = ND_;
     static_assert(ND >= 1 && ND <= 8, "drain waves");
     constexpr int RR = kRR;
     constexpr int NT = 64 * (NCW + 1 + ND);
     constexpr int RQ = LX_REC_Q;
-    constexpr int KB = 1024 / CPW;               // recent (seq -> event) entries per owned branch
+    constexpr int KB = CPW == 12 ? 64 : 1024 / CPW;   // recent (seq -> event) entries per owned branch
     constexpr int RN = Ring<CPW>::N;
     constexpr int RB16 = Ring<CPW>::BYTES / 16;
     static_assert(RR % 64 == 0 && RR / 64 >= 4 && RR >= 2 * 16 * NCW, "record ring");
@@ -578,8 +580,8 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t w)
     __shared__ uint2 brc[CPW * KB];              // {seq, event} of recent events of owned branches
     __shared__ uint4 dummy[128];                 // per-lane targets of suppressed writes
     __shared__ WalkShared sh;
+    __shared__ uint32_t sjs[CPW];                // segment walk: J_k of the slice's columns (drains)
 
-    const uint32_t slice = (w % 8) * a.slices_per_xcd + (w / 8);   // XCD-aware: neighbouring slices share an L2
     if (slice >= a.n_slices) return;
 
     // null slot: unit A right after the A array (uint4 index RN, or RN / 2 for
@@ -590,6 +592,10 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t w)
     for (int i = threadIdx.x; i < RR / 64; i += NT) rtag[i] = 0;
     for (int i = threadIdx.x; i < CPW * KB; i += NT) brc[i] = make_uint2(0, LX_NONE);
     if (threadIdx.x < ND) { sh.copied[threadIdx.x] = 0; sh.stored[threadIdx.x] = 0; }
+    if (threadIdx.x < CPW) {
+        const uint32_t ci = slice * CPW + threadIdx.x;
+        sjs[threadIdx.x] = a.seg && ci < a.ncols ? a.seg_j[CPW == 12 ? ci : a.col_list[ci]] : 0u;
+    }
     if (threadIdx.x == 0) { sh.req = 0; sh.p_issued = 0; sh.p_done = 0; }
     __syncthreads();
 
@@ -611,8 +617,14 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t w)
     for (int k = 0; k < CPW; k++) {
         const uint32_t ci = slice * CPW + k;
         valid[k] = ci < a.ncols;
-        col[k] = valid[k] ? a.col_list[ci] : 0;
-        pc[k] = valid[k] ? (a.cmap ? a.cmap[col[k]] : col[k]) : 0;
+        if constexpr (CPW == 12) {
+            // whole handles only (launch_index): the column list is the identity
+            col[k] = valid[k] ? ci : 0;
+            pc[k] = col[k];
+        } else {
+            col[k] = valid[k] ? a.col_list[ci] : 0;
+            pc[k] = valid[k] ? (a.cmap ? a.cmap[col[k]] : col[k]) : 0;
+        }
         first[k] = valid[k] ? a.branch_first[col[k]] : 1;
         contig &= valid[k] && pc[k] == pc[0] + k;
     }
@@ -700,9 +712,7 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t w)
         // ------------------------------------------------------------ drain
         const uint32_t d = wave - NCW - 1;
         uint32_t nd = 0;                 // rounds of this wave completed
-        uint32_t sj[CPW];                // segment walk: J_k of the slice's columns
-#pragma unroll
-        for (int k = 0; k < CPW; k++) sj[k] = a.seg && valid[k] ? a.seg_j[col[k]] : 0u;
+        const uint32_t *sj = sjs;        // segment walk: J_k of the slice's columns (LDS)
 #ifdef LX_WALKER_PROF
         uint32_t d_spin = 0, d_fill = 0, d_miss = 0;
         const unsigned long long dt0 = wall_clock64();
@@ -790,8 +800,10 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t w)
                     else if (CPW == 2) *reinterpret_cast<uint2 *>(hrow + pc[0]) = make_uint2(r[0], r[1 % CPW]);
                     else if (CPW == 4) *reinterpret_cast<uint4 *>(hrow + pc[0]) = make_uint4(r[0], r[1 % CPW], r[2 % CPW], r[3 % CPW]);
                     else {
-                        *reinterpret_cast<uint4 *>(hrow + pc[0]) = make_uint4(r[0], r[1 % CPW], r[2 % CPW], r[3 % CPW]);
-                        *reinterpret_cast<uint4 *>(hrow + pc[0] + 4) = make_uint4(r[4 % CPW], r[5 % CPW], r[6 % CPW], r[7 % CPW]);
+#pragma unroll
+                        for (int q = 0; q < CPW / 4; q++)
+                            *reinterpret_cast<uint4 *>(hrow + pc[0] + 4 * q) =
+                                make_uint4(r[(4 * q) % CPW], r[(4 * q + 1) % CPW], r[(4 * q + 2) % CPW], r[(4 * q + 3) % CPW]);
                     }
                 } else {
 #pragma unroll
@@ -976,10 +988,20 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t w)
                 wstuck = __any(far_parent(px, lp, (uint32_t)RN - kLeanFar)) ? kLeanStuck : 0u;
                 {
                     const uint32_t rs = (lp % RN) * UA;
-                    wa_pub = j == 0 ? RA + rs : (((CPW == 4 && !PK) || CPW == 8) && j == 1) ? RB + (lp % RN) * 16u : dmy;
-                    wb_pub = (myvalid && mycol == br) ? lds_addr(brc) + ((j & (CPW - 1)) * KB + seq % KB) * 8u
-                             : (CPW == 8 && myvalid2 && mycol2 == br) ? lds_addr(brc) + (((j + 4) & (CPW - 1)) * KB + seq % KB) * 8u
-                                                                       : dmy + 1024u;
+                    wa_pub = j == 0 ? RA + rs : (((CPW == 4 && !PK) || CPW >= 8) && j == 1) ? RB + (lp % RN) * 16u : dmy;
+                    if constexpr (CPW == 12) {
+                        // lane j of a quad owns columns j, j + 4, j + 8 (recent-event entries)
+                        uint32_t wb = dmy + 1024u;
+#pragma unroll
+                        for (int k = 0; k < CPW; k++)
+                            if ((uint32_t)(k & 3) == j && valid[k] && col[k] == br)
+                                wb = lds_addr(brc) + ((uint32_t)k * KB + seq % KB) * 8u;
+                        wb_pub = wb;
+                    } else {
+                        wb_pub = (myvalid && mycol == br) ? lds_addr(brc) + ((j & (CPW - 1)) * KB + seq % KB) * 8u
+                                 : (CPW == 8 && myvalid2 && mycol2 == br) ? lds_addr(brc) + (((j + 4) & (CPW - 1)) * KB + seq % KB) * 8u
+                                                                           : dmy + 1024u;
+                    }
                     // the slot's previous occupant lp - RN is drained once its
                     // drain wave's `copied` count exceeds its round / ND
                     const uint32_t rr = (lp - RN) / 64;
@@ -1099,10 +1121,11 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t w)
                     u2v x;
                     x.x = lp + 1; x.y = m[0];
                     asm volatile("ds_write_b64 %2, %3\n\tds_write_b64 %0, %1" : : "v"(wa), "v"(x), "v"(wb), "v"(y) : "memory");
-                } else if constexpr (PK && CPW == 8) {
-                    u4v x;   // lane 0: {tag, s01, s23, s45}, lane 1: {tag, s67, 0, 0}
-                    x.x = lp + 1; x.y = j == 0 ? mp[0] : mp[3 % NH]; x.z = j == 0 ? mp[1 % NH] : 0u;
-                    x.w = j == 0 ? mp[2 % NH] : 0u;
+                } else if constexpr (PK && CPW >= 8) {
+                    u4v x;   // lane 0: {tag, s01, s23, s45}, lane 1: {tag, s67, 0, 0} (12: {tag, s67, s89, s1011})
+                    x.x = lp + 1; x.y = j == 0 ? mp[0] : mp[3 % NH];
+                    x.z = j == 0 ? mp[1 % NH] : CPW == 12 ? mp[4 % NH] : 0u;
+                    x.w = j == 0 ? mp[2 % NH] : CPW == 12 ? mp[5 % NH] : 0u;
                     asm volatile("ds_write_b64 %2, %3\n\tds_write_b128 %0, %1" : : "v"(wa), "v"(x), "v"(wb), "v"(y) : "memory");
                 } else if constexpr (PK) {
                     u4v x;   // lane 0: {tag, s0 | s1 << 16, s2 | s3 << 16, 0}
@@ -1167,7 +1190,32 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t w)
 
 template <int CPW, int NCW, bool MASKED, bool PK, int ND = kND>
 __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
-    index_body<CPW, NCW, MASKED, PK, ND>(a, blockIdx.x);
+    // XCD-aware: neighbouring slices share an L2
+    index_body<CPW, NCW, MASKED, PK, ND>(a, (blockIdx.x % 8) * a.slices_per_xcd + blockIdx.x / 8);
+}
+
+// 12-column slices, seg_g walks side by side: workgroup g runs on XCD g % 8
+// (dispatch deals workgroups round-robin over the XCDs), which takes a
+// contiguous chunk of each walk's slices in turn -- walk k gives its S % 8
+// remainder slices to the XCDs (x - k * rem) mod 8 < rem, so every XCD holds
+// at most ceil(seg_g * S / 8) workgroups (V = 1000: 84 slices, three walks,
+// 31-32 per XCD of 32 CUs) and the rounding workgroups leave at once
+__device__ __forceinline__ bool seg_chunk(uint32_t g, uint32_t G, uint32_t S, uint32_t *k, uint32_t *slice) {
+    const uint32_t base = S / 8, rem = S % 8, x = g % 8;
+    uint32_t p = g / 8;
+    for (uint32_t kk = 0; kk < G; kk++) {
+        const uint32_t sh = (kk * rem) % 8;
+        const uint32_t sz = base + (((x + 8 - sh) % 8) < rem ? 1u : 0u);
+        if (p < sz) {
+            uint32_t start = x * base;
+            for (uint32_t y = 0; y < x; y++) start += ((y + 8 - sh) % 8) < rem ? 1u : 0u;
+            *k = kk;
+            *slice = start + p;
+            return true;
+        }
+        p -= sz;
+    }
+    return false;
 }
 
 // seg_g Add-order segments of a batch walked by one launch, side by side on
@@ -1176,7 +1224,14 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
 // segment's own batch window, J table and partial-event lists (lx_segment.hip)
 template <int CPW, int NCW, bool MASKED, bool PK, int ND = kND>
 __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index_segs(IndexArgs a0) {
-    const uint32_t per = gridDim.x / a0.seg_g, k = blockIdx.x / per;
+    uint32_t k, slice;
+    if constexpr (CPW == 12) {
+        if (!seg_chunk(blockIdx.x, a0.seg_g, a0.n_slices, &k, &slice)) return;
+    } else {
+        const uint32_t per = gridDim.x / a0.seg_g, w = blockIdx.x % per;
+        k = blockIdx.x / per;
+        slice = (w % 8) * a0.slices_per_xcd + w / 8;   // XCD-aware: neighbouring slices share an L2
+    }
     IndexArgs a = a0;
     const uint32_t lo = a0.seg_lo[k], off = lo - a0.batch_start;
     a.batch_start = lo;
@@ -1187,7 +1242,7 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index_segs(IndexArgs a0
     a.seg_flag = a0.seg_flag + off;
     a.seg_list = a0.seg_list + off;
     a.seg_count = a0.seg_count + k;
-    index_body<CPW, NCW, MASKED, PK, ND>(a, blockIdx.x - k * per);
+    index_body<CPW, NCW, MASKED, PK, ND>(a, slice);
 }
 
 template <int CPW, int NCW, int ND = kND>
@@ -1197,9 +1252,12 @@ static hipError_t launch_index_t(const IndexArgs &a0, hipStream_t s) {
     a.slices_per_xcd = (a.n_slices + 7) / 8;
     const uint32_t grid = a.slices_per_xcd * 8;
     const dim3 blk(64 * (NCW + 1 + ND));
-    if constexpr (CPW == 8) {   // packed fork-free epochs only
+    if constexpr (CPW >= 8) {   // packed fork-free epochs only
         if (!a.pack16 || a.mask) return hipErrorInvalidValue;
-        if (a.seg_g) hipLaunchKernelGGL((k_index_segs<CPW, NCW, false, true, ND>), dim3(grid * a.seg_g), blk, 0, s, a);
+        // (12 columns: at most ceil(seg_g * slices / 8) workgroups per XCD, seg_chunk)
+        const uint32_t sgrid = CPW == 12 ? 8 * (a.seg_g * (a.n_slices / 8) + (a.seg_g * (a.n_slices % 8) + 7) / 8)
+                                         : grid * a.seg_g;
+        if (a.seg_g) hipLaunchKernelGGL((k_index_segs<CPW, NCW, false, true, ND>), dim3(sgrid), blk, 0, s, a);
         else hipLaunchKernelGGL((k_index<CPW, NCW, false, true, ND>), dim3(grid), blk, 0, s, a);
         return hipGetLastError();
     } else {
@@ -1243,6 +1301,8 @@ hipError_t launch_index(const IndexArgs &a, hipStream_t s) {
     // 8 columns: twice the drains' work per event (HB row, range fills), so
     // 7 drain waves beside 8 compute waves
     if (cpw == 8) return launch_index_t<8, 8, 7>(a, s);
+    // 12 columns (V = 1000: 84 slices, three walks side by side on 256 CUs)
+    if (cpw == 12) return a.cmap ? launch_index_t<8, 8, 7>(a, s) : launch_index_t<12, 8, 7>(a, s);
     return launch_index_t<4, 11>(a, s);
 }
 

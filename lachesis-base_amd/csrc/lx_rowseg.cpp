@@ -200,7 +200,7 @@ int rs_begin(lx_index *h, IndexArgs ia, const uint32_t *poff, hipStream_t s) {
     const uint32_t k0 = a.own_seg;
     // the own sub-segments: one k_index_segs launch side by side when they fit
     // the CUs (as a single-GPU batch), else one walk each
-    if (S > 1) ia.cpw_hint = cpw == 8 && (!ia.pack16 || ia.mask) ? 4 : cpw;
+    if (S > 1) ia.cpw_hint = cpw >= 8 && (!ia.pack16 || ia.mask) ? 4 : cpw;
     const bool conc = S > 1 && S * seg_walk_grid(h, ia.cpw_hint) <= h->n_cus;
     HIPCHK(h, hipEventRecord(h->seg_ev[0], s));
     for (uint32_t t = 0; t < S; t++) {

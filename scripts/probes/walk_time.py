@@ -22,7 +22,8 @@ w = [(1 << 20) // (i + 1) for i in range(V)]
 dev = torch.device("cuda", 0)
 to_dev = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int32)).to(dev)
 dc, ds, dp, do = to_dev(d.creator), to_dev(d.seq), to_dev(d.par), to_dev(d.poff.astype(np.uint32))
-ix = lx.Index(event_capacity=N)
+# WT_OPTS: index options as JSON, e.g. '{"cpw": 8}'
+ix = lx.Index(event_capacity=N, options=json.loads(os.environ.get("WT_OPTS", "{}")))
 ks, walks = [], []
 for r in range(6):
     ix.reset(w)
@@ -31,6 +32,6 @@ for r in range(6):
     ks.append(ix.last_stats()["ms_index"])
     st = ix.segment_stats()
     walks.append(max(st["walk_ms"]) if st["segments"] else None)
-print(json.dumps({"lib": os.environ.get("LX_LIB", "build/liblachesis_hip.so"), "events": N,
+print(json.dumps({"lib": os.environ.get("LX_LIB", "build/liblachesis_hip.so"), "opts": os.environ.get("WT_OPTS", "{}"), "events": N,
                   "ms_index_median": float(np.median(ks[1:])), "ms_index": ks[1:],
                   "walk_ms": walks[1:], "segments": ix.segment_stats()["segments"]}))

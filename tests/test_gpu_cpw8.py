@@ -1,5 +1,5 @@
-"""The walker on 8-column slices (packed 16-bit slot units in two 16-B units:
-fork-free epochs whose seqs fit 16 bits), alone and as side-by-side segments:
+"""The walker on 8- and 12-column slices (packed 16-bit slot units in two 16-B
+units: fork-free epochs whose seqs fit 16 bits), alone and as side-by-side segments:
 rows and ForklessCause against the C oracle, planes byte-identical to the
 4-column walk."""
 
@@ -39,8 +39,9 @@ def planes_of(lx, d, w, opts):
     return ix, out
 
 
+@pytest.mark.parametrize("cpw", [8, 12])
 @pytest.mark.parametrize("shape", [(24, 250, 6), (13, 400, 5), (30, 120, 16), (200, 60, 10)])
-def test_cpw8_walk_vs_oracle_and_cpw4(lx, shape):
+def test_cpw8_walk_vs_oracle_and_cpw4(lx, shape, cpw):
     """One walk on 8-column slices (ring slots reused, parents beyond the
     inline twelve, a partly filled last slice, many slices)."""
     V, epv, P = shape
@@ -49,7 +50,7 @@ def test_cpw8_walk_vs_oracle_and_cpw4(lx, shape):
     N = len(d)
     o = corc.OracleIndex(w)
     assert o.add_batch(d.creator, d.seq, d.poff, d.par) == -1
-    ix8, p8 = planes_of(lx, d, w, {"cpw": 8, "seg_auto": 0})
+    ix8, p8 = planes_of(lx, d, w, {"cpw": cpw, "seg_auto": 0})
     ix4, p4 = planes_of(lx, d, w, {"cpw": 4, "seg_auto": 0})
     np.testing.assert_array_equal(p8[0], p4[0])
     np.testing.assert_array_equal(p8[1], p4[1])
@@ -62,16 +63,18 @@ def test_cpw8_walk_vs_oracle_and_cpw4(lx, shape):
     ix4.close()
 
 
-@pytest.mark.parametrize("shape", [(64, 2100, 10), (100, 1400, 8)])
-def test_cpw8_side_by_side_segments(lx, shape):
-    """Segments side by side on 8-column slices (one k_index_segs launch)
+@pytest.mark.parametrize("cpw,G", [(8, 4), (12, 3), (12, 4)])
+@pytest.mark.parametrize("shape", [(64, 2100, 10), (100, 1400, 8), (1000, 60, 10)])
+def test_cpw8_side_by_side_segments(lx, shape, cpw, G):
+    """Segments side by side on 8- / 12-column slices (one k_index_segs
+    launch; V = 1000 at 12 columns: 84 slices, three walks on 256 CUs)
     byte-identical to one walk."""
     V, epv, P = shape
     d = lx.tools.gen_dag(V, epv, P, seed=5)
     w = [1] * V
-    ix8, p8 = planes_of(lx, d, w, {"cpw": 8, "segments": 4})
+    ix8, p8 = planes_of(lx, d, w, {"cpw": cpw, "segments": G})
     st = ix8.segment_stats()
-    assert st["segments"] == 4, st
+    assert st["segments"] == G, st
     ix1, p1 = planes_of(lx, d, w, {"seg_auto": 0})
     np.testing.assert_array_equal(p8[0], p1[0])
     np.testing.assert_array_equal(p8[1], p1[1])
@@ -79,14 +82,15 @@ def test_cpw8_side_by_side_segments(lx, shape):
     ix1.close()
 
 
-def test_cpw8_falls_back_with_forks(lx):
-    """cpw = 8 on a fork epoch walks 4-column slices (8-column slots need
+@pytest.mark.parametrize("cpw", [8, 12])
+def test_cpw8_falls_back_with_forks(lx, cpw):
+    """cpw = 8 / 12 on a fork epoch walks 4-column slices (8-column slots need
     packed fork-free values): rows still equal the oracle."""
     d = lx.tools.gen_dag(20, 150, 6, 3, 4, seed=9)
     w = [2] * 20
     o = corc.OracleIndex(w)
     assert o.add_batch(d.creator, d.seq, d.poff, d.par) == -1
-    ix, _ = planes_of(lx, d, w, {"cpw": 8})
+    ix, _ = planes_of(lx, d, w, {"cpw": cpw})
     ev = np.arange(0, len(d), 3, dtype=np.uint32)
     for mode in (0, 1):
         assert np.array_equal(ix.rows_np(mode, ev)[1], o.rows(mode, ev)[1]), mode

@@ -412,14 +412,14 @@ def test_full_size_config3_prefix_vs_oracle(lx):
 
 
 @pytest.mark.big_only
-def test_config3_shape_1m_default_two_segments_vs_oracle(lx):
+def test_config3_shape_1m_default_segments_vs_oracle(lx):
     """The headline walk as shipped, pinned end to end: BASELINE configs[2]'s
     shape (V=1000, Zipf stakes, P=10) at 1,000 events per validator (1M
     events), indexed as one batch with DEFAULT options.  seg_auto then walks
-    it as two side-by-side Add-order segments of 8-column slices (the 10M
-    headline's exact configuration: k_index_segs<8 columns, 7 drains>), so the
-    second segment -- its boundary parents, its partial-event fix-up
-    (k_seg_partial) and its edge LowestAfter pass (k_seg_la_edge) -- lies
+    it as three side-by-side Add-order segments of 12-column slices (the 10M
+    headline's exact configuration: k_index_segs<12 columns, 7 drains>), so the
+    later segments -- their boundary parents, their partial-event fix-up
+    (k_seg_partial) and their edge LowestAfter pass (k_seg_la_edge) -- lie
     inside the oracle's coverage.  EVERY HighestBefore and LowestAfter row of
     the epoch byte-identical, branch IDs, and 1M ForklessCause pairs of which
     most span the segment boundary (vecengine/index.go:144-233,
@@ -432,9 +432,10 @@ def test_config3_shape_1m_default_two_segments_vs_oracle(lx):
     ix.reset(w)
     br = ix.add_batch(d.creator, d.seq, d.poff, d.par, want_branches=True)
     st = ix.segment_stats()
-    assert st["segments"] == 2, st                        # the side-by-side form of the headline
-    cut = st["first_event"][1]
-    assert cut == N // 2 // 64 * 64 and st["partial"][1] > 0, st
+    assert st["segments"] == 3, st                        # the side-by-side form of the headline
+    cut, cut2 = st["first_event"][1], st["first_event"][2]
+    assert 0 < cut < cut2 < N and cut % 64 == 0 and cut2 % 64 == 0, st
+    assert st["partial"][1] > 0 and st["partial"][2] > 0, st
     assert np.array_equal(np.asarray(br, dtype=np.uint32), d.creator)   # fork-free: branch = creator
     o = corc.OracleIndex(w)
     assert o.add_batch(d.creator, d.seq, d.poff, d.par) == -1
@@ -443,16 +444,16 @@ def test_config3_shape_1m_default_two_segments_vs_oracle(lx):
         for (go, gb), (oo, ob) in _rows_in_chunks(ix, o, mode, ev, 50_000):
             np.testing.assert_array_equal(go, oo)
             assert np.array_equal(gb, ob), mode
-    # 1M pairs: half with a among the first 20k events of segment 1 and b up to
-    # 25k events before it (most of them in segment 0), half of the bench's
-    # shape (a uniform, b within 64 Lamport of a)
+    # 1M pairs: half with a among the first 20k events of segment 1 or 2 and b
+    # up to 25k events before it (most of them in the segment before), half of
+    # the bench's shape (a uniform, b within 64 Lamport of a)
     rng = np.random.default_rng(12)
-    qa1 = (cut + rng.integers(0, 20_000, 500_000)).astype(np.int64)
+    qa1 = (np.where(rng.integers(0, 2, 500_000) == 0, cut, cut2) + rng.integers(0, 20_000, 500_000)).astype(np.int64)
     qb1 = qa1 - rng.integers(1, 25_000, 500_000)
     qa2, qb2 = lx.tools.fc_queries(d.lamport, 500_000, window=64, seed=13)
     qa = np.concatenate([qa1, qa2]).astype(np.uint32)
     qb = np.concatenate([qb1, qb2]).astype(np.uint32)
-    assert int(((qa >= cut) & (qb < cut)).sum()) > 250_000
+    assert int((((qa >= cut) & (qb < cut)) | ((qa >= cut2) & (qb < cut2))).sum()) > 250_000
     got = ix.forkless_cause_batch(qa, qb)
     want = o.forkless_cause_batch_mt(qa, qb, 16)
     np.testing.assert_array_equal(got, want)
@@ -489,10 +490,10 @@ def _planes_equal_on_device(ixs, n, cols, chunk_rows=1 << 18):
 @pytest.mark.big_only
 def test_full_size_config3_segments_equal_single_walk(lx):
     """BASELINE configs[2] at full size (10M events, the bench workload): the
-    default handle (two side-by-side segments of 8-column slices) and a
+    default handle (three side-by-side segments of 12-column slices) and a
     seg_auto=0 handle (ONE 4-column walk of the batch) hold byte-identical
-    HighestBefore and LowestAfter planes, every row -- the half of the
-    shipped walk after event 5M included.  The single walk is the one pinned
+    HighestBefore and LowestAfter planes, every row -- the segments of the
+    shipped walk after the first included.  The single walk is the one pinned
     to the oracle at full size on its 500k prefix (above) and in every
     smaller configs[2]-shaped test."""
     V = 1000
@@ -506,7 +507,7 @@ def test_full_size_config3_segments_equal_single_walk(lx):
         ix.add_batch(d.creator, d.seq, d.poff, d.par)
         ix.sync()
         st = ix.segment_stats()
-        assert st["segments"] == (2 if auto else 0), st
+        assert st["segments"] == (3 if auto else 0), st
         ixs.append(ix)
     _planes_equal_on_device(ixs, N, V)
     qa, qb = lx.tools.fc_queries(d.lamport, 1 << 22, seed=21)

@@ -210,7 +210,7 @@ def _planes_equal(ix, ref, lo, hi, B, chunk=50_000):
 def test_native_row_segments_c3_shape_auto_sub(lx, fake, world):
     """The multi-GPU default at the headline shape (V = 1000, Zipf stakes, 10
     parents; 1M events here): every rank walks its segment as the side-by-side
-    sub-segments it picks on its own (seg_sub auto, 8-column slices, one
+    sub-segments it picks on its own (seg_sub auto, 12-column slices, one
     launch), and every own HB / LA row equals the single walk's byte for byte;
     ForklessCause of pairs across the rank boundaries equals the whole index's."""
     import torch
