@@ -67,8 +67,8 @@ const char *lx_last_error(const lx_index *h);
  * parity tests run each of them), so no setting changes an answer:
  *   "small_max"  largest host-pointer batch on the latency path (lx_small; 0 = never)
  *   "fc_fk"      0: ForklessCause on fork DAGs by the fix-up loop instead of the cheater-mask kernel
- *   "cpw"        walker columns per workgroup: 0 (auto), 1, 2, 4 or 8 (8: packed fork-free
- *                epochs, else 4)
+ *   "cpw"        walker columns per workgroup: 0 (auto), 1, 2, 4, 8 or 12 (8, 12: packed
+ *                fork-free epochs, else 4; 12: whole handles, a sharded one walks 8)
  *   "pack16"     0: two slot units per event even when every seq fits 16 bits
  *   "dbl"        0: the column walker also for fork-free batches of <= 16 branches
  *                (default: HighestBefore by frontier doubling in one workgroup, lx_dbl.hip)
