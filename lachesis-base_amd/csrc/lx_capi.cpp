@@ -496,7 +496,6 @@ uint32_t seg_pick(const lx_index *h, uint64_t n, uint32_t *cpw) {
     float best = 1.0f;   // one walk at the default width
     for (uint32_t c : {1u, 2u, 4u, 8u, 12u}) {
         if ((h->cpw_hint && c != h->cpw_hint) || (c >= 8 && !w8)) continue;
-        if (c == 12 && !h->cpw_hint && h->ncols <= 512) continue;   // few columns: 8-column slices already give >= 4 walks
         uint32_t G = std::min<uint32_t>(h->n_cus / walk_grid(h, c), kSegLaunchMax);
         while (G >= 2 && n < (uint64_t)G * kAutoSegEvents) G--;
         if (G >= 2 && kPass[c] / G < best) {
