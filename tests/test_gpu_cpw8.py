@@ -95,3 +95,27 @@ def test_cpw8_falls_back_with_forks(lx, cpw):
     for mode in (0, 1):
         assert np.array_equal(ix.rows_np(mode, ev)[1], o.rows(mode, ev)[1]), mode
     ix.close()
+
+
+@pytest.mark.parametrize("shape", [(600, 300, 8), (250, 700, 10)])
+def test_auto_12_column_segments_equal_single_walk(lx, shape):
+    """Default options on fork-free epochs whose width seg_pick walks as
+    side-by-side 12-column segments (V = 600: 50 slices, 5 walks; V = 250:
+    21 slices, many walks): planes byte-identical to one 4-column walk, and
+    a prefix of rows equal to the oracle."""
+    V, epv, P = shape
+    d = lx.tools.gen_dag(V, epv, P, seed=V)
+    w = [1 + (i * 7) % 11 for i in range(V)]
+    ixa, pa = planes_of(lx, d, w, {})
+    st = ixa.segment_stats()
+    assert st["segments"] >= 2 and st["one_launch"], st
+    ix1, p1 = planes_of(lx, d, w, {"seg_auto": 0, "cpw": 4})
+    np.testing.assert_array_equal(pa[0], p1[0])
+    np.testing.assert_array_equal(pa[1], p1[1])
+    o = corc.OracleIndex(w)
+    n = 20_000
+    assert o.add_batch(d.creator[:n], d.seq[:n], d.poff[:n + 1], d.par) == -1
+    ev = np.arange(0, n, 7, dtype=np.uint32)
+    assert np.array_equal(ixa.rows_np(0, ev)[1], o.rows(0, ev)[1])
+    ixa.close()
+    ix1.close()
