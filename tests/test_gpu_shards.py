@@ -60,10 +60,10 @@ def fc(lx, shards, qa, qb):
     return out.cpu().numpy()
 
 
-def sharded_fc(lx, d, weights, G, qa, qb):
+def sharded_fc(lx, d, weights, G, qa, qb, options=None):
     shards = []
     for r in range(G):
-        ix = lx.Index(shard_rank=r, shard_count=G)
+        ix = lx.Index(shard_rank=r, shard_count=G, options=options)
         ix.reset(weights)
         ix.add_batch(d.creator, d.seq, d.poff, d.par)
         shards.append(ix)
@@ -88,6 +88,21 @@ def test_sharded_fc_matches_oracle(G, shape):
     ranges = [shards[0].shard_range(r) for r in range(G)]
     assert ranges[0][0] == 0 and ranges[-1][1] == n
     assert all(ranges[i][1] == ranges[i + 1][0] for i in range(G - 1))
+
+
+@pytest.mark.parametrize("cpw", [8, 12])
+def test_sharded_wide_slices_fall_back(cpw):
+    """Option cpw 8 / 12 on column shards (their column lists are not the
+    identity: 12-column slices walk as 8) on a fork-free DAG whose seqs fit
+    16 bits: ForklessCause equals the oracle."""
+    import lachesis_hip as lx
+    d = lx.tools.gen_dag(40, 60, 6, 0, 0, 3)
+    weights = [1 + (i % 5) for i in range(40)]
+    o = corc.OracleIndex(weights)
+    assert o.add_batch(d.creator, d.seq, d.poff, d.par) == -1
+    qa, qb = lx.tools.fc_queries(d.lamport, 50_000, window=24, seed=3)
+    got, _ = sharded_fc(lx, d, weights, 3, qa, qb, options={"cpw": cpw, "small_max": 0, "dbl": 0})
+    np.testing.assert_array_equal(got, o.forkless_cause_batch(qa, qb))
 
 
 @pytest.mark.parametrize("force", [None, "4"])
