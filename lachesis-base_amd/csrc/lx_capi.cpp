@@ -872,6 +872,23 @@ int lx_fc_args(lx_index *h, uint64_t n, const uint32_t *a, const uint32_t *b, ui
     f.own_hi = h->own_hi;
     f.branch_creator = h->branch_creator;
     f.status = h->status;
+    // early exit for k_fc (fork-free, whole rows): when the heaviest 256
+    // columns can reach the quorum alone, their count decides most queries
+    if (!partial && !h->sharded() && h->B == h->V && h->fc_early && f.vhi4 - f.vlo4 > 64) {
+        uint64_t w0 = 0, wt = 0;
+        for (uint32_t c = f.vlo4 * 4; c < h->V && c < f.vhi4 * 4; c++) {
+            wt += h->weights[c];
+            if (c < f.vlo4 * 4 + 256) w0 += h->weights[c];
+        }
+        if (w0 >= h->quorum && wt - w0 <= 0xFFFFFFFFull) {
+            if (!h->d_fc_full && hipMalloc((void **)&h->d_fc_full, 8) == hipSuccess)
+                (void)hipMemsetAsync(h->d_fc_full, 0, 8, h->stream);
+            f.early = 1;
+            f.early_rest = (uint32_t)(wt - w0);
+            f.early_full = h->d_fc_full;
+            h->fc_early_q += n;
+        }
+    }
     h->fc_unchecked = true;   // a query it cannot answer flags status[1]; lx_sync reports it
     *fa = f;
     return 0;
@@ -1698,11 +1715,27 @@ void lx_destroy(lx_index *h) {
         if (p) (void)hipFree(p);
     if (h->qp) (void)hipHostFree(h->qp);
     if (h->ld_buf) (void)hipFree(h->ld_buf);
+    if (h->d_fc_full) (void)hipFree(h->d_fc_full);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
 }
 
 const char *lx_last_error(const lx_index *h) { return h ? h->err.c_str() : "null handle"; }
+
+int lx_fc_early_counters(lx_index *h, uint64_t *queries, uint64_t *full_rows) {
+    if (!h || !queries || !full_rows) return LX_ERR_ARG;
+    HIPCHK(h, set_dev(h->device));
+    uint64_t full = 0;
+    if (h->d_fc_full) {
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        HIPCHK(h, hipMemcpy(&full, h->d_fc_full, 8, hipMemcpyDeviceToHost));
+        HIPCHK(h, hipMemset(h->d_fc_full, 0, 8));
+    }
+    *queries = h->fc_early_q;
+    *full_rows = full;
+    h->fc_early_q = 0;
+    return 0;
+}
 
 int lx_set_option(lx_index *h, const char *name, int64_t value) {
     if (!h || !name) return LX_ERR_ARG;
@@ -1712,6 +1745,8 @@ int lx_set_option(lx_index *h, const char *name, int64_t value) {
         h->small_max = (uint32_t)std::min<int64_t>(value, kSmallMaxN);
     } else if (k == "fc_fk") {
         h->fc_fk = value != 0;
+    } else if (k == "fc_early") {
+        h->fc_early = value != 0;
     } else if (k == "cpw") {
         if (value != 0 && value != 1 && value != 2 && value != 4 && value != 8 && value != 12)
             return h->fail(LX_ERR_ARG, "cpw must be 0, 1, 2, 4, 8 or 12 (8, 12: fork-free epochs with seqs <= 0xFFFF)");

@@ -259,6 +259,9 @@ struct lx_index {
     bool fcc_slots_set = false;            // set by the option (else sized at lx_reset from V)
     // segmented walk (option segments, lx_segment.hip): scratch and timings of the last batch
     uint32_t segments = 0;
+    bool fc_early = true;                  // option fc_early=0: k_fc always reads whole rows
+    unsigned long long *d_fc_full = nullptr;   // early exit: queries that read whole rows (device)
+    uint64_t fc_early_q = 0;               // queries launched with the early exit
     bool seg_auto = true;                  // option seg_auto=0: never split a batch on its own
     uint32_t n_cus = 256;                  // compute units of the device (auto segments)
     uint32_t *seg_jt = nullptr, *seg_cnt = nullptr, *seg_mf = nullptr, *seg_plist = nullptr, *seg_elist = nullptr;

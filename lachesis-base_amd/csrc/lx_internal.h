@@ -155,6 +155,13 @@ struct FcArgs {
     const uint32_t *wpad;        // weight per column (0 outside [vlo, vhi) originals)
     uint32_t vlo4, vhi4;         // column range in uint4 units
     uint32_t quorum;
+    // early exit (k_fc, fork-free, 64 lanes per query; 0 = off): the weight
+    // of the columns outside the first 256 of the range.  The first 256
+    // columns are the heaviest validators (pos.Validators idx order), so
+    // their count alone often decides the quorum either way
+    uint32_t early_rest;
+    uint32_t early;
+    unsigned long long *early_full;   // += queries that read the rest of their rows
     const uint32_t *ev_branch;
     const uint32_t *ev_creator;  // creator per event (= creator of its branch)
     // cheaters of this shard: CSR over all their branches (first = original)

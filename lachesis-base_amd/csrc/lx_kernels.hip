@@ -1387,6 +1387,7 @@ __global__ __launch_bounds__(256) void k_fc(FcArgs a) {
         const uint32_t i = lane + t * LPQ;
         wr[t] = i < nv ? wv[i] : make_uint4(0, 0, 0, 0);
     }
+    uint32_t n_full = 0;   // early exit: queries of this lane group that read whole rows
     for (uint64_t q = blockIdx.x * qpb + threadIdx.x / LPQ; q < a.n; q += (uint64_t)gridDim.x * qpb) {
         uint32_t A = a.qa[a.qa_bcast ? 0 : q], Bq = a.qb[q];
         const bool bad = fc_bad(a, A, Bq);
@@ -1399,6 +1400,41 @@ __global__ __launch_bounds__(256) void k_fc(FcArgs a) {
         }
         const uint4 *ha = reinterpret_cast<const uint4 *>(a.hb + (uint64_t)A * a.stride) + a.vlo4;
         const uint4 *lb = reinterpret_cast<const uint4 *>(a.la + (uint64_t)Bq * a.stride) + a.vlo4;
+        if constexpr (!FORKS && LPQ == 64) {
+            if (a.early) {
+                // the heaviest 256 columns first; the rest of both rows only
+                // when their count leaves the quorum open (same answer: the
+                // sum is only compared with the quorum)
+                const uint32_t i0 = min((uint32_t)lane, nv ? nv - 1u : 0u);
+                const u4v hv = __builtin_nontemporal_load(reinterpret_cast<const u4v *>(ha + i0));
+                const u4v lv = __builtin_nontemporal_load(reinterpret_cast<const u4v *>(lb + i0));
+                uint32_t s0 = fc_term(lv.x, hv.x, wr[0].x, false) + fc_term(lv.y, hv.y, wr[0].y, false) +
+                              fc_term(lv.z, hv.z, wr[0].z, false) + fc_term(lv.w, hv.w, wr[0].w, false);
+#pragma unroll
+                for (int off = 32; off > 0; off >>= 1) s0 += __shfl_xor(s0, off, 64);
+                uint32_t sum = s0;
+                if (s0 < a.quorum && s0 + a.early_rest >= a.quorum) {
+                    uint32_t s1 = 0;
+                    for (uint32_t i = lane + 64; i < nv; i += 64) {
+                        const u4v hh = __builtin_nontemporal_load(reinterpret_cast<const u4v *>(ha + i));
+                        const u4v ll = __builtin_nontemporal_load(reinterpret_cast<const u4v *>(lb + i));
+                        const uint4 w = wv[i];
+                        s1 += fc_term(ll.x, hh.x, w.x, false) + fc_term(ll.y, hh.y, w.y, false) +
+                              fc_term(ll.z, hh.z, w.z, false) + fc_term(ll.w, hh.w, w.w, false);
+                    }
+#pragma unroll
+                    for (int off = 32; off > 0; off >>= 1) s1 += __shfl_xor(s1, off, 64);
+                    sum += s1;
+                    n_full++;
+                }
+                if (lane == 0) {
+                    const uint8_t r = bad ? 0xFF : (uint8_t)(sum >= a.quorum);
+                    a.out[q] = a.out_tag && !bad ? (uint8_t)(a.out_tag[q] << 1 | r) : r;
+                    if (bad) atomicOr(&a.status[1], 1u);
+                }
+                continue;
+            }
+        }
         uint4 h[kR], l[kR];
 #pragma unroll
         for (int t = 0; t < kR; t++) {
@@ -1463,6 +1499,8 @@ __global__ __launch_bounds__(256) void k_fc(FcArgs a) {
             if (bad) atomicOr(&a.status[1], 1u);
         }
     }
+    if (!FORKS && LPQ == 64 && a.early && a.early_full && lane == 0 && n_full)
+        atomicAdd(a.early_full, (unsigned long long)n_full);
 }
 
 // Fork DAGs (few cheaters): every plane column is streamed -- originals and
