@@ -690,7 +690,7 @@ def main():
     fc_kernel_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
     # k_fc's early exit (option fc_early): queries decided
     # by the 256 heaviest columns read 2 x 1 KB, the others both whole rows
-    fc_early_q, fc_full_q = ix.fc_early_counters() if not (shard or solo or rowseg) else (0, 0)
+    fc_early_q, fc_second_q, fc_full_q = ix.fc_early_counters() if not (shard or solo or rowseg) else (0, 0, 0)
 
     # correctness spot check: this run's first 4096 ForklessCause answers
     # recomputed on the host from the index's own HighestBefore / LowestAfter
@@ -721,15 +721,16 @@ def main():
         lo, hi = ix.shard_range(rank)
         B = hi - lo                         # columns this rank streams (no forks in the bench DAG)
     fc_bytes = 8.0 * B * args.fc_queries                       # HB(a).Seq 4B + LA(b) 4B per branch
-    # bytes k_fc reads per launch: whole rows (2 x 4 B per branch, the row's
-    # uint4 groups) for every query without the early exit or past it, the
-    # 256 heaviest columns of both rows (2 x 64 lanes x 16 B) for the others
+    # bytes k_fc reads per launch: whole rows (8 B per branch) without the
+    # early exit; with it 2 x 1 KB (the 256 heaviest columns of both rows) per
+    # query, 2 x 1 KB more past the first round, the rest of both rows
+    # (2 x (row - 2 KB)) past the second
     fc_read = fc_bytes
     if fc_early_q:
         row16 = ((B + 3) // 4) * 16
         ef = min(1.0, fc_early_q / (args.fc_queries * args.steps))   # queries launched with the early exit
-        ff = fc_full_q / fc_early_q                                  # of those, read whole rows
-        fc_read = args.fc_queries * (ef * (2 * 1024 * (1 - ff) + 2 * row16 * ff) + (1 - ef) * 8.0 * B)
+        f2, fw = fc_second_q / fc_early_q, fc_full_q / fc_early_q
+        fc_read = args.fc_queries * (ef * (2048 + 2048 * f2 + 2 * max(0, row16 - 2048) * fw) + (1 - ef) * 8.0 * B)
     fc_achieved = fc_read / (fc_kernel_ms * 1e-3) / 1e9
     kidx = float(np.mean(k_index_ms))
     # index algorithmic bytes/event: (P+1)*4*B parent+own HB + 4*B LA + 8 B metadata
@@ -779,8 +780,9 @@ def main():
         "roofline": {"bound": "hbm", "kernel": "k_fc (ForklessCause)", "achieved": fc_achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": fc_achieved / HBM_PEAK_GBS,
                      "bytes_read_per_launch": fc_read,
-                     "early_exit": {"queries": fc_early_q, "full_rows": fc_full_q,
-                                    "note": "queries the 256 heaviest validators' columns decide read 2 x 1 KB; "
+                     "early_exit": {"queries": fc_early_q, "second_round": fc_second_q, "whole_rows": fc_full_q,
+                                    "note": "queries the 256 heaviest validators' columns decide read 2 x 1 KB, "
+                                            "the next 256 columns 2 x 1 KB more, the rest only past both; "
                                             "achieved = bytes_read_per_launch / kernel time; "
                                             "algorithmic_bytes_per_launch is SURVEY 8d's whole-row figure"} if fc_early_q else None,
                      "traffic": traffic["k_fc"]["hbm_bytes"] if traffic and "k_fc" in traffic else None,

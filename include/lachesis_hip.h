@@ -69,7 +69,7 @@ const char *lx_last_error(const lx_index *h);
  *   "fc_fk"      0: ForklessCause on fork DAGs by the fix-up loop instead of the cheater-mask kernel
  *   "fc_early"   0: batched ForklessCause always reads whole rows (default 1: on fork-free
  *                epochs where the 256 heaviest validators' stake alone can reach the quorum,
- *                a query reads the rest of its rows only when their count leaves it open;
+ *                a query reads more of its rows only while their count leaves it open;
  *                lx_fc_early_counters)
  *   "cpw"        walker columns per workgroup: 0 (auto), 1, 2, 4, 8 or 12 (8, 12: packed
  *                fork-free epochs, else 4; 12: whole handles, a sharded one walks 8)
@@ -215,10 +215,11 @@ typedef struct lx_fc_stats {
 int lx_fc_cache_stats(const lx_index *h, lx_fc_stats *out);
 
 /* Batched ForklessCause's early exit (option fc_early) since the last call:
- * queries launched with it, and how many of them read the rest of their rows
- * (the others read 2 x 1 KB: the 256 heaviest columns of HB(a) and LA(b)).
- * Synchronizes the handle's stream; resets both counts.  Diagnostics (bench). */
-int lx_fc_early_counters(lx_index *h, uint64_t *queries, uint64_t *full_rows);
+ * queries launched with it; of them, how many read a second round (columns
+ * 256-511 of HB(a) and LA(b), 2 x 1 KB more) and how many read the rest of
+ * both rows (the others read 2 x 1 KB: the 256 heaviest columns).
+ * Synchronizes the handle's stream; resets the counts.  Diagnostics (bench). */
+int lx_fc_early_counters(lx_index *h, uint64_t *queries, uint64_t *second_round, uint64_t *whole_rows);
 
 /* Column-sharded partial: stake sum over this shard's creators, plus
  * 0x80000000 when this shard owns branch(b) and A observes it as forked.

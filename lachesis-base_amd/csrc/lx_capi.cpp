@@ -875,16 +875,18 @@ int lx_fc_args(lx_index *h, uint64_t n, const uint32_t *a, const uint32_t *b, ui
     // early exit for k_fc (fork-free, whole rows): when the heaviest 256
     // columns can reach the quorum alone, their count decides most queries
     if (!partial && !h->sharded() && h->B == h->V && h->fc_early && f.vhi4 - f.vlo4 > 64) {
-        uint64_t w0 = 0, wt = 0;
+        uint64_t w0 = 0, w1 = 0, wt = 0;
         for (uint32_t c = f.vlo4 * 4; c < h->V && c < f.vhi4 * 4; c++) {
             wt += h->weights[c];
             if (c < f.vlo4 * 4 + 256) w0 += h->weights[c];
+            else if (c < f.vlo4 * 4 + 512) w1 += h->weights[c];
         }
         if (w0 >= h->quorum && wt - w0 <= 0xFFFFFFFFull) {
-            if (!h->d_fc_full && hipMalloc((void **)&h->d_fc_full, 8) == hipSuccess)
-                (void)hipMemsetAsync(h->d_fc_full, 0, 8, h->stream);
+            if (!h->d_fc_full && hipMalloc((void **)&h->d_fc_full, 16) == hipSuccess)
+                (void)hipMemsetAsync(h->d_fc_full, 0, 16, h->stream);
             f.early = 1;
             f.early_rest = (uint32_t)(wt - w0);
+            f.early_rest2 = (uint32_t)(wt - w0 - w1);
             f.early_full = h->d_fc_full;
             h->fc_early_q += n;
         }
@@ -1722,17 +1724,18 @@ void lx_destroy(lx_index *h) {
 
 const char *lx_last_error(const lx_index *h) { return h ? h->err.c_str() : "null handle"; }
 
-int lx_fc_early_counters(lx_index *h, uint64_t *queries, uint64_t *full_rows) {
-    if (!h || !queries || !full_rows) return LX_ERR_ARG;
+int lx_fc_early_counters(lx_index *h, uint64_t *queries, uint64_t *second_round, uint64_t *whole_rows) {
+    if (!h || !queries || !second_round || !whole_rows) return LX_ERR_ARG;
     HIPCHK(h, set_dev(h->device));
-    uint64_t full = 0;
+    uint64_t c[2] = {0, 0};
     if (h->d_fc_full) {
         HIPCHK(h, hipStreamSynchronize(h->stream));
-        HIPCHK(h, hipMemcpy(&full, h->d_fc_full, 8, hipMemcpyDeviceToHost));
-        HIPCHK(h, hipMemset(h->d_fc_full, 0, 8));
+        HIPCHK(h, hipMemcpy(c, h->d_fc_full, 16, hipMemcpyDeviceToHost));
+        HIPCHK(h, hipMemset(h->d_fc_full, 0, 16));
     }
     *queries = h->fc_early_q;
-    *full_rows = full;
+    *second_round = c[0];
+    *whole_rows = c[1];
     h->fc_early_q = 0;
     return 0;
 }

@@ -160,8 +160,9 @@ struct FcArgs {
     // columns are the heaviest validators (pos.Validators idx order), so
     // their count alone often decides the quorum either way
     uint32_t early_rest;
+    uint32_t early_rest2;        // the weight past the first 512 columns
     uint32_t early;
-    unsigned long long *early_full;   // += queries that read the rest of their rows
+    unsigned long long *early_full;   // [0] += queries past the first round, [1] += past the second
     const uint32_t *ev_branch;
     const uint32_t *ev_creator;  // creator per event (= creator of its branch)
     // cheaters of this shard: CSR over all their branches (first = original)

@@ -1387,7 +1387,83 @@ __global__ __launch_bounds__(256) void k_fc(FcArgs a) {
         const uint32_t i = lane + t * LPQ;
         wr[t] = i < nv ? wv[i] : make_uint4(0, 0, 0, 0);
     }
-    uint32_t n_full = 0;   // early exit: queries of this lane group that read whole rows
+    uint32_t n_full = 0, n_rest = 0;   // early exit: queries past the first round / past the second
+    if constexpr (!FORKS && LPQ == 64) {
+        if (a.early) {
+            // the heaviest 256 columns first (lane i: uint4 i of both rows); the
+            // rest of both rows only when their count leaves the quorum open
+            // (same answer: the sum is only compared with the quorum).  The
+            // next query's first round is in flight while this one is decided.
+            const uint64_t step = (uint64_t)gridDim.x * qpb;
+            uint64_t q = blockIdx.x * qpb + threadIdx.x / LPQ;
+            uint32_t A = 0, Bq = 0;
+            bool bad = false;
+            u4v hv = {0, 0, 0, 0}, lv = {0, 0, 0, 0};
+            auto first = [&](uint64_t qq, uint32_t &A_, uint32_t &B_, bool &bad_, u4v &h_, u4v &l_) {
+                A_ = a.qa[a.qa_bcast ? 0 : qq];
+                B_ = a.qb[qq];
+                bad_ = fc_bad(a, A_, B_);
+                if (bad_) { A_ = 0; B_ = 0; }
+                h_ = __builtin_nontemporal_load(reinterpret_cast<const u4v *>(a.hb + (uint64_t)A_ * a.stride) + a.vlo4 + lane);
+                l_ = __builtin_nontemporal_load(reinterpret_cast<const u4v *>(a.la + (uint64_t)B_ * a.stride) + a.vlo4 + lane);
+            };
+            if (q < a.n) first(q, A, Bq, bad, hv, lv);
+            for (; q < a.n; q += step) {
+                uint32_t An = 0, Bn = 0;
+                bool badn = false;
+                u4v hn = {0, 0, 0, 0}, ln = {0, 0, 0, 0};
+                if (q + step < a.n) first(q + step, An, Bn, badn, hn, ln);
+                uint32_t s0 = fc_term(lv.x, hv.x, wr[0].x, false) + fc_term(lv.y, hv.y, wr[0].y, false) +
+                              fc_term(lv.z, hv.z, wr[0].z, false) + fc_term(lv.w, hv.w, wr[0].w, false);
+#pragma unroll
+                for (int off = 32; off > 0; off >>= 1) s0 += __shfl_xor(s0, off, 64);
+                uint32_t sum = s0;
+                if (s0 < a.quorum && s0 + a.early_rest >= a.quorum) {
+                    const uint4 *ha = reinterpret_cast<const uint4 *>(a.hb + (uint64_t)A * a.stride) + a.vlo4;
+                    const uint4 *lb = reinterpret_cast<const uint4 *>(a.la + (uint64_t)Bq * a.stride) + a.vlo4;
+                    // second round (columns 256-511), then the same test once more
+                    uint32_t s1 = 0;
+                    if (lane + 64 < nv) {
+                        const u4v hh = __builtin_nontemporal_load(reinterpret_cast<const u4v *>(ha + lane + 64));
+                        const u4v ll = __builtin_nontemporal_load(reinterpret_cast<const u4v *>(lb + lane + 64));
+                        s1 = fc_term(ll.x, hh.x, wr[1].x, false) + fc_term(ll.y, hh.y, wr[1].y, false) +
+                             fc_term(ll.z, hh.z, wr[1].z, false) + fc_term(ll.w, hh.w, wr[1].w, false);
+                    }
+#pragma unroll
+                    for (int off = 32; off > 0; off >>= 1) s1 += __shfl_xor(s1, off, 64);
+                    sum += s1;
+                    n_full++;
+                }
+                if (sum < a.quorum && sum + a.early_rest2 >= a.quorum && s0 < a.quorum && s0 + a.early_rest >= a.quorum) {
+                    const uint4 *ha = reinterpret_cast<const uint4 *>(a.hb + (uint64_t)A * a.stride) + a.vlo4;
+                    const uint4 *lb = reinterpret_cast<const uint4 *>(a.la + (uint64_t)Bq * a.stride) + a.vlo4;
+                    uint32_t s1 = 0;
+                    n_rest++;
+                    for (uint32_t i = lane + 128; i < nv; i += 64) {
+                        const u4v hh = __builtin_nontemporal_load(reinterpret_cast<const u4v *>(ha + i));
+                        const u4v ll = __builtin_nontemporal_load(reinterpret_cast<const u4v *>(lb + i));
+                        const uint4 w = wv[i];
+                        s1 += fc_term(ll.x, hh.x, w.x, false) + fc_term(ll.y, hh.y, w.y, false) +
+                              fc_term(ll.z, hh.z, w.z, false) + fc_term(ll.w, hh.w, w.w, false);
+                    }
+#pragma unroll
+                    for (int off = 32; off > 0; off >>= 1) s1 += __shfl_xor(s1, off, 64);
+                    sum += s1;
+                }
+                if (lane == 0) {
+                    const uint8_t r = bad ? 0xFF : (uint8_t)(sum >= a.quorum);
+                    a.out[q] = a.out_tag && !bad ? (uint8_t)(a.out_tag[q] << 1 | r) : r;
+                    if (bad) atomicOr(&a.status[1], 1u);
+                }
+                A = An; Bq = Bn; bad = badn; hv = hn; lv = ln;
+            }
+            if (a.early_full && lane == 0 && n_full) {
+                atomicAdd(a.early_full, (unsigned long long)n_full);
+                if (n_rest) atomicAdd(a.early_full + 1, (unsigned long long)n_rest);
+            }
+            return;
+        }
+    }
     for (uint64_t q = blockIdx.x * qpb + threadIdx.x / LPQ; q < a.n; q += (uint64_t)gridDim.x * qpb) {
         uint32_t A = a.qa[a.qa_bcast ? 0 : q], Bq = a.qb[q];
         const bool bad = fc_bad(a, A, Bq);
@@ -1400,41 +1476,6 @@ __global__ __launch_bounds__(256) void k_fc(FcArgs a) {
         }
         const uint4 *ha = reinterpret_cast<const uint4 *>(a.hb + (uint64_t)A * a.stride) + a.vlo4;
         const uint4 *lb = reinterpret_cast<const uint4 *>(a.la + (uint64_t)Bq * a.stride) + a.vlo4;
-        if constexpr (!FORKS && LPQ == 64) {
-            if (a.early) {
-                // the heaviest 256 columns first; the rest of both rows only
-                // when their count leaves the quorum open (same answer: the
-                // sum is only compared with the quorum)
-                const uint32_t i0 = min((uint32_t)lane, nv ? nv - 1u : 0u);
-                const u4v hv = __builtin_nontemporal_load(reinterpret_cast<const u4v *>(ha + i0));
-                const u4v lv = __builtin_nontemporal_load(reinterpret_cast<const u4v *>(lb + i0));
-                uint32_t s0 = fc_term(lv.x, hv.x, wr[0].x, false) + fc_term(lv.y, hv.y, wr[0].y, false) +
-                              fc_term(lv.z, hv.z, wr[0].z, false) + fc_term(lv.w, hv.w, wr[0].w, false);
-#pragma unroll
-                for (int off = 32; off > 0; off >>= 1) s0 += __shfl_xor(s0, off, 64);
-                uint32_t sum = s0;
-                if (s0 < a.quorum && s0 + a.early_rest >= a.quorum) {
-                    uint32_t s1 = 0;
-                    for (uint32_t i = lane + 64; i < nv; i += 64) {
-                        const u4v hh = __builtin_nontemporal_load(reinterpret_cast<const u4v *>(ha + i));
-                        const u4v ll = __builtin_nontemporal_load(reinterpret_cast<const u4v *>(lb + i));
-                        const uint4 w = wv[i];
-                        s1 += fc_term(ll.x, hh.x, w.x, false) + fc_term(ll.y, hh.y, w.y, false) +
-                              fc_term(ll.z, hh.z, w.z, false) + fc_term(ll.w, hh.w, w.w, false);
-                    }
-#pragma unroll
-                    for (int off = 32; off > 0; off >>= 1) s1 += __shfl_xor(s1, off, 64);
-                    sum += s1;
-                    n_full++;
-                }
-                if (lane == 0) {
-                    const uint8_t r = bad ? 0xFF : (uint8_t)(sum >= a.quorum);
-                    a.out[q] = a.out_tag && !bad ? (uint8_t)(a.out_tag[q] << 1 | r) : r;
-                    if (bad) atomicOr(&a.status[1], 1u);
-                }
-                continue;
-            }
-        }
         uint4 h[kR], l[kR];
 #pragma unroll
         for (int t = 0; t < kR; t++) {
@@ -1499,8 +1540,6 @@ __global__ __launch_bounds__(256) void k_fc(FcArgs a) {
             if (bad) atomicOr(&a.status[1], 1u);
         }
     }
-    if (!FORKS && LPQ == 64 && a.early && a.early_full && lane == 0 && n_full)
-        atomicAdd(a.early_full, (unsigned long long)n_full);
 }
 
 // Fork DAGs (few cheaters): every plane column is streamed -- originals and

@@ -37,7 +37,8 @@ SIGNATURES = [
     ("lx_forkless_cause", ctypes.c_int, [vp, ctypes.c_uint32, ctypes.c_uint32, u8p]),
     ("lx_fc_cache_stats", ctypes.c_int, [vp, vp]),
     ("lx_forkless_cause_batch_dev", ctypes.c_int, [vp, ctypes.c_uint64, vp, vp, vp, vp]),
-    ("lx_fc_early_counters", ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
+    ("lx_fc_early_counters", ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
+                                            ctypes.POINTER(ctypes.c_uint64)]),
     ("lx_forkless_cause_partial_dev", ctypes.c_int, [vp, ctypes.c_uint64, vp, vp, vp, vp]),
     ("lx_fc_combine_dev", ctypes.c_int, [vp, ctypes.c_uint64, vp, vp, vp]),
     ("lx_quorum", ctypes.c_uint32, [vp]),
@@ -359,10 +360,11 @@ class Index:
         self._chk(self.L.lx_forkless_cause_batch_dev(self.h, n, a_ptr, b_ptr, out_ptr, stream))
 
     def fc_early_counters(self):
-        """(queries launched with the early exit, queries that read whole rows) since the last call."""
-        q, f = ctypes.c_uint64(0), ctypes.c_uint64(0)
-        self._chk(self.L.lx_fc_early_counters(self.h, ctypes.byref(q), ctypes.byref(f)))
-        return q.value, f.value
+        """(queries launched with the early exit, of them past the first round,
+        past the second: whole rows) since the last call."""
+        q, f2, fw = ctypes.c_uint64(0), ctypes.c_uint64(0), ctypes.c_uint64(0)
+        self._chk(self.L.lx_fc_early_counters(self.h, ctypes.byref(q), ctypes.byref(f2), ctypes.byref(fw)))
+        return q.value, f2.value, fw.value
 
     def forkless_cause_partial_dev(self, n, a_ptr, b_ptr, partial_ptr, stream=None):
         self._chk(self.L.lx_forkless_cause_partial_dev(self.h, n, a_ptr, b_ptr, partial_ptr, stream))
