@@ -882,8 +882,12 @@ int lx_fc_args(lx_index *h, uint64_t n, const uint32_t *a, const uint32_t *b, ui
             else if (c < f.vlo4 * 4 + 512) w1 += h->weights[c];
         }
         if (w0 >= h->quorum && wt - w0 <= 0xFFFFFFFFull) {
-            if (!h->d_fc_full && hipMalloc((void **)&h->d_fc_full, 16) == hipSuccess)
-                (void)hipMemsetAsync(h->d_fc_full, 0, 16, h->stream);
+            // (zeroed before any launch can count into it, whatever stream runs it)
+            if (!h->d_fc_full && hipMalloc((void **)&h->d_fc_full, 16) == hipSuccess &&
+                hipMemset(h->d_fc_full, 0, 16) != hipSuccess) {
+                (void)hipFree(h->d_fc_full);
+                h->d_fc_full = nullptr;
+            }
             f.early = 1;
             f.early_rest = (uint32_t)(wt - w0);
             f.early_rest2 = (uint32_t)(wt - w0 - w1);
