@@ -215,7 +215,9 @@ typedef struct lx_fc_stats {
 int lx_fc_cache_stats(const lx_index *h, lx_fc_stats *out);
 
 /* Batched ForklessCause's early exit (option fc_early) since the last call:
- * queries launched with it; of them, how many read a second round (columns
+ * queries the kernel decided on its early path (device count; the path runs
+ * on fork-free epochs whose rows exceed 512 columns and whose 256 heaviest
+ * validators can reach the quorum alone); of them, how many read a second round (columns
  * 256-511 of HB(a) and LA(b), 2 x 1 KB more) and how many read the rest of
  * both rows (the others read 2 x 1 KB: the 256 heaviest columns).
  * Synchronizes the handle's stream; resets the counts.  Diagnostics (bench). */
@@ -240,10 +242,17 @@ int lx_get_merged_highest_before(lx_index *h, uint32_t ev, uint8_t *out, uint32_
  * (the row server) when the handle's stream is idle: no launch per call, the
  * row and a completion tag land in pinned memory.  It leaves after 250 us
  * without a request (and after 0.5 s in all), so a device-wide synchronization
- * right after a getter may wait that long; option get_server = 0 turns it off
- * (every call launches).  out[0] rows it served, out[1] its launches, out[2]
- * single-row calls that launched instead (stream busy or option off). */
+ * right after a getter may wait that long.  While resident it holds one of
+ * the process's hardware queues (GPU_MAX_HW_QUEUES, 4 by default): with more
+ * streams than queues, work on a stream sharing its queue would wait for its
+ * idle exit.  Option get_server: 1 (default) uses it only while the handle is
+ * the process's only one (lx_live_handles), 2 always, 0 never (every call
+ * launches).  Either way the kernel refuses an event outside the handle's
+ * rows by itself (LX_ERR_ARG), whatever the request word names.  out[0] rows
+ * it served, out[1] its launches, out[2] single-row calls that launched
+ * instead (stream busy, option off, other handles alive). */
 int lx_get_server_stats(const lx_index *h, uint64_t out[3]);
+int lx_live_handles(void);   /* index handles created and not destroyed in this process */
 /* The same for n events in one call (applyAtropos, abft/lachesis.go:57, and the
  * emitter's candidate loops call GetMergedHighestBefore per event): row i is
  * written at out + off[i], off has n+1 entries (byte offsets, always filled);

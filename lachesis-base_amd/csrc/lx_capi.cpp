@@ -45,6 +45,9 @@ extern "C" void lx_host_prof(uint64_t out[16], int reset) {
         if ((h)->rowseg()) return (h)->fail(LX_ERR_STATE, "needs a whole index (a row-segment rank holds its own rows)"); \
     } while (0)
 
+// index handles alive in this process (the row server's option get_server = 1)
+static std::atomic<int> g_live_handles{0};
+
 namespace {
 
 void free_wb(lx_index *h) {
@@ -874,7 +877,9 @@ int lx_fc_args(lx_index *h, uint64_t n, const uint32_t *a, const uint32_t *b, ui
     f.status = h->status;
     // early exit for k_fc (fork-free, whole rows): when the heaviest 256
     // columns can reach the quorum alone, their count decides most queries
-    if (!partial && !h->sharded() && h->B == h->V && h->fc_early && f.vhi4 - f.vlo4 > 64) {
+    // (launch_fc gives rows of more than 128 uint4 64 lanes per query, the only
+    // width whose kernel has the early path: the gate matches what runs)
+    if (!partial && !h->sharded() && h->B == h->V && h->fc_early && f.vhi4 - f.vlo4 > 128) {
         uint64_t w0 = 0, w1 = 0, wt = 0;
         for (uint32_t c = f.vlo4 * 4; c < h->V && c < f.vhi4 * 4; c++) {
             wt += h->weights[c];
@@ -882,17 +887,23 @@ int lx_fc_args(lx_index *h, uint64_t n, const uint32_t *a, const uint32_t *b, ui
             else if (c < f.vlo4 * 4 + 512) w1 += h->weights[c];
         }
         if (w0 >= h->quorum && wt - w0 <= 0xFFFFFFFFull) {
-            // (zeroed before any launch can count into it, whatever stream runs it)
-            if (!h->d_fc_full && hipMalloc((void **)&h->d_fc_full, 16) == hipSuccess &&
-                hipMemset(h->d_fc_full, 0, 16) != hipSuccess) {
-                (void)hipFree(h->d_fc_full);
-                h->d_fc_full = nullptr;
+            if (!h->d_fc_full) {
+                // zeroed and synchronized before any launch can count into it,
+                // whatever stream runs that launch
+                unsigned long long *p = nullptr;
+                HIPCHK(h, hipMalloc((void **)&p, 32));
+                hipError_t e = hipMemsetAsync(p, 0, 32, h->stream);
+                if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+                if (e != hipSuccess) {
+                    (void)hipFree(p);
+                    return h->hip(e, "ForklessCause early-exit counters");
+                }
+                h->d_fc_full = p;
             }
             f.early = 1;
             f.early_rest = (uint32_t)(wt - w0);
             f.early_rest2 = (uint32_t)(wt - w0 - w1);
             f.early_full = h->d_fc_full;
-            h->fc_early_q += n;
         }
     }
     h->fc_unchecked = true;   // a query it cannot answer flags status[1]; lx_sync reports it
@@ -1696,12 +1707,14 @@ int lx_create(const lx_config *cfg, lx_index **out) {
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device) == hipSuccess && cus > 0)
             h->n_cus = (uint32_t)cus;
     }
+    g_live_handles.fetch_add(1, std::memory_order_relaxed);
     *out = h;
     return 0;
 }
 
 void lx_destroy(lx_index *h) {
     if (!h) return;
+    g_live_handles.fetch_sub(1, std::memory_order_relaxed);
     (void)hipSetDevice(h->device);
     srv_stop(h);
     if (h->srv_stream) (void)hipStreamDestroy(h->srv_stream);
@@ -1731,16 +1744,16 @@ const char *lx_last_error(const lx_index *h) { return h ? h->err.c_str() : "null
 int lx_fc_early_counters(lx_index *h, uint64_t *queries, uint64_t *second_round, uint64_t *whole_rows) {
     if (!h || !queries || !second_round || !whole_rows) return LX_ERR_ARG;
     HIPCHK(h, set_dev(h->device));
-    uint64_t c[2] = {0, 0};
+    uint64_t c[3] = {0, 0, 0};
     if (h->d_fc_full) {
         HIPCHK(h, hipStreamSynchronize(h->stream));
-        HIPCHK(h, hipMemcpy(c, h->d_fc_full, 16, hipMemcpyDeviceToHost));
-        HIPCHK(h, hipMemset(h->d_fc_full, 0, 16));
+        HIPCHK(h, hipMemcpy(c, h->d_fc_full, 24, hipMemcpyDeviceToHost));
+        HIPCHK(h, hipMemsetAsync(h->d_fc_full, 0, 24, h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
     }
-    *queries = h->fc_early_q;
+    *queries = c[2];   // queries the kernel decided on the early path (device count)
     *second_round = c[0];
     *whole_rows = c[1];
-    h->fc_early_q = 0;
     return 0;
 }
 
@@ -1788,8 +1801,13 @@ int lx_set_option(lx_index *h, const char *name, int64_t value) {
         h->rs_sub_opt = (uint32_t)value;
     } else if (k == "get_server") {
         // single-row getters through the resident row server (default 1)
-        h->srv_opt = value != 0;
+        if (value < 0 || value > 2) return h->fail(LX_ERR_ARG, "get_server must be 0, 1 (auto) or 2");
+        h->srv_opt = (int)value;
         if (!h->srv_opt) srv_stop(h);
+    } else if (k == "getter_host_check") {
+        // 0 (tests only): getters skip the host's event check, so an unknown
+        // event reaches the row kernel's / row server's own bound
+        h->get_host_check = value != 0;
     } else if (k == "fc_cache") {
         if (value < 0 || value > 16384) return h->fail(LX_ERR_ARG, "fc_cache must be 0..16384");
         fcc_destroy(h);
@@ -2307,6 +2325,11 @@ namespace {
 int srv_post(lx_index *h, const GetArgs &a, bool *posted) {
     *posted = false;
     if (!h->srv_opt || a.n != 1 || a.ev) return 0;
+    if (h->srv_opt == 1 && g_live_handles.load(std::memory_order_relaxed) > 1) {
+        // another handle's streams may share the server's hardware queue
+        if (h->srv_live) srv_stop(h);
+        return 0;
+    }
     // the rows it reads must be final: wait for the stream (usually the tail
     // of a launch whose results the host already has -- a pinned-path
     // ForklessCause, a getter that launched -- so that the next call finds it
@@ -2324,7 +2347,7 @@ int srv_post(lx_index *h, const GetArgs &a, bool *posted) {
         if (!ok) {
             if (p) (void)hipHostFree(p);
             (void)hipGetLastError();
-            h->srv_opt = false;
+            h->srv_opt = 0;
             return 0;
         }
         memset(p, 0, 64);
@@ -2374,6 +2397,9 @@ int get_rows(lx_index *h, uint32_t mode, uint32_t n, const uint32_t *ev, uint8_t
     a.len = reinterpret_cast<uint32_t *>(dp + 4ull * n);
     a.out = dp + head;
     a.slot = sl;
+    // the device's own bound (k_get_server takes the event from a request word)
+    a.row_lo = h->rowseg() ? h->rs_lo : 0u;
+    a.row_hi = h->rowseg() ? h->rs_hi : (uint32_t)std::min<uint64_t>(h->n_cap, 0xFFFFFFFFull);
     if (n == 1) {
         // one row (the reference's per-call getters): the resident server
         // answers it when the handle's stream is idle (no launch); otherwise a
@@ -2424,6 +2450,8 @@ int get_rows(lx_index *h, uint32_t mode, uint32_t n, const uint32_t *ev, uint8_t
     *rows = hp + head;
     *slot = sl;
     *len = reinterpret_cast<const uint32_t *>(hp + 4ull * n);
+    for (uint32_t i = 0; i < n; i++)
+        if ((*len)[i] == kGetBadLen) return h->fail(LX_ERR_ARG, "unknown event %u (refused by the row kernel)", ev[i]);
     return 0;
 }
 
@@ -2436,8 +2464,9 @@ int get_check(lx_index *h, uint32_t n, const uint32_t *ev) {
         const int rc = flush_pending(h);
         if (rc) return rc;
     }
-    for (uint32_t i = 0; i < n; i++)
-        if (ev[i] >= h->n_events) return h->fail(LX_ERR_ARG, "unknown event %u", ev[i]);
+    if (h->get_host_check)
+        for (uint32_t i = 0; i < n; i++)
+            if (ev[i] >= h->n_events) return h->fail(LX_ERR_ARG, "unknown event %u", ev[i]);
     HIPCHK(h, set_dev(h->device));
     return 0;
 }
@@ -2481,6 +2510,8 @@ int get_batch(lx_index *h, uint32_t mode, uint32_t n, const uint32_t *ev, uint64
 }  // namespace
 
 extern "C" {
+
+int lx_live_handles(void) { return g_live_handles.load(std::memory_order_relaxed); }
 
 int lx_get_server_stats(const lx_index *h, uint64_t out[3]) {
     if (!h || !out) return LX_ERR_ARG;

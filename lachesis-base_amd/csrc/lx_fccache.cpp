@@ -61,14 +61,16 @@ struct FcCache {
     std::vector<uint8_t> dmark;
     bool dirty_all = true;
     uint8_t *M = nullptr, *M_dev = nullptr;         // [W][W], pinned and device-mapped: answers land here
-    uint32_t *qa = nullptr, *qa_dev = nullptr;      // the row's a
     // the last fill: it writes row inflight_sa of M (a tile fill: every row)
     // while the host goes on as soon as its own answer landed; a row is reused
-    // (cleared for a new occupant) only after that fill has finished: an event
-    // recorded after k_fc / tile fills, the row's entries for k_add1_row
+    // (cleared for a new occupant) only after that fill has finished.  A fill
+    // of a row cleared for it (a new asking event) is finished once every
+    // entry carries the generation it was launched with; any other fill (a
+    // refill of a row whose entries already match, a tile fill) by an event
+    // recorded after it
     hipEvent_t filled = nullptr;
     bool inflight = false;
-    bool inflight_row = false;                      // k_add1_row (no event recorded)
+    bool inflight_fresh = false;                    // the row was cleared for this fill: generations tell
     bool inflight_tile = false;
     uint32_t inflight_sa = 0, inflight_n = 0;
     std::vector<uint8_t> g7_launch;                 // the column generations the in-flight row fill writes
@@ -169,7 +171,7 @@ namespace {
 
 void fcc_free(FcCache *c) {
     if (!c) return;
-    for (void *p : {(void *)c->evk, (void *)c->g7, (void *)c->M, (void *)c->qa})
+    for (void *p : {(void *)c->evk, (void *)c->g7, (void *)c->M})
         if (p) (void)hipHostFree(p);
     if (c->evk_d) (void)hipFree(c->evk_d);
     if (c->g7_d) (void)hipFree(c->g7_d);
@@ -197,7 +199,6 @@ int fcc_make(lx_index *h) {
     if (e == hipSuccess) e = hipMalloc((void **)&c->evk_d, 4ull * W);
     if (e == hipSuccess) e = hipMalloc((void **)&c->g7_d, W);
     if (e == hipSuccess) { e = pin((void **)&c->M, &d, (uint64_t)W * W); c->M_dev = static_cast<uint8_t *>(d); }
-    if (e == hipSuccess) { e = pin((void **)&c->qa, &d, 64); c->qa_dev = static_cast<uint32_t *>(d); }
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->filled, hipEventDisableTiming);
     if (e == hipSuccess) e = hipMalloc((void **)&c->d_rsum, 8ull * kAdd1PsumStride * W);
     if (e == hipSuccess) e = hipMemsetAsync(c->d_rsum, 0, 8ull * kAdd1PsumStride * W, h->stream);
@@ -266,13 +267,15 @@ int fcc_sync_mirror(lx_index *h, FcCache *c) {
     return 0;
 }
 
-// a against every slot in use: one k_fc launch, answers into M's row sa
+// a against every slot in use: one k_fc launch, answers into M's row sa.  The
+// asking event travels in the kernel arguments: the host may move on to the
+// next miss (and its next a) while this fill still runs
 int fcc_row(lx_index *h, FcCache *c, uint32_t a, uint32_t sa) {
-    c->qa[0] = a;
     FcArgs f;
-    int rc = lx_fc_args(h, c->used, c->qa_dev, c->evk_d, c->M_dev + (uint64_t)sa * c->W, nullptr, &f);
+    int rc = lx_fc_args(h, c->used, c->evk_d, c->evk_d, c->M_dev + (uint64_t)sa * c->W, nullptr, &f);
     if (rc) return rc;
     f.qa_bcast = 1;
+    f.qa_imm = a;
     f.out_tag = c->g7_d;
     f.status = h->status + 2;   // the pinned-path sink: every slot holds a known event
     HIPCHK(h, lx::launch_fc(f, h->ncols, h->B > h->V, h->stream));
@@ -330,12 +333,13 @@ int fcc_tile(lx_index *h, FcCache *c) {
 }
 
 // the last fill has finished writing M (by the time the caller asks again it
-// normally has): a row fill once every entry of its row carries the generation
-// it was launched with, a tile fill by its event
+// normally has): a fill of a freshly cleared row once every entry of its row
+// carries the generation it was launched with (the entries were 0 before it);
+// a refill of a row whose entries already matched, or a tile fill, by its event
 int fcc_quiesce(lx_index *h, FcCache *c) {
     if (!c->inflight) return 0;
     const auto tq = std::chrono::steady_clock::now();
-    if (!c->inflight_tile) {
+    if (!c->inflight_tile && c->inflight_fresh) {
         const volatile uint8_t *row = c->M + (uint64_t)c->inflight_sa * c->W;
         const auto t0 = std::chrono::steady_clock::now();
         uint32_t s = 0;
@@ -353,7 +357,7 @@ int fcc_quiesce(lx_index *h, FcCache *c) {
         HIPCHK(h, hipEventSynchronize(c->filled));
     }
     c->inflight = false;
-    c->inflight_row = c->inflight_tile = false;
+    c->inflight_fresh = c->inflight_tile = false;
     c->st.quiesce_ns +=
         (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - tq).count();
     return 0;
@@ -453,11 +457,11 @@ int fcc_query(lx_index *h, uint32_t a, uint32_t b, uint8_t *out) {
     }
     if (rc) return rc;
     c->inflight = true;
-    c->inflight_row = !tile;
+    c->inflight_fresh = !tile && a_new;   // k_add1_row runs only for a new asking event
     c->inflight_tile = tile;
     c->inflight_sa = sa;
     c->inflight_n = c->used;
-    if (!tile) memcpy(c->g7_launch.data(), c->g7, c->used);
+    if (c->inflight_fresh) memcpy(c->g7_launch.data(), c->g7, c->used);
     else HIPCHK(h, hipEventRecord(c->filled, h->stream));
     const auto t_wait = std::chrono::steady_clock::now();
     c->st.launch_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t_wait - t_launch).count();

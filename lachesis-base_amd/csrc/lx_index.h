@@ -235,7 +235,11 @@ struct lx_index {
     uint32_t get_tag = 0;                  // completion tag of the last single-row getter
     bool fc_unchecked = false;             // a ForklessCause launch may have flagged status[1] since lx_sync looked
     // the resident single-row server (k_get_server, option get_server)
-    bool srv_opt = true;
+    // 0 off; 1 auto: only while this handle is the process's only one (the
+    // server holds a hardware queue while resident, and GPU_MAX_HW_QUEUES = 4
+    // lets more streams share queues: work queued behind the resident kernel
+    // would wait up to its 250-us idle exit); 2 on whatever the handle count
+    int srv_opt = 1;
     hipStream_t srv_stream = nullptr;      // its own (high-priority) stream
     uint64_t *srv_host = nullptr, *srv_dev = nullptr;   // pinned: [0] request word, [1] exited gen
     bool srv_live = false;                 // launched and not known to have left
@@ -244,6 +248,7 @@ struct lx_index {
     uint64_t srv_ticks_us = 0;             // wall clock ticks per microsecond
     uint64_t srv_served = 0, srv_launches = 0, srv_fallbacks = 0;
     uint32_t *q_sink = nullptr;            // status word the pinned FC path lets the kernel flag into
+    bool get_host_check = true;            // option getter_host_check=0 (tests): device bound only
 
     // timing (HIP events on `stream`)
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -260,8 +265,7 @@ struct lx_index {
     // segmented walk (option segments, lx_segment.hip): scratch and timings of the last batch
     uint32_t segments = 0;
     bool fc_early = true;                  // option fc_early=0: k_fc always reads whole rows
-    unsigned long long *d_fc_full = nullptr;   // early exit: queries that read whole rows (device)
-    uint64_t fc_early_q = 0;               // queries launched with the early exit
+    unsigned long long *d_fc_full = nullptr;   // early exit counters (device): past round 1, past round 2, all
     bool seg_auto = true;                  // option seg_auto=0: never split a batch on its own
     uint32_t n_cus = 256;                  // compute units of the device (auto segments)
     uint32_t *seg_jt = nullptr, *seg_cnt = nullptr, *seg_mf = nullptr, *seg_plist = nullptr, *seg_elist = nullptr;

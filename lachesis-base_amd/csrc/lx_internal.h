@@ -150,7 +150,9 @@ struct FcArgs {
     const uint32_t *qb;
     uint8_t *out;                // bool result (or NULL)
     const uint8_t *out_tag;      // optional: out[q] = out_tag[q] << 1 | result (FC cache generations)
-    uint32_t qa_bcast;           // 1: every query's a is qa[0] (a row of the FC cache)
+    uint32_t qa_bcast;           // 1: every query's a is qa_imm (a row of the FC cache; never read from
+                                 // memory the host may rewrite while the fill runs)
+    uint32_t qa_imm;
     uint32_t *partial;           // partial sum (or NULL)
     const uint32_t *wpad;        // weight per column (0 outside [vlo, vhi) originals)
     uint32_t vlo4, vhi4;         // column range in uint4 units
@@ -162,7 +164,8 @@ struct FcArgs {
     uint32_t early_rest;
     uint32_t early_rest2;        // the weight past the first 512 columns
     uint32_t early;
-    unsigned long long *early_full;   // [0] += queries past the first round, [1] += past the second
+    unsigned long long *early_full;   // [0] += queries past the first round, [1] += past the second,
+                                      // [2] += queries decided on the early path
     const uint32_t *ev_branch;
     const uint32_t *ev_creator;  // creator per event (= creator of its branch)
     // cheaters of this shard: CSR over all their branches (first = original)
@@ -441,7 +444,12 @@ struct GetArgs {
     // length, so the host spins on it instead of synchronizing the stream
     uint32_t *done;
     uint32_t tag;
+    // rows the kernel may read: events outside [row_lo, row_hi) are answered
+    // with length kGetBadLen and no row (the host turns it into LX_ERR_ARG) --
+    // the device's own bound, whatever event a request word names
+    uint32_t row_lo, row_hi;
 };
+constexpr uint32_t kGetBadLen = 0xFFFFFFFFu;
 
 // the resident single-row server (k_get_server): `g` with plane / ev0 / mode /
 // tag filled per request from the request word *req

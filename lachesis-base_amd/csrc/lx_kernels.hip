@@ -422,15 +422,6 @@ __device__ __forceinline__ uint32_t rec_off(uint32_t slot, uint32_t q) {
 // Per-wave walker counters (LX_PROF=1) are compiled in only with
 // -DLX_WALKER_PROF (make WPROF=1): the increments cost the compute pass
 // several VALU instructions.
-// `make nofill` (build_nofill/, never loaded by the tests or bench.py): the
-// drains skip the LowestAfter range fill, so the LA plane is WRONG; the build
-// exists only to time the walk with and without the 4-B scatter
-// (scripts/probes/nofill_ab.sh)
-#ifdef LX_TIMING_NO_LA_FILL
-constexpr bool kTimingNoLaFill = true;
-#else
-constexpr bool kTimingNoLaFill = false;
-#endif
 
 #ifdef LX_WALKER_PROF
 #define LX_WP(x) x
@@ -810,7 +801,7 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
                     for (int k = 0; k < CPW; k++)
                         if (valid[k]) hrow[pc[k]] = r[k];
                 }
-                if (!kTimingNoLaFill) {
+                {
                     // LowestAfter range fill: events (col, s), s in (h0, r], are first
                     // observed from branch `br` by this event.
                     uint32_t lo[CPW], hi[CPW];
@@ -1387,7 +1378,7 @@ __global__ __launch_bounds__(256) void k_fc(FcArgs a) {
         const uint32_t i = lane + t * LPQ;
         wr[t] = i < nv ? wv[i] : make_uint4(0, 0, 0, 0);
     }
-    uint32_t n_full = 0, n_rest = 0;   // early exit: queries past the first round / past the second
+    uint32_t n_full = 0, n_rest = 0, n_early = 0;   // early exit: queries past the first round / the second / all
     if constexpr (!FORKS && LPQ == 64) {
         if (a.early) {
             // the heaviest 256 columns first (lane i: uint4 i of both rows); the
@@ -1400,7 +1391,7 @@ __global__ __launch_bounds__(256) void k_fc(FcArgs a) {
             bool bad = false;
             u4v hv = {0, 0, 0, 0}, lv = {0, 0, 0, 0};
             auto first = [&](uint64_t qq, uint32_t &A_, uint32_t &B_, bool &bad_, u4v &h_, u4v &l_) {
-                A_ = a.qa[a.qa_bcast ? 0 : qq];
+                A_ = a.qa_bcast ? a.qa_imm : a.qa[qq];
                 B_ = a.qb[qq];
                 bad_ = fc_bad(a, A_, B_);
                 if (bad_) { A_ = 0; B_ = 0; }
@@ -1456,16 +1447,18 @@ __global__ __launch_bounds__(256) void k_fc(FcArgs a) {
                     if (bad) atomicOr(&a.status[1], 1u);
                 }
                 A = An; Bq = Bn; bad = badn; hv = hn; lv = ln;
+                n_early++;
             }
-            if (a.early_full && lane == 0 && n_full) {
-                atomicAdd(a.early_full, (unsigned long long)n_full);
+            if (a.early_full && lane == 0 && n_early) {
+                if (n_full) atomicAdd(a.early_full, (unsigned long long)n_full);
                 if (n_rest) atomicAdd(a.early_full + 1, (unsigned long long)n_rest);
+                atomicAdd(a.early_full + 2, (unsigned long long)n_early);
             }
             return;
         }
     }
     for (uint64_t q = blockIdx.x * qpb + threadIdx.x / LPQ; q < a.n; q += (uint64_t)gridDim.x * qpb) {
-        uint32_t A = a.qa[a.qa_bcast ? 0 : q], Bq = a.qb[q];
+        uint32_t A = a.qa_bcast ? a.qa_imm : a.qa[q], Bq = a.qb[q];
         const bool bad = fc_bad(a, A, Bq);
         if (bad) { A = 0; Bq = 0; }
         // FORKS, lane 0: the early-false inputs first (their loads overlap the rows')
@@ -1581,7 +1574,7 @@ __global__ __launch_bounds__(256) void k_fc_fk(FcArgs a) {
         wch[t] = k < a.n_cheat ? a.fk_wch[k] : 0u;
     }
     for (uint64_t q = blockIdx.x * qpb + threadIdx.x / LPQ; q < a.n; q += (uint64_t)gridDim.x * qpb) {
-        uint32_t A = a.qa[a.qa_bcast ? 0 : q], Bq = a.qb[q];
+        uint32_t A = a.qa_bcast ? a.qa_imm : a.qa[q], Bq = a.qb[q];
         const bool bad = fc_bad(a, A, Bq);
         if (bad) { A = 0; Bq = 0; }
         uint32_t e_bb = 0, e_cb = 0;

@@ -156,6 +156,12 @@ __device__ __forceinline__ void get_done(const GetArgs &a, uint32_t lane) {
 
 // row i (event e) by one wave
 __device__ __forceinline__ void get_row(const GetArgs &a, uint32_t i, uint32_t e, uint32_t lane) {
+    if (e < a.row_lo || e >= a.row_hi || a.mode > 2) {
+        // not a row of this handle (or no such mode): no read, an error length
+        if (lane == 0) a.len[i] = kGetBadLen;
+        get_done(a, lane);
+        return;
+    }
     const uint32_t *row = a.plane + (uint64_t)e * a.stride;
     uint32_t *o = reinterpret_cast<uint32_t *>(a.out + (uint64_t)i * a.slot);
     if (a.mode == 2 && a.forks) {
@@ -291,7 +297,7 @@ __global__ __launch_bounds__(64) void k_get_server(GetSrvArgs s) {
         // rows written by kernels on other queues (and XCDs) since the last request
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
         GetArgs a = s.g;
-        a.mode = __builtin_amdgcn_readfirstlane((uint32_t)w >> 30);
+        a.mode = __builtin_amdgcn_readfirstlane((uint32_t)w >> 30);   // 3: refused by get_row
         a.plane = a.mode == 1 ? s.la : s.hb;
         a.tag = q;
         get_row(a, 0, __builtin_amdgcn_readfirstlane((uint32_t)(w >> 32)), lane);

@@ -50,6 +50,7 @@ SIGNATURES = [
     ("lx_get_merged_highest_before_batch", ctypes.c_int, [vp, ctypes.c_uint32, u32p, u64p, u8p, ctypes.c_uint64]),
     ("lx_get_event_branch_id", ctypes.c_int, [vp, ctypes.c_uint32, u32p]),
     ("lx_get_server_stats", ctypes.c_int, [vp, u64p]),
+    ("lx_live_handles", ctypes.c_int, []),
     ("lx_get_branches_info", ctypes.c_int, [vp, u32p, u32p, ctypes.c_uint32, u32p]),
     ("lx_shard_of", ctypes.c_int, [vp, u32p, u32p]),
     ("lx_shard_range", ctypes.c_int, [vp, ctypes.c_uint32, u32p, u32p]),
@@ -356,12 +357,16 @@ class Index:
         self._chk(self.L.lx_get_server_stats(self.h, _p(out, u64p)))
         return {"served": int(out[0]), "launches": int(out[1]), "fallbacks": int(out[2])}
 
+    def live_handles(self):
+        """Index handles alive in this process (the row server's auto mode)."""
+        return int(self.L.lx_live_handles())
+
     def forkless_cause_batch_dev(self, n, a_ptr, b_ptr, out_ptr, stream=None):
         self._chk(self.L.lx_forkless_cause_batch_dev(self.h, n, a_ptr, b_ptr, out_ptr, stream))
 
     def fc_early_counters(self):
-        """(queries launched with the early exit, of them past the first round,
-        past the second: whole rows) since the last call."""
+        """(queries the kernel decided on its early path, of them past the first
+        round, past the second: whole rows) since the last call."""
         q, f2, fw = ctypes.c_uint64(0), ctypes.c_uint64(0), ctypes.c_uint64(0)
         self._chk(self.L.lx_fc_early_counters(self.h, ctypes.byref(q), ctypes.byref(f2), ctypes.byref(fw)))
         return q.value, f2.value, fw.value

@@ -272,3 +272,40 @@ def test_drop_readd_different_fork_suffix(lx, seed):
         assert int(o.num_events()) == n_before
     assert ix.fc_cache_stats()["tile_fills"] > 0
     ix.close()
+
+
+@pytest.mark.parametrize("fork", [False, True])
+def test_back_to_back_row_fills_different_asking_events(lx, fork):
+    """Misses of different asking events right after one another, nothing
+    pending (the k_fc row-fill path, not the fused Add + row launch): the host
+    returns as soon as its own answer lands while the rest of the row is still
+    being written, and moves on to the next asking event.  Every row must hold
+    its own asking event's answers -- then read back as hits and compared with
+    the oracle (vecfc/forkless_cause.go:28-38: a cached answer is the answer)."""
+    V = 100
+    d = lx.tools.gen_dag(V, 40, 10, cheaters=4 if fork else 0, forks=3 if fork else 0, seed=17)
+    w = [(1 << 12) // (i + 1) + 1 for i in range(V)]
+    N = len(d)
+    o = _oracle(d, w, N)
+    ix = lx.Index(options={"fc_cache": 4096})
+    ix.reset(w)
+    ix.add_batch(d.creator, d.seq, d.poff, d.par)
+    ix.flush()
+    ix.sync()
+    rng = np.random.default_rng(5)
+    # a working set of ~3000 b's (each first question brings its next 64 events)
+    bs = list(range(N - 3000, N, 64))
+    for b in bs:
+        assert ix.forkless_cause(N - 1, b) == bool(o.forkless_cause(N - 1, b))
+    # back-to-back misses, each a new asking event with one question
+    asks = [int(x) for x in rng.choice(np.arange(N // 2, N - 1), 300, replace=False)]
+    for a in asks:
+        b = int(rng.integers(N - 3000, N))
+        assert ix.forkless_cause(a, b) == bool(o.forkless_cause(a, b)), (a, b)
+    # the rows those fills wrote: every answer, hits or refills
+    for a in asks[::5]:
+        for b in range(N - 3000, N, 37):
+            assert ix.forkless_cause(a, b) == bool(o.forkless_cause(a, b)), (a, b)
+    st = ix.fc_cache_stats()
+    assert st["row_fills"] >= len(asks) and st["hits"] > 0, st
+    ix.close()
