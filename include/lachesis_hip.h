@@ -266,6 +266,16 @@ int lx_get_lowest_after_batch(lx_index *h, uint32_t n, const uint32_t *ev, uint6
 int lx_get_merged_highest_before_batch(lx_index *h, uint32_t n, const uint32_t *ev, uint64_t *off, uint8_t *out,
                                        uint64_t cap);
 int lx_get_event_branch_id(lx_index *h, uint32_t ev, uint32_t *out);
+/* The same rows with device ids in and device rows out (mode 0 HighestBefore,
+ * 1 LowestAfter, 2 merged HighestBefore): row i at out_dev + i * slot_bytes,
+ * its byte length in len_dev[i] (slot_bytes >= lx_row_bytes_max); an event
+ * the handle does not hold -- not indexed, or another row-segment rank's --
+ * gets length 0xFFFFFFFF and no row.  Completed on return.  The row-segment
+ * getters route ids to their owners and call this there
+ * (lachesis_hip/rowseg.py, lx_rowseg_get_rows). */
+int lx_get_rows_dev(lx_index *h, uint32_t mode, uint32_t n, const uint32_t *ev_dev, uint8_t *out_dev,
+                    uint64_t slot_bytes, uint32_t *len_dev);
+int lx_row_bytes_max(const lx_index *h, uint64_t *bytes);   /* 8 x max(branches, validators) */
 
 /* BranchesInfo (vecengine/branches_info.go:9-14): per branch last seq and
  * creator idx (arrays of cap entries; *n_branches receives B). */
@@ -454,8 +464,17 @@ int lx_rowseg_fc_unroute(lx_index *h, uint64_t n, const uint32_t *perm_dev, cons
 int lx_rowseg_forkless_cause(lx_shard_comm *c, uint64_t n, const uint32_t *qa_dev, const uint32_t *qb_dev,
                              uint8_t *out_dev, uint64_t stats[4]);
 
-/* Device views for benchmarks/tests (valid until the next add/reset). */
+/* Device views for benchmarks/tests (valid until the next add/reset).  On a
+ * row-segment rank the planes hold its own rows only: row e is at
+ * hb + e * stride for e in lx_rowseg_range, nothing else is addressable. */
 int lx_device_planes(lx_index *h, void **hb, void **la, uint32_t *stride, void **stream);
+/* Device memory the handle holds, in bytes: out[0] the HighestBefore and
+ * LowestAfter planes (a column shard: plus its produced LowestAfter rows;
+ * a row-segment rank: its own rows), out[1] a row-segment rank's receive
+ * areas (rows of other ranks), out[2] per-event metadata and per-event
+ * scratch, out[3] everything else it allocated (branch tables, batch and
+ * query scratch). */
+int lx_device_bytes(const lx_index *h, uint64_t out[4]);
 int lx_sync(lx_index *h);
 
 #ifdef __cplusplus

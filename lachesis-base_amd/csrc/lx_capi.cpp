@@ -65,6 +65,7 @@ void free_wb(lx_index *h) {
 
 void free_all(lx_index *h) {
     free_wb(h);
+    rs_planes_free(h);   // a row-segment rank's hb / la are virtual bases into its own allocations
     void *ptrs[] = {h->hb, h->la, h->ev_creator, h->ev_seq, h->ev_branch, h->ev_bbefore, h->ev_sp,
                     h->first_child, h->first_root, h->branch_first, h->branch_creator, h->branch_len, h->brow,
                     h->wpad, h->col_list, h->cheat_off, h->cheat_br, h->cheat_creator, h->b_creator, h->b_seq,
@@ -161,8 +162,11 @@ int grow_events(lx_index *h, uint64_t need) {
         *a = n;
     }
     HIPCHK(h, lx::launch_fill_u32(h->first_child + keep, cap - keep, LX_NONE, h->stream));
+    // (a row-segment rank allocates the planes of its own rows when it takes
+    // its batch: rs_planes)
     uint32_t **planes[] = {&h->hb, &h->la};
     for (uint32_t **p : planes) {
+        if (h->rowseg()) break;
         uint32_t *n = nullptr;
         HIPCHK(h, dalloc(&n, cap * h->pstride));
         HIPCHK(h, hipMemsetAsync(n, 0, cap * h->pstride * 4, h->stream));
@@ -231,7 +235,7 @@ int grow_branches(lx_index *h, uint32_t need) {
         if (h->cmap) (void)hipFree(h->cmap);
         h->cmap = nc;
         h->cmap_cap = ns;
-    } else if (h->hb) {
+    } else if (h->hb && !h->rowseg()) {   // (row-segment planes: rs_planes, at the batch)
         uint32_t **planes[] = {&h->hb, &h->la};
         for (uint32_t **p : planes) {
             uint32_t *n = nullptr;
@@ -722,6 +726,9 @@ int add_batch_dev(lx_index *h, uint32_t n, const uint32_t *creator, const uint32
     }
     HIPCHK(h, hipEventRecord(h->ev[1], s));
     if (h->rowseg()) {
+        if ((rc = rs_planes(h, n))) return rc;   // own rows only (+ the virtual bases)
+        ia.hb = h->hb;
+        ia.la = h->la;
         if ((rc = rs_begin(h, ia, poff, s))) return rc;
     } else if (h->segments > 1 && !h->sharded() && n >= 64ull * h->segments) {
         if ((rc = seg_walk(h, ia, poff, s, h->segments, h->cpw_hint))) return rc;
@@ -842,6 +849,9 @@ int lx_fc_args(lx_index *h, uint64_t n, const uint32_t *a, const uint32_t *b, ui
     f.ev_lo = h->rowseg() ? h->rs_lo : 0u;
     f.b_stamp = h->rowseg() ? h->rs_stamp : nullptr;
     f.n_all = (uint32_t)h->n_events;
+    f.la_recv = h->rowseg() ? h->rs_rla : nullptr;
+    f.b_slot = h->rowseg() ? h->rs_lslot : nullptr;
+    f.b_arrived = 2 * h->rs_gen + 1;
     f.n = n;
     f.qa = a;
     f.qb = b;
@@ -1860,6 +1870,11 @@ int lx_reset(lx_index *h, uint32_t nv, const uint32_t *w) {
         if ((rc = grow_scap(h, s0))) return rc;
         h->hwm = 0;
         if ((rc = grow_events(h, h->cap_hint ? h->cap_hint : 4096))) return rc;
+    } else if (h->hwm && h->rowseg()) {
+        // a row-segment rank: its own rows are rewritten (HB by the walk and the
+        // fix-up, LA zeroed at the batch, rs_begin); only the metadata resets
+        HIPCHK(h, lx::launch_fill_u32(h->first_child, h->hwm, LX_NONE, h->stream));
+        h->hwm = 0;
     } else if (h->hwm) {
         // HB: the walker rewrites the original columns of every new event's row
         // (the original branches always exist); only the fork-branch columns can
@@ -2457,9 +2472,18 @@ int get_rows(lx_index *h, uint32_t mode, uint32_t n, const uint32_t *ev, uint8_t
 
 int get_check(lx_index *h, uint32_t n, const uint32_t *ev) {
     if (h->sharded()) return h->fail(LX_ERR_STATE, "vector getters need an unsharded handle (shards hold their own columns)");
-    WHOLE_INDEX(h);
     if (!h->have_epoch) return h->fail(LX_ERR_STATE, "getter before lx_reset");
     NOT_LOADING(h);
+    if (h->rowseg()) {
+        // a row-segment rank answers for its own rows (final after lx_rowseg_finish);
+        // the others' are routed to their owners (lachesis_hip/rowseg.py, lx_rowseg_get_rows)
+        if (h->rs_state != 4) return h->fail(LX_ERR_STATE, "row-segment rank: getters before lx_rowseg_finish");
+        if (h->get_host_check)
+            for (uint32_t i = 0; i < n; i++)
+                if (ev[i] < h->rs_lo || ev[i] >= h->rs_hi)
+                    return h->fail(ev[i] < h->n_events ? LX_ERR_STATE : LX_ERR_ARG,
+                                   "event %u is not a row of this row-segment rank [%u, %u)", ev[i], h->rs_lo, h->rs_hi);
+    }
     {
         const int rc = flush_pending(h);
         if (rc) return rc;
@@ -2545,6 +2569,51 @@ int lx_get_lowest_after_batch(lx_index *h, uint32_t n, const uint32_t *ev, uint6
 int lx_get_merged_highest_before_batch(lx_index *h, uint32_t n, const uint32_t *ev, uint64_t *off, uint8_t *out,
                                        uint64_t cap) {
     return get_batch(h, 2, n, ev, off, out, cap);
+}
+
+int lx_row_bytes_max(const lx_index *h, uint64_t *bytes) {
+    if (!h || !bytes) return LX_ERR_ARG;
+    *bytes = 8ull * std::max(h->B, h->V);
+    return 0;
+}
+
+int lx_get_rows_dev(lx_index *h, uint32_t mode, uint32_t n, const uint32_t *ev_dev, uint8_t *out_dev,
+                    uint64_t slot_bytes, uint32_t *len_dev) {
+    if (!h || mode > 2 || (n && (!ev_dev || !out_dev || !len_dev))) return LX_ERR_ARG;
+    if (h->sharded()) return h->fail(LX_ERR_STATE, "vector getters need an unsharded handle (shards hold their own columns)");
+    if (!h->have_epoch) return h->fail(LX_ERR_STATE, "getter before lx_reset");
+    NOT_LOADING(h);
+    if (h->rowseg() && h->rs_state != 4) return h->fail(LX_ERR_STATE, "row-segment rank: getters before lx_rowseg_finish");
+    if (slot_bytes < 8ull * std::max(h->B, h->V) || slot_bytes % 8)
+        return h->fail(LX_ERR_ARG, "row slot of %llu bytes < %llu", (unsigned long long)slot_bytes,
+                       8ull * std::max(h->B, h->V));
+    int rc;
+    if ((rc = flush_pending(h))) return rc;
+    HIPCHK(h, set_dev(h->device));
+    if (!n) return 0;
+    GetArgs a{};
+    a.plane = mode == 1 ? h->la : h->hb;
+    a.stride = h->pstride;
+    a.ev = ev_dev;
+    a.n = n;
+    a.B = h->B;
+    a.V = h->V;
+    a.mode = mode;
+    a.forks = h->B > h->V ? 1u : 0u;
+    a.ev_bbefore = h->ev_bbefore;
+    a.ev_branch = h->ev_branch;
+    a.branch_first = h->branch_first;
+    a.cheat_of = h->cheat_of;
+    a.cheat_off = h->cheat_off;
+    a.cheat_br = h->cheat_br;
+    a.len = len_dev;
+    a.out = out_dev;
+    a.slot = slot_bytes;
+    a.row_lo = h->rowseg() ? h->rs_lo : 0u;
+    a.row_hi = h->rowseg() ? h->rs_hi : (uint32_t)h->n_events;
+    HIPCHK(h, lx::launch_get_rows(a, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return 0;
 }
 
 int lx_get_branches_info(lx_index *h, uint32_t *last_seq, uint32_t *creator_idx, uint32_t cap, uint32_t *n_branches) {
@@ -2819,6 +2888,27 @@ int lx_device_planes(lx_index *h, void **hb, void **la, uint32_t *stride, void *
     if (la) *la = h->la;
     if (stride) *stride = h->pstride;
     if (stream) *stream = h->stream;
+    return 0;
+}
+
+int lx_device_bytes(const lx_index *h, uint64_t out[4]) {
+    if (!h || !out) return LX_ERR_ARG;
+    const uint64_t ps = h->pstride;
+    uint64_t planes = h->rs_hb_mem ? 2 * h->rs_mem_rows * ps * 4 : (h->hb ? 2 * h->n_cap * ps * 4 : 0);
+    if (h->lap) planes += (uint64_t)h->pstride * h->s_cap * h->stride * 4;
+    const uint64_t recv = 4 * (h->rs_rhb_cap + h->rs_rla_cap);
+    uint64_t per_ev = 6 * 4 * h->n_cap;   // creator, seq, branch, bbefore, sp, first_child
+    for (uint64_t c : {h->seg_mf_cap, h->seg_plist_cap, h->seg_elist_cap, h->rs_need_cap, h->rs_hslot_cap,
+                       h->rs_lslot_cap, h->rs_stamp_cap, h->wb_cap})
+        per_ev += 4 * c;
+    uint64_t other = 4 * ((uint64_t)h->stride * h->s_cap + 5ull * h->stride + h->tail_cap * (uint64_t)h->tail_cap * 2);
+    other += 4 * (8 * h->batch_cap + h->par_cap + 2 * h->q_cap) + h->q_cap + 16 * h->batch_cap;
+    other += 4 * (h->rs_req_cap + h->rs_ids_cap + h->rs_out_cap + h->rs_send_cap + h->rsq_scratch_cap + h->rsq_list_cap) +
+             h->rsq_tmp_bytes + h->scan_bytes;
+    out[0] = planes;
+    out[1] = recv;
+    out[2] = per_ev;
+    out[3] = other;
     return 0;
 }
 

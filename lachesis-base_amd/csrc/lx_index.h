@@ -298,6 +298,17 @@ struct lx_index {
     void *rsq_tmp = nullptr;
     size_t rsq_tmp_bytes = 0;
     uint32_t rsq_nlist = 0;                // distinct remote rows of the last lx_rowseg_fc_need
+    // the planes of a row-segment rank hold its own rows only (rs_planes):
+    // hb / la are virtual bases (own row e at hb + e * pstride, inside the
+    // allocations rs_hb_mem / rs_la_mem of rs_mem_rows rows); rows of other
+    // ranks it receives go to receive areas: HighestBefore rows for the
+    // partial fix-up (rs_rhb, row rs_hslot[x]), LowestAfter rows for one
+    // ForklessCause batch (rs_rla, row rs_lslot[x])
+    uint32_t *rs_hb_mem = nullptr, *rs_la_mem = nullptr;
+    uint64_t rs_mem_rows = 0;
+    uint32_t rs_mem_pstride = 0;
+    uint32_t *rs_hslot = nullptr, *rs_rhb = nullptr, *rs_lslot = nullptr, *rs_rla = nullptr;
+    uint64_t rs_hslot_cap = 0, rs_rhb_cap = 0, rs_lslot_cap = 0, rs_rla_cap = 0;   // (receive areas: rows x pstride)
     bool rowseg() const { return rs_count > 1; }
 
     int fail(int code, const char *fmt, ...) {
@@ -335,6 +346,8 @@ struct Add1Delta {
 int flush_add1_row(lx_index *h, uint32_t a, uint32_t *evk_dev, uint32_t n_slots, uint8_t *tag_dev, uint8_t *out_dev,
                    uint32_t *psum_dev, const Add1Delta *delta);   // 1: not applicable
 int rs_begin(lx_index *h, IndexArgs ia, const uint32_t *poff, hipStream_t s);   // lx_rowseg.cpp
+int rs_planes(lx_index *h, uint32_t n);          // lx_rowseg.cpp: own rows of an n-event epoch
+void rs_planes_free(lx_index *h);
 uint32_t seg_pick(const lx_index *h, uint64_t n, uint32_t *cpw);    // lx_capi.cpp (auto_segments)
 uint32_t seg_walk_grid(const lx_index *h, uint32_t cpw);
 void rs_free(lx_index *h);

@@ -145,6 +145,11 @@ struct FcArgs {
     // row was received (b_stamp[b] odd; lx_rowseg_fc.hip); NULL elsewhere
     const uint32_t *b_stamp;
     uint32_t n_all;              // events of the epoch (b_stamp's length)
+    // row-segment rank: the LA rows received for this batch live in la_recv
+    // (row b_slot[b]); b_stamp[b] == b_arrived marks them (lx_rowseg_fc.hip)
+    const uint32_t *la_recv;
+    const uint32_t *b_slot;
+    uint32_t b_arrived;
     uint64_t n;
     const uint32_t *qa;
     const uint32_t *qb;
@@ -600,6 +605,11 @@ struct SegArgs {
     // row-segment rank: segments per rank (its own segment walked as per_rank
     // side-by-side sub-segments); the owner rank of segment k is k / per_rank
     uint32_t per_rank;
+    // row-segment rank: the planes hold the own rows [own_lo, hi) only; the
+    // rows of other ranks it received live in rhb at row hslot[x] (NULL:
+    // whole planes, every row at its own index)
+    const uint32_t *rhb;
+    const uint32_t *hslot;
 };
 
 // Row-segment multi-GPU exchange (lx_rowseg.cpp): rows a rank needs from the
@@ -616,6 +626,10 @@ struct RsArgs {
     uint32_t *req;               // requested rows (appended)
     uint32_t *req_count;
     uint32_t *remaining;
+    // received rows: row x of another rank at rhb + hslot[x] * stride (hslot =
+    // its position in req, set when it is first requested)
+    uint32_t *rhb;
+    uint32_t *hslot;
 };
 
 // ForklessCause across row-segment ranks (lx_rowseg_fc.hip)
@@ -645,8 +659,8 @@ hipError_t launch_rsq_group(const RsqArgs &a, const uint32_t *list, uint32_t n, 
                             uint32_t *ids, uint32_t *counts, hipStream_t s);
 hipError_t launch_rsq_la_gather(const RsqArgs &a, const uint32_t *la, uint64_t stride, const uint32_t *ids,
                                 uint32_t n, uint32_t *rows, hipStream_t s);
-hipError_t launch_rsq_la_store(const RsqArgs &a, uint32_t *la, uint64_t stride, const uint32_t *ids, uint32_t n,
-                               const uint32_t *rows, uint32_t *stamp, uint32_t arrived, hipStream_t s);
+hipError_t launch_rsq_la_store(const RsqArgs &a, uint32_t *la_recv, uint64_t stride, const uint32_t *ids, uint32_t n,
+                               const uint32_t *rows, uint32_t *stamp, uint32_t *slot, uint32_t arrived, hipStream_t s);
 hipError_t launch_rsq_unroute(const uint32_t *perm, const uint8_t *ans, uint64_t n, uint8_t *out, hipStream_t s);
 hipError_t launch_rs_bucket(const SegArgs &a, const RsArgs &r, uint32_t n_req, uint32_t *out, uint32_t *counts,
                             hipStream_t s);

@@ -1352,13 +1352,22 @@ __device__ __forceinline__ uint32_t fc_term(uint32_t l, uint32_t h, uint32_t w, 
 }
 
 // a query the handle cannot answer: a outside [ev_lo, n_events); b too,
-// unless a row-segment rank received b's final LowestAfter row (b_stamp odd)
+// unless a row-segment rank received b's final LowestAfter row for this batch
+// (b_stamp[b] == b_arrived).  Such queries read the row ev_lo instead (an own
+// row: a row-segment rank's planes start there) and answer 0xFF
 __device__ __forceinline__ bool fc_bad(const FcArgs &a, uint32_t A, uint32_t Bq) {
     const bool b_out = (Bq >= a.n_events) | (Bq < a.ev_lo);
     bool bad = (A >= a.n_events) | (A < a.ev_lo);
-    if (a.b_stamp) bad |= b_out && (Bq >= a.n_all || !(a.b_stamp[Bq] & 1u));
+    if (a.b_stamp) bad |= b_out && (Bq >= a.n_all || a.b_stamp[Bq] != a.b_arrived);
     else bad |= b_out;
     return bad;
+}
+
+// LowestAfter row of b: the plane's own row, or (row-segment rank, b another
+// rank's event) the row received for this batch
+__device__ __forceinline__ const uint32_t *fc_la(const FcArgs &a, uint32_t Bq) {
+    if (a.la_recv && (Bq < a.ev_lo || Bq >= a.n_events)) return a.la_recv + (uint64_t)a.b_slot[Bq] * a.stride;
+    return a.la + (uint64_t)Bq * a.stride;
 }
 
 template <int LPQ, bool FORKS>
@@ -1394,9 +1403,9 @@ __global__ __launch_bounds__(256) void k_fc(FcArgs a) {
                 A_ = a.qa_bcast ? a.qa_imm : a.qa[qq];
                 B_ = a.qb[qq];
                 bad_ = fc_bad(a, A_, B_);
-                if (bad_) { A_ = 0; B_ = 0; }
+                if (bad_) { A_ = a.ev_lo; B_ = a.ev_lo; }
                 h_ = __builtin_nontemporal_load(reinterpret_cast<const u4v *>(a.hb + (uint64_t)A_ * a.stride) + a.vlo4 + lane);
-                l_ = __builtin_nontemporal_load(reinterpret_cast<const u4v *>(a.la + (uint64_t)B_ * a.stride) + a.vlo4 + lane);
+                l_ = __builtin_nontemporal_load(reinterpret_cast<const u4v *>(fc_la(a, B_)) + a.vlo4 + lane);
             };
             if (q < a.n) first(q, A, Bq, bad, hv, lv);
             for (; q < a.n; q += step) {
@@ -1411,7 +1420,7 @@ __global__ __launch_bounds__(256) void k_fc(FcArgs a) {
                 uint32_t sum = s0;
                 if (s0 < a.quorum && s0 + a.early_rest >= a.quorum) {
                     const uint4 *ha = reinterpret_cast<const uint4 *>(a.hb + (uint64_t)A * a.stride) + a.vlo4;
-                    const uint4 *lb = reinterpret_cast<const uint4 *>(a.la + (uint64_t)Bq * a.stride) + a.vlo4;
+                    const uint4 *lb = reinterpret_cast<const uint4 *>(fc_la(a, Bq)) + a.vlo4;
                     // second round (columns 256-511), then the same test once more
                     uint32_t s1 = 0;
                     if (lane + 64 < nv) {
@@ -1427,7 +1436,7 @@ __global__ __launch_bounds__(256) void k_fc(FcArgs a) {
                 }
                 if (sum < a.quorum && sum + a.early_rest2 >= a.quorum && s0 < a.quorum && s0 + a.early_rest >= a.quorum) {
                     const uint4 *ha = reinterpret_cast<const uint4 *>(a.hb + (uint64_t)A * a.stride) + a.vlo4;
-                    const uint4 *lb = reinterpret_cast<const uint4 *>(a.la + (uint64_t)Bq * a.stride) + a.vlo4;
+                    const uint4 *lb = reinterpret_cast<const uint4 *>(fc_la(a, Bq)) + a.vlo4;
                     uint32_t s1 = 0;
                     n_rest++;
                     for (uint32_t i = lane + 128; i < nv; i += 64) {
@@ -1460,7 +1469,7 @@ __global__ __launch_bounds__(256) void k_fc(FcArgs a) {
     for (uint64_t q = blockIdx.x * qpb + threadIdx.x / LPQ; q < a.n; q += (uint64_t)gridDim.x * qpb) {
         uint32_t A = a.qa_bcast ? a.qa_imm : a.qa[q], Bq = a.qb[q];
         const bool bad = fc_bad(a, A, Bq);
-        if (bad) { A = 0; Bq = 0; }
+        if (bad) { A = a.ev_lo; Bq = a.ev_lo; }
         // FORKS, lane 0: the early-false inputs first (their loads overlap the rows')
         uint32_t e_bb = 0, e_cb = 0;
         if (FORKS && lane == 0) {
@@ -1468,7 +1477,7 @@ __global__ __launch_bounds__(256) void k_fc(FcArgs a) {
             e_cb = a.ev_creator[Bq];
         }
         const uint4 *ha = reinterpret_cast<const uint4 *>(a.hb + (uint64_t)A * a.stride) + a.vlo4;
-        const uint4 *lb = reinterpret_cast<const uint4 *>(a.la + (uint64_t)Bq * a.stride) + a.vlo4;
+        const uint4 *lb = reinterpret_cast<const uint4 *>(fc_la(a, Bq)) + a.vlo4;
         uint4 h[kR], l[kR];
 #pragma unroll
         for (int t = 0; t < kR; t++) {
@@ -1499,7 +1508,7 @@ __global__ __launch_bounds__(256) void k_fc(FcArgs a) {
         uint32_t early = 0;
         if (FORKS) {
             const uint32_t *hrow = a.hb + (uint64_t)A * a.stride;
-            const uint32_t *lrow = a.la + (uint64_t)Bq * a.stride;
+            const uint32_t *lrow = fc_la(a, Bq);
             uint32_t hm = 0;
             if (lane == 0) {
                 const uint32_t hc = a.cmap ? a.cmap[e_bb] : e_bb;   // NONE: another shard's branch
@@ -1576,14 +1585,14 @@ __global__ __launch_bounds__(256) void k_fc_fk(FcArgs a) {
     for (uint64_t q = blockIdx.x * qpb + threadIdx.x / LPQ; q < a.n; q += (uint64_t)gridDim.x * qpb) {
         uint32_t A = a.qa_bcast ? a.qa_imm : a.qa[q], Bq = a.qb[q];
         const bool bad = fc_bad(a, A, Bq);
-        if (bad) { A = 0; Bq = 0; }
+        if (bad) { A = a.ev_lo; Bq = a.ev_lo; }
         uint32_t e_bb = 0, e_cb = 0;
         if (lane == 0) {
             e_bb = a.ev_branch[Bq];
             e_cb = a.ev_creator[Bq];
         }
         const uint4 *ha = reinterpret_cast<const uint4 *>(a.hb + (uint64_t)A * a.stride);
-        const uint4 *lb = reinterpret_cast<const uint4 *>(a.la + (uint64_t)Bq * a.stride);
+        const uint4 *lb = reinterpret_cast<const uint4 *>(fc_la(a, Bq));
         uint4 h[kR], l[kR];
 #pragma unroll
         for (int t = 0; t < kR; t++) {

@@ -20,6 +20,14 @@
 //             (lx_rowseg_la_apply).
 // lx_rowseg_finish sets the own rows' fork marks; then ForklessCause answers
 // queries between own events.
+//
+// Memory: a rank's planes hold its own rows only -- [lo, hi), about 1/G of
+// the epoch (rs_planes) -- plus two receive areas sized by what arrives: the
+// HighestBefore rows its partial events and its LowestAfter pass read from
+// other ranks (rs_rhb, one row per distinct requested row), and the
+// LowestAfter rows of one ForklessCause batch's remote b (rs_rla).  The
+// reference's tables S / s (vecfc/store_vectors.go:26-65) have no epoch-height
+// limit; neither has the G-GPU index: its height per GPU falls as 1/G.
 #include "lx_index.h"
 
 using namespace lxi;
@@ -55,6 +63,8 @@ SegArgs rs_seg_args(lx_index *h) {
     a.own_seg = h->rs_rank * h->rs_sub;
     a.own_lo = h->rs_lo;
     a.per_rank = h->rs_sub;
+    a.rhb = h->rs_rhb;
+    a.hslot = h->rs_hslot;
     return a;
 }
 
@@ -72,7 +82,18 @@ RsArgs rs_args(lx_index *h) {
     r.req = h->rs_req;
     r.req_count = h->rs_ctr;
     r.remaining = h->rs_ctr + 1;
+    r.rhb = h->rs_rhb;
+    r.hslot = h->rs_hslot;
     return r;
+}
+
+// the rank's own rows of an n-event epoch (the bounds rs_begin cuts: Add-order
+// thirds on multiples of 64); hb / la become virtual bases, so every kernel
+// addresses an own row e at plane + e * pstride as in whole planes
+void own_bounds(const lx_index *h, uint32_t n, uint32_t *lo, uint32_t *hi) {
+    const uint32_t G = h->rs_count, k = h->rs_rank;
+    *lo = (uint32_t)((uint64_t)n * k / G / 64 * 64);
+    *hi = k + 1 == G ? n : (uint32_t)((uint64_t)n * (k + 1) / G / 64 * 64);
 }
 
 RsqArgs rsq_args(const lx_index *h) {
@@ -129,11 +150,44 @@ int rs_fix_partials(lx_index *h) {
 
 }  // namespace
 
+int rs_planes(lx_index *h, uint32_t n) {
+    uint32_t lo, hi;
+    own_bounds(h, n, &lo, &hi);
+    const uint64_t rows = hi - lo;
+    if (!h->rs_hb_mem || rows > h->rs_mem_rows || h->rs_mem_pstride != h->pstride) {
+        rs_planes_free(h);
+        HIPCHK(h, dalloc(&h->rs_hb_mem, rows * h->pstride));
+        HIPCHK(h, dalloc(&h->rs_la_mem, rows * h->pstride));
+        // (HB rows are rewritten whole for every branch of the epoch by the
+        // walk; LA is zeroed at the batch: a new allocation starts clean anyway)
+        HIPCHK(h, hipMemsetAsync(h->rs_hb_mem, 0, rows * h->pstride * 4, h->stream));
+        h->rs_mem_rows = rows;
+        h->rs_mem_pstride = h->pstride;
+    }
+    h->hb = h->rs_hb_mem - (uint64_t)lo * h->pstride;
+    h->la = h->rs_la_mem - (uint64_t)lo * h->pstride;
+    return 0;
+}
+
+void rs_planes_free(lx_index *h) {
+    if (!h->rs_hb_mem && !h->rs_la_mem) return;
+    (void)hipStreamSynchronize(h->stream);
+    if (h->rs_hb_mem) (void)hipFree(h->rs_hb_mem);
+    if (h->rs_la_mem) (void)hipFree(h->rs_la_mem);
+    h->rs_hb_mem = h->rs_la_mem = nullptr;
+    h->hb = h->la = nullptr;
+    h->rs_mem_rows = 0;
+    h->rs_mem_pstride = 0;
+}
+
 void rs_free(lx_index *h) {
     void *p[] = {h->rs_need, h->rs_req, h->rs_ctr, h->rs_ids, h->rs_out, h->rs_send,
-                 h->rs_stamp, h->rsq_scratch, h->rsq_list, h->rsq_ctr, h->rsq_tmp};
+                 h->rs_stamp, h->rsq_scratch, h->rsq_list, h->rsq_ctr, h->rsq_tmp,
+                 h->rs_hslot, h->rs_rhb, h->rs_lslot, h->rs_rla};
     for (void *q : p)
         if (q) (void)hipFree(q);
+    h->rs_hslot = h->rs_rhb = h->rs_lslot = h->rs_rla = nullptr;
+    h->rs_hslot_cap = h->rs_rhb_cap = h->rs_lslot_cap = h->rs_rla_cap = 0;
     h->rs_need = h->rs_req = h->rs_ctr = h->rs_ids = h->rs_out = h->rs_send = nullptr;
     h->rs_need_cap = h->rs_req_cap = h->rs_ids_cap = h->rs_out_cap = h->rs_send_cap = h->rs_ctr_cap = 0;
     h->rs_stamp = h->rsq_scratch = h->rsq_list = h->rsq_ctr = nullptr;
@@ -169,6 +223,11 @@ int rs_begin(lx_index *h, IndexArgs ia, const uint32_t *poff, hipStream_t s) {
     h->rs_seg_lo[G * S] = n;
     h->rs_lo = h->rs_seg_lo[k * S];
     h->rs_hi = h->rs_seg_lo[(k + 1) * S];
+    {
+        uint32_t lo, hi;
+        own_bounds(h, n, &lo, &hi);
+        if (lo != h->rs_lo || hi != h->rs_hi) return h->fail(LX_ERR_STATE, "row-segment bounds disagree with the planes");
+    }
     int rc;
     if ((rc = grow_scratch(h, &h->seg_jt, &h->seg_jt_cap, (uint64_t)(G * S + 1) * h->B)) ||
         (rc = grow_scratch(h, &h->seg_cnt, &h->seg_cnt_cap, (uint64_t)h->B + 2 * kMaxSegments)) ||
@@ -176,6 +235,8 @@ int rs_begin(lx_index *h, IndexArgs ia, const uint32_t *poff, hipStream_t s) {
         (rc = grow_scratch(h, &h->seg_plist, &h->seg_plist_cap, (uint64_t)n)) ||
         (rc = grow_scratch(h, &h->seg_elist, &h->seg_elist_cap, (uint64_t)n)) ||
         (rc = grow_scratch(h, &h->rs_need, &h->rs_need_cap, (uint64_t)n)) ||
+        (rc = grow_scratch(h, &h->rs_hslot, &h->rs_hslot_cap, (uint64_t)n)) ||
+        (rc = grow_scratch(h, &h->rs_lslot, &h->rs_lslot_cap, (uint64_t)n)) ||
         (rc = grow_scratch(h, &h->rs_ctr, &h->rs_ctr_cap, (uint64_t)2 + 2 * kMaxSegments)))
         return rc;
     while (h->seg_ev.size() < 6) {
@@ -242,6 +303,9 @@ int rs_begin(lx_index *h, IndexArgs ia, const uint32_t *poff, hipStream_t s) {
     HIPCHK(h, hipMemcpyAsync(&nreq, h->rs_ctr, 4, hipMemcpyDeviceToHost, s));
     HIPCHK(h, hipStreamSynchronize(s));
     h->rs_nreq = nreq;
+    // the receive area: one row per distinct requested row (rs_hslot set by k_rs_refs)
+    if ((rc = grow_scratch(h, &h->rs_rhb, &h->rs_rhb_cap, (uint64_t)std::max<uint32_t>(nreq, 1) * h->pstride)))
+        return rc;
     lx_seg_stats &st = h->seg_stats;
     st = lx_seg_stats{};
     st.segments = G;
@@ -482,8 +546,10 @@ int lx_rowseg_la_store(lx_index *h, uint64_t n, const uint32_t *ids, const uint3
     if ((rc = rs_check(h, 4))) return rc;
     if (n && (!ids || !rows)) return LX_ERR_ARG;
     if (n > 0xFFFFFFFFull) return LX_ERR_ARG;
-    HIPCHK(h, lx::launch_rsq_la_store(rsq_args(h), h->la, h->pstride, ids, (uint32_t)n, rows, h->rs_stamp,
-                                      2 * h->rs_gen + 1, h->stream));
+    // the batch's receive area: row i = ids[i] (one store per batch, after lx_rowseg_fc_need)
+    if ((rc = grow_scratch(h, &h->rs_rla, &h->rs_rla_cap, std::max<uint64_t>(n, 1) * h->pstride))) return rc;
+    HIPCHK(h, lx::launch_rsq_la_store(rsq_args(h), h->rs_rla, h->pstride, ids, (uint32_t)n, rows, h->rs_stamp,
+                                      h->rs_lslot, 2 * h->rs_gen + 1, h->stream));
     return 0;
 }
 

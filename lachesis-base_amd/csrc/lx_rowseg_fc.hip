@@ -12,10 +12,11 @@
 //             batch by a stamp per event: atomicMax to 2 gen), grouped by
 //             owner(b);
 //   serve / store -- their LA rows (B words each) are gathered by owner(b),
-//             moved back and written into the receiving rank's own LA plane
-//             at their own row (those rows are unused there), stamp 2 gen + 1;
-//   then k_fc over the routed pairs: b is valid when own or stamped odd
-//             (a final LA row received in this epoch);
+//             moved back and written into the receiving rank's receive area
+//             (row i of the batch's sorted id list; b_slot[b] = i), stamp
+//             2 gen + 1 -- the planes hold the own rows only;
+//   then k_fc over the routed pairs: b is valid when own or stamped 2 gen + 1
+//             (a final LA row received for this batch);
 //   unroute -- the answers back in the caller's order.
 // For the bench's query shape (b within 64 Lamport of a) only the pairs near
 // a segment boundary cross: a few thousand LA rows per batch.
@@ -97,16 +98,20 @@ __global__ void __launch_bounds__(256) k_rsq_la_gather(RsqArgs a, const uint32_t
     for (uint32_t c = threadIdx.x; c < a.B; c += blockDim.x) dst[c] = own ? src[c] : 0u;
 }
 
-// store: received LA rows into this rank's plane at their own rows, then the
-// arrival stamp (k_fc, a later launch, checks it)
-__global__ void __launch_bounds__(256) k_rsq_la_store(RsqArgs a, uint32_t *la, uint64_t stride, const uint32_t *ids,
-                                                      const uint32_t *rows, uint32_t *stamp, uint32_t arrived) {
+// store: received LA row i into row i of the receive area, then its slot and
+// the arrival stamp (k_fc, a later launch, checks both)
+__global__ void __launch_bounds__(256) k_rsq_la_store(RsqArgs a, uint32_t *la_recv, uint64_t stride,
+                                                      const uint32_t *ids, const uint32_t *rows, uint32_t *stamp,
+                                                      uint32_t *slot, uint32_t arrived) {
     const uint32_t x = ids[blockIdx.x];
-    if (x >= a.n_all || (x >= a.lo && x < a.hi)) return;   // never overwrite an own row
-    uint32_t *dst = la + (uint64_t)x * stride;
+    if (x >= a.n_all || (x >= a.lo && x < a.hi)) return;   // an own row is never received
+    uint32_t *dst = la_recv + (uint64_t)blockIdx.x * stride;
     const uint32_t *src = rows + (uint64_t)blockIdx.x * a.B;
     for (uint32_t c = threadIdx.x; c < a.B; c += blockDim.x) dst[c] = src[c];
-    if (threadIdx.x == 0) stamp[x] = arrived;
+    if (threadIdx.x == 0) {
+        slot[x] = blockIdx.x;
+        stamp[x] = arrived;
+    }
 }
 
 __global__ void k_rsq_unroute(const uint32_t *perm, const uint8_t *ans, uint64_t n, uint8_t *out) {
@@ -175,10 +180,10 @@ hipError_t launch_rsq_la_gather(const RsqArgs &a, const uint32_t *la, uint64_t s
     return hipGetLastError();
 }
 
-hipError_t launch_rsq_la_store(const RsqArgs &a, uint32_t *la, uint64_t stride, const uint32_t *ids, uint32_t n,
-                               const uint32_t *rows, uint32_t *stamp, uint32_t arrived, hipStream_t s) {
+hipError_t launch_rsq_la_store(const RsqArgs &a, uint32_t *la_recv, uint64_t stride, const uint32_t *ids, uint32_t n,
+                               const uint32_t *rows, uint32_t *stamp, uint32_t *slot, uint32_t arrived, hipStream_t s) {
     if (!n) return hipSuccess;
-    hipLaunchKernelGGL(k_rsq_la_store, dim3(n), dim3(256), 0, s, a, la, stride, ids, rows, stamp, arrived);
+    hipLaunchKernelGGL(k_rsq_la_store, dim3(n), dim3(256), 0, s, a, la_recv, stride, ids, rows, stamp, slot, arrived);
     return hipGetLastError();
 }
 

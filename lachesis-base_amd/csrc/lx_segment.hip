@@ -50,6 +50,13 @@ __device__ __forceinline__ uint32_t row_of(const SegArgs &a, uint32_t c, uint32_
     return a.brow[(uint64_t)c * a.s_cap + (s - a.branch_first[c])];
 }
 
+// the final HighestBefore row of event x: at its own index in whole planes and
+// for a row-segment rank's own rows; another rank's row it received in rhb
+__device__ __forceinline__ const uint32_t *seg_hrow(const SegArgs &a, uint32_t x) {
+    if (a.rhb && x < a.own_lo) return a.rhb + (uint64_t)a.hslot[x] * a.stride;
+    return a.hb + (uint64_t)x * a.stride;
+}
+
 // per batch event, without atomics (a branch is a seq-consecutive chain in
 // Add order, so each entry has exactly one writer): the last event of its
 // branch in its segment writes its seq as that segment's entry, the branch's
@@ -88,7 +95,7 @@ __global__ void k_seg_prefix_j(SegArgs a) {
 // streams its columns of those rows eight at a time -- the loads of a group
 // in flight together instead of one brow -> row -> max chain per branch
 __global__ void __launch_bounds__(256) k_seg_partial(SegArgs a, uint32_t k) {
-    extern __shared__ uint32_t refs[];   // <= B referenced rows
+    extern __shared__ const uint32_t *refs[];   // <= B referenced rows (resolved to their storage)
     __shared__ uint32_t n_refs;
     const uint32_t e = a.plist[a.seg_lo[k] - a.bs + blockIdx.x];
     const uint32_t *J = a.jt + (uint64_t)k * a.B;
@@ -97,7 +104,7 @@ __global__ void __launch_bounds__(256) k_seg_partial(SegArgs a, uint32_t k) {
     __syncthreads();
     for (uint32_t c = threadIdx.x; c < a.B; c += blockDim.x) {
         const uint32_t m = min(row[c], J[c]);
-        if (m) refs[atomicAdd(&n_refs, 1u)] = row_of(a, c, m);
+        if (m) refs[atomicAdd(&n_refs, 1u)] = seg_hrow(a, row_of(a, c, m));
     }
     __syncthreads();
     const uint32_t n = n_refs;
@@ -112,7 +119,7 @@ __global__ void __launch_bounds__(256) k_seg_partial(SegArgs a, uint32_t k) {
             uint4 v[U];
 #pragma unroll
             for (uint32_t u = 0; u < U; u++)
-                v[u] = *reinterpret_cast<const uint4 *>(a.hb + (uint64_t)refs[i + u] * a.stride + c0);
+                v[u] = *reinterpret_cast<const uint4 *>(refs[i + u] + c0);
 #pragma unroll
             for (uint32_t u = 0; u < U; u++) {
                 acc[0] = max(acc[0], v[u].x & LX_SEQ_MASK);
@@ -122,7 +129,7 @@ __global__ void __launch_bounds__(256) k_seg_partial(SegArgs a, uint32_t k) {
             }
         }
         for (; i < n; i++) {
-            const uint4 v = *reinterpret_cast<const uint4 *>(a.hb + (uint64_t)refs[i] * a.stride + c0);
+            const uint4 v = *reinterpret_cast<const uint4 *>(refs[i] + c0);
             acc[0] = max(acc[0], v.x & LX_SEQ_MASK);
             acc[1] = max(acc[1], v.y & LX_SEQ_MASK);
             acc[2] = max(acc[2], v.z & LX_SEQ_MASK);
@@ -161,7 +168,7 @@ __global__ void __launch_bounds__(256) k_seg_la_edge(SegArgs a, uint32_t k) {
     const uint32_t j = a.ev_branch[e], sq = a.ev_seq[e];
     const uint32_t *J = a.jt + (uint64_t)k * a.B;
     const uint32_t *re = a.hb + (uint64_t)e * a.stride;
-    const uint32_t *rp = sq > a.branch_first[j] ? a.hb + (uint64_t)row_of(a, j, sq - 1) * a.stride : nullptr;
+    const uint32_t *rp = sq > a.branch_first[j] ? seg_hrow(a, row_of(a, j, sq - 1)) : nullptr;
     for (uint32_t c = threadIdx.x; c < a.B; c += blockDim.x) {
         const uint32_t hi = min(re[c] & LX_SEQ_MASK, J[c]);
         const uint32_t lo = max(rp ? (rp[c] & LX_SEQ_MASK) + 1u : 1u, a.branch_first[c]);
@@ -186,7 +193,11 @@ __global__ void __launch_bounds__(256) k_seg_la_edge(SegArgs a, uint32_t k) {
 
 // ------------------------------------------------------------------ row segments (lx_rowseg.cpp)
 __device__ __forceinline__ void rs_want(const RsArgs &r, uint32_t x) {
-    if (atomicOr(r.need + x, 1u) == 0u) r.req[atomicAdd(r.req_count, 1u)] = x;
+    if (atomicOr(r.need + x, 1u) == 0u) {
+        const uint32_t p = atomicAdd(r.req_count, 1u);
+        r.req[p] = x;
+        r.hslot[x] = p;   // its row in the receive area
+    }
 }
 
 // the rows the partial events of own segment k reference (one workgroup per
@@ -262,7 +273,7 @@ __global__ void __launch_bounds__(256) k_rs_scatter(RsArgs r, const uint32_t *id
                                                     const uint32_t *ready) {
     if (!ready[blockIdx.x]) return;
     const uint32_t x = ids[blockIdx.x];
-    uint32_t *dst = r.hb + (uint64_t)x * r.stride;
+    uint32_t *dst = r.rhb + (uint64_t)r.hslot[x] * r.stride;   // another rank's row: the receive area
     const uint32_t *src = rows + (uint64_t)blockIdx.x * r.B;
     for (uint32_t c = threadIdx.x; c < r.B; c += blockDim.x) dst[c] = src[c];
     if (threadIdx.x == 0 && atomicExch(r.need + x, 0u) == 1u) atomicSub(r.remaining, 1u);
@@ -291,7 +302,7 @@ hipError_t launch_seg_tables(const SegArgs &a, hipStream_t s) {
 
 hipError_t launch_seg_partial(const SegArgs &a, uint32_t k, uint32_t count, hipStream_t s) {
     if (!count) return hipSuccess;
-    hipLaunchKernelGGL(k_seg_partial, dim3(count), dim3(256), (size_t)a.B * 4, s, a, k);
+    hipLaunchKernelGGL(k_seg_partial, dim3(count), dim3(256), (size_t)a.B * sizeof(void *), s, a, k);
     return hipGetLastError();
 }
 

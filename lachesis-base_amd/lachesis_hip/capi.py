@@ -51,6 +51,9 @@ SIGNATURES = [
     ("lx_get_event_branch_id", ctypes.c_int, [vp, ctypes.c_uint32, u32p]),
     ("lx_get_server_stats", ctypes.c_int, [vp, u64p]),
     ("lx_live_handles", ctypes.c_int, []),
+    ("lx_device_bytes", ctypes.c_int, [vp, u64p]),
+    ("lx_get_rows_dev", ctypes.c_int, [vp, ctypes.c_uint32, ctypes.c_uint32, vp, vp, ctypes.c_uint64, vp]),
+    ("lx_row_bytes_max", ctypes.c_int, [vp, u64p]),
     ("lx_get_branches_info", ctypes.c_int, [vp, u32p, u32p, ctypes.c_uint32, u32p]),
     ("lx_shard_of", ctypes.c_int, [vp, u32p, u32p]),
     ("lx_shard_range", ctypes.c_int, [vp, ctypes.c_uint32, u32p, u32p]),
@@ -357,6 +360,13 @@ class Index:
         self._chk(self.L.lx_get_server_stats(self.h, _p(out, u64p)))
         return {"served": int(out[0]), "launches": int(out[1]), "fallbacks": int(out[2])}
 
+    def device_bytes(self):
+        """Device memory this handle holds (lx_device_bytes), bytes."""
+        out = np.zeros(4, dtype=np.uint64)
+        self._chk(self.L.lx_device_bytes(self.h, _p(out, u64p)))
+        return {"planes": int(out[0]), "receive": int(out[1]), "per_event": int(out[2]), "other": int(out[3]),
+                "total": int(out.sum())}
+
     def live_handles(self):
         """Index handles alive in this process (the row server's auto mode)."""
         return int(self.L.lx_live_handles())
@@ -521,6 +531,17 @@ class Index:
         b = np.zeros(G + 1, dtype=np.uint32)
         self._chk(self.L.lx_rowseg_bounds(self.h, _p(b, u32p)))
         return [int(x) for x in b]
+
+    def row_bytes_max(self):
+        """The longest row a getter can return (8 x max(branches, validators))."""
+        b = ctypes.c_uint64()
+        self._chk(self.L.lx_row_bytes_max(self.h, ctypes.byref(b)))
+        return b.value
+
+    def get_rows_dev(self, mode, n, ev_ptr, out_ptr, slot_bytes, len_ptr):
+        """lx_get_rows_dev: rows of n device event ids into a device buffer
+        (row i at out + i * slot_bytes, lengths as uint32; 0xFFFFFFFF: not held)."""
+        self._chk(self.L.lx_get_rows_dev(self.h, mode, n, ev_ptr, out_ptr, slot_bytes, len_ptr))
 
     def rowseg_row_words(self):
         w = ctypes.c_uint32()

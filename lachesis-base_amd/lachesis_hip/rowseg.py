@@ -18,11 +18,19 @@ then connects the segments:
 * LowestAfter -- a rank's range fill reaches rows of earlier segments: those
   entries travel as (row, column, seq) triples to their owners.
 
+A rank's planes hold its own rows only (about 1/G of the epoch, plus receive
+areas for the rows it gets from the others), so a G-GPU index holds an epoch
+G times the height one GPU can.
+
 Afterwards :meth:`RowSegments.forkless_cause_dev` answers ForklessCause of ANY
 pair of the epoch (vecfc/forkless_cause.go:40-82): each rank's queries go to
 owner(a), which holds HB(a); the LowestAfter rows of the b outside its
 segment come from their owners; the answers go back in the caller's order
-(DESIGN.md section 6c).  The reference has no multi-process index
+(DESIGN.md section 6c), and :meth:`RowSegments.get_rows_dev` /
+:meth:`RowSegments.get_rows` answer the vector getters (GetHighestBefore,
+GetLowestAfter, GetMergedHighestBefore; vecfc/store_vectors.go:26-51,
+vecengine/index.go:235-250) for events of every rank the same way: ids to
+their owners, encoded rows back.  The reference has no multi-process index
 (vecfc/index.go is single-node): this is the MI355X scale-out of the same
 computation, bit-exact to the single index (tests/test_gpu_rowseg.py).
 """
@@ -149,3 +157,44 @@ class RowSegments:
         ix.rowseg_fc_unroute(n, perm.data_ptr(), back.data_ptr(), out.data_ptr())
         self.last_fc = {"routed_away": n - send_n[self.rank], "answered": m, "rows_received": nn, "rows_sent": na}
         return self.last_fc
+
+    def get_rows_dev(self, mode, n, ev):
+        """The vector getter rows of this rank's n events (device int32 tensor
+        ``ev``, events of any rank), collectively with every rank: mode 0
+        HighestBefore, 1 LowestAfter, 2 merged HighestBefore (reference byte
+        layouts).  Returns (rows uint8 [n, slot] on the device, lengths int64
+        [n]); a length of 0xFFFFFFFF marks an event outside the epoch."""
+        ix, G = self.ix, self.world
+        slot = (ix.row_bytes_max() + 15) // 16 * 16
+        ra, rb = self._buf("g_ra", n), self._buf("g_rb", n)
+        perm = self._buf("g_perm", n)
+        # owner(ev) routing (the ForklessCause route with b = a), permutation kept
+        send_n = ix.rowseg_fc_route(n, ev.data_ptr(), ev.data_ptr(), ra.data_ptr(), rb.data_ptr(), perm.data_ptr(), G)
+        recv_n = self._counts(send_n)
+        m = sum(recv_n)
+        asked = self._buf("g_asked", m)
+        self._a2a(asked[:m], ra[:n], recv_n, send_n)
+        words = slot // 4
+        rows = self._buf("g_rows", m * words)
+        lens = self._buf("g_lens", m)
+        ix.get_rows_dev(mode, m, asked.data_ptr(), rows.data_ptr(), slot, lens.data_ptr())
+        back = self._buf("g_back", n * words)
+        blen = self._buf("g_blen", n)
+        self._a2a(back[:n * words], rows[:m * words], [c * words for c in send_n], [c * words for c in recv_n])
+        self._a2a(blen[:n], lens[:m], send_n, recv_n)
+        p = perm[:n].long()
+        out = torch.empty((n, words), dtype=torch.int32, device=self.device)
+        out[p] = back[:n * words].view(n, words)
+        olen = torch.empty(n, dtype=torch.int64, device=self.device)
+        olen[p] = blen[:n].long() & 0xFFFFFFFF
+        self.last_get = {"routed_away": n - send_n[self.rank], "answered": m}
+        return out.view(torch.uint8).view(n, slot), olen
+
+    def get_rows(self, mode, events):
+        """get_rows_dev from host event ids: a list of byte rows (None for an
+        event outside the epoch)."""
+        import numpy as np
+        ev = torch.from_numpy(np.ascontiguousarray(events, dtype=np.uint32).view(np.int32)).to(self.device)
+        rows, lens = self.get_rows_dev(mode, len(events), ev)
+        rows, lens = rows.cpu().numpy(), lens.cpu().numpy()
+        return [None if int(k) == 0xFFFFFFFF else bytes(rows[i, :int(k)]) for i, k in enumerate(lens)]

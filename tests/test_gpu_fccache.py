@@ -283,7 +283,7 @@ def test_back_to_back_row_fills_different_asking_events(lx, fork):
     its own asking event's answers -- then read back as hits and compared with
     the oracle (vecfc/forkless_cause.go:28-38: a cached answer is the answer)."""
     V = 100
-    d = lx.tools.gen_dag(V, 40, 10, cheaters=4 if fork else 0, forks=3 if fork else 0, seed=17)
+    d = lx.tools.gen_dag(V, 100, 10, cheaters=4 if fork else 0, forks=3 if fork else 0, seed=17)
     w = [(1 << 12) // (i + 1) + 1 for i in range(V)]
     N = len(d)
     o = _oracle(d, w, N)
@@ -297,8 +297,9 @@ def test_back_to_back_row_fills_different_asking_events(lx, fork):
     bs = list(range(N - 3000, N, 64))
     for b in bs:
         assert ix.forkless_cause(N - 1, b) == bool(o.forkless_cause(N - 1, b))
-    # back-to-back misses, each a new asking event with one question
-    asks = [int(x) for x in rng.choice(np.arange(N // 2, N - 1), 300, replace=False)]
+    # back-to-back misses, each a new asking event (not in the working set: a
+    # row fill of its own, no tile fill) with one question
+    asks = [int(x) for x in rng.choice(np.arange(N // 4, N - 3100), 300, replace=False)]
     for a in asks:
         b = int(rng.integers(N - 3000, N))
         assert ix.forkless_cause(a, b) == bool(o.forkless_cause(a, b)), (a, b)

@@ -5,7 +5,9 @@ walk only their own Add-order segment and run RowSegments.exchange (row
 requests in rounds, LowestAfter triples to their owners).  Every rank's own
 HighestBefore / LowestAfter rows must equal an ordinary single index's rows,
 byte for byte (that index is pinned to the oracle by the parity tests), and
-its ForklessCause answers between own events must equal the C oracle's."""
+its ForklessCause answers between own events must equal the C oracle's, and
+so must ForklessCause of any pair and the vector getters of events on any
+rank, routed to their owners.  A rank's planes hold only its own rows."""
 
 import ctypes
 import multiprocessing as mp
@@ -93,6 +95,25 @@ def _worker(rank, world, port, q, shape, sub=0):
         fc = rs.forkless_cause_dev(k, ta, tb, out)
         ok = ok and bool(np.array_equal(out.cpu().numpy(), o.forkless_cause_batch(qa2, qb2)))
         info = dict(info, fc=fc)
+        # the vector getters of events on EVERY rank (RowSegments.get_rows:
+        # ids to their owners, encoded rows back) and of own events directly
+        ev = [int(x) for x in rng.integers(0, N, 150)] + [0, N - 1]
+        for mode, want in ((0, o.hb), (1, o.la), (2, o.merged_hb)):
+            rows = rs.get_rows(mode, ev)
+            ok = ok and all(r == want(e) for r, e in zip(rows, ev))
+        ok = ok and rs.get_rows(0, [N + 5])[0] is None
+        own = [int(x) for x in rng.integers(lo, hi, 20)]
+        ok = ok and all(ix.highest_before(e) == o.hb(e) and ix.lowest_after(e) == o.la(e) and
+                        ix.merged_highest_before(e) == o.merged_hb(e) for e in own)
+        try:
+            ix.highest_before(lo - 1 if lo else hi)      # another rank's row: routed, not answered here
+            ok = False
+        except Exception:
+            pass
+        # the planes hold the own rows only
+        mem = ix.device_bytes()
+        info = dict(info, planes=mem["planes"], plane_rows=(hi - lo), stride=ix.device_planes()[2])
+        ok = ok and mem["planes"] == 2 * 4 * (hi - lo) * ix.device_planes()[2]
         q.put((rank, ok, info))
     except Exception as e:   # report instead of hanging the other ranks' queue reads
         q.put((rank, False, repr(e)))
