@@ -518,6 +518,8 @@ def main():
     ap.add_argument("--no-dropin", action="store_true", help="skip the configs[4] drop-in (unchanged caller) leg")
     ap.add_argument("--no-latency", action="store_true", help="skip the per-call latency / antichain-fed leg")
     ap.add_argument("--no-configs", action="store_true", help="skip the secondary C1/C2/C4 lines")
+    ap.add_argument("--no-colshard", action="store_true",
+                    help="N > 1 row segments: skip the column-shard leg of the same run (BASELINE configs[2])")
     ap.add_argument("--segments", type=int, default=0,
                     help="single GPU: walk the epoch as G Add-order segments + fix-up (option segments, the "
                          "per-rank work of the row-segment multi-GPU mode timed segment by segment)")
@@ -550,10 +552,10 @@ def main():
 
     import lachesis_hip as lx
 
-    V, epv, P, cheaters, forks, wkind = CONFIGS[args.config]
+    V, epv, P_, cheaters, forks, wkind = CONFIGS[args.config]
     weights = weights_for(V, wkind)
     t_gen = time.perf_counter()
-    dag = lx.tools.gen_dag(V, epv, P, cheaters, forks, seed=1)
+    dag = lx.tools.gen_dag(V, epv, P_, cheaters, forks, seed=1)
     if args.order == "level":
         dag = lx.tools.level_order(dag)
     # every rank asks 2^k queries of the same shape (a uniform over the epoch, b
@@ -580,158 +582,214 @@ def main():
 
     shard = args.mode == "shard" and world > 1
     solo = args.shard_solo if world == 1 and args.shard_solo > 1 else 0
-    if solo:
-        ix = lx.Index(device=local, event_capacity=N, shard_rank=0, shard_count=solo)
-        d_part = torch.empty(args.fc_queries, dtype=torch.int32, device=dev)
-        d_blk = None
-    elif rowseg:
-        ix = lx.Index(device=local, event_capacity=N, options={"seg_count": world, "seg_rank": rank})
-        from lachesis_hip.rowseg import RowSegments
-        rsx = RowSegments(ix, device=dev)
-    elif shard:
-        ix = lx.Index(device=local, event_capacity=N, shard_rank=rank, shard_count=world)
-        from lachesis_hip.shard import ShardedIndex
-        sx = ShardedIndex(ix, device=dev)
-        d_part = torch.empty(args.fc_queries, dtype=torch.int32, device=dev)
-    else:
-        ix = lx.Index(device=local, event_capacity=N, options={"segments": args.segments} if args.segments > 1 else None)
-
-    st_x = []   # shard mode: LowestAfter all-to-all (pack + collective + unpack) per step, ms
-
-    def index_step():
-        ix.reset(weights)
-        st_idx = 0.0
-        st_asg = 0.0
-        for lo, hi, off, pbase in batches:
-            ix.add_batch_dev(hi - lo, d_creator.data_ptr() + 4 * lo, d_seq.data_ptr() + 4 * lo,
-                             off.data_ptr(), d_par.data_ptr() + 4 * pbase)
-            s = ix.last_stats()
-            st_idx += s["ms_index"]
-            st_asg += s["ms_assign"] + s["ms_marks"]
-        if shard:
-            tx = time.perf_counter()
-            sx.exchange()
-            st_x.append((time.perf_counter() - tx) * 1e3)
-        if rowseg:
-            tx = time.perf_counter()
-            rsx.exchange()
-            st_x.append((time.perf_counter() - tx) * 1e3)
-        if solo:
-            nonlocal d_blk
-            sizes = [ix.shard_block(0, t) for t in range(1, solo)]
-            if d_blk is None:
-                d_blk = torch.empty(max(sizes + [1]), dtype=torch.int32, device=dev)
-            for t in range(1, solo):
-                ix.la_pack_dev(t, d_blk.data_ptr())
-            ix.la_own_dev()
-        return st_idx, st_asg
-
-    _, _, _, stream_ptr = ix.device_planes()
-    lib_stream = torch.cuda.ExternalStream(stream_ptr, device=dev)
-
-    def fc_step(evs=None):
-        if evs is not None:
-            evs[0].record(lib_stream)
-        if shard or solo:
-            ix.forkless_cause_partial_dev(args.fc_queries, d_qa.data_ptr(), d_qb.data_ptr(), d_part.data_ptr())
-        elif rowseg:
-            # any pair: queries to owner(a), remote LowestAfter rows to it, answers
-            # back; the HIP events then bracket the whole protocol
-            rsx.forkless_cause_dev(args.fc_queries, d_qa, d_qb, d_out)
-        else:
-            ix.forkless_cause_batch_dev(args.fc_queries, d_qa.data_ptr(), d_qb.data_ptr(), d_out.data_ptr())
-        if evs is not None:
-            evs[1].record(lib_stream)
-        if shard:
-            ix.sync()
-            sx.all_reduce_sum(d_part)   # int32 wrap-around = exact uint32 sum
-            torch.cuda.current_stream(dev).synchronize()
-            ix.fc_combine_dev(args.fc_queries, d_part.data_ptr(), d_out.data_ptr())
 
     def barrier():
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize(dev)
 
-    def max_over_ranks(x):
+    def reduce_over_ranks(x, op):
         if world == 1:
             return x
         t = torch.tensor([x], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t, op=op)
         return float(t.item())
 
-    # ---- index: warmup + K timed steps
-    for _ in range(args.warmup):
-        index_step()
-    barrier()
-    t0 = time.perf_counter()
-    k_index_ms, k_assign_ms = [], []
-    for _ in range(args.steps):
-        a, b = index_step()
-        k_index_ms.append(a)
-        k_assign_ms.append(b)
-    barrier()
-    t_index = max_over_ranks(time.perf_counter() - t0)
+    def max_over_ranks(x):
+        return reduce_over_ranks(x, dist.ReduceOp.MAX) if world > 1 else x
 
-    # ---- FC: warmup + K timed steps (HIP events on the library's stream)
-    for _ in range(args.warmup):
-        fc_step()
-    ix.sync()
-    barrier()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    if not (shard or solo or rowseg):
+    def sum_over_ranks(x):
+        return reduce_over_ranks(x, dist.ReduceOp.SUM) if world > 1 else x
+
+    def fc_bytes_read(nq, B, early):
+        """Bytes k_fc reads for nq queries over rows of B branches: whole rows
+        (8 B per branch: HB(a) 4 B + LA(b) 4 B) without the early exit; with it
+        (device counters: queries decided on the early path, of them past the
+        first round, past the second) 2 x 1 KB per early-path query (the 256
+        heaviest columns of both rows), 2 x 1 KB more past the first round, the
+        rest of both rows past the second."""
+        qe, q2, qw = early
+        row16 = ((B + 3) // 4) * 16
+        return qe * 2048.0 + q2 * 2048.0 + qw * 2.0 * max(0, row16 - 2048) + (nq - qe) * 8.0 * B
+
+    def leg(kind):
+        """One index + ForklessCause measurement: kind 'single' (one GPU, or
+        one independent epoch per rank), 'solo' (rank 0 of a column shard
+        alone), 'rowseg' (the epoch as Add-order row segments, one per rank),
+        'shard' (the epoch's creator columns split over the ranks).  Warmup +
+        K timed steps each, barrier + device sync on both sides, the max over
+        ranks; k_fc timed by HIP events on the library's stream."""
+        if kind == "solo":
+            ix = lx.Index(device=local, event_capacity=N, shard_rank=0, shard_count=solo)
+            d_part = torch.empty(args.fc_queries, dtype=torch.int32, device=dev)
+        elif kind == "rowseg":
+            ix = lx.Index(device=local, event_capacity=N, options={"seg_count": world, "seg_rank": rank})
+            from lachesis_hip.rowseg import RowSegments
+            rsx = RowSegments(ix, device=dev)
+        elif kind == "shard":
+            ix = lx.Index(device=local, event_capacity=N, shard_rank=rank, shard_count=world)
+            from lachesis_hip.shard import ShardedIndex
+            sx = ShardedIndex(ix, device=dev)
+            d_part = torch.empty(args.fc_queries, dtype=torch.int32, device=dev)
+        else:
+            ix = lx.Index(device=local, event_capacity=N,
+                          options={"segments": args.segments} if args.segments > 1 else None)
+        st_x = []   # shard / rowseg: the exchange of each step, ms
+        d_blk = None
+
+        def index_step():
+            nonlocal d_blk
+            ix.reset(weights)
+            st_idx = 0.0
+            st_asg = 0.0
+            for lo, hi, off, pbase in batches:
+                ix.add_batch_dev(hi - lo, d_creator.data_ptr() + 4 * lo, d_seq.data_ptr() + 4 * lo,
+                                 off.data_ptr(), d_par.data_ptr() + 4 * pbase)
+                s = ix.last_stats()
+                st_idx += s["ms_index"]
+                st_asg += s["ms_assign"] + s["ms_marks"]
+            if kind == "shard":
+                tx = time.perf_counter()
+                sx.exchange()
+                st_x.append((time.perf_counter() - tx) * 1e3)
+            if kind == "rowseg":
+                tx = time.perf_counter()
+                rsx.exchange()
+                st_x.append((time.perf_counter() - tx) * 1e3)
+            if kind == "solo":
+                sizes = [ix.shard_block(0, t) for t in range(1, solo)]
+                if d_blk is None:
+                    d_blk = torch.empty(max(sizes + [1]), dtype=torch.int32, device=dev)
+                for t in range(1, solo):
+                    ix.la_pack_dev(t, d_blk.data_ptr())
+                ix.la_own_dev()
+            return st_idx, st_asg
+
+        _, _, _, stream_ptr = ix.device_planes()
+        lib_stream = torch.cuda.ExternalStream(stream_ptr, device=dev)
+        kern_ms = []
+
+        def fc_step(evs=None):
+            if evs is not None:
+                evs[0].record(lib_stream)
+            if kind in ("shard", "solo"):
+                ix.forkless_cause_partial_dev(args.fc_queries, d_qa.data_ptr(), d_qb.data_ptr(), d_part.data_ptr())
+            elif kind == "rowseg":
+                # any pair: queries to owner(a), remote LowestAfter rows to it,
+                # answers back (DESIGN.md 6c); k_fc itself timed inside
+                rsx.forkless_cause_dev(args.fc_queries, d_qa, d_qb, d_out, timing=evs is not None)
+            else:
+                ix.forkless_cause_batch_dev(args.fc_queries, d_qa.data_ptr(), d_qb.data_ptr(), d_out.data_ptr())
+            if evs is not None:
+                evs[1].record(lib_stream)
+            if kind == "shard":
+                ix.sync()
+                sx.all_reduce_sum(d_part)   # int32 wrap-around = exact uint32 sum
+                torch.cuda.current_stream(dev).synchronize()
+                ix.fc_combine_dev(args.fc_queries, d_part.data_ptr(), d_out.data_ptr())
+            if evs is not None and kind == "rowseg":
+                kern_ms.append(rsx.last_fc["kernel_ms"])
+
+        # ---- index: warmup + K timed steps
+        for _ in range(args.warmup):
+            index_step()
+        barrier()
+        t0 = time.perf_counter()
+        k_index_ms, k_assign_ms = [], []
+        for _ in range(args.steps):
+            a, b = index_step()
+            k_index_ms.append(a)
+            k_assign_ms.append(b)
+        barrier()
+        t_index = max_over_ranks(time.perf_counter() - t0)
+
+        # ---- FC: warmup + K timed steps
+        for _ in range(args.warmup):
+            fc_step()
+        ix.sync()
+        barrier()
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
         ix.fc_early_counters()          # reset (the warmup's launches)
-    t1 = time.perf_counter()
-    for k in range(args.steps):
-        fc_step(evs[k])
-    ix.sync()
-    barrier()
-    t_fc = max_over_ranks(time.perf_counter() - t1)
-    fc_kernel_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
-    # k_fc's early exit (option fc_early): queries decided
-    # by the 256 heaviest columns read 2 x 1 KB, the others both whole rows
-    fc_early_q, fc_second_q, fc_full_q = ix.fc_early_counters() if not (shard or solo or rowseg) else (0, 0, 0)
+        t1 = time.perf_counter()
+        for k in range(args.steps):
+            fc_step(evs[k])
+        ix.sync()
+        barrier()
+        t_fc = max_over_ranks(time.perf_counter() - t1)
+        step_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
+        # k_fc's own time on this rank: the launch (single / shard partial), or
+        # the launch inside the row-segment protocol (the rest is routing)
+        fc_kernel_ms = float(np.mean(kern_ms)) if kind == "rowseg" else step_ms
+        early = ix.fc_early_counters()
+        # the queries this rank's k_fc answered per step: its own, or (row
+        # segments) the ones routed to it as owner(a)
+        nq = rsx.last_fc["answered"] if kind == "rowseg" else args.fc_queries
+        B = ix.num_branches()
+        if kind in ("shard", "solo"):
+            lo_c, hi_c = ix.shard_range(rank if kind == "shard" else 0)
+            B = hi_c - lo_c                 # columns this rank streams (no forks in the bench DAG)
+        fc_read = fc_bytes_read(nq * args.steps, B, early) / args.steps
+        # per-GPU bandwidth over all ranks: sum of the ranks' bytes over the sum
+        # of their k_fc times (equal to the rank's own at N = 1)
+        fc_read_all = sum_over_ranks(fc_read)
+        fc_ms_all = sum_over_ranks(fc_kernel_ms)
+        early_all = [sum_over_ranks(float(x)) for x in early]
+        nq_all = sum_over_ranks(float(nq))
+        out = {"ix": ix, "kind": kind, "t_index": t_index, "t_fc": t_fc, "k_index_ms": k_index_ms,
+               "k_assign_ms": k_assign_ms, "fc_kernel_ms": fc_kernel_ms, "fc_step_ms": step_ms, "B": B,
+               "fc_read": fc_read, "fc_achieved": fc_read_all / (fc_ms_all * 1e-3) / 1e9,
+               "fc_kernel_ms_max": max_over_ranks(fc_kernel_ms),
+               "early": {"queries": int(early_all[0]), "second_round": int(early_all[1]),
+                         "whole_rows": int(early_all[2]), "answered": int(nq_all) * args.steps}
+               if early_all[0] else None,
+               "whole_row_bytes": 8.0 * B * nq, "st_x": st_x,
+               "mem": ix.device_bytes()}
+        if kind == "rowseg":
+            out["rsx"] = rsx
+        if kind == "shard":
+            out["sx"] = sx
+        return out
+
+    primary = "solo" if solo else "rowseg" if rowseg else "shard" if shard else "single"
+    P = leg(primary)
+    ix = P["ix"]
+    k_index_ms, k_assign_ms, t_index, t_fc = P["k_index_ms"], P["k_assign_ms"], P["t_index"], P["t_fc"]
+    fc_kernel_ms = P["fc_kernel_ms"]
+    B = P["B"]
 
     # correctness spot check: this run's first 4096 ForklessCause answers
     # recomputed on the host from the index's own HighestBefore / LowestAfter
-    # rows (reference byte layouts through the batched getters):
-    # sum of stakes over branches j with 0 < LA(b)[j] <= HB(a)[j].Seq >= quorum
-    # (vecfc/forkless_cause.go:63-82; the bench DAG has no forks)
+    # rows (reference byte layouts through the batched getters; row segments:
+    # routed to their owners): sum of stakes over branches j with
+    # 0 < LA(b)[j] <= HB(a)[j].Seq >= quorum (vecfc/forkless_cause.go:63-82;
+    # the bench DAG has no forks)
     spot_n = 0
-    if not (shard or solo or rowseg):
-        import numpy as np
+    if primary in ("single", "rowseg"):
         qa_s, qb_s = qa[:4096], qb[:4096]
         got = d_out[:4096].cpu().numpy()
-        _, hbb = ix.rows_np(0, qa_s)
-        _, lab = ix.rows_np(1, qb_s)
-        hbs = hbb.view(np.uint32).reshape(len(qa_s), -1, 2)[:, :V, 0].astype(np.int64)
-        las = lab.view(np.uint32).reshape(len(qb_s), -1)[:, :V].astype(np.int64)
+        if primary == "rowseg":
+            hb_rows = P["rsx"].get_rows(0, qa_s)
+            la_rows = P["rsx"].get_rows(1, qb_s)
+            hbs = np.stack([np.frombuffer(r, dtype=np.uint32)[0::2][:V] for r in hb_rows]).astype(np.int64)
+            las = np.stack([np.frombuffer(r, dtype=np.uint32)[:V] for r in la_rows]).astype(np.int64)
+        else:
+            _, hbb = ix.rows_np(0, qa_s)
+            _, lab = ix.rows_np(1, qb_s)
+            hbs = hbb.view(np.uint32).reshape(len(qa_s), -1, 2)[:, :V, 0].astype(np.int64)
+            las = lab.view(np.uint32).reshape(len(qb_s), -1)[:, :V].astype(np.int64)
         wv = np.asarray(weights, dtype=np.int64)
         stake = (((las > 0) & (las <= hbs)) * wv).sum(axis=1)
         want = (stake >= ix.quorum()).astype(np.uint8)
         assert np.array_equal(got, want), "ForklessCause spot check failed"
-        spot_n = len(got)
+        spot_n = int(sum_over_ranks(float(len(got))))
 
     units = 1 if (shard or rowseg) else world          # shard / rowseg: the ranks share one epoch
     fc_units = 1 if shard else world                   # rowseg / replica: every rank asks its own 2^k queries
     events_per_s = N * args.steps * units / t_index
     fc_per_s = args.fc_queries * args.steps * fc_units / t_fc
-    B = ix.num_branches()
-    if shard or solo:
-        lo, hi = ix.shard_range(rank)
-        B = hi - lo                         # columns this rank streams (no forks in the bench DAG)
-    fc_bytes = 8.0 * B * args.fc_queries                       # HB(a).Seq 4B + LA(b) 4B per branch
-    # bytes k_fc reads per launch: whole rows (8 B per branch) without the
-    # early exit; with it 2 x 1 KB (the 256 heaviest columns of both rows) per
-    # query, 2 x 1 KB more past the first round, the rest of both rows
-    # (2 x (row - 2 KB)) past the second
-    fc_read = fc_bytes
-    if fc_early_q:
-        row16 = ((B + 3) // 4) * 16
-        ef = min(1.0, fc_early_q / (args.fc_queries * args.steps))   # queries launched with the early exit
-        f2, fw = fc_second_q / fc_early_q, fc_full_q / fc_early_q
-        fc_read = args.fc_queries * (ef * (2048 + 2048 * f2 + 2 * max(0, row16 - 2048) * fw) + (1 - ef) * 8.0 * B)
-    fc_achieved = fc_read / (fc_kernel_ms * 1e-3) / 1e9
+    fc_bytes = P["whole_row_bytes"]
+    fc_read = P["fc_read"]
+    fc_achieved = P["fc_achieved"]
     kidx = float(np.mean(k_index_ms))
     # index algorithmic bytes/event: (P+1)*4*B parent+own HB + 4*B LA + 8 B metadata (SURVEY 8d)
     p_mean = float(len(dag.par)) / N
@@ -745,15 +803,19 @@ def main():
     # walked as side-by-side segments, else k_index; the traffic
     # figure must be that kernel's own, or null
     walk_kernel = "k_index"
-    if not (shard or rowseg or solo):
+    if primary in ("single", "rowseg"):
         sg0 = ix.segment_stats()
-        if sg0["segments"] >= 2 and sg0["one_launch"]:
+        if primary == "rowseg" or (sg0["segments"] >= 2 and sg0["one_launch"]):
             walk_kernel = "k_index_segs"
     idx_traffic = traffic.get(walk_kernel) if traffic else None
-    # compulsory HBM bytes of the walk: every HB and LA row of the epoch written
-    # once at the plane's row stride (8 * stride bytes per event)
+    # compulsory HBM bytes of the walk: every HB and LA row this rank walks
+    # written once at the plane's row stride (8 * stride bytes per event)
     plane_stride = ix.device_planes()[2]
-    idx_compulsory = 8.0 * plane_stride * N
+    walked = N
+    if primary == "rowseg":
+        r0, r1 = ix.rowseg_range()
+        walked = r1 - r0
+    idx_compulsory = 8.0 * plane_stride * walked
     result = {
         "metric": "events indexed/sec + ForklessCause queries/sec at 1000 validators, 1/2/4/8 GPU",
         "value": events_per_s,
@@ -768,8 +830,8 @@ def main():
         "dtype": "u32",
         "data": "synthetic tdag-structured DAG (splitmix64 seed 1), no forks",
         "config": {"workload": "%s: V=%d, %d events (%d/validator), P=%d, %s stakes, cheaters=%d; FC 2^%d queries, b within 64 Lamport of a"
-                   % (args.config, V, N, epv, P, wkind, cheaters, int(np.log2(args.fc_queries)), ),
-                   "validators": V, "events": N, "parents": P, "fc_queries": args.fc_queries,
+                   % (args.config, V, N, epv, P_, wkind, cheaters, int(np.log2(args.fc_queries)), ),
+                   "validators": V, "events": N, "parents": P_, "fc_queries": args.fc_queries,
                    "parallelism": ("solo-shard0-of-%d" % solo) if solo else
                                   ("colshard%d" if shard else "rowseg%d" if rowseg else "replica%d") % world,
                    "batch": batch},
@@ -780,14 +842,19 @@ def main():
         "roofline": {"bound": "hbm", "kernel": "k_fc (ForklessCause)", "achieved": fc_achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": fc_achieved / HBM_PEAK_GBS,
                      "bytes_read_per_launch": fc_read,
-                     "early_exit": {"queries": fc_early_q, "second_round": fc_second_q, "whole_rows": fc_full_q,
-                                    "note": "queries the 256 heaviest validators' columns decide read 2 x 1 KB, "
-                                            "the next 256 columns 2 x 1 KB more, the rest only past both; "
-                                            "achieved = bytes_read_per_launch / kernel time; "
-                                            "algorithmic_bytes_per_launch is SURVEY 8d's whole-row figure"} if fc_early_q else None,
+                     "early_exit": dict(P["early"], note="device counters summed over the ranks: queries the 256 "
+                                        "heaviest validators' columns decide read 2 x 1 KB, the next 256 columns 2 x 1 KB "
+                                        "more, the rest only past both; achieved = the ranks' bytes read / the sum of "
+                                        "their k_fc times (per-GPU bandwidth); algorithmic_bytes_per_launch is SURVEY "
+                                        "8d's whole-row figure") if P["early"] else None,
                      "traffic": traffic["k_fc"]["hbm_bytes"] if traffic and "k_fc" in traffic else None,
                      "traffic_source": traffic_src,
-                     "algorithmic_bytes_per_launch": fc_bytes, "kernel_ms": fc_kernel_ms},
+                     "algorithmic_bytes_per_launch": fc_bytes, "kernel_ms": fc_kernel_ms,
+                     "kernel_ms_max_over_ranks": P["fc_kernel_ms_max"],
+                     "whole_row_equiv_frac": fc_bytes / (fc_kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                     "whole_row_equiv_note": "SURVEY 8d's whole-row bytes (8 B per branch per query) over the kernel "
+                                             "time: above 1 when the early exit skips most of the rows -- a rate of "
+                                             "answered queries, not HBM use"},
         "roofline_index": {"bound": "latency (DAG depth x pass latency); hbm ceiling", "kernel": walk_kernel,
                            "achieved": idx_compulsory / (kidx * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                            "frac": idx_compulsory / (kidx * 1e-3) / 1e9 / HBM_PEAK_GBS,
@@ -799,11 +866,12 @@ def main():
                            "algorithmic_bytes_per_launch": idx_bytes,
                            "survey_formula_achieved": idx_achieved,
                            "survey_formula_frac": idx_achieved / HBM_PEAK_GBS,
-                           "note": "achieved / frac: the compulsory HBM bytes (every HB and LA row written once, "
-                                   "8 x row stride bytes per event) over the kernel time; survey_formula_* follow "
-                                   "SURVEY 8d's per-event formula, which also counts every parent-row read -- the "
-                                   "walker serves those from LDS, so it can exceed the HBM peak: the walk is "
-                                   "latency-bound (DAG depth x pass latency)"},
+                           "note": "achieved / frac: the compulsory HBM bytes (every HB and LA row this rank walks "
+                                   "written once, 8 x row stride bytes per event) over the kernel time; "
+                                   "survey_formula_* follow SURVEY 8d's per-event formula, which also counts every "
+                                   "parent-row read -- the walker serves those from LDS, so it can exceed the HBM "
+                                   "peak: the walk is latency-bound (DAG depth x pass latency)"},
+        "device_bytes_per_rank": P["mem"],
         "host_gen_s": t_gen,
         "fc_spot_checked": spot_n,
     }
@@ -817,21 +885,54 @@ def main():
         result["segments"] = sg
     if rowseg:
         sg = ix.segment_stats()
+        rsx = P["rsx"]
         result["rowseg"] = {"rows": [int(x) for x in ix.rowseg_range()], "walk_ms": sg["walk_ms"][rank],
                             "partial_events": sg["partial"][rank], "partial_ms": sg["partial_ms"], "la_ms": sg["la_ms"],
-                            "exchange_ms": float(np.mean(st_x[-args.steps:])) if st_x else None,
+                            "exchange_ms": float(np.mean(P["st_x"][-args.steps:])) if P["st_x"] else None,
                             "exchange": rsx.last, "fc": rsx.last_fc,
+                            "fc_kernel_ms": fc_kernel_ms, "fc_protocol_ms": P["fc_step_ms"] - fc_kernel_ms,
+                            "fc_step_ms": P["fc_step_ms"],
+                            "device_bytes": P["mem"],
                             "note": "index step = assignment of every event + walk of the own segment + row "
                                     "requests, partial fix-up, LowestAfter pass and triples (exchange_ms), timed "
                                     "inside value; FC: every rank asks 2^k queries of the N=1 shape over the whole "
                                     "epoch, routed to owner(a) with the LowestAfter rows of remote b shipped to it "
-                                    "(DESIGN.md 6c), timed inside fc_queries_per_sec"}
+                                    "(DESIGN.md 6c), timed inside fc_queries_per_sec; fc_kernel_ms = k_fc alone, "
+                                    "fc_protocol_ms = the routing around it (rank 0)"}
     if shard or solo:
+        sx = P.get("sx")
         wire = sorted(set(w for w in sx.last_wire[0] if w)) if shard and getattr(sx, "last_wire", None) else \
             [ix.shard_wire_bytes()]
         result["shard"] = {"columns": B, "wire_bytes_per_entry": wire,
-                           "exchange_ms": float(np.mean(st_x[-args.steps:])) if st_x else None,
+                           "exchange_ms": float(np.mean(P["st_x"][-args.steps:])) if P["st_x"] else None,
                            "note": "index step = walk of own columns + LowestAfter all-to-all (timed inside value)"}
+    if rowseg and not args.no_colshard:
+        # BASELINE configs[2] as it names it: the same epoch column-sharded over
+        # the same ranks (north_star (5)); the row-segment handle is freed first
+        ix.close()
+        C = leg("shard")
+        cx = C["ix"]
+        sx = C["sx"]
+        result["colshard"] = {
+            "events_per_sec": N * args.steps / C["t_index"], "ms_per_step": C["t_index"] / args.steps * 1e3,
+            "fc_queries_per_sec": args.fc_queries * args.steps / C["t_fc"],
+            "fc_ms_per_step": C["t_fc"] / args.steps * 1e3,
+            "index_kernel_ms": float(np.mean(C["k_index_ms"])),
+            "exchange_ms": float(np.mean(C["st_x"][-args.steps:])) if C["st_x"] else None,
+            "columns": C["B"], "wire_bytes_per_entry": sorted(set(w for w in sx.last_wire[0] if w))
+            if getattr(sx, "last_wire", None) else None,
+            "roofline": {"bound": "hbm", "kernel": "k_fc partial (own columns)", "achieved": C["fc_achieved"],
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": C["fc_achieved"] / HBM_PEAK_GBS,
+                         "bytes_read_per_launch": C["fc_read"], "algorithmic_bytes_per_launch": C["whole_row_bytes"],
+                         "kernel_ms": C["fc_kernel_ms"], "kernel_ms_max_over_ranks": C["fc_kernel_ms_max"]},
+            "device_bytes": C["mem"],
+            "scaling": "strong",
+            "note": "the epoch's creator columns split over the ranks (DESIGN.md 6): each rank walks its columns of "
+                    "every event, the LowestAfter all-to-all makes the shards FC-ready (inside events_per_sec), FC "
+                    "sums the ranks' partial stakes with an all-reduce (inside fc_queries_per_sec); every rank "
+                    "answers the same 2^k queries"}
+        cx.close()
+        ix = cx
 
     if not args.no_latency and world == 1 and not solo:
         ix.close()   # free the bench epoch's planes first

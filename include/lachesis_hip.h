@@ -83,8 +83,9 @@ const char *lx_last_error(const lx_index *h);
  *                The result matrix is W^2 bytes of PINNED host memory per handle (64 MiB at
  *                8192, 256 MiB at the 16384 maximum), allocated on the first lx_forkless_cause;
  *                if it cannot be pinned the handle answers through lx_forkless_cause_batch
- *   "seg_count", "seg_rank"  G in 2..64 and r < G, before lx_reset: a row-segment rank
- *                (lx_rowseg_*, below); 0 = off
+ *   "seg_count", "seg_rank"  G in 1..64 and r < G, before lx_reset: a row-segment rank
+ *                (lx_rowseg_*, below; G = 1: one rank holding the whole epoch, every
+ *                exchange and route run with nothing to move); 0 = off
  *   "seg_sub"    row-segment rank: its own segment walked as this many side-by-side
  *                sub-segments (0: auto, as "seg_auto" would split the rank's share; the
  *                same value on every rank of a job)
@@ -408,11 +409,14 @@ int lx_last_segment_stats(const lx_index *h, lx_seg_stats *out);
  *     device buffer; each owner lx_rowseg_la_apply's what it gets;
  * then lx_rowseg_finish.  After it, ForklessCause answers queries between own
  * events, and any pair of the epoch through the cross-rank protocol below;
- * getters, write-back, DropNotFlushed and the abft / emitter views need a whole
- * index (LX_ERR_STATE).  Every call has completed on the device when it
- * returns. */
+ * the vector getters answer own events (another rank's: LX_ERR_STATE; the
+ * caller routes them, lachesis_hip/rowseg.py get_rows over lx_get_rows_dev);
+ * write-back, DropNotFlushed and the abft / emitter views need a whole index
+ * (LX_ERR_STATE).  The planes hold the own rows only (plus receive areas for
+ * rows of other ranks): about 1/G of the epoch per GPU.  Every call has
+ * completed on the device when it returns. */
 int lx_rowseg_range(const lx_index *h, uint32_t *lo, uint32_t *hi);
-int lx_rowseg_of(const lx_index *h, uint32_t *rank, uint32_t *count);   /* options seg_rank / seg_count (1: whole) */
+int lx_rowseg_of(const lx_index *h, uint32_t *rank, uint32_t *count);   /* options seg_rank / seg_count (0 / 1 when off) */
 
 /* Row segments over RCCL for callers without a Python host (the Go shim): the
  * exchanges above (the protocol of lachesis_hip/rowseg.py) issued by the library

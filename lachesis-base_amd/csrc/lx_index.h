@@ -309,7 +309,7 @@ struct lx_index {
     uint32_t rs_mem_pstride = 0;
     uint32_t *rs_hslot = nullptr, *rs_rhb = nullptr, *rs_lslot = nullptr, *rs_rla = nullptr;
     uint64_t rs_hslot_cap = 0, rs_rhb_cap = 0, rs_lslot_cap = 0, rs_rla_cap = 0;   // (receive areas: rows x pstride)
-    bool rowseg() const { return rs_count > 1; }
+    bool rowseg() const { return rs_count >= 1; }   // seg_count = 1: one rank, the whole epoch
 
     int fail(int code, const char *fmt, ...) {
         char buf[512];

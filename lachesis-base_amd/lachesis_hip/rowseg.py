@@ -125,9 +125,12 @@ class RowSegments:
             self._bufs[name] = b
         return b
 
-    def forkless_cause_dev(self, n, qa, qb, out):
+    def forkless_cause_dev(self, n, qa, qb, out, timing=False):
         """ForklessCause of this rank's n queries (device tensors qa, qb of
-        int32 event ids, out uint8), collectively with every rank."""
+        int32 event ids, out uint8), collectively with every rank.  With
+        ``timing`` the k_fc launch over the routed pairs is bracketed by HIP
+        events on the library's stream: last_fc["kernel_ms"] (the rest of the
+        call is the routing protocol)."""
         ix, G = self.ix, self.world
         ra, rb = self._buf("ra", n), self._buf("rb", n)
         perm = self._buf("perm", n)
@@ -150,12 +153,21 @@ class RowSegments:
         self._a2a(got[:nn * W], rows[:na * W], [c * W for c in need_n], [c * W for c in ask_n])
         ix.rowseg_la_store(nn, ids.data_ptr(), got.data_ptr())
         ans = self._buf("ans", m, torch.uint8)
+        ev = None
+        if timing:
+            st = torch.cuda.ExternalStream(ix.device_planes()[3], device=self.device)
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record(st)
         ix.forkless_cause_batch_dev(m, xa.data_ptr(), xb.data_ptr(), ans.data_ptr())
+        if ev is not None:
+            ev[1].record(st)
         ix.sync()
         back = self._buf("back", n, torch.uint8)
         self._a2a(back[:n], ans[:m], send_n, recv_n)
         ix.rowseg_fc_unroute(n, perm.data_ptr(), back.data_ptr(), out.data_ptr())
         self.last_fc = {"routed_away": n - send_n[self.rank], "answered": m, "rows_received": nn, "rows_sent": na}
+        if ev is not None:
+            self.last_fc["kernel_ms"] = ev[0].elapsed_time(ev[1])
         return self.last_fc
 
     def get_rows_dev(self, mode, n, ev):

@@ -93,6 +93,17 @@ class ShardedIndex:
         G-int all-to-all tells the receivers the widths; every block starts at
         a multiple of 4 bytes on both sides (shard_layout)."""
         r, G = self.rank, self.world
+        if G == 1 and self.ix.shard_of()[1] == 1:
+            # one rank, a whole handle: every row is local, nothing moves -- the
+            # collectives still run (zero-length blocks), so a one-rank group
+            # exercises the same device-tensor paths as G ranks
+            self._min([0])
+            w = self._widths([0])
+            buf = self._buf("send", 4)
+            self.all_to_all(self._buf("recv", 4)[:0], buf[:0], [0], [0])
+            self.last_wire = ([0], w)
+            self.last_bytes = 0
+            return [0]
         incr = hasattr(self.ix, "shard_dirty")
         if incr:
             # only the rows written since the last exchange (lx_shard_dirty): each
@@ -163,7 +174,7 @@ class ShardedIndex:
     def _min(self, v):
         """Element-wise minimum over the ranks of a uint32 numpy vector."""
         import numpy as np
-        if self.world == 1 or len(v) == 0:
+        if len(v) == 0:
             return v
         dev = self.device if (self.device.type == "cuda" and not self.stage) else torch.device("cpu")
         t = torch.from_numpy(np.asarray(v, dtype=np.int64)).to(dev)
@@ -173,8 +184,6 @@ class ShardedIndex:
     def _widths(self, send_w):
         """Tell every rank the width of the block this rank sends it; returns recv widths."""
         G = self.world
-        if G == 1:
-            return list(send_w)
         dev = self.device if (self.device.type == "cuda" and not self.stage) else torch.device("cpu")
         sw = torch.tensor(send_w, dtype=torch.int32, device=dev)
         rw = torch.empty(G, dtype=torch.int32, device=dev)
@@ -200,8 +209,7 @@ class ShardedIndex:
         # partials are uint32 (stake sum < 2^31 plus at most one bit-31 mark, from
         # the rank owning branch(b)); the true total fits 32 bits, so the int32
         # wrap-around sum of the all-reduce is exact
-        if self.world > 1:
-            self.all_reduce_sum(part)
+        self.all_reduce_sum(part)   # (one rank: the identity, through the same collective)
         if self.device.type == "cuda":
             torch.cuda.current_stream(self.device).synchronize()
         s32 = part
