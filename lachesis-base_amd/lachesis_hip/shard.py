@@ -93,7 +93,7 @@ class ShardedIndex:
         G-int all-to-all tells the receivers the widths; every block starts at
         a multiple of 4 bytes on both sides (shard_layout)."""
         r, G = self.rank, self.world
-        if G == 1 and self.ix.shard_of()[1] == 1:
+        if G == 1 and hasattr(self.ix, "shard_of") and self.ix.shard_of()[1] == 1:
             # one rank, a whole handle: every row is local, nothing moves -- the
             # collectives still run (zero-length blocks), so a one-rank group
             # exercises the same device-tensor paths as G ranks
