@@ -128,21 +128,26 @@ def latency_leg(lx, dag, weights, device, history=200_000, reps=2000, feed=1_000
     cr = np.ascontiguousarray(dag.creator[:n])
     sq = np.ascontiguousarray(dag.seq[:n])
     po = np.ascontiguousarray(dag.poff[:n + 1])
-    out = (ctypes.c_double * 64)()
+    out = (ctypes.c_double * 128)()
     err = ctypes.create_string_buffer(512)
     rc = f(device, len(w), w.ctypes.data_as(u32p), n, cr.ctypes.data_as(u32p), sq.ctypes.data_as(u32p),
            po.ctypes.data_as(u64p), dag.par.ctypes.data_as(u32p), history, reps, feed, out, err, 512)
     if rc != 0:
         raise RuntimeError("lx_bench_latency: " + err.value.decode())
     res = {"unit": "us", "history_events": history, "reps": reps,
-           "calls": {k: {"p50": out[3 * i], "p99": out[3 * i + 1], "mean": out[3 * i + 2]} for i, k in enumerate(LAT_KINDS)},
+           "calls": {k: {"p50": out[3 * i], "p99": out[3 * i + 1], "mean": out[3 * i + 2], "p999": out[48 + 4 * i],
+                         "max": out[48 + 4 * i + 1], "first_call": out[48 + 4 * i + 2], "n": int(out[48 + 4 * i + 3])}
+                     for i, k in enumerate(LAT_KINDS)},
+           "add1024_split": {"add_call_p50": out[96], "add_call_p99": out[97], "sync_p50": out[98], "sync_p99": out[99]},
            "antichain_fed_events_per_sec": out[33], "batcher_fed_events_per_sec": out[36],
            "fc_pair_cached": {"first_call_miss": {"p50": out[40], "p99": out[41], "mean": out[42]},
                               "next_calls_hit": {"p50": out[43], "p99": out[44], "mean": out[45]}},
            "fed_events": int(out[34]), "fed_levels": int(out[35]), "mean_events_per_level": out[37],
            "note": "add1_async = host time of lx_add_batch(n=1) + lx_flush (the launch is not waited for); "
                    "*_sync include lx_sync (completion); fc/getters are synchronous calls; fc1 / fc667 = "
-                   "lx_forkless_cause_batch (no cache); fc_pair_cached = lx_forkless_cause (the drop-in path)"}
+                   "lx_forkless_cause_batch (no cache); fc_pair_cached = lx_forkless_cause (the drop-in path); "
+                   "each kind's first call (one-time setup: pinned buffers, the row server's stream, a kernel's "
+                   "first launch) is first_call, then 3 untimed calls, then the timed ones"}
     return res
 
 

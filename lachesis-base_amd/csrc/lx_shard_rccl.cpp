@@ -457,7 +457,8 @@ int lx_rowseg_exchange(lx_shard_comm *c, uint64_t stats[4]) {
     if (!c->rowseg) return c->fail(LX_ERR_STATE, "not a row-segment communicator (lx_rowseg_comm_create)");
     LXC(c->hip(hipSetDevice(c->device), "hipSetDevice"));
     const uint32_t G = c->nranks;
-    if (G == 1) return 0;   // a whole index: nothing to join
+    uint32_t lo = 0, hi = 0;
+    if (G == 1 && lx_rowseg_range(c->ix, &lo, &hi) != 0) return 0;   // a whole index: nothing to join
     if (!c->udev) LXC(c->hip(hipMalloc(reinterpret_cast<void **>(&c->udev), 8ull * (2 * G + 1)), "hipMalloc"));
     RcclRowOps ops{c};
     RcclRowNet net{c};
@@ -483,7 +484,8 @@ int lx_rowseg_forkless_cause(lx_shard_comm *c, uint64_t n, const uint32_t *qa, c
     if (!c->rowseg) return c->fail(LX_ERR_STATE, "not a row-segment communicator (lx_rowseg_comm_create)");
     LXC(c->hip(hipSetDevice(c->device), "hipSetDevice"));
     const uint32_t G = c->nranks;
-    if (G == 1) {   // a whole index
+    uint32_t lo = 0, hi = 0;
+    if (G == 1 && lx_rowseg_range(c->ix, &lo, &hi) != 0) {   // a whole index
         LXC(c->index(lx_forkless_cause_batch_dev(c->ix, n, qa, qb, out, nullptr), "lx_forkless_cause_batch_dev"));
         return c->index(lx_sync(c->ix), "lx_sync");
     }

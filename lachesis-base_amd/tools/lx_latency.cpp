@@ -32,7 +32,7 @@ inline double us_since(clk::time_point t0) {
 }
 
 struct Stat {
-    double p50 = 0, p99 = 0, mean = 0;
+    double p50 = 0, p99 = 0, mean = 0, p999 = 0, max = 0;
 };
 Stat stat_of(std::vector<double> v) {
     Stat s;
@@ -40,11 +40,18 @@ Stat stat_of(std::vector<double> v) {
     std::sort(v.begin(), v.end());
     s.p50 = v[v.size() / 2];
     s.p99 = v[std::min(v.size() - 1, (size_t)(v.size() * 0.99))];
+    s.p999 = v[std::min(v.size() - 1, (size_t)(v.size() * 0.999))];
+    s.max = v.back();
     double t = 0;
     for (double x : v) t += x;
     s.mean = t / v.size();
     return s;
 }
+
+// calls of each kind made before its timed ones: the first call of a kind pays
+// one-time setup (a getter's pinned buffers, the row server's stream and its
+// kernel's code object, a fill's scratch), reported apart as first_us
+constexpr uint32_t kWarm = 3;
 
 // the DAG re-ordered by topological level (stable inside a level), parents remapped
 struct Leveled {
@@ -91,7 +98,7 @@ Leveled by_level(uint64_t N, const uint32_t *creator, const uint32_t *seq, const
 
 extern "C" {
 
-// out receives kLatOut doubles: for each of the 11 call kinds p50, p99, mean (us):
+// out receives 128 doubles: for each of the 11 call kinds p50, p99, mean (us):
 //   0 add n=1 (Process: Add + Flush; host call time, the launch is not waited for)
 //   1 add n=1 + lx_sync (completion)
 //   2 Build: add n=1 + DropNotFlushed + lx_sync
@@ -104,7 +111,9 @@ extern "C" {
 // [35] levels fed, [36] batcher-fed events/s (push a level, pop, add, flush),
 // [37] mean events per level; [40..42] lx_forkless_cause of a new event's
 // first pair (a cache miss: pending Add + row fill), [43..45] its next pairs
-// (hits).
+// (hits); [48 + 4 k ..] for call kind k: p99.9, max, the first call of the
+// kind (before kWarm untimed calls), the timed calls' count; [96..99] add
+// n=1024 + sync split: the add call's p50 / p99, the sync's p50 / p99.
 int lx_bench_latency(int device, uint32_t V, const uint32_t *weights, uint64_t N, const uint32_t *creator,
                      const uint32_t *seq, const uint64_t *poff, const uint32_t *par, uint64_t history,
                      uint32_t reps, uint64_t feed_events, double *out, char *err, uint32_t err_cap) {
@@ -135,25 +144,32 @@ int lx_bench_latency(int device, uint32_t V, const uint32_t *weights, uint64_t N
                             d.par.data(), nullptr, nullptr);
     };
     std::vector<double> t[11];
+    double first[11] = {0};
+    // record call r of a kind: the first is one-time setup, the next kWarm - 1
+    // are dropped, the rest timed
+    auto rec = [&](int kind, uint32_t r, double us) {
+        if (r == 0) first[kind] = us;
+        if (r >= kWarm) t[kind].push_back(us);
+    };
     // 0/1: single events, Process pattern (async; then with completion)
     for (int mode = 0; mode < 2; mode++) {
-        for (uint32_t r = 0; r < reps && next < N; r++, next++) {
+        for (uint32_t r = 0; r < reps + kWarm && next < N; r++, next++) {
             auto t0 = clk::now();
             if (add(next, next + 1)) return fail("add1", h);
             lx_flush(h);
             if (mode == 1 && lx_sync(h)) return fail("sync", h);
-            t[mode].push_back(us_since(t0));
+            rec(mode, r, us_since(t0));
         }
         if (lx_sync(h)) return fail("sync", h);
     }
     while (lv + 1 < d.lvl_off.size() && d.lvl_off[lv + 1] <= next) lv++;
     // 2: Build pattern on the next event, repeated (each Build is rolled back)
-    for (uint32_t r = 0; r < reps; r++) {
+    for (uint32_t r = 0; r < reps + kWarm; r++) {
         auto t0 = clk::now();
         if (add(next, next + 1)) return fail("build", h);
         if (lx_drop_not_flushed(h)) return fail("drop", h);
         if (lx_sync(h)) return fail("sync", h);
-        t[2].push_back(us_since(t0));
+        rec(2, r, us_since(t0));
     }
     // 3: antichains: finish the current level, then whole levels
     if (next < d.lvl_off[lv + 1]) {
@@ -162,22 +178,34 @@ int lx_bench_latency(int device, uint32_t V, const uint32_t *weights, uint64_t N
         next = d.lvl_off[++lv];
     }
     const uint32_t lreps = std::max<uint32_t>(reps / 4, 50);
-    for (uint32_t r = 0; r < lreps && lv + 1 < d.lvl_off.size(); r++, lv++) {
+    for (uint32_t r = 0; r < lreps + kWarm && lv + 1 < d.lvl_off.size(); r++, lv++) {
         auto t0 = clk::now();
         if (add(d.lvl_off[lv], d.lvl_off[lv + 1])) return fail("level", h);
         lx_flush(h);
         if (lx_sync(h)) return fail("sync", h);
-        t[3].push_back(us_since(t0));
+        rec(3, r, us_since(t0));
         next = d.lvl_off[lv + 1];
     }
-    // 4: 1024-event batches (continuing in level order)
-    for (uint32_t r = 0; r < std::max<uint32_t>(reps / 20, 20) && next + 1024 <= N; r++) {
+    // 4: 1024-event batches (continuing in level order); the add call and the
+    // sync timed apart too
+    std::vector<double> t4a, t4s;
+    for (uint32_t r = 0; r < std::max<uint32_t>(reps / 10, 200) + kWarm && next + 1024 <= N; r++) {
         auto t0 = clk::now();
         if (add(next, next + 1024)) return fail("add1024", h);
         lx_flush(h);
+        const double ta = us_since(t0);
         if (lx_sync(h)) return fail("sync", h);
-        t[4].push_back(us_since(t0));
+        const double tt = us_since(t0);
+        rec(4, r, tt);
+        if (r >= kWarm) {
+            t4a.push_back(ta);
+            t4s.push_back(tt - ta);
+        }
         next += 1024;
+    }
+    {
+        Stat a = stat_of(t4a), b = stat_of(t4s);
+        out[96] = a.p50; out[97] = a.p99; out[98] = b.p50; out[99] = b.p99;
     }
     while (lv + 1 < d.lvl_off.size() && d.lvl_off[lv + 1] <= next) lv++;
     if (next < d.lvl_off[lv + 1] && lv + 1 < d.lvl_off.size()) {   // realign to a level boundary
@@ -197,19 +225,19 @@ int lx_bench_latency(int device, uint32_t V, const uint32_t *weights, uint64_t N
     std::vector<uint8_t> qo(667);
     for (int kind = 5; kind <= 6; kind++) {
         const uint32_t n = kind == 5 ? 1 : 667;
-        for (uint32_t r = 0; r < reps; r++) {
+        for (uint32_t r = 0; r < reps + kWarm; r++) {
             for (uint32_t i = 0; i < n; i++) {
                 qa[i] = (uint32_t)(next - 1 - rnd(std::min<uint64_t>(next, 5000)));
                 qb[i] = (uint32_t)rnd(next);
             }
             auto t0 = clk::now();
             if (lx_forkless_cause_batch(h, n, qa.data(), qb.data(), qo.data())) return fail("fc", h);
-            t[kind].push_back(us_since(t0));
+            rec(kind, r, us_since(t0));
         }
     }
     std::vector<uint8_t> row(16 * (V + 4096));
     for (int kind = 7; kind <= 9; kind++) {
-        for (uint32_t r = 0; r < reps; r++) {
+        for (uint32_t r = 0; r < reps + kWarm; r++) {
             const uint32_t ev = (uint32_t)(next - 1 - rnd(std::min<uint64_t>(next, 5000)));
             uint32_t len = 0;
             auto t0 = clk::now();
@@ -217,19 +245,19 @@ int lx_bench_latency(int device, uint32_t V, const uint32_t *weights, uint64_t N
                      : kind == 8 ? lx_get_lowest_after(h, ev, row.data(), (uint32_t)row.size(), &len)
                                  : lx_get_merged_highest_before(h, ev, row.data(), (uint32_t)row.size(), &len);
             if (rc) return fail("getter", h);
-            t[kind].push_back(us_since(t0));
+            rec(kind, r, us_since(t0));
         }
     }
     {
         std::vector<uint32_t> evs(64);
         std::vector<uint64_t> off(65);
         std::vector<uint8_t> buf(64ull * 8 * V);
-        for (uint32_t r = 0; r < reps / 4 + 1; r++) {
+        for (uint32_t r = 0; r < reps / 4 + 1 + kWarm; r++) {
             for (auto &e : evs) e = (uint32_t)(next - 1 - rnd(std::min<uint64_t>(next, 5000)));
             auto t0 = clk::now();
             if (lx_get_merged_highest_before_batch(h, 64, evs.data(), off.data(), buf.data(), buf.size()))
                 return fail("getter batch", h);
-            t[10].push_back(us_since(t0));
+            rec(10, r, us_since(t0));
         }
     }
     // ForklessCause of one pair through lx_forkless_cause (the drop-in path), as
@@ -270,6 +298,10 @@ int lx_bench_latency(int device, uint32_t V, const uint32_t *weights, uint64_t N
         out[3 * k] = s.p50;
         out[3 * k + 1] = s.p99;
         out[3 * k + 2] = s.mean;
+        out[48 + 4 * k] = s.p999;
+        out[48 + 4 * k + 1] = s.max;
+        out[48 + 4 * k + 2] = first[k];
+        out[48 + 4 * k + 3] = (double)t[k].size();
     }
     // antichain-fed throughput: levels as batches, Add + Flush each, one sync at the end
     {
