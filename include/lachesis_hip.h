@@ -467,6 +467,19 @@ int lx_rowseg_fc_unroute(lx_index *h, uint64_t n, const uint32_t *perm_dev, cons
 /* stats (optional): queries routed away, pairs answered here, LA rows received, sent */
 int lx_rowseg_forkless_cause(lx_shard_comm *c, uint64_t n, const uint32_t *qa_dev, const uint32_t *qb_dev,
                              uint8_t *out_dev, uint64_t stats[4]);
+/* The vector getters of events on any rank (GetHighestBefore / GetLowestAfter
+ * / GetMergedHighestBefore, vecfc/store_vectors.go:26-51,
+ * vecengine/index.go:235-250), collectively: each rank's n device ids are
+ * routed to their owners (lx_rowseg_fc_route with b = a), answered there by
+ * lx_get_rows_dev, and the rows come back in the caller's order
+ * (lx_rowseg_rows_unroute: row i of `rows` to row perm[i] of out, slot_bytes
+ * each, lengths with them).  lx_rowseg_get_rows does all of it over RCCL;
+ * lachesis_hip/rowseg.py get_rows over torch.distributed.  Mode and
+ * lengths as lx_get_rows_dev (0xFFFFFFFF: no such event). */
+int lx_rowseg_rows_unroute(lx_index *h, uint64_t n, const uint32_t *perm_dev, const uint8_t *rows_dev,
+                           uint64_t slot_bytes, const uint32_t *len_dev, uint8_t *out_dev, uint32_t *out_len_dev);
+int lx_rowseg_get_rows(lx_shard_comm *c, uint32_t mode, uint64_t n, const uint32_t *ev_dev, uint8_t *out_dev,
+                       uint64_t slot_bytes, uint32_t *len_dev);
 
 /* Device views for benchmarks/tests (valid until the next add/reset).  On a
  * row-segment rank the planes hold its own rows only: row e is at

@@ -662,6 +662,8 @@ hipError_t launch_rsq_la_gather(const RsqArgs &a, const uint32_t *la, uint64_t s
 hipError_t launch_rsq_la_store(const RsqArgs &a, uint32_t *la_recv, uint64_t stride, const uint32_t *ids, uint32_t n,
                                const uint32_t *rows, uint32_t *stamp, uint32_t *slot, uint32_t arrived, hipStream_t s);
 hipError_t launch_rsq_unroute(const uint32_t *perm, const uint8_t *ans, uint64_t n, uint8_t *out, hipStream_t s);
+hipError_t launch_rows_unroute(const uint32_t *perm, const uint8_t *rows, uint64_t slot, const uint32_t *len,
+                               uint64_t n, uint8_t *out, uint32_t *out_len, hipStream_t s);
 hipError_t launch_rs_bucket(const SegArgs &a, const RsArgs &r, uint32_t n_req, uint32_t *out, uint32_t *counts,
                             hipStream_t s);
 hipError_t launch_rs_gather(const RsArgs &r, const uint32_t *ids, uint32_t n, uint32_t *rows, uint32_t *ready,

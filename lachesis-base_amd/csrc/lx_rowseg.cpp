@@ -562,6 +562,17 @@ int lx_rowseg_fc_unroute(lx_index *h, uint64_t n, const uint32_t *perm, const ui
     return 0;
 }
 
+int lx_rowseg_rows_unroute(lx_index *h, uint64_t n, const uint32_t *perm, const uint8_t *rows, uint64_t slot_bytes,
+                           const uint32_t *len, uint8_t *out, uint32_t *out_len) {
+    int rc;
+    if ((rc = rs_check(h, 4))) return rc;
+    if (n && (!perm || !rows || !len || !out || !out_len)) return LX_ERR_ARG;
+    if (slot_bytes % 16 || n > 0x7FFFFFFFull) return h->fail(LX_ERR_ARG, "row slot must be a multiple of 16 bytes");
+    HIPCHK(h, lx::launch_rows_unroute(perm, rows, slot_bytes, len, n, out, out_len, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return 0;
+}
+
 int lx_rowseg_of(const lx_index *h, uint32_t *rank, uint32_t *count) {
     if (!h || !rank || !count) return LX_ERR_ARG;
     *rank = h->rowseg() ? h->rs_rank : 0u;

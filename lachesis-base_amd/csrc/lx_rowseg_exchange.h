@@ -38,6 +38,8 @@ enum RowsegBuf : int {
     kRsIds = 0, kRsAsked, kRsOutRows, kRsOutReady, kRsGotRows, kRsGotReady, kRsLaSend, kRsLaRecv,
     // ForklessCause across ranks (rowseg_fc_run)
     kRqA, kRqB, kRqPerm, kRqRecvA, kRqRecvB, kRqIds, kRqAsked, kRqRows, kRqGotRows, kRqAns, kRqAnsBack,
+    // the vector getters across ranks (rowseg_get_run)
+    kRgA, kRgB, kRgPerm, kRgAsked, kRgRows, kRgLens, kRgBack, kRgBackLens,
     kRsBufs
 };
 
@@ -161,6 +163,40 @@ int rowseg_fc_run(Ops &ops, Net &net, uint32_t G, uint64_t n, const uint32_t *qa
     for (uint32_t q = 0; q < G; q++) sb[q] = recv_n[q], rb[q] = send_n[q];
     if ((rc = net.move(ans, sb.data(), back, rb.data()))) return rc;
     return ops.fc_unroute(n, perm, back, out);
+}
+
+// The vector getters of events on any rank (lx_rowseg_get_rows): ids to their
+// owners (the ForklessCause route with b = a), rows encoded there
+// (lx_get_rows_dev), rows and lengths back, put in the caller's order.  More
+// Ops: get_rows(mode, m, ids, rows, slot, lens) (completed on return),
+// rows_unroute(n, perm, rows, slot, lens, out, out_lens).
+template <class Ops, class Net>
+int rowseg_get_run(Ops &ops, Net &net, uint32_t G, uint32_t mode, uint64_t n, const uint32_t *ev, uint8_t *out,
+                   uint64_t slot, uint32_t *out_len) {
+    int rc;
+    std::vector<uint64_t> send_n(G), recv_n(G), sb(G), rb(G);
+    uint32_t *ra = static_cast<uint32_t *>(ops.buf(kRgA, 4 * (n + 1)));
+    uint32_t *rbq = static_cast<uint32_t *>(ops.buf(kRgB, 4 * (n + 1)));
+    uint32_t *perm = static_cast<uint32_t *>(ops.buf(kRgPerm, 4 * (n + 1)));
+    if (!ra || !rbq || !perm) return LX_ERR_NOMEM;
+    if ((rc = ops.fc_route(n, ev, ev, ra, rbq, perm, send_n.data()))) return rc;
+    if ((rc = net.counts(send_n.data(), recv_n.data()))) return rc;
+    uint64_t m = 0;
+    for (uint32_t q = 0; q < G; q++) m += recv_n[q];
+    uint32_t *asked = static_cast<uint32_t *>(ops.buf(kRgAsked, 4 * (m + 1)));
+    uint8_t *rows = static_cast<uint8_t *>(ops.buf(kRgRows, slot * (m + 1)));
+    uint32_t *lens = static_cast<uint32_t *>(ops.buf(kRgLens, 4 * (m + 1)));
+    uint8_t *back = static_cast<uint8_t *>(ops.buf(kRgBack, slot * (n + 1)));
+    uint32_t *blen = static_cast<uint32_t *>(ops.buf(kRgBackLens, 4 * (n + 1)));
+    if (!asked || !rows || !lens || !back || !blen) return LX_ERR_NOMEM;
+    for (uint32_t q = 0; q < G; q++) sb[q] = 4 * send_n[q], rb[q] = 4 * recv_n[q];
+    if ((rc = net.move(ra, sb.data(), asked, rb.data()))) return rc;
+    if ((rc = ops.get_rows(mode, m, asked, rows, slot, lens))) return rc;
+    for (uint32_t q = 0; q < G; q++) sb[q] = slot * recv_n[q], rb[q] = slot * send_n[q];
+    if ((rc = net.move(rows, sb.data(), back, rb.data()))) return rc;
+    for (uint32_t q = 0; q < G; q++) sb[q] = 4 * recv_n[q], rb[q] = 4 * send_n[q];
+    if ((rc = net.move(lens, sb.data(), blen, rb.data()))) return rc;
+    return ops.rows_unroute(n, perm, back, slot, blen, out, out_len);
 }
 
 }  // namespace lx

@@ -119,6 +119,18 @@ __global__ void k_rsq_unroute(const uint32_t *perm, const uint8_t *ans, uint64_t
     if (i < n) out[perm[i]] = ans[i];
 }
 
+// routed getter rows back in the caller's order: row i (slot bytes, a multiple
+// of 16) to row perm[i], its length with it; one workgroup per row
+__global__ void __launch_bounds__(256) k_rows_unroute(const uint32_t *perm, const uint8_t *rows, uint64_t slot,
+                                                      const uint32_t *len, uint8_t *out, uint32_t *out_len) {
+    const uint64_t i = blockIdx.x;
+    const uint32_t p = perm[i];
+    const uint4 *src = reinterpret_cast<const uint4 *>(rows + i * slot);
+    uint4 *dst = reinterpret_cast<uint4 *>(out + (uint64_t)p * slot);
+    for (uint64_t k = threadIdx.x; k < slot / 16; k += blockDim.x) dst[k] = src[k];
+    if (threadIdx.x == 0) out_len[p] = len[i];
+}
+
 inline uint32_t nb(uint64_t n, uint32_t t) { return (uint32_t)((n + t - 1) / t); }
 
 uint32_t owner_bits(uint32_t G) {
@@ -184,6 +196,13 @@ hipError_t launch_rsq_la_store(const RsqArgs &a, uint32_t *la_recv, uint64_t str
                                const uint32_t *rows, uint32_t *stamp, uint32_t *slot, uint32_t arrived, hipStream_t s) {
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(k_rsq_la_store, dim3(n), dim3(256), 0, s, a, la_recv, stride, ids, rows, stamp, slot, arrived);
+    return hipGetLastError();
+}
+
+hipError_t launch_rows_unroute(const uint32_t *perm, const uint8_t *rows, uint64_t slot, const uint32_t *len,
+                               uint64_t n, uint8_t *out, uint32_t *out_len, hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_rows_unroute, dim3((uint32_t)n), dim3(256), 0, s, perm, rows, slot, len, out, out_len);
     return hipGetLastError();
 }
 

@@ -398,6 +398,15 @@ struct RcclRowOps {
     int fc_unroute(uint64_t n, const uint32_t *perm, const uint8_t *ans, uint8_t *out) {
         return c->index(lx_rowseg_fc_unroute(c->ix, n, perm, ans, out), "lx_rowseg_fc_unroute");
     }
+    int get_rows(uint32_t mode, uint64_t m, const uint32_t *ids, uint8_t *rows, uint64_t slot, uint32_t *lens) {
+        if (m > 0xFFFFFFFFull) return c->fail(LX_ERR_ARG, "too many rows in one call");
+        return c->index(lx_get_rows_dev(c->ix, mode, (uint32_t)m, ids, rows, slot, lens), "lx_get_rows_dev");
+    }
+    int rows_unroute(uint64_t n, const uint32_t *perm, const uint8_t *rows, uint64_t slot, const uint32_t *lens,
+                     uint8_t *out, uint32_t *out_len) {
+        return c->index(lx_rowseg_rows_unroute(c->ix, n, perm, rows, slot, lens, out, out_len),
+                        "lx_rowseg_rows_unroute");
+    }
 };
 
 // the collectives on the handle's stream; the own block moves by a local copy
@@ -506,6 +515,26 @@ int lx_rowseg_forkless_cause(lx_shard_comm *c, uint64_t n, const uint32_t *qa, c
         stats[3] = st.rows_sent;
     }
     return 0;
+}
+
+int lx_rowseg_get_rows(lx_shard_comm *c, uint32_t mode, uint64_t n, const uint32_t *ev, uint8_t *out, uint64_t slot,
+                       uint32_t *len) {
+    if (!c || mode > 2 || (n && (!ev || !out || !len))) return LX_ERR_ARG;
+    if (!c->rowseg) return c->fail(LX_ERR_STATE, "not a row-segment communicator (lx_rowseg_comm_create)");
+    LXC(c->hip(hipSetDevice(c->device), "hipSetDevice"));
+    const uint32_t G = c->nranks;
+    uint32_t lo = 0, hi = 0;
+    if (G == 1 && lx_rowseg_range(c->ix, &lo, &hi) != 0) {   // a whole index
+        if (n > 0xFFFFFFFFull) return c->fail(LX_ERR_ARG, "too many rows in one call");
+        return c->index(lx_get_rows_dev(c->ix, mode, (uint32_t)n, ev, out, slot, len), "lx_get_rows_dev");
+    }
+    if (!c->udev) LXC(c->hip(hipMalloc(reinterpret_cast<void **>(&c->udev), 8ull * (2 * G + 1)), "hipMalloc"));
+    RcclRowOps ops{c};
+    RcclRowNet net{c};
+    c->err.clear();
+    const int rc = lx::rowseg_get_run(ops, net, G, mode, n, ev, out, slot, len);
+    if (rc && c->err.empty()) c->fail(rc, "row-segment getters failed (%d)", rc);
+    return rc;
 }
 
 }  // extern "C"

@@ -54,6 +54,8 @@ SIGNATURES = [
     ("lx_device_bytes", ctypes.c_int, [vp, u64p]),
     ("lx_get_rows_dev", ctypes.c_int, [vp, ctypes.c_uint32, ctypes.c_uint32, vp, vp, ctypes.c_uint64, vp]),
     ("lx_row_bytes_max", ctypes.c_int, [vp, u64p]),
+    ("lx_rowseg_rows_unroute", ctypes.c_int, [vp, ctypes.c_uint64, vp, vp, ctypes.c_uint64, vp, vp, vp]),
+    ("lx_rowseg_get_rows", ctypes.c_int, [vp, ctypes.c_uint32, ctypes.c_uint64, vp, vp, ctypes.c_uint64, vp]),
     ("lx_get_branches_info", ctypes.c_int, [vp, u32p, u32p, ctypes.c_uint32, u32p]),
     ("lx_shard_of", ctypes.c_int, [vp, u32p, u32p]),
     ("lx_shard_range", ctypes.c_int, [vp, ctypes.c_uint32, u32p, u32p]),
@@ -691,3 +693,8 @@ class RowsegComm(ShardComm):
         self._chk(self.L.lx_rowseg_forkless_cause(self.c, n, a_ptr, b_ptr, out_ptr, _p(st, u64p)))
         return {"routed_away": int(st[0]), "answered": int(st[1]), "rows_received": int(st[2]),
                 "rows_sent": int(st[3])}
+
+    def get_rows_dev(self, mode, n, ev_ptr, out_ptr, slot_bytes, len_ptr):
+        """The vector getter rows of n device ids of any rank
+        (lx_rowseg_get_rows, collective): row i at out + i * slot_bytes."""
+        self._chk(self.L.lx_rowseg_get_rows(self.c, mode, n, ev_ptr, out_ptr, slot_bytes, len_ptr))

@@ -90,6 +90,13 @@ struct Ops {
     int fc_unroute(uint64_t n, const uint32_t *perm, const uint8_t *ans, uint8_t *out) {
         return lx_rowseg_fc_unroute(h, n, perm, ans, out);
     }
+    int get_rows(uint32_t mode, uint64_t m, const uint32_t *ids, uint8_t *rows, uint64_t slot, uint32_t *lens) {
+        return lx_get_rows_dev(h, mode, (uint32_t)m, ids, rows, slot, lens);
+    }
+    int rows_unroute(uint64_t n, const uint32_t *perm, const uint8_t *rows, uint64_t slot, const uint32_t *lens,
+                     uint8_t *out, uint32_t *out_len) {
+        return lx_rowseg_rows_unroute(h, n, perm, rows, slot, lens, out, out_len);
+    }
     void *buf(int k, size_t bytes) {
         if (bytes > caps[k]) {
             (void)hipFree(bufs[k]);
@@ -207,6 +214,35 @@ extern "C" int lx_fake_rowseg_fc(void **handles, uint32_t G, const uint64_t *n, 
             stats[4 * r + 1] = st.answered;
             stats[4 * r + 2] = st.rows_received;
             stats[4 * r + 3] = st.rows_sent;
+        });
+    for (auto &t : th) t.join();
+    snprintf(err, err_cap, "%s", w.err.c_str());
+    for (int rc : rcs)
+        if (rc) return rc;
+    return 0;
+}
+
+// the vector getters across ranks: rank r asks for the rows of its n[r] device
+// ids (mode 0 HighestBefore, 1 LowestAfter, 2 merged HighestBefore)
+extern "C" int lx_fake_rowseg_get_rows(void **handles, uint32_t G, uint32_t mode, const uint64_t *n, void **ev,
+                                       void **out, uint64_t slot, void **len, char *err, uint32_t err_cap) {
+    World w(G);
+    std::vector<int> rcs(G, 0);
+    std::vector<std::thread> th;
+    for (uint32_t r = 0; r < G; r++)
+        th.emplace_back([&, r] {
+            (void)hipSetDevice(0);
+            Ops ops{static_cast<lx_index *>(handles[r])};
+            ops.r = r;
+            Net net{w, r};
+            rcs[r] = lx::rowseg_get_run(ops, net, G, mode, n[r], static_cast<const uint32_t *>(ev[r]),
+                                        static_cast<uint8_t *>(out[r]), slot, static_cast<uint32_t *>(len[r]));
+            if (rcs[r]) {
+                w.fail("rank " + std::to_string(r) + ": " + lx_last_error(ops.h));
+                std::lock_guard<std::mutex> l(w.m);
+                w.broken = true;
+                w.cv.notify_all();
+            }
         });
     for (auto &t : th) t.join();
     snprintf(err, err_cap, "%s", w.err.c_str());

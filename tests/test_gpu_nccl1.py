@@ -94,6 +94,16 @@ def _worker(case, port, q):
             comm.forkless_cause_dev(len(qa), ta.data_ptr(), tb.data_ptr(), out.data_ptr())
             ix.sync()
             ok = ok and bool(np.array_equal(out.cpu().numpy(), want))
+            ev = np.array([int(x) for x in rng.integers(0, N, 100)] + [N + 1], dtype=np.uint32)
+            slot = (ix.row_bytes_max() + 15) // 16 * 16
+            te = torch.from_numpy(ev.view(np.int32)).to(dev)
+            for mode, f in ((0, o.hb), (1, o.la), (2, o.merged_hb)):
+                rows = torch.zeros(len(ev) * slot, dtype=torch.uint8, device=dev)
+                lens = torch.zeros(len(ev), dtype=torch.int32, device=dev)
+                comm.get_rows_dev(mode, len(ev), te.data_ptr(), rows.data_ptr(), slot, lens.data_ptr())
+                rr, ll = rows.cpu().numpy().reshape(len(ev), slot), lens.cpu().numpy().view(np.uint32)
+                ok = ok and ll[-1] == 0xFFFFFFFF and all(bytes(rr[i, :ll[i]]) == f(int(e))
+                                                         for i, e in enumerate(ev[:-1]))
             comm.close()
             ix.close()
         q.put((ok, repr(info)))

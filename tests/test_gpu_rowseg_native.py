@@ -44,6 +44,9 @@ def fake(lx):
     L.lx_fake_rowseg_fc.restype = ctypes.c_int
     L.lx_fake_rowseg_fc.argtypes = [vpp, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64), vpp, vpp, vpp,
                                     ctypes.POINTER(ctypes.c_uint64), ctypes.c_char_p, ctypes.c_uint32]
+    L.lx_fake_rowseg_get_rows.restype = ctypes.c_int
+    L.lx_fake_rowseg_get_rows.argtypes = [vpp, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64), vpp,
+                                          vpp, ctypes.c_uint64, vpp, ctypes.c_char_p, ctypes.c_uint32]
     return L
 
 
@@ -264,3 +267,52 @@ def test_native_row_segments_c3_shape_auto_sub(lx, fake, world):
     for ix in ranks:
         ix.close()
     ref.close()
+
+
+@pytest.mark.parametrize("world,shape", [(2, "forks"), (3, "forks"), (4, "wide")])
+def test_native_row_segment_getters_any_rank(lx, fake, world, shape):
+    """The vector getters of events on every rank through the native driver
+    (csrc/lx_rowseg_exchange.h rowseg_get_run, which lx_rowseg_get_rows runs
+    over RCCL): each rank asks for rows of events anywhere in the epoch (and
+    one past it), in every mode, and gets the oracle's bytes in its own order
+    (vecfc/store_vectors.go:26-51, vecengine/index.go:235-250)."""
+    import torch
+    V, epv, P, ch, fk, seed = SHAPES[shape]
+    d = lx.tools.gen_dag(V, epv, P, ch, fk, seed)
+    N = len(d)
+    rng = np.random.default_rng(seed + 7)
+    weights = [int(x) for x in rng.integers(1, 40, V)]
+    ranks = []
+    for r in range(world):
+        ix = lx.Index(device=0, options={"seg_count": world, "seg_rank": r, "small_max": 0})
+        ix.reset(weights)
+        ix.add_batch(d.creator, d.seq, d.poff, d.par)
+        ranks.append(ix)
+    hs = (ctypes.c_void_p * world)(*[ix.h for ix in ranks])
+    stats = (ctypes.c_uint64 * (4 * world))()
+    err = ctypes.create_string_buffer(512)
+    assert fake.lx_fake_rowseg_exchange(hs, world, stats, err, 512) == 0, err.value.decode()
+    o = corc.OracleIndex(weights)
+    assert o.add_batch(d.creator, d.seq, d.poff, d.par) == -1
+    dev = torch.device("cuda", 0)
+    slot = (ranks[0].row_bytes_max() + 15) // 16 * 16
+    evs = [np.concatenate([rng.integers(0, N, 200 + 13 * r), [N + 3]]).astype(np.uint32) for r in range(world)]
+    n = (ctypes.c_uint64 * world)(*[len(e) for e in evs])
+    t_ev = [torch.from_numpy(e.view(np.int32)).to(dev) for e in evs]
+    for mode, want in ((0, o.hb), (1, o.la), (2, o.merged_hb)):
+        t_out = [torch.zeros(len(e) * slot, dtype=torch.uint8, device=dev) for e in evs]
+        t_len = [torch.zeros(len(e), dtype=torch.int32, device=dev) for e in evs]
+        pv = lambda ts: (ctypes.c_void_p * world)(*[t.data_ptr() for t in ts])
+        rc = fake.lx_fake_rowseg_get_rows(hs, world, mode, n, pv(t_ev), pv(t_out), slot, pv(t_len), err, 512)
+        assert rc == 0, err.value.decode()
+        for r in range(world):
+            rows = t_out[r].cpu().numpy().reshape(len(evs[r]), slot)
+            lens = t_len[r].cpu().numpy().view(np.uint32)
+            for i, e in enumerate(evs[r]):
+                if e >= N:
+                    assert lens[i] == 0xFFFFFFFF
+                else:
+                    assert bytes(rows[i, :lens[i]]) == want(int(e)), (mode, r, int(e))
+    for ix in ranks:
+        ix.close()
+
