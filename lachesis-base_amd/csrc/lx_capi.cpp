@@ -1205,29 +1205,33 @@ int hm_sync(lx_index *h) {
 }
 
 // pinned staging image of `words` uint32 (the slot's previous copy has finished
-// reading it) and a device image at least as large
+// reading it) and a device image at least as large.  A slot that must grow
+// grows every slot to the same size at once: the slots are used in turn, and
+// growing them one by one put a pinned allocation (~0.1-0.3 ms) into each of
+// the next kSlots calls -- the latency leg's add1024 tail
 int stage_slot(lx_index *h, uint64_t words, uint32_t **out, int *slot) {
     const int k = (int)h->st_next;
     h->st_next = (h->st_next + 1) % lx_index::kSlots;
     if (h->st_used[k]) HIPCHK(h, hipEventSynchronize(h->st_copied[k]));
-    if (words > h->st_pin_cap[k]) {
-        if (h->st_pin[k]) (void)hipHostFree(h->st_pin[k]);
-        h->st_pin[k] = nullptr;
-        h->st_pin_cap[k] = 0;
+    if (words > h->st_pin_cap[k] || words > h->st_dev_cap[k]) {
         const uint64_t cap = std::max<uint64_t>(words + words / 2, 16384);
-        HIPCHK(h, hipHostMalloc((void **)&h->st_pin[k], cap * 4, hipHostMallocDefault));
-        h->st_pin_cap[k] = cap;
-    }
-    if (words > h->st_dev_cap[k]) {
-        if (h->st_dev[k]) {
-            if (h->st_used[k]) HIPCHK(h, hipStreamSynchronize(h->stream));   // the kernel that read it
-            (void)hipFree(h->st_dev[k]);
+        HIPCHK(h, hipStreamSynchronize(h->stream));   // every copy and kernel that read a slot
+        for (int j = 0; j < lx_index::kSlots; j++) {
+            if (cap > h->st_pin_cap[j]) {
+                if (h->st_pin[j]) (void)hipHostFree(h->st_pin[j]);
+                h->st_pin[j] = nullptr;
+                h->st_pin_cap[j] = 0;
+                HIPCHK(h, hipHostMalloc((void **)&h->st_pin[j], cap * 4, hipHostMallocDefault));
+                h->st_pin_cap[j] = cap;
+            }
+            if (cap > h->st_dev_cap[j]) {
+                if (h->st_dev[j]) (void)hipFree(h->st_dev[j]);
+                h->st_dev[j] = nullptr;
+                h->st_dev_cap[j] = 0;
+                HIPCHK(h, dalloc(&h->st_dev[j], cap));
+                h->st_dev_cap[j] = cap;
+            }
         }
-        h->st_dev[k] = nullptr;
-        h->st_dev_cap[k] = 0;
-        const uint64_t cap = std::max<uint64_t>(words + words / 2, 16384);
-        HIPCHK(h, dalloc(&h->st_dev[k], cap));
-        h->st_dev_cap[k] = cap;
     }
     *out = h->st_pin[k];
     *slot = k;
