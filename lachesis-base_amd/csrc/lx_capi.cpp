@@ -476,7 +476,7 @@ BatchArgs batch_args(lx_index *h, uint32_t n, const uint32_t *creator, const uin
 uint32_t walk_grid(const lx_index *h, uint32_t cpw_hint) {
     const uint32_t nc = h->ncols, cpw = cpw_hint ? cpw_hint : (nc <= 256 ? 1 : nc <= 512 ? 2 : 4);
     const uint32_t slices = (nc + cpw - 1) / cpw;
-    return cpw >= 12 ? slices : (slices + 7) / 8 * 8;
+    return cpw == 12 ? slices : (slices + 7) / 8 * 8;
 }
 
 // Segments walked at once on idle compute units: a walk of few columns leaves
@@ -496,12 +496,12 @@ uint32_t auto_segments(const lx_index *h, uint64_t n, uint32_t *cpw) {
 // the segment count and slice width auto_segments would pick for n events
 // (row-segment ranks split their own segment by it too, lx_rowseg.cpp)
 uint32_t seg_pick(const lx_index *h, uint64_t n, uint32_t *cpw) {
-    static const float kPass[17] = {0, 1.0f, 1.15f, 0, 1.28f, 0, 0, 0, kPass8, 0, 0, 0, kPass12, 0, 0, 0, kPass16};
-    // 8-, 12- and 16-column slices: packed 16-bit slots only (every seq <= 0xFFFF, no forks)
+    static const float kPass[13] = {0, 1.0f, 1.15f, 0, 1.28f, 0, 0, 0, kPass8, 0, 0, 0, kPass12};
+    // 8- and 12-column slices: packed 16-bit slots only (every seq <= 0xFFFF, no forks)
     const bool w8 = h->pack16 && h->max_seq <= 0xFFFFu && h->B <= h->V;
     uint32_t best_g = 0;
     float best = 1.0f;   // one walk at the default width
-    for (uint32_t c : {1u, 2u, 4u, 8u, 12u, 16u}) {
+    for (uint32_t c : {1u, 2u, 4u, 8u, 12u}) {
         if ((h->cpw_hint && c != h->cpw_hint) || (c >= 8 && !w8)) continue;
         uint32_t G = std::min<uint32_t>(h->n_cus / walk_grid(h, c), kSegLaunchMax);
         while (G >= 2 && n < (uint64_t)G * kAutoSegEvents) G--;
@@ -1782,8 +1782,8 @@ int lx_set_option(lx_index *h, const char *name, int64_t value) {
     } else if (k == "fc_early") {
         h->fc_early = value != 0;
     } else if (k == "cpw") {
-        if (value != 0 && value != 1 && value != 2 && value != 4 && value != 8 && value != 12 && value != 16)
-            return h->fail(LX_ERR_ARG, "cpw must be 0, 1, 2, 4, 8, 12 or 16 (8-16: fork-free epochs with seqs <= 0xFFFF)");
+        if (value != 0 && value != 1 && value != 2 && value != 4 && value != 8 && value != 12)
+            return h->fail(LX_ERR_ARG, "cpw must be 0, 1, 2, 4, 8 or 12 (8, 12: fork-free epochs with seqs <= 0xFFFF)");
         h->cpw_hint = (uint32_t)value;
     } else if (k == "pack16") {
         h->pack16 = value != 0;

@@ -399,13 +399,22 @@ int fcc_query(lx_index *h, uint32_t a, uint32_t b, uint8_t *out) {
     c->st.calls++;
     int rc;
     const auto t_miss = std::chrono::steady_clock::now();
-    if (c->inflight && (c->inflight_tile || c->find(a) == c->inflight_sa)) {
+    if (c->inflight) {
         // the last fill may still be writing this entry (the caller returned as
-        // soon as its own answer landed): let it finish, then look again
-        if ((rc = fcc_quiesce(h, c))) return rc;
-        if (fcc_hit(c, a, b, out)) {
-            c->st.hits++;
-            return 0;
+        // soon as its own answer landed): when that fill answers it -- its row
+        // (or the tile), a column whose generation has not changed since the
+        // launch -- wait for the entry alone, then it is a hit.  (A tag that
+        // matches is always a right answer: the row belongs to the same asking
+        // event since its clear, and FC(a, b) never changes; only reusing a
+        // row needs the whole fill finished, insert() waits for that.)
+        const uint32_t sa = c->find(a), sb = c->find(b);
+        if (sa != LX_NONE && sb != LX_NONE && (c->inflight_tile || sa == c->inflight_sa) && sa < c->inflight_n &&
+            sb < c->inflight_n && c->g7_launch[sb] == c->g7[sb]) {
+            if ((rc = fcc_wait_answer(h, c, sa, sb))) return rc;
+            if (fcc_hit(c, a, b, out)) {
+                c->st.hits++;
+                return 0;
+            }
         }
     }
     HIPCHK(h, set_dev(h->device));
@@ -461,8 +470,8 @@ int fcc_query(lx_index *h, uint32_t a, uint32_t b, uint8_t *out) {
     c->inflight_tile = tile;
     c->inflight_sa = sa;
     c->inflight_n = c->used;
-    if (c->inflight_fresh) memcpy(c->g7_launch.data(), c->g7, c->used);
-    else HIPCHK(h, hipEventRecord(c->filled, h->stream));
+    memcpy(c->g7_launch.data(), c->g7, c->used);
+    if (!c->inflight_fresh) HIPCHK(h, hipEventRecord(c->filled, h->stream));
     const auto t_wait = std::chrono::steady_clock::now();
     c->st.launch_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t_wait - t_launch).count();
     if ((rc = fcc_wait_answer(h, c, sa, sb))) return rc;

@@ -572,7 +572,6 @@ struct VoteArgs {
 // then fixed up to the reference's rows.
 constexpr uint32_t kMaxSegments = 64;
 constexpr uint64_t kAutoSegEvents = 32768;
-constexpr float kPass16 = 99.0f;  // 16-column slices: not picked until measured (option cpw = 16 forces them)
 constexpr float kPass12 = 2.1f;  // 12-column slices (C3: three walks 50.0 ms vs two 8-column walks 61.2 ms -> 1.7 x 3 / 2 x 50.0 / 61.2)
 constexpr float kPass8 = 1.7f;   // pass cost of 8- vs 1-column slices (8 compute + 7 drain waves; C3 one walk: 121.7 ms at 8 columns, 91.4 at 4 = 1.28)
 struct SegArgs {

@@ -314,11 +314,9 @@ constexpr int kRR = 1024;            // record ring (events)
 
 template <int CPW>
 struct Ring {
-    // slots: 64 KB of units (CPW 2 uses one 16-B unit per slot: 2048 slots in
-    // 32 KB; CPW 16 three 16-B units per slot: 2048 slots in 96 KB)
-    static constexpr int BYTES = CPW == 2 ? 32768 : CPW == 16 ? 98304 : 65536;
-    static constexpr int N = BYTES / (CPW == 1 ? 8 : CPW == 2 ? 16 : CPW == 16 ? 48 : 32);
-    static constexpr int UNITS = CPW == 16 ? 3 : CPW >= 4 ? 2 : 1;   // unit arrays, each followed by a null unit
+    // slots: 64 KB of units (CPW 2 uses one 16-B unit per slot: 2048 slots in 32 KB)
+    static constexpr int BYTES = CPW == 2 ? 32768 : 65536;
+    static constexpr int N = BYTES / (CPW == 1 ? 8 : CPW == 2 ? 16 : 32);
 };
 
 struct alignas(16) WalkShared {
@@ -348,9 +346,7 @@ __device__ __forceinline__ uint32_t lds_ld32(uint32_t addr) {
 // a slot as read: tag(s) and seqs
 template <int CPW>
 struct Slot {
-    uint32_t t0, t1;       // t1 = second unit's tag (CPW 4 - 12), else t0; CPW 16: the second and
-                           // third units' tag when they agree, else their max with bit 31 set
-                           // (never a ready tag; reads as "reused": the L2 row once stored)
+    uint32_t t0, t1;       // t1 = second unit's tag (CPW 4), else t0
     uint32_t v[CPW];
 };
 
@@ -361,23 +357,9 @@ struct Slot {
 __device__ __forceinline__ void unpack16(const u4v &x, uint32_t *v) {
     v[0] = x.y & 0xFFFFu; v[1] = x.y >> 16; v[2] = x.z & 0xFFFFu; v[3] = x.z >> 16;
 }
-template <int CPW, bool PK = false, int RN = 0>
+template <int CPW, bool PK = false>
 __device__ __forceinline__ void ring_read1(uint32_t A, uint32_t B, uint32_t s, Slot<CPW> &o) {
-    if constexpr (PK && CPW == 16) {
-        // three units {tag, s0|s1, s2|s3, s4|s5}, {tag, s6|s7, s8|s9, s10|s11},
-        // {tag, s12|s13, s14|s15, 0}; the third array follows the second
-        u4v x, y, z;
-        asm volatile("ds_read_b128 %0, %3\n\tds_read_b128 %1, %4\n\tds_read_b128 %2, %5\n\ts_waitcnt lgkmcnt(0)"
-                     : "=&v"(x), "=&v"(y), "=&v"(z)
-                     : "v"(A + s * 16u), "v"(B + s * 16u), "v"(B + (uint32_t)(RN + 1) * 16u + s * 16u)
-                     : "memory");
-        o.t0 = x.x;
-        o.t1 = y.x == z.x ? y.x : (max(y.x, z.x) | 0x80000000u);
-        const uint32_t w[8] = {x.y, x.z, x.w, y.y, y.z, y.w, z.y, z.z};
-#pragma unroll
-        for (int k = 0; k < CPW; k++) o.v[k] = (k & 1) ? w[(k / 2) % 8] >> 16 : w[(k / 2) % 8] & 0xFFFFu;
-        return;
-    } else if constexpr (PK && (CPW == 8 || CPW == 12)) {
+    if constexpr (PK && (CPW == 8 || CPW == 12)) {
         // two units {tag, s0 | s1 << 16, s2 | s3 << 16, s4 | s5 << 16}, {tag, s6 | s7 << 16, 0, 0}
         // (12 columns: {tag, s6 | s7 << 16, s8 | s9 << 16, s10 | s11 << 16})
         u4v x, y;
@@ -485,43 +467,8 @@ __device__ __forceinline__ uint32_t quad_and(uint32_t v) {
 // watermark at W, one LDS round trip.  tg[k] = the units' tags (equal for one
 // unit), pv[k] = the parent's CPW seqs.
 template <int CPW, int RN, bool PK = false>
-__device__ __forceinline__ void blk_fold(const uint32_t pa[3], uint32_t W, uint32_t tg[3][3], uint32_t pv[3][CPW],
+__device__ __forceinline__ void blk_fold(const uint32_t pa[3], uint32_t W, uint32_t tg[3][2], uint32_t pv[3][CPW],
                                          uint32_t &cw) {
-    if constexpr (CPW == 16) {
-        // three units per slot (packed column pairs): A at pa, B one array
-        // further, C two arrays further (past the ds offset field: its own address)
-        constexpr uint32_t BOFF = (RN + 1) * 16;
-        static_assert(BOFF < 65536, "ds offset field");
-        u4v xa0, xb0, xc0, xa1, xb1, xc1, xa2, xb2, xc2;
-        const uint32_t c0 = pa[0] + 2 * BOFF, c1 = pa[1] + 2 * BOFF, c2 = pa[2] + 2 * BOFF;
-        asm volatile(
-            "ds_read_b128 %0, %10\n\t"
-            "ds_read_b128 %1, %10 offset:%16\n\t"
-            "ds_read_b128 %2, %13\n\t"
-            "ds_read_b128 %3, %11\n\t"
-            "ds_read_b128 %4, %11 offset:%16\n\t"
-            "ds_read_b128 %5, %14\n\t"
-            "ds_read_b128 %6, %12\n\t"
-            "ds_read_b128 %7, %12 offset:%16\n\t"
-            "ds_read_b128 %8, %15\n\t"
-            "ds_read_b32 %9, %17\n\t"
-            "s_waitcnt lgkmcnt(0)"
-            : "=&v"(xa0), "=&v"(xb0), "=&v"(xc0), "=&v"(xa1), "=&v"(xb1), "=&v"(xc1), "=&v"(xa2), "=&v"(xb2),
-              "=&v"(xc2), "=&v"(cw)
-            : "v"(pa[0]), "v"(pa[1]), "v"(pa[2]), "v"(c0), "v"(c1), "v"(c2), "i"(BOFF), "v"(W)
-            : "memory");
-        const u4v xa[3] = {xa0, xa1, xa2};
-        const u4v xb[3] = {xb0, xb1, xb2};
-        const u4v xc[3] = {xc0, xc1, xc2};
-#pragma unroll
-        for (int k = 0; k < 3; k++) {
-            tg[k][0] = xa[k].x; tg[k][1] = xb[k].x; tg[k][2] = xc[k].x;
-            pv[k][0] = xa[k].y; pv[k][1] = xa[k].z; pv[k][2] = xa[k].w;
-            pv[k][3] = xb[k].y; pv[k][4] = xb[k].z; pv[k][5] = xb[k].w;
-            pv[k][6] = xc[k].y; pv[k][7] = xc[k].z;
-        }
-        return;
-    }
     if constexpr (PK && CPW == 4) {
         u4v x0, x1, x2;
         asm volatile(
@@ -538,7 +485,7 @@ __device__ __forceinline__ void blk_fold(const uint32_t pa[3], uint32_t W, uint3
         for (int k = 0; k < 3; k++) {
             // packed: pv[k][0] = s0 | s1 << 16, pv[k][1] = s2 | s3 << 16 (the
             // fold takes packed 16-bit maxima)
-            tg[k][0] = tg[k][1] = tg[k][2] = x[k].x;
+            tg[k][0] = tg[k][1] = x[k].x;
             pv[k][0] = x[k].y; pv[k][1 % CPW] = x[k].z; pv[k][2 % CPW] = 0u; pv[k][3 % CPW] = 0u;
         }
         return;
@@ -564,7 +511,7 @@ __device__ __forceinline__ void blk_fold(const uint32_t pa[3], uint32_t W, uint3
         const u4v xb[3] = {xb0, xb1, xb2};
 #pragma unroll
         for (int k = 0; k < 3; k++) {
-            tg[k][0] = xa[k].x; tg[k][1] = tg[k][2] = xb[k].x;
+            tg[k][0] = xa[k].x; tg[k][1] = xb[k].x;
             pv[k][0] = xa[k].y; pv[k][1 % CPW] = xa[k].z; pv[k][2 % CPW] = xa[k].w; pv[k][3 % CPW] = xb[k].y;
             if constexpr (CPW == 12) { pv[k][4] = xb[k].z; pv[k][5] = xb[k].w; }
         }
@@ -581,7 +528,7 @@ __device__ __forceinline__ void blk_fold(const uint32_t pa[3], uint32_t W, uint3
             : "memory");
         const u4v x[3] = {x0, x1, x2};
 #pragma unroll
-        for (int k = 0; k < 3; k++) { tg[k][0] = tg[k][1] = tg[k][2] = x[k].x; pv[k][0] = x[k].y; pv[k][1 % CPW] = x[k].z; }
+        for (int k = 0; k < 3; k++) { tg[k][0] = tg[k][1] = x[k].x; pv[k][0] = x[k].y; pv[k][1 % CPW] = x[k].z; }
     } else {
         u2v x0, x1, x2;
         asm volatile(
@@ -595,7 +542,7 @@ __device__ __forceinline__ void blk_fold(const uint32_t pa[3], uint32_t W, uint3
             : "memory");
         const u2v x[3] = {x0, x1, x2};
 #pragma unroll
-        for (int k = 0; k < 3; k++) { tg[k][0] = tg[k][1] = tg[k][2] = x[k].x; pv[k][0] = x[k].y; }
+        for (int k = 0; k < 3; k++) { tg[k][0] = tg[k][1] = x[k].x; pv[k][0] = x[k].y; }
     }
 }
 
@@ -604,24 +551,21 @@ __device__ __forceinline__ void blk_fold(const uint32_t pa[3], uint32_t W, uint3
 // epoch <= 0xFFFF).
 template <int CPW, int NCW, bool MASKED, bool PK, int ND_ = kND>
 __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t slice) {
-    static_assert(!PK || CPW >= 4, "packed slots: 4-, 8-, 12- or 16-column slices");
-    static_assert(CPW == 1 || CPW == 2 || CPW == 4 || ((CPW == 8 || CPW == 12 || CPW == 16) && PK && !MASKED),
-                  "slot layout");
+    static_assert(!PK || CPW >= 4, "packed slots: 4-, 8- or 12-column slices");
+    static_assert(CPW == 1 || CPW == 2 || CPW == 4 || ((CPW == 8 || CPW == 12) && PK && !MASKED), "slot layout");
     static_assert(LX_MAXP == 12, "block walker: 12 inline parents, three per lane of a quad");
     constexpr int ND = ND_;
     static_assert(ND >= 1 && ND <= 8, "drain waves");
-    // (16 columns: the 96-KB slot ring leaves room for a 512-record ring)
-    constexpr int RR = CPW == 16 ? 512 : kRR;
+    constexpr int RR = kRR;
     constexpr int NT = 64 * (NCW + 1 + ND);
     constexpr int RQ = LX_REC_Q;
-    constexpr int KB = CPW >= 12 ? 64 : 1024 / CPW;   // recent (seq -> event) entries per owned branch
+    constexpr int KB = CPW == 12 ? 64 : 1024 / CPW;   // recent (seq -> event) entries per owned branch
     constexpr int RN = Ring<CPW>::N;
     constexpr int RB16 = Ring<CPW>::BYTES / 16;
     static_assert(RR % 64 == 0 && RR / 64 >= 4 && RR >= 2 * 16 * NCW, "record ring");
     // slot units (A array, then B array for CPW 4), each followed by a null
     // slot (tag kNullTag, values 0) that absent parents point at
-    constexpr int NU = Ring<CPW>::UNITS;
-    __shared__ uint4 ring[RB16 + NU];
+    __shared__ uint4 ring[RB16 + 2];
     __shared__ uint4 rrec[RR * RQ];              // event records
     __shared__ uint32_t rtag[RR / 64];           // per record round: batch round index + 1
     __shared__ uint2 brc[CPW * KB];              // {seq, event} of recent events of owned branches
@@ -634,15 +578,14 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
     // null slot: unit A right after the A array (uint4 index RN, or RN / 2 for
     // 8-B units), unit B (CPW 4) after the B array
     constexpr int kNullA = CPW == 1 ? RN / 2 : RN;
-    for (int i = threadIdx.x; i < RB16 + NU; i += NT)
-        ring[i] = make_uint4((i == kNullA || (NU >= 2 && i == 2 * RN + 1) || (NU == 3 && i == 3 * RN + 2)) ? kNullTag : 0u,
-                             0, 0, 0);
+    for (int i = threadIdx.x; i < RB16 + 2; i += NT)
+        ring[i] = make_uint4((i == kNullA || (CPW >= 4 && i == 2 * RN + 1)) ? kNullTag : 0u, 0, 0, 0);
     for (int i = threadIdx.x; i < RR / 64; i += NT) rtag[i] = 0;
     for (int i = threadIdx.x; i < CPW * KB; i += NT) brc[i] = make_uint2(0, LX_NONE);
     if (threadIdx.x < ND) { sh.copied[threadIdx.x] = 0; sh.stored[threadIdx.x] = 0; }
     if (threadIdx.x < CPW) {
         const uint32_t ci = slice * CPW + threadIdx.x;
-        sjs[threadIdx.x] = a.seg && ci < a.ncols ? a.seg_j[CPW >= 12 ? ci : a.col_list[ci]] : 0u;
+        sjs[threadIdx.x] = a.seg && ci < a.ncols ? a.seg_j[CPW == 12 ? ci : a.col_list[ci]] : 0u;
     }
     if (threadIdx.x == 0) { sh.req = 0; sh.p_issued = 0; sh.p_done = 0; }
     __syncthreads();
@@ -665,7 +608,7 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
     for (int k = 0; k < CPW; k++) {
         const uint32_t ci = slice * CPW + k;
         valid[k] = ci < a.ncols;
-        if constexpr (CPW >= 12) {
+        if constexpr (CPW == 12) {
             // whole handles only (launch_index): the column list is the identity
             col[k] = valid[k] ? ci : 0;
             pc[k] = col[k];
@@ -775,7 +718,7 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
             while (true) {
                 bool ready = true;
                 if (ev < n) {
-                    ring_read1<CPW, PK, RN>(RA, RB, sl, me);
+                    ring_read1<CPW, PK>(RA, RB, sl, me);
                     ready = me.t0 == ev + 1 && me.t1 == ev + 1;
                 }
                 if (__all(ready)) break;
@@ -801,7 +744,7 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
                     bool got = false;
                     if (pl < n) {
                         Slot<CPW> ps;
-                        ring_read1<CPW, PK, RN>(RA, RB, pl % RN, ps);
+                        ring_read1<CPW, PK>(RA, RB, pl % RN, ps);
                         if (ps.t0 == pl + 1 && ps.t1 == pl + 1) {
 #pragma unroll
                             for (int k = 0; k < CPW; k++) h0[k] = ps.v[k];
@@ -878,29 +821,23 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
                                 a.lap[((uint64_t)pc[k] * a.s_cap + (s - first[k])) * a.lap_stride + br] = seq;
                     } else {
                         // the first (usually only) seq of every column's range: all
-                        // the recent-event lookups in one LDS round trip (16-column
-                        // slices: two of eight columns, fewer live registers)
-                        constexpr int CH = CPW == 16 ? 8 : CPW;
+                        // the recent-event lookups in one LDS round trip
+                        uint64_t c0[CPW];
 #pragma unroll
-                        for (int k0 = 0; k0 < CPW; k0 += CH) {
-                            uint64_t c0[CH];
+                        for (int k = 0; k < CPW; k++)
+                            c0[k] = __hip_atomic_load(reinterpret_cast<const uint64_t *>(brc + k * KB + lo[k] % KB),
+                                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 #pragma unroll
-                            for (int k = 0; k < CH; k++)
-                                c0[k] = __hip_atomic_load(reinterpret_cast<const uint64_t *>(brc + (k0 + k) * KB + lo[k0 + k] % KB),
-                                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#pragma unroll
-                            for (int kk = 0; kk < CH; kk++) {
-                                const int k = k0 + kk;
-                                for (uint32_t s = lo[k]; s <= hi[k]; s++) {
-                                    const uint64_t cc = s == lo[k] ? c0[kk]
-                                                                   : __hip_atomic_load(reinterpret_cast<const uint64_t *>(brc + k * KB + s % KB),
-                                                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                                    uint32_t row = (uint32_t)(cc >> 32);
-                                    LX_WP(d_fill++;)
-                                    LX_WP(if ((uint32_t)cc != s) d_miss++;)
-                                    if ((uint32_t)cc != s) row = ld_l2_now(a.brow + (uint64_t)col[k] * a.s_cap + (s - first[k]));
-                                    a.la[(uint64_t)row * stride + br] = seq;
-                                }
+                        for (int k = 0; k < CPW; k++) {
+                            for (uint32_t s = lo[k]; s <= hi[k]; s++) {
+                                const uint64_t cc = s == lo[k] ? c0[k]
+                                                               : __hip_atomic_load(reinterpret_cast<const uint64_t *>(brc + k * KB + s % KB),
+                                                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                                uint32_t row = (uint32_t)(cc >> 32);
+                                LX_WP(d_fill++;)
+                                LX_WP(if ((uint32_t)cc != s) d_miss++;)
+                                if ((uint32_t)cc != s) row = ld_l2_now(a.brow + (uint64_t)col[k] * a.s_cap + (s - first[k]));
+                                a.la[(uint64_t)row * stride + br] = seq;
                             }
                         }
                     }
@@ -1042,10 +979,9 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
                 wstuck = __any(far_parent(px, lp, (uint32_t)RN - kLeanFar)) ? kLeanStuck : 0u;
                 {
                     const uint32_t rs = (lp % RN) * UA;
-                    wa_pub = j == 0 ? RA + rs : (((CPW == 4 && !PK) || CPW >= 8) && j == 1) ? RB + (lp % RN) * 16u
-                             : (CPW == 16 && j == 2) ? RB + (uint32_t)(RN + 1) * 16u + (lp % RN) * 16u : dmy;
-                    if constexpr (CPW >= 12) {
-                        // lane j of a quad owns columns j, j + 4, j + 8 (, j + 12) (recent-event entries)
+                    wa_pub = j == 0 ? RA + rs : (((CPW == 4 && !PK) || CPW >= 8) && j == 1) ? RB + (lp % RN) * 16u : dmy;
+                    if constexpr (CPW == 12) {
+                        // lane j of a quad owns columns j, j + 4, j + 8 (recent-event entries)
                         uint32_t wb = dmy + 1024u;
 #pragma unroll
                         for (int k = 0; k < CPW; k++)
@@ -1084,16 +1020,14 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
             // reads carried the expected tags, so that pass's unconditional
             // max over them is the event's value; r holds only what does not
             // come from the ring (own seq, L2 rows of old / overflow parents)
-            uint32_t tg[3][3], pv[3][CPW];
+            uint32_t tg[3][2], pv[3][CPW];
             blk_fold<CPW, RN, PK>(pa, wm_addr, tg, pv, cw);
             // tag mismatches OR-ed on the VALU: no compare masks and no mask
             // ANDs on the scalar unit, which the CU's waves share (C3 -1.9 %,
             // C2 -5.2 % against v_cmp + s_and)
             uint32_t tx = 0;
 #pragma unroll
-            for (int k = 0; k < 3; k++)
-                tx |= (tg[k][0] ^ px[k]) | ((PK && CPW == 4) || CPW < 4 ? 0u : (tg[k][1] ^ px[k])) |
-                      (CPW == 16 ? (tg[k][2] ^ px[k]) : 0u);
+            for (int k = 0; k < 3; k++) tx |= (tg[k][0] ^ px[k]) | ((PK && CPW == 4) || CPW < 4 ? 0u : (tg[k][1] ^ px[k]));
             uint32_t m[CPW];
             constexpr int NH = CPW / 2 > 0 ? CPW / 2 : 1;
             uint32_t mp[NH];   // PK: the quad's maxima, two columns per dword
@@ -1129,7 +1063,7 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
                 bool ok = false, old = lpp >= n;
                 if (!old) {
                     Slot<CPW> ps;
-                    ring_read1<CPW, PK, RN>(RA, RB, lpp % RN, ps);
+                    ring_read1<CPW, PK>(RA, RB, lpp % RN, ps);
                     if (ps.t0 == lpp + 1 && ps.t1 == lpp + 1) {
 #pragma unroll
                         for (int c = 0; c < CPW; c++) r[c] = max(r[c], ps.v[c]);
@@ -1178,13 +1112,6 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
                     u2v x;
                     x.x = lp + 1; x.y = m[0];
                     asm volatile("ds_write_b64 %2, %3\n\tds_write_b64 %0, %1" : : "v"(wa), "v"(x), "v"(wb), "v"(y) : "memory");
-                } else if constexpr (PK && CPW == 16) {
-                    u4v x;   // lane 0: {tag, s01, s23, s45}, lane 1: {tag, s67, s89, s1011}, lane 2: {tag, s1213, s1415, 0}
-                    x.x = lp + 1;
-                    x.y = j == 0 ? mp[0] : j == 1 ? mp[3] : mp[6];
-                    x.z = j == 0 ? mp[1] : j == 1 ? mp[4] : mp[7];
-                    x.w = j == 0 ? mp[2] : j == 1 ? mp[5] : 0u;
-                    asm volatile("ds_write_b64 %2, %3\n\tds_write_b128 %0, %1" : : "v"(wa), "v"(x), "v"(wb), "v"(y) : "memory");
                 } else if constexpr (PK && CPW >= 8) {
                     u4v x;   // lane 0: {tag, s01, s23, s45}, lane 1: {tag, s67, 0, 0} (12: {tag, s67, s89, s1011})
                     x.x = lp + 1; x.y = j == 0 ? mp[0] : mp[3 % NH];
@@ -1289,7 +1216,7 @@ __device__ __forceinline__ bool seg_chunk(uint32_t g, uint32_t G, uint32_t S, ui
 template <int CPW, int NCW, bool MASKED, bool PK, int ND = kND>
 __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index_segs(IndexArgs a0) {
     uint32_t k, slice;
-    if constexpr (CPW >= 12) {
+    if constexpr (CPW == 12) {
         if (!seg_chunk(blockIdx.x, a0.seg_g, a0.n_slices, &k, &slice)) return;
     } else {
         const uint32_t per = gridDim.x / a0.seg_g, w = blockIdx.x % per;
@@ -1318,8 +1245,8 @@ static hipError_t launch_index_t(const IndexArgs &a0, hipStream_t s) {
     const dim3 blk(64 * (NCW + 1 + ND));
     if constexpr (CPW >= 8) {   // packed fork-free epochs only
         if (!a.pack16 || a.mask) return hipErrorInvalidValue;
-        // (12 / 16 columns: at most ceil(seg_g * slices / 8) workgroups per XCD, seg_chunk)
-        const uint32_t sgrid = CPW >= 12 ? 8 * (a.seg_g * (a.n_slices / 8) + (a.seg_g * (a.n_slices % 8) + 7) / 8)
+        // (12 columns: at most ceil(seg_g * slices / 8) workgroups per XCD, seg_chunk)
+        const uint32_t sgrid = CPW == 12 ? 8 * (a.seg_g * (a.n_slices / 8) + (a.seg_g * (a.n_slices % 8) + 7) / 8)
                                          : grid * a.seg_g;
         if (a.seg_g) hipLaunchKernelGGL((k_index_segs<CPW, NCW, false, true, ND>), dim3(sgrid), blk, 0, s, a);
         else hipLaunchKernelGGL((k_index<CPW, NCW, false, true, ND>), dim3(grid), blk, 0, s, a);
@@ -1367,9 +1294,6 @@ hipError_t launch_index(const IndexArgs &a, hipStream_t s) {
     if (cpw == 8) return launch_index_t<8, 8, 7>(a, s);
     // 12 columns (V = 1000: 84 slices, three walks side by side on 256 CUs)
     if (cpw == 12) return a.cmap ? launch_index_t<8, 8, 7>(a, s) : launch_index_t<12, 8, 7>(a, s);
-    // 16 columns (V = 1000: 63 slices, four walks side by side; three 16-B slot
-    // units, a 512-record ring)
-    if (cpw == 16) return a.cmap ? launch_index_t<8, 8, 7>(a, s) : launch_index_t<16, 8, 7>(a, s);
     return launch_index_t<4, 11>(a, s);
 }
 
@@ -1441,8 +1365,8 @@ __device__ __forceinline__ bool fc_bad(const FcArgs &a, uint32_t A, uint32_t Bq)
 
 // LowestAfter row of b: the plane's own row, or (RS: a row-segment rank, b
 // another rank's event) the row received for this batch.  A compile-time
-// switch: the whole-index kernels carry none of it (their registers, and so
-// their occupancy, stay as before)
+// switch: the whole-index kernels carry none of it (an extra branch per
+// query had cost k_fc<64> two VGPRs and a wave per SIMD: C3 FC 6.7 -> 9.9 ms)
 template <bool RS>
 __device__ __forceinline__ const uint32_t *fc_la(const FcArgs &a, uint32_t Bq) {
     if constexpr (RS)

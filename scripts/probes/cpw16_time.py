@@ -1,4 +1,7 @@
-"""C3 walk on 16-column slices (three 16-B slot units, 63 slices at V = 1000,
+"""(Needs the 16-column walker of commit 85cab53, measured slower and removed
+from the library: profiles/r05/cpw16/)
+
+C3 walk on 16-column slices (three 16-B slot units, 63 slices at V = 1000,
 four Add-order segments side by side on 256 CUs) against the shipped
 12-column form (three segments), same box, alternating A B A B; the planes
 of the two forms compared on the device (both must equal the 4-column walk

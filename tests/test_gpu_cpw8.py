@@ -39,7 +39,7 @@ def planes_of(lx, d, w, opts):
     return ix, out
 
 
-@pytest.mark.parametrize("cpw", [8, 12, 16])
+@pytest.mark.parametrize("cpw", [8, 12])
 @pytest.mark.parametrize("shape", [(24, 250, 6), (13, 400, 5), (30, 120, 16), (200, 60, 10)])
 def test_cpw8_walk_vs_oracle_and_cpw4(lx, shape, cpw):
     """One walk on 8-column slices (ring slots reused, parents beyond the
@@ -63,7 +63,7 @@ def test_cpw8_walk_vs_oracle_and_cpw4(lx, shape, cpw):
     ix4.close()
 
 
-@pytest.mark.parametrize("cpw,G", [(8, 4), (12, 3), (12, 4), (16, 4), (16, 2)])
+@pytest.mark.parametrize("cpw,G", [(8, 4), (12, 3), (12, 4)])
 @pytest.mark.parametrize("shape", [(64, 2100, 10), (100, 1400, 8), (1000, 60, 10)])
 def test_cpw8_side_by_side_segments(lx, shape, cpw, G):
     """Segments side by side on 8- / 12-column slices (one k_index_segs
@@ -82,7 +82,7 @@ def test_cpw8_side_by_side_segments(lx, shape, cpw, G):
     ix1.close()
 
 
-@pytest.mark.parametrize("cpw", [8, 12, 16])
+@pytest.mark.parametrize("cpw", [8, 12])
 def test_cpw8_falls_back_with_forks(lx, cpw):
     """cpw = 8 / 12 on a fork epoch walks 4-column slices (8-column slots need
     packed fork-free values): rows still equal the oracle."""
