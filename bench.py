@@ -609,13 +609,14 @@ def main():
     def fc_bytes_read(nq, B, early):
         """Bytes k_fc reads for nq queries over rows of B branches: whole rows
         (8 B per branch: HB(a) 4 B + LA(b) 4 B) without the early exit; with it
-        (device counters: queries decided on the early path, of them past the
-        first round, past the second) 2 x 1 KB per early-path query (the 256
-        heaviest columns of both rows), 2 x 1 KB more past the first round, the
-        rest of both rows past the second."""
-        qe, q2, qw = early
+        (k_fc_early, device counters: queries on the early path, of them the
+        ones that read columns 128-255, 256-511, the rest) 2 x 512 B per query
+        (the 128 heaviest columns of both rows), 2 x 512 B more past round 1,
+        2 x 1 KB past round 2, the rest of both rows past round 3."""
+        qe, q2, q3, qw = early
         row16 = ((B + 3) // 4) * 16
-        return qe * 2048.0 + q2 * 2048.0 + qw * 2.0 * max(0, row16 - 2048) + (nq - qe) * 8.0 * B
+        return (qe * 1024.0 + q2 * 1024.0 + q3 * 2048.0 + qw * 2.0 * max(0, row16 - 4096) +
+                (nq - qe) * 8.0 * B)
 
     def leg(kind):
         """One index + ForklessCause measurement: kind 'single' (one GPU, or
@@ -714,7 +715,7 @@ def main():
         ix.sync()
         barrier()
         evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-        ix.fc_early_counters()          # reset (the warmup's launches)
+        ix.fc_early_rounds()            # reset (the warmup's launches)
         t1 = time.perf_counter()
         for k in range(args.steps):
             fc_step(evs[k])
@@ -725,7 +726,7 @@ def main():
         # k_fc's own time on this rank: the launch (single / shard partial), or
         # the launch inside the row-segment protocol (the rest is routing)
         fc_kernel_ms = float(np.mean(kern_ms)) if kind == "rowseg" else step_ms
-        early = ix.fc_early_counters()
+        early = ix.fc_early_rounds()
         # the queries this rank's k_fc answered per step: its own, or (row
         # segments) the ones routed to it as owner(a)
         nq = rsx.last_fc["answered"] if kind == "rowseg" else args.fc_queries
@@ -744,8 +745,8 @@ def main():
                "k_assign_ms": k_assign_ms, "fc_kernel_ms": fc_kernel_ms, "fc_step_ms": step_ms, "B": B,
                "fc_read": fc_read, "fc_achieved": fc_read_all / (fc_ms_all * 1e-3) / 1e9,
                "fc_kernel_ms_max": max_over_ranks(fc_kernel_ms),
-               "early": {"queries": int(early_all[0]), "second_round": int(early_all[1]),
-                         "whole_rows": int(early_all[2]), "answered": int(nq_all) * args.steps}
+               "early": {"queries": int(early_all[0]), "round2": int(early_all[1]), "round3": int(early_all[2]),
+                         "whole_rows": int(early_all[3]), "answered": int(nq_all) * args.steps}
                if early_all[0] else None,
                "whole_row_bytes": 8.0 * B * nq, "st_x": st_x,
                "mem": ix.device_bytes()}
@@ -793,6 +794,8 @@ def main():
     events_per_s = N * args.steps * units / t_index
     fc_per_s = args.fc_queries * args.steps * fc_units / t_fc
     fc_bytes = P["whole_row_bytes"]
+    # the ForklessCause kernel this run timed (its traffic figure must be its own)
+    fc_kernel_name = "k_fc_early" if P["early"] else "k_fc"
     fc_read = P["fc_read"]
     fc_achieved = P["fc_achieved"]
     kidx = float(np.mean(k_index_ms))
@@ -844,15 +847,15 @@ def main():
         "fc_ms_per_step": t_fc / args.steps * 1e3,
         "index_kernel_ms": kidx,
         "assign_and_marks_ms": float(np.mean(k_assign_ms)),
-        "roofline": {"bound": "hbm", "kernel": "k_fc (ForklessCause)", "achieved": fc_achieved, "peak": HBM_PEAK_GBS,
+        "roofline": {"bound": "hbm", "kernel": fc_kernel_name, "achieved": fc_achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": fc_achieved / HBM_PEAK_GBS,
                      "bytes_read_per_launch": fc_read,
-                     "early_exit": dict(P["early"], note="device counters summed over the ranks: queries the 256 "
-                                        "heaviest validators' columns decide read 2 x 1 KB, the next 256 columns 2 x 1 KB "
-                                        "more, the rest only past both; achieved = the ranks' bytes read / the sum of "
-                                        "their k_fc times (per-GPU bandwidth); algorithmic_bytes_per_launch is SURVEY "
-                                        "8d's whole-row figure") if P["early"] else None,
-                     "traffic": traffic["k_fc"]["hbm_bytes"] if traffic and "k_fc" in traffic else None,
+                     "early_exit": dict(P["early"], note="k_fc_early, device counters summed over the ranks: every "
+                                        "query reads columns 0-127 of both rows (2 x 512 B), round2 of them 128-255 "
+                                        "(2 x 512 B more), round3 256-511 (2 x 1 KB), whole_rows the rest; achieved = "
+                                        "the ranks' bytes read / the sum of their k_fc times (per-GPU bandwidth); "
+                                        "algorithmic_bytes_per_launch is SURVEY 8d's whole-row figure") if P["early"] else None,
+                     "traffic": traffic[fc_kernel_name]["hbm_bytes"] if traffic and fc_kernel_name in traffic else None,
                      "traffic_source": traffic_src,
                      "algorithmic_bytes_per_launch": fc_bytes, "kernel_ms": fc_kernel_ms,
                      "kernel_ms_max_over_ranks": P["fc_kernel_ms_max"],

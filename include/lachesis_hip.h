@@ -215,13 +215,16 @@ typedef struct lx_fc_stats {
 } lx_fc_stats;
 int lx_fc_cache_stats(const lx_index *h, lx_fc_stats *out);
 
-/* Batched ForklessCause's early exit (option fc_early) since the last call:
- * queries the kernel decided on its early path (device count; the path runs
- * on fork-free epochs whose rows exceed 512 columns and whose 256 heaviest
- * validators can reach the quorum alone); of them, how many read a second round (columns
- * 256-511 of HB(a) and LA(b), 2 x 1 KB more) and how many read the rest of
- * both rows (the others read 2 x 1 KB: the 256 heaviest columns).
- * Synchronizes the handle's stream; resets the counts.  Diagnostics (bench). */
+/* Batched ForklessCause's early exit (option fc_early) since the last call.
+ * The path runs on fork-free epochs whose rows exceed 512 columns and whose
+ * 512 heaviest validators can reach the quorum alone; it reads both rows in
+ * rounds of columns [0, 128), [128, 256), [256, 512) and the rest, each only
+ * when the count so far leaves the quorum open.  lx_fc_early_rounds: out[0]
+ * queries decided on the path (device count), out[1..3] of them the ones that
+ * read round 2, round 3, the rest.  lx_fc_early_counters: (out[0], out[1],
+ * out[3]).  Synchronize the handle's stream; reset the counts.  Diagnostics
+ * (bench). */
+int lx_fc_early_rounds(lx_index *h, uint64_t out[4]);
 int lx_fc_early_counters(lx_index *h, uint64_t *queries, uint64_t *second_round, uint64_t *whole_rows);
 
 /* Column-sharded partial: stake sum over this shard's creators, plus

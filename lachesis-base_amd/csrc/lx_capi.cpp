@@ -885,18 +885,20 @@ int lx_fc_args(lx_index *h, uint64_t n, const uint32_t *a, const uint32_t *b, ui
     f.own_hi = h->own_hi;
     f.branch_creator = h->branch_creator;
     f.status = h->status;
-    // early exit for k_fc (fork-free, whole rows): when the heaviest 256
-    // columns can reach the quorum alone, their count decides most queries
-    // (launch_fc gives rows of more than 128 uint4 64 lanes per query, the only
-    // width whose kernel has the early path: the gate matches what runs)
+    // early exit (k_fc_early: fork-free whole rows of more than 512 columns --
+    // launch_fc's 64-lane width, the gate matches what runs): rounds of the
+    // first 128, 256, 512 columns and the rest, when the heaviest 512 columns
+    // can reach the quorum alone (else no round before the last can decide)
     if (!partial && !h->sharded() && h->B == h->V && h->fc_early && f.vhi4 - f.vlo4 > 128) {
-        uint64_t w0 = 0, w1 = 0, wt = 0;
+        uint64_t w128 = 0, w256 = 0, w512 = 0, wt = 0;
         for (uint32_t c = f.vlo4 * 4; c < h->V && c < f.vhi4 * 4; c++) {
+            const uint32_t k = c - f.vlo4 * 4;
             wt += h->weights[c];
-            if (c < f.vlo4 * 4 + 256) w0 += h->weights[c];
-            else if (c < f.vlo4 * 4 + 512) w1 += h->weights[c];
+            if (k < 128) w128 += h->weights[c];
+            if (k < 256) w256 += h->weights[c];
+            if (k < 512) w512 += h->weights[c];
         }
-        if (w0 >= h->quorum && wt - w0 <= 0xFFFFFFFFull) {
+        if (w512 >= h->quorum && wt - w128 <= 0xFFFFFFFFull) {
             if (!h->d_fc_full) {
                 // zeroed and synchronized before any launch can count into it,
                 // whatever stream runs that launch
@@ -911,8 +913,9 @@ int lx_fc_args(lx_index *h, uint64_t n, const uint32_t *a, const uint32_t *b, ui
                 h->d_fc_full = p;
             }
             f.early = 1;
-            f.early_rest = (uint32_t)(wt - w0);
-            f.early_rest2 = (uint32_t)(wt - w0 - w1);
+            f.early_rest = (uint32_t)(wt - w128);
+            f.early_rest2 = (uint32_t)(wt - w256);
+            f.early_rest3 = (uint32_t)(wt - w512);
             f.early_full = h->d_fc_full;
         }
     }
@@ -1755,19 +1758,31 @@ void lx_destroy(lx_index *h) {
 
 const char *lx_last_error(const lx_index *h) { return h ? h->err.c_str() : "null handle"; }
 
-int lx_fc_early_counters(lx_index *h, uint64_t *queries, uint64_t *second_round, uint64_t *whole_rows) {
-    if (!h || !queries || !second_round || !whole_rows) return LX_ERR_ARG;
+int lx_fc_early_rounds(lx_index *h, uint64_t out[4]) {
+    if (!h || !out) return LX_ERR_ARG;
     HIPCHK(h, set_dev(h->device));
-    uint64_t c[3] = {0, 0, 0};
+    uint64_t c[4] = {0, 0, 0, 0};
     if (h->d_fc_full) {
         HIPCHK(h, hipStreamSynchronize(h->stream));
-        HIPCHK(h, hipMemcpy(c, h->d_fc_full, 24, hipMemcpyDeviceToHost));
-        HIPCHK(h, hipMemsetAsync(h->d_fc_full, 0, 24, h->stream));
+        HIPCHK(h, hipMemcpy(c, h->d_fc_full, 32, hipMemcpyDeviceToHost));
+        HIPCHK(h, hipMemsetAsync(h->d_fc_full, 0, 32, h->stream));
         HIPCHK(h, hipStreamSynchronize(h->stream));
     }
-    *queries = c[2];   // queries the kernel decided on the early path (device count)
-    *second_round = c[0];
-    *whole_rows = c[1];
+    out[0] = c[2];   // queries the kernel decided on the early path (device count)
+    out[1] = c[0];   // of them read columns 128-255
+    out[2] = c[1];   // ... 256-511
+    out[3] = c[3];   // ... the rest of both rows
+    return 0;
+}
+
+int lx_fc_early_counters(lx_index *h, uint64_t *queries, uint64_t *second_round, uint64_t *whole_rows) {
+    if (!queries || !second_round || !whole_rows) return LX_ERR_ARG;
+    uint64_t r[4];
+    const int rc = lx_fc_early_rounds(h, r);
+    if (rc) return rc;
+    *queries = r[0];
+    *second_round = r[1];
+    *whole_rows = r[3];
     return 0;
 }
 

@@ -162,15 +162,16 @@ struct FcArgs {
     const uint32_t *wpad;        // weight per column (0 outside [vlo, vhi) originals)
     uint32_t vlo4, vhi4;         // column range in uint4 units
     uint32_t quorum;
-    // early exit (k_fc, fork-free, 64 lanes per query; 0 = off): the weight
-    // of the columns outside the first 256 of the range.  The first 256
-    // columns are the heaviest validators (pos.Validators idx order), so
+    // early exit (k_fc_early: fork-free rows of > 512 columns; 0 = off): the
+    // weight of the columns past the first 128, 256 and 512 of the range.  The
+    // first columns are the heaviest validators (pos.Validators idx order), so
     // their count alone often decides the quorum either way
     uint32_t early_rest;
-    uint32_t early_rest2;        // the weight past the first 512 columns
+    uint32_t early_rest2;
+    uint32_t early_rest3;
     uint32_t early;
-    unsigned long long *early_full;   // [0] += queries past the first round, [1] += past the second,
-                                      // [2] += queries decided on the early path
+    unsigned long long *early_full;   // [0] += queries past round 1, [1] += past round 2, [2] += queries
+                                      // on the early path, [3] += past round 3 (whole rows)
     const uint32_t *ev_branch;
     const uint32_t *ev_creator;  // creator per event (= creator of its branch)
     // cheaters of this shard: CSR over all their branches (first = original)

@@ -1391,85 +1391,6 @@ __global__ __launch_bounds__(256) void k_fc(FcArgs a) {
         const uint32_t i = lane + t * LPQ;
         wr[t] = i < nv ? wv[i] : make_uint4(0, 0, 0, 0);
     }
-    uint32_t n_full = 0, n_rest = 0, n_early = 0;   // early exit: queries past the first round / the second / all
-    if constexpr (!FORKS && LPQ == 64) {
-        if (a.early) {
-            // the heaviest 256 columns first (lane i: uint4 i of both rows); the
-            // rest of both rows only when their count leaves the quorum open
-            // (same answer: the sum is only compared with the quorum).  The
-            // next query's first round is in flight while this one is decided.
-            const uint64_t step = (uint64_t)gridDim.x * qpb;
-            uint64_t q = blockIdx.x * qpb + threadIdx.x / LPQ;
-            uint32_t A = 0, Bq = 0;
-            bool bad = false;
-            u4v hv = {0, 0, 0, 0}, lv = {0, 0, 0, 0};
-            auto first = [&](uint64_t qq, uint32_t &A_, uint32_t &B_, bool &bad_, u4v &h_, u4v &l_) {
-                A_ = a.qa_bcast ? a.qa_imm : a.qa[qq];
-                B_ = a.qb[qq];
-                bad_ = fc_bad(a, A_, B_);
-                if (bad_) { A_ = a.ev_lo; B_ = a.ev_lo; }
-                h_ = __builtin_nontemporal_load(reinterpret_cast<const u4v *>(a.hb + (uint64_t)A_ * a.stride) + a.vlo4 + lane);
-                l_ = __builtin_nontemporal_load(reinterpret_cast<const u4v *>(fc_la<RS>(a, B_)) + a.vlo4 + lane);
-            };
-            if (q < a.n) first(q, A, Bq, bad, hv, lv);
-            for (; q < a.n; q += step) {
-                uint32_t An = 0, Bn = 0;
-                bool badn = false;
-                u4v hn = {0, 0, 0, 0}, ln = {0, 0, 0, 0};
-                if (q + step < a.n) first(q + step, An, Bn, badn, hn, ln);
-                uint32_t s0 = fc_term(lv.x, hv.x, wr[0].x, false) + fc_term(lv.y, hv.y, wr[0].y, false) +
-                              fc_term(lv.z, hv.z, wr[0].z, false) + fc_term(lv.w, hv.w, wr[0].w, false);
-#pragma unroll
-                for (int off = 32; off > 0; off >>= 1) s0 += __shfl_xor(s0, off, 64);
-                uint32_t sum = s0;
-                if (s0 < a.quorum && s0 + a.early_rest >= a.quorum) {
-                    const uint4 *ha = reinterpret_cast<const uint4 *>(a.hb + (uint64_t)A * a.stride) + a.vlo4;
-                    const uint4 *lb = reinterpret_cast<const uint4 *>(fc_la<RS>(a, Bq)) + a.vlo4;
-                    // second round (columns 256-511), then the same test once more
-                    uint32_t s1 = 0;
-                    if (lane + 64 < nv) {
-                        const u4v hh = __builtin_nontemporal_load(reinterpret_cast<const u4v *>(ha + lane + 64));
-                        const u4v ll = __builtin_nontemporal_load(reinterpret_cast<const u4v *>(lb + lane + 64));
-                        s1 = fc_term(ll.x, hh.x, wr[1].x, false) + fc_term(ll.y, hh.y, wr[1].y, false) +
-                             fc_term(ll.z, hh.z, wr[1].z, false) + fc_term(ll.w, hh.w, wr[1].w, false);
-                    }
-#pragma unroll
-                    for (int off = 32; off > 0; off >>= 1) s1 += __shfl_xor(s1, off, 64);
-                    sum += s1;
-                    n_full++;
-                }
-                if (sum < a.quorum && sum + a.early_rest2 >= a.quorum && s0 < a.quorum && s0 + a.early_rest >= a.quorum) {
-                    const uint4 *ha = reinterpret_cast<const uint4 *>(a.hb + (uint64_t)A * a.stride) + a.vlo4;
-                    const uint4 *lb = reinterpret_cast<const uint4 *>(fc_la<RS>(a, Bq)) + a.vlo4;
-                    uint32_t s1 = 0;
-                    n_rest++;
-                    for (uint32_t i = lane + 128; i < nv; i += 64) {
-                        const u4v hh = __builtin_nontemporal_load(reinterpret_cast<const u4v *>(ha + i));
-                        const u4v ll = __builtin_nontemporal_load(reinterpret_cast<const u4v *>(lb + i));
-                        const uint4 w = wv[i];
-                        s1 += fc_term(ll.x, hh.x, w.x, false) + fc_term(ll.y, hh.y, w.y, false) +
-                              fc_term(ll.z, hh.z, w.z, false) + fc_term(ll.w, hh.w, w.w, false);
-                    }
-#pragma unroll
-                    for (int off = 32; off > 0; off >>= 1) s1 += __shfl_xor(s1, off, 64);
-                    sum += s1;
-                }
-                if (lane == 0) {
-                    const uint8_t r = bad ? 0xFF : (uint8_t)(sum >= a.quorum);
-                    a.out[q] = a.out_tag && !bad ? (uint8_t)(a.out_tag[q] << 1 | r) : r;
-                    if (bad) atomicOr(&a.status[1], 1u);
-                }
-                A = An; Bq = Bn; bad = badn; hv = hn; lv = ln;
-                n_early++;
-            }
-            if (a.early_full && lane == 0 && n_early) {
-                if (n_full) atomicAdd(a.early_full, (unsigned long long)n_full);
-                if (n_rest) atomicAdd(a.early_full + 1, (unsigned long long)n_rest);
-                atomicAdd(a.early_full + 2, (unsigned long long)n_early);
-            }
-            return;
-        }
-    }
     for (uint64_t q = blockIdx.x * qpb + threadIdx.x / LPQ; q < a.n; q += (uint64_t)gridDim.x * qpb) {
         uint32_t A = a.qa_bcast ? a.qa_imm : a.qa[q], Bq = a.qb[q];
         const bool bad = fc_bad(a, A, Bq);
@@ -1545,6 +1466,109 @@ __global__ __launch_bounds__(256) void k_fc(FcArgs a) {
             }
             if (bad) atomicOr(&a.status[1], 1u);
         }
+    }
+}
+
+// The early exit (option fc_early; fork-free rows of more than 512 columns):
+// ForklessCause compares a stake-weighted count with the quorum
+// (vecfc/forkless_cause.go:63-82), and branch j < V is validator j in
+// pos.Validators order -- heaviest first -- so the count of the first columns
+// often decides the answer: >= quorum is true whatever the rest holds, and
+// count + the weight of every remaining column < quorum is false.  32 lanes
+// per query (two queries per wave), in rounds of columns [0, 128) (1 KB of
+// HB(a) and LA(b)), [128, 256), [256, 512) and the rest, each read only when
+// the count so far leaves the quorum open; the next query's first round is in
+// flight while the current one is decided.  Same answers as the whole-row
+// kernel by construction.  Counters: [0] queries past round 1, [1] past round
+// 2, [2] every query of the early path, [3] past round 3.
+template <bool RS>
+__global__ __launch_bounds__(256) void k_fc_early(FcArgs a) {
+    constexpr int L = 32;
+    const int lane = threadIdx.x % L;
+    const uint64_t qpb = 256 / L;
+    const uint32_t nv = a.vhi4 - a.vlo4;   // > 128 (launch_fc)
+    const uint4 *wv = reinterpret_cast<const uint4 *>(a.wpad) + a.vlo4;
+    // this lane's weights of the first 512 columns: uint4 lane, 32 + lane, 64 + lane, 96 + lane
+    uint4 wr[4];
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+        const uint32_t i = lane + t * L;
+        wr[t] = i < nv ? wv[i] : make_uint4(0, 0, 0, 0);
+    }
+    auto terms = [](const u4v &l, const u4v &h, const uint4 &w) {
+        return fc_term(l.x, h.x, w.x, false) + fc_term(l.y, h.y, w.y, false) + fc_term(l.z, h.z, w.z, false) +
+               fc_term(l.w, h.w, w.w, false);
+    };
+    auto reduce = [](uint32_t v) {
+#pragma unroll
+        for (int off = L / 2; off > 0; off >>= 1) v += __shfl_xor(v, off, L);
+        return v;
+    };
+    uint32_t n1 = 0, n2 = 0, n3 = 0, ne = 0;
+    const uint64_t step = (uint64_t)gridDim.x * qpb;
+    uint64_t q = blockIdx.x * qpb + threadIdx.x / L;
+    uint32_t A = 0, Bq = 0;
+    bool bad = false;
+    u4v hv = {0, 0, 0, 0}, lv = {0, 0, 0, 0};
+    auto first = [&](uint64_t qq, uint32_t &A_, uint32_t &B_, bool &bad_, u4v &h_, u4v &l_) {
+        A_ = a.qa_bcast ? a.qa_imm : a.qa[qq];
+        B_ = a.qb[qq];
+        bad_ = fc_bad(a, A_, B_);
+        if (bad_) { A_ = a.ev_lo; B_ = a.ev_lo; }
+        h_ = __builtin_nontemporal_load(reinterpret_cast<const u4v *>(a.hb + (uint64_t)A_ * a.stride) + a.vlo4 + lane);
+        l_ = __builtin_nontemporal_load(reinterpret_cast<const u4v *>(fc_la<RS>(a, B_)) + a.vlo4 + lane);
+    };
+    if (q < a.n) first(q, A, Bq, bad, hv, lv);
+    for (; q < a.n; q += step) {
+        uint32_t An = 0, Bn = 0;
+        bool badn = false;
+        u4v hn = {0, 0, 0, 0}, ln = {0, 0, 0, 0};
+        if (q + step < a.n) first(q + step, An, Bn, badn, hn, ln);
+        uint32_t sum = reduce(terms(lv, hv, wr[0]));
+        if (sum < a.quorum && sum + a.early_rest >= a.quorum) {
+            // round 2: columns 128-255
+            const u4v *ha = reinterpret_cast<const u4v *>(a.hb + (uint64_t)A * a.stride) + a.vlo4;
+            const u4v *lb = reinterpret_cast<const u4v *>(fc_la<RS>(a, Bq)) + a.vlo4;
+            uint32_t s1 = 0;
+            if (lane + L < nv) s1 = terms(__builtin_nontemporal_load(lb + lane + L), __builtin_nontemporal_load(ha + lane + L), wr[1]);
+            sum += reduce(s1);
+            n1++;
+            if (sum < a.quorum && sum + a.early_rest2 >= a.quorum) {
+                // round 3: columns 256-511, two uint4 per lane in flight
+                uint32_t s2 = 0;
+                const uint32_t i2 = lane + 2 * L, i3 = lane + 3 * L;
+                u4v h2 = {0, 0, 0, 0}, l2 = {0, 0, 0, 0}, h3 = {0, 0, 0, 0}, l3 = {0, 0, 0, 0};
+                if (i2 < nv) { h2 = __builtin_nontemporal_load(ha + i2); l2 = __builtin_nontemporal_load(lb + i2); }
+                if (i3 < nv) { h3 = __builtin_nontemporal_load(ha + i3); l3 = __builtin_nontemporal_load(lb + i3); }
+                s2 = terms(l2, h2, wr[2]) + terms(l3, h3, wr[3]);
+                sum += reduce(s2);
+                n2++;
+                if (sum < a.quorum && sum + a.early_rest3 >= a.quorum) {
+                    // the rest of both rows
+                    uint32_t s3 = 0;
+                    for (uint32_t i = lane + 4 * L; i < nv; i += L) {
+                        const u4v hh = __builtin_nontemporal_load(ha + i);
+                        const u4v ll = __builtin_nontemporal_load(lb + i);
+                        s3 += terms(ll, hh, wv[i]);
+                    }
+                    sum += reduce(s3);
+                    n3++;
+                }
+            }
+        }
+        if (lane == 0) {
+            const uint8_t r = bad ? 0xFF : (uint8_t)(sum >= a.quorum);
+            a.out[q] = a.out_tag && !bad ? (uint8_t)(a.out_tag[q] << 1 | r) : r;
+            if (bad) atomicOr(&a.status[1], 1u);
+        }
+        A = An; Bq = Bn; bad = badn; hv = hn; lv = ln;
+        ne++;
+    }
+    if (a.early_full && lane == 0 && ne) {
+        if (n1) atomicAdd(a.early_full, (unsigned long long)n1);
+        if (n2) atomicAdd(a.early_full + 1, (unsigned long long)n2);
+        atomicAdd(a.early_full + 2, (unsigned long long)ne);
+        if (n3) atomicAdd(a.early_full + 3, (unsigned long long)n3);
     }
 }
 
@@ -1681,6 +1705,14 @@ static hipError_t launch_fc_t(const FcArgs &a, bool forks, hipStream_t s) {
     if (blocks > 256 * 32) blocks = 256 * 32;
     if (blocks == 0) return hipSuccess;
     const dim3 g((uint32_t)blocks), b(256);
+    if constexpr (LPQ == 64) {
+        if (a.early && !forks) {   // rows of > 128 uint4: the early exit (32 lanes per query)
+            const uint64_t eb = std::min<uint64_t>((a.n + 7) / 8, 256 * 32);
+            if (a.la_recv) hipLaunchKernelGGL((k_fc_early<true>), dim3((uint32_t)eb), b, 0, s, a);
+            else hipLaunchKernelGGL((k_fc_early<false>), dim3((uint32_t)eb), b, 0, s, a);
+            return hipGetLastError();
+        }
+    }
     if (a.la_recv) {   // a row-segment rank: LowestAfter rows of other ranks in the receive area
         if (forks && a.fk_hi4 && a.n_cheat <= 32) hipLaunchKernelGGL((k_fc_fk<LPQ, uint32_t, true>), g, b, 0, s, a);
         else if (forks && a.fk_hi4) hipLaunchKernelGGL((k_fc_fk<LPQ, uint64_t, true>), g, b, 0, s, a);

@@ -51,6 +51,7 @@ SIGNATURES = [
     ("lx_get_event_branch_id", ctypes.c_int, [vp, ctypes.c_uint32, u32p]),
     ("lx_get_server_stats", ctypes.c_int, [vp, u64p]),
     ("lx_live_handles", ctypes.c_int, []),
+    ("lx_fc_early_rounds", ctypes.c_int, [vp, u64p]),
     ("lx_device_bytes", ctypes.c_int, [vp, u64p]),
     ("lx_get_rows_dev", ctypes.c_int, [vp, ctypes.c_uint32, ctypes.c_uint32, vp, vp, ctypes.c_uint64, vp]),
     ("lx_row_bytes_max", ctypes.c_int, [vp, u64p]),
@@ -375,6 +376,13 @@ class Index:
 
     def forkless_cause_batch_dev(self, n, a_ptr, b_ptr, out_ptr, stream=None):
         self._chk(self.L.lx_forkless_cause_batch_dev(self.h, n, a_ptr, b_ptr, out_ptr, stream))
+
+    def fc_early_rounds(self):
+        """(queries on the early path, of them reading columns 128-255, 256-511,
+        the rest) since the last call (lx_fc_early_rounds)."""
+        out = np.zeros(4, dtype=np.uint64)
+        self._chk(self.L.lx_fc_early_rounds(self.h, _p(out, u64p)))
+        return tuple(int(x) for x in out)
 
     def fc_early_counters(self):
         """(queries the kernel decided on its early path, of them past the first

@@ -22,7 +22,8 @@ def main():
     out = {"source": "rocprofv3 --kernel-trace of `python3 bench.py --no-cpu` (scripts/prof_round.sh)", "kernels": {}}
     # the C3 walk: one 4-column k_index, or (side-by-side segments)
     # one 8-column k_index_segs launch
-    for key, match, min_ms in (("k_index_c3", "k_index", 20.0), ("k_fc_c3", "k_fc<64, false>", 5.0)):
+    # (the C3 ForklessCause steps run the early-exit kernel since round 5)
+    for key, match, min_ms in (("k_index_c3", "k_index", 20.0), ("k_fc_c3", "k_fc_early<false>", 2.0)):
         d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in rows
              if match in r["Kernel_Name"]]
         big = sorted(x for x in d if x >= min_ms)

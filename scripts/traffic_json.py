@@ -31,7 +31,7 @@ def per_kernel(root, counters):
                 # keyed by the kernel's own name (k_fc, k_index, k_index_segs):
                 # bench.py takes the figure of the kernel it timed, never a
                 # neighbour's
-                key = next((k for k in ("k_index_segs", "k_index", "k_fc") if name.startswith("void lx::" + k + "<")
+                key = next((k for k in ("k_index_segs", "k_index", "k_fc_early", "k_fc") if name.startswith("void lx::" + k + "<")
                             or name.startswith(k + "<") or ("lx::" + k + "<") in name), None)
                 if key is None:
                     continue
