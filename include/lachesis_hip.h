@@ -216,8 +216,10 @@ typedef struct lx_fc_stats {
 int lx_fc_cache_stats(const lx_index *h, lx_fc_stats *out);
 
 /* Batched ForklessCause's early exit (option fc_early) since the last call.
- * The path runs on fork-free epochs whose rows exceed 512 columns and whose
- * 512 heaviest validators can reach the quorum alone; it reads both rows in
+ * The path runs on launches of >= 2^14 queries over fork-free epochs whose
+ * rows exceed 512 columns and whose 512 heaviest validators can reach the
+ * quorum alone (smaller launches keep one round of whole rows: shorter
+ * latency); it reads both rows in
  * rounds of columns [0, 128), [128, 256), [256, 512) and the rest, each only
  * when the count so far leaves the quorum open.  lx_fc_early_rounds: out[0]
  * queries decided on the path (device count), out[1..3] of them the ones that

@@ -889,7 +889,11 @@ int lx_fc_args(lx_index *h, uint64_t n, const uint32_t *a, const uint32_t *b, ui
     // launch_fc's 64-lane width, the gate matches what runs): rounds of the
     // first 128, 256, 512 columns and the rest, when the heaviest 512 columns
     // can reach the quorum alone (else no round before the last can decide)
-    if (!partial && !h->sharded() && h->B == h->V && h->fc_early && f.vhi4 - f.vlo4 > 128) {
+    // Small launches (the FC cache's row fills, calcFrameIdx-sized batches) keep
+    // whole rows: all of a row's loads in one round is the shortest latency,
+    // and the caller waits for the launch (drop-in C5: 4 rounds cost ~1.4 us
+    // per miss)
+    if (!partial && !h->sharded() && h->B == h->V && h->fc_early && f.vhi4 - f.vlo4 > 128 && n >= kFcEarlyMinQueries) {
         uint64_t w128 = 0, w256 = 0, w512 = 0, wt = 0;
         for (uint32_t c = f.vlo4 * 4; c < h->V && c < f.vhi4 * 4; c++) {
             const uint32_t k = c - f.vlo4 * 4;

@@ -195,6 +195,7 @@ struct FcArgs {
     uint32_t fk_hi4;
 };
 constexpr uint32_t kFcFkMaxCheaters = 64;   // one 64-bit mask per query
+constexpr uint64_t kFcEarlyMinQueries = 1u << 14;   // launches this large take the early exit (k_fc_early)
 
 struct MarkArgs {
     uint32_t *hb;

@@ -57,8 +57,9 @@ def test_early_exit_equals_whole_rows_and_oracle(lx, V, epv, zipf):
 
 def test_early_exit_unknown_events(lx):
     """Queries on events past the index answer 0xFF through the early path too
-    (V = 600: rows of 150 uint4, 64 lanes per query; the device's counter shows
-    all three queries went through the early path)."""
+    (V = 600: rows of 150 uint4; a launch of 2^14 queries, the smallest that
+    takes the early path; the device's counter shows every query went through
+    it).  A small launch keeps whole rows."""
     V = 600
     d = lx.tools.gen_dag(V, 20, 10, seed=4)
     w = [(1 << 20) // (i + 1) for i in range(V)]
@@ -68,17 +69,25 @@ def test_early_exit_unknown_events(lx):
     ix.sync()
     import torch
     dev = torch.device("cuda", 0)
-    qa = np.array([0, len(d) + 5, 7], dtype=np.uint32)
-    qb = np.array([len(d) + 9, 1, 3], dtype=np.uint32)
+    n = 1 << 14
+    qa, qb = lx.tools.fc_queries(d.lamport, n, window=64, seed=5)
+    qa[:3] = [0, len(d) + 5, 7]
+    qb[:3] = [len(d) + 9, 1, 3]
     ta = torch.from_numpy(qa.view(np.int32)).to(dev)
     tb = torch.from_numpy(qb.view(np.int32)).to(dev)
-    out = torch.zeros(3, dtype=torch.uint8, device=dev)
+    out = torch.zeros(n, dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()
     ix.fc_early_counters()
-    ix.forkless_cause_batch_dev(3, ta.data_ptr(), tb.data_ptr(), out.data_ptr())
+    ix.forkless_cause_batch_dev(n, ta.data_ptr(), tb.data_ptr(), out.data_ptr())
     with pytest.raises(Exception):
         ix.sync()                                        # the unknown-event flag is reported
     got = out.cpu().numpy()
     assert got[0] == 0xFF and got[1] == 0xFF and got[2] in (0, 1)
-    assert ix.fc_early_counters()[0] == 3
+    o = corc.OracleIndex(w)
+    assert o.add_batch(d.creator, d.seq, d.poff, d.par) == -1
+    np.testing.assert_array_equal(got[3:], o.forkless_cause_batch(qa[3:], qb[3:]))
+    assert ix.fc_early_counters()[0] == n
+    # a launch below 2^14 queries reads whole rows
+    ix.forkless_cause_batch(qa[3:1000], qb[3:1000])
+    assert ix.fc_early_counters()[0] == 0
     ix.close()
