@@ -606,16 +606,20 @@ def main():
     def sum_over_ranks(x):
         return reduce_over_ranks(x, dist.ReduceOp.SUM) if world > 1 else x
 
+    early_lanes = 32   # k_fc_early's lanes per query (lx_capi.cpp: option fc_early_lanes)
+
     def fc_bytes_read(nq, B, early):
         """Bytes k_fc reads for nq queries over rows of B branches: whole rows
         (8 B per branch: HB(a) 4 B + LA(b) 4 B) without the early exit; with it
         (k_fc_early, device counters: queries on the early path, of them the
-        ones that read columns 128-255, 256-511, the rest) 2 x 512 B per query
-        (the 128 heaviest columns of both rows), 2 x 512 B more past round 1,
-        2 x 1 KB past round 2, the rest of both rows past round 3."""
+        ones that read round 2, round 3, the rest; rounds of 4 x L columns, 4 x L
+        more, 8 x L more, the rest, L = lanes per query) 2 x 4 x L x 4 B per
+        query, as much again past round 1, twice that past round 2, the rest
+        of both rows past round 3."""
         qe, q2, q3, qw = early
         row16 = ((B + 3) // 4) * 16
-        return (qe * 1024.0 + q2 * 1024.0 + q3 * 2048.0 + qw * 2.0 * max(0, row16 - 4096) +
+        r1 = 32.0 * early_lanes                       # bytes of round 1, both rows
+        return (qe * r1 + q2 * r1 + q3 * 2 * r1 + qw * 2.0 * max(0, row16 - 64 * early_lanes) +
                 (nq - qe) * 8.0 * B)
 
     def leg(kind):

@@ -894,13 +894,14 @@ int lx_fc_args(lx_index *h, uint64_t n, const uint32_t *a, const uint32_t *b, ui
     // and the caller waits for the launch (drop-in C5: 4 rounds cost ~1.4 us
     // per miss)
     if (!partial && !h->sharded() && h->B == h->V && h->fc_early && f.vhi4 - f.vlo4 > 128 && n >= kFcEarlyMinQueries) {
+        const uint32_t L = h->fc_early_lanes;   // rounds of 4L, 8L, 16L columns
         uint64_t w128 = 0, w256 = 0, w512 = 0, wt = 0;
         for (uint32_t c = f.vlo4 * 4; c < h->V && c < f.vhi4 * 4; c++) {
             const uint32_t k = c - f.vlo4 * 4;
             wt += h->weights[c];
-            if (k < 128) w128 += h->weights[c];
-            if (k < 256) w256 += h->weights[c];
-            if (k < 512) w512 += h->weights[c];
+            if (k < 4 * L) w128 += h->weights[c];
+            if (k < 8 * L) w256 += h->weights[c];
+            if (k < 16 * L) w512 += h->weights[c];
         }
         if (w512 >= h->quorum && wt - w128 <= 0xFFFFFFFFull) {
             if (!h->d_fc_full) {
@@ -920,6 +921,7 @@ int lx_fc_args(lx_index *h, uint64_t n, const uint32_t *a, const uint32_t *b, ui
             f.early_rest = (uint32_t)(wt - w128);
             f.early_rest2 = (uint32_t)(wt - w256);
             f.early_rest3 = (uint32_t)(wt - w512);
+            f.early_lanes = L;
             f.early_full = h->d_fc_full;
         }
     }
@@ -1800,6 +1802,9 @@ int lx_set_option(lx_index *h, const char *name, int64_t value) {
         h->fc_fk = value != 0;
     } else if (k == "fc_early") {
         h->fc_early = value != 0;
+    } else if (k == "fc_early_lanes") {
+        if (value != 16 && value != 32) return h->fail(LX_ERR_ARG, "fc_early_lanes must be 16 or 32");
+        h->fc_early_lanes = (uint32_t)value;
     } else if (k == "cpw") {
         if (value != 0 && value != 1 && value != 2 && value != 4 && value != 8 && value != 12)
             return h->fail(LX_ERR_ARG, "cpw must be 0, 1, 2, 4, 8 or 12 (8, 12: fork-free epochs with seqs <= 0xFFFF)");

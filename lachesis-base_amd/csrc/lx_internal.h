@@ -163,13 +163,14 @@ struct FcArgs {
     uint32_t vlo4, vhi4;         // column range in uint4 units
     uint32_t quorum;
     // early exit (k_fc_early: fork-free rows of > 512 columns; 0 = off): the
-    // weight of the columns past the first 128, 256 and 512 of the range.  The
+    // weight of the columns past the first 4L, 8L and 16L of the range (L = early_lanes).  The
     // first columns are the heaviest validators (pos.Validators idx order), so
     // their count alone often decides the quorum either way
     uint32_t early_rest;
     uint32_t early_rest2;
     uint32_t early_rest3;
     uint32_t early;
+    uint32_t early_lanes;        // lanes per query of k_fc_early: 32 (rounds 128 / 256 / 512 columns) or 16 (64 / 128 / 256)
     unsigned long long *early_full;   // [0] += queries past round 1, [1] += past round 2, [2] += queries
                                       // on the early path, [3] += past round 3 (whole rows)
     const uint32_t *ev_branch;

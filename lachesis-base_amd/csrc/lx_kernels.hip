@@ -1474,21 +1474,21 @@ __global__ __launch_bounds__(256) void k_fc(FcArgs a) {
 // (vecfc/forkless_cause.go:63-82), and branch j < V is validator j in
 // pos.Validators order -- heaviest first -- so the count of the first columns
 // often decides the answer: >= quorum is true whatever the rest holds, and
-// count + the weight of every remaining column < quorum is false.  32 lanes
-// per query (two queries per wave), in rounds of columns [0, 128) (1 KB of
-// HB(a) and LA(b)), [128, 256), [256, 512) and the rest, each read only when
-// the count so far leaves the quorum open; the next query's first round is in
-// flight while the current one is decided.  Same answers as the whole-row
-// kernel by construction.  Counters: [0] queries past round 1, [1] past round
-// 2, [2] every query of the early path, [3] past round 3.
-template <bool RS>
+// count + the weight of every remaining column < quorum is false.  L lanes
+// per query (L = 32: two queries per wave), in rounds of columns [0, 4L)
+// (L = 32: 128 columns, 1 KB of HB(a) and LA(b)), [4L, 8L), [8L, 16L) and the
+// rest, each read only when the count so far leaves the quorum open; the next
+// query's first round is in flight while the current one is decided.  Same
+// answers as the whole-row kernel by construction.  Counters: [0] queries
+// past round 1, [1] past round 2, [2] every query of the early path, [3] past
+// round 3.
+template <bool RS, int L>
 __global__ __launch_bounds__(256) void k_fc_early(FcArgs a) {
-    constexpr int L = 32;
     const int lane = threadIdx.x % L;
     const uint64_t qpb = 256 / L;
-    const uint32_t nv = a.vhi4 - a.vlo4;   // > 128 (launch_fc)
+    const uint32_t nv = a.vhi4 - a.vlo4;   // > 128 (lx_fc_args)
     const uint4 *wv = reinterpret_cast<const uint4 *>(a.wpad) + a.vlo4;
-    // this lane's weights of the first 512 columns: uint4 lane, 32 + lane, 64 + lane, 96 + lane
+    // this lane's weights of the first 16 L columns: uint4 lane, L + lane, 2 L + lane, 3 L + lane
     uint4 wr[4];
 #pragma unroll
     for (int t = 0; t < 4; t++) {
@@ -1526,7 +1526,7 @@ __global__ __launch_bounds__(256) void k_fc_early(FcArgs a) {
         if (q + step < a.n) first(q + step, An, Bn, badn, hn, ln);
         uint32_t sum = reduce(terms(lv, hv, wr[0]));
         if (sum < a.quorum && sum + a.early_rest >= a.quorum) {
-            // round 2: columns 128-255
+            // round 2: columns 4L-8L
             const u4v *ha = reinterpret_cast<const u4v *>(a.hb + (uint64_t)A * a.stride) + a.vlo4;
             const u4v *lb = reinterpret_cast<const u4v *>(fc_la<RS>(a, Bq)) + a.vlo4;
             uint32_t s1 = 0;
@@ -1534,7 +1534,7 @@ __global__ __launch_bounds__(256) void k_fc_early(FcArgs a) {
             sum += reduce(s1);
             n1++;
             if (sum < a.quorum && sum + a.early_rest2 >= a.quorum) {
-                // round 3: columns 256-511, two uint4 per lane in flight
+                // round 3: columns 8L-16L, two uint4 per lane in flight
                 uint32_t s2 = 0;
                 const uint32_t i2 = lane + 2 * L, i3 = lane + 3 * L;
                 u4v h2 = {0, 0, 0, 0}, l2 = {0, 0, 0, 0}, h3 = {0, 0, 0, 0}, l3 = {0, 0, 0, 0};
@@ -1705,14 +1705,6 @@ static hipError_t launch_fc_t(const FcArgs &a, bool forks, hipStream_t s) {
     if (blocks > 256 * 32) blocks = 256 * 32;
     if (blocks == 0) return hipSuccess;
     const dim3 g((uint32_t)blocks), b(256);
-    if constexpr (LPQ == 64) {
-        if (a.early && !forks) {   // rows of > 128 uint4: the early exit (32 lanes per query)
-            const uint64_t eb = std::min<uint64_t>((a.n + 7) / 8, 256 * 32);
-            if (a.la_recv) hipLaunchKernelGGL((k_fc_early<true>), dim3((uint32_t)eb), b, 0, s, a);
-            else hipLaunchKernelGGL((k_fc_early<false>), dim3((uint32_t)eb), b, 0, s, a);
-            return hipGetLastError();
-        }
-    }
     if (a.la_recv) {   // a row-segment rank: LowestAfter rows of other ranks in the receive area
         if (forks && a.fk_hi4 && a.n_cheat <= 32) hipLaunchKernelGGL((k_fc_fk<LPQ, uint32_t, true>), g, b, 0, s, a);
         else if (forks && a.fk_hi4) hipLaunchKernelGGL((k_fc_fk<LPQ, uint64_t, true>), g, b, 0, s, a);
@@ -1730,8 +1722,18 @@ static hipError_t launch_fc_t(const FcArgs &a, bool forks, hipStream_t s) {
 // lanes per query: ~4 uint4 per lane, so every lane has ~8 16-B loads in flight
 // (HB and LA) whatever the row length -- short rows (few validators, or a
 // column shard) would otherwise leave one load pair per lane and stay latency-bound
+template <int L>
+static hipError_t launch_fc_early_t(const FcArgs &a, hipStream_t s) {
+    const uint64_t eb = std::min<uint64_t>((a.n + 256 / L - 1) / (256 / L), 256 * 32);
+    if (!eb) return hipSuccess;
+    if (a.la_recv) hipLaunchKernelGGL((k_fc_early<true, L>), dim3((uint32_t)eb), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((k_fc_early<false, L>), dim3((uint32_t)eb), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
 hipError_t launch_fc(const FcArgs &a, uint32_t cols, bool forks, hipStream_t s) {
     if (forks && !a.fk_hi4 && !a.n_cheat) forks = false;   // no cheater among this handle's creators
+    if (a.early && !forks) return a.early_lanes == 16 ? launch_fc_early_t<16>(a, s) : launch_fc_early_t<32>(a, s);
     const uint32_t nv = forks && a.fk_hi4 ? a.fk_hi4 : a.vhi4 - a.vlo4;
     // (rows of <= 8 branches: 2 lanes, twice the queries per wave -- C1's
     // 20-B rows 0.078 -> 0.072 ms per 2^22 queries, profiles/r04/fc_small_rows_r04y.jsonl)

@@ -28,8 +28,11 @@ qa, qb = lx.tools.fc_queries(d.lamport, 1 << 24, window=64, seed=7)
 ta, tb = to_dev(qa), to_dev(qb)
 res = {"V": V, "events": N, "zipf": zipf, "queries": len(qa)}
 outs = {}
-for early in (1, 0, 1, 0):
-    ix.set_option("fc_early", early)
+# variants: 0 = whole rows, 32 / 16 = the early exit with that many lanes per query
+for early in (32, 0, 16, 32, 0, 16):
+    ix.set_option("fc_early", 1 if early else 0)
+    if early:
+        ix.set_option("fc_early_lanes", early)
     out = torch.empty(len(qa), dtype=torch.uint8, device=dev)
     ts = []
     for rep in range(6):
@@ -44,6 +47,12 @@ for early in (1, 0, 1, 0):
         ts.append(ms)
     outs[early] = out.cpu().numpy()
     res.setdefault("ms_early%d" % early, []).append(float(np.median(ts[1:])))
-res["identical"] = bool(np.array_equal(outs[0], outs[1]))
-res["true_frac"] = float(outs[1].mean())
+res["identical"] = bool(np.array_equal(outs[0], outs[32]) and np.array_equal(outs[0], outs[16]))
+res["true_frac"] = float(outs[0].mean())
+for L in (32, 16):
+    ix.set_option("fc_early", 1)
+    ix.set_option("fc_early_lanes", L)
+    ix.fc_early_rounds()
+    ix.forkless_cause_batch_dev(len(qa), ta.data_ptr(), tb.data_ptr(), out.data_ptr())
+    res["rounds_L%d" % L] = ix.fc_early_rounds()
 print(json.dumps(res))
