@@ -15,12 +15,17 @@ before timing.
 
 value = events indexed/sec (whole job, all ranks); fc_queries_per_sec is
 reported beside it.  Multi-GPU: one process per GPU.
-  --mode shard (default for N > 1, BASELINE configs[2] "column-sharded across
-      8xMI355X"): the ranks split ONE epoch by creator columns
-      (lachesis_hip/shard.py): each indexes its columns,
-      the index step ends with the RCCL all-to-all of LowestAfter blocks, and
-      FC sums per-rank partial stakes with an RCCL all-reduce (strong scaling:
-      value = the epoch's events / time).
+  --mode rowseg (default for N > 1): the epoch's Add order split into N row
+      segments, one per rank: each rank walks its segment
+      and holds its own rows, the row / LowestAfter exchange is inside the
+      index step; FC routes every rank's 2^24 queries to owner(a) (6c).  The
+      same run then measures BASELINE configs[2] as it names it -- "column-
+      sharded across 8xMI355X" -- in the line's `colshard` block (skip with
+      --no-colshard): each rank indexes its creator columns, the index step
+      ends with the all-to-all of LowestAfter blocks, FC sums per-rank partial
+      stakes with an all-reduce (strong scaling: value = the epoch's events /
+      time, both modes).
+  --mode shard: column shards as the line's primary measurement.
   --mode replica: each rank indexes its own copy of the workload (independent
       epochs; no data-path collective; weak scaling).
 LX_DIST_BACKEND=gloo (rehearsal only) lets several ranks share one GPU.
