@@ -905,6 +905,15 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
         uint32_t r[CPW];
 #pragma unroll
         for (int k = 0; k < CPW; k++) r[k] = 0;
+        // PK: r packed two columns per dword, refreshed wherever r changes
+        // (block fetch, extra parents, the L2 path) instead of every pass
+        constexpr int NH = CPW / 2 > 0 ? CPW / 2 : 1;
+        uint32_t rpk[NH];
+        auto repack = [&]() {
+#pragma unroll
+            for (int h = 0; h < NH; h++) rpk[h] = r[(2 * h) % CPW] | (r[(2 * h + 1) % CPW] << 16);
+        };
+        repack();
         // per-event publish constants, set at the block fetch: LDS targets of
         // this lane's slot unit and recent-event entry (dummy when not its
         // role), the drain watermark that frees the event's slot and the value
@@ -1001,6 +1010,7 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
                 }
                 done = !live;
                 loaded = true;
+                repack();
 #ifdef LX_WALKER_PROF
                 {
                     const uint32_t pd = __hip_atomic_load(&sh.p_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1028,8 +1038,13 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
             uint32_t tx = 0;
 #pragma unroll
             for (int k = 0; k < 3; k++) tx |= (tg[k][0] ^ px[k]) | ((PK && CPW == 4) || CPW < 4 ? 0u : (tg[k][1] ^ px[k]));
+            // the quad's readiness: its four lanes' mismatches OR-ed by DPP
+            // (two VALU steps; the ballot / scalar-shift / per-lane bit test it
+            // replaced cost 7 VALU and 3 SALU: C3 walk -3.4 %)
+            tx |= (uint32_t)__builtin_amdgcn_mov_dpp((int)tx, kQuadSwap1, 0xF, 0xF, true);
+            tx |= (uint32_t)__builtin_amdgcn_mov_dpp((int)tx, kQuadSwap2, 0xF, 0xF, true);
+            const bool rdy = tx == 0u;   // all twelve slot tags of the quad as expected
             uint32_t m[CPW];
-            constexpr int NH = CPW / 2 > 0 ? CPW / 2 : 1;
             uint32_t mp[NH];   // PK: the quad's maxima, two columns per dword
 #pragma unroll
             for (int h = 0; h < NH; h++) mp[h] = 0u;
@@ -1038,7 +1053,7 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
                 // reduction on packed words
 #pragma unroll
                 for (int h = 0; h < NH; h++) {
-                    const uint32_t rp = r[(2 * h) % CPW] | (r[(2 * h + 1) % CPW] << 16);
+                    const uint32_t rp = rpk[h];
                     mp[h] = quad_pk_max(pk_max(pk_max(rp, pv[0][h % CPW]), pk_max(pv[1][h % CPW], pv[2][h % CPW])));
                 }
             } else {
@@ -1049,13 +1064,6 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
                     m[c] = quad_max(max(t, pv[2][c]));
                 }
             }
-            // the quad's readiness: AND of its four lanes on the scalar unit
-            // the quad's readiness: its four lanes' mismatches OR-ed by DPP
-            // (two VALU steps; the ballot / scalar-shift / per-lane bit test it
-            // replaced cost 7 VALU and 3 SALU: C3 walk -3.4 %)
-            tx |= (uint32_t)__builtin_amdgcn_mov_dpp((int)tx, kQuadSwap1, 0xF, 0xF, true);
-            tx |= (uint32_t)__builtin_amdgcn_mov_dpp((int)tx, kQuadSwap2, 0xF, 0xF, true);
-            const bool rdy = tx == 0u;   // all twelve slot tags of the quad as expected
             if (rdy && !done && xi < np) {
                 // parents beyond the inline twelve (rare): one per pass, the same on every lane of the quad
                 const uint32_t pg = ld_l2_now(a.par_in + a.poff_in[lp] + xi);
@@ -1088,9 +1096,9 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
                 }
                 // the same parent on every lane of the quad: m stays the quad's value
                 if constexpr (PK) {
+                    repack();
 #pragma unroll
-                    for (int h = 0; h < NH; h++)
-                        mp[h] = pk_max(mp[h], r[(2 * h) % CPW] | (r[(2 * h + 1) % CPW] << 16));
+                    for (int h = 0; h < NH; h++) mp[h] = pk_max(mp[h], rpk[h]);
                 } else {
 #pragma unroll
                     for (int c = 0; c < CPW; c++) m[c] = max(m[c], r[c]);
@@ -1131,6 +1139,12 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
                 LX_WP(c_done += fin ? 1u : 0u;)
                 LX_WP(c_wm += (rdy && !done && !fin) ? 1u : 0u;)
                 done = done || fin;
+                // a published quad reads the null slot from now on: one
+                // address for all its lanes, a broadcast instead of twelve
+                // scattered 16-B reads in the passes its wave still makes
+                // (C3 walk -2 %)
+#pragma unroll
+                for (int k = 0; k < 3; k++) pa[k] = done ? ANULL : pa[k];
             }
             if (++wstuck >= kLeanStuck && !rdy && !done) {
                 // waiting long (the wave's block fetched >= 64 passes ago): a
@@ -1153,6 +1167,7 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
                     px[k] = kNullTag;
                     pa[k] = ANULL;
                 }
+                repack();
             }
             if (__all(done)) {
                 blk += NCW;

@@ -1,0 +1,14 @@
+#!/bin/bash
+# A/B of a walker change: scripts/probes/walk_time.py alternately on the
+# baseline build (make ab: the change compiled out by -DLX_AB_BASE) and the
+# shipped build, R rounds each, one JSON line per run.
+#   OUT=gpurun_out/wab R=3 bash scripts/probes/walk_ab.sh     (WT_V / WT_EPV / WT_OPTS pass through)
+cd "$(dirname "$0")/../.."
+O=${OUT:-gpurun_out/wab}
+mkdir -p $O
+for i in $(seq 1 ${R:-3}); do
+  for lib in lachesis-base_amd/build_ab/liblachesis_hip.so lachesis-base_amd/build/liblachesis_hip.so; do
+    LX_LIB=$lib timeout -k 10 240 python3 scripts/probes/walk_time.py >> $O/walk_ab.jsonl || exit $?
+  done
+done
+cat $O/walk_ab.jsonl
