@@ -572,6 +572,7 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
     __shared__ uint4 dummy[128];                 // per-lane targets of suppressed writes
     __shared__ WalkShared sh;
     __shared__ uint32_t sjs[CPW];                // segment walk: J_k of the slice's columns (drains)
+    __shared__ uint32_t sfirst[CPW];             // 12-column slices: first seq of each column (drains)
 
     if (slice >= a.n_slices) return;
 
@@ -586,6 +587,7 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
     if (threadIdx.x < CPW) {
         const uint32_t ci = slice * CPW + threadIdx.x;
         sjs[threadIdx.x] = a.seg && ci < a.ncols ? a.seg_j[CPW == 12 ? ci : a.col_list[ci]] : 0u;
+        sfirst[threadIdx.x] = CPW == 12 && ci < a.ncols ? a.branch_first[ci] : 1u;
     }
     if (threadIdx.x == 0) { sh.req = 0; sh.p_issued = 0; sh.p_done = 0; }
     __syncthreads();
@@ -600,26 +602,37 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
     const uint32_t RB = RA + (uint32_t)((RN + 1) * 16);   // second units (CPW 4 only)
 
     // col = global branch (semantics), pc = plane column (addressing; differs
-    // from col only in a column-sharded handle, which stores its own columns)
-    uint32_t col[CPW], first[CPW], pc[CPW];
-    bool valid[CPW];
+    // from col only in a column-sharded handle, which stores its own columns).
+    // 12-column slices (whole handles only, launch_index) use the identity
+    // column list: col = pc = c0 + k, computed where used, and the first seqs
+    // live in LDS -- as per-column arrays they held ~60 SGPRs, which spilled
+    // to VGPR lanes and cost a v_readlane at every use
+    constexpr bool ID = CPW == 12;
+    const uint32_t c0 = slice * CPW;
+    const uint32_t nval = a.ncols - c0 < (uint32_t)CPW ? a.ncols - c0 : (uint32_t)CPW;
+    uint32_t col_[ID ? 1 : CPW], first_[ID ? 1 : CPW], pc_[ID ? 1 : CPW];
+    bool valid_[ID ? 1 : CPW];
     bool contig = true;
+    if constexpr (ID) {
+        contig = nval == (uint32_t)CPW && (c0 % 4) == 0;
+    } else {
 #pragma unroll
-    for (int k = 0; k < CPW; k++) {
-        const uint32_t ci = slice * CPW + k;
-        valid[k] = ci < a.ncols;
-        if constexpr (CPW == 12) {
-            // whole handles only (launch_index): the column list is the identity
-            col[k] = valid[k] ? ci : 0;
-            pc[k] = col[k];
-        } else {
-            col[k] = valid[k] ? a.col_list[ci] : 0;
-            pc[k] = valid[k] ? (a.cmap ? a.cmap[col[k]] : col[k]) : 0;
+        for (int k = 0; k < CPW; k++) {
+            const uint32_t ci = c0 + k;
+            valid_[k] = ci < a.ncols;
+            col_[k] = valid_[k] ? a.col_list[ci] : 0;
+            pc_[k] = valid_[k] ? (a.cmap ? a.cmap[col_[k]] : col_[k]) : 0;
+            first_[k] = valid_[k] ? a.branch_first[col_[k]] : 1;
+            contig &= valid_[k] && pc_[k] == pc_[0] + k;
         }
-        first[k] = valid[k] ? a.branch_first[col[k]] : 1;
-        contig &= valid[k] && pc[k] == pc[0] + k;
+        contig &= (pc_[0] % CPW) == 0;
     }
-    contig &= (pc[0] % CPW) == 0;
+    auto col = [&](int k) -> uint32_t { return ID ? c0 + k : col_[k % (ID ? 1 : CPW)]; };
+    auto pc = [&](int k) -> uint32_t { return ID ? c0 + k : pc_[k % (ID ? 1 : CPW)]; };
+    auto valid = [&](int k) -> bool { return ID ? (uint32_t)k < nval : valid_[k % (ID ? 1 : CPW)]; };
+    auto first = [&](int k) -> uint32_t {
+        return ID ? (uint32_t)__builtin_amdgcn_readfirstlane(sfirst[k]) : first_[k % (ID ? 1 : CPW)];
+    };
 
     if (wave == NCW) {
         // ------------------------------------------------------------ loader
@@ -766,7 +779,7 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
                     if (!got && !(a.seg && pl >= n)) {   // (segment walk: a prev before the segment counts below as J_k)
                         const uint32_t *row = a.hb + (uint64_t)prev * stride;
 #pragma unroll
-                        for (int k = 0; k < CPW; k++) h0[k] = valid[k] ? ld_l2_now(row + pc[k]) : 0u;
+                        for (int k = 0; k < CPW; k++) h0[k] = valid(k) ? ld_l2_now(row + pc(k)) : 0u;
                     }
 #pragma unroll
                     for (int k = 0; k < CPW; k++) h0[k] &= mask;
@@ -781,25 +794,25 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
                     // event of some branch is "partial" (lx_segment.hip fixes it up)
                     bool unc = false;
 #pragma unroll
-                    for (int k = 0; k < CPW; k++) unc |= valid[k] && (r[k] & mask) < sj[k];
+                    for (int k = 0; k < CPW; k++) unc |= valid(k) && (r[k] & mask) < sj[k];
                     if (unc && atomicOr(a.seg_flag + ev, 1u) == 0u) a.seg_list[atomicAdd(a.seg_count, 1u)] = bs + ev;
                 }
                 // HB row (raw values incl. fork bits as published)
                 uint32_t *hrow = a.hb + (uint64_t)(bs + ev) * stride;
                 if (contig) {
-                    if (CPW == 1) hrow[pc[0]] = r[0];
-                    else if (CPW == 2) *reinterpret_cast<uint2 *>(hrow + pc[0]) = make_uint2(r[0], r[1 % CPW]);
-                    else if (CPW == 4) *reinterpret_cast<uint4 *>(hrow + pc[0]) = make_uint4(r[0], r[1 % CPW], r[2 % CPW], r[3 % CPW]);
+                    if (CPW == 1) hrow[pc(0)] = r[0];
+                    else if (CPW == 2) *reinterpret_cast<uint2 *>(hrow + pc(0)) = make_uint2(r[0], r[1 % CPW]);
+                    else if (CPW == 4) *reinterpret_cast<uint4 *>(hrow + pc(0)) = make_uint4(r[0], r[1 % CPW], r[2 % CPW], r[3 % CPW]);
                     else {
 #pragma unroll
                         for (int q = 0; q < CPW / 4; q++)
-                            *reinterpret_cast<uint4 *>(hrow + pc[0] + 4 * q) =
+                            *reinterpret_cast<uint4 *>(hrow + pc(0) + 4 * q) =
                                 make_uint4(r[(4 * q) % CPW], r[(4 * q + 1) % CPW], r[(4 * q + 2) % CPW], r[(4 * q + 3) % CPW]);
                     }
                 } else {
 #pragma unroll
                     for (int k = 0; k < CPW; k++)
-                        if (valid[k]) hrow[pc[k]] = r[k];
+                        if (valid(k)) hrow[pc(k)] = r[k];
                 }
                 {
                     // LowestAfter range fill: events (col, s), s in (h0, r], are first
@@ -810,15 +823,15 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
                         // segment walk: the rows after J_k only; L is RAW there for this
                         // event and its prev (lx_segment.hip), the rows up to J_k are
                         // filled by k_seg_la_edge
-                        lo[k] = max(max(h0[k], sj[k]) + 1u, first[k]);
-                        hi[k] = valid[k] ? (r[k] & mask) : 0u;
+                        lo[k] = max(max(h0[k], sj[k]) + 1u, first(k));
+                        hi[k] = valid(k) ? (r[k] & mask) : 0u;
                     }
                     if (a.lap) {
                         // sharded: rows of own branches addressed by (column, seq)
 #pragma unroll
                         for (int k = 0; k < CPW; k++)
                             for (uint32_t s = lo[k]; s <= hi[k]; s++)
-                                a.lap[((uint64_t)pc[k] * a.s_cap + (s - first[k])) * a.lap_stride + br] = seq;
+                                a.lap[((uint64_t)pc(k) * a.s_cap + (s - first(k))) * a.lap_stride + br] = seq;
                     } else {
                         // the first (usually only) seq of every column's range: all
                         // the recent-event lookups in one LDS round trip
@@ -836,7 +849,7 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
                                 uint32_t row = (uint32_t)(cc >> 32);
                                 LX_WP(d_fill++;)
                                 LX_WP(if ((uint32_t)cc != s) d_miss++;)
-                                if ((uint32_t)cc != s) row = ld_l2_now(a.brow + (uint64_t)col[k] * a.s_cap + (s - first[k]));
+                                if ((uint32_t)cc != s) row = ld_l2_now(a.brow + (uint64_t)col(k) * a.s_cap + (s - first(k)));
                                 a.la[(uint64_t)row * stride + br] = seq;
                             }
                         }
@@ -886,15 +899,15 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
         constexpr uint32_t UA = CPW == 1 ? 8u : 16u;   // bytes of unit A
         const uint32_t ANULL = RA + (uint32_t)RN * UA;
         const uint32_t j = lane & 3, quad = lane >> 2;
-        const uint32_t mycol = col[j & (CPW - 1)];
-        const bool myvalid = j < (uint32_t)CPW && valid[j & (CPW - 1)];
+        const uint32_t mycol = col(j & (CPW - 1));
+        const bool myvalid = j < (uint32_t)CPW && valid(j & (CPW - 1));
         // CPW 8: lane j of a quad also owns column j + 4 (recent-event entries)
         uint32_t mycol2 = 0;
         bool myvalid2 = false;
         if constexpr (CPW == 8) {
 #pragma unroll
             for (int k = 4; k < CPW; k++)
-                if ((uint32_t)k == j + 4) { mycol2 = col[k]; myvalid2 = valid[k]; }
+                if ((uint32_t)k == j + 4) { mycol2 = col(k); myvalid2 = valid(k); }
         }
         uint32_t blk = __builtin_amdgcn_readfirstlane(wave);   // wave-uniform: scalar loop control
         bool loaded = false, done = true;
@@ -909,11 +922,16 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
         // (block fetch, extra parents, the L2 path) instead of every pass
         constexpr int NH = CPW / 2 > 0 ? CPW / 2 : 1;
         uint32_t rpk[NH];
-        auto repack = [&]() {
+        // (merged, not overwritten, after the block fetch: rpk also holds the
+        // retired parents' values, and r only grows)
+        auto repack = [&](bool fresh) {
 #pragma unroll
-            for (int h = 0; h < NH; h++) rpk[h] = r[(2 * h) % CPW] | (r[(2 * h + 1) % CPW] << 16);
+            for (int h = 0; h < NH; h++) {
+                const uint32_t p = r[(2 * h) % CPW] | (r[(2 * h + 1) % CPW] << 16);
+                rpk[h] = fresh ? p : pk_max(rpk[h], p);
+            }
         };
-        repack();
+        repack(true);
         // per-event publish constants, set at the block fetch: LDS targets of
         // this lane's slot unit and recent-event entry (dummy when not its
         // role), the drain watermark that frees the event's slot and the value
@@ -959,7 +977,7 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
                     pa[k] = in ? RA + (pl % RN) * UA : ANULL;
                 }
 #pragma unroll
-                for (int k = 0; k < CPW; k++) r[k] = (col[k] == br) ? seq : 0u;
+                for (int k = 0; k < CPW; k++) r[k] = (col(k) == br) ? seq : 0u;
                 if (j < np && w0 - bs >= n) {
                     // parents from earlier batches (sorted oldest first): final rows
 #pragma unroll
@@ -971,12 +989,12 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
                             const uint32_t pb = a.ev_branch[w[k]], ps = a.ev_seq[w[k]];
 #pragma unroll
                             for (int c = 0; c < CPW; c++)
-                                if (valid[c] && col[c] == pb) r[c] = max(r[c], ps);
+                                if (valid(c) && col(c) == pb) r[c] = max(r[c], ps);
                         } else {
                             const uint32_t *row = a.hb + (uint64_t)w[k] * stride;
 #pragma unroll
                             for (int c = 0; c < CPW; c++)
-                                if (valid[c]) r[c] = max(r[c], ld_l2_now(row + pc[c]) & mask);
+                                if (valid(c)) r[c] = max(r[c], ld_l2_now(row + pc(c)) & mask);
                         }
                         px[k] = kNullTag;
                         pa[k] = ANULL;
@@ -994,7 +1012,7 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
                         uint32_t wb = dmy + 1024u;
 #pragma unroll
                         for (int k = 0; k < CPW; k++)
-                            if ((uint32_t)(k & 3) == j && valid[k] && col[k] == br)
+                            if ((uint32_t)(k & 3) == j && valid(k) && col(k) == br)
                                 wb = lds_addr(brc) + ((uint32_t)k * KB + seq % KB) * 8u;
                         wb_pub = wb;
                     } else {
@@ -1010,7 +1028,7 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
                 }
                 done = !live;
                 loaded = true;
-                repack();
+                repack(true);
 #ifdef LX_WALKER_PROF
                 {
                     const uint32_t pd = __hip_atomic_load(&sh.p_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1085,18 +1103,18 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
                     const uint32_t pb = a.ev_branch[pg], ps = a.ev_seq[pg];
 #pragma unroll
                     for (int c = 0; c < CPW; c++)
-                        if (valid[c] && col[c] == pb) r[c] = max(r[c], ps);
+                        if (valid(c) && col(c) == pb) r[c] = max(r[c], ps);
                     ok = true;
                 } else if (old) {
                     const uint32_t *row = a.hb + (uint64_t)pg * stride;
 #pragma unroll
                     for (int c = 0; c < CPW; c++)
-                        if (valid[c]) r[c] = max(r[c], ld_l2_now(row + pc[c]) & mask);
+                        if (valid(c)) r[c] = max(r[c], ld_l2_now(row + pc(c)) & mask);
                     ok = true;
                 }
                 // the same parent on every lane of the quad: m stays the quad's value
                 if constexpr (PK) {
-                    repack();
+                    repack(false);
 #pragma unroll
                     for (int h = 0; h < NH; h++) mp[h] = pk_max(mp[h], rpk[h]);
                 } else {
@@ -1163,11 +1181,11 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
                     const uint32_t *row = a.hb + (uint64_t)(x - 1u + bs) * stride;
 #pragma unroll
                     for (int c = 0; c < CPW; c++)
-                        if (valid[c]) r[c] = max(r[c], ld_l2_now(row + pc[c]) & mask);
+                        if (valid(c)) r[c] = max(r[c], ld_l2_now(row + pc(c)) & mask);
                     px[k] = kNullTag;
                     pa[k] = ANULL;
                 }
-                repack();
+                repack(false);
             }
             if (__all(done)) {
                 blk += NCW;
