@@ -434,10 +434,11 @@ __device__ __forceinline__ uint32_t rec_off(uint32_t slot, uint32_t q) {
 constexpr uint32_t kNullTag = 0xFFFFFFFFu;   // null slot: never an event tag (tags are lp + 1 <= n)
 // any of a lane's three parents (expected tag = local index + 1, or kNullTag)
 // at least `reach` events before event lp
-__device__ __forceinline__ bool far_parent(const uint32_t px[3], uint32_t lp, uint32_t reach) {
+template <int NPL>
+__device__ __forceinline__ bool far_parent(const uint32_t px[NPL], uint32_t lp, uint32_t reach) {
     bool f = false;
 #pragma unroll
-    for (int k = 0; k < 3; k++) f |= px[k] != kNullTag && lp - (px[k] - 1u) >= reach;
+    for (int k = 0; k < NPL; k++) f |= px[k] != kNullTag && lp - (px[k] - 1u) >= reach;
     return f;
 }
 // DPP quad permutations (lanes 4q..4q+3): swap neighbours, swap pairs
@@ -826,13 +827,15 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
                         lo[k] = max(max(h0[k], sj[k]) + 1u, first(k));
                         hi[k] = valid(k) ? (r[k] & mask) : 0u;
                     }
-                    if (a.lap) {
+                    if (!ID && a.lap) {
                         // sharded: rows of own branches addressed by (column, seq)
 #pragma unroll
                         for (int k = 0; k < CPW; k++)
                             for (uint32_t s = lo[k]; s <= hi[k]; s++)
                                 a.lap[((uint64_t)pc(k) * a.s_cap + (s - first(k))) * a.lap_stride + br] = seq;
                     } else {
+                        char *const la_br = reinterpret_cast<char *>(a.la + br);
+                        const uint32_t pitch = (uint32_t)stride * 4u;
                         // the first (usually only) seq of every column's range: all
                         // the recent-event lookups in one LDS round trip
                         uint64_t c0[CPW];
@@ -850,7 +853,10 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
                                 LX_WP(d_fill++;)
                                 LX_WP(if ((uint32_t)cc != s) d_miss++;)
                                 if ((uint32_t)cc != s) row = ld_l2_now(a.brow + (uint64_t)col(k) * a.s_cap + (s - first(k)));
-                                a.la[(uint64_t)row * stride + br] = seq;
+                                // one 32 x 32 + 64 multiply-add per store: column br of
+                                // the LA plane as the base, the row pitch in bytes
+                                // (< 4 GB, launch_index) as a 32-bit factor
+                                *reinterpret_cast<uint32_t *>(la_br + (uint64_t)row * pitch) = seq;
                             }
                         }
                     }
@@ -913,22 +919,44 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
         bool loaded = false, done = true;
         uint32_t br = 0, seq = 0, np = 0, xi = 0;
         uint32_t wstuck = 0;   // passes since the block fetch (wave-uniform)
-        uint32_t px[3] = {kNullTag, kNullTag, kNullTag};
-        uint32_t pa[3] = {ANULL, ANULL, ANULL};
+        // SPLIT (packed 8- / 12-column slots, two 16-B units per event): lane j
+        // of a quad reads unit j & 1 of the parents (j >> 1) + 2i, i < 6, so a
+        // lane folds the three data words of one unit and the quad reduces over
+        // one DPP step (lanes j, j ^ 2) instead of two, with no unit selects at
+        // the publish: ~45 VALU per pass instead of ~70, C3 walk 47.1 -> 43.4 ms
+        // (same six 16-B LDS reads per lane); otherwise lane j reads both units
+        // of parents j + 4i, i < 3
+        constexpr bool SPLIT = PK && CPW >= 8;
+        constexpr int NPL = SPLIT ? 6 : 3;   // parent slots per lane
+        const uint32_t uoff = (SPLIT && (j & 1)) ? (uint32_t)(RN + 1) * 16u : 0u;   // unit B array
+        const uint32_t ANUL = ANULL + uoff;  // this lane's null unit
+        auto pidx = [&](int i) -> uint32_t { return SPLIT ? (j >> 1) + 2u * i : j + 4u * i; };
+        uint32_t px[NPL], pa[NPL];
+#pragma unroll
+        for (int i = 0; i < NPL; i++) { px[i] = kNullTag; pa[i] = ANUL; }
         uint32_t r[CPW];
 #pragma unroll
         for (int k = 0; k < CPW; k++) r[k] = 0;
         // PK: r packed two columns per dword, refreshed wherever r changes
-        // (block fetch, extra parents, the L2 path) instead of every pass
+        // (block fetch, extra parents, the L2 path) instead of every pass;
+        // SPLIT keeps only the lane's unit (rpk[0..2])
         constexpr int NH = CPW / 2 > 0 ? CPW / 2 : 1;
         uint32_t rpk[NH];
-        // (merged, not overwritten, after the block fetch: rpk also holds the
-        // retired parents' values, and r only grows)
         auto repack = [&](bool fresh) {
+            if constexpr (SPLIT) {
 #pragma unroll
-            for (int h = 0; h < NH; h++) {
-                const uint32_t p = r[(2 * h) % CPW] | (r[(2 * h + 1) % CPW] << 16);
-                rpk[h] = fresh ? p : pk_max(rpk[h], p);
+                for (int d = 0; d < 3; d++) {
+                    const uint32_t pA = r[(2 * d) % CPW] | (r[(2 * d + 1) % CPW] << 16);
+                    const uint32_t pB = 6 + 2 * d < CPW ? r[(6 + 2 * d) % CPW] | (r[(7 + 2 * d) % CPW] << 16) : 0u;
+                    const uint32_t q = (j & 1) ? pB : pA;
+                    rpk[d] = fresh ? q : pk_max(rpk[d], q);
+                }
+            } else {
+#pragma unroll
+                for (int h = 0; h < NH; h++) {
+                    const uint32_t q = r[(2 * h) % CPW] | (r[(2 * h + 1) % CPW] << 16);
+                    rpk[h] = fresh ? q : pk_max(rpk[h], q);
+                }
             }
         };
         repack(true);
@@ -951,38 +979,56 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
             if (!loaded) {
                 const uint32_t slot = lp % RR;
                 const uint32_t ra = lds_addr(rrec) + rec_off(slot, 0) * 16u;
-                uint32_t tg, w0, w1, w2;
+                uint32_t tg, w[NPL];
                 u4v q0;
-                asm volatile(
-                    "ds_read_b32 %0, %5\n\t"
-                    "ds_read_b128 %1, %6\n\t"
-                    "ds_read_b32 %2, %7 offset:1024\n\t"
-                    "ds_read_b32 %3, %7 offset:2048\n\t"
-                    "ds_read_b32 %4, %7 offset:3072\n\t"
-                    "s_waitcnt lgkmcnt(0)"
-                    : "=&v"(tg), "=&v"(q0), "=&v"(w0), "=&v"(w1), "=&v"(w2)
-                    : "v"(lds_addr(&rtag[slot / 64])), "v"(ra), "v"(ra + j * 4u)
-                    : "memory");
+                if constexpr (SPLIT) {
+                    // parents (j >> 1) + 2i: words j >> 1 and (j >> 1) + 2 of
+                    // parent fields 1-3 (1 KB apart)
+                    asm volatile(
+                        "ds_read_b32 %0, %8\n\t"
+                        "ds_read_b128 %1, %9\n\t"
+                        "ds_read_b32 %2, %10 offset:1024\n\t"
+                        "ds_read_b32 %3, %10 offset:1032\n\t"
+                        "ds_read_b32 %4, %10 offset:2048\n\t"
+                        "ds_read_b32 %5, %10 offset:2056\n\t"
+                        "ds_read_b32 %6, %10 offset:3072\n\t"
+                        "ds_read_b32 %7, %10 offset:3080\n\t"
+                        "s_waitcnt lgkmcnt(0)"
+                        : "=&v"(tg), "=&v"(q0), "=&v"(w[0]), "=&v"(w[1 % NPL]), "=&v"(w[2 % NPL]), "=&v"(w[3 % NPL]),
+                          "=&v"(w[4 % NPL]), "=&v"(w[5 % NPL])
+                        : "v"(lds_addr(&rtag[slot / 64])), "v"(ra), "v"(ra + (j >> 1) * 4u)
+                        : "memory");
+                } else {
+                    asm volatile(
+                        "ds_read_b32 %0, %5\n\t"
+                        "ds_read_b128 %1, %6\n\t"
+                        "ds_read_b32 %2, %7 offset:1024\n\t"
+                        "ds_read_b32 %3, %7 offset:2048\n\t"
+                        "ds_read_b32 %4, %7 offset:3072\n\t"
+                        "s_waitcnt lgkmcnt(0)"
+                        : "=&v"(tg), "=&v"(q0), "=&v"(w[0]), "=&v"(w[1 % NPL]), "=&v"(w[2 % NPL])
+                        : "v"(lds_addr(&rtag[slot / 64])), "v"(ra), "v"(ra + j * 4u)
+                        : "memory");
+                }
                 if (!__all(!live || tg == lp / 64 + 1)) {
                     LX_WP(c_norec++;)
                     continue;   // wave-uniform: the loader is behind
                 }
                 br = q0.x; seq = q0.y; np = live ? q0.z : 0u;
-                const uint32_t w[3] = {w0, w1, w2};
 #pragma unroll
-                for (int k = 0; k < 3; k++) {
+                for (int k = 0; k < NPL; k++) {
                     const uint32_t pl = w[k] - bs;
-                    const bool in = j + 4 * k < np;
+                    const bool in = pidx(k) < np;
                     px[k] = in ? pl + 1u : kNullTag;
-                    pa[k] = in ? RA + (pl % RN) * UA : ANULL;
+                    pa[k] = in ? RA + uoff + (pl % RN) * UA : ANUL;
                 }
 #pragma unroll
                 for (int k = 0; k < CPW; k++) r[k] = (col(k) == br) ? seq : 0u;
-                if (j < np && w0 - bs >= n) {
+                if (pidx(0) < np && w[0] - bs >= n) {
                     // parents from earlier batches (sorted oldest first): final rows
 #pragma unroll
-                    for (int k = 0; k < 3; k++) {
-                        if (j + 4 * k >= np || w[k] - bs < n) continue;
+                    for (int k = 0; k < NPL; k++) {
+                        if (pidx(k) >= np || w[k] - bs < n) continue;
                         LX_WP(c_slow++;)
                         if (a.seg) {
                             // segment walk: a boundary parent is its own entry only
@@ -997,13 +1043,13 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
                                 if (valid(c)) r[c] = max(r[c], ld_l2_now(row + pc(c)) & mask);
                         }
                         px[k] = kNullTag;
-                        pa[k] = ANULL;
+                        pa[k] = ANUL;
                     }
                 }
                 xi = LX_MAXP;
                 // a parent far enough back that its slot may already hold a newer event
                 // is checked against the L2 path from the first pass on
-                wstuck = __any(far_parent(px, lp, (uint32_t)RN - kLeanFar)) ? kLeanStuck : 0u;
+                wstuck = __any(far_parent<NPL>(px, lp, (uint32_t)RN - kLeanFar)) ? kLeanStuck : 0u;
                 {
                     const uint32_t rs = (lp % RN) * UA;
                     wa_pub = j == 0 ? RA + rs : (((CPW == 4 && !PK) || CPW >= 8) && j == 1) ? RB + (lp % RN) * 16u : dmy;
@@ -1048,14 +1094,34 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
             // reads carried the expected tags, so that pass's unconditional
             // max over them is the event's value; r holds only what does not
             // come from the ring (own seq, L2 rows of old / overflow parents)
-            uint32_t tg[3][2], pv[3][CPW];
-            blk_fold<CPW, RN, PK>(pa, wm_addr, tg, pv, cw);
-            // tag mismatches OR-ed on the VALU: no compare masks and no mask
-            // ANDs on the scalar unit, which the CU's waves share (C3 -1.9 %,
-            // C2 -5.2 % against v_cmp + s_and)
+            uint32_t tg[NPL][2], pv[3][CPW];
+            u4v xs[SPLIT ? NPL : 1];   // SPLIT: the lane's six units
             uint32_t tx = 0;
+            if constexpr (SPLIT) {
+                asm volatile(
+                    "ds_read_b128 %0, %7\n\t"
+                    "ds_read_b128 %1, %8\n\t"
+                    "ds_read_b128 %2, %9\n\t"
+                    "ds_read_b128 %3, %10\n\t"
+                    "ds_read_b128 %4, %11\n\t"
+                    "ds_read_b128 %5, %12\n\t"
+                    "ds_read_b32 %6, %13\n\t"
+                    "s_waitcnt lgkmcnt(0)"
+                    : "=&v"(xs[0]), "=&v"(xs[1 % NPL]), "=&v"(xs[2 % NPL]), "=&v"(xs[3 % NPL]), "=&v"(xs[4 % NPL]),
+                      "=&v"(xs[5 % NPL]), "=&v"(cw)
+                    : "v"(pa[0]), "v"(pa[1 % NPL]), "v"(pa[2 % NPL]), "v"(pa[3 % NPL]), "v"(pa[4 % NPL]),
+                      "v"(pa[5 % NPL]), "v"(wm_addr)
+                    : "memory");
 #pragma unroll
-            for (int k = 0; k < 3; k++) tx |= (tg[k][0] ^ px[k]) | ((PK && CPW == 4) || CPW < 4 ? 0u : (tg[k][1] ^ px[k]));
+                for (int k = 0; k < NPL; k++) { tg[k][0] = tg[k][1] = xs[k].x; tx |= xs[k].x ^ px[k]; }
+            } else {
+                blk_fold<CPW, RN, PK>(pa, wm_addr, tg, pv, cw);
+                // tag mismatches OR-ed on the VALU: no compare masks and no mask
+                // ANDs on the scalar unit, which the CU's waves share (C3 -1.9 %,
+                // C2 -5.2 % against v_cmp + s_and)
+#pragma unroll
+                for (int k = 0; k < 3; k++) tx |= (tg[k][0] ^ px[k]) | ((PK && CPW == 4) || CPW < 4 ? 0u : (tg[k][1] ^ px[k]));
+            }
             // the quad's readiness: its four lanes' mismatches OR-ed by DPP
             // (two VALU steps; the ballot / scalar-shift / per-lane bit test it
             // replaced cost 7 VALU and 3 SALU: C3 walk -3.4 %)
@@ -1066,7 +1132,19 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
             uint32_t mp[NH];   // PK: the quad's maxima, two columns per dword
 #pragma unroll
             for (int h = 0; h < NH; h++) mp[h] = 0u;
-            if constexpr (PK) {
+            if constexpr (SPLIT) {
+                // the lane's unit over its six parents, then lanes j and j ^ 2
+                // (same unit, the other parents): mp[0..2] = the event's unit
+#pragma unroll
+                for (int d = 0; d < 3; d++) {
+                    uint32_t v[NPL];
+#pragma unroll
+                    for (int k = 0; k < NPL; k++) v[k] = d == 0 ? xs[k].y : d == 1 ? xs[k].z : xs[k].w;
+                    const uint32_t t = pk_max(pk_max(pk_max(rpk[d], v[0]), pk_max(v[1 % NPL], v[2 % NPL])),
+                                              pk_max(pk_max(v[3 % NPL], v[4 % NPL]), v[5 % NPL]));
+                    mp[d] = pk_max(t, (uint32_t)__builtin_amdgcn_mov_dpp((int)t, kQuadSwap2, 0xF, 0xF, true));
+                }
+            } else if constexpr (PK) {
                 // two columns per dword: three packed maxima per dword, the quad
                 // reduction on packed words
 #pragma unroll
@@ -1116,7 +1194,7 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
                 if constexpr (PK) {
                     repack(false);
 #pragma unroll
-                    for (int h = 0; h < NH; h++) mp[h] = pk_max(mp[h], rpk[h]);
+                    for (int h = 0; h < (SPLIT ? 3 : NH); h++) mp[h] = pk_max(mp[h], rpk[h]);
                 } else {
 #pragma unroll
                     for (int c = 0; c < CPW; c++) m[c] = max(m[c], r[c]);
@@ -1140,9 +1218,14 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
                     asm volatile("ds_write_b64 %2, %3\n\tds_write_b64 %0, %1" : : "v"(wa), "v"(x), "v"(wb), "v"(y) : "memory");
                 } else if constexpr (PK && CPW >= 8) {
                     u4v x;   // lane 0: {tag, s01, s23, s45}, lane 1: {tag, s67, 0, 0} (12: {tag, s67, s89, s1011})
-                    x.x = lp + 1; x.y = j == 0 ? mp[0] : mp[3 % NH];
-                    x.z = j == 0 ? mp[1 % NH] : CPW == 12 ? mp[4 % NH] : 0u;
-                    x.w = j == 0 ? mp[2 % NH] : CPW == 12 ? mp[5 % NH] : 0u;
+                    x.x = lp + 1;
+                    if constexpr (SPLIT) {
+                        x.y = mp[0]; x.z = mp[1 % NH]; x.w = mp[2 % NH];
+                    } else {
+                        x.y = j == 0 ? mp[0] : mp[3 % NH];
+                        x.z = j == 0 ? mp[1 % NH] : CPW == 12 ? mp[4 % NH] : 0u;
+                        x.w = j == 0 ? mp[2 % NH] : CPW == 12 ? mp[5 % NH] : 0u;
+                    }
                     asm volatile("ds_write_b64 %2, %3\n\tds_write_b128 %0, %1" : : "v"(wa), "v"(x), "v"(wb), "v"(y) : "memory");
                 } else if constexpr (PK) {
                     u4v x;   // lane 0: {tag, s0 | s1 << 16, s2 | s3 << 16, 0}
@@ -1162,14 +1245,14 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
                 // scattered 16-B reads in the passes its wave still makes
                 // (C3 walk -2 %)
 #pragma unroll
-                for (int k = 0; k < 3; k++) pa[k] = done ? ANULL : pa[k];
+                for (int k = 0; k < NPL; k++) pa[k] = done ? ANUL : pa[k];
             }
             if (++wstuck >= kLeanStuck && !rdy && !done) {
                 // waiting long (the wave's block fetched >= 64 passes ago): a
                 // parent's slot may have been reused by a newer event; its HB
                 // row from L2 once its drain stored it
 #pragma unroll
-                for (int k = 0; k < 3; k++) {
+                for (int k = 0; k < NPL; k++) {
                     const uint32_t x = px[k];
                     if (x == kNullTag || (tg[k][0] == x && tg[k][1] == x) || max(tg[k][0], tg[k][1]) <= x) continue;
                     if (!round_done<ND>(sh.stored, x - 1u)) {
@@ -1183,7 +1266,7 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
                     for (int c = 0; c < CPW; c++)
                         if (valid(c)) r[c] = max(r[c], ld_l2_now(row + pc(c)) & mask);
                     px[k] = kNullTag;
-                    pa[k] = ANULL;
+                    pa[k] = ANUL;
                 }
                 repack(false);
             }
@@ -1313,6 +1396,7 @@ static hipError_t launch_index_t(const IndexArgs &a0, hipStream_t s) {
 
 hipError_t launch_index(const IndexArgs &a, hipStream_t s) {
     if (a.n == 0 || a.ncols == 0) return hipSuccess;
+    if (a.stride * 4 > 0xFFFFFFFFull) return hipErrorInvalidValue;   // the drains' 32-bit row pitch
     // columns per workgroup: the fewest that still leave at most ~256
     // workgroups (one per CU); the pass gets shorter with fewer columns per
     // slice, and the walk time is levels x pass latency whatever the number of

@@ -7,7 +7,10 @@ cd "$(dirname "$0")/../.."
 O=${OUT:-gpurun_out/wab}
 mkdir -p $O
 for i in $(seq 1 ${R:-3}); do
-  for lib in lachesis-base_amd/build_ab/liblachesis_hip.so lachesis-base_amd/build/liblachesis_hip.so; do
+  # SWAP=1: the shipped build first in each pair
+  L1=lachesis-base_amd/build_ab/liblachesis_hip.so L2=lachesis-base_amd/build/liblachesis_hip.so
+  [ "${SWAP:-0}" = 1 ] && { t=$L1; L1=$L2; L2=$t; }
+  for lib in $L1 $L2; do
     LX_LIB=$lib timeout -k 10 240 python3 scripts/probes/walk_time.py >> $O/walk_ab.jsonl || exit $?
   done
 done

@@ -1,9 +1,8 @@
 """Walk time of the headline config (C3: V = 1000, Zipf stakes, 10M events,
-one batch, default options = two side-by-side segments of 8-column slices)
+one batch, default options = three side-by-side segments of 12-column slices)
 with whichever library LX_LIB names: median of 5 index steps (ms_index and
-the segment walk from lx_last_segment_stats).  scripts/probes/nofill_ab.sh
-runs it alternately on the shipped build and the timing-only build without
-the LowestAfter range fill."""
+the segment walk from lx_last_segment_stats).  scripts/probes/walk_ab.sh runs
+it alternately on the shipped build and an A/B baseline build."""
 import json
 import os
 import sys
@@ -34,4 +33,6 @@ for r in range(6):
     walks.append(max(st["walk_ms"]) if st["segments"] else None)
 print(json.dumps({"lib": os.environ.get("LX_LIB", "build/liblachesis_hip.so"), "opts": os.environ.get("WT_OPTS", "{}"), "events": N,
                   "ms_index_median": float(np.median(ks[1:])), "ms_index": ks[1:],
-                  "walk_ms": walks[1:], "segments": ix.segment_stats()["segments"]}))
+                  "walk_ms": walks[1:], "segments": ix.segment_stats()["segments"],
+                  # partial events per segment: a walk that publishes wrong rows shows up here
+                  "partial": ix.segment_stats()["partial"]}))
