@@ -70,7 +70,7 @@ void free_all(lx_index *h) {
                     h->first_child, h->first_root, h->branch_first, h->branch_creator, h->branch_len, h->brow,
                     h->wpad, h->col_list, h->cheat_off, h->cheat_br, h->cheat_creator, h->b_creator, h->b_seq,
                     h->b_poff, h->b_par, h->b_isfork, h->b_rank, h->b_tmpbr, h->b_jmp, h->b_rec, h->scan_tmp,
-                    h->q_a, h->q_b, h->q_out};
+                    h->q_a, h->q_b, h->q_out, h->b_crec};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     void *tptrs[] = {h->tail_zw, h->tail_lo, h->tail_cmin, h->wire_flag};
@@ -120,6 +120,7 @@ void free_all(lx_index *h) {
     h->cheat_off = h->cheat_br = h->cheat_creator = nullptr;
     h->b_creator = h->b_seq = h->b_poff = h->b_par = h->b_isfork = h->b_rank = h->b_tmpbr = h->b_jmp = nullptr;
     h->b_rec = nullptr;
+    h->b_crec = nullptr;
     h->scan_tmp = nullptr;
     h->q_a = h->q_b = nullptr;
     h->q_out = nullptr;
@@ -327,6 +328,8 @@ int ensure_batch(lx_index *h, uint64_t n, uint64_t npar) {
         HIPCHK(h, dalloc(&h->b_poff, cap + 1));
         if (h->b_rec) (void)hipFree(h->b_rec);
         HIPCHK(h, dalloc(&h->b_rec, (cap + 63) / 64 * 64));   // whole 64-record rounds (round-blocked SoA)
+        if (h->b_crec) (void)hipFree(h->b_crec);
+        HIPCHK(h, dalloc(&h->b_crec, (cap + 63) / 64 * 64));
         size_t sb = 0;
         HIPCHK(h, lx::scan_tmp_bytes((uint32_t)cap, &sb));
         if (h->scan_tmp) (void)hipFree(h->scan_tmp);
@@ -585,6 +588,7 @@ int seg_walk(lx_index *h, IndexArgs ia, const uint32_t *poff, hipStream_t s, uin
         sk.batch_start = a.seg_lo[k];
         sk.n = a.seg_lo[k + 1] - a.seg_lo[k];
         sk.rec = ia.rec + (a.seg_lo[k] - bs);
+        sk.crec = ia.crec ? ia.crec + (a.seg_lo[k] - bs) : nullptr;
         sk.poff_in = poff + (a.seg_lo[k] - bs);
         sk.seg_j = a.jt + (uint64_t)k * a.B;
         sk.seg_flag = a.pflag + (a.seg_lo[k] - bs);
@@ -670,6 +674,10 @@ int add_batch_dev(lx_index *h, uint32_t n, const uint32_t *creator, const uint32
     if ((rc = grow_scap(h, h->max_seq))) return rc;
     a = batch_args(h, n, creator, seq, poff, par);   // pointers may have moved
     a.nofork = (nforks == 0 && B_new == h->V) ? 1u : 0u;
+    // compact records for the 8- / 12-column walks: fork-free epoch, every
+    // branch and seq within 16 bits (the packed-slot condition)
+    h->b_crec_ok = a.nofork && h->B == h->V && h->pack16 && h->max_seq <= 0xFFFFu && B_new <= 0xFFFFu && h->crec_opt;
+    a.crec = h->b_crec_ok ? h->b_crec : nullptr;
     // pointer jumping along in-batch self-parent chains: a chain has at most
     // min(n, max seq) events, ceil(log2) + 1 rounds resolve it (k_finalize flags
     // an unresolved event, checked below); none without forks
@@ -708,6 +716,7 @@ int add_batch_dev(lx_index *h, uint32_t n, const uint32_t *creator, const uint32
     ia.batch_start = (uint32_t)h->n_events;
     ia.n = n;
     ia.rec = h->b_rec;
+    ia.crec = h->b_crec_ok ? h->b_crec : nullptr;
     ia.par_in = par;
     ia.poff_in = poff;
     ia.col_list = h->col_list;
@@ -773,6 +782,27 @@ int add_batch_dev(lx_index *h, uint32_t n, const uint32_t *creator, const uint32
             for (int i = 0; i < kProfWaves * kProfSlots; i++) sum[i] += (double)pb[i];
         }
         fprintf(stderr, "[lx_prof] n=%u blocks=%u (means per block)\n", n, nb);
+        {
+            // the slowest workgroups: wall (max over its waves) and the compute waves' no-record passes
+            std::vector<std::pair<double, uint32_t>> wb;
+            for (uint32_t b = 0; b < (uint32_t)kProfBlocks; b++) {
+                const unsigned long long *pb = pv.data() + (size_t)b * kProfWaves * kProfSlots;
+                double wmax = 0;
+                for (int w = 0; w < kProfWaves; w++) wmax = std::max(wmax, (double)pb[w * kProfSlots + 9]);
+                if (wmax > 0) wb.push_back({wmax, b});
+            }
+            std::sort(wb.rbegin(), wb.rend());
+            for (size_t i = 0; i < wb.size() && i < 6; i++) {
+                const unsigned long long *pb = pv.data() + (size_t)wb[i].second * kProfWaves * kProfSlots;
+                double norec = 0;
+                for (int w = 0; w < kProfWaves; w++)
+                    if (pb[w * kProfSlots + 10] == 0) norec += (double)pb[w * kProfSlots + 7];
+                fprintf(stderr, "[lx_prof] slow block %u (xcd %u): wall_us=%.0f compute norec=%.0f\n", wb[i].second,
+                        wb[i].second % 8, wb[i].first / 100.0, norec);
+            }
+            if (!wb.empty())
+                fprintf(stderr, "[lx_prof] median block wall_us=%.0f\n", wb[wb.size() / 2].first / 100.0);
+        }
         for (int w = 0; w < kProfWaves; w++) {
             const double *q = sum + w * kProfSlots;
             if (!q[9]) continue;
@@ -1811,6 +1841,8 @@ int lx_set_option(lx_index *h, const char *name, int64_t value) {
         h->cpw_hint = (uint32_t)value;
     } else if (k == "pack16") {
         h->pack16 = value != 0;
+    } else if (k == "crec") {
+        h->crec_opt = value != 0;
     } else if (k == "dbl") {
         h->dbl = value != 0;
     } else if (k == "seg_auto") {

@@ -147,6 +147,8 @@ struct lx_index {
     uint32_t *b_creator = nullptr, *b_seq = nullptr, *b_poff = nullptr, *b_par = nullptr;
     uint32_t *b_isfork = nullptr, *b_rank = nullptr, *b_tmpbr = nullptr, *b_jmp = nullptr;
     EventRec *b_rec = nullptr;
+    CRec *b_crec = nullptr;                // compact records (lx_internal.h) of the last batch
+    bool b_crec_ok = false;                // ... written (fork-free, 16-bit branches and seqs)
     void *scan_tmp = nullptr;
     size_t scan_bytes = 0;
 
@@ -257,6 +259,7 @@ struct lx_index {
     bool small_timing = false;             // option timing=1: time small-path launches (two event records)
     uint32_t cpw_hint = 0;                 // option cpw: walker columns per workgroup (0 = auto)
     bool pack16 = true;                    // option pack16=0: two slot units per event even for small seqs
+    bool crec_opt = false;                 // option crec=1: the 8- / 12-column walks stream the 32-B compact records
     bool prof = false;                     // LX_PROF=1 in make WPROF=1 builds: per-wave walker counters
     uint64_t last_npar = 0;                // parents in the current batch
     FcCache *fcc = nullptr;                // per-pair ForklessCause result cache (lx_fccache.cpp)

@@ -38,6 +38,23 @@ struct EventRec {
     uint4 q[LX_REC_Q];
 };
 
+// Compact event record (2 x uint4 = 32 B, same round-blocked SoA), written
+// beside EventRec for fork-free epochs whose seqs and branches fit 16 bits;
+// the 8- / 12-column walkers stream it instead (half the record bytes, twice
+// the events in the same LDS ring, 31 DMA rounds in flight instead of 15):
+//   c0 branch | seq << 16
+//   c1 number of parents | (event - previous event of the branch) << 8
+//      (0 when the event opens its branch), or kCrecWide: a parent or the
+//      previous event too far back (or > 255 parents) -- that event's walker
+//      reads its EventRec from global memory instead
+//   c2..c7 the first 12 parents as distances back (event - parent, 16 bits
+//      each, low half first), sorted oldest first, 0 past the last parent
+#define LX_CREC_Q 2
+struct CRec {
+    uint4 q[LX_CREC_Q];
+};
+constexpr uint32_t kCrecWide = 0xFFFFFFFFu;
+
 constexpr uint32_t kSegLaunchMax = 32;   // segments of one k_index_segs launch
 struct IndexArgs {
     uint32_t *hb;
@@ -46,6 +63,7 @@ struct IndexArgs {
     uint32_t batch_start;
     uint32_t n;
     const EventRec *rec;
+    const CRec *crec;            // compact records (CPW 8 / 12 walks), or NULL
     const uint32_t *par_in;      // batch parent array (overflow parents)
     const uint32_t *poff_in;     // batch parent offsets
     const uint32_t *col_list;
@@ -131,6 +149,7 @@ struct BatchArgs {
     uint32_t *tmp_br;
     uint32_t *jmp;
     EventRec *rec;
+    CRec *crec;                  // non-NULL: also write the compact records
     uint32_t *status;            // [0] err index, [1] err code, [2] max seq, [3..] jump flags
     uint32_t nofork;             // no fork branch in the epoch nor in the batch: branch = creator
 };

@@ -268,6 +268,21 @@ __global__ void k_finalize(BatchArgs a) {
         for (int t = 0; t < 4; t++) v[t] = (4 * k + t < (int)np) ? w[4 * k + t] : LX_NONE;
         rq[64 * (1 + k)] = make_uint4(v[0], v[1], v[2], v[3]);
     }
+    if (a.crec) {
+        // compact record (lx_internal.h): distances back instead of indices
+        // (the host enables it only when every branch and seq fits 16 bits)
+        uint32_t d[LX_MAXP];
+        bool wide = np > 255u || (prev != LX_NONE && g - prev >= 0xFFFFFFu);
+#pragma unroll
+        for (int k = 0; k < LX_MAXP; k++) {
+            d[k] = (k < (int)np) ? g - w[k] : 0u;
+            wide |= d[k] >= 0xFFFFu;
+        }
+        uint4 *cq = reinterpret_cast<uint4 *>(a.crec) + (uint64_t)(e / 64) * 64 * LX_CREC_Q + (e % 64);
+        const uint32_t c1 = wide ? kCrecWide : np | ((prev == LX_NONE ? 0u : g - prev) << 8);
+        cq[0] = make_uint4(br | (s << 16), c1, d[0] | (d[1] << 16), d[2] | (d[3] << 16));
+        cq[64] = make_uint4(d[4] | (d[5] << 16), d[6] | (d[7] << 16), d[8] | (d[9] << 16), d[10] | (d[11] << 16));
+    }
 }
 
 hipError_t launch_batch_finish(const BatchArgs &a, uint32_t jump_rounds, hipStream_t s) {
@@ -414,9 +429,34 @@ __device__ __forceinline__ uint32_t lds_addr(const void *p) {
     return (uint32_t)(uintptr_t)p;
 }
 
-// field q of the record in record-ring slot `slot` (round-blocked SoA)
+// field q of the record in record-ring slot `slot` (round-blocked SoA, RQ
+// 16-B fields per record: EventRec 4, CRec 2)
+template <int RQ = LX_REC_Q>
 __device__ __forceinline__ uint32_t rec_off(uint32_t slot, uint32_t q) {
-    return (slot & ~63u) * LX_REC_Q + q * 64u + (slot & 63u);
+    return (slot & ~63u) * RQ + q * 64u + (slot & 63u);
+}
+
+// the loader's wait for its oldest record round: all but the RQ DMAs of each
+// of the k younger rounds landed (vmcnt is an immediate: one case per k)
+template <int RQ>
+__device__ __forceinline__ void wait_rounds(uint32_t k) {
+#define LX_VMW(c) case c: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(RQ * c) : "memory"); break;
+    switch (k) {
+        LX_VMW(0) LX_VMW(1) LX_VMW(2) LX_VMW(3) LX_VMW(4) LX_VMW(5) LX_VMW(6) LX_VMW(7)
+        LX_VMW(8) LX_VMW(9) LX_VMW(10) LX_VMW(11) LX_VMW(12) LX_VMW(13) LX_VMW(14)
+        default:
+            if constexpr (RQ == 2) {
+                switch (k) {
+                    LX_VMW(15) LX_VMW(16) LX_VMW(17) LX_VMW(18) LX_VMW(19) LX_VMW(20) LX_VMW(21) LX_VMW(22)
+                    LX_VMW(23) LX_VMW(24) LX_VMW(25) LX_VMW(26) LX_VMW(27) LX_VMW(28) LX_VMW(29)
+                    default: asm volatile("s_waitcnt vmcnt(60)" ::: "memory"); break;
+                }
+            } else {
+                asm volatile("s_waitcnt vmcnt(56)" ::: "memory");
+            }
+            break;
+    }
+#undef LX_VMW
 }
 
 // Per-wave walker counters (LX_PROF=1) are compiled in only with
@@ -550,16 +590,18 @@ __device__ __forceinline__ void blk_fold(const uint32_t pa[3], uint32_t W, uint3
 // The walker kernel.  MASKED: older rows may carry fork marks in bit 31
 // (B > V); PK: 4-column slices with 16-bit packed slot units (every seq of the
 // epoch <= 0xFFFF).
-template <int CPW, int NCW, bool MASKED, bool PK, int ND_ = kND>
+// CR: the compact records (CRec) of 8- / 12-column packed walks
+template <int CPW, int NCW, bool MASKED, bool PK, int ND_ = kND, bool CR = false>
 __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t slice) {
     static_assert(!PK || CPW >= 4, "packed slots: 4-, 8- or 12-column slices");
+    static_assert(!CR || (PK && CPW >= 8), "compact records: 8- / 12-column packed walks");
     static_assert(CPW == 1 || CPW == 2 || CPW == 4 || ((CPW == 8 || CPW == 12) && PK && !MASKED), "slot layout");
     static_assert(LX_MAXP == 12, "block walker: 12 inline parents, three per lane of a quad");
     constexpr int ND = ND_;
     static_assert(ND >= 1 && ND <= 8, "drain waves");
-    constexpr int RR = kRR;
+    constexpr int RR = CR ? 2 * kRR : kRR;   // record ring (events): 64 KB either way
     constexpr int NT = 64 * (NCW + 1 + ND);
-    constexpr int RQ = LX_REC_Q;
+    constexpr int RQ = CR ? LX_CREC_Q : LX_REC_Q;
     constexpr int KB = CPW == 12 ? 64 : 1024 / CPW;   // recent (seq -> event) entries per owned branch
     constexpr int RN = Ring<CPW>::N;
     constexpr int RB16 = Ring<CPW>::BYTES / 16;
@@ -640,13 +682,15 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
         const uint32_t nrounds = (n + 63) / 64;
         // rounds in flight: the DMA round trip is long while the CU's memory
         // queue also carries the drains' stores (the block walker starved at 8)
-        constexpr uint32_t D = RR / 64 - 1 < 15 ? RR / 64 - 1 : 15;
+        constexpr uint32_t DMAX = CR ? 31 : 15;   // vmcnt (6 bits): RQ DMAs per younger round <= 60
+        constexpr uint32_t D = RR / 64 - 1 < DMAX ? RR / 64 - 1 : DMAX;
         uint32_t issued = 0, done = 0;
 #ifdef LX_WALKER_PROF
         uint32_t l_iter = 0, l_slot = 0, l_sleep = 0;
         const unsigned long long lt0 = wall_clock64();
 #endif
-        const char *recb = reinterpret_cast<const char *>(a.rec);
+        const char *recb = CR ? reinterpret_cast<const char *>(a.crec) : reinterpret_cast<const char *>(a.rec);
+        constexpr uint32_t RB_ = RQ * 16;   // record bytes
         while (done < nrounds) {
             bool progressed = false;
             LX_WP(l_iter++;)
@@ -660,8 +704,8 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
             LX_WP(if (issued < nrounds && issued - done < D && !free) l_slot++;)
             if (issued < nrounds && issued - done < D && free) {
                 const uint32_t s0 = (issued * 64) % RR;
-                char *dst = reinterpret_cast<char *>(rrec) + (uint64_t)s0 * sizeof(EventRec);
-                const uint64_t base = (uint64_t)issued * 64 * sizeof(EventRec);
+                char *dst = reinterpret_cast<char *>(rrec) + (uint64_t)s0 * RB_;
+                const uint64_t base = (uint64_t)issued * 64 * RB_;
 #pragma unroll
                 for (int i = 0; i < RQ; i++)
                     __builtin_amdgcn_global_load_lds((const void *)(recb + base + (uint64_t)(i * 64 + lane) * 16),
@@ -672,24 +716,7 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
             }
             if (!progressed && issued > done) {
                 // the oldest round landed once at most RQ DMAs per younger round remain
-                static_assert(D <= 15 && RQ == 4, "vmcnt field (6 bits): at most 14 younger rounds of 4 DMAs");
-                switch (issued - done - 1) {
-                    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-                    case 1: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-                    case 2: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-                    case 3: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
-                    case 4: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
-                    case 5: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
-                    case 6: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
-                    case 7: asm volatile("s_waitcnt vmcnt(28)" ::: "memory"); break;
-                    case 8: asm volatile("s_waitcnt vmcnt(32)" ::: "memory"); break;
-                    case 9: asm volatile("s_waitcnt vmcnt(36)" ::: "memory"); break;
-                    case 10: asm volatile("s_waitcnt vmcnt(40)" ::: "memory"); break;
-                    case 11: asm volatile("s_waitcnt vmcnt(44)" ::: "memory"); break;
-                    case 12: asm volatile("s_waitcnt vmcnt(48)" ::: "memory"); break;
-                    case 13: asm volatile("s_waitcnt vmcnt(52)" ::: "memory"); break;
-                    default: asm volatile("s_waitcnt vmcnt(56)" ::: "memory"); break;
-                }
+                wait_rounds<RQ>(issued - done - 1);
                 // (the vmcnt wait above landed the round; a release store would wait for all)
                 asm volatile("ds_write_b32 %0, %1" : : "v"(lds_addr(&rtag[done % (RR / 64)])), "v"(done + 1) : "memory");
                 done++;
@@ -749,8 +776,18 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
             uint32_t h0[CPW];
             uint32_t prev = LX_NONE, br = 0, seq = 0;
             if (ev < n) {
-                const uint4 q0 = rrec[rec_off(ev % RR, 0)];
-                br = q0.x; seq = q0.y; prev = q0.w;
+                const uint4 q0 = rrec[rec_off<RQ>(ev % RR, 0)];
+                if constexpr (CR) {
+                    br = q0.x & 0xFFFFu; seq = q0.x >> 16;
+                    if (q0.y != kCrecWide) {
+                        prev = (q0.y >> 8) ? bs + ev - (q0.y >> 8) : LX_NONE;
+                    } else {   // rare: the full record (its load waits for this wave's stores)
+                        prev = ld_l2_now(reinterpret_cast<const uint32_t *>(
+                                             reinterpret_cast<const uint4 *>(a.rec) + (uint64_t)(ev / 64) * 64 * LX_REC_Q + ev % 64) + 3);
+                    }
+                } else {
+                    br = q0.x; seq = q0.y; prev = q0.w;
+                }
 #pragma unroll
                 for (int k = 0; k < CPW; k++) h0[k] = 0;
                 if (prev != LX_NONE) {
@@ -978,10 +1015,43 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
             const bool live = lp < n;
             if (!loaded) {
                 const uint32_t slot = lp % RR;
-                const uint32_t ra = lds_addr(rrec) + rec_off(slot, 0) * 16u;
+                const uint32_t ra = lds_addr(rrec) + rec_off<RQ>(slot, 0) * 16u;
                 uint32_t tg, w[NPL];
                 u4v q0;
-                if constexpr (SPLIT) {
+                if constexpr (CR) {
+                    // compact record: c0..c3, c4..c7 (the next field, 1 KB on)
+                    u4v q1;
+                    asm volatile(
+                        "ds_read_b32 %0, %3\n\t"
+                        "ds_read_b128 %1, %4\n\t"
+                        "ds_read_b128 %2, %4 offset:1024\n\t"
+                        "s_waitcnt lgkmcnt(0)"
+                        : "=&v"(tg), "=&v"(q0), "=&v"(q1)
+                        : "v"(lds_addr(&rtag[slot / 64])), "v"(ra)
+                        : "memory");
+                    // this lane's parents (j >> 1) + 2i: half j >> 1 of word 2 + i
+                    const uint32_t dw[6] = {q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+                    const uint32_t gl = bs + lp;
+                    if (q0.y != kCrecWide) {
+#pragma unroll
+                        for (int i = 0; i < NPL; i++) w[i] = gl - ((dw[i % 6] >> (16 * (j >> 1))) & 0xFFFFu);
+                        q0.z = q0.y & 0xFFu;   // np
+                    } else if (live) {
+                        // rare: parents too far back for 16 bits -- the full record
+                        const uint4 *er = reinterpret_cast<const uint4 *>(a.rec) + (uint64_t)(lp / 64) * 64 * LX_REC_Q + lp % 64;
+                        q0.z = ld_l2_now(reinterpret_cast<const uint32_t *>(er) + 2);
+#pragma unroll
+                        for (int i = 0; i < NPL; i++) {
+                            const uint32_t pk = (j >> 1) + 2 * i;
+                            w[i] = ld_l2_now(reinterpret_cast<const uint32_t *>(er + 64 * (1 + pk / 4)) + pk % 4);
+                        }
+                    }
+                    {
+                        const uint32_t c0 = q0.x;
+                        q0.x = c0 & 0xFFFFu;   // branch
+                        q0.y = c0 >> 16;       // seq
+                    }
+                } else if constexpr (SPLIT) {
                     // parents (j >> 1) + 2i: words j >> 1 and (j >> 1) + 2 of
                     // parent fields 1-3 (1 KB apart)
                     asm volatile(
@@ -1295,10 +1365,10 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
     }
 }
 
-template <int CPW, int NCW, bool MASKED, bool PK, int ND = kND>
+template <int CPW, int NCW, bool MASKED, bool PK, int ND = kND, bool CR = false>
 __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
     // XCD-aware: neighbouring slices share an L2
-    index_body<CPW, NCW, MASKED, PK, ND>(a, (blockIdx.x % 8) * a.slices_per_xcd + blockIdx.x / 8);
+    index_body<CPW, NCW, MASKED, PK, ND, CR>(a, (blockIdx.x % 8) * a.slices_per_xcd + blockIdx.x / 8);
 }
 
 // 12-column slices, seg_g walks side by side: workgroup g runs on XCD g % 8
@@ -1329,7 +1399,7 @@ __device__ __forceinline__ bool seg_chunk(uint32_t g, uint32_t G, uint32_t S, ui
 // idle CUs (a walk of few columns leaves most of them idle): workgroup
 // blockIdx.x walks segment blockIdx.x / (gridDim.x / seg_g) with the
 // segment's own batch window, J table and partial-event lists (lx_segment.hip)
-template <int CPW, int NCW, bool MASKED, bool PK, int ND = kND>
+template <int CPW, int NCW, bool MASKED, bool PK, int ND = kND, bool CR = false>
 __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index_segs(IndexArgs a0) {
     uint32_t k, slice;
     if constexpr (CPW == 12) {
@@ -1344,12 +1414,13 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index_segs(IndexArgs a0
     a.batch_start = lo;
     a.n = a0.seg_lo[k + 1] - lo;
     a.rec = a0.rec + off;
+    a.crec = a0.crec ? a0.crec + off : nullptr;
     a.poff_in = a0.poff_in + off;
     a.seg_j = a0.seg_j + (uint64_t)k * a0.seg_B;
     a.seg_flag = a0.seg_flag + off;
     a.seg_list = a0.seg_list + off;
     a.seg_count = a0.seg_count + k;
-    index_body<CPW, NCW, MASKED, PK, ND>(a, slice);
+    index_body<CPW, NCW, MASKED, PK, ND, CR>(a, slice);
 }
 
 template <int CPW, int NCW, int ND = kND>
@@ -1364,7 +1435,10 @@ static hipError_t launch_index_t(const IndexArgs &a0, hipStream_t s) {
         // (12 columns: at most ceil(seg_g * slices / 8) workgroups per XCD, seg_chunk)
         const uint32_t sgrid = CPW == 12 ? 8 * (a.seg_g * (a.n_slices / 8) + (a.seg_g * (a.n_slices % 8) + 7) / 8)
                                          : grid * a.seg_g;
-        if (a.seg_g) hipLaunchKernelGGL((k_index_segs<CPW, NCW, false, true, ND>), dim3(sgrid), blk, 0, s, a);
+        // compact records when the batch wrote them (fork-free, 16-bit branches and seqs)
+        if (a.crec && a.seg_g) hipLaunchKernelGGL((k_index_segs<CPW, NCW, false, true, ND, true>), dim3(sgrid), blk, 0, s, a);
+        else if (a.crec) hipLaunchKernelGGL((k_index<CPW, NCW, false, true, ND, true>), dim3(grid), blk, 0, s, a);
+        else if (a.seg_g) hipLaunchKernelGGL((k_index_segs<CPW, NCW, false, true, ND>), dim3(sgrid), blk, 0, s, a);
         else hipLaunchKernelGGL((k_index<CPW, NCW, false, true, ND>), dim3(grid), blk, 0, s, a);
         return hipGetLastError();
     } else {

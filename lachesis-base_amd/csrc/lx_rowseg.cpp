@@ -271,6 +271,7 @@ int rs_begin(lx_index *h, IndexArgs ia, const uint32_t *poff, hipStream_t s) {
         sk.batch_start = conc ? h->rs_lo : b0;
         sk.n = conc ? h->rs_hi - h->rs_lo : h->rs_seg_lo[k0 + t + 1] - b0;
         sk.rec = ib.rec + sk.batch_start;
+        sk.crec = ib.crec ? ib.crec + sk.batch_start : nullptr;
         sk.poff_in = poff + sk.batch_start;
         sk.seg_j = a.jt + (uint64_t)(k0 + t) * a.B;
         sk.seg_flag = a.pflag + sk.batch_start;

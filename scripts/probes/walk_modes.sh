@@ -5,8 +5,10 @@
 cd "$(dirname "$0")/../.."
 O=${OUT:-gpurun_out/wmodes}
 mkdir -p $O
+# AB_OPTS: odd processes run with WT_OPTS=$AB_OPTS, even ones with the defaults
 for i in $(seq 1 ${N:-4}); do
-  LX_PROF=1 LX_LIB=${WLIB:-lachesis-base_amd/build_ab/liblachesis_wprof.so} timeout -k 10 240 \
+  o='{}'; [ -n "$AB_OPTS" ] && [ $((i % 2)) = 1 ] && o="$AB_OPTS"
+  WT_OPTS="$o" LX_PROF=1 LX_LIB=${WLIB:-lachesis-base_amd/build_ab/liblachesis_wprof.so} timeout -k 10 240 \
       python3 scripts/probes/walk_time.py > $O/p$i.log 2>&1 || exit $?
   tail -n 1 $O/p$i.log
 done

@@ -119,3 +119,61 @@ def test_auto_12_column_segments_equal_single_walk(lx, shape):
     assert np.array_equal(ixa.rows_np(0, ev)[1], o.rows(0, ev)[1])
     ixa.close()
     ix1.close()
+
+
+def _far_dag(lx, n_nodes, n, seed):
+    """Valid fork-free DAG whose non-self parents are uniform over all earlier
+    events: with n >> 65535, many parents lie more than 16 bits of distance
+    back, so their compact records are 'wide' (lx_internal.h CRec)."""
+    rng = np.random.default_rng(seed)
+    creator = rng.integers(0, n_nodes, size=n).astype(np.uint32)
+    seq = np.zeros(n, dtype=np.uint32)
+    lam = np.zeros(n, dtype=np.uint32)
+    last = [-1] * n_nodes
+    poff = [0]
+    par = []
+    for i in range(n):
+        c = int(creator[i])
+        ps = [last[c]] if last[c] >= 0 else []
+        if i:
+            for x in rng.integers(0, i, size=int(rng.integers(0, 4))):
+                x = int(x)
+                if x not in ps and int(creator[x]) != c:
+                    ps.append(x)
+        seq[i] = seq[last[c]] + 1 if last[c] >= 0 else 1
+        lam[i] = 1 + max((int(lam[p]) for p in ps), default=0)
+        last[c] = i
+        par.extend(ps)
+        poff.append(len(par))
+    return lx.tools.Dag(creator, seq, lam, np.array(poff, dtype=np.uint64), np.array(par, dtype=np.uint32), n_nodes)
+
+
+@pytest.mark.parametrize("cpw", [8, 12])
+def test_compact_records_far_parents(lx, cpw):
+    """The 8- / 12-column walks stream 32-B compact records (parents as 16-bit
+    distances back); events with a parent 65535+ events back fall back to the
+    full record.  Planes equal the walk over the 64-B records (option crec=0)
+    and the 4-column walk, rows equal the C oracle, one walk and three
+    segments side by side (option crec=1; the default streams the 64-B
+    records)."""
+    V = 16
+    d = _far_dag(lx, V, 90_000, 5)
+    dist = np.repeat(np.arange(len(d), dtype=np.int64), np.diff(d.poff.astype(np.int64))) - d.par.astype(np.int64)
+    assert (dist >= 0xFFFF).sum() > 1000   # many wide records
+    w = list(range(40, 40 - V, -1))
+    o = corc.OracleIndex(w)
+    assert o.add_batch(d.creator, d.seq, d.poff, d.par) == -1
+    ixc, pc = planes_of(lx, d, w, {"cpw": cpw, "seg_auto": 0, "crec": 1})
+    ixf, pf = planes_of(lx, d, w, {"cpw": cpw, "seg_auto": 0, "crec": 0})
+    ix4, p4 = planes_of(lx, d, w, {"cpw": 4, "seg_auto": 0})
+    for k in (0, 1):
+        np.testing.assert_array_equal(pc[k], pf[k])
+        np.testing.assert_array_equal(pc[k], p4[k])
+    ev = np.arange(0, len(d), 7, dtype=np.uint32)
+    for mode in (0, 1):
+        assert np.array_equal(ixc.rows_np(mode, ev)[1], o.rows(mode, ev)[1]), mode
+    ixs, ps = planes_of(lx, d, w, {"cpw": cpw, "segments": 3, "crec": 1})
+    for k in (0, 1):
+        np.testing.assert_array_equal(ps[k], p4[k])
+    for ix in (ixc, ixf, ix4, ixs):
+        ix.close()
