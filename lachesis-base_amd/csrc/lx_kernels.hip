@@ -755,12 +755,23 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
             const uint32_t sl = ev % RN;
             Slot<CPW> me;
             me.t0 = me.t1 = 0;
+            // packed 8- / 12-column slots: the spin keeps the raw units and
+            // unpacks once after it (12 VALU per spin otherwise)
+            u4v mx = {0, 0, 0, 0}, my = {0, 0, 0, 0};
             // wait for the round (keep publishing progress: others may wait on it)
             while (true) {
                 bool ready = true;
                 if (ev < n) {
-                    ring_read1<CPW, PK>(RA, RB, sl, me);
-                    ready = me.t0 == ev + 1 && me.t1 == ev + 1;
+                    if constexpr (PK && CPW >= 8) {
+                        asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %3\n\ts_waitcnt lgkmcnt(0)"
+                                     : "=&v"(mx), "=&v"(my)
+                                     : "v"(RA + sl * 16u), "v"(RB + sl * 16u)
+                                     : "memory");
+                        ready = mx.x == ev + 1 && my.x == ev + 1;
+                    } else {
+                        ring_read1<CPW, PK>(RA, RB, sl, me);
+                        ready = me.t0 == ev + 1 && me.t1 == ev + 1;
+                    }
                 }
                 if (__all(ready)) break;
                 LX_WP(d_spin++;)
@@ -769,6 +780,12 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
                     if (lane == 0) __hip_atomic_store(&sh.stored[d], nd, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
                 __builtin_amdgcn_s_sleep(1);
+            }
+            if constexpr (PK && CPW >= 8) {
+                me.t0 = mx.x; me.t1 = my.x;
+                const uint32_t w6[6] = {mx.y, mx.z, mx.w, my.y, my.z, my.w};
+#pragma unroll
+                for (int k = 0; k < CPW; k++) me.v[k] = (k & 1) ? w6[(k / 2) % 6] >> 16 : w6[(k / 2) % 6] & 0xFFFFu;
             }
 #ifdef LX_WALKER_PROF
             const unsigned long long tb0 = wall_clock64();
@@ -832,7 +849,7 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
                     // event of some branch is "partial" (lx_segment.hip fixes it up)
                     bool unc = false;
 #pragma unroll
-                    for (int k = 0; k < CPW; k++) unc |= valid(k) && (r[k] & mask) < sj[k];
+                    for (int k = 0; k < CPW; k++) unc |= (ID || valid(k)) && (r[k] & mask) < sj[k];
                     if (unc && atomicOr(a.seg_flag + ev, 1u) == 0u) a.seg_list[atomicAdd(a.seg_count, 1u)] = bs + ev;
                 }
                 // HB row (raw values incl. fork bits as published)
@@ -862,7 +879,10 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
                         // event and its prev (lx_segment.hip), the rows up to J_k are
                         // filled by k_seg_la_edge
                         lo[k] = max(max(h0[k], sj[k]) + 1u, first(k));
-                        hi[k] = valid(k) ? (r[k] & mask) : 0u;
+                        // (12-column slices: a column past the epoch's holds 0 in
+                        // every slot -- its col never equals a branch -- so it
+                        // fills nothing without a check)
+                        hi[k] = (ID || valid(k)) ? (r[k] & mask) : 0u;
                     }
                     if (!ID && a.lap) {
                         // sharded: rows of own branches addressed by (column, seq)
