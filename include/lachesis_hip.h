@@ -74,6 +74,9 @@ const char *lx_last_error(const lx_index *h);
  *   "cpw"        walker columns per workgroup: 0 (auto), 1, 2, 4, 8 or 12 (8, 12: packed
  *                fork-free epochs, else 4; 12: whole handles, a sharded one walks 8)
  *   "pack16"     0: two slot units per event even when every seq fits 16 bits
+ *   "crec"       1: the 8- / 12-column walks stream 32-B compact event records instead of
+ *                the 64-B ones (fork-free epochs, 16-bit branches and seqs)
+ *   "fc_early_lanes" 32 (default) or 16 lanes per query in the early-exit ForklessCause
  *   "dbl"        0: the column walker also for fork-free batches of <= 16 branches
  *                (default: HighestBefore by frontier doubling in one workgroup, lx_dbl.hip)
  *   "la_memset"  1: zero the whole LowestAfter plane at lx_reset instead of the tail pass (before lx_reset)
@@ -97,7 +100,8 @@ const char *lx_last_error(const lx_index *h);
  *                side in one launch, G = CUs / walk workgroups, >= 32k events each)
  *   "get_server" 0: every single-row getter launches its kernel (default 1: the resident
  *                row server answers them while the stream is idle, lx_get_server_stats)
- * The library reads no environment variables. */
+ * The library reads no environment variables (the walker-counters build,
+ * make WPROF=1, reads LX_PROF). */
 int lx_set_option(lx_index *h, const char *name, int64_t value);
 
 /* Reset (vecfc/index.go:98-105, vecengine/index.go:56-68): new epoch with
