@@ -975,6 +975,7 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
         uint32_t blk = __builtin_amdgcn_readfirstlane(wave);   // wave-uniform: scalar loop control
         bool loaded = false, done = true;
         uint32_t br = 0, seq = 0, np = 0, xi = 0;
+        bool wxi = false;   // some event of the wave's block has parents beyond the inline twelve (wave-uniform)
         uint32_t wstuck = 0;   // passes since the block fetch (wave-uniform)
         // SPLIT (packed 8- / 12-column slots, two 16-B units per event): lane j
         // of a quad reads unit j & 1 of the parents (j >> 1) + 2i, i < 6, so a
@@ -1137,6 +1138,7 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
                     }
                 }
                 xi = LX_MAXP;
+                wxi = __any(np > (uint32_t)LX_MAXP);
                 // a parent far enough back that its slot may already hold a newer event
                 // is checked against the L2 path from the first pass on
                 wstuck = __any(far_parent<NPL>(px, lp, (uint32_t)RN - kLeanFar)) ? kLeanStuck : 0u;
@@ -1250,7 +1252,7 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
                     m[c] = quad_max(max(t, pv[2][c]));
                 }
             }
-            if (rdy && !done && xi < np) {
+            if (wxi && rdy && !done && xi < np) {   // (the scalar test first: most blocks have none)
                 // parents beyond the inline twelve (rare): one per pass, the same on every lane of the quad
                 const uint32_t pg = ld_l2_now(a.par_in + a.poff_in[lp] + xi);
                 const uint32_t lpp = pg - bs;
