@@ -9,7 +9,7 @@ O=${OUT:-gpurun_out/wab}
 mkdir -p $O
 for i in $(seq 1 ${R:-3}); do
   # SWAP=1: the shipped build first in each pair
-  L1=lachesis-base_amd/build_ab/liblachesis_hip.so L2=lachesis-base_amd/build/liblachesis_hip.so
+  L1=${LIB_A:-lachesis-base_amd/build_ab/liblachesis_hip.so} L2=${LIB_B:-lachesis-base_amd/build/liblachesis_hip.so}
   [ "${SWAP:-0}" = 1 ] && { t=$L1; L1=$L2; L2=$t; }
   if [ -n "$AB_OPTS" ]; then
     # one library, an option set A/B instead: WT_OPTS=$AB_OPTS against the default
