@@ -1000,8 +1000,24 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
         // SPLIT keeps only the lane's unit (rpk[0..2])
         constexpr int NH = CPW / 2 > 0 ? CPW / 2 : 1;
         uint32_t rpk[NH];
+        // FASTR (12-column slices, SPLIT): r is never materialised -- the own
+        // seq and the rare row contributions go straight into the lane's
+        // packed unit (rpk[0..2]), which saves the block fetch ~60 VALU
+        // (12 compares and selects for r, the repack, the recent-entry select)
+        constexpr bool FASTR = SPLIT && ID;
+        auto addcol = [&](int c, uint32_t v) {
+            if constexpr (FASTR) {
+                // column c: unit c / 6, word (c % 6) / 2, half c & 1 (v <= 0xFFFF)
+                const uint32_t wv = (c & 1) ? v << 16 : v;
+                rpk[((c % 6) / 2) % NH] = (uint32_t)(c / 6) == (j & 1) ? pk_max(rpk[((c % 6) / 2) % NH], wv) : rpk[((c % 6) / 2) % NH];
+            } else {
+                r[c] = max(r[c], v);
+            }
+        };
         auto repack = [&](bool fresh) {
-            if constexpr (SPLIT) {
+            if constexpr (FASTR) {
+                return;
+            } else if constexpr (SPLIT) {
 #pragma unroll
                 for (int d = 0; d < 3; d++) {
                     const uint32_t pA = r[(2 * d) % CPW] | (r[(2 * d + 1) % CPW] << 16);
@@ -1113,8 +1129,16 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
                     px[k] = in ? pl + 1u : kNullTag;
                     pa[k] = in ? RA + uoff + (pl % RN) * UA : ANUL;
                 }
+                if constexpr (FASTR) {
+                    // the own seq in column br - c0 (past the slice: no column)
+                    const uint32_t c = br - c0;
+                    const uint32_t hv = (c & 1) ? seq << 16 : seq;
 #pragma unroll
-                for (int k = 0; k < CPW; k++) r[k] = (col(k) == br) ? seq : 0u;
+                    for (int d = 0; d < 3; d++) rpk[d] = c < nval && c / 6 == (j & 1) && (c % 6) / 2 == (uint32_t)d ? hv : 0u;
+                } else {
+#pragma unroll
+                    for (int k = 0; k < CPW; k++) r[k] = (col(k) == br) ? seq : 0u;
+                }
                 if (pidx(0) < np && w[0] - bs >= n) {
                     // parents from earlier batches (sorted oldest first): final rows
 #pragma unroll
@@ -1126,12 +1150,12 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
                             const uint32_t pb = a.ev_branch[w[k]], ps = a.ev_seq[w[k]];
 #pragma unroll
                             for (int c = 0; c < CPW; c++)
-                                if (valid(c) && col(c) == pb) r[c] = max(r[c], ps);
+                                if (valid(c) && col(c) == pb) addcol(c, ps);
                         } else {
                             const uint32_t *row = a.hb + (uint64_t)w[k] * stride;
 #pragma unroll
                             for (int c = 0; c < CPW; c++)
-                                if (valid(c)) r[c] = max(r[c], ld_l2_now(row + pc(c)) & mask);
+                                if (valid(c)) addcol(c, ld_l2_now(row + pc(c)) & mask);
                         }
                         px[k] = kNullTag;
                         pa[k] = ANUL;
@@ -1146,13 +1170,10 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
                     const uint32_t rs = (lp % RN) * UA;
                     wa_pub = j == 0 ? RA + rs : (((CPW == 4 && !PK) || CPW >= 8) && j == 1) ? RB + (lp % RN) * 16u : dmy;
                     if constexpr (CPW == 12) {
-                        // lane j of a quad owns columns j, j + 4, j + 8 (recent-event entries)
-                        uint32_t wb = dmy + 1024u;
-#pragma unroll
-                        for (int k = 0; k < CPW; k++)
-                            if ((uint32_t)(k & 3) == j && valid(k) && col(k) == br)
-                                wb = lds_addr(brc) + ((uint32_t)k * KB + seq % KB) * 8u;
-                        wb_pub = wb;
+                        // lane j of a quad owns columns j, j + 4, j + 8 (recent-event
+                        // entries): the own column br - c0 when it is one of them
+                        const uint32_t c = br - c0;
+                        wb_pub = c < nval && (c & 3) == j ? lds_addr(brc) + (c * KB + seq % KB) * 8u : dmy + 1024u;
                     } else {
                         wb_pub = (myvalid && mycol == br) ? lds_addr(brc) + ((j & (CPW - 1)) * KB + seq % KB) * 8u
                                  : (CPW == 8 && myvalid2 && mycol2 == br) ? lds_addr(brc) + (((j + 4) & (CPW - 1)) * KB + seq % KB) * 8u
@@ -1262,7 +1283,7 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
                     ring_read1<CPW, PK>(RA, RB, lpp % RN, ps);
                     if (ps.t0 == lpp + 1 && ps.t1 == lpp + 1) {
 #pragma unroll
-                        for (int c = 0; c < CPW; c++) r[c] = max(r[c], ps.v[c]);
+                        for (int c = 0; c < CPW; c++) addcol(c, ps.v[c]);
                         ok = true;
                     } else if (max(ps.t0, ps.t1) > lpp + 1) {
                         if (round_done<ND>(sh.stored, lpp)) old = true;
@@ -1273,13 +1294,13 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
                     const uint32_t pb = a.ev_branch[pg], ps = a.ev_seq[pg];
 #pragma unroll
                     for (int c = 0; c < CPW; c++)
-                        if (valid(c) && col(c) == pb) r[c] = max(r[c], ps);
+                        if (valid(c) && col(c) == pb) addcol(c, ps);
                     ok = true;
                 } else if (old) {
                     const uint32_t *row = a.hb + (uint64_t)pg * stride;
 #pragma unroll
                     for (int c = 0; c < CPW; c++)
-                        if (valid(c)) r[c] = max(r[c], ld_l2_now(row + pc(c)) & mask);
+                        if (valid(c)) addcol(c, ld_l2_now(row + pc(c)) & mask);
                     ok = true;
                 }
                 // the same parent on every lane of the quad: m stays the quad's value
@@ -1356,7 +1377,7 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
                     const uint32_t *row = a.hb + (uint64_t)(x - 1u + bs) * stride;
 #pragma unroll
                     for (int c = 0; c < CPW; c++)
-                        if (valid(c)) r[c] = max(r[c], ld_l2_now(row + pc(c)) & mask);
+                        if (valid(c)) addcol(c, ld_l2_now(row + pc(c)) & mask);
                     px[k] = kNullTag;
                     pa[k] = ANUL;
                 }
