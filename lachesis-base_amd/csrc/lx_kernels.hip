@@ -616,6 +616,7 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
     __shared__ WalkShared sh;
     __shared__ uint32_t sjs[CPW];                // segment walk: J_k of the slice's columns (drains)
     __shared__ uint32_t sfirst[CPW];             // 12-column slices: first seq of each column (drains)
+    __shared__ uint32_t slof[CPW];               // drains: max(J_k + 1, first seq) -- the range fill's floor
 
     if (slice >= a.n_slices) return;
 
@@ -631,6 +632,8 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
         const uint32_t ci = slice * CPW + threadIdx.x;
         sjs[threadIdx.x] = a.seg && ci < a.ncols ? a.seg_j[CPW == 12 ? ci : a.col_list[ci]] : 0u;
         sfirst[threadIdx.x] = CPW == 12 && ci < a.ncols ? a.branch_first[ci] : 1u;
+        const uint32_t cf = ci < a.ncols ? a.branch_first[CPW == 12 ? ci : a.col_list[ci]] : 1u;
+        slof[threadIdx.x] = max(sjs[threadIdx.x] + 1u, cf);
     }
     if (threadIdx.x == 0) { sh.req = 0; sh.p_issued = 0; sh.p_done = 0; }
     __syncthreads();
@@ -878,7 +881,7 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
                         // segment walk: the rows after J_k only; L is RAW there for this
                         // event and its prev (lx_segment.hip), the rows up to J_k are
                         // filled by k_seg_la_edge
-                        lo[k] = max(max(h0[k], sj[k]) + 1u, first(k));
+                        lo[k] = max(h0[k] + 1u, slof[k]);
                         // (12-column slices: a column past the epoch's holds 0 in
                         // every slot -- its col never equals a branch -- so it
                         // fills nothing without a check)
