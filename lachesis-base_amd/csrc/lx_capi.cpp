@@ -2360,6 +2360,11 @@ GetSrvArgs srv_args_of(const lx_index *h, const GetArgs &a) {
     s.g.ev0 = 0;
     s.g.mode = 0;
     s.g.tag = 0;
+    // a server outlives Adds: its bound is the handle's capacity (rows past
+    // n_events are zero or stale there; the host check, option
+    // getter_host_check, refuses such events before any request is posted),
+    // so that an Add between two getters does not relaunch it
+    if (!h->rowseg()) s.g.row_hi = (uint32_t)std::min<uint64_t>(h->n_cap, 0xFFFFFFFFull);
     s.hb = h->hb;
     s.la = h->la;
     s.req = h->srv_dev;
@@ -2472,9 +2477,10 @@ int get_rows(lx_index *h, uint32_t mode, uint32_t n, const uint32_t *ev, uint8_t
     a.len = reinterpret_cast<uint32_t *>(dp + 4ull * n);
     a.out = dp + head;
     a.slot = sl;
-    // the device's own bound (k_get_server takes the event from a request word)
+    // the device's own bound: the events indexed so far on a launch (the
+    // resident server's bound is the capacity instead, srv_args_of)
     a.row_lo = h->rowseg() ? h->rs_lo : 0u;
-    a.row_hi = h->rowseg() ? h->rs_hi : (uint32_t)std::min<uint64_t>(h->n_cap, 0xFFFFFFFFull);
+    a.row_hi = h->rowseg() ? h->rs_hi : (uint32_t)h->n_events;
     if (n == 1) {
         // one row (the reference's per-call getters): the resident server
         // answers it when the handle's stream is idle (no launch); otherwise a

@@ -857,20 +857,34 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
                 }
                 // HB row (raw values incl. fork bits as published)
                 uint32_t *hrow = a.hb + (uint64_t)(bs + ev) * stride;
+#ifdef LX_PROBE_NOHB
+                (void)hrow;    // probe build: HB row stores compiled out (timing / write counters only)
+                if (false) {
+#else
                 if (contig) {
+#endif
                     if (CPW == 1) hrow[pc(0)] = r[0];
                     else if (CPW == 2) *reinterpret_cast<uint2 *>(hrow + pc(0)) = make_uint2(r[0], r[1 % CPW]);
                     else if (CPW == 4) *reinterpret_cast<uint4 *>(hrow + pc(0)) = make_uint4(r[0], r[1 % CPW], r[2 % CPW], r[3 % CPW]);
                     else {
 #pragma unroll
-                        for (int q = 0; q < CPW / 4; q++)
+                        for (int q = 0; q < CPW / 4; q++) {
+#if defined(LX_PROBE_HBNT) || defined(LX_PROBE_NT)   // probe: nontemporal HB stores
+                            __builtin_nontemporal_store(
+                                u4v{r[(4 * q) % CPW], r[(4 * q + 1) % CPW], r[(4 * q + 2) % CPW], r[(4 * q + 3) % CPW]},
+                                reinterpret_cast<u4v *>(hrow + pc(0) + 4 * q));
+#else
                             *reinterpret_cast<uint4 *>(hrow + pc(0) + 4 * q) =
                                 make_uint4(r[(4 * q) % CPW], r[(4 * q + 1) % CPW], r[(4 * q + 2) % CPW], r[(4 * q + 3) % CPW]);
+#endif
+                        }
                     }
                 } else {
+#ifndef LX_PROBE_NOHB
 #pragma unroll
                     for (int k = 0; k < CPW; k++)
                         if (valid(k)) hrow[pc(k)] = r[k];
+#endif
                 }
                 {
                     // LowestAfter range fill: events (col, s), s in (h0, r], are first
@@ -916,7 +930,16 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
                                 // one 32 x 32 + 64 multiply-add per store: column br of
                                 // the LA plane as the base, the row pitch in bytes
                                 // (< 4 GB, launch_index) as a 32-bit factor
+#if defined(LX_PROBE_LANT) || defined(LX_PROBE_NT)   // probe: nontemporal LA stores
+                                __builtin_nontemporal_store(seq, reinterpret_cast<uint32_t *>(la_br + (uint64_t)row * pitch));
+#elif defined(LX_PROBE_LASC1)   // probe: LA stores at agent scope (sc1)
+                                __hip_atomic_store(reinterpret_cast<uint32_t *>(la_br + (uint64_t)row * pitch), seq,
+                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#elif !defined(LX_PROBE_NOLA)   // probe build NOLA: LowestAfter range-fill stores compiled out
                                 *reinterpret_cast<uint32_t *>(la_br + (uint64_t)row * pitch) = seq;
+#else
+                                asm volatile("" ::"v"(row), "v"(seq));
+#endif
                             }
                         }
                     }

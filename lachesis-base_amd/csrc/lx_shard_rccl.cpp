@@ -30,6 +30,7 @@
 #include <vector>
 
 #include "lachesis_hip.h"
+#include "lx_index.h"
 #include "lx_rowseg_exchange.h"
 #include "lx_shard_exchange.h"
 
@@ -461,13 +462,24 @@ struct RcclRowNet {
     }
 };
 
+// A whole index (no row segments) on a one-rank communicator: nothing to
+// join, the calls go straight to the index.  A row-segment handle (seg_count
+// >= 1) before its batch is not whole: LX_ERR_STATE, as every step out of order.
+static int rs_whole(lx_shard_comm *c, bool *whole) {
+    *whole = c->nranks == 1 && !c->ix->rowseg();
+    if (c->ix->rowseg() && !c->ix->rs_state)
+        return c->fail(LX_ERR_STATE, "row-segment handle has no batch yet (lx_add_batch first)");
+    return 0;
+}
+
 int lx_rowseg_exchange(lx_shard_comm *c, uint64_t stats[4]) {
     if (!c) return LX_ERR_ARG;
     if (!c->rowseg) return c->fail(LX_ERR_STATE, "not a row-segment communicator (lx_rowseg_comm_create)");
     LXC(c->hip(hipSetDevice(c->device), "hipSetDevice"));
     const uint32_t G = c->nranks;
-    uint32_t lo = 0, hi = 0;
-    if (G == 1 && lx_rowseg_range(c->ix, &lo, &hi) != 0) return 0;   // a whole index: nothing to join
+    bool whole = false;
+    LXC(rs_whole(c, &whole));
+    if (whole) return 0;   // a whole index: nothing to join
     if (!c->udev) LXC(c->hip(hipMalloc(reinterpret_cast<void **>(&c->udev), 8ull * (2 * G + 1)), "hipMalloc"));
     RcclRowOps ops{c};
     RcclRowNet net{c};
@@ -493,8 +505,9 @@ int lx_rowseg_forkless_cause(lx_shard_comm *c, uint64_t n, const uint32_t *qa, c
     if (!c->rowseg) return c->fail(LX_ERR_STATE, "not a row-segment communicator (lx_rowseg_comm_create)");
     LXC(c->hip(hipSetDevice(c->device), "hipSetDevice"));
     const uint32_t G = c->nranks;
-    uint32_t lo = 0, hi = 0;
-    if (G == 1 && lx_rowseg_range(c->ix, &lo, &hi) != 0) {   // a whole index
+    bool whole = false;
+    LXC(rs_whole(c, &whole));
+    if (whole) {
         LXC(c->index(lx_forkless_cause_batch_dev(c->ix, n, qa, qb, out, nullptr), "lx_forkless_cause_batch_dev"));
         return c->index(lx_sync(c->ix), "lx_sync");
     }
@@ -523,8 +536,15 @@ int lx_rowseg_get_rows(lx_shard_comm *c, uint32_t mode, uint64_t n, const uint32
     if (!c->rowseg) return c->fail(LX_ERR_STATE, "not a row-segment communicator (lx_rowseg_comm_create)");
     LXC(c->hip(hipSetDevice(c->device), "hipSetDevice"));
     const uint32_t G = c->nranks;
-    uint32_t lo = 0, hi = 0;
-    if (G == 1 && lx_rowseg_range(c->ix, &lo, &hi) != 0) {   // a whole index
+    // one slot rule for both paths, checked before any collective: a slot
+    // holds the longest row (8 B per branch, HB) and is a multiple of 16 B
+    // (lx_rowseg_rows_unroute)
+    if (n && (slot < 8ull * std::max(c->ix->B, c->ix->V) || slot % 16))
+        return c->fail(LX_ERR_ARG, "row slot of %llu bytes: needs >= %llu and a multiple of 16",
+                       (unsigned long long)slot, 8ull * std::max(c->ix->B, c->ix->V));
+    bool whole = false;
+    LXC(rs_whole(c, &whole));
+    if (whole) {
         if (n > 0xFFFFFFFFull) return c->fail(LX_ERR_ARG, "too many rows in one call");
         return c->index(lx_get_rows_dev(c->ix, mode, (uint32_t)n, ev, out, slot, len), "lx_get_rows_dev");
     }

@@ -1,0 +1,42 @@
+"""Is the walk's slow mode a property of the process or of the allocation?
+
+One process, WM_INST fresh Index handles one after the other (each allocates
+its own HB / LA planes and record buffers, and frees them before the next),
+WM_WALKS walks of the headline config (C3: V = 1000, Zipf stakes, 10M events,
+one batch, default options) on each.  One JSON line per handle: walk ms per
+step.  LX_LIB picks the library (probe builds: make build_pNOLA/... or
+build_pNOHB/..., the LowestAfter range-fill or HB row stores compiled out).
+"""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "lachesis-base_amd")]
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import lachesis_hip as lx  # noqa: E402
+
+V, epv = int(os.environ.get("WT_V", "1000")), int(os.environ.get("WT_EPV", "10000"))
+n_inst, n_walk = int(os.environ.get("WM_INST", "3")), int(os.environ.get("WM_WALKS", "4"))
+d = lx.tools.gen_dag(V, epv, 10, seed=1)
+N = len(d)
+w = [(1 << 20) // (i + 1) for i in range(V)]
+dev = torch.device("cuda", 0)
+to_dev = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int32)).to(dev)
+dc, ds, dp, do = to_dev(d.creator), to_dev(d.seq), to_dev(d.par), to_dev(d.poff.astype(np.uint32))
+lib = os.path.basename(os.path.dirname(os.environ.get("LX_LIB", "build/x")))
+for inst in range(n_inst):
+    ix = lx.Index(event_capacity=N, options=json.loads(os.environ.get("WT_OPTS", "{}")))
+    hb_ptr, la_ptr, stride, _ = ix.device_planes()
+    walks = []
+    for r in range(n_walk):
+        ix.reset(w)
+        ix.add_batch_dev(N, dc.data_ptr(), ds.data_ptr(), do.data_ptr(), dp.data_ptr())
+        ix.sync()
+        st = ix.segment_stats()
+        walks.append(round(max(st["walk_ms"]), 2) if st["segments"] else round(ix.last_stats()["ms_index"], 2))
+    print(json.dumps({"lib": lib, "pid": os.getpid(), "inst": inst, "walk_ms": walks,
+                      "hb": hex(hb_ptr or 0), "la": hex(la_ptr or 0), "partial": st["partial"]}), flush=True)
+    ix.close()
+    del ix

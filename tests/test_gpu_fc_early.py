@@ -19,14 +19,19 @@ def lx():
     return lachesis_hip
 
 
+# fc_early_lanes: 32 lanes per query (rounds of 128 / 256 / 512 columns, the
+# default) or 16 (k_fc_early<., 16>: its own width-16 shuffles, rounds of 64 /
+# 128 / 256 columns)
+@pytest.mark.parametrize("lanes", [32, 16])
 @pytest.mark.parametrize("V,epv,zipf", [(300, 60, True), (1000, 30, True), (600, 40, True), (300, 60, False),
                                          (1000, 30, False)])
-def test_early_exit_equals_whole_rows_and_oracle(lx, V, epv, zipf):
+def test_early_exit_equals_whole_rows_and_oracle(lx, V, epv, zipf, lanes):
     d = lx.tools.gen_dag(V, epv, 10, seed=V + epv)
     w = [(1 << 20) // (i + 1) for i in range(V)] if zipf else [3] * V
     o = corc.OracleIndex(w)
     assert o.add_batch(d.creator, d.seq, d.poff, d.par) == -1
     ix = lx.Index(event_capacity=len(d))
+    ix.set_option("fc_early_lanes", lanes)
     ix.reset(w)
     ix.add_batch(d.creator, d.seq, d.poff, d.par)
     ix.sync()
@@ -55,7 +60,8 @@ def test_early_exit_equals_whole_rows_and_oracle(lx, V, epv, zipf):
     ix.close()
 
 
-def test_early_exit_unknown_events(lx):
+@pytest.mark.parametrize("lanes", [32, 16])
+def test_early_exit_unknown_events(lx, lanes):
     """Queries on events past the index answer 0xFF through the early path too
     (V = 600: rows of 150 uint4; a launch of 2^14 queries, the smallest that
     takes the early path; the device's counter shows every query went through
@@ -64,6 +70,7 @@ def test_early_exit_unknown_events(lx):
     d = lx.tools.gen_dag(V, 20, 10, seed=4)
     w = [(1 << 20) // (i + 1) for i in range(V)]
     ix = lx.Index(event_capacity=len(d))
+    ix.set_option("fc_early_lanes", lanes)
     ix.reset(w)
     ix.add_batch(d.creator, d.seq, d.poff, d.par)
     ix.sync()
