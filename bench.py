@@ -650,6 +650,7 @@ def main():
             ix = lx.Index(device=local, event_capacity=N,
                           options={"segments": args.segments} if args.segments > 1 else None)
         st_x = []   # shard / rowseg: the exchange of each step, ms
+        clk_log = []   # shader clock of each step's walk (lx_last_walk_clock)
         d_blk = None
 
         def index_step():
@@ -663,6 +664,7 @@ def main():
                 s = ix.last_stats()
                 st_idx += s["ms_index"]
                 st_asg += s["ms_assign"] + s["ms_marks"]
+            clk_log.append(ix.walk_clock())
             if kind == "shard":
                 tx = time.perf_counter()
                 sx.exchange()
@@ -758,12 +760,27 @@ def main():
                          "whole_rows": int(early_all[3]), "answered": int(nq_all) * args.steps}
                if early_all[0] else None,
                "whole_row_bytes": 8.0 * B * nq, "st_x": st_x,
-               "mem": ix.device_bytes()}
+               "mem": ix.device_bytes(), "clk": clk_log[-args.steps:]}
         if kind == "rowseg":
             out["rsx"] = rsx
         if kind == "shard":
             out["sx"] = sx
         return out
+
+    def walk_clock_summary(clk):
+        """The shader clock each timed step's walk ran at (lx_last_walk_clock:
+        s_memtime cycles over s_memrealtime ticks of every workgroup's compute
+        wave 0), and the walk's cycle count: the walk's time is a fixed number
+        of cycles over the clock the box gives it."""
+        c = [x for x in clk if x["mhz_median"] > 0]
+        if not c:
+            return None
+        mhz = [x["mhz_median"] for x in c]
+        mcyc = [x["mhz_median"] * x["walk_ms"] / 1e3 for x in c]
+        return {"mhz_median": float(np.median(mhz)), "mhz_min_step": float(min(mhz)), "mhz_max_step": float(max(mhz)),
+                "mhz_min_workgroup": float(min(x["mhz_min"] for x in c)),
+                "walk_mcycles_median": float(np.median(mcyc)), "steps": len(c),
+                "source": "lx_last_walk_clock after each timed step (median over workgroups per step)"}
 
     primary = "solo" if solo else "rowseg" if rowseg else "shard" if shard else "single"
     P = leg(primary)
@@ -855,6 +872,7 @@ def main():
         "fc_queries_per_sec": fc_per_s,
         "fc_ms_per_step": t_fc / args.steps * 1e3,
         "index_kernel_ms": kidx,
+        "walk_clock": walk_clock_summary(P["clk"]),
         "assign_and_marks_ms": float(np.mean(k_assign_ms)),
         "roofline": {"bound": "hbm", "kernel": fc_kernel_name, "achieved": fc_achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": fc_achieved / HBM_PEAK_GBS,

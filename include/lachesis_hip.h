@@ -239,6 +239,32 @@ int lx_fc_early_counters(lx_index *h, uint64_t *queries, uint64_t *second_round,
 int lx_forkless_cause_partial_dev(lx_index *h, uint64_t n, const uint32_t *a_dev, const uint32_t *b_dev,
                                   uint32_t *partial_dev, void *stream);
 int lx_fc_combine_dev(lx_index *h, uint64_t n, const uint32_t *sum_dev, uint8_t *out_dev, void *stream);
+
+/* Column-shard early exit: ForklessCause compares a stake sum
+ * in pos.Validators idx order with the quorum (vecfc/forkless_cause.go:63-82),
+ * and shard 0 holds the heaviest creators.  From its own partial it decides a
+ * query when the partial reaches the quorum (true) or cannot reach it with
+ * every other shard's stake added (false); only the undecided queries need the
+ * other shards' partials and the all-reduce.  Applies on fork-free epochs
+ * where shard 0 can decide something (lx_fc_shard_early: 1, *rest = the stake
+ * of shards 1..G-1).  Every rank, collectively:
+ *   shard 0:   lx_forkless_cause_partial_dev over all n queries, then
+ *              lx_fc_shard_decide_dev -> mask (2 ceil(n/64) words: decided bits,
+ *              then answer bits); the mask is broadcast from shard 0;
+ *   all:       lx_fc_shard_undecided_dev -> the m undecided queries in query
+ *              order (idx, a, b; shard 0 also its partials) -- completed on
+ *              return, *m on the host;
+ *   shards>0:  lx_forkless_cause_partial_dev over the m undecided pairs;
+ *   all:       sum the m partials over the shards, lx_fc_shard_answer_dev.
+ * The answers equal lx_fc_combine_dev over the full sums
+ * (lx_forkless_cause_sharded_dev and lachesis_hip.shard run it). */
+int lx_fc_shard_early(const lx_index *h, uint32_t *rest);
+int lx_fc_shard_decide_dev(lx_index *h, uint64_t n, const uint32_t *partial_dev, uint64_t *mask_dev, void *stream);
+int lx_fc_shard_undecided_dev(lx_index *h, uint64_t n, const uint64_t *mask_dev, const uint32_t *a_dev,
+                              const uint32_t *b_dev, const uint32_t *partial_dev, uint32_t *idx_dev, uint32_t *a_out_dev,
+                              uint32_t *b_out_dev, uint32_t *partial_out_dev, uint64_t *m);
+int lx_fc_shard_answer_dev(lx_index *h, uint64_t n, const uint64_t *mask_dev, uint64_t m, const uint32_t *idx_dev,
+                           const uint32_t *sum_dev, uint8_t *out_dev, void *stream);
 uint32_t lx_quorum(const lx_index *h);                 /* pos/validators.go:187-189 */
 
 /* Getters.  *len receives the byte length; out may be NULL to query it.
@@ -282,7 +308,11 @@ int lx_get_event_branch_id(lx_index *h, uint32_t ev, uint32_t *out);
  * the handle does not hold -- not indexed, or another row-segment rank's --
  * gets length 0xFFFFFFFF and no row.  Completed on return.  The row-segment
  * getters route ids to their owners and call this there
- * (lachesis_hip/rowseg.py, lx_rowseg_get_rows). */
+ * (lachesis_hip/rowseg.py, lx_rowseg_get_rows).  On a column shard each slot
+ * holds this shard's branches (merged HighestBefore: its creators) and zeros
+ * elsewhere, and len_dev the length this shard's entries imply: the word-wise
+ * sum of all shards' slots is the whole row and the maximum of their lengths
+ * its length (lx_shard_get_rows; LowestAfter after the exchange). */
 int lx_get_rows_dev(lx_index *h, uint32_t mode, uint32_t n, const uint32_t *ev_dev, uint8_t *out_dev,
                     uint64_t slot_bytes, uint32_t *len_dev);
 int lx_row_bytes_max(const lx_index *h, uint64_t *bytes);   /* 8 x max(branches, validators) */
@@ -354,7 +384,10 @@ int lx_shard_dirty_commit(lx_index *h);
  * stream; unpack; own block);
  * lx_forkless_cause_sharded_dev = partial stake sums, an ncclAllReduce (sum,
  * uint32: exact, the true total fits 32 bits) and the quorum test, all
- * stream-ordered on the handle's stream.  Every rank must make the same calls
+ * stream-ordered on the handle's stream (calls of >= 2^14 queries on epochs
+ * where lx_fc_shard_early applies: shard 0's partials first, an ncclBroadcast
+ * of its decisions, the other shards' partials and the all-reduce over the
+ * undecided queries only).  Every rank must make the same calls
  * in the same order (collectives).  RCCL is loaded on first use (dlopen of
  * librccl.so.1, reusing a copy the process already holds); nranks must equal
  * the handle's shard_count and rank its shard_rank; one GPU per rank (RCCL
@@ -375,6 +408,19 @@ int lx_shard_exchange_layout(uint32_t G, uint32_t self, const uint64_t *entries,
                              uint64_t *off);
 int lx_forkless_cause_sharded_dev(lx_shard_comm *c, uint64_t n, const uint32_t *a_dev, const uint32_t *b_dev,
                                   uint8_t *out_dev);
+/* Queries the last lx_forkless_cause_sharded_dev sent to every shard: the
+ * undecided ones of the early exit (lx_fc_shard_early; calls of >= 2^14
+ * queries), else all of them. */
+int lx_shard_fc_undecided(const lx_shard_comm *c, uint64_t *undecided);
+/* The vector getters on column shards (GetHighestBefore / GetLowestAfter /
+ * GetMergedHighestBefore, vecfc/store_vectors.go:26-51, vecengine/index.go:235-250):
+ * every rank calls collectively with the same events; each encodes its own
+ * branches (lx_get_rows_dev), an ncclAllReduce sums the slots and another takes
+ * the maximum length, so every rank gets the whole rows.  LowestAfter rows
+ * need the LowestAfter exchange since the last Add (lx_shard_exchange).  slot:
+ * >= lx_row_bytes_max, a multiple of 16. */
+int lx_shard_get_rows(lx_shard_comm *c, uint32_t mode, uint64_t n, const uint32_t *ev_dev, uint8_t *out_dev,
+                      uint64_t slot_bytes, uint32_t *len_dev);
 
 /* Timing of the last lx_add_batch* call, measured with HIP events on the
  * handle's stream (milliseconds): branch assignment + record packing,
@@ -386,6 +432,14 @@ typedef struct lx_stats {
     uint32_t index_launches;
 } lx_stats;
 int lx_last_stats(const lx_index *h, lx_stats *out);
+
+/* The shader clock of the last walk (k_index / k_index_segs): compute wave 0
+ * of every workgroup stamps s_memtime (shader cycles) and s_memrealtime
+ * (100 MHz) around its walk.  out[0] median, out[1] min, out[2] max clock over
+ * the workgroups (MHz), out[3] the median workgroup's walk (ms).  A walk's
+ * cycle count is set by the DAG; its time is cycles / clock.
+ * Synchronizes the handle's stream; zeros before the first walk.  Diagnostics. */
+int lx_last_walk_clock(lx_index *h, float out[4]);
 
 /* Timings of the last segmented batch (option "segments"): per segment its
  * first event, walk time and number of "partial" events (rows that needed

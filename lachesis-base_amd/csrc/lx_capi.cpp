@@ -729,6 +729,11 @@ int add_batch_dev(lx_index *h, uint32_t n, const uint32_t *creator, const uint32
     ia.pack16 = h->pack16 && h->max_seq <= 0xFFFFu;
     if (ia.cpw_hint >= 8 && (!ia.pack16 || ia.mask)) ia.cpw_hint = 4;   // 8- / 12-column slots: packed, fork-free
     const size_t prof_n = (size_t)kProfBlocks * kProfWaves * kProfSlots;
+    if (!h->d_clk) {
+        HIPCHK(h, hipMalloc(&h->d_clk, (1 + 3ull * kClkBlocks) * 8));
+        HIPCHK(h, hipMemsetAsync(h->d_clk, 0, (1 + 3ull * kClkBlocks) * 8, s));
+    }
+    ia.clk = h->d_clk;
     if (h->prof) {
         HIPCHK(h, hipMalloc(&ia.prof, prof_n * 8));
         HIPCHK(h, hipMemsetAsync(ia.prof, 0, prof_n * 8, s));
@@ -1788,11 +1793,40 @@ void lx_destroy(lx_index *h) {
     if (h->qp) (void)hipHostFree(h->qp);
     if (h->ld_buf) (void)hipFree(h->ld_buf);
     if (h->d_fc_full) (void)hipFree(h->d_fc_full);
+    if (h->d_clk) (void)hipFree(h->d_clk);
+    for (void *q : {(void *)h->fcs_flag, (void *)h->fcs_pos, h->fcs_tmp})
+        if (q) (void)hipFree(q);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
 }
 
 const char *lx_last_error(const lx_index *h) { return h ? h->err.c_str() : "null handle"; }
+
+int lx_last_walk_clock(lx_index *h, float out[4]) {
+    if (!h || !out) return LX_ERR_ARG;
+    out[0] = out[1] = out[2] = out[3] = 0.0f;
+    if (!h->d_clk) return 0;
+    HIPCHK(h, set_dev(h->device));
+    std::vector<unsigned long long> v(1 + 3ull * kClkBlocks);
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    HIPCHK(h, hipMemcpy(v.data(), h->d_clk, v.size() * 8, hipMemcpyDeviceToHost));
+    std::vector<float> mhz, ms;
+    const uint64_t g = std::min<uint64_t>(v[0], kClkBlocks);
+    for (uint64_t b = 0; b < g; b++) {
+        const unsigned long long cyc = v[1 + 3 * b], tick = v[2 + 3 * b];
+        if (!tick || !cyc) continue;   // a workgroup without a walk (rounding, or none of the columns)
+        mhz.push_back((float)((double)cyc / (double)tick * 100.0));
+        ms.push_back((float)((double)tick / 1e5));
+    }
+    if (mhz.empty()) return 0;
+    std::sort(mhz.begin(), mhz.end());
+    std::sort(ms.begin(), ms.end());
+    out[0] = mhz[mhz.size() / 2];
+    out[1] = mhz.front();
+    out[2] = mhz.back();
+    out[3] = ms[ms.size() / 2];
+    return 0;
+}
 
 int lx_fc_early_rounds(lx_index *h, uint64_t out[4]) {
     if (!h || !out) return LX_ERR_ARG;
@@ -2247,6 +2281,78 @@ int lx_forkless_cause_partial_dev(lx_index *h, uint64_t n, const uint32_t *a, co
     return 0;
 }
 
+// ---- column-shard early exit
+int lx_fc_shard_early(const lx_index *h, uint32_t *rest) {
+    if (!h) return 0;
+    if (rest) *rest = 0;
+    // fork-free (no shard's partial carries a mark or exceeds its stake) and
+    // shard 0 able to decide something alone
+    if (!h->sharded() || !h->have_epoch || h->B != h->V || h->weights.size() != h->V) return 0;
+    uint32_t lo, hi;
+    shard_bounds(h, 0, &lo, &hi);
+    uint64_t w0 = 0, wt = 0;
+    for (uint32_t c = 0; c < h->V; c++) {
+        wt += h->weights[c];
+        if (c >= lo && c < hi) w0 += h->weights[c];
+    }
+    if (wt - w0 > 0xFFFFFFFFull) return 0;
+    if (rest) *rest = (uint32_t)(wt - w0);
+    return (w0 >= h->quorum || wt - w0 < h->quorum) ? 1 : 0;
+}
+
+int lx_fc_shard_decide_dev(lx_index *h, uint64_t n, const uint32_t *partial, uint64_t *mask, void *stream) {
+    if (!h || (n && (!partial || !mask))) return LX_ERR_ARG;
+    uint32_t rest = 0;
+    if (!lx_fc_shard_early(h, &rest)) return h->fail(LX_ERR_STATE, "the column-shard early exit does not apply (lx_fc_shard_early)");
+    if (h->shard_rank != 0) return h->fail(LX_ERR_STATE, "only shard 0 decides early (its creators are the heaviest)");
+    hipStream_t s = stream ? (hipStream_t)stream : h->stream;
+    const uint64_t W = (n + 63) / 64;
+    HIPCHK(h, lx::launch_fcs_decide(partial, n, h->quorum, rest, reinterpret_cast<unsigned long long *>(mask),
+                                    reinterpret_cast<unsigned long long *>(mask) + W, s));
+    return 0;
+}
+
+int lx_fc_shard_undecided_dev(lx_index *h, uint64_t n, const uint64_t *mask, const uint32_t *a, const uint32_t *b,
+                              const uint32_t *partial, uint32_t *idx, uint32_t *a_out, uint32_t *b_out, uint32_t *p_out,
+                              uint64_t *m) {
+    if (!h || !m || (n && (!mask || !a || !b || !idx || !a_out || !b_out || (partial && !p_out)))) return LX_ERR_ARG;
+    if (!h->sharded()) return h->fail(LX_ERR_STATE, "the column-shard early exit needs a column-sharded handle");
+    if (n > 0x7FFFFFFFull) return h->fail(LX_ERR_ARG, "too many queries in one call");
+    *m = 0;
+    if (!n) return 0;
+    HIPCHK(h, set_dev(h->device));
+    if (n > h->fcs_cap) {
+        (void)hipStreamSynchronize(h->stream);
+        for (void *q : {(void *)h->fcs_flag, (void *)h->fcs_pos, h->fcs_tmp})
+            if (q) (void)hipFree(q);
+        h->fcs_flag = h->fcs_pos = nullptr;
+        h->fcs_tmp = nullptr;
+        h->fcs_cap = 0;
+        HIPCHK(h, lxi::dalloc(&h->fcs_flag, n));
+        HIPCHK(h, lxi::dalloc(&h->fcs_pos, n));
+        HIPCHK(h, lx::fcs_scan_bytes(n, &h->fcs_tmp_bytes));
+        HIPCHK(h, hipMalloc(&h->fcs_tmp, std::max<size_t>(h->fcs_tmp_bytes, 16)));
+        h->fcs_cap = n;
+    }
+    HIPCHK(h, lx::launch_fcs_undecided(reinterpret_cast<const unsigned long long *>(mask), n, a, b, partial, h->fcs_flag,
+                                       h->fcs_pos, h->fcs_tmp, h->fcs_tmp_bytes, idx, a_out, b_out, p_out, h->stream));
+    uint32_t cnt = 0;
+    HIPCHK(h, hipMemcpyAsync(&cnt, h->fcs_pos + (n - 1), 4, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    *m = cnt;
+    return 0;
+}
+
+int lx_fc_shard_answer_dev(lx_index *h, uint64_t n, const uint64_t *mask, uint64_t m, const uint32_t *idx,
+                           const uint32_t *sum, uint8_t *out, void *stream) {
+    if (!h || (n && (!mask || !out)) || (m && (!idx || !sum)) || m > n) return LX_ERR_ARG;
+    hipStream_t s = stream ? (hipStream_t)stream : h->stream;
+    const uint64_t W = (n + 63) / 64;
+    const auto *dec = reinterpret_cast<const unsigned long long *>(mask);
+    HIPCHK(h, lx::launch_fcs_answer(dec, dec + W, n, m, idx, sum, h->quorum, out, s));
+    return 0;
+}
+
 int lx_fc_combine_dev(lx_index *h, uint64_t n, const uint32_t *sum, uint8_t *out, void *stream) {
     if (!h) return LX_ERR_ARG;
     hipStream_t s = stream ? (hipStream_t)stream : h->stream;
@@ -2537,7 +2643,8 @@ int get_rows(lx_index *h, uint32_t mode, uint32_t n, const uint32_t *ev, uint8_t
 }
 
 int get_check(lx_index *h, uint32_t n, const uint32_t *ev) {
-    if (h->sharded()) return h->fail(LX_ERR_STATE, "vector getters need an unsharded handle (shards hold their own columns)");
+    if (h->sharded())
+        return h->fail(LX_ERR_STATE, "a column shard holds its own columns: lx_shard_get_rows (or lx_get_rows_dev + a sum over the shards)");
     if (!h->have_epoch) return h->fail(LX_ERR_STATE, "getter before lx_reset");
     NOT_LOADING(h);
     if (h->rowseg()) {
@@ -2646,7 +2753,6 @@ int lx_row_bytes_max(const lx_index *h, uint64_t *bytes) {
 int lx_get_rows_dev(lx_index *h, uint32_t mode, uint32_t n, const uint32_t *ev_dev, uint8_t *out_dev,
                     uint64_t slot_bytes, uint32_t *len_dev) {
     if (!h || mode > 2 || (n && (!ev_dev || !out_dev || !len_dev))) return LX_ERR_ARG;
-    if (h->sharded()) return h->fail(LX_ERR_STATE, "vector getters need an unsharded handle (shards hold their own columns)");
     if (!h->have_epoch) return h->fail(LX_ERR_STATE, "getter before lx_reset");
     NOT_LOADING(h);
     if (h->rowseg() && h->rs_state != 4) return h->fail(LX_ERR_STATE, "row-segment rank: getters before lx_rowseg_finish");
@@ -2677,6 +2783,12 @@ int lx_get_rows_dev(lx_index *h, uint32_t mode, uint32_t n, const uint32_t *ev_d
     a.slot = slot_bytes;
     a.row_lo = h->rowseg() ? h->rs_lo : 0u;
     a.row_hi = h->rowseg() ? h->rs_hi : (uint32_t)h->n_events;
+    if (h->sharded()) {
+        // this shard's branches only, the rest of every slot zero: the shards'
+        // slots sum word by word to the whole row (lx_shard_get_rows)
+        a.cmap = h->cmap;
+        HIPCHK(h, hipMemsetAsync(out_dev, 0, (uint64_t)n * slot_bytes, h->stream));
+    }
     HIPCHK(h, lx::launch_get_rows(a, h->stream));
     HIPCHK(h, hipStreamSynchronize(h->stream));
     return 0;

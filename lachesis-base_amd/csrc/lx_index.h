@@ -269,6 +269,12 @@ struct lx_index {
     uint32_t segments = 0;
     bool fc_early = true;                  // option fc_early=0: k_fc always reads whole rows
     uint32_t fc_early_lanes = 32;          // option fc_early_lanes: k_fc_early's lanes per query (16 or 32)
+    unsigned long long *d_clk = nullptr;       // walk clock records (IndexArgs::clk)
+    // column-shard early exit (lx_fc_shard_undecided_dev): flags, scan, scan scratch
+    uint32_t *fcs_flag = nullptr, *fcs_pos = nullptr;
+    void *fcs_tmp = nullptr;
+    uint64_t fcs_cap = 0;
+    size_t fcs_tmp_bytes = 0;
     unsigned long long *d_fc_full = nullptr;   // early exit counters (device): past round 1, past round 2, all
     bool seg_auto = true;                  // option seg_auto=0: never split a batch on its own
     uint32_t n_cus = 256;                  // compute units of the device (auto segments)

@@ -76,6 +76,8 @@ struct IndexArgs {
     uint32_t mask;               // older rows may carry fork marks
     uint32_t cpw_hint;           // columns per workgroup (0 = auto; lx_set_option "cpw", tests)
     unsigned long long *prof;    // per-wave counters (make WPROF=1 builds only), kProfSlots per wave
+    unsigned long long *clk;     // walk clock (lx_last_walk_clock): [0] grid size, then per workgroup
+                                 // < kClkBlocks {shader cycles, 100 MHz ticks, XCD} of compute wave 0
     const uint32_t *cmap;        // sharded: global branch -> plane column (NULL = identity)
     uint32_t *lap;               // sharded: LowestAfter rows of own branches (fill target)
     uint64_t lap_stride;         // = global branch capacity
@@ -122,6 +124,7 @@ __host__ __device__ inline uint64_t dbl_lds_bytes(uint64_t n, uint64_t B) {
 constexpr int kProfSlots = 16;   // see k_index: passes, spin misses, chunk folds, completes, ...
 constexpr int kProfWaves = 16;   // waves per workgroup in the counter layout
 constexpr int kProfBlocks = 4096;
+constexpr int kClkBlocks = 1024;   // walk clock records (IndexArgs::clk)
 
 struct BatchArgs {
     uint32_t n;
@@ -475,6 +478,9 @@ struct GetArgs {
     // with length kGetBadLen and no row (the host turns it into LX_ERR_ARG) --
     // the device's own bound, whatever event a request word names
     uint32_t row_lo, row_hi;
+    // column shard: branch -> plane column (LX_NONE: another shard's branch,
+    // read as 0); NULL: whole rows
+    const uint32_t *cmap;
 };
 constexpr uint32_t kGetBadLen = 0xFFFFFFFFu;
 
@@ -707,6 +713,17 @@ hipError_t launch_stage(uint32_t *dst, const uint32_t *src, uint64_t words, hipS
 hipError_t launch_marks(const MarkArgs &a, hipStream_t s);
 hipError_t launch_fc(const FcArgs &a, uint32_t cols, bool forks, hipStream_t s);
 hipError_t launch_fc_combine(const uint32_t *sum, uint8_t *out, uint64_t n, uint32_t quorum, hipStream_t s);
+// column-shard early exit (lx_fc_shard_*): shard 0's decisions as bits per
+// query (dec: decided, ans: the answer), the undecided queries compacted in
+// query order, the answers from both
+hipError_t launch_fcs_decide(const uint32_t *part, uint64_t n, uint32_t quorum, uint32_t rest, unsigned long long *dec,
+                             unsigned long long *ans, hipStream_t s);
+hipError_t fcs_scan_bytes(uint64_t n, size_t *bytes);
+hipError_t launch_fcs_undecided(const unsigned long long *dec, uint64_t n, const uint32_t *a, const uint32_t *b,
+                                const uint32_t *p0, uint32_t *flag, uint32_t *pos, void *tmp, size_t tmp_bytes,
+                                uint32_t *idx, uint32_t *a2, uint32_t *b2, uint32_t *p2, hipStream_t s);
+hipError_t launch_fcs_answer(const unsigned long long *dec, const unsigned long long *ans, uint64_t n, uint64_t m,
+                             const uint32_t *idx, const uint32_t *sum, uint32_t quorum, uint8_t *out, hipStream_t s);
 hipError_t launch_unfill(const UnfillArgs &a, hipStream_t s);
 hipError_t launch_zero_rows(uint32_t *hb, uint32_t *la, uint64_t stride, uint32_t lo, uint32_t hi, hipStream_t s);
 hipError_t launch_la_tail(const TailArgs &a, hipStream_t s);

@@ -1434,10 +1434,39 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
     }
 }
 
+// Walk clock (lx_last_walk_clock): compute wave 0 of each workgroup stamps
+// s_memtime (shader cycles) and s_memrealtime (100 MHz) around its walk; the
+// ratio is the shader clock the walk ran at (the walk's cycle count is fixed
+// by the DAG, its time is cycles / clock: DESIGN.md section 14)
+struct WalkClock {
+    unsigned long long c0 = 0, r0 = 0;
+    __device__ __forceinline__ void start() {
+        if (threadIdx.x == 0) asm volatile("s_memtime %0\n\ts_memrealtime %1\n\ts_waitcnt lgkmcnt(0)" : "=s"(c0), "=s"(r0) :: "memory");
+    }
+    // ran = false: the workgroup had no walk (a zero record)
+    __device__ __forceinline__ void stop(unsigned long long *clk, bool ran) {
+        if (threadIdx.x != 0 || !clk) return;
+        unsigned long long c1, r1;
+        uint32_t xcc;
+        asm volatile("s_memtime %0\n\ts_memrealtime %1\n\ts_waitcnt lgkmcnt(0)" : "=s"(c1), "=s"(r1) :: "memory");
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        if (blockIdx.x == 0) clk[0] = gridDim.x;
+        if (blockIdx.x < (uint32_t)kClkBlocks) {
+            clk[1 + 3 * blockIdx.x] = ran ? c1 - c0 : 0ull;
+            clk[2 + 3 * blockIdx.x] = ran ? r1 - r0 : 0ull;
+            clk[3 + 3 * blockIdx.x] = xcc;
+        }
+    }
+};
+
 template <int CPW, int NCW, bool MASKED, bool PK, int ND = kND, bool CR = false>
 __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
+    WalkClock wc;
+    wc.start();
     // XCD-aware: neighbouring slices share an L2
-    index_body<CPW, NCW, MASKED, PK, ND, CR>(a, (blockIdx.x % 8) * a.slices_per_xcd + blockIdx.x / 8);
+    const uint32_t slice = (blockIdx.x % 8) * a.slices_per_xcd + blockIdx.x / 8;
+    index_body<CPW, NCW, MASKED, PK, ND, CR>(a, slice);
+    wc.stop(a.clk, slice < a.n_slices);
 }
 
 // 12-column slices, seg_g walks side by side: workgroup g runs on XCD g % 8
@@ -1468,11 +1497,17 @@ __device__ __forceinline__ bool seg_chunk(uint32_t g, uint32_t G, uint32_t S, ui
 // idle CUs (a walk of few columns leaves most of them idle): workgroup
 // blockIdx.x walks segment blockIdx.x / (gridDim.x / seg_g) with the
 // segment's own batch window, J table and partial-event lists (lx_segment.hip)
+
 template <int CPW, int NCW, bool MASKED, bool PK, int ND = kND, bool CR = false>
 __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index_segs(IndexArgs a0) {
+    WalkClock wc;
+    wc.start();
     uint32_t k, slice;
     if constexpr (CPW == 12) {
-        if (!seg_chunk(blockIdx.x, a0.seg_g, a0.n_slices, &k, &slice)) return;
+        if (!seg_chunk(blockIdx.x, a0.seg_g, a0.n_slices, &k, &slice)) {
+            wc.stop(a0.clk, false);
+            return;
+        }
     } else {
         const uint32_t per = gridDim.x / a0.seg_g, w = blockIdx.x % per;
         k = blockIdx.x / per;
@@ -1490,6 +1525,7 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index_segs(IndexArgs a0
     a.seg_list = a0.seg_list + off;
     a.seg_count = a0.seg_count + k;
     index_body<CPW, NCW, MASKED, PK, ND, CR>(a, slice);
+    wc.stop(a0.clk, slice < a.n_slices);
 }
 
 template <int CPW, int NCW, int ND = kND>
@@ -2013,6 +2049,86 @@ __global__ void k_fc_combine(const uint32_t *sum, uint8_t *out, uint64_t n, uint
 hipError_t launch_fc_combine(const uint32_t *sum, uint8_t *out, uint64_t n, uint32_t quorum, hipStream_t s) {
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(k_fc_combine, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, sum, out, n, quorum);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------- column-shard early exit
+//  Shard 0 holds the heaviest creators (pos.Validators idx
+// order, vecfc/forkless_cause.go:63-82 sums stake in that order): from its own
+// partial p it decides a query when p >= quorum (true whatever the other
+// shards add) or p + rest < quorum (false whatever they add), rest = the stake
+// of every other shard -- on fork-free epochs, where no shard's partial
+// exceeds its creators' stake and none carries a mark bit.  One bit per query
+// in 64-query words: dec (decided), ans (the answer of a decided query).
+__global__ __launch_bounds__(256) void k_fcs_decide(const uint32_t *part, uint64_t n, uint32_t quorum, uint32_t rest,
+                                                    unsigned long long *dec, unsigned long long *ans) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t p = i < n ? part[i] : 0u;
+    const bool t = i < n && p >= quorum;
+    const bool d = t || (i < n && (uint64_t)p + rest < quorum);
+    const unsigned long long bd = __ballot(d), bt = __ballot(t);
+    if ((threadIdx.x & 63) == 0 && i < n) {
+        dec[i / 64] = bd;
+        ans[i / 64] = bt;
+    }
+}
+
+hipError_t launch_fcs_decide(const uint32_t *part, uint64_t n, uint32_t quorum, uint32_t rest, unsigned long long *dec,
+                             unsigned long long *ans, hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_fcs_decide, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, part, n, quorum, rest, dec, ans);
+    return hipGetLastError();
+}
+
+__global__ void k_fcs_flags(const unsigned long long *dec, uint64_t n, uint32_t *flag) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) flag[i] = ((dec[i / 64] >> (i % 64)) & 1ull) ? 0u : 1u;
+}
+
+// the undecided queries in query order (every rank compacts the same bits the
+// same way: the all-reduce adds matching partials), shard 0's partials with them
+__global__ void k_fcs_gather(const uint32_t *flag, const uint32_t *pos, uint64_t n, const uint32_t *a, const uint32_t *b,
+                             const uint32_t *p0, uint32_t *idx, uint32_t *a2, uint32_t *b2, uint32_t *p2) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || !flag[i]) return;
+    const uint32_t j = pos[i] - 1;
+    idx[j] = (uint32_t)i;
+    a2[j] = a[i];
+    b2[j] = b[i];
+    if (p0) p2[j] = p0[i];
+}
+
+hipError_t fcs_scan_bytes(uint64_t n, size_t *bytes) {
+    return hipcub::DeviceScan::InclusiveSum(nullptr, *bytes, (uint32_t *)nullptr, (uint32_t *)nullptr, (int)n);
+}
+
+hipError_t launch_fcs_undecided(const unsigned long long *dec, uint64_t n, const uint32_t *a, const uint32_t *b,
+                                const uint32_t *p0, uint32_t *flag, uint32_t *pos, void *tmp, size_t tmp_bytes,
+                                uint32_t *idx, uint32_t *a2, uint32_t *b2, uint32_t *p2, hipStream_t s) {
+    if (!n) return hipSuccess;
+    const dim3 g((uint32_t)((n + 255) / 256));
+    hipLaunchKernelGGL(k_fcs_flags, g, dim3(256), 0, s, dec, n, flag);
+    size_t tb = tmp_bytes;
+    hipError_t r = hipcub::DeviceScan::InclusiveSum(tmp, tb, flag, pos, (int)n, s);
+    if (r != hipSuccess) return r;
+    hipLaunchKernelGGL(k_fcs_gather, g, dim3(256), 0, s, flag, pos, n, a, b, p0, idx, a2, b2, p2);
+    return hipGetLastError();
+}
+
+__global__ void k_fcs_answer(const unsigned long long *dec, const unsigned long long *ans, uint64_t n, uint8_t *out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = (uint8_t)((dec[i / 64] & ans[i / 64]) >> (i % 64) & 1ull);
+}
+
+__global__ void k_fcs_scatter(const uint32_t *idx, uint64_t m, const uint32_t *sum, uint32_t quorum, uint8_t *out) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < m) out[idx[j]] = (uint8_t)(sum[j] < LX_MARK && sum[j] >= quorum);
+}
+
+hipError_t launch_fcs_answer(const unsigned long long *dec, const unsigned long long *ans, uint64_t n, uint64_t m,
+                             const uint32_t *idx, const uint32_t *sum, uint32_t quorum, uint8_t *out, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(k_fcs_answer, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, dec, ans, n, out);
+    if (m) hipLaunchKernelGGL(k_fcs_scatter, dim3((uint32_t)((m + 255) / 256)), dim3(256), 0, s, idx, m, sum, quorum, out);
     return hipGetLastError();
 }
 

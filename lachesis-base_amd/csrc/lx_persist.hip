@@ -164,6 +164,14 @@ __device__ __forceinline__ void get_row(const GetArgs &a, uint32_t i, uint32_t e
     }
     const uint32_t *row = a.plane + (uint64_t)e * a.stride;
     uint32_t *o = reinterpret_cast<uint32_t *>(a.out + (uint64_t)i * a.slot);
+    // entry of branch c: a column shard holds its own branches' columns only
+    // (the others read as 0: the caller sums the shards' rows)
+    const uint32_t *cmap = a.cmap;
+    auto at = [row, cmap](uint32_t c) -> uint32_t {
+        if (!cmap) return row[c];
+        const uint32_t pc = cmap[c];
+        return pc == LX_NONE ? 0u : row[pc];
+    };
     if (a.mode == 2 && a.forks) {
         // 8 creators per lane computed before their stores (loads after a store
         // to host memory would wait for it, see below)
@@ -176,12 +184,12 @@ __device__ __forceinline__ void get_row(const GetArgs &a, uint32_t i, uint32_t e
                 if (c < a.V) {
                     const int32_t k = a.cheat_of[c];
                     if (k < 0) {
-                        const uint32_t v = row[c];
+                        const uint32_t v = at(c);
                         if (v) x = make_uint2(v & LX_SEQ_MASK, a.branch_first[c]);
                     } else {
                         for (uint32_t j = a.cheat_off[k]; j < a.cheat_off[k + 1]; j++) {
                             const uint32_t b = a.cheat_br[j];
-                            const uint32_t v = row[b];
+                            const uint32_t v = at(b);
                             if (v & LX_MARK) { x = make_uint2(0u, 0x7FFFFFFFu); break; }
                             if (v > x.x) x = make_uint2(v, a.branch_first[b]);
                         }
@@ -213,7 +221,7 @@ __device__ __forceinline__ void get_row(const GetArgs &a, uint32_t i, uint32_t e
 #pragma unroll
     for (uint32_t u = 0; u < kGetR; u++) {
         const uint32_t c = lane + 64 * u;
-        v[u] = c < a.B ? row[c] : 0u;
+        v[u] = c < a.B ? at(c) : 0u;
         f[u] = hb && c < a.B ? a.branch_first[c] : 0u;
     }
 #pragma unroll
@@ -224,7 +232,7 @@ __device__ __forceinline__ void get_row(const GetArgs &a, uint32_t i, uint32_t e
     for (uint32_t u = 0; u < kGetR; u++)
         if (v[u]) last = (int)(lane + 64 * u);
     for (uint32_t c = lane + 64 * kGetR; c < lim; c += 64)   // rows wider than 1024 columns
-        if (row[c]) last = (int)c;
+        if (at(c)) last = (int)c;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) last = max(last, __shfl_xor(last, off, 64));
     const uint32_t ent = max(bb, (uint32_t)(last + 1));
@@ -243,7 +251,7 @@ __device__ __forceinline__ void get_row(const GetArgs &a, uint32_t i, uint32_t e
 #pragma unroll
         for (uint32_t u = 0; u < kGetR; u++) {
             const uint32_t c = c0 + lane + 64 * u;
-            v[u] = c < lim ? row[c] : 0u;
+            v[u] = c < lim ? at(c) : 0u;
             f[u] = hb && c < lim ? a.branch_first[c] : 0u;
         }
 #pragma unroll

@@ -158,8 +158,11 @@ int rs_planes(lx_index *h, uint32_t n) {
         rs_planes_free(h);
         HIPCHK(h, dalloc(&h->rs_hb_mem, rows * h->pstride));
         HIPCHK(h, dalloc(&h->rs_la_mem, rows * h->pstride));
-        // (HB rows are rewritten whole for every branch of the epoch by the
-        // walk; LA is zeroed at the batch: a new allocation starts clean anyway)
+        // a new HB allocation is zeroed here (its pad columns past the
+        // epoch's branches are never written by the walk); the LA rows are
+        // not: rs_begin zeroes the own rows at every batch before the walk
+        // fills them.  Receive-area rows are read only where rs_lslot /
+        // rs_hslot stamp them for the current batch.
         HIPCHK(h, hipMemsetAsync(h->rs_hb_mem, 0, rows * h->pstride * 4, h->stream));
         h->rs_mem_rows = rows;
         h->rs_mem_pstride = h->pstride;

@@ -46,6 +46,7 @@ struct RcclApi {
     ncclResult_t (*Recv)(void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
     ncclResult_t (*AllReduce)(const void *, void *, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
                               hipStream_t) = nullptr;
+    ncclResult_t (*Broadcast)(const void *, void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
     const char *(*ErrorString)(ncclResult_t) = nullptr;
     std::string error;
     bool ok = false;
@@ -74,6 +75,7 @@ RcclApi &rccl() {
         get(api.Send, "ncclSend");
         get(api.Recv, "ncclRecv");
         get(api.AllReduce, "ncclAllReduce");
+        get(api.Broadcast, "ncclBroadcast");
         get(api.ErrorString, "ncclGetErrorString");
         api.ok = all;
         if (!all) api.error = "RCCL library lacks a required symbol";
@@ -102,6 +104,9 @@ struct lx_shard_comm {
     size_t mbuf_cap = 0;
     uint32_t *part = nullptr;                    // FC partial sums, grown on demand
     uint64_t part_cap = 0;
+    uint8_t *ebuf = nullptr;                     // FC early exit: mask, idx, a, b, partials (grown on demand)
+    size_t ecap = 0;
+    uint64_t last_undecided = 0;                 // FC early exit: queries the last call sent to every shard
     uint32_t *wdev = nullptr;                    // wire widths: [0, G) sent, [G, 2G) received
     lx::ExchangeState xs;                        // byte-wire fallbacks remembered per destination
     bool rowseg = false;                         // a row-segment rank (lx_rowseg_comm_create)
@@ -223,10 +228,17 @@ void lx_shard_comm_destroy(lx_shard_comm *c) {
     (void)hipFree(c->recv);
     (void)hipFree(c->mbuf);
     (void)hipFree(c->part);
+    (void)hipFree(c->ebuf);
     (void)hipFree(c->wdev);
     for (uint8_t *p : c->rbuf) (void)hipFree(p);
     (void)hipFree(c->udev);
     delete c;
+}
+
+int lx_shard_fc_undecided(const lx_shard_comm *c, uint64_t *undecided) {
+    if (!c || !undecided) return LX_ERR_ARG;
+    *undecided = c->last_undecided;
+    return 0;
 }
 
 const char *lx_shard_comm_last_error(const lx_shard_comm *c) {
@@ -337,6 +349,10 @@ int lx_shard_exchange_layout(uint32_t G, uint32_t self, const uint64_t *entries,
     return 0;
 }
 
+// the early exit's fixed cost (a broadcast, a scan, a host round trip) pays
+// from this many queries on (smaller calls: the FC cache's fills, one pair)
+constexpr uint64_t kShardEarlyMin = 1ull << 14;
+
 int lx_forkless_cause_sharded_dev(lx_shard_comm *c, uint64_t n, const uint32_t *a, const uint32_t *b, uint8_t *out) {
     if (!c || (n && (!a || !b || !out))) return LX_ERR_ARG;
     if (c->rowseg) return c->fail(LX_ERR_STATE, "row segments answer ForklessCause through the index");
@@ -352,10 +368,58 @@ int lx_forkless_cause_sharded_dev(lx_shard_comm *c, uint64_t n, const uint32_t *
         c->part = reinterpret_cast<uint32_t *>(p);
         c->part_cap = n;
     }
+    if (n >= kShardEarlyMin && lx_fc_shard_early(c->ix, nullptr)) {
+        // early exit: shard 0 decides most queries alone, the
+        // others add partials for the rest only
+        const uint64_t W = (n + 63) / 64;
+        LXC(c->grow(&c->ebuf, &c->ecap, 16 * W + 16 * n));
+        uint64_t *mask = reinterpret_cast<uint64_t *>(c->ebuf);
+        uint32_t *idx = reinterpret_cast<uint32_t *>(c->ebuf + 16 * W);
+        uint32_t *a2 = idx + n, *b2 = a2 + n, *p2 = b2 + n;
+        const bool s0 = c->rank == 0;
+        if (s0) {
+            LXC(c->index(lx_forkless_cause_partial_dev(c->ix, n, a, b, c->part, nullptr), "lx_forkless_cause_partial_dev"));
+            LXC(c->index(lx_fc_shard_decide_dev(c->ix, n, c->part, mask, nullptr), "lx_fc_shard_decide_dev"));
+        }
+        LXC(c->nccl(api.Broadcast(mask, mask, 2 * W, ncclUint64, 0, c->comm, c->stream), "ncclBroadcast"));
+        LXC(c->hip(hipStreamSynchronize(c->stream), "hipStreamSynchronize"));
+        uint64_t m = 0;
+        LXC(c->index(lx_fc_shard_undecided_dev(c->ix, n, mask, a, b, s0 ? c->part : nullptr, idx, a2, b2,
+                                               s0 ? p2 : nullptr, &m), "lx_fc_shard_undecided_dev"));
+        c->last_undecided = m;
+        if (m) {
+            if (!s0) LXC(c->index(lx_forkless_cause_partial_dev(c->ix, m, a2, b2, p2, nullptr), "lx_forkless_cause_partial_dev"));
+            LXC(c->nccl(api.AllReduce(p2, p2, m, ncclUint32, ncclSum, c->comm, c->stream), "ncclAllReduce"));
+        }
+        LXC(c->index(lx_fc_shard_answer_dev(c->ix, n, mask, m, idx, p2, out, nullptr), "lx_fc_shard_answer_dev"));
+        return 0;
+    }
+    c->last_undecided = n;
     LXC(c->index(lx_forkless_cause_partial_dev(c->ix, n, a, b, c->part, nullptr), "lx_forkless_cause_partial_dev"));
     LXC(c->nccl(api.AllReduce(c->part, c->part, n, ncclUint32, ncclSum, c->comm, c->stream), "ncclAllReduce"));
     LXC(c->index(lx_fc_combine_dev(c->ix, n, c->part, out, nullptr), "lx_fc_combine_dev"));
     return 0;
+}
+
+int lx_shard_get_rows(lx_shard_comm *c, uint32_t mode, uint64_t n, const uint32_t *ev, uint8_t *out, uint64_t slot,
+                      uint32_t *len) {
+    if (!c || mode > 2 || (n && (!ev || !out || !len))) return LX_ERR_ARG;
+    if (c->rowseg) return c->fail(LX_ERR_STATE, "row segments route their getters (lx_rowseg_get_rows)");
+    if (n > 0xFFFFFFFFull) return c->fail(LX_ERR_ARG, "too many rows in one call");
+    if (n && (slot < 8ull * std::max(c->ix->B, c->ix->V) || slot % 16))
+        return c->fail(LX_ERR_ARG, "row slot of %llu bytes: needs >= %llu and a multiple of 16",
+                       (unsigned long long)slot, 8ull * std::max(c->ix->B, c->ix->V));
+    if (!n) return 0;
+    RcclApi &api = rccl();
+    LXC(c->hip(hipSetDevice(c->device), "hipSetDevice"));
+    // this shard's branches, zeros elsewhere (completed on return) ...
+    LXC(c->index(lx_get_rows_dev(c->ix, mode, (uint32_t)n, ev, out, slot, len), "lx_get_rows_dev"));
+    if (c->nranks == 1) return 0;
+    // ... summed word by word over the shards (each word has one writer), and
+    // the longest length any shard's entries imply
+    LXC(c->nccl(api.AllReduce(out, out, n * slot / 4, ncclUint32, ncclSum, c->comm, c->stream), "ncclAllReduce"));
+    LXC(c->nccl(api.AllReduce(len, len, n, ncclUint32, ncclMax, c->comm, c->stream), "ncclAllReduce"));
+    return c->hip(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
 }
 
 // ---- row segments: the driver of lx_rowseg_exchange.h over the rowseg ABI

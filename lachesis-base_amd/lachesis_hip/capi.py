@@ -41,6 +41,10 @@ SIGNATURES = [
                                             ctypes.POINTER(ctypes.c_uint64)]),
     ("lx_forkless_cause_partial_dev", ctypes.c_int, [vp, ctypes.c_uint64, vp, vp, vp, vp]),
     ("lx_fc_combine_dev", ctypes.c_int, [vp, ctypes.c_uint64, vp, vp, vp]),
+    ("lx_fc_shard_early", ctypes.c_int, [vp, u32p]),
+    ("lx_fc_shard_decide_dev", ctypes.c_int, [vp, ctypes.c_uint64, vp, vp, vp]),
+    ("lx_fc_shard_undecided_dev", ctypes.c_int, [vp, ctypes.c_uint64, vp, vp, vp, vp, vp, vp, vp, vp, u64p]),
+    ("lx_fc_shard_answer_dev", ctypes.c_int, [vp, ctypes.c_uint64, vp, ctypes.c_uint64, vp, vp, vp, vp]),
     ("lx_quorum", ctypes.c_uint32, [vp]),
     ("lx_get_highest_before", ctypes.c_int, [vp, ctypes.c_uint32, u8p, ctypes.c_uint32, u32p]),
     ("lx_get_lowest_after", ctypes.c_int, [vp, ctypes.c_uint32, u8p, ctypes.c_uint32, u32p]),
@@ -72,6 +76,7 @@ SIGNATURES = [
     ("lx_la_pack_wire_dev", ctypes.c_int, [vp, ctypes.c_uint32, vp, ctypes.c_uint32]),
     ("lx_la_unpack_wire_dev", ctypes.c_int, [vp, ctypes.c_uint32, vp, ctypes.c_uint32]),
     ("lx_last_stats", ctypes.c_int, [vp, vp]),
+    ("lx_last_walk_clock", ctypes.c_int, [vp, vp]),
     ("lx_last_segment_stats", ctypes.c_int, [vp, vp]),
     ("lx_rowseg_range", ctypes.c_int, [vp, u32p, u32p]),
     ("lx_rowseg_bounds", ctypes.c_int, [vp, u32p]),
@@ -102,6 +107,8 @@ SIGNATURES = [
     ("lx_rowseg_exchange", ctypes.c_int, [vp, u64p]),
     ("lx_shard_exchange_layout", ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint32, u64p, u32p, u64p]),
     ("lx_forkless_cause_sharded_dev", ctypes.c_int, [vp, ctypes.c_uint64, vp, vp, vp]),
+    ("lx_shard_fc_undecided", ctypes.c_int, [vp, u64p]),
+    ("lx_shard_get_rows", ctypes.c_int, [vp, ctypes.c_uint32, ctypes.c_uint64, vp, vp, ctypes.c_uint64, vp]),
     # include/lachesis_abft.h
     ("lx_abft_create", ctypes.c_int, [vp, ctypes.POINTER(vp)]),
     ("lx_abft_destroy", None, [vp]),
@@ -397,6 +404,27 @@ class Index:
     def fc_combine_dev(self, n, sum_ptr, out_ptr, stream=None):
         self._chk(self.L.lx_fc_combine_dev(self.h, n, sum_ptr, out_ptr, stream))
 
+    # ---- column-shard early exit (include/lachesis_hip.h lx_fc_shard_*)
+    def fc_shard_early(self):
+        """(applies, rest): whether shard 0 can decide queries alone on this
+        epoch, and the stake of the other shards."""
+        rest = ctypes.c_uint32()
+        ok = self.L.lx_fc_shard_early(self.h, ctypes.byref(rest))
+        return bool(ok), rest.value
+
+    def fc_shard_decide_dev(self, n, partial_ptr, mask_ptr, stream=None):
+        self._chk(self.L.lx_fc_shard_decide_dev(self.h, n, partial_ptr, mask_ptr, stream))
+
+    def fc_shard_undecided_dev(self, n, mask_ptr, a_ptr, b_ptr, partial_ptr, idx_ptr, a_out, b_out, p_out):
+        """The undecided queries compacted in query order; returns their count."""
+        m = ctypes.c_uint64()
+        self._chk(self.L.lx_fc_shard_undecided_dev(self.h, n, mask_ptr, a_ptr, b_ptr, partial_ptr, idx_ptr, a_out, b_out,
+                                                   p_out, ctypes.byref(m)))
+        return m.value
+
+    def fc_shard_answer_dev(self, n, mask_ptr, m, idx_ptr, sum_ptr, out_ptr, stream=None):
+        self._chk(self.L.lx_fc_shard_answer_dev(self.h, n, mask_ptr, m, idx_ptr, sum_ptr, out_ptr, stream))
+
     def sync(self):
         self._chk(self.L.lx_sync(self.h))
 
@@ -524,6 +552,13 @@ class Index:
         st = LxStats()
         self._chk(self.L.lx_last_stats(self.h, ctypes.byref(st)))
         return {"ms_assign": st.ms_assign, "ms_index": st.ms_index, "ms_marks": st.ms_marks}
+
+    def walk_clock(self):
+        """Shader clock of the last walk (lx_last_walk_clock): median / min / max
+        MHz over its workgroups and the median workgroup's walk in ms."""
+        out = (ctypes.c_float * 4)()
+        self._chk(self.L.lx_last_walk_clock(self.h, out))
+        return {"mhz_median": out[0], "mhz_min": out[1], "mhz_max": out[2], "walk_ms": out[3]}
 
     # ---- row-segment rank (options seg_count / seg_rank; lachesis_hip.rowseg drives the exchange)
     def rowseg_range(self):
@@ -660,6 +695,16 @@ class ShardComm:
 
     def forkless_cause_dev(self, n, a_ptr, b_ptr, out_ptr):
         self._chk(self.L.lx_forkless_cause_sharded_dev(self.c, n, a_ptr, b_ptr, out_ptr))
+
+    def fc_undecided(self):
+        """Queries the last forkless_cause_dev sent to every shard (lx_shard_fc_undecided)."""
+        u = ctypes.c_uint64()
+        self._chk(self.L.lx_shard_fc_undecided(self.c, ctypes.byref(u)))
+        return u.value
+
+    def get_rows_dev(self, mode, n, ev_ptr, out_ptr, slot_bytes, len_ptr):
+        """Whole vector getter rows on column shards (lx_shard_get_rows, collective)."""
+        self._chk(self.L.lx_shard_get_rows(self.c, mode, n, ev_ptr, out_ptr, slot_bytes, len_ptr))
 
     def close(self):
         if self.c:

@@ -199,22 +199,186 @@ class ShardedIndex:
             self._bufs[name] = cur
         return cur
 
+    def all_reduce_max(self, t):
+        if self.stage:
+            h = t.cpu()
+            dist.all_reduce(h, op=dist.ReduceOp.MAX, group=self.group)
+            t.copy_(h)
+        else:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+
+    def broadcast0(self, t):
+        """Rank 0's tensor to every rank (in place)."""
+        if self.stage:
+            h = t.cpu()
+            dist.broadcast(h, 0, group=self.group)
+            t.copy_(h)
+        else:
+            dist.broadcast(t, 0, group=self.group)
+
     # ------------------------------------------------------------------ FC
-    def forkless_cause_dev(self, a, b, out=None):
-        """ForklessCause for device int32 index tensors ``a``, ``b`` -> uint8 tensor."""
+    EARLY_MIN = 1 << 14   # csrc/lx_shard_rccl.cpp kShardEarlyMin: smaller calls keep one pass
+
+    def forkless_cause_dev(self, a, b, out=None, early=None):
+        """ForklessCause for device int32 index tensors ``a``, ``b`` -> uint8 tensor.
+
+        Calls of >= EARLY_MIN queries on epochs where shard 0 can decide alone
+        (lx_fc_shard_early: fork-free, shard 0's heaviest creators) take the
+        early exit: shard 0 sums its creators' stake for every
+        query and decides those whose sum reaches the quorum or cannot reach it
+        with the other shards' stake added; its decisions are broadcast and
+        only the undecided queries get the other shards' partials and the
+        all-reduce.  ``early``: None (auto), False (always one pass)."""
         n = a.numel()
-        part = torch.empty(n, dtype=torch.int32, device=self.device)
-        self.ix.forkless_cause_partial_dev(n, a.data_ptr(), b.data_ptr(), part.data_ptr())
-        self.ix.sync()
-        # partials are uint32 (stake sum < 2^31 plus at most one bit-31 mark, from
-        # the rank owning branch(b)); the true total fits 32 bits, so the int32
-        # wrap-around sum of the all-reduce is exact
-        self.all_reduce_sum(part)   # (one rank: the identity, through the same collective)
-        if self.device.type == "cuda":
-            torch.cuda.current_stream(self.device).synchronize()
-        s32 = part
         if out is None:
             out = torch.empty(n, dtype=torch.uint8, device=self.device)
-        self.ix.fc_combine_dev(n, s32.data_ptr(), out.data_ptr())
+        ok = False
+        if early is not False and n >= self.EARLY_MIN and self.world > 1 and hasattr(self.ix, "fc_shard_early"):
+            ok = self.ix.fc_shard_early()[0]
+        if not ok:
+            part = self._buf("fc_part", 4 * n).view(torch.int32)[:n]
+            self.ix.forkless_cause_partial_dev(n, a.data_ptr(), b.data_ptr(), part.data_ptr())
+            self.ix.sync()
+            # partials are uint32 (stake sum < 2^31 plus at most one bit-31 mark, from
+            # the rank owning branch(b)); the true total fits 32 bits, so the int32
+            # wrap-around sum of the all-reduce is exact
+            self.all_reduce_sum(part)   # (one rank: the identity, through the same collective)
+            if self.device.type == "cuda":
+                torch.cuda.current_stream(self.device).synchronize()
+            self.ix.fc_combine_dev(n, part.data_ptr(), out.data_ptr())
+            self.ix.sync()
+            self.last_fc = {"n": n, "undecided": n, "early": False}
+            return out
+        W = (n + 63) // 64
+        mask = self._buf("fc_mask", 16 * W).view(torch.int64)[:2 * W]
+        q = self._buf("fc_q", 16 * n).view(torch.int32)
+        idx, a2, b2, p2 = q[:n], q[n:2 * n], q[2 * n:3 * n], q[3 * n:4 * n]
+        s0 = self.rank == 0
+        part = None
+        if s0:
+            part = self._buf("fc_part", 4 * n).view(torch.int32)[:n]
+            self.ix.forkless_cause_partial_dev(n, a.data_ptr(), b.data_ptr(), part.data_ptr())
+            self.ix.fc_shard_decide_dev(n, part.data_ptr(), mask.data_ptr())
         self.ix.sync()
+        self.broadcast0(mask)
+        if self.device.type == "cuda":
+            torch.cuda.current_stream(self.device).synchronize()
+        m = self.ix.fc_shard_undecided_dev(n, mask.data_ptr(), a.data_ptr(), b.data_ptr(),
+                                           part.data_ptr() if s0 else None, idx.data_ptr(), a2.data_ptr(),
+                                           b2.data_ptr(), p2.data_ptr() if s0 else None)
+        if m:
+            if not s0:
+                self.ix.forkless_cause_partial_dev(m, a2.data_ptr(), b2.data_ptr(), p2.data_ptr())
+                self.ix.sync()
+            self.all_reduce_sum(p2[:m])
+            if self.device.type == "cuda":
+                torch.cuda.current_stream(self.device).synchronize()
+        self.ix.fc_shard_answer_dev(n, mask.data_ptr(), m, idx.data_ptr(), p2.data_ptr(), out.data_ptr())
+        self.ix.sync()
+        self.last_fc = {"n": n, "undecided": m, "early": True}
         return out
+
+    # ------------------------------------------------------------------ getters
+    def get_rows_dev(self, mode, n, ev):
+        """Whole vector getter rows (mode 0 HighestBefore, 1 LowestAfter, 2
+        merged HighestBefore; reference byte layouts) of n device int32 event
+        ids, collectively with every rank (the same ids): each rank encodes its
+        own branches (lx_get_rows_dev on a shard: zeros elsewhere), a sum over
+        the ranks joins them (every word has one writer) and a max gives the
+        length.  LowestAfter needs the exchange since the last Add.  Returns
+        (rows uint8 [n, slot] on the device, lengths int64 [n]; 0xFFFFFFFF: not
+        an event of the epoch)."""
+        slot = (self.ix.row_bytes_max() + 15) // 16 * 16
+        words = slot // 4
+        rows = self._buf("g_rows", 4 * n * words).view(torch.int32)[:n * words]
+        lens = self._buf("g_lens", 4 * n).view(torch.int32)[:n]
+        self.ix.get_rows_dev(mode, n, ev.data_ptr(), rows.data_ptr(), slot, lens.data_ptr())
+        self.all_reduce_sum(rows)
+        ln = lens.long() & 0xFFFFFFFF           # (int32 max would order 0xFFFFFFFF below every length)
+        self.all_reduce_max(ln)
+        if self.device.type == "cuda":
+            torch.cuda.current_stream(self.device).synchronize()
+        return rows.view(torch.uint8).view(n, slot).clone(), ln
+
+    def get_rows(self, mode, events):
+        """get_rows_dev from host event ids: a list of byte rows (None for an
+        event outside the epoch)."""
+        import numpy as np
+        ev = torch.from_numpy(np.ascontiguousarray(events, dtype=np.uint32).view(np.int32)).to(self.device)
+        rows, lens = self.get_rows_dev(mode, len(events), ev)
+        rows, lens = rows.cpu().numpy(), lens.cpu().numpy()
+        return [None if int(k) == 0xFFFFFFFF else bytes(rows[i, :int(k)]) for i, k in enumerate(lens)]
+
+
+class ShardedDagIndexer:
+    """abft.DagIndexer (vecfc.Index's surface as abft/indexed_lachesis.go:17-99
+    and abft/lachesis.go:56-57 use it) over a column-sharded index: every rank
+    runs the same caller on the same events, and each call here is collective.
+
+    add / flush / drop_not_flushed go to this rank's shard handle (each indexes
+    every event, its own creators' columns); forkless_cause runs the LowestAfter
+    exchange when an Add changed the LowestAfter rows since the last one, then
+    the partial sums and their all-reduce; get_merged_highest_before joins the
+    shards' rows (creators are shard-local, so every shard encodes its own
+    creators' merged entries).  Event ids map to dense indices in Add order,
+    as the cgo shim keeps them."""
+
+    def __init__(self, sharded):
+        self.sx = sharded
+        self.ix = sharded.ix
+        self.validators = None
+
+    def reset(self, validators, get_event=None):
+        self.validators = validators
+        self.ix.reset(list(validators.weights))
+        self.pos, self.ids, self.n_flushed = {}, [], 0
+        self._stale = False
+
+    def add(self, e):
+        ps = []
+        for p in e.parents:    # self-parent first, as dag.Event keeps them
+            if p not in self.pos:
+                raise ValueError("processed out of order, parent not found")   # vecengine/index.go:159-161
+            ps.append(self.pos[p])
+        self.ix.add(self.validators.idxs[e.creator], e.seq, ps)
+        self.pos[e.id] = len(self.ids)
+        self.ids.append(e.id)
+        self._stale = True
+
+    def flush(self):
+        self.ix.flush()
+        self.n_flushed = len(self.ids)
+
+    def drop_not_flushed(self):
+        if len(self.ids) == self.n_flushed:
+            return
+        self.ix.drop_not_flushed()
+        for eid in self.ids[self.n_flushed:]:
+            del self.pos[eid]
+        del self.ids[self.n_flushed:]
+        self._stale = True
+
+    def _fresh(self):
+        if self._stale:
+            self.sx.exchange()
+            self._stale = False
+
+    def forkless_cause(self, a, b):
+        self._fresh()
+        d = self.sx.device
+        qa = torch.tensor([self.pos[a]], dtype=torch.int32, device=d)
+        qb = torch.tensor([self.pos[b]], dtype=torch.int32, device=d)
+        return bool(self.sx.forkless_cause_dev(qa, qb, early=False).cpu()[0])
+
+    def get_merged_highest_before(self, eid):
+        from .vecfc import HighestBeforeSeq
+        return HighestBeforeSeq(self.sx.get_rows(2, [self.pos[eid]])[0])
+
+    def get_highest_before(self, eid):
+        from .vecfc import HighestBeforeSeq
+        return HighestBeforeSeq(self.sx.get_rows(0, [self.pos[eid]])[0])
+
+    def get_lowest_after(self, eid):
+        from .vecfc import LowestAfterSeq
+        self._fresh()
+        return LowestAfterSeq(self.sx.get_rows(1, [self.pos[eid]])[0])

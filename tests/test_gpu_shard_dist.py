@@ -43,6 +43,10 @@ def _worker(rank, world, port, q, kind="tdag"):
         if kind == "skewed":
             d = _skewed_dag()
             weights = [1] * 8
+        elif kind == "early":
+            # Zipf stakes: shard 0 (the heaviest creators) decides most queries alone
+            d = lx.tools.gen_dag(240, 30, 8, seed=11)
+            weights = [(1 << 20) // (i + 1) for i in range(240)]
         else:
             d = lx.tools.gen_dag(28, 40, 6, 5, 6, 3)
             rng = np.random.default_rng(3)
@@ -61,8 +65,14 @@ def _worker(rank, world, port, q, kind="tdag"):
         else:
             assert set(w for w in si.last_wire[0] if w) == {1}              # balanced DAG: byte wire
             qa, qb = lx.tools.fc_queries(d.lamport, 30_000, window=30, seed=5)
-        out = si.forkless_cause_dev(torch.from_numpy(qa.view(np.int32)).to(dev),
-                                    torch.from_numpy(qb.view(np.int32)).to(dev)).cpu().numpy()
+        ta, tb = torch.from_numpy(qa.view(np.int32)).to(dev), torch.from_numpy(qb.view(np.int32)).to(dev)
+        out = si.forkless_cause_dev(ta, tb).cpu().numpy()
+        if kind == "early":
+            # the early exit ran (2^14 queries or more, fork-free, Zipf) and left
+            # only the undecided queries to the other shards; one pass agrees
+            assert si.last_fc["early"] and 0 < si.last_fc["undecided"] < len(qa) // 3, si.last_fc
+            assert np.array_equal(out, si.forkless_cause_dev(ta, tb, early=False).cpu().numpy())
+            assert not si.last_fc["early"]
         o = corc.OracleIndex(weights)
         assert o.add_batch(d.creator, d.seq, d.poff, d.par) == -1
         q.put((rank, bool(np.array_equal(out, o.forkless_cause_batch(qa, qb))), int(out.sum())))
@@ -78,7 +88,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("world,kind", [(2, "tdag"), (3, "tdag"), (2, "skewed")])
+@pytest.mark.parametrize("world,kind", [(2, "tdag"), (3, "tdag"), (2, "skewed"), (2, "early"), (3, "early")])
 def test_sharded_index_over_torch_distributed(world, kind):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
