@@ -508,6 +508,65 @@ def dropin_leg(lx, device, want_cpu, cpu_events=4000):
     return res
 
 
+def smi_json(argv, timeout=10):
+    """amd-smi (read-only queries) as JSON, or None when it is absent or fails."""
+    import subprocess
+    try:
+        r = subprocess.run(["amd-smi"] + argv + ["--json"], capture_output=True, text=True, timeout=timeout)
+        return json.loads(r.stdout)
+    except Exception:
+        return None
+
+
+def power_probe(step, seconds=2.5):
+    """The board's socket power and GFX clocks (amd-smi metric, sampled by a
+    host thread) while the index step runs back to back for ~`seconds`,
+    untimed, after the timed steps; and the socket power limit.  The walk's
+    time is a fixed number of shader cycles over the clock the box gives it
+    (walk_clock), and the walk draws within ~15 % of the limit:
+    these samples say what the box did with its power budget."""
+    import threading
+
+    import numpy as np
+    lim = smi_json(["static", "--limit"])
+    samples, stop = [], threading.Event()
+
+    def gpu0(d):
+        return d["gpu_data"][0] if isinstance(d, dict) else d[0]
+
+    def sampler():
+        while not stop.is_set():
+            d = smi_json(["metric", "-p", "-c"])
+            try:
+                g = gpu0(d)
+                clk = [g["clock"][k]["clk"]["value"] for k in g["clock"] if k.startswith("gfx")]
+                samples.append((time.time(), float(g["power"]["socket_power"]["value"]), float(np.mean(clk))))
+            except Exception:
+                time.sleep(0.2)
+
+    th = threading.Thread(target=sampler, daemon=True)
+    th.start()
+    t_start = time.time()
+    steps = 0
+    while time.time() < t_start + seconds:
+        step()
+        steps += 1
+    t_end = time.time()
+    stop.set()
+    th.join(timeout=15)
+    s = [x for x in samples if t_start + 0.3 <= x[0] <= t_end]
+    try:
+        limit_w = float(gpu0(lim)["limit"]["ppt0"]["socket_power_limit"]["value"])
+    except Exception:
+        limit_w = None
+    if not s:
+        return {"samples": 0, "socket_power_limit_w": limit_w, "note": "amd-smi gave no samples"}
+    return {"samples": len(s), "steps": steps, "socket_power_w_mean": float(np.mean([x[1] for x in s])),
+            "socket_power_w_max": float(max(x[1] for x in s)), "smi_gfx_mhz_mean": float(np.mean([x[2] for x in s])),
+            "socket_power_limit_w": limit_w,
+            "source": "amd-smi metric -p -c (read-only) sampled during back-to-back index steps after the timed ones"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -521,6 +580,8 @@ def main():
                          "level-synchronous batcher releases the epoch (same DAG, renumbered)")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-power", action="store_true",
+                    help="skip the untimed amd-smi power / clock samples beside back-to-back index steps")
     ap.add_argument("--mode", default="rowseg", choices=["replica", "shard", "rowseg"],
                     help="N > 1: rowseg = the epoch split into N Add-order row segments, one walk per rank "
                          "(DESIGN.md 6b, the default); shard = column shards; replica = independent epochs")
@@ -685,11 +746,19 @@ def main():
         _, _, _, stream_ptr = ix.device_planes()
         lib_stream = torch.cuda.ExternalStream(stream_ptr, device=dev)
         kern_ms = []
+        shard_q = []   # column shards: queries this rank's partial-sum launch summed per step
+        proto_split = []   # row segments: (device steps, collectives) of the FC protocol per step, ms
 
         def fc_step(evs=None):
             if evs is not None:
                 evs[0].record(lib_stream)
-            if kind in ("shard", "solo"):
+            if kind == "shard":
+                # partial stake sums + all-reduce; shard 0 decides most queries
+                # alone when the epoch allows (the early exit), the
+                # other ranks sum the undecided ones only; the partial-sum
+                # launches timed inside
+                sx.forkless_cause_dev(d_qa, d_qb, d_out, timing=evs is not None)
+            elif kind == "solo":
                 ix.forkless_cause_partial_dev(args.fc_queries, d_qa.data_ptr(), d_qb.data_ptr(), d_part.data_ptr())
             elif kind == "rowseg":
                 # any pair: queries to owner(a), remote LowestAfter rows to it,
@@ -699,13 +768,12 @@ def main():
                 ix.forkless_cause_batch_dev(args.fc_queries, d_qa.data_ptr(), d_qb.data_ptr(), d_out.data_ptr())
             if evs is not None:
                 evs[1].record(lib_stream)
-            if kind == "shard":
-                ix.sync()
-                sx.all_reduce_sum(d_part)   # int32 wrap-around = exact uint32 sum
-                torch.cuda.current_stream(dev).synchronize()
-                ix.fc_combine_dev(args.fc_queries, d_part.data_ptr(), d_out.data_ptr())
             if evs is not None and kind == "rowseg":
                 kern_ms.append(rsx.last_fc["kernel_ms"])
+                proto_split.append((rsx.last_fc["device_ms"], rsx.last_fc["collective_ms"]))
+            if evs is not None and kind == "shard":
+                kern_ms.append(sx.last_fc["kernel_ms"])
+                shard_q.append(sx.last_fc["partial_queries"])
 
         # ---- index: warmup + K timed steps
         for _ in range(args.warmup):
@@ -719,6 +787,10 @@ def main():
             k_assign_ms.append(b)
         barrier()
         t_index = max_over_ranks(time.perf_counter() - t0)
+        clk_timed = list(clk_log[-args.steps:])
+        power = None
+        if kind == "single" and rank == 0 and world == 1 and not args.no_power:
+            power = power_probe(index_step)   # untimed, after the timed steps
 
         # ---- FC: warmup + K timed steps
         for _ in range(args.warmup):
@@ -736,11 +808,14 @@ def main():
         step_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
         # k_fc's own time on this rank: the launch (single / shard partial), or
         # the launch inside the row-segment protocol (the rest is routing)
-        fc_kernel_ms = float(np.mean(kern_ms)) if kind == "rowseg" else step_ms
+        fc_kernel_ms = float(np.mean(kern_ms)) if kind in ("rowseg", "shard") else step_ms
         early = ix.fc_early_rounds()
         # the queries this rank's k_fc answered per step: its own, or (row
         # segments) the ones routed to it as owner(a)
         nq = rsx.last_fc["answered"] if kind == "rowseg" else args.fc_queries
+        if kind == "shard":
+            # shard 0 sums every query, the others the undecided ones (early exit)
+            nq = float(np.mean(shard_q))
         B = ix.num_branches()
         if kind in ("shard", "solo"):
             lo_c, hi_c = ix.shard_range(rank if kind == "shard" else 0)
@@ -760,9 +835,10 @@ def main():
                          "whole_rows": int(early_all[3]), "answered": int(nq_all) * args.steps}
                if early_all[0] else None,
                "whole_row_bytes": 8.0 * B * nq, "st_x": st_x,
-               "mem": ix.device_bytes(), "clk": clk_log[-args.steps:]}
+               "mem": ix.device_bytes(), "clk": clk_timed, "power": power}
         if kind == "rowseg":
             out["rsx"] = rsx
+            out["proto_split"] = proto_split
         if kind == "shard":
             out["sx"] = sx
         return out
@@ -873,6 +949,7 @@ def main():
         "fc_ms_per_step": t_fc / args.steps * 1e3,
         "index_kernel_ms": kidx,
         "walk_clock": walk_clock_summary(P["clk"]),
+        "walk_power": P["power"],
         "assign_and_marks_ms": float(np.mean(k_assign_ms)),
         "roofline": {"bound": "hbm", "kernel": fc_kernel_name, "achieved": fc_achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": fc_achieved / HBM_PEAK_GBS,
@@ -927,6 +1004,14 @@ def main():
                             "exchange": rsx.last, "fc": rsx.last_fc,
                             "fc_kernel_ms": fc_kernel_ms, "fc_protocol_ms": P["fc_step_ms"] - fc_kernel_ms,
                             "fc_step_ms": P["fc_step_ms"],
+                            # the routing protocol split (rank 0, mean per step): the library's
+                            # device steps (route, need, serve, store, unroute -- each completed
+                            # on return) and the collectives between them (gloo staging on a
+                            # shared-GPU rehearsal, RCCL over xGMI on the driver's node)
+                            "fc_protocol_device_ms": float(np.mean([d for d, _ in P["proto_split"]]))
+                            if P["proto_split"] else None,
+                            "fc_protocol_collective_ms": float(np.mean([c for _, c in P["proto_split"]]))
+                            if P["proto_split"] else None,
                             "device_bytes": P["mem"],
                             "note": "index step = assignment of every event + walk of the own segment + row "
                                     "requests, partial fix-up, LowestAfter pass and triples (exchange_ms), timed "
@@ -961,11 +1046,14 @@ def main():
                          "bytes_read_per_launch": C["fc_read"], "algorithmic_bytes_per_launch": C["whole_row_bytes"],
                          "kernel_ms": C["fc_kernel_ms"], "kernel_ms_max_over_ranks": C["fc_kernel_ms_max"]},
             "device_bytes": C["mem"],
+            "fc_early": {k: v for k, v in getattr(sx, "last_fc", {}).items() if k != "kernel_ms"},
             "scaling": "strong",
             "note": "the epoch's creator columns split over the ranks (DESIGN.md 6): each rank walks its columns of "
                     "every event, the LowestAfter all-to-all makes the shards FC-ready (inside events_per_sec), FC "
                     "sums the ranks' partial stakes with an all-reduce (inside fc_queries_per_sec); every rank "
-                    "answers the same 2^k queries"}
+                    "answers the same 2^k queries; shard 0 decides most of them alone on Zipf stakes (DESIGN.md 6f: the "
+                    "others sum and all-reduce the undecided ones only), so bytes_read_per_launch sums rank 0's whole "
+                    "pass and the others' undecided queries"}
         cx.close()
         ix = cx
 

@@ -727,6 +727,7 @@ int add_batch_dev(lx_index *h, uint32_t n, const uint32_t *creator, const uint32
     ia.mask = (h->B > h->V) ? 1u : 0u;
     ia.cpw_hint = h->cpw_hint;
     ia.pack16 = h->pack16 && h->max_seq <= 0xFFFFu;
+    ia.seg_xmap = h->seg_xmap_opt ? 1u : 0u;
     if (ia.cpw_hint >= 8 && (!ia.pack16 || ia.mask)) ia.cpw_hint = 4;   // 8- / 12-column slots: packed, fork-free
     const size_t prof_n = (size_t)kProfBlocks * kProfWaves * kProfSlots;
     if (!h->d_clk) {
@@ -1877,6 +1878,8 @@ int lx_set_option(lx_index *h, const char *name, int64_t value) {
         h->pack16 = value != 0;
     } else if (k == "crec") {
         h->crec_opt = value != 0;
+    } else if (k == "seg_xmap") {
+        h->seg_xmap_opt = value != 0;
     } else if (k == "dbl") {
         h->dbl = value != 0;
     } else if (k == "seg_auto") {

@@ -97,6 +97,13 @@ struct IndexArgs {
     uint32_t seg_g;
     uint32_t seg_B;
     uint32_t seg_lo[kSegLaunchMax + 1];
+    // 12-column side-by-side walks: workgroup -> (walk << 8 | slice), 0xFFFF
+    // idle, for workgroups < seg_map_n (launch_index fills it when option
+    // seg_xmap is on: every 128-B HB line written by workgroups of one XCD);
+    // seg_map_n = 0: seg_chunk's mapping
+    uint32_t seg_xmap;           // option seg_xmap (lx_set_option)
+    uint32_t seg_map_n;
+    uint16_t seg_map[256];
 };
 // k_dbl (lx_dbl.hip): HighestBefore by frontier doubling in one workgroup's
 // LDS, for fork-free batches with few branches

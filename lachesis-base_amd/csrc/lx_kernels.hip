@@ -12,6 +12,8 @@
 //   k_unfill/k_unclaim   : DropNotFlushed rollback (vecengine/index.go:88-96)
 #include <hipcub/hipcub.hpp>
 
+#include <vector>
+
 #include "lx_internal.h"
 
 namespace lx {
@@ -1504,7 +1506,16 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index_segs(IndexArgs a0
     wc.start();
     uint32_t k, slice;
     if constexpr (CPW == 12) {
-        if (!seg_chunk(blockIdx.x, a0.seg_g, a0.n_slices, &k, &slice)) {
+        bool ok;
+        if (a0.seg_map_n) {
+            const uint32_t m = blockIdx.x < a0.seg_map_n ? a0.seg_map[blockIdx.x] : 0xFFFFu;
+            ok = m != 0xFFFFu;
+            k = m >> 8;
+            slice = m & 0xFFu;
+        } else {
+            ok = seg_chunk(blockIdx.x, a0.seg_g, a0.n_slices, &k, &slice);
+        }
+        if (!ok) {
             wc.stop(a0.clk, false);
             return;
         }
@@ -1538,8 +1549,34 @@ static hipError_t launch_index_t(const IndexArgs &a0, hipStream_t s) {
     if constexpr (CPW >= 8) {   // packed fork-free epochs only
         if (!a.pack16 || a.mask) return hipErrorInvalidValue;
         // (12 columns: at most ceil(seg_g * slices / 8) workgroups per XCD, seg_chunk)
-        const uint32_t sgrid = CPW == 12 ? 8 * (a.seg_g * (a.n_slices / 8) + (a.seg_g * (a.n_slices % 8) + 7) / 8)
-                                         : grid * a.seg_g;
+        uint32_t sgrid = CPW == 12 ? 8 * (a.seg_g * (a.n_slices / 8) + (a.seg_g * (a.n_slices % 8) + 7) / 8)
+                                   : grid * a.seg_g;
+        a.seg_map_n = 0;
+        if (CPW == 12 && a.seg_g && a.seg_xmap && a.n_slices <= 255) {
+            // option seg_xmap: groups of 8 slices (96 columns = three 128-B HB
+            // lines) stay on one XCD, so every HB line is assembled in one L2;
+            // whole groups go round-robin to the least-loaded XCD, the short
+            // last group of each walk after them
+            std::vector<std::vector<uint16_t>> xl(8);
+            auto put = [&](uint32_t k, uint32_t s0, uint32_t cnt) {
+                uint32_t x = 0;
+                for (uint32_t y = 1; y < 8; y++)
+                    if (xl[y].size() < xl[x].size()) x = y;
+                for (uint32_t s = s0; s < s0 + cnt; s++) xl[x].push_back((uint16_t)(k << 8 | s));
+            };
+            for (uint32_t k = 0; k < a.seg_g; k++)
+                for (uint32_t s0 = 0; s0 + 8 <= a.n_slices; s0 += 8) put(k, s0, 8);
+            if (a.n_slices % 8)
+                for (uint32_t k = 0; k < a.seg_g; k++) put(k, a.n_slices / 8 * 8, a.n_slices % 8);
+            size_t mx = 0;
+            for (auto &l : xl) mx = std::max(mx, l.size());
+            if (8 * mx <= 256 && 8 * mx <= sgrid + 8) {
+                a.seg_map_n = (uint32_t)(8 * mx);
+                for (uint32_t g = 0; g < a.seg_map_n; g++)
+                    a.seg_map[g] = g / 8 < xl[g % 8].size() ? xl[g % 8][g / 8] : (uint16_t)0xFFFFu;
+                sgrid = a.seg_map_n;
+            }
+        }
         // compact records when the batch wrote them (fork-free, 16-bit branches and seqs)
         if (a.crec && a.seg_g) hipLaunchKernelGGL((k_index_segs<CPW, NCW, false, true, ND, true>), dim3(sgrid), blk, 0, s, a);
         else if (a.crec) hipLaunchKernelGGL((k_index<CPW, NCW, false, true, ND, true>), dim3(grid), blk, 0, s, a);

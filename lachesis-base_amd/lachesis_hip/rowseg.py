@@ -129,43 +129,67 @@ class RowSegments:
         """ForklessCause of this rank's n queries (device tensors qa, qb of
         int32 event ids, out uint8), collectively with every rank.  With
         ``timing`` the k_fc launch over the routed pairs is bracketed by HIP
-        events on the library's stream: last_fc["kernel_ms"] (the rest of the
-        call is the routing protocol)."""
+        events on the library's stream (last_fc["kernel_ms"]), and the rest of
+        the call is split by host clocks into the library's device steps
+        (route, need, serve, store, unroute: each completed on return --
+        last_fc["device_ms"], per step in "device_steps_ms") and the
+        collectives between them (last_fc["collective_ms"])."""
+        import time
         ix, G = self.ix, self.world
+        dev_ms = {}
+        coll = [0.0]
+
+        def dstep(name, f, *a):
+            t = time.perf_counter()
+            r = f(*a)
+            dev_ms[name] = dev_ms.get(name, 0.0) + (time.perf_counter() - t) * 1e3
+            return r
+
+        def cstep(f, *a):
+            t = time.perf_counter()
+            r = f(*a)
+            coll[0] += (time.perf_counter() - t) * 1e3
+            return r
+
         ra, rb = self._buf("ra", n), self._buf("rb", n)
         perm = self._buf("perm", n)
-        send_n = ix.rowseg_fc_route(n, qa.data_ptr(), qb.data_ptr(), ra.data_ptr(), rb.data_ptr(), perm.data_ptr(), G)
-        recv_n = self._counts(send_n)
+        send_n = dstep("route", ix.rowseg_fc_route, n, qa.data_ptr(), qb.data_ptr(), ra.data_ptr(), rb.data_ptr(),
+                       perm.data_ptr(), G)
+        recv_n = cstep(self._counts, send_n)
         m = sum(recv_n)
         xa, xb = self._buf("xa", m), self._buf("xb", m)
-        self._a2a(xa[:m], ra[:n], recv_n, send_n)
-        self._a2a(xb[:m], rb[:n], recv_n, send_n)
+        cstep(self._a2a, xa[:m], ra[:n], recv_n, send_n)
+        cstep(self._a2a, xb[:m], rb[:n], recv_n, send_n)
         ids = self._buf("ids", m)
-        need_n = ix.rowseg_fc_need(m, xa.data_ptr(), xb.data_ptr(), ids.data_ptr(), max(1, m), G)
-        ask_n = self._counts(need_n)
+        need_n = dstep("need", ix.rowseg_fc_need, m, xa.data_ptr(), xb.data_ptr(), ids.data_ptr(), max(1, m), G)
+        ask_n = cstep(self._counts, need_n)
         nn, na = sum(need_n), sum(ask_n)
         W = ix.rowseg_row_words()
         asked = self._buf("asked", na)
-        self._a2a(asked[:na], ids[:nn], ask_n, need_n)
+        cstep(self._a2a, asked[:na], ids[:nn], ask_n, need_n)
         rows = self._buf("rows", na * W)
-        ix.rowseg_la_serve(na, asked.data_ptr(), rows.data_ptr())
+        dstep("serve", ix.rowseg_la_serve, na, asked.data_ptr(), rows.data_ptr())
         got = self._buf("got", nn * W)
-        self._a2a(got[:nn * W], rows[:na * W], [c * W for c in need_n], [c * W for c in ask_n])
-        ix.rowseg_la_store(nn, ids.data_ptr(), got.data_ptr())
+        cstep(self._a2a, got[:nn * W], rows[:na * W], [c * W for c in need_n], [c * W for c in ask_n])
+        dstep("store", ix.rowseg_la_store, nn, ids.data_ptr(), got.data_ptr())
         ans = self._buf("ans", m, torch.uint8)
         ev = None
         if timing:
             st = torch.cuda.ExternalStream(ix.device_planes()[3], device=self.device)
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record(st)
+        t = time.perf_counter()
         ix.forkless_cause_batch_dev(m, xa.data_ptr(), xb.data_ptr(), ans.data_ptr())
         if ev is not None:
             ev[1].record(st)
         ix.sync()
+        fc_wall = (time.perf_counter() - t) * 1e3
         back = self._buf("back", n, torch.uint8)
-        self._a2a(back[:n], ans[:m], send_n, recv_n)
-        ix.rowseg_fc_unroute(n, perm.data_ptr(), back.data_ptr(), out.data_ptr())
-        self.last_fc = {"routed_away": n - send_n[self.rank], "answered": m, "rows_received": nn, "rows_sent": na}
+        cstep(self._a2a, back[:n], ans[:m], send_n, recv_n)
+        dstep("unroute", ix.rowseg_fc_unroute, n, perm.data_ptr(), back.data_ptr(), out.data_ptr())
+        self.last_fc = {"routed_away": n - send_n[self.rank], "answered": m, "rows_received": nn, "rows_sent": na,
+                        "device_ms": sum(dev_ms.values()), "device_steps_ms": dev_ms, "collective_ms": coll[0],
+                        "fc_wall_ms": fc_wall}
         if ev is not None:
             self.last_fc["kernel_ms"] = ev[0].elapsed_time(ev[1])
         return self.last_fc

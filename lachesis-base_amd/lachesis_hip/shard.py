@@ -219,7 +219,16 @@ class ShardedIndex:
     # ------------------------------------------------------------------ FC
     EARLY_MIN = 1 << 14   # csrc/lx_shard_rccl.cpp kShardEarlyMin: smaller calls keep one pass
 
-    def forkless_cause_dev(self, a, b, out=None, early=None):
+    def _kernel_timer(self, timing):
+        """HIP events on the library's stream around the partial-sum launches
+        (kernel_ms in last_fc), or None."""
+        if not timing or self.device.type != "cuda" or not hasattr(self.ix, "device_planes"):
+            return None
+        if getattr(self, "_lib_stream", None) is None:
+            self._lib_stream = torch.cuda.ExternalStream(self.ix.device_planes()[3], device=self.device)
+        return [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)]
+
+    def forkless_cause_dev(self, a, b, out=None, early=None, timing=False):
         """ForklessCause for device int32 index tensors ``a``, ``b`` -> uint8 tensor.
 
         Calls of >= EARLY_MIN queries on epochs where shard 0 can decide alone
@@ -228,16 +237,22 @@ class ShardedIndex:
         query and decides those whose sum reaches the quorum or cannot reach it
         with the other shards' stake added; its decisions are broadcast and
         only the undecided queries get the other shards' partials and the
-        all-reduce.  ``early``: None (auto), False (always one pass)."""
+        all-reduce.  ``early``: None (auto), False (always one pass).
+        ``timing``: last_fc["kernel_ms"] = this rank's partial-sum launch(es)."""
         n = a.numel()
         if out is None:
             out = torch.empty(n, dtype=torch.uint8, device=self.device)
         ok = False
         if early is not False and n >= self.EARLY_MIN and self.world > 1 and hasattr(self.ix, "fc_shard_early"):
             ok = self.ix.fc_shard_early()[0]
+        tm = self._kernel_timer(timing)
         if not ok:
             part = self._buf("fc_part", 4 * n).view(torch.int32)[:n]
+            if tm:
+                tm[0].record(self._lib_stream)
             self.ix.forkless_cause_partial_dev(n, a.data_ptr(), b.data_ptr(), part.data_ptr())
+            if tm:
+                tm[1].record(self._lib_stream)
             self.ix.sync()
             # partials are uint32 (stake sum < 2^31 plus at most one bit-31 mark, from
             # the rank owning branch(b)); the true total fits 32 bits, so the int32
@@ -247,7 +262,9 @@ class ShardedIndex:
                 torch.cuda.current_stream(self.device).synchronize()
             self.ix.fc_combine_dev(n, part.data_ptr(), out.data_ptr())
             self.ix.sync()
-            self.last_fc = {"n": n, "undecided": n, "early": False}
+            self.last_fc = {"n": n, "undecided": n, "early": False, "partial_queries": n}
+            if tm:
+                self.last_fc["kernel_ms"] = tm[0].elapsed_time(tm[1])
             return out
         W = (n + 63) // 64
         mask = self._buf("fc_mask", 16 * W).view(torch.int64)[:2 * W]
@@ -257,7 +274,11 @@ class ShardedIndex:
         part = None
         if s0:
             part = self._buf("fc_part", 4 * n).view(torch.int32)[:n]
+            if tm:
+                tm[0].record(self._lib_stream)
             self.ix.forkless_cause_partial_dev(n, a.data_ptr(), b.data_ptr(), part.data_ptr())
+            if tm:
+                tm[1].record(self._lib_stream)
             self.ix.fc_shard_decide_dev(n, part.data_ptr(), mask.data_ptr())
         self.ix.sync()
         self.broadcast0(mask)
@@ -268,14 +289,20 @@ class ShardedIndex:
                                            b2.data_ptr(), p2.data_ptr() if s0 else None)
         if m:
             if not s0:
+                if tm:
+                    tm[0].record(self._lib_stream)
                 self.ix.forkless_cause_partial_dev(m, a2.data_ptr(), b2.data_ptr(), p2.data_ptr())
+                if tm:
+                    tm[1].record(self._lib_stream)
                 self.ix.sync()
             self.all_reduce_sum(p2[:m])
             if self.device.type == "cuda":
                 torch.cuda.current_stream(self.device).synchronize()
         self.ix.fc_shard_answer_dev(n, mask.data_ptr(), m, idx.data_ptr(), p2.data_ptr(), out.data_ptr())
         self.ix.sync()
-        self.last_fc = {"n": n, "undecided": m, "early": True}
+        self.last_fc = {"n": n, "undecided": m, "early": True, "partial_queries": n if s0 else m}
+        if tm:
+            self.last_fc["kernel_ms"] = tm[0].elapsed_time(tm[1]) if (s0 or m) else 0.0
         return out
 
     # ------------------------------------------------------------------ getters

@@ -46,6 +46,9 @@ class HighestBeforeSeq:
             return BranchSeq(0, 0)
         return BranchSeq(*struct.unpack_from("<II", self.raw, 8 * i))
 
+    def is_fork_detected(self, i):                    # vector_ops.go:31-33
+        return self.get(i).is_fork_detected()
+
     def to_bytes(self):
         return self.raw
 
