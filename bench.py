@@ -829,7 +829,7 @@ def main():
         nq_all = sum_over_ranks(float(nq))
         out = {"ix": ix, "kind": kind, "t_index": t_index, "t_fc": t_fc, "k_index_ms": k_index_ms,
                "k_assign_ms": k_assign_ms, "fc_kernel_ms": fc_kernel_ms, "fc_step_ms": step_ms, "B": B,
-               "fc_read": fc_read, "fc_achieved": fc_read_all / (fc_ms_all * 1e-3) / 1e9,
+               "fc_read": fc_read, "fc_read_all": fc_read_all, "fc_achieved": fc_read_all / (fc_ms_all * 1e-3) / 1e9,
                "fc_kernel_ms_max": max_over_ranks(fc_kernel_ms),
                "early": {"queries": int(early_all[0]), "round2": int(early_all[1]), "round3": int(early_all[2]),
                          "whole_rows": int(early_all[3]), "answered": int(nq_all) * args.steps}
@@ -853,7 +853,9 @@ def main():
             return None
         mhz = [x["mhz_median"] for x in c]
         mcyc = [x["mhz_median"] * x["walk_ms"] / 1e3 for x in c]
+        xcd = [float(np.median([x["xcd_mhz"][k] for x in c])) for k in range(8)] if "xcd_mhz" in c[0] else None
         return {"mhz_median": float(np.median(mhz)), "mhz_min_step": float(min(mhz)), "mhz_max_step": float(max(mhz)),
+                "mhz_by_xcd": xcd,
                 "mhz_min_workgroup": float(min(x["mhz_min"] for x in c)),
                 "walk_mcycles_median": float(np.median(mcyc)), "steps": len(c),
                 "source": "lx_last_walk_clock after each timed step (median over workgroups per step)"}
@@ -1043,7 +1045,9 @@ def main():
             if getattr(sx, "last_wire", None) else None,
             "roofline": {"bound": "hbm", "kernel": "k_fc partial (own columns)", "achieved": C["fc_achieved"],
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": C["fc_achieved"] / HBM_PEAK_GBS,
-                         "bytes_read_per_launch": C["fc_read"], "algorithmic_bytes_per_launch": C["whole_row_bytes"],
+                         # summed over the ranks (as the row-segment leg counts), rank 0's own beside it
+                         "bytes_read_per_launch": C["fc_read_all"], "bytes_read_per_launch_rank0": C["fc_read"],
+                         "algorithmic_bytes_per_launch": C["whole_row_bytes"] * world,
                          "kernel_ms": C["fc_kernel_ms"], "kernel_ms_max_over_ranks": C["fc_kernel_ms_max"]},
             "device_bytes": C["mem"],
             "fc_early": {k: v for k, v in getattr(sx, "last_fc", {}).items() if k != "kernel_ms"},

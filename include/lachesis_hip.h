@@ -436,10 +436,12 @@ int lx_last_stats(const lx_index *h, lx_stats *out);
 /* The shader clock of the last walk (k_index / k_index_segs): compute wave 0
  * of every workgroup stamps s_memtime (shader cycles) and s_memrealtime
  * (100 MHz) around its walk.  out[0] median, out[1] min, out[2] max clock over
- * the workgroups (MHz), out[3] the median workgroup's walk (ms).  A walk's
- * cycle count is set by the DAG; its time is cycles / clock.
- * Synchronizes the handle's stream; zeros before the first walk.  Diagnostics. */
-int lx_last_walk_clock(lx_index *h, float out[4]);
+ * the workgroups (MHz), out[3] the median workgroup's walk (ms); per XCD x
+ * (HW_REG_XCC_ID): out[4 + x] the median clock of its workgroups, out[12 + x]
+ * its slowest workgroup's walk (ms).  A walk's cycle count is set by the DAG;
+ * its time is cycles / clock.  Synchronizes the handle's
+ * stream; zeros before the first walk.  Diagnostics. */
+int lx_last_walk_clock(lx_index *h, float out[20]);
 
 /* Timings of the last segmented batch (option "segments"): per segment its
  * first event, walk time and number of "partial" events (rows that needed

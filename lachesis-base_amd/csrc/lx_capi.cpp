@@ -735,6 +735,12 @@ int add_batch_dev(lx_index *h, uint32_t n, const uint32_t *creator, const uint32
         HIPCHK(h, hipMemsetAsync(h->d_clk, 0, (1 + 3ull * kClkBlocks) * 8, s));
     }
     ia.clk = h->d_clk;
+    ia.lock_k = h->lock_k;
+    if (h->lock_k) {
+        if (!h->d_prog) HIPCHK(h, hipMalloc(&h->d_prog, 4ull * kSegLaunchMax * 256));
+        HIPCHK(h, hipMemsetAsync(h->d_prog, 0, 4ull * kSegLaunchMax * 256, s));
+        ia.prog = h->d_prog;
+    }
     if (h->prof) {
         HIPCHK(h, hipMalloc(&ia.prof, prof_n * 8));
         HIPCHK(h, hipMemsetAsync(ia.prof, 0, prof_n * 8, s));
@@ -1795,6 +1801,7 @@ void lx_destroy(lx_index *h) {
     if (h->ld_buf) (void)hipFree(h->ld_buf);
     if (h->d_fc_full) (void)hipFree(h->d_fc_full);
     if (h->d_clk) (void)hipFree(h->d_clk);
+    if (h->d_prog) (void)hipFree(h->d_prog);
     for (void *q : {(void *)h->fcs_flag, (void *)h->fcs_pos, h->fcs_tmp})
         if (q) (void)hipFree(q);
     if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -1803,29 +1810,41 @@ void lx_destroy(lx_index *h) {
 
 const char *lx_last_error(const lx_index *h) { return h ? h->err.c_str() : "null handle"; }
 
-int lx_last_walk_clock(lx_index *h, float out[4]) {
+int lx_last_walk_clock(lx_index *h, float out[20]) {
     if (!h || !out) return LX_ERR_ARG;
-    out[0] = out[1] = out[2] = out[3] = 0.0f;
+    for (int i = 0; i < 20; i++) out[i] = 0.0f;
     if (!h->d_clk) return 0;
     HIPCHK(h, set_dev(h->device));
     std::vector<unsigned long long> v(1 + 3ull * kClkBlocks);
     HIPCHK(h, hipStreamSynchronize(h->stream));
     HIPCHK(h, hipMemcpy(v.data(), h->d_clk, v.size() * 8, hipMemcpyDeviceToHost));
-    std::vector<float> mhz, ms;
+    std::vector<float> mhz, ms, xm[8], xt[8];
     const uint64_t g = std::min<uint64_t>(v[0], kClkBlocks);
     for (uint64_t b = 0; b < g; b++) {
-        const unsigned long long cyc = v[1 + 3 * b], tick = v[2 + 3 * b];
+        const unsigned long long cyc = v[1 + 3 * b], tick = v[2 + 3 * b], xcc = v[3 + 3 * b];
         if (!tick || !cyc) continue;   // a workgroup without a walk (rounding, or none of the columns)
-        mhz.push_back((float)((double)cyc / (double)tick * 100.0));
-        ms.push_back((float)((double)tick / 1e5));
+        const float f = (float)((double)cyc / (double)tick * 100.0), t = (float)((double)tick / 1e5);
+        mhz.push_back(f);
+        ms.push_back(t);
+        if (xcc < 8) {
+            xm[xcc].push_back(f);
+            xt[xcc].push_back(t);
+        }
     }
     if (mhz.empty()) return 0;
-    std::sort(mhz.begin(), mhz.end());
-    std::sort(ms.begin(), ms.end());
-    out[0] = mhz[mhz.size() / 2];
+    auto med = [](std::vector<float> &x) {
+        std::sort(x.begin(), x.end());
+        return x.empty() ? 0.0f : x[x.size() / 2];
+    };
+    out[0] = med(mhz);
     out[1] = mhz.front();
     out[2] = mhz.back();
-    out[3] = ms[ms.size() / 2];
+    out[3] = med(ms);
+    for (int x = 0; x < 8; x++) {
+        out[4 + x] = med(xm[x]);
+        std::sort(xt[x].begin(), xt[x].end());
+        out[12 + x] = xt[x].empty() ? 0.0f : xt[x].back();
+    }
     return 0;
 }
 
@@ -1880,6 +1899,9 @@ int lx_set_option(lx_index *h, const char *name, int64_t value) {
         h->crec_opt = value != 0;
     } else if (k == "seg_xmap") {
         h->seg_xmap_opt = value != 0;
+    } else if (k == "lockstep") {
+        if (value < 0 || value > 4096) return h->fail(LX_ERR_ARG, "lockstep must be 0..4096 rounds");
+        h->lock_k = (uint32_t)value;
     } else if (k == "dbl") {
         h->dbl = value != 0;
     } else if (k == "seg_auto") {

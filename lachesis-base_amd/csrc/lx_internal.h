@@ -101,6 +101,12 @@ struct IndexArgs {
     // idle, for workgroups < seg_map_n (launch_index fills it when option
     // seg_xmap is on: every 128-B HB line written by workgroups of one XCD);
     // seg_map_n = 0: seg_chunk's mapping
+    // lockstep (option lockstep = K rounds; 12-column side-by-side walks): the
+    // loader of a slice issues no record round more than K rounds past the
+    // walk's slowest slice as it last read them; prog = the walk's per-slice
+    // issued-round counts (k_index_segs: kSegLaunchMax x 256, zeroed per launch)
+    uint32_t *prog;
+    uint32_t lock_k;
     uint32_t seg_xmap;           // option seg_xmap (lx_set_option)
     uint32_t seg_map_n;
     uint16_t seg_map[256];

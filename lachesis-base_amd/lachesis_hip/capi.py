@@ -555,10 +555,13 @@ class Index:
 
     def walk_clock(self):
         """Shader clock of the last walk (lx_last_walk_clock): median / min / max
-        MHz over its workgroups and the median workgroup's walk in ms."""
-        out = (ctypes.c_float * 4)()
+        MHz over its workgroups, the median workgroup's walk in ms, and per XCD
+        the median clock and the slowest workgroup's walk."""
+        out = (ctypes.c_float * 20)()
         self._chk(self.L.lx_last_walk_clock(self.h, out))
-        return {"mhz_median": out[0], "mhz_min": out[1], "mhz_max": out[2], "walk_ms": out[3]}
+        return {"mhz_median": out[0], "mhz_min": out[1], "mhz_max": out[2], "walk_ms": out[3],
+                "xcd_mhz": [round(out[4 + x], 1) for x in range(8)],
+                "xcd_walk_ms_max": [round(out[12 + x], 2) for x in range(8)]}
 
     # ---- row-segment rank (options seg_count / seg_rank; lachesis_hip.rowseg drives the exchange)
     def rowseg_range(self):

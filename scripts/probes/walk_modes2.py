@@ -60,7 +60,7 @@ for inst in range(n_inst):
         elif os.environ.get("WM_SHIPCLK") == "1":
             # the shipped walker's own clock record (lx_last_walk_clock)
             c = ix.walk_clock()
-            clks.append({k: round(v, 2) for k, v in c.items()} | {"t": round(time.time(), 3)})
+            clks.append({k: (round(v, 2) if isinstance(v, float) else v) for k, v in c.items()} | {"t": round(time.time(), 3)})
     print(json.dumps({"lib": lib, "pid": os.getpid(), "inst": inst, "walk_ms": walks,
                       "hb": hex(hb_ptr or 0), "la": hex(la_ptr or 0), "partial": st["partial"],
                       **({"clk": clks} if clks else {})}), flush=True)
