@@ -735,12 +735,6 @@ int add_batch_dev(lx_index *h, uint32_t n, const uint32_t *creator, const uint32
         HIPCHK(h, hipMemsetAsync(h->d_clk, 0, (1 + 3ull * kClkBlocks) * 8, s));
     }
     ia.clk = h->d_clk;
-    ia.lock_k = h->lock_k;
-    if (h->lock_k) {
-        if (!h->d_prog) HIPCHK(h, hipMalloc(&h->d_prog, 4ull * kSegLaunchMax * 256));
-        HIPCHK(h, hipMemsetAsync(h->d_prog, 0, 4ull * kSegLaunchMax * 256, s));
-        ia.prog = h->d_prog;
-    }
     if (h->prof) {
         HIPCHK(h, hipMalloc(&ia.prof, prof_n * 8));
         HIPCHK(h, hipMemsetAsync(ia.prof, 0, prof_n * 8, s));
@@ -1801,7 +1795,6 @@ void lx_destroy(lx_index *h) {
     if (h->ld_buf) (void)hipFree(h->ld_buf);
     if (h->d_fc_full) (void)hipFree(h->d_fc_full);
     if (h->d_clk) (void)hipFree(h->d_clk);
-    if (h->d_prog) (void)hipFree(h->d_prog);
     for (void *q : {(void *)h->fcs_flag, (void *)h->fcs_pos, h->fcs_tmp})
         if (q) (void)hipFree(q);
     if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -1899,9 +1892,6 @@ int lx_set_option(lx_index *h, const char *name, int64_t value) {
         h->crec_opt = value != 0;
     } else if (k == "seg_xmap") {
         h->seg_xmap_opt = value != 0;
-    } else if (k == "lockstep") {
-        if (value < 0 || value > 4096) return h->fail(LX_ERR_ARG, "lockstep must be 0..4096 rounds");
-        h->lock_k = (uint32_t)value;
     } else if (k == "dbl") {
         h->dbl = value != 0;
     } else if (k == "seg_auto") {

@@ -708,16 +708,6 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
 #endif
         const char *recb = CR ? reinterpret_cast<const char *>(a.crec) : reinterpret_cast<const char *>(a.rec);
         constexpr uint32_t RB_ = RQ * 16;   // record bytes
-        // lockstep (option lockstep): the slices of a walk read the same record
-        // rounds through their XCD's L2 and write neighbouring pieces of the
-        // same HB lines; a slice that falls far behind the others reads its
-        // records from HBM instead of L2 and falls further behind (DESIGN.md
-        // 14).  A loader that has issued lock_k rounds past the walk's slowest
-        // slice (as it last read the counts) reads them again, and waits while
-        // it is still that far ahead.  The slowest slice never waits on itself
-        // (its own count is the minimum), so the walk always advances.
-        const bool lock = a.prog != nullptr && a.lock_k != 0;
-        uint32_t lmin = 0;   // the walk's least issued count, as last read
         while (done < nrounds) {
             bool progressed = false;
             LX_WP(l_iter++;)
@@ -729,18 +719,6 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
                 free = __builtin_amdgcn_readfirstlane(lds_ld32(lds_addr(&sh.copied[r % ND]))) > r / ND;
             }
             LX_WP(if (issued < nrounds && issued - done < D && !free) l_slot++;)
-            if (lock && free && issued < nrounds && issued - done < D && issued >= lmin + a.lock_k) {
-                uint32_t m = 0xFFFFFFFFu;
-                for (uint32_t i = lane; i < a.n_slices; i += 64)
-                    m = min(m, __hip_atomic_load(a.prog + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-#pragma unroll
-                for (int o = 32; o > 0; o >>= 1) m = min(m, (uint32_t)__shfl_xor((int)m, o, 64));
-                lmin = __builtin_amdgcn_readfirstlane(m);
-                if (issued >= lmin + a.lock_k) {
-                    free = false;
-                    __builtin_amdgcn_s_sleep(4);
-                }
-            }
             if (issued < nrounds && issued - done < D && free) {
                 const uint32_t s0 = (issued * 64) % RR;
                 char *dst = reinterpret_cast<char *>(rrec) + (uint64_t)s0 * RB_;
@@ -750,7 +728,6 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
                     __builtin_amdgcn_global_load_lds((const void *)(recb + base + (uint64_t)(i * 64 + lane) * 16),
                                                      (void *)(dst + i * 1024), 16, 0, 0);
                 issued++;
-                if (lock && lane == 0) __hip_atomic_store(a.prog + slice, issued, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 LX_WP(asm volatile("ds_write_b32 %0, %1" : : "v"(lds_addr(&sh.p_issued)), "v"(issued) : "memory");)
                 progressed = true;
             }
@@ -1505,7 +1482,6 @@ template <int CPW, int NCW, bool MASKED, bool PK, int ND = kND, bool CR = false>
 __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index(IndexArgs a) {
     WalkClock wc;
     wc.start();
-    a.prog = nullptr;   // (lockstep: the 12-column side-by-side walks only)
     // XCD-aware: neighbouring slices share an L2
     const uint32_t slice = (blockIdx.x % 8) * a.slices_per_xcd + blockIdx.x / 8;
     index_body<CPW, NCW, MASKED, PK, ND, CR>(a, slice);
@@ -1576,7 +1552,6 @@ __global__ __launch_bounds__(64 * (NCW + 1 + ND)) void k_index_segs(IndexArgs a0
     a.seg_flag = a0.seg_flag + off;
     a.seg_list = a0.seg_list + off;
     a.seg_count = a0.seg_count + k;
-    a.prog = CPW == 12 && a0.prog && a0.lock_k && a0.n_slices <= 256 ? a0.prog + (uint64_t)k * 256 : nullptr;
 #ifdef LX_PROBE_SKEW
     if (threadIdx.x == 0 && blockIdx.x < 1024) g_probe_map[blockIdx.x] = k << 16 | slice;
 #endif

@@ -78,7 +78,8 @@ class AbftStats(ctypes.Structure):
     _fields_ = [("ms_index", ctypes.c_float), ("ms_frames", ctypes.c_float), ("ms_election", ctypes.c_float),
                 ("ms_blocks", ctypes.c_float), ("frame_steps", ctypes.c_uint32), ("fc_launches", ctypes.c_uint32),
                 ("vote_launches", ctypes.c_uint32), ("blocks", ctypes.c_uint32), ("fc_pairs", ctypes.c_uint64),
-                ("fc_pair_cols", ctypes.c_uint64), ("ms_root_fc_gpu", ctypes.c_float)]
+                ("fc_pair_cols", ctypes.c_uint64), ("ms_root_fc_gpu", ctypes.c_float),
+                ("fc_pair_cols_tiled", ctypes.c_uint64)]
 
 
 class _StoreView:
@@ -276,6 +277,10 @@ class IndexedLachesis:
         self._chk(self.L.lx_abft_last_stats(self.h, ctypes.byref(st)))
         return {f: getattr(st, f) for f, _ in AbftStats._fields_}
 
+    def set_option(self, name, value):
+        """lx_abft_set_option (path selection; results never change)."""
+        self._chk(self.L.lx_abft_set_option(self.h, name.encode(), int(value)))
+
 
 class DenseLachesis:
     """Dense-index handle over lx_abft_* (what a cgo shim binds 1:1): events
@@ -364,3 +369,9 @@ class DenseLachesis:
         st = AbftStats()
         self.L.lx_abft_last_stats(self.h, ctypes.byref(st))
         return {f: getattr(st, f) for f, _ in AbftStats._fields_}
+
+    def set_option(self, name, value):
+        """lx_abft_set_option (path selection; results never change)."""
+        rc = self.L.lx_abft_set_option(self.h, name.encode(), int(value))
+        if rc != 0:
+            raise LxError(rc, self.L.lx_abft_last_error(self.h).decode())

@@ -113,6 +113,7 @@ SIGNATURES = [
     ("lx_abft_create", ctypes.c_int, [vp, ctypes.POINTER(vp)]),
     ("lx_abft_destroy", None, [vp]),
     ("lx_abft_last_error", ctypes.c_char_p, [vp]),
+    ("lx_abft_set_option", ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_int64]),
     ("lx_abft_bootstrap", ctypes.c_int, [vp, ctypes.c_uint32, ctypes.c_uint32, u32p, vp]),
     ("lx_abft_reset", ctypes.c_int, [vp, ctypes.c_uint32, ctypes.c_uint32, u32p]),
     ("lx_abft_process_batch", ctypes.c_int, [vp, ctypes.c_uint32, u32p, u32p, u64p, u32p, u32p, u32p, u32p]),

@@ -62,6 +62,9 @@ def test_multi_gpu_line_keys():
     assert "whole_row_equiv_frac" in roof
     rs = r["rowseg"]
     assert rs["fc_kernel_ms"] > 0 and rs["fc_protocol_ms"] > 0
+    # the protocol split into the library's device steps and the collectives (round 6)
+    assert rs["fc_protocol_device_ms"] > 0 and rs["fc_protocol_collective_ms"] > 0
+    assert rs["fc_protocol_device_ms"] + rs["fc_protocol_collective_ms"] <= rs["fc_protocol_ms"] * 1.05
     assert abs(rs["fc_kernel_ms"] + rs["fc_protocol_ms"] - rs["fc_step_ms"]) < 1e-6 * rs["fc_step_ms"] + 1e-9
     cs = r["colshard"]
     assert cs["events_per_sec"] > 0 and cs["fc_queries_per_sec"] > 0 and cs["exchange_ms"] is not None

@@ -412,8 +412,8 @@ def test_full_size_config3_prefix_vs_oracle(lx):
 
 
 @pytest.mark.big_only
-@pytest.mark.parametrize("opts", [None, {"seg_xmap": 1}, {"lockstep": 4}, {"lockstep": 16}])
-def test_config3_shape_1m_default_segments_vs_oracle(lx, opts):
+@pytest.mark.parametrize("walk_opts", [None, {"seg_xmap": 1}])
+def test_config3_shape_1m_default_segments_vs_oracle(lx, walk_opts):
     """The headline walk as shipped, pinned end to end: BASELINE configs[2]'s
     shape (V=1000, Zipf stakes, P=10) at 1,000 events per validator (1M
     events), indexed as one batch with DEFAULT options.  seg_auto then walks
@@ -424,14 +424,14 @@ def test_config3_shape_1m_default_segments_vs_oracle(lx, opts):
     inside the oracle's coverage.  EVERY HighestBefore and LowestAfter row of
     the epoch byte-identical, branch IDs, and 1M ForklessCause pairs of which
     most span the segment boundary (vecengine/index.go:144-233,
-    vecengine/traversal.go:13-37, vecfc/forkless_cause.go:40-82).  opts: the
-    slice -> workgroup mapping of option seg_xmap (whole 8-slice groups per
-    XCD), the loaders' lockstep (option lockstep)."""
+    vecengine/traversal.go:13-37, vecfc/forkless_cause.go:40-82).  walk_opts:
+    the slice -> workgroup mapping of option seg_xmap (whole 8-slice groups
+    per XCD)."""
     V = 1000
     w = [(1 << 20) // (i + 1) for i in range(V)]
     d = lx.tools.gen_dag(V, 1000, 10, seed=11)
     N = len(d)
-    ix = lx.Index(event_capacity=N, options=opts)
+    ix = lx.Index(event_capacity=N, options=walk_opts)
     ix.reset(w)
     br = ix.add_batch(d.creator, d.seq, d.poff, d.par, want_branches=True)
     st = ix.segment_stats()
