@@ -933,7 +933,10 @@ def main():
     if primary == "rowseg":
         r0, r1 = ix.rowseg_range()
         walked = r1 - r0
-    idx_compulsory = 8.0 * plane_stride * walked
+    # (the row stride's padding columns are never written: 8 x B bytes per event
+    # is the algorithmic write, 8 x stride the planes' footprint)
+    idx_compulsory = 8.0 * B * walked
+    idx_footprint = 8.0 * plane_stride * walked
     result = {
         "metric": "events indexed/sec + ForklessCause queries/sec at 1000 validators, 1/2/4/8 GPU",
         "value": events_per_s,
@@ -981,13 +984,16 @@ def main():
                            "traffic": idx_traffic["hbm_bytes"] if idx_traffic else None,
                            "traffic_kernel_names": idx_traffic.get("kernel_names") if idx_traffic else None,
                            "traffic_source": traffic_src if idx_traffic else None,
-                           "compulsory_bytes_per_launch": idx_compulsory, "kernel_ms": kidx,
+                           "compulsory_bytes_per_launch": idx_compulsory,
+                           "plane_footprint_bytes_per_launch": idx_footprint, "kernel_ms": kidx,
+                           "traffic_over_compulsory": (idx_traffic["hbm_bytes"] / idx_compulsory) if idx_traffic else None,
                            "compulsory_frac": idx_compulsory / (kidx * 1e-3) / 1e9 / HBM_PEAK_GBS,
                            "algorithmic_bytes_per_launch": idx_bytes,
                            "survey_formula_achieved": idx_achieved,
                            "survey_formula_frac": idx_achieved / HBM_PEAK_GBS,
-                           "note": "achieved / frac: the compulsory HBM bytes (every HB and LA row this rank walks "
-                                   "written once, 8 x row stride bytes per event) over the kernel time; "
+                           "note": "achieved / frac: the compulsory HBM bytes (every HB and LA entry of the rows "
+                                   "this rank walks written once, 8 x B bytes per event; the planes' padded stride "
+                                   "in plane_footprint_bytes_per_launch) over the kernel time; "
                                    "survey_formula_* follow SURVEY 8d's per-event formula, which also counts every "
                                    "parent-row read -- the walker serves those from LDS, so it can exceed the HBM "
                                    "peak: the walk is latency-bound (DAG depth x pass latency)"},
