@@ -795,7 +795,9 @@ def main():
         t_index = max_over_ranks(time.perf_counter() - t0)
         clk_timed = list(clk_log[-args.steps:])
         power = None
-        if kind == "single" and rank == 0 and world == 1 and not args.no_power:
+        # (not under rocprofv3: its tool library would load into the amd-smi child too)
+        profiled = any(k.startswith("ROCPROF") for k in os.environ)
+        if kind == "single" and rank == 0 and world == 1 and not args.no_power and not profiled:
             power = power_probe(index_step)   # untimed, after the timed steps
 
         # ---- FC: warmup + K timed steps

@@ -185,11 +185,21 @@ hipError_t launch_root_fc(const RootFcArgs &a, bool forks, hipStream_t s) {
 __global__ __launch_bounds__(256) void k_rfc_decide(RfcRestArgs a) {
     const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t c = (uint32_t)(p / a.rp), r = (uint32_t)(p % a.rp);
-    if (c >= a.n_cand || r >= a.n_roots) return;
-    uint32_t sum = 0;
-    for (uint32_t z = 0; z < a.n_split; z++) sum += a.psum[((uint64_t)z * a.n_cand + c) * a.rp + r];
-    a.psum[(uint64_t)c * a.rp + r] = sum;
-    if (sum < a.quorum && (uint64_t)sum + a.rest >= a.quorum) a.list[atomicAdd(a.count, 1u)] = (uint32_t)p;
+    bool open = false;
+    if (c < a.n_cand && r < a.n_roots) {
+        uint32_t sum = 0;
+        for (uint32_t z = 0; z < a.n_split; z++) sum += a.psum[((uint64_t)z * a.n_cand + c) * a.rp + r];
+        a.psum[(uint64_t)c * a.rp + r] = sum;
+        open = sum < a.quorum && (uint64_t)sum + a.rest >= a.quorum;
+    }
+    // one atomic per wave for its open pairs (a single counter for the launch)
+    const unsigned long long m = __ballot(open);
+    if (!m) return;
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t base = 0;
+    if (lane == (uint32_t)__builtin_ctzll(m)) base = atomicAdd(a.count, (uint32_t)__builtin_popcountll(m));
+    base = __shfl(base, (int)__builtin_ctzll(m), 64);
+    if (open) a.list[base + __builtin_popcountll(m & ((1ull << lane) - 1ull))] = (uint32_t)p;
 }
 
 __global__ __launch_bounds__(256) void k_rfc_rest(RfcRestArgs a) {

@@ -102,6 +102,7 @@ struct IndexArgs {
     // seg_xmap is on: every 128-B HB line written by workgroups of one XCD);
     // seg_map_n = 0: seg_chunk's mapping
     uint32_t seg_xmap;           // option seg_xmap (lx_set_option)
+    uint32_t rec_pf;             // option rec_pf: drains touch the record round this many rounds ahead (0 off)
     uint32_t seg_map_n;
     uint16_t seg_map[256];
 };
