@@ -423,16 +423,10 @@ def abft_leg(lx, steps, warmup, device, cpu_budget, want_cpu):
     if st["ms_root_fc_gpu"] > 0:
         pc = st["fc_pair_cols"] / (st["ms_root_fc_gpu"] * 1e-3)
         ach = ROOT_FC_OPS_PER_PAIR_COL * pc / 1e12
-        # the early exit tiles the heaviest 256 columns of every
-        # pair and the rest only for the pairs still open: `achieved` counts the
-        # algorithmic pair-columns (all V per pair), `tiled_frac` the columns
-        # the tiles actually compared
-        tiled = st.get("fc_pair_cols_tiled", st["fc_pair_cols"])
         res["roofline_root_fc"] = {"bound": "valu", "achieved": ach, "peak": VALU_PEAK_TOPS,
                                    "unit": "T int32 lane-ops/s", "frac": ach / VALU_PEAK_TOPS,
                                    "pair_cols_per_s": pc, "ops_per_pair_col": ROOT_FC_OPS_PER_PAIR_COL,
-                                   "ms_per_epoch": st["ms_root_fc_gpu"],
-                                   "tiled_pair_cols_frac": tiled / st["fc_pair_cols"] if st["fc_pair_cols"] else None}
+                                   "ms_per_epoch": st["ms_root_fc_gpu"]}
     lch.close()
     if want_cpu:
         from oracle import corc

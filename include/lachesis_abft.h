@@ -57,11 +57,8 @@ int lx_abft_create(lx_index *index, lx_abft **out);
 void lx_abft_destroy(lx_abft *a);
 const char *lx_abft_last_error(const lx_abft *a);
 /* Path selection (results never change):
- *   "rfc_early"  1 (default): on fork-free frames whose 256 heaviest validators
- *                can reach the quorum alone, the root ForklessCause tiles sum
- *                those columns only and the pairs the rest of the stake could
- *                still swing get the rest; 0: every column tiled
- *   "spec_depth" self-children evaluated speculatively per frame step (0..16) */
+ *   "spec_depth" self-children evaluated speculatively per frame step (0..16,
+ *                default 4) */
 int lx_abft_set_option(lx_abft *a, const char *name, int64_t value);
 
 /* ApplyGenesis + Bootstrap (abft/apply_genesis.go:17-44, bootstrap.go:30-52):
@@ -113,7 +110,6 @@ typedef struct lx_abft_stats {
     uint64_t fc_pairs;   /* (event, root) pairs evaluated */
     uint64_t fc_pair_cols;   /* pairs x validator columns compared by k_root_fc */
     float ms_root_fc_gpu;    /* k_root_fc time on the stream (HIP events around each launch) */
-    uint64_t fc_pair_cols_tiled;   /* of them compared by the tiles (the early exit tiles the heaviest 256) */
 } lx_abft_stats;
 int lx_abft_last_stats(const lx_abft *a, lx_abft_stats *out);
 

@@ -177,10 +177,6 @@ struct lx_abft {
 
     // scratch
     DVec<uint32_t> d_cand, d_psum;
-    DVec<uint32_t> d_rfc_list;          // k_root_fc early exit: open pairs + their count
-    uint32_t rfc_j1 = 256;              // its heaviest columns (0: off; LX_RFC_EARLY=0 / option)
-    uint64_t rfc_w1 = 0;                // their stake
-    uint32_t rfc_rest = 0;              // the stake of every other column
     DVec<uint8_t> d_q;
     DVec<unsigned long long> d_dec;
     DVec<uint32_t> d_err;
@@ -371,14 +367,6 @@ int start_epoch(lx_abft *a, uint32_t epoch, uint32_t nv, const uint32_t *w) {
     a->V = nv;
     a->weights.assign(w, w + nv);
     a->quorum = iv.quorum;
-    // the root ForklessCause early exit's split of the stake (idx order)
-    a->rfc_w1 = 0;
-    uint64_t wt = 0;
-    for (uint32_t c = 0; c < nv; c++) {
-        wt += w[c];
-        if (c < a->rfc_j1) a->rfc_w1 += w[c];
-    }
-    a->rfc_rest = (uint32_t)std::min<uint64_t>(wt - a->rfc_w1, 0xFFFFFFFFull);
     return 0;
 }
 
@@ -440,14 +428,9 @@ int eval_frame(lx_abft *a, const IndexView &iv, uint32_t f, const std::vector<ui
         AHIP(a, hipHostGetDevicePointer(&q_dev, a->q_pin, 0));
         // split the columns when the tiles alone cannot fill the chip
         const uint32_t ncols = (iv.V + 31) / 32 * 32;
-        // early exit (fork-free frames whose heaviest j1 columns can reach the
-        // quorum alone): the tiles sum [0, j1), k_rfc_rest the rest for the
-        // pairs still open (lx_abft_kernels.hip)
-        const uint32_t j1 = a->rfc_j1 && iv.B == iv.V && ncols > 2 * a->rfc_j1 && a->rfc_w1 >= a->quorum ? a->rfc_j1 : 0u;
-        const uint32_t tile_cols = j1 ? j1 : ncols;
-        const uint32_t splits = lx::root_fc_splits(n, R, tile_cols);
-        const uint32_t col_split = ((tile_cols + splits - 1) / splits + 31) / 32 * 32;
-        const uint32_t n_split = (tile_cols + col_split - 1) / col_split;
+        const uint32_t splits = lx::root_fc_splits(n, R, ncols);
+        const uint32_t col_split = ((ncols + splits - 1) / splits + 31) / 32 * 32;
+        const uint32_t n_split = (ncols + col_split - 1) / col_split;
         ARC(reserve(a, a->d_psum, (uint64_t)n_split * n * words * 32, 0, s));
         RootFcArgs r{};
         r.hb = iv.hb;
@@ -458,7 +441,7 @@ int eval_frame(lx_abft *a, const IndexView &iv, uint32_t f, const std::vector<ui
         r.roots = fr.d_ev.p;
         r.n_roots = R;
         r.roots_fallback = cand[0];
-        r.ncols = tile_cols;
+        r.ncols = ncols;
         r.wpad = iv.wpad;
         r.quorum = a->quorum;
         r.n_k = a->n_k;
@@ -477,35 +460,10 @@ int eval_frame(lx_abft *a, const IndexView &iv, uint32_t f, const std::vector<ui
         }
         AHIP(a, hipEventRecord(a->ev_fc[0], s));
         AHIP(a, lx::launch_root_fc(r, iv.B > iv.V, s));
-        if (j1) {
-            const uint64_t pairs = (uint64_t)n * words * 32;
-            ARC(reserve(a, a->d_rfc_list, pairs + 1, 0, s));
-            AHIP(a, hipMemsetAsync(a->d_rfc_list.p + pairs, 0, 4, s));
-            RfcRestArgs x{};
-            x.hb = iv.hb;
-            x.la = iv.la;
-            x.stride = iv.stride;
-            x.cand = a->d_cand.p;
-            x.n_cand = n;
-            x.roots = fr.d_ev.p;
-            x.n_roots = R;
-            x.roots_fallback = cand[0];
-            x.rp = words * 32;
-            x.psum = a->d_psum.p;
-            x.n_split = n_split;
-            x.quorum = a->quorum;
-            x.rest = a->rfc_rest;
-            x.j1 = j1;
-            x.ncols = ncols;
-            x.wpad = iv.wpad;
-            x.list = a->d_rfc_list.p;
-            x.count = a->d_rfc_list.p + pairs;
-            AHIP(a, lx::launch_rfc_rest(x, s));
-        }
         AHIP(a, hipEventRecord(a->ev_fc[1], s));
         QuorumArgs qa{};
         qa.psum = a->d_psum.p;
-        qa.n_split = j1 ? 1u : n_split;   // (the early exit folded its splits into layer 0)
+        qa.n_split = n_split;
         qa.bits = bits;
         qa.words = words;
         qa.n_roots = R;
@@ -526,7 +484,6 @@ int eval_frame(lx_abft *a, const IndexView &iv, uint32_t f, const std::vector<ui
         a->stats.fc_launches++;
         a->stats.fc_pairs += (uint64_t)n * R;
         a->stats.fc_pair_cols += (uint64_t)n * R * iv.V;
-        a->stats.fc_pair_cols_tiled += (uint64_t)n * R * std::min(tile_cols, iv.V);
     } else {
         q.assign(n, 0);   // no roots in frame f: no quorum (WeightCounter of nothing)
     }
@@ -976,7 +933,6 @@ void lx_abft_destroy(lx_abft *a) {
     a->arena.release();
     a->d_cand.release();
     a->d_psum.release();
-    a->d_rfc_list.release();
     a->d_q.release();
     a->d_dec.release();
     a->d_err.release();
@@ -1007,17 +963,7 @@ int lx_abft_bootstrap(lx_abft *a, uint32_t epoch, uint32_t nv, const uint32_t *w
 int lx_abft_set_option(lx_abft *a, const char *name, int64_t value) {
     if (!a || !name) return LX_ERR_ARG;
     const std::string k(name);
-    if (k == "rfc_early") {
-        a->rfc_j1 = value ? 256u : 0u;
-        // (the stake split follows at the next epoch start; recompute it now)
-        a->rfc_w1 = 0;
-        uint64_t wt = 0;
-        for (uint32_t c = 0; c < a->weights.size(); c++) {
-            wt += a->weights[c];
-            if (c < a->rfc_j1) a->rfc_w1 += a->weights[c];
-        }
-        a->rfc_rest = (uint32_t)std::min<uint64_t>(wt - a->rfc_w1, 0xFFFFFFFFull);
-    } else if (k == "spec_depth") {
+    if (k == "spec_depth") {
         if (value < 0 || value > 16) return a->fail(LX_ERR_ARG, "spec_depth must be 0..16");
         a->spec_depth = (uint32_t)value;
     } else {

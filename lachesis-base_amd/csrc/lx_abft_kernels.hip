@@ -173,67 +173,6 @@ hipError_t launch_root_fc(const RootFcArgs &a, bool forks, hipStream_t s) {
     return hipGetLastError();
 }
 
-// ---------------------------------------------------------------------------- k_root_fc early exit
-// ForklessCause is a stake sum in pos.Validators idx order compared with the
-// quorum (vecfc/forkless_cause.go:63-82): after the heaviest j1 columns a pair
-// whose sum reaches the quorum is true, and one whose sum plus the stake of
-// every other column stays below it is false, whatever those columns hold
-// (fork-free frames: no marks, no cheater fix-ups).  k_root_fc sums [0, j1);
-// k_rfc_decide folds its splits into layer 0 and lists the other pairs;
-// k_rfc_rest adds their columns [j1, ncols) from the rows (L2-resident: a
-// frame's candidates and roots are a few MB).
-__global__ __launch_bounds__(256) void k_rfc_decide(RfcRestArgs a) {
-    const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t c = (uint32_t)(p / a.rp), r = (uint32_t)(p % a.rp);
-    bool open = false;
-    if (c < a.n_cand && r < a.n_roots) {
-        uint32_t sum = 0;
-        for (uint32_t z = 0; z < a.n_split; z++) sum += a.psum[((uint64_t)z * a.n_cand + c) * a.rp + r];
-        a.psum[(uint64_t)c * a.rp + r] = sum;
-        open = sum < a.quorum && (uint64_t)sum + a.rest >= a.quorum;
-    }
-    // one atomic per wave for its open pairs (a single counter for the launch)
-    const unsigned long long m = __ballot(open);
-    if (!m) return;
-    const uint32_t lane = threadIdx.x & 63;
-    uint32_t base = 0;
-    if (lane == (uint32_t)__builtin_ctzll(m)) base = atomicAdd(a.count, (uint32_t)__builtin_popcountll(m));
-    base = __shfl(base, (int)__builtin_ctzll(m), 64);
-    if (open) a.list[base + __builtin_popcountll(m & ((1ull << lane) - 1ull))] = (uint32_t)p;
-}
-
-__global__ __launch_bounds__(256) void k_rfc_rest(RfcRestArgs a) {
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t m = *a.count;
-    const uint32_t q0 = a.j1 / 4, q1 = a.ncols / 4;
-    for (uint32_t k = blockIdx.x * 4 + threadIdx.x / 64; k < m; k += gridDim.x * 4) {
-        const uint32_t p = a.list[k];
-        const uint32_t c = p / a.rp, r = p % a.rp;
-        uint32_t root = a.roots[r];
-        if (root == LX_NONE) root = a.roots_fallback;
-        const uint4 *h = reinterpret_cast<const uint4 *>(a.hb + (uint64_t)a.cand[c] * a.stride);
-        const uint4 *l = reinterpret_cast<const uint4 *>(a.la + (uint64_t)root * a.stride);
-        const uint4 *w = reinterpret_cast<const uint4 *>(a.wpad);
-        uint32_t sum = 0;
-        for (uint32_t q = q0 + lane; q < q1; q += 64) {
-            const uint4 hv = h[q], lv = l[q], wv = w[q];
-            sum += (lv.x - 1u < hv.x ? wv.x : 0u) + (lv.y - 1u < hv.y ? wv.y : 0u) +
-                   (lv.z - 1u < hv.z ? wv.z : 0u) + (lv.w - 1u < hv.w ? wv.w : 0u);
-        }
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) sum += __shfl_xor(sum, off, 64);
-        if (lane == 0) a.psum[p] += sum;
-    }
-}
-
-hipError_t launch_rfc_rest(const RfcRestArgs &a, hipStream_t s) {
-    const uint64_t pairs = (uint64_t)a.n_cand * a.rp;
-    if (!pairs) return hipSuccess;
-    hipLaunchKernelGGL(k_rfc_decide, dim3((uint32_t)((pairs + 255) / 256)), dim3(256), 0, s, a);
-    hipLaunchKernelGGL(k_rfc_rest, dim3(1024), dim3(256), 0, s, a);
-    return hipGetLastError();
-}
-
 // ---------------------------------------------------------------------------- k_root_quorum
 // One wave per candidate: FC bit per root = (sum over the column splits >=
 // quorum, no early-false flag), written to the bit row; then the stake of the

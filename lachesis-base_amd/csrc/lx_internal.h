@@ -102,7 +102,6 @@ struct IndexArgs {
     // seg_xmap is on: every 128-B HB line written by workgroups of one XCD);
     // seg_map_n = 0: seg_chunk's mapping
     uint32_t seg_xmap;           // option seg_xmap (lx_set_option)
-    uint32_t rec_pf;             // option rec_pf: drains touch the record round this many rounds ahead (0 off)
     uint32_t seg_map_n;
     uint16_t seg_map[256];
 };
@@ -557,30 +556,6 @@ struct RootFcArgs {
     uint32_t n_split;            // column splits (grid z)
 };
 
-// k_root_fc's early exit (fork-free frames, columns in pos.Validators idx
-// order): k_root_fc over the heaviest j1 columns, then k_rfc_decide sums the
-// splits into layer 0 and lists the pairs the rest of the stake could still
-// swing, and k_rfc_rest adds their columns [j1, ncols) (one wave per pair)
-struct RfcRestArgs {
-    const uint32_t *hb;
-    const uint32_t *la;
-    uint64_t stride;
-    const uint32_t *cand;
-    uint32_t n_cand;
-    const uint32_t *roots;
-    uint32_t n_roots;
-    uint32_t roots_fallback;
-    uint32_t rp;                 // psum row pitch (words * 32)
-    uint32_t *psum;              // layers of k_root_fc over [0, j1); layer 0 = the final sums
-    uint32_t n_split;
-    uint32_t quorum;
-    uint32_t rest;               // stake of columns [j1, V)
-    uint32_t j1, ncols;          // columns k_root_fc summed, all columns (multiples of 4)
-    const uint32_t *wpad;
-    uint32_t *list;              // undecided pairs c * rp + r
-    uint32_t *count;             // their number (zeroed before k_rfc_decide)
-};
-
 struct QuorumArgs {
     const uint32_t *psum;        // partial stake sums of k_root_fc
     uint32_t n_split;
@@ -792,7 +767,6 @@ hipError_t launch_qi_metric(const QiArgs &a, const uint32_t *ev, uint32_t n, uin
                             hipStream_t s);
 uint32_t root_fc_splits(uint32_t n_cand, uint32_t n_roots, uint32_t ncols);
 hipError_t launch_root_fc(const RootFcArgs &a, bool forks, hipStream_t s);
-hipError_t launch_rfc_rest(const RfcRestArgs &a, hipStream_t s);
 hipError_t launch_root_quorum(const QuorumArgs &a, hipStream_t s);
 hipError_t launch_fc_tile_out(const uint32_t *psum, uint32_t n_split, uint32_t n_cand, uint32_t rp, uint32_t n_roots,
                               uint32_t quorum, const uint8_t *tag, uint8_t *out, uint64_t pitch, hipStream_t s);

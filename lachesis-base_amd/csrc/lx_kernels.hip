@@ -859,13 +859,6 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
             }
             // ring and record data of this round consumed: slots may be reused
             if (lane == 0) __hip_atomic_store(&sh.copied[d], nd + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (!CR && a.rec_pf && (R + a.rec_pf) * 64 < n) {
-                // option rec_pf: touch the record round rec_pf rounds ahead (one
-                // 4-B LDS-DMA per 64 B of its 4-KB block, into the dummy area) so
-                // that the loader's DMA of it finds it nearer than HBM
-                const char *blk = reinterpret_cast<const char *>(a.rec) + (uint64_t)(R + a.rec_pf) * 64 * sizeof(EventRec);
-                __builtin_amdgcn_global_load_lds((const void *)(blk + lane * 64u), (void *)dummy, 4, 0, 0);
-            }
 #ifdef LX_PROBE_SKEW
             // probe build: when each 32nd round was drained, per workgroup (lx_probe_skew_read)
             if (lane == 0 && R % 32 == 0 && R / 32 < kProbeSkewSlots && blockIdx.x < 1024)
