@@ -519,7 +519,7 @@ def smi_json(argv, timeout=10):
 
 
 def power_probe(step, seconds=2.5):
-    """The board's socket power and GFX clocks (amd-smi metric, sampled by a
+    """The board's socket power, GFX clocks and hotspot / HBM temperatures (amd-smi metric, sampled by a
     host thread) while the index step runs back to back for ~`seconds`,
     untimed, after the timed steps; and the socket power limit.  The walk's
     time is a fixed number of shader cycles over the clock the box gives it
@@ -536,11 +536,14 @@ def power_probe(step, seconds=2.5):
 
     def sampler():
         while not stop.is_set():
-            d = smi_json(["metric", "-p", "-c"])
+            d = smi_json(["metric", "-p", "-c", "-t"])
             try:
                 g = gpu0(d)
                 clk = [g["clock"][k]["clk"]["value"] for k in g["clock"] if k.startswith("gfx")]
-                samples.append((time.time(), float(g["power"]["socket_power"]["value"]), float(np.mean(clk))))
+                t = g.get("temperature", {})
+                tv = lambda k: float(t[k]["value"]) if isinstance(t.get(k), dict) else float("nan")
+                samples.append((time.time(), float(g["power"]["socket_power"]["value"]), float(np.mean(clk)),
+                                tv("hotspot"), tv("mem")))
             except Exception:
                 time.sleep(0.2)
 
@@ -563,6 +566,8 @@ def power_probe(step, seconds=2.5):
         return {"samples": 0, "socket_power_limit_w": limit_w, "note": "amd-smi gave no samples"}
     return {"samples": len(s), "steps": steps, "socket_power_w_mean": float(np.mean([x[1] for x in s])),
             "socket_power_w_max": float(max(x[1] for x in s)), "smi_gfx_mhz_mean": float(np.mean([x[2] for x in s])),
+            "hotspot_c_max": max((x[3] for x in s if x[3] == x[3]), default=None),
+            "hbm_c_max": max((x[4] for x in s if x[4] == x[4]), default=None),
             "socket_power_limit_w": limit_w,
             "source": "amd-smi metric -p -c (read-only) sampled during back-to-back index steps after the timed ones"}
 
