@@ -56,6 +56,10 @@ for r in range(int(os.environ.get("WS_WALKS", "3"))):
             "neighbour_us": {"p50": q(nb, 50), "p90": q(nb, 90), "p99": q(nb, 99), "max": q(nb, 100)},
             "neighbour_events_p90": round(float(np.percentile(nb, 90)) * rate, 0),
             "slowest_slice_at_end": int(sl[int(np.argmax(M[:, -1]))]),
+            # where the slowest slice lost its time: marks (x 2048 events into the
+            # walk) at which its lag behind the median slice grew by > 200 us
+            "lag_jumps": [(int(t), round(float(dl), 0)) for t, dl in enumerate(np.diff(
+                M[int(np.argmax(M[:, -1]))] - np.median(M, axis=0))) if dl > 200.0][:40],
             # each XCD group's (g % 8) slowest slice end, ms after the walk's first mark
             "end_ms_by_block_group": {x: round(float(max(M[i, -1] for i, s_ in enumerate(sl) if xcd_of[s_] == x)) / 1e3, 2)
                                       for x in sorted(set(xcd_of.values()))}})
