@@ -728,8 +728,6 @@ int add_batch_dev(lx_index *h, uint32_t n, const uint32_t *creator, const uint32
     ia.cpw_hint = h->cpw_hint;
     ia.pack16 = h->pack16 && h->max_seq <= 0xFFFFu;
     ia.seg_xmap = h->seg_xmap_opt ? 1u : 0u;
-    ia.drain_margin = h->drain_margin;
-    ia.pad_slice = h->pad_slice ? 1u : 0u;
     if (ia.cpw_hint >= 8 && (!ia.pack16 || ia.mask)) ia.cpw_hint = 4;   // 8- / 12-column slots: packed, fork-free
     const size_t prof_n = (size_t)kProfBlocks * kProfWaves * kProfSlots;
     if (!h->d_clk) {
@@ -1894,13 +1892,6 @@ int lx_set_option(lx_index *h, const char *name, int64_t value) {
         h->crec_opt = value != 0;
     } else if (k == "seg_xmap") {
         h->seg_xmap_opt = value != 0;
-    } else if (k == "pad_slice") {
-        h->pad_slice = value != 0;
-    } else if (k == "drain_margin") {
-        // (events; every walker's slot ring holds >= 2048 events: the waited-for
-        // round stays strictly older than the publishing event's)
-        if (value < 0 || value > 1920 || value % 64) return h->fail(LX_ERR_ARG, "drain_margin must be a multiple of 64 in 0..1920");
-        h->drain_margin = (uint32_t)value;
     } else if (k == "dbl") {
         h->dbl = value != 0;
     } else if (k == "seg_auto") {

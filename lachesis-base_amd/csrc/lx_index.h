@@ -259,8 +259,6 @@ struct lx_index {
     bool small_timing = false;             // option timing=1: time small-path launches (two event records)
     uint32_t cpw_hint = 0;                 // option cpw: walker columns per workgroup (0 = auto)
     bool pack16 = true;                    // option pack16=0: two slot units per event even for small seqs
-    uint32_t drain_margin = 0;             // option drain_margin (IndexArgs::drain_margin)
-    bool pad_slice = false;                // option pad_slice (IndexArgs::pad_slice)
     bool seg_xmap_opt = false;             // option seg_xmap=1: 12-column walks keep each HB line's slices on one XCD
     bool crec_opt = false;                 // option crec=1: the 8- / 12-column walks stream the 32-B compact records
     bool prof = false;                     // LX_PROF=1 in make WPROF=1 builds: per-wave walker counters

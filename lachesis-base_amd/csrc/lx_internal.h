@@ -102,8 +102,6 @@ struct IndexArgs {
     // seg_xmap is on: every 128-B HB line written by workgroups of one XCD);
     // seg_map_n = 0: seg_chunk's mapping
     uint32_t seg_xmap;           // option seg_xmap (lx_set_option)
-    uint32_t pad_slice;          // option pad_slice (12-column walks: the last slice's whole-piece stores)
-    uint32_t drain_margin;       // option drain_margin: events (multiple of 64, < ring - 64; 0 = the slot's own occupant)
     uint32_t seg_map_n;
     uint16_t seg_map[256];
 };

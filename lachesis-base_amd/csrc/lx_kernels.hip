@@ -674,10 +674,7 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
     bool valid_[ID ? 1 : CPW];
     bool contig = true;
     if constexpr (ID) {
-        // (option pad_slice: the epoch's last, partial slice stores its row
-        // piece whole too -- its columns past the epoch's hold 0 -- when the
-        // planes' row stride has room for it)
-        contig = (nval == (uint32_t)CPW || (a.pad_slice && c0 + CPW <= stride)) && (c0 % 4) == 0;
+        contig = nval == (uint32_t)CPW && (c0 % 4) == 0;
     } else {
 #pragma unroll
         for (int k = 0; k < CPW; k++) {
@@ -1228,15 +1225,9 @@ __device__ __forceinline__ void index_body(const IndexArgs &a, const uint32_t sl
                                                                            : dmy + 1024u;
                     }
                     // the slot's previous occupant lp - RN is drained once its
-                    // drain wave's `copied` count exceeds its round / ND.
-                    // Option drain_margin M: wait instead for event lp - RN + M
-                    // to be drained, so the compute waves run at most RN - M
-                    // events ahead of the drains and a drain still finds the
-                    // slot of its event's previous branch event (prev is at most
-                    // M back) instead of waiting for stores and reading L2
-                    const uint32_t mg = a.drain_margin;
-                    const uint32_t rr = (lp + mg - RN) / 64;
-                    wneed = lp + mg >= (uint32_t)RN ? rr / ND + 1 : 0u;
+                    // drain wave's `copied` count exceeds its round / ND
+                    const uint32_t rr = (lp - RN) / 64;
+                    wneed = lp >= (uint32_t)RN ? rr / ND + 1 : 0u;
                     wm_addr = lds_addr(&sh.copied[rr % ND]);
                 }
                 done = !live;

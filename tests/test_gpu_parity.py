@@ -412,7 +412,7 @@ def test_full_size_config3_prefix_vs_oracle(lx):
 
 
 @pytest.mark.big_only
-@pytest.mark.parametrize("walk_opts", [None, {"seg_xmap": 1}, {"drain_margin": 1024}, {"pad_slice": 1}])
+@pytest.mark.parametrize("walk_opts", [None, {"seg_xmap": 1}])
 def test_config3_shape_1m_default_segments_vs_oracle(lx, walk_opts):
     """The headline walk as shipped, pinned end to end: BASELINE configs[2]'s
     shape (V=1000, Zipf stakes, P=10) at 1,000 events per validator (1M
@@ -426,8 +426,7 @@ def test_config3_shape_1m_default_segments_vs_oracle(lx, walk_opts):
     most span the segment boundary (vecengine/index.go:144-233,
     vecengine/traversal.go:13-37, vecfc/forkless_cause.go:40-82).  walk_opts:
     the slice -> workgroup mapping of option seg_xmap (whole 8-slice groups
-    per XCD), the compute waves' lead over the drains (option drain_margin),
-    the last slice's whole-piece HB stores (option pad_slice)."""
+    per XCD)."""
     V = 1000
     w = [(1 << 20) // (i + 1) for i in range(V)]
     d = lx.tools.gen_dag(V, 1000, 10, seed=11)
@@ -595,8 +594,7 @@ def test_full_size_properties_config2(lx):
 # The shipped walker (block layout: 16-event blocks per wave, a quad of lanes
 # per event, 4 drain waves) on 1-, 2- and 4-column slices, the last with the
 # 16-bit packed slot unit (default while every seq fits) and with two units.
-WALKER_VARIANTS = [{"cpw": 0}, {"cpw": 1}, {"cpw": 2}, {"cpw": 4}, {"cpw": 4, "pack16": 0},
-                   {"cpw": 1, "drain_margin": 1920}, {"cpw": 4, "pack16": 0, "drain_margin": 1024}]
+WALKER_VARIANTS = [{"cpw": 0}, {"cpw": 1}, {"cpw": 2}, {"cpw": 4}, {"cpw": 4, "pack16": 0}]
 
 
 @pytest.mark.big_only
