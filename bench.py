@@ -373,7 +373,6 @@ def config_leg(lx, name, steps, warmup, device, want_cpu, cpu_budget, fc_n=1 << 
 ABFT_CONFIG = ("c5", 1000, 50, 10, "zipf")   # BASELINE configs[4]: V, events/validator, parents, stakes
 
 
-ROOT_FC_OPS_PER_PAIR_COL = 2.5
 VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12   # 78.6 T lane-ops/s
 
 
@@ -415,17 +414,24 @@ def abft_leg(lx, steps, warmup, device, cpu_budget, want_cpu):
            "max_frame": int(claimed.max()), "phase_ms": {k: st[k] for k in ("ms_index", "ms_frames", "ms_election", "ms_blocks")},
            "frame_steps": st["frame_steps"], "fc_launches": st["fc_launches"], "vote_launches": st["vote_launches"],
            "root_fc_pairs": st["fc_pairs"]}
-    # k_root_fc is VALU-bound integer work: per (pair, column) one compare and
-    # one select, and one 3-input add per two columns (gfx950 ISA of the inner
-    # loop: v_cmp_lt_u32 + v_cndmask_b32 per column, v_add3_u32 per two) =
-    # 2.5 lane-ops; peak = 256 CUs x 4 SIMDs x 32 lanes x 2.4 GHz
-    # (MI355X_MICROARCH.md: wave64 VALU op = 2 cycles on a SIMD).
+    # The root-FC kernels are VALU-bound integer work.  k_root_fc (32-bit):
+    # per (pair, column) one compare and one select, and one 3-input add per
+    # two columns (gfx950 ISA of the inner loop: v_cmp_lt_u32 + v_cndmask_b32
+    # per column, v_add3_u32 per two) = 2.5 lane-ops.  k_root_fc16 (fork-free
+    # epochs with 16-bit seqs, the C5 case): per pair and two columns one
+    # v_pk_sub_u16 (clamp), one v_pk_min_u16 and one v_dot2_u32_u16 per weight
+    # half = 1.5 lane-ops per column, 2 in 32-column chunks holding a weight >=
+    # 2^16.  fc_lane_ops counts what the launches issued (padded columns);
+    # peak = 256 CUs x 4 SIMDs x 32 lanes x 2.4 GHz (MI355X_MICROARCH.md:
+    # wave64 VALU op = 2 cycles on a SIMD).
     if st["ms_root_fc_gpu"] > 0:
-        pc = st["fc_pair_cols"] / (st["ms_root_fc_gpu"] * 1e-3)
-        ach = ROOT_FC_OPS_PER_PAIR_COL * pc / 1e12
+        sec = st["ms_root_fc_gpu"] * 1e-3
+        pc = st["fc_pair_cols"] / sec
+        ach = st["fc_lane_ops"] / sec / 1e12
         res["roofline_root_fc"] = {"bound": "valu", "achieved": ach, "peak": VALU_PEAK_TOPS,
                                    "unit": "T int32 lane-ops/s", "frac": ach / VALU_PEAK_TOPS,
-                                   "pair_cols_per_s": pc, "ops_per_pair_col": ROOT_FC_OPS_PER_PAIR_COL,
+                                   "pair_cols_per_s": pc,
+                                   "ops_per_pair_col": st["fc_lane_ops"] / max(st["fc_pair_cols"], 1),
                                    "ms_per_epoch": st["ms_root_fc_gpu"]}
     lch.close()
     if want_cpu:

@@ -58,7 +58,16 @@ void lx_abft_destroy(lx_abft *a);
 const char *lx_abft_last_error(const lx_abft *a);
 /* Path selection (results never change):
  *   "spec_depth" self-children evaluated speculatively per frame step (0..16,
- *                default 4) */
+ *                default 4)
+ *   "fc16"       1 (default): fork-free epochs whose seqs fit 16 bits take the
+ *                packed root-FC kernel (two columns per dword); 0: the 32-bit
+ *                kernel always
+ *   "claimed_batch" 1 (default): a batch whose every event claims its frame
+ *                enqueues all its frame steps and waits once; 0: step by step
+ *                as in Build
+ *   "elect_ahead" rounds per election when the elections of every frame are
+ *                enqueued together and read back with one wait (2..8, default
+ *                2; 0: round by round, one wait per round) */
 int lx_abft_set_option(lx_abft *a, const char *name, int64_t value);
 
 /* ApplyGenesis + Bootstrap (abft/apply_genesis.go:17-44, bootstrap.go:30-52):
@@ -82,7 +91,9 @@ int lx_abft_reset(lx_abft *a, uint32_t epoch, uint32_t n_validators, const uint3
  *   - a block sealed the epoch: returns 0, *consumed counts the events up to
  *     the one whose processing decided the sealing frame; the rest belong to
  *     no epoch and must be re-submitted by the caller (as the reference test
- *     drivers do, abft/event_processing_test.go:145-150). */
+ *     drivers do, abft/event_processing_test.go:145-150).
+ * Every claim of the batch is checked before its elections run, so events
+ * past a sealing frame carry this epoch's frame or LX_FRAME_BUILD. */
 int lx_abft_process_batch(lx_abft *a, uint32_t n, const uint32_t *creator_idx, const uint32_t *seq,
                           const uint64_t *parent_off, const uint32_t *parent_idx, const uint32_t *claimed_frame,
                           uint32_t *out_frame, uint32_t *consumed);
@@ -110,6 +121,11 @@ typedef struct lx_abft_stats {
     uint64_t fc_pairs;   /* (event, root) pairs evaluated */
     uint64_t fc_pair_cols;   /* pairs x validator columns compared by k_root_fc */
     float ms_root_fc_gpu;    /* k_root_fc time on the stream (HIP events around each launch) */
+    uint64_t fc_lane_ops;    /* VALU lane-ops the root-FC inner loops issue (ISA count per pair and
+                                column: 2.5 in k_root_fc; 1.5 in k_root_fc16, 2 in its 32-column
+                                chunks holding a weight >= 2^16) over the padded columns */
+    uint32_t elections_ahead;   /* elections decided by run_elections_ahead (all their rounds
+                                   enqueued at once) rather than round by round */
 } lx_abft_stats;
 int lx_abft_last_stats(const lx_abft *a, lx_abft_stats *out);
 

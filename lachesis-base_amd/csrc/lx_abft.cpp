@@ -51,6 +51,7 @@ constexpr uint32_t NONE = LX_NONE;
 constexpr uint32_t kSpecDepth = 4;      // self-children evaluated ahead per launch (LX_SPEC overrides)
 constexpr uint32_t kBuildCap = 100;     // calcFrameIdx: selfParentFrame + 100 in Build
 constexpr uint32_t kVoteWindow = 64;    // subjects voted on first (chooseAtropos walks idx order)
+constexpr uint32_t kElectAhead = 2;     // rounds per election in run_elections_ahead (3: 72 vote launches, slower)
 
 // Device buffers recycled within one abft handle.  Every device operation of
 // the handle is enqueued on the index's stream, so a buffer handed back here
@@ -170,7 +171,8 @@ struct lx_abft {
     uint64_t q_pin_cap = 0;
     uint32_t *rb_pin = nullptr;         // k_readback target (decisions + error word, atropos HB row)
     uint64_t rb_cap = 0;
-    hipEvent_t ev_fc[2] = {};           // around each k_root_fc launch (stats.ms_root_fc_gpu)
+    std::vector<hipEvent_t> fc_ev;      // pairs around k_root_fc launches (stats.ms_root_fc_gpu)
+    uint32_t fc_ev_used = 0;
     std::vector<Frame> frames;          // [0] unused
     DVec<uint32_t> arena;               // bit rows (observed roots) of k_root_fc launches
     uint64_t arena_used = 0;
@@ -181,12 +183,17 @@ struct lx_abft {
     DVec<unsigned long long> d_dec;
     DVec<uint32_t> d_err;
     DVec<uint32_t> d_kcol, d_kflag, d_kw;
+    DVec<uint32_t> ea_votes, ea_err;      // elections decided ahead: vote tables, error words
+    DVec<unsigned long long> ea_dec;      // ... decision words per election x subject
     uint32_t n_k = 0;
     uint32_t k_B = NONE;                // branch count the cheater columns were built for
     std::vector<uint32_t> h_row;
     bool dec_dirty = true;
     uint32_t vw = 0;                    // subject window [0, vw) of the current election
     uint32_t spec_depth = kSpecDepth;
+    bool fc16 = true;                   // option fc16=0: k_root_fc (32-bit) even for 16-bit seqs
+    bool claimed_batch = true;          // option claimed_batch=0: claimed batches take the Build path's steps
+    uint32_t elect_ahead = kElectAhead;  // option elect_ahead: rounds per election decided ahead (0 = off)
 
     lx_abft_stats stats{};
 
@@ -311,6 +318,29 @@ int readback(lx_abft *a, hipStream_t s, const uint32_t *x, uint32_t na, const ui
     return 0;
 }
 
+// HB rows of events rows[k] into a->rb_pin (k * V), then wait for the stream
+int readback_rows(lx_abft *a, const IndexView &iv, const std::vector<uint32_t> &rows, const uint32_t **out) {
+    const uint64_t need = (uint64_t)rows.size() * a->V;
+    if (need > a->rb_cap) {
+        if (a->rb_pin) {
+            AHIP(a, hipStreamSynchronize(iv.stream));
+            (void)hipHostFree(a->rb_pin);
+        }
+        a->rb_pin = nullptr;
+        a->rb_cap = 0;
+        const uint64_t cap = std::max<uint64_t>(need * 2, 4096);
+        AHIP(a, hipHostMalloc((void **)&a->rb_pin, cap * 4, hipHostMallocMapped));
+        a->rb_cap = cap;
+    }
+    void *dp = nullptr;
+    AHIP(a, hipHostGetDevicePointer(&dp, a->rb_pin, 0));
+    AHIP(a, lx::launch_gather_rows(static_cast<uint32_t *>(dp), iv.hb, iv.stride, a->V, rows.data(),
+                                   (uint32_t)rows.size(), iv.stream));
+    AHIP(a, hipStreamSynchronize(iv.stream));
+    *out = a->rb_pin;
+    return 0;
+}
+
 Frame &frame_at(lx_abft *a, uint32_t f) {
     if (a->frames.size() <= f) a->frames.resize(f + 1);
     return a->frames[f];
@@ -393,107 +423,267 @@ int refresh_cheaters(lx_abft *a, const IndexView &iv) {
     return 0;
 }
 
-// One frame step: bits (cands x roots(f)) into the arena, q per candidate.
-int eval_frame(lx_abft *a, const IndexView &iv, uint32_t f, const std::vector<uint32_t> &cand, uint64_t *row0,
-               uint32_t *words_out, std::vector<uint8_t> &q) {
+// One frame step enqueued: bits (cands x roots(f)) into the arena at *row0,
+// q per candidate into q_dev (device-mapped pinned memory); nothing waits.
+// *launched = false when frame f has no roots (no quorum: the caller's q is 0).
+int launch_eval(lx_abft *a, const IndexView &iv, uint32_t f, const uint32_t *cand, uint32_t n, uint8_t *q_dev,
+                uint64_t *row0, uint32_t *words_out, bool *launched) {
     hipStream_t s = iv.stream;
     Frame &fr = frame_at(a, f);
     ARC(sync_frame(a, fr, s));
     const uint32_t R = (uint32_t)fr.ev.size();
     const uint32_t words = (R + 31) / 32;
-    const uint32_t n = (uint32_t)cand.size();
     *row0 = a->arena_used;
     *words_out = words;
+    *launched = false;
     ARC(reserve(a, a->arena, a->arena_used + (uint64_t)n * words + 1, a->arena_used, s));
-    ARC(reserve(a, a->d_cand, n, 0, s));
-    ARC(reserve(a, a->d_q, n, 0, s));
-    uint32_t *bits = a->arena.p + a->arena_used;
-    if (words) {
-        // queued only when this step launches (flush_uploads below): a frame
-        // without roots must not leave a pending descriptor for d_cand that a
-        // later step's upload of the same range could race with
-        a->up.add(a->d_cand.p, cand.data(), n * 4ull);
-        ARC(refresh_cheaters(a, iv));
-        if (n > a->q_pin_cap) {
-            if (a->q_pin) {
-                AHIP(a, hipStreamSynchronize(s));
-                (void)hipHostFree(a->q_pin);
-            }
-            a->q_pin = nullptr;
-            a->q_pin_cap = 0;
-            AHIP(a, hipHostMalloc((void **)&a->q_pin, std::max<uint64_t>(n, 4096), hipHostMallocMapped));
-            a->q_pin_cap = std::max<uint64_t>(n, 4096);
-        }
-        void *q_dev = nullptr;
-        AHIP(a, hipHostGetDevicePointer(&q_dev, a->q_pin, 0));
-        // split the columns when the tiles alone cannot fill the chip
-        const uint32_t ncols = (iv.V + 31) / 32 * 32;
-        const uint32_t splits = lx::root_fc_splits(n, R, ncols);
-        const uint32_t col_split = ((ncols + splits - 1) / splits + 31) / 32 * 32;
-        const uint32_t n_split = (ncols + col_split - 1) / col_split;
-        ARC(reserve(a, a->d_psum, (uint64_t)n_split * n * words * 32, 0, s));
-        RootFcArgs r{};
-        r.hb = iv.hb;
-        r.la = iv.la;
-        r.stride = iv.stride;
-        r.cand = a->d_cand.p;
-        r.n_cand = n;
-        r.roots = fr.d_ev.p;
-        r.n_roots = R;
-        r.roots_fallback = cand[0];
-        r.ncols = ncols;
-        r.wpad = iv.wpad;
-        r.quorum = a->quorum;
-        r.n_k = a->n_k;
-        r.kcol = a->d_kcol.p;
-        r.kflag = a->d_kflag.p;
-        r.kw = a->d_kw.p;
-        r.ev_branch = iv.ev_branch;
-        r.psum = a->d_psum.p;
-        r.words = words;
-        r.col_split = col_split;
-        r.n_split = n_split;
-        ARC(flush_uploads(a, s));
-        if (!a->ev_fc[0]) {
-            AHIP(a, hipEventCreate(&a->ev_fc[0]));
-            AHIP(a, hipEventCreate(&a->ev_fc[1]));
-        }
-        AHIP(a, hipEventRecord(a->ev_fc[0], s));
-        AHIP(a, lx::launch_root_fc(r, iv.B > iv.V, s));
-        AHIP(a, hipEventRecord(a->ev_fc[1], s));
-        QuorumArgs qa{};
-        qa.psum = a->d_psum.p;
-        qa.n_split = n_split;
-        qa.bits = bits;
-        qa.words = words;
-        qa.n_roots = R;
-        qa.n_cand = n;
-        qa.cand = a->d_cand.p;
-        qa.root_ev = fr.d_ev.p;
-        qa.creator = fr.d_creator.p;
-        qa.dup = fr.d_dup.p;
-        qa.wcreator = iv.wpad;
-        qa.quorum = a->quorum;
-        qa.q = static_cast<uint8_t *>(q_dev);   // answers land in pinned host memory
-        AHIP(a, lx::launch_root_quorum(qa, s));
-        AHIP(a, hipStreamSynchronize(s));
-        q.assign(a->q_pin, a->q_pin + n);
-        float ms = 0;
-        AHIP(a, hipEventElapsedTime(&ms, a->ev_fc[0], a->ev_fc[1]));
-        a->stats.ms_root_fc_gpu += ms;
-        a->stats.fc_launches++;
-        a->stats.fc_pairs += (uint64_t)n * R;
-        a->stats.fc_pair_cols += (uint64_t)n * R * iv.V;
-    } else {
-        q.assign(n, 0);   // no roots in frame f: no quorum (WeightCounter of nothing)
-    }
     a->arena_used += (uint64_t)n * words;
+    if (!words) return 0;
+    ARC(reserve(a, a->d_cand, n, 0, s));
+    uint32_t *bits = a->arena.p + *row0;
+    // queued only when this step launches (flush_uploads below): a frame
+    // without roots must not leave a pending descriptor for d_cand that a
+    // later step's upload of the same range could race with
+    a->up.add(a->d_cand.p, cand, n * 4ull);
+    ARC(refresh_cheaters(a, iv));
+    // split the columns when the tiles alone cannot fill the chip
+    const uint32_t ncols = (iv.V + 31) / 32 * 32;
+    const uint32_t splits = lx::root_fc_splits(n, R, ncols);
+    const uint32_t col_split = ((ncols + splits - 1) / splits + 31) / 32 * 32;
+    const uint32_t n_split = (ncols + col_split - 1) / col_split;
+    ARC(reserve(a, a->d_psum, (uint64_t)n_split * n * words * 32, 0, s));
+    RootFcArgs r{};
+    r.hb = iv.hb;
+    r.la = iv.la;
+    r.stride = iv.stride;
+    r.cand = a->d_cand.p;
+    r.n_cand = n;
+    r.roots = fr.d_ev.p;
+    r.n_roots = R;
+    r.roots_fallback = cand[0];
+    r.ncols = ncols;
+    r.wpad = iv.wpad;
+    r.quorum = a->quorum;
+    r.n_k = a->n_k;
+    r.kcol = a->d_kcol.p;
+    r.kflag = a->d_kflag.p;
+    r.kw = a->d_kw.p;
+    r.ev_branch = iv.ev_branch;
+    r.psum = a->d_psum.p;
+    r.words = words;
+    r.col_split = col_split;
+    r.n_split = n_split;
+    ARC(flush_uploads(a, s));
+    const uint32_t k = a->fc_ev_used;
+    while (a->fc_ev.size() < 2ull * (k + 1)) {
+        hipEvent_t e;
+        AHIP(a, hipEventCreate(&e));
+        a->fc_ev.push_back(e);
+    }
+    const bool forks = iv.B > iv.V, seq16 = a->fc16 && iv.max_seq <= 0xFFFFu;
+    AHIP(a, hipEventRecord(a->fc_ev[2 * k], s));
+    AHIP(a, lx::launch_root_fc(r, forks, seq16, s));
+    AHIP(a, hipEventRecord(a->fc_ev[2 * k + 1], s));
+    a->fc_ev_used = k + 1;
+    QuorumArgs qa{};
+    qa.psum = a->d_psum.p;
+    qa.n_split = n_split;
+    qa.bits = bits;
+    qa.words = words;
+    qa.n_roots = R;
+    qa.n_cand = n;
+    qa.cand = a->d_cand.p;
+    qa.root_ev = fr.d_ev.p;
+    qa.creator = fr.d_creator.p;
+    qa.dup = fr.d_dup.p;
+    qa.wcreator = iv.wpad;
+    qa.quorum = a->quorum;
+    qa.q = q_dev;   // answers land in pinned host memory
+    AHIP(a, lx::launch_root_quorum(qa, s));
+    a->stats.fc_launches++;
+    a->stats.fc_pairs += (uint64_t)n * R;
+    a->stats.fc_pair_cols += (uint64_t)n * R * iv.V;
+    uint64_t hi_cols = 0;   // columns of the 32-column chunks holding a weight >= 2^16
+    for (uint32_t c = 0; c < iv.V; c += 32)
+        for (uint32_t j = c; j < std::min(c + 32, iv.V); j++)
+            if (a->weights[j] >> 16) {
+                hi_cols += 32;
+                break;
+            }
+    a->stats.fc_lane_ops +=
+        (uint64_t)n * R * (!forks && seq16 ? (3 * (uint64_t)ncols + hi_cols) / 2 : 5 * (uint64_t)ncols / 2);
+    *launched = true;
+    return 0;
+}
+
+// after the stream has drained: k_root_fc times of the launches since the last call
+int collect_fc_times(lx_abft *a) {
+    for (uint32_t k = 0; k < a->fc_ev_used; k++) {
+        float ms = 0;
+        AHIP(a, hipEventElapsedTime(&ms, a->fc_ev[2 * k], a->fc_ev[2 * k + 1]));
+        a->stats.ms_root_fc_gpu += ms;
+    }
+    a->fc_ev_used = 0;
+    return 0;
+}
+
+// pinned, device-mapped q answers for n candidates (contents not kept)
+int q_buffer(lx_abft *a, uint64_t n, hipStream_t s, uint8_t **q_dev) {
+    if (n > a->q_pin_cap) {
+        if (a->q_pin) {
+            AHIP(a, hipStreamSynchronize(s));
+            (void)hipHostFree(a->q_pin);
+        }
+        a->q_pin = nullptr;
+        a->q_pin_cap = 0;
+        const uint64_t cap = std::max<uint64_t>(n, 4096);
+        AHIP(a, hipHostMalloc((void **)&a->q_pin, cap, hipHostMallocMapped));
+        a->q_pin_cap = cap;
+    }
+    void *q_dev_v = nullptr;
+    AHIP(a, hipHostGetDevicePointer(&q_dev_v, a->q_pin, 0));
+    *q_dev = static_cast<uint8_t *>(q_dev_v);
+    return 0;
+}
+
+// One frame step, answered: bits (cands x roots(f)) into the arena, q per candidate.
+int eval_frame(lx_abft *a, const IndexView &iv, uint32_t f, const std::vector<uint32_t> &cand, uint64_t *row0,
+               uint32_t *words_out, std::vector<uint8_t> &q) {
+    const uint32_t n = (uint32_t)cand.size();
+    uint8_t *q_dev = nullptr;
+    ARC(q_buffer(a, n, iv.stream, &q_dev));
+    bool launched;
+    ARC(launch_eval(a, iv, f, cand.data(), n, q_dev, row0, words_out, &launched));
+    if (!launched) {
+        q.assign(n, 0);   // no roots in frame f: no quorum (WeightCounter of nothing)
+        return 0;
+    }
+    AHIP(a, hipStreamSynchronize(iv.stream));
+    q.assign(a->q_pin, a->q_pin + n);
+    return collect_fc_times(a);
+}
+
+// Frames of a batch in which every event claims its frame (Process,
+// event_processing.go:163-189 with the claimed frame as the loop bound).
+// Taking the claims of in-batch self-parents as given, every question is
+// known up front: event i asks q_f(i) for f in [selfParentFrame(i), claim(i)),
+// and roots(f) = the roots of f so far plus the batch events claiming f or
+// more above a self-parent frame below f (Store.AddRoot adds a root to every
+// frame it passes, store_roots.go:23-27), in event order (the order
+// per-event Process adds them).  ForklessCause(i, r) is false for every r that is not an ancestor of
+// i, so roots later in event order change none of i's answers.  All frame
+// steps are enqueued back to back and answered after one wait.  Up to the
+// first event whose computed frame differs from its claim, every claim used
+// was verified, so the answers are exact there; process() redoes that prefix
+// alone (nothing after it is reported).  A claim above every root frame so far
+// + 1 cannot verify (frame top+1 has no roots): the batch is cut there.
+int compute_frames_claimed(lx_abft *a, uint64_t base, uint32_t n, const uint32_t *creator, const uint32_t *claimed) {
+    IndexView iv;
+    int rc = lx_index_view(a->ix, &iv);
+    if (rc) return a->ixfail(rc);
+    hipStream_t s = iv.stream;
+    uint32_t top = 0;   // highest frame with a root
+    for (uint32_t f = 1; f < a->frames.size(); f++)
+        if (!a->frames[f].ev.empty()) top = f;
+    std::vector<uint32_t> spf(n, 0), rf(n, NONE);
+    uint32_t cut = n, fmin = NONE, fmax = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        const uint32_t sp = a->ev_sp[base + i];
+        if (sp == NONE) {   // f = 0: roots(0) is empty -> frame 1 (:184-187)
+            rf[i] = 1;
+            top = std::max(top, 1u);
+            continue;
+        }
+        spf[i] = sp < base ? a->ev_frame[sp] : claimed[sp - base];
+        const uint32_t c = claimed[i];
+        if (spf[i] == 0 || c > top + 1) {
+            cut = i;
+            break;
+        }
+        if (c > spf[i]) {
+            rf[i] = c;
+            top = std::max(top, c);
+            fmin = std::min(fmin, spf[i]);
+            fmax = std::max(fmax, c - 1);
+        }
+    }
+    // candidates per frame step (event order) and each event's q slots
+    const uint32_t nf = fmin == NONE ? 0 : fmax - fmin + 1;
+    std::vector<std::vector<uint32_t>> cand(nf);
+    std::vector<std::vector<uint32_t>> new_roots(top + 2);
+    std::vector<uint64_t> qoff(nf + 1, 0), row0(nf, 0);
+    std::vector<uint32_t> words(nf, 0), pos0(n, 0);
+    for (uint32_t i = 0; i < cut; i++) {
+        if (a->ev_sp[base + i] == NONE) {
+            new_roots[1].push_back(i);
+            continue;
+        }
+        if (rf[i] == NONE) continue;
+        // a root of every frame it passes: spf+1 .. claim (Store.AddRoot, store_roots.go:23-27)
+        for (uint32_t f = spf[i] + 1; f <= rf[i]; f++) new_roots[f].push_back(i);
+        pos0[i] = (uint32_t)cand[spf[i] - fmin].size();   // position in its first step
+        for (uint32_t f = spf[i]; f < claimed[i]; f++) cand[f - fmin].push_back((uint32_t)(base + i));
+    }
+    for (uint32_t k = 0; k < nf; k++) qoff[k + 1] = qoff[k] + cand[k].size();
+    uint8_t *q_dev = nullptr;
+    ARC(q_buffer(a, std::max<uint64_t>(qoff[nf], 1), s, &q_dev));
+    std::vector<uint8_t> launched(nf, 0);
+    // a root's position in the step at f (binary search: cand lists are sorted)
+    auto pos_in = [&](uint32_t f, uint32_t i) {
+        const auto &c = cand[f - fmin];
+        return (uint32_t)(std::lower_bound(c.begin(), c.end(), (uint32_t)(base + i)) - c.begin());
+    };
+    uint32_t steps = 0;
+    for (uint32_t f = 1; f <= std::max(top, fmax); f++) {
+        // roots of f first (event order): their bit rows come from the step at f - 1
+        if (f < new_roots.size())
+            for (uint32_t i : new_roots[f]) {
+                if (f == 1 && a->ev_sp[base + i] == NONE) {
+                    add_slot(a, 1, (uint32_t)(base + i), creator[i], 0, 0);
+                    continue;
+                }
+                const uint32_t k = f - 1 - fmin;
+                // observed roots of f - 1 at i's turn: those before i in event order
+                const auto &nr = new_roots[f - 1];
+                const uint32_t before = (uint32_t)(std::lower_bound(nr.begin(), nr.end(), i) - nr.begin());
+                const uint32_t len = (uint32_t)(frame_at(a, f - 1).ev.size() - nr.size()) + before;
+                add_slot(a, f, (uint32_t)(base + i), creator[i], row0[k] + (uint64_t)pos_in(f - 1, i) * words[k], len);
+            }
+        if (f < fmin || f > fmax || cand[f - fmin].empty()) continue;
+        const uint32_t k = f - fmin;
+        bool l = false;
+        ARC(launch_eval(a, iv, f, cand[k].data(), (uint32_t)cand[k].size(), q_dev + qoff[k], &row0[k], &words[k], &l));
+        launched[k] = l;
+        steps++;
+    }
+    AHIP(a, hipStreamSynchronize(s));
+    ARC(collect_fc_times(a));
+    a->stats.frame_steps += steps;
+    for (uint32_t i = 0; i < n; i++) {
+        if (i >= cut) {
+            a->ev_frame[base + i] = NONE;   // never equals a claim: process() stops here
+            continue;
+        }
+        if (a->ev_sp[base + i] == NONE) {
+            a->ev_frame[base + i] = 1;
+            continue;
+        }
+        uint32_t f = spf[i];
+        for (uint32_t p = pos0[i]; f < claimed[i]; f++) {
+            const uint32_t k = f - fmin;
+            if (!launched[k] || !a->q_pin[qoff[k] + (f == spf[i] ? p : pos_in(f, i))]) break;
+        }
+        a->ev_frame[base + i] = f;
+    }
     return 0;
 }
 
 // Frames of events [base, base+n) (all already added to the index).
 // cap[i]: claimed frame (Process) or NONE = Build's selfParentFrame + 100.
 int compute_frames(lx_abft *a, uint64_t base, uint32_t n, const uint32_t *creator, const uint32_t *claimed) {
+    if (claimed && a->claimed_batch &&
+        std::none_of(claimed, claimed + n, [](uint32_t c) { return c == LX_FRAME_BUILD; }))
+        return compute_frames_claimed(a, base, n, creator, claimed);
     IndexView iv;
     int rc = lx_index_view(a->ix, &iv);
     if (rc) return a->ixfail(rc);
@@ -671,6 +861,22 @@ int widen_window(lx_abft *a, const IndexView &iv, uint32_t F, uint32_t nw) {
     return 0;
 }
 
+// chooseAtropos (SortedIDs = idx order) over the decisions of subjects
+// [0, vw): 0 pending, 1 decided (*t, *atropos slot), 2 every subject decided "no"
+int atropos_state(const unsigned long long *dec, uint32_t vw, uint64_t *t, uint32_t *obs) {
+    uint64_t tmax = 0;
+    for (uint32_t v = 0; v < vw; v++) {
+        if (dec[v] == ~0ull) return 0;
+        tmax = std::max<uint64_t>(tmax, dec[v] >> 32);
+        if (dec[v] & 0x80000000ull) {
+            *t = tmax;
+            *obs = (uint32_t)(dec[v] & kVoteNoRoot);
+            return 1;
+        }
+    }
+    return 2;
+}
+
 // decision of election F: 0 pending, 1 decided (*t, *atropos slot),
 // 2 every subject of the window decided "no" (widen it)
 int check_decision(lx_abft *a, const IndexView &iv, uint32_t F, uint64_t *t, uint32_t *obs, int *state) {
@@ -685,22 +891,8 @@ int check_decision(lx_abft *a, const IndexView &iv, uint32_t F, uint64_t *t, uin
         return a->fail(LX_ERR_BYZANTINE, "root must be forkless caused by at least 2/3W of prev roots (election frame=%u)", F);
     if (err & kVoteErrMissing)
         return a->fail(LX_ERR_BYZANTINE, "every root must vote for every not decided subject (election frame=%u)", F);
-    *state = 0;
-    uint64_t tmax = 0;
-    for (uint32_t v = 0; v < a->vw; v++) {   // chooseAtropos: SortedIDs = idx order
-        if (dec[v] == ~0ull) return 0;
-        tmax = std::max<uint64_t>(tmax, dec[v] >> 32);
-        if (dec[v] & 0x80000000ull) {
-            *t = tmax;
-            *obs = (uint32_t)(dec[v] & kVoteNoRoot);
-            *state = 1;
-            return 0;
-        }
-    }
-    if (a->vw < a->V) {
-        *state = 2;
-        return 0;
-    }
+    *state = atropos_state(dec.data(), a->vw, t, obs);
+    if (*state != 2 || a->vw < a->V) return 0;
     return a->fail(LX_ERR_BYZANTINE, "all the roots are decided as 'no', which is possible only if more than 1/3W are Byzantine");
 }
 
@@ -716,12 +908,12 @@ int reset_election(lx_abft *a, const IndexView &iv) {
 }
 
 // cheaters + confirmation DFS + callbacks; returns 1 in *sealed when EndBlock seals
+// (row: the Atropos' HB row already read back, or nullptr)
 int apply_block(lx_abft *a, const IndexView &iv, uint32_t F, uint32_t atropos, bool *sealed,
-                std::vector<uint32_t> *new_w) {
+                std::vector<uint32_t> *new_w, const uint32_t *row = nullptr) {
     *sealed = false;
     std::vector<uint32_t> cheaters;
-    const uint32_t *row = nullptr;
-    ARC(readback(a, iv.stream, iv.hb + (uint64_t)atropos * iv.stride, a->V, nullptr, 0, &row));
+    if (!row) ARC(readback(a, iv.stream, iv.hb + (uint64_t)atropos * iv.stride, a->V, nullptr, 0, &row));
     for (uint32_t c = 0; c < a->V; c++)
         if (row[c] & LX_MARK) cheaters.push_back(c);   // GetMergedHighestBefore(atropos)[c].IsForkDetected()
     if (!a->cb.begin_block) return 0;   // BeginBlock == nil: no confirmation, no seal (lachesis.go:69-71)
@@ -751,6 +943,115 @@ int apply_block(lx_abft *a, const IndexView &iv, uint32_t F, uint32_t atropos, b
     return 0;
 }
 
+// Elections decided ahead.  Election F reads only the root slots of frames
+// > F (processKnownRoots replays them after every decision), never the
+// outcome of election F-1, so the elections of every frame with two frames of
+// roots above it are enqueued together: each with its own vote tables over
+// the first subject window and its own decision words, for elect_ahead rounds
+// (frames F+1 .. F+elect_ahead), read back after one wait.  The host then
+// takes them in frame order as the step-by-step loop would: an election
+// decided and final within those rounds is applied (the Atropos HB rows of
+// all of them come back in a second wait); the first one that is not
+// (pending, every subject of the window "no", a vote error, a slot older than
+// its decision left unvoted) hands over to the step-by-step loop, which
+// redoes it from scratch.  *sealed_at as in run_elections.
+int run_elections_ahead(lx_abft *a, const IndexView &iv, uint64_t *sealed_at, std::vector<uint32_t> *new_w) {
+    hipStream_t s = iv.stream;
+    const uint32_t R = a->elect_ahead, F0 = a->last_decided + 1;
+    if (R < 2 || a->frames.size() < F0 + 3) return 0;
+    const uint32_t maxf = (uint32_t)a->frames.size() - 1;
+    const uint32_t nE = maxf - 1 - F0;    // elections F0 .. maxf - 2
+    const uint32_t vw = std::min<uint32_t>(a->V, kVoteWindow);
+    for (uint32_t f = F0; f <= maxf; f++) ARC(sync_frame(a, frame_at(a, f), s));
+    // vote tables: election e, round g -> slots(g) x vw
+    std::vector<uint64_t> voff;
+    uint64_t vtot = 0;
+    for (uint32_t e = 0; e < nE; e++)
+        for (uint32_t g = F0 + e + 1; g <= std::min(F0 + e + R, maxf); g++) {
+            voff.push_back(vtot);
+            vtot += (uint64_t)a->frames[g].ev.size() * vw;
+        }
+    ARC(reserve(a, a->ea_votes, std::max<uint64_t>(vtot, 1), 0, s));
+    ARC(reserve(a, a->ea_dec, (uint64_t)nE * vw, 0, s));
+    ARC(reserve(a, a->ea_err, nE, 0, s));
+    ARC(flush_uploads(a, s));
+    AHIP(a, hipMemsetAsync(a->ea_dec.p, 0xFF, (uint64_t)nE * vw * 8, s));
+    AHIP(a, hipMemsetAsync(a->ea_err.p, 0, nE * 4ull, s));
+    size_t vi = 0;
+    for (uint32_t e = 0; e < nE; e++) {
+        const uint32_t F = F0 + e;
+        const uint32_t *prev = nullptr;
+        for (uint32_t g = F + 1; g <= std::min(F + R, maxf); g++, vi++) {
+            Frame &fg = a->frames[g], &fp = a->frames[g - 1];
+            VoteArgs v{};
+            v.V = vw;   // row stride of these tables: subjects [0, vw) only
+            v.voter_ev = fg.d_ev.p;
+            v.bm_off = fg.d_bm_off.p;
+            v.bm_len = fg.d_bm_len.p;
+            v.bm = a->arena.p;
+            v.prev_creator = fp.d_creator.p;
+            v.prev_dup = fp.d_dup.p;
+            v.prev_votes = prev;
+            v.prev_has_dup = std::any_of(fp.dup.begin(), fp.dup.end(), [](uint32_t d) { return d != NONE; }) ? 1u : 0u;
+            v.v_lo = 0;
+            v.v_hi = vw;
+            v.wcreator = iv.wpad;
+            v.quorum = a->quorum;
+            v.votes = a->ea_votes.p + voff[vi];
+            v.dec = a->ea_dec.p + (uint64_t)e * vw;
+            v.err = a->ea_err.p + e;
+            AHIP(a, lx::launch_votes(v, (uint32_t)fg.ev.size(), g == F + 1, s));
+            a->stats.vote_launches++;
+            prev = v.votes;
+        }
+    }
+    const uint32_t *rb = nullptr;
+    ARC(readback(a, s, reinterpret_cast<const uint32_t *>(a->ea_dec.p), 2 * nE * vw, a->ea_err.p, nE, &rb));
+    std::vector<unsigned long long> dec((uint64_t)nE * vw);
+    memcpy(dec.data(), rb, dec.size() * 8);
+    std::vector<uint32_t> err(rb + 2ull * nE * vw, rb + 2ull * nE * vw + nE);
+    // decided prefix of the elections, in frame order
+    struct Decided {
+        uint32_t F, atropos;
+        uint64_t t;
+    };
+    std::vector<Decided> done;
+    std::vector<uint64_t> L(maxf + 2, ~0ull);   // L[h] = oldest slot of frames >= h
+    for (uint32_t h = maxf; h >= 1; h--) {
+        L[h] = L[h + 1];
+        for (uint32_t x : a->frames[h].ev) L[h] = std::min<uint64_t>(L[h], x);
+    }
+    for (uint32_t e = 0; e < nE; e++) {
+        const uint32_t F = F0 + e;
+        uint64_t t = 0;
+        uint32_t obs = 0;
+        if (err[e] || atropos_state(dec.data() + (uint64_t)e * vw, vw, &t, &obs) != 1) break;
+        if (t > L[std::min(F + R, maxf) + 1]) break;   // an older slot is not voted yet
+        if (obs >= a->frames[F].ev.size()) break;
+        done.push_back({F, a->frames[F].ev[obs], t});
+    }
+    if (done.empty()) return 0;
+    std::vector<uint32_t> rows(done.size());
+    for (size_t k = 0; k < done.size(); k++) rows[k] = done[k].atropos;
+    const uint32_t *hb_rows = nullptr;
+    ARC(readback_rows(a, iv, rows, &hb_rows));
+    for (size_t k = 0; k < done.size(); k++) {
+        const uint64_t decided_at = std::max<uint64_t>(done[k].t, a->t_prev);
+        bool sealed;
+        ARC(apply_block(a, iv, done[k].F, done[k].atropos, &sealed, new_w, hb_rows + k * (uint64_t)a->V));
+        if (sealed) {
+            *sealed_at = decided_at;
+            return 0;
+        }
+        a->t_prev = decided_at;
+        a->last_decided = done[k].F;
+    }
+    for (uint32_t g = 1; g <= a->last_decided && g < a->frames.size(); g++) a->frames[g].votes.release();
+    a->dec_dirty = true;
+    a->stats.elections_ahead += (uint32_t)done.size();
+    return 0;
+}
+
 // Runs elections over all known root slots; *sealed_at = event that decided a
 // sealing frame (NONE if none).
 int run_elections(lx_abft *a, uint64_t *sealed_at, std::vector<uint32_t> *new_w) {
@@ -758,6 +1059,8 @@ int run_elections(lx_abft *a, uint64_t *sealed_at, std::vector<uint32_t> *new_w)
     IndexView iv;
     int rc = lx_index_view(a->ix, &iv);
     if (rc) return a->ixfail(rc);
+    ARC(run_elections_ahead(a, iv, sealed_at, new_w));
+    if (*sealed_at != ~0ull) return 0;
     for (;;) {
         const uint32_t F = a->last_decided + 1;
         if (a->dec_dirty) ARC(reset_election(a, iv));
@@ -939,12 +1242,14 @@ void lx_abft_destroy(lx_abft *a) {
     a->d_kcol.release();
     a->d_kflag.release();
     a->d_kw.release();
+    a->ea_votes.release();
+    a->ea_err.release();
+    a->ea_dec.release();
     (void)hipDeviceSynchronize();   // queued work may still use pooled buffers
     a->up.release();
     if (a->q_pin) (void)hipHostFree(a->q_pin);
     if (a->rb_pin) (void)hipHostFree(a->rb_pin);
-    for (hipEvent_t e : a->ev_fc)
-        if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : a->fc_ev) (void)hipEventDestroy(e);
     a->pool.drain();
     delete a;
 }
@@ -966,6 +1271,15 @@ int lx_abft_set_option(lx_abft *a, const char *name, int64_t value) {
     if (k == "spec_depth") {
         if (value < 0 || value > 16) return a->fail(LX_ERR_ARG, "spec_depth must be 0..16");
         a->spec_depth = (uint32_t)value;
+    } else if (k == "fc16") {
+        if (value < 0 || value > 1) return a->fail(LX_ERR_ARG, "fc16 must be 0 or 1");
+        a->fc16 = value != 0;
+    } else if (k == "claimed_batch") {
+        if (value < 0 || value > 1) return a->fail(LX_ERR_ARG, "claimed_batch must be 0 or 1");
+        a->claimed_batch = value != 0;
+    } else if (k == "elect_ahead") {
+        if (value < 0 || value > 8 || value == 1) return a->fail(LX_ERR_ARG, "elect_ahead must be 0 or 2..8");
+        a->elect_ahead = (uint32_t)value;
     } else {
         return a->fail(LX_ERR_ARG, "unknown option %s", name);
     }

@@ -156,6 +156,135 @@ __global__ __launch_bounds__(256) void k_root_fc(RootFcArgs a) {
     }
 }
 
+// k_root_fc16: the fork-free k_root_fc for epochs whose seqs fit 16 bits
+// (every HB and LA entry <= 0xFFFF).  Two columns share a dword in LDS and one
+// packed subtract with unsigned saturation, one packed min and one 2-way dot
+// product per weight half take a pair over two columns:
+//   max(h - l', 0) != 0  <=>  l' < h      (l' = la - 1 in 16 bits: la = 0
+//   never counts, as 0xFFFF < h is false for h <= 0xFFFF)
+// min(., 1) is the 0/1 term, and dot2(term, {w_j, w_j+1}) adds the weights of
+// both columns; weights >= 2^16 take a second dot2 on their high halves
+// (uniform per LDS chunk: __syncthreads_or of the chunk's high halves).
+// 1.5 VALU ops per (pair, column) with 16-bit weights, 2 otherwise, against 3
+// (compare, select, add) in k_root_fc.
+constexpr int kKp = kKc / 2;   // packed dwords per LDS chunk
+
+typedef unsigned short lx_u16x2 __attribute__((ext_vector_type(2)));
+// min against an opaque {1, 1}: with a literal one clang rewrites the
+// saturating-sub + min pair into two compares and two selects per half
+__device__ __forceinline__ uint32_t fc16_term(uint32_t h, uint32_t l, uint32_t ones) {
+    const lx_u16x2 d = __builtin_elementwise_sub_sat(__builtin_bit_cast(lx_u16x2, h), __builtin_bit_cast(lx_u16x2, l));
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(d, __builtin_bit_cast(lx_u16x2, ones)));
+}
+
+__device__ __forceinline__ uint32_t udot2(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_udot2(__builtin_bit_cast(lx_u16x2, a), __builtin_bit_cast(lx_u16x2, b), c, false);
+}
+
+__global__ __launch_bounds__(256) void k_root_fc16(RootFcArgs a) {
+    __shared__ uint32_t sH[kKp][kLdsPitch];
+    __shared__ uint32_t sL[kKp][kLdsPitch];
+    __shared__ uint32_t sWl[kKp], sWh[kKp];
+
+    const uint32_t tid = threadIdx.x;
+    const uint32_t tx = tid & 15, ty = tid >> 4;          // roots tx*4.., events ty*4..
+    const uint32_t r0 = blockIdx.x * kTile, e0 = blockIdx.y * kTile;
+
+    // staging role: row = tid / 4, 8 columns = (tid % 4) * 8 -> 4 packed dwords
+    const uint32_t srow = tid >> 2, spart = (tid & 3) * 8;
+    const uint32_t se = e0 + srow < a.n_cand ? a.cand[e0 + srow] : a.cand[0];
+    uint32_t sr = r0 + srow < a.n_roots ? a.roots[r0 + srow] : LX_NONE;
+    if (sr == LX_NONE) sr = a.roots_fallback;
+    const uint4 *hrow = reinterpret_cast<const uint4 *>(a.hb + (uint64_t)se * a.stride + spart);
+    const uint4 *lrow = reinterpret_cast<const uint4 *>(a.la + (uint64_t)sr * a.stride + spart);
+
+    uint32_t ones = 0x00010001u;
+    asm("" : "+v"(ones));   // opaque (fc16_term)
+    uint32_t lo[4][4], hi[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+        for (int k = 0; k < 4; k++) lo[i][k] = hi[i][k] = 0;
+
+    const uint32_t cs = a.col_split, jlo = blockIdx.z * cs, jhi = jlo + cs < a.ncols ? jlo + cs : a.ncols;
+    for (uint32_t j0 = jlo; j0 < jhi; j0 += kKc) {
+        const uint4 h0 = hrow[j0 / 4], h1 = hrow[j0 / 4 + 1];
+        const uint4 l0 = lrow[j0 / 4], l1 = lrow[j0 / 4 + 1];
+        const uint32_t hv[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+        const uint32_t lv[8] = {l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, l1.z, l1.w};
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            sH[spart / 2 + q][srow] = hv[2 * q] | (hv[2 * q + 1] << 16);
+            sL[spart / 2 + q][srow] = ((lv[2 * q] - 1u) & 0xFFFFu) | ((lv[2 * q + 1] - 1u) << 16);
+        }
+        uint32_t wh = 0;
+        if (tid < kKp) {
+            const uint32_t w0 = a.wpad[j0 + 2 * tid], w1 = a.wpad[j0 + 2 * tid + 1];
+            sWl[tid] = (w0 & 0xFFFFu) | (w1 << 16);
+            wh = (w0 >> 16) | (w1 & 0xFFFF0000u);
+            sWh[tid] = wh;
+        }
+        const bool any_hi = __syncthreads_or(wh != 0);
+        if (any_hi) {
+#pragma unroll 4
+            for (int j = 0; j < kKp; j++) {
+                const uint4 h = *reinterpret_cast<const uint4 *>(&sH[j][ty * 4]);
+                const uint4 l = *reinterpret_cast<const uint4 *>(&sL[j][tx * 4]);
+                const uint32_t wl = sWl[j], wv = sWh[j];
+                const uint32_t hh[4] = {h.x, h.y, h.z, h.w};
+                const uint32_t ll[4] = {l.x, l.y, l.z, l.w};
+uint32_t t[4][4];
+#pragma unroll
+                for (int i = 0; i < 4; i++)
+#pragma unroll
+                    for (int k = 0; k < 4; k++) t[i][k] = fc16_term(hh[i], ll[k], ones);
+#pragma unroll
+                for (int i = 0; i < 4; i++)
+#pragma unroll
+                    for (int k = 0; k < 4; k++) {
+                        lo[i][k] = udot2(t[i][k], wl, lo[i][k]);
+                        hi[i][k] = udot2(t[i][k], wv, hi[i][k]);
+                    }
+            }
+        } else {
+#pragma unroll 4
+            for (int j = 0; j < kKp; j++) {
+                const uint4 h = *reinterpret_cast<const uint4 *>(&sH[j][ty * 4]);
+                const uint4 l = *reinterpret_cast<const uint4 *>(&sL[j][tx * 4]);
+                const uint32_t wl = sWl[j];
+                const uint32_t hh[4] = {h.x, h.y, h.z, h.w};
+                const uint32_t ll[4] = {l.x, l.y, l.z, l.w};
+uint32_t t[4][4];
+#pragma unroll
+                for (int i = 0; i < 4; i++)
+#pragma unroll
+                    for (int k = 0; k < 4; k++) t[i][k] = fc16_term(hh[i], ll[k], ones);
+#pragma unroll
+                for (int i = 0; i < 4; i++)
+#pragma unroll
+                    for (int k = 0; k < 4; k++) lo[i][k] = udot2(t[i][k], wl, lo[i][k]);
+            }
+        }
+        __syncthreads();
+    }
+
+    // partial stake sums of this column split (no cheaters, no early-false flag)
+    const uint32_t rp = a.words * 32;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const uint32_t ei = e0 + ty * 4 + i;
+        if (ei >= a.n_cand) continue;
+        uint4 o;
+        o.x = lo[i][0] + (hi[i][0] << 16);
+        o.y = lo[i][1] + (hi[i][1] << 16);
+        o.z = lo[i][2] + (hi[i][2] << 16);
+        o.w = lo[i][3] + (hi[i][3] << 16);
+        const uint32_t ri = r0 + tx * 4;
+        if (ri < rp)
+            *reinterpret_cast<uint4 *>(a.psum + ((uint64_t)blockIdx.z * a.n_cand + ei) * rp + ri) = o;
+    }
+}
+
 uint32_t root_fc_splits(uint32_t n_cand, uint32_t n_roots, uint32_t ncols) {
     // enough workgroups to fill 256 CUs x 4, at least 4 LDS chunks per split
     const uint32_t tiles = ((n_roots + kTile - 1) / kTile) * ((n_cand + kTile - 1) / kTile);
@@ -165,10 +294,11 @@ uint32_t root_fc_splits(uint32_t n_cand, uint32_t n_roots, uint32_t ncols) {
     return s < 1 ? 1 : (s > max_s ? max_s : s);
 }
 
-hipError_t launch_root_fc(const RootFcArgs &a, bool forks, hipStream_t s) {
+hipError_t launch_root_fc(const RootFcArgs &a, bool forks, bool seq16, hipStream_t s) {
     if (!a.n_cand || !a.words) return hipSuccess;
     dim3 grid((a.n_roots + kTile - 1) / kTile, (a.n_cand + kTile - 1) / kTile, a.n_split);
-    if (forks) hipLaunchKernelGGL(k_root_fc<true>, grid, dim3(256), 0, s, a);
+    if (!forks && seq16) hipLaunchKernelGGL(k_root_fc16, grid, dim3(256), 0, s, a);
+    else if (forks) hipLaunchKernelGGL(k_root_fc<true>, grid, dim3(256), 0, s, a);
     else hipLaunchKernelGGL(k_root_fc<false>, grid, dim3(256), 0, s, a);
     return hipGetLastError();
 }
@@ -435,6 +565,33 @@ hipError_t launch_readback(uint32_t *dst, const uint32_t *a, uint32_t na, const 
     const uint32_t n = na + nb;
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(k_readback, dim3((n + 255) / 256), dim3(256), 0, s, dst, a, na, b, nb);
+    return hipGetLastError();
+}
+
+// Rows src[row[k]] (V words each) into dst[k * V] -- the Atropos HB rows of
+// the elections decided ahead, written into pinned, device-mapped memory.
+constexpr uint32_t kGatherRows = 64;
+struct RowList {
+    uint32_t row[kGatherRows];
+};
+
+__global__ __launch_bounds__(256) void k_gather_rows(uint32_t *dst, const uint32_t *src, uint64_t stride, uint32_t V,
+                                                     RowList l) {
+    const uint32_t k = blockIdx.y;
+    for (uint32_t c = blockIdx.x * 256 + threadIdx.x; c < V; c += gridDim.x * 256)
+        dst[(uint64_t)k * V + c] = src[(uint64_t)l.row[k] * stride + c];
+}
+
+hipError_t launch_gather_rows(uint32_t *dst, const uint32_t *src, uint64_t stride, uint32_t V, const uint32_t *rows,
+                              uint32_t n, hipStream_t s) {
+    for (uint32_t k0 = 0; k0 < n; k0 += kGatherRows) {
+        RowList l{};
+        const uint32_t m = n - k0 < kGatherRows ? n - k0 : kGatherRows;
+        for (uint32_t k = 0; k < m; k++) l.row[k] = rows[k0 + k];
+        const uint32_t gx = (V + 255) / 256 < 4 ? (V + 255) / 256 : 4;
+        hipLaunchKernelGGL(k_gather_rows, dim3(gx ? gx : 1, m), dim3(256), 0, s, dst + (uint64_t)k0 * V, src, stride, V,
+                           l);
+    }
     return hipGetLastError();
 }
 

@@ -3549,6 +3549,7 @@ int lx_index_view(lx_index *h, IndexView *o) {
     o->V = h->V;
     o->B = h->B;
     o->quorum = h->quorum;
+    o->max_seq = h->max_seq;
     o->wpad = h->wpad;
     o->ev_branch = h->ev_branch;
     o->ev_creator = h->ev_creator;

@@ -325,7 +325,7 @@ int fcc_tile(lx_index *h, FcCache *c) {
     r.words = words;
     r.col_split = col_split;
     r.n_split = n_split;
-    HIPCHK(h, lx::launch_root_fc(r, h->B > h->V, h->stream));
+    HIPCHK(h, lx::launch_root_fc(r, h->B > h->V, h->pack16 && h->max_seq <= 0xFFFFu, h->stream));
     HIPCHK(h, lx::launch_fc_tile_out(c->d_psum, n_split, n, rp, n, h->quorum, c->g7_d, c->M_dev, c->W, h->stream));
     c->st.tile_fills++;
     c->st.pairs += (uint64_t)n * n;

@@ -766,13 +766,15 @@ hipError_t launch_qi_median(const QiArgs &a, hipStream_t s);
 hipError_t launch_qi_metric(const QiArgs &a, const uint32_t *ev, uint32_t n, uint32_t cap, unsigned long long *out,
                             hipStream_t s);
 uint32_t root_fc_splits(uint32_t n_cand, uint32_t n_roots, uint32_t ncols);
-hipError_t launch_root_fc(const RootFcArgs &a, bool forks, hipStream_t s);
+hipError_t launch_root_fc(const RootFcArgs &a, bool forks, bool seq16, hipStream_t s);
 hipError_t launch_root_quorum(const QuorumArgs &a, hipStream_t s);
 hipError_t launch_fc_tile_out(const uint32_t *psum, uint32_t n_split, uint32_t n_cand, uint32_t rp, uint32_t n_roots,
                               uint32_t quorum, const uint8_t *tag, uint8_t *out, uint64_t pitch, hipStream_t s);
 hipError_t launch_votes(const VoteArgs &a, uint32_t n_voters, bool round1, hipStream_t s);
 hipError_t launch_scatter(const ScatterDesc *desc, uint32_t n, uint64_t max_bytes, const uint8_t *base,
                           hipStream_t s);
+hipError_t launch_gather_rows(uint32_t *dst, const uint32_t *src, uint64_t stride, uint32_t V, const uint32_t *rows,
+                              uint32_t n, hipStream_t s);
 hipError_t launch_readback(uint32_t *dst, const uint32_t *a, uint32_t na, const uint32_t *b, uint32_t nb,
                            hipStream_t s);
 hipError_t launch_copy_rows(uint32_t *dst, uint64_t dst_stride, const uint32_t *src, uint64_t src_stride,
@@ -789,6 +791,7 @@ struct IndexView {
     uint64_t stride;
     uint64_t n_events;
     uint32_t V, B, quorum;
+    uint32_t max_seq;            // largest seq indexed this epoch
     const uint32_t *wpad;
     const uint32_t *ev_branch;
     const uint32_t *ev_creator;

@@ -78,7 +78,8 @@ class AbftStats(ctypes.Structure):
     _fields_ = [("ms_index", ctypes.c_float), ("ms_frames", ctypes.c_float), ("ms_election", ctypes.c_float),
                 ("ms_blocks", ctypes.c_float), ("frame_steps", ctypes.c_uint32), ("fc_launches", ctypes.c_uint32),
                 ("vote_launches", ctypes.c_uint32), ("blocks", ctypes.c_uint32), ("fc_pairs", ctypes.c_uint64),
-                ("fc_pair_cols", ctypes.c_uint64), ("ms_root_fc_gpu", ctypes.c_float)]
+                ("fc_pair_cols", ctypes.c_uint64), ("ms_root_fc_gpu", ctypes.c_float),
+                ("fc_lane_ops", ctypes.c_uint64), ("elections_ahead", ctypes.c_uint32)]
 
 
 class _StoreView:

@@ -1,9 +1,13 @@
 set -o pipefail
-mkdir -p gpurun_out/r06_recpf
-# record prefetch A/B, settings interleaved walk by walk in each process
-for i in 1 2 3; do
-  WL_OPT=rec_pf WL_VALUES=0,24,64,160 WL_ROUNDS=3 timeout -k 10 300 python3 scripts/probes/walk_lock_ab.py >> gpurun_out/r06_recpf/recpf_ab.jsonl 2>> gpurun_out/r06_recpf/recpf_ab.err || exit $?
-done
-
-AB_ROUNDS=4 timeout -k 10 300 python3 scripts/probes/abft_rfc_ab.py > gpurun_out/r06_recpf/abft_rfc_ab.jsonl 2> gpurun_out/r06_recpf/abft_rfc_ab.err || exit $?
-cat gpurun_out/r06_recpf/abft_rfc_ab.jsonl
+O=gpurun_out/r06_fc16
+mkdir -p $O
+timeout -k 10 900 python -u -m pytest -x -v --timeout 600 --timeout-method thread tests/test_gpu_abft.py tests/test_gpu_fccache.py tests/test_gpu_dropin.py > $O/pytest.log 2>&1
+rc=$?; tail -5 $O/pytest.log; [ $rc = 0 ] || exit $rc
+timeout -k 10 300 python3 scripts/probes/abft_fc16_ab.py > $O/fc16_ab.jsonl 2> $O/fc16_ab.err || exit $?
+cat $O/fc16_ab.jsonl
+AB_OPT=claimed_batch timeout -k 10 300 python3 scripts/probes/abft_fc16_ab.py > $O/claimed_batch_ab.jsonl 2> $O/claimed_batch_ab.err || exit $?
+cat $O/claimed_batch_ab.jsonl
+AB_OPT=elect_ahead AB_VALUES=3,0,2 timeout -k 10 300 python3 scripts/probes/abft_fc16_ab.py > $O/elect_ahead_ab.jsonl 2> $O/elect_ahead_ab.err || exit $?
+cat $O/elect_ahead_ab.jsonl
+timeout -k 10 300 python3 scripts/bench_abft_only.py 5 > $O/abft_leg.json 2> $O/abft_leg.err || exit $?
+cat $O/abft_leg.json

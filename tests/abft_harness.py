@@ -14,12 +14,14 @@ class FakeLachesis:
     """TestLachesis of abft/common_test.go:30-115 over the oracle (``index`` = a vecfc.Index
     restatement)."""
 
-    def __init__(self, weights_by_id, index=None, backend="oracle"):
+    def __init__(self, weights_by_id, index=None, backend="oracle", options=None):
         self.events = {}
         if backend == "gpu":
             # the product: lachesis_hip.abft over the HIP library
             from lachesis_hip import abft
             self.lch = abft.IndexedLachesis(pos.Validators(weights_by_id), epoch=ao.FIRST_EPOCH)
+            for k, v in (options or {}).items():
+                self.lch.set_option(k, v)
             self.store = self.lch.store
         else:
             self.store = ao.Store()

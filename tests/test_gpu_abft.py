@@ -51,10 +51,11 @@ def gen_events(weights, cheaters, events_per_node, parent_count, seed, forks=10)
     return nodes, evs
 
 
-def run(backend, nodes, weights, evs, mode, chunk=None, seal_every=None, mutate=False):
-    """Processes evs (frames computed by Build semantics) and returns the
-    observable results."""
-    t = FakeLachesis(dict(zip(nodes, weights)), backend=backend)
+def run(backend, nodes, weights, evs, mode, chunk=None, seal_every=None, mutate=False, options=None, claim=None):
+    """Processes evs (frames computed by Build semantics, or claimed: claim =
+    {event id: frame}, Process's checkAndSaveEvent) and returns the observable
+    results."""
+    t = FakeLachesis(dict(zip(nodes, weights)), backend=backend, options=options)
     sealed_at = []
     if seal_every:
         def apply_block(block):
@@ -72,8 +73,8 @@ def run(backend, nodes, weights, evs, mode, chunk=None, seal_every=None, mutate=
         else:
             part = evs[i:i + (chunk or len(evs))]
         for e in part:
-            e.frame = 0
-        consumed, err = t.process_batch(part, claimed=False)
+            e.frame = claim[e.id] if claim else 0
+        consumed, err = t.process_batch(part, claimed=bool(claim))
         assert err is None, err
         for e in part[:consumed]:
             frames[e.id] = e.frame
@@ -98,29 +99,47 @@ SHAPES = [
 ]
 
 
+@pytest.mark.parametrize("fc16", [1, 0])
 @pytest.mark.parametrize("shape", SHAPES, ids=[str(i) for i in range(len(SHAPES))])
-def test_abft_matches_oracle(shape):
+def test_abft_matches_oracle(shape, fc16):
+    """fc16: fork-free epochs take the packed root-FC kernel (k_root_fc16,
+    16-bit seqs; shape 6's weights >= 2^16 take its high-half dot products)
+    or the 32-bit one."""
     weights, cheaters, epn, pc, seed = shape
     nodes, evs = gen_events(weights, cheaters, epn, pc, seed)
     ref = run("oracle", nodes, weights, evs, "event")
     assert len(ref["blocks"]) >= 3
     for mode, chunk in (("event", None), ("batch", None), ("batch", 7), ("batch", 64)):
-        got = run("gpu", nodes, weights, evs, mode, chunk)
+        got = run("gpu", nodes, weights, evs, mode, chunk, options={"fc16": fc16})
         assert got["frames"] == ref["frames"], (mode, chunk)
         assert got["blocks"] == ref["blocks"], (mode, chunk)
         assert got["last"] == ref["last"], (mode, chunk)
+    # claimed frames (Process): all frame steps of a batch enqueued at once
+    # (claimed_batch) or step by step; elections decided ahead (elect_ahead
+    # rounds each, one wait) or round by round (0)
+    for cb, chunk, ea in ((1, None, 3), (1, 7, 3), (0, None, 0), (1, None, 2), (1, 64, 0)):
+        got = run("gpu", nodes, weights, evs, "batch", chunk,
+                  options={"fc16": fc16, "claimed_batch": cb, "elect_ahead": ea}, claim=ref["frames"])
+        assert got["frames"] == ref["frames"], ("claimed", cb, chunk, ea)
+        assert got["blocks"] == ref["blocks"], ("claimed", cb, chunk, ea)
+        assert got["last"] == ref["last"], ("claimed", cb, chunk, ea)
 
 
+@pytest.mark.parametrize("elect_ahead", [3, 0])
 @pytest.mark.parametrize("mutate", [False, True])
-def test_abft_seal_matches_oracle(mutate):
+def test_abft_seal_matches_oracle(mutate, elect_ahead):
     """Epoch sealed by EndBlock: same sealing event, same blocks, validators
     mutated or not (frame_decide.go:11-58)."""
     weights = [1, 2, 1, 2, 1, 2, 1, 2, 1, 2]
     nodes, evs = gen_events(weights, 0, 60, 5, 11)
     ref = run("oracle", nodes, weights, evs, "event", seal_every=3, mutate=mutate)
     assert ref["sealed_at"]
-    for chunk in (None, 50):
-        got = run("gpu", nodes, weights, evs, "batch", chunk, seal_every=3, mutate=mutate)
+    # claimed: the events up to the sealing one (the later ones' frames belong
+    # to the next epoch; a batch checks every claim before its elections)
+    upto = [e for e in evs if e.id in ref["frames"]]
+    for chunk, claim in ((None, None), (50, None), (None, ref["frames"]), (50, ref["frames"])):
+        got = run("gpu", nodes, weights, upto if claim else evs, "batch", chunk, seal_every=3, mutate=mutate,
+                  claim=claim, options={"elect_ahead": elect_ahead})
         assert got["sealed_at"] == ref["sealed_at"]
         assert got["blocks"] == ref["blocks"]
         assert got["last"] == ref["last"]
@@ -173,20 +192,37 @@ def test_abft_three_instances_reordered_gpu():
     compare_results(lchs)
 
 
-def test_abft_wrong_frame_gpu():
+@pytest.mark.parametrize("delta", [1, -1, 1000])
+@pytest.mark.parametrize("claimed_batch", [1, 0])
+def test_abft_wrong_frame_gpu(delta, claimed_batch):
     """checkAndSaveEvent: a wrong claimed frame is rejected (ErrWrongFrame),
-    the events before it are processed, the event is dropped from the index."""
+    the events before it are processed, the event is dropped from the index.
+    delta 1000: a claim above every root frame (the batched path cuts there);
+    delta -1: an under-claim, which calcFrameIdx's loop bound accepts
+    (event_processing.go:180-186) -- the oracle, Process per event on the same
+    claims, says where the first error falls."""
     weights = [1, 1, 1, 1]
     nodes, evs = gen_events(weights, 0, 30, 3, 21)
     ref = run("oracle", nodes, weights, evs, "event")
-    t = FakeLachesis(dict(zip(nodes, weights)), backend="gpu")
+    t = FakeLachesis(dict(zip(nodes, weights)), backend="gpu", options={"claimed_batch": claimed_batch})
     good = [ref["frames"][e.id] for e in evs]
     bad = next(i for i, e in enumerate(evs) if i > 40 and ao.self_parent(e) is not None)
     for e, f in zip(evs, good):
         e.frame = f
-    evs[bad].frame = good[bad] + 1
+    evs[bad].frame = good[bad] + delta
+    o = FakeLachesis(dict(zip(nodes, weights)))
+    o_consumed = len(evs)
+    for i, e in enumerate(evs):
+        if o.process(e) is not None:
+            o_consumed = i
+            break
     consumed, err = t.process_batch(evs)
-    assert consumed == bad and err is not None
+    assert consumed == o_consumed and (err is None) == (o_consumed == len(evs))
+    assert [e.frame for e in evs[:consumed]] == [o.frame_of(e.id) for e in evs[:consumed]]
+    assert t.block_list == o.block_list
+    if delta == -1:
+        return
+    assert consumed == bad
     evs[bad].frame = good[bad]
     consumed2, err = t.process_batch(evs[bad:])
     assert err is None and consumed2 == len(evs) - bad
@@ -226,8 +262,10 @@ def blocks_of(g):
     return out
 
 
-@pytest.mark.parametrize("name,chunks", [("c4", 1), ("c4", 7), ("c5", 1), ("c5", 3)])
-def test_abft_full_size_vs_oracle(name, chunks):
+@pytest.mark.parametrize("name,chunks,fc16,claimed", [("c4", 1, 1, 0), ("c4", 7, 1, 0), ("c5", 1, 1, 0), ("c5", 3, 1, 0),
+                                                      ("c5", 1, 0, 0), ("c4", 1, 1, 1), ("c4", 7, 1, 1),
+                                                      ("c5", 1, 1, 1), ("c5", 3, 0, 1)])
+def test_abft_full_size_vs_oracle(name, chunks, fc16, claimed):
     """BASELINE configs 4 (100 validators, 10 % double-signers, 100k events)
     and 5 (1000 validators, Zipf stakes, 50k events) at full size: frames of
     every event, roots per frame and every block (Atropos, cheaters, ApplyEvent
@@ -239,11 +277,13 @@ def test_abft_full_size_vs_oracle(name, chunks):
     V, epn, P, ch, fk, seed = map(int, g["config"])
     d = tools.gen_dag(V, epn, P, cheaters=ch, forks=fk, seed=seed)
     lch = abft.DenseLachesis(g["weights"], event_capacity=len(d))
+    lch.set_option("fc16", fc16)   # c5 (Zipf stakes, no forks): packed root-FC kernel unless 0
     frames = np.zeros(len(d), dtype=np.uint32)
     bounds = np.linspace(0, len(d), chunks + 1).astype(np.int64)
     for lo, hi in zip(bounds[:-1], bounds[1:]):
         c, s, off, par = d.slice(lo, hi)
-        rc, consumed, out = lch.process_batch(c, s, off, par)
+        # claimed: the golden frames as Process's claims (bench.py's abft leg)
+        rc, consumed, out = lch.process_batch(c, s, off, par, g["frames"][lo:hi] if claimed else None)
         assert rc == 0 and consumed == hi - lo
         frames[lo:hi] = out
 
