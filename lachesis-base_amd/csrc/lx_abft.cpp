@@ -185,6 +185,9 @@ struct lx_abft {
     DVec<uint32_t> d_kcol, d_kflag, d_kw;
     DVec<uint32_t> ea_votes, ea_err;      // elections decided ahead: vote tables, error words
     DVec<unsigned long long> ea_dec;      // ... decision words per election x subject
+    DVec<VoteArgs> ea_args;               // ... launch args, grouped by round
+    DVec<RootFcArgs> d_fcargs;            // merged frame steps of a claimed batch: per-step args
+    DVec<QuorumArgs> d_qargs;
     uint32_t n_k = 0;
     uint32_t k_B = NONE;                // branch count the cheater columns were built for
     std::vector<uint32_t> h_row;
@@ -423,6 +426,21 @@ int refresh_cheaters(lx_abft *a, const IndexView &iv) {
     return 0;
 }
 
+// VALU lane-ops per (event, root) pair of the root-FC inner loops (ISA count):
+// 2.5 per column in k_root_fc, 1.5 in k_root_fc16 (2 in its 32-column chunks
+// holding a weight >= 2^16), over the padded columns
+uint64_t fc_ops_per_pair(const lx_abft *a, const IndexView &iv, bool forks, bool seq16, uint32_t ncols) {
+    if (forks || !seq16) return 5 * (uint64_t)ncols / 2;
+    uint64_t hi_cols = 0;
+    for (uint32_t c = 0; c < iv.V; c += 32)
+        for (uint32_t j = c; j < std::min(c + 32, iv.V); j++)
+            if (a->weights[j] >> 16) {
+                hi_cols += 32;
+                break;
+            }
+    return (3 * (uint64_t)ncols + hi_cols) / 2;
+}
+
 // One frame step enqueued: bits (cands x roots(f)) into the arena at *row0,
 // q per candidate into q_dev (device-mapped pinned memory); nothing waits.
 // *launched = false when frame f has no roots (no quorum: the caller's q is 0).
@@ -503,15 +521,7 @@ int launch_eval(lx_abft *a, const IndexView &iv, uint32_t f, const uint32_t *can
     a->stats.fc_launches++;
     a->stats.fc_pairs += (uint64_t)n * R;
     a->stats.fc_pair_cols += (uint64_t)n * R * iv.V;
-    uint64_t hi_cols = 0;   // columns of the 32-column chunks holding a weight >= 2^16
-    for (uint32_t c = 0; c < iv.V; c += 32)
-        for (uint32_t j = c; j < std::min(c + 32, iv.V); j++)
-            if (a->weights[j] >> 16) {
-                hi_cols += 32;
-                break;
-            }
-    a->stats.fc_lane_ops +=
-        (uint64_t)n * R * (!forks && seq16 ? (3 * (uint64_t)ncols + hi_cols) / 2 : 5 * (uint64_t)ncols / 2);
+    a->stats.fc_lane_ops += (uint64_t)n * R * fc_ops_per_pair(a, iv, forks, seq16, ncols);
     *launched = true;
     return 0;
 }
@@ -633,32 +643,130 @@ int compute_frames_claimed(lx_abft *a, uint64_t base, uint32_t n, const uint32_t
         const auto &c = cand[f - fmin];
         return (uint32_t)(std::lower_bound(c.begin(), c.end(), (uint32_t)(base + i)) - c.begin());
     };
-    uint32_t steps = 0;
-    for (uint32_t f = 1; f <= std::max(top, fmax); f++) {
-        // roots of f first (event order): their bit rows come from the step at f - 1
-        if (f < new_roots.size())
-            for (uint32_t i : new_roots[f]) {
-                if (f == 1 && a->ev_sp[base + i] == NONE) {
-                    add_slot(a, 1, (uint32_t)(base + i), creator[i], 0, 0);
-                    continue;
-                }
-                const uint32_t k = f - 1 - fmin;
-                // observed roots of f - 1 at i's turn: those before i in event order
-                const auto &nr = new_roots[f - 1];
-                const uint32_t before = (uint32_t)(std::lower_bound(nr.begin(), nr.end(), i) - nr.begin());
-                const uint32_t len = (uint32_t)(frame_at(a, f - 1).ev.size() - nr.size()) + before;
-                add_slot(a, f, (uint32_t)(base + i), creator[i], row0[k] + (uint64_t)pos_in(f - 1, i) * words[k], len);
+    // layout: step k (frame fmin + k) asks cand[k] against every root of its
+    // frame (the ones so far + this batch's), bit rows at row0[k] in the arena
+    const uint64_t arena0 = a->arena_used;
+    std::vector<uint32_t> nroots(nf, 0);
+    for (uint32_t k = 0; k < nf; k++) {
+        const uint32_t f = fmin + k;
+        nroots[k] = (uint32_t)(frame_at(a, f).ev.size() + (f < new_roots.size() ? new_roots[f].size() : 0));
+        words[k] = (nroots[k] + 31) / 32;
+        row0[k] = a->arena_used;
+        a->arena_used += (uint64_t)cand[k].size() * words[k];
+        launched[k] = !cand[k].empty() && words[k];
+    }
+    // the roots, frame by frame in event order: a root of f observes the step at f - 1
+    for (uint32_t f = 1; f < new_roots.size(); f++)
+        for (uint32_t i : new_roots[f]) {
+            if (f == 1 && a->ev_sp[base + i] == NONE) {
+                add_slot(a, 1, (uint32_t)(base + i), creator[i], 0, 0);
+                continue;
             }
-        if (f < fmin || f > fmax || cand[f - fmin].empty()) continue;
-        const uint32_t k = f - fmin;
-        bool l = false;
-        ARC(launch_eval(a, iv, f, cand[k].data(), (uint32_t)cand[k].size(), q_dev + qoff[k], &row0[k], &words[k], &l));
-        launched[k] = l;
-        steps++;
+            const uint32_t k = f - 1 - fmin;
+            // observed roots of f - 1 at i's turn: those before i in event order
+            const auto &nr = new_roots[f - 1];
+            const uint32_t before = (uint32_t)(std::lower_bound(nr.begin(), nr.end(), i) - nr.begin());
+            const uint32_t len = (uint32_t)(frame_at(a, f - 1).ev.size() - nr.size()) + before;
+            add_slot(a, f, (uint32_t)(base + i), creator[i], row0[k] + (uint64_t)pos_in(f - 1, i) * words[k], len);
+        }
+    // every step in one k_root_fc and one k_root_quorum launch
+    ARC(reserve(a, a->arena, a->arena_used + 1, arena0, s));
+    uint64_t ncand = 0, tiles = 0;
+    std::vector<uint32_t> act;
+    for (uint32_t k = 0; k < nf; k++)
+        if (launched[k]) {
+            ARC(sync_frame(a, frame_at(a, fmin + k), s));
+            act.push_back(k);
+            ncand += cand[k].size();
+            tiles += (uint64_t)((nroots[k] + 63) / 64) * ((cand[k].size() + 63) / 64);
+        }
+    if (!act.empty()) {
+        const uint32_t ncols = (iv.V + 31) / 32 * 32;
+        const uint32_t max_s = ncols / 128 ? ncols / 128 : 1;   // >= 4 LDS chunks of 32 columns per split
+        const uint32_t splits = (uint32_t)std::min<uint64_t>(std::max<uint64_t>((1024 + tiles - 1) / tiles, 1), max_s);
+        const uint32_t col_split = ((ncols + splits - 1) / splits + 31) / 32 * 32;
+        const uint32_t n_split = (ncols + col_split - 1) / col_split;
+        uint64_t npsum = 0;
+        for (uint32_t k : act) npsum += (uint64_t)n_split * cand[k].size() * words[k] * 32;
+        ARC(reserve(a, a->d_cand, ncand, 0, s));
+        ARC(reserve(a, a->d_psum, npsum, 0, s));
+        ARC(reserve(a, a->d_fcargs, act.size(), 0, s));
+        ARC(reserve(a, a->d_qargs, act.size(), 0, s));
+        ARC(refresh_cheaters(a, iv));
+        std::vector<RootFcArgs> fa(act.size());
+        std::vector<QuorumArgs> qa(act.size());
+        uint64_t coff = 0, poff = 0, pairs = 0;
+        uint32_t blocks = 0, qblocks = 0;
+        for (size_t j = 0; j < act.size(); j++) {
+            const uint32_t k = act[j], n_k = (uint32_t)cand[k].size();
+            Frame &fr = a->frames[fmin + k];
+            a->up.add(a->d_cand.p + coff, cand[k].data(), n_k * 4ull);
+            RootFcArgs &r = fa[j];
+            r.hb = iv.hb;
+            r.la = iv.la;
+            r.stride = iv.stride;
+            r.cand = a->d_cand.p + coff;
+            r.n_cand = n_k;
+            r.roots = fr.d_ev.p;
+            r.n_roots = nroots[k];
+            r.roots_fallback = cand[k][0];
+            r.ncols = ncols;
+            r.wpad = iv.wpad;
+            r.quorum = a->quorum;
+            r.n_k = a->n_k;
+            r.kcol = a->d_kcol.p;
+            r.kflag = a->d_kflag.p;
+            r.kw = a->d_kw.p;
+            r.ev_branch = iv.ev_branch;
+            r.psum = a->d_psum.p + poff;
+            r.words = words[k];
+            r.col_split = col_split;
+            r.n_split = n_split;
+            r.block0 = blocks;
+            blocks += lx::root_fc_blocks(r);
+            QuorumArgs &q = qa[j];
+            q.psum = r.psum;
+            q.n_split = n_split;
+            q.bits = a->arena.p + row0[k];
+            q.words = words[k];
+            q.n_roots = nroots[k];
+            q.n_cand = n_k;
+            q.cand = r.cand;
+            q.root_ev = fr.d_ev.p;
+            q.creator = fr.d_creator.p;
+            q.dup = fr.d_dup.p;
+            q.wcreator = iv.wpad;
+            q.quorum = a->quorum;
+            q.q = q_dev + qoff[k];
+            q.block0 = qblocks;
+            qblocks += (n_k + 3) / 4;
+            coff += n_k;
+            poff += (uint64_t)n_split * n_k * words[k] * 32;
+            pairs += (uint64_t)n_k * nroots[k];
+        }
+        a->stats.fc_pairs += pairs;
+        a->stats.fc_pair_cols += pairs * iv.V;
+        a->up.add(a->d_fcargs.p, fa.data(), fa.size() * sizeof(RootFcArgs));
+        a->up.add(a->d_qargs.p, qa.data(), qa.size() * sizeof(QuorumArgs));
+        ARC(flush_uploads(a, s));
+        const bool forks = iv.B > iv.V, seq16 = a->fc16 && iv.max_seq <= 0xFFFFu;
+        const uint32_t k = a->fc_ev_used;
+        while (a->fc_ev.size() < 2ull * (k + 1)) {
+            hipEvent_t e;
+            AHIP(a, hipEventCreate(&e));
+            a->fc_ev.push_back(e);
+        }
+        AHIP(a, hipEventRecord(a->fc_ev[2 * k], s));
+        AHIP(a, lx::launch_root_fc_multi(a->d_fcargs.p, (uint32_t)act.size(), blocks, forks, seq16, s));
+        AHIP(a, hipEventRecord(a->fc_ev[2 * k + 1], s));
+        a->fc_ev_used = k + 1;
+        AHIP(a, lx::launch_root_quorum_multi(a->d_qargs.p, (uint32_t)act.size(), qblocks, s));
+        a->stats.fc_launches++;
+        a->stats.fc_lane_ops += pairs * fc_ops_per_pair(a, iv, forks, seq16, ncols);
     }
     AHIP(a, hipStreamSynchronize(s));
     ARC(collect_fc_times(a));
-    a->stats.frame_steps += steps;
+    a->stats.frame_steps += (uint32_t)act.size();
     for (uint32_t i = 0; i < n; i++) {
         if (i >= cut) {
             a->ev_frame[base + i] = NONE;   // never equals a claim: process() stops here
@@ -974,9 +1082,10 @@ int run_elections_ahead(lx_abft *a, const IndexView &iv, uint64_t *sealed_at, st
     ARC(reserve(a, a->ea_votes, std::max<uint64_t>(vtot, 1), 0, s));
     ARC(reserve(a, a->ea_dec, (uint64_t)nE * vw, 0, s));
     ARC(reserve(a, a->ea_err, nE, 0, s));
-    ARC(flush_uploads(a, s));
-    AHIP(a, hipMemsetAsync(a->ea_dec.p, 0xFF, (uint64_t)nE * vw * 8, s));
-    AHIP(a, hipMemsetAsync(a->ea_err.p, 0, nE * 4ull, s));
+    ARC(reserve(a, a->ea_args, voff.size(), 0, s));
+    // the tables of round r of every election go out in one launch per kernel
+    // (args on the device, grouped by round)
+    std::vector<std::vector<VoteArgs>> by_round(R);
     size_t vi = 0;
     for (uint32_t e = 0; e < nE; e++) {
         const uint32_t F = F0 + e;
@@ -1000,10 +1109,24 @@ int run_elections_ahead(lx_abft *a, const IndexView &iv, uint64_t *sealed_at, st
             v.votes = a->ea_votes.p + voff[vi];
             v.dec = a->ea_dec.p + (uint64_t)e * vw;
             v.err = a->ea_err.p + e;
-            AHIP(a, lx::launch_votes(v, (uint32_t)fg.ev.size(), g == F + 1, s));
-            a->stats.vote_launches++;
+            v.n_voters = (uint32_t)fg.ev.size();
+            by_round[g - F - 1].push_back(v);
             prev = v.votes;
         }
+    }
+    std::vector<uint64_t> aoff(R + 1, 0);
+    for (uint32_t r = 0; r < R; r++) {
+        aoff[r + 1] = aoff[r] + by_round[r].size();
+        a->up.add(a->ea_args.p + aoff[r], by_round[r].data(), by_round[r].size() * sizeof(VoteArgs));
+    }
+    ARC(flush_uploads(a, s));
+    AHIP(a, hipMemsetAsync(a->ea_dec.p, 0xFF, (uint64_t)nE * vw * 8, s));
+    AHIP(a, hipMemsetAsync(a->ea_err.p, 0, nE * 4ull, s));
+    for (uint32_t r = 0; r < R; r++) {
+        uint32_t mx = 0;
+        for (const VoteArgs &v : by_round[r]) mx = std::max(mx, v.n_voters);
+        AHIP(a, lx::launch_votes_multi(a->ea_args.p + aoff[r], (uint32_t)by_round[r].size(), mx, vw, r == 0, s));
+        a->stats.vote_launches++;
     }
     const uint32_t *rb = nullptr;
     ARC(readback(a, s, reinterpret_cast<const uint32_t *>(a->ea_dec.p), 2 * nE * vw, a->ea_err.p, nE, &rb));
@@ -1245,6 +1368,9 @@ void lx_abft_destroy(lx_abft *a) {
     a->ea_votes.release();
     a->ea_err.release();
     a->ea_dec.release();
+    a->ea_args.release();
+    a->d_fcargs.release();
+    a->d_qargs.release();
     (void)hipDeviceSynchronize();   // queued work may still use pooled buffers
     a->up.release();
     if (a->q_pin) (void)hipHostFree(a->q_pin);

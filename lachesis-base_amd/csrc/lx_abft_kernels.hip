@@ -36,16 +36,45 @@ __device__ __forceinline__ uint32_t hb_prep(uint32_t h) {
     return FORKS ? (((int32_t)h < 0) ? 0u : h) : h;
 }
 
+// Merged launches (MULTI): the frame steps of a claimed batch in one grid.
+// Step k owns blocks [am[k].block0, am[k + 1].block0); its args come from the
+// device table (uniform per workgroup: scalar loads).
+template <typename A>
+__device__ __forceinline__ uint32_t step_of(const A *am, uint32_t n_steps, uint32_t b) {
+    uint32_t lo = 0, hi = n_steps;   // last k with am[k].block0 <= b
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) / 2;
+        if (am[mid].block0 <= b) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// the step's args and this workgroup's tile (roots bx, events by, column split bz)
+__device__ __forceinline__ RootFcArgs fc_step(const RootFcArgs *am, uint32_t n_steps, uint32_t *bx, uint32_t *by,
+                                              uint32_t *bz) {
+    const uint32_t k = step_of(am, n_steps, blockIdx.x);
+    const RootFcArgs a = am[k];
+    const uint32_t t = blockIdx.x - a.block0;
+    const uint32_t tx = (a.n_roots + kTile - 1) / kTile, ty = (a.n_cand + kTile - 1) / kTile;
+    *bx = t % tx;
+    *by = (t / tx) % ty;
+    *bz = t / (tx * ty);
+    return a;
+}
+
 // fc_term of k_fc in staged form: (la - 1) < hb'  <=>  la != 0 && la <= hb
-template <bool FORKS>
-__global__ __launch_bounds__(256) void k_root_fc(RootFcArgs a) {
+template <bool FORKS, bool MULTI>
+__global__ __launch_bounds__(256) void k_root_fc(RootFcArgs a1, const RootFcArgs *am, uint32_t n_steps) {
+    uint32_t bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+    const RootFcArgs a = MULTI ? fc_step(am, n_steps, &bx, &by, &bz) : a1;
     __shared__ uint32_t sH[kKc][kLdsPitch];
     __shared__ uint32_t sL[kKc][kLdsPitch];
     __shared__ uint32_t sW[kKc];
 
     const uint32_t tid = threadIdx.x;
     const uint32_t tx = tid & 15, ty = tid >> 4;          // roots tx*4.., events ty*4..
-    const uint32_t r0 = blockIdx.x * kTile, e0 = blockIdx.y * kTile;
+    const uint32_t r0 = bx * kTile, e0 = by * kTile;
 
     // staging role: row = tid / 4, 8 columns = (tid % 4) * 8
     const uint32_t srow = tid >> 2, spart = (tid & 3) * 8;
@@ -61,7 +90,7 @@ __global__ __launch_bounds__(256) void k_root_fc(RootFcArgs a) {
 #pragma unroll
         for (int k = 0; k < 4; k++) sum[i][k] = 0;
 
-    const uint32_t cs = a.col_split, jlo = blockIdx.z * cs, jhi = jlo + cs < a.ncols ? jlo + cs : a.ncols;
+    const uint32_t cs = a.col_split, jlo = bz * cs, jhi = jlo + cs < a.ncols ? jlo + cs : a.ncols;
     for (uint32_t j0 = jlo; j0 < jhi; j0 += kKc) {
         const uint4 h0 = hrow[j0 / 4], h1 = hrow[j0 / 4 + 1];
         const uint4 l0 = lrow[j0 / 4], l1 = lrow[j0 / 4 + 1];
@@ -99,7 +128,7 @@ __global__ __launch_bounds__(256) void k_root_fc(RootFcArgs a) {
     }
 
     uint32_t early = 0;   // bit i*4+k: A observes creator(branch(r)) as forked
-    if (FORKS && blockIdx.z == 0) {
+    if (FORKS && bz == 0) {
         // Cheaters' branches: creator n counts once if any of its branches
         // counts (WeightCounter.CountByIdx, inter/pos/stake.go:47-55); the main
         // loop counted only the original column n.  Columns come grouped by
@@ -152,7 +181,7 @@ __global__ __launch_bounds__(256) void k_root_fc(RootFcArgs a) {
         o.w = sum[i][3] | (((early >> (i * 4 + 3)) & 1u) << 31);
         const uint32_t ri = r0 + tx * 4;
         if (ri < rp)
-            *reinterpret_cast<uint4 *>(a.psum + ((uint64_t)blockIdx.z * a.n_cand + ei) * rp + ri) = o;
+            *reinterpret_cast<uint4 *>(a.psum + ((uint64_t)bz * a.n_cand + ei) * rp + ri) = o;
     }
 }
 
@@ -181,14 +210,17 @@ __device__ __forceinline__ uint32_t udot2(uint32_t a, uint32_t b, uint32_t c) {
     return __builtin_amdgcn_udot2(__builtin_bit_cast(lx_u16x2, a), __builtin_bit_cast(lx_u16x2, b), c, false);
 }
 
-__global__ __launch_bounds__(256) void k_root_fc16(RootFcArgs a) {
+template <bool MULTI>
+__global__ __launch_bounds__(256) void k_root_fc16(RootFcArgs a1, const RootFcArgs *am, uint32_t n_steps) {
+    uint32_t bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+    const RootFcArgs a = MULTI ? fc_step(am, n_steps, &bx, &by, &bz) : a1;
     __shared__ uint32_t sH[kKp][kLdsPitch];
     __shared__ uint32_t sL[kKp][kLdsPitch];
     __shared__ uint32_t sWl[kKp], sWh[kKp];
 
     const uint32_t tid = threadIdx.x;
     const uint32_t tx = tid & 15, ty = tid >> 4;          // roots tx*4.., events ty*4..
-    const uint32_t r0 = blockIdx.x * kTile, e0 = blockIdx.y * kTile;
+    const uint32_t r0 = bx * kTile, e0 = by * kTile;
 
     // staging role: row = tid / 4, 8 columns = (tid % 4) * 8 -> 4 packed dwords
     const uint32_t srow = tid >> 2, spart = (tid & 3) * 8;
@@ -206,7 +238,7 @@ __global__ __launch_bounds__(256) void k_root_fc16(RootFcArgs a) {
 #pragma unroll
         for (int k = 0; k < 4; k++) lo[i][k] = hi[i][k] = 0;
 
-    const uint32_t cs = a.col_split, jlo = blockIdx.z * cs, jhi = jlo + cs < a.ncols ? jlo + cs : a.ncols;
+    const uint32_t cs = a.col_split, jlo = bz * cs, jhi = jlo + cs < a.ncols ? jlo + cs : a.ncols;
     for (uint32_t j0 = jlo; j0 < jhi; j0 += kKc) {
         const uint4 h0 = hrow[j0 / 4], h1 = hrow[j0 / 4 + 1];
         const uint4 l0 = lrow[j0 / 4], l1 = lrow[j0 / 4 + 1];
@@ -281,7 +313,7 @@ uint32_t t[4][4];
         o.w = lo[i][3] + (hi[i][3] << 16);
         const uint32_t ri = r0 + tx * 4;
         if (ri < rp)
-            *reinterpret_cast<uint4 *>(a.psum + ((uint64_t)blockIdx.z * a.n_cand + ei) * rp + ri) = o;
+            *reinterpret_cast<uint4 *>(a.psum + ((uint64_t)bz * a.n_cand + ei) * rp + ri) = o;
     }
 }
 
@@ -297,9 +329,23 @@ uint32_t root_fc_splits(uint32_t n_cand, uint32_t n_roots, uint32_t ncols) {
 hipError_t launch_root_fc(const RootFcArgs &a, bool forks, bool seq16, hipStream_t s) {
     if (!a.n_cand || !a.words) return hipSuccess;
     dim3 grid((a.n_roots + kTile - 1) / kTile, (a.n_cand + kTile - 1) / kTile, a.n_split);
-    if (!forks && seq16) hipLaunchKernelGGL(k_root_fc16, grid, dim3(256), 0, s, a);
-    else if (forks) hipLaunchKernelGGL(k_root_fc<true>, grid, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL(k_root_fc<false>, grid, dim3(256), 0, s, a);
+    if (!forks && seq16) hipLaunchKernelGGL(k_root_fc16<false>, grid, dim3(256), 0, s, a, nullptr, 0);
+    else if (forks) hipLaunchKernelGGL((k_root_fc<true, false>), grid, dim3(256), 0, s, a, nullptr, 0);
+    else hipLaunchKernelGGL((k_root_fc<false, false>), grid, dim3(256), 0, s, a, nullptr, 0);
+    return hipGetLastError();
+}
+
+uint32_t root_fc_blocks(const RootFcArgs &a) {
+    if (!a.n_cand || !a.words) return 0;
+    return ((a.n_roots + kTile - 1) / kTile) * ((a.n_cand + kTile - 1) / kTile) * a.n_split;
+}
+
+hipError_t launch_root_fc_multi(const RootFcArgs *am, uint32_t n_steps, uint32_t blocks, bool forks, bool seq16,
+                                hipStream_t s) {
+    if (!n_steps || !blocks) return hipSuccess;
+    if (!forks && seq16) hipLaunchKernelGGL(k_root_fc16<true>, dim3(blocks), dim3(256), 0, s, RootFcArgs{}, am, n_steps);
+    else if (forks) hipLaunchKernelGGL((k_root_fc<true, true>), dim3(blocks), dim3(256), 0, s, RootFcArgs{}, am, n_steps);
+    else hipLaunchKernelGGL((k_root_fc<false, true>), dim3(blocks), dim3(256), 0, s, RootFcArgs{}, am, n_steps);
     return hipGetLastError();
 }
 
@@ -309,10 +355,12 @@ hipError_t launch_root_fc(const RootFcArgs &a, bool forks, bool seq16, hipStream
 // distinct creators of the roots it forkless-causes (dup[r] = previous root of
 // the same creator in the frame list), its own root slot excluded.
 constexpr uint32_t kRowWords = 512;   // bit row kept in LDS: up to 16384 roots per frame
-__global__ __launch_bounds__(256) void k_root_quorum(QuorumArgs a) {
+template <bool MULTI>
+__global__ __launch_bounds__(256) void k_root_quorum(QuorumArgs a1, const QuorumArgs *am, uint32_t n_steps) {
     __shared__ uint32_t sRow[4][kRowWords];
+    const QuorumArgs a = MULTI ? am[step_of(am, n_steps, blockIdx.x)] : a1;
     const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint32_t wave = blockIdx.x * 4 + wv;
+    const uint32_t wave = (blockIdx.x - (MULTI ? a.block0 : 0u)) * 4 + wv;
     if (wave >= a.n_cand) return;
     const uint32_t rp = a.words * 32;
     uint32_t *row = a.bits + (uint64_t)wave * a.words;
@@ -353,7 +401,13 @@ __global__ __launch_bounds__(256) void k_root_quorum(QuorumArgs a) {
 
 hipError_t launch_root_quorum(const QuorumArgs &a, hipStream_t s) {
     if (!a.n_cand) return hipSuccess;
-    hipLaunchKernelGGL(k_root_quorum, dim3((a.n_cand + 3) / 4), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_root_quorum<false>, dim3((a.n_cand + 3) / 4), dim3(256), 0, s, a, nullptr, 0);
+    return hipGetLastError();
+}
+
+hipError_t launch_root_quorum_multi(const QuorumArgs *am, uint32_t n_steps, uint32_t blocks, hipStream_t s) {
+    if (!n_steps || !blocks) return hipSuccess;
+    hipLaunchKernelGGL(k_root_quorum<true>, dim3(blocks), dim3(256), 0, s, QuorumArgs{}, am, n_steps);
     return hipGetLastError();
 }
 
@@ -386,18 +440,25 @@ hipError_t launch_fc_tile_out(const uint32_t *psum, uint32_t n_split, uint32_t n
 // Votes of different subjects never mix (election_math.go:53-110 reads only
 // votes for the same subject), so each launch computes a subject window
 // [v_lo, v_hi); the host widens the window only while chooseAtropos needs it.
-__global__ void k_vote_init(VoteArgs a, uint32_t n_voters) {
+// MULTI: one launch for many (election, round) tables, args am[blockIdx.y]
+// (init) / am[blockIdx.z] (rounds), each with its own n_voters.
+template <bool MULTI>
+__global__ void k_vote_init(VoteArgs a1, const VoteArgs *am) {
+    const VoteArgs &a = MULTI ? am[blockIdx.y] : a1;
     const uint32_t w = a.v_hi - a.v_lo;
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < (uint64_t)n_voters * w)
+    if (i < (uint64_t)a.n_voters * w)
         a.votes[(i / w) * a.V + a.v_lo + i % w] = kVoteVoted | kVoteNoRoot;
 }
 
 // round 1 (election_math.go:40-52): yes iff the voter forkless-causes the
 // subject's root of the frame to decide; observedRootsMap keeps the last root
 // of a validator in list order -> atomicMax over the list index.
-__global__ void k_vote_round1(VoteArgs a) {
+template <bool MULTI>
+__global__ void k_vote_round1(VoteArgs a1, const VoteArgs *am) {
+    const VoteArgs &a = MULTI ? am[blockIdx.z] : a1;
     const uint32_t s = blockIdx.y;
+    if (s >= a.n_voters) return;
     if (a.voter_ev[s] == LX_NONE) return;
     const uint64_t off = a.bm_off[s];
     const uint32_t len = a.bm_len[s];
@@ -415,7 +476,10 @@ __global__ void k_vote_round1(VoteArgs a) {
 // independent, so many are in flight), then the 4 partial tallies merge.
 constexpr int kVoteSlices = 4;
 constexpr uint32_t kObsChunk = 2048;   // observed-root bits compacted per pass
-__global__ __launch_bounds__(256) void k_vote_round(VoteArgs a, uint32_t n_voters) {
+template <bool MULTI>
+__global__ __launch_bounds__(256) void k_vote_round(VoteArgs a1, const VoteArgs *am) {
+    const VoteArgs &a = MULTI ? am[blockIdx.z] : a1;
+    if (blockIdx.y >= a.n_voters) return;   // the whole workgroup: before any barrier
     __shared__ uint32_t sObs[kObsChunk];
     __shared__ uint32_t sN;
     __shared__ uint32_t sYes[kVoteSlices][64], sNo[kVoteSlices][64], sAll[kVoteSlices][64], sSubj[kVoteSlices][64],
@@ -503,16 +567,34 @@ __global__ __launch_bounds__(256) void k_vote_round(VoteArgs a, uint32_t n_voter
     }
 }
 
-hipError_t launch_votes(const VoteArgs &a, uint32_t n_voters, bool round1, hipStream_t s) {
-    if (!n_voters || a.v_hi <= a.v_lo) return hipSuccess;
+hipError_t launch_votes(const VoteArgs &a0, uint32_t n_voters, bool round1, hipStream_t s) {
+    if (!n_voters || a0.v_hi <= a0.v_lo) return hipSuccess;
+    VoteArgs a = a0;
+    a.n_voters = n_voters;
     const uint32_t w = a.v_hi - a.v_lo;
     const uint64_t n = (uint64_t)n_voters * w;
-    hipLaunchKernelGGL(k_vote_init, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, a, n_voters);
+    hipLaunchKernelGGL(k_vote_init<false>, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, a, nullptr);
     if (round1) {
-        hipLaunchKernelGGL(k_vote_round1, dim3(2, n_voters), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(k_vote_round1<false>, dim3(2, n_voters), dim3(256), 0, s, a, nullptr);
     } else {
         const uint32_t gx = (w + 63) / 64 < 16 ? (w + 63) / 64 : 16;
-        hipLaunchKernelGGL(k_vote_round, dim3(gx, n_voters), dim3(256), 0, s, a, n_voters);
+        hipLaunchKernelGGL(k_vote_round<false>, dim3(gx, n_voters), dim3(256), 0, s, a, nullptr);
+    }
+    return hipGetLastError();
+}
+
+// n tables of one round kind in one launch each: args am[0, n) on the device
+// (n_voters set per table, max_voters = the largest, w = every table's window)
+hipError_t launch_votes_multi(const VoteArgs *am, uint32_t n, uint32_t max_voters, uint32_t w, bool round1,
+                              hipStream_t s) {
+    if (!n || !max_voters || !w) return hipSuccess;
+    const uint64_t cells = (uint64_t)max_voters * w;
+    hipLaunchKernelGGL(k_vote_init<true>, dim3((uint32_t)((cells + 255) / 256), n), dim3(256), 0, s, VoteArgs{}, am);
+    if (round1) {
+        hipLaunchKernelGGL(k_vote_round1<true>, dim3(2, max_voters, n), dim3(256), 0, s, VoteArgs{}, am);
+    } else {
+        const uint32_t gx = (w + 63) / 64 < 16 ? (w + 63) / 64 : 16;
+        hipLaunchKernelGGL(k_vote_round<true>, dim3(gx, max_voters, n), dim3(256), 0, s, VoteArgs{}, am);
     }
     return hipGetLastError();
 }

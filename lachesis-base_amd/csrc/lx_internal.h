@@ -554,6 +554,7 @@ struct RootFcArgs {
     uint32_t words;
     uint32_t col_split;          // columns per split (multiple of 32)
     uint32_t n_split;            // column splits (grid z)
+    uint32_t block0;             // merged launch: this step's first workgroup
 };
 
 struct QuorumArgs {
@@ -570,6 +571,7 @@ struct QuorumArgs {
     const uint32_t *wcreator;    // weight by creator idx
     uint32_t quorum;
     uint8_t *q;                  // out
+    uint32_t block0;             // merged launch: this step's first workgroup
 };
 
 constexpr uint32_t kVoteVoted = 0x80000000u, kVoteYes = 0x40000000u, kVoteDecided = 0x20000000u,
@@ -599,6 +601,7 @@ struct VoteArgs {
     uint32_t *votes;             // out [voter][V]
     unsigned long long *dec;     // per subject: min (event << 32 | yes << 31 | observed root)
     uint32_t *err;
+    uint32_t n_voters;           // voter slots (set by the launchers)
 };
 
 // Segmented walk of one batch (lx_segment.hip): the
@@ -767,10 +770,16 @@ hipError_t launch_qi_metric(const QiArgs &a, const uint32_t *ev, uint32_t n, uin
                             hipStream_t s);
 uint32_t root_fc_splits(uint32_t n_cand, uint32_t n_roots, uint32_t ncols);
 hipError_t launch_root_fc(const RootFcArgs &a, bool forks, bool seq16, hipStream_t s);
+uint32_t root_fc_blocks(const RootFcArgs &a);
+hipError_t launch_root_fc_multi(const RootFcArgs *am, uint32_t n_steps, uint32_t blocks, bool forks, bool seq16,
+                                hipStream_t s);
+hipError_t launch_root_quorum_multi(const QuorumArgs *am, uint32_t n_steps, uint32_t blocks, hipStream_t s);
 hipError_t launch_root_quorum(const QuorumArgs &a, hipStream_t s);
 hipError_t launch_fc_tile_out(const uint32_t *psum, uint32_t n_split, uint32_t n_cand, uint32_t rp, uint32_t n_roots,
                               uint32_t quorum, const uint8_t *tag, uint8_t *out, uint64_t pitch, hipStream_t s);
 hipError_t launch_votes(const VoteArgs &a, uint32_t n_voters, bool round1, hipStream_t s);
+hipError_t launch_votes_multi(const VoteArgs *am, uint32_t n, uint32_t max_voters, uint32_t w, bool round1,
+                              hipStream_t s);
 hipError_t launch_scatter(const ScatterDesc *desc, uint32_t n, uint64_t max_bytes, const uint8_t *base,
                           hipStream_t s);
 hipError_t launch_gather_rows(uint32_t *dst, const uint32_t *src, uint64_t stride, uint32_t V, const uint32_t *rows,
