@@ -96,6 +96,29 @@ double now_ms() {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+// LX_ABFT_TIMING=1: host wall time between the marks of the batched frame and
+// election passes, one line per pass on stderr (diagnostics only)
+struct PassTimer {
+    const char *name;
+    bool on;
+    double t0, last;
+    std::string out;
+    explicit PassTimer(const char *n) : name(n), on(getenv("LX_ABFT_TIMING") != nullptr) {
+        if (on) t0 = last = now_ms();
+    }
+    void mark(const char *what) {
+        if (!on) return;
+        const double t = now_ms();
+        char b[64];
+        snprintf(b, sizeof b, " %s=%.3f", what, t - last);
+        out += b;
+        last = t;
+    }
+    ~PassTimer() {
+        if (on) fprintf(stderr, "abft_timing %s total=%.3f%s\n", name, now_ms() - t0, out.c_str());
+    }
+};
+
 struct Frame {
     std::vector<uint32_t> ev, creator, dup, bm_len;
     std::vector<uint64_t> bm_off;
@@ -137,6 +160,15 @@ struct Uploader {
         desc.push_back(ScatterDesc{dst, off, bytes});
     }
     bool pending() const { return !desc.empty(); }
+    // a pending upload writes into [p, p + bytes)
+    bool targets(const void *p, uint64_t bytes) const {
+        const uint8_t *lo = static_cast<const uint8_t *>(p), *hi = lo + bytes;
+        for (const ScatterDesc &d : desc) {
+            const uint8_t *x = static_cast<const uint8_t *>(d.dst);
+            if (x >= lo && x < hi) return true;
+        }
+        return false;
+    }
     void release() {
         for (int k = 0; k < kSlots; k++) {
             if (pin[k]) (void)hipHostFree(pin[k]);
@@ -237,7 +269,7 @@ int flush_uploads(lx_abft *a, hipStream_t s);
 template <typename T>
 int reserve(lx_abft *a, DVec<T> &v, uint64_t n, uint64_t keep, hipStream_t s) {
     if (n <= v.cap) return 0;
-    if (a->up.pending()) ARC(flush_uploads(a, s));   // their destinations may be about to move
+    if (v.p && a->up.targets(v.p, v.cap * sizeof(T))) ARC(flush_uploads(a, s));   // the buffer is about to move
     uint64_t cap = std::max<uint64_t>({n, v.cap + v.cap / 2, 256});
     uint64_t got = 0;
     T *p = static_cast<T *>(a->pool.take(cap * sizeof(T), &got));
@@ -588,9 +620,11 @@ int eval_frame(lx_abft *a, const IndexView &iv, uint32_t f, const std::vector<ui
 // alone (nothing after it is reported).  A claim above every root frame so far
 // + 1 cannot verify (frame top+1 has no roots): the batch is cut there.
 int compute_frames_claimed(lx_abft *a, uint64_t base, uint32_t n, const uint32_t *creator, const uint32_t *claimed) {
+    PassTimer pt("frames");
     IndexView iv;
     int rc = lx_index_view(a->ix, &iv);
     if (rc) return a->ixfail(rc);
+    pt.mark("view");
     hipStream_t s = iv.stream;
     uint32_t top = 0;   // highest frame with a root
     for (uint32_t f = 1; f < a->frames.size(); f++)
@@ -655,20 +689,30 @@ int compute_frames_claimed(lx_abft *a, uint64_t base, uint32_t n, const uint32_t
         a->arena_used += (uint64_t)cand[k].size() * words[k];
         launched[k] = !cand[k].empty() && words[k];
     }
-    // the roots, frame by frame in event order: a root of f observes the step at f - 1
-    for (uint32_t f = 1; f < new_roots.size(); f++)
-        for (uint32_t i : new_roots[f]) {
-            if (f == 1 && a->ev_sp[base + i] == NONE) {
-                add_slot(a, 1, (uint32_t)(base + i), creator[i], 0, 0);
-                continue;
-            }
-            const uint32_t k = f - 1 - fmin;
-            // observed roots of f - 1 at i's turn: those before i in event order
-            const auto &nr = new_roots[f - 1];
-            const uint32_t before = (uint32_t)(std::lower_bound(nr.begin(), nr.end(), i) - nr.begin());
-            const uint32_t len = (uint32_t)(frame_at(a, f - 1).ev.size() - nr.size()) + before;
-            add_slot(a, f, (uint32_t)(base + i), creator[i], row0[k] + (uint64_t)pos_in(f - 1, i) * words[k], len);
+    // the roots, frame by frame in event order: a root of f observes the step at
+    // f - 1 (its position there and the roots of f - 1 before it by merge walks:
+    // every list is in event order)
+    for (uint32_t f = 1; f < new_roots.size(); f++) {
+        if (new_roots[f].empty()) continue;
+        Frame &fr = frame_at(a, f);
+        fr.ev.reserve(fr.ev.size() + new_roots[f].size());
+        if (f == 1) {
+            for (uint32_t i : new_roots[1]) add_slot(a, 1, (uint32_t)(base + i), creator[i], 0, 0);
+            continue;
         }
+        const uint32_t k = f - 1 - fmin;
+        const auto &nr = new_roots[f - 1];
+        const auto &cl = cand[k];
+        const uint32_t old_roots = (uint32_t)(frame_at(a, f - 1).ev.size() - nr.size());
+        size_t pc = 0, pb = 0;
+        for (uint32_t i : new_roots[f]) {
+            const uint32_t e = (uint32_t)(base + i);
+            while (pc < cl.size() && cl[pc] < e) pc++;
+            while (pb < nr.size() && nr[pb] < i) pb++;
+            add_slot(a, f, e, creator[i], row0[k] + (uint64_t)pc * words[k], old_roots + (uint32_t)pb);
+        }
+    }
+    pt.mark("plan");
     // every step in one k_root_fc and one k_root_quorum launch
     ARC(reserve(a, a->arena, a->arena_used + 1, arena0, s));
     uint64_t ncand = 0, tiles = 0;
@@ -748,7 +792,9 @@ int compute_frames_claimed(lx_abft *a, uint64_t base, uint32_t n, const uint32_t
         a->stats.fc_pair_cols += pairs * iv.V;
         a->up.add(a->d_fcargs.p, fa.data(), fa.size() * sizeof(RootFcArgs));
         a->up.add(a->d_qargs.p, qa.data(), qa.size() * sizeof(QuorumArgs));
+        pt.mark("args");
         ARC(flush_uploads(a, s));
+        pt.mark("upload");
         const bool forks = iv.B > iv.V, seq16 = a->fc16 && iv.max_seq <= 0xFFFFu;
         const uint32_t k = a->fc_ev_used;
         while (a->fc_ev.size() < 2ull * (k + 1)) {
@@ -764,7 +810,9 @@ int compute_frames_claimed(lx_abft *a, uint64_t base, uint32_t n, const uint32_t
         a->stats.fc_launches++;
         a->stats.fc_lane_ops += pairs * fc_ops_per_pair(a, iv, forks, seq16, ncols);
     }
+    pt.mark("launch");
     AHIP(a, hipStreamSynchronize(s));
+    pt.mark("wait");
     ARC(collect_fc_times(a));
     a->stats.frame_steps += (uint32_t)act.size();
     for (uint32_t i = 0; i < n; i++) {
@@ -1070,7 +1118,9 @@ int run_elections_ahead(lx_abft *a, const IndexView &iv, uint64_t *sealed_at, st
     const uint32_t maxf = (uint32_t)a->frames.size() - 1;
     const uint32_t nE = maxf - 1 - F0;    // elections F0 .. maxf - 2
     const uint32_t vw = std::min<uint32_t>(a->V, kVoteWindow);
+    PassTimer pt("elect");
     for (uint32_t f = F0; f <= maxf; f++) ARC(sync_frame(a, frame_at(a, f), s));
+    pt.mark("sync_frames");
     // vote tables: election e, round g -> slots(g) x vw
     std::vector<uint64_t> voff;
     uint64_t vtot = 0;
@@ -1128,8 +1178,10 @@ int run_elections_ahead(lx_abft *a, const IndexView &iv, uint64_t *sealed_at, st
         AHIP(a, lx::launch_votes_multi(a->ea_args.p + aoff[r], (uint32_t)by_round[r].size(), mx, vw, r == 0, s));
         a->stats.vote_launches++;
     }
+    pt.mark("launch");
     const uint32_t *rb = nullptr;
     ARC(readback(a, s, reinterpret_cast<const uint32_t *>(a->ea_dec.p), 2 * nE * vw, a->ea_err.p, nE, &rb));
+    pt.mark("wait");
     std::vector<unsigned long long> dec((uint64_t)nE * vw);
     memcpy(dec.data(), rb, dec.size() * 8);
     std::vector<uint32_t> err(rb + 2ull * nE * vw, rb + 2ull * nE * vw + nE);
@@ -1156,8 +1208,10 @@ int run_elections_ahead(lx_abft *a, const IndexView &iv, uint64_t *sealed_at, st
     if (done.empty()) return 0;
     std::vector<uint32_t> rows(done.size());
     for (size_t k = 0; k < done.size(); k++) rows[k] = done[k].atropos;
+    pt.mark("decide");
     const uint32_t *hb_rows = nullptr;
     ARC(readback_rows(a, iv, rows, &hb_rows));
+    pt.mark("rows");
     for (size_t k = 0; k < done.size(); k++) {
         const uint64_t decided_at = std::max<uint64_t>(done[k].t, a->t_prev);
         bool sealed;

@@ -481,6 +481,7 @@ __global__ __launch_bounds__(256) void k_vote_round(VoteArgs a1, const VoteArgs 
     const VoteArgs &a = MULTI ? am[blockIdx.z] : a1;
     if (blockIdx.y >= a.n_voters) return;   // the whole workgroup: before any barrier
     __shared__ uint32_t sObs[kObsChunk];
+    __shared__ uint32_t sWc[kObsChunk];   // stake of each observed root's creator
     __shared__ uint32_t sN;
     __shared__ uint32_t sYes[kVoteSlices][64], sNo[kVoteSlices][64], sAll[kVoteSlices][64], sSubj[kVoteSlices][64],
         sErr[kVoteSlices][64];
@@ -519,12 +520,16 @@ __global__ __launch_bounds__(256) void k_vote_round(VoteArgs a1, const VoteArgs 
             }
             __syncthreads();
             const uint32_t n = sN;
+            // creator stakes of the observed roots, all threads at once (the
+            // subject loop below then reads one global word per root: the vote)
+            for (uint32_t k = threadIdx.x; k < n; k += blockDim.x) sWc[k] = a.wcreator[a.prev_creator[sObs[k]]];
+            __syncthreads();
             if (v < a.v_hi) {
-#pragma unroll 4
+#pragma unroll 8
                 for (uint32_t k = slice; k < n; k += kVoteSlices) {
                     const uint32_t r = sObs[k];
                     const uint32_t pv = a.prev_votes[(uint64_t)r * a.V + v];
-                    const uint32_t wc = a.wcreator[a.prev_creator[r]];
+                    const uint32_t wc = sWc[k];
                     if (!(pv & kVoteVoted)) err |= kVoteErrMissing;
                     const bool py = (pv & kVoteYes) != 0;
                     const uint32_t ix = pv & kVoteNoRoot;

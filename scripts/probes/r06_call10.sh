@@ -1,6 +1,7 @@
 set -o pipefail
-mkdir -p gpurun_out/r06_skew3
-for i in 1 2 3; do
-LX_LIB=lachesis-base_amd/build_pSKEW/liblachesis_hip.so WS_WALKS=2 timeout -k 10 240 python3 scripts/probes/walk_skew.py >> gpurun_out/r06_skew3/skew.jsonl 2>> gpurun_out/r06_skew3/skew.err || exit $?
-done
-echo done
+O=gpurun_out/r06_abftprof
+mkdir -p $O
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/kt -o run -- python3 scripts/bench_abft_only.py 5 > $O/leg.json 2> $O/leg.err || exit $?
+find $O/kt -name "*kernel_stats.csv" | head -3
+f=$(find $O/kt -name "*kernel_stats.csv" | head -1); cp $f $O/kernel_stats.csv; head -30 $O/kernel_stats.csv | cut -c1-200

@@ -1,8 +1,8 @@
 set -o pipefail
-mkdir -p gpurun_out/r06_margin
-for i in 1 2; do
-  WL_OPT=drain_margin WL_VALUES=0,1024,512 WL_ROUNDS=3 timeout -k 10 300 python3 scripts/probes/walk_lock_ab.py >> gpurun_out/r06_margin/margin_ab.jsonl 2>> gpurun_out/r06_margin/ab.err || exit $?
-  WL_OPT=pad_slice WL_VALUES=0,1 WL_ROUNDS=3 timeout -k 10 300 python3 scripts/probes/walk_lock_ab.py >> gpurun_out/r06_margin/pad_ab.jsonl 2>> gpurun_out/r06_margin/ab.err || exit $?
-done
-timeout -k 10 900 python -u -m pytest -x -v --timeout 600 --timeout-method thread "tests/test_gpu_parity.py::test_config3_shape_1m_default_segments_vs_oracle" "tests/test_gpu_parity.py::test_walker_variants" > gpurun_out/r06_margin/pytest.log 2>&1
-rc=$?; tail -4 gpurun_out/r06_margin/pytest.log; exit $rc
+O=gpurun_out/r06_abfttime
+mkdir -p $O
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_abft.py tests/test_gpu_fccache.py tests/test_gpu_dropin.py > $O/pytest.log 2>&1
+rc=$?; tail -2 $O/pytest.log; [ $rc = 0 ] || exit $rc
+LX_ABFT_TIMING=1 timeout -k 10 200 python3 scripts/bench_abft_only.py 4 > $O/leg.json 2> $O/timing.err || exit $?
+grep abft_timing $O/timing.err | tail -6
+cut -c1-400 $O/leg.json
