@@ -16,6 +16,8 @@
 // speculatively in the same launch (their self-parent usually stops at f).
 // An event that passes q_f becomes a root of f+1; its bit row of that launch
 // is exactly the observed-roots set the election needs for that root slot.
+// A batch in which every event claims its frame needs no steps at all: every
+// question is known up front (compute_frames_claimed), one launch answers all.
 //
 // Election (abft/election/election_math.go:13-114).  Votes of a root slot
 // depend only on the slots it observes, so votes are computed per frame
@@ -27,6 +29,8 @@
 // t = max(previous decision, max_{v <= Atropos subject} first decision(v))
 // (chooseAtropos, sort_roots.go:10-25), final once no uncomputed slot is older
 // than t.  Frames are replayed after each decision as processKnownRoots does.
+// Elections of different frames do not read each other, so all of them run
+// side by side first (run_elections_ahead), round by round only what remains.
 //
 // Blocks (abft/lachesis.go:40-86): cheaters from the Atropos' HighestBefore
 // fork markers, confirmation DFS in the reference's stack order on the host.
