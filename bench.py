@@ -373,7 +373,12 @@ def config_leg(lx, name, steps, warmup, device, want_cpu, cpu_budget, fc_n=1 << 
 ABFT_CONFIG = ("c5", 1000, 50, 10, "zipf")   # BASELINE configs[4]: V, events/validator, parents, stakes
 
 
-VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12   # 78.6 T lane-ops/s
+VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12   # 78.6 T lane-ops/s (2-cycle wave64 VALU ops)
+# k_root_fc16 issues only v_pk_sub_u16, v_pk_min_u16 and v_dot2_u32_u16, each 4
+# shader cycles per wave-instruction on a SIMD (scripts/probes/valu_rate.hip,
+# profiles/r06/abft/valu_rate.json: 4.19-4.22 measured against 2.31 for
+# v_add_u32 / v_fma_f32 in the same harness), so its issue peak is half
+VALU_PEAK_4CYC_TOPS = 256 * 4 * 64 / 4 * 2.4e9 / 1e12   # 39.3 T lane-ops/s
 
 
 def abft_leg(lx, steps, warmup, device, cpu_budget, want_cpu):
@@ -423,13 +428,18 @@ def abft_leg(lx, steps, warmup, device, cpu_budget, want_cpu):
     # half = 1.5 lane-ops per column, 2 in 32-column chunks holding a weight >=
     # 2^16.  fc_lane_ops counts what the launches issued (padded columns);
     # peak = 256 CUs x 4 SIMDs x 32 lanes x 2.4 GHz (MI355X_MICROARCH.md:
-    # wave64 VALU op = 2 cycles on a SIMD).
+    # wave64 VALU op = 2 cycles on a SIMD) for k_root_fc; half that for
+    # k_root_fc16, whose three instructions all take 4 cycles (measured).
     if st["ms_root_fc_gpu"] > 0:
         sec = st["ms_root_fc_gpu"] * 1e-3
         pc = st["fc_pair_cols"] / sec
         ach = st["fc_lane_ops"] / sec / 1e12
-        res["roofline_root_fc"] = {"bound": "valu", "achieved": ach, "peak": VALU_PEAK_TOPS,
-                                   "unit": "T int32 lane-ops/s", "frac": ach / VALU_PEAK_TOPS,
+        opc = st["fc_lane_ops"] / max(st["fc_pair_cols"], 1)
+        packed = opc < 2.4   # 1.5-2 lane-ops per pair-column: k_root_fc16 ran
+        peak = VALU_PEAK_4CYC_TOPS if packed else VALU_PEAK_TOPS
+        res["roofline_root_fc"] = {"bound": "valu", "kernel": "k_root_fc16" if packed else "k_root_fc",
+                                   "achieved": ach, "peak": peak,
+                                   "unit": "T int32 lane-ops/s", "frac": ach / peak,
                                    "pair_cols_per_s": pc,
                                    "ops_per_pair_col": st["fc_lane_ops"] / max(st["fc_pair_cols"], 1),
                                    "ms_per_epoch": st["ms_root_fc_gpu"]}

@@ -239,24 +239,37 @@ __global__ __launch_bounds__(256) void k_root_fc16(RootFcArgs a1, const RootFcAr
         for (int k = 0; k < 4; k++) lo[i][k] = hi[i][k] = 0;
 
     const uint32_t cs = a.col_split, jlo = bz * cs, jhi = jlo + cs < a.ncols ? jlo + cs : a.ncols;
+    // the next chunk's rows are loaded into registers while this one computes
+    uint4 h0 = hrow[jlo / 4], h1 = hrow[jlo / 4 + 1], l0 = lrow[jlo / 4], l1 = lrow[jlo / 4 + 1];
+    uint32_t w0 = tid < kKp ? a.wpad[jlo + 2 * tid] : 0u, w1 = tid < kKp ? a.wpad[jlo + 2 * tid + 1] : 0u;
     for (uint32_t j0 = jlo; j0 < jhi; j0 += kKc) {
-        const uint4 h0 = hrow[j0 / 4], h1 = hrow[j0 / 4 + 1];
-        const uint4 l0 = lrow[j0 / 4], l1 = lrow[j0 / 4 + 1];
-        const uint32_t hv[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
-        const uint32_t lv[8] = {l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, l1.z, l1.w};
+        {
+            const uint32_t hv[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+            const uint32_t lv[8] = {l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, l1.z, l1.w};
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-            sH[spart / 2 + q][srow] = hv[2 * q] | (hv[2 * q + 1] << 16);
-            sL[spart / 2 + q][srow] = ((lv[2 * q] - 1u) & 0xFFFFu) | ((lv[2 * q + 1] - 1u) << 16);
+            for (int q = 0; q < 4; q++) {
+                sH[spart / 2 + q][srow] = hv[2 * q] | (hv[2 * q + 1] << 16);
+                sL[spart / 2 + q][srow] = ((lv[2 * q] - 1u) & 0xFFFFu) | ((lv[2 * q + 1] - 1u) << 16);
+            }
         }
         uint32_t wh = 0;
         if (tid < kKp) {
-            const uint32_t w0 = a.wpad[j0 + 2 * tid], w1 = a.wpad[j0 + 2 * tid + 1];
             sWl[tid] = (w0 & 0xFFFFu) | (w1 << 16);
             wh = (w0 >> 16) | (w1 & 0xFFFF0000u);
             sWh[tid] = wh;
         }
         const bool any_hi = __syncthreads_or(wh != 0);
+        const uint32_t jn = j0 + kKc;
+        if (jn < jhi) {
+            h0 = hrow[jn / 4];
+            h1 = hrow[jn / 4 + 1];
+            l0 = lrow[jn / 4];
+            l1 = lrow[jn / 4 + 1];
+            if (tid < kKp) {
+                w0 = a.wpad[jn + 2 * tid];
+                w1 = a.wpad[jn + 2 * tid + 1];
+            }
+        }
         if (any_hi) {
 #pragma unroll 4
             for (int j = 0; j < kKp; j++) {
