@@ -45,16 +45,55 @@ def clocks():
     return {"mhz_median": round(float(np.median(mhz)), 1), "mhz_min": round(float(mhz.min()), 1),
             "mhz_max": round(float(mhz.max()), 1), "wave0_ms_max": round(float(a[:, 1].max()) / 1e5, 2),
             "mhz_by_xcd": per_xcd}
+
+
+def kfd_self():
+    """KFD's counters of every process holding a GPU (the container's pid
+    namespace hides which host pid is ours: the caller takes the one whose
+    VRAM holds this process's planes): pid -> evicted_ms, vram GiB, page moves."""
+    base = "/sys/class/kfd/kfd/proc"
+    out = {}
+    try:
+        pids = os.listdir(base)
+    except OSError:
+        return None
+    for pid in pids:
+        d = os.path.join(base, pid)
+        r = {"evicted_ms": 0, "vram_gib": 0.0, "page_in": 0, "page_out": 0}
+        try:
+            for e in os.listdir(d):
+                if e.startswith("stats_"):
+                    r["evicted_ms"] += int(open(os.path.join(d, e, "evicted_ms")).read())
+                elif e.startswith("vram_"):
+                    r["vram_gib"] += int(open(os.path.join(d, e)).read()) / 2**30
+                elif e.startswith("counters_"):
+                    r["page_in"] += int(open(os.path.join(d, e, "page_in")).read())
+                    r["page_out"] += int(open(os.path.join(d, e, "page_out")).read())
+        except (OSError, ValueError):
+            continue
+        out[pid] = r
+    return out
+
+
 for inst in range(n_inst):
     ix = lx.Index(event_capacity=N, options=json.loads(os.environ.get("WT_OPTS", "{}")))
     hb_ptr, la_ptr, stride, _ = ix.device_planes()
-    walks, clks = [], []
+    walks, clks, kfd = [], [], []
     for r in range(n_walk):
+        k0 = kfd_self()
         ix.reset(w)
         ix.add_batch_dev(N, dc.data_ptr(), ds.data_ptr(), do.data_ptr(), dp.data_ptr())
         ix.sync()
         st = ix.segment_stats()
         walks.append(round(max(st["walk_ms"]), 2) if st["segments"] else round(ix.last_stats()["ms_index"], 2))
+        k1 = kfd_self()
+        if k0 and k1:
+            # the process holding >= 60 GiB (this one's planes), its changes over the walk
+            mine = [p for p in k1 if k1[p]["vram_gib"] >= 60]
+            kfd.append({p: {"evicted_ms": k1[p]["evicted_ms"] - k0.get(p, k1[p])["evicted_ms"],
+                            "page_in": k1[p]["page_in"] - k0.get(p, k1[p])["page_in"],
+                            "page_out": k1[p]["page_out"] - k0.get(p, k1[p])["page_out"],
+                            "vram_gib": round(k1[p]["vram_gib"], 1)} for p in mine})
         if clk is not None:
             clks.append(clocks())
         elif os.environ.get("WM_SHIPCLK") == "1":
@@ -63,6 +102,6 @@ for inst in range(n_inst):
             clks.append({k: (round(v, 2) if isinstance(v, float) else v) for k, v in c.items()} | {"t": round(time.time(), 3)})
     print(json.dumps({"lib": lib, "pid": os.getpid(), "inst": inst, "walk_ms": walks,
                       "hb": hex(hb_ptr or 0), "la": hex(la_ptr or 0), "partial": st["partial"],
-                      **({"clk": clks} if clks else {})}), flush=True)
+                      **({"clk": clks} if clks else {}), **({"kfd_delta": kfd} if kfd else {})}), flush=True)
     ix.close()
     del ix
