@@ -1084,7 +1084,9 @@ int apply_block(lx_abft *a, const IndexView &iv, uint32_t F, uint32_t atropos, b
         if (a->ev_confirmed[walk] == 0) {
             a->ev_confirmed[walk] = F;
             if (a->cb.apply_event) a->cb.apply_event(a->cb.user, walk);
-            for (uint64_t k = a->par_off[walk]; k < a->par_off[walk + 1]; k++) stack.push_back(a->par[k]);
+            // a parent already confirmed would be popped and skipped: not pushed
+            for (uint64_t k = a->par_off[walk]; k < a->par_off[walk + 1]; k++)
+                if (a->ev_confirmed[a->par[k]] == 0) stack.push_back(a->par[k]);
         }
         if (stack.empty()) break;
         walk = stack.back();
@@ -1227,6 +1229,7 @@ int run_elections_ahead(lx_abft *a, const IndexView &iv, uint64_t *sealed_at, st
         a->t_prev = decided_at;
         a->last_decided = done[k].F;
     }
+    pt.mark("apply");
     for (uint32_t g = 1; g <= a->last_decided && g < a->frames.size(); g++) a->frames[g].votes.release();
     a->dec_dirty = true;
     a->stats.elections_ahead += (uint32_t)done.size();
