@@ -17,6 +17,8 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "lachesis-base_amd")]
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import lachesis_hip as lx  # noqa: E402
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from kfd_stats import kfd_self  # noqa: E402
 
 V, epv = int(os.environ.get("WT_V", "1000")), int(os.environ.get("WT_EPV", "10000"))
 n_inst, n_walk = int(os.environ.get("WM_INST", "3")), int(os.environ.get("WM_WALKS", "4"))
@@ -45,34 +47,6 @@ def clocks():
     return {"mhz_median": round(float(np.median(mhz)), 1), "mhz_min": round(float(mhz.min()), 1),
             "mhz_max": round(float(mhz.max()), 1), "wave0_ms_max": round(float(a[:, 1].max()) / 1e5, 2),
             "mhz_by_xcd": per_xcd}
-
-
-def kfd_self():
-    """KFD's counters of every process holding a GPU (the container's pid
-    namespace hides which host pid is ours: the caller takes the one whose
-    VRAM holds this process's planes): pid -> evicted_ms, vram GiB, page moves."""
-    base = "/sys/class/kfd/kfd/proc"
-    out = {}
-    try:
-        pids = os.listdir(base)
-    except OSError:
-        return None
-    for pid in pids:
-        d = os.path.join(base, pid)
-        r = {"evicted_ms": 0, "vram_gib": 0.0, "page_in": 0, "page_out": 0}
-        try:
-            for e in os.listdir(d):
-                if e.startswith("stats_"):
-                    r["evicted_ms"] += int(open(os.path.join(d, e, "evicted_ms")).read())
-                elif e.startswith("vram_"):
-                    r["vram_gib"] += int(open(os.path.join(d, e)).read()) / 2**30
-                elif e.startswith("counters_"):
-                    r["page_in"] += int(open(os.path.join(d, e, "page_in")).read())
-                    r["page_out"] += int(open(os.path.join(d, e, "page_out")).read())
-        except (OSError, ValueError):
-            continue
-        out[pid] = r
-    return out
 
 
 for inst in range(n_inst):
