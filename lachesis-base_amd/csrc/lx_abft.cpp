@@ -1339,17 +1339,24 @@ void restore_snapshot(lx_abft *a, const Snapshot &s) {
 // adds the batch to the index and the host event tables
 int add_events(lx_abft *a, uint32_t n, const uint32_t *creator, const uint32_t *seq, const uint64_t *poff,
                const uint32_t *par) {
+    PassTimer pt("index");
     uint32_t err_index = 0;
     int rc = lx_add_batch(a->ix, n, creator, seq, poff, par, nullptr, &err_index);
     if (rc) return a->ixfail(rc);
+    pt.mark("add_batch");
+    const uint64_t e0 = a->ev_sp.size();
+    a->ev_sp.resize(e0 + n);
+    a->ev_frame.resize(e0 + n, 0);
+    a->ev_confirmed.resize(e0 + n, 0);
+    a->par_off.reserve(a->par_off.size() + n);
+    const uint64_t q0 = a->par.size();
+    a->par.insert(a->par.end(), par + poff[0], par + poff[n]);
     for (uint32_t i = 0; i < n; i++) {
         const uint64_t p0 = poff[i], p1 = poff[i + 1];
-        a->ev_sp.push_back(seq[i] > 1 && p1 > p0 ? par[p0] : NONE);   // inter/dag/event.go:87-92
-        a->ev_frame.push_back(0);
-        a->ev_confirmed.push_back(0);
-        a->par.insert(a->par.end(), par + p0, par + p1);
-        a->par_off.push_back(a->par.size());
+        a->ev_sp[e0 + i] = seq[i] > 1 && p1 > p0 ? par[p0] : NONE;   // inter/dag/event.go:87-92
+        a->par_off.push_back(q0 + (p1 - poff[0]));
     }
+    pt.mark("tables");
     return 0;
 }
 

@@ -2080,20 +2080,31 @@ int lx_add_batch(lx_index *h, uint32_t n, const uint32_t *creator, const uint32_
         return rs;
     }
     HIPCHK(h, set_dev(h->device));
-    std::vector<uint32_t> off(n + 1);
+    int rc;
+    if ((rc = flush_pending(h))) return rc;
+    // the batch goes to the device as one pinned image {creator, seq, parent
+    // offsets, parents} (16-B aligned parts) copied by k_stage into a device
+    // image the walk reads in place: pageable hipMemcpyAsync of the four arrays
+    // cost ~0.5 ms per 50k-event batch
+    const uint64_t a4 = (n + 3ull) / 4 * 4, o4 = (n + 4ull) / 4 * 4;
+    const uint64_t words = 2 * a4 + o4 + npar;
+    uint32_t *img = nullptr;
+    int slot = 0;
+    if ((rc = stage_slot(h, words, &img, &slot))) return rc;
+    memcpy(img, creator, n * 4ull);
+    memcpy(img + a4, seq, n * 4ull);
+    uint32_t *off = img + 2 * a4;
     for (uint32_t i = 0; i <= n; i++) {
         if (i && poff[i] < poff[i - 1]) return h->fail(LX_ERR_ARG, "parent offsets not monotone");
         off[i] = (uint32_t)(poff[i] - base);
     }
-    int rc;
-    if ((rc = flush_pending(h))) return rc;
-    if ((rc = ensure_batch(h, n, npar))) return rc;
-    HIPCHK(h, hipMemcpyAsync(h->b_creator, creator, n * 4ull, hipMemcpyHostToDevice, h->stream));
-    HIPCHK(h, hipMemcpyAsync(h->b_seq, seq, n * 4ull, hipMemcpyHostToDevice, h->stream));
-    HIPCHK(h, hipMemcpyAsync(h->b_poff, off.data(), (n + 1) * 4ull, hipMemcpyHostToDevice, h->stream));
-    if (npar) HIPCHK(h, hipMemcpyAsync(h->b_par, par + base, npar * 4, hipMemcpyHostToDevice, h->stream));
+    if (npar) memcpy(img + 2 * a4 + o4, par + base, npar * 4);
+    uint32_t *dimg = h->st_dev[slot];
+    HIPCHK(h, lx::launch_stage(dimg, img, words, h->stream));
+    HIPCHK(h, hipEventRecord(h->st_copied[slot], h->stream));
+    h->st_used[slot] = true;
     uint64_t start = h->n_events;
-    if ((rc = add_batch_dev(h, n, h->b_creator, h->b_seq, h->b_poff, h->b_par, err_index))) return rc;
+    if ((rc = add_batch_dev(h, n, dimg, dimg + a4, dimg + 2 * a4, dimg + 2 * a4 + o4, err_index))) return rc;
     if (out_branch) HIPCHK(h, hipMemcpy(out_branch, h->ev_branch + start, n * 4ull, hipMemcpyDeviceToHost));
     return 0;
 }
