@@ -393,7 +393,9 @@ def abft_leg(lx, steps, warmup, device, cpu_budget, want_cpu):
     weights = weights_for(V, wkind)
     dag = lx.tools.gen_dag(V, epv, P, 0, 0, seed=1)
     N = len(dag)
-    lch = lx.abft.DenseLachesis(weights, device=device, event_capacity=N, apply_events=False)
+    # the blocks come back through the library's block log (the confirmation
+    # DFS runs as under a BeginBlock callback; no Python callback per block)
+    lch = lx.abft.DenseLachesis(weights, device=device, event_capacity=N, apply_events=False, block_log=True)
     rc, consumed, frames = lch.process_batch(dag.creator, dag.seq, dag.poff, dag.par)   # Build-path frames
     assert rc == 0 and consumed == N
     claimed = frames.copy()

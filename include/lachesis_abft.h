@@ -67,7 +67,13 @@ const char *lx_abft_last_error(const lx_abft *a);
  *                as in Build
  *   "elect_ahead" rounds per election when the elections of every frame are
  *                enqueued together and read back with one wait (2..8, default
- *                2; 0: round by round, one wait per round) */
+ *                2; 0: round by round, one wait per round)
+ *   "block_log"  without a begin_block callback: 1 = the handle logs each
+ *                decided block (frame, Atropos, cheaters) and runs the
+ *                confirmation as a BeginBlock would, never sealing (no
+ *                EndBlock); 2 = also the confirmed events in ApplyEvent order;
+ *                read with lx_abft_block_log after the batch.  0 (default):
+ *                nil BeginBlock semantics */
 int lx_abft_set_option(lx_abft *a, const char *name, int64_t value);
 
 /* ApplyGenesis + Bootstrap (abft/apply_genesis.go:17-44, bootstrap.go:30-52):
@@ -97,6 +103,14 @@ int lx_abft_reset(lx_abft *a, uint32_t epoch, uint32_t n_validators, const uint3
 int lx_abft_process_batch(lx_abft *a, uint32_t n, const uint32_t *creator_idx, const uint32_t *seq,
                           const uint64_t *parent_off, const uint32_t *parent_idx, const uint32_t *claimed_frame,
                           uint32_t *out_frame, uint32_t *consumed);
+
+/* The blocks the last lx_abft_process_batch decided (option block_log):
+ * block k = frame[k], atropos[k], cheaters[cheat_off[k] .. cheat_off[k+1]),
+ * confirmed[conf_off[k] .. conf_off[k+1]) (block_log 2; empty ranges with 1).
+ * Pointers stay valid until the next call into the handle; any may be NULL. */
+int lx_abft_block_log(const lx_abft *a, uint32_t *n_blocks, const uint32_t **frame, const uint32_t **atropos,
+                      const uint32_t **cheat_off, const uint32_t **cheaters, const uint32_t **conf_off,
+                      const uint32_t **confirmed);
 
 /* IndexedLachesis.Build (indexed_lachesis.go:53-63): frame of a self-emitted
  * event (added, evaluated, then dropped again). */

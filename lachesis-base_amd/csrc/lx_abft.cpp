@@ -185,6 +185,19 @@ struct Uploader {
 
 }  // namespace
 
+// blocks decided by the last lx_abft_process_batch (option block_log)
+struct BlockLog {
+    std::vector<uint32_t> frame, atropos, cheaters, cheat_off{0}, confirmed, conf_off{0};
+    void clear() {
+        frame.clear();
+        atropos.clear();
+        cheaters.clear();
+        confirmed.clear();
+        cheat_off.assign(1, 0);
+        conf_off.assign(1, 0);
+    }
+};
+
 struct lx_abft {
     lx_index *ix = nullptr;
     std::string err;
@@ -233,6 +246,9 @@ struct lx_abft {
     bool fc16 = true;                   // option fc16=0: k_root_fc (32-bit) even for 16-bit seqs
     bool claimed_batch = true;          // option claimed_batch=0: claimed batches take the Build path's steps
     uint32_t elect_ahead = kElectAhead;  // option elect_ahead: rounds per election decided ahead (0 = off)
+    uint32_t block_log = 0;             // option block_log: without callbacks, log blocks (2: with confirmed events)
+    BlockLog blog;
+    std::vector<uint32_t> sweep_atropos, sweep_frame, sweep_label;   // confirmations queued for confirm_sweep
 
     lx_abft_stats stats{};
 
@@ -415,6 +431,8 @@ void clear_epoch(lx_abft *a) {
     a->ev_frame.clear();
     a->ev_sp.clear();
     a->ev_confirmed.clear();
+    a->sweep_atropos.clear();
+    a->sweep_frame.clear();
     a->par_off.assign(1, 0);
     a->par.clear();
     a->arena_used = 0;
@@ -1067,6 +1085,35 @@ int reset_election(lx_abft *a, const IndexView &iv) {
     return 0;
 }
 
+// The confirmations of the blocks queued by apply_block (block_log 1, no
+// ApplyEvent): block F confirms every not yet confirmed ancestor of its
+// Atropos (the DFS of lachesis.go:40-55 stops at confirmed events, whose
+// ancestors are all confirmed already), so each event takes the first queued
+// block whose Atropos it is an ancestor of.  Events are in Add order (parents
+// first): one sweep from the highest Atropos down carries the earliest block
+// index to the parents -- the same sets as the blocks' DFS, in one pass over
+// the parent lists instead of one stack walk per block.
+void confirm_sweep(lx_abft *a) {
+    const size_t nb = a->sweep_atropos.size();
+    if (!nb) return;
+    uint32_t hi = 0;
+    for (uint32_t e : a->sweep_atropos) hi = std::max(hi, e);
+    std::vector<uint32_t> &lab = a->sweep_label;
+    lab.assign((size_t)hi + 1, NONE);
+    for (size_t k = nb; k-- > 0;) lab[a->sweep_atropos[k]] = (uint32_t)k;   // earliest block wins
+    for (uint32_t e = hi + 1; e-- > 0;) {
+        const uint32_t k = lab[e];
+        if (k == NONE || a->ev_confirmed[e]) continue;
+        a->ev_confirmed[e] = a->sweep_frame[k];
+        for (uint64_t j = a->par_off[e]; j < a->par_off[e + 1]; j++) {
+            const uint32_t p = a->par[j];
+            if (!a->ev_confirmed[p] && k < lab[p]) lab[p] = k;
+        }
+    }
+    a->sweep_atropos.clear();
+    a->sweep_frame.clear();
+}
+
 // cheaters + confirmation DFS + callbacks; returns 1 in *sealed when EndBlock seals
 // (row: the Atropos' HB row already read back, or nullptr)
 int apply_block(lx_abft *a, const IndexView &iv, uint32_t F, uint32_t atropos, bool *sealed,
@@ -1076,14 +1123,35 @@ int apply_block(lx_abft *a, const IndexView &iv, uint32_t F, uint32_t atropos, b
     if (!row) ARC(readback(a, iv.stream, iv.hb + (uint64_t)atropos * iv.stride, a->V, nullptr, 0, &row));
     for (uint32_t c = 0; c < a->V; c++)
         if (row[c] & LX_MARK) cheaters.push_back(c);   // GetMergedHighestBefore(atropos)[c].IsForkDetected()
-    if (!a->cb.begin_block) return 0;   // BeginBlock == nil: no confirmation, no seal (lachesis.go:69-71)
+    // BeginBlock == nil: no confirmation, no seal (lachesis.go:69-71) -- unless
+    // the handle logs its blocks itself (option block_log: a BeginBlock that
+    // records, no EndBlock)
+    const uint32_t log = a->cb.begin_block ? 0u : a->block_log;
+    if (!a->cb.begin_block && !log) return 0;
     if (a->cb.begin_block) a->cb.begin_block(a->cb.user, F, atropos, cheaters.data(), (uint32_t)cheaters.size());
+    if (log) {
+        BlockLog &L = a->blog;
+        L.frame.push_back(F);
+        L.atropos.push_back(atropos);
+        L.cheaters.insert(L.cheaters.end(), cheaters.begin(), cheaters.end());
+        L.cheat_off.push_back((uint32_t)L.cheaters.size());
+    }
+    if (log == 1 && !a->cb.apply_event) {
+        // nobody sees the order: the confirmations of this batch's blocks are
+        // made by one sweep (confirm_sweep) before anything reads them
+        a->sweep_atropos.push_back(atropos);
+        a->sweep_frame.push_back(F);
+        a->blog.conf_off.push_back(0);
+        a->stats.blocks++;
+        return 0;
+    }
     // dfsSubgraph(atropos, filter) (abft/traversal.go:13-37, lachesis.go:40-55)
     std::vector<uint32_t> stack;
     for (uint32_t walk = atropos;;) {
         if (a->ev_confirmed[walk] == 0) {
             a->ev_confirmed[walk] = F;
             if (a->cb.apply_event) a->cb.apply_event(a->cb.user, walk);
+            if (log == 2) a->blog.confirmed.push_back(walk);
             // a parent already confirmed would be popped and skipped: not pushed
             for (uint64_t k = a->par_off[walk]; k < a->par_off[walk + 1]; k++)
                 if (a->ev_confirmed[a->par[k]] == 0) stack.push_back(a->par[k]);
@@ -1101,6 +1169,7 @@ int apply_block(lx_abft *a, const IndexView &iv, uint32_t F, uint32_t atropos, b
             *sealed = true;
         }
     }
+    if (log) a->blog.conf_off.push_back((uint32_t)a->blog.confirmed.size());
     a->stats.blocks++;
     return 0;
 }
@@ -1332,6 +1401,8 @@ void restore_snapshot(lx_abft *a, const Snapshot &s) {
     a->ev_frame.resize(s.n_events);
     a->ev_sp.resize(s.n_events);
     a->ev_confirmed.resize(s.n_events);
+    a->sweep_atropos.clear();
+    a->sweep_frame.clear();
     a->par_off.resize(s.n_events + 1);
     a->par.resize(a->par_off.back());
 }
@@ -1393,6 +1464,7 @@ int process(lx_abft *a, uint32_t n, const uint32_t *creator, const uint32_t *seq
     std::vector<uint32_t> new_w;
     double t3 = now_ms();
     ARC(run_elections(a, &sealed_at, &new_w));
+    confirm_sweep(a);
     double t4 = now_ms();
     a->stats.ms_election += (float)(t4 - t3);
     uint32_t done = n;
@@ -1471,6 +1543,9 @@ int lx_abft_set_option(lx_abft *a, const char *name, int64_t value) {
     } else if (k == "claimed_batch") {
         if (value < 0 || value > 1) return a->fail(LX_ERR_ARG, "claimed_batch must be 0 or 1");
         a->claimed_batch = value != 0;
+    } else if (k == "block_log") {
+        if (value < 0 || value > 2) return a->fail(LX_ERR_ARG, "block_log must be 0, 1 or 2");
+        a->block_log = (uint32_t)value;
     } else if (k == "elect_ahead") {
         if (value < 0 || value > 8 || value == 1) return a->fail(LX_ERR_ARG, "elect_ahead must be 0 or 2..8");
         a->elect_ahead = (uint32_t)value;
@@ -1492,7 +1567,23 @@ int lx_abft_process_batch(lx_abft *a, uint32_t n, const uint32_t *creator, const
     if (!a || !consumed) return LX_ERR_ARG;
     if (!a->booted) return a->fail(LX_ERR_STATE, "not bootstrapped");
     a->stats = lx_abft_stats{};
+    a->blog.clear();
     return process(a, n, creator, seq, poff, par, claimed, out_frame, consumed);
+}
+
+int lx_abft_block_log(const lx_abft *a, uint32_t *n_blocks, const uint32_t **frame, const uint32_t **atropos,
+                      const uint32_t **cheat_off, const uint32_t **cheaters, const uint32_t **conf_off,
+                      const uint32_t **confirmed) {
+    if (!a || !n_blocks) return LX_ERR_ARG;
+    const BlockLog &L = a->blog;
+    *n_blocks = (uint32_t)L.frame.size();
+    if (frame) *frame = L.frame.data();
+    if (atropos) *atropos = L.atropos.data();
+    if (cheat_off) *cheat_off = L.cheat_off.data();
+    if (cheaters) *cheaters = L.cheaters.data();
+    if (conf_off) *conf_off = L.conf_off.data();
+    if (confirmed) *confirmed = L.confirmed.data();
+    return 0;
 }
 
 int lx_abft_build(lx_abft *a, uint32_t creator, uint32_t seq, uint32_t np, const uint32_t *parents,

@@ -288,9 +288,12 @@ class DenseLachesis:
     weights.  Records blocks as (epoch, frame, atropos, cheaters, confirmed);
     ``apply_events=False`` skips the per-event ApplyEvent callback (the
     confirmation DFS still runs; GetEventConfirmedOn still answers).
-    ``seal(epoch, frame)`` may return the next epoch's weights."""
+    ``seal(epoch, frame)`` may return the next epoch's weights.
+    ``block_log=True``: no callbacks at all -- the library logs each decided
+    block itself (option block_log, with the confirmed events when
+    apply_events) and the blocks are read after each batch; never seals."""
 
-    def __init__(self, weights, epoch=1, device=0, event_capacity=0, apply_events=True, seal=None):
+    def __init__(self, weights, epoch=1, device=0, event_capacity=0, apply_events=True, seal=None, block_log=False):
         self.ix = Index(device=device, event_capacity=event_capacity)
         self.L = self.ix.L
         h = vp()
@@ -302,12 +305,19 @@ class DenseLachesis:
         self.seal = seal
         self._cur = None
         self._seal_w = None
-        self._cb = Callbacks(None, BEGIN_BLOCK(self._begin), APPLY_EVENT(self._apply) if apply_events else APPLY_EVENT(),
-                             END_BLOCK(self._end))
+        self.block_log = bool(block_log)
+        if self.block_log and seal is not None:
+            raise ValueError("block_log never seals: no seal callback")
+        self._cb = None if self.block_log else Callbacks(
+            None, BEGIN_BLOCK(self._begin), APPLY_EVENT(self._apply) if apply_events else APPLY_EVENT(),
+            END_BLOCK(self._end))
         w = np.ascontiguousarray(weights, dtype=np.uint32)
-        rc = self.L.lx_abft_bootstrap(self.h, epoch, len(w), _p(w, u32p), ctypes.byref(self._cb))
+        rc = self.L.lx_abft_bootstrap(self.h, epoch, len(w), _p(w, u32p),
+                                      None if self._cb is None else ctypes.byref(self._cb))
         if rc != 0:
             raise LxError(rc, self.L.lx_abft_last_error(self.h).decode())
+        if self.block_log:
+            self.set_option("block_log", 2 if apply_events else 1)
 
     def close(self):
         if getattr(self, "h", None):
@@ -350,10 +360,38 @@ class DenseLachesis:
                                           ctypes.byref(consumed))
         if rc not in (0, ERR_FRAME):
             raise LxError(rc, self.L.lx_abft_last_error(self.h).decode())
+        if self.block_log:
+            self._read_block_log()
         return rc, consumed.value, out
+
+    def _read_block_log(self):
+        nb = ctypes.c_uint32()
+        ptr = [ctypes.POINTER(ctypes.c_uint32)() for _ in range(6)]
+        rc = self.L.lx_abft_block_log(self.h, ctypes.byref(nb), *[ctypes.byref(q) for q in ptr])
+        if rc != 0:
+            raise LxError(rc, self.L.lx_abft_last_error(self.h).decode())
+        n = nb.value
+        if not n:
+            return
+        fr, at, co, ch, fo, cf = ptr
+        ep = self.epoch()
+        for k in range(n):
+            self.blocks.append((ep, fr[k], at[k], tuple(ch[i] for i in range(co[k], co[k + 1])),
+                                tuple(cf[i] for i in range(fo[k], fo[k + 1]))))
 
     def epoch(self):
         return self.L.lx_abft_epoch(self.h)
+
+    def confirmed_on(self, n):
+        """GetEventConfirmedOn of events [0, n) of the epoch (0 = not confirmed)."""
+        out = np.zeros(n, dtype=np.uint32)
+        f = ctypes.c_uint32()
+        for i in range(n):
+            rc = self.L.lx_abft_event_confirmed_on(self.h, i, ctypes.byref(f))
+            if rc != 0:
+                raise LxError(rc, self.L.lx_abft_last_error(self.h).decode())
+            out[i] = f.value
+        return out
 
     def last_decided_frame(self):
         return self.L.lx_abft_last_decided_frame(self.h)

@@ -124,6 +124,7 @@ SIGNATURES = [
     ("lx_abft_event_frame", ctypes.c_int, [vp, ctypes.c_uint32, u32p]),
     ("lx_abft_event_confirmed_on", ctypes.c_int, [vp, ctypes.c_uint32, u32p]),
     ("lx_abft_last_stats", ctypes.c_int, [vp, vp]),
+    ("lx_abft_block_log", ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp]),
     # include/lachesis_emitter.h
     ("lx_qi_create", ctypes.c_int, [vp, ctypes.POINTER(vp)]),
     ("lx_qi_destroy", None, [vp]),

@@ -262,10 +262,11 @@ def blocks_of(g):
     return out
 
 
-@pytest.mark.parametrize("name,chunks,fc16,claimed", [("c4", 1, 1, 0), ("c4", 7, 1, 0), ("c5", 1, 1, 0), ("c5", 3, 1, 0),
-                                                      ("c5", 1, 0, 0), ("c4", 1, 1, 1), ("c4", 7, 1, 1),
-                                                      ("c5", 1, 1, 1), ("c5", 3, 0, 1)])
-def test_abft_full_size_vs_oracle(name, chunks, fc16, claimed):
+@pytest.mark.parametrize("name,chunks,fc16,claimed,blog", [("c4", 1, 1, 0, 0), ("c4", 7, 1, 0, 0), ("c5", 1, 1, 0, 0),
+                                                           ("c5", 3, 1, 0, 0), ("c5", 1, 0, 0, 0), ("c4", 1, 1, 1, 0),
+                                                           ("c4", 7, 1, 1, 0), ("c5", 1, 1, 1, 0), ("c5", 3, 0, 1, 0),
+                                                           ("c4", 7, 1, 1, 1), ("c5", 1, 1, 1, 1)])
+def test_abft_full_size_vs_oracle(name, chunks, fc16, claimed, blog):
     """BASELINE configs 4 (100 validators, 10 % double-signers, 100k events)
     and 5 (1000 validators, Zipf stakes, 50k events) at full size: frames of
     every event, roots per frame and every block (Atropos, cheaters, ApplyEvent
@@ -276,7 +277,8 @@ def test_abft_full_size_vs_oracle(name, chunks, fc16, claimed):
     g = load_golden(name)
     V, epn, P, ch, fk, seed = map(int, g["config"])
     d = tools.gen_dag(V, epn, P, cheaters=ch, forks=fk, seed=seed)
-    lch = abft.DenseLachesis(g["weights"], event_capacity=len(d))
+    # blog: no callbacks, the library's block log (option block_log 2)
+    lch = abft.DenseLachesis(g["weights"], event_capacity=len(d), block_log=bool(blog))
     lch.set_option("fc16", fc16)   # c5 (Zipf stakes, no forks): packed root-FC kernel unless 0
     frames = np.zeros(len(d), dtype=np.uint32)
     bounds = np.linspace(0, len(d), chunks + 1).astype(np.int64)
@@ -290,3 +292,32 @@ def test_abft_full_size_vs_oracle(name, chunks, fc16, claimed):
     assert np.array_equal(frames, g["frames"])
     assert [len(lch.frame_roots(f)) for f in range(len(g["roots_per_frame"]))] == list(g["roots_per_frame"])
     assert lch.blocks == blocks_of(g)
+
+
+@pytest.mark.parametrize("name", ["c4", "c5"])
+def test_abft_block_log_sweep_equals_dfs(name):
+    """block_log 1 without ApplyEvent confirms a batch's blocks by one sweep
+    over the parent lists (lx_abft.cpp confirm_sweep) instead of one DFS per
+    block: the same GetEventConfirmedOn for every event and the same blocks
+    as the callbacks' DFS path, claimed batches whole and in chunks."""
+    import numpy as np
+    from lachesis_hip import abft, tools
+    g = load_golden(name)
+    V, epn, P, ch, fk, seed = map(int, g["config"])
+    d = tools.gen_dag(V, epn, P, cheaters=ch, forks=fk, seed=seed)
+    want = blocks_of(g)
+    for chunks in (1, 5):
+        runs = {}
+        for mode in ("dfs", "sweep"):
+            lch = abft.DenseLachesis(g["weights"], event_capacity=len(d), apply_events=False,
+                                     block_log=(mode == "sweep"))
+            bounds = np.linspace(0, len(d), chunks + 1).astype(np.int64)
+            for lo, hi in zip(bounds[:-1], bounds[1:]):
+                c, s_, off, par = d.slice(lo, hi)
+                rc, consumed, out = lch.process_batch(c, s_, off, par, g["frames"][lo:hi])
+                assert rc == 0 and consumed == hi - lo
+            runs[mode] = (lch.confirmed_on(len(d)), [b[:4] for b in lch.blocks])
+            lch.close()
+        assert np.array_equal(runs["dfs"][0], runs["sweep"][0]), chunks
+        assert runs["dfs"][1] == runs["sweep"][1] == [b[:4] for b in want], chunks
+        assert (runs["sweep"][0] > 0).sum() == sum(len(b[4]) for b in want)
