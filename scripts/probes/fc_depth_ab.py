@@ -1,5 +1,5 @@
 """k_fc_early with one or two queries in flight ahead per half-wave (option
-fc_early_depth), interleaved in one process on the headline config (C3, 2^24
+fc_early_depth, removed after this A/B), interleaved in one process on the headline config (C3, 2^24
 queries of the bench's shape, device arrays): per setting and round the
 median of 5 launches; answers compared byte for byte.  One JSON line."""
 import json
