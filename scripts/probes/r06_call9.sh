@@ -7,7 +7,7 @@ timeout -k 10 300 python3 scripts/probes/abft_fc16_ab.py > $O/fc16_ab.jsonl 2> $
 cat $O/fc16_ab.jsonl
 AB_OPT=claimed_batch timeout -k 10 300 python3 scripts/probes/abft_fc16_ab.py > $O/claimed_batch_ab.jsonl 2> $O/claimed_batch_ab.err || exit $?
 cat $O/claimed_batch_ab.jsonl
-AB_OPT=elect_ahead AB_VALUES=3,0,2 timeout -k 10 300 python3 scripts/probes/abft_fc16_ab.py > $O/elect_ahead_ab.jsonl 2> $O/elect_ahead_ab.err || exit $?
+AB_OPT=elect_ahead AB_VALUES=2,0 timeout -k 10 300 python3 scripts/probes/abft_fc16_ab.py > $O/elect_ahead_ab.jsonl 2> $O/elect_ahead_ab.err || exit $?
 cat $O/elect_ahead_ab.jsonl
 timeout -k 10 300 python3 scripts/bench_abft_only.py 5 > $O/abft_leg.json 2> $O/abft_leg.err || exit $?
 cat $O/abft_leg.json
