@@ -100,8 +100,11 @@ const char *lx_last_error(const lx_index *h);
  *                side in one launch, G = CUs / walk workgroups, >= 32k events each)
  *   "get_server" 0: every single-row getter launches its kernel (default 1: the resident
  *                row server answers them while the stream is idle, lx_get_server_stats)
- * The library reads no environment variables (the walker-counters build,
- * make WPROF=1, reads LX_PROF). */
+ *   "realloc_records" 1: diagnostics -- move the batch record buffers to a fresh
+ *                allocation now (the walk slow-mode probe)
+ * The library reads no environment variables except two diagnostics: the
+ * walker-counters build (make WPROF=1) reads LX_PROF, and LX_ABFT_TIMING=1
+ * prints the abft passes' host timing marks to stderr. */
 int lx_set_option(lx_index *h, const char *name, int64_t value);
 
 /* Reset (vecfc/index.go:98-105, vecengine/index.go:56-68): new epoch with

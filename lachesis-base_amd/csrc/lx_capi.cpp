@@ -1892,6 +1892,24 @@ int lx_set_option(lx_index *h, const char *name, int64_t value) {
         h->crec_opt = value != 0;
     } else if (k == "seg_xmap") {
         h->seg_xmap_opt = value != 0;
+    } else if (k == "realloc_records") {
+        // diagnostics (walk slow-mode probe): move the batch's record buffers
+        // to a fresh allocation now (the new one taken before the old is freed)
+        if (value) {
+            HIPCHK(h, set_dev(h->device));
+            HIPCHK(h, hipStreamSynchronize(h->stream));
+            const uint64_t n = (h->batch_cap + 63) / 64 * 64;
+            auto move = [&](auto **b) -> int {
+                if (!*b) return 0;
+                std::remove_reference_t<decltype(*b)> nb = nullptr;
+                HIPCHK(h, dalloc(&nb, n));
+                (void)hipFree(*b);
+                *b = nb;
+                return 0;
+            };
+            if (int rc = move(&h->b_rec)) return rc;
+            if (int rc = move(&h->b_crec)) return rc;
+        }
     } else if (k == "dbl") {
         h->dbl = value != 0;
     } else if (k == "seg_auto") {
