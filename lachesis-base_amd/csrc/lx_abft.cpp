@@ -673,12 +673,30 @@ int compute_frames_claimed(lx_abft *a, uint64_t base, uint32_t n, const uint32_t
             fmax = std::max(fmax, c - 1);
         }
     }
+    pt.mark("scan");
     // candidates per frame step (event order) and each event's q slots
     const uint32_t nf = fmin == NONE ? 0 : fmax - fmin + 1;
     std::vector<std::vector<uint32_t>> cand(nf);
     std::vector<std::vector<uint32_t>> new_roots(top + 2);
     std::vector<uint64_t> qoff(nf + 1, 0), row0(nf, 0);
     std::vector<uint32_t> words(nf, 0), pos0(n, 0);
+    {
+        // list sizes first: one allocation per list
+        std::vector<uint32_t> nc(nf, 0), nr(top + 2, 0);
+        for (uint32_t i = 0; i < cut; i++) {
+            if (a->ev_sp[base + i] == NONE) {
+                nr[1]++;
+                continue;
+            }
+            if (rf[i] == NONE) continue;
+            for (uint32_t f = spf[i]; f < rf[i]; f++) {
+                nc[f - fmin]++;
+                nr[f + 1]++;
+            }
+        }
+        for (uint32_t k = 0; k < nf; k++) cand[k].reserve(nc[k]);
+        for (uint32_t f = 0; f < top + 2; f++) new_roots[f].reserve(nr[f]);
+    }
     for (uint32_t i = 0; i < cut; i++) {
         if (a->ev_sp[base + i] == NONE) {
             new_roots[1].push_back(i);
@@ -699,6 +717,7 @@ int compute_frames_claimed(lx_abft *a, uint64_t base, uint32_t n, const uint32_t
         const auto &c = cand[f - fmin];
         return (uint32_t)(std::lower_bound(c.begin(), c.end(), (uint32_t)(base + i)) - c.begin());
     };
+    pt.mark("cands");
     // layout: step k (frame fmin + k) asks cand[k] against every root of its
     // frame (the ones so far + this batch's), bit rows at row0[k] in the arena
     const uint64_t arena0 = a->arena_used;
@@ -711,13 +730,19 @@ int compute_frames_claimed(lx_abft *a, uint64_t base, uint32_t n, const uint32_t
         a->arena_used += (uint64_t)cand[k].size() * words[k];
         launched[k] = !cand[k].empty() && words[k];
     }
+    pt.mark("layout");
     // the roots, frame by frame in event order: a root of f observes the step at
     // f - 1 (its position there and the roots of f - 1 before it by merge walks:
     // every list is in event order)
     for (uint32_t f = 1; f < new_roots.size(); f++) {
         if (new_roots[f].empty()) continue;
         Frame &fr = frame_at(a, f);
-        fr.ev.reserve(fr.ev.size() + new_roots[f].size());
+        const size_t want = fr.ev.size() + new_roots[f].size();
+        fr.ev.reserve(want);
+        fr.creator.reserve(want);
+        fr.dup.reserve(want);
+        fr.bm_off.reserve(want);
+        fr.bm_len.reserve(want);
         if (f == 1) {
             for (uint32_t i : new_roots[1]) add_slot(a, 1, (uint32_t)(base + i), creator[i], 0, 0);
             continue;
@@ -734,7 +759,7 @@ int compute_frames_claimed(lx_abft *a, uint64_t base, uint32_t n, const uint32_t
             add_slot(a, f, e, creator[i], row0[k] + (uint64_t)pc * words[k], old_roots + (uint32_t)pb);
         }
     }
-    pt.mark("plan");
+    pt.mark("slots");
     // every step in one k_root_fc and one k_root_quorum launch
     ARC(reserve(a, a->arena, a->arena_used + 1, arena0, s));
     uint64_t ncand = 0, tiles = 0;
